@@ -1,0 +1,164 @@
+#!/usr/bin/env python3
+"""Benchmark: Lanczos iterations/s and achieved SpMV HBM GB/s on the 3-D Poisson 7-point matrix,
+256^3 DoF (BASELINE.json metric), fp64, 1..8 MI355X.
+
+One "step" = one Lanczos three-term-recurrence iteration (no re-orthogonalisation) of the whole
+256^3 problem: the fused SpMV kernel (t = A u sig - gam u_prev, t.u) + the fused update kernel
+(u_next = t - alpha sig u, ||u_next||^2), plus at N > 1 the one-plane RCCL halo exchange and two
+one-double allreduces.  The matrix is row-partitioned in z-slabs (strong scaling: the total work
+is fixed as N grows).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 --master-port P \
+        bench.py --gpus N --steps K --warmup W
+
+torch.distributed (gloo) is only the bootstrap / barrier / max-over-ranks channel; the data path
+is libeigmi's own RCCL communicator over xGMI.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "dune-eigensolver_amd"))
+
+import numpy as np  # noqa: E402
+
+import eigmi  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+
+
+def cpu_baseline(N, rp, c, v, steps, gpu_alpha):
+    """The reference CPU path's Lanczos step (oracle restatement: a3 SpMV + the BLAS-1 loops of
+    ARPACK), single thread, on the same matrix and start vector; a bounded sample of steps."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # noqa: E402  (checker / baseline only)
+    n = N ** 3
+    u0, u1, u2 = np.zeros(n), np.zeros(n), np.zeros(n)
+    oracle.lib.orc_random_vec(n, 123, u0)
+    alpha, beta = np.zeros(steps), np.zeros(steps + 1)
+    t0 = time.perf_counter()
+    oracle.lib.orc_lanczos_rotating(n, rp, c, v, steps, u0, u1, u2, alpha, beta)
+    dt = time.perf_counter() - t0
+    k = min(steps, len(gpu_alpha))
+    rel = float(np.max(np.abs(alpha[:k] - gpu_alpha[:k]) / np.abs(alpha[:k]))) if k else None
+    return steps / dt, dt, rel
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--N", type=int, default=256, help="grid points per axis (n = N^3)")
+    ap.add_argument("--cpu-steps", type=int, default=16, help="Lanczos steps of the CPU baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-kernel-events", action="store_true", help="skip per-kernel HIP events")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    ctx = eigmi.Context(local)
+    if world > 1:
+        import torch
+        uid = eigmi.Context.unique_id() if rank == 0 else bytes(128)
+        t = torch.tensor(list(uid), dtype=torch.uint8)
+        dist.broadcast(t, 0)
+        ctx.comm_init(world, rank, bytes(t.tolist()))
+
+    N = args.N
+    n = N ** 3
+    b, cnt = eigmi.row_partition(n, world, rank, align=N * N)
+    rp, c, v = eigmi.gen_rows(eigmi.GEN_POISSON3D, N, b, cnt)
+    if world > 1:
+        M = eigmi.Matrix.from_rows(ctx, n, b, rp, c, v)
+    else:
+        M = eigmi.Matrix.from_bcsr(ctx, rp, c, v)
+    nnz_total = int(eigmi.lib.eig_gen_nnzb(eigmi.GEN_POISSON3D, N))
+    nnz_local = int(rp[-1])
+
+    K, W = args.steps, args.warmup
+    ws = eigmi.LanczosWorkspace(M, W + K, seed=123)
+    if W:
+        ws.step(W)
+    barrier()
+    ctx.sync()
+    t0 = time.perf_counter()
+    tim = ws.step(K, timed=not args.no_kernel_events)
+    ctx.sync()
+    barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        tt = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    alpha, beta = ws.tridiag()
+    ok = bool(np.all(np.isfinite(alpha)) and np.all(beta[1:] > 0))
+
+    # dominant kernel: the fused SpMV (k_lanczos_spmv_b1), HIP events on the library stream
+    k1_bytes = eigmi.bytes_lanczos_k1(cnt, nnz_local)
+    k1_ms = tim.spmv_ms / K if tim.spmv_launches else None
+    roofline = None
+    if k1_ms:
+        ach = k1_bytes / (k1_ms * 1e-3) / 1e9
+        roofline = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                    "kernel": "k_lanczos_spmv_b1", "bytes_per_launch": k1_bytes,
+                    "avg_launch_us": round(k1_ms * 1e3, 2)}
+    step_bytes = eigmi.bytes_lanczos_step(n, nnz_total)
+    value = K / dt
+    out = {
+        "metric": "Lanczos iters/sec + achieved SpMV HBM GB/s, 3D Poisson 256^3",
+        "value": round(value, 3),
+        "unit": "iters/s",
+        "n_gpus": world,
+        "steps": K,
+        "warmup": W,
+        "ms_per_step": round(dt / K * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (generated 7-point Poisson matrix, mt19937 seed-123 start vector)",
+        "config": {"workload": f"3D Poisson 7-pt {N}^3 Lanczos 3-term step, no re-orthogonalisation",
+                   "N": N, "n": n, "nnz": nnz_total, "parallelism": f"row-partition z-slabs x{world} (RCCL halo + allreduce)"},
+        "step_hbm_gbs": round(step_bytes / (dt / K) / 1e9, 1),
+        "step_roofline_frac": round(step_bytes / (dt / K) / 1e9 / HBM_PEAK_GBS / max(world, 1), 4),
+        "roofline": roofline,
+        "spmv_hbm_gbs": roofline["achieved"] if roofline else None,
+        "device_ms": {"total": round(tim.total_ms, 3), "spmv": round(tim.spmv_ms, 3),
+                      "update": round(tim.update_ms, 3), "comm": round(tim.comm_ms, 3)},
+        "recurrence_finite": ok,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cv, cdt, rel = cpu_baseline(N, rp, c, v, args.cpu_steps, alpha)
+        out["cpu_baseline"] = {"value": round(cv, 4), "unit": "iters/s", "cores": 1, "kind": "port",
+                               "sample": f"{args.cpu_steps} Lanczos steps on the same {N}^3 matrix and start "
+                                         f"vector, oracle/oracle.cc single thread ({cdt:.1f} s)",
+                               "alpha_max_rel_diff_vs_gpu": rel}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    ws.close()
+    M.close()
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,936 @@
+// api.cpp -- the C ABI of libeigmi (include/eigmi.h): contexts, device memory, matrix upload
+// into the SELL-64 image, the halo plan of row-partitioned matrices, BlockVector and
+// MultiVector operations.  Drivers live in drivers.cpp.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <random>
+#include <thread>
+
+#include "internal.h"
+
+using namespace eigmi;
+
+namespace {
+
+thread_local std::string g_tls_error;
+
+template <class F>
+int guard(eig_ctx_t ctx, F &&f)
+{
+  try
+  {
+    f();
+    return EIG_OK;
+  }
+  catch (const Error &e)
+  {
+    (ctx ? ctx->last_error : g_tls_error) = e.what();
+    return e.code;
+  }
+  catch (const std::bad_alloc &)
+  {
+    (ctx ? ctx->last_error : g_tls_error) = "host allocation failed";
+    return EIG_ERR_ARG;
+  }
+  catch (const std::exception &e)
+  {
+    (ctx ? ctx->last_error : g_tls_error) = e.what();
+    return EIG_ERR_ARG;
+  }
+}
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev)
+  {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) EIG_HIP(hipSetDevice(dev));
+  }
+  ~DeviceGuard()
+  {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+template <class T>
+T *dev_alloc(size_t count)
+{
+  void *p = nullptr;
+  if (count == 0) count = 1;
+  EIG_HIP(hipMalloc(&p, count * sizeof(T)));
+  return static_cast<T *>(p);
+}
+
+}  // namespace
+
+// ============================================================================================
+// internal helpers shared with drivers.cpp
+// ============================================================================================
+namespace eigmi {
+
+void *ctx_buffer(eig_ctx_t ctx, int slot, size_t bytes)
+{
+  if ((int)ctx->pool.size() <= slot) ctx->pool.resize(slot + 1, {nullptr, 0});
+  auto &e = ctx->pool[slot];
+  if (e.second < bytes)
+  {
+    if (e.first) EIG_HIP(hipFree(e.first));
+    e.first = nullptr;
+    e.second = 0;
+    EIG_HIP(hipMalloc(&e.first, bytes));
+    e.second = bytes;
+  }
+  return e.first;
+}
+
+void allreduce_sum(eig_ctx_t ctx, double *buf, i64 count, hipStream_t s)
+{
+  if (!ctx->comm || ctx->nranks == 1) return;
+  EIG_NCCL(ncclAllReduce(buf, buf, (size_t)count, ncclDouble, ncclSum, ctx->comm, s));
+}
+
+// Exchange the ghost entries of the window-layout vector x.  Runs on stream s.
+void halo_exchange(const eig_mat_s &A, double *x, hipStream_t s)
+{
+  eig_ctx_t ctx = A.ctx;
+  if (!ctx->comm || ctx->nranks == 1 || (A.sends.empty() && A.recvs.empty())) return;
+  EIG_NCCL(ncclGroupStart());
+  for (const auto &r : A.recvs) EIG_NCCL(ncclRecv(x + r.offset, (size_t)r.count, ncclDouble, r.peer, ctx->comm, s));
+  for (const auto &r : A.sends) EIG_NCCL(ncclSend(x + r.offset, (size_t)r.count, ncclDouble, r.peer, ctx->comm, s));
+  EIG_NCCL(ncclGroupEnd());
+}
+
+// eigensolver.hh:49-55 generator (libstdc++ mt19937 + normal_distribution, bitwise the
+// reference's sequence).
+void host_random_normal(i64 count, unsigned seed, double *out)
+{
+  std::mt19937 urbg{seed};
+  std::normal_distribution<double> gen{0.0, 1.0};
+  for (i64 i = 0; i < count; ++i) out[i] = gen(urbg);
+}
+
+}  // namespace eigmi
+
+// ============================================================================================
+// context
+// ============================================================================================
+extern "C" int eig_device_count(int *count)
+{
+  return guard(nullptr, [&] {
+    EIG_CHECK(count, EIG_ERR_ARG, "eig_device_count: null");
+    int c = 0;
+    hipError_t e = hipGetDeviceCount(&c);
+    *count = (e == hipSuccess) ? c : 0;
+  });
+}
+
+extern "C" const char *eig_version(void) { return "eigmi 0.1 gfx950 (SELL-64 SpMV, MFMA f64 Gram, RCCL halo)"; }
+
+extern "C" int eig_ctx_create(int device, eig_ctx_t *out)
+{
+  return guard(nullptr, [&] {
+    EIG_CHECK(out, EIG_ERR_ARG, "eig_ctx_create: null output");
+    int c = 0;
+    if (hipGetDeviceCount(&c) != hipSuccess || c == 0) throw Error(EIG_ERR_NODEVICE, "no HIP device visible");
+    EIG_CHECK(device >= 0 && device < c, EIG_ERR_ARG, "eig_ctx_create: bad device index");
+    EIG_HIP(hipSetDevice(device));
+    auto *ctx = new eig_ctx_s();
+    ctx->device = device;
+    try
+    {
+      EIG_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+      EIG_HIP(hipStreamCreateWithFlags(&ctx->comm_stream, hipStreamNonBlocking));
+      hipDeviceProp_t prop;
+      EIG_HIP(hipGetDeviceProperties(&prop, device));
+      ctx->num_cu = prop.multiProcessorCount;
+      ctx->red.partials = dev_alloc<double>((size_t)kMaxRedBlocks * kMaxRedVals);
+      ctx->red.tickets = dev_alloc<unsigned>(kNumTickets);
+      EIG_HIP(hipMemset(ctx->red.tickets, 0, kNumTickets * sizeof(unsigned)));
+      ctx->scratch = dev_alloc<double>(4096);
+      EIG_HIP(hipMemset(ctx->scratch, 0, 4096 * sizeof(double)));
+    }
+    catch (...)
+    {
+      eig_ctx_destroy(ctx);
+      throw;
+    }
+    *out = ctx;
+  });
+}
+
+extern "C" int eig_ctx_destroy(eig_ctx_t ctx)
+{
+  if (!ctx) return EIG_OK;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
+  for (auto &e : ctx->pool)
+    if (e.first) (void)hipFree(e.first);
+  if (ctx->red.partials) (void)hipFree(ctx->red.partials);
+  if (ctx->red.tickets) (void)hipFree(ctx->red.tickets);
+  if (ctx->scratch) (void)hipFree(ctx->scratch);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  if (ctx->comm_stream) (void)hipStreamDestroy(ctx->comm_stream);
+  delete ctx;
+  return EIG_OK;
+}
+
+extern "C" const char *eig_last_error(eig_ctx_t ctx) { return ctx ? ctx->last_error.c_str() : g_tls_error.c_str(); }
+
+extern "C" int eig_ctx_sync(eig_ctx_t ctx)
+{
+  return guard(ctx, [&] {
+    EIG_CHECK(ctx, EIG_ERR_ARG, "null context");
+    EIG_HIP(hipStreamSynchronize(ctx->stream));
+  });
+}
+
+extern "C" int eig_ctx_stream(eig_ctx_t ctx, void **stream)
+{
+  return guard(ctx, [&] {
+    EIG_CHECK(ctx && stream, EIG_ERR_ARG, "null argument");
+    *stream = (void *)ctx->stream;
+  });
+}
+
+// ============================================================================================
+// communicator
+// ============================================================================================
+extern "C" int eig_comm_unique_id(unsigned char id[128])
+{
+  return guard(nullptr, [&] {
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+    ncclUniqueId u;
+    EIG_NCCL(ncclGetUniqueId(&u));
+    std::memcpy(id, &u, 128);
+  });
+}
+
+extern "C" int eig_comm_init(eig_ctx_t ctx, int nranks, int rank, const unsigned char id[128])
+{
+  return guard(ctx, [&] {
+    EIG_CHECK(ctx && id && nranks >= 1 && rank >= 0 && rank < nranks, EIG_ERR_ARG, "eig_comm_init: bad arguments");
+    DeviceGuard dg(ctx->device);
+    ncclUniqueId u;
+    std::memcpy(&u, id, 128);
+    EIG_NCCL(ncclCommInitRank(&ctx->comm, nranks, u, rank));
+    ctx->nranks = nranks;
+    ctx->rank = rank;
+  });
+}
+
+extern "C" int eig_comm_allreduce_sum(eig_ctx_t ctx, double *buf, int64_t count)
+{
+  return guard(ctx, [&] {
+    EIG_CHECK(ctx && buf && count >= 0, EIG_ERR_ARG, "eig_comm_allreduce_sum: bad arguments");
+    allreduce_sum(ctx, buf, count, ctx->stream);
+  });
+}
+
+extern "C" int eig_comm_barrier(eig_ctx_t ctx)
+{
+  return guard(ctx, [&] {
+    EIG_CHECK(ctx, EIG_ERR_ARG, "null context");
+    double *d = ctx->scratch + 4000;
+    EIG_HIP(hipMemsetAsync(d, 0, sizeof(double), ctx->stream));
+    allreduce_sum(ctx, d, 1, ctx->stream);
+    EIG_HIP(hipStreamSynchronize(ctx->stream));
+  });
+}
+
+// ============================================================================================
+// device memory
+// ============================================================================================
+extern "C" int eig_malloc(eig_ctx_t ctx, size_t bytes, void **ptr)
+{
+  return guard(ctx, [&] {
+    EIG_CHECK(ctx && ptr, EIG_ERR_ARG, "eig_malloc: null argument");
+    DeviceGuard dg(ctx->device);
+    EIG_HIP(hipMalloc(ptr, bytes ? bytes : 1));
+  });
+}
+extern "C" int eig_free(eig_ctx_t ctx, void *ptr)
+{
+  return guard(ctx, [&] {
+    EIG_CHECK(ctx, EIG_ERR_ARG, "null context");
+    if (ptr) EIG_HIP(hipFree(ptr));
+  });
+}
+extern "C" int eig_memcpy_h2d(eig_ctx_t ctx, void *dst, const void *src, size_t bytes)
+{
+  return guard(ctx, [&] {
+    EIG_CHECK(ctx, EIG_ERR_ARG, "null context");
+    EIG_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+    EIG_HIP(hipStreamSynchronize(ctx->stream));
+  });
+}
+extern "C" int eig_memcpy_d2h(eig_ctx_t ctx, void *dst, const void *src, size_t bytes)
+{
+  return guard(ctx, [&] {
+    EIG_CHECK(ctx, EIG_ERR_ARG, "null context");
+    EIG_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    EIG_HIP(hipStreamSynchronize(ctx->stream));
+  });
+}
+extern "C" int eig_memcpy_d2d(eig_ctx_t ctx, void *dst, const void *src, size_t bytes)
+{
+  return guard(ctx, [&] {
+    EIG_CHECK(ctx, EIG_ERR_ARG, "null context");
+    EIG_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, ctx->stream));
+  });
+}
+extern "C" int eig_memset(eig_ctx_t ctx, void *dst, int value, size_t bytes)
+{
+  return guard(ctx, [&] {
+    EIG_CHECK(ctx, EIG_ERR_ARG, "null context");
+    EIG_HIP(hipMemsetAsync(dst, value, bytes, ctx->stream));
+  });
+}
+
+// ============================================================================================
+// matrices
+// ============================================================================================
+namespace {
+
+// Build the SELL-64 image of `nb` block rows (rowptr/col/vals on the host, col already mapped to
+// window-local block columns by `colmap`) and upload it.
+void build_sell(eig_mat_s &A, i64 nb, const int64_t *rowptr, const int32_t *col, const double *vals, i64 col_shift)
+{
+  const int bb = A.br * A.bc;
+  const i64 ns = (nb + 63) / 64;
+  std::vector<i64> sp(ns + 1, 0);
+  for (i64 s = 0; s < ns; ++s)
+  {
+    i64 w = 0;
+    for (i64 r = s * 64; r < std::min(nb, s * 64 + 64); ++r) w = std::max<i64>(w, rowptr[r + 1] - rowptr[r]);
+    sp[s + 1] = sp[s] + 64 * w;
+  }
+  const i64 total = sp[ns];
+  std::vector<i32> cimg(std::max<i64>(total, 1));
+  std::vector<double> vimg(std::max<i64>(total * bb, 1));
+  // parallel fill over slice ranges
+  unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  if (ns < 4096) nt = 1;
+  auto work = [&](i64 s0, i64 s1) {
+    for (i64 s = s0; s < s1; ++s)
+    {
+      const i64 base = sp[s], w = (sp[s + 1] - base) / 64;
+      for (int l = 0; l < 64; ++l)
+      {
+        const i64 r = s * 64 + l;
+        const i64 len = (r < nb) ? rowptr[r + 1] - rowptr[r] : 0;
+        for (i64 k = 0; k < w; ++k)
+        {
+          const i64 ci = base + k * 64 + l;
+          if (k < len)
+          {
+            const i64 p = rowptr[r] + k;
+            cimg[ci] = (i32)(col[p] - col_shift);
+            for (int t = 0; t < bb; ++t) vimg[(base + k * 64) * bb + t * 64 + l] = vals[p * bb + t];
+          }
+          else
+          {
+            cimg[ci] = -1;
+            for (int t = 0; t < bb; ++t) vimg[(base + k * 64) * bb + t * 64 + l] = 0.0;
+          }
+        }
+      }
+    }
+  };
+  if (nt == 1) work(0, ns);
+  else
+  {
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < nt; ++t) th.emplace_back(work, ns * t / nt, ns * (t + 1) / nt);
+    for (auto &t : th) t.join();
+  }
+  A.nslices = ns;
+  A.nnzb_padded = total;
+  A.slice_ptr = dev_alloc<i64>(ns + 1);
+  A.col = dev_alloc<i32>(total);
+  A.val = dev_alloc<double>(total * bb);
+  hipStream_t s = A.ctx->stream;
+  EIG_HIP(hipMemcpyAsync(A.slice_ptr, sp.data(), (ns + 1) * sizeof(i64), hipMemcpyHostToDevice, s));
+  EIG_HIP(hipMemcpyAsync(A.col, cimg.data(), total * sizeof(i32), hipMemcpyHostToDevice, s));
+  EIG_HIP(hipMemcpyAsync(A.val, vimg.data(), total * bb * sizeof(double), hipMemcpyHostToDevice, s));
+  EIG_HIP(hipStreamSynchronize(s));
+  A.device_bytes = (ns + 1) * 8 + total * 4 + total * bb * 8;
+}
+
+void validate_csr(i64 nb, i64 ncols, const int64_t *rowptr, const int32_t *col)
+{
+  EIG_CHECK(rowptr[0] == 0, EIG_ERR_ARG, "rowptr[0] must be 0");
+  for (i64 r = 0; r < nb; ++r)
+  {
+    EIG_CHECK(rowptr[r + 1] >= rowptr[r], EIG_ERR_ARG, "rowptr must be non-decreasing");
+    for (i64 p = rowptr[r]; p < rowptr[r + 1]; ++p)
+    {
+      EIG_CHECK(col[p] >= 0 && col[p] < ncols, EIG_ERR_SHAPE, "column index out of range");
+      if (p > rowptr[r]) EIG_CHECK(col[p] > col[p - 1], EIG_ERR_ARG, "columns must be strictly ascending per row");
+    }
+  }
+}
+
+void destroy_mat(eig_mat_s *A)
+{
+  if (!A) return;
+  if (A->slice_ptr) (void)hipFree(A->slice_ptr);
+  if (A->col) (void)hipFree(A->col);
+  if (A->val) (void)hipFree(A->val);
+  if (A->slice_list) (void)hipFree(A->slice_list);
+  delete A;
+}
+
+}  // namespace
+
+extern "C" int eig_mat_create_bcsr(eig_ctx_t ctx, int64_t nb_rows, int64_t nb_cols, int br, int bc,
+                                   const int64_t *rowptr, const int32_t *col, const double *vals, eig_mat_t *out)
+{
+  return guard(ctx, [&] {
+    EIG_CHECK(ctx && out && rowptr && (rowptr[nb_rows] == 0 || (col && vals)), EIG_ERR_ARG,
+              "eig_mat_create_bcsr: null argument");
+    EIG_CHECK(nb_rows >= 0 && nb_cols >= 0, EIG_ERR_ARG, "eig_mat_create_bcsr: negative size");
+    EIG_CHECK(br >= 1 && br <= 4 && bc >= 1 && bc <= 4, EIG_ERR_BLOCKSIZE, "block size must be in 1..4");
+    EIG_CHECK(nb_cols * bc < (int64_t)INT32_MAX, EIG_ERR_SHAPE, "matrix too large for int32 column indices");
+    DeviceGuard dg(ctx->device);
+    validate_csr(nb_rows, nb_cols, rowptr, col);
+    auto *A = new eig_mat_s();
+    A->ctx = ctx;
+    A->br = br;
+    A->bc = bc;
+    A->nb_rows = A->nb_rows_global = nb_rows;
+    A->nb_cols = nb_cols;
+    A->row_begin = 0;
+    A->win_begin = 0;
+    A->window = nb_cols * bc;
+    A->own_offset = 0;
+    A->nnzb = rowptr[nb_rows];
+    try
+    {
+      build_sell(*A, nb_rows, rowptr, col, vals, 0);
+    }
+    catch (...)
+    {
+      destroy_mat(A);
+      throw;
+    }
+    *out = A;
+  });
+}
+
+extern "C" int eig_mat_create_bcsr_dist(eig_ctx_t ctx, int64_t nb_rows_global, int64_t row_begin,
+                                        int64_t nb_local, int br, int bc, const int64_t *rowptr, const int32_t *col,
+                                        const double *vals, eig_mat_t *out)
+{
+  return guard(ctx, [&] {
+    EIG_CHECK(ctx && out && rowptr, EIG_ERR_ARG, "eig_mat_create_bcsr_dist: null argument");
+    EIG_CHECK(br == bc && br >= 1 && br <= 4, EIG_ERR_BLOCKSIZE, "distributed matrices need square blocks 1..4");
+    EIG_CHECK(row_begin >= 0 && nb_local >= 0 && row_begin + nb_local <= nb_rows_global, EIG_ERR_SHAPE,
+              "eig_mat_create_bcsr_dist: row range outside the matrix");
+    EIG_CHECK(nb_rows_global * bc < (int64_t)INT32_MAX, EIG_ERR_SHAPE, "matrix too large for int32 column indices");
+    DeviceGuard dg(ctx->device);
+    validate_csr(nb_local, nb_rows_global, rowptr, col);
+    const int P = ctx->nranks, me = ctx->rank;
+    int64_t plan[5];
+    {
+      int rc = eig_plan_window(row_begin, nb_local, bc, rowptr, col, plan);
+      EIG_CHECK(rc == EIG_OK, rc, "eig_plan_window failed");
+    }
+    const i64 wb_blk = plan[0], cmin = plan[3], cmax = plan[4];
+    auto *A = new eig_mat_s();
+    A->ctx = ctx;
+    A->br = br;
+    A->bc = bc;
+    A->nb_rows = nb_local;
+    A->nb_rows_global = nb_rows_global;
+    A->nb_cols = nb_rows_global;
+    A->row_begin = row_begin;
+    A->win_begin = wb_blk * bc;
+    A->window = plan[1];
+    A->own_offset = plan[2];
+    A->nnzb = rowptr[nb_local];
+    try
+    {
+      build_sell(*A, nb_local, rowptr, col, vals, wb_blk);
+      // --- halo plan: allgather (row_begin, nb_local, cmin, cmax) of every rank ---
+      std::vector<i64> mine = {row_begin, nb_local, cmin, cmax};
+      std::vector<i64> all(4 * (size_t)P, 0);
+      if (ctx->comm && P > 1)
+      {
+        i64 *d = dev_alloc<i64>(4 * (size_t)P);
+        EIG_HIP(hipMemcpy(d + 4 * me, mine.data(), 4 * sizeof(i64), hipMemcpyHostToDevice));
+        EIG_NCCL(ncclAllGather(d + 4 * me, d, 4 * sizeof(i64), ncclChar, ctx->comm, ctx->stream));
+        EIG_HIP(hipStreamSynchronize(ctx->stream));
+        EIG_HIP(hipMemcpy(all.data(), d, 4 * P * sizeof(i64), hipMemcpyDeviceToHost));
+        (void)hipFree(d);
+      }
+      else
+      {
+        all = mine;
+      }
+      const int nr = (ctx->comm && P > 1) ? P : 1;
+      std::vector<int64_t> rv(3 * (size_t)nr), sd(3 * (size_t)nr);
+      int nrecv = 0, nsend = 0;
+      {
+        int rc = eig_plan_halo(nr, nr > 1 ? me : 0, all.data(), bc, wb_blk, rv.data(), &nrecv, sd.data(), &nsend);
+        EIG_CHECK(rc == EIG_OK, rc, "eig_plan_halo failed");
+      }
+      for (int k = 0; k < nrecv; ++k) A->recvs.push_back({(int)rv[3 * k], rv[3 * k + 1], rv[3 * k + 2]});
+      for (int k = 0; k < nsend; ++k) A->sends.push_back({(int)sd[3 * k], sd[3 * k + 1], sd[3 * k + 2]});
+      for (auto &r : A->recvs) A->halo_recv += r.count;
+      for (auto &r : A->sends) A->halo_send += r.count;
+      // interior / boundary slices: a slice is interior when every column is owned
+      std::vector<i32> inter, bound;
+      const i64 own_lo = row_begin, own_hi = row_begin + nb_local;
+      for (i64 s = 0; s < A->nslices; ++s)
+      {
+        bool in = true;
+        for (i64 r = s * 64; r < std::min(nb_local, s * 64 + 64) && in; ++r)
+          for (i64 p = rowptr[r]; p < rowptr[r + 1]; ++p)
+            if (col[p] < own_lo || col[p] >= own_hi)
+            {
+              in = false;
+              break;
+            }
+        (in ? inter : bound).push_back((i32)s);
+      }
+      A->n_interior = (i64)inter.size();
+      A->n_boundary = (i64)bound.size();
+      std::vector<i32> lst(inter);
+      lst.insert(lst.end(), bound.begin(), bound.end());
+      A->slice_list = dev_alloc<i32>(std::max<size_t>(lst.size(), 1));
+      if (!lst.empty()) EIG_HIP(hipMemcpy(A->slice_list, lst.data(), lst.size() * sizeof(i32), hipMemcpyHostToDevice));
+    }
+    catch (...)
+    {
+      destroy_mat(A);
+      throw;
+    }
+    *out = A;
+  });
+}
+
+extern "C" int eig_mat_destroy(eig_mat_t A)
+{
+  if (!A) return EIG_OK;
+  (void)hipSetDevice(A->ctx->device);
+  (void)hipStreamSynchronize(A->ctx->stream);
+  destroy_mat(A);
+  return EIG_OK;
+}
+
+extern "C" int eig_mat_get_info(eig_mat_t A, eig_mat_info *info)
+{
+  return guard(A ? A->ctx : nullptr, [&] {
+    EIG_CHECK(A && info, EIG_ERR_ARG, "null argument");
+    info->n = A->nb_rows * A->br;
+    info->n_global = A->nb_rows_global * A->br;
+    info->ncols = A->nb_cols * A->bc;
+    info->row_begin = A->row_begin * A->br;
+    info->window = A->window;
+    info->own_offset = A->own_offset;
+    info->nnzb = A->nnzb;
+    info->nnzb_padded = A->nnzb_padded;
+    info->nslices = A->nslices;
+    info->br = A->br;
+    info->bc = A->bc;
+    info->halo_recv = A->halo_recv;
+    info->halo_send = A->halo_send;
+    info->device_bytes = A->device_bytes;
+  });
+}
+
+extern "C" int eig_mat_shift_diag(eig_mat_t A, double shift)
+{
+  return guard(A ? A->ctx : nullptr, [&] {
+    EIG_CHECK(A, EIG_ERR_ARG, "null matrix");
+    EIG_CHECK(A->br == A->bc, EIG_ERR_BLOCKSIZE, "StandardLargest: blocks of input matrix must be square");
+    DeviceGuard dg(A->ctx->device);
+    launch_shift_diag(*A, shift, A->ctx->stream);
+  });
+}
+
+namespace eigmi {
+// y = A x with halo exchange overlapped with the interior slices when distributed.
+void mv_device(eig_mat_s &A, double *x, double *y)
+{
+  eig_ctx_t ctx = A.ctx;
+  if (!ctx->comm || ctx->nranks == 1 || (A.recvs.empty() && A.sends.empty()))
+  {
+    launch_spmv(A, x, y, nullptr, 0, A.nslices, ctx->stream);
+    return;
+  }
+  hipEvent_t e0, e1;
+  EIG_HIP(hipEventCreateWithFlags(&e0, hipEventDisableTiming));
+  EIG_HIP(hipEventCreateWithFlags(&e1, hipEventDisableTiming));
+  EIG_HIP(hipEventRecord(e0, ctx->stream));
+  EIG_HIP(hipStreamWaitEvent(ctx->comm_stream, e0, 0));
+  halo_exchange(A, x, ctx->comm_stream);
+  EIG_HIP(hipEventRecord(e1, ctx->comm_stream));
+  launch_spmv(A, x, y, A.slice_list, 0, A.n_interior, ctx->stream);
+  EIG_HIP(hipStreamWaitEvent(ctx->stream, e1, 0));
+  launch_spmv(A, x, y, A.slice_list, A.n_interior, A.n_boundary, ctx->stream);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+}
+}  // namespace eigmi
+
+extern "C" int eig_mv(eig_mat_t A, const double *x, double *y)
+{
+  return guard(A ? A->ctx : nullptr, [&] {
+    EIG_CHECK(A && x && y, EIG_ERR_ARG, "eig_mv: null argument");
+    DeviceGuard dg(A->ctx->device);
+    mv_device(*A, const_cast<double *>(x), y);
+  });
+}
+
+extern "C" int eig_mv_host(eig_mat_t A, const double *xh, double *yh)
+{
+  return guard(A ? A->ctx : nullptr, [&] {
+    EIG_CHECK(A && xh && yh, EIG_ERR_ARG, "eig_mv_host: null argument");
+    DeviceGuard dg(A->ctx->device);
+    eig_ctx_t ctx = A->ctx;
+    const size_t wb = (size_t)A->window * sizeof(double);
+    double *x = (double *)ctx_buffer(ctx, 0, wb);
+    double *y = (double *)ctx_buffer(ctx, 1, wb);
+    const i64 n = A->nb_rows * A->br;
+    if (A->nb_rows_global == A->nb_rows && (!ctx->comm || ctx->nranks == 1))
+    {
+      // square or rectangular single-rank operator: x has ncols entries
+      EIG_HIP(hipMemcpyAsync(x, xh, (size_t)A->nb_cols * A->bc * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+    }
+    else
+    {
+      EIG_HIP(hipMemsetAsync(x, 0, wb, ctx->stream));
+      EIG_HIP(hipMemcpyAsync(x + A->own_offset, xh, n * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+    }
+    mv_device(*A, x, y);
+    EIG_HIP(hipMemcpyAsync(yh, y + A->own_offset, n * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    EIG_HIP(hipStreamSynchronize(ctx->stream));
+  });
+}
+
+// ============================================================================================
+// BlockVector ops
+// ============================================================================================
+extern "C" int eig_dot(eig_ctx_t ctx, int64_t n, const double *x, const double *y, double *result)
+{
+  return guard(ctx, [&] {
+    EIG_CHECK(ctx && x && y && result && n >= 0, EIG_ERR_ARG, "eig_dot: bad argument");
+    DeviceGuard dg(ctx->device);
+    launch_dot(n, x, y, result, 0, ctx->stream, ctx->red);
+    allreduce_sum(ctx, result, 1, ctx->stream);
+  });
+}
+extern "C" int eig_nrm2(eig_ctx_t ctx, int64_t n, const double *x, double *result)
+{
+  return guard(ctx, [&] {
+    EIG_CHECK(ctx && x && result && n >= 0, EIG_ERR_ARG, "eig_nrm2: bad argument");
+    DeviceGuard dg(ctx->device);
+    launch_nrm2sq(n, x, result, 0, ctx->stream, ctx->red);
+    allreduce_sum(ctx, result, 1, ctx->stream);
+    launch_sqrt_inplace(result, 1, ctx->stream);
+  });
+}
+extern "C" int eig_axpy(eig_ctx_t ctx, int64_t n, double a, const double *x, double *y)
+{
+  return guard(ctx, [&] {
+    EIG_CHECK(ctx && x && y && n >= 0, EIG_ERR_ARG, "eig_axpy: bad argument");
+    DeviceGuard dg(ctx->device);
+    launch_axpy(n, a, x, y, ctx->stream);
+  });
+}
+extern "C" int eig_scal(eig_ctx_t ctx, int64_t n, double a, double *x)
+{
+  return guard(ctx, [&] {
+    EIG_CHECK(ctx && x && n >= 0, EIG_ERR_ARG, "eig_scal: bad argument");
+    DeviceGuard dg(ctx->device);
+    launch_scal(n, a, x, ctx->stream);
+  });
+}
+extern "C" int eig_copy(eig_ctx_t ctx, int64_t n, const double *x, double *y)
+{
+  return guard(ctx, [&] {
+    EIG_CHECK(ctx && x && y && n >= 0, EIG_ERR_ARG, "eig_copy: bad argument");
+    DeviceGuard dg(ctx->device);
+    EIG_HIP(hipMemcpyAsync(y, x, n * sizeof(double), hipMemcpyDeviceToDevice, ctx->stream));
+  });
+}
+
+// ============================================================================================
+// MultiVector<double,8>
+// ============================================================================================
+#define EIG_MV8_CHECK(m)                                                                             \
+  EIG_CHECK((m) % 8 == 0, EIG_ERR_SHAPE, "number of cols must be a multiple of block size");       \
+  EIG_CHECK((m) >= 0, EIG_ERR_ARG, "negative column count")
+
+extern "C" int eig_spmm_mv8(eig_mat_t A, int64_t m, const double *Qin, double *Qout)
+{
+  return guard(A ? A->ctx : nullptr, [&] {
+    EIG_CHECK(A && Qin && Qout, EIG_ERR_ARG, "eig_spmm_mv8: null argument");
+    EIG_MV8_CHECK(m);
+    EIG_CHECK(A->nb_rows == A->nb_cols && (!A->ctx->comm || A->ctx->nranks == 1), EIG_ERR_SHAPE,
+              "eig_spmm_mv8: square single-rank matrix required");
+    DeviceGuard dg(A->ctx->device);
+    if (m > 0) launch_spmm_mv8(*A, m, Qin, Qout, A->ctx->stream);
+  });
+}
+
+extern "C" int eig_dot_diag_mv8(eig_ctx_t ctx, int64_t n, int64_t m, const double *Q1, const double *Q2, double *dp)
+{
+  return guard(ctx, [&] {
+    EIG_CHECK(ctx && Q1 && Q2 && dp && n >= 0, EIG_ERR_ARG, "eig_dot_diag_mv8: bad argument");
+    EIG_MV8_CHECK(m);
+    DeviceGuard dg(ctx->device);
+    for (i64 b = 0; b < m; b += 8 * 32)
+    {
+      const i64 mm = std::min<i64>(m - b, 8 * 32);
+      launch_dot_diag_mv8(n, mm, Q1 + b * n, Q2 + b * n, dp + b, 0, ctx->stream, ctx->red);
+    }
+    allreduce_sum(ctx, dp, m, ctx->stream);
+  });
+}
+
+namespace eigmi {
+// G (m1 x m2 row-major) = Q1^T Q2, tiled so that one launch stays within the ticket pool.
+void gram_device(eig_ctx_t ctx, i64 n, i64 m1, i64 m2, const double *Q1, const double *Q2, double *G)
+{
+  // one launch per group of 16-column output tiles that fits 48 tickets
+  const i64 ti = (m1 + 15) / 16, tj = (m2 + 15) / 16;
+  if (ti * tj <= 48)
+  {
+    launch_gram_mv8(n, m1, m2, Q1, Q2, G, 0, ctx->stream, ctx->red);
+  }
+  else
+  {
+    // row panels of Q1 (16 columns each) against all of Q2 in chunks; write into a temp then scatter
+    EIG_CHECK(tj <= 48, EIG_ERR_ARG, "gram: Q2 too wide (> 768 columns)");
+    double *tmp = (double *)ctx_buffer(ctx, 2, (size_t)16 * m2 * sizeof(double));
+    for (i64 r = 0; r < m1; r += 16)
+    {
+      const i64 mr = std::min<i64>(16, m1 - r);
+      launch_gram_mv8(n, mr, m2, Q1 + r * n, Q2, tmp, 0, ctx->stream, ctx->red);
+      EIG_HIP(hipMemcpyAsync(G + r * m2, tmp, mr * m2 * sizeof(double), hipMemcpyDeviceToDevice, ctx->stream));
+    }
+  }
+  allreduce_sum(ctx, G, m1 * m2, ctx->stream);
+}
+
+void orthonormalize_device(eig_ctx_t ctx, i64 n, i64 m, double *Q, int variant)
+{
+  hipStream_t s = ctx->stream;
+  double *S = (double *)ctx_buffer(ctx, 3, 64 * sizeof(double));
+  double *U = S + 0;  // reused: Ssum for MGS, Gram for CholQR
+  double *U2 = (double *)ctx_buffer(ctx, 4, 64 * sizeof(double));
+  double *Sg = nullptr;
+  if (m > 8) Sg = (double *)ctx_buffer(ctx, 5, (size_t)8 * m * sizeof(double));
+  for (i64 bk = 0; bk < m; bk += 8)
+  {
+    double *Qb = Q + bk * n;
+    if (variant == EIG_ORTHO_MGS)
+    {
+      for (int k = 0; k <= 8; ++k)
+      {
+        launch_mgs_pass(n, Qb, k, S, 0, s, ctx->red);
+        if (k < 8) allreduce_sum(ctx, S + 8 * k, 8, s);
+      }
+    }
+    else
+    {
+      gram_device(ctx, n, 8, 8, Qb, Qb, U);
+      launch_cholqr_factor(U, U2, nullptr, 0, s);
+      launch_apply_upper(n, Qb, U2, s);
+    }
+    const i64 mrest = m - bk - 8;
+    if (mrest > 0)
+    {
+      gram_device(ctx, n, 8, mrest, Qb, Qb + 8 * n, Sg);
+      launch_project(n, mrest, Qb, Qb + 8 * n, Sg, s);
+    }
+  }
+}
+}  // namespace eigmi
+
+extern "C" int eig_gram_mv8(eig_ctx_t ctx, int64_t n, int64_t m1, int64_t m2, const double *Q1, const double *Q2,
+                            double *G)
+{
+  return guard(ctx, [&] {
+    EIG_CHECK(ctx && Q1 && Q2 && G && n >= 0, EIG_ERR_ARG, "eig_gram_mv8: bad argument");
+    EIG_MV8_CHECK(m1);
+    EIG_MV8_CHECK(m2);
+    DeviceGuard dg(ctx->device);
+    if (m1 > 0 && m2 > 0) gram_device(ctx, n, m1, m2, Q1, Q2, G);
+  });
+}
+
+extern "C" int eig_orthonormalize_mv8(eig_ctx_t ctx, int64_t n, int64_t m, double *Q, int variant)
+{
+  return guard(ctx, [&] {
+    EIG_CHECK(ctx && Q && n >= 0, EIG_ERR_ARG, "eig_orthonormalize_mv8: bad argument");
+    EIG_CHECK(variant == EIG_ORTHO_MGS || variant == EIG_ORTHO_CHOLQR, EIG_ERR_ARG, "unknown variant");
+    EIG_MV8_CHECK(m);
+    DeviceGuard dg(ctx->device);
+    orthonormalize_device(ctx, n, m, Q, variant);
+  });
+}
+
+extern "C" int eig_orthonormalize_naive(eig_ctx_t ctx, int64_t n, int64_t m, double *Q)
+{
+  return guard(ctx, [&] {
+    EIG_CHECK(ctx && Q && n >= 0 && m >= 0, EIG_ERR_ARG, "eig_orthonormalize_naive: bad argument");
+    EIG_CHECK(m <= 512, EIG_ERR_ARG, "eig_orthonormalize_naive: at most 512 columns");
+    DeviceGuard dg(ctx->device);
+    hipStream_t s = ctx->stream;
+    double *d = (double *)ctx_buffer(ctx, 6, (size_t)(m + 1) * sizeof(double));
+    // kernels_cpp.hh:128-154: normalise q_k, then q_j -= (q_k . q_j) q_k for every j > k.
+    for (i64 k = 0; k < m; ++k)
+    {
+      double *qk = Q + k * n;
+      launch_nrm2sq(n, qk, d + m, 0, s, ctx->red);
+      allreduce_sum(ctx, d + m, 1, s);
+      launch_scal_dev(n, d + m, true, qk, s);
+      const i64 rest = m - k - 1;
+      for (i64 j0 = 0; j0 < rest; j0 += 8 * 48)
+      {
+        const int kk = (int)std::min<i64>(rest - j0, 8 * 48);
+        launch_gemv_t(n, kk, Q + (k + 1 + j0) * n, n, qk, d + j0, 0, s, ctx->red);
+      }
+      allreduce_sum(ctx, d, rest, s);
+      // q_j -= d_j q_k : rank-1 update, one axpy per column (same rounding as the reference)
+      for (i64 j = 0; j < rest; ++j) launch_axpy_dev(n, d + j, -1.0, qk, Q + (k + 1 + j) * n, s);
+    }
+  });
+}
+
+extern "C" int eig_b_orthonormalize_mv8(eig_mat_t B, int64_t m, double *Q, double *norm)
+{
+  return guard(B ? B->ctx : nullptr, [&] {
+    EIG_CHECK(B && Q && norm, EIG_ERR_ARG, "eig_b_orthonormalize_mv8: null argument");
+    EIG_CHECK(B->br == 1 && B->bc == 1, EIG_ERR_BLOCKSIZE,
+              "B_orthonormalize_blocked: only implemented for FieldMatrix<..,1,1>");
+    EIG_MV8_CHECK(m);
+    EIG_CHECK(!B->ctx->comm || B->ctx->nranks == 1, EIG_ERR_ARG, "eig_b_orthonormalize_mv8: single rank only");
+    eig_ctx_t ctx = B->ctx;
+    DeviceGuard dg(ctx->device);
+    hipStream_t s = ctx->stream;
+    const i64 n = B->nb_rows;
+    double *P = (double *)ctx_buffer(ctx, 7, (size_t)n * 8 * sizeof(double));
+    double *G = (double *)ctx_buffer(ctx, 3, 64 * sizeof(double));
+    double *U = (double *)ctx_buffer(ctx, 4, 64 * sizeof(double));
+    double *Sg = m > 8 ? (double *)ctx_buffer(ctx, 5, (size_t)8 * m * sizeof(double)) : nullptr;
+    EIG_HIP(hipMemsetAsync(norm, 0, sizeof(double), s));
+    for (i64 bk = 0; bk < m; bk += 8)
+    {
+      double *Qb = Q + bk * n;
+      launch_spmm_mv8(*B, 8, Qb, P, s);                  // P = B Q_bk          (:378-395)
+      gram_device(ctx, n, 8, 8, P, Qb, G);               // s = P^T Q_bk        (:450-456)
+      launch_cholqr_factor(G, U, norm, 1, s);            // mirror upper, norm, U (:457-526)
+      launch_apply_upper(n, Qb, U, s);                   // Q_bk := Q_bk U      (:528-539)
+      launch_apply_upper(n, P, U, s);                    // P := P U            (:540-552)
+      const i64 mrest = m - bk - 8;
+      if (mrest > 0)
+      {
+        gram_device(ctx, n, 8, mrest, P, Qb + 8 * n, Sg);  // S = P^T Q_bj     (:559-565)
+        launch_max_offdiag(Sg, 8, mrest, false, norm, s);  // norm (:566-568)
+        launch_project(n, mrest, Qb, Qb + 8 * n, Sg, s);   // Q_bj -= Q_bk S   (:570-584)
+      }
+    }
+  });
+}
+
+extern "C" int eig_random_mv8(eig_ctx_t ctx, int64_t n, int64_t m, unsigned seed, double *Q)
+{
+  return guard(ctx, [&] {
+    EIG_CHECK(ctx && Q && n >= 0, EIG_ERR_ARG, "eig_random_mv8: bad argument");
+    EIG_MV8_CHECK(m);
+    DeviceGuard dg(ctx->device);
+    std::vector<double> h((size_t)(n * m));
+    // (block, row, col) fill order == the flat block-column-major order
+    host_random_normal(n * m, seed, h.data());
+    EIG_HIP(hipMemcpyAsync(Q, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+    EIG_HIP(hipStreamSynchronize(ctx->stream));
+  });
+}
+
+extern "C" double eig_flops_orthonormalize(int64_t n, int64_t m)
+{
+  // kernels_cpp.hh:98-106
+  double f = 0.0;
+  for (i64 k = m; k > 0; k--) f += 2.0 * n + n + (k - 1) * 4.0 * n;
+  return f;
+}
+
+extern "C" double eig_bytes_orthonormalize_blocked(int64_t n, int64_t m, int b)
+{
+  // kernels_cpp.hh:157-175
+  double c = 0.0;
+  for (i64 bk = 0; bk < m; bk += b)
+  {
+    for (int k = b; k > 0; k--) c += (double)n * k + (double)n * (1 + (k - 1) + 1);
+    for (i64 bj = bk + b; bj < m; bj += b) c += 5.0 * b * n;
+  }
+  return c * 8;
+}
+
+// ============================================================================================
+// partition planning (host only)
+// ============================================================================================
+extern "C" int eig_plan_window(int64_t row_begin, int64_t nb_local, int bc, const int64_t *rowptr,
+                               const int32_t *col, int64_t out[5])
+{
+  if (!rowptr || !out || nb_local < 0 || row_begin < 0 || bc < 1) return EIG_ERR_ARG;
+  if (rowptr[nb_local] > 0 && !col) return EIG_ERR_ARG;
+  i64 cmin = row_begin, cmax = row_begin + nb_local;  // [cmin, cmax) in block columns
+  for (i64 p = 0; p < rowptr[nb_local]; ++p)
+  {
+    cmin = std::min<i64>(cmin, col[p]);
+    cmax = std::max<i64>(cmax, (i64)col[p] + 1);
+  }
+  const i64 lo = row_begin - cmin;
+  const i64 pad = (8 - lo % 8) % 8;  // (lo + pad) * bc is a multiple of 8 scalar entries
+  const i64 wb = cmin - pad;
+  i64 wlen = (cmax - wb) * bc;
+  wlen = (wlen + 7) / 8 * 8;
+  out[0] = wb;
+  out[1] = wlen;
+  out[2] = (row_begin - wb) * bc;
+  out[3] = cmin;
+  out[4] = cmax;
+  return EIG_OK;
+}
+
+extern "C" int eig_plan_halo(int nranks, int me, const int64_t *ranks, int bc, int64_t wb_blk, int64_t *recv,
+                             int *nrecv, int64_t *send, int *nsend)
+{
+  if (!ranks || !recv || !send || !nrecv || !nsend || nranks < 1 || me < 0 || me >= nranks) return EIG_ERR_ARG;
+  const i64 rb0 = ranks[4 * me], nl = ranks[4 * me + 1], cmin = ranks[4 * me + 2], cmax = ranks[4 * me + 3];
+  int nr = 0, ns = 0;
+  for (int q = 0; q < nranks; ++q)
+  {
+    if (q == me) continue;
+    const i64 qb = ranks[4 * q], qe = ranks[4 * q] + ranks[4 * q + 1];
+    // receive from q: q's rows inside my window
+    const i64 rb = std::max(qb, cmin), re = std::min(qe, cmax);
+    if (re > rb)
+    {
+      recv[3 * nr] = q;
+      recv[3 * nr + 1] = (rb - wb_blk) * bc;
+      recv[3 * nr + 2] = (re - rb) * bc;
+      ++nr;
+    }
+    // send to q: my rows inside q's referenced range
+    const i64 qwb = ranks[4 * q + 2], qwe = ranks[4 * q + 3];
+    const i64 sb = std::max(rb0, qwb), se = std::min(rb0 + nl, qwe);
+    if (se > sb)
+    {
+      send[3 * ns] = q;
+      send[3 * ns + 1] = (sb - wb_blk) * bc;
+      send[3 * ns + 2] = (se - sb) * bc;
+      ++ns;
+    }
+  }
+  *nrecv = nr;
+  *nsend = ns;
+  return EIG_OK;
+}

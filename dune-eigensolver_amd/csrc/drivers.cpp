@@ -1,0 +1,524 @@
+// drivers.cpp -- host drivers over the device kernels:
+//   eig_standard_largest  StandardLargest subspace iteration (eigensolver.hh:28-112)
+//   eig_lanczos_run       the Lanczos three-term recurrence ARPACK's dsaupd runs around multMv
+//                         (arpack_geneo_wrapper.hh:257-279, :621-632) -- the benchmark unit
+//   eig_lanczos_solve     Lanczos with full (DGKS / CGS2) re-orthogonalisation + Ritz extraction
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <numeric>
+#include <vector>
+
+#include "internal.h"
+
+using namespace eigmi;
+
+namespace {
+
+thread_local std::string g_drv_error;
+
+template <class F>
+int guard(eig_ctx_t ctx, F &&f)
+{
+  try
+  {
+    f();
+    return EIG_OK;
+  }
+  catch (const Error &e)
+  {
+    (ctx ? ctx->last_error : g_drv_error) = e.what();
+    return e.code;
+  }
+  catch (const std::exception &e)
+  {
+    (ctx ? ctx->last_error : g_drv_error) = e.what();
+    return EIG_ERR_ARG;
+  }
+}
+
+struct DevBuf {
+  void *p = nullptr;
+  explicit DevBuf(size_t bytes) { EIG_HIP(hipMalloc(&p, bytes ? bytes : 1)); }
+  ~DevBuf()
+  {
+    if (p) (void)hipFree(p);
+  }
+  DevBuf(const DevBuf &) = delete;
+  DevBuf &operator=(const DevBuf &) = delete;
+  double *d() const { return static_cast<double *>(p); }
+};
+
+bool distributed(const eig_mat_s &A) { return A.ctx->comm && A.ctx->nranks > 1; }
+
+// ---------------------------------------------------------------------------------------------
+// Symmetric tridiagonal eigenproblem (implicit QL with Wilkinson shifts).  d[k] diagonal,
+// e[k-1] off-diagonal; on return d holds the eigenvalues (ascending) and Z (k x k, column j =
+// eigenvector j, row-major Z[i*k + j]).
+// ---------------------------------------------------------------------------------------------
+void tridiag_eig(int k, std::vector<double> &d, std::vector<double> e, std::vector<double> &Z)
+{
+  Z.assign((size_t)k * k, 0.0);
+  for (int i = 0; i < k; ++i) Z[(size_t)i * k + i] = 1.0;
+  e.resize(k, 0.0);
+  if (k > 0) e[k - 1] = 0.0;
+  const double eps = 2.220446049250313e-16;
+  for (int l = 0; l < k; ++l)
+  {
+    int iter = 0, m;
+    do
+    {
+      for (m = l; m < k - 1; ++m)
+      {
+        const double dd = std::fabs(d[m]) + std::fabs(d[m + 1]);
+        if (std::fabs(e[m]) <= eps * dd) break;
+      }
+      if (m != l)
+      {
+        if (iter++ == 100) throw Error(EIG_ERR_BREAKDOWN, "tridiagonal QL did not converge");
+        double g = (d[l + 1] - d[l]) / (2.0 * e[l]);
+        double r = std::hypot(g, 1.0);
+        g = d[m] - d[l] + e[l] / (g + std::copysign(r, g));
+        double s = 1.0, c = 1.0, p = 0.0;
+        int i;
+        for (i = m - 1; i >= l; --i)
+        {
+          double f = s * e[i], b = c * e[i];
+          e[i + 1] = (r = std::hypot(f, g));
+          if (r == 0.0)
+          {
+            d[i + 1] -= p;
+            e[m] = 0.0;
+            break;
+          }
+          s = f / r;
+          c = g / r;
+          g = d[i + 1] - p;
+          r = (d[i] - g) * s + 2.0 * c * b;
+          d[i + 1] = g + (p = s * r);
+          g = c * r - b;
+          for (int q = 0; q < k; ++q)
+          {
+            f = Z[(size_t)q * k + i + 1];
+            Z[(size_t)q * k + i + 1] = s * Z[(size_t)q * k + i] + c * f;
+            Z[(size_t)q * k + i] = c * Z[(size_t)q * k + i] - s * f;
+          }
+        }
+        if (r == 0.0 && i >= l) continue;
+        d[l] -= p;
+        e[l] = g;
+        e[m] = 0.0;
+      }
+    } while (m != l);
+  }
+  // sort ascending with vectors
+  std::vector<int> idx(k);
+  std::iota(idx.begin(), idx.end(), 0);
+  std::sort(idx.begin(), idx.end(), [&](int a, int b) { return d[a] < d[b]; });
+  std::vector<double> d2(k), Z2((size_t)k * k);
+  for (int j = 0; j < k; ++j)
+  {
+    d2[j] = d[idx[j]];
+    for (int q = 0; q < k; ++q) Z2[(size_t)q * k + j] = Z[(size_t)q * k + idx[j]];
+  }
+  d.swap(d2);
+  Z.swap(Z2);
+}
+
+}  // namespace
+
+// ============================================================================================
+// a12: StandardLargest (eigensolver.hh:28-112)
+// ============================================================================================
+extern "C" int eig_standard_largest(eig_mat_t A, double shift, double tol, int maxiter, int nev, unsigned seed,
+                                    double *eval_host, double *evec_host, int *iters, int verbose)
+{
+  return guard(A ? A->ctx : nullptr, [&] {
+    EIG_CHECK(A && eval_host && nev > 0, EIG_ERR_ARG, "eig_standard_largest: bad argument");
+    EIG_CHECK(A->br == A->bc, EIG_ERR_ARG, "StandardLargest: blocks of input matrix must be square");
+    EIG_CHECK(A->br == 1, EIG_ERR_BLOCKSIZE,
+              "matmul_sparse_tallskinny_blocked: only implemented for FieldMatrix<..,1,1>");
+    EIG_CHECK(!distributed(*A), EIG_ERR_ARG, "eig_standard_largest: single rank only");
+    eig_ctx_t ctx = A->ctx;
+    EIG_HIP(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    const i64 n = A->nb_rows;
+    const i64 m = (nev / 8 + std::min(nev % 8, 1)) * 8;  // eigensolver.hh:43
+    DevBuf Q1b(n * m * 8), Q2b(n * m * 8), dpb(m * 8);
+    double *Q1 = Q1b.d(), *Q2 = Q2b.d();
+    {
+      std::vector<double> h((size_t)(n * m));
+      host_random_normal(n * m, seed, h.data());  // eigensolver.hh:50-55
+      EIG_HIP(hipMemcpyAsync(Q1, h.data(), h.size() * 8, hipMemcpyHostToDevice, s));
+      EIG_HIP(hipStreamSynchronize(s));
+    }
+    if (shift != 0.0) launch_shift_diag(*A, shift, s);  // eigensolver.hh:59-66
+    orthonormalize_device(ctx, n, m, Q1, EIG_ORTHO_MGS); // eigensolver.hh:69
+    std::vector<double> s1(m, 0.0), s2(m, 0.0);
+    int kk = 1;
+    for (int k = 1; k < maxiter; ++k)
+    {
+      kk = k;
+      launch_spmm_mv8(*A, m, Q1, Q2, s);                 // :78
+      orthonormalize_device(ctx, n, m, Q2, EIG_ORTHO_MGS); // :81
+      launch_spmm_mv8(*A, m, Q2, Q1, s);                 // :84
+      launch_dot_diag_mv8(n, m, Q2, Q1, dpb.d(), 0, s, ctx->red);  // :85
+      EIG_HIP(hipMemcpyAsync(s1.data(), dpb.d(), m * 8, hipMemcpyDeviceToHost, s));
+      EIG_HIP(hipStreamSynchronize(s));
+      for (auto &x : s1) x -= shift;
+      double dist = 0.0;
+      for (i64 i = 0; i < m; ++i) dist = std::max(dist, std::fabs(s1[i] - s2[i]));
+      if (verbose > 0 && k > 1) fprintf(stdout, "Iter=%d %.17g\n", k, dist);
+      std::swap(s1, s2);
+      std::swap(Q1, Q2);
+      if (k > 1 && dist < tol) break;
+    }
+    for (int j = 0; j < nev; ++j) eval_host[j] = s2[j];
+    if (evec_host)
+    {
+      // evec[j][i] = Q1(i, j): column j sits at Q1 + (j/8)*8n + i*8 + j%8
+      std::vector<double> h((size_t)(n * m));
+      EIG_HIP(hipMemcpyAsync(h.data(), Q1, h.size() * 8, hipMemcpyDeviceToHost, s));
+      EIG_HIP(hipStreamSynchronize(s));
+      for (int j = 0; j < nev; ++j)
+        for (i64 i = 0; i < n; ++i) evec_host[(i64)j * n + i] = h[((j / 8) * n + i) * 8 + j % 8];
+    }
+    if (iters) *iters = kk;
+  });
+}
+
+// ============================================================================================
+// Lanczos three-term recurrence (DESIGN.md "Lanczos step")
+// ============================================================================================
+namespace {
+
+struct LanczosBufs {
+  DevBuf scal;
+  LanczosState st;
+  double *carry;
+  explicit LanczosBufs(int steps) : scal((size_t)(4 * (steps + 2) + 8) * sizeof(double))
+  {
+    double *b = scal.d();
+    st.dsum = b;
+    st.nsum = b + (steps + 2);
+    st.alpha = b + 2 * (steps + 2);
+    st.beta = b + 3 * (steps + 2);
+    carry = b + 4 * (steps + 2);
+  }
+};
+
+// One step j: t = A u sig - gam up (+ dot), allreduce, u_{j+1} = t - alpha sig u (+ norm), allreduce.
+// Optional event timing: ev[0..5] = before K1, after K1, after allreduce 1, after K2, after allreduce 2.
+void lanczos_step(eig_mat_s &A, double *u, double *up, double *t, int j, LanczosBufs &lb, hipEvent_t *ev,
+                  hipEvent_t halo_ev0, hipEvent_t halo_ev1)
+{
+  eig_ctx_t ctx = A.ctx;
+  hipStream_t s = ctx->stream;
+  const i64 own = A.own_offset;
+  const i64 n = A.nb_rows;
+  if (ev) EIG_HIP(hipEventRecord(ev[0], s));
+  if (!distributed(A) || (A.recvs.empty() && A.sends.empty()))
+  {
+    launch_lanczos_spmv(A, u, up, t, j, lb.st, nullptr, 0, A.nslices, lb.st.dsum + j, lb.st.beta + j, nullptr, 0, s,
+                        ctx->red);
+  }
+  else
+  {
+    // halo of u on the comm stream, interior slices meanwhile, boundary slices after
+    EIG_HIP(hipEventRecord(halo_ev0, s));
+    EIG_HIP(hipStreamWaitEvent(ctx->comm_stream, halo_ev0, 0));
+    halo_exchange(A, u, ctx->comm_stream);
+    EIG_HIP(hipEventRecord(halo_ev1, ctx->comm_stream));
+    const bool has_in = A.n_interior > 0, has_bd = A.n_boundary > 0;
+    if (has_in)
+      launch_lanczos_spmv(A, u, up, t, j, lb.st, A.slice_list, 0, A.n_interior,
+                          has_bd ? lb.carry : lb.st.dsum + j, lb.st.beta + j, nullptr, 0, s, ctx->red);
+    EIG_HIP(hipStreamWaitEvent(s, halo_ev1, 0));
+    if (has_bd)
+      launch_lanczos_spmv(A, u, up, t, j, lb.st, A.slice_list, A.n_interior, A.n_boundary, lb.st.dsum + j,
+                          lb.st.beta + j, has_in ? lb.carry : nullptr, 0, s, ctx->red);
+  }
+  if (ev) EIG_HIP(hipEventRecord(ev[1], s));
+  allreduce_sum(ctx, lb.st.dsum + j, 1, s);
+  if (ev) EIG_HIP(hipEventRecord(ev[2], s));
+  launch_lanczos_update(n, u + own, t + own, j, lb.st, 0, s, ctx->red);
+  if (ev) EIG_HIP(hipEventRecord(ev[3], s));
+  allreduce_sum(ctx, lb.st.nsum + j + 1, 1, s);
+  if (ev) EIG_HIP(hipEventRecord(ev[4], s));
+}
+
+// Start vector into the owned rows of a zeroed window buffer: u0 (device, window layout) or
+// mt19937(seed) normal numbers for the GLOBAL vector, of which this rank keeps its rows.
+void init_start(eig_mat_s &A, double *U0, const double *u0, unsigned seed)
+{
+  eig_ctx_t ctx = A.ctx;
+  hipStream_t s = ctx->stream;
+  EIG_HIP(hipMemsetAsync(U0, 0, A.window * sizeof(double), s));
+  const i64 n = A.nb_rows * A.br;
+  if (u0)
+  {
+    EIG_HIP(hipMemcpyAsync(U0 + A.own_offset, u0 + A.own_offset, n * sizeof(double), hipMemcpyDeviceToDevice, s));
+  }
+  else
+  {
+    const i64 first = A.row_begin * A.br;
+    std::vector<double> h((size_t)(first + n));
+    host_random_normal(first + n, seed, h.data());
+    EIG_HIP(hipMemcpyAsync(U0 + A.own_offset, h.data() + first, n * sizeof(double), hipMemcpyHostToDevice, s));
+    EIG_HIP(hipStreamSynchronize(s));
+  }
+}
+
+}  // namespace
+
+struct eig_lanczos_s {
+  eig_mat_s *A = nullptr;
+  int max_steps = 0, k = 0;
+  DevBuf *B[3] = {nullptr, nullptr, nullptr};
+  LanczosBufs *lb = nullptr;
+  hipEvent_t h0 = nullptr, h1 = nullptr;
+  ~eig_lanczos_s()
+  {
+    for (auto *b : B) delete b;
+    delete lb;
+    if (h0) (void)hipEventDestroy(h0);
+    if (h1) (void)hipEventDestroy(h1);
+  }
+};
+
+namespace {
+
+void check_lanczos_matrix(const eig_mat_s *A)
+{
+  EIG_CHECK(A->br == 1 && A->bc == 1, EIG_ERR_BLOCKSIZE, "Lanczos driver: 1x1 blocks only");
+  EIG_CHECK(A->nb_rows_global == A->nb_cols, EIG_ERR_SHAPE, "Lanczos needs a square matrix");
+}
+
+}  // namespace
+
+extern "C" int eig_lanczos_create(eig_mat_t A, int max_steps, const double *u0, unsigned seed, eig_lanczos_t *out)
+{
+  return guard(A ? A->ctx : nullptr, [&] {
+    EIG_CHECK(A && out && max_steps >= 0, EIG_ERR_ARG, "eig_lanczos_create: bad argument");
+    check_lanczos_matrix(A);
+    eig_ctx_t ctx = A->ctx;
+    EIG_HIP(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    auto *ws = new eig_lanczos_s();
+    try
+    {
+      ws->A = A;
+      ws->max_steps = max_steps;
+      const size_t wb = (size_t)A->window * sizeof(double);
+      for (auto &b : ws->B) b = new DevBuf(wb);
+      EIG_HIP(hipMemsetAsync(ws->B[1]->d(), 0, wb, s));
+      EIG_HIP(hipMemsetAsync(ws->B[2]->d(), 0, wb, s));
+      init_start(*A, ws->B[0]->d(), u0, seed);
+      ws->lb = new LanczosBufs(max_steps);
+      launch_nrm2sq(A->nb_rows, ws->B[0]->d() + A->own_offset, ws->lb->st.nsum, 0, s, ctx->red);
+      allreduce_sum(ctx, ws->lb->st.nsum, 1, s);
+      EIG_HIP(hipEventCreateWithFlags(&ws->h0, hipEventDisableTiming));
+      EIG_HIP(hipEventCreateWithFlags(&ws->h1, hipEventDisableTiming));
+      EIG_HIP(hipStreamSynchronize(s));
+    }
+    catch (...)
+    {
+      delete ws;
+      throw;
+    }
+    *out = ws;
+  });
+}
+
+extern "C" int eig_lanczos_step(eig_lanczos_t ws, int steps, int flags, eig_timing *timing)
+{
+  return guard(ws ? ws->A->ctx : nullptr, [&] {
+    EIG_CHECK(ws && steps >= 0, EIG_ERR_ARG, "eig_lanczos_step: bad argument");
+    EIG_CHECK(ws->k + steps <= ws->max_steps, EIG_ERR_ARG, "eig_lanczos_step: more steps than max_steps");
+    EIG_CHECK((flags & ~EIG_LANCZOS_TIME_KERNELS) == 0, EIG_ERR_ARG, "eig_lanczos_step: unknown flag");
+    eig_mat_s &A = *ws->A;
+    eig_ctx_t ctx = A.ctx;
+    EIG_HIP(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    const bool timed = (flags & EIG_LANCZOS_TIME_KERNELS) != 0;
+    std::vector<hipEvent_t> ev;
+    hipEvent_t tbeg, tend;
+    EIG_HIP(hipEventCreate(&tbeg));
+    EIG_HIP(hipEventCreate(&tend));
+    if (timed)
+    {
+      ev.resize((size_t)5 * steps);
+      for (auto &e : ev) EIG_HIP(hipEventCreate(&e));
+    }
+    double *U[3] = {ws->B[0]->d(), ws->B[1]->d(), ws->B[2]->d()};
+    EIG_HIP(hipEventRecord(tbeg, s));
+    for (int i = 0; i < steps; ++i)
+    {
+      const int j = ws->k + i;
+      lanczos_step(A, U[j % 3], U[(j + 2) % 3], U[(j + 1) % 3], j, *ws->lb, timed ? &ev[(size_t)5 * i] : nullptr,
+                   ws->h0, ws->h1);
+    }
+    EIG_HIP(hipEventRecord(tend, s));
+    EIG_HIP(hipStreamSynchronize(s));
+    ws->k += steps;
+    if (timing)
+    {
+      std::memset(timing, 0, sizeof(*timing));
+      float ms = 0.f;
+      EIG_HIP(hipEventElapsedTime(&ms, tbeg, tend));
+      timing->total_ms = ms;
+      if (timed)
+      {
+        for (int i = 0; i < steps; ++i)
+        {
+          hipEvent_t *e = &ev[(size_t)5 * i];
+          float a = 0, b = 0, c = 0, d = 0;
+          EIG_HIP(hipEventElapsedTime(&a, e[0], e[1]));
+          EIG_HIP(hipEventElapsedTime(&b, e[1], e[2]));
+          EIG_HIP(hipEventElapsedTime(&c, e[2], e[3]));
+          EIG_HIP(hipEventElapsedTime(&d, e[3], e[4]));
+          timing->spmv_ms += a;
+          timing->comm_ms += b + d;
+          timing->update_ms += c;
+        }
+        timing->spmv_launches = steps;
+      }
+    }
+    for (auto &e : ev) (void)hipEventDestroy(e);
+    (void)hipEventDestroy(tbeg);
+    (void)hipEventDestroy(tend);
+  });
+}
+
+extern "C" int eig_lanczos_tridiag(eig_lanczos_t ws, int *k, double *alpha_host, double *beta_host)
+{
+  return guard(ws ? ws->A->ctx : nullptr, [&] {
+    EIG_CHECK(ws, EIG_ERR_ARG, "eig_lanczos_tridiag: null workspace");
+    eig_ctx_t ctx = ws->A->ctx;
+    EIG_HIP(hipSetDevice(ctx->device));
+    launch_beta_tail(ws->lb->st, ws->k, ctx->stream);
+    EIG_HIP(hipStreamSynchronize(ctx->stream));
+    if (k) *k = ws->k;
+    if (alpha_host && ws->k > 0)
+      EIG_HIP(hipMemcpy(alpha_host, ws->lb->st.alpha, ws->k * sizeof(double), hipMemcpyDeviceToHost));
+    if (beta_host) EIG_HIP(hipMemcpy(beta_host, ws->lb->st.beta, (ws->k + 1) * sizeof(double), hipMemcpyDeviceToHost));
+  });
+}
+
+extern "C" int eig_lanczos_destroy(eig_lanczos_t ws)
+{
+  if (!ws) return EIG_OK;
+  (void)hipSetDevice(ws->A->ctx->device);
+  (void)hipStreamSynchronize(ws->A->ctx->stream);
+  delete ws;
+  return EIG_OK;
+}
+
+extern "C" int eig_lanczos_run(eig_mat_t A, int steps, const double *u0, unsigned seed, int flags, double *alpha_host,
+                               double *beta_host, eig_timing *timing)
+{
+  eig_lanczos_t ws = nullptr;
+  int rc = eig_lanczos_create(A, steps, u0, seed, &ws);
+  if (rc != EIG_OK) return rc;
+  rc = eig_lanczos_step(ws, steps, flags, timing);
+  if (rc == EIG_OK) rc = eig_lanczos_tridiag(ws, nullptr, alpha_host, beta_host);
+  eig_lanczos_destroy(ws);
+  return rc;
+}
+
+// ============================================================================================
+// Lanczos eigensolver with full re-orthogonalisation
+// ============================================================================================
+extern "C" int eig_lanczos_solve(eig_mat_t A, int nev, int ncv, int which, unsigned seed, double *eval_host,
+                                 double *evec_host, double *resid_host)
+{
+  return guard(A ? A->ctx : nullptr, [&] {
+    EIG_CHECK(A && eval_host && nev > 0 && ncv >= nev && ncv <= 512, EIG_ERR_ARG,
+              "eig_lanczos_solve: need 0 < nev <= ncv <= 512");
+    EIG_CHECK(which == EIG_WHICH_LA || which == EIG_WHICH_SA, EIG_ERR_ARG, "eig_lanczos_solve: bad `which`");
+    EIG_CHECK(A->br == 1 && A->bc == 1, EIG_ERR_BLOCKSIZE, "Lanczos driver: 1x1 blocks only");
+    EIG_CHECK(A->nb_rows_global == A->nb_cols, EIG_ERR_SHAPE, "Lanczos needs a square matrix");
+    EIG_CHECK(ncv <= A->nb_rows_global, EIG_ERR_SHAPE, "ncv larger than the matrix");
+    eig_ctx_t ctx = A->ctx;
+    EIG_HIP(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    const i64 W = A->window, own = A->own_offset, n = A->nb_rows;
+    DevBuf Vb((size_t)(ncv + 1) * W * sizeof(double));
+    double *V = Vb.d();
+    EIG_HIP(hipMemsetAsync(V, 0, (size_t)(ncv + 1) * W * sizeof(double), s));
+    init_start(*A, V, nullptr, seed);
+    LanczosBufs lb(ncv);
+    DevBuf cb((size_t)(ncv + 8) * sizeof(double));
+    launch_nrm2sq(n, V + own, lb.st.nsum, 0, s, ctx->red);
+    allreduce_sum(ctx, lb.st.nsum, 1, s);
+    hipEvent_t h0, h1;
+    EIG_HIP(hipEventCreateWithFlags(&h0, hipEventDisableTiming));
+    EIG_HIP(hipEventCreateWithFlags(&h1, hipEventDisableTiming));
+    for (int j = 0; j < ncv; ++j)
+    {
+      double *u = V + (i64)j * W, *up = j > 0 ? V + (i64)(j - 1) * W : V + (i64)j * W, *t = V + (i64)(j + 1) * W;
+      lanczos_step(*A, u, up, t, j, lb, nullptr, h0, h1);
+      // DGKS: two classical Gram-Schmidt passes against v_0..v_j (v_q = u_q / sqrt(nsum[q]))
+      for (int pass = 0; pass < 2; ++pass)
+      {
+        for (int q0 = 0; q0 <= j; q0 += 8 * 48)
+        {
+          const int kq = std::min(j + 1 - q0, 8 * 48);
+          launch_gemv_t(n, kq, V + (i64)q0 * W + own, W, t + own, cb.d() + q0, 0, s, ctx->red);
+        }
+        allreduce_sum(ctx, cb.d(), j + 1, s);
+        launch_gemv_n_sub(n, j + 1, V + own, W, cb.d(), lb.st.nsum, t + own, s);
+      }
+      launch_nrm2sq(n, t + own, lb.st.nsum + j + 1, 0, s, ctx->red);
+      allreduce_sum(ctx, lb.st.nsum + j + 1, 1, s);
+    }
+    (void)hipEventDestroy(h0);
+    (void)hipEventDestroy(h1);
+    // T = tridiag(beta_1..beta_{k-1}; alpha_0..alpha_{k-1})
+    std::vector<double> alpha(ncv), nsum(ncv + 1);
+    EIG_HIP(hipStreamSynchronize(s));
+    EIG_HIP(hipMemcpy(alpha.data(), lb.st.alpha, ncv * sizeof(double), hipMemcpyDeviceToHost));
+    EIG_HIP(hipMemcpy(nsum.data(), lb.st.nsum, (ncv + 1) * sizeof(double), hipMemcpyDeviceToHost));
+    int k = ncv;
+    for (int j = 1; j < ncv; ++j)
+      if (!(nsum[j] > 1e-28 * nsum[0]) || !std::isfinite(alpha[j]))
+      {
+        k = j;  // invariant subspace found: T_k is exact
+        break;
+      }
+    EIG_CHECK(k >= nev, EIG_ERR_BREAKDOWN, "Lanczos breakdown before nev Ritz values were available");
+    std::vector<double> d(alpha.begin(), alpha.begin() + k), e(k > 0 ? k - 1 : 0), Z;
+    for (int j = 1; j < k; ++j) e[j - 1] = std::sqrt(nsum[j]);
+    tridiag_eig(k, d, e, Z);
+    std::vector<int> pick(nev);
+    for (int i = 0; i < nev; ++i) pick[i] = (which == EIG_WHICH_LA) ? k - 1 - i : i;
+    for (int i = 0; i < nev; ++i) eval_host[i] = d[pick[i]];
+    if (evec_host || resid_host)
+    {
+      DevBuf Y(W * sizeof(double)), AY(W * sizeof(double)), coef((size_t)(k + 1) * sizeof(double));
+      double *r2 = cb.d();
+      std::vector<double> zc(k);
+      for (int i = 0; i < nev; ++i)
+      {
+        for (int q = 0; q < k; ++q) zc[q] = Z[(size_t)q * k + pick[i]];
+        EIG_HIP(hipMemcpyAsync(coef.d(), zc.data(), k * sizeof(double), hipMemcpyHostToDevice, s));
+        EIG_HIP(hipMemsetAsync(Y.d(), 0, W * sizeof(double), s));
+        launch_gemv_n_set(n, k, V + own, W, coef.d(), lb.st.nsum, Y.d() + own, s);
+        if (evec_host)
+          EIG_HIP(hipMemcpyAsync(evec_host + (i64)i * n, Y.d() + own, n * sizeof(double), hipMemcpyDeviceToHost, s));
+        if (resid_host)
+        {
+          mv_device(*A, Y.d(), AY.d());
+          launch_resid_sq(n, AY.d() + own, Y.d() + own, d[pick[i]], r2 + i, 0, s, ctx->red);
+          allreduce_sum(ctx, r2 + i, 1, s);
+        }
+        EIG_HIP(hipStreamSynchronize(s));
+      }
+      if (resid_host)
+      {
+        EIG_HIP(hipMemcpy(resid_host, r2, nev * sizeof(double), hipMemcpyDeviceToHost));
+        for (int i = 0; i < nev; ++i) resid_host[i] = std::sqrt(resid_host[i]);
+      }
+    }
+  });
+}

@@ -1,0 +1,145 @@
+// gen.cpp -- synthetic matrices of the reference harness (src/dune-eigensolver.cc:98-156) and of
+// SURVEY 8(d), generated row by row on the host so that a rank can build only its own rows.
+//
+//   kind 0  2-D Dirichlet 5-point, N*N rows, dune-istl setupLaplacian semantics: k = y N + x,
+//           columns ascending {k-N, k-1, k, k+1, k+N}, diagonal 4, off-diagonal -1
+//   kind 1  2-D Neumann: diagonal := |sum of off-diagonals|           (.cc:105-121)
+//   kind 2  2-D partition-of-unity B: a_kl *= pu_k pu_l               (.cc:124-143)
+//   kind 3  2-D identity values on the Laplacian pattern              (.cc:145-156)
+//   kind 4  3-D 7-point Poisson, N^3 rows, diagonal 6                  (configs C2 / C4)
+//   kind 5  3-D Q1 "elasticity" L_Q1 (x) C on N^3 nodes, 3x3 blocks     (config C3)
+#include <cmath>
+#include <cstdint>
+#include <cstdlib>
+
+#include "../../include/eigmi.h"
+
+namespace {
+
+typedef int64_t i64;
+
+inline double k1(int d) { return d == 0 ? 2.0 : -1.0; }
+inline double m1(int d) { return d == 0 ? 4.0 / 6.0 : 1.0 / 6.0; }
+
+// Entries of global block row k; returns the count.  cols/vals may be null (count only).
+int gen_row(int kind, int N, int overlap, i64 k, int32_t *cols, double *vals)
+{
+  int c = 0;
+  auto put = [&](i64 col, double v) {
+    if (cols) cols[c] = (int32_t)col;
+    if (vals) vals[c] = v;
+    ++c;
+  };
+  if (kind >= 0 && kind <= 3)
+  {
+    const int x = (int)(k % N), y = (int)(k / N);
+    auto pu = [&](i64 q) {
+      const int i = (int)(q / N), j = (int)(q % N);
+      return (i < overlap || i > N - 1 - overlap || j < overlap || j > N - 1 - overlap) ? 0.0 : 1.0;
+    };
+    const bool nb[5] = {y > 0, x > 0, true, x < N - 1, y < N - 1};
+    const i64 off[5] = {-(i64)N, -1, 0, 1, (i64)N};
+    int noff = 0;
+    for (int t = 0; t < 5; ++t)
+      if (nb[t] && t != 2) ++noff;
+    for (int t = 0; t < 5; ++t)
+    {
+      if (!nb[t]) continue;
+      const i64 q = k + off[t];
+      double v = (t == 2) ? 4.0 : -1.0;
+      if (kind == 1 && t == 2) v = std::fabs(-1.0 * noff);       // |sum of off-diagonals|
+      if (kind == 2) v *= pu(k) * pu(q);
+      if (kind == 3) v = (t == 2) ? 1.0 : 0.0;
+      put(q, v);
+    }
+    return c;
+  }
+  const i64 NN = (i64)N * N;
+  const int x = (int)(k % N), y = (int)((k / N) % N), z = (int)(k / NN);
+  if (kind == 4)
+  {
+    if (z > 0) put(k - NN, -1.0);
+    if (y > 0) put(k - N, -1.0);
+    if (x > 0) put(k - 1, -1.0);
+    put(k, 6.0);
+    if (x < N - 1) put(k + 1, -1.0);
+    if (y < N - 1) put(k + N, -1.0);
+    if (z < N - 1) put(k + NN, -1.0);
+    return c;
+  }
+  if (kind == 5)
+  {
+    static const double C[9] = {2, 1, 0, 1, 2, 1, 0, 1, 2};
+    for (int dz = -1; dz <= 1; ++dz)
+      for (int dy = -1; dy <= 1; ++dy)
+        for (int dx = -1; dx <= 1; ++dx)
+        {
+          const int xx = x + dx, yy = y + dy, zz = z + dz;
+          if (xx < 0 || yy < 0 || zz < 0 || xx >= N || yy >= N || zz >= N) continue;
+          const int ax = std::abs(dx), ay = std::abs(dy), az = std::abs(dz);
+          const double l = k1(ax) * m1(ay) * m1(az) + m1(ax) * k1(ay) * m1(az) + m1(ax) * m1(ay) * k1(az);
+          if (cols) cols[c] = (int32_t)((zz * (i64)N + yy) * N + xx);
+          if (vals)
+            for (int t = 0; t < 9; ++t) vals[(i64)c * 9 + t] = l * C[t];
+          ++c;
+        }
+    return c;
+  }
+  return -1;
+}
+
+i64 nrows_of(int kind, int N) { return (kind <= 3) ? (i64)N * N : (i64)N * N * N; }
+int blk_of(int kind) { return kind == 5 ? 9 : 1; }
+
+}  // namespace
+
+extern "C" int64_t eig_gen_nnzb_rows(int kind, int N, int64_t row_begin, int64_t nrows)
+{
+  if (kind < 0 || kind > 5 || N <= 0) return -1;
+  i64 s = 0;
+  for (i64 k = row_begin; k < row_begin + nrows; ++k) s += gen_row(kind, N, 0, k, nullptr, nullptr);
+  return s;
+}
+
+extern "C" int64_t eig_gen_nnzb(int kind, int N)
+{
+  if (kind == 0 || kind == 1 || kind == 2 || kind == 3) return (i64)5 * N * N - 4 * (i64)N;
+  if (kind == 4) return (i64)7 * N * N * N - (i64)6 * N * N;
+  if (kind == 5)
+  {
+    const i64 t = 3 * (i64)N - 2;
+    return t * t * t;
+  }
+  return -1;
+}
+
+extern "C" int eig_gen_matrix_rows(int kind, int N, int64_t row_begin, int64_t nrows, int64_t *rowptr, int32_t *col,
+                                   double *vals)
+{
+  if (kind < 0 || kind > 5 || N <= 0 || !rowptr || !col || !vals) return EIG_ERR_ARG;
+  if (row_begin < 0 || row_begin + nrows > nrows_of(kind, N)) return EIG_ERR_SHAPE;
+  const int bb = blk_of(kind);
+  i64 p = 0;
+  for (i64 r = 0; r < nrows; ++r)
+  {
+    rowptr[r] = p;
+    p += gen_row(kind, N, 3, row_begin + r, col + p, vals + p * bb);
+  }
+  rowptr[nrows] = p;
+  return EIG_OK;
+}
+
+extern "C" int eig_gen_matrix(int kind, int N, int overlap, int64_t *rowptr, int32_t *col, double *vals)
+{
+  if (kind < 0 || kind > 5 || N <= 0 || !rowptr || !col || !vals) return EIG_ERR_ARG;
+  const int bb = blk_of(kind);
+  const i64 n = nrows_of(kind, N);
+  i64 p = 0;
+  for (i64 r = 0; r < n; ++r)
+  {
+    rowptr[r] = p;
+    p += gen_row(kind, N, overlap, r, col + p, vals + p * bb);
+  }
+  rowptr[n] = p;
+  return EIG_OK;
+}

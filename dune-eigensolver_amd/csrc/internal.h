@@ -1,0 +1,182 @@
+// internal.h -- shared host-side structures of libeigmi (not part of the C ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/eigmi.h"
+
+namespace eigmi {
+
+typedef int64_t i64;
+typedef int32_t i32;
+
+// Status-carrying exception used inside the library; every C entry point catches it and turns
+// it into the int status + eig_last_error message.
+struct Error : std::runtime_error {
+  int code;
+  Error(int c, const std::string &m) : std::runtime_error(m), code(c) {}
+};
+
+#define EIG_HIP(call)                                                                          \
+  do {                                                                                         \
+    hipError_t e_ = (call);                                                                    \
+    if (e_ != hipSuccess)                                                                      \
+      throw ::eigmi::Error(EIG_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(e_));     \
+  } while (0)
+
+#define EIG_NCCL(call)                                                                         \
+  do {                                                                                         \
+    ncclResult_t r_ = (call);                                                                  \
+    if (r_ != ncclSuccess)                                                                     \
+      throw ::eigmi::Error(EIG_ERR_RCCL, std::string(#call) + ": " + ncclGetErrorString(r_));  \
+  } while (0)
+
+#define EIG_CHECK(cond, code, msg)                                                             \
+  do {                                                                                         \
+    if (!(cond)) throw ::eigmi::Error((code), (msg));                                          \
+  } while (0)
+
+// Streaming kernels use this many workgroups (8 per CU x 256 CUs) and grid-stride inside.
+constexpr int kStreamBlocks = 2048;
+constexpr int kStreamThreads = 256;
+// Reduction workspace: per-block partials (sc1 stores) + one ticket per concurrent reduction.
+constexpr int kMaxRedBlocks = 2048;
+constexpr int kMaxRedVals = 256;   // values reduced by one launch (e.g. a 16x16 Gram tile)
+constexpr int kNumTickets = 64;
+
+struct ReduceWS {
+  double *partials = nullptr;  // kMaxRedBlocks * kMaxRedVals
+  unsigned *tickets = nullptr; // kNumTickets, zero between launches (the last block resets)
+};
+
+}  // namespace eigmi
+
+struct eig_ctx_s {
+  int device = 0;
+  hipStream_t stream = nullptr;      // compute stream
+  hipStream_t comm_stream = nullptr; // halo exchange stream
+  std::string last_error;
+  eigmi::ReduceWS red;
+  double *scratch = nullptr;         // small device scalars (reduction results)
+  int num_cu = 256;
+  // RCCL
+  ncclComm_t comm = nullptr;
+  int nranks = 1, rank = 0;
+  // reusable device buffers for drivers (grown on demand)
+  std::vector<std::pair<void *, size_t>> pool;
+};
+
+namespace eigmi {
+
+// Halo plan of a row-partitioned matrix (scalar units): the window covers global scalar
+// columns [win_begin, win_begin + window); owned rows sit at own_offset.  For every peer,
+// `sends` lists owned ranges it needs and `recvs` the window ranges it fills.
+struct HaloRange {
+  int peer;
+  i64 offset;  // scalar offset inside the window (recv) or inside the window (send: own rows)
+  i64 count;   // scalar entries
+};
+
+}  // namespace eigmi
+
+struct eig_mat_s {
+  eig_ctx_t ctx = nullptr;
+  int br = 1, bc = 1;
+  eigmi::i64 nb_rows = 0;         // owned block rows
+  eigmi::i64 nb_rows_global = 0;
+  eigmi::i64 nb_cols = 0;         // global block columns
+  eigmi::i64 row_begin = 0;       // first owned global block row
+  eigmi::i64 win_begin = 0;       // first global scalar column in the window
+  eigmi::i64 window = 0;          // window length (scalar)
+  eigmi::i64 own_offset = 0;      // owned rows' offset in the window (scalar)
+  eigmi::i64 nnzb = 0, nnzb_padded = 0;
+  eigmi::i64 nslices = 0;
+  // SELL-64 device image: slice s covers block rows [64 s, 64 s + 64); block k of lane l sits at
+  // slice_ptr[s] + k*64 + l (cols) and (slice_ptr[s] + k*64)*br*bc + t*64 + l (values, t < br*bc).
+  eigmi::i64 *slice_ptr = nullptr;  // nslices + 1
+  eigmi::i32 *col = nullptr;        // nnzb_padded, window-local block columns, -1 = padding
+  double *val = nullptr;            // nnzb_padded * br * bc
+  // Interior / boundary slice split for halo overlap (distributed only).
+  eigmi::i32 *slice_list = nullptr; // [interior..., boundary...]
+  eigmi::i64 n_interior = 0, n_boundary = 0;
+  std::vector<eigmi::HaloRange> sends, recvs;
+  eigmi::i64 halo_send = 0, halo_recv = 0;
+  eigmi::i64 device_bytes = 0;
+};
+
+namespace eigmi {
+
+// ---- kernel launchers (k_*.hip) -------------------------------------------------------------
+// Scalar results land in `out` (device); reductions use ctx->red.
+
+// SpMV over the SELL image: y[own_offset + r] = (A x)[r] for the slices [first, first+count) of
+// `slices` (or all slices when slices == nullptr).
+void launch_spmv(const eig_mat_s &A, const double *x, double *y, const i32 *slices, i64 first, i64 count,
+                 hipStream_t s);
+
+// Lanczos fused kernels (see DESIGN.md "Lanczos step").  Device scalar arrays live in `st`.
+struct LanczosState {
+  double *dsum;   // dsum[j]  = t . u_j (local, then allreduced)
+  double *nsum;   // nsum[j]  = ||u_j||^2 (local, then allreduced); nsum[0] from the start vector
+  double *alpha;  // alpha[j]
+  double *beta;   // beta[j]  = sqrt(nsum[j])
+};
+void launch_lanczos_spmv(const eig_mat_s &A, const double *u, const double *up, double *t, int j,
+                         const LanczosState &st, const i32 *slices, i64 first, i64 count, double *dot_out,
+                         double *beta_out, const double *carry, int ticket, hipStream_t s, ReduceWS red);
+void launch_lanczos_update(i64 n, const double *u, double *t, int j, const LanczosState &st, int ticket,
+                           hipStream_t s, ReduceWS red);
+void launch_beta_tail(const LanczosState &st, int j, hipStream_t s);
+
+// BLAS-1 (results to device memory).
+void launch_dot(i64 n, const double *x, const double *y, double *out, int ticket, hipStream_t s, ReduceWS red);
+void launch_nrm2sq(i64 n, const double *x, double *out, int ticket, hipStream_t s, ReduceWS red);
+void launch_axpy(i64 n, double a, const double *x, double *y, hipStream_t s);
+void launch_axpy_dev(i64 n, const double *a, double scale, const double *x, double *y, hipStream_t s);
+void launch_scal(i64 n, double a, double *x, hipStream_t s);
+void launch_scal_dev(i64 n, const double *a, bool reciprocal_sqrt, double *x, hipStream_t s);
+void launch_sqrt_inplace(double *v, int count, hipStream_t s);
+void launch_shift_diag(eig_mat_s &A, double shift, hipStream_t s);
+
+// MultiVector<double,8> kernels.
+void launch_spmm_mv8(const eig_mat_s &A, i64 m, const double *Qin, double *Qout, hipStream_t s);
+void launch_dot_diag_mv8(i64 n, i64 m, const double *Q1, const double *Q2, double *dp, int ticket,
+                         hipStream_t s, ReduceWS red);
+void launch_gram_mv8(i64 n, i64 m1, i64 m2, const double *Q1, const double *Q2, double *G, int ticket,
+                     hipStream_t s, ReduceWS red);
+// Block Gram-Schmidt building blocks, see k_mv8.hip.
+void launch_mgs_pass(i64 n, double *Qb, int k, double *S, int ticket, hipStream_t s, ReduceWS red);
+void launch_apply_upper(i64 n, double *Qb, const double *U, hipStream_t s);
+void launch_cholqr_factor(const double *G, double *U, double *normmax, int flags, hipStream_t s);
+void launch_project(i64 n, i64 mrest, const double *Qk, double *Qrest, const double *S, hipStream_t s);
+void launch_max_offdiag(const double *S, i64 rows, i64 cols, bool upper_only, double *normmax, hipStream_t s);
+
+// Column-major (b = 1) GEMV-type helpers for the Lanczos re-orthogonalisation:
+// c = V^T w (V: k columns of length ld, owned slice at off), w -= V c.
+void launch_gemv_t(i64 n, int k, const double *V, i64 ldv, const double *w, double *c, int ticket,
+                   hipStream_t s, ReduceWS red);
+// w -= sum_q V_q * c[q] / (scale2 ? scale2[q] : 1)
+void launch_gemv_n_sub(i64 n, int k, const double *V, i64 ldv, const double *c, const double *scale2, double *w,
+                       hipStream_t s);
+// y = sum_q V_q * c[q] / sqrt(nsum[q])   (Ritz vector assembly from an unnormalised basis)
+void launch_gemv_n_set(i64 n, int k, const double *V, i64 ldv, const double *c, const double *nsum, double *y,
+                       hipStream_t s);
+// r = ||A y - theta y|| helper: out = ||x - theta*y||^2
+void launch_resid_sq(i64 n, const double *x, const double *y, double theta, double *out, int ticket,
+                     hipStream_t s, ReduceWS red);
+
+// ---- helpers in api.cpp --------------------------------------------------------------------
+void halo_exchange(const eig_mat_s &A, double *x, hipStream_t s);
+void mv_device(eig_mat_s &A, double *x, double *y);
+void gram_device(eig_ctx_t ctx, i64 n, i64 m1, i64 m2, const double *Q1, const double *Q2, double *G);
+void orthonormalize_device(eig_ctx_t ctx, i64 n, i64 m, double *Q, int variant);
+void allreduce_sum(eig_ctx_t ctx, double *buf, i64 count, hipStream_t s);
+void *ctx_buffer(eig_ctx_t ctx, int slot, size_t bytes);
+void host_random_normal(i64 count, unsigned seed, double *out);
+
+}  // namespace eigmi

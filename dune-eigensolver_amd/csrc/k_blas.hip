@@ -1,0 +1,293 @@
+// k_blas.hip -- BlockVector-level kernels (dot / axpy / norm), the fused Lanczos update and
+// the column-major GEMV pair used by the Lanczos re-orthogonalisation (gfx950).
+//
+// All streaming kernels read 16 B per lane (double2) where alignment allows and grid-stride
+// over 2048 workgroups; every reduction is the deterministic grid_sum of reduce_dev.h.
+#include "internal.h"
+#include "reduce_dev.h"
+
+namespace eigmi {
+
+static inline int stream_grid(i64 n, int per_thread = 2)
+{
+  const i64 need = (n + (i64)kStreamThreads * per_thread - 1) / ((i64)kStreamThreads * per_thread);
+  if (need < 1) return 1;
+  return (int)(need < kStreamBlocks ? need : kStreamBlocks);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Lanczos step, kernel 2 (DESIGN.md "Lanczos step"):
+//   alpha_j = sig_j * dsum[j];  u_{j+1} = t - (alpha_j sig_j) u_j;  nsum[j+1] = ||u_{j+1}||^2
+// t is updated in place (it becomes u_{j+1}).  Same rounding sequence as orc_lanczos.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kStreamThreads) void k_lanczos_update(i64 n, const double *__restrict__ u,
+                                                                   double *__restrict__ t, int j,
+                                                                   const double *__restrict__ dsum,
+                                                                   const double *__restrict__ nsum,
+                                                                   double *__restrict__ alpha_out,
+                                                                   double *__restrict__ nsum_out, double *partials,
+                                                                   unsigned *ticket)
+{
+  __shared__ double tot[1];
+  const double sig = 1.0 / sqrt(nsum[j]);
+  const double alpha = sig * dsum[j];
+  const double as = alpha * sig;
+  double acc = 0.0;
+  const i64 n2 = n >> 1;
+  const double2 *u2 = reinterpret_cast<const double2 *>(u);
+  double2 *t2 = reinterpret_cast<double2 *>(t);
+  for (i64 i = (i64)blockIdx.x * kStreamThreads + threadIdx.x; i < n2; i += (i64)gridDim.x * kStreamThreads)
+  {
+    double2 tv = t2[i], uv = u2[i];
+    double2 r;
+    r.x = tv.x - as * uv.x;
+    r.y = tv.y - as * uv.y;
+    t2[i] = r;
+    acc += r.x * r.x;
+    acc += r.y * r.y;
+  }
+  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0)
+  {
+    double r = t[n - 1] - as * u[n - 1];
+    t[n - 1] = r;
+    acc += r * r;
+  }
+  double v[1] = {acc};
+  if (grid_sum<1, kStreamThreads>(v, partials, ticket, tot))
+  {
+    if (threadIdx.x == 0)
+    {
+      nsum_out[0] = tot[0];
+      if (alpha_out) alpha_out[0] = alpha;
+    }
+  }
+}
+
+void launch_lanczos_update(i64 n, const double *u, double *t, int j, const LanczosState &st, int ticket,
+                           hipStream_t s, ReduceWS red)
+{
+  EIG_CHECK((((uintptr_t)u | (uintptr_t)t) & 15) == 0, EIG_ERR_ARG, "lanczos update: vectors must be 16-B aligned");
+  hipLaunchKernelGGL(k_lanczos_update, dim3(stream_grid(n)), dim3(kStreamThreads), 0, s, n, u, t, j, st.dsum,
+                     st.nsum, st.alpha + j, st.nsum + j + 1, red.partials, red.tickets + ticket);
+}
+
+// beta[j] = sqrt(nsum[j]) (records the final beta of a run).
+__global__ void k_beta_tail(const double *nsum, double *beta, int j)
+{
+  if (threadIdx.x == 0 && blockIdx.x == 0) beta[j] = sqrt(nsum[j]);
+}
+void launch_beta_tail(const LanczosState &st, int j, hipStream_t s)
+{
+  hipLaunchKernelGGL(k_beta_tail, dim3(1), dim3(64), 0, s, st.nsum, st.beta, j);
+}
+
+// ---------------------------------------------------------------------------------------------
+// BlockVector ops.  Dots sum per lane in index order, then the fixed grid tree.
+// ---------------------------------------------------------------------------------------------
+template <bool SQ>
+__global__ __launch_bounds__(kStreamThreads) void k_dot(i64 n, const double *__restrict__ x,
+                                                        const double *__restrict__ y, double *out, double *partials,
+                                                        unsigned *ticket)
+{
+  __shared__ double tot[1];
+  double acc = 0.0;
+  for (i64 i = (i64)blockIdx.x * kStreamThreads + threadIdx.x; i < n; i += (i64)gridDim.x * kStreamThreads)
+  {
+    const double a = x[i];
+    acc += a * (SQ ? a : y[i]);
+  }
+  double v[1] = {acc};
+  if (grid_sum<1, kStreamThreads>(v, partials, ticket, tot))
+    if (threadIdx.x == 0) out[0] = tot[0];
+}
+
+void launch_dot(i64 n, const double *x, const double *y, double *out, int ticket, hipStream_t s, ReduceWS red)
+{
+  hipLaunchKernelGGL(k_dot<false>, dim3(stream_grid(n, 4)), dim3(kStreamThreads), 0, s, n, x, y, out, red.partials,
+                     red.tickets + ticket);
+}
+void launch_nrm2sq(i64 n, const double *x, double *out, int ticket, hipStream_t s, ReduceWS red)
+{
+  hipLaunchKernelGGL(k_dot<true>, dim3(stream_grid(n, 4)), dim3(kStreamThreads), 0, s, n, x, x, out, red.partials,
+                     red.tickets + ticket);
+}
+
+// y += a x   (a from the host, or a = scale * (*a_dev) from device memory)
+__global__ __launch_bounds__(kStreamThreads) void k_axpy(i64 n, double a, const double *a_dev, double scale,
+                                                         const double *__restrict__ x, double *__restrict__ y)
+{
+  if (a_dev) a = scale * a_dev[0];
+  for (i64 i = (i64)blockIdx.x * kStreamThreads + threadIdx.x; i < n; i += (i64)gridDim.x * kStreamThreads)
+    y[i] += a * x[i];
+}
+void launch_axpy(i64 n, double a, const double *x, double *y, hipStream_t s)
+{
+  hipLaunchKernelGGL(k_axpy, dim3(stream_grid(n, 4)), dim3(kStreamThreads), 0, s, n, a, (const double *)nullptr, 1.0,
+                     x, y);
+}
+void launch_axpy_dev(i64 n, const double *a, double scale, const double *x, double *y, hipStream_t s)
+{
+  hipLaunchKernelGGL(k_axpy, dim3(stream_grid(n, 4)), dim3(kStreamThreads), 0, s, n, 0.0, a, scale, x, y);
+}
+
+// x *= a ; or x *= 1/sqrt(*a_dev) (normalise by a device-resident squared norm)
+__global__ __launch_bounds__(kStreamThreads) void k_scal(i64 n, double a, const double *a_dev, int rsqrt_mode,
+                                                         double *__restrict__ x)
+{
+  if (a_dev) a = rsqrt_mode ? 1.0 / sqrt(a_dev[0]) : a_dev[0];
+  for (i64 i = (i64)blockIdx.x * kStreamThreads + threadIdx.x; i < n; i += (i64)gridDim.x * kStreamThreads)
+    x[i] *= a;
+}
+void launch_scal(i64 n, double a, double *x, hipStream_t s)
+{
+  hipLaunchKernelGGL(k_scal, dim3(stream_grid(n, 4)), dim3(kStreamThreads), 0, s, n, a, (const double *)nullptr, 0,
+                     x);
+}
+void launch_scal_dev(i64 n, const double *a, bool reciprocal_sqrt, double *x, hipStream_t s)
+{
+  hipLaunchKernelGGL(k_scal, dim3(stream_grid(n, 4)), dim3(kStreamThreads), 0, s, n, 0.0, a, reciprocal_sqrt ? 1 : 0,
+                     x);
+}
+
+__global__ void k_sqrt_inplace(double *v, int count)
+{
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < count) v[i] = sqrt(v[i]);
+}
+void launch_sqrt_inplace(double *v, int count, hipStream_t s)
+{
+  hipLaunchKernelGGL(k_sqrt_inplace, dim3((count + 63) / 64), dim3(64), 0, s, v, count);
+}
+
+// ---------------------------------------------------------------------------------------------
+// a13: A += shift * I on the SELL image (eigensolver.hh:59-66).  The diagonal block of block
+// row r has window-local block column r + own_offset / bc.
+// ---------------------------------------------------------------------------------------------
+__global__ void k_shift_diag(i64 nbrows, i64 own_blk, const i64 *__restrict__ slice_ptr, const i32 *__restrict__ col,
+                             double *__restrict__ val, int br, int bc, i64 nslices, double shift)
+{
+  const i64 s = (i64)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (s >= nslices) return;
+  const i64 r = s * 64 + lane;
+  if (r >= nbrows) return;
+  const i64 base = slice_ptr[s];
+  const int width = (int)((slice_ptr[s + 1] - base) >> 6);
+  const int bb = br * bc, nd = br < bc ? br : bc;
+  for (int k = 0; k < width; ++k)
+  {
+    const i32 c = col[base + (i64)k * 64 + lane];
+    if (c == (i32)(r + own_blk))
+      for (int d = 0; d < nd; ++d) val[(base + (i64)k * 64) * bb + (d * bc + d) * 64 + lane] += shift;
+  }
+}
+void launch_shift_diag(eig_mat_s &A, double shift, hipStream_t s)
+{
+  const int wpb = 4;
+  const i64 G = (A.nslices + wpb - 1) / wpb;
+  if (G == 0) return;
+  hipLaunchKernelGGL(k_shift_diag, dim3((unsigned)G), dim3(64 * wpb), 0, s, A.nb_rows, A.own_offset / A.bc,
+                     A.slice_ptr, A.col, A.val, A.br, A.bc, A.nslices, shift);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Re-orthogonalisation GEMVs on a column-major basis V (k columns, leading dimension ldv):
+//   c = V^T w  (column tiles of 8 on grid.y, one grid reduction per tile)
+//   w -= V c
+// ---------------------------------------------------------------------------------------------
+constexpr int kGemvBlocks = 512;
+
+__global__ __launch_bounds__(kStreamThreads) void k_gemv_t(i64 n, int k, const double *__restrict__ V, i64 ldv,
+                                                           const double *__restrict__ w, double *__restrict__ c,
+                                                           double *partials, unsigned *tickets)
+{
+  __shared__ double tot[8];
+  const int c0 = blockIdx.y * 8;
+  double acc[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) acc[q] = 0.0;
+  for (i64 i = (i64)blockIdx.x * kStreamThreads + threadIdx.x; i < n; i += (i64)gridDim.x * kStreamThreads)
+  {
+    const double wi = w[i];
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (c0 + q < k) acc[q] += V[(i64)(c0 + q) * ldv + i] * wi;
+  }
+  if (grid_sum_n<8, kStreamThreads>(acc, partials + (size_t)blockIdx.y * gridDim.x * 8, tickets + blockIdx.y, tot,
+                                    blockIdx.x, gridDim.x))
+  {
+    if (threadIdx.x < 8 && c0 + (int)threadIdx.x < k) c[c0 + threadIdx.x] = tot[threadIdx.x];
+  }
+}
+
+void launch_gemv_t(i64 n, int k, const double *V, i64 ldv, const double *w, double *c, int ticket, hipStream_t s,
+                   ReduceWS red)
+{
+  const int tiles = (k + 7) / 8;
+  EIG_CHECK(ticket + tiles <= kNumTickets, EIG_ERR_ARG, "gemv_t: too many column tiles for the ticket pool");
+  int G = stream_grid(n, 4);
+  if (G > kGemvBlocks) G = kGemvBlocks;
+  EIG_CHECK((i64)G * tiles * 8 <= (i64)kMaxRedBlocks * kMaxRedVals, EIG_ERR_ARG, "gemv_t: partials overflow");
+  hipLaunchKernelGGL(k_gemv_t, dim3(G, tiles), dim3(kStreamThreads), 0, s, n, k, V, ldv, w, c, red.partials,
+                     red.tickets + ticket);
+}
+
+__global__ __launch_bounds__(kStreamThreads) void k_gemv_n(i64 n, int k, const double *__restrict__ V, i64 ldv,
+                                                           const double *__restrict__ c, const double *__restrict__ sc,
+                                                           int mode, double *__restrict__ w)
+{
+  // mode 0: w -= sum V_q c_q / sc_q (sc may be null)  ; mode 1: w = sum V_q c_q / sqrt(sc_q)
+  __shared__ double coef[512];
+  for (int q = threadIdx.x; q < k && q < 512; q += blockDim.x)
+  {
+    double cq = c[q];
+    if (sc) cq = (mode == 0) ? cq / sc[q] : cq * (1.0 / sqrt(sc[q]));
+    coef[q] = cq;
+  }
+  __syncthreads();
+  for (i64 i = (i64)blockIdx.x * kStreamThreads + threadIdx.x; i < n; i += (i64)gridDim.x * kStreamThreads)
+  {
+    double s = 0.0;
+    for (int q = 0; q < k; ++q) s += V[(i64)q * ldv + i] * coef[q];
+    if (mode == 0) w[i] -= s;
+    else w[i] = s;
+  }
+}
+void launch_gemv_n_sub(i64 n, int k, const double *V, i64 ldv, const double *c, const double *scale2, double *w,
+                       hipStream_t s)
+{
+  EIG_CHECK(k <= 512, EIG_ERR_ARG, "gemv_n: at most 512 basis vectors");
+  if (k <= 0) return;
+  hipLaunchKernelGGL(k_gemv_n, dim3(stream_grid(n, 4)), dim3(kStreamThreads), 0, s, n, k, V, ldv, c, scale2, 0, w);
+}
+void launch_gemv_n_set(i64 n, int k, const double *V, i64 ldv, const double *c, const double *nsum, double *y,
+                       hipStream_t s)
+{
+  EIG_CHECK(k <= 512, EIG_ERR_ARG, "gemv_n: at most 512 basis vectors");
+  hipLaunchKernelGGL(k_gemv_n, dim3(stream_grid(n, 4)), dim3(kStreamThreads), 0, s, n, k, V, ldv, c, nsum, 1, y);
+}
+
+// out = ||x - theta*y||^2
+__global__ __launch_bounds__(kStreamThreads) void k_resid_sq(i64 n, const double *__restrict__ x,
+                                                             const double *__restrict__ y, double theta, double *out,
+                                                             double *partials, unsigned *ticket)
+{
+  __shared__ double tot[1];
+  double acc = 0.0;
+  for (i64 i = (i64)blockIdx.x * kStreamThreads + threadIdx.x; i < n; i += (i64)gridDim.x * kStreamThreads)
+  {
+    const double r = x[i] - theta * y[i];
+    acc += r * r;
+  }
+  double v[1] = {acc};
+  if (grid_sum<1, kStreamThreads>(v, partials, ticket, tot))
+    if (threadIdx.x == 0) out[0] = tot[0];
+}
+void launch_resid_sq(i64 n, const double *x, const double *y, double theta, double *out, int ticket, hipStream_t s,
+                     ReduceWS red)
+{
+  hipLaunchKernelGGL(k_resid_sq, dim3(stream_grid(n, 4)), dim3(kStreamThreads), 0, s, n, x, y, theta, out,
+                     red.partials, red.tickets + ticket);
+}
+
+}  // namespace eigmi

@@ -1,0 +1,424 @@
+// k_mv8.hip -- MultiVector<double,8> kernels (gfx950): SpMM, column dots, the tall-skinny Gram
+// panel on MFMA, and the building blocks of block Gram-Schmidt / B-Gram-Schmidt.
+//
+// Layout is the reference's block-column-major MultiVector<double,8> (multivector.hh:130-139):
+// column block b of an n x m multivector is n rows of 8 contiguous doubles (64 B) starting at
+// Q + b*8*n.  Kernels keep the reference's per-element operation order wherever the result is
+// not a reduction, so SpMM / projections are bitwise the reference arithmetic on equal inputs.
+#include "internal.h"
+#include "reduce_dev.h"
+
+namespace eigmi {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+static inline int grid_for(i64 work, i64 per_block, int cap)
+{
+  i64 g = (work + per_block - 1) / per_block;
+  if (g < 1) g = 1;
+  return (int)(g < cap ? g : cap);
+}
+
+// ---------------------------------------------------------------------------------------------
+// a2: Qout = A Qin (matmul_sparse_tallskinny_blocked, kernels_cpp.hh:626-657).
+// A workgroup (4 waves) takes one 64-row SELL slice at a time; lane L of wave w handles row
+// 16 w + L/4 of the slice and the column pair 2 (L%4), 2 (L%4)+1 (16-B loads of Qin rows) for up
+// to MB column blocks, so the matrix slice is read once for MB column blocks.
+// ---------------------------------------------------------------------------------------------
+template <int MB>
+__global__ __launch_bounds__(256) void k_spmm_mv8(i64 nrows, i64 nslices, const i64 *__restrict__ slice_ptr,
+                                                  const double *__restrict__ val, const i32 *__restrict__ col,
+                                                  const double *__restrict__ Qin, double *__restrict__ Qout, i64 n,
+                                                  int nblk_total)
+{
+  const int wave = threadIdx.x >> 6, L = threadIdx.x & 63;
+  const int ri = wave * 16 + (L >> 2), cp = L & 3;
+  const int b0 = blockIdx.y * MB;
+  for (i64 s = blockIdx.x; s < nslices; s += gridDim.x)
+  {
+    const i64 base = slice_ptr[s];
+    const int width = (int)((slice_ptr[s + 1] - base) >> 6);
+    double2 acc[MB];
+#pragma unroll
+    for (int q = 0; q < MB; ++q) acc[q] = make_double2(0.0, 0.0);
+    for (int k = 0; k < width; ++k)
+    {
+      const i32 c = col[base + (i64)k * 64 + ri];
+      if (c < 0) continue;
+      const double a = val[base + (i64)k * 64 + ri];
+#pragma unroll
+      for (int q = 0; q < MB; ++q)
+      {
+        if (b0 + q < nblk_total)
+        {
+          const double2 xv = *reinterpret_cast<const double2 *>(Qin + ((i64)(b0 + q) * n + c) * 8 + 2 * cp);
+          acc[q].x += a * xv.x;
+          acc[q].y += a * xv.y;
+        }
+      }
+    }
+    const i64 r = s * 64 + ri;
+    if (r < nrows)
+    {
+#pragma unroll
+      for (int q = 0; q < MB; ++q)
+        if (b0 + q < nblk_total) *reinterpret_cast<double2 *>(Qout + ((i64)(b0 + q) * n + r) * 8 + 2 * cp) = acc[q];
+    }
+  }
+}
+
+void launch_spmm_mv8(const eig_mat_s &A, i64 m, const double *Qin, double *Qout, hipStream_t s)
+{
+  EIG_CHECK(A.br == 1 && A.bc == 1, EIG_ERR_BLOCKSIZE,
+            "matmul_sparse_tallskinny_blocked: only implemented for FieldMatrix<..,1,1>");
+  const int nblk = (int)(m / 8);
+  const int MB = 4;
+  const int gy = (nblk + MB - 1) / MB;
+  const int gx = grid_for(A.nslices, 1, kStreamBlocks);
+  // Qin is a window-layout multivector on one rank (window == n); columns index it directly.
+  hipLaunchKernelGGL(k_spmm_mv8<MB>, dim3(gx, gy), dim3(256), 0, s, A.nb_rows, A.nslices, A.slice_ptr, A.val, A.col,
+                     Qin, Qout, A.nb_rows, nblk);
+}
+
+// ---------------------------------------------------------------------------------------------
+// a5: dp[j] = q1_j . q2_j (dot_products_diagonal_blocked, kernels_cpp.hh:24-55).  grid.y = column
+// block; thread t always sees the column pair 2 (t%4) because the grid stride is a multiple of 4.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kStreamThreads) void k_dot_diag_mv8(i64 n, const double *__restrict__ Q1,
+                                                                 const double *__restrict__ Q2, double *dp,
+                                                                 double *partials, unsigned *tickets)
+{
+  __shared__ double tot[8];
+  const i64 off = (i64)blockIdx.y * n * 8;
+  const double2 *a = reinterpret_cast<const double2 *>(Q1 + off);
+  const double2 *b = reinterpret_cast<const double2 *>(Q2 + off);
+  const i64 n4 = n * 4;
+  double sx = 0.0, sy = 0.0;
+  for (i64 i = (i64)blockIdx.x * kStreamThreads + threadIdx.x; i < n4; i += (i64)gridDim.x * kStreamThreads)
+  {
+    const double2 x = a[i], y = b[i];
+    sx += x.x * y.x;
+    sy += x.y * y.y;
+  }
+  const int cp = threadIdx.x & 3;
+  double v[8];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+  {
+    v[2 * q] = (q == cp) ? sx : 0.0;
+    v[2 * q + 1] = (q == cp) ? sy : 0.0;
+  }
+  if (grid_sum_n<8, kStreamThreads>(v, partials + (size_t)blockIdx.y * gridDim.x * 8, tickets + blockIdx.y, tot,
+                                    blockIdx.x, gridDim.x))
+  {
+    if (threadIdx.x < 8) dp[blockIdx.y * 8 + threadIdx.x] = tot[threadIdx.x];
+  }
+}
+
+void launch_dot_diag_mv8(i64 n, i64 m, const double *Q1, const double *Q2, double *dp, int ticket, hipStream_t s,
+                         ReduceWS red)
+{
+  const int nb = (int)(m / 8);
+  EIG_CHECK(ticket + nb <= kNumTickets, EIG_ERR_ARG, "dot_diag_mv8: too many column blocks");
+  int G = grid_for(n * 4, (i64)kStreamThreads * 4, 1024);
+  while ((i64)G * nb * 8 > (i64)kMaxRedBlocks * kMaxRedVals) G /= 2;
+  hipLaunchKernelGGL(k_dot_diag_mv8, dim3(G, nb), dim3(kStreamThreads), 0, s, n, Q1, Q2, dp, red.partials,
+                     red.tickets + ticket);
+}
+
+// ---------------------------------------------------------------------------------------------
+// a6: G = Q1^T Q2 on MFMA (v_mfma_f64_16x16x4f64), one 16x16 output tile per grid.y.
+// Lane l supplies A[i = l&15][k = l>>4] = Q1(row r0+k, c1 + i) and B[k][j = l&15] = Q2(row r0+k,
+// c2 + j); the f64 accumulator holds C[row (l>>4) + 4 q][col l&15] in register q.  Columns past
+// m1 / m2 read as zero (an m = 8 Gram uses the top-left 8x8 quadrant).  Per workgroup the 4
+// waves' tiles are summed in LDS, then across workgroups in block order (deterministic).
+// ---------------------------------------------------------------------------------------------
+constexpr int kGramThreads = 256;
+
+__device__ __forceinline__ double mv8_at(const double *Q, i64 n, i64 r, i64 c) { return Q[((c >> 3) * n + r) * 8 + (c & 7)]; }
+
+__global__ __launch_bounds__(kGramThreads) void k_gram_mv8(i64 n, i64 m1, i64 m2, const double *__restrict__ Q1,
+                                                           const double *__restrict__ Q2, double *__restrict__ G,
+                                                           int tiles_j, double *partials, unsigned *tickets)
+{
+  __shared__ double sh[kGramThreads / 64][256];
+  __shared__ unsigned s_last;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int ti = blockIdx.y / tiles_j, tj = blockIdx.y % tiles_j;
+  const i64 c1 = (i64)ti * 16 + (lane & 15), c2 = (i64)tj * 16 + (lane & 15);
+  const bool ok1 = c1 < m1, ok2 = c2 < m2;
+  const int kk = lane >> 4;
+  d4 acc = {0.0, 0.0, 0.0, 0.0};
+  // rows in groups of 4 (one MFMA), 4 groups per wave iteration
+  const i64 ngroups = (n + 3) / 4;
+  const i64 wstride = (i64)gridDim.x * (kGramThreads / 64);
+  for (i64 g = (i64)blockIdx.x * (kGramThreads / 64) + wave; g < ngroups; g += wstride)
+  {
+    const i64 r = g * 4 + kk;
+    const bool rok = r < n;
+    const double a = (ok1 && rok) ? mv8_at(Q1, n, r, c1) : 0.0;
+    const double b = (ok2 && rok) ? mv8_at(Q2, n, r, c2) : 0.0;
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+  }
+  // tile element (row, col) = (kk + 4 q, lane & 15)
+#pragma unroll
+  for (int q = 0; q < 4; ++q) sh[wave][(kk + 4 * q) * 16 + (lane & 15)] = acc[q];
+  __syncthreads();
+  const int t = threadIdx.x;  // 256 threads = 256 tile elements
+  double bsum = 0.0;
+#pragma unroll
+  for (int w = 0; w < kGramThreads / 64; ++w) bsum += sh[w][t];
+  double *part = partials + (size_t)blockIdx.y * gridDim.x * 256;
+  st_sc1(&part[(size_t)blockIdx.x * 256 + t], bsum);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0)
+  {
+    unsigned prev = __hip_atomic_fetch_add(tickets + blockIdx.y, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = (prev == gridDim.x - 1) ? 1u : 0u;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  double tot = 0.0;
+  for (unsigned b = 0; b < gridDim.x; ++b) tot += ld_sc1(&part[(size_t)b * 256 + t]);
+  const int row = t >> 4, cl = t & 15;
+  const i64 gi = (i64)ti * 16 + row, gj = (i64)tj * 16 + cl;
+  if (gi < m1 && gj < m2) G[gi * m2 + gj] = tot;
+  if (t == 0) __hip_atomic_store(tickets + blockIdx.y, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+void launch_gram_mv8(i64 n, i64 m1, i64 m2, const double *Q1, const double *Q2, double *G, int ticket,
+                     hipStream_t s, ReduceWS red)
+{
+  const int tiles_i = (int)((m1 + 15) / 16), tiles_j = (int)((m2 + 15) / 16);
+  const int tiles = tiles_i * tiles_j;
+  EIG_CHECK(tiles >= 1 && ticket + tiles <= kNumTickets, EIG_ERR_ARG, "gram_mv8: too many output tiles");
+  int gx = grid_for((n + 3) / 4, 4 * 8, 256);
+  while ((i64)gx * tiles * 256 > (i64)kMaxRedBlocks * kMaxRedVals && gx > 1) gx /= 2;
+  hipLaunchKernelGGL(k_gram_mv8, dim3(gx, tiles), dim3(kGramThreads), 0, s, n, m1, m2, Q1, Q2, G, tiles_j,
+                     red.partials, red.tickets + ticket);
+}
+
+// ---------------------------------------------------------------------------------------------
+// a9 diagonal block, fused column MGS (kernels_cpp.hh:202-229).  Pass k (0..8) over the n x 8
+// block Qb, one thread per row.  Ssum (8x8) holds the RAW sums s[k][j] = q_k . q_j of each pass
+// (so a distributed run can allreduce them between passes); pass k first finalises row k-1
+// exactly like the reference,  S[k-1][j] = s/s[k-1][k-1] (j > k-1), S[k-1][k-1] = 1/sqrt(s),
+// then applies it:  q_j -= S[k-1][j] q_{k-1} (j > k-1), q_{k-1} *= S[k-1][k-1], and (k < 8)
+// accumulates the new sums s[k][j] (j >= k) on the updated row.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kStreamThreads) void k_mgs_pass(i64 n, double *__restrict__ Qb, int k,
+                                                             double *__restrict__ Ssum, double *partials,
+                                                             unsigned *ticket)
+{
+  __shared__ double tot[8];
+  double sp[8];
+  if (k > 0)
+  {
+    const int kp = k - 1;
+    const double skk = Ssum[kp * 8 + kp];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      sp[j] = (j > kp) ? Ssum[kp * 8 + j] / skk : ((j == kp) ? 1.0 / sqrt(skk) : 0.0);
+  }
+  double acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = 0.0;
+  for (i64 i = (i64)blockIdx.x * kStreamThreads + threadIdx.x; i < n; i += (i64)gridDim.x * kStreamThreads)
+  {
+    double q[8];
+    double2 *row = reinterpret_cast<double2 *>(Qb + i * 8);
+#pragma unroll
+    for (int h = 0; h < 4; ++h)
+    {
+      const double2 v = row[h];
+      q[2 * h] = v.x;
+      q[2 * h + 1] = v.y;
+    }
+    if (k > 0)
+    {
+      const int kp = k - 1;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (j > kp) q[j] -= sp[j] * q[kp];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (j == kp) q[j] *= sp[kp];
+#pragma unroll
+      for (int h = 0; h < 4; ++h) row[h] = make_double2(q[2 * h], q[2 * h + 1]);
+    }
+    if (k < 8)
+    {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (j >= k) acc[j] += q[k] * q[j];
+    }
+  }
+  if (k >= 8) return;
+  if (grid_sum<8, kStreamThreads>(acc, partials, ticket, tot))
+  {
+    if (threadIdx.x < 8) Ssum[k * 8 + threadIdx.x] = (threadIdx.x >= (unsigned)k) ? tot[threadIdx.x] : 0.0;
+  }
+}
+
+void launch_mgs_pass(i64 n, double *Qb, int k, double *Ssum, int ticket, hipStream_t s, ReduceWS red)
+{
+  const int G = grid_for(n, kStreamThreads * 4, 1024);
+  hipLaunchKernelGGL(k_mgs_pass, dim3(G), dim3(kStreamThreads), 0, s, n, Qb, k, Ssum, red.partials,
+                     red.tickets + ticket);
+}
+
+// ---------------------------------------------------------------------------------------------
+// CholQR factor of an 8x8 Gram (kernels_avx2.hh:185-252 / kernels_cpp.hh:474-526), one thread:
+// LU without pivoting, D = diag^-1/2, U = L^-T D.  flags & 1: take the UPPER triangle of G and
+// mirror it (B_orthonormalize_blocked :457-459), and fold max_{k<j} G[k][j] into *normmax.
+// Writes U (8x8 row-major).  A non-positive pivot yields NaN/inf like the reference.
+// ---------------------------------------------------------------------------------------------
+__global__ void k_cholqr_factor(const double *__restrict__ G, double *__restrict__ U, double *normmax, int flags)
+{
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  double s[8][8], LU[8][8], UU[8][8], D[8];
+  for (int i = 0; i < 8; ++i)
+    for (int j = 0; j < 8; ++j) s[i][j] = G[i * 8 + j];
+  if (flags & 1)
+  {
+    for (int k = 0; k < 8; ++k)
+      for (int j = 0; j < k; ++j) s[k][j] = s[j][k];
+    double nm = normmax[0];
+    for (int k = 0; k < 8; ++k)
+      for (int j = k + 1; j < 8; ++j) nm = fmax(nm, s[k][j]);
+    normmax[0] = nm;
+  }
+  for (int i = 0; i < 8; ++i)
+    for (int j = 0; j < 8; ++j) LU[i][j] = s[i][j];
+  for (int k = 0; k < 8; ++k)
+    for (int i = k + 1; i < 8; ++i)
+    {
+      LU[i][k] /= LU[k][k];
+      for (int j = k + 1; j < 8; ++j) LU[i][j] -= LU[i][k] * LU[k][j];
+    }
+  for (int i = 0; i < 8; ++i) D[i] = 1.0 / sqrt(LU[i][i]);
+  for (int i = 0; i < 8; ++i)
+  {
+    LU[i][i] = 1.0;
+    for (int j = i + 1; j < 8; ++j) LU[i][j] = 0.0;
+  }
+  for (int i = 0; i < 8; ++i)
+    for (int j = 0; j < 8; ++j) UU[i][j] = (i == j) ? 1.0 : 0.0;
+  for (int i = 1; i < 8; ++i)
+    for (int j = 0; j < i; ++j)
+      for (int k = 0; k < 8; ++k) UU[i][k] -= LU[i][j] * UU[j][k];
+  for (int i = 0; i < 8; ++i)
+    for (int j = 0; j < i; ++j)
+    {
+      double tmp = UU[i][j];
+      UU[i][j] = UU[j][i];
+      UU[j][i] = tmp;
+    }
+  for (int i = 0; i < 8; ++i)
+    for (int j = i; j < 8; ++j) UU[i][j] *= D[j];
+  for (int i = 0; i < 8; ++i)
+    for (int j = 0; j < 8; ++j) U[i * 8 + j] = UU[i][j];
+}
+
+void launch_cholqr_factor(const double *G, double *U, double *normmax, int flags, hipStream_t s)
+{
+  hipLaunchKernelGGL(k_cholqr_factor, dim3(1), dim3(64), 0, s, G, U, normmax, flags);
+}
+
+// v_i := v_i U in place, j descending, sum over k <= j (kernels_cpp.hh:556-568).
+__global__ __launch_bounds__(kStreamThreads) void k_apply_upper(i64 n, double *__restrict__ Qb,
+                                                                const double *__restrict__ Ug)
+{
+  __shared__ double U[64];
+  if (threadIdx.x < 64) U[threadIdx.x] = Ug[threadIdx.x];
+  __syncthreads();
+  for (i64 i = (i64)blockIdx.x * kStreamThreads + threadIdx.x; i < n; i += (i64)gridDim.x * kStreamThreads)
+  {
+    double v[8];
+    double2 *row = reinterpret_cast<double2 *>(Qb + i * 8);
+#pragma unroll
+    for (int h = 0; h < 4; ++h)
+    {
+      const double2 x = row[h];
+      v[2 * h] = x.x;
+      v[2 * h + 1] = x.y;
+    }
+#pragma unroll
+    for (int j = 7; j >= 0; --j)
+    {
+      double sum = 0.0;
+#pragma unroll
+      for (int k = 0; k <= j; ++k) sum += v[k] * U[k * 8 + j];
+      v[j] = sum;
+    }
+#pragma unroll
+    for (int h = 0; h < 4; ++h) row[h] = make_double2(v[2 * h], v[2 * h + 1]);
+  }
+}
+
+void launch_apply_upper(i64 n, double *Qb, const double *U, hipStream_t s)
+{
+  hipLaunchKernelGGL(k_apply_upper, dim3(grid_for(n, kStreamThreads * 4, kStreamBlocks)), dim3(kStreamThreads), 0, s,
+                     n, Qb, U);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Later-block projection (kernels_cpp.hh:335-348): Q_rest(i, j) -= sum_k S[k][j] Q_k(i, k), k
+// ascending, element by element in the reference order.  S is 8 x mrest row-major (the Gram
+// Q_k^T Q_rest).  One thread per (row, column block of Q_rest).
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kStreamThreads) void k_project(i64 n, i64 mrest, const double *__restrict__ Qk,
+                                                            double *__restrict__ Qrest, const double *__restrict__ S)
+{
+  const int nb = (int)(mrest / 8);
+  const i64 total = n * nb;
+  for (i64 idx = (i64)blockIdx.x * kStreamThreads + threadIdx.x; idx < total; idx += (i64)gridDim.x * kStreamThreads)
+  {
+    const int b = (int)(idx / n);
+    const i64 i = idx - (i64)b * n;
+    double qk[8], qj[8];
+    const double2 *rk = reinterpret_cast<const double2 *>(Qk + i * 8);
+    double2 *rj = reinterpret_cast<double2 *>(Qrest + ((i64)b * n + i) * 8);
+#pragma unroll
+    for (int h = 0; h < 4; ++h)
+    {
+      const double2 x = rk[h], y = rj[h];
+      qk[2 * h] = x.x;
+      qk[2 * h + 1] = x.y;
+      qj[2 * h] = y.x;
+      qj[2 * h + 1] = y.y;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+    {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qj[j] -= S[k * mrest + b * 8 + j] * qk[k];
+    }
+#pragma unroll
+    for (int h = 0; h < 4; ++h) rj[h] = make_double2(qj[2 * h], qj[2 * h + 1]);
+  }
+}
+
+void launch_project(i64 n, i64 mrest, const double *Qk, double *Qrest, const double *S, hipStream_t s)
+{
+  if (mrest <= 0) return;
+  hipLaunchKernelGGL(k_project, dim3(grid_for(n * (mrest / 8), kStreamThreads * 4, kStreamBlocks)),
+                     dim3(kStreamThreads), 0, s, n, mrest, Qk, Qrest, S);
+}
+
+// *normmax = max(*normmax, max over S (rows x cols, row-major) [strict upper triangle only]).
+__global__ void k_max_offdiag(const double *S, i64 rows, i64 cols, int upper_only, double *normmax)
+{
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  double nm = normmax[0];
+  for (i64 k = 0; k < rows; ++k)
+    for (i64 j = upper_only ? k + 1 : 0; j < cols; ++j) nm = fmax(nm, S[k * cols + j]);
+  normmax[0] = nm;
+}
+void launch_max_offdiag(const double *S, i64 rows, i64 cols, bool upper_only, double *normmax, hipStream_t s)
+{
+  hipLaunchKernelGGL(k_max_offdiag, dim3(1), dim3(64), 0, s, S, rows, cols, upper_only ? 1 : 0, normmax);
+}
+
+}  // namespace eigmi

@@ -1,0 +1,116 @@
+// reduce_dev.h -- deterministic grid-wide reductions for gfx950.
+//
+// Pattern (MI355X_MICROARCH "Valid forms", first row): every workgroup reduces its values
+// (wave shuffle tree + LDS, fixed order), ONE wave stores the block partials write-through
+// (`sc1`, agent-scope relaxed atomic stores), every wave drains `s_waitcnt vmcnt(0)`, a
+// workgroup barrier, then ONE lane takes an agent-scope ticket.  The workgroup whose ticket
+// comes last reads all partials with `sc1` loads and sums them in block-index order, so the
+// result does not depend on dispatch order or XCD placement and is bitwise reproducible.
+// The last workgroup also resets the ticket to zero for the next launch on the stream.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace eigmi {
+
+__device__ __forceinline__ double wave_sum(double v)
+{
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+  return v;  // valid in lane 0
+}
+
+__device__ __forceinline__ void st_sc1(double *p, double v)
+{
+  __hip_atomic_store(reinterpret_cast<unsigned long long *>(p), __double_as_longlong(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_sc1(const double *p)
+{
+  unsigned long long b = __hip_atomic_load(reinterpret_cast<const unsigned long long *>(p), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+  return __longlong_as_double((long long)b);
+}
+
+// Block-wide sum of NV values per thread, in a fixed order.  Result valid in thread 0's out[].
+template <int NV, int NT>
+__device__ __forceinline__ void block_sum(double (&v)[NV], double (&out)[NV])
+{
+  __shared__ double sh[NT / 64][NV];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+  {
+    double w = wave_sum(v[i]);
+    if (lane == 0) sh[wid][i] = w;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0)
+  {
+#pragma unroll
+    for (int i = 0; i < NV; ++i)
+    {
+      double s = 0.0;
+#pragma unroll
+      for (int w = 0; w < NT / 64; ++w) s += sh[w][i];
+      out[i] = s;
+    }
+  }
+}
+
+// Grid-wide sum.  Returns true in every thread of the LAST workgroup; there tot[0..NV) (LDS,
+// visible to all its threads) holds the grid totals.  partials: >= gridDim.x*NV doubles.
+template <int NV, int NT>
+__device__ bool grid_sum_n(double (&v)[NV], double *partials, unsigned *ticket, double *tot, unsigned bid,
+                           unsigned nblk);
+
+template <int NV, int NT>
+__device__ __forceinline__ bool grid_sum(double (&v)[NV], double *partials, unsigned *ticket, double *tot)
+{
+  return grid_sum_n<NV, NT>(v, partials, ticket, tot, blockIdx.x, gridDim.x);
+}
+
+// Same with an explicit reduction group: `nblk` workgroups with ids `bid` share one ticket and
+// partials[0 .. nblk*NV) (used by 2-D grids that run several independent reductions).
+template <int NV, int NT>
+__device__ bool grid_sum_n(double (&v)[NV], double *partials, unsigned *ticket, double *tot, unsigned bid,
+                           unsigned nblk)
+{
+  __shared__ unsigned s_last;
+  double bs[NV];
+  block_sum<NV, NT>(v, bs);
+  if (threadIdx.x == 0)
+  {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) st_sc1(&partials[(size_t)bid * NV + i], bs[i]);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+  {
+    unsigned prev = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = (prev == nblk - 1) ? 1u : 0u;
+  }
+  __syncthreads();
+  if (!s_last) return false;
+  // Last workgroup: thread t sums partials t, t+NT, ... then a fixed-order block tree.
+  double acc[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) acc[i] = 0.0;
+  for (unsigned b = threadIdx.x; b < nblk; b += NT)
+  {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) acc[i] += ld_sc1(&partials[(size_t)b * NV + i]);
+  }
+  double r[NV];
+  block_sum<NV, NT>(acc, r);
+  if (threadIdx.x == 0)
+  {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) tot[i] = r[i];
+    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  return true;
+}
+
+}  // namespace eigmi

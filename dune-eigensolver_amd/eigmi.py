@@ -1,0 +1,489 @@
+"""Python binding of libeigmi's C ABI (include/eigmi.h) -- the ctypes stub a maintainer would
+add on the reference side, plus thin host-side helpers for tests and the benchmark.
+
+The compute path is libeigmi.so (hand-written HIP for gfx950).  Loading fails loudly when the
+library is missing; there is no CPU fallback in this module.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libeigmi.so")
+
+EIG_OK, EIG_ERR_SHAPE, EIG_ERR_BLOCKSIZE, EIG_ERR_HIP, EIG_ERR_RCCL, EIG_ERR_BREAKDOWN, EIG_ERR_ARG, EIG_ERR_NODEVICE = range(8)
+ORTHO_MGS, ORTHO_CHOLQR = 0, 1
+WHICH_LA, WHICH_SA = 0, 1
+LANCZOS_TIME_KERNELS = 1
+GEN_LAPLACE2D, GEN_NEUMANN2D, GEN_PU2D, GEN_IDENTITY2D, GEN_POISSON3D, GEN_Q1ELAST3D = range(6)
+
+
+class EigError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"[{code}] {msg}")
+        self.code = code
+
+
+class EigShapeError(EigError, ValueError):
+    """SHAPE / BLOCKSIZE errors: the reference throws std::invalid_argument for these."""
+
+
+class _MatInfo(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_int64) for k in ("n", "n_global", "ncols", "row_begin", "window", "own_offset", "nnzb",
+                                              "nnzb_padded", "nslices")] + \
+               [("br", ctypes.c_int), ("bc", ctypes.c_int)] + \
+               [(k, ctypes.c_int64) for k in ("halo_recv", "halo_send", "device_bytes")]
+
+
+class Timing(ctypes.Structure):
+    _fields_ = [("total_ms", ctypes.c_double), ("spmv_ms", ctypes.c_double), ("update_ms", ctypes.c_double),
+                ("comm_ms", ctypes.c_double), ("spmv_launches", ctypes.c_int64)]
+
+
+_vp = ctypes.c_void_p
+_i64 = ctypes.c_int64
+_int = ctypes.c_int
+_dbl = ctypes.c_double
+_u = ctypes.c_uint
+
+# name -> (restype, argtypes); this is the complete exported surface of include/eigmi.h
+SIGNATURES = {
+    "eig_ctx_create": (_int, [_int, ctypes.POINTER(_vp)]),
+    "eig_ctx_destroy": (_int, [_vp]),
+    "eig_last_error": (ctypes.c_char_p, [_vp]),
+    "eig_ctx_sync": (_int, [_vp]),
+    "eig_ctx_stream": (_int, [_vp, ctypes.POINTER(_vp)]),
+    "eig_device_count": (_int, [ctypes.POINTER(_int)]),
+    "eig_version": (ctypes.c_char_p, []),
+    "eig_comm_unique_id": (_int, [ctypes.c_char_p]),
+    "eig_comm_init": (_int, [_vp, _int, _int, ctypes.c_char_p]),
+    "eig_comm_allreduce_sum": (_int, [_vp, _vp, _i64]),
+    "eig_comm_barrier": (_int, [_vp]),
+    "eig_malloc": (_int, [_vp, ctypes.c_size_t, ctypes.POINTER(_vp)]),
+    "eig_free": (_int, [_vp, _vp]),
+    "eig_memcpy_h2d": (_int, [_vp, _vp, _vp, ctypes.c_size_t]),
+    "eig_memcpy_d2h": (_int, [_vp, _vp, _vp, ctypes.c_size_t]),
+    "eig_memcpy_d2d": (_int, [_vp, _vp, _vp, ctypes.c_size_t]),
+    "eig_memset": (_int, [_vp, _vp, _int, ctypes.c_size_t]),
+    "eig_mat_create_bcsr": (_int, [_vp, _i64, _i64, _int, _int, _vp, _vp, _vp, ctypes.POINTER(_vp)]),
+    "eig_mat_create_bcsr_dist": (_int, [_vp, _i64, _i64, _i64, _int, _int, _vp, _vp, _vp, ctypes.POINTER(_vp)]),
+    "eig_mat_destroy": (_int, [_vp]),
+    "eig_mat_get_info": (_int, [_vp, ctypes.POINTER(_MatInfo)]),
+    "eig_mat_shift_diag": (_int, [_vp, _dbl]),
+    "eig_mv": (_int, [_vp, _vp, _vp]),
+    "eig_mv_host": (_int, [_vp, _vp, _vp]),
+    "eig_dot": (_int, [_vp, _i64, _vp, _vp, _vp]),
+    "eig_nrm2": (_int, [_vp, _i64, _vp, _vp]),
+    "eig_axpy": (_int, [_vp, _i64, _dbl, _vp, _vp]),
+    "eig_scal": (_int, [_vp, _i64, _dbl, _vp]),
+    "eig_copy": (_int, [_vp, _i64, _vp, _vp]),
+    "eig_spmm_mv8": (_int, [_vp, _i64, _vp, _vp]),
+    "eig_dot_diag_mv8": (_int, [_vp, _i64, _i64, _vp, _vp, _vp]),
+    "eig_gram_mv8": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _vp]),
+    "eig_orthonormalize_mv8": (_int, [_vp, _i64, _i64, _vp, _int]),
+    "eig_orthonormalize_naive": (_int, [_vp, _i64, _i64, _vp]),
+    "eig_b_orthonormalize_mv8": (_int, [_vp, _i64, _vp, _vp]),
+    "eig_random_mv8": (_int, [_vp, _i64, _i64, _u, _vp]),
+    "eig_standard_largest": (_int, [_vp, _dbl, _dbl, _int, _int, _u, _vp, _vp, ctypes.POINTER(_int), _int]),
+    "eig_lanczos_run": (_int, [_vp, _int, _vp, _u, _int, _vp, _vp, ctypes.POINTER(Timing)]),
+    "eig_lanczos_solve": (_int, [_vp, _int, _int, _int, _u, _vp, _vp, _vp]),
+    "eig_lanczos_create": (_int, [_vp, _int, _vp, _u, ctypes.POINTER(_vp)]),
+    "eig_lanczos_step": (_int, [_vp, _int, _int, ctypes.POINTER(Timing)]),
+    "eig_lanczos_tridiag": (_int, [_vp, ctypes.POINTER(_int), _vp, _vp]),
+    "eig_lanczos_destroy": (_int, [_vp]),
+    "eig_flops_orthonormalize": (_dbl, [_i64, _i64]),
+    "eig_bytes_orthonormalize_blocked": (_dbl, [_i64, _i64, _int]),
+    "eig_gen_nnzb": (_i64, [_int, _int]),
+    "eig_gen_matrix": (_int, [_int, _int, _int, _vp, _vp, _vp]),
+    "eig_gen_nnzb_rows": (_i64, [_int, _int, _i64, _i64]),
+    "eig_gen_matrix_rows": (_int, [_int, _int, _i64, _i64, _vp, _vp, _vp]),
+    "eig_plan_window": (_int, [_i64, _i64, _int, _vp, _vp, _vp]),
+    "eig_plan_halo": (_int, [_int, _int, _vp, _int, _i64, _vp, ctypes.POINTER(_int), _vp, ctypes.POINTER(_int)]),
+}
+
+
+def load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"libeigmi.so not built ({LIB_PATH}); run `make -C dune-eigensolver_amd` "
+                          "or __graft_entry__.build() -- there is no CPU fallback")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    return lib
+
+
+lib = load()
+
+
+def _np_ptr(a):
+    return a.ctypes.data_as(_vp)
+
+
+def device_count():
+    c = _int(0)
+    lib.eig_device_count(ctypes.byref(c))
+    return c.value
+
+
+class Context:
+    """eig_ctx_t: one GPU, one HIP stream, optional RCCL communicator."""
+
+    def __init__(self, device=0):
+        h = _vp()
+        rc = lib.eig_ctx_create(device, ctypes.byref(h))
+        if rc != EIG_OK:
+            raise EigError(rc, lib.eig_last_error(None).decode())
+        self.h = h
+        self.device = device
+        self.nranks, self.rank = 1, 0
+
+    def check(self, rc):
+        if rc != EIG_OK:
+            msg = lib.eig_last_error(self.h).decode()
+            if rc in (EIG_ERR_SHAPE, EIG_ERR_BLOCKSIZE):
+                raise EigShapeError(rc, msg)
+            raise EigError(rc, msg)
+
+    def close(self):
+        if self.h:
+            lib.eig_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def sync(self):
+        self.check(lib.eig_ctx_sync(self.h))
+
+    # --- communicator
+    @staticmethod
+    def unique_id():
+        buf = ctypes.create_string_buffer(128)
+        rc = lib.eig_comm_unique_id(buf)
+        if rc != EIG_OK:
+            raise EigError(rc, lib.eig_last_error(None).decode())
+        return buf.raw
+
+    def comm_init(self, nranks, rank, uid):
+        self.check(lib.eig_comm_init(self.h, nranks, rank, uid))
+        self.nranks, self.rank = nranks, rank
+
+    def barrier(self):
+        self.check(lib.eig_comm_barrier(self.h))
+
+    # --- memory
+    def empty(self, n):
+        return DeviceArray(self, n)
+
+    def array(self, host):
+        host = np.ascontiguousarray(host, dtype=np.float64)
+        d = DeviceArray(self, host.size)
+        d.upload(host)
+        return d
+
+    def zeros(self, n):
+        d = DeviceArray(self, n)
+        self.check(lib.eig_memset(self.h, d.ptr, 0, max(n, 1) * 8))
+        return d
+
+
+class DeviceArray:
+    """A float64 device buffer owned by the library allocator."""
+
+    def __init__(self, ctx, n):
+        self.ctx, self.n = ctx, int(n)
+        p = _vp()
+        ctx.check(lib.eig_malloc(ctx.h, max(self.n, 1) * 8, ctypes.byref(p)))
+        self.ptr = p
+
+    def offset(self, k):
+        """Raw pointer to element k (for window / owned-slice addressing)."""
+        return _vp(self.ptr.value + 8 * int(k))
+
+    def upload(self, host, at=0):
+        host = np.ascontiguousarray(host, dtype=np.float64)
+        assert at + host.size <= self.n
+        self.ctx.check(lib.eig_memcpy_h2d(self.ctx.h, self.offset(at), _np_ptr(host), host.size * 8))
+
+    def get(self, count=None, at=0):
+        count = self.n - at if count is None else count
+        out = np.empty(count, np.float64)
+        self.ctx.check(lib.eig_memcpy_d2h(self.ctx.h, _np_ptr(out), self.offset(at), count * 8))
+        return out
+
+    def free(self):
+        if self.ptr is not None and self.ctx.h:
+            lib.eig_free(self.ctx.h, self.ptr)
+        self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Matrix:
+    """eig_mat_t: a BCRSMatrix<FieldMatrix<double,br,bc>> in HBM (SELL-64 image)."""
+
+    def __init__(self, ctx, handle):
+        self.ctx, self.h = ctx, handle
+        info = _MatInfo()
+        ctx.check(lib.eig_mat_get_info(handle, ctypes.byref(info)))
+        self.info = info
+
+    @classmethod
+    def from_bcsr(cls, ctx, rowptr, col, vals, br=1, bc=1, ncols_blocks=None):
+        rowptr = np.ascontiguousarray(rowptr, np.int64)
+        col = np.ascontiguousarray(col, np.int32)
+        vals = np.ascontiguousarray(vals, np.float64)
+        nb = rowptr.size - 1
+        nbc = nb if ncols_blocks is None else ncols_blocks
+        h = _vp()
+        ctx.check(lib.eig_mat_create_bcsr(ctx.h, nb, nbc, br, bc, _np_ptr(rowptr), _np_ptr(col), _np_ptr(vals),
+                                          ctypes.byref(h)))
+        return cls(ctx, h)
+
+    @classmethod
+    def from_rows(cls, ctx, nb_global, row_begin, rowptr, col, vals, br=1, bc=1):
+        rowptr = np.ascontiguousarray(rowptr, np.int64)
+        col = np.ascontiguousarray(col, np.int32)
+        vals = np.ascontiguousarray(vals, np.float64)
+        h = _vp()
+        ctx.check(lib.eig_mat_create_bcsr_dist(ctx.h, nb_global, row_begin, rowptr.size - 1, br, bc, _np_ptr(rowptr),
+                                               _np_ptr(col), _np_ptr(vals), ctypes.byref(h)))
+        return cls(ctx, h)
+
+    def close(self):
+        if self.h:
+            lib.eig_mat_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def n(self):
+        return self.info.n
+
+    def window_vector(self, owned=None):
+        """Zeroed window-layout vector; `owned` (host, n) goes to the owned slice."""
+        v = self.ctx.zeros(self.info.window)
+        if owned is not None:
+            v.upload(owned, at=self.info.own_offset)
+        return v
+
+    def owned(self, v):
+        return v.get(self.info.n, at=self.info.own_offset)
+
+    def mv(self, x, y):
+        self.ctx.check(lib.eig_mv(self.h, x.ptr, y.ptr))
+
+    def mv_host(self, x):
+        x = np.ascontiguousarray(x, np.float64)
+        y = np.zeros(self.info.n)
+        self.ctx.check(lib.eig_mv_host(self.h, _np_ptr(x), _np_ptr(y)))
+        return y
+
+    def shift_diag(self, shift):
+        self.ctx.check(lib.eig_mat_shift_diag(self.h, shift))
+
+
+# --------------------------------------------------------------------------------------- ops
+def dot(ctx, n, x, y, out, xo=0, yo=0):
+    ctx.check(lib.eig_dot(ctx.h, n, x.offset(xo), y.offset(yo), out.ptr))
+
+
+def nrm2(ctx, n, x, out, xo=0):
+    ctx.check(lib.eig_nrm2(ctx.h, n, x.offset(xo), out.ptr))
+
+
+def axpy(ctx, n, a, x, y):
+    ctx.check(lib.eig_axpy(ctx.h, n, a, x.ptr, y.ptr))
+
+
+def scal(ctx, n, a, x):
+    ctx.check(lib.eig_scal(ctx.h, n, a, x.ptr))
+
+
+def copy(ctx, n, x, y):
+    ctx.check(lib.eig_copy(ctx.h, n, x.ptr, y.ptr))
+
+
+def spmm_mv8(A, m, Qin, Qout):
+    A.ctx.check(lib.eig_spmm_mv8(A.h, m, Qin.ptr, Qout.ptr))
+
+
+def dot_diag_mv8(ctx, n, m, Q1, Q2, dp):
+    ctx.check(lib.eig_dot_diag_mv8(ctx.h, n, m, Q1.ptr, Q2.ptr, dp.ptr))
+
+
+def gram_mv8(ctx, n, m1, m2, Q1, Q2, G):
+    ctx.check(lib.eig_gram_mv8(ctx.h, n, m1, m2, Q1.ptr, Q2.ptr, G.ptr))
+
+
+def orthonormalize_mv8(ctx, n, m, Q, variant=ORTHO_MGS):
+    ctx.check(lib.eig_orthonormalize_mv8(ctx.h, n, m, Q.ptr, variant))
+
+
+def orthonormalize_naive(ctx, n, m, Q):
+    ctx.check(lib.eig_orthonormalize_naive(ctx.h, n, m, Q.ptr))
+
+
+def b_orthonormalize_mv8(B, m, Q, norm):
+    B.ctx.check(lib.eig_b_orthonormalize_mv8(B.h, m, Q.ptr, norm.ptr))
+
+
+def random_mv8(ctx, n, m, seed, Q):
+    ctx.check(lib.eig_random_mv8(ctx.h, n, m, seed, Q.ptr))
+
+
+def standard_largest(A, shift, tol, maxiter, nev, seed=123, want_evec=True, verbose=0):
+    ev = np.zeros(nev)
+    evec = np.zeros(nev * A.n) if want_evec else None
+    it = _int(0)
+    A.ctx.check(lib.eig_standard_largest(A.h, shift, tol, maxiter, nev, seed, _np_ptr(ev),
+                                         _np_ptr(evec) if want_evec else None, ctypes.byref(it), verbose))
+    return ev, (evec.reshape(nev, A.n) if want_evec else None), it.value
+
+
+def lanczos_run(A, steps, u0=None, seed=123, timed=False):
+    alpha = np.zeros(max(steps, 1))
+    beta = np.zeros(steps + 1)
+    t = Timing()
+    A.ctx.check(lib.eig_lanczos_run(A.h, steps, u0.ptr if u0 is not None else None, seed,
+                                    LANCZOS_TIME_KERNELS if timed else 0, _np_ptr(alpha), _np_ptr(beta),
+                                    ctypes.byref(t)))
+    return alpha[:steps], beta, t
+
+
+class LanczosWorkspace:
+    """eig_lanczos_t: the three-term recurrence as a persistent workspace (setup outside any
+    timed region; step() advances and returns the eig_timing of that batch)."""
+
+    def __init__(self, A, max_steps, u0=None, seed=123):
+        self.A = A
+        h = _vp()
+        A.ctx.check(lib.eig_lanczos_create(A.h, max_steps, u0.ptr if u0 is not None else None, seed,
+                                           ctypes.byref(h)))
+        self.h = h
+
+    def step(self, steps, timed=False):
+        t = Timing()
+        self.A.ctx.check(lib.eig_lanczos_step(self.h, steps, LANCZOS_TIME_KERNELS if timed else 0, ctypes.byref(t)))
+        return t
+
+    def tridiag(self):
+        k = _int(0)
+        self.A.ctx.check(lib.eig_lanczos_tridiag(self.h, ctypes.byref(k), None, None))
+        alpha = np.zeros(max(k.value, 1))
+        beta = np.zeros(k.value + 1)
+        self.A.ctx.check(lib.eig_lanczos_tridiag(self.h, ctypes.byref(k), _np_ptr(alpha), _np_ptr(beta)))
+        return alpha[:k.value], beta
+
+    def close(self):
+        if self.h:
+            lib.eig_lanczos_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def lanczos_solve(A, nev, ncv, which=WHICH_LA, seed=123, want_evec=True):
+    ev = np.zeros(nev)
+    evec = np.zeros(nev * A.n) if want_evec else None
+    res = np.zeros(nev)
+    A.ctx.check(lib.eig_lanczos_solve(A.h, nev, ncv, which, seed, _np_ptr(ev), _np_ptr(evec) if want_evec else None,
+                                      _np_ptr(res)))
+    return ev, (evec.reshape(nev, A.n) if want_evec else None), res
+
+
+# --------------------------------------------------------------------------------------- generators
+def gen_matrix(kind, N, overlap=3):
+    nnzb = lib.eig_gen_nnzb(kind, N)
+    nrows = N * N if kind <= 3 else N ** 3
+    bb = 9 if kind == GEN_Q1ELAST3D else 1
+    rp = np.zeros(nrows + 1, np.int64)
+    c = np.zeros(nnzb, np.int32)
+    v = np.zeros(nnzb * bb, np.float64)
+    rc = lib.eig_gen_matrix(kind, N, overlap, _np_ptr(rp), _np_ptr(c), _np_ptr(v))
+    if rc != EIG_OK:
+        raise EigError(rc, "eig_gen_matrix failed")
+    return rp, c, v
+
+
+def gen_rows(kind, N, row_begin, nrows):
+    nnzb = lib.eig_gen_nnzb_rows(kind, N, row_begin, nrows)
+    bb = 9 if kind == GEN_Q1ELAST3D else 1
+    rp = np.zeros(nrows + 1, np.int64)
+    c = np.zeros(max(nnzb, 1), np.int32)
+    v = np.zeros(max(nnzb, 1) * bb, np.float64)
+    rc = lib.eig_gen_matrix_rows(kind, N, row_begin, nrows, _np_ptr(rp), _np_ptr(c), _np_ptr(v))
+    if rc != EIG_OK:
+        raise EigError(rc, "eig_gen_matrix_rows failed")
+    return rp, c, v
+
+
+def row_partition(n, nranks, rank, align=1):
+    """Contiguous row block of `rank` (z-slabs for the 3-D stencil when align = N*N)."""
+    units = n // align
+    b = (units * rank) // nranks
+    e = (units * (rank + 1)) // nranks
+    if rank == nranks - 1:
+        return b * align, n - b * align
+    return b * align, (e - b) * align
+
+
+# Algorithmic byte models (DESIGN.md "Roofline accounting")
+def bytes_spmv(n, nnz):
+    return 12 * nnz + 4 * (n + 1) + 16 * n
+
+
+def bytes_lanczos_step(n, nnz):
+    return bytes_spmv(n, nnz) + 32 * n
+
+
+def bytes_lanczos_k1(n, nnz):
+    """Fused SpMV kernel of a Lanczos step: CSR stream + x + y write + u_{j-1} read."""
+    return bytes_spmv(n, nnz) + 8 * n
+
+
+# --------------------------------------------------------------------------------------- planning
+def plan_window(row_begin, nb_local, rowptr, col, bc=1):
+    """-> (win_begin_blk, window, own_offset, cmin, cmax) -- eig_plan_window."""
+    out = np.zeros(5, np.int64)
+    rowptr = np.ascontiguousarray(rowptr, np.int64)
+    col = np.ascontiguousarray(col, np.int32)
+    rc = lib.eig_plan_window(row_begin, nb_local, bc, _np_ptr(rowptr), _np_ptr(col), _np_ptr(out))
+    if rc != EIG_OK:
+        raise EigError(rc, "eig_plan_window failed")
+    return tuple(int(v) for v in out)
+
+
+def plan_halo(nranks, me, ranks, win_begin_blk, bc=1):
+    """ranks: (nranks, 4) int64 [row_begin, nb_local, cmin, cmax] -> (recvs, sends), lists of
+    (peer, window offset, count) -- eig_plan_halo."""
+    ranks = np.ascontiguousarray(ranks, np.int64).reshape(-1)
+    rv = np.zeros(3 * nranks, np.int64)
+    sd = np.zeros(3 * nranks, np.int64)
+    nr, ns = _int(0), _int(0)
+    rc = lib.eig_plan_halo(nranks, me, _np_ptr(ranks), bc, win_begin_blk, _np_ptr(rv), ctypes.byref(nr),
+                           _np_ptr(sd), ctypes.byref(ns))
+    if rc != EIG_OK:
+        raise EigError(rc, "eig_plan_halo failed")
+    recvs = [tuple(int(x) for x in rv[3 * k:3 * k + 3]) for k in range(nr.value)]
+    sends = [tuple(int(x) for x in sd[3 * k:3 * k + 3]) for k in range(ns.value)]
+    return recvs, sends

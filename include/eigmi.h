@@ -1,0 +1,235 @@
+/* eigmi.h -- C ABI of the MI355X-native eigensolver inner loop (libeigmi.so).
+ *
+ * Drop-in boundary for the dune-eigensolver hot path.  Plain C: opaque
+ * handles, raw pointers, sizes, int status codes.  No HIP / torch / ISTL types appear here;
+ * the header-only C++ facade (eigmi.hh) maps these calls onto the reference's ISTL-style API.
+ *
+ * Conventions
+ *  - Every `double*` vector / multivector argument is a DEVICE pointer unless the name ends in
+ *    `_host`.  Small results (dot products, Gram matrices, norms) are written to DEVICE memory
+ *    so that iterations never synchronise with the host; eigmi.hh copies them back.
+ *  - Calls are stream-ordered on the context's stream; eig_ctx_sync() waits.  Calls that return
+ *    host results (suffix _host, the drivers) are synchronous at return, like the reference.
+ *  - MultiVector<double,8> buffers use the reference's block-column-major layout
+ *    ((j/8)*n + i)*8 + j%8 (multivector.hh:130-139), so a host MultiVector mirrors with one copy.
+ *  - Distributed vectors (a context with a communicator) use the matrix's WINDOW layout:
+ *    length info.window, owned rows at offset info.own_offset; ghost rows are filled by the
+ *    halo exchange inside eig_mv / the drivers.  On one rank window == n, own_offset == 0.
+ *  - Errors: 0 = EIG_OK; otherwise an EIG_ERR_* code and eig_last_error(ctx) holds the message.
+ *    The C++ facade rethrows SHAPE / BLOCKSIZE as std::invalid_argument, like the reference
+ *    (kernels_cpp.hh:29-32, :632-633; multivector.hh:48-49).
+ */
+#ifndef EIGMI_H
+#define EIGMI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define EIGMI_VERSION_MAJOR 0
+#define EIGMI_VERSION_MINOR 1
+
+enum eig_status {
+  EIG_OK = 0,
+  EIG_ERR_SHAPE = 1,      /* size mismatch (reference: std::invalid_argument "... does not match") */
+  EIG_ERR_BLOCKSIZE = 2,  /* unsupported block size (reference: "only implemented for FieldMatrix<..,1,1>") */
+  EIG_ERR_HIP = 3,        /* HIP runtime failure */
+  EIG_ERR_RCCL = 4,       /* RCCL failure */
+  EIG_ERR_BREAKDOWN = 5,  /* Krylov breakdown (beta == 0) or non-positive pivot in (B-)Gram-Schmidt */
+  EIG_ERR_ARG = 6,        /* invalid argument (null handle, negative size, bad enum) */
+  EIG_ERR_NODEVICE = 7    /* no HIP device visible */
+};
+
+typedef struct eig_ctx_s *eig_ctx_t;
+typedef struct eig_mat_s *eig_mat_t;
+
+/* ---------------------------------------------------------------- context ------------------ */
+/* One context = one GPU + one HIP stream (+ optional RCCL communicator).  One per host thread. */
+int eig_ctx_create(int device, eig_ctx_t *ctx);
+int eig_ctx_destroy(eig_ctx_t ctx);
+const char *eig_last_error(eig_ctx_t ctx);
+int eig_ctx_sync(eig_ctx_t ctx);
+/* The hipStream_t the context enqueues on, as an opaque pointer. */
+int eig_ctx_stream(eig_ctx_t ctx, void **stream);
+int eig_device_count(int *count);
+/* Library version string, e.g. "eigmi 0.1 gfx950". */
+const char *eig_version(void);
+
+/* ---------------------------------------------------------------- communicator ------------- */
+/* RCCL bootstrap in the ncclGetUniqueId / ncclCommInitRank pattern: rank 0 calls
+ * eig_comm_unique_id, the 128 bytes travel by any side channel (MPI_Bcast, a TCP store),
+ * then every rank calls eig_comm_init.  Afterwards dots / norms are global (allreduce over
+ * xGMI) and matrices created with eig_mat_create_bcsr_dist exchange halos. */
+int eig_comm_unique_id(unsigned char id[128]);
+int eig_comm_init(eig_ctx_t ctx, int nranks, int rank, const unsigned char id[128]);
+int eig_comm_allreduce_sum(eig_ctx_t ctx, double *buf, int64_t count);
+int eig_comm_barrier(eig_ctx_t ctx);
+
+/* ---------------------------------------------------------------- device memory ------------ */
+int eig_malloc(eig_ctx_t ctx, size_t bytes, void **ptr);
+int eig_free(eig_ctx_t ctx, void *ptr);
+int eig_memcpy_h2d(eig_ctx_t ctx, void *dst, const void *src_host, size_t bytes);
+int eig_memcpy_d2h(eig_ctx_t ctx, void *dst_host, const void *src, size_t bytes);
+int eig_memcpy_d2d(eig_ctx_t ctx, void *dst, const void *src, size_t bytes);
+int eig_memset(eig_ctx_t ctx, void *dst, int value, size_t bytes);
+
+/* ---------------------------------------------------------------- matrices ----------------- */
+/* Replaces Dune::BCRSMatrix<FieldMatrix<double,br,bc>> on the device.  Host arrays follow the
+ * ISTL row/col iteration (kernels_cpp.hh:644-655): rowptr[nb_rows+1] (int64), col[nnzb]
+ * (int32 block column, ascending per row), vals[nnzb*br*bc] (row-major blocks, FieldMatrix
+ * layout).  Supported blocks: br, bc in 1..4 (any combination).  The device copy is a sliced
+ * ELLPACK (SELL-64, one wavefront per 64-row slice) that keeps every row's stored order, so
+ * y = A x is bitwise identical to BCRSMatrix::mv. */
+int eig_mat_create_bcsr(eig_ctx_t ctx, int64_t nb_rows, int64_t nb_cols, int br, int bc,
+                        const int64_t *rowptr_host, const int32_t *col_host, const double *vals_host,
+                        eig_mat_t *mat);
+/* Row-partitioned variant: this rank owns global block rows [row_begin, row_begin+nb_rows_local);
+ * rowptr/col/vals describe those rows only, col holds GLOBAL block columns.  Collective over
+ * the context's communicator (the halo plan is agreed with the other ranks). */
+int eig_mat_create_bcsr_dist(eig_ctx_t ctx, int64_t nb_rows_global, int64_t row_begin,
+                             int64_t nb_rows_local, int br, int bc, const int64_t *rowptr_host,
+                             const int32_t *col_host, const double *vals_host, eig_mat_t *mat);
+int eig_mat_destroy(eig_mat_t mat);
+
+typedef struct eig_mat_info {
+  int64_t n;            /* owned scalar rows (nb_rows_local * br) */
+  int64_t n_global;     /* global scalar rows */
+  int64_t ncols;        /* scalar columns (global) */
+  int64_t row_begin;    /* first owned global scalar row */
+  int64_t window;       /* length of a distributed vector buffer (scalar entries) */
+  int64_t own_offset;   /* offset of the owned rows inside the window */
+  int64_t nnzb;         /* stored blocks (true, not padded) */
+  int64_t nnzb_padded;  /* blocks in the SELL-64 image including padding */
+  int64_t nslices;
+  int br, bc;
+  int64_t halo_recv;    /* ghost scalar entries received per exchange */
+  int64_t halo_send;    /* scalar entries sent per exchange */
+  int64_t device_bytes; /* matrix image size in HBM */
+} eig_mat_info;
+int eig_mat_get_info(eig_mat_t mat, eig_mat_info *info);
+
+/* a13: A += shift*I on the diagonal of every diagonal block (eigensolver.hh:59-66). */
+int eig_mat_shift_diag(eig_mat_t mat, double shift);
+
+/* a4: y = A x  (BCRSMatrix::mv; the ARPACK++ multMvB callback, arpack_geneo_wrapper.hh:269-279).
+ * x: window layout (ghosts exchanged here when distributed); y: owned rows written at own_offset. */
+int eig_mv(eig_mat_t mat, const double *x, double *y);
+/* Same with caller-owned HOST arrays of length n (ARPACK's workd): stage, multiply, copy back. */
+int eig_mv_host(eig_mat_t mat, const double *x_host, double *y_host);
+
+/* ---------------------------------------------------------------- BlockVector ops ---------- */
+/* n = owned length; pointers address the owned slice.  Results to device memory. */
+int eig_dot(eig_ctx_t ctx, int64_t n, const double *x, const double *y, double *result);
+int eig_nrm2(eig_ctx_t ctx, int64_t n, const double *x, double *result);
+int eig_axpy(eig_ctx_t ctx, int64_t n, double a, const double *x, double *y);   /* y += a x */
+int eig_scal(eig_ctx_t ctx, int64_t n, double a, double *x);                    /* x *= a */
+int eig_copy(eig_ctx_t ctx, int64_t n, const double *x, double *y);
+
+/* ---------------------------------------------------------------- MultiVector<double,8> ---- */
+/* a2: Qout = A Qin, m columns (m % 8 == 0), br = bc = 1 (kernels_cpp.hh:626-657). */
+int eig_spmm_mv8(eig_mat_t mat, int64_t m, const double *Qin, double *Qout);
+/* a5: dp[j] = q1_j . q2_j, j < m (kernels_cpp.hh:24-55).  dp: device, m doubles. */
+int eig_dot_diag_mv8(eig_ctx_t ctx, int64_t n, int64_t m, const double *Q1, const double *Q2, double *dp);
+/* a6: G = Q1^T Q2 (m1 x m2, row-major, device) -- the tall-skinny panel product, on MFMA
+ * (v_mfma_f64_16x16x4f64).  Q1 has m1 columns, Q2 m2 columns, both MultiVector<double,8>. */
+int eig_gram_mv8(eig_ctx_t ctx, int64_t n, int64_t m1, int64_t m2, const double *Q1, const double *Q2, double *G);
+/* a9 / a10: orthonormalise the m columns of Q in place.
+ * EIG_ORTHO_MGS    = orthonormalize_blocked (kernels_cpp.hh:180-351): diagonal block by column MGS,
+ *                    later blocks by one block-CGS pass.
+ * EIG_ORTHO_CHOLQR = orthonormalize_avx2_b8_v2 / _neon_b8_v2 (kernels_avx2.hh:385-622): CholQR of
+ *                    the diagonal block, one 8x8 projection per later block. */
+enum eig_ortho_variant { EIG_ORTHO_MGS = 0, EIG_ORTHO_CHOLQR = 1 };
+int eig_orthonormalize_mv8(eig_ctx_t ctx, int64_t n, int64_t m, double *Q, int variant);
+/* a8: orthonormalize_naive on a column-major (MultiVector<double,1>) block (kernels_cpp.hh:121-155). */
+int eig_orthonormalize_naive(eig_ctx_t ctx, int64_t n, int64_t m, double *Q);
+/* a11: B-orthonormalise Q (B_orthonormalize_blocked, kernels_cpp.hh:356-591); *norm (device)
+ * receives the max off-diagonal R coefficient the reference returns. */
+int eig_b_orthonormalize_mv8(eig_mat_t B, int64_t m, double *Q, double *norm);
+/* eigensolver.hh:49-55 start block: mt19937(seed) + normal_distribution(0,1), fill order
+ * (block, row, col); generated on the host (bitwise the reference's numbers), uploaded. */
+int eig_random_mv8(eig_ctx_t ctx, int64_t n, int64_t m, unsigned seed, double *Q);
+
+/* ---------------------------------------------------------------- drivers ------------------ */
+/* a12: StandardLargest (eigensolver.hh:28-112) on the device.  Mutates the matrix when
+ * shift != 0 (like the reference).  eval_host[nev] (column order, unsorted, like the reference);
+ * evec_host: nev vectors of n doubles each, or NULL.  *iters: the k at exit. */
+int eig_standard_largest(eig_mat_t A, double shift, double tol, int maxiter, int nev, unsigned seed,
+                         double *eval_host, double *evec_host, int *iters, int verbose);
+
+/* Lanczos three-term recurrence on A (the loop ARPACK's dsaupd runs around multMv):
+ * `steps` steps from the start vector u0 (device, window layout; NULL = mt19937(seed) normal).
+ * Only three vectors are kept (no basis); alpha_host[steps], beta_host[steps+1] receive the
+ * tridiagonal T (beta[0] = ||u0||).  This is the benchmark's unit of work. */
+typedef struct eig_timing {
+  double total_ms;        /* wall time of the stepping loop (device events, first to last) */
+  double spmv_ms;         /* summed duration of the fused SpMV kernel launches */
+  double update_ms;       /* summed duration of the fused axpy/norm kernel launches */
+  double comm_ms;         /* summed duration of halo exchange + allreduce segments */
+  int64_t spmv_launches;  /* number of SpMV kernel launches timed */
+} eig_timing;
+enum eig_lanczos_flags {
+  EIG_LANCZOS_TIME_KERNELS = 1  /* record HIP events around every kernel (eig_timing fields) */
+};
+int eig_lanczos_run(eig_mat_t A, int steps, const double *u0, unsigned seed, int flags,
+                    double *alpha_host, double *beta_host, eig_timing *timing);
+
+/* The same recurrence as a persistent workspace (ARPACK's reverse-communication shape): create
+ * allocates the three window vectors and the device scalar arrays for up to max_steps steps and
+ * normalises the start vector; each eig_lanczos_step call advances `steps` more steps
+ * (synchronous at return); eig_lanczos_tridiag copies alpha[0..k), beta[0..k] of the k steps
+ * done so far.  No host synchronisation happens inside a step batch. */
+typedef struct eig_lanczos_s *eig_lanczos_t;
+int eig_lanczos_create(eig_mat_t A, int max_steps, const double *u0, unsigned seed, eig_lanczos_t *ws);
+int eig_lanczos_step(eig_lanczos_t ws, int steps, int flags, eig_timing *timing);
+int eig_lanczos_tridiag(eig_lanczos_t ws, int *k, double *alpha_host, double *beta_host);
+int eig_lanczos_destroy(eig_lanczos_t ws);
+
+/* Lanczos eigensolver: ncv-step Lanczos with full re-orthogonalisation (classical Gram-Schmidt
+ * twice, the DGKS scheme ARPACK uses) and Ritz extraction from T.  which: EIG_WHICH_LA (largest
+ * algebraic) or EIG_WHICH_SA (smallest algebraic).  eval_host[nev] sorted (LA: descending,
+ * SA: ascending); evec_host: nev owned-row vectors or NULL; resid_host[nev] (optional):
+ * ||A y - theta y|| of each returned pair (computed on the device). */
+enum eig_which { EIG_WHICH_LA = 0, EIG_WHICH_SA = 1 };
+int eig_lanczos_solve(eig_mat_t A, int nev, int ncv, int which, unsigned seed, double *eval_host,
+                      double *evec_host, double *resid_host);
+
+/* a14: the reference's analytic GS models (kernels_cpp.hh:98-116, :157-175). */
+double eig_flops_orthonormalize(int64_t n, int64_t m);
+double eig_bytes_orthonormalize_blocked(int64_t n, int64_t m, int b);
+
+/* ---------------------------------------------------------------- generators --------------- */
+/* Synthetic matrices of the reference harness (src/dune-eigensolver.cc:98-156) and SURVEY 8(d),
+ * produced on the host into caller buffers (sizes from the *_nnz functions).  kind:
+ *   0 2-D Dirichlet 5-pt N*N (setupLaplacian)      1 2-D Neumann (.cc:105-121)
+ *   2 2-D partition-of-unity B (.cc:124-143)       3 2-D identity pattern (.cc:145-156)
+ *   4 3-D Poisson 7-pt N^3                          5 3-D Q1 "elasticity" L_Q1 (x) C, 3x3 blocks */
+int64_t eig_gen_nnzb(int kind, int N);
+int eig_gen_matrix(int kind, int N, int overlap, int64_t *rowptr, int32_t *col, double *vals);
+/* Rows [row_begin, row_begin + nrows) of the same matrix (for eig_mat_create_bcsr_dist). */
+int64_t eig_gen_nnzb_rows(int kind, int N, int64_t row_begin, int64_t nrows);
+int eig_gen_matrix_rows(int kind, int N, int64_t row_begin, int64_t nrows, int64_t *rowptr,
+                        int32_t *col, double *vals);
+
+/* ---------------------------------------------------------------- partition planning ------ */
+/* Host-only helpers (no device needed) used by eig_mat_create_bcsr_dist; exported so the
+ * partition / halo logic can be exercised and reused by other front ends.
+ * eig_plan_window: from a rank's rows (global block columns) compute
+ *   out[0] = window begin (global BLOCK column of window index 0, padded so that the owned rows
+ *            start at a multiple of 8 scalar entries), out[1] = window length (scalar, multiple
+ *            of 8), out[2] = own_offset (scalar), out[3] = cmin, out[4] = cmax (referenced block
+ *            columns [cmin, cmax) including the owned rows).
+ * eig_plan_halo: given every rank's (row_begin, nb_local, cmin, cmax) in ranks[4*nranks], list
+ *   what rank `me` receives (recv[3*k] = peer, offset in the window (scalar), count) and sends
+ *   (send[3*k] = peer, offset in the window of the owned rows, count); *nrecv / *nsend entries. */
+int eig_plan_window(int64_t row_begin, int64_t nb_local, int bc, const int64_t *rowptr_host,
+                    const int32_t *col_host, int64_t out[5]);
+int eig_plan_halo(int nranks, int me, const int64_t *ranks, int bc, int64_t win_begin_blk,
+                  int64_t *recv, int *nrecv, int64_t *send, int *nsend);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* EIGMI_H */

@@ -1,0 +1,225 @@
+"""ctypes wrapper of oracle/liboracle.so -- the CPU restatement of the reference hot path.
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg, never by the product package.  See oracle/oracle.cc for the per-function
+reference citations and DESIGN.md "Oracle" for how the restatement is pinned.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = os.path.join(_HERE, "liboracle.so")
+
+_i64p = np.ctypeslib.ndpointer(np.int64, flags="C_CONTIGUOUS")
+_i32p = np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")
+_f64p = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
+_i64 = ctypes.c_int64
+_int = ctypes.c_int
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+
+
+def _load():
+    if not os.path.exists(_LIB) or os.path.getmtime(_LIB) < os.path.getmtime(os.path.join(_HERE, "oracle.cc")):
+        build()
+    lib = ctypes.CDLL(_LIB)
+    sig = {
+        "orc_laplace2d_nnz": (_i64, [_int]),
+        "orc_laplace2d": (None, [_int, _i64p, _i32p, _f64p]),
+        "orc_laplace2d_neumann": (None, [_int, _i64p, _i32p, _f64p]),
+        "orc_laplace2d_pu": (None, [_int, _int, _i64p, _i32p, _f64p]),
+        "orc_identity2d": (None, [_int, _i64p, _i32p, _f64p]),
+        "orc_poisson3d_nnz": (_i64, [_int]),
+        "orc_poisson3d": (None, [_int, _i64p, _i32p, _f64p]),
+        "orc_q1elast_nnzb": (_i64, [_int]),
+        "orc_q1elast": (None, [_int, _i64p, _i32p, _f64p]),
+        "orc_eig_laplace2d": (None, [_int, _f64p]),
+        "orc_csr_mv": (None, [_i64, _i64p, _i32p, _f64p, _f64p, _f64p]),
+        "orc_bcsr_mv": (None, [_i64, _int, _int, _i64p, _i32p, _f64p, _f64p, _f64p]),
+        "orc_spmm_mv8": (None, [_i64, _i64, _i64p, _i32p, _f64p, _f64p, _f64p]),
+        "orc_dot_diag_mv8": (None, [_i64, _i64, _f64p, _f64p, _f64p]),
+        "orc_gram_mv8": (None, [_i64, _i64, _f64p, _f64p, _f64p]),
+        "orc_orthonormalize_naive": (None, [_i64, _i64, _f64p]),
+        "orc_orthonormalize_mv8": (None, [_i64, _i64, _f64p]),
+        "orc_orthonormalize_cholqr_mv8": (None, [_i64, _i64, _f64p]),
+        "orc_b_orthonormalize_mv8": (ctypes.c_double, [_i64, _i64, _i64p, _i32p, _f64p, _f64p]),
+        "orc_flops_orthonormalize": (ctypes.c_double, [_int, _int]),
+        "orc_bytes_orthonormalize_naive": (ctypes.c_double, [_int, _int]),
+        "orc_bytes_orthonormalize_blocked": (ctypes.c_double, [_int, _int, _int]),
+        "orc_random_mv8": (None, [_i64, _i64, ctypes.c_uint, _f64p]),
+        "orc_random_vec": (None, [_i64, ctypes.c_uint, _f64p]),
+        "orc_shift_diag": (None, [_i64, _i64p, _i32p, _f64p, ctypes.c_double]),
+        "orc_standard_largest": (_int, [_i64, _i64p, _i32p, _f64p, ctypes.c_double, ctypes.c_double,
+                                        _int, _int, ctypes.c_uint, _f64p, _f64p]),
+        "orc_lanczos": (None, [_i64, _i64p, _i32p, _f64p, _int, _f64p, _f64p, _f64p]),
+        "orc_lanczos_rotating": (None, [_i64, _i64p, _i32p, _f64p, _int, _f64p, _f64p, _f64p, _f64p, _f64p]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+class CSR:
+    """Host CSR (or BCSR when br/bc > 1): int64 rowptr, int32 col, float64 val (row-major blocks)."""
+
+    def __init__(self, nrows, rowptr, col, val, br=1, bc=1):
+        self.nrows, self.rowptr, self.col, self.val, self.br, self.bc = nrows, rowptr, col, val, br, bc
+
+    @property
+    def n(self):
+        return self.nrows * self.br
+
+    @property
+    def nnz(self):
+        return int(self.rowptr[-1])
+
+    def to_scipy(self):
+        import scipy.sparse as sp
+        if self.br == 1 and self.bc == 1:
+            return sp.csr_matrix((self.val, self.col, self.rowptr), shape=(self.nrows, self.nrows))
+        data = self.val.reshape(-1, self.br, self.bc)
+        return sp.bsr_matrix((data, self.col, self.rowptr), shape=(self.nrows * self.br, self.nrows * self.bc))
+
+
+def _alloc(nrows, nnz, blk=1):
+    return np.zeros(nrows + 1, np.int64), np.zeros(nnz, np.int32), np.zeros(nnz * blk, np.float64)
+
+
+def laplace2d(N, kind="dirichlet", overlap=3):
+    nnz = lib.orc_laplace2d_nnz(N)
+    rp, c, v = _alloc(N * N, nnz)
+    if kind == "dirichlet":
+        lib.orc_laplace2d(N, rp, c, v)
+    elif kind == "neumann":
+        lib.orc_laplace2d_neumann(N, rp, c, v)
+    elif kind == "pu":
+        lib.orc_laplace2d_pu(N, overlap, rp, c, v)
+    elif kind == "identity":
+        lib.orc_identity2d(N, rp, c, v)
+    else:
+        raise ValueError(kind)
+    return CSR(N * N, rp, c, v)
+
+
+def poisson3d(N):
+    nnz = lib.orc_poisson3d_nnz(N)
+    rp, c, v = _alloc(N ** 3, nnz)
+    lib.orc_poisson3d(N, rp, c, v)
+    return CSR(N ** 3, rp, c, v)
+
+
+def q1elast(N):
+    nnzb = lib.orc_q1elast_nnzb(N)
+    rp, c, v = _alloc(N ** 3, nnzb, 9)
+    lib.orc_q1elast(N, rp, c, v)
+    return CSR(N ** 3, rp, c, v, 3, 3)
+
+
+def eig_laplace2d(N):
+    ev = np.zeros(N * N)
+    lib.orc_eig_laplace2d(N, ev)
+    return ev
+
+
+def csr_mv(A, x):
+    y = np.zeros(A.nrows * A.br)
+    if A.br == 1 and A.bc == 1:
+        lib.orc_csr_mv(A.nrows, A.rowptr, A.col, A.val, np.ascontiguousarray(x, np.float64), y)
+    else:
+        lib.orc_bcsr_mv(A.nrows, A.br, A.bc, A.rowptr, A.col, A.val, np.ascontiguousarray(x, np.float64), y)
+    return y
+
+
+def spmm_mv8(A, Q, m):
+    out = np.zeros_like(Q)
+    lib.orc_spmm_mv8(A.nrows, m, A.rowptr, A.col, A.val, Q, out)
+    return out
+
+
+def dot_diag_mv8(Q1, Q2, n, m):
+    dp = np.zeros(m)
+    lib.orc_dot_diag_mv8(n, m, Q1, Q2, dp)
+    return dp
+
+
+def gram_mv8(Q1, Q2, n, m):
+    G = np.zeros((m, m))
+    lib.orc_gram_mv8(n, m, Q1, Q2, G.reshape(-1))
+    return G
+
+
+def orthonormalize_mv8(Q, n, m, variant="mgs"):
+    Q = Q.copy()
+    if variant == "mgs":
+        lib.orc_orthonormalize_mv8(n, m, Q)
+    elif variant == "cholqr":
+        lib.orc_orthonormalize_cholqr_mv8(n, m, Q)
+    else:
+        raise ValueError(variant)
+    return Q
+
+
+def orthonormalize_naive(Q, n, m):
+    Q = Q.copy()
+    lib.orc_orthonormalize_naive(n, m, Q)
+    return Q
+
+
+def b_orthonormalize_mv8(B, Q, n, m):
+    Q = Q.copy()
+    norm = lib.orc_b_orthonormalize_mv8(n, m, B.rowptr, B.col, B.val, Q)
+    return Q, norm
+
+
+def random_mv8(n, m, seed=123):
+    Q = np.zeros(n * m)
+    lib.orc_random_mv8(n, m, seed, Q)
+    return Q
+
+
+def random_vec(n, seed=123):
+    x = np.zeros(n)
+    lib.orc_random_vec(n, seed, x)
+    return x
+
+
+def standard_largest(A, shift, tol, maxiter, nev, seed=123):
+    val = A.val.copy()
+    ev = np.zeros(nev)
+    evec = np.zeros(nev * A.n)
+    it = lib.orc_standard_largest(A.n, A.rowptr, A.col, val, shift, tol, maxiter, nev, seed, ev, evec)
+    return ev, evec.reshape(nev, A.n), it
+
+
+def lanczos(A, u0, k):
+    U = np.zeros((k + 1) * A.n)
+    U[: A.n] = u0
+    alpha = np.zeros(k)
+    beta = np.zeros(k + 1)
+    lib.orc_lanczos(A.n, A.rowptr, A.col, A.val, k, U, alpha, beta)
+    return U.reshape(k + 1, A.n), alpha, beta
+
+
+def mv_index(n, i, j):
+    """MultiVector<double,8> flat index (multivector.hh:130-139)."""
+    return ((j // 8) * n + i) * 8 + (j % 8)
+
+
+def mv_to_cols(Q, n, m):
+    """Block-column-major MultiVector<double,8> -> (n, m) dense array."""
+    return Q.reshape(m // 8, n, 8).transpose(1, 0, 2).reshape(n, m)
+
+
+def cols_to_mv(X):
+    n, m = X.shape
+    return np.ascontiguousarray(X.reshape(n, m // 8, 8).transpose(1, 0, 2).reshape(-1))

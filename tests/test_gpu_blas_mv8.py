@@ -1,0 +1,126 @@
+"""GPU parity: BlockVector ops and the MultiVector<double,8> kernels (SpMM, dots, MFMA Gram,
+block Gram-Schmidt, B-Gram-Schmidt) vs the oracle.  Element-wise kernels that keep the
+reference's operation order are compared BITWISE; reductions (different summation order) within
+the tolerance written at each assert."""
+import numpy as np
+import pytest
+
+import eigmi
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("n", [0, 1, 7, 1000, 65537, 1 << 20])
+def test_blas1(ctx, n):
+    rng = np.random.default_rng(n)
+    x, y = rng.standard_normal(n), rng.standard_normal(n)
+    dx, dy, out = ctx.array(x), ctx.array(y), ctx.zeros(2)
+    eigmi.dot(ctx, n, dx, dy, out)
+    d = out.get(1)[0]
+    # tolerance: |sum order error| <= n * eps * sum |x_i y_i|
+    assert abs(d - np.dot(x, y)) <= 4 * max(n, 1) * 2.3e-16 * np.abs(x * y).sum() + 1e-300
+    eigmi.nrm2(ctx, n, dx, out)
+    assert abs(out.get(1)[0] - np.sqrt(np.dot(x, x))) <= 1e-13 * max(1.0, np.sqrt(np.dot(x, x)))
+    eigmi.axpy(ctx, n, -0.75, dx, dy)
+    assert np.array_equal(dy.get(), y + (-0.75) * x)  # y += a x, one rounding per op: bitwise
+    eigmi.scal(ctx, n, 3.0, dx)
+    assert np.array_equal(dx.get(), x * 3.0)
+    dz = ctx.zeros(n)
+    eigmi.copy(ctx, n, dx, dz)
+    ctx.sync()
+    assert np.array_equal(dz.get(), x * 3.0)
+
+
+def test_random_mv8_bitwise(ctx):
+    n, m = 1000, 16
+    Q = ctx.zeros(n * m)
+    eigmi.random_mv8(ctx, n, m, 123, Q)
+    assert np.array_equal(Q.get(), oracle.random_mv8(n, m, 123))
+
+
+@pytest.mark.parametrize("m", [8, 16, 40])
+def test_spmm_bitwise(ctx, m):
+    A = oracle.poisson3d(12)
+    M = eigmi.Matrix.from_bcsr(ctx, A.rowptr, A.col, A.val)
+    Qh = oracle.random_mv8(A.n, m, 11)
+    Q, Y = ctx.array(Qh), ctx.zeros(A.n * m)
+    eigmi.spmm_mv8(M, m, Q, Y)
+    assert np.array_equal(Y.get(), oracle.spmm_mv8(A, Qh, m))
+
+
+def test_spmm_rejects_blocks_and_bad_m(ctx):
+    A = oracle.q1elast(3)
+    M = eigmi.Matrix.from_bcsr(ctx, A.rowptr, A.col, A.val, 3, 3)
+    Q = ctx.zeros(A.n * 8)
+    with pytest.raises(eigmi.EigShapeError):
+        eigmi.spmm_mv8(M, 8, Q, Q)
+    A1 = oracle.laplace2d(8)
+    M1 = eigmi.Matrix.from_bcsr(ctx, A1.rowptr, A1.col, A1.val)
+    with pytest.raises(eigmi.EigShapeError):
+        eigmi.spmm_mv8(M1, 12, Q, Q)  # "number of cols must be a multiple of block size"
+
+
+@pytest.mark.parametrize("n,m", [(4096, 8), (4096, 32), (12345, 16)])
+def test_dot_diag(ctx, n, m):
+    Q1h, Q2h = oracle.random_mv8(n, m, 1), oracle.random_mv8(n, m, 2)
+    dp = ctx.zeros(m)
+    eigmi.dot_diag_mv8(ctx, n, m, ctx.array(Q1h), ctx.array(Q2h), dp)
+    ref = oracle.dot_diag_mv8(Q1h, Q2h, n, m)
+    X1, X2 = oracle.mv_to_cols(Q1h, n, m), oracle.mv_to_cols(Q2h, n, m)
+    bound = 4 * n * 2.3e-16 * np.einsum("ij,ij->j", np.abs(X1), np.abs(X2))
+    assert np.all(np.abs(dp.get() - ref) <= bound)
+
+
+@pytest.mark.parametrize("n,m1,m2", [(4096, 8, 8), (4096, 16, 16), (3001, 8, 24), (10000, 32, 32), (777, 48, 8)])
+def test_gram_mfma(ctx, n, m1, m2):
+    Q1h, Q2h = oracle.random_mv8(n, m1, 3), oracle.random_mv8(n, m2, 4)
+    G = ctx.zeros(m1 * m2)
+    eigmi.gram_mv8(ctx, n, m1, m2, ctx.array(Q1h), ctx.array(Q2h), G)
+    X1, X2 = oracle.mv_to_cols(Q1h, n, m1), oracle.mv_to_cols(Q2h, n, m2)
+    ref = X1.T @ X2
+    if m1 == m2:
+        assert np.allclose(oracle.gram_mv8(Q1h, Q2h, n, m1), ref, atol=1e-11)
+    bound = 4 * n * 2.3e-16 * (np.abs(X1).T @ np.abs(X2))
+    assert np.all(np.abs(G.get().reshape(m1, m2) - ref) <= bound)
+
+
+@pytest.mark.parametrize("variant,name", [(eigmi.ORTHO_MGS, "mgs"), (eigmi.ORTHO_CHOLQR, "cholqr")])
+@pytest.mark.parametrize("n,m", [(4096, 8), (4096, 32), (5000, 16)])
+def test_orthonormalize_blocked(ctx, variant, name, n, m):
+    Qh = oracle.random_mv8(n, m, 21)
+    Q = ctx.array(Qh)
+    eigmi.orthonormalize_mv8(ctx, n, m, Q, variant)
+    got = oracle.mv_to_cols(Q.get(), n, m)
+    ref = oracle.mv_to_cols(oracle.orthonormalize_mv8(Qh, n, m, name), n, m)
+    assert np.abs(got.T @ got - np.eye(m)).max() < 1e-13
+    # same thin QR as the reference algorithm: elementwise within 1e-12 (random, well conditioned)
+    assert np.abs(got - ref).max() < 1e-12
+
+
+def test_orthonormalize_naive(ctx):
+    n, m = 3000, 12
+    X = np.random.default_rng(8).standard_normal((n, m))
+    cm = np.ascontiguousarray(X.T.reshape(-1))
+    Q = ctx.array(cm)
+    eigmi.orthonormalize_naive(ctx, n, m, Q)
+    got = Q.get().reshape(m, n).T
+    ref = oracle.orthonormalize_naive(cm, n, m).reshape(m, n).T
+    assert np.abs(got - ref).max() < 1e-12
+
+
+@pytest.mark.parametrize("kind", ["laplace", "identity"])
+def test_b_orthonormalize(ctx, kind):
+    N, m = 48, 24
+    B = oracle.laplace2d(N) if kind == "laplace" else oracle.laplace2d(N, "identity")
+    n = B.n
+    Qh = oracle.random_mv8(n, m, 77)
+    MB = eigmi.Matrix.from_bcsr(ctx, B.rowptr, B.col, B.val)
+    Q, norm = ctx.array(Qh), ctx.zeros(1)
+    eigmi.b_orthonormalize_mv8(MB, m, Q, norm)
+    refQ, refnorm = oracle.b_orthonormalize_mv8(B, Qh, n, m)
+    got = oracle.mv_to_cols(Q.get(), n, m)
+    Bs = B.to_scipy()
+    assert np.abs(got.T @ (Bs @ got) - np.eye(m)).max() < 1e-10
+    assert np.abs(got - oracle.mv_to_cols(refQ, n, m)).max() < 1e-10
+    assert abs(norm.get(1)[0] - refnorm) <= 1e-12 * abs(refnorm)

@@ -1,0 +1,126 @@
+"""CPU tests: pin the oracle (oracle/oracle.cc) against the reference's known answers and the
+golden fixtures, before it is trusted as the checker of the HIP path."""
+import json
+import os
+
+import numpy as np
+import pytest
+import scipy.linalg as sla
+
+import oracle
+
+
+def test_generators_match_scipy_patterns():
+    A = oracle.laplace2d(64)
+    assert A.nnz == 20224  # SURVEY 8(a) C1 and reference_run.json
+    S = A.to_scipy().toarray()
+    assert np.array_equal(S, S.T)
+    assert np.all(np.diag(S) == 4.0)
+    P = oracle.poisson3d(8)
+    assert P.nnz == 7 * 8 ** 3 - 6 * 8 ** 2
+    for r in range(P.nrows):  # ISTL rows: strictly ascending columns
+        c = P.col[P.rowptr[r]:P.rowptr[r + 1]]
+        assert np.all(np.diff(c) > 0)
+
+
+def test_c1_analytic_known_answer(golden_dir):
+    """src/dune-eigensolver.cc:437-446 spectrum == ARPACK (scipy) == dense eigh."""
+    g = np.load(os.path.join(golden_dir, "c1_arpack.npz"))
+    ana = oracle.eig_laplace2d(64)
+    assert np.allclose(g["analytic"], ana, rtol=0, atol=1e-15)
+    assert np.allclose(g["la_w"], ana[::-1][:4], rtol=0, atol=1e-12)
+    assert np.allclose(g["sa_w"], ana[:4], rtol=0, atol=1e-12)
+    w = sla.eigvalsh(oracle.laplace2d(16).to_scipy().toarray())
+    assert np.allclose(w, oracle.eig_laplace2d(16), atol=1e-12)
+
+
+def test_standard_largest_matches_recorded_reference_run(golden_dir):
+    """the compiled reference stopped after 50 iterations with Ritz_0 = 7.9037."""
+    rec = json.load(open(os.path.join(golden_dir, "reference_run.json")))
+    r = rec["StandardLargest_laplace2d_N64_nev4_seed123_tol2e-3"]
+    ev, evec, it = oracle.standard_largest(oracle.laplace2d(64), 0.0, 2e-3, 4000, 4, 123)
+    assert it == r["iterations"]
+    assert round(ev[0], 4) == r["ritz0_rounded_4"]
+    assert evec.shape == (4, 4096)
+
+
+@pytest.mark.parametrize("m", [8, 16, 32])
+@pytest.mark.parametrize("variant", ["mgs", "cholqr"])
+def test_orthonormalize_blocked(m, variant):
+    n = 1000
+    Q = oracle.random_mv8(n, m, 7)
+    Qo = oracle.orthonormalize_mv8(Q, n, m, variant)
+    X = oracle.mv_to_cols(Qo, n, m)
+    assert np.abs(X.T @ X - np.eye(m)).max() < 1e-13
+    # same thin QR as numpy (unique with positive diagonal R)
+    q, r = np.linalg.qr(oracle.mv_to_cols(Q, n, m))
+    q = q * np.sign(np.diag(r))
+    assert np.abs(q - X).max() < 1e-12
+
+
+def test_orthonormalize_naive_matches_blocked_span():
+    n, m = 500, 8
+    Q = oracle.random_mv8(n, m, 3)
+    X = oracle.mv_to_cols(Q, n, m)
+    cm = np.ascontiguousarray(X.T.reshape(-1))  # MultiVector<double,1>: column after column
+    on = oracle.orthonormalize_naive(cm, n, m).reshape(m, n).T
+    ob = oracle.mv_to_cols(oracle.orthonormalize_mv8(Q, n, m), n, m)
+    assert np.abs(on - ob).max() < 1e-12
+
+
+def test_b_orthonormalize_identity_B_equals_cholqr():
+    n, m = 64 * 64, 16
+    B = oracle.laplace2d(64, "identity")
+    Q = oracle.random_mv8(n, m, 5)
+    Qb, norm = oracle.b_orthonormalize_mv8(B, Q, n, m)
+    X = oracle.mv_to_cols(Qb, n, m)
+    assert np.abs(X.T @ X - np.eye(m)).max() < 1e-13
+    assert norm > 0
+
+
+def test_b_orthonormalize_spd_B():
+    n, m = 32 * 32, 16
+    B = oracle.laplace2d(32)
+    Q = oracle.random_mv8(n, m, 9)
+    Qb, norm = oracle.b_orthonormalize_mv8(B, Q, n, m)
+    X = oracle.mv_to_cols(Qb, n, m)
+    Bs = B.to_scipy()
+    assert np.abs(X.T @ (Bs @ X) - np.eye(m)).max() < 1e-11
+
+
+def test_spmm_and_dots_against_numpy():
+    A = oracle.poisson3d(10)
+    n, m = A.n, 16
+    Q = oracle.random_mv8(n, m, 1)
+    Y = oracle.spmm_mv8(A, Q, m)
+    X = oracle.mv_to_cols(Q, n, m)
+    assert np.abs(oracle.mv_to_cols(Y, n, m) - A.to_scipy() @ X).max() < 1e-12
+    dp = oracle.dot_diag_mv8(Q, Y, n, m)
+    assert np.allclose(dp, np.einsum("ij,ij->j", X, A.to_scipy() @ X), rtol=1e-12)
+    G = oracle.gram_mv8(Q, Y, n, m)
+    assert np.allclose(G, X.T @ (A.to_scipy() @ X), rtol=1e-12, atol=1e-9)
+
+
+def test_bcsr_mv_matches_scipy_bsr_and_kron_known_answer(golden_dir):
+    g = np.load(os.path.join(golden_dir, "q1elast_6_bsr.npz"))
+    A = oracle.q1elast(6)
+    y = oracle.csr_mv(A, g["x"])
+    assert np.abs(y - g["y_bsr"]).max() < 1e-13
+    assert np.allclose(np.sort(g["eig_dense"]), g["analytic"], atol=1e-12)
+
+
+def test_lanczos_oracle_ritz_values_converge(golden_dir):
+    """The restated three-term recurrence reproduces ARPACK's extremal eigenvalues (C1)."""
+    A = oracle.laplace2d(64)
+    u0 = oracle.random_vec(A.n, 123)
+    U, alpha, beta = oracle.lanczos(A, u0, 300)
+    T = np.diag(alpha) + np.diag(beta[1:-1], 1) + np.diag(beta[1:-1], -1)
+    w = np.linalg.eigvalsh(T)
+    g = np.load(os.path.join(golden_dir, "c1_arpack.npz"))
+    assert abs(w[-1] - g["la_w"][0]) < 1e-10
+    assert abs(w[0] - g["sa_w"][0]) < 1e-6
+
+
+def test_flop_byte_models():
+    assert oracle.lib.orc_flops_orthonormalize(10, 2) == 2 * 10 + 10 + 2 * 10 + 10 + 4 * 10
+    assert oracle.lib.orc_bytes_orthonormalize_blocked(100, 16, 8) > 0
