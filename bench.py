@@ -48,13 +48,33 @@ def cpu_baseline(N, rp, c, v, steps, gpu_alpha):
     return steps / dt, dt, rel
 
 
+def committed_traffic(kernel, N, world):
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
+    (profiles/<tag>_pmc_summary.json, FETCH_SIZE x2 + WRITE_SIZE, KiB -> B; tools/profile_round.sh)
+    taken on the same configuration; None when no matching profile exists."""
+    import glob
+    best = None
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json"))):
+        try:
+            d = json.load(open(p))
+            line = d.get("bench_line_under_trace", {})
+            if line.get("config", {}).get("N") != N or line.get("n_gpus") != world:
+                continue
+            k = d["kernels"].get("eigmi::" + kernel)
+            if k:
+                best = (k["hbm_bytes"], os.path.relpath(p, ROOT))
+        except (OSError, ValueError, KeyError):
+            continue
+    return best
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--N", type=int, default=256, help="grid points per axis (n = N^3)")
-    ap.add_argument("--cpu-steps", type=int, default=16, help="Lanczos steps of the CPU baseline sample")
+    ap.add_argument("--cpu-steps", type=int, default=160, help="Lanczos steps of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-events", action="store_true", help="skip per-kernel HIP events")
     args = ap.parse_args()
@@ -116,8 +136,10 @@ def main():
     roofline = None
     if k1_ms:
         ach = k1_bytes / (k1_ms * 1e-3) / 1e9
+        tr = committed_traffic("k_lanczos_spmv_b1", N, world)
         roofline = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": tr[0] if tr else None,
+                    "traffic_source": tr[1] if tr else None,
                     "kernel": "k_lanczos_spmv_b1", "bytes_per_launch": k1_bytes,
                     "avg_launch_us": round(k1_ms * 1e3, 2)}
     step_bytes = eigmi.bytes_lanczos_step(n, nnz_total)

@@ -261,9 +261,9 @@ class Matrix:
         return cls(ctx, h)
 
     def close(self):
-        if self.h:
+        if self.h and self.ctx.h:  # a destroyed context already released the device
             lib.eig_mat_destroy(self.h)
-            self.h = None
+        self.h = None
 
     def __del__(self):
         try:
@@ -391,9 +391,9 @@ class LanczosWorkspace:
         return alpha[:k.value], beta
 
     def close(self):
-        if self.h:
+        if self.h and self.A.h and self.A.ctx.h:
             lib.eig_lanczos_destroy(self.h)
-            self.h = None
+        self.h = None
 
     def __del__(self):
         try:

@@ -1,0 +1,208 @@
+// facade_test.cc -- the drop-in demonstration: reference-style code (an ISTL-concept BCRS matrix,
+// a MultiVector<double,8>-compatible container, the reference's kernel names and the ARPACK++
+// operator signature) driven through include/eigmi.hh.
+//
+// The matrix / multivector types below are this test's own minimal stand-ins for the two
+// concepts the reference's templates require (kernels_cpp.hh:629-655, multivector.hh:17-146);
+// they are the caller's types, not part of the library.
+//
+//   facade_test            full run on cuda:0 (GPU tests)
+//   facade_test --no-device  expects the library to report "no device" (CPU build check)
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <random>
+#include <vector>
+
+#include "eigmi.hh"
+
+template <int R, int C>
+struct Block {  // FieldMatrix<double,R,C>-like: b[i][j]
+  static constexpr int rows = R, cols = C;
+  double a[R][C];
+  const double *operator[](int i) const { return a[i]; }
+  double *operator[](int i) { return a[i]; }
+  operator double() const { return a[0][0]; }
+};
+
+template <int R, int C>
+struct TestBCRS {  // BCRSMatrix-like iteration concept
+  using block_type = Block<R, C>;
+  std::vector<std::vector<std::pair<std::size_t, block_type>>> rows;
+  std::size_t ncols = 0;
+  struct ColIter {
+    const std::pair<std::size_t, block_type> *p;
+    std::size_t index() const { return p->first; }
+    const block_type &operator*() const { return p->second; }
+    ColIter &operator++() { ++p; return *this; }
+    bool operator!=(const ColIter &o) const { return p != o.p; }
+  };
+  struct Row {
+    const std::vector<std::pair<std::size_t, block_type>> *r;
+    ColIter begin() const { return {r->data()}; }
+    ColIter end() const { return {r->data() + r->size()}; }
+  };
+  struct RowIter {
+    const TestBCRS *m;
+    std::size_t i;
+    mutable Row row;
+    std::size_t index() const { return i; }
+    const Row *operator->() const { row.r = &m->rows[i]; return &row; }
+    RowIter &operator++() { ++i; return *this; }
+    bool operator!=(const RowIter &o) const { return i != o.i; }
+  };
+  RowIter begin() const { return {this, 0, {}}; }
+  RowIter end() const { return {this, rows.size(), {}}; }
+  std::size_t N() const { return rows.size(); }
+  std::size_t M() const { return ncols; }
+};
+
+struct MV8 {  // MultiVector<double,8>-like: block-column-major ((j/8)*n+i)*8 + j%8
+  static const std::size_t blocksize = 8;
+  std::vector<double> p;
+  std::size_t n, m;
+  MV8(std::size_t n_, std::size_t m_) : p(n_ * m_), n(n_), m(m_) {}
+  double &operator()(std::size_t i, std::size_t j) { return p[((j / 8) * n + i) * 8 + j % 8]; }
+  const double &operator()(std::size_t i, std::size_t j) const { return p[((j / 8) * n + i) * 8 + j % 8]; }
+  std::size_t rows() const { return n; }
+  std::size_t cols() const { return m; }
+};
+
+static TestBCRS<1, 1> laplace2d(int N)
+{
+  TestBCRS<1, 1> A;
+  A.rows.resize((std::size_t)N * N);
+  A.ncols = (std::size_t)N * N;
+  for (std::size_t k = 0; k < A.rows.size(); ++k)
+  {
+    int x = (int)(k % N), y = (int)(k / N);
+    auto put = [&](std::size_t c, double v) { Block<1, 1> b; b.a[0][0] = v; A.rows[k].push_back({c, b}); };
+    if (y > 0) put(k - N, -1);
+    if (x > 0) put(k - 1, -1);
+    put(k, 4);
+    if (x < N - 1) put(k + 1, -1);
+    if (y < N - 1) put(k + N, -1);
+  }
+  return A;
+}
+
+static int failures = 0;
+#define EXPECT(c)                                                        \
+  do {                                                                   \
+    if (!(c)) { std::printf("FAIL %s:%d %s\n", __FILE__, __LINE__, #c); ++failures; } \
+  } while (0)
+
+int main(int argc, char **argv)
+{
+  if (argc > 1 && std::strcmp(argv[1], "--no-device") == 0)
+  {
+    try
+    {
+      eigmi::Context ctx(0);
+      std::printf("unexpected: a device is visible\n");
+      return 2;
+    }
+    catch (const std::runtime_error &e)
+    {
+      std::printf("no device (expected): %s\n", e.what());
+      return 0;
+    }
+  }
+  eigmi::Context ctx(0);
+  std::mt19937 g(5);
+  std::normal_distribution<double> nd(0.0, 1.0);
+
+  // 1) BCRSMatrix::mv, scalar blocks: bitwise vs the ISTL row loop
+  auto A = laplace2d(64);
+  auto dA = eigmi::Matrix::upload(ctx, A);
+  std::vector<double> x(A.N()), y(A.N()), ref(A.N());
+  for (auto &v : x) v = nd(g);
+  dA.mv_host(x.data(), y.data());
+  for (auto r = A.begin(); r != A.end(); ++r)
+  {
+    double s = 0.0;
+    for (auto c = r->begin(); c != r->end(); ++c) s += (double)(*c) * x[c.index()];
+    ref[r.index()] = s;
+  }
+  EXPECT(std::memcmp(y.data(), ref.data(), y.size() * 8) == 0);
+
+  // 2) 3x3 blocks
+  TestBCRS<3, 3> B;
+  B.rows.resize(100);
+  B.ncols = 100;
+  for (std::size_t k = 0; k < 100; ++k)
+    for (std::size_t c : {k >= 7 ? k - 7 : k, k, (k + 11) % 100})
+    {
+      if (!B.rows[k].empty() && B.rows[k].back().first >= c) continue;
+      Block<3, 3> b;
+      for (auto &row : b.a)
+        for (auto &v : row) v = nd(g);
+      B.rows[k].push_back({c, b});
+    }
+  auto dB = eigmi::Matrix::upload(ctx, B);
+  std::vector<double> xb(300), yb(300), rb(300, 0.0);
+  for (auto &v : xb) v = nd(g);
+  dB.mv_host(xb.data(), yb.data());
+  for (auto r = B.begin(); r != B.end(); ++r)
+    for (auto c = r->begin(); c != r->end(); ++c)
+      for (int i = 0; i < 3; ++i)
+      {
+        double s = rb[r.index() * 3 + i];
+        for (int j = 0; j < 3; ++j) s += (*c)[i][j] * xb[c.index() * 3 + j];
+        rb[r.index() * 3 + i] = s;
+      }
+  EXPECT(std::memcmp(yb.data(), rb.data(), 300 * 8) == 0);
+
+  // 3) ARPACK++ operator signature
+  eigmi::ArpackOperator op(dA);
+  EXPECT(op.nrows() == 4096 && op.ncols() == 4096);
+  std::vector<double> w(4096);
+  op.multMvB(x.data(), w.data());
+  EXPECT(std::memcmp(w.data(), ref.data(), 4096 * 8) == 0);
+
+  // 4) MultiVector kernels under the reference names
+  const std::size_t n = A.N(), m = 16;
+  MV8 Q(n, m), Y(n, m);
+  for (auto &v : Q.p) v = nd(g);
+  eigmi::matmul_sparse_tallskinny_blocked(Y, dA, Q);
+  bool ok = true;
+  for (std::size_t j = 0; j < m; ++j)
+    for (auto r = A.begin(); r != A.end(); ++r)
+    {
+      double s = 0.0;
+      for (auto c = r->begin(); c != r->end(); ++c) s += (double)(*c) * Q(c.index(), j);
+      ok = ok && (s == Y(r.index(), j));
+    }
+  EXPECT(ok);
+  eigmi::orthonormalize_blocked(ctx, Q);
+  std::vector<std::vector<double>> G;
+  eigmi::dot_products_all_blocked(ctx, G, Q, Q);
+  double off = 0.0;
+  for (std::size_t i = 0; i < m; ++i)
+    for (std::size_t j = 0; j < m; ++j) off = std::max(off, std::fabs(G[i][j] - (i == j ? 1.0 : 0.0)));
+  EXPECT(off < 1e-13);
+  std::vector<double> dp;
+  eigmi::dot_products_diagonal_blocked(ctx, dp, Q, Q);
+  EXPECT(dp.size() == m && std::fabs(dp[3] - 1.0) < 1e-13);
+  bool threw = false;
+  try
+  {
+    MV8 bad1(n, 8), bad2(n + 1, 8);
+    eigmi::dot_products_diagonal_blocked(ctx, dp, bad1, bad2);
+  }
+  catch (const std::invalid_argument &)
+  {
+    threw = true;
+  }
+  EXPECT(threw);
+
+  // 5) StandardLargest: the reference run: 50 iterations, Ritz_0 7.9037
+  std::vector<double> eval(4);
+  std::vector<std::vector<double>> evec(4, std::vector<double>(n));
+  int it = eigmi::StandardLargest(dA, 0.0, 2e-3, 4000, 4, eval, evec, 0, 123);
+  EXPECT(it == 50);
+  EXPECT(std::fabs(eval[0] - 7.9037) < 5e-5);
+
+  std::printf(failures ? "FAILED %d\n" : "ALL OK\n", failures);
+  return failures ? 1 : 0;
+}
