@@ -86,7 +86,27 @@ void *ctx_buffer(eig_ctx_t ctx, int slot, size_t bytes)
 
 void allreduce_sum(eig_ctx_t ctx, double *buf, i64 count, hipStream_t s)
 {
-  if (!ctx->comm || ctx->nranks == 1) return;
+  if (!ctx->distributed() || count <= 0) return;
+  if (ctx->loop)
+  {
+    // loopback: every virtual rank publishes its values, then sums all ranks in rank order
+    LoopHub &h = *ctx->loop;
+    std::vector<double> mine((size_t)count);
+    EIG_HIP(hipMemcpyAsync(mine.data(), buf, count * sizeof(double), hipMemcpyDeviceToHost, s));
+    EIG_HIP(hipStreamSynchronize(s));
+    {
+      std::lock_guard<std::mutex> lk(h.m);
+      h.red[ctx->rank] = mine;
+    }
+    h.barrier();
+    std::vector<double> tot((size_t)count, 0.0);
+    for (int r = 0; r < h.P; ++r)
+      for (i64 i = 0; i < count; ++i) tot[i] += h.red[r][i];
+    h.barrier();
+    EIG_HIP(hipMemcpyAsync(buf, tot.data(), count * sizeof(double), hipMemcpyHostToDevice, s));
+    EIG_HIP(hipStreamSynchronize(s));
+    return;
+  }
   EIG_NCCL(ncclAllReduce(buf, buf, (size_t)count, ncclDouble, ncclSum, ctx->comm, s));
 }
 
@@ -94,7 +114,29 @@ void allreduce_sum(eig_ctx_t ctx, double *buf, i64 count, hipStream_t s)
 void halo_exchange(const eig_mat_s &A, double *x, hipStream_t s)
 {
   eig_ctx_t ctx = A.ctx;
-  if (!ctx->comm || ctx->nranks == 1 || (A.sends.empty() && A.recvs.empty())) return;
+  if (!ctx->distributed()) return;
+  if (ctx->loop)
+  {
+    // loopback: publish (x, window begin), then pull every recv range from the owner's vector
+    LoopHub &h = *ctx->loop;
+    EIG_HIP(hipStreamSynchronize(s));
+    {
+      std::lock_guard<std::mutex> lk(h.m);
+      h.xptr[ctx->rank] = x;
+      h.win_begin[ctx->rank] = A.win_begin;
+    }
+    h.barrier();
+    for (const auto &r : A.recvs)
+    {
+      const i64 global = A.win_begin + r.offset;
+      const double *src = h.xptr[r.peer] + (global - h.win_begin[r.peer]);
+      EIG_HIP(hipMemcpyAsync(x + r.offset, src, r.count * sizeof(double), hipMemcpyDeviceToDevice, s));
+    }
+    EIG_HIP(hipStreamSynchronize(s));
+    h.barrier();
+    return;
+  }
+  if (A.sends.empty() && A.recvs.empty()) return;
   EIG_NCCL(ncclGroupStart());
   for (const auto &r : A.recvs) EIG_NCCL(ncclRecv(x + r.offset, (size_t)r.count, ncclDouble, r.peer, ctx->comm, s));
   for (const auto &r : A.sends) EIG_NCCL(ncclSend(x + r.offset, (size_t)r.count, ncclDouble, r.peer, ctx->comm, s));
@@ -165,6 +207,7 @@ extern "C" int eig_ctx_destroy(eig_ctx_t ctx)
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
+  ctx->loop = nullptr;  // the hub is owned by eig_loopback_create / _destroy
   for (auto &e : ctx->pool)
     if (e.first) (void)hipFree(e.first);
   if (ctx->red.partials) (void)hipFree(ctx->red.partials);
@@ -216,6 +259,38 @@ extern "C" int eig_comm_init(eig_ctx_t ctx, int nranks, int rank, const unsigned
     std::memcpy(&u, id, 128);
     EIG_NCCL(ncclCommInitRank(&ctx->comm, nranks, u, rank));
     ctx->nranks = nranks;
+    ctx->rank = rank;
+  });
+}
+
+extern "C" int eig_loopback_create(int nranks, void **hub)
+{
+  return guard(nullptr, [&] {
+    EIG_CHECK(hub && nranks >= 1, EIG_ERR_ARG, "eig_loopback_create: bad arguments");
+    auto *h = new LoopHub();
+    h->P = nranks;
+    h->xptr.assign(nranks, nullptr);
+    h->win_begin.assign(nranks, 0);
+    h->red.assign(nranks, {});
+    h->gather.assign(4 * (size_t)nranks, 0);
+    *hub = h;
+  });
+}
+
+extern "C" int eig_loopback_destroy(void *hub)
+{
+  delete static_cast<LoopHub *>(hub);
+  return EIG_OK;
+}
+
+extern "C" int eig_comm_init_loopback(eig_ctx_t ctx, void *hub, int rank)
+{
+  return guard(ctx, [&] {
+    auto *h = static_cast<LoopHub *>(hub);
+    EIG_CHECK(ctx && h && rank >= 0 && rank < h->P, EIG_ERR_ARG, "eig_comm_init_loopback: bad arguments");
+    EIG_CHECK(!ctx->comm, EIG_ERR_ARG, "context already has an RCCL communicator");
+    ctx->loop = h;
+    ctx->nranks = h->P;
     ctx->rank = rank;
   });
 }
@@ -456,7 +531,18 @@ extern "C" int eig_mat_create_bcsr_dist(eig_ctx_t ctx, int64_t nb_rows_global, i
       // --- halo plan: allgather (row_begin, nb_local, cmin, cmax) of every rank ---
       std::vector<i64> mine = {row_begin, nb_local, cmin, cmax};
       std::vector<i64> all(4 * (size_t)P, 0);
-      if (ctx->comm && P > 1)
+      if (ctx->loop && P > 1)
+      {
+        LoopHub &h = *ctx->loop;
+        {
+          std::lock_guard<std::mutex> lk(h.m);
+          for (int t = 0; t < 4; ++t) h.gather[4 * me + t] = mine[t];
+        }
+        h.barrier();
+        all = h.gather;
+        h.barrier();
+      }
+      else if (ctx->comm && P > 1)
       {
         i64 *d = dev_alloc<i64>(4 * (size_t)P);
         EIG_HIP(hipMemcpy(d + 4 * me, mine.data(), 4 * sizeof(i64), hipMemcpyHostToDevice));
@@ -469,7 +555,7 @@ extern "C" int eig_mat_create_bcsr_dist(eig_ctx_t ctx, int64_t nb_rows_global, i
       {
         all = mine;
       }
-      const int nr = (ctx->comm && P > 1) ? P : 1;
+      const int nr = ctx->distributed() ? P : 1;
       std::vector<int64_t> rv(3 * (size_t)nr), sd(3 * (size_t)nr);
       int nrecv = 0, nsend = 0;
       {
@@ -556,8 +642,14 @@ namespace eigmi {
 void mv_device(eig_mat_s &A, double *x, double *y)
 {
   eig_ctx_t ctx = A.ctx;
-  if (!ctx->comm || ctx->nranks == 1 || (A.recvs.empty() && A.sends.empty()))
+  if (!ctx->distributed() || (A.recvs.empty() && A.sends.empty()))
   {
+    launch_spmv(A, x, y, nullptr, 0, A.nslices, ctx->stream);
+    return;
+  }
+  if (ctx->loop)
+  {
+    halo_exchange(A, x, ctx->stream);
     launch_spmv(A, x, y, nullptr, 0, A.nslices, ctx->stream);
     return;
   }
@@ -595,7 +687,7 @@ extern "C" int eig_mv_host(eig_mat_t A, const double *xh, double *yh)
     double *x = (double *)ctx_buffer(ctx, 0, wb);
     double *y = (double *)ctx_buffer(ctx, 1, wb);
     const i64 n = A->nb_rows * A->br;
-    if (A->nb_rows_global == A->nb_rows && (!ctx->comm || ctx->nranks == 1))
+    if (A->nb_rows_global == A->nb_rows && !ctx->distributed())
     {
       // square or rectangular single-rank operator: x has ncols entries
       EIG_HIP(hipMemcpyAsync(x, xh, (size_t)A->nb_cols * A->bc * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
@@ -670,7 +762,7 @@ extern "C" int eig_spmm_mv8(eig_mat_t A, int64_t m, const double *Qin, double *Q
   return guard(A ? A->ctx : nullptr, [&] {
     EIG_CHECK(A && Qin && Qout, EIG_ERR_ARG, "eig_spmm_mv8: null argument");
     EIG_MV8_CHECK(m);
-    EIG_CHECK(A->nb_rows == A->nb_cols && (!A->ctx->comm || A->ctx->nranks == 1), EIG_ERR_SHAPE,
+    EIG_CHECK(A->nb_rows == A->nb_cols && !A->ctx->distributed(), EIG_ERR_SHAPE,
               "eig_spmm_mv8: square single-rank matrix required");
     DeviceGuard dg(A->ctx->device);
     if (m > 0) launch_spmm_mv8(*A, m, Qin, Qout, A->ctx->stream);
@@ -810,7 +902,7 @@ extern "C" int eig_b_orthonormalize_mv8(eig_mat_t B, int64_t m, double *Q, doubl
     EIG_CHECK(B->br == 1 && B->bc == 1, EIG_ERR_BLOCKSIZE,
               "B_orthonormalize_blocked: only implemented for FieldMatrix<..,1,1>");
     EIG_MV8_CHECK(m);
-    EIG_CHECK(!B->ctx->comm || B->ctx->nranks == 1, EIG_ERR_ARG, "eig_b_orthonormalize_mv8: single rank only");
+    EIG_CHECK(!B->ctx->distributed(), EIG_ERR_ARG, "eig_b_orthonormalize_mv8: single rank only");
     eig_ctx_t ctx = B->ctx;
     DeviceGuard dg(ctx->device);
     hipStream_t s = ctx->stream;

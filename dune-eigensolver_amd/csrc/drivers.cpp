@@ -49,7 +49,7 @@ struct DevBuf {
   double *d() const { return static_cast<double *>(p); }
 };
 
-bool distributed(const eig_mat_s &A) { return A.ctx->comm && A.ctx->nranks > 1; }
+bool distributed(const eig_mat_s &A) { return A.ctx->distributed(); }
 
 // ---------------------------------------------------------------------------------------------
 // Symmetric tridiagonal eigenproblem (implicit QL with Wilkinson shifts).  d[k] diagonal,
@@ -217,8 +217,9 @@ void lanczos_step(eig_mat_s &A, double *u, double *up, double *t, int j, Lanczos
   const i64 own = A.own_offset;
   const i64 n = A.nb_rows;
   if (ev) EIG_HIP(hipEventRecord(ev[0], s));
-  if (!distributed(A) || (A.recvs.empty() && A.sends.empty()))
+  if (!distributed(A) || (A.recvs.empty() && A.sends.empty()) || ctx->loop)
   {
+    if (distributed(A)) halo_exchange(A, u, s);  // loopback transport: synchronous exchange
     launch_lanczos_spmv(A, u, up, t, j, lb.st, nullptr, 0, A.nslices, lb.st.dsum + j, lb.st.beta + j, nullptr, 0, s,
                         ctx->red);
   }

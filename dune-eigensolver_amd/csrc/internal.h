@@ -3,7 +3,9 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <condition_variable>
 #include <cstdint>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -54,6 +56,34 @@ struct ReduceWS {
   unsigned *tickets = nullptr; // kNumTickets, zero between launches (the last block resets)
 };
 
+// In-process loopback transport: P virtual ranks (one host thread + context each, usually on the
+// same device) exchange through this hub instead of RCCL.  Test-only path for the distributed
+// code on a single GPU; every operation is synchronous.
+struct LoopHub {
+  int P = 1;
+  std::mutex m;
+  std::condition_variable cv;
+  int arrived = 0;
+  unsigned long gen = 0;
+  std::vector<double *> xptr;      // per rank: vector being exchanged
+  std::vector<i64> win_begin;      // per rank: window begin (scalar)
+  std::vector<std::vector<double>> red;
+  std::vector<i64> gather;
+  void barrier()
+  {
+    std::unique_lock<std::mutex> lk(m);
+    const unsigned long g = gen;
+    if (++arrived == P)
+    {
+      arrived = 0;
+      ++gen;
+      cv.notify_all();
+    }
+    else
+      cv.wait(lk, [&] { return gen != g; });
+  }
+};
+
 }  // namespace eigmi
 
 struct eig_ctx_s {
@@ -66,7 +96,9 @@ struct eig_ctx_s {
   int num_cu = 256;
   // RCCL
   ncclComm_t comm = nullptr;
+  eigmi::LoopHub *loop = nullptr;    // in-process loopback transport (tests), exclusive with comm
   int nranks = 1, rank = 0;
+  bool distributed() const { return nranks > 1 && (comm || loop); }
   // reusable device buffers for drivers (grown on demand)
   std::vector<std::pair<void *, size_t>> pool;
 };

@@ -60,6 +60,9 @@ SIGNATURES = {
     "eig_comm_init": (_int, [_vp, _int, _int, ctypes.c_char_p]),
     "eig_comm_allreduce_sum": (_int, [_vp, _vp, _i64]),
     "eig_comm_barrier": (_int, [_vp]),
+    "eig_loopback_create": (_int, [_int, ctypes.POINTER(_vp)]),
+    "eig_loopback_destroy": (_int, [_vp]),
+    "eig_comm_init_loopback": (_int, [_vp, _vp, _int]),
     "eig_malloc": (_int, [_vp, ctypes.c_size_t, ctypes.POINTER(_vp)]),
     "eig_free": (_int, [_vp, _vp]),
     "eig_memcpy_h2d": (_int, [_vp, _vp, _vp, ctypes.c_size_t]),

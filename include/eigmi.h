@@ -66,6 +66,13 @@ const char *eig_version(void);
 int eig_comm_unique_id(unsigned char id[128]);
 int eig_comm_init(eig_ctx_t ctx, int nranks, int rank, const unsigned char id[128]);
 int eig_comm_allreduce_sum(eig_ctx_t ctx, double *buf, int64_t count);
+/* In-process loopback transport for testing the distributed path on ONE device: create a hub for
+ * nranks virtual ranks, give each rank its own host thread + context and attach it with
+ * eig_comm_init_loopback.  Halo exchange and allreduce then go through device copies and a host
+ * barrier instead of RCCL (synchronous; not a performance path). */
+int eig_loopback_create(int nranks, void **hub);
+int eig_loopback_destroy(void *hub);
+int eig_comm_init_loopback(eig_ctx_t ctx, void *hub, int rank);
 int eig_comm_barrier(eig_ctx_t ctx);
 
 /* ---------------------------------------------------------------- device memory ------------ */

@@ -1,0 +1,154 @@
+// loopback_test.cc -- the distributed device path on ONE GPU: P virtual ranks (host threads, one
+// context each) over libeigmi's in-process loopback transport.  Exercises the row-partitioned
+// SELL image with window-local columns, the halo plan, the interior / boundary slice split, the
+// split-K1 carry and the allreduce placement of the Lanczos drivers; only the RCCL calls
+// themselves are replaced.  Compared with the single-rank run of the same matrix.
+//
+//   loopback_test P N     (defaults 3, 24)
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "eigmi.h"
+
+#define CK(x)                                                                               \
+  do {                                                                                      \
+    int rc_ = (x);                                                                          \
+    if (rc_ != EIG_OK) {                                                                    \
+      std::printf("FAIL %s -> %d (%s)\n", #x, rc_, eig_last_error(nullptr));                 \
+      std::exit(3);                                                                         \
+    }                                                                                       \
+  } while (0)
+
+struct Rows {
+  std::vector<int64_t> rp;
+  std::vector<int32_t> c;
+  std::vector<double> v;
+};
+
+static Rows gen(int N, int64_t b, int64_t cnt)
+{
+  Rows r;
+  int64_t nnz = eig_gen_nnzb_rows(4, N, b, cnt);
+  r.rp.resize(cnt + 1);
+  r.c.resize(nnz > 0 ? nnz : 1);
+  r.v.resize(nnz > 0 ? nnz : 1);
+  CK(eig_gen_matrix_rows(4, N, b, cnt, r.rp.data(), r.c.data(), r.v.data()));
+  return r;
+}
+
+int main(int argc, char **argv)
+{
+  const int P = argc > 1 ? std::atoi(argv[1]) : 3;
+  const int N = argc > 2 ? std::atoi(argv[2]) : 24;
+  const int64_t n = (int64_t)N * N * N;
+  const int steps = 30, nev = 3, ncv = 120;
+  int failures = 0;
+
+  // ---- serial reference on one context
+  std::vector<double> x(n), y_ser(n), a_ser(steps), b_ser(steps + 1), ev_ser(nev);
+  for (int64_t i = 0; i < n; ++i) x[i] = std::sin(0.37 * i) + 0.01 * (i % 7);
+  {
+    eig_ctx_t ctx;
+    CK(eig_ctx_create(0, &ctx));
+    Rows r = gen(N, 0, n);
+    eig_mat_t A;
+    CK(eig_mat_create_bcsr(ctx, n, n, 1, 1, r.rp.data(), r.c.data(), r.v.data(), &A));
+    CK(eig_mv_host(A, x.data(), y_ser.data()));
+    CK(eig_lanczos_run(A, steps, nullptr, 123, 0, a_ser.data(), b_ser.data(), nullptr));
+    CK(eig_lanczos_solve(A, nev, ncv, EIG_WHICH_LA, 123, ev_ser.data(), nullptr, nullptr));
+    eig_mat_destroy(A);
+    eig_ctx_destroy(ctx);
+  }
+
+  // ---- P virtual ranks
+  void *hub;
+  CK(eig_loopback_create(P, &hub));
+  std::vector<std::vector<double>> y(P), al(P, std::vector<double>(steps)), be(P, std::vector<double>(steps + 1)),
+      ev(P, std::vector<double>(nev));
+  std::vector<int64_t> rb(P), rc(P), halo(P);
+  std::vector<double> dots(P);
+  std::vector<std::thread> th;
+  for (int r = 0; r < P; ++r)
+    th.emplace_back([&, r] {
+      eig_ctx_t ctx;
+      CK(eig_ctx_create(0, &ctx));
+      CK(eig_comm_init_loopback(ctx, hub, r));
+      const int64_t planes = N;
+      const int64_t p0 = planes * r / P, p1 = planes * (r + 1) / P;
+      const int64_t b = p0 * N * N, cnt = (p1 - p0) * N * N;
+      rb[r] = b;
+      rc[r] = cnt;
+      Rows rows = gen(N, b, cnt);
+      eig_mat_t A;
+      CK(eig_mat_create_bcsr_dist(ctx, n, b, cnt, 1, 1, rows.rp.data(), rows.c.data(), rows.v.data(), &A));
+      eig_mat_info info;
+      CK(eig_mat_get_info(A, &info));
+      halo[r] = info.halo_recv;
+      // y = A x through window vectors
+      double *dx, *dy, *dd;
+      CK(eig_malloc(ctx, info.window * 8, (void **)&dx));
+      CK(eig_malloc(ctx, info.window * 8, (void **)&dy));
+      CK(eig_malloc(ctx, 8, (void **)&dd));
+      CK(eig_memset(ctx, dx, 0, info.window * 8));
+      CK(eig_memcpy_h2d(ctx, dx + info.own_offset, x.data() + b, cnt * 8));
+      CK(eig_mv(A, dx, dy));
+      y[r].resize(cnt);
+      CK(eig_memcpy_d2h(ctx, y[r].data(), dy + info.own_offset, cnt * 8));
+      // global dot of the owned slices
+      CK(eig_dot(ctx, cnt, dx + info.own_offset, dx + info.own_offset, dd));
+      CK(eig_memcpy_d2h(ctx, &dots[r], dd, 8));
+      // Lanczos recurrence and solver
+      CK(eig_lanczos_run(A, steps, nullptr, 123, EIG_LANCZOS_TIME_KERNELS, al[r].data(), be[r].data(), nullptr));
+      CK(eig_lanczos_solve(A, nev, ncv, EIG_WHICH_LA, 123, ev[r].data(), nullptr, nullptr));
+      eig_free(ctx, dx);
+      eig_free(ctx, dy);
+      eig_free(ctx, dd);
+      eig_mat_destroy(A);
+      eig_ctx_destroy(ctx);
+    });
+  for (auto &t : th) t.join();
+  eig_loopback_destroy(hub);
+
+  double xx = 0.0;
+  for (double v : x) xx += v * v;
+  for (int r = 0; r < P; ++r)
+  {
+    if (std::memcmp(y[r].data(), y_ser.data() + rb[r], rc[r] * 8) != 0)
+    {
+      std::printf("FAIL rank %d: distributed SpMV not bitwise equal to the serial one\n", r);
+      ++failures;
+    }
+    const int64_t expect_halo = (r > 0 ? N * N : 0) + (r < P - 1 ? N * N : 0);
+    if (halo[r] != expect_halo)
+    {
+      std::printf("FAIL rank %d: halo %ld != %ld\n", r, (long)halo[r], (long)expect_halo);
+      ++failures;
+    }
+    if (std::fabs(dots[r] - xx) > 1e-12 * xx)
+    {
+      std::printf("FAIL rank %d: global dot %.17g vs %.17g\n", r, dots[r], xx);
+      ++failures;
+    }
+    for (int j = 0; j < steps; ++j)
+      if (std::fabs(al[r][j] - a_ser[j]) > 1e-12 * std::fabs(a_ser[j]) ||
+          std::fabs(be[r][j + 1] - b_ser[j + 1]) > 1e-12 * std::fabs(b_ser[j + 1]))
+      {
+        std::printf("FAIL rank %d step %d: alpha %.17g/%.17g beta %.17g/%.17g\n", r, j, al[r][j], a_ser[j],
+                    be[r][j + 1], b_ser[j + 1]);
+        ++failures;
+        break;
+      }
+    for (int i = 0; i < nev; ++i)
+      if (std::fabs(ev[r][i] - ev_ser[i]) > 1e-10)
+      {
+        std::printf("FAIL rank %d: Ritz %d %.17g vs %.17g\n", r, i, ev[r][i], ev_ser[i]);
+        ++failures;
+      }
+  }
+  std::printf(failures ? "FAILED %d\n" : "ALL OK (P=%d, N=%d)\n", failures ? failures : P, N);
+  return failures ? 1 : 0;
+}
