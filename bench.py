@@ -92,7 +92,8 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    ctx = eigmi.Context(local)
+    # EIGMI_FORCE_DEVICE pins every rank to one device (RCCL path rehearsal on a 1-GPU box)
+    ctx = eigmi.Context(int(os.environ.get("EIGMI_FORCE_DEVICE", local)))
     if world > 1:
         import torch
         uid = eigmi.Context.unique_id() if rank == 0 else bytes(128)

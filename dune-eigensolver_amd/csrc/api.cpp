@@ -3,6 +3,7 @@
 // MultiVector operations.  Drivers live in drivers.cpp.
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <random>
 #include <thread>
@@ -368,58 +369,119 @@ extern "C" int eig_memset(eig_ctx_t ctx, void *dst, int value, size_t bytes)
 // ============================================================================================
 namespace {
 
-// Build the SELL-64 image of `nb` block rows (rowptr/col/vals on the host, col already mapped to
-// window-local block columns by `colmap`) and upload it.
-void build_sell(eig_mat_s &A, i64 nb, const int64_t *rowptr, const int32_t *col, const double *vals, i64 col_shift)
+// Rows per lane of the SELL image for 1x1 matrices (EIGMI_SELL_R overrides; 1, 2 or 4).
+int sell_rows_per_lane(int br, int bc)
 {
-  const int bb = A.br * A.bc;
-  const i64 ns = (nb + 63) / 64;
-  std::vector<i64> sp(ns + 1, 0);
-  for (i64 s = 0; s < ns; ++s)
+  if (br != 1 || bc != 1) return 1;
+  int R = 1;  // measured best for the fused Lanczos kernel (tools/spmv_sweep.py)
+  if (const char *e = std::getenv("EIGMI_SELL_R"))
   {
-    i64 w = 0;
-    for (i64 r = s * 64; r < std::min(nb, s * 64 + 64); ++r) w = std::max<i64>(w, rowptr[r + 1] - rowptr[r]);
-    sp[s + 1] = sp[s] + 64 * w;
+    const int v = std::atoi(e);
+    if (v == 1 || v == 2 || v == 4) R = v;
   }
-  const i64 total = sp[ns];
-  std::vector<i32> cimg(std::max<i64>(total, 1));
-  std::vector<double> vimg(std::max<i64>(total * bb, 1));
-  // parallel fill over slice ranges
+  return R;
+}
+
+// Build the SELL-C image (C = 64 R) of `nb` block rows (rowptr/col/vals on the host; columns are
+// shifted by col_shift into window-local block columns) and upload it.
+bool stencil_enabled()
+{
+  const char *e = std::getenv("EIGMI_STENCIL");
+  return !(e && e[0] == '0');
+}
+
+template <class F>
+void parallel_slices(i64 ns, F &&f)
+{
   unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
   if (ns < 4096) nt = 1;
-  auto work = [&](i64 s0, i64 s1) {
-    for (i64 s = s0; s < s1; ++s)
-    {
-      const i64 base = sp[s], w = (sp[s + 1] - base) / 64;
-      for (int l = 0; l < 64; ++l)
-      {
-        const i64 r = s * 64 + l;
-        const i64 len = (r < nb) ? rowptr[r + 1] - rowptr[r] : 0;
-        for (i64 k = 0; k < w; ++k)
-        {
-          const i64 ci = base + k * 64 + l;
-          if (k < len)
-          {
-            const i64 p = rowptr[r] + k;
-            cimg[ci] = (i32)(col[p] - col_shift);
-            for (int t = 0; t < bb; ++t) vimg[(base + k * 64) * bb + t * 64 + l] = vals[p * bb + t];
-          }
-          else
-          {
-            cimg[ci] = -1;
-            for (int t = 0; t < bb; ++t) vimg[(base + k * 64) * bb + t * 64 + l] = 0.0;
-          }
-        }
-      }
-    }
-  };
-  if (nt == 1) work(0, ns);
+  if (nt == 1) f(0, ns);
   else
   {
     std::vector<std::thread> th;
-    for (unsigned t = 0; t < nt; ++t) th.emplace_back(work, ns * t / nt, ns * (t + 1) / nt);
+    for (unsigned t = 0; t < nt; ++t) th.emplace_back([&, t] { f(ns * t / nt, ns * (t + 1) / nt); });
     for (auto &t : th) t.join();
   }
+}
+
+// Build the SELL-C image (C = 64 R) of `nb` block rows (rowptr/col/vals on the host; columns are
+// shifted by col_shift into window-local block columns; global row = row_begin + r) and upload.
+// 1x1 slices whose rows use at most 8 distinct offsets (col - row) become stencil slices: their
+// value slots are indexed by offset and a per-row mask marks the stored entries (internal.h).
+void build_sell(eig_mat_s &A, i64 nb, const int64_t *rowptr, const int32_t *col, const double *vals, i64 col_shift)
+{
+  const int bb = A.br * A.bc;
+  A.R = sell_rows_per_lane(A.br, A.bc);
+  const i64 C = 64 * (i64)A.R;
+  const i64 ns = (nb + C - 1) / C;
+  const bool try_stencil = (bb == 1) && stencil_enabled();
+  const i64 row0 = A.row_begin;
+  std::vector<i32> swidth(ns, -1), sdelta(8 * (size_t)ns, 0);
+  std::vector<i64> sp(ns + 1, 0), wdt(ns, 0);
+  parallel_slices(ns, [&](i64 s0, i64 s1) {
+    std::vector<i64> offs;
+    for (i64 s = s0; s < s1; ++s)
+    {
+      i64 w = 0;
+      offs.clear();
+      bool ok = try_stencil;
+      for (i64 r = s * C; r < std::min(nb, s * C + C); ++r)
+      {
+        w = std::max<i64>(w, rowptr[r + 1] - rowptr[r]);
+        for (i64 p = rowptr[r]; ok && p < rowptr[r + 1]; ++p)
+        {
+          const i64 d = (i64)col[p] - (row0 + r);
+          if (std::find(offs.begin(), offs.end(), d) == offs.end())
+          {
+            if (offs.size() == 8 || d < INT32_MIN || d > INT32_MAX) ok = false;
+            else offs.push_back(d);
+          }
+        }
+      }
+      if (ok && !offs.empty())
+      {
+        std::sort(offs.begin(), offs.end());
+        swidth[s] = (i32)offs.size();
+        for (size_t k = 0; k < offs.size(); ++k) sdelta[8 * s + k] = (i32)offs[k];
+        w = (i64)offs.size();
+      }
+      wdt[s] = w;
+    }
+  });
+  for (i64 s = 0; s < ns; ++s) sp[s + 1] = sp[s] + C * wdt[s];
+  const i64 total = sp[ns];
+  std::vector<i32> cimg(std::max<i64>(total, 1));
+  std::vector<double> vimg(std::max<i64>(total * bb, 1));
+  std::vector<uint8_t> mimg(try_stencil ? (size_t)(ns * C) : 0, 0);
+  parallel_slices(ns, [&](i64 s0, i64 s1) {
+    for (i64 s = s0; s < s1; ++s)
+    {
+      const i64 base = sp[s], w = (sp[s + 1] - base) / C;
+      for (i64 l = 0; l < C; ++l)
+      {
+        const i64 r = s * C + l;
+        const i64 len = (r < nb) ? rowptr[r + 1] - rowptr[r] : 0;
+        for (i64 k = 0; k < w; ++k)
+        {
+          cimg[base + k * C + l] = -1;
+          for (int t = 0; t < bb; ++t) vimg[(base + k * C) * bb + t * C + l] = 0.0;
+        }
+        for (i64 e = 0; e < len; ++e)
+        {
+          const i64 p = rowptr[r] + e;
+          i64 k = e;
+          if (swidth[s] > 0)
+          {
+            const i64 d = (i64)col[p] - (row0 + r);
+            k = std::find(&sdelta[8 * s], &sdelta[8 * s] + swidth[s], (i32)d) - &sdelta[8 * s];
+            mimg[s * C + l] |= (uint8_t)(1u << k);
+          }
+          cimg[base + k * C + l] = (i32)(col[p] - col_shift);
+          for (int t = 0; t < bb; ++t) vimg[(base + k * C) * bb + t * C + l] = vals[p * bb + t];
+        }
+      }
+    }
+  });
   A.nslices = ns;
   A.nnzb_padded = total;
   A.slice_ptr = dev_alloc<i64>(ns + 1);
@@ -429,8 +491,19 @@ void build_sell(eig_mat_s &A, i64 nb, const int64_t *rowptr, const int32_t *col,
   EIG_HIP(hipMemcpyAsync(A.slice_ptr, sp.data(), (ns + 1) * sizeof(i64), hipMemcpyHostToDevice, s));
   EIG_HIP(hipMemcpyAsync(A.col, cimg.data(), total * sizeof(i32), hipMemcpyHostToDevice, s));
   EIG_HIP(hipMemcpyAsync(A.val, vimg.data(), total * bb * sizeof(double), hipMemcpyHostToDevice, s));
+  A.n_stencil_slices = 0;
+  for (i64 q = 0; q < ns; ++q) A.n_stencil_slices += swidth[q] > 0;
+  if (A.n_stencil_slices > 0)
+  {
+    A.st_width = dev_alloc<i32>(ns);
+    A.st_delta = dev_alloc<i32>(8 * ns);
+    A.st_mask = dev_alloc<uint8_t>(ns * C);
+    EIG_HIP(hipMemcpyAsync(A.st_width, swidth.data(), ns * sizeof(i32), hipMemcpyHostToDevice, s));
+    EIG_HIP(hipMemcpyAsync(A.st_delta, sdelta.data(), 8 * ns * sizeof(i32), hipMemcpyHostToDevice, s));
+    EIG_HIP(hipMemcpyAsync(A.st_mask, mimg.data(), ns * C, hipMemcpyHostToDevice, s));
+  }
   EIG_HIP(hipStreamSynchronize(s));
-  A.device_bytes = (ns + 1) * 8 + total * 4 + total * bb * 8;
+  A.device_bytes = (ns + 1) * 8 + total * 4 + total * bb * 8 + (A.n_stencil_slices ? ns * (36 + C) : 0);
 }
 
 void validate_csr(i64 nb, i64 ncols, const int64_t *rowptr, const int32_t *col)
@@ -453,6 +526,9 @@ void destroy_mat(eig_mat_s *A)
   if (A->slice_ptr) (void)hipFree(A->slice_ptr);
   if (A->col) (void)hipFree(A->col);
   if (A->val) (void)hipFree(A->val);
+  if (A->st_width) (void)hipFree(A->st_width);
+  if (A->st_delta) (void)hipFree(A->st_delta);
+  if (A->st_mask) (void)hipFree(A->st_mask);
   if (A->slice_list) (void)hipFree(A->slice_list);
   delete A;
 }
@@ -572,7 +648,8 @@ extern "C" int eig_mat_create_bcsr_dist(eig_ctx_t ctx, int64_t nb_rows_global, i
       for (i64 s = 0; s < A->nslices; ++s)
       {
         bool in = true;
-        for (i64 r = s * 64; r < std::min(nb_local, s * 64 + 64) && in; ++r)
+        const i64 C = 64 * (i64)A->R;
+        for (i64 r = s * C; r < std::min(nb_local, s * C + C) && in; ++r)
           for (i64 p = rowptr[r]; p < rowptr[r + 1]; ++p)
             if (col[p] < own_lo || col[p] >= own_hi)
             {
@@ -624,6 +701,8 @@ extern "C" int eig_mat_get_info(eig_mat_t A, eig_mat_info *info)
     info->halo_recv = A->halo_recv;
     info->halo_send = A->halo_send;
     info->device_bytes = A->device_bytes;
+    info->stencil_slices = A->n_stencil_slices;
+    info->rows_per_lane = A->R;
   });
 }
 

@@ -128,8 +128,20 @@ struct eig_mat_s {
   eigmi::i64 own_offset = 0;      // owned rows' offset in the window (scalar)
   eigmi::i64 nnzb = 0, nnzb_padded = 0;
   eigmi::i64 nslices = 0;
-  // SELL-64 device image: slice s covers block rows [64 s, 64 s + 64); block k of lane l sits at
-  // slice_ptr[s] + k*64 + l (cols) and (slice_ptr[s] + k*64)*br*bc + t*64 + l (values, t < br*bc).
+  // SELL-C device image, C = 64 R: slice s covers block rows [C s, C s + C); entry k of slice row
+  // r sits at slice_ptr[s] + k*C + r (cols) and (slice_ptr[s] + k*C)*br*bc + t*C + r (values,
+  // t < br*bc).  Lane l of the slice's wavefront owns rows l R .. l R + R - 1.  R = 1 for blocks.
+  int R = 1;
+  // Stencil slices (1x1 blocks only): when every row of slice s draws its columns from one set of
+  // at most 8 offsets delta = global col - global row (structured-grid / banded matrices), the
+  // slice is read through st_delta[8 s + k] (ascending) and a per-row bit mask st_mask[r] (bit k
+  // = row r stores the entry at delta_k) instead of the per-entry columns: 1 B per row instead of
+  // 4 B per entry.  st_width[s] = number of offsets, or -1 for an explicit-column slice.  Entries
+  // keep their ascending-column order, so results stay bitwise identical.
+  eigmi::i32 *st_width = nullptr;   // nslices
+  eigmi::i32 *st_delta = nullptr;   // 8 * nslices
+  uint8_t *st_mask = nullptr;       // nslices * C
+  eigmi::i64 n_stencil_slices = 0;
   eigmi::i64 *slice_ptr = nullptr;  // nslices + 1
   eigmi::i32 *col = nullptr;        // nnzb_padded, window-local block columns, -1 = padding
   double *val = nullptr;            // nnzb_padded * br * bc

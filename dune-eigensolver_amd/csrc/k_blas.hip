@@ -164,30 +164,27 @@ void launch_sqrt_inplace(double *v, int count, hipStream_t s)
 // row r has window-local block column r + own_offset / bc.
 // ---------------------------------------------------------------------------------------------
 __global__ void k_shift_diag(i64 nbrows, i64 own_blk, const i64 *__restrict__ slice_ptr, const i32 *__restrict__ col,
-                             double *__restrict__ val, int br, int bc, i64 nslices, double shift)
+                             double *__restrict__ val, int br, int bc, int C, double shift)
 {
-  const i64 s = (i64)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (s >= nslices) return;
-  const i64 r = s * 64 + lane;
+  const i64 r = (i64)blockIdx.x * blockDim.x + threadIdx.x;  // block row
   if (r >= nbrows) return;
+  const i64 s = r / C, l = r % C;
   const i64 base = slice_ptr[s];
-  const int width = (int)((slice_ptr[s + 1] - base) >> 6);
+  const int width = (int)((slice_ptr[s + 1] - base) / C);
   const int bb = br * bc, nd = br < bc ? br : bc;
   for (int k = 0; k < width; ++k)
   {
-    const i32 c = col[base + (i64)k * 64 + lane];
+    const i32 c = col[base + (i64)k * C + l];
     if (c == (i32)(r + own_blk))
-      for (int d = 0; d < nd; ++d) val[(base + (i64)k * 64) * bb + (d * bc + d) * 64 + lane] += shift;
+      for (int d = 0; d < nd; ++d) val[(base + (i64)k * C) * bb + (i64)(d * bc + d) * C + l] += shift;
   }
 }
 void launch_shift_diag(eig_mat_s &A, double shift, hipStream_t s)
 {
-  const int wpb = 4;
-  const i64 G = (A.nslices + wpb - 1) / wpb;
+  const i64 G = (A.nb_rows + 255) / 256;
   if (G == 0) return;
-  hipLaunchKernelGGL(k_shift_diag, dim3((unsigned)G), dim3(64 * wpb), 0, s, A.nb_rows, A.own_offset / A.bc,
-                     A.slice_ptr, A.col, A.val, A.br, A.bc, A.nslices, shift);
+  hipLaunchKernelGGL(k_shift_diag, dim3((unsigned)G), dim3(256), 0, s, A.nb_rows, A.own_offset / A.bc, A.slice_ptr,
+                     A.col, A.val, A.br, A.bc, 64 * A.R, shift);
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -29,23 +29,26 @@ template <int MB>
 __global__ __launch_bounds__(256) void k_spmm_mv8(i64 nrows, i64 nslices, const i64 *__restrict__ slice_ptr,
                                                   const double *__restrict__ val, const i32 *__restrict__ col,
                                                   const double *__restrict__ Qin, double *__restrict__ Qout, i64 n,
-                                                  int nblk_total)
+                                                  int nblk_total, int C)
 {
   const int wave = threadIdx.x >> 6, L = threadIdx.x & 63;
-  const int ri = wave * 16 + (L >> 2), cp = L & 3;
+  const int cp = L & 3;
   const int b0 = blockIdx.y * MB;
-  for (i64 s = blockIdx.x; s < nslices; s += gridDim.x)
+  const i64 nsub = (i64)nslices * (C / 64);  // 64-row sub-slices
+  for (i64 ss = blockIdx.x; ss < nsub; ss += gridDim.x)
   {
+    const i64 s = ss / (C / 64);
+    const int ri = (int)(ss % (C / 64)) * 64 + wave * 16 + (L >> 2);
     const i64 base = slice_ptr[s];
-    const int width = (int)((slice_ptr[s + 1] - base) >> 6);
+    const int width = (int)((slice_ptr[s + 1] - base) / C);
     double2 acc[MB];
 #pragma unroll
     for (int q = 0; q < MB; ++q) acc[q] = make_double2(0.0, 0.0);
     for (int k = 0; k < width; ++k)
     {
-      const i32 c = col[base + (i64)k * 64 + ri];
+      const i32 c = col[base + (i64)k * C + ri];
       if (c < 0) continue;
-      const double a = val[base + (i64)k * 64 + ri];
+      const double a = val[base + (i64)k * C + ri];
 #pragma unroll
       for (int q = 0; q < MB; ++q)
       {
@@ -57,7 +60,7 @@ __global__ __launch_bounds__(256) void k_spmm_mv8(i64 nrows, i64 nslices, const 
         }
       }
     }
-    const i64 r = s * 64 + ri;
+    const i64 r = s * C + ri;
     if (r < nrows)
     {
 #pragma unroll
@@ -74,10 +77,10 @@ void launch_spmm_mv8(const eig_mat_s &A, i64 m, const double *Qin, double *Qout,
   const int nblk = (int)(m / 8);
   const int MB = 4;
   const int gy = (nblk + MB - 1) / MB;
-  const int gx = grid_for(A.nslices, 1, kStreamBlocks);
+  const int gx = grid_for(A.nslices * A.R, 1, kStreamBlocks);
   // Qin is a window-layout multivector on one rank (window == n); columns index it directly.
   hipLaunchKernelGGL(k_spmm_mv8<MB>, dim3(gx, gy), dim3(256), 0, s, A.nb_rows, A.nslices, A.slice_ptr, A.val, A.col,
-                     Qin, Qout, A.nb_rows, nblk);
+                     Qin, Qout, A.nb_rows, nblk, 64 * A.R);
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -1,18 +1,17 @@
-// k_spmv.hip -- sparse matrix x vector on the SELL-64 image (gfx950).
+// k_spmv.hip -- sparse matrix x vector on the SELL-C image (gfx950).
 //
 // Replaces BCRSMatrix::mv (dune-istl; called at arpack_geneo_wrapper.hh:275 through multMvB)
 // and the b = 1 product matmul_sparse_tallskinny_naive (kernels_cpp.hh:596-621).
 //
-// Layout (internal.h): one wavefront owns one 64-row slice, lane l = block row 64 s + l.  Block
-// k of the slice is column-major across lanes, so every wave-instruction that fetches the k-th
-// value / column of 64 rows reads 512 B / 256 B contiguous (coalesced), and the row's stored
-// (ascending-column) order is kept: each lane accumulates exactly like the ISTL row loop, from
-// 0.0, mul then add (built with -ffp-contract=off), so y is bitwise BCRSMatrix::mv.
-// Padding entries carry column -1 and are skipped (no 0*x term, no -0.0 / NaN side effects).
+// Layout (internal.h): slices of C = 64 R block rows, one wavefront per slice; lane l owns the R
+// adjacent rows l R .. l R + R - 1.  Entry k of slice row r sits at slice_ptr[s] + k C + r
+// (column-major over the slice), so the k-th (value, column) of a lane's R rows is one R-wide
+// vector load and a wave-instruction reads 512 R bytes contiguous.  Every row keeps its stored
+// (ascending-column) order and accumulates from 0.0, mul then add (-ffp-contract=off): y is
+// bitwise BCRSMatrix::mv.  Padding entries carry column -1 and are skipped.
 //
-// Work split: a workgroup of 4 waves walks a CONTIGUOUS chunk of slices (waves interleaved),
-// so consecutive rows -- which share x lines -- stay in one CU / one XCD's L2; at 2048
-// workgroups (8 per CU) the whole grid is resident.
+// Work split: a workgroup of 4 waves walks a CONTIGUOUS chunk of slices (waves interleaved), so
+// rows that share x lines stay in one CU / one XCD's L2; 2048 workgroups (8 per CU) are resident.
 #include "internal.h"
 #include "reduce_dev.h"
 
@@ -20,9 +19,36 @@ namespace eigmi {
 
 constexpr int kWaves = kStreamThreads / 64;
 
-struct SliceRange {
-  i64 begin, end;  // slice work items handled by this wave: [begin, end) step kWaves
+template <int R>
+struct Vec;
+template <>
+struct Vec<1> {
+  typedef double d;
+  typedef i32 i;
 };
+template <>
+struct Vec<2> {
+  typedef double d __attribute__((ext_vector_type(2)));
+  typedef i32 i __attribute__((ext_vector_type(2)));
+};
+template <>
+struct Vec<4> {
+  typedef double d __attribute__((ext_vector_type(4)));
+  typedef i32 i __attribute__((ext_vector_type(4)));
+};
+
+template <int R>
+__device__ __forceinline__ double lane_get(const typename Vec<R>::d &v, int q)
+{
+  if constexpr (R == 1) return v;
+  else return v[q];
+}
+template <int R>
+__device__ __forceinline__ i32 lane_geti(const typename Vec<R>::i &v, int q)
+{
+  if constexpr (R == 1) return v;
+  else return v[q];
+}
 
 __device__ __forceinline__ void chunk_of(i64 count, i64 &b, i64 &e)
 {
@@ -33,61 +59,168 @@ __device__ __forceinline__ void chunk_of(i64 count, i64 &b, i64 &e)
   if (e > count) e = count;
 }
 
-// One scalar row of a 1x1-block SELL slice: prefetch 8 (val, col) pairs, then gather x.
-__device__ __forceinline__ double row_dot_b1(const double *__restrict__ val, const i32 *__restrict__ col,
-                                             const double *__restrict__ x, i64 base, int width, int lane)
+// acc[q] = sum_k a[k][q] * x[c[k][q]] for the R rows of this lane, k ascending.  KC entries are
+// prefetched per round (8 (value, column) loads in flight per lane for every R).
+template <int R>
+__device__ __forceinline__ void rows_dot(const double *__restrict__ val, const i32 *__restrict__ col,
+                                         const double *__restrict__ x, i64 base, int width, int lane, double (&acc)[R])
 {
-  double acc = 0.0;
-  for (int k0 = 0; k0 < width; k0 += 8)
-  {
-    double a[8];
-    i32 c[8];
+  constexpr int C = 64 * R;
+  constexpr int KC = 8 / R;
+  typedef typename Vec<R>::d dv;
+  typedef typename Vec<R>::i iv;
 #pragma unroll
-    for (int k = 0; k < 8; ++k)
+  for (int q = 0; q < R; ++q) acc[q] = 0.0;
+  // slice base pointers are wave-uniform (scalar); per-lane offsets are 32-bit
+  const double *vs = val + base;
+  const i32 *cs = col + base;
+  for (int k0 = 0; k0 < width; k0 += KC)
+  {
+    dv a[KC];
+    iv c[KC];
+#pragma unroll
+    for (int k = 0; k < KC; ++k)
     {
       if (k0 + k < width)
       {
-        const i64 idx = base + (i64)(k0 + k) * 64 + lane;
-        c[k] = __builtin_nontemporal_load(col + idx);
-        a[k] = __builtin_nontemporal_load(val + idx);
+        const int idx = (k0 + k) * C + lane * R;
+        c[k] = __builtin_nontemporal_load(reinterpret_cast<const iv *>(cs + idx));
+        a[k] = __builtin_nontemporal_load(reinterpret_cast<const dv *>(vs + idx));
       }
       else
       {
-        c[k] = -1;
-        a[k] = 0.0;
+        c[k] = (iv)(-1);
+        a[k] = (dv)(0.0);
       }
     }
-    double xv[8];
+    double xv[KC][R];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) xv[k] = (c[k] >= 0) ? x[c[k]] : 0.0;
+    for (int k = 0; k < KC; ++k)
 #pragma unroll
-    for (int k = 0; k < 8; ++k)
-      if (c[k] >= 0) acc += a[k] * xv[k];
+      for (int q = 0; q < R; ++q)
+      {
+        const i32 cc = lane_geti<R>(c[k], q);
+        xv[k][q] = (cc >= 0) ? x[cc] : 0.0;
+      }
+#pragma unroll
+    for (int k = 0; k < KC; ++k)
+#pragma unroll
+      for (int q = 0; q < R; ++q)
+        if (lane_geti<R>(c[k], q) >= 0) acc[q] += lane_get<R>(a[k], q) * xv[k][q];
   }
-  return acc;
 }
 
-// y[own + r] = (A x)[r], 1x1 blocks.
-__global__ __launch_bounds__(kStreamThreads) void k_spmv_b1(i64 nrows, const i64 *__restrict__ slice_ptr,
-                                                            const i32 *__restrict__ slices, i64 first, i64 count,
-                                                            const double *__restrict__ val, const i32 *__restrict__ col,
-                                                            const double *__restrict__ x, double *__restrict__ y)
+// Stencil slice: entry k of row r is stored iff bit k of mask[r]; its column is r + own + delta_k
+// (window-local).  Offsets ascend, so each row still accumulates in ascending-column order.
+template <int R>
+__device__ __forceinline__ void rows_dot_stencil(const double *__restrict__ val, const i32 *__restrict__ delta,
+                                                 const uint8_t *__restrict__ mask, const double *__restrict__ x,
+                                                 i64 base, int width, int lane, i64 xrow0, double (&acc)[R])
 {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  constexpr int C = 64 * R;
+  constexpr int KC = 8 / R;
+  typedef typename Vec<R>::d dv;
+#pragma unroll
+  for (int q = 0; q < R; ++q) acc[q] = 0.0;
+  const double *vs = val + base;
+  unsigned m[R];
+#pragma unroll
+  for (int q = 0; q < R; ++q) m[q] = mask[lane * R + q];
+  const double *xr = x + xrow0;  // x of this lane's first row
+  for (int k0 = 0; k0 < width; k0 += KC)
+  {
+    dv a[KC];
+    int dk[KC];
+#pragma unroll
+    for (int k = 0; k < KC; ++k)
+    {
+      dk[k] = (k0 + k < width) ? delta[k0 + k] : 0;  // wave-uniform (scalar) loads
+      a[k] = (k0 + k < width) ? __builtin_nontemporal_load(reinterpret_cast<const dv *>(vs + (k0 + k) * C + lane * R))
+                              : (dv)(0.0);
+    }
+    double xv[KC][R];
+#pragma unroll
+    for (int k = 0; k < KC; ++k)
+#pragma unroll
+      for (int q = 0; q < R; ++q) xv[k][q] = ((m[q] >> (k0 + k)) & 1u) ? xr[q + dk[k]] : 0.0;
+#pragma unroll
+    for (int k = 0; k < KC; ++k)
+#pragma unroll
+      for (int q = 0; q < R; ++q)
+        if ((m[q] >> (k0 + k)) & 1u) acc[q] += lane_get<R>(a[k], q) * xv[k][q];
+  }
+}
+
+struct SellB1 {
+  const i64 *slice_ptr;
+  const double *val;
+  const i32 *col;
+  const i32 *st_width;  // null when the image has no stencil slices
+  const i32 *st_delta;
+  const uint8_t *st_mask;
+};
+
+// Image modes: every slice explicit, every slice stencil, or mixed (per-slice wave-uniform branch).
+enum { kExplicit = 0, kStencil = 1, kMixed = 2 };
+
+// Row sums of slice s for this lane's R rows.
+template <int R, int MODE>
+__device__ __forceinline__ void slice_dot(const SellB1 &A, i64 s, const double *__restrict__ x, i64 own, int lane,
+                                          double (&acc)[R])
+{
+  constexpr int C = 64 * R;
+  const i64 base = A.slice_ptr[s];
+  const int width = (int)((A.slice_ptr[s + 1] - base) / C);
+  const bool st = (MODE == kStencil) || (MODE == kMixed && A.st_width[s] > 0);
+  if (MODE != kExplicit && st)
+    rows_dot_stencil<R>(A.val, A.st_delta + 8 * s, A.st_mask + s * C, x, base, width, lane,
+                        own + s * C + (i64)lane * R, acc);
+  else
+    rows_dot<R>(A.val, A.col, x, base, width, lane, acc);
+}
+
+static SellB1 sell_b1(const eig_mat_s &A)
+{
+  return SellB1{A.slice_ptr, A.val, A.col, A.st_width, A.st_delta, A.st_mask};
+}
+
+static int image_mode(const eig_mat_s &A)
+{
+  if (A.n_stencil_slices == 0) return kExplicit;
+  return A.n_stencil_slices == A.nslices ? kStencil : kMixed;
+}
+
+// 8 waves per SIMD (8 workgroups per CU) except the mixed image, which carries both row paths.
+template <int MODE>
+constexpr int min_waves()
+{
+  return MODE == kMixed ? 1 : 8;
+}
+
+// y[own + r] = (A x)[r], 1x1 blocks (x: window base).
+template <int R, int MODE>
+__global__ __launch_bounds__(kStreamThreads, min_waves<MODE>()) void k_spmv_b1(i64 nrows, i64 own, SellB1 A,
+                                                               const i32 *__restrict__ slices, i64 first, i64 count,
+                                                               const double *__restrict__ x, double *__restrict__ y)
+{
+  constexpr int C = 64 * R;
+  // wave index through readfirstlane: the slice loop, slice_ptr loads and row bases stay scalar
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   i64 b, e;
   chunk_of(count, b, e);
   for (i64 it = b + wave; it < e; it += kWaves)
   {
     const i64 s = slices ? (i64)slices[first + it] : first + it;
-    const i64 base = slice_ptr[s];
-    const int width = (int)((slice_ptr[s + 1] - base) >> 6);
-    const double acc = row_dot_b1(val, col, x, base, width, lane);
-    const i64 r = s * 64 + lane;
-    if (r < nrows) y[r] = acc;
+    double acc[R];
+    slice_dot<R, MODE>(A, s, x, own, lane, acc);
+    const i64 r0 = s * C + (i64)lane * R;
+#pragma unroll
+    for (int q = 0; q < R; ++q)
+      if (r0 + q < nrows) y[own + r0 + q] = acc[q];
   }
 }
 
-// General br x bc blocks: lane = block row, per block br*bc values (column-major over lanes).
+// General br x bc blocks (C = 64): lane = block row, per block br*bc values column-major over lanes.
 template <int BR, int BC>
 __global__ __launch_bounds__(kStreamThreads) void k_spmv_blk(i64 nbrows, const i64 *__restrict__ slice_ptr,
                                                              const i32 *__restrict__ slices, i64 first, i64 count,
@@ -96,7 +229,8 @@ __global__ __launch_bounds__(kStreamThreads) void k_spmv_blk(i64 nbrows, const i
                                                              const double *__restrict__ x, double *__restrict__ y)
 {
   constexpr int BB = BR * BC;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // wave index through readfirstlane: the slice loop, slice_ptr loads and row bases stay scalar
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   i64 b, e;
   chunk_of(count, b, e);
   for (i64 it = b + wave; it < e; it += kWaves)
@@ -143,15 +277,18 @@ __global__ __launch_bounds__(kStreamThreads) void k_spmv_blk(i64 nbrows, const i
 // u, up, t are WINDOW buffers; owned rows at `own`.  `carry` (nullable) is a partial dot from a
 // previous launch of the same step (interior slices), added first by the last workgroup.
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kStreamThreads) void k_lanczos_spmv_b1(
-    i64 nrows, i64 own, const i64 *__restrict__ slice_ptr, const i32 *__restrict__ slices, i64 first, i64 count,
-    const double *__restrict__ val, const i32 *__restrict__ col, const double *__restrict__ u,
-    const double *__restrict__ up, double *__restrict__ t, int j, const double *__restrict__ nsum,
+template <int R, int MODE>
+__global__ __launch_bounds__(kStreamThreads, min_waves<MODE>()) void k_lanczos_spmv_b1(
+    i64 nrows, i64 own, SellB1 A, const i32 *__restrict__ slices, i64 first, i64 count,
+    const double *__restrict__ u, const double *__restrict__ up, double *__restrict__ t, int j,
+    const double *__restrict__ nsum,
     double *__restrict__ dot_out, double *__restrict__ beta_out, const double *__restrict__ carry,
     double *partials, unsigned *ticket)
 {
+  constexpr int C = 64 * R;
   __shared__ double tot[1];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // wave index through readfirstlane: the slice loop, slice_ptr loads and row bases stay scalar
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const double beta = sqrt(nsum[j]);
   const double sig = 1.0 / beta;
   const double gam = (j > 0) ? beta * (1.0 / sqrt(nsum[j - 1])) : 0.0;
@@ -161,16 +298,29 @@ __global__ __launch_bounds__(kStreamThreads) void k_lanczos_spmv_b1(
   for (i64 it = b + wave; it < e; it += kWaves)
   {
     const i64 s = slices ? (i64)slices[first + it] : first + it;
-    const i64 base = slice_ptr[s];
-    const int width = (int)((slice_ptr[s + 1] - base) >> 6);
-    const double acc = row_dot_b1(val, col, u, base, width, lane);
-    const i64 r = s * 64 + lane;
-    if (r < nrows)
+    const i64 r0 = s * C + (i64)lane * R;
+    // epilogue operands issued before the row loop so their latency hides under the matrix stream
+    double upv[R], uv[R];
+#pragma unroll
+    for (int q = 0; q < R; ++q)
     {
-      double ti = acc * sig;
-      if (j > 0) ti = ti - gam * up[own + r];
-      t[own + r] = ti;
-      d += ti * u[own + r];
+      const bool ok = r0 + q < nrows;
+      upv[q] = (ok && j > 0) ? up[own + r0 + q] : 0.0;
+      uv[q] = ok ? u[own + r0 + q] : 0.0;
+    }
+    double acc[R];
+    slice_dot<R, MODE>(A, s, u, own, lane, acc);
+#pragma unroll
+    for (int q = 0; q < R; ++q)
+    {
+      const i64 r = r0 + q;
+      if (r < nrows)
+      {
+        double ti = acc[q] * sig;
+        if (j > 0) ti = ti - gam * upv[q];
+        t[own + r] = ti;
+        d += ti * uv[q];
+      }
     }
   }
   double v[1] = {d};
@@ -184,27 +334,63 @@ __global__ __launch_bounds__(kStreamThreads) void k_lanczos_spmv_b1(
   }
 }
 
+// Grid = min(work, resident workgroups): every workgroup takes one contiguous chunk, so a grid
+// larger than what the CUs hold at once would leave a tail of late chunks.
+template <class K>
+static int grid_for_slices(K kernel, i64 count, int num_cu)
+{
+  static thread_local std::pair<const void *, int> cache{nullptr, 0};
+  int per_cu = 0;
+  if (cache.first == (const void *)kernel) per_cu = cache.second;
+  else
+  {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kStreamThreads, 0) != hipSuccess || per_cu < 1)
+      per_cu = 4;
+    cache = {(const void *)kernel, per_cu};
+  }
+  const i64 cap = (i64)per_cu * num_cu;
+  const i64 need = (count + kWaves - 1) / kWaves;
+  if (need < 1) return 1;
+  return (int)(need < cap ? need : cap);
+}
+
 void launch_spmv(const eig_mat_s &A, const double *x, double *y, const i32 *slices, i64 first, i64 count,
                  hipStream_t s)
 {
   if (count <= 0) return;
-  const i64 need = (count + kWaves - 1) / kWaves;
-  const int G = (int)(need < kStreamBlocks ? need : kStreamBlocks);
-  const double *xw = x;  // window-local columns index x directly
+  const int ncu = A.ctx->num_cu;
   double *yo = y + A.own_offset;
-#define EIG_BLK(R, C)                                                                                  \
-  if (A.br == R && A.bc == C)                                                                          \
-  {                                                                                                    \
-    hipLaunchKernelGGL((k_spmv_blk<R, C>), dim3(G), dim3(kStreamThreads), 0, s, A.nb_rows, A.slice_ptr, \
-                       slices, first, count, A.val, A.col, xw, yo);                                    \
-    return;                                                                                            \
+#define EIG_BLK(R_, C_)                                                                                 \
+  if (A.br == R_ && A.bc == C_)                                                                         \
+  {                                                                                                     \
+    const int G = grid_for_slices(k_spmv_blk<R_, C_>, count, ncu);                                      \
+    hipLaunchKernelGGL((k_spmv_blk<R_, C_>), dim3(G), dim3(kStreamThreads), 0, s, A.nb_rows, A.slice_ptr, \
+                       slices, first, count, A.val, A.col, x, yo);                                      \
+    return;                                                                                             \
+  }
+#define EIG_B1(R_, M_)                                                                                   \
+  {                                                                                                      \
+    const int G = grid_for_slices(k_spmv_b1<R_, M_>, count, ncu);                                        \
+    hipLaunchKernelGGL((k_spmv_b1<R_, M_>), dim3(G), dim3(kStreamThreads), 0, s, A.nb_rows, A.own_offset, \
+                       sell_b1(A), slices, first, count, x, y);                                          \
+  }
+#define EIG_B1M(R_)                                                                                      \
+  {                                                                                                      \
+    const int m_ = image_mode(A);                                                                        \
+    if (m_ == kExplicit) EIG_B1(R_, kExplicit)                                                           \
+    else if (m_ == kStencil) EIG_B1(R_, kStencil)                                                        \
+    else EIG_B1(R_, kMixed)                                                                              \
   }
   if (A.br == 1 && A.bc == 1)
   {
-    hipLaunchKernelGGL(k_spmv_b1, dim3(G), dim3(kStreamThreads), 0, s, A.nb_rows, A.slice_ptr, slices, first,
-                       count, A.val, A.col, xw, yo);
+    if (A.R == 1) EIG_B1M(1)
+    else if (A.R == 2) EIG_B1M(2)
+    else EIG_B1M(4)
     return;
   }
+#undef EIG_B1M
+#undef EIG_B1
+  EIG_CHECK(A.R == 1, EIG_ERR_ARG, "block matrices use 64-row slices");
   EIG_BLK(1, 2) EIG_BLK(1, 3) EIG_BLK(1, 4)
   EIG_BLK(2, 1) EIG_BLK(2, 2) EIG_BLK(2, 3) EIG_BLK(2, 4)
   EIG_BLK(3, 1) EIG_BLK(3, 2) EIG_BLK(3, 3) EIG_BLK(3, 4)
@@ -218,12 +404,23 @@ void launch_lanczos_spmv(const eig_mat_s &A, const double *u, const double *up, 
                          double *beta_out, const double *carry, int ticket, hipStream_t s, ReduceWS red)
 {
   EIG_CHECK(A.br == 1 && A.bc == 1, EIG_ERR_BLOCKSIZE, "Lanczos driver: 1x1 blocks only");
-  const i64 need = (count + kWaves - 1) / kWaves;
-  int G = (int)(need < kStreamBlocks ? need : kStreamBlocks);
-  if (G < 1) G = 1;
-  hipLaunchKernelGGL(k_lanczos_spmv_b1, dim3(G), dim3(kStreamThreads), 0, s, A.nb_rows, A.own_offset, A.slice_ptr,
-                     slices, first, count, A.val, A.col, u, up, t, j, st.nsum, dot_out, beta_out, carry,
-                     red.partials, red.tickets + ticket);
+#define EIG_LZ(R_, M_)                                                                                       \
+  hipLaunchKernelGGL((k_lanczos_spmv_b1<R_, M_>),                                                           \
+                     dim3(grid_for_slices(k_lanczos_spmv_b1<R_, M_>, count, A.ctx->num_cu)), dim3(kStreamThreads), \
+                     0, s, A.nb_rows, A.own_offset, sell_b1(A), slices, first, count, u, up, t, j, st.nsum, dot_out, \
+                     beta_out, carry, red.partials, red.tickets + ticket)
+#define EIG_LZM(R_)                                                                                          \
+  {                                                                                                          \
+    const int m_ = image_mode(A);                                                                            \
+    if (m_ == kExplicit) EIG_LZ(R_, kExplicit);                                                              \
+    else if (m_ == kStencil) EIG_LZ(R_, kStencil);                                                           \
+    else EIG_LZ(R_, kMixed);                                                                                 \
+  }
+  if (A.R == 1) EIG_LZM(1)
+  else if (A.R == 2) EIG_LZM(2)
+  else EIG_LZM(4)
+#undef EIG_LZM
+#undef EIG_LZ
 }
 
 }  // namespace eigmi

@@ -33,7 +33,8 @@ class _MatInfo(ctypes.Structure):
     _fields_ = [(k, ctypes.c_int64) for k in ("n", "n_global", "ncols", "row_begin", "window", "own_offset", "nnzb",
                                               "nnzb_padded", "nslices")] + \
                [("br", ctypes.c_int), ("bc", ctypes.c_int)] + \
-               [(k, ctypes.c_int64) for k in ("halo_recv", "halo_send", "device_bytes")]
+               [(k, ctypes.c_int64) for k in ("halo_recv", "halo_send", "device_bytes", "stencil_slices",
+                                              "rows_per_lane")]
 
 
 class Timing(ctypes.Structure):
