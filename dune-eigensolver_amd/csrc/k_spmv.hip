@@ -115,7 +115,8 @@ __device__ __forceinline__ void rows_dot(const double *__restrict__ val, const i
 template <int R>
 __device__ __forceinline__ void rows_dot_stencil(const double *__restrict__ val, const i32 *__restrict__ delta,
                                                  const uint8_t *__restrict__ mask, const double *__restrict__ x,
-                                                 i64 base, int width, int lane, i64 xrow0, double (&acc)[R])
+                                                 i64 base, int width, int lane, i64 xrow0, i64 xlast,
+                                                 double (&acc)[R])
 {
   constexpr int C = 64 * R;
   constexpr int KC = 8 / R;
@@ -126,7 +127,6 @@ __device__ __forceinline__ void rows_dot_stencil(const double *__restrict__ val,
   unsigned m[R];
 #pragma unroll
   for (int q = 0; q < R; ++q) m[q] = mask[lane * R + q];
-  const double *xr = x + xrow0;  // x of this lane's first row
   for (int k0 = 0; k0 < width; k0 += KC)
   {
     dv a[KC];
@@ -138,11 +138,18 @@ __device__ __forceinline__ void rows_dot_stencil(const double *__restrict__ val,
       a[k] = (k0 + k < width) ? __builtin_nontemporal_load(reinterpret_cast<const dv *>(vs + (k0 + k) * C + lane * R))
                               : (dv)(0.0);
     }
+    // gather addresses do not depend on the mask (clamped into the window instead), so the x loads
+    // issue together with the value loads; the mask only gates the accumulation below.
     double xv[KC][R];
 #pragma unroll
     for (int k = 0; k < KC; ++k)
 #pragma unroll
-      for (int q = 0; q < R; ++q) xv[k][q] = ((m[q] >> (k0 + k)) & 1u) ? xr[q + dk[k]] : 0.0;
+      for (int q = 0; q < R; ++q)
+      {
+        i64 g = xrow0 + q + dk[k];
+        g = g < 0 ? 0 : (g > xlast ? xlast : g);
+        xv[k][q] = x[g];
+      }
 #pragma unroll
     for (int k = 0; k < KC; ++k)
 #pragma unroll
@@ -158,6 +165,7 @@ struct SellB1 {
   const i32 *st_width;  // null when the image has no stencil slices
   const i32 *st_delta;
   const uint8_t *st_mask;
+  i64 xlast;  // window length - 1 (gather clamp)
 };
 
 // Image modes: every slice explicit, every slice stencil, or mixed (per-slice wave-uniform branch).
@@ -174,14 +182,14 @@ __device__ __forceinline__ void slice_dot(const SellB1 &A, i64 s, const double *
   const bool st = (MODE == kStencil) || (MODE == kMixed && A.st_width[s] > 0);
   if (MODE != kExplicit && st)
     rows_dot_stencil<R>(A.val, A.st_delta + 8 * s, A.st_mask + s * C, x, base, width, lane,
-                        own + s * C + (i64)lane * R, acc);
+                        own + s * C + (i64)lane * R, A.xlast, acc);
   else
     rows_dot<R>(A.val, A.col, x, base, width, lane, acc);
 }
 
 static SellB1 sell_b1(const eig_mat_s &A)
 {
-  return SellB1{A.slice_ptr, A.val, A.col, A.st_width, A.st_delta, A.st_mask};
+  return SellB1{A.slice_ptr, A.val, A.col, A.st_width, A.st_delta, A.st_mask, A.window - 1};
 }
 
 static int image_mode(const eig_mat_s &A)
@@ -334,6 +342,125 @@ __global__ __launch_bounds__(kStreamThreads, min_waves<MODE>()) void k_lanczos_s
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Software-pipelined Lanczos kernel 1 for all-stencil images, one row per lane (R = 1).  Per
+// slice iteration the wave issues, in this order: (1) the x gathers of the current slice (their
+// addresses need only the scalar offsets), (2) the value / mask / epilogue loads of the NEXT
+// slice, (3) the arithmetic of the current slice, which waits only for (1) -- vmcnt retires in
+// issue order, so (2) stays in flight behind the computation.  Same per-row arithmetic and
+// order as k_lanczos_spmv_b1 (bitwise identical results).
+// ---------------------------------------------------------------------------------------------
+struct StSlice {
+  double a[8];
+  unsigned m;
+  double upv, uv;
+};
+
+__device__ __forceinline__ void st_load(const SellB1 &A, i64 s, int w, int lane, i64 own, i64 nrows, int j,
+                                        const double *__restrict__ u, const double *__restrict__ up, StSlice &L)
+{
+  const double *vs = A.val + A.slice_ptr[s];  // wave-uniform base, 32-bit lane offsets
+#pragma unroll
+  for (int k = 0; k < 8; ++k) L.a[k] = (k < w) ? __builtin_nontemporal_load(vs + (k * 64 + lane)) : 0.0;
+  L.m = A.st_mask[s * 64 + lane];
+  const i64 r = s * 64 + lane;
+  const bool ok = r < nrows;
+  L.upv = (ok && j > 0) ? up[own + r] : 0.0;
+  L.uv = ok ? u[own + r] : 0.0;
+}
+
+template <int MINW>
+__global__ __launch_bounds__(kStreamThreads, MINW) void k_lanczos_spmv_st1_pipe(
+    i64 nrows, i64 own, SellB1 A, const i32 *__restrict__ slices, i64 first, i64 count,
+    const double *__restrict__ u, const double *__restrict__ up, double *__restrict__ t, int j,
+    const double *__restrict__ nsum, double *__restrict__ dot_out, double *__restrict__ beta_out,
+    const double *__restrict__ carry, double *partials, unsigned *ticket)
+{
+  __shared__ double tot[1];
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const double beta = sqrt(nsum[j]);
+  const double sig = 1.0 / beta;
+  const double gam = (j > 0) ? beta * (1.0 / sqrt(nsum[j - 1])) : 0.0;
+  i64 b, e;
+  chunk_of(count, b, e);
+  double d = 0.0;
+  i64 it = b + wave;
+  StSlice cur;
+  i64 s = 0;
+  int w = 0;
+  if (it < e)
+  {
+    s = slices ? (i64)slices[first + it] : first + it;
+    w = A.st_width[s];
+    st_load(A, s, w, lane, own, nrows, j, u, up, cur);
+  }
+  for (; it < e; it += kWaves)
+  {
+    // (1) gathers of the current slice (32-bit window offsets: the window is < 2^31 entries)
+    const i32 *dl = A.st_delta + 8 * s;
+    const int xr = (int)(own + s * 64) + lane;
+    const int xl = (int)A.xlast;
+    double xv[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+    {
+      if (k < w)
+      {
+        int g = xr + dl[k];
+        g = g < 0 ? 0 : (g > xl ? xl : g);
+        xv[k] = u[g];
+      }
+      else
+        xv[k] = 0.0;
+    }
+    // (2) next slice's streams
+    const i64 itn = it + kWaves;
+    StSlice nxt;
+    i64 sn = s;
+    int wn = 0;
+    if (itn < e)
+    {
+      sn = slices ? (i64)slices[first + itn] : first + itn;
+      wn = A.st_width[sn];
+      st_load(A, sn, wn, lane, own, nrows, j, u, up, nxt);
+    }
+    // (3) current slice arithmetic (ascending offsets = ascending columns)
+    double acc = 0.0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (k < w && ((cur.m >> k) & 1u)) acc += cur.a[k] * xv[k];
+    const i64 r = s * 64 + lane;
+    if (r < nrows)
+    {
+      double ti = acc * sig;
+      if (j > 0) ti = ti - gam * cur.upv;
+      t[own + r] = ti;
+      d += ti * cur.uv;
+    }
+    cur = nxt;
+    s = sn;
+    w = wn;
+  }
+  double v[1] = {d};
+  if (grid_sum<1, kStreamThreads>(v, partials, ticket, tot))
+  {
+    if (threadIdx.x == 0)
+    {
+      dot_out[0] = carry ? (carry[0] + tot[0]) : tot[0];
+      if (beta_out) beta_out[0] = beta;
+    }
+  }
+}
+
+// EIGMI_K1_PIPE: 0 = plain kernel (default: measured equal to 1 and faster than 2, see
+// tools/spmv_sweep.py), 1 = pipelined at 7 waves / SIMD, 2 = pipelined at 8 (spills)
+static int k1_pipe_mode()
+{
+  const char *e = std::getenv("EIGMI_K1_PIPE");
+  if (!e) return 0;
+  return e[0] == '0' ? 0 : (e[0] == '2' ? 2 : 1);
+}
+
 // Grid = min(work, resident workgroups): every workgroup takes one contiguous chunk, so a grid
 // larger than what the CUs hold at once would leave a tail of late chunks.
 template <class K>
@@ -416,11 +543,20 @@ void launch_lanczos_spmv(const eig_mat_s &A, const double *u, const double *up, 
     else if (m_ == kStencil) EIG_LZ(R_, kStencil);                                                           \
     else EIG_LZ(R_, kMixed);                                                                                 \
   }
-  if (A.R == 1) EIG_LZM(1)
+  const int pm = k1_pipe_mode();
+#define EIG_PIPE(W_)                                                                                            \
+  hipLaunchKernelGGL(k_lanczos_spmv_st1_pipe<W_>,                                                              \
+                     dim3(grid_for_slices(k_lanczos_spmv_st1_pipe<W_>, count, A.ctx->num_cu)), dim3(kStreamThreads), \
+                     0, s, A.nb_rows, A.own_offset, sell_b1(A), slices, first, count, u, up, t, j, st.nsum, dot_out, \
+                     beta_out, carry, red.partials, red.tickets + ticket)
+  if (A.R == 1 && image_mode(A) == kStencil && pm == 1) EIG_PIPE(7);
+  else if (A.R == 1 && image_mode(A) == kStencil && pm == 2) EIG_PIPE(8);
+  else if (A.R == 1) EIG_LZM(1)
   else if (A.R == 2) EIG_LZM(2)
   else EIG_LZM(4)
 #undef EIG_LZM
 #undef EIG_LZ
+#undef EIG_PIPE
 }
 
 }  // namespace eigmi

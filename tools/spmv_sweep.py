@@ -30,15 +30,19 @@ def main():
     rp, c, v = eigmi.gen_matrix(eigmi.GEN_POISSON3D, N)
     nnz = int(rp[-1])
     mats = {}
-    for var in args.variants.split(","):  # "<R>[s|e]": rows per lane, stencil slices on / off
-        os.environ["EIGMI_SELL_R"] = var[0]
-        os.environ["EIGMI_STENCIL"] = "0" if var.endswith("e") else "1"
+    pipe = {}
+    for var in args.variants.split(","):  # "<R><s|e>[:p<0|1|2>]": rows per lane, stencil on/off, K1 kernel
+        img, _, pm = var.partition(":")
+        os.environ["EIGMI_SELL_R"] = img[0]
+        os.environ["EIGMI_STENCIL"] = "0" if img.endswith("e") else "1"
         mats[var] = eigmi.Matrix.from_bcsr(ctx, rp, c, v)
+        pipe[var] = pm[1:] if pm else "0"
     x = ctx.array(np.random.default_rng(0).standard_normal(n))
     y = ctx.zeros(n)
     res = {R: {"k1_us": [], "k2_us": [], "step_us": [], "mv_us": []} for R in mats}
     for _ in range(args.rounds):
         for R, M in mats.items():
+            os.environ["EIGMI_K1_PIPE"] = pipe[R]
             ws = eigmi.LanczosWorkspace(M, args.steps + 2, seed=123)
             ws.step(2)
             t = ws.step(args.steps, timed=True)
