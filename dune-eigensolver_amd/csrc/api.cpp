@@ -188,8 +188,8 @@ extern "C" int eig_ctx_create(int device, eig_ctx_t *out)
       EIG_HIP(hipGetDeviceProperties(&prop, device));
       ctx->num_cu = prop.multiProcessorCount;
       ctx->red.partials = dev_alloc<double>((size_t)kMaxRedBlocks * kMaxRedVals);
-      ctx->red.tickets = dev_alloc<unsigned>(kNumTickets);
-      EIG_HIP(hipMemset(ctx->red.tickets, 0, kNumTickets * sizeof(unsigned)));
+      ctx->red.tickets = dev_alloc<unsigned>((size_t)kNumTickets * kTicketStride);
+      EIG_HIP(hipMemset(ctx->red.tickets, 0, (size_t)kNumTickets * kTicketStride * sizeof(unsigned)));
       ctx->scratch = dev_alloc<double>(4096);
       EIG_HIP(hipMemset(ctx->scratch, 0, 4096 * sizeof(double)));
     }
@@ -753,6 +753,27 @@ extern "C" int eig_mv(eig_mat_t A, const double *x, double *y)
     EIG_CHECK(A && x && y, EIG_ERR_ARG, "eig_mv: null argument");
     DeviceGuard dg(A->ctx->device);
     mv_device(*A, const_cast<double *>(x), y);
+  });
+}
+
+extern "C" int eig_mv_timed(eig_mat_t A, const double *x, double *y, int reps, double *avg_ms)
+{
+  return guard(A ? A->ctx : nullptr, [&] {
+    EIG_CHECK(A && x && y && avg_ms && reps > 0, EIG_ERR_ARG, "eig_mv_timed: bad argument");
+    DeviceGuard dg(A->ctx->device);
+    hipStream_t s = A->ctx->stream;
+    hipEvent_t e0, e1;
+    EIG_HIP(hipEventCreate(&e0));
+    EIG_HIP(hipEventCreate(&e1));
+    EIG_HIP(hipEventRecord(e0, s));
+    for (int r = 0; r < reps; ++r) mv_device(*A, const_cast<double *>(x), y);
+    EIG_HIP(hipEventRecord(e1, s));
+    EIG_HIP(hipEventSynchronize(e1));
+    float ms = 0.f;
+    EIG_HIP(hipEventElapsedTime(&ms, e0, e1));
+    *avg_ms = ms / reps;
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
   });
 }
 

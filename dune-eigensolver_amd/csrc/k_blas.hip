@@ -68,7 +68,7 @@ void launch_lanczos_update(i64 n, const double *u, double *t, int j, const Lancz
 {
   EIG_CHECK((((uintptr_t)u | (uintptr_t)t) & 15) == 0, EIG_ERR_ARG, "lanczos update: vectors must be 16-B aligned");
   hipLaunchKernelGGL(k_lanczos_update, dim3(stream_grid(n)), dim3(kStreamThreads), 0, s, n, u, t, j, st.dsum,
-                     st.nsum, st.alpha + j, st.nsum + j + 1, red.partials, red.tickets + ticket);
+                     st.nsum, st.alpha + j, st.nsum + j + 1, red.partials, red.ticket(ticket));
 }
 
 // beta[j] = sqrt(nsum[j]) (records the final beta of a run).
@@ -104,12 +104,12 @@ __global__ __launch_bounds__(kStreamThreads) void k_dot(i64 n, const double *__r
 void launch_dot(i64 n, const double *x, const double *y, double *out, int ticket, hipStream_t s, ReduceWS red)
 {
   hipLaunchKernelGGL(k_dot<false>, dim3(stream_grid(n, 4)), dim3(kStreamThreads), 0, s, n, x, y, out, red.partials,
-                     red.tickets + ticket);
+                     red.ticket(ticket));
 }
 void launch_nrm2sq(i64 n, const double *x, double *out, int ticket, hipStream_t s, ReduceWS red)
 {
   hipLaunchKernelGGL(k_dot<true>, dim3(stream_grid(n, 4)), dim3(kStreamThreads), 0, s, n, x, x, out, red.partials,
-                     red.tickets + ticket);
+                     red.ticket(ticket));
 }
 
 // y += a x   (a from the host, or a = scale * (*a_dev) from device memory)
@@ -210,7 +210,7 @@ __global__ __launch_bounds__(kStreamThreads) void k_gemv_t(i64 n, int k, const d
     for (int q = 0; q < 8; ++q)
       if (c0 + q < k) acc[q] += V[(i64)(c0 + q) * ldv + i] * wi;
   }
-  if (grid_sum_n<8, kStreamThreads>(acc, partials + (size_t)blockIdx.y * gridDim.x * 8, tickets + blockIdx.y, tot,
+  if (grid_sum_n<8, kStreamThreads>(acc, partials + (size_t)blockIdx.y * gridDim.x * 8, tickets + (size_t)blockIdx.y * kTicketStride, tot,
                                     blockIdx.x, gridDim.x))
   {
     if (threadIdx.x < 8 && c0 + (int)threadIdx.x < k) c[c0 + threadIdx.x] = tot[threadIdx.x];
@@ -226,7 +226,7 @@ void launch_gemv_t(i64 n, int k, const double *V, i64 ldv, const double *w, doub
   if (G > kGemvBlocks) G = kGemvBlocks;
   EIG_CHECK((i64)G * tiles * 8 <= (i64)kMaxRedBlocks * kMaxRedVals, EIG_ERR_ARG, "gemv_t: partials overflow");
   hipLaunchKernelGGL(k_gemv_t, dim3(G, tiles), dim3(kStreamThreads), 0, s, n, k, V, ldv, w, c, red.partials,
-                     red.tickets + ticket);
+                     red.ticket(ticket));
 }
 
 __global__ __launch_bounds__(kStreamThreads) void k_gemv_n(i64 n, int k, const double *__restrict__ V, i64 ldv,
@@ -284,7 +284,7 @@ void launch_resid_sq(i64 n, const double *x, const double *y, double theta, doub
                      ReduceWS red)
 {
   hipLaunchKernelGGL(k_resid_sq, dim3(stream_grid(n, 4)), dim3(kStreamThreads), 0, s, n, x, y, theta, out,
-                     red.partials, red.tickets + ticket);
+                     red.partials, red.ticket(ticket));
 }
 
 }  // namespace eigmi

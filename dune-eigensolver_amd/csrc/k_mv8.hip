@@ -70,11 +70,104 @@ __global__ __launch_bounds__(256) void k_spmm_mv8(i64 nrows, i64 nslices, const 
   }
 }
 
+// Row-per-lane SpMM for 64-row slices (R = 1): lane l computes all 8 columns of row 64 s + l for
+// MB column blocks; the slice's value / column (or offset + mask) streams are read once per MB
+// column blocks, coalesced; each gathered Qin row is four 16-B loads.  Per column j the row sum
+// runs over the stored entries in ascending-column order from 0.0 (bitwise the reference).
+template <int MB, bool STENCIL>
+__global__ __launch_bounds__(256) void k_spmm_mv8_rows(i64 nrows, i64 nslices, const i64 *__restrict__ slice_ptr,
+                                                       const double *__restrict__ val, const i32 *__restrict__ col,
+                                                       const i32 *__restrict__ st_delta,
+                                                       const uint8_t *__restrict__ st_mask,
+                                                       const double *__restrict__ Qin, double *__restrict__ Qout,
+                                                       i64 n, int b0, int nb)
+{
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const i64 per = (nslices + gridDim.x - 1) / gridDim.x;
+  const i64 sb = (i64)blockIdx.x * per, se = sb + per < nslices ? sb + per : nslices;
+  for (i64 s = sb + wave; s < se; s += 4)
+  {
+    const i64 base = slice_ptr[s];
+    const int width = (int)((slice_ptr[s + 1] - base) >> 6);
+    const i64 r = s * 64 + lane;
+    unsigned m = 0;
+    if (STENCIL) m = st_mask[s * 64 + lane];
+    double acc[MB][8];
+#pragma unroll
+    for (int q = 0; q < MB; ++q)
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) acc[q][jj] = 0.0;
+    for (int k = 0; k < width; ++k)
+    {
+      const double a = __builtin_nontemporal_load(val + base + k * 64 + lane);
+      i64 c;
+      bool ok;
+      if (STENCIL)
+      {
+        ok = (m >> k) & 1u;
+        c = r + st_delta[8 * s + k];
+      }
+      else
+      {
+        const i32 cc = __builtin_nontemporal_load(col + base + k * 64 + lane);
+        ok = cc >= 0;
+        c = cc;
+      }
+      if (!ok) continue;
+#pragma unroll
+      for (int q = 0; q < MB; ++q)
+      {
+        if (q < nb)
+        {
+          const double2 *xr = reinterpret_cast<const double2 *>(Qin + ((i64)(b0 + q) * n + c) * 8);
+#pragma unroll
+          for (int h = 0; h < 4; ++h)
+          {
+            const double2 xv = xr[h];
+            acc[q][2 * h] += a * xv.x;
+            acc[q][2 * h + 1] += a * xv.y;
+          }
+        }
+      }
+    }
+    if (r < nrows)
+    {
+#pragma unroll
+      for (int q = 0; q < MB; ++q)
+        if (q < nb)
+        {
+          double2 *yr = reinterpret_cast<double2 *>(Qout + ((i64)(b0 + q) * n + r) * 8);
+#pragma unroll
+          for (int h = 0; h < 4; ++h) yr[h] = make_double2(acc[q][2 * h], acc[q][2 * h + 1]);
+        }
+    }
+  }
+}
+
 void launch_spmm_mv8(const eig_mat_s &A, i64 m, const double *Qin, double *Qout, hipStream_t s)
 {
   EIG_CHECK(A.br == 1 && A.bc == 1, EIG_ERR_BLOCKSIZE,
             "matmul_sparse_tallskinny_blocked: only implemented for FieldMatrix<..,1,1>");
   const int nblk = (int)(m / 8);
+  if (A.R == 1)
+  {
+    // stencil offsets are global col - global row; on one rank the window starts at 0, so
+    // window-local column = r + delta.  Mixed images use the explicit columns (always present).
+    const bool st = A.n_stencil_slices == A.nslices && A.n_stencil_slices > 0 && A.own_offset == 0;
+    constexpr int MB = 2;
+    const int gx = grid_for(A.nslices, 4, kStreamBlocks);
+    for (int b0 = 0; b0 < nblk; b0 += MB)
+    {
+      const int nb = nblk - b0 < MB ? nblk - b0 : MB;
+      if (st)
+        hipLaunchKernelGGL((k_spmm_mv8_rows<MB, true>), dim3(gx), dim3(256), 0, s, A.nb_rows, A.nslices, A.slice_ptr,
+                           A.val, A.col, A.st_delta, A.st_mask, Qin, Qout, A.nb_rows, b0, nb);
+      else
+        hipLaunchKernelGGL((k_spmm_mv8_rows<MB, false>), dim3(gx), dim3(256), 0, s, A.nb_rows, A.nslices,
+                           A.slice_ptr, A.val, A.col, A.st_delta, A.st_mask, Qin, Qout, A.nb_rows, b0, nb);
+    }
+    return;
+  }
   const int MB = 4;
   const int gy = (nblk + MB - 1) / MB;
   const int gx = grid_for(A.nslices * A.R, 1, kStreamBlocks);
@@ -111,7 +204,7 @@ __global__ __launch_bounds__(kStreamThreads) void k_dot_diag_mv8(i64 n, const do
     v[2 * q] = (q == cp) ? sx : 0.0;
     v[2 * q + 1] = (q == cp) ? sy : 0.0;
   }
-  if (grid_sum_n<8, kStreamThreads>(v, partials + (size_t)blockIdx.y * gridDim.x * 8, tickets + blockIdx.y, tot,
+  if (grid_sum_n<8, kStreamThreads>(v, partials + (size_t)blockIdx.y * gridDim.x * 8, tickets + (size_t)blockIdx.y * kTicketStride, tot,
                                     blockIdx.x, gridDim.x))
   {
     if (threadIdx.x < 8) dp[blockIdx.y * 8 + threadIdx.x] = tot[threadIdx.x];
@@ -126,7 +219,7 @@ void launch_dot_diag_mv8(i64 n, i64 m, const double *Q1, const double *Q2, doubl
   int G = grid_for(n * 4, (i64)kStreamThreads * 4, 1024);
   while ((i64)G * nb * 8 > (i64)kMaxRedBlocks * kMaxRedVals) G /= 2;
   hipLaunchKernelGGL(k_dot_diag_mv8, dim3(G, nb), dim3(kStreamThreads), 0, s, n, Q1, Q2, dp, red.partials,
-                     red.tickets + ticket);
+                     red.ticket(ticket));
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -177,17 +270,23 @@ __global__ __launch_bounds__(kGramThreads) void k_gram_mv8(i64 n, i64 m1, i64 m2
   __syncthreads();
   if (t == 0)
   {
-    unsigned prev = __hip_atomic_fetch_add(tickets + blockIdx.y, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = (prev == gridDim.x - 1) ? 1u : 0u;
+    s_last = ticket_arrive(tickets + (size_t)blockIdx.y * kTicketStride, blockIdx.x, gridDim.x) ? 1u : 0u;
   }
   __syncthreads();
   if (!s_last) return;
   double tot = 0.0;
-  for (unsigned b = 0; b < gridDim.x; ++b) tot += ld_sc1(&part[(size_t)b * 256 + t]);
+  for (unsigned b0 = 0; b0 < gridDim.x; b0 += 16)
+  {
+    double v[16];  // 16 independent sc1 loads in flight, then the adds in block order
+#pragma unroll
+    for (int u = 0; u < 16; ++u) v[u] = (b0 + u < gridDim.x) ? ld_sc1(&part[(size_t)(b0 + u) * 256 + t]) : 0.0;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) tot += v[u];
+  }
   const int row = t >> 4, cl = t & 15;
   const i64 gi = (i64)ti * 16 + row, gj = (i64)tj * 16 + cl;
   if (gi < m1 && gj < m2) G[gi * m2 + gj] = tot;
-  if (t == 0) __hip_atomic_store(tickets + blockIdx.y, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (t == 0) ticket_reset(tickets + (size_t)blockIdx.y * kTicketStride);
 }
 
 void launch_gram_mv8(i64 n, i64 m1, i64 m2, const double *Q1, const double *Q2, double *G, int ticket,
@@ -199,7 +298,7 @@ void launch_gram_mv8(i64 n, i64 m1, i64 m2, const double *Q1, const double *Q2, 
   int gx = grid_for((n + 3) / 4, 4 * 8, 256);
   while ((i64)gx * tiles * 256 > (i64)kMaxRedBlocks * kMaxRedVals && gx > 1) gx /= 2;
   hipLaunchKernelGGL(k_gram_mv8, dim3(gx, tiles), dim3(kGramThreads), 0, s, n, m1, m2, Q1, Q2, G, tiles_j,
-                     red.partials, red.tickets + ticket);
+                     red.partials, red.ticket(ticket));
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -268,7 +367,7 @@ void launch_mgs_pass(i64 n, double *Qb, int k, double *Ssum, int ticket, hipStre
 {
   const int G = grid_for(n, kStreamThreads * 4, 1024);
   hipLaunchKernelGGL(k_mgs_pass, dim3(G), dim3(kStreamThreads), 0, s, n, Qb, k, Ssum, red.partials,
-                     red.tickets + ticket);
+                     red.ticket(ticket));
 }
 
 // ---------------------------------------------------------------------------------------------

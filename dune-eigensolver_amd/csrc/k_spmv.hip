@@ -535,7 +535,7 @@ void launch_lanczos_spmv(const eig_mat_s &A, const double *u, const double *up, 
   hipLaunchKernelGGL((k_lanczos_spmv_b1<R_, M_>),                                                           \
                      dim3(grid_for_slices(k_lanczos_spmv_b1<R_, M_>, count, A.ctx->num_cu)), dim3(kStreamThreads), \
                      0, s, A.nb_rows, A.own_offset, sell_b1(A), slices, first, count, u, up, t, j, st.nsum, dot_out, \
-                     beta_out, carry, red.partials, red.tickets + ticket)
+                     beta_out, carry, red.partials, red.ticket(ticket))
 #define EIG_LZM(R_)                                                                                          \
   {                                                                                                          \
     const int m_ = image_mode(A);                                                                            \
@@ -548,7 +548,7 @@ void launch_lanczos_spmv(const eig_mat_s &A, const double *u, const double *up, 
   hipLaunchKernelGGL(k_lanczos_spmv_st1_pipe<W_>,                                                              \
                      dim3(grid_for_slices(k_lanczos_spmv_st1_pipe<W_>, count, A.ctx->num_cu)), dim3(kStreamThreads), \
                      0, s, A.nb_rows, A.own_offset, sell_b1(A), slices, first, count, u, up, t, j, st.nsum, dot_out, \
-                     beta_out, carry, red.partials, red.tickets + ticket)
+                     beta_out, carry, red.partials, red.ticket(ticket))
   if (A.R == 1 && image_mode(A) == kStencil && pm == 1) EIG_PIPE(7);
   else if (A.R == 1 && image_mode(A) == kStencil && pm == 2) EIG_PIPE(8);
   else if (A.R == 1) EIG_LZM(1)

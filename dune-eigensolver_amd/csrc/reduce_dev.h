@@ -31,6 +31,27 @@ __device__ __forceinline__ double ld_sc1(const double *p)
   return __longlong_as_double((long long)b);
 }
 
+// Sharded arrival ticket (internal.h kTicketStride): workgroup bid adds to shard bid % 8; the
+// workgroup that completes a shard adds to the top counter; the one that completes the top is
+// the last of all.  Called by ONE lane after the workgroup's partial stores have drained.
+// Returns true for exactly one workgroup of the launch.
+__device__ __forceinline__ bool ticket_arrive(unsigned *t, unsigned bid, unsigned nblk)
+{
+  constexpr unsigned L = 32;  // words per 128-B line
+  const unsigned shard = bid & 7u;
+  const unsigned shard_n = nblk / 8u + ((shard < nblk % 8u) ? 1u : 0u);
+  const unsigned nshards = nblk < 8u ? nblk : 8u;
+  const unsigned prev = __hip_atomic_fetch_add(t + shard * L, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (prev != shard_n - 1u) return false;
+  const unsigned top = __hip_atomic_fetch_add(t + 8u * L, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return top == nshards - 1u;
+}
+
+__device__ __forceinline__ void ticket_reset(unsigned *t)
+{
+  for (unsigned i = 0; i < 9u; ++i) __hip_atomic_store(t + i * 32u, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Block-wide sum of NV values per thread, in a fixed order.  Result valid in thread 0's out[].
 template <int NV, int NT>
 __device__ __forceinline__ void block_sum(double (&v)[NV], double (&out)[NV])
@@ -85,21 +106,30 @@ __device__ bool grid_sum_n(double (&v)[NV], double *partials, unsigned *ticket, 
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0)
-  {
-    unsigned prev = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = (prev == nblk - 1) ? 1u : 0u;
-  }
+  if (threadIdx.x == 0) s_last = ticket_arrive(ticket, bid, nblk) ? 1u : 0u;
   __syncthreads();
   if (!s_last) return false;
-  // Last workgroup: thread t sums partials t, t+NT, ... then a fixed-order block tree.
+  // Last workgroup: thread t sums partials t, t+NT, ... then a fixed-order block tree.  The loads
+  // of a round are issued together (independent sc1 loads) before any add, so the tail pays about
+  // one memory latency per 8 partials per thread instead of one per partial.
   double acc[NV];
 #pragma unroll
   for (int i = 0; i < NV; ++i) acc[i] = 0.0;
-  for (unsigned b = threadIdx.x; b < nblk; b += NT)
+  constexpr int U = NV <= 2 ? 8 : 2;
+  for (unsigned b0 = threadIdx.x; b0 < nblk; b0 += NT * U)
   {
+    double vals[U][NV];
 #pragma unroll
-    for (int i = 0; i < NV; ++i) acc[i] += ld_sc1(&partials[(size_t)b * NV + i]);
+    for (int u = 0; u < U; ++u)
+    {
+      const unsigned b = b0 + (unsigned)u * NT;
+#pragma unroll
+      for (int i = 0; i < NV; ++i) vals[u][i] = (b < nblk) ? ld_sc1(&partials[(size_t)b * NV + i]) : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int i = 0; i < NV; ++i) acc[i] += vals[u][i];
   }
   double r[NV];
   block_sum<NV, NT>(acc, r);
@@ -107,7 +137,7 @@ __device__ bool grid_sum_n(double (&v)[NV], double *partials, unsigned *ticket, 
   {
 #pragma unroll
     for (int i = 0; i < NV; ++i) tot[i] = r[i];
-    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    ticket_reset(ticket);
   }
   __syncthreads();
   return true;

@@ -77,6 +77,7 @@ SIGNATURES = {
     "eig_mat_shift_diag": (_int, [_vp, _dbl]),
     "eig_mv": (_int, [_vp, _vp, _vp]),
     "eig_mv_host": (_int, [_vp, _vp, _vp]),
+    "eig_mv_timed": (_int, [_vp, _vp, _vp, _int, ctypes.POINTER(_dbl)]),
     "eig_dot": (_int, [_vp, _i64, _vp, _vp, _vp]),
     "eig_nrm2": (_int, [_vp, _i64, _vp, _vp]),
     "eig_axpy": (_int, [_vp, _i64, _dbl, _vp, _vp]),
@@ -291,6 +292,12 @@ class Matrix:
 
     def mv(self, x, y):
         self.ctx.check(lib.eig_mv(self.h, x.ptr, y.ptr))
+
+    def mv_timed(self, x, y, reps):
+        """Average device time (ms) of `reps` back-to-back y = A x launches (HIP events)."""
+        ms = _dbl(0.0)
+        self.ctx.check(lib.eig_mv_timed(self.h, x.ptr, y.ptr, reps, ctypes.byref(ms)))
+        return ms.value
 
     def mv_host(self, x):
         x = np.ascontiguousarray(x, np.float64)

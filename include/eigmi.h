@@ -128,6 +128,9 @@ int eig_mat_shift_diag(eig_mat_t mat, double shift);
 int eig_mv(eig_mat_t mat, const double *x, double *y);
 /* Same with caller-owned HOST arrays of length n (ARPACK's workd): stage, multiply, copy back. */
 int eig_mv_host(eig_mat_t mat, const double *x_host, double *y_host);
+/* Measurement helper: `reps` back-to-back eig_mv launches bracketed by HIP events on the
+ * context stream; *avg_ms = elapsed / reps (synchronous). */
+int eig_mv_timed(eig_mat_t mat, const double *x, double *y, int reps, double *avg_ms);
 
 /* ---------------------------------------------------------------- BlockVector ops ---------- */
 /* n = owned length; pointers address the owned slice.  Results to device memory. */

@@ -1,0 +1,138 @@
+#!/usr/bin/env python3
+"""Per-configuration measurements beside bench.py's headline line (BASELINE.json configs):
+
+  C1  2-D Poisson 64x64: StandardLargest (ini defaults) and the Lanczos solver on the GPU, the
+      oracle (reference CPU path) timed on the same inputs
+  C2  3-D Poisson 128^3: SpMV (cache-resident: 217 MB < 256 MB MALL), Lanczos step, the b = 8
+      SpMM, block Gram-Schmidt (m = 8, 32) and one StandardLargest iteration vs the CPU path
+  C3  3-D Q1 elasticity 64^3, 3x3 blocks: BCSR SpMV against 76 nnzb + 4 (nb+1) + 48 nb bytes
+
+One JSON line per measurement; algorithmic bytes per SURVEY 8(d); peak 8 TB/s.
+"""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "dune-eigensolver_amd"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+import numpy as np  # noqa: E402
+
+import eigmi  # noqa: E402
+import oracle  # noqa: E402  (CPU baseline only)
+
+PEAK = 8000.0
+
+
+def emit(**kw):
+    print(json.dumps(kw), flush=True)
+
+
+def wall(f, reps=1):
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        r = f()
+    return (time.perf_counter() - t0) / reps, r
+
+
+def c1(ctx):
+    A = oracle.laplace2d(64)
+    M = eigmi.Matrix.from_bcsr(ctx, A.rowptr, A.col, A.val)
+    eigmi.standard_largest(M, 0.0, 2e-3, 4000, 4, 123, want_evec=False)  # warm-up
+    tg, (ev, _, it) = wall(lambda: eigmi.standard_largest(M, 0.0, 2e-3, 4000, 4, 123, want_evec=False), 3)
+    tc, (rev, _, rit) = wall(lambda: oracle.standard_largest(A, 0.0, 2e-3, 4000, 4, 123), 3)
+    emit(config="C1 2D Poisson 64^2", op="StandardLargest nev=4 tol=2e-3 seed=123", gpu_s=round(tg, 5),
+         cpu_s=round(tc, 5), iterations=it, cpu_iterations=rit, ritz0=ev[0], max_abs_diff_vs_cpu=float(np.abs(ev - rev).max()))
+    tl, (ev, _, res) = wall(lambda: eigmi.lanczos_solve(M, 4, 300, eigmi.WHICH_LA, want_evec=False))
+    emit(config="C1 2D Poisson 64^2", op="Lanczos solve LA nev=4 ncv=300 (full re-orth)", gpu_s=round(tl, 5),
+         eigenvalues=list(ev), max_residual=float(res.max()))
+
+
+def c2(ctx):
+    N = 128
+    n = N ** 3
+    rp, c, v = eigmi.gen_matrix(eigmi.GEN_POISSON3D, N)
+    nnz = int(rp[-1])
+    M = eigmi.Matrix.from_bcsr(ctx, rp, c, v)
+    x = ctx.array(np.random.default_rng(0).standard_normal(n))
+    y = ctx.zeros(n)
+    M.mv_timed(x, y, 10)
+    ms = M.mv_timed(x, y, 200)
+    b = eigmi.bytes_spmv(n, nnz)
+    gbs = b / (ms * 1e-3) / 1e9
+    A = oracle.CSR(n, rp, c, v)
+    xh = x.get()
+    tc, _ = wall(lambda: oracle.csr_mv(A, xh), 3)
+    emit(config="C2 3D Poisson 128^3", op="SpMV (cache-resident: 217 MB < 256 MB MALL)", us=round(ms * 1e3, 2),
+         algorithmic_bytes=b, GBs=round(gbs, 1), frac=round(gbs / PEAK, 4), cpu_us=round(tc * 1e6, 1),
+         cpu_GBs=round(b / tc / 1e9, 2))
+    ws = eigmi.LanczosWorkspace(M, 210, seed=123)
+    ws.step(10)
+    t = ws.step(200, timed=True)
+    emit(config="C2 3D Poisson 128^3", op="Lanczos step", it_per_s=round(200 / (t.total_ms * 1e-3), 1),
+         k1_us=round(t.spmv_ms / 200 * 1e3, 2), k2_us=round(t.update_ms / 200 * 1e3, 2),
+         step_frac=round(eigmi.bytes_lanczos_step(n, nnz) / (t.total_ms / 200 * 1e-3) / 1e9 / PEAK, 4))
+    ws.close()
+    for m in (8, 32):
+        Qh = oracle.random_mv8(n, m, 1)
+        Q, Y = ctx.array(Qh), ctx.zeros(n * m)
+        eigmi.spmm_mv8(M, m, Q, Y)
+        ctx.sync()
+        tg, _ = wall(lambda: (eigmi.spmm_mv8(M, m, Q, Y), ctx.sync()), 10)
+        sb = 12 * nnz + 4 * (n + 1) + 128 * n * (m // 8)
+        emit(config="C2 3D Poisson 128^3", op=f"SpMM b=8 m={m}", us=round(tg * 1e6, 1),
+             GBs=round(sb / tg / 1e9, 1), frac=round(sb / tg / 1e9 / PEAK, 4))
+        Q.upload(Qh)
+        eigmi.orthonormalize_mv8(ctx, n, m, Q)
+        ctx.sync()
+
+        def ortho():
+            Q.upload(Qh)
+            ctx.sync()
+            t0 = time.perf_counter()
+            eigmi.orthonormalize_mv8(ctx, n, m, Q)
+            ctx.sync()
+            return time.perf_counter() - t0
+        tg = min(ortho() for _ in range(3))
+        tc, _ = wall(lambda: oracle.orthonormalize_mv8(Qh, n, m))
+        ob = eigmi.lib.eig_bytes_orthonormalize_blocked(n, m, 8)
+        of = eigmi.lib.eig_flops_orthonormalize(n, m)
+        emit(config="C2 3D Poisson 128^3", op=f"orthonormalize_blocked (MGS) m={m}", gpu_ms=round(tg * 1e3, 3),
+             cpu_ms=round(tc * 1e3, 1), model_bytes=ob, model_GBs=round(ob / tg / 1e9, 1),
+             model_GFLOPs=round(of / tg / 1e9, 1), speedup=round(tc / tg, 1))
+    # one StandardLargest iteration (SpMM + GS + SpMM + dots) at m = 8
+    _, (_, _, it) = wall(lambda: eigmi.standard_largest(M, 0.0, 0.0, 2, 8, 123, want_evec=False))
+    tg1, _ = wall(lambda: eigmi.standard_largest(M, 0.0, 0.0, 2, 8, 123, want_evec=False))
+    tg11, _ = wall(lambda: eigmi.standard_largest(M, 0.0, 0.0, 12, 8, 123, want_evec=False))
+    tc1, _ = wall(lambda: oracle.standard_largest(A, 0.0, 0.0, 2, 8, 123))
+    tc2, _ = wall(lambda: oracle.standard_largest(A, 0.0, 0.0, 3, 8, 123))
+    emit(config="C2 3D Poisson 128^3", op="StandardLargest iteration m=8", gpu_ms_per_iter=round((tg11 - tg1) / 10 * 1e3, 3),
+         cpu_ms_per_iter=round((tc2 - tc1) * 1e3, 1), speedup=round((tc2 - tc1) / ((tg11 - tg1) / 10), 1))
+
+
+def c3(ctx):
+    N = 64
+    rp, c, v = eigmi.gen_matrix(eigmi.GEN_Q1ELAST3D, N)
+    nb = N ** 3
+    nnzb = int(rp[-1])
+    M = eigmi.Matrix.from_bcsr(ctx, rp, c, v, 3, 3)
+    x = ctx.array(np.random.default_rng(0).standard_normal(3 * nb))
+    y = ctx.zeros(3 * nb)
+    M.mv_timed(x, y, 5)
+    ms = M.mv_timed(x, y, 100)
+    b = 76 * nnzb + 4 * (nb + 1) + 48 * nb
+    gbs = b / (ms * 1e-3) / 1e9
+    A = oracle.CSR(nb, rp, c, v, 3, 3)
+    xh = x.get()
+    tc, _ = wall(lambda: oracle.csr_mv(A, xh))
+    emit(config="C3 Q1 elasticity 64^3 3x3 BCSR", op="BCSR SpMV", us=round(ms * 1e3, 2), nnzb=nnzb,
+         algorithmic_bytes=b, GBs=round(gbs, 1), frac=round(gbs / PEAK, 4), cpu_us=round(tc * 1e6, 1),
+         cpu_GBs=round(b / tc / 1e9, 2))
+
+
+if __name__ == "__main__":
+    ctx = eigmi.Context(0)
+    which = sys.argv[1:] or ["c1", "c2", "c3"]
+    for w in which:
+        globals()[w](ctx)
