@@ -54,18 +54,20 @@ def committed_traffic(kernel, N, world):
     taken on the same configuration; None when no matching profile exists."""
     import glob
     best = None
-    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json"))):
+    for p in glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json")):
         try:
             d = json.load(open(p))
             line = d.get("bench_line_under_trace", {})
             if line.get("config", {}).get("N") != N or line.get("n_gpus") != world:
                 continue
-            k = d["kernels"].get("eigmi::" + kernel)
-            if k:
-                best = (k["hbm_bytes"], os.path.relpath(p, ROOT))
+            for name, k in d["kernels"].items():  # template instances: "eigmi::k_..._b1<1, 1>"
+                if name.split("<")[0] == "eigmi::" + kernel:
+                    stamp = d.get("collected", os.path.getmtime(p))
+                    if best is None or stamp > best[2]:
+                        best = (k["hbm_bytes"], os.path.relpath(p, ROOT), stamp)
         except (OSError, ValueError, KeyError):
             continue
-    return best
+    return best[:2] if best else None
 
 
 def main():
@@ -141,6 +143,10 @@ def main():
         roofline = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": tr[0] if tr else None,
                     "traffic_source": tr[1] if tr else None,
+                    # measured HBM bytes / launch time: the stencil-slice image moves fewer bytes
+                    # than the CSR algorithmic count (column indices -> per-slice offsets + masks)
+                    "traffic_GBs": round(tr[0] / (k1_ms * 1e-3) / 1e9, 1) if tr else None,
+                    "traffic_frac": round(tr[0] / (k1_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if tr else None,
                     "kernel": "k_lanczos_spmv_b1", "bytes_per_launch": k1_bytes,
                     "avg_launch_us": round(k1_ms * 1e3, 2)}
     step_bytes = eigmi.bytes_lanczos_step(n, nnz_total)

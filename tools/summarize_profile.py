@@ -37,7 +37,9 @@ def main(src, tag):
     stats = {}
     for r in csv.DictReader(open(os.path.join(src, "trace", "trace_kernel_stats.csv"))):
         stats[r["Name"].split("(")[0].replace("void ", "")] = float(r["AverageNs"])
-    out = {"tag": tag, "units": "bytes per launch (FETCH_SIZE x 2 x 1024 + WRITE_SIZE x 1024)", "kernels": {}}
+    import time
+    out = {"tag": tag, "collected": time.time(),
+           "units": "bytes per launch (FETCH_SIZE x 2 x 1024 + WRITE_SIZE x 1024)", "kernels": {}}
     for k in sorted(set(fetch) | set(write)):
         name = k.replace("void ", "")
         f = fetch.get(k, 0.0) * 2 * 1024
