@@ -209,14 +209,21 @@ struct LanczosBufs {
 
 // One step j: t = A u sig - gam up (+ dot), allreduce, u_{j+1} = t - alpha sig u (+ norm), allreduce.
 // Optional event timing: ev[0..5] = before K1, after K1, after allreduce 1, after K2, after allreduce 2.
-void lanczos_step(eig_mat_s &A, double *u, double *up, double *t, int j, LanczosBufs &lb, hipEvent_t *ev,
-                  hipEvent_t halo_ev0, hipEvent_t halo_ev1)
+// ev_external: the step is being captured into a hipGraph, so the timing events become external
+// event-record nodes (a plain record during capture is only a fork/join marker).
+// ev: nullptr, 2 events (K1 bracket) or 5 (detail: + after allreduce 1, after K2, after allreduce 2).
+void lanczos_step(eig_mat_s &A, double *u, double *up, double *t, int j, LanczosBufs &lb, hipEvent_t *ev, int nev,
+                  hipEvent_t halo_ev0, hipEvent_t halo_ev1, bool ev_external = false)
 {
   eig_ctx_t ctx = A.ctx;
   hipStream_t s = ctx->stream;
   const i64 own = A.own_offset;
   const i64 n = A.nb_rows;
-  if (ev) EIG_HIP(hipEventRecord(ev[0], s));
+  auto mark = [&](int i) {
+    if (ev && i < nev)
+      EIG_HIP(hipEventRecordWithFlags(ev[i], s, ev_external ? hipEventRecordExternal : hipEventRecordDefault));
+  };
+  mark(0);
   if (!distributed(A) || (A.recvs.empty() && A.sends.empty()) || ctx->loop)
   {
     if (distributed(A)) halo_exchange(A, u, s);  // loopback transport: synchronous exchange
@@ -239,13 +246,13 @@ void lanczos_step(eig_mat_s &A, double *u, double *up, double *t, int j, Lanczos
       launch_lanczos_spmv(A, u, up, t, j, lb.st, A.slice_list, A.n_interior, A.n_boundary, lb.st.dsum + j,
                           lb.st.beta + j, has_in ? lb.carry : nullptr, 0, s, ctx->red);
   }
-  if (ev) EIG_HIP(hipEventRecord(ev[1], s));
+  mark(1);
   allreduce_sum(ctx, lb.st.dsum + j, 1, s);
-  if (ev) EIG_HIP(hipEventRecord(ev[2], s));
+  mark(2);
   launch_lanczos_update(n, u + own, t + own, j, lb.st, 0, s, ctx->red);
-  if (ev) EIG_HIP(hipEventRecord(ev[3], s));
+  mark(3);
   allreduce_sum(ctx, lb.st.nsum + j + 1, 1, s);
-  if (ev) EIG_HIP(hipEventRecord(ev[4], s));
+  mark(4);
 }
 
 // Start vector into the owned rows of a zeroed window buffer: u0 (device, window layout) or
@@ -278,8 +285,24 @@ struct eig_lanczos_s {
   DevBuf *B[3] = {nullptr, nullptr, nullptr};
   LanczosBufs *lb = nullptr;
   hipEvent_t h0 = nullptr, h1 = nullptr;
+  // pending eig_lanczos_capture batch (graph == nullptr with g_steps > 0: eager fallback)
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t gexec = nullptr;
+  int g_steps = 0, g_flags = 0;
+  std::vector<hipEvent_t> g_ev;  // [beg, end, events_per_step(g_flags) per step]
+  void drop_graph()
+  {
+    if (gexec) (void)hipGraphExecDestroy(gexec);
+    if (graph) (void)hipGraphDestroy(graph);
+    for (auto &e : g_ev) (void)hipEventDestroy(e);
+    gexec = nullptr;
+    graph = nullptr;
+    g_ev.clear();
+    g_steps = 0;
+  }
   ~eig_lanczos_s()
   {
+    drop_graph();
     for (auto *b : B) delete b;
     delete lb;
     if (h0) (void)hipEventDestroy(h0);
@@ -293,6 +316,62 @@ void check_lanczos_matrix(const eig_mat_s *A)
 {
   EIG_CHECK(A->br == 1 && A->bc == 1, EIG_ERR_BLOCKSIZE, "Lanczos driver: 1x1 blocks only");
   EIG_CHECK(A->nb_rows_global == A->nb_cols, EIG_ERR_SHAPE, "Lanczos needs a square matrix");
+}
+
+// Events per step for the timing flags: EIG_LANCZOS_TIME_KERNELS brackets the fused SpMV only (two
+// timestamps per step keep the perturbation of the timed loop small), EIG_LANCZOS_TIME_DETAIL adds the
+// allreduce / update boundaries.
+int events_per_step(int flags)
+{
+  return (flags & EIG_LANCZOS_TIME_DETAIL) ? 5 : (flags & EIG_LANCZOS_TIME_KERNELS) ? 2 : 0;
+}
+
+// ev = [beg, end, nps per step]; enqueues steps k .. k+steps-1 on the library stream.
+void enqueue_steps(eig_lanczos_s &ws, int steps, int nps, hipEvent_t *ev, bool external)
+{
+  eig_mat_s &A = *ws.A;
+  hipStream_t s = A.ctx->stream;
+  const unsigned fl = external ? hipEventRecordExternal : hipEventRecordDefault;
+  double *U[3] = {ws.B[0]->d(), ws.B[1]->d(), ws.B[2]->d()};
+  EIG_HIP(hipEventRecordWithFlags(ev[0], s, fl));
+  for (int i = 0; i < steps; ++i)
+  {
+    const int j = ws.k + i;
+    lanczos_step(A, U[j % 3], U[(j + 2) % 3], U[(j + 1) % 3], j, *ws.lb, nps ? ev + 2 + (size_t)nps * i : nullptr,
+                 nps, ws.h0, ws.h1, external);
+  }
+  EIG_HIP(hipEventRecordWithFlags(ev[1], s, fl));
+}
+
+std::vector<hipEvent_t> make_events(int steps, int nps)
+{
+  std::vector<hipEvent_t> ev(2 + (size_t)nps * steps);
+  for (auto &e : ev) EIG_HIP(hipEventCreate(&e));
+  return ev;
+}
+
+void read_timing(const std::vector<hipEvent_t> &ev, int steps, int nps, eig_timing *timing)
+{
+  if (!timing) return;
+  std::memset(timing, 0, sizeof(*timing));
+  float ms = 0.f;
+  EIG_HIP(hipEventElapsedTime(&ms, ev[0], ev[1]));
+  timing->total_ms = ms;
+  if (!nps) return;
+  for (int i = 0; i < steps; ++i)
+  {
+    const hipEvent_t *e = &ev[2 + (size_t)nps * i];
+    float a = 0, b = 0, c = 0, d = 0;
+    EIG_HIP(hipEventElapsedTime(&a, e[0], e[1]));
+    timing->spmv_ms += a;
+    if (nps < 5) continue;
+    EIG_HIP(hipEventElapsedTime(&b, e[1], e[2]));
+    EIG_HIP(hipEventElapsedTime(&c, e[2], e[3]));
+    EIG_HIP(hipEventElapsedTime(&d, e[3], e[4]));
+    timing->comm_ms += b + d;
+    timing->update_ms += c;
+  }
+  timing->spmv_launches = steps;
 }
 
 }  // namespace
@@ -336,58 +415,93 @@ extern "C" int eig_lanczos_step(eig_lanczos_t ws, int steps, int flags, eig_timi
   return guard(ws ? ws->A->ctx : nullptr, [&] {
     EIG_CHECK(ws && steps >= 0, EIG_ERR_ARG, "eig_lanczos_step: bad argument");
     EIG_CHECK(ws->k + steps <= ws->max_steps, EIG_ERR_ARG, "eig_lanczos_step: more steps than max_steps");
-    EIG_CHECK((flags & ~EIG_LANCZOS_TIME_KERNELS) == 0, EIG_ERR_ARG, "eig_lanczos_step: unknown flag");
-    eig_mat_s &A = *ws->A;
-    eig_ctx_t ctx = A.ctx;
+    EIG_CHECK((flags & ~(EIG_LANCZOS_TIME_KERNELS | EIG_LANCZOS_TIME_DETAIL)) == 0, EIG_ERR_ARG, "eig_lanczos_step: unknown flag");
+    ws->drop_graph();  // a pending capture is for steps that are about to be taken eagerly
+    eig_ctx_t ctx = ws->A->ctx;
     EIG_HIP(hipSetDevice(ctx->device));
-    hipStream_t s = ctx->stream;
-    const bool timed = (flags & EIG_LANCZOS_TIME_KERNELS) != 0;
-    std::vector<hipEvent_t> ev;
-    hipEvent_t tbeg, tend;
-    EIG_HIP(hipEventCreate(&tbeg));
-    EIG_HIP(hipEventCreate(&tend));
-    if (timed)
+    const int nps = events_per_step(flags);
+    std::vector<hipEvent_t> ev = make_events(steps, nps);
+    try
     {
-      ev.resize((size_t)5 * steps);
-      for (auto &e : ev) EIG_HIP(hipEventCreate(&e));
+      enqueue_steps(*ws, steps, nps, ev.data(), false);
+      EIG_HIP(hipStreamSynchronize(ctx->stream));
+      ws->k += steps;
+      read_timing(ev, steps, nps, timing);
     }
-    double *U[3] = {ws->B[0]->d(), ws->B[1]->d(), ws->B[2]->d()};
-    EIG_HIP(hipEventRecord(tbeg, s));
-    for (int i = 0; i < steps; ++i)
+    catch (...)
     {
-      const int j = ws->k + i;
-      lanczos_step(A, U[j % 3], U[(j + 2) % 3], U[(j + 1) % 3], j, *ws->lb, timed ? &ev[(size_t)5 * i] : nullptr,
-                   ws->h0, ws->h1);
-    }
-    EIG_HIP(hipEventRecord(tend, s));
-    EIG_HIP(hipStreamSynchronize(s));
-    ws->k += steps;
-    if (timing)
-    {
-      std::memset(timing, 0, sizeof(*timing));
-      float ms = 0.f;
-      EIG_HIP(hipEventElapsedTime(&ms, tbeg, tend));
-      timing->total_ms = ms;
-      if (timed)
-      {
-        for (int i = 0; i < steps; ++i)
-        {
-          hipEvent_t *e = &ev[(size_t)5 * i];
-          float a = 0, b = 0, c = 0, d = 0;
-          EIG_HIP(hipEventElapsedTime(&a, e[0], e[1]));
-          EIG_HIP(hipEventElapsedTime(&b, e[1], e[2]));
-          EIG_HIP(hipEventElapsedTime(&c, e[2], e[3]));
-          EIG_HIP(hipEventElapsedTime(&d, e[3], e[4]));
-          timing->spmv_ms += a;
-          timing->comm_ms += b + d;
-          timing->update_ms += c;
-        }
-        timing->spmv_launches = steps;
-      }
+      for (auto &e : ev) (void)hipEventDestroy(e);
+      throw;
     }
     for (auto &e : ev) (void)hipEventDestroy(e);
-    (void)hipEventDestroy(tbeg);
-    (void)hipEventDestroy(tend);
+  });
+}
+
+extern "C" int eig_lanczos_capture(eig_lanczos_t ws, int steps, int flags, int *captured)
+{
+  return guard(ws ? ws->A->ctx : nullptr, [&] {
+    EIG_CHECK(ws && steps > 0, EIG_ERR_ARG, "eig_lanczos_capture: bad argument");
+    EIG_CHECK(ws->k + steps <= ws->max_steps, EIG_ERR_ARG, "eig_lanczos_capture: more steps than max_steps");
+    EIG_CHECK((flags & ~(EIG_LANCZOS_TIME_KERNELS | EIG_LANCZOS_TIME_DETAIL)) == 0, EIG_ERR_ARG, "eig_lanczos_capture: unknown flag");
+    ws->drop_graph();
+    eig_ctx_t ctx = ws->A->ctx;
+    EIG_HIP(hipSetDevice(ctx->device));
+    ws->g_steps = steps;
+    ws->g_flags = flags;
+    ws->g_ev = make_events(steps, events_per_step(flags));
+    if (captured) *captured = 0;
+    // the loopback transport synchronises with the host inside the step: eager replay only
+    if (ctx->loop) return;
+    hipStream_t s = ctx->stream;
+    EIG_HIP(hipStreamSynchronize(s));
+    EIG_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
+    hipGraph_t g = nullptr;
+    bool ok = true;
+    try
+    {
+      enqueue_steps(*ws, steps, events_per_step(flags), ws->g_ev.data(), true);
+    }
+    catch (...)
+    {
+      ok = false;
+    }
+    hipError_t e = hipStreamEndCapture(s, &g);
+    if (!ok || e != hipSuccess || !g)
+    {
+      if (g) (void)hipGraphDestroy(g);
+      (void)hipGetLastError();
+      return;  // capture refused (e.g. by the collective library): eager replay
+    }
+    ws->graph = g;
+    if (hipGraphInstantiate(&ws->gexec, g, nullptr, nullptr, 0) != hipSuccess)
+    {
+      (void)hipGetLastError();
+      (void)hipGraphDestroy(g);
+      ws->graph = nullptr;
+      ws->gexec = nullptr;
+      return;
+    }
+    if (captured) *captured = 1;
+  });
+}
+
+extern "C" int eig_lanczos_replay(eig_lanczos_t ws, eig_timing *timing)
+{
+  return guard(ws ? ws->A->ctx : nullptr, [&] {
+    EIG_CHECK(ws && ws->g_steps > 0, EIG_ERR_ARG, "eig_lanczos_replay: nothing captured");
+    eig_ctx_t ctx = ws->A->ctx;
+    EIG_HIP(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    const int steps = ws->g_steps;
+    const int nps = events_per_step(ws->g_flags);
+    if (ws->gexec)
+      EIG_HIP(hipGraphLaunch(ws->gexec, s));
+    else
+      enqueue_steps(*ws, steps, nps, ws->g_ev.data(), false);
+    EIG_HIP(hipStreamSynchronize(s));
+    ws->k += steps;
+    read_timing(ws->g_ev, steps, nps, timing);
+    ws->drop_graph();
   });
 }
 
@@ -458,7 +572,7 @@ extern "C" int eig_lanczos_solve(eig_mat_t A, int nev, int ncv, int which, unsig
     for (int j = 0; j < ncv; ++j)
     {
       double *u = V + (i64)j * W, *up = j > 0 ? V + (i64)(j - 1) * W : V + (i64)j * W, *t = V + (i64)(j + 1) * W;
-      lanczos_step(*A, u, up, t, j, lb, nullptr, h0, h1);
+      lanczos_step(*A, u, up, t, j, lb, nullptr, 0, h0, h1);
       // DGKS: two classical Gram-Schmidt passes against v_0..v_j (v_q = u_q / sqrt(nsum[q]))
       for (int pass = 0; pass < 2; ++pass)
       {

@@ -16,6 +16,16 @@ EIG_OK, EIG_ERR_SHAPE, EIG_ERR_BLOCKSIZE, EIG_ERR_HIP, EIG_ERR_RCCL, EIG_ERR_BRE
 ORTHO_MGS, ORTHO_CHOLQR = 0, 1
 WHICH_LA, WHICH_SA = 0, 1
 LANCZOS_TIME_KERNELS = 1
+LANCZOS_TIME_DETAIL = 2
+
+
+def _tflags(timed):
+    """timed: False | True (fused-SpMV events) | "detail" (+ update / allreduce boundaries)."""
+    if timed == "detail":
+        return LANCZOS_TIME_KERNELS | LANCZOS_TIME_DETAIL
+    return LANCZOS_TIME_KERNELS if timed else 0
+
+
 GEN_LAPLACE2D, GEN_NEUMANN2D, GEN_PU2D, GEN_IDENTITY2D, GEN_POISSON3D, GEN_Q1ELAST3D = range(6)
 
 
@@ -97,6 +107,8 @@ SIGNATURES = {
     "eig_lanczos_step": (_int, [_vp, _int, _int, ctypes.POINTER(Timing)]),
     "eig_lanczos_tridiag": (_int, [_vp, ctypes.POINTER(_int), _vp, _vp]),
     "eig_lanczos_destroy": (_int, [_vp]),
+    "eig_lanczos_capture": (_int, [_vp, _int, _int, ctypes.POINTER(_int)]),
+    "eig_lanczos_replay": (_int, [_vp, ctypes.POINTER(Timing)]),
     "eig_flops_orthonormalize": (_dbl, [_i64, _i64]),
     "eig_bytes_orthonormalize_blocked": (_dbl, [_i64, _i64, _int]),
     "eig_gen_nnzb": (_i64, [_int, _int]),
@@ -372,7 +384,7 @@ def lanczos_run(A, steps, u0=None, seed=123, timed=False):
     beta = np.zeros(steps + 1)
     t = Timing()
     A.ctx.check(lib.eig_lanczos_run(A.h, steps, u0.ptr if u0 is not None else None, seed,
-                                    LANCZOS_TIME_KERNELS if timed else 0, _np_ptr(alpha), _np_ptr(beta),
+                                    _tflags(timed), _np_ptr(alpha), _np_ptr(beta),
                                     ctypes.byref(t)))
     return alpha[:steps], beta, t
 
@@ -390,7 +402,20 @@ class LanczosWorkspace:
 
     def step(self, steps, timed=False):
         t = Timing()
-        self.A.ctx.check(lib.eig_lanczos_step(self.h, steps, LANCZOS_TIME_KERNELS if timed else 0, ctypes.byref(t)))
+        self.A.ctx.check(lib.eig_lanczos_step(self.h, steps, _tflags(timed), ctypes.byref(t)))
+        return t
+
+    def capture(self, steps, timed=False):
+        """Record the next `steps` steps as one hipGraph (nothing runs); True when the runtime
+        accepted the capture, False when replay() will take the steps eagerly."""
+        c = _int(0)
+        self.A.ctx.check(lib.eig_lanczos_capture(self.h, steps, _tflags(timed),
+                                                 ctypes.byref(c)))
+        return bool(c.value)
+
+    def replay(self):
+        t = Timing()
+        self.A.ctx.check(lib.eig_lanczos_replay(self.h, ctypes.byref(t)))
         return t
 
     def tridiag(self):

@@ -178,12 +178,13 @@ int eig_standard_largest(eig_mat_t A, double shift, double tol, int maxiter, int
 typedef struct eig_timing {
   double total_ms;        /* wall time of the stepping loop (device events, first to last) */
   double spmv_ms;         /* summed duration of the fused SpMV kernel launches */
-  double update_ms;       /* summed duration of the fused axpy/norm kernel launches */
-  double comm_ms;         /* summed duration of halo exchange + allreduce segments */
+  double update_ms;       /* summed duration of the fused axpy/norm kernel launches (TIME_DETAIL) */
+  double comm_ms;         /* summed duration of the allreduce segments (TIME_DETAIL) */
   int64_t spmv_launches;  /* number of SpMV kernel launches timed */
 } eig_timing;
 enum eig_lanczos_flags {
-  EIG_LANCZOS_TIME_KERNELS = 1  /* record HIP events around every kernel (eig_timing fields) */
+  EIG_LANCZOS_TIME_KERNELS = 1, /* HIP events around every fused SpMV launch (spmv_ms) */
+  EIG_LANCZOS_TIME_DETAIL = 2   /* + events after each allreduce and update (update_ms, comm_ms) */
 };
 int eig_lanczos_run(eig_mat_t A, int steps, const double *u0, unsigned seed, int flags,
                     double *alpha_host, double *beta_host, eig_timing *timing);
@@ -198,6 +199,13 @@ int eig_lanczos_create(eig_mat_t A, int max_steps, const double *u0, unsigned se
 int eig_lanczos_step(eig_lanczos_t ws, int steps, int flags, eig_timing *timing);
 int eig_lanczos_tridiag(eig_lanczos_t ws, int *k, double *alpha_host, double *beta_host);
 int eig_lanczos_destroy(eig_lanczos_t ws);
+/* hipGraph form of eig_lanczos_step: capture the next `steps` steps (kernels, halo exchange,
+ * allreduces; plus per-step kernel events when flags has EIG_LANCZOS_TIME_KERNELS) into one
+ * graph and instantiate it -- nothing runs yet.  eig_lanczos_replay launches it once
+ * (synchronous) and advances the step count.  *captured = 0 when the runtime refused the capture
+ * (the replay then runs the same steps eagerly). */
+int eig_lanczos_capture(eig_lanczos_t ws, int steps, int flags, int *captured);
+int eig_lanczos_replay(eig_lanczos_t ws, eig_timing *timing);
 
 /* Lanczos eigensolver: ncv-step Lanczos with full re-orthogonalisation (classical Gram-Schmidt
  * twice, the DGKS scheme ARPACK uses) and Ritz extraction from T.  which: EIG_WHICH_LA (largest

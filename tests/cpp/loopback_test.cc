@@ -67,6 +67,7 @@ int main(int argc, char **argv)
   // ---- P virtual ranks
   void *hub;
   CK(eig_loopback_create(P, &hub));
+  std::vector<int> graph_ok(P, 0);
   std::vector<std::vector<double>> y(P), al(P, std::vector<double>(steps)), be(P, std::vector<double>(steps + 1)),
       ev(P, std::vector<double>(nev));
   std::vector<int64_t> rb(P), rc(P), halo(P);
@@ -103,6 +104,19 @@ int main(int argc, char **argv)
       CK(eig_memcpy_d2h(ctx, &dots[r], dd, 8));
       // Lanczos recurrence and solver
       CK(eig_lanczos_run(A, steps, nullptr, 123, EIG_LANCZOS_TIME_KERNELS, al[r].data(), be[r].data(), nullptr));
+      {
+        // capture/replay: the loopback transport cannot be captured, replay must take the same steps eagerly
+        std::vector<double> ag(steps), bg(steps + 1);
+        eig_lanczos_t ws;
+        CK(eig_lanczos_create(A, steps, nullptr, 123, &ws));
+        int cap = -1;
+        CK(eig_lanczos_capture(ws, steps, 0, &cap));
+        CK(eig_lanczos_replay(ws, nullptr));
+        CK(eig_lanczos_tridiag(ws, nullptr, ag.data(), bg.data()));
+        CK(eig_lanczos_destroy(ws));
+        graph_ok[r] = cap == 0 && std::memcmp(ag.data(), al[r].data(), steps * 8) == 0 &&
+                      std::memcmp(bg.data(), be[r].data(), (steps + 1) * 8) == 0;
+      }
       CK(eig_lanczos_solve(A, nev, ncv, EIG_WHICH_LA, 123, ev[r].data(), nullptr, nullptr));
       eig_free(ctx, dx);
       eig_free(ctx, dy);
@@ -117,6 +131,11 @@ int main(int argc, char **argv)
   for (double v : x) xx += v * v;
   for (int r = 0; r < P; ++r)
   {
+    if (!graph_ok[r])
+    {
+      std::printf("FAIL rank %d: capture/replay differs from eig_lanczos_run\n", r);
+      ++failures;
+    }
     if (std::memcmp(y[r].data(), y_ser.data() + rb[r], rc[r] * 8) != 0)
     {
       std::printf("FAIL rank %d: distributed SpMV not bitwise equal to the serial one\n", r);

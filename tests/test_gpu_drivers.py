@@ -71,6 +71,33 @@ def test_lanczos_run_device_start_vector(ctx):
     assert t.spmv_launches == 10 and t.spmv_ms > 0 and t.total_ms >= t.spmv_ms
 
 
+@pytest.mark.parametrize("timed", [False, True])
+def test_lanczos_graph_replay_bitwise_vs_eager(ctx, timed):
+    """eig_lanczos_capture/replay runs the same kernels in the same order as eig_lanczos_step:
+    the recurrence must be bitwise identical, also when eager and graph batches are mixed."""
+    A = oracle.poisson3d(24)
+    M = upload(ctx, A)
+    ref = eigmi.LanczosWorkspace(M, 30, seed=7)
+    ref.step(30)
+    ra, rb = ref.tridiag()
+    ws = eigmi.LanczosWorkspace(M, 30, seed=7)
+    ws.step(5)
+    assert ws.capture(20, timed=timed)  # single rank: the capture must be accepted
+    t = ws.replay()
+    assert t.total_ms > 0
+    if timed:
+        assert t.spmv_launches == 20 and 0 < t.spmv_ms < t.total_ms
+    ws.step(5)
+    a, b = ws.tridiag()
+    assert np.array_equal(a, ra) and np.array_equal(b, rb)
+    with pytest.raises(eigmi.EigError):
+        ws.replay()  # the graph is consumed by its replay
+    with pytest.raises(eigmi.EigError):
+        ws.capture(1)  # past max_steps
+    ws.close()
+    ref.close()
+
+
 @pytest.mark.parametrize("which", ["LA", "SA"])
 def test_lanczos_solve_c1_vs_analytic_and_arpack(ctx, golden_dir, which):
     g = np.load(os.path.join(golden_dir, "c1_arpack.npz"))

@@ -69,7 +69,7 @@ def c2(ctx):
          cpu_GBs=round(b / tc / 1e9, 2))
     ws = eigmi.LanczosWorkspace(M, 210, seed=123)
     ws.step(10)
-    t = ws.step(200, timed=True)
+    t = ws.step(200, timed="detail")
     emit(config="C2 3D Poisson 128^3", op="Lanczos step", it_per_s=round(200 / (t.total_ms * 1e-3), 1),
          k1_us=round(t.spmv_ms / 200 * 1e3, 2), k2_us=round(t.update_ms / 200 * 1e3, 2),
          step_frac=round(eigmi.bytes_lanczos_step(n, nnz) / (t.total_ms / 200 * 1e-3) / 1e9 / PEAK, 4))

@@ -45,7 +45,7 @@ def main():
             os.environ["EIGMI_K1_PIPE"] = pipe[R]
             ws = eigmi.LanczosWorkspace(M, args.steps + 2, seed=123)
             ws.step(2)
-            t = ws.step(args.steps, timed=True)
+            t = ws.step(args.steps, timed="detail")
             res[R]["k1_us"].append(t.spmv_ms / args.steps * 1e3)
             res[R]["k2_us"].append(t.update_ms / args.steps * 1e3)
             res[R]["step_us"].append(t.total_ms / args.steps * 1e3)
