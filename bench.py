@@ -173,7 +173,8 @@ def main():
         "dtype": "f64",
         "data": "synthetic (generated 7-point Poisson matrix, mt19937 seed-123 start vector)",
         "config": {"workload": f"3D Poisson 7-pt {N}^3 Lanczos 3-term step, no re-orthogonalisation",
-                   "N": N, "n": n, "nnz": nnz_total, "parallelism": f"row-partition z-slabs x{world} (RCCL halo + allreduce)"},
+                   "N": N, "n": n, "nnz": nnz_total,
+                   "parallelism": f"row-partition z-slabs x{world} (RCCL halo, {ctx.comm_info()['allreduce']} allreduce)"},
         "step_hbm_gbs": round(step_bytes / (dt / K) / 1e9, 1),
         "step_roofline_frac": round(step_bytes / (dt / K) / 1e9 / HBM_PEAK_GBS / max(world, 1), 4),
         "roofline": roofline,

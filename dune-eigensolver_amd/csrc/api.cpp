@@ -88,6 +88,13 @@ void *ctx_buffer(eig_ctx_t ctx, int slot, size_t bytes)
 void allreduce_sum(eig_ctx_t ctx, double *buf, i64 count, hipStream_t s)
 {
   if (!ctx->distributed() || count <= 0) return;
+  if (ctx->mbox && ctx->mbox->ready)
+  {
+    for (i64 off = 0; off < count; off += kMailboxVals)
+      launch_mailbox_allreduce(buf + off, (int)std::min<i64>(kMailboxVals, count - off), ctx->mbox->dev,
+                               kMailboxTimeout, s);
+    return;
+  }
   if (ctx->loop)
   {
     // loopback: every virtual rank publishes its values, then sums all ranks in rank order
@@ -109,6 +116,87 @@ void allreduce_sum(eig_ctx_t ctx, double *buf, i64 count, hipStream_t s)
     return;
   }
   EIG_NCCL(ncclAllReduce(buf, buf, (size_t)count, ncclDouble, ncclSum, ctx->comm, s));
+}
+
+// ---------------------------------------------------------------------------------------------
+// xGMI mailbox (k_comm.hip).  prepare: allocate my uncached mailbox + state and export it;
+// open: map every peer's mailbox; validate: one allreduce of rank+1 must give P(P+1)/2 exactly.
+// ---------------------------------------------------------------------------------------------
+void mailbox_free(eig_ctx_t ctx)
+{
+  MailboxHost *m = ctx->mbox;
+  if (!m) return;
+  for (void *p : m->opened) (void)hipIpcCloseMemHandle(p);
+  if (m->local) (void)hipFree(m->local);
+  if (m->state) (void)hipFree(m->state);
+  delete m;
+  ctx->mbox = nullptr;
+}
+
+void mailbox_prepare(eig_ctx_t ctx, int nranks, int rank, unsigned char handle[HIP_IPC_HANDLE_SIZE])
+{
+  EIG_CHECK(nranks >= 1 && nranks <= kMaxMailboxRanks && rank >= 0 && rank < nranks, EIG_ERR_ARG,
+            "mailbox: rank count outside 1..16");
+  mailbox_free(ctx);
+  auto *m = new MailboxHost();
+  ctx->mbox = m;
+  const size_t bytes = (size_t)2 * nranks * (1 + kMailboxVals) * sizeof(u64);
+  // uncached: a peer's stores over xGMI land in HBM and my polling loads must see them while
+  // the kernel runs; fine-grained is the fallback where uncached memory cannot be exported
+  void *p = nullptr;
+  if (hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached) != hipSuccess)
+  {
+    (void)hipGetLastError();
+    EIG_HIP(hipExtMallocWithFlags(&p, bytes, hipDeviceMallocFinegrained));
+  }
+  m->local = static_cast<u64 *>(p);
+  EIG_HIP(hipMemset(m->local, 0, bytes));
+  EIG_HIP(hipMalloc(&m->state, 256));
+  EIG_HIP(hipMemset(m->state, 0, 256));
+  m->dev.local = m->local;
+  m->dev.ctr = static_cast<u64 *>(m->state);
+  m->dev.err = reinterpret_cast<int *>(static_cast<char *>(m->state) + 128);
+  m->dev.P = nranks;
+  m->dev.me = rank;
+  hipIpcMemHandle_t h;
+  EIG_HIP(hipIpcGetMemHandle(&h, m->local));
+  std::memcpy(handle, &h, HIP_IPC_HANDLE_SIZE);
+}
+
+void mailbox_open(eig_ctx_t ctx, const unsigned char *handles)
+{
+  MailboxHost *m = ctx->mbox;
+  EIG_CHECK(m && m->local, EIG_ERR_ARG, "mailbox: open before prepare");
+  for (int r = 0; r < m->dev.P; ++r)
+  {
+    if (r == m->dev.me)
+    {
+      m->dev.peer[r] = m->local;
+      continue;
+    }
+    hipIpcMemHandle_t h;
+    std::memcpy(&h, handles + (size_t)r * HIP_IPC_HANDLE_SIZE, HIP_IPC_HANDLE_SIZE);
+    void *p = nullptr;
+    EIG_HIP(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
+    m->opened.push_back(p);
+    m->dev.peer[r] = static_cast<u64 *>(p);
+  }
+}
+
+bool mailbox_validate(eig_ctx_t ctx)
+{
+  MailboxHost *m = ctx->mbox;
+  double *d = ctx->scratch;
+  const int P = m->dev.P;
+  double v[3] = {(double)(m->dev.me + 1), 1.0, (double)(m->dev.me + 1) * 0.5};
+  EIG_HIP(hipMemcpy(d, v, sizeof(v), hipMemcpyHostToDevice));
+  launch_mailbox_allreduce(d, 3, m->dev, 200000000ull /* 2 s */, ctx->stream);
+  EIG_HIP(hipStreamSynchronize(ctx->stream));
+  int err = 1;
+  EIG_HIP(hipMemcpy(v, d, sizeof(v), hipMemcpyDeviceToHost));
+  EIG_HIP(hipMemcpy(&err, m->dev.err, sizeof(int), hipMemcpyDeviceToHost));
+  const double want = 0.5 * P * (P + 1);
+  return err == 0 && v[0] == want && v[1] == (double)P && v[2] == 0.5 * want;
 }
 
 // Exchange the ghost entries of the window-layout vector x.  Runs on stream s.
@@ -138,6 +226,7 @@ void halo_exchange(const eig_mat_s &A, double *x, hipStream_t s)
     return;
   }
   if (A.sends.empty() && A.recvs.empty()) return;
+  EIG_CHECK(ctx->comm, EIG_ERR_ARG, "halo exchange needs RCCL or the loopback transport");
   EIG_NCCL(ncclGroupStart());
   for (const auto &r : A.recvs) EIG_NCCL(ncclRecv(x + r.offset, (size_t)r.count, ncclDouble, r.peer, ctx->comm, s));
   for (const auto &r : A.sends) EIG_NCCL(ncclSend(x + r.offset, (size_t)r.count, ncclDouble, r.peer, ctx->comm, s));
@@ -207,6 +296,7 @@ extern "C" int eig_ctx_destroy(eig_ctx_t ctx)
   if (!ctx) return EIG_OK;
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  mailbox_free(ctx);
   if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
   ctx->loop = nullptr;  // the hub is owned by eig_loopback_create / _destroy
   for (auto &e : ctx->pool)
@@ -251,16 +341,124 @@ extern "C" int eig_comm_unique_id(unsigned char id[128])
   });
 }
 
+namespace {
+
+// RCCL-agreed minimum of a per-rank flag (every rank takes the same branch afterwards).
+bool all_ranks(eig_ctx_t ctx, bool mine)
+{
+  int *d = dev_alloc<int>(1);
+  const int v = mine ? 1 : 0;
+  EIG_HIP(hipMemcpy(d, &v, sizeof(int), hipMemcpyHostToDevice));
+  EIG_NCCL(ncclAllReduce(d, d, 1, ncclInt32, ncclMin, ctx->comm, ctx->stream));
+  EIG_HIP(hipStreamSynchronize(ctx->stream));
+  int r = 0;
+  EIG_HIP(hipMemcpy(&r, d, sizeof(int), hipMemcpyDeviceToHost));
+  (void)hipFree(d);
+  return r == 1;
+}
+
+// Mailbox allreduce next to the RCCL communicator; each stage is agreed by all ranks, so a rank
+// whose export, mapping or validation fails makes every rank stay on ncclAllReduce.
+void mailbox_setup_rccl(eig_ctx_t ctx)
+{
+  const int P = ctx->nranks, me = ctx->rank;
+  const char *env = std::getenv("EIGMI_ALLREDUCE");
+  const bool want = P > 1 && P <= kMaxMailboxRanks && !(env && std::string(env) == "rccl");
+  if (!all_ranks(ctx, want)) return;
+  std::vector<unsigned char> h((size_t)P * HIP_IPC_HANDLE_SIZE, 0);
+  bool ok = true;
+  try
+  {
+    mailbox_prepare(ctx, P, me, h.data() + (size_t)me * HIP_IPC_HANDLE_SIZE);
+  }
+  catch (const Error &)
+  {
+    ok = false;
+  }
+  if (!all_ranks(ctx, ok)) return mailbox_free(ctx);
+  unsigned char *d = dev_alloc<unsigned char>(h.size());
+  EIG_HIP(hipMemcpy(d + (size_t)me * HIP_IPC_HANDLE_SIZE, h.data() + (size_t)me * HIP_IPC_HANDLE_SIZE,
+                    HIP_IPC_HANDLE_SIZE, hipMemcpyHostToDevice));
+  EIG_NCCL(ncclAllGather(d + (size_t)me * HIP_IPC_HANDLE_SIZE, d, HIP_IPC_HANDLE_SIZE, ncclChar, ctx->comm,
+                         ctx->stream));
+  EIG_HIP(hipStreamSynchronize(ctx->stream));
+  EIG_HIP(hipMemcpy(h.data(), d, h.size(), hipMemcpyDeviceToHost));
+  (void)hipFree(d);
+  try
+  {
+    mailbox_open(ctx, h.data());
+  }
+  catch (const Error &)
+  {
+    ok = false;
+  }
+  if (!all_ranks(ctx, ok)) return mailbox_free(ctx);
+  ok = mailbox_validate(ctx);
+  if (!all_ranks(ctx, ok)) return mailbox_free(ctx);
+  ctx->mbox->ready = true;
+}
+
+}  // namespace
+
 extern "C" int eig_comm_init(eig_ctx_t ctx, int nranks, int rank, const unsigned char id[128])
 {
   return guard(ctx, [&] {
     EIG_CHECK(ctx && id && nranks >= 1 && rank >= 0 && rank < nranks, EIG_ERR_ARG, "eig_comm_init: bad arguments");
+    EIG_CHECK(!ctx->loop && !ctx->mbox, EIG_ERR_ARG, "context already has a transport");
     DeviceGuard dg(ctx->device);
     ncclUniqueId u;
     std::memcpy(&u, id, 128);
     EIG_NCCL(ncclCommInitRank(&ctx->comm, nranks, u, rank));
     ctx->nranks = nranks;
     ctx->rank = rank;
+    mailbox_setup_rccl(ctx);
+  });
+}
+
+extern "C" int eig_comm_ipc_handle(eig_ctx_t ctx, int nranks, int rank, unsigned char handle[EIG_IPC_HANDLE_BYTES])
+{
+  return guard(ctx, [&] {
+    EIG_CHECK(ctx && handle, EIG_ERR_ARG, "eig_comm_ipc_handle: bad arguments");
+    EIG_CHECK(!ctx->comm && !ctx->loop, EIG_ERR_ARG, "context already has a transport");
+    DeviceGuard dg(ctx->device);
+    mailbox_prepare(ctx, nranks, rank, handle);
+  });
+}
+
+extern "C" int eig_comm_ipc_open(eig_ctx_t ctx, const unsigned char *handles)
+{
+  return guard(ctx, [&] {
+    EIG_CHECK(ctx && handles && ctx->mbox && !ctx->mbox->ready, EIG_ERR_ARG,
+              "eig_comm_ipc_open: call eig_comm_ipc_handle first");
+    DeviceGuard dg(ctx->device);
+    mailbox_open(ctx, handles);
+    ctx->nranks = ctx->mbox->dev.P;
+    ctx->rank = ctx->mbox->dev.me;
+    ctx->mbox->ready = true;
+  });
+}
+
+extern "C" int eig_comm_info(eig_ctx_t ctx, int *nranks, int *rank, int *allreduce, int *mailbox_errors)
+{
+  return guard(ctx, [&] {
+    EIG_CHECK(ctx, EIG_ERR_ARG, "null context");
+    if (nranks) *nranks = ctx->nranks;
+    if (rank) *rank = ctx->rank;
+    if (allreduce)
+      *allreduce = !ctx->distributed()                 ? EIG_AR_NONE
+                   : (ctx->mbox && ctx->mbox->ready)   ? EIG_AR_MAILBOX
+                   : ctx->loop                         ? EIG_AR_LOOPBACK
+                                                       : EIG_AR_RCCL;
+    if (mailbox_errors)
+    {
+      *mailbox_errors = 0;
+      if (ctx->mbox && ctx->mbox->ready)
+      {
+        DeviceGuard dg(ctx->device);
+        EIG_HIP(hipStreamSynchronize(ctx->stream));
+        EIG_HIP(hipMemcpy(mailbox_errors, ctx->mbox->dev.err, sizeof(int), hipMemcpyDeviceToHost));
+      }
+    }
   });
 }
 
@@ -289,7 +487,7 @@ extern "C" int eig_comm_init_loopback(eig_ctx_t ctx, void *hub, int rank)
   return guard(ctx, [&] {
     auto *h = static_cast<LoopHub *>(hub);
     EIG_CHECK(ctx && h && rank >= 0 && rank < h->P, EIG_ERR_ARG, "eig_comm_init_loopback: bad arguments");
-    EIG_CHECK(!ctx->comm, EIG_ERR_ARG, "context already has an RCCL communicator");
+    EIG_CHECK(!ctx->comm && !ctx->mbox, EIG_ERR_ARG, "context already has a transport");
     ctx->loop = h;
     ctx->nranks = h->P;
     ctx->rank = rank;

@@ -16,6 +16,7 @@ namespace eigmi {
 
 typedef int64_t i64;
 typedef int32_t i32;
+typedef uint64_t u64;
 
 // Status-carrying exception used inside the library; every C entry point catches it and turns
 // it into the int status + eig_last_error message.
@@ -90,6 +91,27 @@ struct LoopHub {
   }
 };
 
+// xGMI mailbox allreduce (k_comm.hip): each rank's uncached mailbox, IPC-mapped by every peer.
+constexpr int kMaxMailboxRanks = 16;
+constexpr int kMailboxVals = 63;  // values per call (slot = 1 sequence word + 63 values = 512 B)
+struct Mailbox {
+  u64 *local = nullptr;                  // my mailbox: [2][P][1 + kMailboxVals]
+  u64 *peer[kMaxMailboxRanks] = {};      // peer[r] = rank r's mailbox mapped here (peer[me] = local)
+  u64 *ctr = nullptr;                    // device: sequence number of the last completed call
+  int *err = nullptr;                    // device: set when a call timed out
+  int P = 1, me = 0;
+};
+// Host-side ownership of the mailbox resources of a context.
+struct MailboxHost {
+  Mailbox dev;
+  u64 *local = nullptr;          // hipExtMallocWithFlags allocation (exported)
+  void *state = nullptr;         // ctr + err (hipMalloc)
+  std::vector<void *> opened;    // IPC-opened peer mappings (closed on destroy)
+  bool ready = false;            // peers opened and validated: allreduce_sum uses it
+};
+constexpr unsigned long long kMailboxTimeout = 1000000000ull;  // 10 s of s_memrealtime (100 MHz)
+void launch_mailbox_allreduce(double *buf, int count, const Mailbox &mb, unsigned long long timeout, hipStream_t s);
+
 }  // namespace eigmi
 
 struct eig_ctx_s {
@@ -103,8 +125,9 @@ struct eig_ctx_s {
   // RCCL
   ncclComm_t comm = nullptr;
   eigmi::LoopHub *loop = nullptr;    // in-process loopback transport (tests), exclusive with comm
+  eigmi::MailboxHost *mbox = nullptr; // xGMI mailbox allreduce (with RCCL, or alone for tests)
   int nranks = 1, rank = 0;
-  bool distributed() const { return nranks > 1 && (comm || loop); }
+  bool distributed() const { return nranks > 1 && (comm || loop || (mbox && mbox->ready)); }
   // reusable device buffers for drivers (grown on demand)
   std::vector<std::pair<void *, size_t>> pool;
 };

@@ -17,6 +17,8 @@ ORTHO_MGS, ORTHO_CHOLQR = 0, 1
 WHICH_LA, WHICH_SA = 0, 1
 LANCZOS_TIME_KERNELS = 1
 LANCZOS_TIME_DETAIL = 2
+IPC_HANDLE_BYTES = 64
+ALLREDUCE_KINDS = {0: "none", 1: "rccl", 2: "xgmi-mailbox", 3: "loopback"}
 
 
 def _tflags(timed):
@@ -74,6 +76,10 @@ SIGNATURES = {
     "eig_loopback_create": (_int, [_int, ctypes.POINTER(_vp)]),
     "eig_loopback_destroy": (_int, [_vp]),
     "eig_comm_init_loopback": (_int, [_vp, _vp, _int]),
+    "eig_comm_ipc_handle": (_int, [_vp, _int, _int, ctypes.c_char_p]),
+    "eig_comm_ipc_open": (_int, [_vp, ctypes.c_char_p]),
+    "eig_comm_info": (_int, [_vp, ctypes.POINTER(_int), ctypes.POINTER(_int), ctypes.POINTER(_int),
+                             ctypes.POINTER(_int)]),
     "eig_malloc": (_int, [_vp, ctypes.c_size_t, ctypes.POINTER(_vp)]),
     "eig_free": (_int, [_vp, _vp]),
     "eig_memcpy_h2d": (_int, [_vp, _vp, _vp, ctypes.c_size_t]),
@@ -193,6 +199,27 @@ class Context:
 
     def barrier(self):
         self.check(lib.eig_comm_barrier(self.h))
+
+    def ipc_handle(self, nranks, rank):
+        """Export this rank's xGMI mailbox (64 bytes); see eig_comm_ipc_handle."""
+        buf = ctypes.create_string_buffer(IPC_HANDLE_BYTES)
+        self.check(lib.eig_comm_ipc_handle(self.h, nranks, rank, buf))
+        return buf.raw
+
+    def ipc_open(self, handles):
+        """handles: the nranks exported handles concatenated in rank order."""
+        self.check(lib.eig_comm_ipc_open(self.h, bytes(handles)))
+        info = self.comm_info()
+        self.nranks, self.rank = info["nranks"], info["rank"]
+
+    def allreduce_sum(self, arr, count=None):
+        self.check(lib.eig_comm_allreduce_sum(self.h, arr.ptr, arr.n if count is None else count))
+
+    def comm_info(self):
+        v = [_int(0) for _ in range(4)]
+        self.check(lib.eig_comm_info(self.h, *[ctypes.byref(x) for x in v]))
+        return {"nranks": v[0].value, "rank": v[1].value, "allreduce": ALLREDUCE_KINDS[v[2].value],
+                "mailbox_errors": v[3].value}
 
     # --- memory
     def empty(self, n):

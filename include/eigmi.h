@@ -74,6 +74,19 @@ int eig_loopback_create(int nranks, void **hub);
 int eig_loopback_destroy(void *hub);
 int eig_comm_init_loopback(eig_ctx_t ctx, void *hub, int rank);
 int eig_comm_barrier(eig_ctx_t ctx);
+/* Allreduce transport.  With RCCL, eig_comm_init also sets up the xGMI mailbox allreduce (every
+ * rank exports a small uncached mailbox through IPC; one launch stores this rank's values into
+ * every peer's mailbox and sums all slots in rank order) for up to 16 ranks, validated and agreed
+ * by all ranks, else ncclAllReduce stays in use; EIGMI_ALLREDUCE=rccl forces RCCL.
+ * eig_comm_ipc_handle / eig_comm_ipc_open attach the mailbox alone (no RCCL; allreduce and dots
+ * only -- distributed matrices need RCCL or loopback): every rank exports its handle, the
+ * nranks x 64 bytes travel by any side channel (rank order), then every rank opens them. */
+#define EIG_IPC_HANDLE_BYTES 64
+enum eig_allreduce_kind { EIG_AR_NONE = 0, EIG_AR_RCCL = 1, EIG_AR_MAILBOX = 2, EIG_AR_LOOPBACK = 3 };
+int eig_comm_ipc_handle(eig_ctx_t ctx, int nranks, int rank, unsigned char handle[EIG_IPC_HANDLE_BYTES]);
+int eig_comm_ipc_open(eig_ctx_t ctx, const unsigned char *handles);
+/* nranks / rank / the allreduce in use (eig_allreduce_kind) / mailbox timeouts so far (syncs). */
+int eig_comm_info(eig_ctx_t ctx, int *nranks, int *rank, int *allreduce, int *mailbox_errors);
 
 /* ---------------------------------------------------------------- device memory ------------ */
 int eig_malloc(eig_ctx_t ctx, size_t bytes, void **ptr);
