@@ -31,9 +31,9 @@ import eigmi  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 
 
-def cpu_baseline(N, rp, c, v, steps, gpu_alpha):
-    """The reference CPU path's Lanczos step (oracle restatement: a3 SpMV + the BLAS-1 loops of
-    ARPACK), single thread, on the same matrix and start vector; a bounded sample of steps."""
+def cpu_baseline(N, rp, c, v, steps, gpu_alpha, fused):
+    """The Lanczos step on the CPU (oracle restatement: a3 SpMV + the BLAS-1 loops of ARPACK; the
+    same variant the GPU ran), single thread, same matrix and start vector; a bounded sample."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # noqa: E402  (checker / baseline only)
     n = N ** 3
@@ -41,7 +41,10 @@ def cpu_baseline(N, rp, c, v, steps, gpu_alpha):
     oracle.lib.orc_random_vec(n, 123, u0)
     alpha, beta = np.zeros(steps), np.zeros(steps + 1)
     t0 = time.perf_counter()
-    oracle.lib.orc_lanczos_rotating(n, rp, c, v, steps, u0, u1, u2, alpha, beta)
+    if fused:
+        oracle.lib.orc_lanczos_fused(n, rp, c, v, steps, u0, alpha, beta)
+    else:
+        oracle.lib.orc_lanczos_rotating(n, rp, c, v, steps, u0, u1, u2, alpha, beta)
     dt = time.perf_counter() - t0
     k = min(steps, len(gpu_alpha))
     rel = float(np.max(np.abs(alpha[:k] - gpu_alpha[:k]) / np.abs(alpha[:k]))) if k else None
@@ -79,6 +82,9 @@ def main():
     ap.add_argument("--cpu-steps", type=int, default=160, help="Lanczos steps of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-events", action="store_true", help="skip per-kernel HIP events")
+    ap.add_argument("--variant", choices=["fused", "classic"], default="fused",
+                    help="fused: one kernel + one 3-value allreduce per step (EIG_LANCZOS_FUSED); "
+                         "classic: SpMV kernel + update kernel, two allreduces")
     ap.add_argument("--launch", choices=["auto", "graph", "eager"], default="auto",
                     help="timed steps as one hipGraph replay or launched one by one; auto = graph when "
                          "N > 1 (host-bound halo/allreduce calls), eager at N = 1 (measured faster there)")
@@ -118,7 +124,8 @@ def main():
     nnz_local = int(rp[-1])
 
     K, W = args.steps, args.warmup
-    ws = eigmi.LanczosWorkspace(M, W + K, seed=123)
+    fused = args.variant == "fused"
+    ws = eigmi.LanczosWorkspace(M, W + K, seed=123, fused=fused)
     if W:
         ws.step(W)
     # the K timed steps are captured as one hipGraph before the clock starts (kernels, halo
@@ -141,13 +148,15 @@ def main():
     alpha, beta = ws.tridiag()
     ok = bool(np.all(np.isfinite(alpha)) and np.all(beta[1:] > 0))
 
-    # dominant kernel: the fused SpMV (k_lanczos_spmv_b1), HIP events on the library stream
-    k1_bytes = eigmi.bytes_lanczos_k1(cnt, nnz_local)
+    # dominant kernel: the step kernel (fused) or the SpMV kernel (classic), HIP events on the
+    # library stream around every launch of the timed region
+    kname = "k_lanczos_fused_b1" if fused else "k_lanczos_spmv_b1"
+    k1_bytes = eigmi.bytes_lanczos_fused(cnt, nnz_local) if fused else eigmi.bytes_lanczos_k1(cnt, nnz_local)
     k1_ms = tim.spmv_ms / K if tim.spmv_launches else None
     roofline = None
     if k1_ms:
         ach = k1_bytes / (k1_ms * 1e-3) / 1e9
-        tr = committed_traffic("k_lanczos_spmv_b1", N, world)
+        tr = committed_traffic(kname, N, world)
         roofline = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": tr[0] if tr else None,
                     "traffic_source": tr[1] if tr else None,
@@ -155,7 +164,7 @@ def main():
                     # than the CSR algorithmic count (column indices -> per-slice offsets + masks)
                     "traffic_GBs": round(tr[0] / (k1_ms * 1e-3) / 1e9, 1) if tr else None,
                     "traffic_frac": round(tr[0] / (k1_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if tr else None,
-                    "kernel": "k_lanczos_spmv_b1", "bytes_per_launch": k1_bytes,
+                    "kernel": kname, "bytes_per_launch": k1_bytes,
                     "avg_launch_us": round(k1_ms * 1e3, 2)}
     step_bytes = eigmi.bytes_lanczos_step(n, nnz_total)
     value = K / dt
@@ -172,9 +181,11 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (generated 7-point Poisson matrix, mt19937 seed-123 start vector)",
-        "config": {"workload": f"3D Poisson 7-pt {N}^3 Lanczos 3-term step, no re-orthogonalisation",
+        "config": {"workload": f"3D Poisson 7-pt {N}^3 Lanczos 3-term step, no re-orthogonalisation"
+                               f" ({'fused one-reduction step' if fused else 'SpMV + update kernels'})",
                    "N": N, "n": n, "nnz": nnz_total,
-                   "parallelism": f"row-partition z-slabs x{world} (RCCL halo, {ctx.comm_info()['allreduce']} allreduce)"},
+                   "parallelism": (f"row-partition z-slabs x{world} (RCCL halo, {ctx.comm_info()['allreduce']} "
+                                   "allreduce)") if world > 1 else "single GPU"},
         "step_hbm_gbs": round(step_bytes / (dt / K) / 1e9, 1),
         "step_roofline_frac": round(step_bytes / (dt / K) / 1e9 / HBM_PEAK_GBS / max(world, 1), 4),
         "roofline": roofline,
@@ -186,7 +197,7 @@ def main():
         "launch": "hipGraph replay of the K steps" if graph else "eager",
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cv, cdt, rel = cpu_baseline(N, rp, c, v, args.cpu_steps, alpha)
+        cv, cdt, rel = cpu_baseline(N, rp, c, v, args.cpu_steps, alpha, fused)
         out["cpu_baseline"] = {"value": round(cv, 4), "unit": "iters/s", "cores": 1, "kind": "port",
                                "sample": f"{args.cpu_steps} Lanczos steps on the same {N}^3 matrix and start "
                                          f"vector, oracle/oracle.cc single thread ({cdt:.1f} s)",

@@ -200,10 +200,11 @@ bool mailbox_validate(eig_ctx_t ctx)
 }
 
 // Exchange the ghost entries of the window-layout vector x.  Runs on stream s.
-void halo_exchange(const eig_mat_s &A, double *x, hipStream_t s)
+void halo_exchange(const eig_mat_s &A, double *x, hipStream_t s, double *x2, int width)
 {
   eig_ctx_t ctx = A.ctx;
   if (!ctx->distributed()) return;
+  const i64 w = width;
   if (ctx->loop)
   {
     // loopback: publish (x, window begin), then pull every recv range from the owner's vector
@@ -218,18 +219,28 @@ void halo_exchange(const eig_mat_s &A, double *x, hipStream_t s)
     for (const auto &r : A.recvs)
     {
       const i64 global = A.win_begin + r.offset;
-      const double *src = h.xptr[r.peer] + (global - h.win_begin[r.peer]);
-      EIG_HIP(hipMemcpyAsync(x + r.offset, src, r.count * sizeof(double), hipMemcpyDeviceToDevice, s));
+      const double *src = h.xptr[r.peer] + (global - h.win_begin[r.peer]) * w;
+      EIG_HIP(hipMemcpyAsync(x + r.offset * w, src, r.count * w * sizeof(double), hipMemcpyDeviceToDevice, s));
     }
     EIG_HIP(hipStreamSynchronize(s));
     h.barrier();
+    if (x2) halo_exchange(A, x2, s, nullptr, width);
     return;
   }
   if (A.sends.empty() && A.recvs.empty()) return;
   EIG_CHECK(ctx->comm, EIG_ERR_ARG, "halo exchange needs RCCL or the loopback transport");
   EIG_NCCL(ncclGroupStart());
-  for (const auto &r : A.recvs) EIG_NCCL(ncclRecv(x + r.offset, (size_t)r.count, ncclDouble, r.peer, ctx->comm, s));
-  for (const auto &r : A.sends) EIG_NCCL(ncclSend(x + r.offset, (size_t)r.count, ncclDouble, r.peer, ctx->comm, s));
+  // per peer, x then x2 on both sides: point-to-point operations match in issue order
+  for (const auto &r : A.recvs)
+  {
+    EIG_NCCL(ncclRecv(x + r.offset * w, (size_t)(r.count * w), ncclDouble, r.peer, ctx->comm, s));
+    if (x2) EIG_NCCL(ncclRecv(x2 + r.offset * w, (size_t)(r.count * w), ncclDouble, r.peer, ctx->comm, s));
+  }
+  for (const auto &r : A.sends)
+  {
+    EIG_NCCL(ncclSend(x + r.offset * w, (size_t)(r.count * w), ncclDouble, r.peer, ctx->comm, s));
+    if (x2) EIG_NCCL(ncclSend(x2 + r.offset * w, (size_t)(r.count * w), ncclDouble, r.peer, ctx->comm, s));
+  }
   EIG_NCCL(ncclGroupEnd());
 }
 

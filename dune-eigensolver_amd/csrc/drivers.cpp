@@ -39,7 +39,9 @@ int guard(eig_ctx_t ctx, F &&f)
 
 struct DevBuf {
   void *p = nullptr;
-  explicit DevBuf(size_t bytes) { EIG_HIP(hipMalloc(&p, bytes ? bytes : 1)); }
+  size_t n = 0;
+  explicit DevBuf(size_t bytes) : n(bytes) { EIG_HIP(hipMalloc(&p, bytes ? bytes : 1)); }
+  size_t bytes() const { return n; }
   ~DevBuf()
   {
     if (p) (void)hipFree(p);
@@ -196,14 +198,15 @@ struct LanczosBufs {
   DevBuf scal;
   LanczosState st;
   double *carry;
-  explicit LanczosBufs(int steps) : scal((size_t)(4 * (steps + 2) + 8) * sizeof(double))
+  explicit LanczosBufs(int steps) : scal((size_t)(7 * (steps + 2) + 8) * sizeof(double))
   {
     double *b = scal.d();
     st.dsum = b;
     st.nsum = b + (steps + 2);
     st.alpha = b + 2 * (steps + 2);
     st.beta = b + 3 * (steps + 2);
-    carry = b + 4 * (steps + 2);
+    st.fred = b + 4 * (steps + 2);
+    carry = b + 7 * (steps + 2);
   }
 };
 
@@ -255,6 +258,48 @@ void lanczos_step(eig_mat_s &A, double *u, double *up, double *t, int j, Lanczos
   mark(4);
 }
 
+// One fused step k (DESIGN.md "Fused step"): P = interleaved (t_{k-1}, u_{k-1}) pairs (window
+// layout, ghosts exchanged here), writes the pairs (t_k, u_k) into Pout; one allreduce of
+// (dsum_k, tsq_k, m_k).  Events as lanczos_step: ev[0] before, ev[1] after the kernel, ev[2..4]
+// after the allreduce.
+void lanczos_fused_step(eig_mat_s &A, double *P, double *Pout, int k, LanczosBufs &lb, hipEvent_t *ev, int nev,
+                        hipEvent_t halo_ev0, hipEvent_t halo_ev1, bool ev_external)
+{
+  eig_ctx_t ctx = A.ctx;
+  hipStream_t s = ctx->stream;
+  auto mark = [&](int i) {
+    if (ev && i < nev)
+      EIG_HIP(hipEventRecordWithFlags(ev[i], s, ev_external ? hipEventRecordExternal : hipEventRecordDefault));
+  };
+  double *out = lb.st.fred + 3 * (i64)k;
+  mark(0);
+  if (!distributed(A) || (A.recvs.empty() && A.sends.empty()) || ctx->loop)
+  {
+    if (distributed(A)) halo_exchange(A, P, s, nullptr, 2);  // loopback transport: synchronous exchange
+    launch_lanczos_fused(A, P, Pout, k, lb.st, nullptr, 0, A.nslices, nullptr, out, 0, s, ctx->red);
+  }
+  else
+  {
+    EIG_HIP(hipEventRecord(halo_ev0, s));
+    EIG_HIP(hipStreamWaitEvent(ctx->comm_stream, halo_ev0, 0));
+    halo_exchange(A, P, ctx->comm_stream, nullptr, 2);
+    EIG_HIP(hipEventRecord(halo_ev1, ctx->comm_stream));
+    const bool has_in = A.n_interior > 0, has_bd = A.n_boundary > 0;
+    if (has_in)
+      launch_lanczos_fused(A, P, Pout, k, lb.st, A.slice_list, 0, A.n_interior, nullptr, has_bd ? lb.carry : out, 0,
+                           s, ctx->red);
+    EIG_HIP(hipStreamWaitEvent(s, halo_ev1, 0));
+    if (has_bd)
+      launch_lanczos_fused(A, P, Pout, k, lb.st, A.slice_list, A.n_interior, A.n_boundary,
+                           has_in ? lb.carry : nullptr, out, 0, s, ctx->red);
+  }
+  mark(1);
+  allreduce_sum(ctx, out, 3, s);
+  mark(2);
+  mark(3);
+  mark(4);
+}
+
 // Start vector into the owned rows of a zeroed window buffer: u0 (device, window layout) or
 // mt19937(seed) normal numbers for the GLOBAL vector, of which this rank keeps its rows.
 void init_start(eig_mat_s &A, double *U0, const double *u0, unsigned seed)
@@ -282,7 +327,8 @@ void init_start(eig_mat_s &A, double *U0, const double *u0, unsigned seed)
 struct eig_lanczos_s {
   eig_mat_s *A = nullptr;
   int max_steps = 0, k = 0;
-  DevBuf *B[3] = {nullptr, nullptr, nullptr};
+  bool fused = false;  // EIG_LANCZOS_FUSED: B = {P0, P1} (2-wide pair vectors); else B = {u_j rotation of 3}
+  DevBuf *B[4] = {nullptr, nullptr, nullptr, nullptr};
   LanczosBufs *lb = nullptr;
   hipEvent_t h0 = nullptr, h1 = nullptr;
   // pending eig_lanczos_capture batch (graph == nullptr with g_steps > 0: eager fallback)
@@ -332,13 +378,20 @@ void enqueue_steps(eig_lanczos_s &ws, int steps, int nps, hipEvent_t *ev, bool e
   eig_mat_s &A = *ws.A;
   hipStream_t s = A.ctx->stream;
   const unsigned fl = external ? hipEventRecordExternal : hipEventRecordDefault;
-  double *U[3] = {ws.B[0]->d(), ws.B[1]->d(), ws.B[2]->d()};
   EIG_HIP(hipEventRecordWithFlags(ev[0], s, fl));
   for (int i = 0; i < steps; ++i)
   {
     const int j = ws.k + i;
-    lanczos_step(A, U[j % 3], U[(j + 2) % 3], U[(j + 1) % 3], j, *ws.lb, nps ? ev + 2 + (size_t)nps * i : nullptr,
-                 nps, ws.h0, ws.h1, external);
+    hipEvent_t *e = nps ? ev + 2 + (size_t)nps * i : nullptr;
+    if (ws.fused)
+    {
+      lanczos_fused_step(A, ws.B[j & 1]->d(), ws.B[(j + 1) & 1]->d(), j, *ws.lb, e, nps, ws.h0, ws.h1, external);
+    }
+    else
+    {
+      double *U[3] = {ws.B[0]->d(), ws.B[1]->d(), ws.B[2]->d()};
+      lanczos_step(A, U[j % 3], U[(j + 2) % 3], U[(j + 1) % 3], j, *ws.lb, e, nps, ws.h0, ws.h1, external);
+    }
   }
   EIG_HIP(hipEventRecordWithFlags(ev[1], s, fl));
 }
@@ -378,8 +431,15 @@ void read_timing(const std::vector<hipEvent_t> &ev, int steps, int nps, eig_timi
 
 extern "C" int eig_lanczos_create(eig_mat_t A, int max_steps, const double *u0, unsigned seed, eig_lanczos_t *out)
 {
+  return eig_lanczos_create_ex(A, max_steps, u0, seed, 0, out);
+}
+
+extern "C" int eig_lanczos_create_ex(eig_mat_t A, int max_steps, const double *u0, unsigned seed, int flags,
+                                     eig_lanczos_t *out)
+{
   return guard(A ? A->ctx : nullptr, [&] {
     EIG_CHECK(A && out && max_steps >= 0, EIG_ERR_ARG, "eig_lanczos_create: bad argument");
+    EIG_CHECK((flags & ~EIG_LANCZOS_FUSED) == 0, EIG_ERR_ARG, "eig_lanczos_create_ex: unknown flag");
     check_lanczos_matrix(A);
     eig_ctx_t ctx = A->ctx;
     EIG_HIP(hipSetDevice(ctx->device));
@@ -389,13 +449,24 @@ extern "C" int eig_lanczos_create(eig_mat_t A, int max_steps, const double *u0, 
     {
       ws->A = A;
       ws->max_steps = max_steps;
+      ws->fused = (flags & EIG_LANCZOS_FUSED) != 0;
       const size_t wb = (size_t)A->window * sizeof(double);
-      for (auto &b : ws->B) b = new DevBuf(wb);
-      EIG_HIP(hipMemsetAsync(ws->B[1]->d(), 0, wb, s));
-      EIG_HIP(hipMemsetAsync(ws->B[2]->d(), 0, wb, s));
-      init_start(*A, ws->B[0]->d(), u0, seed);
+      for (int i = 0; i < 3; ++i)
+      {
+        // fused: B[0], B[1] = pair vectors (2 doubles per row), B[2] = start vector scratch
+        ws->B[i] = new DevBuf(ws->fused && i < 2 ? 2 * wb : wb);
+        if (i) EIG_HIP(hipMemsetAsync(ws->B[i]->d(), 0, ws->B[i]->bytes(), s));
+      }
+      double *U0 = ws->fused ? ws->B[2]->d() : ws->B[0]->d();
+      init_start(*A, U0, u0, seed);
       ws->lb = new LanczosBufs(max_steps);
-      launch_nrm2sq(A->nb_rows, ws->B[0]->d() + A->own_offset, ws->lb->st.nsum, 0, s, ctx->red);
+      launch_nrm2sq(A->nb_rows, U0 + A->own_offset, ws->lb->st.nsum, 0, s, ctx->red);
+      if (ws->fused)  // P0 = (u_0, 0) interleaved; the whole window (ghosts are refilled per step)
+      {
+        EIG_HIP(hipMemsetAsync(ws->B[0]->d(), 0, 2 * wb, s));
+        EIG_HIP(hipMemcpy2DAsync(ws->B[0]->d(), 2 * sizeof(double), U0, sizeof(double), sizeof(double), A->window,
+                                 hipMemcpyDeviceToDevice, s));
+      }
       allreduce_sum(ctx, ws->lb->st.nsum, 1, s);
       EIG_HIP(hipEventCreateWithFlags(&ws->h0, hipEventDisableTiming));
       EIG_HIP(hipEventCreateWithFlags(&ws->h1, hipEventDisableTiming));
@@ -511,7 +582,10 @@ extern "C" int eig_lanczos_tridiag(eig_lanczos_t ws, int *k, double *alpha_host,
     EIG_CHECK(ws, EIG_ERR_ARG, "eig_lanczos_tridiag: null workspace");
     eig_ctx_t ctx = ws->A->ctx;
     EIG_HIP(hipSetDevice(ctx->device));
-    launch_beta_tail(ws->lb->st, ws->k, ctx->stream);
+    if (ws->fused)
+      launch_fused_tail(ws->lb->st, ws->k, ctx->stream);
+    else
+      launch_beta_tail(ws->lb->st, ws->k, ctx->stream);
     EIG_HIP(hipStreamSynchronize(ctx->stream));
     if (k) *k = ws->k;
     if (alpha_host && ws->k > 0)
@@ -533,9 +607,9 @@ extern "C" int eig_lanczos_run(eig_mat_t A, int steps, const double *u0, unsigne
                                double *beta_host, eig_timing *timing)
 {
   eig_lanczos_t ws = nullptr;
-  int rc = eig_lanczos_create(A, steps, u0, seed, &ws);
+  int rc = eig_lanczos_create_ex(A, steps, u0, seed, flags & EIG_LANCZOS_FUSED, &ws);
   if (rc != EIG_OK) return rc;
-  rc = eig_lanczos_step(ws, steps, flags, timing);
+  rc = eig_lanczos_step(ws, steps, flags & ~EIG_LANCZOS_FUSED, timing);
   if (rc == EIG_OK) rc = eig_lanczos_tridiag(ws, nullptr, alpha_host, beta_host);
   eig_lanczos_destroy(ws);
   return rc;

@@ -198,7 +198,13 @@ struct LanczosState {
   double *nsum;   // nsum[j]  = ||u_j||^2 (local, then allreduced); nsum[0] from the start vector
   double *alpha;  // alpha[j]
   double *beta;   // beta[j]  = sqrt(nsum[j])
+  double *fred;   // fused step: fred[3k..3k+2] = (t_k . u_k, t_k . t_k, u_k . u_k) (local, then allreduced)
 };
+// P, Pout: interleaved (t, u) pair vectors in window layout (2 doubles per row).
+void launch_lanczos_fused(const eig_mat_s &A, const double *P, double *Pout, int k,
+                          const LanczosState &st, const i32 *slices, i64 first, i64 count, const double *carry,
+                          double *out, int ticket, hipStream_t s, ReduceWS red);
+void launch_fused_tail(const LanczosState &st, int K, hipStream_t s);
 void launch_lanczos_spmv(const eig_mat_s &A, const double *u, const double *up, double *t, int j,
                          const LanczosState &st, const i32 *slices, i64 first, i64 count, double *dot_out,
                          double *beta_out, const double *carry, int ticket, hipStream_t s, ReduceWS red);
@@ -244,7 +250,9 @@ void launch_resid_sq(i64 n, const double *x, const double *y, double theta, doub
                      hipStream_t s, ReduceWS red);
 
 // ---- helpers in api.cpp --------------------------------------------------------------------
-void halo_exchange(const eig_mat_s &A, double *x, hipStream_t s);
+// Ghost entries of window vector x (and x2 when given) from their owners.
+// width: doubles per row of x (2 for the fused step's interleaved pair vectors).
+void halo_exchange(const eig_mat_s &A, double *x, hipStream_t s, double *x2 = nullptr, int width = 1);
 void mv_device(eig_mat_s &A, double *x, double *y);
 void gram_device(eig_ctx_t ctx, i64 n, i64 m1, i64 m2, const double *Q1, const double *Q2, double *G);
 void orthonormalize_device(eig_ctx_t ctx, i64 n, i64 m, double *Q, int variant);

@@ -50,20 +50,66 @@ __device__ __forceinline__ i32 lane_geti(const typename Vec<R>::i &v, int q)
   else return v[q];
 }
 
-__device__ __forceinline__ void chunk_of(i64 count, i64 &b, i64 &e)
+// Chunk order is XCD-aware: workgroups are dealt round-robin over the 8 XCDs (MI355X_MICROARCH
+// "Workgroup dispatch"), so workgroup b takes logical chunk swz(b) and each XCD walks ONE
+// contiguous eighth of the slices -- the stencil's +-plane neighbours of a workgroup's rows are
+// then the current rows of workgroups on the same XCD (its L2) instead of another XCD's.
+// Bijective for any grid size (the first G % 8 groups hold one workgroup more).  OFF by default:
+// measured (tools/lanczos_sweep.py, 256^3) +12 us on the two-kernel K1 and +24 us on the 8-wave
+// fused kernel -- the 256 MB MALL already serves the plane re-reads; EIGMI_XCD_SWIZZLE=1 enables.
+__device__ __forceinline__ i64 swizzled_block(int swz)
+{
+  const int G = gridDim.x, bid = blockIdx.x;
+  if (!swz || G < 16) return bid;
+  const int q = G >> 3, r = G & 7, x = bid & 7, i = bid >> 3;
+  return (i64)(x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
+}
+
+__device__ __forceinline__ void chunk_of(i64 count, i64 &b, i64 &e, int swz = 0)
 {
   const i64 G = gridDim.x;
   const i64 per = (count + G - 1) / G;
-  b = (i64)blockIdx.x * per;
+  b = swizzled_block(swz) * per;
   e = b + per;
   if (e > count) e = count;
 }
 
+static int nt_store()
+{
+  const char *e = std::getenv("EIGMI_NT_STORE");
+  return (e && e[0] == '1') ? 1 : 0;
+}
+
+static int xcd_swizzle()
+{
+  const char *e = std::getenv("EIGMI_XCD_SWIZZLE");
+  return (e && e[0] == '1') ? 1 : 0;
+}
+
+// Gathered operand x[g]: a plain vector, or the fused Lanczos step's u_k = t_{k-1} - c u_{k-1}
+// formed on the fly from the interleaved (t, u) pair vector (mul then sub, -ffp-contract=off:
+// bitwise what the step stores for u_k).
+struct XPlain {
+  const double *__restrict__ x;
+  __device__ __forceinline__ double operator()(i64 g) const { return x[g]; }
+};
+// (t, u) interleaved: one 16-B gather fetches both operands of an entry.
+typedef double dpair __attribute__((ext_vector_type(2)));
+struct XPair {
+  const dpair *__restrict__ p;
+  double c;
+  __device__ __forceinline__ double operator()(i64 g) const
+  {
+    const dpair v = p[g];
+    return v.x - c * v.y;
+  }
+};
+
 // acc[q] = sum_k a[k][q] * x[c[k][q]] for the R rows of this lane, k ascending.  KC entries are
 // prefetched per round (8 (value, column) loads in flight per lane for every R).
-template <int R>
-__device__ __forceinline__ void rows_dot(const double *__restrict__ val, const i32 *__restrict__ col,
-                                         const double *__restrict__ x, i64 base, int width, int lane, double (&acc)[R])
+template <int R, class X>
+__device__ __forceinline__ void rows_dot(const double *__restrict__ val, const i32 *__restrict__ col, const X &x,
+                                         i64 base, int width, int lane, double (&acc)[R])
 {
   constexpr int C = 64 * R;
   constexpr int KC = 8 / R;
@@ -100,7 +146,7 @@ __device__ __forceinline__ void rows_dot(const double *__restrict__ val, const i
       for (int q = 0; q < R; ++q)
       {
         const i32 cc = lane_geti<R>(c[k], q);
-        xv[k][q] = (cc >= 0) ? x[cc] : 0.0;
+        xv[k][q] = (cc >= 0) ? x(cc) : 0.0;
       }
 #pragma unroll
     for (int k = 0; k < KC; ++k)
@@ -112,9 +158,9 @@ __device__ __forceinline__ void rows_dot(const double *__restrict__ val, const i
 
 // Stencil slice: entry k of row r is stored iff bit k of mask[r]; its column is r + own + delta_k
 // (window-local).  Offsets ascend, so each row still accumulates in ascending-column order.
-template <int R>
+template <int R, class X>
 __device__ __forceinline__ void rows_dot_stencil(const double *__restrict__ val, const i32 *__restrict__ delta,
-                                                 const uint8_t *__restrict__ mask, const double *__restrict__ x,
+                                                 const uint8_t *__restrict__ mask, const X &x,
                                                  i64 base, int width, int lane, i64 xrow0, i64 xlast,
                                                  double (&acc)[R])
 {
@@ -148,7 +194,7 @@ __device__ __forceinline__ void rows_dot_stencil(const double *__restrict__ val,
       {
         i64 g = xrow0 + q + dk[k];
         g = g < 0 ? 0 : (g > xlast ? xlast : g);
-        xv[k][q] = x[g];
+        xv[k][q] = x(g);
       }
 #pragma unroll
     for (int k = 0; k < KC; ++k)
@@ -166,30 +212,38 @@ struct SellB1 {
   const i32 *st_delta;
   const uint8_t *st_mask;
   i64 xlast;  // window length - 1 (gather clamp)
+  int swz;    // XCD-aware chunk order (chunk_of)
+  int nts;    // nontemporal stores of the step vectors (EIGMI_NT_STORE)
 };
+
+// Store of a streamed result vector entry: nontemporal (no L2 allocation) when A.nts.
+__device__ __forceinline__ void put(double *p, double v, int nts)
+{
+  if (nts) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
 
 // Image modes: every slice explicit, every slice stencil, or mixed (per-slice wave-uniform branch).
 enum { kExplicit = 0, kStencil = 1, kMixed = 2 };
 
 // Row sums of slice s for this lane's R rows.
-template <int R, int MODE>
-__device__ __forceinline__ void slice_dot(const SellB1 &A, i64 s, const double *__restrict__ x, i64 own, int lane,
-                                          double (&acc)[R])
+template <int R, int MODE, class X>
+__device__ __forceinline__ void slice_dot(const SellB1 &A, i64 s, const X &x, i64 own, int lane, double (&acc)[R])
 {
   constexpr int C = 64 * R;
   const i64 base = A.slice_ptr[s];
   const int width = (int)((A.slice_ptr[s + 1] - base) / C);
   const bool st = (MODE == kStencil) || (MODE == kMixed && A.st_width[s] > 0);
   if (MODE != kExplicit && st)
-    rows_dot_stencil<R>(A.val, A.st_delta + 8 * s, A.st_mask + s * C, x, base, width, lane,
+    rows_dot_stencil<R, X>(A.val, A.st_delta + 8 * s, A.st_mask + s * C, x, base, width, lane,
                         own + s * C + (i64)lane * R, A.xlast, acc);
   else
-    rows_dot<R>(A.val, A.col, x, base, width, lane, acc);
+    rows_dot<R, X>(A.val, A.col, x, base, width, lane, acc);
 }
 
 static SellB1 sell_b1(const eig_mat_s &A)
 {
-  return SellB1{A.slice_ptr, A.val, A.col, A.st_width, A.st_delta, A.st_mask, A.window - 1};
+  return SellB1{A.slice_ptr, A.val, A.col, A.st_width, A.st_delta, A.st_mask, A.window - 1, xcd_swizzle(), nt_store()};
 }
 
 static int image_mode(const eig_mat_s &A)
@@ -215,12 +269,12 @@ __global__ __launch_bounds__(kStreamThreads, min_waves<MODE>()) void k_spmv_b1(i
   // wave index through readfirstlane: the slice loop, slice_ptr loads and row bases stay scalar
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   i64 b, e;
-  chunk_of(count, b, e);
+  chunk_of(count, b, e, A.swz);
   for (i64 it = b + wave; it < e; it += kWaves)
   {
     const i64 s = slices ? (i64)slices[first + it] : first + it;
     double acc[R];
-    slice_dot<R, MODE>(A, s, x, own, lane, acc);
+    slice_dot<R, MODE>(A, s, XPlain{x}, own, lane, acc);
     const i64 r0 = s * C + (i64)lane * R;
 #pragma unroll
     for (int q = 0; q < R; ++q)
@@ -301,7 +355,7 @@ __global__ __launch_bounds__(kStreamThreads, min_waves<MODE>()) void k_lanczos_s
   const double sig = 1.0 / beta;
   const double gam = (j > 0) ? beta * (1.0 / sqrt(nsum[j - 1])) : 0.0;
   i64 b, e;
-  chunk_of(count, b, e);
+  chunk_of(count, b, e, A.swz);
   double d = 0.0;
   for (i64 it = b + wave; it < e; it += kWaves)
   {
@@ -317,7 +371,7 @@ __global__ __launch_bounds__(kStreamThreads, min_waves<MODE>()) void k_lanczos_s
       uv[q] = ok ? u[own + r0 + q] : 0.0;
     }
     double acc[R];
-    slice_dot<R, MODE>(A, s, u, own, lane, acc);
+    slice_dot<R, MODE>(A, s, XPlain{u}, own, lane, acc);
 #pragma unroll
     for (int q = 0; q < R; ++q)
     {
@@ -326,7 +380,7 @@ __global__ __launch_bounds__(kStreamThreads, min_waves<MODE>()) void k_lanczos_s
       {
         double ti = acc[q] * sig;
         if (j > 0) ti = ti - gam * upv[q];
-        t[own + r] = ti;
+        put(t + own + r, ti, A.nts);
         d += ti * uv[q];
       }
     }
@@ -340,6 +394,183 @@ __global__ __launch_bounds__(kStreamThreads, min_waves<MODE>()) void k_lanczos_s
       if (beta_out) beta_out[0] = beta;
     }
   }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Fused one-reduction Lanczos step (DESIGN.md "Fused step").  u_k = t_{k-1} - c u_{k-1} is formed
+// inside the gathers of the SpMV that needs it (XComb), and its squared norm is PREDICTED from the
+// previous step's reductions instead of being reduced before the SpMV:
+//   c = dsum/m,  nt_k = tsq - c dsum       (m = measured ||u_{k-1}||^2, reduced when u_{k-1} was
+//                                             formed; using it keeps the prediction error at
+//                                             rounding level -- tsq - alpha^2 alone diverges)
+//   t_k = (A u_k) sig_k - gam_k u_{k-1},  sig_k = 1/sqrt(nt_k)
+//   (dsum_k, tsq_k, m_k) = (t_k . u_k, t_k . t_k, u_k . u_k)   -> ONE allreduce of 3 doubles
+// P is the WINDOW buffer of the interleaved pairs (t_{k-1}, u_{k-1}) (ghosts exchanged); the pairs
+// (t_k, u_k) go to the owned rows of Pout.  Step 0: P = (u_0, 0), c = gam = 0.  out[0..2] receive the three sums (red + 3k,
+// or a carry slot for the interior half of a split step); red[3(k-1)..] are the previous step's
+// allreduced sums; block 0 stores nsum[k] = nt_k, alpha[k-1], beta[k].  Same formulas as
+// orc_lanczos_fused (oracle.cc).
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ void fused_scalars(double nt_prev, double d, double q, double m, double &c,
+                                              double &alpha_prev, double &nt, double &beta, double &gam)
+{
+  const double rn = sqrt(nt_prev);
+  const double rm = sqrt(m);
+  c = d / m;
+  alpha_prev = c * rn;
+  nt = q - c * d;
+  beta = sqrt(nt) * rn / rm;
+  gam = beta / rm;
+}
+
+// Fused step, one stencil slice, one row per lane: gathers the (t, u) pairs at the slice's offsets
+// (16-B loads, clamped addresses as rows_dot_stencil), accumulates sum a (t - c u) in offset order
+// and takes the row's own (t, u) from the delta = 0 gather instead of a separate load.  KC entries
+// in flight per round.  Same arithmetic and order as the generic path (bitwise equal).
+template <int KC>
+__device__ __forceinline__ void fused_row_stencil(const SellB1 &A, i64 s, const dpair *__restrict__ P, double c,
+                                                  i64 own, int lane, double &acc, double &tv, double &uv)
+{
+  const i64 base = A.slice_ptr[s];
+  const int width = (int)((A.slice_ptr[s + 1] - base) >> 6);
+  const i32 *dl = A.st_delta + 8 * s;
+  const unsigned m = A.st_mask[s * 64 + lane];
+  const double *vs = A.val + base;
+  const i64 xrow0 = own + s * 64 + lane;
+  const i64 xl = A.xlast;
+  acc = 0.0;
+  bool centre = false;  // wave-uniform: the offset list holds delta = 0
+  for (int k0 = 0; k0 < width; k0 += KC)
+  {
+    double a[KC];
+    dpair pr[KC];
+    int dk[KC];
+#pragma unroll
+    for (int k = 0; k < KC; ++k)
+    {
+      const bool in = k0 + k < width;
+      dk[k] = in ? dl[k0 + k] : 0;
+      a[k] = in ? __builtin_nontemporal_load(vs + (k0 + k) * 64 + lane) : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < KC; ++k)
+    {
+      i64 g = xrow0 + dk[k];
+      g = g < 0 ? 0 : (g > xl ? xl : g);
+      pr[k] = (k0 + k < width) ? P[g] : dpair{0.0, 0.0};
+    }
+#pragma unroll
+    for (int k = 0; k < KC; ++k)
+    {
+      if (k0 + k < width && dk[k] == 0)
+      {
+        tv = pr[k].x;
+        uv = pr[k].y;
+        centre = true;
+      }
+      if ((m >> (k0 + k)) & 1u) acc += a[k] * (pr[k].x - c * pr[k].y);
+    }
+  }
+  if (!centre)
+  {
+    const i64 g = xrow0 > xl ? xl : xrow0;
+    const dpair pv = P[g];
+    tv = pv.x;
+    uv = pv.y;
+  }
+}
+
+// W = waves per SIMD the register budget is sized for (W >= 8: stencil rows take 4 entries per
+// round to fit 64 VGPRs; EIGMI_FUSED_WAVES picks 4/5/6/8, see launch_lanczos_fused).
+template <int R, int MODE, int W>
+__global__ __launch_bounds__(kStreamThreads, W) void k_lanczos_fused_b1(
+    i64 nrows, i64 own, SellB1 A, const i32 *__restrict__ slices, i64 first, i64 count,
+    const dpair *__restrict__ P, dpair *__restrict__ Pout, int k, double *__restrict__ nsum, double *__restrict__ alpha,
+    double *__restrict__ beta, const double *__restrict__ red, double *__restrict__ out,
+    const double *__restrict__ carry, double *partials, unsigned *ticket)
+{
+  constexpr int C = 64 * R;
+  __shared__ double tot[3];
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  double nt, c = 0.0, gam = 0.0, ap = 0.0, bk = 0.0;
+  if (k > 0)
+    fused_scalars(nsum[k - 1], red[3 * (k - 1)], red[3 * (k - 1) + 1], red[3 * (k - 1) + 2], c, ap, nt, bk, gam);
+  else
+    nt = nsum[0];
+  const double sig = 1.0 / sqrt(nt);
+  if (blockIdx.x == 0 && threadIdx.x == 0)  // (both launches of a split step store the same values)
+  {
+    if (k > 0)
+    {
+      nsum[k] = nt;
+      alpha[k - 1] = ap;
+      beta[k] = bk;
+    }
+    else
+      beta[0] = sqrt(nt);
+  }
+  const XPair xc{P, c};
+  i64 b, e;
+  chunk_of(count, b, e, A.swz);
+  double d = 0.0, q2 = 0.0, m2 = 0.0;
+  for (i64 it = b + wave; it < e; it += kWaves)
+  {
+    const i64 s = slices ? (i64)slices[first + it] : first + it;
+    const i64 r0 = s * C + (i64)lane * R;
+    double tv[R], uv[R], acc[R];
+    if (R == 1 && MODE != kExplicit && (MODE == kStencil || A.st_width[s] > 0))
+    {
+      fused_row_stencil<(W >= 8 ? 4 : 8)>(A, s, P, c, own, lane, acc[0], tv[0], uv[0]);
+    }
+    else
+    {
+#pragma unroll
+      for (int q = 0; q < R; ++q)
+      {
+        const bool ok = r0 + q < nrows;
+        const dpair pv = ok ? P[own + r0 + q] : dpair{0.0, 0.0};
+        tv[q] = pv.x;
+        uv[q] = pv.y;
+      }
+      slice_dot<R, MODE>(A, s, xc, own, lane, acc);
+    }
+#pragma unroll
+    for (int q = 0; q < R; ++q)
+    {
+      const i64 r = r0 + q;
+      if (r < nrows)
+      {
+        const double uk = tv[q] - c * uv[q];
+        double ti = acc[q] * sig;
+        if (k > 0) ti = ti - gam * uv[q];
+        Pout[own + r] = dpair{ti, uk};
+        d += ti * uk;
+        q2 += ti * ti;
+        m2 += uk * uk;
+      }
+    }
+  }
+  double v[3] = {d, q2, m2};
+  if (grid_sum<3, kStreamThreads>(v, partials, ticket, tot))
+  {
+    if (threadIdx.x < 3) out[threadIdx.x] = carry ? (carry[threadIdx.x] + tot[threadIdx.x]) : tot[threadIdx.x];
+  }
+}
+
+// After the last fused step K-1: alpha[K-1], nsum[K], beta[K] (same formulas as the prologue).
+__global__ void k_fused_tail(double *nsum, double *alpha, double *beta, const double *red, int K)
+{
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  if (K > 0)
+  {
+    double c, ap, nt, bk, gam;
+    fused_scalars(nsum[K - 1], red[3 * (K - 1)], red[3 * (K - 1) + 1], red[3 * (K - 1) + 2], c, ap, nt, bk, gam);
+    alpha[K - 1] = ap;
+    nsum[K] = nt;
+    beta[K] = bk;
+  }
+  else
+    beta[0] = sqrt(nsum[0]);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -382,7 +613,7 @@ __global__ __launch_bounds__(kStreamThreads, MINW) void k_lanczos_spmv_st1_pipe(
   const double sig = 1.0 / beta;
   const double gam = (j > 0) ? beta * (1.0 / sqrt(nsum[j - 1])) : 0.0;
   i64 b, e;
-  chunk_of(count, b, e);
+  chunk_of(count, b, e, A.swz);
   double d = 0.0;
   i64 it = b + wave;
   StSlice cur;
@@ -557,6 +788,55 @@ void launch_lanczos_spmv(const eig_mat_s &A, const double *u, const double *up, 
 #undef EIG_LZM
 #undef EIG_LZ
 #undef EIG_PIPE
+}
+
+static int fused_waves()
+{
+  const char *e = std::getenv("EIGMI_FUSED_WAVES");
+  // 8 (default): 4 entries per round, 59 VGPRs, 340 us at 256^3; 5: 8 entries per round, 83 VGPRs,
+  // 341-343 us; 6 spills (350 us)
+  const int w = e ? std::atoi(e) : 8;
+  return (w == 4 || w == 5 || w == 6) ? w : 8;
+}
+
+void launch_lanczos_fused(const eig_mat_s &A, const double *P, double *Pout, int k,
+                          const LanczosState &st, const i32 *slices, i64 first, i64 count, const double *carry,
+                          double *out, int ticket, hipStream_t s, ReduceWS red)
+{
+  EIG_CHECK(A.br == 1 && A.bc == 1, EIG_ERR_BLOCKSIZE, "Lanczos driver: 1x1 blocks only");
+#define EIG_LF(R_, M_, W_)                                                                                    \
+  hipLaunchKernelGGL((k_lanczos_fused_b1<R_, M_, W_>),                                                       \
+                     dim3(grid_for_slices(k_lanczos_fused_b1<R_, M_, W_>, count, A.ctx->num_cu)),             \
+                     dim3(kStreamThreads), 0, s, A.nb_rows, A.own_offset, sell_b1(A), slices, first, count,      \
+                     reinterpret_cast<const dpair *>(P), reinterpret_cast<dpair *>(Pout), k, st.nsum, st.alpha,  \
+                     st.beta, st.fred, out, carry, red.partials,                                              \
+                     red.ticket(ticket))
+#define EIG_LFW(R_, M_)                                                                                       \
+  {                                                                                                           \
+    const int w_ = fused_waves();                                                                             \
+    if (w_ == 4) EIG_LF(R_, M_, 4);                                                                           \
+    else if (w_ == 5) EIG_LF(R_, M_, 5);                                                                      \
+    else if (w_ == 6) EIG_LF(R_, M_, 6);                                                                      \
+    else EIG_LF(R_, M_, 8);                                                                                   \
+  }
+#define EIG_LFM(R_)                                                                                           \
+  {                                                                                                           \
+    const int m_ = image_mode(A);                                                                             \
+    if (m_ == kExplicit) EIG_LFW(R_, kExplicit)                                                               \
+    else if (m_ == kStencil) EIG_LFW(R_, kStencil)                                                            \
+    else EIG_LFW(R_, kMixed)                                                                                  \
+  }
+  if (A.R == 1) EIG_LFM(1)
+  else if (A.R == 2) EIG_LFM(2)
+  else EIG_LFM(4)
+#undef EIG_LFM
+#undef EIG_LFW
+#undef EIG_LF
+}
+
+void launch_fused_tail(const LanczosState &st, int K, hipStream_t s)
+{
+  hipLaunchKernelGGL(k_fused_tail, dim3(1), dim3(64), 0, s, st.nsum, st.alpha, st.beta, st.fred, K);
 }
 
 }  // namespace eigmi

@@ -17,6 +17,7 @@ ORTHO_MGS, ORTHO_CHOLQR = 0, 1
 WHICH_LA, WHICH_SA = 0, 1
 LANCZOS_TIME_KERNELS = 1
 LANCZOS_TIME_DETAIL = 2
+LANCZOS_FUSED = 4
 IPC_HANDLE_BYTES = 64
 ALLREDUCE_KINDS = {0: "none", 1: "rccl", 2: "xgmi-mailbox", 3: "loopback"}
 
@@ -110,6 +111,7 @@ SIGNATURES = {
     "eig_lanczos_run": (_int, [_vp, _int, _vp, _u, _int, _vp, _vp, ctypes.POINTER(Timing)]),
     "eig_lanczos_solve": (_int, [_vp, _int, _int, _int, _u, _vp, _vp, _vp]),
     "eig_lanczos_create": (_int, [_vp, _int, _vp, _u, ctypes.POINTER(_vp)]),
+    "eig_lanczos_create_ex": (_int, [_vp, _int, _vp, _u, _int, ctypes.POINTER(_vp)]),
     "eig_lanczos_step": (_int, [_vp, _int, _int, ctypes.POINTER(Timing)]),
     "eig_lanczos_tridiag": (_int, [_vp, ctypes.POINTER(_int), _vp, _vp]),
     "eig_lanczos_destroy": (_int, [_vp]),
@@ -406,12 +408,13 @@ def standard_largest(A, shift, tol, maxiter, nev, seed=123, want_evec=True, verb
     return ev, (evec.reshape(nev, A.n) if want_evec else None), it.value
 
 
-def lanczos_run(A, steps, u0=None, seed=123, timed=False):
+def lanczos_run(A, steps, u0=None, seed=123, timed=False, fused=False):
+    """fused: the one-reduction single-kernel step (EIG_LANCZOS_FUSED) instead of K1 + K2."""
     alpha = np.zeros(max(steps, 1))
     beta = np.zeros(steps + 1)
     t = Timing()
     A.ctx.check(lib.eig_lanczos_run(A.h, steps, u0.ptr if u0 is not None else None, seed,
-                                    _tflags(timed), _np_ptr(alpha), _np_ptr(beta),
+                                    _tflags(timed) | (LANCZOS_FUSED if fused else 0), _np_ptr(alpha), _np_ptr(beta),
                                     ctypes.byref(t)))
     return alpha[:steps], beta, t
 
@@ -420,11 +423,12 @@ class LanczosWorkspace:
     """eig_lanczos_t: the three-term recurrence as a persistent workspace (setup outside any
     timed region; step() advances and returns the eig_timing of that batch)."""
 
-    def __init__(self, A, max_steps, u0=None, seed=123):
+    def __init__(self, A, max_steps, u0=None, seed=123, fused=False):
         self.A = A
+        self.fused = fused
         h = _vp()
-        A.ctx.check(lib.eig_lanczos_create(A.h, max_steps, u0.ptr if u0 is not None else None, seed,
-                                           ctypes.byref(h)))
+        A.ctx.check(lib.eig_lanczos_create_ex(A.h, max_steps, u0.ptr if u0 is not None else None, seed,
+                                              LANCZOS_FUSED if fused else 0, ctypes.byref(h)))
         self.h = h
 
     def step(self, steps, timed=False):
@@ -522,6 +526,12 @@ def bytes_lanczos_step(n, nnz):
 def bytes_lanczos_k1(n, nnz):
     """Fused SpMV kernel of a Lanczos step: CSR stream + x + y write + u_{j-1} read."""
     return bytes_spmv(n, nnz) + 8 * n
+
+
+def bytes_lanczos_fused(n, nnz):
+    """Fused one-reduction step kernel: CSR stream + gathers of t_{k-1} and u_{k-1} + writes of
+    t_k and u_k (the whole step; 16n fewer than bytes_lanczos_step)."""
+    return 12 * nnz + 4 * (n + 1) + 32 * n
 
 
 # --------------------------------------------------------------------------------------- planning

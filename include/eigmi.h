@@ -197,7 +197,12 @@ typedef struct eig_timing {
 } eig_timing;
 enum eig_lanczos_flags {
   EIG_LANCZOS_TIME_KERNELS = 1, /* HIP events around every fused SpMV launch (spmv_ms) */
-  EIG_LANCZOS_TIME_DETAIL = 2   /* + events after each allreduce and update (update_ms, comm_ms) */
+  EIG_LANCZOS_TIME_DETAIL = 2,  /* + events after each allreduce and update (update_ms, comm_ms) */
+  /* One-reduction fused step: ||u_{k}||^2 = ||t_{k-1}||^2 - alpha_{k-1}^2, so u_k is formed inside
+   * the next SpMV's gathers and a step is ONE kernel + ONE allreduce of two doubles (4 window
+   * vectors instead of 3).  Same Krylov process; alpha/beta agree with the two-kernel form to
+   * rounding (cancellation only when beta_{k} << |alpha_{k-1}|). */
+  EIG_LANCZOS_FUSED = 4
 };
 int eig_lanczos_run(eig_mat_t A, int steps, const double *u0, unsigned seed, int flags,
                     double *alpha_host, double *beta_host, eig_timing *timing);
@@ -209,6 +214,9 @@ int eig_lanczos_run(eig_mat_t A, int steps, const double *u0, unsigned seed, int
  * done so far.  No host synchronisation happens inside a step batch. */
 typedef struct eig_lanczos_s *eig_lanczos_t;
 int eig_lanczos_create(eig_mat_t A, int max_steps, const double *u0, unsigned seed, eig_lanczos_t *ws);
+/* flags: 0 (two-kernel step, as eig_lanczos_create) or EIG_LANCZOS_FUSED. */
+int eig_lanczos_create_ex(eig_mat_t A, int max_steps, const double *u0, unsigned seed, int flags,
+                          eig_lanczos_t *ws);
 int eig_lanczos_step(eig_lanczos_t ws, int steps, int flags, eig_timing *timing);
 int eig_lanczos_tridiag(eig_lanczos_t ws, int *k, double *alpha_host, double *beta_host);
 int eig_lanczos_destroy(eig_lanczos_t ws);

@@ -617,4 +617,72 @@ void orc_lanczos_rotating(i64 n, const i64 *rowptr, const i32 *col, const double
   }
 }
 
+// One-reduction fused Lanczos step, the restatement of the GPU's fused step (k_lanczos_fused_b1;
+// DESIGN.md "Fused step").  The same Krylov process as orc_lanczos: u_k = t_{k-1} - c u_{k-1} is
+// formed right before the SpMV that needs it, and its squared norm is PREDICTED from the previous
+// step's reductions, nt_k = tsq - c dsum with c = dsum / m (m = the measured ||u_{k-1}||^2, reduced
+// in the step that formed u_{k-1}), so a step needs one reduction of (dsum, tsq, m).  Every scalar
+// formula is written exactly as fused_scalars() in k_spmv.hip evaluates it.
+static void fused_scalars(double nt_prev, double d, double q, double m, double &c, double &alpha_prev, double &nt,
+                          double &beta, double &gam)
+{
+  const double rn = std::sqrt(nt_prev);
+  const double rm = std::sqrt(m);
+  c = d / m;
+  alpha_prev = c * rn;
+  nt = q - c * d;
+  beta = std::sqrt(nt) * rn / rm;
+  gam = beta / rm;
+}
+
+void orc_lanczos_fused(i64 n, const i64 *rowptr, const i32 *col, const double *val, int steps, const double *u0,
+                       double *alpha, double *beta)
+{
+  std::vector<double> T(u0, u0 + n), U(n, 0.0), Tn(n), Un(n), ux(n);
+  std::vector<double> nt(steps + 1), red(3 * (size_t)(steps > 0 ? steps : 1));
+  double s0 = 0.0;
+  for (i64 i = 0; i < n; ++i) s0 += u0[i] * u0[i];
+  nt[0] = s0;
+  beta[0] = std::sqrt(s0);
+  for (int k = 0; k < steps; ++k)
+  {
+    double c = 0.0, gam = 0.0;
+    if (k > 0)
+    {
+      double ap, bk;
+      fused_scalars(nt[k - 1], red[3 * (k - 1)], red[3 * (k - 1) + 1], red[3 * (k - 1) + 2], c, ap, nt[k], bk, gam);
+      alpha[k - 1] = ap;
+      beta[k] = bk;
+    }
+    const double sig = 1.0 / std::sqrt(nt[k]);
+    for (i64 i = 0; i < n; ++i) ux[i] = T[i] - c * U[i];
+    double d = 0.0, q = 0.0, m = 0.0;
+    for (i64 i = 0; i < n; ++i)
+    {
+      double acc = 0.0;
+      for (i64 p = rowptr[i]; p < rowptr[i + 1]; ++p) acc += val[p] * ux[col[p]];
+      double ti = acc * sig;
+      if (k > 0) ti = ti - gam * U[i];
+      Tn[i] = ti;
+      Un[i] = ux[i];
+      d += ti * ux[i];
+      q += ti * ti;
+      m += ux[i] * ux[i];
+    }
+    red[3 * k] = d;
+    red[3 * k + 1] = q;
+    red[3 * k + 2] = m;
+    std::swap(T, Tn);
+    std::swap(U, Un);
+  }
+  if (steps > 0)
+  {
+    double c, ap, bk, gam;
+    fused_scalars(nt[steps - 1], red[3 * (steps - 1)], red[3 * (steps - 1) + 1], red[3 * (steps - 1) + 2], c, ap,
+                  nt[steps], bk, gam);
+    alpha[steps - 1] = ap;
+    beta[steps] = bk;
+  }
+}
+
 } // extern "C"

@@ -58,6 +58,7 @@ def _load():
                                         _int, _int, ctypes.c_uint, _f64p, _f64p]),
         "orc_lanczos": (None, [_i64, _i64p, _i32p, _f64p, _int, _f64p, _f64p, _f64p]),
         "orc_lanczos_rotating": (None, [_i64, _i64p, _i32p, _f64p, _int, _f64p, _f64p, _f64p, _f64p, _f64p]),
+        "orc_lanczos_fused": (None, [_i64, _i64p, _i32p, _f64p, _int, _f64p, _f64p, _f64p]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -208,6 +209,14 @@ def lanczos(A, u0, k):
     beta = np.zeros(k + 1)
     lib.orc_lanczos(A.n, A.rowptr, A.col, A.val, k, U, alpha, beta)
     return U.reshape(k + 1, A.n), alpha, beta
+
+
+def lanczos_fused(A, u0, k):
+    """The fused one-reduction recurrence (orc_lanczos_fused): alpha[k], beta[k+1]."""
+    alpha = np.zeros(max(k, 1))
+    beta = np.zeros(k + 1)
+    lib.orc_lanczos_fused(A.n, A.rowptr, A.col, A.val, k, np.ascontiguousarray(u0, dtype=np.float64), alpha, beta)
+    return alpha[:k], beta
 
 
 def mv_index(n, i, j):

@@ -49,7 +49,7 @@ int main(int argc, char **argv)
   int failures = 0;
 
   // ---- serial reference on one context
-  std::vector<double> x(n), y_ser(n), a_ser(steps), b_ser(steps + 1), ev_ser(nev);
+  std::vector<double> x(n), y_ser(n), a_ser(steps), b_ser(steps + 1), ev_ser(nev), fa_ser(steps), fb_ser(steps + 1);
   for (int64_t i = 0; i < n; ++i) x[i] = std::sin(0.37 * i) + 0.01 * (i % 7);
   {
     eig_ctx_t ctx;
@@ -59,6 +59,7 @@ int main(int argc, char **argv)
     CK(eig_mat_create_bcsr(ctx, n, n, 1, 1, r.rp.data(), r.c.data(), r.v.data(), &A));
     CK(eig_mv_host(A, x.data(), y_ser.data()));
     CK(eig_lanczos_run(A, steps, nullptr, 123, 0, a_ser.data(), b_ser.data(), nullptr));
+    CK(eig_lanczos_run(A, steps, nullptr, 123, EIG_LANCZOS_FUSED, fa_ser.data(), fb_ser.data(), nullptr));
     CK(eig_lanczos_solve(A, nev, ncv, EIG_WHICH_LA, 123, ev_ser.data(), nullptr, nullptr));
     eig_mat_destroy(A);
     eig_ctx_destroy(ctx);
@@ -68,6 +69,7 @@ int main(int argc, char **argv)
   void *hub;
   CK(eig_loopback_create(P, &hub));
   std::vector<int> graph_ok(P, 0);
+  std::vector<std::vector<double>> fal(P, std::vector<double>(steps)), fbe(P, std::vector<double>(steps + 1));
   std::vector<std::vector<double>> y(P), al(P, std::vector<double>(steps)), be(P, std::vector<double>(steps + 1)),
       ev(P, std::vector<double>(nev));
   std::vector<int64_t> rb(P), rc(P), halo(P);
@@ -104,6 +106,7 @@ int main(int argc, char **argv)
       CK(eig_memcpy_d2h(ctx, &dots[r], dd, 8));
       // Lanczos recurrence and solver
       CK(eig_lanczos_run(A, steps, nullptr, 123, EIG_LANCZOS_TIME_KERNELS, al[r].data(), be[r].data(), nullptr));
+      CK(eig_lanczos_run(A, steps, nullptr, 123, EIG_LANCZOS_FUSED, fal[r].data(), fbe[r].data(), nullptr));
       {
         // capture/replay: the loopback transport cannot be captured, replay must take the same steps eagerly
         std::vector<double> ag(steps), bg(steps + 1);
@@ -158,6 +161,15 @@ int main(int argc, char **argv)
       {
         std::printf("FAIL rank %d step %d: alpha %.17g/%.17g beta %.17g/%.17g\n", r, j, al[r][j], a_ser[j],
                     be[r][j + 1], b_ser[j + 1]);
+        ++failures;
+        break;
+      }
+    for (int j = 0; j < steps; ++j)
+      if (std::fabs(fal[r][j] - fa_ser[j]) > 1e-12 * std::fabs(fa_ser[j]) ||
+          std::fabs(fbe[r][j + 1] - fb_ser[j + 1]) > 1e-12 * std::fabs(fb_ser[j + 1]))
+      {
+        std::printf("FAIL rank %d fused step %d: alpha %.17g/%.17g beta %.17g/%.17g\n", r, j, fal[r][j], fa_ser[j],
+                    fbe[r][j + 1], fb_ser[j + 1]);
         ++failures;
         break;
       }

@@ -61,6 +61,39 @@ def test_lanczos_recurrence_matches_oracle(ctx, mat, steps):
     assert np.allclose(beta, rb, rtol=LANCZOS_RTOL, atol=0)
 
 
+@pytest.mark.parametrize("mat,steps", [("c1", 40), ("p3d_20", 40), ("p3d_20", 1)])
+def test_lanczos_fused_matches_oracle(ctx, mat, steps):
+    """Fused one-kernel step vs orc_lanczos_fused (same formulas; only the reductions' summation
+    order differs) and vs the two-kernel GPU step (same Krylov process)."""
+    A = oracle.laplace2d(64) if mat == "c1" else oracle.poisson3d(20)
+    M = upload(ctx, A)
+    alpha, beta, _ = eigmi.lanczos_run(M, steps, seed=123, fused=True)
+    ra, rb = oracle.lanczos_fused(A, oracle.random_vec(A.n, 123), steps)
+    assert np.allclose(alpha, ra, rtol=LANCZOS_RTOL, atol=0)
+    assert np.allclose(beta, rb, rtol=LANCZOS_RTOL, atol=0)
+    ca, cb, _ = eigmi.lanczos_run(M, steps, seed=123)
+    assert np.allclose(alpha, ca, rtol=1e-11, atol=0) and np.allclose(beta, cb, rtol=1e-11, atol=0)
+
+
+def test_lanczos_fused_graph_and_batches_bitwise(ctx):
+    """Fused steps in batches, eager and as a replayed graph: bitwise the one-batch run."""
+    A = oracle.poisson3d(24)
+    M = upload(ctx, A)
+    ref = eigmi.LanczosWorkspace(M, 30, seed=5, fused=True)
+    ref.step(30)
+    ra, rb = ref.tridiag()
+    ws = eigmi.LanczosWorkspace(M, 30, seed=5, fused=True)
+    ws.step(7)
+    assert ws.capture(13, timed=True)
+    t = ws.replay()
+    assert t.spmv_launches == 13 and 0 < t.spmv_ms <= t.total_ms
+    ws.step(10)
+    a, b = ws.tridiag()
+    assert np.array_equal(a, ra) and np.array_equal(b, rb)
+    ws.close()
+    ref.close()
+
+
 def test_lanczos_run_device_start_vector(ctx):
     A = oracle.poisson3d(16)
     M = upload(ctx, A)
@@ -199,3 +232,18 @@ def test_full_size_lanczos_matches_oracle(ctx, p256):
     oracle.lib.orc_lanczos_rotating(N ** 3, rp, c, v, 4, U0, u1, u2, ra, rb)
     assert np.allclose(alpha, ra, rtol=1e-12)
     assert np.allclose(beta, rb, rtol=1e-12)
+
+
+def test_full_size_lanczos_fused_matches_oracle(ctx, p256):
+    """The benchmark's fused step at 256^3: 3 steps vs orc_lanczos_fused, then 30 GPU steps
+    against the two-kernel GPU recurrence (same Krylov process)."""
+    N, M, (rp, c, v) = p256
+    alpha, beta, _ = eigmi.lanczos_run(M, 3, seed=123, fused=True)
+    A = oracle.CSR(N ** 3, rp, c, v)
+    U0 = np.zeros(N ** 3)
+    oracle.lib.orc_random_vec(N ** 3, 123, U0)
+    ra, rb = oracle.lanczos_fused(A, U0, 3)
+    assert np.allclose(alpha, ra, rtol=1e-12) and np.allclose(beta, rb, rtol=1e-12)
+    fa, fb, _ = eigmi.lanczos_run(M, 30, seed=123, fused=True)
+    ca, cb, _ = eigmi.lanczos_run(M, 30, seed=123)
+    assert np.allclose(fa, ca, rtol=1e-11) and np.allclose(fb, cb, rtol=1e-11)

@@ -121,6 +121,26 @@ def test_lanczos_oracle_ritz_values_converge(golden_dir):
     assert abs(w[0] - g["sa_w"][0]) < 1e-6
 
 
+@pytest.mark.parametrize("mat", ["c1", "p3d_20"])
+def test_lanczos_fused_oracle_matches_two_reduction_form(mat, golden_dir):
+    """The one-reduction recurrence (orc_lanczos_fused) is the same Krylov process: alpha/beta
+    agree with orc_lanczos to rounding over 40 and 100 steps (measured <= 2e-12; two runs of
+    the classic form whose start vectors differ by 1e-16 differ by as much), and its Ritz values
+    converge to ARPACK's (C1)."""
+    A = oracle.laplace2d(64) if mat == "c1" else oracle.poisson3d(20)
+    u0 = oracle.random_vec(A.n, 123)
+    for k in (40, 100):
+        _, a, b = oracle.lanczos(A, u0, k)
+        fa, fb = oracle.lanczos_fused(A, u0, k)
+        assert np.allclose(fa, a, rtol=1e-11, atol=0) and np.allclose(fb, b, rtol=1e-11, atol=0)
+    if mat == "c1":
+        fa, fb = oracle.lanczos_fused(A, u0, 300)
+        T = np.diag(fa) + np.diag(fb[1:-1], 1) + np.diag(fb[1:-1], -1)
+        w = np.linalg.eigvalsh(T)
+        g = np.load(os.path.join(golden_dir, "c1_arpack.npz"))
+        assert abs(w[-1] - g["la_w"][0]) < 1e-10
+
+
 def test_flop_byte_models():
     assert oracle.lib.orc_flops_orthonormalize(10, 2) == 2 * 10 + 10 + 2 * 10 + 10 + 4 * 10
     assert oracle.lib.orc_bytes_orthonormalize_blocked(100, 16, 8) > 0

@@ -1,0 +1,78 @@
+#!/usr/bin/env python3
+"""A/B of Lanczos step variants on one GPU, interleaved rounds in ONE process (guide rule 24).
+
+Variant spec "<fused|classic>[:swz0|swz1][:w4|w5|w6|w8][:nt0|nt1]": step form, XCD-aware chunk
+order (EIGMI_XCD_SWIZZLE), register budget of the fused kernel (EIGMI_FUSED_WAVES), nontemporal
+stores of the step vectors (EIGMI_NT_STORE).  The environment is
+read at every launch, so all variants share one matrix upload.  One JSON line per variant:
+median / min over rounds of the step time and of the dominant kernel's time.
+
+    python tools/lanczos_sweep.py --variants classic:swz0,classic:swz1,fused:swz1:w5
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "dune-eigensolver_amd"))
+import numpy as np  # noqa: E402
+
+import eigmi  # noqa: E402
+
+
+def parse(spec):
+    parts = spec.split(":")
+    env = {"EIGMI_XCD_SWIZZLE": "0", "EIGMI_FUSED_WAVES": "8", "EIGMI_NT_STORE": "0"}
+    for p in parts[1:]:
+        if p.startswith("nt"):
+            env["EIGMI_NT_STORE"] = p[2:]
+        elif p.startswith("swz"):
+            env["EIGMI_XCD_SWIZZLE"] = p[3:]
+        elif p.startswith("w"):
+            env["EIGMI_FUSED_WAVES"] = p[1:]
+    return parts[0] == "fused", env
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--N", type=int, default=256)
+    ap.add_argument("--variants", default="classic:swz0,classic:swz1,fused:swz0,fused:swz1")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=30)
+    args = ap.parse_args()
+    ctx = eigmi.Context(0)
+    N = args.N
+    n = N ** 3
+    rp, c, v = eigmi.gen_matrix(eigmi.GEN_POISSON3D, N)
+    nnz = int(rp[-1])
+    M = eigmi.Matrix.from_bcsr(ctx, rp, c, v)
+    specs = args.variants.split(",")
+    res = {s: {"k_us": [], "step_us": []} for s in specs}
+    for _ in range(args.rounds):
+        for spec in specs:
+            fused, env = parse(spec)
+            os.environ.update(env)
+            ws = eigmi.LanczosWorkspace(M, args.steps + 2, seed=123, fused=fused)
+            ws.step(2)
+            t = ws.step(args.steps, timed=True)
+            res[spec]["k_us"].append(t.spmv_ms / args.steps * 1e3)
+            res[spec]["step_us"].append(t.total_ms / args.steps * 1e3)
+            ws.close()
+    for spec in specs:
+        fused, _ = parse(spec)
+        kb = eigmi.bytes_lanczos_fused(n, nnz) if fused else eigmi.bytes_lanczos_k1(n, nnz)
+        r = res[spec]
+        km = float(np.median(r["k_us"]))
+        sm = float(np.median(r["step_us"]))
+        print(json.dumps({"variant": spec, "kernel_us_med": round(km, 2), "kernel_us_min": round(min(r["k_us"]), 2),
+                          "kernel_GBs": round(kb / km / 1e3, 1), "step_us_med": round(sm, 2),
+                          "steps_per_s": round(1e6 / sm, 1),
+                          "step_frac_survey_bytes": round(eigmi.bytes_lanczos_step(n, nnz) / sm / 1e3 / 8000, 4)}),
+              flush=True)
+    M.close()
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()
