@@ -937,8 +937,10 @@ void mv_device(eig_mat_s &A, double *x, double *y)
   }
   if (ctx->loop)
   {
+    // synchronous exchange, then the same interior / boundary launches as the RCCL path
     halo_exchange(A, x, ctx->stream);
-    launch_spmv(A, x, y, nullptr, 0, A.nslices, ctx->stream);
+    launch_spmv(A, x, y, A.slice_list, 0, A.n_interior, ctx->stream);
+    launch_spmv(A, x, y, A.slice_list, A.n_interior, A.n_boundary, ctx->stream);
     return;
   }
   hipEvent_t e0, e1;

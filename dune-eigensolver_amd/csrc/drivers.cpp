@@ -212,6 +212,38 @@ struct LanczosBufs {
 
 // One step j: t = A u sig - gam up (+ dot), allreduce, u_{j+1} = t - alpha sig u (+ norm), allreduce.
 // Optional event timing: ev[0..5] = before K1, after K1, after allreduce 1, after K2, after allreduce 2.
+// Halo exchange + SpMV-type launch split into interior slices (no ghost columns) and boundary
+// slices.  RCCL: the exchange runs on the comm stream while the interior launch computes; the
+// loopback transport exchanges synchronously first (same launches, so its tests cover the split
+// and the carry of the partial reductions).  launch(slices, first, count, part): part 0 = the
+// only launch of the step, 1 = first of two (writes its partial sums to the carry slot), 2 =
+// second (adds the carry).
+enum { kPartOnly = 0, kPartFirst = 1, kPartSecond = 2 };
+template <class Halo, class Launch>
+void halo_split(eig_mat_s &A, hipEvent_t e0, hipEvent_t e1, Halo halo, Launch launch)
+{
+  eig_ctx_t ctx = A.ctx;
+  hipStream_t s = ctx->stream;
+  if (!distributed(A) || (A.recvs.empty() && A.sends.empty()))
+  {
+    launch(nullptr, 0, A.nslices, kPartOnly);
+    return;
+  }
+  if (ctx->loop)
+    halo(s);
+  else
+  {
+    EIG_HIP(hipEventRecord(e0, s));
+    EIG_HIP(hipStreamWaitEvent(ctx->comm_stream, e0, 0));
+    halo(ctx->comm_stream);
+    EIG_HIP(hipEventRecord(e1, ctx->comm_stream));
+  }
+  const bool has_in = A.n_interior > 0, has_bd = A.n_boundary > 0;
+  if (has_in) launch(A.slice_list, 0, A.n_interior, has_bd ? kPartFirst : kPartOnly);
+  if (!ctx->loop) EIG_HIP(hipStreamWaitEvent(s, e1, 0));
+  if (has_bd) launch(A.slice_list, A.n_interior, A.n_boundary, has_in ? kPartSecond : kPartOnly);
+}
+
 // ev_external: the step is being captured into a hipGraph, so the timing events become external
 // event-record nodes (a plain record during capture is only a fork/join marker).
 // ev: nullptr, 2 events (K1 bracket) or 5 (detail: + after allreduce 1, after K2, after allreduce 2).
@@ -227,28 +259,12 @@ void lanczos_step(eig_mat_s &A, double *u, double *up, double *t, int j, Lanczos
       EIG_HIP(hipEventRecordWithFlags(ev[i], s, ev_external ? hipEventRecordExternal : hipEventRecordDefault));
   };
   mark(0);
-  if (!distributed(A) || (A.recvs.empty() && A.sends.empty()) || ctx->loop)
-  {
-    if (distributed(A)) halo_exchange(A, u, s);  // loopback transport: synchronous exchange
-    launch_lanczos_spmv(A, u, up, t, j, lb.st, nullptr, 0, A.nslices, lb.st.dsum + j, lb.st.beta + j, nullptr, 0, s,
-                        ctx->red);
-  }
-  else
-  {
-    // halo of u on the comm stream, interior slices meanwhile, boundary slices after
-    EIG_HIP(hipEventRecord(halo_ev0, s));
-    EIG_HIP(hipStreamWaitEvent(ctx->comm_stream, halo_ev0, 0));
-    halo_exchange(A, u, ctx->comm_stream);
-    EIG_HIP(hipEventRecord(halo_ev1, ctx->comm_stream));
-    const bool has_in = A.n_interior > 0, has_bd = A.n_boundary > 0;
-    if (has_in)
-      launch_lanczos_spmv(A, u, up, t, j, lb.st, A.slice_list, 0, A.n_interior,
-                          has_bd ? lb.carry : lb.st.dsum + j, lb.st.beta + j, nullptr, 0, s, ctx->red);
-    EIG_HIP(hipStreamWaitEvent(s, halo_ev1, 0));
-    if (has_bd)
-      launch_lanczos_spmv(A, u, up, t, j, lb.st, A.slice_list, A.n_interior, A.n_boundary, lb.st.dsum + j,
-                          lb.st.beta + j, has_in ? lb.carry : nullptr, 0, s, ctx->red);
-  }
+  halo_split(
+      A, halo_ev0, halo_ev1, [&](hipStream_t hs) { halo_exchange(A, u, hs); },
+      [&](const i32 *sl, i64 first, i64 count, int part) {
+        launch_lanczos_spmv(A, u, up, t, j, lb.st, sl, first, count, part == kPartFirst ? lb.carry : lb.st.dsum + j,
+                            lb.st.beta + j, part == kPartSecond ? lb.carry : nullptr, 0, s, ctx->red);
+      });
   mark(1);
   allreduce_sum(ctx, lb.st.dsum + j, 1, s);
   mark(2);
@@ -273,26 +289,12 @@ void lanczos_fused_step(eig_mat_s &A, double *P, double *Pout, int k, LanczosBuf
   };
   double *out = lb.st.fred + 3 * (i64)k;
   mark(0);
-  if (!distributed(A) || (A.recvs.empty() && A.sends.empty()) || ctx->loop)
-  {
-    if (distributed(A)) halo_exchange(A, P, s, nullptr, 2);  // loopback transport: synchronous exchange
-    launch_lanczos_fused(A, P, Pout, k, lb.st, nullptr, 0, A.nslices, nullptr, out, 0, s, ctx->red);
-  }
-  else
-  {
-    EIG_HIP(hipEventRecord(halo_ev0, s));
-    EIG_HIP(hipStreamWaitEvent(ctx->comm_stream, halo_ev0, 0));
-    halo_exchange(A, P, ctx->comm_stream, nullptr, 2);
-    EIG_HIP(hipEventRecord(halo_ev1, ctx->comm_stream));
-    const bool has_in = A.n_interior > 0, has_bd = A.n_boundary > 0;
-    if (has_in)
-      launch_lanczos_fused(A, P, Pout, k, lb.st, A.slice_list, 0, A.n_interior, nullptr, has_bd ? lb.carry : out, 0,
-                           s, ctx->red);
-    EIG_HIP(hipStreamWaitEvent(s, halo_ev1, 0));
-    if (has_bd)
-      launch_lanczos_fused(A, P, Pout, k, lb.st, A.slice_list, A.n_interior, A.n_boundary,
-                           has_in ? lb.carry : nullptr, out, 0, s, ctx->red);
-  }
+  halo_split(
+      A, halo_ev0, halo_ev1, [&](hipStream_t hs) { halo_exchange(A, P, hs, nullptr, 2); },
+      [&](const i32 *sl, i64 first, i64 count, int part) {
+        launch_lanczos_fused(A, P, Pout, k, lb.st, sl, first, count, part == kPartSecond ? lb.carry : nullptr,
+                             part == kPartFirst ? lb.carry : out, 0, s, ctx->red);
+      });
   mark(1);
   allreduce_sum(ctx, out, 3, s);
   mark(2);
