@@ -14,33 +14,6 @@ using namespace eigmi;
 
 namespace {
 
-thread_local std::string g_tls_error;
-
-template <class F>
-int guard(eig_ctx_t ctx, F &&f)
-{
-  try
-  {
-    f();
-    return EIG_OK;
-  }
-  catch (const Error &e)
-  {
-    (ctx ? ctx->last_error : g_tls_error) = e.what();
-    return e.code;
-  }
-  catch (const std::bad_alloc &)
-  {
-    (ctx ? ctx->last_error : g_tls_error) = "host allocation failed";
-    return EIG_ERR_ARG;
-  }
-  catch (const std::exception &e)
-  {
-    (ctx ? ctx->last_error : g_tls_error) = e.what();
-    return EIG_ERR_ARG;
-  }
-}
-
 struct DeviceGuard {
   int prev = -1;
   explicit DeviceGuard(int dev)
@@ -321,7 +294,15 @@ extern "C" int eig_ctx_destroy(eig_ctx_t ctx)
   return EIG_OK;
 }
 
-extern "C" const char *eig_last_error(eig_ctx_t ctx) { return ctx ? ctx->last_error.c_str() : g_tls_error.c_str(); }
+namespace eigmi {
+std::string &tls_error()
+{
+  thread_local std::string e;
+  return e;
+}
+}  // namespace eigmi
+
+extern "C" const char *eig_last_error(eig_ctx_t ctx) { return ctx ? ctx->last_error.c_str() : tls_error().c_str(); }
 
 extern "C" int eig_ctx_sync(eig_ctx_t ctx)
 {

@@ -1,0 +1,448 @@
+// blanczos.cpp -- block Lanczos for the symmetric-definite pencil K x = lambda M x (config C5):
+// M-inner-product block Lanczos on the operator M^-1 K, with
+//   * K V_j on the SELL image (k_sell_mv8),
+//   * M^-1 by the Chebyshev-Jacobi semi-iteration fused into the M SpMM (k_sell_mv8<kCheb>) --
+//     reduction-free, so a distributed run exchanges halos but never allreduces inside the solve,
+//   * full re-orthogonalisation: two classical Gram-Schmidt passes in the M-inner product (the
+//     tall-skinny panel V^T (M Z) on MFMA, then Z -= V C),
+//   * CholQR2 in the M-inner product for the new block (Gram on MFMA, 32x32 Cholesky on the host).
+// The reference reaches the same pencil through GeneralizedInverse (UMFPACK LU + subspace
+// iteration, eigensolver.hh:204-351) or ARPACK shift-invert (arpack_geneo_wrapper.hh:581-658);
+// both need a sparse factorisation, which does not exist at C5's size (hard part 4).
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <random>
+#include <vector>
+
+#include "internal.h"
+
+using namespace eigmi;
+
+struct eig_blanczos_s {
+  eig_mat_s *K = nullptr, *M = nullptr;
+  int b = 32, max_steps = 0, k = 0, degree = 36;
+  double lmin = 0.5, lmax = 2.5;
+  i64 ld = 0, own = 0, n = 0;
+  DevBuf *V = nullptr;                   // (max_steps + 1) * b columns, window layout
+  DevBuf *W = nullptr, *Xa = nullptr, *Xb = nullptr, *MZ = nullptr;  // b columns each
+  DevBuf *dinv = nullptr;                // 1 / diag(M), owned rows
+  DevBuf *small = nullptr;               // Gram / coefficient panels
+  std::vector<double> A, B;              // host: A_j (b x b), B_{j+1} (b x b, upper) per step
+  ~eig_blanczos_s()
+  {
+    delete V;
+    delete W;
+    delete Xa;
+    delete Xb;
+    delete MZ;
+    delete dinv;
+    delete small;
+  }
+};
+
+namespace {
+
+// Exchange the ghost rows of every column block of a window-layout multivector.
+void halo_mv(const eig_mat_s &A, double *X, i64 m, hipStream_t s)
+{
+  if (!A.ctx->distributed()) return;
+  for (i64 c = 0; c < m / 8; ++c) halo_exchange(A, X + c * A.window * 8, s, nullptr, 8);
+}
+
+// Chebyshev-Jacobi semi-iteration (Golub-Varga three-term form) for M X = Bv, `degree` steps on
+// the spectrum bounds [lmin, lmax] of diag(M)^-1 M: x_1 = gamma D^-1 b, then degree - 1 fused
+// steps  x_{k+1} = omega_{k+1} (x_k + gamma D^-1 (b - M x_k) - x_{k-1}) + x_{k-1}.  Returns the
+// buffer (Xa or Xb) that holds x_degree.  Error in the D-norm <= 2 rho^degree,
+// rho = (sqrt(kappa) - 1) / (sqrt(kappa) + 1), kappa = lmax / lmin.
+double *cheb_solve(eig_mat_s &M, i64 m, int degree, double lmin, double lmax, const double *Bv, const double *dinv,
+                   double *Xa, double *Xb, hipStream_t s)
+{
+  const i64 n = M.nb_rows, ld = M.window, own = M.own_offset;
+  const double gamma = 2.0 / (lmin + lmax), mu = (lmax - lmin) / (lmax + lmin);
+  launch_cheb_init(n, ld, own, m, Bv, dinv, gamma, Xa, s);
+  if (degree <= 1) return Xa;
+  EIG_HIP(hipMemsetAsync(Xb, 0, (size_t)ld * m * sizeof(double), s));  // x_0 = 0
+  double omega = 1.0;
+  for (int k = 1; k < degree; ++k)
+  {
+    omega = (k == 1) ? 1.0 / (1.0 - 0.5 * mu * mu) : 1.0 / (1.0 - 0.25 * mu * mu * omega);
+    halo_mv(M, Xa, m, s);
+    launch_cheb_step(M, m, Xa, Xb, Bv, dinv, omega, gamma, s);
+    std::swap(Xa, Xb);
+  }
+  return Xa;
+}
+
+double *dptr(DevBuf *b) { return b->d(); }
+
+// Z (b columns) = Vdst R with Vdst M-orthonormal (CholQR twice); R (b x b upper, row-major) on
+// the host.  Vdst may equal Z.
+void mcholqr2(eig_blanczos_s &w, double *Z, double *Vdst, std::vector<double> &Rtot)
+{
+  eig_mat_s &M = *w.M;
+  eig_ctx_t ctx = M.ctx;
+  hipStream_t s = ctx->stream;
+  const int b = w.b;
+  const i64 n = w.n, ld = w.ld, own = w.own;
+  double *Gd = w.small->d();
+  double *Sd = Gd + (size_t)b * b;
+  std::vector<double> G((size_t)b * b), R((size_t)b * b), Ri((size_t)b * b), T((size_t)b * b);
+  Rtot.assign((size_t)b * b, 0.0);
+  for (int i = 0; i < b; ++i) Rtot[(size_t)i * b + i] = 1.0;
+  for (int pass = 0; pass < 2; ++pass)
+  {
+    halo_mv(M, Z, b, s);
+    launch_sell_mv8(M, b, Z, dptr(w.MZ), s);
+    launch_panel_gram(ctx, n, ld, b, b, Z + own * 8, dptr(w.MZ) + own * 8, Gd, s);
+    allreduce_sum(ctx, Gd, (i64)b * b, s);
+    EIG_HIP(hipMemcpyAsync(G.data(), Gd, G.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+    EIG_HIP(hipStreamSynchronize(s));
+    for (int i = 0; i < b; ++i)
+      for (int j = i + 1; j < b; ++j) G[(size_t)i * b + j] = G[(size_t)j * b + i] = 0.5 * (G[(size_t)i * b + j] + G[(size_t)j * b + i]);
+    EIG_CHECK(chol_upper(b, G.data(), R.data()), EIG_ERR_BREAKDOWN,
+              "block Lanczos: M-Gram of the new block is not positive definite (Krylov space exhausted)");
+    tri_upper_inv(b, R.data(), Ri.data());
+    EIG_HIP(hipMemcpyAsync(Sd, Ri.data(), Ri.size() * sizeof(double), hipMemcpyHostToDevice, s));
+    launch_panel_update(n, ld, ld, b, b, Z + own * 8, Sd, 1.0, 0.0, (pass == 1 ? Vdst : Z) + own * 8, s);
+    // Rtot <- R Rtot
+    for (int i = 0; i < b; ++i)
+      for (int j = 0; j < b; ++j)
+      {
+        double acc = 0.0;
+        for (int q = i; q <= j; ++q) acc += R[(size_t)i * b + q] * Rtot[(size_t)q * b + j];
+        T[(size_t)i * b + j] = acc;
+      }
+    Rtot = T;
+    EIG_HIP(hipStreamSynchronize(s));  // Ri's host buffer is reused next pass
+  }
+}
+
+void check_pair(const eig_mat_s *K, const eig_mat_s *M)
+{
+  EIG_CHECK(K && M && K->ctx == M->ctx, EIG_ERR_ARG, "block Lanczos: K and M must share a context");
+  EIG_CHECK(K->br == 1 && K->bc == 1 && M->br == 1 && M->bc == 1, EIG_ERR_BLOCKSIZE,
+            "block Lanczos: FieldMatrix<double,1,1> only");
+  EIG_CHECK(K->nb_rows == M->nb_rows && K->row_begin == M->row_begin && K->window == M->window &&
+                K->own_offset == M->own_offset && K->nb_rows_global == M->nb_rows_global,
+            EIG_ERR_SHAPE, "block Lanczos: K and M must have the same rows and column window");
+  EIG_CHECK(K->nb_rows_global == K->nb_cols, EIG_ERR_SHAPE, "block Lanczos: square matrices required");
+}
+
+}  // namespace
+
+extern "C" int eig_blanczos_create(eig_mat_t K, eig_mat_t M, int block, int max_steps, int degree, double lmin,
+                                   double lmax, unsigned seed, eig_blanczos_t *out)
+{
+  return guard(K ? K->ctx : nullptr, [&] {
+    EIG_CHECK(out && block >= 8 && block <= 32 && block % 8 == 0 && max_steps >= 1 && degree >= 1 && lmin > 0.0 &&
+                  lmax > lmin,
+              EIG_ERR_ARG, "eig_blanczos_create: block in {8,16,24,32}, max_steps >= 1, degree >= 1, 0 < lmin < lmax");
+    check_pair(K, M);
+    EIG_CHECK((i64)(max_steps + 1) * block <= K->nb_rows_global, EIG_ERR_SHAPE,
+              "eig_blanczos_create: (max_steps + 1) * block exceeds the matrix size");
+    eig_ctx_t ctx = K->ctx;
+    EIG_HIP(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    auto *w = new eig_blanczos_s();
+    try
+    {
+      w->K = K;
+      w->M = M;
+      w->b = block;
+      w->max_steps = max_steps;
+      w->degree = degree;
+      w->lmin = lmin;
+      w->lmax = lmax;
+      w->ld = K->window;
+      w->own = K->own_offset;
+      w->n = K->nb_rows;
+      const size_t blk = (size_t)w->ld * block * sizeof(double);
+      w->V = new DevBuf(blk * (max_steps + 1));
+      w->W = new DevBuf(blk);
+      w->Xa = new DevBuf(blk);
+      w->Xb = new DevBuf(blk);
+      w->MZ = new DevBuf(blk);
+      w->dinv = new DevBuf((size_t)std::max<i64>(w->n, 1) * sizeof(double));
+      w->small = new DevBuf((size_t)(max_steps + 2) * block * block * sizeof(double) * 2);
+      EIG_HIP(hipMemsetAsync(w->V->d(), 0, w->V->bytes(), s));
+      for (DevBuf *d : {w->W, w->Xa, w->Xb, w->MZ}) EIG_HIP(hipMemsetAsync(d->d(), 0, d->bytes(), s));
+      launch_diag_inv(*M, w->dinv->d(), s);
+      // start block: mt19937(seed) + normal(0,1) in MultiVector fill order (block, row, col) over
+      // the GLOBAL rows (eigensolver.hh:49-55), this rank keeps its own rows
+      {
+        const i64 ng = K->nb_rows_global, rb = K->row_begin, n = w->n;
+        std::vector<double> h((size_t)w->ld * block, 0.0);
+        std::mt19937 urbg{seed};
+        std::normal_distribution<double> gen{0.0, 1.0};
+        for (int c = 0; c < block / 8; ++c)
+          for (i64 i = 0; i < ng; ++i)
+            for (int j = 0; j < 8; ++j)
+            {
+              const double v = gen(urbg);
+              if (i >= rb && i < rb + n) h[((size_t)c * w->ld + w->own + (i - rb)) * 8 + j] = v;
+            }
+        EIG_HIP(hipMemcpyAsync(w->Xa->d(), h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice, s));
+        EIG_HIP(hipStreamSynchronize(s));
+      }
+      std::vector<double> R;
+      mcholqr2(*w, w->Xa->d(), w->V->d(), R);  // V_0 = M-orthonormal start block
+    }
+    catch (...)
+    {
+      delete w;
+      throw;
+    }
+    *out = w;
+  });
+}
+
+extern "C" int eig_blanczos_step(eig_blanczos_t w, int steps, eig_blanczos_timing *timing)
+{
+  return guard(w ? w->K->ctx : nullptr, [&] {
+    EIG_CHECK(w && steps >= 0, EIG_ERR_ARG, "eig_blanczos_step: bad argument");
+    EIG_CHECK(w->k + steps <= w->max_steps, EIG_ERR_ARG, "eig_blanczos_step: more steps than max_steps");
+    eig_ctx_t ctx = w->K->ctx;
+    EIG_HIP(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    const int b = w->b;
+    const i64 n = w->n, ld = w->ld, own = w->own;
+    const size_t bs = (size_t)ld * b;  // doubles per basis block
+    std::vector<hipEvent_t> ev((size_t)5 * steps);
+    for (auto &e : ev) EIG_HIP(hipEventCreate(&e));
+    struct EvGuard {
+      std::vector<hipEvent_t> &v;
+      ~EvGuard()
+      {
+        for (auto &e : v) (void)hipEventDestroy(e);
+      }
+    } evg{ev};
+    double *Ad = w->small->d();
+    double *Cd = Ad + (size_t)b * b;
+    for (int i = 0; i < steps; ++i)
+    {
+      const int j = w->k;
+      hipEvent_t *e = &ev[(size_t)5 * i];
+      double *Vj = w->V->d() + (size_t)j * bs;
+      EIG_HIP(hipEventRecord(e[0], s));
+      // W = K V_j;  A_j = V_j^T W
+      halo_mv(*w->K, Vj, b, s);
+      launch_sell_mv8(*w->K, b, Vj, w->W->d(), s);
+      launch_panel_gram(ctx, n, ld, b, b, Vj + own * 8, w->W->d() + own * 8, Ad, s);
+      allreduce_sum(ctx, Ad, (i64)b * b, s);
+      EIG_HIP(hipEventRecord(e[1], s));
+      // Z = M^-1 W
+      double *Z = cheb_solve(*w->M, b, w->degree, w->lmin, w->lmax, w->W->d(), w->dinv->d(), w->Xa->d(), w->Xb->d(), s);
+      EIG_HIP(hipEventRecord(e[2], s));
+      // two CGS passes against V_0..V_j in the M-inner product: C = V^T (M Z), Z -= V C
+      const i64 m1 = (i64)(j + 1) * b;
+      for (int pass = 0; pass < 2; ++pass)
+      {
+        halo_mv(*w->M, Z, b, s);
+        launch_sell_mv8(*w->M, b, Z, w->MZ->d(), s);
+        launch_panel_gram(ctx, n, ld, m1, b, w->V->d() + own * 8, w->MZ->d() + own * 8, Cd, s);
+        allreduce_sum(ctx, Cd, m1 * b, s);
+        launch_panel_update(n, ld, ld, m1, b, w->V->d() + own * 8, Cd, -1.0, 1.0, Z + own * 8, s);
+      }
+      EIG_HIP(hipEventRecord(e[3], s));
+      std::vector<double> Ah((size_t)b * b);
+      EIG_HIP(hipMemcpyAsync(Ah.data(), Ad, Ah.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+      std::vector<double> R;
+      mcholqr2(*w, Z, w->V->d() + (size_t)(j + 1) * bs, R);  // syncs
+      EIG_HIP(hipEventRecord(e[4], s));
+      for (int r = 0; r < b; ++r)
+        for (int c = r + 1; c < b; ++c)
+          Ah[(size_t)r * b + c] = Ah[(size_t)c * b + r] = 0.5 * (Ah[(size_t)r * b + c] + Ah[(size_t)c * b + r]);
+      w->A.insert(w->A.end(), Ah.begin(), Ah.end());
+      w->B.insert(w->B.end(), R.begin(), R.end());
+      w->k = j + 1;
+    }
+    EIG_HIP(hipStreamSynchronize(s));
+    if (timing)
+    {
+      std::memset(timing, 0, sizeof(*timing));
+      for (int i = 0; i < steps; ++i)
+      {
+        hipEvent_t *e = &ev[(size_t)5 * i];
+        float t[4] = {0, 0, 0, 0};
+        for (int q = 0; q < 4; ++q) EIG_HIP(hipEventElapsedTime(&t[q], e[q], e[q + 1]));
+        timing->kspmm_ms += t[0];
+        timing->cheb_ms += t[1];
+        timing->orth_ms += t[2];
+        timing->norm_ms += t[3];
+      }
+      if (steps > 0)
+      {
+        float tt = 0.f;
+        EIG_HIP(hipEventElapsedTime(&tt, ev[0], ev[(size_t)5 * (steps - 1) + 4]));
+        timing->total_ms = tt;
+      }
+      timing->steps = steps;
+      timing->cheb_launches = (int64_t)steps * std::max(0, w->degree - 1) * ((b / 8 + 1) / 2);
+    }
+  });
+}
+
+namespace {
+// The block tridiagonal T (k b x k b, row-major) of the k completed steps.
+std::vector<double> assemble_T(const eig_blanczos_s &w)
+{
+  const int b = w.b, k = w.k, N = k * b;
+  std::vector<double> T((size_t)N * N, 0.0);
+  for (int j = 0; j < k; ++j)
+  {
+    for (int r = 0; r < b; ++r)
+      for (int c = 0; c < b; ++c) T[(size_t)(j * b + r) * N + j * b + c] = w.A[((size_t)j * b + r) * b + c];
+    if (j + 1 < k)  // T_{j+1,j} = B_{j+1}, T_{j,j+1} = B_{j+1}^T
+      for (int r = 0; r < b; ++r)
+        for (int c = 0; c < b; ++c)
+        {
+          const double v = w.B[((size_t)j * b + r) * b + c];
+          T[(size_t)((j + 1) * b + r) * N + j * b + c] = v;
+          T[(size_t)(j * b + c) * N + (j + 1) * b + r] = v;
+        }
+  }
+  return T;
+}
+}  // namespace
+
+extern "C" int eig_blanczos_tmatrix(eig_blanczos_t w, int *dim, double *T_host)
+{
+  return guard(w ? w->K->ctx : nullptr, [&] {
+    EIG_CHECK(w && dim, EIG_ERR_ARG, "eig_blanczos_tmatrix: bad argument");
+    *dim = w->k * w->b;
+    if (T_host)
+    {
+      std::vector<double> T = assemble_T(*w);
+      std::memcpy(T_host, T.data(), T.size() * sizeof(double));
+    }
+  });
+}
+
+extern "C" int eig_blanczos_ritz(eig_blanczos_t w, int nev, int which, double *eval_host, double *evec_host,
+                                 double *resid_host)
+{
+  return guard(w ? w->K->ctx : nullptr, [&] {
+    EIG_CHECK(w && eval_host && nev > 0, EIG_ERR_ARG, "eig_blanczos_ritz: bad argument");
+    EIG_CHECK(which == EIG_WHICH_LA || which == EIG_WHICH_SA, EIG_ERR_ARG, "eig_blanczos_ritz: bad `which`");
+    const int b = w->b, N = w->k * b;
+    EIG_CHECK(w->k >= 1 && nev <= N, EIG_ERR_ARG, "eig_blanczos_ritz: take steps first (nev <= steps * block)");
+    eig_ctx_t ctx = w->K->ctx;
+    EIG_HIP(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    std::vector<double> T = assemble_T(*w), th, S;
+    sym_eig(N, T, th, S);
+    std::vector<int> pick(nev);
+    for (int i = 0; i < nev; ++i) pick[i] = (which == EIG_WHICH_LA) ? N - 1 - i : i;
+    for (int i = 0; i < nev; ++i) eval_host[i] = th[pick[i]];
+    if (!evec_host && !resid_host) return;
+    const i64 n = w->n, ld = w->ld, own = w->own;
+    double *Sd = w->small->d();
+    std::vector<double> Sh, rs(nev, 0.0);
+    // 32 Ritz vectors at a time: Y = V_{0..k-1} S(:, cols) into Xa; KY into W, MY into MZ
+    for (int c0 = 0; c0 < nev; c0 += 32)
+    {
+      const int nc = std::min(32, nev - c0), m2 = (nc + 7) / 8 * 8;
+      Sh.assign((size_t)N * m2, 0.0);
+      for (int q = 0; q < N; ++q)
+        for (int c = 0; c < nc; ++c) Sh[(size_t)q * m2 + c] = S[(size_t)q * N + pick[c0 + c]];
+      DevBuf Sb(Sh.size() * sizeof(double));
+      EIG_HIP(hipMemcpyAsync(Sb.d(), Sh.data(), Sh.size() * sizeof(double), hipMemcpyHostToDevice, s));
+      double *Y = w->Xa->d();
+      EIG_HIP(hipMemsetAsync(Y, 0, (size_t)ld * m2 * sizeof(double), s));
+      launch_panel_update(n, ld, ld, N, m2, w->V->d() + own * 8, Sb.d(), 1.0, 0.0, Y + own * 8, s);
+      std::vector<double> hy((size_t)ld * m2), hk, hm;
+      if (resid_host)
+      {
+        halo_mv(*w->K, Y, m2, s);
+        launch_sell_mv8(*w->K, m2, Y, w->W->d(), s);
+        launch_sell_mv8(*w->M, m2, Y, w->MZ->d(), s);
+        hk.resize(hy.size());
+        hm.resize(hy.size());
+        EIG_HIP(hipMemcpyAsync(hk.data(), w->W->d(), hk.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+        EIG_HIP(hipMemcpyAsync(hm.data(), w->MZ->d(), hm.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+      }
+      EIG_HIP(hipMemcpyAsync(hy.data(), Y, hy.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+      EIG_HIP(hipStreamSynchronize(s));
+      for (int c = 0; c < nc; ++c)
+      {
+        const int blk = c / 8, jj = c % 8;
+        const double theta = th[pick[c0 + c]];
+        double r2 = 0.0;
+        for (i64 r = 0; r < n; ++r)
+        {
+          const size_t at = ((size_t)blk * ld + own + r) * 8 + jj;
+          if (evec_host) evec_host[(size_t)(c0 + c) * n + r] = hy[at];
+          if (resid_host)
+          {
+            const double d = hk[at] - theta * hm[at];
+            r2 += d * d;
+          }
+        }
+        rs[c0 + c] = r2;
+      }
+    }
+    if (resid_host)
+    {
+      double *rd = Sd;
+      EIG_HIP(hipMemcpyAsync(rd, rs.data(), nev * sizeof(double), hipMemcpyHostToDevice, s));
+      allreduce_sum(ctx, rd, nev, s);
+      EIG_HIP(hipMemcpyAsync(rs.data(), rd, nev * sizeof(double), hipMemcpyDeviceToHost, s));
+      EIG_HIP(hipStreamSynchronize(s));
+      for (int i = 0; i < nev; ++i) resid_host[i] = std::sqrt(rs[i]);
+    }
+  });
+}
+
+extern "C" int eig_blanczos_destroy(eig_blanczos_t w)
+{
+  if (!w) return EIG_OK;
+  (void)hipSetDevice(w->K->ctx->device);
+  (void)hipStreamSynchronize(w->K->ctx->stream);
+  delete w;
+  return EIG_OK;
+}
+
+// M^-1 B by the Chebyshev-Jacobi semi-iteration (the block Lanczos operator's inner solve).
+extern "C" int eig_mass_solve_mv8(eig_mat_t M, int64_t m, int degree, double lmin, double lmax, const double *B,
+                                  double *X)
+{
+  return guard(M ? M->ctx : nullptr, [&] {
+    EIG_CHECK(M && B && X && m > 0 && m % 8 == 0 && degree >= 1 && lmin > 0.0 && lmax > lmin, EIG_ERR_ARG,
+              "eig_mass_solve_mv8: bad argument");
+    EIG_CHECK(M->br == 1 && M->bc == 1 && M->nb_rows_global == M->nb_cols, EIG_ERR_BLOCKSIZE,
+              "eig_mass_solve_mv8: square FieldMatrix<double,1,1> only");
+    eig_ctx_t ctx = M->ctx;
+    EIG_HIP(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    const size_t bytes = (size_t)M->window * m * sizeof(double);
+    DevBuf dinv((size_t)std::max<i64>(M->nb_rows, 1) * sizeof(double)), Xb(bytes);
+    launch_diag_inv(*M, dinv.d(), s);
+    EIG_HIP(hipMemsetAsync(X, 0, bytes, s));
+    double *res = cheb_solve(*M, m, degree, lmin, lmax, B, dinv.d(), X, Xb.d(), s);
+    if (res != X) EIG_HIP(hipMemcpyAsync(X, res, bytes, hipMemcpyDeviceToDevice, s));
+    EIG_HIP(hipStreamSynchronize(s));
+  });
+}
+
+extern "C" int eig_panel_update_mv8(eig_ctx_t ctx, int64_t n, int64_t m1, int64_t m2, const double *Q, const double *S,
+                                    double alpha, double beta, double *Y)
+{
+  return guard(ctx, [&] {
+    EIG_CHECK(ctx && Q && S && Y && n >= 0 && m1 >= 0 && m1 % 8 == 0 && m2 % 8 == 0 && m2 >= 8 && m2 <= 32,
+              EIG_ERR_ARG, "eig_panel_update_mv8: m1 % 8 == 0, m2 in {8,16,24,32}");
+    EIG_HIP(hipSetDevice(ctx->device));
+    launch_panel_update(n, n, n, m1, m2, Q, S, alpha, beta, Y, ctx->stream);
+  });
+}
+
+extern "C" int eig_panel_gram_mv8(eig_ctx_t ctx, int64_t n, int64_t m1, int64_t m2, const double *Q1, const double *Q2,
+                                  double *G)
+{
+  return guard(ctx, [&] {
+    EIG_CHECK(ctx && Q1 && Q2 && G && n >= 0 && m1 > 0 && m2 > 0 && m1 % 8 == 0 && m2 % 8 == 0, EIG_ERR_ARG,
+              "eig_panel_gram_mv8: bad argument");
+    EIG_HIP(hipSetDevice(ctx->device));
+    launch_panel_gram(ctx, n, n, m1, m2, Q1, Q2, G, ctx->stream);
+  });
+}

@@ -15,117 +15,7 @@ using namespace eigmi;
 
 namespace {
 
-thread_local std::string g_drv_error;
-
-template <class F>
-int guard(eig_ctx_t ctx, F &&f)
-{
-  try
-  {
-    f();
-    return EIG_OK;
-  }
-  catch (const Error &e)
-  {
-    (ctx ? ctx->last_error : g_drv_error) = e.what();
-    return e.code;
-  }
-  catch (const std::exception &e)
-  {
-    (ctx ? ctx->last_error : g_drv_error) = e.what();
-    return EIG_ERR_ARG;
-  }
-}
-
-struct DevBuf {
-  void *p = nullptr;
-  size_t n = 0;
-  explicit DevBuf(size_t bytes) : n(bytes) { EIG_HIP(hipMalloc(&p, bytes ? bytes : 1)); }
-  size_t bytes() const { return n; }
-  ~DevBuf()
-  {
-    if (p) (void)hipFree(p);
-  }
-  DevBuf(const DevBuf &) = delete;
-  DevBuf &operator=(const DevBuf &) = delete;
-  double *d() const { return static_cast<double *>(p); }
-};
-
 bool distributed(const eig_mat_s &A) { return A.ctx->distributed(); }
-
-// ---------------------------------------------------------------------------------------------
-// Symmetric tridiagonal eigenproblem (implicit QL with Wilkinson shifts).  d[k] diagonal,
-// e[k-1] off-diagonal; on return d holds the eigenvalues (ascending) and Z (k x k, column j =
-// eigenvector j, row-major Z[i*k + j]).
-// ---------------------------------------------------------------------------------------------
-void tridiag_eig(int k, std::vector<double> &d, std::vector<double> e, std::vector<double> &Z)
-{
-  Z.assign((size_t)k * k, 0.0);
-  for (int i = 0; i < k; ++i) Z[(size_t)i * k + i] = 1.0;
-  e.resize(k, 0.0);
-  if (k > 0) e[k - 1] = 0.0;
-  const double eps = 2.220446049250313e-16;
-  for (int l = 0; l < k; ++l)
-  {
-    int iter = 0, m;
-    do
-    {
-      for (m = l; m < k - 1; ++m)
-      {
-        const double dd = std::fabs(d[m]) + std::fabs(d[m + 1]);
-        if (std::fabs(e[m]) <= eps * dd) break;
-      }
-      if (m != l)
-      {
-        if (iter++ == 100) throw Error(EIG_ERR_BREAKDOWN, "tridiagonal QL did not converge");
-        double g = (d[l + 1] - d[l]) / (2.0 * e[l]);
-        double r = std::hypot(g, 1.0);
-        g = d[m] - d[l] + e[l] / (g + std::copysign(r, g));
-        double s = 1.0, c = 1.0, p = 0.0;
-        int i;
-        for (i = m - 1; i >= l; --i)
-        {
-          double f = s * e[i], b = c * e[i];
-          e[i + 1] = (r = std::hypot(f, g));
-          if (r == 0.0)
-          {
-            d[i + 1] -= p;
-            e[m] = 0.0;
-            break;
-          }
-          s = f / r;
-          c = g / r;
-          g = d[i + 1] - p;
-          r = (d[i] - g) * s + 2.0 * c * b;
-          d[i + 1] = g + (p = s * r);
-          g = c * r - b;
-          for (int q = 0; q < k; ++q)
-          {
-            f = Z[(size_t)q * k + i + 1];
-            Z[(size_t)q * k + i + 1] = s * Z[(size_t)q * k + i] + c * f;
-            Z[(size_t)q * k + i] = c * Z[(size_t)q * k + i] - s * f;
-          }
-        }
-        if (r == 0.0 && i >= l) continue;
-        d[l] -= p;
-        e[l] = g;
-        e[m] = 0.0;
-      }
-    } while (m != l);
-  }
-  // sort ascending with vectors
-  std::vector<int> idx(k);
-  std::iota(idx.begin(), idx.end(), 0);
-  std::sort(idx.begin(), idx.end(), [&](int a, int b) { return d[a] < d[b]; });
-  std::vector<double> d2(k), Z2((size_t)k * k);
-  for (int j = 0; j < k; ++j)
-  {
-    d2[j] = d[idx[j]];
-    for (int q = 0; q < k; ++q) Z2[(size_t)q * k + j] = Z[(size_t)q * k + idx[j]];
-  }
-  d.swap(d2);
-  Z.swap(Z2);
-}
 
 }  // namespace
 

@@ -8,9 +8,14 @@
 //   kind 3  2-D identity values on the Laplacian pattern              (.cc:145-156)
 //   kind 4  3-D 7-point Poisson, N^3 rows, diagonal 6                  (configs C2 / C4)
 //   kind 5  3-D Q1 "elasticity" L_Q1 (x) C on N^3 nodes, 3x3 blocks     (config C3)
+//   kind 6  3-D P1 stiffness K on the Kuhn 6-tetrahedra split of the unit cube, N^3 interior
+//           nodes, h = 1/(N+1), Dirichlet nodes eliminated, 15-point edge pattern   (config C5)
+//   kind 7  3-D P1 consistent mass M on the same mesh and the SAME 15-point pattern (config C5;
+//           the reference assumes pattern(A) contains pattern(B), eigensolver.hh:202-203)
 #include <cmath>
 #include <cstdint>
 #include <cstdlib>
+#include <utility>
 
 #include "../../include/eigmi.h"
 
@@ -20,6 +25,75 @@ typedef int64_t i64;
 
 inline double k1(int d) { return d == 0 ? 2.0 : -1.0; }
 inline double m1(int d) { return d == 0 ? 4.0 / 6.0 : 1.0 / 6.0; }
+
+// P1 on the Kuhn split: the cube with lower corner c is cut into 6 tetrahedra, one per axis
+// permutation p: v0 = c, v1 = v0 + e_p0, v2 = v1 + e_p1, v3 = c + (1,1,1).  Barycentric gradients
+// are -e_p0, e_p0 - e_p1, e_p1 - e_p2, e_p2 (over h), so every element stiffness is the path
+// Laplacian (h/6) [1 -1 0 0; -1 2 -1 0; 0 -1 2 -1; 0 0 -1 1] and every element mass is
+// (h^3/120)(1 + delta_ab).  Edges are +-e_i, +-(e_i + e_j), +-(1,1,1): 14 neighbours + self.
+const int kPerm[6][3] = {{0, 1, 2}, {0, 2, 1}, {1, 0, 2}, {1, 2, 0}, {2, 0, 1}, {2, 1, 0}};
+int gen_p1_row(bool mass, int N, i64 k, int32_t *cols, double *vals)
+{
+  const i64 NN = (i64)N * N;
+  const int P[3] = {(int)(k % N) + 1, (int)((k / N) % N) + 1, (int)(k / NN) + 1};  // grid coords 1..N
+  const double h = 1.0 / (N + 1);
+  double acc[27] = {0.0};
+  bool nb[27] = {false};
+  static const double path[4][4] = {{1, -1, 0, 0}, {-1, 2, -1, 0}, {0, -1, 2, -1}, {0, 0, -1, 1}};
+  const double ks = h / 6.0, ms = h * h * h / 120.0;
+  for (int dz = 0; dz <= 1; ++dz)
+    for (int dy = 0; dy <= 1; ++dy)
+      for (int dx = 0; dx <= 1; ++dx)
+      {
+        const int c[3] = {P[0] - dx, P[1] - dy, P[2] - dz};  // cube lower corner, 0..N
+        if (c[0] < 0 || c[1] < 0 || c[2] < 0 || c[0] > N || c[1] > N || c[2] > N) continue;
+        for (int t = 0; t < 6; ++t)
+        {
+          int v[4][3];
+          for (int a = 0; a < 3; ++a) v[0][a] = c[a];
+          for (int a = 0; a < 3; ++a) v[1][a] = v[0][a] + (kPerm[t][0] == a);
+          for (int a = 0; a < 3; ++a) v[2][a] = v[1][a] + (kPerm[t][1] == a);
+          for (int a = 0; a < 3; ++a) v[3][a] = c[a] + 1;
+          int me = -1;
+          for (int a = 0; a < 4; ++a)
+            if (v[a][0] == P[0] && v[a][1] == P[1] && v[a][2] == P[2]) me = a;
+          if (me < 0) continue;
+          for (int b = 0; b < 4; ++b)
+          {
+            bool interior = true;
+            for (int a = 0; a < 3; ++a) interior = interior && v[b][a] >= 1 && v[b][a] <= N;
+            if (!interior) continue;
+            const int slot = ((v[b][2] - P[2] + 1) * 3 + (v[b][1] - P[1] + 1)) * 3 + (v[b][0] - P[0] + 1);
+            acc[slot] += mass ? ms * (me == b ? 2.0 : 1.0) : ks * path[me][b];
+            nb[slot] = true;
+          }
+        }
+      }
+  // the 14 edge neighbours + self that exist (interior), in ascending global column
+  int32_t cc[27];
+  double vv[27];
+  int cnt = 0;
+  for (int s = 0; s < 27; ++s)
+  {
+    if (!nb[s]) continue;
+    const int ox = s % 3 - 1, oy = (s / 3) % 3 - 1, oz = s / 9 - 1;
+    cc[cnt] = (int32_t)(k + oz * NN + oy * (i64)N + ox);
+    vv[cnt] = acc[s];
+    ++cnt;
+  }
+  for (int i = 1; i < cnt; ++i)  // insertion sort by column
+    for (int j = i; j > 0 && cc[j - 1] > cc[j]; --j)
+    {
+      std::swap(cc[j - 1], cc[j]);
+      std::swap(vv[j - 1], vv[j]);
+    }
+  for (int i = 0; i < cnt; ++i)
+  {
+    if (cols) cols[i] = cc[i];
+    if (vals) vals[i] = vv[i];
+  }
+  return cnt;
+}
 
 // Entries of global block row k; returns the count.  cols/vals may be null (count only).
 int gen_row(int kind, int N, int overlap, i64 k, int32_t *cols, double *vals)
@@ -85,6 +159,7 @@ int gen_row(int kind, int N, int overlap, i64 k, int32_t *cols, double *vals)
         }
     return c;
   }
+  if (kind == 6 || kind == 7) return gen_p1_row(kind == 7, N, k, cols, vals);
   return -1;
 }
 
@@ -95,7 +170,7 @@ int blk_of(int kind) { return kind == 5 ? 9 : 1; }
 
 extern "C" int64_t eig_gen_nnzb_rows(int kind, int N, int64_t row_begin, int64_t nrows)
 {
-  if (kind < 0 || kind > 5 || N <= 0) return -1;
+  if (kind < 0 || kind > 7 || N <= 0) return -1;
   i64 s = 0;
   for (i64 k = row_begin; k < row_begin + nrows; ++k) s += gen_row(kind, N, 0, k, nullptr, nullptr);
   return s;
@@ -110,13 +185,18 @@ extern "C" int64_t eig_gen_nnzb(int kind, int N)
     const i64 t = 3 * (i64)N - 2;
     return t * t * t;
   }
+  if (kind == 6 || kind == 7)
+  {
+    const i64 n = N, m = N - 1;
+    return n * n * n + 6 * n * n * m + 6 * n * m * m + 2 * m * m * m;
+  }
   return -1;
 }
 
 extern "C" int eig_gen_matrix_rows(int kind, int N, int64_t row_begin, int64_t nrows, int64_t *rowptr, int32_t *col,
                                    double *vals)
 {
-  if (kind < 0 || kind > 5 || N <= 0 || !rowptr || !col || !vals) return EIG_ERR_ARG;
+  if (kind < 0 || kind > 7 || N <= 0 || !rowptr || !col || !vals) return EIG_ERR_ARG;
   if (row_begin < 0 || row_begin + nrows > nrows_of(kind, N)) return EIG_ERR_SHAPE;
   const int bb = blk_of(kind);
   i64 p = 0;
@@ -131,7 +211,7 @@ extern "C" int eig_gen_matrix_rows(int kind, int N, int64_t row_begin, int64_t n
 
 extern "C" int eig_gen_matrix(int kind, int N, int overlap, int64_t *rowptr, int32_t *col, double *vals)
 {
-  if (kind < 0 || kind > 5 || N <= 0 || !rowptr || !col || !vals) return EIG_ERR_ARG;
+  if (kind < 0 || kind > 7 || N <= 0 || !rowptr || !col || !vals) return EIG_ERR_ARG;
   const int bb = blk_of(kind);
   const i64 n = nrows_of(kind, N);
   i64 p = 0;

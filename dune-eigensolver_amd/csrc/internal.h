@@ -6,6 +6,7 @@
 #include <condition_variable>
 #include <cstdint>
 #include <mutex>
+#include <new>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -249,6 +250,29 @@ void launch_gemv_n_set(i64 n, int k, const double *V, i64 ldv, const double *c, 
 void launch_resid_sq(i64 n, const double *x, const double *y, double theta, double *out, int ticket,
                      hipStream_t s, ReduceWS red);
 
+// Window-layout multivector kernels (k_block.hip).  m columns (multiple of 8), leading dimension
+// = the matrix window, owned rows at own_offset.
+void launch_sell_mv8(const eig_mat_s &A, i64 m, const double *X, double *Y, hipStream_t s);
+void launch_cheb_step(const eig_mat_s &M, i64 m, const double *Xk, double *Xold, const double *B, const double *dinv,
+                      double omega, double gamma, hipStream_t s);
+void launch_diag_inv(const eig_mat_s &A, double *dinv, hipStream_t s);
+void launch_cheb_init(i64 n, i64 ld, i64 own, i64 m, const double *B, const double *dinv, double gamma, double *X,
+                      hipStream_t s);
+// G (m1 x m2, row-major, device) = Q1^T Q2 over n rows; Q1, Q2 address owned row 0 (pointer + 8 own).
+void launch_panel_gram(eig_ctx_t ctx, i64 n, i64 ld, i64 m1, i64 m2, const double *Q1, const double *Q2, double *G,
+                       hipStream_t s);
+// Y = beta Y + alpha Q S over n rows (owned-row pointers), m2 <= 32.
+void launch_panel_update(i64 n, i64 ldq, i64 ldy, i64 m1, i64 m2, const double *Q, const double *S, double alpha,
+                         double beta, double *Y, hipStream_t s);
+
+// ---- dense host linear algebra (dense.cpp) ---------------------------------------------------
+void tridiag_eig(int k, std::vector<double> &d, std::vector<double> e, std::vector<double> &Z, bool z_identity = true);
+void householder_tridiag(int n, std::vector<double> A, std::vector<double> &d, std::vector<double> &e,
+                         std::vector<double> &Q);
+void sym_eig(int n, const std::vector<double> &A, std::vector<double> &w, std::vector<double> &Z);
+bool chol_upper(int n, const double *G, double *R);
+void tri_upper_inv(int n, const double *R, double *Rinv);
+
 // ---- helpers in api.cpp --------------------------------------------------------------------
 // Ghost entries of window vector x (and x2 when given) from their owners.
 // width: doubles per row of x (2 for the fused step's interleaved pair vectors).
@@ -259,5 +283,52 @@ void orthonormalize_device(eig_ctx_t ctx, i64 n, i64 m, double *Q, int variant);
 void allreduce_sum(eig_ctx_t ctx, double *buf, i64 count, hipStream_t s);
 void *ctx_buffer(eig_ctx_t ctx, int slot, size_t bytes);
 void host_random_normal(i64 count, unsigned seed, double *out);
+
+}  // namespace eigmi
+
+namespace eigmi {
+
+// C-ABI entry guard: runs f, maps exceptions to the int status and stores the message in the
+// context (or the thread's error slot when there is no context; eig_last_error(NULL) reads it).
+std::string &tls_error();
+template <class F>
+int guard(eig_ctx_t ctx, F &&f)
+{
+  try
+  {
+    f();
+    return EIG_OK;
+  }
+  catch (const Error &e)
+  {
+    (ctx ? ctx->last_error : tls_error()) = e.what();
+    return e.code;
+  }
+  catch (const std::bad_alloc &)
+  {
+    (ctx ? ctx->last_error : tls_error()) = "host allocation failed";
+    return EIG_ERR_ARG;
+  }
+  catch (const std::exception &e)
+  {
+    (ctx ? ctx->last_error : tls_error()) = e.what();
+    return EIG_ERR_ARG;
+  }
+}
+
+// Owning device buffer for driver workspaces.
+struct DevBuf {
+  void *p = nullptr;
+  size_t n = 0;
+  explicit DevBuf(size_t bytes) : n(bytes) { EIG_HIP(hipMalloc(&p, bytes ? bytes : 1)); }
+  size_t bytes() const { return n; }
+  ~DevBuf()
+  {
+    if (p) (void)hipFree(p);
+  }
+  DevBuf(const DevBuf &) = delete;
+  DevBuf &operator=(const DevBuf &) = delete;
+  double *d() const { return static_cast<double *>(p); }
+};
 
 }  // namespace eigmi

@@ -70,80 +70,6 @@ __global__ __launch_bounds__(256) void k_spmm_mv8(i64 nrows, i64 nslices, const 
   }
 }
 
-// Row-per-lane SpMM for 64-row slices (R = 1): lane l computes all 8 columns of row 64 s + l for
-// MB column blocks; the slice's value / column (or offset + mask) streams are read once per MB
-// column blocks, coalesced; each gathered Qin row is four 16-B loads.  Per column j the row sum
-// runs over the stored entries in ascending-column order from 0.0 (bitwise the reference).
-template <int MB, bool STENCIL>
-__global__ __launch_bounds__(256) void k_spmm_mv8_rows(i64 nrows, i64 nslices, const i64 *__restrict__ slice_ptr,
-                                                       const double *__restrict__ val, const i32 *__restrict__ col,
-                                                       const i32 *__restrict__ st_delta,
-                                                       const uint8_t *__restrict__ st_mask,
-                                                       const double *__restrict__ Qin, double *__restrict__ Qout,
-                                                       i64 n, int b0, int nb)
-{
-  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const i64 per = (nslices + gridDim.x - 1) / gridDim.x;
-  const i64 sb = (i64)blockIdx.x * per, se = sb + per < nslices ? sb + per : nslices;
-  for (i64 s = sb + wave; s < se; s += 4)
-  {
-    const i64 base = slice_ptr[s];
-    const int width = (int)((slice_ptr[s + 1] - base) >> 6);
-    const i64 r = s * 64 + lane;
-    unsigned m = 0;
-    if (STENCIL) m = st_mask[s * 64 + lane];
-    double acc[MB][8];
-#pragma unroll
-    for (int q = 0; q < MB; ++q)
-#pragma unroll
-      for (int jj = 0; jj < 8; ++jj) acc[q][jj] = 0.0;
-    for (int k = 0; k < width; ++k)
-    {
-      const double a = __builtin_nontemporal_load(val + base + k * 64 + lane);
-      i64 c;
-      bool ok;
-      if (STENCIL)
-      {
-        ok = (m >> k) & 1u;
-        c = r + st_delta[8 * s + k];
-      }
-      else
-      {
-        const i32 cc = __builtin_nontemporal_load(col + base + k * 64 + lane);
-        ok = cc >= 0;
-        c = cc;
-      }
-      if (!ok) continue;
-#pragma unroll
-      for (int q = 0; q < MB; ++q)
-      {
-        if (q < nb)
-        {
-          const double2 *xr = reinterpret_cast<const double2 *>(Qin + ((i64)(b0 + q) * n + c) * 8);
-#pragma unroll
-          for (int h = 0; h < 4; ++h)
-          {
-            const double2 xv = xr[h];
-            acc[q][2 * h] += a * xv.x;
-            acc[q][2 * h + 1] += a * xv.y;
-          }
-        }
-      }
-    }
-    if (r < nrows)
-    {
-#pragma unroll
-      for (int q = 0; q < MB; ++q)
-        if (q < nb)
-        {
-          double2 *yr = reinterpret_cast<double2 *>(Qout + ((i64)(b0 + q) * n + r) * 8);
-#pragma unroll
-          for (int h = 0; h < 4; ++h) yr[h] = make_double2(acc[q][2 * h], acc[q][2 * h + 1]);
-        }
-    }
-  }
-}
-
 void launch_spmm_mv8(const eig_mat_s &A, i64 m, const double *Qin, double *Qout, hipStream_t s)
 {
   EIG_CHECK(A.br == 1 && A.bc == 1, EIG_ERR_BLOCKSIZE,
@@ -151,21 +77,8 @@ void launch_spmm_mv8(const eig_mat_s &A, i64 m, const double *Qin, double *Qout,
   const int nblk = (int)(m / 8);
   if (A.R == 1)
   {
-    // stencil offsets are global col - global row; on one rank the window starts at 0, so
-    // window-local column = r + delta.  Mixed images use the explicit columns (always present).
-    const bool st = A.n_stencil_slices == A.nslices && A.n_stencil_slices > 0 && A.own_offset == 0;
-    constexpr int MB = 2;
-    const int gx = grid_for(A.nslices, 4, kStreamBlocks);
-    for (int b0 = 0; b0 < nblk; b0 += MB)
-    {
-      const int nb = nblk - b0 < MB ? nblk - b0 : MB;
-      if (st)
-        hipLaunchKernelGGL((k_spmm_mv8_rows<MB, true>), dim3(gx), dim3(256), 0, s, A.nb_rows, A.nslices, A.slice_ptr,
-                           A.val, A.col, A.st_delta, A.st_mask, Qin, Qout, A.nb_rows, b0, nb);
-      else
-        hipLaunchKernelGGL((k_spmm_mv8_rows<MB, false>), dim3(gx), dim3(256), 0, s, A.nb_rows, A.nslices,
-                           A.slice_ptr, A.val, A.col, A.st_delta, A.st_mask, Qin, Qout, A.nb_rows, b0, nb);
-    }
+    // row per lane over 64-row slices, window layout (k_block.hip); ld = n on one rank
+    launch_sell_mv8(A, m, Qin, Qout, s);
     return;
   }
   const int MB = 4;

@@ -29,7 +29,7 @@ def _tflags(timed):
     return LANCZOS_TIME_KERNELS if timed else 0
 
 
-GEN_LAPLACE2D, GEN_NEUMANN2D, GEN_PU2D, GEN_IDENTITY2D, GEN_POISSON3D, GEN_Q1ELAST3D = range(6)
+GEN_LAPLACE2D, GEN_NEUMANN2D, GEN_PU2D, GEN_IDENTITY2D, GEN_POISSON3D, GEN_Q1ELAST3D, GEN_P1STIFF3D, GEN_P1MASS3D = range(8)
 
 
 class EigError(RuntimeError):
@@ -48,6 +48,11 @@ class _MatInfo(ctypes.Structure):
                [("br", ctypes.c_int), ("bc", ctypes.c_int)] + \
                [(k, ctypes.c_int64) for k in ("halo_recv", "halo_send", "device_bytes", "stencil_slices",
                                               "rows_per_lane")]
+
+
+class BlockTiming(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_double) for k in ("total_ms", "kspmm_ms", "cheb_ms", "orth_ms", "norm_ms")] + \
+               [("steps", ctypes.c_int64), ("cheb_launches", ctypes.c_int64)]
 
 
 class Timing(ctypes.Structure):
@@ -117,6 +122,14 @@ SIGNATURES = {
     "eig_lanczos_destroy": (_int, [_vp]),
     "eig_lanczos_capture": (_int, [_vp, _int, _int, ctypes.POINTER(_int)]),
     "eig_lanczos_replay": (_int, [_vp, ctypes.POINTER(Timing)]),
+    "eig_blanczos_create": (_int, [_vp, _vp, _int, _int, _int, _dbl, _dbl, _u, ctypes.POINTER(_vp)]),
+    "eig_blanczos_step": (_int, [_vp, _int, ctypes.POINTER(BlockTiming)]),
+    "eig_blanczos_ritz": (_int, [_vp, _int, _int, _vp, _vp, _vp]),
+    "eig_blanczos_tmatrix": (_int, [_vp, ctypes.POINTER(_int), _vp]),
+    "eig_blanczos_destroy": (_int, [_vp]),
+    "eig_mass_solve_mv8": (_int, [_vp, _i64, _int, _dbl, _dbl, _vp, _vp]),
+    "eig_panel_update_mv8": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _dbl, _dbl, _vp]),
+    "eig_panel_gram_mv8": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _vp]),
     "eig_flops_orthonormalize": (_dbl, [_i64, _i64]),
     "eig_bytes_orthonormalize_blocked": (_dbl, [_i64, _i64, _int]),
     "eig_gen_nnzb": (_i64, [_int, _int]),
@@ -476,6 +489,60 @@ def lanczos_solve(A, nev, ncv, which=WHICH_LA, seed=123, want_evec=True):
     A.ctx.check(lib.eig_lanczos_solve(A.h, nev, ncv, which, seed, _np_ptr(ev), _np_ptr(evec) if want_evec else None,
                                       _np_ptr(res)))
     return ev, (evec.reshape(nev, A.n) if want_evec else None), res
+
+
+def panel_update_mv8(ctx, n, m1, m2, Q, S, alpha, beta, Y):
+    ctx.check(lib.eig_panel_update_mv8(ctx.h, n, m1, m2, Q.ptr, S.ptr, alpha, beta, Y.ptr))
+
+
+def panel_gram_mv8(ctx, n, m1, m2, Q1, Q2, G):
+    ctx.check(lib.eig_panel_gram_mv8(ctx.h, n, m1, m2, Q1.ptr, Q2.ptr, G.ptr))
+
+
+def mass_solve_mv8(M, m, degree, B, X, lmin=0.5, lmax=2.5):
+    M.ctx.check(lib.eig_mass_solve_mv8(M.h, m, degree, lmin, lmax, B.ptr, X.ptr))
+
+
+class BlockLanczos:
+    """eig_blanczos_t: block Lanczos for K x = lambda M x (config C5), see include/eigmi.h."""
+
+    def __init__(self, K, M, block=32, max_steps=8, degree=36, lmin=0.5, lmax=2.5, seed=123):
+        self.K, self.M, self.block = K, M, block
+        h = _vp()
+        K.ctx.check(lib.eig_blanczos_create(K.h, M.h, block, max_steps, degree, lmin, lmax, seed, ctypes.byref(h)))
+        self.h = h
+
+    def step(self, steps):
+        t = BlockTiming()
+        self.K.ctx.check(lib.eig_blanczos_step(self.h, steps, ctypes.byref(t)))
+        return t
+
+    def tmatrix(self):
+        d = _int(0)
+        self.K.ctx.check(lib.eig_blanczos_tmatrix(self.h, ctypes.byref(d), None))
+        T = np.zeros((d.value, d.value))
+        self.K.ctx.check(lib.eig_blanczos_tmatrix(self.h, ctypes.byref(d), _np_ptr(T)))
+        return T
+
+    def ritz(self, nev, which=WHICH_LA, want_evec=False, want_resid=True):
+        ev = np.zeros(nev)
+        n = self.K.info.n
+        evec = np.zeros(nev * n) if want_evec else None
+        res = np.zeros(nev) if want_resid else None
+        self.K.ctx.check(lib.eig_blanczos_ritz(self.h, nev, which, _np_ptr(ev), _np_ptr(evec) if want_evec else None,
+                                               _np_ptr(res) if want_resid else None))
+        return ev, (evec.reshape(nev, n) if want_evec else None), res
+
+    def close(self):
+        if self.h and self.K.h and self.K.ctx.h:
+            lib.eig_blanczos_destroy(self.h)
+        self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 # --------------------------------------------------------------------------------------- generators

@@ -237,6 +237,46 @@ enum eig_which { EIG_WHICH_LA = 0, EIG_WHICH_SA = 1 };
 int eig_lanczos_solve(eig_mat_t A, int nev, int ncv, int which, unsigned seed, double *eval_host,
                       double *evec_host, double *resid_host);
 
+/* ---------------------------------------------------------------- block Lanczos (config C5) */
+/* Generalised symmetric-definite eigenproblem K x = lambda M x by block Lanczos in the M-inner
+ * product on the operator M^-1 K (the pencil GeneralizedInverse solves, eigensolver.hh:204-351,
+ * and ARPACK's computeGenSymShiftInvertMinMagnitude, arpack_geneo_wrapper.hh:581-658; both need a
+ * sparse LU that does not exist at C5's size).  Per step j (block size b, basis V_0..V_j):
+ *   W = K V_j,  A_j = V_j^T W;  Z = M^-1 W by `degree` Chebyshev-Jacobi steps on the spectrum
+ *   bounds [lmin, lmax] of diag(M)^-1 M (P1 tetrahedra: [0.5, 2.5], Wathen's element bound; the
+ *   solve has no reductions);  two classical Gram-Schmidt passes of Z against V_0..V_j in the
+ *   M-inner product (panel V^T (M Z) on MFMA);  CholQR2:  Z = V_{j+1} B_{j+1}.
+ * K and M: same rows / column window (shared pattern, e.g. eig_gen kinds 6 and 7), 1x1 blocks;
+ * with a communicator, row-partitioned (eig_mat_create_bcsr_dist) and every panel allreduced.
+ * The start block is mt19937(seed) normal numbers in MultiVector fill order (eigensolver.hh:49-55). */
+typedef struct eig_blanczos_s *eig_blanczos_t;
+typedef struct eig_blanczos_timing {
+  double total_ms;   /* device time of the step batch (events, first to last) */
+  double kspmm_ms;   /* W = K V_j + the A_j Gram */
+  double cheb_ms;    /* the Chebyshev mass solve (degree - 1 fused M SpMM steps) */
+  double orth_ms;    /* two CGS passes: M SpMM + MFMA panel Gram + panel update */
+  double norm_ms;    /* CholQR2: 2 x (M SpMM + Gram + host 32x32 Cholesky + triangular update) */
+  int64_t steps;
+  int64_t cheb_launches; /* fused Chebyshev kernel launches (one per 16 columns per step) */
+} eig_blanczos_timing;
+int eig_blanczos_create(eig_mat_t K, eig_mat_t M, int block, int max_steps, int degree, double lmin, double lmax,
+                        unsigned seed, eig_blanczos_t *ws);
+int eig_blanczos_step(eig_blanczos_t ws, int steps, eig_blanczos_timing *timing);
+/* Ritz pairs of the k steps taken: eval_host[nev] (LA descending / SA ascending), evec_host: nev
+ * owned-row vectors with y^T M y = 1 (or NULL), resid_host[nev]: ||K y - theta M y||_2 (or NULL). */
+int eig_blanczos_ritz(eig_blanczos_t ws, int nev, int which, double *eval_host, double *evec_host, double *resid_host);
+/* The block tridiagonal T (dim = steps * block; T_host dim x dim row-major, or NULL for the size). */
+int eig_blanczos_tmatrix(eig_blanczos_t ws, int *dim, double *T_host);
+int eig_blanczos_destroy(eig_blanczos_t ws);
+/* X = M^-1 B for m columns (window layout) by `degree` Chebyshev-Jacobi steps (the operator's solve). */
+int eig_mass_solve_mv8(eig_mat_t M, int64_t m, int degree, double lmin, double lmax, const double *B, double *X);
+/* Tall-skinny panel kernels on n-row MultiVector<double,8> buffers (single rank):
+ * Y = beta Y + alpha Q S (Q n x m1, S m1 x m2 row-major device, m2 in {8,16,24,32}; Y may be Q), and
+ * G = Q1^T Q2 (m1 x m2 row-major device) on MFMA with a deterministic two-stage reduction. */
+int eig_panel_update_mv8(eig_ctx_t ctx, int64_t n, int64_t m1, int64_t m2, const double *Q, const double *S,
+                         double alpha, double beta, double *Y);
+int eig_panel_gram_mv8(eig_ctx_t ctx, int64_t n, int64_t m1, int64_t m2, const double *Q1, const double *Q2, double *G);
+
 /* a14: the reference's analytic GS models (kernels_cpp.hh:98-116, :157-175). */
 double eig_flops_orthonormalize(int64_t n, int64_t m);
 double eig_bytes_orthonormalize_blocked(int64_t n, int64_t m, int b);
@@ -246,7 +286,9 @@ double eig_bytes_orthonormalize_blocked(int64_t n, int64_t m, int b);
  * produced on the host into caller buffers (sizes from the *_nnz functions).  kind:
  *   0 2-D Dirichlet 5-pt N*N (setupLaplacian)      1 2-D Neumann (.cc:105-121)
  *   2 2-D partition-of-unity B (.cc:124-143)       3 2-D identity pattern (.cc:145-156)
- *   4 3-D Poisson 7-pt N^3                          5 3-D Q1 "elasticity" L_Q1 (x) C, 3x3 blocks */
+ *   4 3-D Poisson 7-pt N^3                          5 3-D Q1 "elasticity" L_Q1 (x) C, 3x3 blocks
+ *   6 3-D P1 stiffness K, Kuhn 6-tet split, N^3     7 3-D P1 consistent mass M, same 15-pt pattern
+ *     interior nodes, h = 1/(N+1) (config C5)            (pattern(K) == pattern(M), config C5) */
 int64_t eig_gen_nnzb(int kind, int N);
 int eig_gen_matrix(int kind, int N, int overlap, int64_t *rowptr, int32_t *col, double *vals);
 /* Rows [row_begin, row_begin + nrows) of the same matrix (for eig_mat_create_bcsr_dist). */

@@ -232,3 +232,106 @@ def mv_to_cols(Q, n, m):
 def cols_to_mv(X):
     n, m = X.shape
     return np.ascontiguousarray(X.reshape(n, m // 8, 8).transpose(1, 0, 2).reshape(-1))
+
+
+# ------------------------------------------------------------------------------- config C5 (numpy)
+# Independent restatements for the generalised block Lanczos: the P1 matrices by GLOBAL element
+# assembly (the product generator, dune-eigensolver_amd/csrc/gen.cpp kinds 6/7, assembles row by
+# row), and the block Lanczos recurrence in dense numpy.  There is no reference block Lanczos; the
+# reference's generalised path is GeneralizedInverse (eigensolver.hh:204-351) / ARPACK shift-invert
+# (arpack_geneo_wrapper.hh:581-658), whose answer -- the eigenpairs of (K, M) -- scipy.linalg.eigh
+# gives exactly at these sizes; that is the parity anchor of the tests.
+
+_KUHN_PERMS = ((0, 1, 2), (0, 2, 1), (1, 0, 2), (1, 2, 0), (2, 0, 1), (2, 1, 0))
+_PATH = np.array([[1, -1, 0, 0], [-1, 2, -1, 0], [0, -1, 2, -1], [0, 0, -1, 1]], np.float64)
+
+
+def p1_kuhn(N):
+    """(K, M) scipy CSR for P1 on the Kuhn 6-tetrahedra split of the unit cube, N^3 interior nodes
+    (lexicographic, x fastest), Dirichlet nodes eliminated; K and M share the 15-point edge
+    pattern (K's entries on the face / body diagonals are exact zeros)."""
+    import scipy.sparse as sp
+    h = 1.0 / (N + 1)
+    c = np.arange(N + 1)
+    cz, cy, cx = np.meshgrid(c, c, c, indexing="ij")
+    corners = np.stack([cx.ravel(), cy.ravel(), cz.ravel()], axis=1)  # cube lower corners (x, y, z)
+    rows, cols, kv, mv = [], [], [], []
+    Ke = (h / 6.0) * _PATH
+    Me = (h ** 3 / 120.0) * (np.ones((4, 4)) + np.eye(4))
+    for p in _KUHN_PERMS:
+        v = [corners.copy()]
+        v1 = corners.copy()
+        v1[:, p[0]] += 1
+        v2 = v1.copy()
+        v2[:, p[1]] += 1
+        v.extend([v1, v2, corners + 1])
+        ids = []
+        for vert in v:
+            inside = np.all((vert >= 1) & (vert <= N), axis=1)
+            g = ((vert[:, 2] - 1) * N + (vert[:, 1] - 1)) * N + (vert[:, 0] - 1)
+            ids.append(np.where(inside, g, -1))
+        for a in range(4):
+            for b in range(4):
+                ok = (ids[a] >= 0) & (ids[b] >= 0)
+                rows.append(ids[a][ok])
+                cols.append(ids[b][ok])
+                kv.append(np.full(ok.sum(), Ke[a, b]))
+                mv.append(np.full(ok.sum(), Me[a, b]))
+    r, cc = np.concatenate(rows), np.concatenate(cols)
+    n = N ** 3
+    K = sp.coo_matrix((np.concatenate(kv), (r, cc)), shape=(n, n)).tocsr()
+    M = sp.coo_matrix((np.concatenate(mv), (r, cc)), shape=(n, n)).tocsr()
+    K.sort_indices()
+    M.sort_indices()
+    return K, M
+
+
+def cheb_solve(M, B, degree, lmin=0.5, lmax=2.5):
+    """x_degree of the Golub-Varga Chebyshev semi-iteration for M X = B with the Jacobi splitting
+    (the same recurrence as k_sell_mv8<kCheb>, dune-eigensolver_amd/csrc/k_block.hip)."""
+    dinv = 1.0 / M.diagonal()
+    gamma, mu = 2.0 / (lmin + lmax), (lmax - lmin) / (lmax + lmin)
+    x_prev = np.zeros_like(B)
+    x = gamma * dinv[:, None] * B
+    omega = 1.0
+    for k in range(1, degree):
+        omega = 1.0 / (1.0 - 0.5 * mu * mu) if k == 1 else 1.0 / (1.0 - 0.25 * mu * mu * omega)
+        x_new = omega * (x + gamma * dinv[:, None] * (B - M @ x) - x_prev) + x_prev
+        x_prev, x = x, x_new
+    return x
+
+
+def block_lanczos_gen(K, M, V0, steps, degree=36, lmin=0.5, lmax=2.5):
+    """Block Lanczos in the M-inner product on M^-1 K (include/eigmi.h, eig_blanczos_*): returns
+    the block tridiagonal T (steps*b square) and the basis [V_0 .. V_steps]."""
+    def mcholqr2(Z):
+        Rt = np.eye(Z.shape[1])
+        for _ in range(2):
+            G = Z.T @ (M @ Z)
+            G = 0.5 * (G + G.T)
+            R = np.linalg.cholesky(G).T
+            Z = np.linalg.solve(R.T, Z.T).T
+            Rt = R @ Rt
+        return Z, Rt
+    b = V0.shape[1]
+    V, _ = mcholqr2(V0)
+    basis = [V]
+    A, Bs = [], []
+    for j in range(steps):
+        W = K @ basis[j]
+        Aj = basis[j].T @ W
+        A.append(0.5 * (Aj + Aj.T))
+        Z = cheb_solve(M, W, degree, lmin, lmax)
+        Vall = np.hstack(basis)
+        for _ in range(2):
+            Z = Z - Vall @ (Vall.T @ (M @ Z))
+        Z, R = mcholqr2(Z)
+        basis.append(Z)
+        Bs.append(R)
+    T = np.zeros((steps * b, steps * b))
+    for j in range(steps):
+        T[j * b:(j + 1) * b, j * b:(j + 1) * b] = A[j]
+        if j + 1 < steps:
+            T[(j + 1) * b:(j + 2) * b, j * b:(j + 1) * b] = Bs[j]
+            T[j * b:(j + 1) * b, (j + 1) * b:(j + 2) * b] = Bs[j].T
+    return T, basis

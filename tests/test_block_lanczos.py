@@ -1,0 +1,166 @@
+"""Config C5: the generalised pencil K x = lambda M x of P1 on the Kuhn split, block
+Lanczos k=32 with the tall-skinny panels on MFMA.
+
+CPU: the product generator (gen.cpp kinds 6/7, row-by-row assembly) against the independent
+global element assembly in oracle.p1_kuhn -- identical pattern, values to 1e-15 relative.
+GPU: the panel kernels against numpy, the Chebyshev mass solve against scipy's sparse direct
+solve, and the block Lanczos Ritz values against (a) the numpy restatement of the same recurrence
+(oracle.block_lanczos_gen, same start block) and (b) the exact eigenvalues of (K, M) from
+scipy.linalg.eigh -- the answer the reference's GeneralizedInverse / ARPACK shift-invert path
+computes (eigensolver.hh:204-351, arpack_geneo_wrapper.hh:581-658).
+
+Tolerances: panel Gram / update 1e-13 relative (summation order differs from numpy); mass solve
+1e-12 relative at degree 36 (Chebyshev bound 2 rho^36 ~ 2e-15 in the D-norm); Ritz values vs the
+numpy recurrence 1e-9 relative (unconverged values amplify rounding differences), converged
+extreme eigenvalues vs eigh 1e-9 relative."""
+import numpy as np
+import pytest
+
+import eigmi
+import oracle
+
+
+@pytest.mark.parametrize("N", [1, 2, 3, 6])
+def test_p1_generator_matches_global_assembly(N):
+    K, M = oracle.p1_kuhn(N)
+    for kind, ref in ((eigmi.GEN_P1STIFF3D, K), (eigmi.GEN_P1MASS3D, M)):
+        rp, c, v = eigmi.gen_matrix(kind, N)
+        assert eigmi.lib.eig_gen_nnzb(kind, N) == ref.nnz
+        assert np.array_equal(rp, ref.indptr) and np.array_equal(c, ref.indices)
+        assert np.max(np.abs(v - ref.data)) <= 1e-15 * np.max(np.abs(ref.data))
+
+
+def test_p1_known_answers():
+    """K = h * (7-point Laplacian) on the shared 15-point pattern (the Kuhn split's P1 stiffness),
+    M symmetric positive definite, and the Jacobi-scaled mass spectrum inside Wathen's element
+    bound [1/2, 5/2] that the Chebyshev solve relies on."""
+    N = 6
+    K, M = oracle.p1_kuhn(N)
+    L7 = oracle.poisson3d(N).to_scipy()
+    assert abs(K - L7 / (N + 1)).max() <= 1e-15
+    d = 1.0 / np.sqrt(M.diagonal())
+    w = np.linalg.eigvalsh((M.multiply(d[:, None]).multiply(d[None, :])).toarray())
+    assert 0.5 <= w[0] and w[-1] <= 2.5
+
+
+def test_p1_rows_partition():
+    N = 5
+    rp, c, v = eigmi.gen_matrix(eigmi.GEN_P1MASS3D, N)
+    b, cnt = 40, 50
+    rr, cc, vv = eigmi.gen_rows(eigmi.GEN_P1MASS3D, N, b, cnt)
+    assert np.array_equal(cc[:rr[-1]], c[rp[b]:rp[b + cnt]])
+    assert np.array_equal(vv[:rr[-1]], v[rp[b]:rp[b + cnt]])
+
+
+def _upload(ctx, A):
+    return eigmi.Matrix.from_bcsr(ctx, A.indptr.astype(np.int64), A.indices.astype(np.int32), A.data)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,m1,m2", [(1000, 32, 32), (5003, 96, 32), (777, 8, 16), (20000, 160, 24)])
+def test_panel_gram(ctx, n, m1, m2):
+    rng = np.random.default_rng(n)
+    Q1, Q2 = rng.standard_normal((n, m1)), rng.standard_normal((n, m2))
+    d1, d2, G = ctx.array(oracle.cols_to_mv(Q1)), ctx.array(oracle.cols_to_mv(Q2)), ctx.zeros(m1 * m2)
+    eigmi.panel_gram_mv8(ctx, n, m1, m2, d1, d2, G)
+    g = G.get().reshape(m1, m2)
+    ref = Q1.T @ Q2
+    assert np.max(np.abs(g - ref)) <= 1e-13 * np.max(np.abs(Q1).sum(0)[:, None] * np.abs(Q2).max())
+    eigmi.panel_gram_mv8(ctx, n, m1, m2, d1, d2, G)
+    assert np.array_equal(G.get().reshape(m1, m2), g), "panel Gram must be run-to-run deterministic"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,m1,m2,alpha,beta", [(1000, 32, 32, -1.0, 1.0), (4099, 64, 8, 1.0, 0.0),
+                                                 (333, 8, 24, 0.5, -2.0)])
+def test_panel_update(ctx, n, m1, m2, alpha, beta):
+    rng = np.random.default_rng(m1 + m2)
+    Q, S, Y = rng.standard_normal((n, m1)), rng.standard_normal((m1, m2)), rng.standard_normal((n, m2))
+    dq, ds, dy = ctx.array(oracle.cols_to_mv(Q)), ctx.array(S.ravel()), ctx.array(oracle.cols_to_mv(Y))
+    eigmi.panel_update_mv8(ctx, n, m1, m2, dq, ds, alpha, beta, dy)
+    got = oracle.mv_to_cols(dy.get(), n, m2)
+    ref = beta * Y + alpha * (Q @ S)
+    assert np.max(np.abs(got - ref)) <= 1e-13 * (np.abs(Q) @ np.abs(S)).max()
+
+
+@pytest.mark.gpu
+def test_panel_update_in_place(ctx):
+    n, m = 2000, 16
+    rng = np.random.default_rng(7)
+    Q, S = rng.standard_normal((n, m)), np.triu(rng.standard_normal((m, m)))
+    dq, ds = ctx.array(oracle.cols_to_mv(Q)), ctx.array(S.ravel())
+    eigmi.panel_update_mv8(ctx, n, m, m, dq, ds, 1.0, 0.0, dq)
+    assert np.allclose(oracle.mv_to_cols(dq.get(), n, m), Q @ S, rtol=0, atol=1e-12)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,m", [(8, 8), (12, 32)])
+def test_mass_solve(ctx, N, m):
+    import scipy.sparse.linalg as sla
+    _, Mh = oracle.p1_kuhn(N)
+    M = _upload(ctx, Mh)
+    n = N ** 3
+    B = np.random.default_rng(N).standard_normal((n, m))
+    dB, dX = ctx.array(oracle.cols_to_mv(B)), ctx.zeros(n * m)
+    eigmi.mass_solve_mv8(M, m, 36, dB, dX)
+    X = oracle.mv_to_cols(dX.get(), n, m)
+    Xe = sla.spsolve(Mh.tocsc(), B)
+    assert np.max(np.abs(X - Xe)) <= 1e-12 * np.max(np.abs(Xe))
+    Xo = oracle.cheb_solve(Mh, B, 36)
+    assert np.max(np.abs(X - Xo)) <= 1e-13 * np.max(np.abs(Xo))
+
+
+@pytest.mark.gpu
+def test_block_lanczos_vs_recurrence_and_eigh(ctx):
+    import scipy.linalg as sl
+    N, b, steps = 10, 32, 14
+    Kh, Mh = oracle.p1_kuhn(N)
+    n = N ** 3
+    K, M = _upload(ctx, Kh), _upload(ctx, Mh)
+    bl = eigmi.BlockLanczos(K, M, block=b, max_steps=steps, degree=36, seed=123)
+    t = bl.step(steps)
+    assert t.steps == steps and t.total_ms > 0
+    T = bl.tmatrix()
+    V0 = oracle.mv_to_cols(oracle.random_mv8(n, b, 123), n, b)
+    Tref, _ = oracle.block_lanczos_gen(Kh, Mh, V0, steps)
+    th, thr = np.linalg.eigvalsh(T), np.linalg.eigvalsh(Tref)
+    assert np.max(np.abs(th - thr) / np.abs(thr)) <= 1e-9
+    exact = sl.eigh(Kh.toarray(), Mh.toarray(), eigvals_only=True)
+    ev, Y, res = bl.ritz(8, eigmi.WHICH_LA, want_evec=True)
+    assert np.max(np.abs(ev - exact[::-1][:8]) / exact[::-1][:8]) <= 1e-9
+    # the device residuals ||K y - theta M y|| are the host's on the returned vectors; relative to
+    # |theta| ||M y|| they are ~ sqrt(eigenvalue error) at this Krylov dimension
+    R = (Kh @ Y.T) - (Mh @ Y.T) * ev[None, :]
+    host_res = np.linalg.norm(R, axis=0)
+    assert np.allclose(res, host_res, rtol=1e-6, atol=0)
+    assert np.all(host_res / (ev * np.linalg.norm(Mh @ Y.T, axis=0)) <= 1e-4)
+    # Ritz vectors are M-orthonormal
+    G = Y @ (Mh @ Y.T)
+    assert np.max(np.abs(G - np.eye(8))) <= 1e-9
+    bl.close()
+
+
+@pytest.mark.gpu
+def test_block_lanczos_smallest_full_space(ctx):
+    """Small pencil (n = 216): with the Krylov space near the whole space the SMALLEST eigenvalues
+    -- the ones GeneralizedInverse returns -- are exact too."""
+    import scipy.linalg as sl
+    N, b, steps = 6, 8, 24
+    Kh, Mh = oracle.p1_kuhn(N)
+    K, M = _upload(ctx, Kh), _upload(ctx, Mh)
+    bl = eigmi.BlockLanczos(K, M, block=b, max_steps=steps, degree=40, seed=7)
+    bl.step(steps)
+    exact = sl.eigh(Kh.toarray(), Mh.toarray(), eigvals_only=True)
+    ev, _, res = bl.ritz(4, eigmi.WHICH_SA)
+    assert np.max(np.abs(ev - exact[:4]) / exact[:4]) <= 1e-8
+    bl.close()
+
+
+@pytest.mark.gpu
+def test_block_lanczos_argument_errors(ctx):
+    Kh, Mh = oracle.p1_kuhn(4)
+    K, M = _upload(ctx, Kh), _upload(ctx, Mh)
+    with pytest.raises(eigmi.EigError):
+        eigmi.BlockLanczos(K, M, block=12, max_steps=2)
+    with pytest.raises(eigmi.EigShapeError):
+        eigmi.BlockLanczos(K, M, block=32, max_steps=2)  # (2+1)*32 > 64 rows
