@@ -672,6 +672,20 @@ void build_sell(eig_mat_s &A, i64 nb, const int64_t *rowptr, const int32_t *col,
       }
     }
   });
+  {
+    std::vector<i64> bw(16, 0);
+    const i64 nt = std::min<i64>(16, std::max<i64>(1, nb / 65536));
+    std::vector<std::thread> th;
+    for (i64 t = 0; t < nt; ++t)
+      th.emplace_back([&, t] {
+        i64 m = 0;
+        for (i64 r = nb * t / nt; r < nb * (t + 1) / nt; ++r)
+          for (i64 p = rowptr[r]; p < rowptr[r + 1]; ++p) m = std::max<i64>(m, std::llabs((i64)col[p] - (row0 + r)));
+        bw[t] = m;
+      });
+    for (auto &x : th) x.join();
+    A.bandwidth = *std::max_element(bw.begin(), bw.end());
+  }
   A.nslices = ns;
   A.nnzb_padded = total;
   A.slice_ptr = dev_alloc<i64>(ns + 1);

@@ -278,7 +278,7 @@ extern "C" int eig_blanczos_step(eig_blanczos_t w, int steps, eig_blanczos_timin
         timing->total_ms = tt;
       }
       timing->steps = steps;
-      timing->cheb_launches = (int64_t)steps * std::max(0, w->degree - 1) * ((b / 8 + 1) / 2);
+      timing->cheb_launches = (int64_t)steps * std::max(0, w->degree - 1) * sell_mv8_launches(b);
     }
   });
 }

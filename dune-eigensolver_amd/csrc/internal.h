@@ -181,6 +181,9 @@ struct eig_mat_s {
   std::vector<eigmi::HaloRange> sends, recvs;
   eigmi::i64 halo_send = 0, halo_recv = 0;
   eigmi::i64 device_bytes = 0;
+  // max |global col - global row| over the stored blocks (block units): the far-neighbour distance
+  // the XCD-aware gather kernels size their grid by (k_block.hip)
+  eigmi::i64 bandwidth = 0;
 };
 
 namespace eigmi {
@@ -253,6 +256,8 @@ void launch_resid_sq(i64 n, const double *x, const double *y, double theta, doub
 // Window-layout multivector kernels (k_block.hip).  m columns (multiple of 8), leading dimension
 // = the matrix window, owned rows at own_offset.
 void launch_sell_mv8(const eig_mat_s &A, i64 m, const double *X, double *Y, hipStream_t s);
+int mv8_kernel_choice();
+int sell_mv8_launches(i64 m);  // kernel launches per launch_sell_mv8 / launch_cheb_step call
 void launch_cheb_step(const eig_mat_s &M, i64 m, const double *Xk, double *Xold, const double *B, const double *dinv,
                       double omega, double gamma, hipStream_t s);
 void launch_diag_inv(const eig_mat_s &A, double *dinv, hipStream_t s);

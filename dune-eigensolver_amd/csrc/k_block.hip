@@ -14,11 +14,15 @@
 // is ld rows of 8 contiguous doubles at Q + 8 b ld; owned row r sits at window row own + r.  On
 // one rank ld = n and own = 0, which is the reference's MultiVector<double,8> layout
 // (multivector.hh:130-139).
+#include <cstdlib>
+#include <string>
+
 #include "internal.h"
 
 namespace eigmi {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
+typedef double dv2 __attribute__((ext_vector_type(2)));
 
 static inline int grid_cap(i64 work, i64 per_block, int cap)
 {
@@ -131,9 +135,167 @@ __global__ __launch_bounds__(256) void k_sell_mv8(i64 nrows, i64 nslices, const 
   }
 }
 
+// Quad mapping: 4 lanes per row (lane owns column pair 2 (l & 3), 2 (l & 3) + 1 of every column
+// block), 16 rows per wave, a workgroup (4 waves) per 64-row slice, MB column blocks per matrix
+// pass.  Entries are consumed U at a time: the U columns / values are loaded first, then all U * MB
+// 16-B gathers are issued before the multiply-adds (memory-level parallelism without holding
+// whole 64-B rows per lane).  Same per-column summation order as k_sell_mv8.
+//
+// XCD-aware plane-slab schedule.  A unit is 16 W rows (W waves of 16 rows; W = 2: two units per
+// 64-row slice).  The rows are cut into "planes" of P8 units (P8 = the matrix bandwidth -- N^2
+// rows for the 3-D grids -- rounded up to 8 segments) and every plane into 8 segments; the
+// workgroups on XCD x (b % 8 == x: blocks are dealt round-robin over the XCDs -- a speed
+// assumption only, any placement gives the same result) sweep segment x of plane 0, then of plane
+// 1, ..., interleaved unit by unit, so the XCD's front of resident workgroups moves through one
+// contiguous slab.  A row's x / y neighbours lie in the front, its z - 1 neighbours in the
+// previous plane's segment the same XCD just streamed: both are read from the XCD's own L2, and
+// each X row comes from HBM about once.
+template <int MB, int U, int W, bool STENCIL, int EPI>
+__global__ __launch_bounds__(64 * W) void k_sell_mv8q(i64 nrows, i64 nslices, const i64 *__restrict__ slice_ptr,
+                                                      const double *__restrict__ val, const i32 *__restrict__ col,
+                                                      const i32 *__restrict__ st_delta,
+                                                      const uint8_t *__restrict__ st_mask, const double *__restrict__ X,
+                                                      double *__restrict__ Y, i64 ld, i64 own, int b0,
+                                                      const double *__restrict__ Bv, const double *__restrict__ dinv,
+                                                      double omega, double gamma, i64 per)
+{
+  constexpr int UPS = 4 / W;  // units per slice
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int cp = lane & 3;
+  const i64 nunits = nslices * UPS;
+  const i64 seg = per;  // units per plane segment; plane = 8 segments
+  const int xcd = blockIdx.x & 7;
+  const i64 nloc = gridDim.x >> 3;  // workgroups per XCD (grid is a multiple of 8)
+  const double *Xc = X + (i64)b0 * ld * 8 + 2 * cp;  // column pair cp of column block b0
+  for (i64 t = blockIdx.x >> 3;; t += nloc)
+  {
+    const i64 pl = t / seg;
+    const i64 un = pl * 8 * seg + xcd * seg + (t - pl * seg);
+    if (pl * 8 * seg >= nunits) break;
+    if (un >= nunits) continue;  // tail of the last plane
+    const i64 s = un / UPS;
+    const int ri = (int)(un % UPS) * 16 * W + wave * 16 + (lane >> 2);
+    const i64 base = slice_ptr[s];
+    const int width = (int)((slice_ptr[s + 1] - base) >> 6);
+    const i64 r = s * 64 + ri;
+    unsigned m = 0;
+    if (STENCIL) m = st_mask[s * 64 + ri];
+    double2 acc[MB];
+#pragma unroll
+    for (int q = 0; q < MB; ++q) acc[q] = make_double2(0.0, 0.0);
+    for (int k0 = 0; k0 < width; k0 += U)
+    {
+      // branch-free: indices clamped into the slice, every load issued before the first wait;
+      // entries that are not stored (padding, mask bit clear, k >= width) gather the row's own
+      // in-window element and are discarded by a select, never multiplied in (the reference
+      // loops over stored entries only: inf * 0 or -0 + 0 must not enter the sum)
+      double a[U];
+      i64 c[U];
+      bool okk[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+      {
+        const int k = k0 + u < width ? k0 + u : width - 1;
+        a[u] = __builtin_nontemporal_load(val + base + k * 64 + ri);
+        if (STENCIL)
+        {
+          okk[u] = (k0 + u < width) && ((m >> (k0 + u)) & 1u);
+          c[u] = own + r + (okk[u] ? st_delta[8 * s + k] : 0);
+        }
+        else
+        {
+          const i32 ci = __builtin_nontemporal_load(col + base + k * 64 + ri);
+          okk[u] = (k0 + u < width) && ci >= 0;
+          c[u] = okk[u] ? (i64)ci : own + r;
+        }
+      }
+      double2 xv[U][MB];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int q = 0; q < MB; ++q) xv[u][q] = *reinterpret_cast<const double2 *>(Xc + ((i64)q * ld + c[u]) * 8);
+      if (EPI == kStore)
+      {
+        // bitwise the reference: separately rounded products and sums over stored entries only
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int q = 0; q < MB; ++q)
+          {
+            const double tx = acc[q].x + a[u] * xv[u][q].x, ty = acc[q].y + a[u] * xv[u][q].y;
+            acc[q].x = okk[u] ? tx : acc[q].x;
+            acc[q].y = okk[u] ? ty : acc[q].y;
+          }
+      }
+      else
+      {
+        // Chebyshev step (tolerance-checked, not bitwise): fused multiply-adds, non-stored
+        // entries contribute 0 * (the row's own finite x) = 0
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+        {
+          const double au = okk[u] ? a[u] : 0.0;
+#pragma unroll
+          for (int q = 0; q < MB; ++q)
+          {
+            acc[q].x = __builtin_fma(au, xv[u][q].x, acc[q].x);
+            acc[q].y = __builtin_fma(au, xv[u][q].y, acc[q].y);
+          }
+        }
+      }
+    }
+    if (r < nrows)
+    {
+      // read-once / write-once streams are non-temporal so that the XCD's L2 keeps X for the
+      // neighbour reuse of the plane-slab schedule
+      double di = 0.0;
+      if (EPI == kCheb) di = __builtin_nontemporal_load(dinv + r);
+#pragma unroll
+      for (int q = 0; q < MB; ++q)
+      {
+        const i64 at = ((i64)(b0 + q) * ld + own + r) * 8 + 2 * cp;
+        double *yr = Y + at;
+        double o0, o1;
+        if (EPI == kStore)
+        {
+          o0 = acc[q].x;
+          o1 = acc[q].y;
+        }
+        else
+        {
+          const double2 xk = *reinterpret_cast<const double2 *>(X + at);
+          const dv2 bb = __builtin_nontemporal_load(reinterpret_cast<const dv2 *>(Bv + at));
+          const dv2 xo = __builtin_nontemporal_load(reinterpret_cast<const dv2 *>(yr));
+          const double gd = gamma * di;
+          o0 = omega * (xk.x + gd * (bb.x - acc[q].x) - xo.x) + xo.x;
+          o1 = omega * (xk.y + gd * (bb.y - acc[q].y) - xo.y) + xo.y;
+        }
+        __builtin_nontemporal_store(dv2{o0, o1}, reinterpret_cast<dv2 *>(yr));
+      }
+    }
+  }
+}
+
 namespace {
 bool all_stencil(const eig_mat_s &A) { return A.n_stencil_slices == A.nslices && A.n_stencil_slices > 0; }
 
+}  // namespace
+
+// Kernel mapping for the window-layout SpMM / Chebyshev step: EIGMI_MV8_KERNEL = rows (lane per
+// row, 16 columns per matrix pass), quad (4 lanes per row, 32 columns per pass; default) or quad2
+// (4 lanes per row, 16 columns per pass).
+int mv8_kernel_choice()
+{
+  static int v = [] {
+    const char *e = std::getenv("EIGMI_MV8_KERNEL");
+    if (e && std::string(e) == "rows") return 0;
+    if (e && std::string(e) == "quad2") return 2;
+    return 1;
+  }();
+  return v;
+}
+
+namespace {
 template <int EPI>
 void sell_mv8(const eig_mat_s &A, i64 m, const double *X, double *Y, const double *Bv, const double *dinv,
               double omega, double gamma, hipStream_t s)
@@ -142,24 +304,82 @@ void sell_mv8(const eig_mat_s &A, i64 m, const double *X, double *Y, const doubl
             "matmul_sparse_tallskinny_blocked: only implemented for FieldMatrix<..,1,1>");
   EIG_CHECK(A.R == 1, EIG_ERR_ARG, "multivector kernels need the R = 1 SELL image (unset EIGMI_SELL_R)");
   const int nblk = (int)(m / 8);
-  constexpr int MB = 2;
-  const int gx = grid_cap(A.nslices, 4, kStreamBlocks);
   const bool st = all_stencil(A);
-  for (int b0 = 0; b0 < nblk; b0 += MB)
+  const int kind = mv8_kernel_choice();
+  if (kind == 0)
   {
-    const int nb = nblk - b0 < MB ? nblk - b0 : MB;
-    if (st)
-      hipLaunchKernelGGL((k_sell_mv8<MB, true, EPI>), dim3(gx), dim3(256), 0, s, A.nb_rows, A.nslices, A.slice_ptr,
-                         A.val, A.col, A.st_delta, A.st_mask, X, Y, A.window, A.own_offset, b0, nb, Bv, dinv, omega,
-                         gamma);
-    else
-      hipLaunchKernelGGL((k_sell_mv8<MB, false, EPI>), dim3(gx), dim3(256), 0, s, A.nb_rows, A.nslices, A.slice_ptr,
-                         A.val, A.col, A.st_delta, A.st_mask, X, Y, A.window, A.own_offset, b0, nb, Bv, dinv, omega,
-                         gamma);
+    constexpr int MB = 2;
+    const int gx = grid_cap(A.nslices, 4, kStreamBlocks);
+    for (int b0 = 0; b0 < nblk; b0 += MB)
+    {
+      const int nb = nblk - b0 < MB ? nblk - b0 : MB;
+      if (st)
+        hipLaunchKernelGGL((k_sell_mv8<MB, true, EPI>), dim3(gx), dim3(256), 0, s, A.nb_rows, A.nslices, A.slice_ptr,
+                           A.val, A.col, A.st_delta, A.st_mask, X, Y, A.window, A.own_offset, b0, nb, Bv, dinv, omega,
+                           gamma);
+      else
+        hipLaunchKernelGGL((k_sell_mv8<MB, false, EPI>), dim3(gx), dim3(256), 0, s, A.nb_rows, A.nslices,
+                           A.slice_ptr, A.val, A.col, A.st_delta, A.st_mask, X, Y, A.window, A.own_offset, b0, nb, Bv,
+                           dinv, omega, gamma);
+    }
+  }
+  else
+  {
+    // quad: 4 column blocks (32 columns) per matrix pass (quad2: 2), 4 entries in flight, 2-wave
+    // workgroups; grid from the XCD-aware schedule (k_sell_mv8q)
+    const int MBq = kind == 2 ? 2 : 4;
+    constexpr int W = 2;
+    const i64 nunits = A.nslices * (4 / W);
+    const i64 rows_per_unit = 16 * W;
+    // resident 2-wave workgroups at the kernel's occupancy (4 waves / SIMD for MB = 4, 8 for MB = 2),
+    // a multiple of 8 (one share per XCD)
+    const i64 resident = (i64)A.ctx->num_cu * 4 * (kind == 2 ? 8 : 4) / W;
+    // half the resident capacity: the plane-slab working set (front + the previous and next
+    // planes' segments) then fits the XCD's 4 MiB L2 better (tools/spmm_sweep.py: -10 % time on
+    // the 7-point SpMM / Chebyshev step at 224^3, equal on the 15-point P1 mass)
+    i64 gcap = resident / 2;
+    if (const char *e = std::getenv("EIGMI_MV8_GX"))  // experiment knob: workgroups in flight
+      gcap = std::max<i64>(8, std::atoll(e));
+    const i64 gx = std::max<i64>(8, std::min<i64>(gcap, (nunits + 7) / 8 * 8) / 8 * 8);
+    // plane segment: bandwidth rows / 8, in units (at least 1); no bandwidth (diagonal): 1/8 of all
+    const i64 prow = A.bandwidth > 0 ? A.bandwidth : std::max<i64>(1, A.nb_rows);
+    const i64 per = std::max<i64>(1, (prow + 8 * rows_per_unit - 1) / (8 * rows_per_unit));
+    for (int b0 = 0; b0 < nblk; b0 += MBq)
+    {
+      const int nb = nblk - b0 < MBq ? nblk - b0 : MBq;
+#define EIGMI_QUAD(MBV, STV)                                                                                        \
+  hipLaunchKernelGGL((k_sell_mv8q<MBV, 4, W, STV, EPI>), dim3((unsigned)gx), dim3(64 * W), 0, s, A.nb_rows, A.nslices, \
+                     A.slice_ptr, A.val, A.col, A.st_delta, A.st_mask, X, Y, A.window, A.own_offset, b0, Bv, dinv,     \
+                     omega, gamma, per)
+#define EIGMI_QUAD_NB(STV)            \
+  switch (nb)                         \
+  {                                   \
+    case 1: EIGMI_QUAD(1, STV); break; \
+    case 2: EIGMI_QUAD(2, STV); break; \
+    case 3: EIGMI_QUAD(3, STV); break; \
+    default: EIGMI_QUAD(4, STV); break; \
+  }
+      if (st)
+      {
+        EIGMI_QUAD_NB(true)
+      }
+      else
+      {
+        EIGMI_QUAD_NB(false)
+      }
+#undef EIGMI_QUAD_NB
+#undef EIGMI_QUAD
+    }
   }
   EIG_HIP(hipGetLastError());
 }
 }  // namespace
+
+int sell_mv8_launches(i64 m)
+{
+  const int nblk = (int)(m / 8), per = mv8_kernel_choice() == 1 ? 4 : 2;
+  return (nblk + per - 1) / per;
+}
 
 void launch_sell_mv8(const eig_mat_s &A, i64 m, const double *X, double *Y, hipStream_t s)
 {

@@ -257,7 +257,7 @@ typedef struct eig_blanczos_timing {
   double orth_ms;    /* two CGS passes: M SpMM + MFMA panel Gram + panel update */
   double norm_ms;    /* CholQR2: 2 x (M SpMM + Gram + host 32x32 Cholesky + triangular update) */
   int64_t steps;
-  int64_t cheb_launches; /* fused Chebyshev kernel launches (one per 16 columns per step) */
+  int64_t cheb_launches; /* fused Chebyshev kernel launches (one per 32 columns per Chebyshev step) */
 } eig_blanczos_timing;
 int eig_blanczos_create(eig_mat_t K, eig_mat_t M, int block, int max_steps, int degree, double lmin, double lmax,
                         unsigned seed, eig_blanczos_t *ws);

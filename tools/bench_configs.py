@@ -6,6 +6,9 @@
   C2  3-D Poisson 128^3: SpMV (cache-resident: 217 MB < 256 MB MALL), Lanczos step, the b = 8
       SpMM, block Gram-Schmidt (m = 8, 32) and one StandardLargest iteration vs the CPU path
   C3  3-D Q1 elasticity 64^3, 3x3 blocks: BCSR SpMV against 76 nnzb + 4 (nb+1) + 48 nb bytes
+  C5  generalised K x = lambda M x, P1 on the Kuhn split (15-pt shared pattern), block Lanczos
+      k = 32: block steps/s with the phase split, the fused Chebyshev SpMM kernel against
+      12 nnz + 4 (n+1) + (32 m + 8) n bytes per m-column launch (EIGMI_C5_N, default 256)
 
 One JSON line per measurement; algorithmic bytes per SURVEY 8(d); peak 8 TB/s.
 """
@@ -129,6 +132,38 @@ def c3(ctx):
     emit(config="C3 Q1 elasticity 64^3 3x3 BCSR", op="BCSR SpMV", us=round(ms * 1e3, 2), nnzb=nnzb,
          algorithmic_bytes=b, GBs=round(gbs, 1), frac=round(gbs / PEAK, 4), cpu_us=round(tc * 1e6, 1),
          cpu_GBs=round(b / tc / 1e9, 2))
+
+
+def c5(ctx):
+    N = int(os.environ.get("EIGMI_C5_N", "256"))
+    steps, warm, b, degree = 3, 1, 32, 36
+    n = N ** 3
+    t0 = time.perf_counter()
+    rk, ck, vk = eigmi.gen_matrix(eigmi.GEN_P1STIFF3D, N)
+    K = eigmi.Matrix.from_bcsr(ctx, rk, ck, vk)
+    del rk, ck, vk
+    rm, cm, vm = eigmi.gen_matrix(eigmi.GEN_P1MASS3D, N)
+    nnz = int(rm[-1])
+    M = eigmi.Matrix.from_bcsr(ctx, rm, cm, vm)
+    del rm, cm, vm
+    bl = eigmi.BlockLanczos(K, M, block=b, max_steps=steps + warm, degree=degree, seed=123)
+    setup_s = time.perf_counter() - t0
+    bl.step(warm)
+    t = bl.step(steps)
+    ev, _, res = bl.ritz(4, eigmi.WHICH_LA, want_resid=False)
+    cols = b // (t.cheb_launches // (steps * (degree - 1)))  # columns per launch
+    # per launch: matrix + (gather x_k, read x_{k-1}, read b, write x_{k+1}) per column + dinv
+    cheb_bytes = 12 * nnz + 4 * (n + 1) + 32 * cols * n + 8 * n
+    cheb_us = t.cheb_ms / t.cheb_launches * 1e3
+    emit(config=f"C5 P1 Kuhn K/M {N}^3, block Lanczos k={b}", op=f"block step (Chebyshev degree {degree}, CGS2, CholQR2)",
+         block_steps_per_s=round(steps / (t.total_ms * 1e-3), 3), ms_per_step=round(t.total_ms / steps, 2),
+         kspmm_ms=round(t.kspmm_ms / steps, 2), cheb_ms=round(t.cheb_ms / steps, 2),
+         orth_ms=round(t.orth_ms / steps, 2), norm_ms=round(t.norm_ms / steps, 2),
+         cheb_kernel_us=round(cheb_us, 1), cheb_bytes_per_launch=cheb_bytes,
+         cheb_GBs=round(cheb_bytes / (cheb_us * 1e-6) / 1e9, 1),
+         cheb_frac=round(cheb_bytes / (cheb_us * 1e-6) / 1e9 / PEAK, 4), nnz=nnz, setup_s=round(setup_s, 1),
+         top_ritz=[float(x) for x in ev], steps_taken=steps + warm)
+    bl.close()
 
 
 if __name__ == "__main__":
