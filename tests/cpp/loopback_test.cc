@@ -2,7 +2,8 @@
 // context each) over libeigmi's in-process loopback transport.  Exercises the row-partitioned
 // SELL image with window-local columns, the halo plan, the interior / boundary slice split, the
 // split-K1 carry and the allreduce placement of the Lanczos drivers; only the RCCL calls
-// themselves are replaced.  Compared with the single-rank run of the same matrix.
+// themselves are replaced.  Compared with the single-rank run of the same matrix; the generalised
+// block Lanczos (config C5, P1 K/M, block 16) likewise, Ritz values to 1e-10 relative.
 //
 //   loopback_test P N     (defaults 3, 24)
 #include <cmath>
@@ -29,15 +30,41 @@ struct Rows {
   std::vector<double> v;
 };
 
-static Rows gen(int N, int64_t b, int64_t cnt)
+static Rows gen(int N, int64_t b, int64_t cnt, int kind = 4)
 {
   Rows r;
-  int64_t nnz = eig_gen_nnzb_rows(4, N, b, cnt);
+  int64_t nnz = eig_gen_nnzb_rows(kind, N, b, cnt);
   r.rp.resize(cnt + 1);
   r.c.resize(nnz > 0 ? nnz : 1);
   r.v.resize(nnz > 0 ? nnz : 1);
-  CK(eig_gen_matrix_rows(4, N, b, cnt, r.rp.data(), r.c.data(), r.v.data()));
+  CK(eig_gen_matrix_rows(kind, N, b, cnt, r.rp.data(), r.c.data(), r.v.data()));
   return r;
+}
+
+// Generalised block Lanczos (config C5) on the P1 pencil: Ritz values of `bsteps` steps, block 16.
+static const int kBlk = 16, kBsteps = 6, kBnev = 4;
+static void block_lanczos(eig_ctx_t ctx, int N, int64_t b, int64_t cnt, bool dist, double *ev)
+{
+  const int64_t n = (int64_t)N * N * N;
+  Rows k = gen(N, b, cnt, 6), m = gen(N, b, cnt, 7);
+  eig_mat_t K, M;
+  if (dist)
+  {
+    CK(eig_mat_create_bcsr_dist(ctx, n, b, cnt, 1, 1, k.rp.data(), k.c.data(), k.v.data(), &K));
+    CK(eig_mat_create_bcsr_dist(ctx, n, b, cnt, 1, 1, m.rp.data(), m.c.data(), m.v.data(), &M));
+  }
+  else
+  {
+    CK(eig_mat_create_bcsr(ctx, n, n, 1, 1, k.rp.data(), k.c.data(), k.v.data(), &K));
+    CK(eig_mat_create_bcsr(ctx, n, n, 1, 1, m.rp.data(), m.c.data(), m.v.data(), &M));
+  }
+  eig_blanczos_t bl;
+  CK(eig_blanczos_create(K, M, kBlk, kBsteps, 36, 0.5, 2.5, 123, &bl));
+  CK(eig_blanczos_step(bl, kBsteps, nullptr));
+  CK(eig_blanczos_ritz(bl, kBnev, EIG_WHICH_LA, ev, nullptr, nullptr));
+  CK(eig_blanczos_destroy(bl));
+  eig_mat_destroy(K);
+  eig_mat_destroy(M);
 }
 
 int main(int argc, char **argv)
@@ -50,6 +77,8 @@ int main(int argc, char **argv)
 
   // ---- serial reference on one context
   std::vector<double> x(n), y_ser(n), a_ser(steps), b_ser(steps + 1), ev_ser(nev), fa_ser(steps), fb_ser(steps + 1);
+  std::vector<double> bev_ser(kBnev);
+  std::vector<std::vector<double>> bev(P, std::vector<double>(kBnev));
   for (int64_t i = 0; i < n; ++i) x[i] = std::sin(0.37 * i) + 0.01 * (i % 7);
   {
     eig_ctx_t ctx;
@@ -62,6 +91,7 @@ int main(int argc, char **argv)
     CK(eig_lanczos_run(A, steps, nullptr, 123, EIG_LANCZOS_FUSED, fa_ser.data(), fb_ser.data(), nullptr));
     CK(eig_lanczos_solve(A, nev, ncv, EIG_WHICH_LA, 123, ev_ser.data(), nullptr, nullptr));
     eig_mat_destroy(A);
+    block_lanczos(ctx, N, 0, n, false, bev_ser.data());
     eig_ctx_destroy(ctx);
   }
 
@@ -121,6 +151,7 @@ int main(int argc, char **argv)
                       std::memcmp(bg.data(), be[r].data(), (steps + 1) * 8) == 0;
       }
       CK(eig_lanczos_solve(A, nev, ncv, EIG_WHICH_LA, 123, ev[r].data(), nullptr, nullptr));
+      block_lanczos(ctx, N, b, cnt, true, bev[r].data());
       eig_free(ctx, dx);
       eig_free(ctx, dy);
       eig_free(ctx, dd);
@@ -177,6 +208,12 @@ int main(int argc, char **argv)
       if (std::fabs(ev[r][i] - ev_ser[i]) > 1e-10)
       {
         std::printf("FAIL rank %d: Ritz %d %.17g vs %.17g\n", r, i, ev[r][i], ev_ser[i]);
+        ++failures;
+      }
+    for (int i = 0; i < kBnev; ++i)
+      if (std::fabs(bev[r][i] - bev_ser[i]) > 1e-10 * std::fabs(bev_ser[i]))
+      {
+        std::printf("FAIL rank %d: block Lanczos Ritz %d %.17g vs %.17g\n", r, i, bev[r][i], bev_ser[i]);
         ++failures;
       }
   }
