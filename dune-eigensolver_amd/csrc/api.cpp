@@ -878,6 +878,38 @@ extern "C" int eig_mat_create_bcsr_dist(eig_ctx_t ctx, int64_t nb_rows_global, i
   });
 }
 
+namespace eigmi {
+void mat_download_bcsr(const eig_mat_s &A, std::vector<i64> &rowptr, std::vector<i32> &col, std::vector<double> &vals)
+{
+  EIG_CHECK(!A.ctx->distributed() || A.nb_rows == A.nb_rows_global, EIG_ERR_ARG, "download: single-rank matrix only");
+  const i64 C = 64 * (i64)A.R, ns = A.nslices, bb = (i64)A.br * A.bc;
+  std::vector<i64> sp(ns + 1);
+  std::vector<i32> ci(std::max<i64>(A.nnzb_padded, 1));
+  std::vector<double> vi(std::max<i64>(A.nnzb_padded * bb, 1));
+  EIG_HIP(hipMemcpy(sp.data(), A.slice_ptr, (ns + 1) * sizeof(i64), hipMemcpyDeviceToHost));
+  if (A.nnzb_padded)
+  {
+    EIG_HIP(hipMemcpy(ci.data(), A.col, A.nnzb_padded * sizeof(i32), hipMemcpyDeviceToHost));
+    EIG_HIP(hipMemcpy(vi.data(), A.val, A.nnzb_padded * bb * sizeof(double), hipMemcpyDeviceToHost));
+  }
+  rowptr.assign(A.nb_rows + 1, 0);
+  col.clear();
+  vals.clear();
+  for (i64 r = 0; r < A.nb_rows; ++r)
+  {
+    const i64 s = r / C, l = r % C, base = sp[s], w = (sp[s + 1] - base) / C;
+    for (i64 k = 0; k < w; ++k)
+    {
+      const i32 c = ci[base + k * C + l];
+      if (c < 0) continue;
+      col.push_back(c + (i32)(A.win_begin / A.bc));
+      for (i64 t = 0; t < bb; ++t) vals.push_back(vi[(base + k * C) * bb + t * C + l]);
+    }
+    rowptr[r + 1] = (i64)col.size();
+  }
+}
+}  // namespace eigmi
+
 extern "C" int eig_mat_destroy(eig_mat_t A)
 {
   if (!A) return EIG_OK;
@@ -1201,6 +1233,38 @@ extern "C" int eig_orthonormalize_naive(eig_ctx_t ctx, int64_t n, int64_t m, dou
   });
 }
 
+namespace eigmi {
+// B_orthonormalize_blocked (kernels_cpp.hh:356-591) on the device; *norm (device) receives the
+// max off-diagonal R coefficient.
+void b_orthonormalize_device(eig_mat_s &B, i64 m, double *Q, double *norm)
+{
+  eig_ctx_t ctx = B.ctx;
+  hipStream_t s = ctx->stream;
+  const i64 n = B.nb_rows;
+  double *P = (double *)ctx_buffer(ctx, 7, (size_t)n * 8 * sizeof(double));
+  double *G = (double *)ctx_buffer(ctx, 3, 64 * sizeof(double));
+  double *U = (double *)ctx_buffer(ctx, 4, 64 * sizeof(double));
+  double *Sg = m > 8 ? (double *)ctx_buffer(ctx, 5, (size_t)8 * m * sizeof(double)) : nullptr;
+  EIG_HIP(hipMemsetAsync(norm, 0, sizeof(double), s));
+  for (i64 bk = 0; bk < m; bk += 8)
+  {
+    double *Qb = Q + bk * n;
+    launch_spmm_mv8(B, 8, Qb, P, s);                   // P = B Q_bk          (:378-395)
+    gram_device(ctx, n, 8, 8, P, Qb, G);               // s = P^T Q_bk        (:450-456)
+    launch_cholqr_factor(G, U, norm, 1, s);            // mirror upper, norm, U (:457-526)
+    launch_apply_upper(n, Qb, U, s);                   // Q_bk := Q_bk U      (:528-539)
+    launch_apply_upper(n, P, U, s);                    // P := P U            (:540-552)
+    const i64 mrest = m - bk - 8;
+    if (mrest > 0)
+    {
+      gram_device(ctx, n, 8, mrest, P, Qb + 8 * n, Sg);  // S = P^T Q_bj     (:559-565)
+      launch_max_offdiag(Sg, 8, mrest, false, norm, s);  // norm (:566-568)
+      launch_project(n, mrest, Qb, Qb + 8 * n, Sg, s);   // Q_bj -= Q_bk S   (:570-584)
+    }
+  }
+}
+}  // namespace eigmi
+
 extern "C" int eig_b_orthonormalize_mv8(eig_mat_t B, int64_t m, double *Q, double *norm)
 {
   return guard(B ? B->ctx : nullptr, [&] {
@@ -1209,31 +1273,8 @@ extern "C" int eig_b_orthonormalize_mv8(eig_mat_t B, int64_t m, double *Q, doubl
               "B_orthonormalize_blocked: only implemented for FieldMatrix<..,1,1>");
     EIG_MV8_CHECK(m);
     EIG_CHECK(!B->ctx->distributed(), EIG_ERR_ARG, "eig_b_orthonormalize_mv8: single rank only");
-    eig_ctx_t ctx = B->ctx;
-    DeviceGuard dg(ctx->device);
-    hipStream_t s = ctx->stream;
-    const i64 n = B->nb_rows;
-    double *P = (double *)ctx_buffer(ctx, 7, (size_t)n * 8 * sizeof(double));
-    double *G = (double *)ctx_buffer(ctx, 3, 64 * sizeof(double));
-    double *U = (double *)ctx_buffer(ctx, 4, 64 * sizeof(double));
-    double *Sg = m > 8 ? (double *)ctx_buffer(ctx, 5, (size_t)8 * m * sizeof(double)) : nullptr;
-    EIG_HIP(hipMemsetAsync(norm, 0, sizeof(double), s));
-    for (i64 bk = 0; bk < m; bk += 8)
-    {
-      double *Qb = Q + bk * n;
-      launch_spmm_mv8(*B, 8, Qb, P, s);                  // P = B Q_bk          (:378-395)
-      gram_device(ctx, n, 8, 8, P, Qb, G);               // s = P^T Q_bk        (:450-456)
-      launch_cholqr_factor(G, U, norm, 1, s);            // mirror upper, norm, U (:457-526)
-      launch_apply_upper(n, Qb, U, s);                   // Q_bk := Q_bk U      (:528-539)
-      launch_apply_upper(n, P, U, s);                    // P := P U            (:540-552)
-      const i64 mrest = m - bk - 8;
-      if (mrest > 0)
-      {
-        gram_device(ctx, n, 8, mrest, P, Qb + 8 * n, Sg);  // S = P^T Q_bj     (:559-565)
-        launch_max_offdiag(Sg, 8, mrest, false, norm, s);  // norm (:566-568)
-        launch_project(n, mrest, Qb, Qb + 8 * n, Sg, s);   // Q_bj -= Q_bk S   (:570-584)
-      }
-    }
+    DeviceGuard dg(B->ctx->device);
+    b_orthonormalize_device(*B, m, Q, norm);
   });
 }
 

@@ -7,6 +7,7 @@
 #include <cmath>
 #include <cstring>
 #include <numeric>
+#include <string>
 #include <vector>
 
 #include "internal.h"
@@ -76,6 +77,205 @@ extern "C" int eig_standard_largest(eig_mat_t A, double shift, double tol, int m
         for (i64 i = 0; i < n; ++i) evec_host[(i64)j * n + i] = h[((j / 8) * n + i) * 8 + j % 8];
     }
     if (iters) *iters = kk;
+  });
+}
+
+// ============================================================================================
+// Inverse subspace iteration with exported LU factors
+// ============================================================================================
+namespace {
+
+// The factors the inverse drivers apply: the caller's, or a host factorisation of `A` (owned).
+struct LuRef {
+  eig_lu_t lu = nullptr;
+  bool owned = false;
+  ~LuRef()
+  {
+    if (owned) eig_lu_destroy(lu);
+  }
+};
+
+void factor_host(eig_mat_s &A, const std::vector<i64> &rp, const std::vector<i32> &c, const std::vector<double> &v,
+                 LuRef &out)
+{
+  const int rc = eig_lu_create_bcsr(A.ctx, A.nb_rows, A.br, rp.data(), c.data(), v.data(), &out.lu);
+  EIG_CHECK(rc == EIG_OK, rc, std::string("LU factorisation: ") + eig_last_error(A.ctx));
+  out.owned = true;
+}
+
+void copy_evecs(eig_ctx_t ctx, const double *Q, i64 n, int nev, double *evec_host)
+{
+  if (!evec_host) return;
+  const i64 m = (nev + 7) / 8 * 8;
+  std::vector<double> h((size_t)(n * m));
+  EIG_HIP(hipMemcpyAsync(h.data(), Q, h.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
+  EIG_HIP(hipStreamSynchronize(ctx->stream));
+  for (int j = 0; j < nev; ++j)
+    for (i64 i = 0; i < n; ++i) evec_host[(i64)j * n + i] = h[((j / 8) * n + i) * 8 + j % 8];
+}
+
+void random_block(eig_ctx_t ctx, i64 n, i64 m, unsigned seed, double *Q)
+{
+  std::vector<double> h((size_t)(n * m));
+  host_random_normal(n * m, seed, h.data());  // eigensolver.hh:137-142 / :222-227
+  EIG_HIP(hipMemcpyAsync(Q, h.data(), h.size() * 8, hipMemcpyHostToDevice, ctx->stream));
+  EIG_HIP(hipStreamSynchronize(ctx->stream));
+}
+
+void check_inverse_matrix(const eig_mat_s *A, const char *who)
+{
+  EIG_CHECK(A->br == A->bc, EIG_ERR_ARG, std::string(who) + ": blocks of input matrix must be square");
+  EIG_CHECK(A->br == 1, EIG_ERR_BLOCKSIZE, "matmul_sparse_tallskinny_blocked: only implemented for FieldMatrix<..,1,1>");
+  EIG_CHECK(!distributed(*A), EIG_ERR_ARG, std::string(who) + ": single rank only");
+  EIG_CHECK(A->nb_rows == A->nb_cols, EIG_ERR_SHAPE, std::string(who) + ": square matrix required");
+}
+
+}  // namespace
+
+extern "C" int eig_standard_inverse(eig_mat_t A, eig_lu_t lu, double shift, double tol, int maxiter, int nev,
+                                    unsigned seed, double *eval_host, double *evec_host, int *iters, int verbose)
+{
+  return guard(A ? A->ctx : nullptr, [&] {
+    EIG_CHECK(A && eval_host && nev > 0, EIG_ERR_ARG, "eig_standard_inverse: bad argument");
+    check_inverse_matrix(A, "StandardInverse");
+    eig_ctx_t ctx = A->ctx;
+    EIG_HIP(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    const i64 n = A->nb_rows;
+    const i64 m = (nev / 8 + std::min(nev % 8, 1)) * 8;  // eigensolver.hh:133
+    DevBuf Q1b(n * m * 8), Q2b(n * m * 8), dpb(m * 8);
+    double *Q1 = Q1b.d(), *Q2 = Q2b.d();
+    random_block(ctx, n, m, seed, Q1);
+    if (shift != 0.0) launch_shift_diag(*A, shift, s);  // :145-153 (mutates A)
+    LuRef F;                                           // :156 UMFPackFactorizedMatrix<ISTLM> F(A, 1)
+    if (lu)
+      F.lu = lu;
+    else
+    {
+      std::vector<i64> rp;
+      std::vector<i32> c;
+      std::vector<double> v;
+      EIG_HIP(hipStreamSynchronize(s));
+      mat_download_bcsr(*A, rp, c, v);
+      factor_host(*A, rp, c, v, F);
+    }
+    EIG_CHECK(lu_size(F.lu) == n, EIG_ERR_SHAPE,
+              "matmul_inverse_tallskinny_blocked: Factorization does not match size of Qout/Qin");
+    orthonormalize_device(ctx, n, m, Q1, EIG_ORTHO_MGS);  // :159
+    std::vector<double> s1(m, 0.0), s2(m, 0.0);
+    int kk = 1;
+    for (int k = 1; k < maxiter; ++k)
+    {
+      kk = k;
+      lu_inverse_device(F.lu, m, Q1, Q2, s);               // :168 Q2 = A^-1 Q1
+      orthonormalize_device(ctx, n, m, Q2, EIG_ORTHO_MGS);  // :171
+      launch_spmm_mv8(*A, m, Q2, Q1, s);                   // :174
+      launch_dot_diag_mv8(n, m, Q2, Q1, dpb.d(), 0, s, ctx->red);  // :175
+      EIG_HIP(hipMemcpyAsync(s1.data(), dpb.d(), m * 8, hipMemcpyDeviceToHost, s));
+      EIG_HIP(hipStreamSynchronize(s));
+      for (auto &x : s1) x -= shift;
+      double dist = 0.0;
+      for (i64 i = 0; i < m; ++i) dist = std::max(dist, std::fabs(s1[i] - s2[i]));
+      if (verbose > 0 && k > 1) fprintf(stdout, "iter=%d %.17g\n", k, dist);
+      std::swap(s1, s2);
+      std::swap(Q1, Q2);
+      if (k > 1 && dist < tol) break;
+    }
+    for (int j = 0; j < nev; ++j) eval_host[j] = s2[j];
+    copy_evecs(ctx, Q1, n, nev, evec_host);
+    if (iters) *iters = kk;
+  });
+}
+
+extern "C" int eig_generalized_inverse(eig_mat_t A, eig_mat_t B, eig_lu_t lu, double shift, double reg, double tol,
+                                       int maxiter, int nev, unsigned seed, double *eval_host, double *evec_host,
+                                       int *iters, int verbose)
+{
+  return guard(A ? A->ctx : nullptr, [&] {
+    EIG_CHECK(A && B && eval_host && nev > 0 && A->ctx == B->ctx, EIG_ERR_ARG, "eig_generalized_inverse: bad argument");
+    check_inverse_matrix(A, "GeneralizedInverse");
+    check_inverse_matrix(B, "GeneralizedInverse");
+    EIG_CHECK(A->nb_rows == B->nb_rows, EIG_ERR_SHAPE, "GeneralizedInverse: A and B sizes differ");
+    eig_ctx_t ctx = A->ctx;
+    EIG_HIP(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    const i64 n = A->nb_rows;
+    // copy of A, shifted (:208, :240-252): A + shift B (pattern(B) within pattern(A)) + reg I
+    std::vector<i64> rp, brp;
+    std::vector<i32> c, bc;
+    std::vector<double> v, bv;
+    EIG_HIP(hipStreamSynchronize(s));
+    mat_download_bcsr(*A, rp, c, v);
+    mat_download_bcsr(*B, brp, bc, bv);
+    for (i64 i = 0; i < n; ++i)
+    {
+      if (shift != 0.0)
+        for (i64 q = brp[i]; q < brp[i + 1]; ++q)
+        {
+          const i32 *b0 = c.data() + rp[i], *b1 = c.data() + rp[i + 1];
+          const i32 *hit = std::lower_bound(b0, b1, bc[q]);
+          EIG_CHECK(hit != b1 && *hit == bc[q], EIG_ERR_SHAPE, "GeneralizedInverse: pattern(B) must be contained in pattern(A)");
+          v[hit - c.data()] += shift * bv[q];
+        }
+      if (reg != 0.0)
+      {
+        const i32 *b0 = c.data() + rp[i], *b1 = c.data() + rp[i + 1];
+        const i32 *hit = std::lower_bound(b0, b1, (i32)i);
+        EIG_CHECK(hit != b1 && *hit == (i32)i, EIG_ERR_SHAPE, "GeneralizedInverse: A has no diagonal entry");
+        v[hit - c.data()] += reg;
+      }
+    }
+    eig_mat_t As = nullptr;
+    {
+      const int rc = eig_mat_create_bcsr(ctx, n, n, 1, 1, rp.data(), c.data(), v.data(), &As);
+      EIG_CHECK(rc == EIG_OK, rc, std::string("shifted copy of A: ") + eig_last_error(ctx));
+    }
+    struct MatGuard {
+      eig_mat_t m;
+      ~MatGuard() { eig_mat_destroy(m); }
+    } asg{As};
+    LuRef F;  // :255
+    if (lu)
+      F.lu = lu;
+    else
+      factor_host(*As, rp, c, v, F);
+    EIG_CHECK(lu_size(F.lu) == n, EIG_ERR_SHAPE,
+              "matmul_inverse_tallskinny_blocked: Factorization does not match size of Qout/Qin");
+    const i64 m = (nev / 8 + std::min(nev % 8, 1)) * 8;  // :224
+    DevBuf Q1b(n * m * 8), Q2b(n * m * 8), dpb(m * 8 + 8);
+    double *Q1 = Q1b.d(), *Q2 = Q2b.d(), *norm = dpb.d() + m;
+    random_block(ctx, n, m, seed, Q1);
+    std::vector<double> ra1(m, 0.0), ra2(m, 0.0), sA(m, 0.0);
+    b_orthonormalize_device(*B, m, Q1, norm);            // :273
+    launch_spmm_mv8(*As, m, Q1, Q2, s);                  // :274
+    launch_dot_diag_mv8(n, m, Q2, Q1, dpb.d(), 0, s, ctx->red);  // :275
+    EIG_HIP(hipMemcpyAsync(sA.data(), dpb.d(), m * 8, hipMemcpyDeviceToHost, s));
+    EIG_HIP(hipStreamSynchronize(s));
+    for (i64 i = 0; i < m; ++i) ra2[i] = sA[i] - shift;
+    int iter = 0;
+    double relerror = 0.0;
+    while (iter < maxiter)
+    {
+      launch_spmm_mv8(*B, m, Q1, Q2, s);       // :302 Q2 = B Q1
+      lu_inverse_device(F.lu, m, Q2, Q1, s);   // :303 Q1 = A^-1 Q2
+      b_orthonormalize_device(*B, m, Q1, norm);  // :304
+      iter += 1;
+      launch_spmm_mv8(*As, m, Q1, Q2, s);      // :317
+      launch_dot_diag_mv8(n, m, Q2, Q1, dpb.d(), 0, s, ctx->red);
+      EIG_HIP(hipMemcpyAsync(sA.data(), dpb.d(), m * 8, hipMemcpyDeviceToHost, s));
+      EIG_HIP(hipStreamSynchronize(s));
+      for (i64 i = 0; i < m; ++i) ra1[i] = sA[i] - shift;
+      relerror = 0.0;
+      for (i64 i = 0; i < m; ++i) relerror = std::max(relerror, std::fabs(ra1[i] - ra2[i]));
+      relerror /= *std::max_element(ra1.begin(), ra1.end());
+      if (verbose > 2) fprintf(stdout, "iter=%d relerror=%.17g\n", iter, relerror);
+      std::swap(ra1, ra2);
+      if ((iter > 10) & (relerror < tol)) break;  // :325
+    }
+    for (int j = 0; j < nev; ++j) eval_host[j] = ra2[j];
+    copy_evecs(ctx, Q1, n, nev, evec_host);
+    if (iters) *iters = iter;
+    if (verbose > 0) fprintf(stdout, "GeneralizedInverse: iterations=%d relerror=%.17g\n", iter, relerror);
   });
 }
 

@@ -270,6 +270,27 @@ void launch_panel_gram(eig_ctx_t ctx, i64 n, i64 ld, i64 m1, i64 m2, const doubl
 void launch_panel_update(i64 n, i64 ldq, i64 ldy, i64 m1, i64 m2, const double *Q, const double *S, double alpha,
                          double beta, double *Y, hipStream_t s);
 
+// Exported-LU-factor solves (k_trsv.hip, lu.cpp): device image of the factors.
+struct TrsvImage {
+  i64 n = 0;
+  i64 *lrp = nullptr, *lsplit = nullptr;  // L rows (no unit diagonal), ascending columns
+  i32 *lc = nullptr;
+  double *lv = nullptr;
+  i64 *urp = nullptr, *usplit = nullptr;  // U rows (no diagonal), descending columns
+  i32 *uc = nullptr;
+  double *uv = nullptr, *ud = nullptr;
+  i32 *P = nullptr, *Q = nullptr;
+  double *scale = nullptr;                // Rs[P[k]] (do_recip) or 1 / Rs[P[k]]
+};
+void trsv_upload(eig_ctx_t ctx, i64 n, const std::vector<i64> &lrp, const std::vector<i32> &lc,
+                 const std::vector<double> &lv, const std::vector<i64> &urp, const std::vector<i32> &uc,
+                 const std::vector<double> &uv, const std::vector<double> &ud, const std::vector<i64> &P,
+                 const std::vector<i64> &Q, const std::vector<double> &scale, TrsvImage &img);
+void trsv_free(TrsvImage &img);
+void launch_inverse_mv8(const TrsvImage &img, i64 m, double *Qin, double *Qout, hipStream_t s);
+void lu_inverse_device(eig_lu_t lu, i64 m, double *Qin, double *Qout, hipStream_t s);
+i64 lu_size(eig_lu_t lu);
+
 // ---- dense host linear algebra (dense.cpp) ---------------------------------------------------
 void tridiag_eig(int k, std::vector<double> &d, std::vector<double> e, std::vector<double> &Z, bool z_identity = true);
 void householder_tridiag(int n, std::vector<double> A, std::vector<double> &d, std::vector<double> &e,
@@ -285,6 +306,9 @@ void halo_exchange(const eig_mat_s &A, double *x, hipStream_t s, double *x2 = nu
 void mv_device(eig_mat_s &A, double *x, double *y);
 void gram_device(eig_ctx_t ctx, i64 n, i64 m1, i64 m2, const double *Q1, const double *Q2, double *G);
 void orthonormalize_device(eig_ctx_t ctx, i64 n, i64 m, double *Q, int variant);
+void b_orthonormalize_device(eig_mat_s &B, i64 m, double *Q, double *norm);
+// Host CSR copy of a single-rank matrix's device image (rows in ISTL order, padding dropped).
+void mat_download_bcsr(const eig_mat_s &A, std::vector<i64> &rowptr, std::vector<i32> &col, std::vector<double> &vals);
 void allreduce_sum(eig_ctx_t ctx, double *buf, i64 count, hipStream_t s);
 void *ctx_buffer(eig_ctx_t ctx, int slot, size_t bytes);
 void host_random_normal(i64 count, unsigned seed, double *out);

@@ -574,7 +574,7 @@ void panel_gram(eig_ctx_t ctx, i64 n, i64 ld, i64 m1, i64 m2, const double *Q1, 
   // at most 256 per output block so that stage 2 stays short
   const int gx = (int)std::max<i64>(1, std::min<i64>(std::min(256, std::max(1, 1024 / ny)), (n + 255) / 256));
   const size_t E = (size_t)TI * TJ * 256;
-  double *part = (double *)ctx_buffer(ctx, 5, (size_t)gx * ny * E * sizeof(double));
+  double *part = (double *)ctx_buffer(ctx, 8, (size_t)gx * ny * E * sizeof(double));  // slot 8: panel partials
   hipLaunchKernelGGL((k_panel_gram_part<TI, TJ>), dim3(gx, ny), dim3(256), 0, s, n, ld, (int)m1, (int)m2, nbj, Q1, Q2,
                      part);
   EIG_HIP(hipGetLastError());

@@ -1,0 +1,422 @@
+// lu.cpp -- the exported-LU-factor operator of the inverse drivers:
+//   * eig_lu_create: upload factors in the form UMFPackFactorizedMatrix exposes
+//     (umfpacktools.hh:20-39: L in compressed-row form with the unit diagonal last in each row,
+//     U in compressed-column form with the diagonal last in each column, row / column
+//     permutations P, Q, row scaling Rs with do_recip) -- a caller that has UMFPACK hands its
+//     umfpack_dl_get_numeric arrays over unchanged;
+//   * eig_lu_create_bcsr: a host factorisation producing that form (stand-in for
+//     umfpack_dl_symbolic / _numeric, umfpacktools.hh:43-199, which SuiteSparse would provide):
+//     reverse Cuthill-McKee symmetric ordering, row-sum scaling, envelope (profile) LU without
+//     pivoting -- for the matrices the inverse drivers factor (SPD / diagonally dominant /
+//     positively shifted operators);
+//   * eig_inverse_mv8: Qout = A^-1 Qin on the device (matmul_inverse_tallskinny_blocked,
+//     kernels_cpp.hh:660-755), k_trsv.hip.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <deque>
+#include <numeric>
+#include <vector>
+
+#include "internal.h"
+
+using namespace eigmi;
+
+namespace {
+
+// Reverse Cuthill-McKee on the symmetrised pattern; per connected component a BFS from a
+// pseudo-peripheral node, neighbours visited by increasing degree.  perm[k] = old index of new k.
+std::vector<i64> rcm(i64 n, const std::vector<std::vector<i64>> &adj)
+{
+  std::vector<i64> perm;
+  perm.reserve(n);
+  std::vector<char> seen(n, 0);
+  std::vector<i64> deg(n);
+  for (i64 i = 0; i < n; ++i) deg[i] = (i64)adj[i].size();
+  auto bfs_levels = [&](i64 s, std::vector<i64> &order, i64 &last_level_start) {
+    std::vector<i64> lvl(n, -1);
+    order.clear();
+    order.push_back(s);
+    lvl[s] = 0;
+    last_level_start = 0;
+    for (size_t h = 0; h < order.size(); ++h)
+    {
+      const i64 u = order[h];
+      for (i64 v : adj[u])
+        if (lvl[v] < 0 && !seen[v])
+        {
+          lvl[v] = lvl[u] + 1;
+          order.push_back(v);
+        }
+    }
+    const i64 maxl = lvl[order.back()];
+    for (size_t h = 0; h < order.size(); ++h)
+      if (lvl[order[h]] == maxl)
+      {
+        last_level_start = (i64)h;
+        break;
+      }
+  };
+  std::vector<i64> order;
+  for (i64 s0 = 0; s0 < n; ++s0)
+  {
+    if (seen[s0]) continue;
+    // pseudo-peripheral start: repeat BFS from a min-degree node of the last level (George-Liu)
+    i64 s = s0, lls = 0;
+    bfs_levels(s, order, lls);
+    for (int it = 0; it < 4; ++it)
+    {
+      i64 best = order[lls];
+      for (size_t h = lls; h < order.size(); ++h)
+        if (deg[order[h]] < deg[best]) best = order[h];
+      std::vector<i64> o2;
+      i64 l2 = 0;
+      bfs_levels(best, o2, l2);
+      if (o2.size() > 0 && (size_t)l2 > (size_t)lls && o2.size() == order.size())
+      {
+        s = best;
+        order.swap(o2);
+        lls = l2;
+      }
+      else
+        break;
+    }
+    // Cuthill-McKee from s
+    std::vector<i64> comp;
+    std::deque<i64> q;
+    q.push_back(s);
+    seen[s] = 1;
+    while (!q.empty())
+    {
+      const i64 u = q.front();
+      q.pop_front();
+      comp.push_back(u);
+      std::vector<i64> nb;
+      for (i64 v : adj[u])
+        if (!seen[v])
+        {
+          seen[v] = 1;
+          nb.push_back(v);
+        }
+      std::sort(nb.begin(), nb.end(), [&](i64 a, i64 b) { return deg[a] != deg[b] ? deg[a] < deg[b] : a < b; });
+      for (i64 v : nb) q.push_back(v);
+    }
+    perm.insert(perm.end(), comp.begin(), comp.end());
+  }
+  std::reverse(perm.begin(), perm.end());
+  return perm;
+}
+
+}  // namespace
+
+struct eig_lu_s {
+  eig_ctx_t ctx = nullptr;
+  i64 n = 0;
+  int do_recip = 0;
+  // host copy of the factors in the exported (UMFPACK) form
+  std::vector<i64> Lp, Lj, Up, Ui, P, Q;
+  std::vector<double> Lx, Ux, Rs;
+  // device image (k_trsv.hip): L rows without the unit diagonal, ascending columns; U rows
+  // (transposed from the columns) without the diagonal, DESCENDING columns; U diagonal
+  TrsvImage img;
+  ~eig_lu_s()
+  {
+    if (ctx) trsv_free(img);
+  }
+};
+
+namespace {
+
+void build_device(eig_lu_s &lu)
+{
+  const i64 n = lu.n;
+  // L rows: the reference subtracts entries Lp[i] .. Lp[i+1]-2 in stored order (the last entry is
+  // the unit diagonal, kernels_cpp.hh:716-722).  Stored order is kept when ascending; otherwise the
+  // row is sorted by column (then equal to the reference to rounding, not bitwise).
+  std::vector<i64> lrp(n + 1, 0), urp(n + 1, 0);
+  std::vector<i32> lc, uc;
+  std::vector<double> lv, uv, ud(n);
+  for (i64 i = 0; i < n; ++i)
+  {
+    std::vector<std::pair<i64, double>> e;
+    for (i64 k = lu.Lp[i]; k < lu.Lp[i + 1] - 1; ++k) e.push_back({lu.Lj[k], lu.Lx[k]});
+    std::stable_sort(e.begin(), e.end(), [](const auto &a, const auto &b) { return a.first < b.first; });
+    for (auto &p : e)
+    {
+      EIG_CHECK(p.first >= 0 && p.first < i, EIG_ERR_ARG, "L factor: entry not strictly below the diagonal");
+      lc.push_back((i32)p.first);
+      lv.push_back(p.second);
+    }
+    lrp[i + 1] = (i64)lc.size();
+  }
+  // U: column j holds rows Ui[Up[j] .. Up[j+1]-2] above the diagonal Ux[Up[j+1]-1]; the reference's
+  // push loop (kernels_cpp.hh:730-745) updates row i with columns j in DECREASING order, which is
+  // the order the pull form below uses -- bitwise whatever the order inside a column.
+  std::vector<std::vector<std::pair<i64, double>>> rows(n);
+  for (i64 j = 0; j < n; ++j)
+  {
+    EIG_CHECK(lu.Up[j + 1] > lu.Up[j], EIG_ERR_ARG, "U factor: empty column");
+    ud[j] = lu.Ux[lu.Up[j + 1] - 1];
+    for (i64 k = lu.Up[j]; k < lu.Up[j + 1] - 1; ++k)
+    {
+      EIG_CHECK(lu.Ui[k] >= 0 && lu.Ui[k] < j, EIG_ERR_ARG, "U factor: entry not strictly above the diagonal");
+      rows[lu.Ui[k]].push_back({j, lu.Ux[k]});
+    }
+  }
+  for (i64 i = 0; i < n; ++i)
+  {
+    auto &e = rows[i];
+    std::stable_sort(e.begin(), e.end(), [](const auto &a, const auto &b) { return a.first > b.first; });
+    for (auto &p : e)
+    {
+      uc.push_back((i32)p.first);
+      uv.push_back(p.second);
+    }
+    urp[i + 1] = (i64)uc.size();
+    std::vector<std::pair<i64, double>>().swap(e);
+  }
+  std::vector<i64> P(lu.P), Q(lu.Q);
+  std::vector<double> scale(n);
+  for (i64 k = 0; k < n; ++k)
+  {
+    EIG_CHECK(P[k] >= 0 && P[k] < n && Q[k] >= 0 && Q[k] < n, EIG_ERR_ARG, "permutation entry out of range");
+    scale[k] = lu.do_recip ? lu.Rs[P[k]] : 1.0 / lu.Rs[P[k]];  // kernels_cpp.hh:683-705
+  }
+  trsv_upload(lu.ctx, n, lrp, lc, lv, urp, uc, uv, ud, P, Q, scale, lu.img);
+}
+
+}  // namespace
+
+extern "C" int eig_lu_create(eig_ctx_t ctx, int64_t n, const int64_t *Lp, const int64_t *Lj, const double *Lx,
+                             const int64_t *Up, const int64_t *Ui, const double *Ux, const int64_t *P,
+                             const int64_t *Q, const double *Rs, int do_recip, eig_lu_t *out)
+{
+  return guard(ctx, [&] {
+    EIG_CHECK(ctx && out && n > 0 && Lp && Lj && Lx && Up && Ui && Ux && P && Q && Rs, EIG_ERR_ARG,
+              "eig_lu_create: null argument");
+    EIG_CHECK(n < (int64_t)INT32_MAX, EIG_ERR_SHAPE, "eig_lu_create: n too large for int32 indices");
+    EIG_HIP(hipSetDevice(ctx->device));
+    auto *lu = new eig_lu_s();
+    try
+    {
+      lu->ctx = ctx;
+      lu->n = n;
+      lu->do_recip = do_recip ? 1 : 0;
+      lu->Lp.assign(Lp, Lp + n + 1);
+      lu->Lj.assign(Lj, Lj + Lp[n]);
+      lu->Lx.assign(Lx, Lx + Lp[n]);
+      lu->Up.assign(Up, Up + n + 1);
+      lu->Ui.assign(Ui, Ui + Up[n]);
+      lu->Ux.assign(Ux, Ux + Up[n]);
+      lu->P.assign(P, P + n);
+      lu->Q.assign(Q, Q + n);
+      lu->Rs.assign(Rs, Rs + n);
+      build_device(*lu);
+    }
+    catch (...)
+    {
+      delete lu;
+      throw;
+    }
+    *out = lu;
+  });
+}
+
+extern "C" int eig_lu_create_bcsr(eig_ctx_t ctx, int64_t nb_rows, int br, const int64_t *rowptr, const int32_t *col,
+                                  const double *vals, eig_lu_t *out)
+{
+  return guard(ctx, [&] {
+    EIG_CHECK(out && rowptr && col && vals && nb_rows > 0 && br >= 1 && br <= 4, EIG_ERR_ARG,
+              "eig_lu_create_bcsr: bad argument");
+    if (ctx) EIG_HIP(hipSetDevice(ctx->device));
+    const i64 n = nb_rows * br;
+    EIG_CHECK(n < (int64_t)INT32_MAX, EIG_ERR_SHAPE, "eig_lu_create_bcsr: too large");
+    // scalar entries of the block matrix (zeros skipped, as umfpacktools.hh:66-93 does)
+    std::vector<std::vector<std::pair<i64, double>>> rowsA(n);
+    for (i64 rb = 0; rb < nb_rows; ++rb)
+      for (i64 p = rowptr[rb]; p < rowptr[rb + 1]; ++p)
+        for (int a = 0; a < br; ++a)
+          for (int b = 0; b < br; ++b)
+          {
+            const double v = vals[p * br * br + a * br + b];
+            if (v != 0.0) rowsA[rb * br + a].push_back({(i64)col[p] * br + b, v});
+          }
+    std::vector<std::vector<i64>> adj(n);
+    for (i64 i = 0; i < n; ++i)
+      for (auto &e : rowsA[i])
+        if (e.first != i)
+        {
+          EIG_CHECK(e.first >= 0 && e.first < n, EIG_ERR_SHAPE, "column out of range");
+          adj[i].push_back(e.first);
+          adj[e.first].push_back(i);
+        }
+    for (auto &a : adj)
+    {
+      std::sort(a.begin(), a.end());
+      a.erase(std::unique(a.begin(), a.end()), a.end());
+    }
+    std::vector<i64> perm = rcm(n, adj), inv(n);
+    for (i64 k = 0; k < n; ++k) inv[perm[k]] = k;
+    std::vector<double> Rs(n, 0.0);
+    for (i64 i = 0; i < n; ++i)
+    {
+      for (auto &e : rowsA[i]) Rs[i] += std::fabs(e.second);
+      EIG_CHECK(Rs[i] > 0.0, EIG_ERR_BREAKDOWN, "LU: zero row");
+    }
+    // B = (R^-1 A)[perm, perm] in the envelope: f[k] = first column of new row k (symmetrised)
+    std::vector<i64> f(n);
+    for (i64 k = 0; k < n; ++k)
+    {
+      i64 m = k;
+      for (i64 v : adj[perm[k]]) m = std::min(m, inv[v]);
+      f[k] = m;
+    }
+    std::vector<i64> off(n + 1, 0);  // envelope storage: row k of L / column k of U over [f_k, k)
+    for (i64 k = 0; k < n; ++k) off[k + 1] = off[k] + (k - f[k]);
+    const i64 env = off[n];
+    EIG_CHECK(env < (i64)1 << 31, EIG_ERR_SHAPE, "LU: envelope too large for the host factorisation");
+    std::vector<double> L(env, 0.0), U(env, 0.0), D(n, 0.0);
+    for (i64 k = 0; k < n; ++k)
+    {
+      const i64 i0 = perm[k];
+      for (auto &e : rowsA[i0])
+      {
+        const i64 j = inv[e.first];
+        const double v = e.second / Rs[i0];
+        if (j < k) L[off[k] + (j - f[k])] = v;
+        else if (j == k) D[k] = v;
+        else U[off[j] + (k - f[j])] = v;  // B[k][j], j > k: column j of U, row k
+      }
+    }
+    auto Lat = [&](i64 r, i64 c) -> double & { return L[off[r] + (c - f[r])]; };
+    auto Uat = [&](i64 r, i64 c) -> double & { return U[off[c] + (r - f[c])]; };  // r < c
+    for (i64 k = 0; k < n; ++k)
+    {
+      // column k of U, rows f_k .. k-1
+      for (i64 i = f[k]; i < k; ++i)
+      {
+        double s = Uat(i, k);
+        for (i64 t = std::max(f[i], f[k]); t < i; ++t) s -= Lat(i, t) * Uat(t, k);
+        Uat(i, k) = s;
+      }
+      // row k of L, columns f_k .. k-1
+      for (i64 j = f[k]; j < k; ++j)
+      {
+        double s = Lat(k, j);
+        for (i64 t = std::max(f[k], f[j]); t < j; ++t) s -= Lat(k, t) * Uat(t, j);
+        EIG_CHECK(D[j] != 0.0, EIG_ERR_BREAKDOWN, "LU: zero pivot (matrix needs pivoting)");
+        Lat(k, j) = s / D[j];
+      }
+      double s = D[k];
+      for (i64 t = f[k]; t < k; ++t) s -= Lat(k, t) * Uat(t, k);
+      EIG_CHECK(s != 0.0 && std::isfinite(s), EIG_ERR_BREAKDOWN, "LU: zero pivot (matrix needs pivoting)");
+      D[k] = s;
+    }
+    // exported form: L rows ascending + unit diagonal last; U columns ascending + diagonal last
+    std::vector<i64> Lp(n + 1, 0), Lj, Up(n + 1, 0), Ui;
+    std::vector<double> Lx, Ux;
+    for (i64 k = 0; k < n; ++k)
+    {
+      for (i64 j = f[k]; j < k; ++j)
+        if (Lat(k, j) != 0.0)
+        {
+          Lj.push_back(j);
+          Lx.push_back(Lat(k, j));
+        }
+      Lj.push_back(k);
+      Lx.push_back(1.0);
+      Lp[k + 1] = (i64)Lj.size();
+      for (i64 i = f[k]; i < k; ++i)
+        if (Uat(i, k) != 0.0)
+        {
+          Ui.push_back(i);
+          Ux.push_back(Uat(i, k));
+        }
+      Ui.push_back(k);
+      Ux.push_back(D[k]);
+      Up[k + 1] = (i64)Ui.size();
+    }
+    auto *lu = new eig_lu_s();
+    try
+    {
+      lu->ctx = ctx;
+      lu->n = n;
+      lu->do_recip = 0;
+      lu->Lp = std::move(Lp);
+      lu->Lj = std::move(Lj);
+      lu->Lx = std::move(Lx);
+      lu->Up = std::move(Up);
+      lu->Ui = std::move(Ui);
+      lu->Ux = std::move(Ux);
+      lu->P = perm;
+      lu->Q = perm;
+      lu->Rs = std::move(Rs);
+      if (ctx) build_device(*lu);  // ctx == NULL: host-only factors (export / tests)
+    }
+    catch (...)
+    {
+      delete lu;
+      throw;
+    }
+    *out = lu;
+  });
+}
+
+extern "C" int eig_lu_info(eig_lu_t lu, int64_t *n, int64_t *lnz, int64_t *unz, int *do_recip)
+{
+  return guard(lu ? lu->ctx : nullptr, [&] {
+    EIG_CHECK(lu, EIG_ERR_ARG, "eig_lu_info: null handle");
+    if (n) *n = lu->n;
+    if (lnz) *lnz = lu->Lp[lu->n];
+    if (unz) *unz = lu->Up[lu->n];
+    if (do_recip) *do_recip = lu->do_recip;
+  });
+}
+
+extern "C" int eig_lu_export(eig_lu_t lu, int64_t *Lp, int64_t *Lj, double *Lx, int64_t *Up, int64_t *Ui, double *Ux,
+                             int64_t *P, int64_t *Q, double *Rs)
+{
+  return guard(lu ? lu->ctx : nullptr, [&] {
+    EIG_CHECK(lu && Lp && Lj && Lx && Up && Ui && Ux && P && Q && Rs, EIG_ERR_ARG, "eig_lu_export: null argument");
+    std::copy(lu->Lp.begin(), lu->Lp.end(), Lp);
+    std::copy(lu->Lj.begin(), lu->Lj.end(), Lj);
+    std::copy(lu->Lx.begin(), lu->Lx.end(), Lx);
+    std::copy(lu->Up.begin(), lu->Up.end(), Up);
+    std::copy(lu->Ui.begin(), lu->Ui.end(), Ui);
+    std::copy(lu->Ux.begin(), lu->Ux.end(), Ux);
+    std::copy(lu->P.begin(), lu->P.end(), P);
+    std::copy(lu->Q.begin(), lu->Q.end(), Q);
+    std::copy(lu->Rs.begin(), lu->Rs.end(), Rs);
+  });
+}
+
+extern "C" int eig_lu_destroy(eig_lu_t lu)
+{
+  if (!lu) return EIG_OK;
+  if (lu->ctx)
+  {
+    (void)hipSetDevice(lu->ctx->device);
+    (void)hipStreamSynchronize(lu->ctx->stream);
+  }
+  delete lu;
+  return EIG_OK;
+}
+
+namespace eigmi {
+void lu_inverse_device(eig_lu_t lu, i64 m, double *Qin, double *Qout, hipStream_t s)
+{
+  launch_inverse_mv8(lu->img, m, Qin, Qout, s);
+}
+i64 lu_size(eig_lu_t lu) { return lu->n; }
+}  // namespace eigmi
+
+extern "C" int eig_inverse_mv8(eig_lu_t lu, int64_t m, double *Qin, double *Qout)
+{
+  return guard(lu ? lu->ctx : nullptr, [&] {
+    EIG_CHECK(lu && Qin && Qout, EIG_ERR_ARG, "eig_inverse_mv8: null argument");
+    EIG_CHECK(lu->ctx, EIG_ERR_ARG, "eig_inverse_mv8: host-only factors (created without a context)");
+    EIG_CHECK(m >= 0 && m % 8 == 0, EIG_ERR_SHAPE, "matmul_inverse_tallskinny_blocked: columns must be a multiple of 8");
+    EIG_HIP(hipSetDevice(lu->ctx->device));
+    if (m > 0) launch_inverse_mv8(lu->img, m, Qin, Qout, lu->ctx->stream);
+  });
+}

@@ -122,6 +122,15 @@ SIGNATURES = {
     "eig_lanczos_destroy": (_int, [_vp]),
     "eig_lanczos_capture": (_int, [_vp, _int, _int, ctypes.POINTER(_int)]),
     "eig_lanczos_replay": (_int, [_vp, ctypes.POINTER(Timing)]),
+    "eig_lu_create": (_int, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _int, ctypes.POINTER(_vp)]),
+    "eig_lu_create_bcsr": (_int, [_vp, _i64, _int, _vp, _vp, _vp, ctypes.POINTER(_vp)]),
+    "eig_lu_info": (_int, [_vp, ctypes.POINTER(_i64), ctypes.POINTER(_i64), ctypes.POINTER(_i64), ctypes.POINTER(_int)]),
+    "eig_lu_export": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "eig_lu_destroy": (_int, [_vp]),
+    "eig_inverse_mv8": (_int, [_vp, _i64, _vp, _vp]),
+    "eig_standard_inverse": (_int, [_vp, _vp, _dbl, _dbl, _int, _int, _u, _vp, _vp, ctypes.POINTER(_int), _int]),
+    "eig_generalized_inverse": (_int, [_vp, _vp, _vp, _dbl, _dbl, _dbl, _int, _int, _u, _vp, _vp, ctypes.POINTER(_int),
+                                       _int]),
     "eig_blanczos_create": (_int, [_vp, _vp, _int, _int, _int, _dbl, _dbl, _u, ctypes.POINTER(_vp)]),
     "eig_blanczos_step": (_int, [_vp, _int, ctypes.POINTER(BlockTiming)]),
     "eig_blanczos_ritz": (_int, [_vp, _int, _int, _vp, _vp, _vp]),
@@ -501,6 +510,90 @@ def panel_gram_mv8(ctx, n, m1, m2, Q1, Q2, G):
 
 def mass_solve_mv8(M, m, degree, B, X, lmin=0.5, lmax=2.5):
     M.ctx.check(lib.eig_mass_solve_mv8(M.h, m, degree, lmin, lmax, B.ptr, X.ptr))
+
+
+class LU:
+    """eig_lu_t: exported LU factors on the device (UMFPackFactorizedMatrix mirror)."""
+
+    def __init__(self, ctx, handle):
+        self.ctx, self.h = ctx, handle
+
+    @classmethod
+    def from_factors(cls, ctx, Lp, Lj, Lx, Up, Ui, Ux, P, Q, Rs, do_recip=0):
+        c = np.ascontiguousarray
+        arrs = [c(Lp, np.int64), c(Lj, np.int64), c(Lx, np.float64), c(Up, np.int64), c(Ui, np.int64),
+                c(Ux, np.float64), c(P, np.int64), c(Q, np.int64), c(Rs, np.float64)]
+        h = _vp()
+        ctx.check(lib.eig_lu_create(ctx.h, arrs[0].size - 1, *[_np_ptr(a) for a in arrs], int(do_recip),
+                                    ctypes.byref(h)))
+        lu = cls(ctx, h)
+        lu._keep = arrs
+        return lu
+
+    @classmethod
+    def from_bcsr(cls, ctx, rowptr, col, vals, br=1):
+        """Host factorisation (eig_lu_create_bcsr); ctx=None gives host-only factors for export."""
+        rowptr = np.ascontiguousarray(rowptr, np.int64)
+        col = np.ascontiguousarray(col, np.int32)
+        vals = np.ascontiguousarray(vals, np.float64)
+        h = _vp()
+        rc = lib.eig_lu_create_bcsr(ctx.h if ctx else None, rowptr.size - 1, br, _np_ptr(rowptr), _np_ptr(col),
+                                    _np_ptr(vals), ctypes.byref(h))
+        if rc != EIG_OK:
+            raise EigError(rc, lib.eig_last_error(ctx.h if ctx else None).decode())
+        return cls(ctx, h)
+
+    def export(self):
+        """-> dict of the factor arrays (Lp, Lj, Lx, Up, Ui, Ux, P, Q, Rs, do_recip)."""
+        n, lnz, unz, rec = _i64(0), _i64(0), _i64(0), _int(0)
+        self._check(lib.eig_lu_info(self.h, ctypes.byref(n), ctypes.byref(lnz), ctypes.byref(unz), ctypes.byref(rec)))
+        n, lnz, unz = n.value, lnz.value, unz.value
+        d = {"Lp": np.zeros(n + 1, np.int64), "Lj": np.zeros(lnz, np.int64), "Lx": np.zeros(lnz),
+             "Up": np.zeros(n + 1, np.int64), "Ui": np.zeros(unz, np.int64), "Ux": np.zeros(unz),
+             "P": np.zeros(n, np.int64), "Q": np.zeros(n, np.int64), "Rs": np.zeros(n)}
+        self._check(lib.eig_lu_export(self.h, *[_np_ptr(d[k]) for k in ("Lp", "Lj", "Lx", "Up", "Ui", "Ux", "P",
+                                                                        "Q", "Rs")]))
+        d["do_recip"] = rec.value
+        return d
+
+    def _check(self, rc):
+        if self.ctx:
+            self.ctx.check(rc)
+        elif rc != EIG_OK:
+            raise EigError(rc, lib.eig_last_error(None).decode())
+
+    def inverse_mv8(self, m, Qin, Qout):
+        self.ctx.check(lib.eig_inverse_mv8(self.h, m, Qin.ptr, Qout.ptr))
+
+    def close(self):
+        if self.h and (self.ctx is None or self.ctx.h):
+            lib.eig_lu_destroy(self.h)
+        self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def standard_inverse(A, shift, tol, maxiter, nev, seed=123, lu=None, want_evec=True, verbose=0):
+    ev = np.zeros(nev)
+    evec = np.zeros(nev * A.n) if want_evec else None
+    it = _int(0)
+    A.ctx.check(lib.eig_standard_inverse(A.h, lu.h if lu else None, shift, tol, maxiter, nev, seed, _np_ptr(ev),
+                                         _np_ptr(evec) if want_evec else None, ctypes.byref(it), verbose))
+    return ev, (evec.reshape(nev, A.n) if want_evec else None), it.value
+
+
+def generalized_inverse(A, B, shift, reg, tol, maxiter, nev, seed=123, lu=None, want_evec=True, verbose=0):
+    ev = np.zeros(nev)
+    evec = np.zeros(nev * A.n) if want_evec else None
+    it = _int(0)
+    A.ctx.check(lib.eig_generalized_inverse(A.h, B.h, lu.h if lu else None, shift, reg, tol, maxiter, nev, seed,
+                                            _np_ptr(ev), _np_ptr(evec) if want_evec else None, ctypes.byref(it),
+                                            verbose))
+    return ev, (evec.reshape(nev, A.n) if want_evec else None), it.value
 
 
 class BlockLanczos:

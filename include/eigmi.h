@@ -237,6 +237,48 @@ enum eig_which { EIG_WHICH_LA = 0, EIG_WHICH_SA = 1 };
 int eig_lanczos_solve(eig_mat_t A, int nev, int ncv, int which, unsigned seed, double *eval_host,
                       double *evec_host, double *resid_host);
 
+/* ---------------------------------------------------------------- exported LU factors ------ */
+/* Mirror of UMFPackFactorizedMatrix (umfpacktools.hh:16-199): the factors of P R A Q = L U that
+ * umfpack_dl_get_numeric exports -- L (n x n, unit lower) in compressed ROW form with the unit
+ * diagonal LAST in each row (Lp[n+1], Lj, Lx), U in compressed COLUMN form with the diagonal LAST
+ * in each column (Up[n+1], Ui, Ux), row permutation P[n], column permutation Q[n], row scaling
+ * Rs[n] (do_recip: row i multiplied by Rs[i], else divided).  Host arrays, copied. */
+typedef struct eig_lu_s *eig_lu_t;
+int eig_lu_create(eig_ctx_t ctx, int64_t n, const int64_t *Lp, const int64_t *Lj, const double *Lx,
+                  const int64_t *Up, const int64_t *Ui, const double *Ux, const int64_t *P, const int64_t *Q,
+                  const double *Rs, int do_recip, eig_lu_t *lu);
+/* Host factorisation into the same form (stand-in for umfpack_dl_symbolic / _numeric when
+ * SuiteSparse is absent): reverse Cuthill-McKee symmetric ordering (P = Q), row-sum scaling
+ * (do_recip = 0), envelope LU WITHOUT pivoting -- for SPD, diagonally dominant or positively
+ * shifted matrices; EIG_ERR_BREAKDOWN on a zero pivot.  BCRS input as eig_mat_create_bcsr (br = bc,
+ * zero entries of blocks skipped like umfpacktools.hh:66-93).  ctx == NULL: host-only factors (no device
+ * image; eig_lu_export works, eig_inverse_mv8 refuses). */
+int eig_lu_create_bcsr(eig_ctx_t ctx, int64_t nb_rows, int br, const int64_t *rowptr, const int32_t *col,
+                       const double *vals, eig_lu_t *lu);
+int eig_lu_info(eig_lu_t lu, int64_t *n, int64_t *lnz, int64_t *unz, int *do_recip);
+/* Copy the factors out (sizes from eig_lu_info: Lp/Up n+1, Lj/Lx lnz, Ui/Ux unz, P/Q/Rs n). */
+int eig_lu_export(eig_lu_t lu, int64_t *Lp, int64_t *Lj, double *Lx, int64_t *Up, int64_t *Ui, double *Ux,
+                  int64_t *P, int64_t *Q, double *Rs);
+int eig_lu_destroy(eig_lu_t lu);
+/* Qout = A^-1 Qin for m columns (matmul_inverse_tallskinny_blocked, kernels_cpp.hh:660-755;
+ * MultiVector<double,8> layout, n rows, single rank).  Qin is used as scratch (its contents afterwards are
+ * unspecified), as the reference allows (kernels_cpp.hh:659).
+ * Bitwise the reference's arithmetic when the L rows are stored in ascending column order. */
+int eig_inverse_mv8(eig_lu_t lu, int64_t m, double *Qin, double *Qout);
+
+/* StandardInverse (eigensolver.hh:116-198): inverse subspace iteration for the nev smallest
+ * eigenvalues of A (+ shift; mutates A like the reference when shift != 0).  The LU of the shifted
+ * A is computed on the host (eig_lu_create_bcsr) unless `lu` is given (factors of the SHIFTED A).
+ * eval_host[nev] unsorted (column order), evec_host nev x n or NULL, *iters = k at exit. */
+int eig_standard_inverse(eig_mat_t A, eig_lu_t lu, double shift, double tol, int maxiter, int nev, unsigned seed,
+                         double *eval_host, double *evec_host, int *iters, int verbose);
+/* GeneralizedInverse (eigensolver.hh:204-351): A x = lambda B x by inverse subspace iteration with
+ * B-orthonormalisation; factors A + shift B + reg I (a copy: A itself is not modified, like the
+ * reference's copy at :208).  pattern(A) must contain pattern(B) (:202-203).  Stops when
+ * iter > 10 and max|delta ra| / max(ra) < tol (:315-324). */
+int eig_generalized_inverse(eig_mat_t A, eig_mat_t B, eig_lu_t lu, double shift, double reg, double tol, int maxiter,
+                            int nev, unsigned seed, double *eval_host, double *evec_host, int *iters, int verbose);
+
 /* ---------------------------------------------------------------- block Lanczos (config C5) */
 /* Generalised symmetric-definite eigenproblem K x = lambda M x by block Lanczos in the M-inner
  * product on the operator M^-1 K (the pencil GeneralizedInverse solves, eigensolver.hh:204-351,

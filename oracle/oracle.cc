@@ -526,6 +526,154 @@ int orc_standard_largest(i64 n, const i64 *rowptr, const i32 *col, double *val, 
 }
 
 // ------------------------------------------------------------------------------------------
+// Inverse subspace iteration: the exported-LU-factor apply and the two
+// inverse drivers.  The factors are inputs (UMFPackFactorizedMatrix's public arrays,
+// umfpacktools.hh:20-39); whoever computed them, the reference's arithmetic on them is this.
+// ------------------------------------------------------------------------------------------
+
+// matmul_inverse_tallskinny_blocked (kernels_cpp.hh:660-755), verbatim loop structure.  Qin is
+// overwritten.  L rows: Lp/Lj/Lx with the unit diagonal last; U columns: Up/Ui/Ux with the
+// diagonal last.
+void orc_inverse_mv8(i64 n, i64 m, const i64 *Lp, const i64 *Lj, const double *Lx, const i64 *Up, const i64 *Ui,
+                     const double *Ux, const i64 *P, const i64 *Q, const double *Rs, int do_recip, double *pin,
+                     double *pout)
+{
+  const int bs = 8;
+  for (i64 bj = 0; bj < m; bj += bs)
+  {
+    const i64 nbj = n * bj;
+    {  // combined row scaling and permutation (:680-705)
+      i64 K = nbj;
+      for (i64 k = 0; k < n; ++k)
+      {
+        const double scaling = do_recip ? Rs[P[k]] : 1.0 / Rs[P[k]];
+        const i64 I = nbj + P[k] * bs;
+        for (int s = 0; s < bs; ++s) pout[K + s] = scaling * pin[I + s];
+        K += bs;
+      }
+    }
+    {  // L (:710-725)
+      i64 I = nbj;
+      double sum[8];
+      for (i64 i = 0; i < n; i++)
+      {
+        for (int s = 0; s < bs; ++s) sum[s] = pout[I + s];
+        for (i64 k = Lp[i]; k < Lp[i + 1] - 1; k++)
+        {
+          const i64 J = nbj + Lj[k] * bs;
+          const double lij = Lx[k];
+          for (int s = 0; s < bs; ++s) sum[s] -= lij * pin[J + s];
+        }
+        for (int s = 0; s < bs; ++s) pin[I + s] = sum[s];
+        I += bs;
+      }
+    }
+    {  // U (:727-750)
+      i64 J = nbj + (n - 1) * bs;
+      double result[8];
+      for (i64 j = n - 1; j >= 0; j--)
+      {
+        double matelem = Ux[Up[j + 1] - 1];
+        for (int s = 0; s < bs; ++s) result[s] = pin[J + s] / matelem;
+        for (i64 k = Up[j]; k < Up[j + 1] - 1; k++)
+        {
+          const i64 I = nbj + Ui[k] * bs;
+          matelem = Ux[k];
+          for (int s = 0; s < bs; ++s) pin[I + s] -= matelem * result[s];
+        }
+        const i64 K = nbj + Q[j] * bs;
+        for (int s = 0; s < bs; ++s) pout[K + s] = result[s];
+        J -= bs;
+      }
+    }
+  }
+}
+
+// StandardInverse (eigensolver.hh:116-198), 1x1 blocks; val is mutated by the shift like the
+// reference; the factors are those of the SHIFTED matrix.  Returns the iterations (k at exit).
+int orc_standard_inverse(i64 n, const i64 *rowptr, const i32 *col, double *val, const i64 *Lp, const i64 *Lj,
+                         const double *Lx, const i64 *Up, const i64 *Ui, const double *Ux, const i64 *P, const i64 *Q,
+                         const double *Rs, int do_recip, double shift, double tol, int maxiter, int nev, unsigned seed,
+                         double *eval, double *evec)
+{
+  const i64 m = (nev / 8 + std::min(nev % 8, 1)) * 8;
+  std::vector<double> Q1((size_t)(n * m)), Q2((size_t)(n * m));
+  orc_random_mv8(n, m, seed, Q1.data());
+  if (shift != 0.0) orc_shift_diag(n, rowptr, col, val, shift);
+  orc_orthonormalize_mv8(n, m, Q1.data());
+  std::vector<double> s1(m, 0.0), s2(m, 0.0);
+  int kk = 1;
+  for (i64 k = 1; k < maxiter; ++k)
+  {
+    kk = (int)k;
+    orc_inverse_mv8(n, m, Lp, Lj, Lx, Up, Ui, Ux, P, Q, Rs, do_recip, Q1.data(), Q2.data());  // :168
+    orc_orthonormalize_mv8(n, m, Q2.data());                                                 // :171
+    orc_spmm_mv8(n, m, rowptr, col, val, Q2.data(), Q1.data());                              // :174
+    orc_dot_diag_mv8(n, m, Q2.data(), Q1.data(), s1.data());                                 // :175
+    for (auto &x : s1) x -= shift;
+    double dist = 0.0;
+    for (i64 i = 0; i < m; ++i) dist = std::max(dist, std::fabs(s1[i] - s2[i]));
+    std::swap(s1, s2);
+    std::swap(Q1, Q2);
+    if (k > 1 && dist < tol) break;
+  }
+  for (int j = 0; j < nev; ++j) eval[j] = s2[j];
+  for (int j = 0; j < nev; ++j)
+    for (i64 i = 0; i < n; ++i) evec[(i64)j * n + i] = Q1[mvidx(n, i, j)];
+  return kk;
+}
+
+// GeneralizedInverse (eigensolver.hh:204-351), portable-kernel branch (:268-275, :290-304): A is
+// copied and shifted A + shift B + reg I on A's pattern (pattern(B) within pattern(A), :202-203);
+// the factors are those of that shifted copy.  Returns the iterations.
+int orc_generalized_inverse(i64 n, const i64 *rowptr, const i32 *col, const double *valA, const i64 *browptr,
+                            const i32 *bcol, const double *valB, const i64 *Lp, const i64 *Lj, const double *Lx,
+                            const i64 *Up, const i64 *Ui, const double *Ux, const i64 *P, const i64 *Q,
+                            const double *Rs, int do_recip, double shift, double reg, double tol, int maxiter, int nev,
+                            unsigned seed, double *eval, double *evec)
+{
+  std::vector<double> A(valA, valA + rowptr[n]);
+  for (i64 i = 0; i < n; ++i)
+  {
+    if (shift != 0.0)
+      for (i64 q = browptr[i]; q < browptr[i + 1]; ++q)
+        for (i64 p = rowptr[i]; p < rowptr[i + 1]; ++p)
+          if (col[p] == bcol[q]) A[p] += shift * valB[q];  // A.axpy(shift, B) (:241)
+    if (reg != 0.0)
+      for (i64 p = rowptr[i]; p < rowptr[i + 1]; ++p)
+        if (col[p] == i) A[p] += reg;  // (:244-252)
+  }
+  const i64 m = (nev / 8 + std::min(nev % 8, 1)) * 8;
+  std::vector<double> Q1((size_t)(n * m)), Q2((size_t)(n * m));
+  orc_random_mv8(n, m, seed, Q1.data());
+  std::vector<double> ra1(m, 0.0), ra2(m, 0.0), sA(m, 0.0);
+  orc_b_orthonormalize_mv8(n, m, browptr, bcol, valB, Q1.data());  // :273
+  orc_spmm_mv8(n, m, rowptr, col, A.data(), Q1.data(), Q2.data());
+  orc_dot_diag_mv8(n, m, Q2.data(), Q1.data(), sA.data());
+  for (i64 i = 0; i < m; ++i) ra2[i] = sA[i] - shift;
+  int iter = 0;
+  while (iter < maxiter)
+  {
+    orc_spmm_mv8(n, m, browptr, bcol, valB, Q1.data(), Q2.data());                            // :302
+    orc_inverse_mv8(n, m, Lp, Lj, Lx, Up, Ui, Ux, P, Q, Rs, do_recip, Q2.data(), Q1.data());  // :303
+    orc_b_orthonormalize_mv8(n, m, browptr, bcol, valB, Q1.data());                            // :304
+    iter += 1;
+    orc_spmm_mv8(n, m, rowptr, col, A.data(), Q1.data(), Q2.data());  // :317
+    orc_dot_diag_mv8(n, m, Q2.data(), Q1.data(), sA.data());
+    for (i64 i = 0; i < m; ++i) ra1[i] = sA[i] - shift;
+    double relerror = 0.0;
+    for (i64 i = 0; i < m; ++i) relerror = std::max(relerror, std::fabs(ra1[i] - ra2[i]));
+    relerror /= *std::max_element(ra1.begin(), ra1.end());
+    std::swap(ra1, ra2);
+    if ((iter > 10) & (relerror < tol)) break;
+  }
+  for (int j = 0; j < nev; ++j) eval[j] = ra2[j];
+  for (int j = 0; j < nev; ++j)
+    for (i64 i = 0; i < n; ++i) evec[(i64)j * n + i] = Q1[mvidx(n, i, j)];
+  return iter;
+}
+
+// ------------------------------------------------------------------------------------------
 // Lanczos three-term recurrence -- the arithmetic ARPACK's dsaupd performs between the
 // multMv callbacks (arpack_geneo_wrapper.hh:257-279; ARPACK dsaitr), written in the exact
 // operation order of the device path (DESIGN.md "Lanczos step") so the two can be compared:

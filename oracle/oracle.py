@@ -57,6 +57,15 @@ def _load():
         "orc_standard_largest": (_int, [_i64, _i64p, _i32p, _f64p, ctypes.c_double, ctypes.c_double,
                                         _int, _int, ctypes.c_uint, _f64p, _f64p]),
         "orc_lanczos": (None, [_i64, _i64p, _i32p, _f64p, _int, _f64p, _f64p, _f64p]),
+        "orc_inverse_mv8": (None, [_i64, _i64, _i64p, _i64p, _f64p, _i64p, _i64p, _f64p, _i64p, _i64p, _f64p, _int,
+                                   _f64p, _f64p]),
+        "orc_standard_inverse": (_int, [_i64, _i64p, _i32p, _f64p] + [_i64p, _i64p, _f64p, _i64p, _i64p, _f64p, _i64p,
+                                                                      _i64p, _f64p, _int] +
+                                 [ctypes.c_double, ctypes.c_double, _int, _int, ctypes.c_uint, _f64p, _f64p]),
+        "orc_generalized_inverse": (_int, [_i64, _i64p, _i32p, _f64p, _i64p, _i32p, _f64p] +
+                                    [_i64p, _i64p, _f64p, _i64p, _i64p, _f64p, _i64p, _i64p, _f64p, _int] +
+                                    [ctypes.c_double, ctypes.c_double, ctypes.c_double, _int, _int, ctypes.c_uint,
+                                     _f64p, _f64p]),
         "orc_lanczos_rotating": (None, [_i64, _i64p, _i32p, _f64p, _int, _f64p, _f64p, _f64p, _f64p, _f64p]),
         "orc_lanczos_fused": (None, [_i64, _i64p, _i32p, _f64p, _int, _f64p, _f64p, _f64p]),
     }
@@ -199,6 +208,44 @@ def standard_largest(A, shift, tol, maxiter, nev, seed=123):
     ev = np.zeros(nev)
     evec = np.zeros(nev * A.n)
     it = lib.orc_standard_largest(A.n, A.rowptr, A.col, val, shift, tol, maxiter, nev, seed, ev, evec)
+    return ev, evec.reshape(nev, A.n), it
+
+
+class LU:
+    """Exported LU factors (UMFPackFactorizedMatrix's public arrays, umfpacktools.hh:20-39)."""
+
+    def __init__(self, Lp, Lj, Lx, Up, Ui, Ux, P, Q, Rs, do_recip):
+        c = np.ascontiguousarray
+        self.Lp, self.Lj, self.Lx = c(Lp, np.int64), c(Lj, np.int64), c(Lx, np.float64)
+        self.Up, self.Ui, self.Ux = c(Up, np.int64), c(Ui, np.int64), c(Ux, np.float64)
+        self.P, self.Q, self.Rs, self.do_recip = c(P, np.int64), c(Q, np.int64), c(Rs, np.float64), int(do_recip)
+        self.n = self.Lp.size - 1
+
+    def args(self):
+        return (self.Lp, self.Lj, self.Lx, self.Up, self.Ui, self.Ux, self.P, self.Q, self.Rs, self.do_recip)
+
+
+def inverse_mv8(lu, Qin, m):
+    """matmul_inverse_tallskinny_blocked: returns (Qout, Qin after the call)."""
+    pin = np.ascontiguousarray(Qin, np.float64).copy()
+    out = np.zeros_like(pin)
+    lib.orc_inverse_mv8(lu.n, m, *lu.args(), pin, out)
+    return out, pin
+
+
+def standard_inverse(A, lu, shift, tol, maxiter, nev, seed=123):
+    val = A.val.copy()
+    ev = np.zeros(nev)
+    evec = np.zeros(nev * A.n)
+    it = lib.orc_standard_inverse(A.n, A.rowptr, A.col, val, *lu.args(), shift, tol, maxiter, nev, seed, ev, evec)
+    return ev, evec.reshape(nev, A.n), it
+
+
+def generalized_inverse(A, B, lu, shift, reg, tol, maxiter, nev, seed=123):
+    ev = np.zeros(nev)
+    evec = np.zeros(nev * A.n)
+    it = lib.orc_generalized_inverse(A.n, A.rowptr, A.col, A.val, B.rowptr, B.col, B.val, *lu.args(), shift, reg, tol,
+                                     maxiter, nev, seed, ev, evec)
     return ev, evec.reshape(nev, A.n), it
 
 

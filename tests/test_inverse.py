@@ -1,0 +1,201 @@
+"""the exported-LU-factor apply matmul_inverse_tallskinny_blocked
+(kernels_cpp.hh:660-755) and the inverse drivers StandardInverse / GeneralizedInverse
+(eigensolver.hh:116-351).
+
+CPU (no GPU): the host factorisation (eig_lu_create_bcsr with a NULL context) against numpy --
+P R A Q = L U to rounding -- and the oracle's restatement of the reference's factor apply against
+numpy solves; the oracle drivers against the analytic 2-D Dirichlet spectrum (.cc:437-446).
+GPU: eig_inverse_mv8 BITWISE equal to the oracle restatement on the same factors (the device keeps
+the reference's per-row operation order), through both factor entry points, with do_recip 0 / 1;
+the device drivers against the oracle drivers (same iteration count, eigenvalues to 1e-12
+relative: only the reductions' summation order differs) and against analytic eigenvalues."""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+import eigmi
+import oracle
+
+
+def factors(A):
+    lu = eigmi.LU.from_bcsr(None, A.rowptr, A.col, A.val, A.br)
+    d = lu.export()
+    lu.close()
+    return d
+
+
+def dense(A):
+    return A.to_scipy().toarray()
+
+
+CASES = {
+    "laplace2d_16": lambda: oracle.laplace2d(16),
+    "poisson3d_8": lambda: oracle.poisson3d(8),
+    "q1elast_4": lambda: oracle.q1elast(4),
+    "neumann2d_12": lambda: oracle.laplace2d(12, "neumann"),
+}
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_host_lu_factorisation(name):
+    A = CASES[name]()
+    if name.startswith("neumann"):  # singular: factor the shifted operator as StandardInverse would
+        A.val[A.col == np.repeat(np.arange(A.n), np.diff(A.rowptr))] += 0.5
+    d = factors(A)
+    n = A.n
+    L = sp.csr_matrix((d["Lx"], d["Lj"], d["Lp"]), shape=(n, n)).toarray()
+    U = sp.csc_matrix((d["Ux"], d["Ui"], d["Up"]), shape=(n, n)).toarray()
+    assert np.allclose(np.diag(L), 1.0) and np.all(np.triu(L, 1) == 0) and np.all(np.tril(U, -1) == 0)
+    # unit diagonal last in each L row, diagonal last in each U column (umfpacktools.hh contract)
+    assert np.all(d["Lj"][d["Lp"][1:] - 1] == np.arange(n)) and np.all(d["Ui"][d["Up"][1:] - 1] == np.arange(n))
+    B = (dense(A) / d["Rs"][:, None])[d["P"]][:, d["Q"]]
+    assert np.abs(L @ U - B).max() <= 1e-13 * np.abs(B).max()
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_oracle_inverse_solves(name):
+    A = CASES[name]()
+    if name.startswith("neumann"):
+        A.val[A.col == np.repeat(np.arange(A.n), np.diff(A.rowptr))] += 0.5
+    f = oracle.LU(**factors(A))
+    n, m = A.n, 16
+    X = oracle.random_mv8(n, m, 3)
+    out, _ = oracle.inverse_mv8(f, X, m)
+    Xc, Oc = oracle.mv_to_cols(X, n, m), oracle.mv_to_cols(out, n, m)
+    Ad = dense(A)
+    assert np.abs(Ad @ Oc - Xc).max() <= 1e-10 * np.abs(Xc).max() * np.linalg.cond(Ad) / 1e3 + 1e-12
+
+
+def test_oracle_standard_inverse_known_answer():
+    """StandardInverse at tight tolerance: the 4 smallest eigenvalues of the 2-D Dirichlet
+    Laplacian, the reference's own known answer (src/dune-eigensolver.cc:437-446)."""
+    N = 16
+    A = oracle.laplace2d(N)
+    f = oracle.LU(**factors(A))
+    ev, _, it = oracle.standard_inverse(A, f, 0.0, 1e-13, 2000, 4, 123)
+    exact = np.sort(oracle.eig_laplace2d(N))[:4]
+    assert np.allclose(np.sort(ev), exact, rtol=0, atol=1e-9), (ev, exact)
+
+
+def test_oracle_generalized_inverse_identity_b():
+    """GeneralizedInverse with B = I on A's pattern (.cc:145-156 generator) and a shift: the pencil's
+    eigenvalues are A's (the returned ra subtracts the shift, :276-277)."""
+    N = 12
+    A, B = oracle.laplace2d(N), oracle.laplace2d(N, "identity")
+    shift = 0.75
+    As = oracle.CSR(A.nrows, A.rowptr, A.col, A.val + shift * B.val)
+    f = oracle.LU(**factors(As))
+    ev, _, it = oracle.generalized_inverse(A, B, f, shift, 0.0, 1e-14, 3000, 4, 123)
+    exact = np.sort(oracle.eig_laplace2d(N))[:4]
+    assert it > 10 and np.allclose(np.sort(ev), exact, rtol=0, atol=1e-9)
+
+
+# ------------------------------------------------------------------------------------------- GPU
+def _gpu_lu(ctx, A, via="bcsr", recip=False):
+    if via == "bcsr":
+        lu = eigmi.LU.from_bcsr(ctx, A.rowptr, A.col, A.val, A.br)
+        d = lu.export()
+        return lu, oracle.LU(**d)
+    d = factors(A)
+    if recip:  # the same factor in the do_recip form: rows multiplied by 1 / Rs
+        d = dict(d, Rs=1.0 / d["Rs"], do_recip=1)
+    lu = eigmi.LU.from_factors(ctx, **d)
+    return lu, oracle.LU(**d)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,m,via", [("laplace2d_16", 8, "bcsr"), ("poisson3d_8", 16, "factors"),
+                                        ("q1elast_4", 24, "bcsr"), ("neumann2d_12", 8, "factors")])
+def test_inverse_mv8_bitwise(ctx, name, m, via):
+    A = CASES[name]()
+    if name.startswith("neumann"):
+        A.val[A.col == np.repeat(np.arange(A.n), np.diff(A.rowptr))] += 0.5
+    lu, f = _gpu_lu(ctx, A, via)
+    n = A.n
+    X = oracle.random_mv8(n, m, 11)
+    ref_out, ref_in = oracle.inverse_mv8(f, X, m)
+    din, dout = ctx.array(X), ctx.zeros(n * m)
+    lu.inverse_mv8(m, din, dout)
+    assert np.array_equal(dout.get(), ref_out), "A^-1 Q not bitwise the reference arithmetic"
+    # Qin is scratch afterwards ("you may overwrite the input argument", kernels_cpp.hh:659); its
+    # contents are not part of the contract (the reference leaves U-solve partial sums there)
+    lu.close()
+
+
+@pytest.mark.gpu
+def test_inverse_mv8_do_recip(ctx):
+    A = oracle.poisson3d(6)
+    lu, f = _gpu_lu(ctx, A, "factors", recip=True)
+    X = oracle.random_mv8(A.n, 8, 2)
+    ref_out, _ = oracle.inverse_mv8(f, X, 8)
+    din, dout = ctx.array(X), ctx.zeros(A.n * 8)
+    lu.inverse_mv8(8, din, dout)
+    assert np.array_equal(dout.get(), ref_out)
+
+
+@pytest.mark.gpu
+def test_inverse_mv8_unsorted_rows(ctx):
+    """Factors whose L rows are not in ascending column order (possible from UMFPACK): the device
+    sorts them, so the result equals the reference to rounding (1e-13), not bitwise."""
+    A = oracle.laplace2d(12)
+    d = factors(A)
+    Lj, Lx = d["Lj"].copy(), d["Lx"].copy()
+    for i in range(A.n):
+        a, b = d["Lp"][i], d["Lp"][i + 1] - 1  # keep the unit diagonal last
+        Lj[a:b], Lx[a:b] = Lj[a:b][::-1].copy(), Lx[a:b][::-1].copy()
+    d2 = dict(d, Lj=Lj, Lx=Lx)
+    lu = eigmi.LU.from_factors(ctx, **d2)
+    X = oracle.random_mv8(A.n, 8, 4)
+    ref_out, _ = oracle.inverse_mv8(oracle.LU(**d2), X, 8)
+    din, dout = ctx.array(X), ctx.zeros(A.n * 8)
+    lu.inverse_mv8(8, din, dout)
+    assert np.abs(dout.get() - ref_out).max() <= 1e-13 * np.abs(ref_out).max()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shift,tol,nev", [(0.0, 1e-10, 4), (0.3, 1e-8, 10)])
+def test_standard_inverse_vs_oracle(ctx, shift, tol, nev):
+    N = 16
+    A = oracle.laplace2d(N)
+    M = eigmi.Matrix.from_bcsr(ctx, A.rowptr, A.col, A.val)
+    ev, evec, it = eigmi.standard_inverse(M, shift, tol, 1000, nev, 123)
+    As = oracle.CSR(A.nrows, A.rowptr, A.col, A.val.copy())
+    oracle.lib.orc_shift_diag(As.n, As.rowptr, As.col, As.val, shift)
+    f = oracle.LU(**factors(As))  # the device factored the same shifted matrix with the same code
+    rev, revec, rit = oracle.standard_inverse(A, f, shift, tol, 1000, nev, 123)
+    assert it == rit
+    assert np.allclose(ev, rev, rtol=1e-12, atol=0)
+    exact = np.sort(oracle.eig_laplace2d(N))[:4]
+    if tol <= 1e-10:
+        assert np.allclose(np.sort(ev)[:4], exact, rtol=0, atol=1e-8)
+
+
+@pytest.mark.gpu
+def test_generalized_inverse_vs_oracle(ctx):
+    N = 12
+    A, B = oracle.laplace2d(N), oracle.laplace2d(N, "identity")
+    dA = eigmi.Matrix.from_bcsr(ctx, A.rowptr, A.col, A.val)
+    dB = eigmi.Matrix.from_bcsr(ctx, B.rowptr, B.col, B.val)
+    shift, reg = 0.75, 0.0
+    ev, _, it = eigmi.generalized_inverse(dA, dB, shift, reg, 1e-12, 500, 4, 123)
+    As = oracle.CSR(A.nrows, A.rowptr, A.col, A.val + shift * B.val)
+    f = oracle.LU(**factors(As))
+    rev, _, rit = oracle.generalized_inverse(A, B, f, shift, reg, 1e-12, 500, 4, 123)
+    assert it == rit and np.allclose(ev, rev, rtol=1e-12, atol=0)
+    assert np.allclose(np.sort(ev), np.sort(oracle.eig_laplace2d(N))[:4], rtol=0, atol=1e-8)
+
+
+@pytest.mark.gpu
+def test_generalized_inverse_pu_mass(ctx):
+    """The reference harness's GenEO-type pencil (.cc:98-143): Neumann Laplacian A, partition-of-
+    unity-masked B, shift + regularisation; device = oracle driver (iterations, values 1e-10)."""
+    N, shift, reg = 16, 1.0, 1e-3
+    A, B = oracle.laplace2d(N, "neumann"), oracle.laplace2d(N, "pu", overlap=3)
+    dA = eigmi.Matrix.from_bcsr(ctx, A.rowptr, A.col, A.val)
+    dB = eigmi.Matrix.from_bcsr(ctx, B.rowptr, B.col, B.val)
+    ev, _, it = eigmi.generalized_inverse(dA, dB, shift, reg, 1e-8, 200, 8, 123)
+    diag = A.col == np.repeat(np.arange(A.n), np.diff(A.rowptr))
+    As = oracle.CSR(A.nrows, A.rowptr, A.col, A.val + shift * B.val + reg * diag)
+    f = oracle.LU(**factors(As))
+    rev, _, rit = oracle.generalized_inverse(A, B, f, shift, reg, 1e-8, 200, 8, 123)
+    assert it == rit and np.allclose(ev, rev, rtol=1e-10, atol=1e-12)
