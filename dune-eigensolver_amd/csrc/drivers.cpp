@@ -280,6 +280,222 @@ extern "C" int eig_generalized_inverse(eig_mat_t A, eig_mat_t B, eig_lu_t lu, do
 }
 
 // ============================================================================================
+// computeGenSymShiftInvertMinMagnitude (arpack_geneo_wrapper.hh:581-658): thick-restart Lanczos
+// in the B-inner product on OP = (A - sigma B)^-1 B, "LM" 
+// ============================================================================================
+namespace {
+
+// Host copy of A - sigma B on A's pattern (pattern(B) within pattern(A); ashiftb.axpy(-sigma, b_),
+// arpack_geneo_wrapper.hh:599-600).
+void shifted_copy(eig_mat_s &A, eig_mat_s *B, double sigma, std::vector<i64> &rp, std::vector<i32> &c,
+                  std::vector<double> &v)
+{
+  mat_download_bcsr(A, rp, c, v);
+  if (sigma == 0.0) return;
+  const i64 n = A.nb_rows;
+  if (!B)
+  {
+    for (i64 i = 0; i < n; ++i)
+    {
+      const i32 *b0 = c.data() + rp[i], *b1 = c.data() + rp[i + 1];
+      const i32 *hit = std::lower_bound(b0, b1, (i32)i);
+      EIG_CHECK(hit != b1 && *hit == (i32)i, EIG_ERR_SHAPE, "shift-invert: A has no diagonal entry");
+      v[hit - c.data()] -= sigma;
+    }
+    return;
+  }
+  std::vector<i64> brp;
+  std::vector<i32> bc;
+  std::vector<double> bv;
+  mat_download_bcsr(*B, brp, bc, bv);
+  for (i64 i = 0; i < n; ++i)
+    for (i64 q = brp[i]; q < brp[i + 1]; ++q)
+    {
+      const i32 *b0 = c.data() + rp[i], *b1 = c.data() + rp[i + 1];
+      const i32 *hit = std::lower_bound(b0, b1, bc[q]);
+      EIG_CHECK(hit != b1 && *hit == bc[q], EIG_ERR_SHAPE, "shift-invert: pattern(B) must be contained in pattern(A)");
+      v[hit - c.data()] -= sigma * bv[q];
+    }
+}
+
+}  // namespace
+
+extern "C" int eig_shift_invert_solve(eig_mat_t A, eig_mat_t B, eig_lu_t lu, double sigma, int nev, int ncv,
+                                      double tol, int maxit, unsigned seed, double *eval_host, double *evec_host,
+                                      int *restarts)
+{
+  return guard(A ? A->ctx : nullptr, [&] {
+    EIG_CHECK(A && eval_host && nev > 0, EIG_ERR_ARG, "eig_shift_invert_solve: bad argument");
+    check_inverse_matrix(A, "computeGenSymShiftInvertMinMagnitude");
+    if (B)
+    {
+      check_inverse_matrix(B, "computeGenSymShiftInvertMinMagnitude");
+      EIG_CHECK(B->ctx == A->ctx && B->nb_rows == A->nb_rows, EIG_ERR_SHAPE, "shift-invert: A and B sizes differ");
+    }
+    eig_ctx_t ctx = A->ctx;
+    EIG_HIP(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    const i64 n = A->nb_rows;
+    if (ncv <= 0) ncv = (int)std::min<i64>(n, std::max(2 * nev + 1, 20));  // ARPACK++ ncv = 0 (auto)
+    EIG_CHECK(nev < ncv && ncv <= n && ncv <= 500, EIG_ERR_ARG, "shift-invert: need nev < ncv <= min(n, 500)");
+    if (tol <= 0.0) tol = 2.220446049250313e-16;  // tol = 0: machine precision (ARPACK)
+    if (maxit <= 0) maxit = 100 * nev;            // maxit = 0: 100 nev (ARPACK++)
+    LuRef F;
+    if (lu)
+      F.lu = lu;
+    else
+    {
+      std::vector<i64> rp;
+      std::vector<i32> c;
+      std::vector<double> v;
+      EIG_HIP(hipStreamSynchronize(s));
+      shifted_copy(*A, B, sigma, rp, c, v);
+      factor_host(*A, rp, c, v, F);
+    }
+    EIG_CHECK(lu_size(F.lu) == n, EIG_ERR_SHAPE, "shift-invert: factorisation size differs from A");
+    const int m = ncv;
+    // basis V and BV (= B V; V itself when B is NULL), column-major, m + 1 vectors each
+    DevBuf Vb((size_t)(m + 1) * n * 8), BVb(B ? (size_t)(m + 1) * n * 8 : 8), Wb(n * 8), BWb(n * 8), X8b(n * 64),
+        Y8b(n * 64), Tb((size_t)2 * (m + 1) * n * 8), cb((size_t)(m + 8) * 8 * 2);
+    double *V = Vb.d(), *BV = B ? BVb.d() : Vb.d(), *W = Wb.d(), *BW = BWb.d(), *X8 = X8b.d(), *Y8 = Y8b.d();
+    double *cd = cb.d(), *sc = cd + m + 8;
+    EIG_HIP(hipMemsetAsync(X8, 0, n * 64, s));
+    auto bmul = [&](double *x, double *y) {  // y = B x
+      if (B) launch_spmv(*B, x, y, nullptr, 0, B->nslices, s);
+      else if (y != x) EIG_HIP(hipMemcpyAsync(y, x, n * 8, hipMemcpyDeviceToDevice, s));
+    };
+    auto dot = [&](const double *x, const double *y) {
+      launch_dot(n, x, y, sc, 0, s, ctx->red);
+      double h = 0.0;
+      EIG_HIP(hipMemcpyAsync(&h, sc, 8, hipMemcpyDeviceToHost, s));
+      EIG_HIP(hipStreamSynchronize(s));
+      return h;
+    };
+    auto op = [&](const double *bx, double *y) {  // y = (A - sigma B)^-1 bx (column 0 of the 8-wide solve)
+      EIG_HIP(hipMemcpy2DAsync(X8, 64, bx, 8, 8, n, hipMemcpyDeviceToDevice, s));
+      lu_inverse_device(F.lu, 8, X8, Y8, s);
+      EIG_HIP(hipMemcpy2DAsync(y, 8, Y8, 64, 8, n, hipMemcpyDeviceToDevice, s));
+    };
+    // start vector: mt19937(seed) normal numbers put into the range of OP (as ARPACK's dgetv0 does
+    // for the generalised modes, so a singular B cannot leave null(B) components in the basis),
+    // B-normalised
+    {
+      std::vector<double> h(n);
+      host_random_normal(n, seed, h.data());
+      EIG_HIP(hipMemcpyAsync(W, h.data(), n * 8, hipMemcpyHostToDevice, s));
+      bmul(W, BW);
+      op(BW, V);
+      bmul(V, BV);
+      const double nb = std::sqrt(dot(V, BV));
+      launch_scal(n, 1.0 / nb, V, s);
+      if (B) launch_scal(n, 1.0 / nb, BV, s);
+    }
+    std::vector<double> T((size_t)m * m, 0.0), ctot(m + 1), ch(m + 1), th, Y;
+    int k = 0, nrestart = 0;
+    double betam = 0.0;
+    std::vector<int> want;
+    bool done = false;
+    while (!done)
+    {
+      // extend the Lanczos factorisation from k to m vectors
+      for (int j = k; j < m; ++j)
+      {
+        double *bvj = BV + (i64)j * n;
+        // w = (A - sigma B)^-1 (B v_j): the reverse-communication product of ARSymGenEig 'S' mode
+        op(bvj, W);
+        std::fill(ctot.begin(), ctot.end(), 0.0);
+        for (int pass = 0; pass < 2; ++pass)  // DGKS / CGS2 against v_0 .. v_j in the B-inner product
+        {
+          launch_gemv_t(n, j + 1, BV, n, W, cd, 0, s, ctx->red);
+          launch_gemv_n_sub(n, j + 1, V, n, cd, nullptr, W, s);
+          EIG_HIP(hipMemcpyAsync(ch.data(), cd, (j + 1) * 8, hipMemcpyDeviceToHost, s));
+          EIG_HIP(hipStreamSynchronize(s));
+          for (int i = 0; i <= j; ++i) ctot[i] += ch[i];
+        }
+        for (int i = 0; i <= j; ++i) T[(size_t)i * m + j] = T[(size_t)j * m + i] = ctot[i];
+        bmul(W, BW);
+        const double beta = std::sqrt(std::max(0.0, dot(W, BW)));
+        double tn = 0.0;
+        for (int i = 0; i <= j; ++i) tn = std::max(tn, std::fabs(ctot[i]));
+        EIG_CHECK(beta > 1e-14 * tn, EIG_ERR_BREAKDOWN,
+                  "shift-invert Lanczos: invariant subspace reached (choose ncv < n or another seed)");
+        double *vn = V + (i64)(j + 1) * n, *bvn = BV + (i64)(j + 1) * n;
+        EIG_HIP(hipMemcpyAsync(vn, W, n * 8, hipMemcpyDeviceToDevice, s));
+        launch_scal(n, 1.0 / beta, vn, s);
+        if (B)
+        {
+          EIG_HIP(hipMemcpyAsync(bvn, BW, n * 8, hipMemcpyDeviceToDevice, s));
+          launch_scal(n, 1.0 / beta, bvn, s);
+        }
+        if (j + 1 < m) T[(size_t)(j + 1) * m + j] = T[(size_t)j * m + (j + 1)] = beta;
+        betam = beta;
+      }
+      sym_eig(m, T, th, Y);
+      // "LM" on OP: the nev Ritz values of largest magnitude (eigenvalues of the pencil nearest sigma)
+      std::vector<int> ord(m);
+      std::iota(ord.begin(), ord.end(), 0);
+      std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return std::fabs(th[a]) > std::fabs(th[b]); });
+      want.assign(ord.begin(), ord.begin() + nev);
+      bool conv = true;
+      for (int i : want)
+        if (std::fabs(betam * Y[(size_t)(m - 1) * m + i]) > tol * std::fabs(th[i])) conv = false;
+      if (conv || nrestart >= maxit)
+      {
+        done = true;
+        break;
+      }
+      // thick restart: keep kk Ritz vectors of largest |theta|, then the residual vector
+      const int kk = std::min(m - 2, nev + (m - nev) / 2);
+      std::vector<double> coef(m);
+      double *Tmp = Tb.d();
+      for (int q = 0; q < kk; ++q)
+      {
+        for (int i = 0; i < m; ++i) coef[i] = Y[(size_t)i * m + ord[q]];
+        EIG_HIP(hipMemcpyAsync(cd, coef.data(), m * 8, hipMemcpyHostToDevice, s));
+        launch_gemv_n_set(n, m, V, n, cd, nullptr, Tmp + (i64)q * n, s);
+        if (B) launch_gemv_n_set(n, m, BV, n, cd, nullptr, Tmp + (i64)(kk + q) * n, s);
+        EIG_HIP(hipStreamSynchronize(s));
+      }
+      EIG_HIP(hipMemcpyAsync(V, Tmp, (size_t)kk * n * 8, hipMemcpyDeviceToDevice, s));
+      EIG_HIP(hipMemcpyAsync(V + (i64)kk * n, V + (i64)m * n, n * 8, hipMemcpyDeviceToDevice, s));
+      if (B)
+      {
+        EIG_HIP(hipMemcpyAsync(BV, Tmp + (i64)kk * n, (size_t)kk * n * 8, hipMemcpyDeviceToDevice, s));
+        EIG_HIP(hipMemcpyAsync(BV + (i64)kk * n, BV + (i64)m * n, n * 8, hipMemcpyDeviceToDevice, s));
+      }
+      std::fill(T.begin(), T.end(), 0.0);
+      for (int q = 0; q < kk; ++q) T[(size_t)q * m + q] = th[ord[q]];
+      k = kk;
+      ++nrestart;
+    }
+    // eigenpairs of the pencil: lambda = sigma + 1 / theta, sorted ascending (:636-648)
+    std::vector<int> idx(nev);
+    std::iota(idx.begin(), idx.end(), 0);
+    std::vector<double> lam(nev);
+    for (int i = 0; i < nev; ++i) lam[i] = sigma + 1.0 / th[want[i]];
+    std::stable_sort(idx.begin(), idx.end(), [&](int a, int b) { return lam[a] < lam[b]; });
+    for (int i = 0; i < nev; ++i) eval_host[i] = lam[idx[i]];
+    if (evec_host)
+    {
+      // x = V y purified with the residual direction, x + (beta_m y_m / theta) v_m = OP(V y) / theta
+      // (ARPACK dseupd's purification for the spectral-transformation modes)
+      std::vector<double> coef(m + 1);
+      for (int q = 0; q < nev; ++q)
+      {
+        const int col = want[idx[q]];
+        for (int i = 0; i < m; ++i) coef[i] = Y[(size_t)i * m + col];
+        coef[m] = betam * Y[(size_t)(m - 1) * m + col] / th[col];
+        EIG_HIP(hipMemcpyAsync(cd, coef.data(), (m + 1) * 8, hipMemcpyHostToDevice, s));
+        launch_gemv_n_set(n, m + 1, V, n, cd, nullptr, W, s);
+        EIG_HIP(hipMemcpyAsync(evec_host + (i64)q * n, W, n * 8, hipMemcpyDeviceToHost, s));
+        EIG_HIP(hipStreamSynchronize(s));
+      }
+    }
+    if (restarts) *restarts = nrestart;
+  });
+}
+
+// ============================================================================================
 // Lanczos three-term recurrence (DESIGN.md "Lanczos step")
 // ============================================================================================
 namespace {

@@ -279,6 +279,18 @@ int eig_standard_inverse(eig_mat_t A, eig_lu_t lu, double shift, double tol, int
 int eig_generalized_inverse(eig_mat_t A, eig_mat_t B, eig_lu_t lu, double shift, double reg, double tol, int maxiter,
                             int nev, unsigned seed, double *eval_host, double *evec_host, int *iters, int verbose);
 
+/* computeGenSymShiftInvertMinMagnitude (arpack_geneo_wrapper.hh:581-658): the nev eigenpairs of
+ * A x = lambda B x nearest sigma ("LM" on OP = (A - sigma B)^-1 B, the operator ARSymGenEig's 'S'
+ * mode builds from multMv / multMvB, :621-622), by thick-restart Lanczos in the B-inner product with
+ * full (DGKS) re-orthogonalisation.  B = NULL: standard problem.  The LU of A - sigma B (A's pattern
+ * must contain B's, :599-600) is computed on the host unless `lu` (factors of A - sigma B) is given.
+ * ncv = 0: min(n, max(2 nev + 1, 20)); tol = 0: machine precision; maxit = 0: 100 nev restarts
+ * (ARPACK++ defaults).  Converged when |beta_m y_m,i| <= tol |theta_i| for the nev wanted pairs.
+ * eval_host[nev] ascending (the reference sorts the unshifted values, :636-648); evec_host nev x n
+ * B-normalised, or NULL; *restarts: thick restarts taken. */
+int eig_shift_invert_solve(eig_mat_t A, eig_mat_t B, eig_lu_t lu, double sigma, int nev, int ncv, double tol,
+                           int maxit, unsigned seed, double *eval_host, double *evec_host, int *restarts);
+
 /* ---------------------------------------------------------------- block Lanczos (config C5) */
 /* Generalised symmetric-definite eigenproblem K x = lambda M x by block Lanczos in the M-inner
  * product on the operator M^-1 K (the pencil GeneralizedInverse solves, eigensolver.hh:204-351,

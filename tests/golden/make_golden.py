@@ -70,6 +70,23 @@ def q1elast():
     np.savez_compressed(os.path.join(HERE, "q1elast_6_bsr.npz"), x=x, y_bsr=y, eig_dense=w, analytic=ana)
 
 
+def geneo():
+    """The reference harness's generalised experiment (src/dune-eigensolver.cc:455-512, ini [ev]):
+    Neumann Laplacian A, partition-of-unity-masked B (overlap 3), ARPACK shift-invert with
+    sigma = -shift = -1e-3 ("LM", computeGenSymShiftInvertMinMagnitude, arpack_geneo_wrapper.hh:
+    581-658), nev = 4 at N = 32; plus the C5 P1 pencil (K, M) at N = 8, sigma = 0, nev = 6."""
+    N, shift = 32, 1e-3
+    A = oracle.laplace2d(N, "neumann").to_scipy()
+    B = oracle.laplace2d(N, "pu", overlap=3).to_scipy()
+    w, v = ssl.eigsh(A, k=4, M=B, sigma=-shift, which="LM", tol=1e-14, v0=np.ones(A.shape[0]))
+    o = np.argsort(w)
+    K, M = oracle.p1_kuhn(8)
+    pw = ssl.eigsh(K, k=6, M=M, sigma=0.0, which="LM", tol=1e-14, v0=np.ones(K.shape[0]),
+                   return_eigenvectors=False)
+    np.savez_compressed(os.path.join(HERE, "geneo_arpack.npz"), geneo_N=N, geneo_shift=shift, geneo_w=w[o],
+                        geneo_v=v[:, o], p1_N=8, p1_w=np.sort(pw))
+
+
 def reference_run():
     rec = {
         "source": "SURVEY.md section 6 / BASELINE.md section 2: reference headers multivector.hh + kernels_cpp.hh + "
@@ -90,5 +107,6 @@ if __name__ == "__main__":
     c1()
     poisson3d()
     q1elast()
+    geneo()
     reference_run()
     print("golden fixtures written to", HERE)
