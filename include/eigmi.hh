@@ -9,9 +9,16 @@
 //   * eigmi::ArpackOperator           multMv / multMvB(double* v, double* w), nrows(), ncols():
 //                                     the member functions ARPACK++ binds
 //                                     (arpack_geneo_wrapper.hh:257-285);
+//   * eigmi::Factorization            the UMFPackFactorizedMatrix role (umfpacktools.hh:16-199):
+//                                     from an ISTL matrix (host factorisation) or from any object
+//                                     exposing UMFPackFactorizedMatrix's public factor arrays;
+//   * eigmi::ShiftInvertOperator      APP_BCRSMatMul_GeneralizedShiftInvertMode's multMv =
+//                                     (A - sigma B)^-1 v and multMvB = B v (arpack_geneo_wrapper.hh:
+//                                     225-285), and computeGenSymShiftInvertMinMagnitude (:581-658);
 //   * free functions with the reference kernel names and MultiVector signatures
-//     (matmul_sparse_tallskinny_blocked, dot_products_diagonal_blocked, dot_products_all_blocked,
-//     orthonormalize_blocked, B_orthonormalize_blocked, StandardLargest) operating on host
+//     (matmul_sparse_tallskinny_blocked, matmul_inverse_tallskinny_blocked,
+//     dot_products_diagonal_blocked, dot_products_all_blocked, orthonormalize_blocked,
+//     B_orthonormalize_blocked, StandardLargest, StandardInverse, GeneralizedInverse) operating on host
 //     MultiVector<double,8>-compatible objects (anything with operator()(i,j), rows(), cols(),
 //     blocksize == 8), staged through HBM, plus DeviceMultiVector variants that stay resident;
 //   * SHAPE / BLOCKSIZE statuses are thrown as std::invalid_argument (as the reference does,
@@ -172,9 +179,9 @@ class Matrix {
 };
 
 // --------------------------------------------------------------- ARPACK++ operator adapter
-// Binds like APP_BCRSMatMul_GeneralizedShiftInvertMode: ARPACK++ calls multMvB(v, w) with its
-// workd arrays (arpack_geneo_wrapper.hh:269-279).  multMv applies the same operator (the
-// shift-invert solve of the reference is out of scope).
+// Binds like the plain-product wrappers: ARPACK++ calls multMv / multMvB(v, w) with its workd arrays
+// (arpack_geneo_wrapper.hh:93-107, :269-279), both y = A x here.  The shift-invert operator of
+// :225-285 is ShiftInvertOperator below.
 class ArpackOperator {
  public:
   explicit ArpackOperator(const Matrix &A) : A_(&A), n_((int)A.info().n) {}
@@ -311,6 +318,198 @@ int StandardLargest(Matrix &A, double shift, double tol, int maxiter, int nev, s
   for (int j = 0; j < nev; ++j)
     for (std::size_t i = 0; i < n; ++i) evec[j][i] = vec[(std::size_t)j * n + i];
   return iters;
+}
+
+// -------------------------------------------------------------- LU factors (UMFPACK's role)
+class Factorization {
+ public:
+  // Host factorisation of an ISTL-concept matrix (eig_lu_create_bcsr: RCM + envelope LU, no
+  // pivoting) -- the stand-in for UMFPackFactorizedMatrix<ISTLM> F(A) when SuiteSparse is absent.
+  template <class ISTLM>
+  static Factorization from_istl(const Context &ctx, const ISTLM &A)
+  {
+    using block_type = typename ISTLM::block_type;
+    constexpr int br = block_type::rows, bc = block_type::cols;
+    static_assert(br == bc, "UMFPackFactorizedMatrix: input matrix must be square");
+    std::vector<int64_t> rowptr(1, 0);
+    std::vector<int32_t> col;
+    std::vector<double> val;
+    for (auto row_iter = A.begin(); row_iter != A.end(); ++row_iter)
+    {
+      for (auto col_iter = row_iter->begin(); col_iter != row_iter->end(); ++col_iter)
+      {
+        col.push_back((int32_t)col_iter.index());
+        for (int i = 0; i < br; ++i)
+          for (int j = 0; j < bc; ++j) val.push_back(entry(*col_iter, i, j));
+      }
+      rowptr.push_back((int64_t)col.size());
+    }
+    eig_lu_t lu = nullptr;
+    check(eig_lu_create_bcsr(ctx.get(), (int64_t)rowptr.size() - 1, br, rowptr.data(), col.data(), val.data(), &lu),
+          ctx.get());
+    return Factorization(ctx.get(), lu);
+  }
+  // From an object with UMFPackFactorizedMatrix's public members (n, Lp, Lj, Lx, Up, Ui, Ux, P, Q,
+  // do_recip, Rs; IntType long), e.g. a real UMFPackFactorizedMatrix<ISTLM>.
+  template <class UMF>
+  static Factorization from_umfpack(const Context &ctx, const UMF &F)
+  {
+    const int64_t n = (int64_t)F.n;
+    auto cp = [](const auto *p, int64_t k) { return std::vector<int64_t>(p, p + k); };
+    std::vector<int64_t> Lp = cp(F.Lp, n + 1), Up = cp(F.Up, n + 1), P = cp(F.P, n), Q = cp(F.Q, n);
+    std::vector<int64_t> Lj = cp(F.Lj, Lp[n]), Ui = cp(F.Ui, Up[n]);
+    eig_lu_t lu = nullptr;
+    check(eig_lu_create(ctx.get(), n, Lp.data(), Lj.data(), F.Lx, Up.data(), Ui.data(), F.Ux, P.data(), Q.data(),
+                        F.Rs, F.do_recip ? 1 : 0, &lu),
+          ctx.get());
+    return Factorization(ctx.get(), lu);
+  }
+  Factorization(Factorization &&o) noexcept : ctx_(o.ctx_), h_(o.h_) { o.h_ = nullptr; }
+  Factorization(const Factorization &) = delete;
+  Factorization &operator=(const Factorization &) = delete;
+  ~Factorization()
+  {
+    if (h_) eig_lu_destroy(h_);
+  }
+  eig_lu_t get() const { return h_; }
+  eig_ctx_t ctx() const { return ctx_; }
+  std::size_t size() const
+  {
+    int64_t n = 0;
+    check(eig_lu_info(h_, &n, nullptr, nullptr, nullptr), ctx_);
+    return (std::size_t)n;
+  }
+
+ private:
+  Factorization(eig_ctx_t c, eig_lu_t h) : ctx_(c), h_(h) {}
+  template <class B>
+  static double entry(const B &b, int i, int j)
+  {
+    if constexpr (std::is_arithmetic<B>::value) return (double)b;
+    else return b[i][j];
+  }
+  eig_ctx_t ctx_;
+  eig_lu_t h_;
+};
+
+// matmul_inverse_tallskinny_blocked (kernels_cpp.hh:660-755): Qout = A^-1 Qin; Qin may be
+// overwritten (as the reference allows).  Same error messages as the reference.
+template <class MV>
+void matmul_inverse_tallskinny_blocked(MV &Qout, Factorization &F, MV &Qin)
+{
+  if (Qout.rows() != Qin.rows() || Qout.cols() != Qin.cols())
+    throw std::invalid_argument("matmul_inverse_tallskinny_blocked: Qout/Qin size mismatch");
+  if (F.size() != Qin.rows() || F.size() != Qout.rows())
+    throw std::invalid_argument("matmul_inverse_tallskinny_blocked: Factorization does not match size of Qout/Qin");
+  eig_ctx_t c = F.ctx();
+  const std::size_t n = Qin.rows(), m = Qin.cols();
+  double *din = nullptr, *dout = nullptr;
+  check(eig_malloc(c, n * m * 8 + 8, (void **)&din), c);
+  check(eig_malloc(c, n * m * 8 + 8, (void **)&dout), c);
+  int rc = eig_memcpy_h2d(c, din, &Qin(0, 0), n * m * 8);
+  if (rc == EIG_OK) rc = eig_inverse_mv8(F.get(), (int64_t)m, din, dout);
+  if (rc == EIG_OK) rc = eig_memcpy_d2h(c, &Qout(0, 0), dout, n * m * 8);
+  eig_free(c, din);
+  eig_free(c, dout);
+  check(rc, c);
+}
+
+// StandardInverse (eigensolver.hh:116-198): same arguments; mutates A when shift != 0.
+template <class VEC>
+int StandardInverse(Matrix &A, double shift, double tol, int maxiter, int nev, std::vector<double> &eval,
+                    std::vector<VEC> &evec, int verbose = 0, unsigned int seed = 123)
+{
+  const std::size_t n = (std::size_t)A.info().n;
+  std::vector<double> ev(nev), vec((std::size_t)nev * n);
+  int iters = 0;
+  check(eig_standard_inverse(A.get(), nullptr, shift, tol, maxiter, nev, seed, ev.data(), vec.data(), &iters, verbose),
+        A.ctx());
+  for (int j = 0; j < nev; ++j) eval[j] = ev[j];
+  for (int j = 0; j < nev; ++j)
+    for (std::size_t i = 0; i < n; ++i) evec[j][i] = vec[(std::size_t)j * n + i];
+  return iters;
+}
+
+// GeneralizedInverse (eigensolver.hh:204-351): A is not modified (the reference copies it); the
+// outputs are resized to nev like the reference (:328-341).
+template <class VEC>
+int GeneralizedInverse(const Matrix &A, const Matrix &B, double shift, double reg, double tol, int maxiter, int nev,
+                       std::vector<double> &eval, std::vector<VEC> &evec, int verbose = 0, unsigned int seed = 123)
+{
+  const std::size_t n = (std::size_t)A.info().n;
+  std::vector<double> ev(nev), vec((std::size_t)nev * n);
+  int iters = 0;
+  check(eig_generalized_inverse(A.get(), B.get(), nullptr, shift, reg, tol, maxiter, nev, seed, ev.data(), vec.data(),
+                                &iters, verbose),
+        A.ctx());
+  if (eval.size() != (std::size_t)nev) eval.resize(nev);
+  if (evec.size() != (std::size_t)nev) evec.resize(nev);
+  for (int j = 0; j < nev; ++j) eval[j] = ev[j];
+  for (int j = 0; j < nev; ++j)
+  {
+    if (evec[j].size() != n) evec[j].resize(n);
+    for (std::size_t i = 0; i < n; ++i) evec[j][i] = vec[(std::size_t)j * n + i];
+  }
+  return iters;
+}
+
+// APP_BCRSMatMul_GeneralizedShiftInvertMode (arpack_geneo_wrapper.hh:225-285): multMv(v, w) =
+// (A - sigma B)^-1 v, multMvB(v, w) = B v, on ARPACK's host workd arrays; plus the driver
+// computeGenSymShiftInvertMinMagnitude (:581-658) with its argument meaning: x.size() eigenpairs
+// nearest sigma, eigenvalues ascending, B-normalised vectors.
+class ShiftInvertOperator {
+ public:
+  template <class ISTLM>
+  ShiftInvertOperator(const Context &ctx, const ISTLM &A_minus_sigma_B, const Matrix &B)
+      : F_(Factorization::from_istl(ctx, A_minus_sigma_B)), B_(&B), n_((int)B.info().n)
+  {
+    if ((int)F_.size() != n_) throw std::invalid_argument("ShiftInvertOperator: Matrix is not square");
+  }
+  void multMv(double *v, double *w)
+  {
+    eig_ctx_t c = F_.ctx();
+    const std::size_t n = (std::size_t)n_;
+    std::vector<double> x(n * 8, 0.0);
+    for (std::size_t i = 0; i < n; ++i) x[i * 8] = v[i];
+    double *din = nullptr, *dout = nullptr;
+    check(eig_malloc(c, n * 64, (void **)&din), c);
+    check(eig_malloc(c, n * 64, (void **)&dout), c);
+    int rc = eig_memcpy_h2d(c, din, x.data(), n * 64);
+    if (rc == EIG_OK) rc = eig_inverse_mv8(F_.get(), 8, din, dout);
+    if (rc == EIG_OK) rc = eig_memcpy_d2h(c, x.data(), dout, n * 64);
+    eig_free(c, din);
+    eig_free(c, dout);
+    check(rc, c);
+    for (std::size_t i = 0; i < n; ++i) w[i] = x[i * 8];
+  }
+  void multMvB(double *v, double *w) { B_->mv_host(v, w); }
+  int nrows() const { return n_; }
+  int ncols() const { return n_; }
+
+ private:
+  Factorization F_;
+  const Matrix *B_;
+  int n_;
+};
+
+template <class BlockVector>
+void computeGenSymShiftInvertMinMagnitude(const Matrix &A, const Matrix &B, double epsilon, std::vector<BlockVector> &x,
+                                          std::vector<double> &lambda, double sigma, int maxit = 0)
+{
+  const int nev = (int)x.size();
+  const std::size_t n = (std::size_t)A.info().n;
+  std::vector<double> ev(nev), vec((std::size_t)nev * n);
+  int restarts = 0;
+  check(eig_shift_invert_solve(A.get(), B.get(), nullptr, sigma, nev, 0, epsilon, maxit, 123, ev.data(), vec.data(),
+                               &restarts),
+        A.ctx());
+  if (lambda.size() < (std::size_t)nev) lambda.resize(nev);
+  for (int i = 0; i < nev; ++i)
+  {
+    lambda[i] = ev[i];
+    double *dst = &x[i][0][0];  // BlockVector<FieldVector<double,k>>: contiguous scalars
+    for (std::size_t r = 0; r < n; ++r) dst[r] = vec[(std::size_t)i * n + r];
+  }
 }
 
 }  // namespace eigmi

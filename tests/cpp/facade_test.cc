@@ -8,9 +8,11 @@
 //
 //   facade_test            full run on cuda:0 (GPU tests)
 //   facade_test --no-device  expects the library to report "no device" (CPU build check)
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <array>
 #include <random>
 #include <vector>
 
@@ -202,6 +204,124 @@ int main(int argc, char **argv)
   int it = eigmi::StandardLargest(dA, 0.0, 2e-3, 4000, 4, eval, evec, 0, 123);
   EXPECT(it == 50);
   EXPECT(std::fabs(eval[0] - 7.9037) < 5e-5);
+
+  // 6) UMFPackFactorizedMatrix role + matmul_inverse_tallskinny_blocked (kernels_cpp.hh:660-755)
+  const int N16 = 16;
+  auto A16 = laplace2d(N16);
+  const std::size_t n16 = A16.N();
+  auto F = eigmi::Factorization::from_istl(ctx, A16);
+  EXPECT(F.size() == n16);
+  MV8 R(n16, 8), Z(n16, 8), Rc(n16, 8);
+  for (auto &v : R.p) v = nd(g);
+  Rc = R;
+  eigmi::matmul_inverse_tallskinny_blocked(Z, F, R);
+  double res = 0.0;
+  for (std::size_t j = 0; j < 8; ++j)
+    for (auto r = A16.begin(); r != A16.end(); ++r)
+    {
+      double s = 0.0;
+      for (auto c = r->begin(); c != r->end(); ++c) s += (double)(*c) * Z(c.index(), j);
+      res = std::max(res, std::fabs(s - Rc(r.index(), j)));
+    }
+  EXPECT(res < 1e-11);
+  {
+    // the same factors through an object shaped like UMFPackFactorizedMatrix (IntType long)
+    eigmi::Factorization Fh = eigmi::Factorization::from_istl(ctx, A16);
+    int64_t nn = 0, lnz = 0, unz = 0;
+    int rec = 0;
+    eigmi::check(eig_lu_info(Fh.get(), &nn, &lnz, &unz, &rec), ctx.get());
+    struct UMFLike {
+      long n;
+      std::vector<long> lp, lj, up, ui, pp, qq;
+      std::vector<double> lx, ux, rs;
+      long *Lp, *Lj, *Up, *Ui, *P, *Q;
+      double *Lx, *Ux, *Rs;
+      long do_recip;
+    } u;
+    std::vector<int64_t> Lp(nn + 1), Lj(lnz), Up(nn + 1), Ui(unz), P(nn), Q(nn);
+    u.lx.resize(lnz);
+    u.ux.resize(unz);
+    u.rs.resize(nn);
+    eigmi::check(eig_lu_export(Fh.get(), Lp.data(), Lj.data(), u.lx.data(), Up.data(), Ui.data(), u.ux.data(), P.data(),
+                               Q.data(), u.rs.data()),
+                 ctx.get());
+    u.n = (long)nn;
+    u.lp.assign(Lp.begin(), Lp.end());
+    u.lj.assign(Lj.begin(), Lj.end());
+    u.up.assign(Up.begin(), Up.end());
+    u.ui.assign(Ui.begin(), Ui.end());
+    u.pp.assign(P.begin(), P.end());
+    u.qq.assign(Q.begin(), Q.end());
+    u.Lp = u.lp.data();
+    u.Lj = u.lj.data();
+    u.Up = u.up.data();
+    u.Ui = u.ui.data();
+    u.P = u.pp.data();
+    u.Q = u.qq.data();
+    u.Lx = u.lx.data();
+    u.Ux = u.ux.data();
+    u.Rs = u.rs.data();
+    u.do_recip = rec;
+    auto Fu = eigmi::Factorization::from_umfpack(ctx, u);
+    MV8 R2 = Rc, Z2(n16, 8);
+    eigmi::matmul_inverse_tallskinny_blocked(Z2, Fu, R2);
+    EXPECT(std::memcmp(Z2.p.data(), Z.p.data(), Z.p.size() * 8) == 0);
+  }
+  bool threw2 = false;
+  try
+  {
+    MV8 a(n16 + 1, 8), b(n16 + 1, 8);
+    eigmi::matmul_inverse_tallskinny_blocked(a, F, b);
+  }
+  catch (const std::invalid_argument &)
+  {
+    threw2 = true;
+  }
+  EXPECT(threw2);
+
+  // 7) StandardInverse / GeneralizedInverse: the smallest eigenvalues of the 2-D Dirichlet
+  //    Laplacian (the reference's known answer, src/dune-eigensolver.cc:437-446)
+  std::vector<double> exact;
+  for (int i = 1; i <= N16; ++i)
+    for (int j = 1; j <= N16; ++j)
+    {
+      const double h = M_PI / (N16 + 1);
+      exact.push_back(4.0 * std::sin(i * h / 2) * std::sin(i * h / 2) + 4.0 * std::sin(j * h / 2) * std::sin(j * h / 2));
+    }
+  std::sort(exact.begin(), exact.end());
+  {
+    auto dA16 = eigmi::Matrix::upload(ctx, A16);
+    std::vector<double> ev(4);
+    std::vector<std::vector<double>> evv(4, std::vector<double>(n16));
+    eigmi::StandardInverse(dA16, 0.0, 1e-12, 2000, 4, ev, evv);
+    std::sort(ev.begin(), ev.end());
+    for (int i = 0; i < 4; ++i) EXPECT(std::fabs(ev[i] - exact[i]) < 1e-8);
+    // B = I on A's pattern
+    TestBCRS<1, 1> I16 = A16;
+    for (auto &row : I16.rows)
+      for (std::size_t q = 0; q < row.size(); ++q) row[q].second.a[0][0] = (row[q].first == (std::size_t)(&row - &I16.rows[0])) ? 1.0 : 0.0;
+    auto dI16 = eigmi::Matrix::upload(ctx, I16);
+    std::vector<double> gv;
+    std::vector<std::vector<double>> gvec;
+    eigmi::GeneralizedInverse(dA16, dI16, 0.5, 0.0, 1e-13, 3000, 4, gv, gvec);
+    EXPECT(gv.size() == 4 && gvec.size() == 4 && gvec[0].size() == n16);
+    std::sort(gv.begin(), gv.end());
+    for (int i = 0; i < 4; ++i) EXPECT(std::fabs(gv[i] - exact[i]) < 1e-8);
+
+    // 8) ARPACK++-style shift-invert operator and computeGenSymShiftInvertMinMagnitude
+    eigmi::ShiftInvertOperator sop(ctx, A16, dI16);  // sigma = 0: A - 0 B = A
+    std::vector<double> v(n16), wv(n16), Av(n16);
+    for (auto &e : v) e = nd(g);
+    sop.multMv(v.data(), wv.data());
+    dA16.mv_host(wv.data(), Av.data());
+    double r2 = 0.0;
+    for (std::size_t i = 0; i < n16; ++i) r2 = std::max(r2, std::fabs(Av[i] - v[i]));
+    EXPECT(r2 < 1e-11);
+    std::vector<std::vector<std::array<double, 1>>> xs(4, std::vector<std::array<double, 1>>(n16));
+    std::vector<double> lam(4);
+    eigmi::computeGenSymShiftInvertMinMagnitude(dA16, dI16, 1e-14, xs, lam, 0.0);
+    for (int i = 0; i < 4; ++i) EXPECT(std::fabs(lam[i] - exact[i]) < 1e-10);
+  }
 
   std::printf(failures ? "FAILED %d\n" : "ALL OK\n", failures);
   return failures ? 1 : 0;
