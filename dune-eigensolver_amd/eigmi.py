@@ -146,6 +146,9 @@ SIGNATURES = {
     "eig_gen_matrix": (_int, [_int, _int, _int, _vp, _vp, _vp]),
     "eig_gen_nnzb_rows": (_i64, [_int, _int, _i64, _i64]),
     "eig_gen_matrix_rows": (_int, [_int, _int, _i64, _i64, _vp, _vp, _vp]),
+    "eig_mm_read_info": (_int, [ctypes.c_char_p, _int, ctypes.POINTER(_i64), ctypes.POINTER(_i64), ctypes.POINTER(_i64)]),
+    "eig_mm_read": (_int, [ctypes.c_char_p, _int, _vp, _vp, _vp]),
+    "eig_mm_write": (_int, [ctypes.c_char_p, _i64, _i64, _int, _int, _vp, _vp, _vp, _int]),
     "eig_plan_window": (_int, [_i64, _i64, _int, _vp, _vp, _vp]),
     "eig_plan_halo": (_int, [_int, _int, _vp, _int, _i64, _vp, ctypes.POINTER(_int), _vp, ctypes.POINTER(_int)]),
 }
@@ -674,6 +677,33 @@ def gen_rows(kind, N, row_begin, nrows):
     if rc != EIG_OK:
         raise EigError(rc, "eig_gen_matrix_rows failed")
     return rp, c, v
+
+
+def mm_read(path, br=1):
+    """Matrix Market file -> (rowptr, col, vals, nb_cols) for Matrix.from_bcsr (eig_mm_read)."""
+    nr, nc, nz = _i64(0), _i64(0), _i64(0)
+    p = os.fsencode(path)
+    rc = lib.eig_mm_read_info(p, br, ctypes.byref(nr), ctypes.byref(nc), ctypes.byref(nz))
+    if rc != EIG_OK:
+        raise EigError(rc, f"eig_mm_read_info({path})")
+    rp = np.zeros(nr.value + 1, np.int64)
+    c = np.zeros(max(nz.value, 1), np.int32)
+    v = np.zeros(max(nz.value, 1) * br * br)
+    rc = lib.eig_mm_read(p, br, _np_ptr(rp), _np_ptr(c), _np_ptr(v))
+    if rc != EIG_OK:
+        raise EigError(rc, f"eig_mm_read({path})")
+    return rp, c[:nz.value], v[:nz.value * br * br], nc.value
+
+
+def mm_write(path, rowptr, col, vals, ncols_blocks=None, br=1, bc=1, symmetric=False):
+    rowptr = np.ascontiguousarray(rowptr, np.int64)
+    col = np.ascontiguousarray(col, np.int32)
+    vals = np.ascontiguousarray(vals, np.float64)
+    nb = rowptr.size - 1
+    rc = lib.eig_mm_write(os.fsencode(path), nb, nb if ncols_blocks is None else ncols_blocks, br, bc, _np_ptr(rowptr),
+                          _np_ptr(col), _np_ptr(vals), int(symmetric))
+    if rc != EIG_OK:
+        raise EigError(rc, f"eig_mm_write({path})")
 
 
 def row_partition(n, nranks, rank, align=1):

@@ -350,6 +350,18 @@ int64_t eig_gen_nnzb_rows(int kind, int N, int64_t row_begin, int64_t nrows);
 int eig_gen_matrix_rows(int kind, int N, int64_t row_begin, int64_t nrows, int64_t *rowptr,
                         int32_t *col, double *vals);
 
+/* ---------------------------------------------------------------- Matrix Market ---------- */
+/* Import / export of real matrices in Matrix Market coordinate form (the format
+ * Dune::storeMatrixMarket writes), host-only.  Read: real | integer | pattern, general | symmetric
+ * (mirrored), 1-based, duplicates summed, columns ascending; br > 1 groups the scalar entries into
+ * br x br blocks (row-major FieldMatrix layout) -> arrays for eig_mat_create_bcsr.  Sizes first
+ * with eig_mm_read_info (rowptr nb_rows+1, col nnzb, vals nnzb*br*br).  Write: every stored scalar
+ * of the blocks (symmetric != 0: the lower triangle only, header "symmetric"). */
+int eig_mm_read_info(const char *path, int br, int64_t *nb_rows, int64_t *nb_cols, int64_t *nnzb);
+int eig_mm_read(const char *path, int br, int64_t *rowptr, int32_t *col, double *vals);
+int eig_mm_write(const char *path, int64_t nb_rows, int64_t nb_cols, int br, int bc, const int64_t *rowptr,
+                 const int32_t *col, const double *vals, int symmetric);
+
 /* ---------------------------------------------------------------- partition planning ------ */
 /* Host-only helpers (no device needed) used by eig_mat_create_bcsr_dist; exported so the
  * partition / halo logic can be exercised and reused by other front ends.
