@@ -305,7 +305,9 @@ void sell_mv8(const eig_mat_s &A, i64 m, const double *X, double *Y, const doubl
   EIG_CHECK(A.R == 1, EIG_ERR_ARG, "multivector kernels need the R = 1 SELL image (unset EIGMI_SELL_R)");
   const int nblk = (int)(m / 8);
   const bool st = all_stencil(A);
-  const int kind = mv8_kernel_choice();
+  // one column block: the lane-per-row kernel reads each 64-B X row with one lane (measured 139
+  // vs 188 us for the m = 8 SpMM at 128^3); wider blocks: the configured mapping (quad default)
+  const int kind = nblk == 1 ? 0 : mv8_kernel_choice();
   if (kind == 0)
   {
     constexpr int MB = 2;
@@ -377,7 +379,7 @@ void sell_mv8(const eig_mat_s &A, i64 m, const double *X, double *Y, const doubl
 
 int sell_mv8_launches(i64 m)
 {
-  const int nblk = (int)(m / 8), per = mv8_kernel_choice() == 1 ? 4 : 2;
+  const int nblk = (int)(m / 8), per = (nblk > 1 && mv8_kernel_choice() == 1) ? 4 : 2;
   return (nblk + per - 1) / per;
 }
 

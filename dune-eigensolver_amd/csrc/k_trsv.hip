@@ -12,7 +12,7 @@
 // workgroup per 8-column block, one wave per column, 64-row blocks in sequence.  Per block:
 //   phase 1  lane r subtracts every entry of row bs + r whose column lies BEFORE the block (all
 //            already solved; a prefix of the row, its end usplit / lsplit precomputed), loads
-//            issued four at a time;
+//            issued eight at a time, x of the last three solved blocks read from an LDS ring;
 //   phase 2  the in-block entries sit in an LDS tile (tile[t][r], bit t of mask[r]); step t
 //            broadcasts row bs + t's final value with readlane and every lane r > t subtracts its
 //            entry in column bs + t -- a register wavefront, no barrier inside the block.
@@ -25,6 +25,7 @@ namespace eigmi {
 namespace {
 constexpr int kTB = 64;       // rows per block
 constexpr int kTThreads = 512;  // 8 waves = the 8 columns of a column block
+constexpr int kRing = 3;        // solved blocks whose x stays in LDS for phase 1
 
 __global__ __launch_bounds__(256) void k_perm_scale(i64 n, int nblk, const i32 *__restrict__ P,
                                                     const double *__restrict__ scale, const double *__restrict__ Qin,
@@ -56,6 +57,15 @@ __global__ __launch_bounds__(256) void k_perm_out(i64 n, int nblk, const i32 *__
   }
 }
 
+// Wave-uniform broadcast of lane t's double (two v_readlane_b32: scalar, no LDS crossbar).
+__device__ __forceinline__ double lane_bcast(double v, int t)
+{
+  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b & 0xffffffffull), t);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), t);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
 // LOWER = true: L solve (blocks top-down, unit diagonal); false: U solve (bottom-up, divide by d).
 // rhs and x are the column block's base pointers (n rows of 8); x may equal rhs (U solve).
 template <bool LOWER>
@@ -65,6 +75,9 @@ __global__ __launch_bounds__(kTThreads) void k_tsolve(i64 n, const i64 *__restri
 {
   __shared__ double tile[kTB][kTB];  // tile[t][r]: entry (row bs + r, column bs + t)
   __shared__ unsigned long long tmask[kTB];
+  // x of the kRing most recently solved blocks, per column: ring[slot][row][col]; a phase-1 entry
+  // whose column falls in one of them is read from LDS instead of global memory
+  __shared__ double ring[kRing][kTB][8];
   const int r = threadIdx.x & 63;
   const int c = threadIdx.x >> 6;  // column inside the block of 8
   const i64 cb = (i64)blockIdx.x * n * 8;
@@ -73,37 +86,67 @@ __global__ __launch_bounds__(kTThreads) void k_tsolve(i64 n, const i64 *__restri
   const i64 nblocks = (n + kTB - 1) / kTB;
   for (i64 bi = 0; bi < nblocks; ++bi)
   {
-    const i64 bs = (LOWER ? bi : nblocks - 1 - bi) * kTB;
+    const i64 blk = LOWER ? bi : nblocks - 1 - bi;
+    const i64 bs = blk * kTB;
     const i64 i = bs + r;
     const bool valid = i < n;
     double sum = valid ? R[i * 8 + c] : 0.0;
     i64 k = valid ? rp[i] : 0;
     const i64 ks = valid ? split[i] : 0, ke = valid ? rp[i + 1] : 0;
-    // phase 1: entries outside the block (columns before it for L, after it for U), in order
-    for (; k + 4 <= ks; k += 4)
+    // blocks [lo_blk, hi_blk] are in the ring (the kRing blocks solved last)
+    const i64 nring = bi < kRing ? bi : kRing;
+    const i64 lo_blk = LOWER ? blk - nring : blk + 1, hi_blk = LOWER ? blk - 1 : blk + nring;
+    // the block's own entries into the LDS tile: all 8 waves, wave c takes entries c, c+8, ... of
+    // each row (a band of 64 is one load round); the row masks are OR-ed together in LDS
+    if (c == 0) tmask[r] = 0ull;
+    __syncthreads();
     {
-      double a[4], xv[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
+      unsigned long long mm = 0;
+      for (i64 q0 = ks + c; q0 < ke; q0 += 64)
       {
-        a[u] = cv[k + u];
-        xv[u] = X[(i64)cj[k + u] * 8 + c];
-      }
+        double a[8];
+        i32 cc[8];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) sum -= a[u] * xv[u];
+        for (int u = 0; u < 8; ++u)
+        {
+          const i64 q = q0 + 8 * u;
+          const i64 qq = q < ke ? q : ke - 1;
+          a[u] = cv[qq];
+          cc[u] = cj[qq];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (q0 + 8 * u < ke)
+          {
+            const int t = (int)(cc[u] - bs);
+            tile[t][r] = a[u];
+            mm |= 1ull << t;
+          }
+      }
+      if (mm) atomicOr(&tmask[r], mm);
     }
-    for (; k < ks; ++k) sum -= cv[k] * X[(i64)cj[k] * 8 + c];
-    // the block's own entries into the LDS tile (wave 0; all 8 columns share the factor)
-    if (c == 0)
+    // phase 1: entries outside the block (columns before it for L, after it for U), in order;
+    // the loads of 32 entries are issued before the 32 dependent subtractions, x of the recent
+    // blocks comes from the LDS ring
+    auto xval = [&](i64 col) -> double {
+      const i64 cbk = col / kTB;
+      if (nring > 0 && cbk >= lo_blk && cbk <= hi_blk) return ring[cbk % kRing][col - cbk * kTB][c];
+      return X[col * 8 + c];
+    };
+    for (; k < ks; k += 32)
     {
-      unsigned long long m = 0;
-      for (i64 q = ks; q < ke; ++q)
+      double a[32];
+      i32 cc[32];
+#pragma unroll
+      for (int u = 0; u < 32; ++u)
       {
-        const int t = (int)(cj[q] - bs);
-        tile[t][r] = cv[q];
-        m |= 1ull << t;
+        const i64 q = k + u < ks ? k + u : ks - 1;
+        a[u] = cv[q];
+        cc[u] = cj[q];
       }
-      tmask[r] = m;
+#pragma unroll
+      for (int u = 0; u < 32; ++u)
+        if (k + u < ks) sum -= a[u] * xval(cc[u]);
     }
     __syncthreads();
     const unsigned long long m = tmask[r];
@@ -113,7 +156,7 @@ __global__ __launch_bounds__(kTThreads) void k_tsolve(i64 n, const i64 *__restri
     {
       for (int t = 0; t < nb; ++t)
       {
-        const double xt = __shfl(sum, t, 64);  // row bs + t is final
+        const double xt = lane_bcast(sum, t);  // row bs + t is final
         if (r == t) mine = xt;
         if (r > t && ((m >> t) & 1ull)) sum -= tile[t][r] * xt;
       }
@@ -122,13 +165,14 @@ __global__ __launch_bounds__(kTThreads) void k_tsolve(i64 n, const i64 *__restri
     {
       for (int t = nb - 1; t >= 0; --t)
       {
-        const double xt = __shfl(sum, t, 64) / diag[bs + t];  // x = (rhs - sum_j u x_j) / u_tt
+        const double xt = lane_bcast(sum, t) / diag[bs + t];  // x = (rhs - sum_j u x_j) / u_tt
         if (r == t) mine = xt;
         if (r < t && ((m >> t) & 1ull)) sum -= tile[t][r] * xt;
       }
     }
     if (valid) X[i * 8 + c] = mine;
-    __syncthreads();  // x of this block visible to the next; the tile free for reuse
+    ring[blk % kRing][r][c] = mine;
+    __syncthreads();  // ring / x of this block visible to the next; the tile free for reuse
   }
 }
 

@@ -6,6 +6,9 @@
   C2  3-D Poisson 128^3: SpMV (cache-resident: 217 MB < 256 MB MALL), Lanczos step, the b = 8
       SpMM, block Gram-Schmidt (m = 8, 32) and one StandardLargest iteration vs the CPU path
   C3  3-D Q1 elasticity 64^3, 3x3 blocks: BCSR SpMV against 76 nnzb + 4 (nb+1) + 48 nb bytes
+  INV inverse iteration with exported LU factors on the harness matrices:
+      matmul_inverse_tallskinny_blocked (m = 8), StandardInverse, GeneralizedInverse (GenEO pencil)
+      and computeGenSymShiftInvertMinMagnitude, GPU vs the oracle / scipy ARPACK on the host
   C5  generalised K x = lambda M x, P1 on the Kuhn split (15-pt shared pattern), block Lanczos
       k = 32: block steps/s with the phase split, the fused Chebyshev SpMM kernel against
       12 nnz + 4 (n+1) + (32 m + 8) n bytes per m-column launch (EIGMI_C5_N, default 256)
@@ -134,6 +137,48 @@ def c3(ctx):
          cpu_GBs=round(b / tc / 1e9, 2))
 
 
+def inv(ctx):
+    import scipy.sparse.linalg as ssl
+    N = int(os.environ.get("EIGMI_INV_N", "64"))
+    A = oracle.laplace2d(N)
+    n = A.n
+    lu = eigmi.LU.from_bcsr(ctx, A.rowptr, A.col, A.val)
+    f = oracle.LU(**lu.export())
+    lnz, unz = f.Lp[-1], f.Up[-1]
+    X = oracle.random_mv8(n, 8, 1)
+    din, dout = ctx.array(X), ctx.zeros(n * 8)
+    lu.inverse_mv8(8, din, dout)
+    ctx.sync()
+    reps = 20
+    tg, _ = wall(lambda: (lu.inverse_mv8(8, din, dout), ctx.sync()), reps)
+    tc, _ = wall(lambda: oracle.inverse_mv8(f, X, 8), 3)
+    emit(config=f"INV 2D Dirichlet {N}^2", op="matmul_inverse_tallskinny_blocked m=8 (RCM envelope factors)",
+         lnz=int(lnz), unz=int(unz), gpu_us=round(tg * 1e6, 1), cpu_us=round(tc * 1e6, 1), speedup=round(tc / tg, 2),
+         note="triangular solves are a row dependency chain: latency-bound, no bandwidth roofline")
+    M = eigmi.Matrix.from_bcsr(ctx, A.rowptr, A.col, A.val)
+    eigmi.standard_inverse(M, 0.0, 1e-10, 2000, 8, 123, want_evec=False)
+    tg, (ev, _, it) = wall(lambda: eigmi.standard_inverse(M, 0.0, 1e-10, 2000, 8, 123, want_evec=False))
+    tc, (rev, _, rit) = wall(lambda: oracle.standard_inverse(A, f, 0.0, 1e-10, 2000, 8, 123))
+    emit(config=f"INV 2D Dirichlet {N}^2", op="StandardInverse nev=8 tol=1e-10", gpu_s=round(tg, 4), cpu_s=round(tc, 4),
+         iterations=it, cpu_iterations=rit, speedup=round(tc / tg, 2), max_rel_diff=float(np.max(np.abs(ev - rev) / np.abs(rev))))
+    shift, reg = 1e-3, 0.0
+    An, Bp = oracle.laplace2d(N, "neumann"), oracle.laplace2d(N, "pu", overlap=3)
+    dA = eigmi.Matrix.from_bcsr(ctx, An.rowptr, An.col, An.val)
+    dB = eigmi.Matrix.from_bcsr(ctx, Bp.rowptr, Bp.col, Bp.val)
+    tg, (ev, _, it) = wall(lambda: eigmi.generalized_inverse(dA, dB, shift, reg, 1e-8, 4000, 8, 123, want_evec=False))
+    As = oracle.CSR(An.nrows, An.rowptr, An.col, An.val + shift * Bp.val)
+    fs = oracle.LU(**eigmi.LU.from_bcsr(None, As.rowptr, As.col, As.val).export())
+    tc, (rev, _, rit) = wall(lambda: oracle.generalized_inverse(An, Bp, fs, shift, reg, 1e-8, 4000, 8, 123))
+    emit(config=f"INV GenEO pencil {N}^2 (.cc:455-512)", op="GeneralizedInverse nev=8 tol=1e-8", gpu_s=round(tg, 4),
+         cpu_s=round(tc, 4), iterations=it, cpu_iterations=rit, speedup=round(tc / tg, 2))
+    tg, (ev, _, r) = wall(lambda: eigmi.shift_invert_solve(dA, 8, sigma=-shift, B=dB, tol=1e-10, want_evec=False))
+    As_, Bs_ = An.to_scipy(), Bp.to_scipy()
+    tc, w = wall(lambda: ssl.eigsh(As_, k=8, M=Bs_, sigma=-shift, which="LM", tol=1e-10, return_eigenvectors=False))
+    emit(config=f"INV GenEO pencil {N}^2 (.cc:455-512)", op="computeGenSymShiftInvertMinMagnitude nev=8 tol=1e-10",
+         gpu_s=round(tg, 4), scipy_arpack_cpu_s=round(tc, 4), restarts=r, speedup=round(tc / tg, 2),
+         max_abs_diff_vs_arpack=float(np.max(np.abs(np.sort(ev) - np.sort(w)))))
+
+
 def c5(ctx):
     N = int(os.environ.get("EIGMI_C5_N", "256"))
     steps, warm, b, degree = 3, 1, 32, 36
@@ -168,6 +213,6 @@ def c5(ctx):
 
 if __name__ == "__main__":
     ctx = eigmi.Context(0)
-    which = sys.argv[1:] or ["c1", "c2", "c3"]
+    which = sys.argv[1:] or ["c1", "c2", "c3", "inv"]
     for w in which:
         globals()[w](ctx)
