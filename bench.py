@@ -51,6 +51,62 @@ def cpu_baseline(N, rp, c, v, steps, gpu_alpha, fused):
     return steps / dt, dt, rel
 
 
+def cpu_replicas(N, steps, fused, threads):
+    """SURVEY 8(d) CPU baseline (ii): the reference's own parallel mode (src/dune-eigensolver.cc:
+    754-760, aggregate as at :292-294) -- `threads` independent replicas of the single-thread solve,
+    each on its own copy of the matrix and vectors, started together behind a barrier; value =
+    replicas x steps / wall time.  ctypes drops the GIL, so the replicas run in parallel."""
+    import threading
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # noqa: E402  (checker / baseline only)
+    n = N ** 3
+    nnz = int(oracle.lib.orc_poisson3d_nnz(N))
+    bar = threading.Barrier(threads + 1)
+    err = []
+
+    def replica():
+        try:
+            rp, c, v = np.zeros(n + 1, np.int64), np.zeros(nnz, np.int32), np.zeros(nnz)
+            oracle.lib.orc_poisson3d(N, rp, c, v)
+            u0, u1, u2 = np.zeros(n), np.zeros(n), np.zeros(n)
+            oracle.lib.orc_random_vec(n, 123, u0)
+            alpha, beta = np.zeros(steps), np.zeros(steps + 1)
+        except MemoryError as e:  # pragma: no cover
+            err.append(e)
+        bar.wait()  # all replicas built
+        bar.wait()  # go
+        if not err:
+            if fused:
+                oracle.lib.orc_lanczos_fused(n, rp, c, v, steps, u0, alpha, beta)
+            else:
+                oracle.lib.orc_lanczos_rotating(n, rp, c, v, steps, u0, u1, u2, alpha, beta)
+        bar.wait()  # done
+
+    ts = [threading.Thread(target=replica) for _ in range(threads)]
+    for t in ts:
+        t.start()
+    bar.wait()
+    t0 = time.perf_counter()
+    bar.wait()
+    bar.wait()
+    dt = time.perf_counter() - t0
+    for t in ts:
+        t.join()
+    if err:
+        return None, dt
+    return threads * steps / dt, dt
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
 def committed_traffic(kernel, N, world):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
     (profiles/<tag>_pmc_summary.json, FETCH_SIZE x2 + WRITE_SIZE, KiB -> B; tools/profile_round.sh)
@@ -81,6 +137,9 @@ def main():
     ap.add_argument("--N", type=int, default=256, help="grid points per axis (n = N^3)")
     ap.add_argument("--cpu-steps", type=int, default=160, help="Lanczos steps of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-replicas", type=int, default=None,
+                    help="replicas of the CPU baseline's parallel mode (default: usable cores, at most 16; 0 = skip)")
+    ap.add_argument("--cpu-replica-steps", type=int, default=40)
     ap.add_argument("--no-kernel-events", action="store_true", help="skip per-kernel HIP events")
     ap.add_argument("--variant", choices=["fused", "classic"], default="fused",
                     help="fused: one kernel + one 3-value allreduce per step (EIG_LANCZOS_FUSED); "
@@ -201,7 +260,16 @@ def main():
         out["cpu_baseline"] = {"value": round(cv, 4), "unit": "iters/s", "cores": 1, "kind": "port",
                                "sample": f"{args.cpu_steps} Lanczos steps on the same {N}^3 matrix and start "
                                          f"vector, oracle/oracle.cc single thread ({cdt:.1f} s)",
-                               "alpha_max_rel_diff_vs_gpu": rel}
+                               "alpha_max_rel_diff_vs_gpu": rel, "cpu_model": cpu_model()}
+        P = args.cpu_replicas
+        if P is None:
+            P = min(16, len(os.sched_getaffinity(0)))
+        if P > 0:
+            pv, pdt = cpu_replicas(N, args.cpu_replica_steps, fused, P)
+            out["cpu_baseline"]["replicas"] = {
+                "value": round(pv, 4) if pv else None, "unit": "iters/s", "cores": P,
+                "sample": f"{P} concurrent replicas x {args.cpu_replica_steps} steps, each on its own "
+                          f"{N}^3 matrix (the reference's numthreads mode, .cc:754-760) ({pdt:.1f} s)"}
     if rank == 0:
         print(json.dumps(out), flush=True)
     ws.close()

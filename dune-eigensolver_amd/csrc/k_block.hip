@@ -276,6 +276,135 @@ __global__ __launch_bounds__(64 * W) void k_sell_mv8q(i64 nrows, i64 nslices, co
   }
 }
 
+// Grouped-quad mapping: a wave owns a whole 64-row slice; lane l owns column pair cp = l & 3 of
+// the four rows (l >> 2) + 16 h, h = 0..3, of every column block, so each 16-B gather instruction
+// of the wave reads 16 consecutive X rows (1 KiB contiguous for a stencil offset: whole cache
+// lines, unlike the lane-per-row mapping whose instructions touch 64 rows at a 64-B stride), and
+// the loop overhead, mask byte and stencil offsets are shared by the lane's 4 rows.  Units of 4
+// slices (4 waves per workgroup) on the XCD plane-slab schedule of k_sell_mv8q.  Per column, the
+// row sum runs over the stored entries in ascending-column order (bitwise the reference for kStore).
+template <int MB, int U, bool STENCIL, int EPI>
+__global__ __launch_bounds__(256) void k_sell_mv8g(i64 nrows, i64 nslices, const i64 *__restrict__ slice_ptr,
+                                                   const double *__restrict__ val, const i32 *__restrict__ col,
+                                                   const i32 *__restrict__ st_delta, const uint8_t *__restrict__ st_mask,
+                                                   const double *__restrict__ X, double *__restrict__ Y, i64 ld, i64 own,
+                                                   int b0, const double *__restrict__ Bv,
+                                                   const double *__restrict__ dinv, double omega, double gamma, i64 per)
+{
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int cp = lane & 3, rq = lane >> 2;
+  const i64 nunits = (nslices + 3) / 4;
+  const i64 seg = per;
+  const int xcd = blockIdx.x & 7;
+  const i64 nloc = gridDim.x >> 3;
+  const double *Xc = X + (i64)b0 * ld * 8 + 2 * cp;
+  for (i64 t = blockIdx.x >> 3;; t += nloc)
+  {
+    const i64 pl = t / seg;
+    const i64 un = pl * 8 * seg + xcd * seg + (t - pl * seg);
+    if (pl * 8 * seg >= nunits) break;
+    const i64 s = un * 4 + wave;
+    if (un >= nunits || s >= nslices) continue;
+    const i64 base = slice_ptr[s];
+    const int width = (int)((slice_ptr[s + 1] - base) >> 6);
+    unsigned m[4] = {0u, 0u, 0u, 0u};
+    if (STENCIL)
+    {
+#pragma unroll
+      for (int h = 0; h < 4; ++h) m[h] = st_mask[s * 64 + rq + 16 * h];
+    }
+    double2 acc[4][MB];
+#pragma unroll
+    for (int h = 0; h < 4; ++h)
+#pragma unroll
+      for (int q = 0; q < MB; ++q) acc[h][q] = make_double2(0.0, 0.0);
+    for (int k0 = 0; k0 < width; k0 += U)
+    {
+      double a[U][4];
+      i64 c[U][4];
+      bool okk[U][4];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+      {
+        const int k = k0 + u < width ? k0 + u : width - 1;
+        i64 dl = 0;
+        if (STENCIL) dl = st_delta[8 * s + k];
+#pragma unroll
+        for (int h = 0; h < 4; ++h)
+        {
+          const int ri = rq + 16 * h;
+          const i64 r = s * 64 + ri;
+          a[u][h] = __builtin_nontemporal_load(val + base + k * 64 + ri);
+          if (STENCIL)
+          {
+            okk[u][h] = (k0 + u < width) && ((m[h] >> (k0 + u)) & 1u);
+            c[u][h] = own + r + (okk[u][h] ? dl : 0);
+          }
+          else
+          {
+            const i32 ci = __builtin_nontemporal_load(col + base + k * 64 + ri);
+            okk[u][h] = (k0 + u < width) && ci >= 0;
+            c[u][h] = okk[u][h] ? (i64)ci : own + r;
+          }
+        }
+      }
+      double2 xv[U][4][MB];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int h = 0; h < 4; ++h)
+#pragma unroll
+          for (int q = 0; q < MB; ++q)
+            xv[u][h][q] = *reinterpret_cast<const double2 *>(Xc + ((i64)q * ld + c[u][h]) * 8);
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int h = 0; h < 4; ++h)
+#pragma unroll
+          for (int q = 0; q < MB; ++q)
+          {
+            if (EPI == kStore)
+            {
+              const double tx = acc[h][q].x + a[u][h] * xv[u][h][q].x, ty = acc[h][q].y + a[u][h] * xv[u][h][q].y;
+              acc[h][q].x = okk[u][h] ? tx : acc[h][q].x;
+              acc[h][q].y = okk[u][h] ? ty : acc[h][q].y;
+            }
+            else
+            {
+              const double au = okk[u][h] ? a[u][h] : 0.0;
+              acc[h][q].x = __builtin_fma(au, xv[u][h][q].x, acc[h][q].x);
+              acc[h][q].y = __builtin_fma(au, xv[u][h][q].y, acc[h][q].y);
+            }
+          }
+    }
+#pragma unroll
+    for (int h = 0; h < 4; ++h)
+    {
+      const i64 r = s * 64 + rq + 16 * h;
+      if (r >= nrows) continue;
+      double di = 0.0;
+      if (EPI == kCheb) di = __builtin_nontemporal_load(dinv + r);
+#pragma unroll
+      for (int q = 0; q < MB; ++q)
+      {
+        const i64 at = ((i64)(b0 + q) * ld + own + r) * 8 + 2 * cp;
+        double *yr = Y + at;
+        double o0 = acc[h][q].x, o1 = acc[h][q].y;
+        if (EPI == kCheb)
+        {
+          const double2 xk = *reinterpret_cast<const double2 *>(X + at);
+          const dv2 bb = __builtin_nontemporal_load(reinterpret_cast<const dv2 *>(Bv + at));
+          const dv2 xo = __builtin_nontemporal_load(reinterpret_cast<const dv2 *>(yr));
+          const double gd = gamma * di;
+          o0 = omega * (xk.x + gd * (bb.x - o0) - xo.x) + xo.x;
+          o1 = omega * (xk.y + gd * (bb.y - o1) - xo.y) + xo.y;
+        }
+        __builtin_nontemporal_store(dv2{o0, o1}, reinterpret_cast<dv2 *>(yr));
+      }
+    }
+  }
+}
+
 namespace {
 bool all_stencil(const eig_mat_s &A) { return A.n_stencil_slices == A.nslices && A.n_stencil_slices > 0; }
 
@@ -283,14 +412,28 @@ bool all_stencil(const eig_mat_s &A) { return A.n_stencil_slices == A.nslices &&
 
 // Kernel mapping for the window-layout SpMM / Chebyshev step: EIGMI_MV8_KERNEL = rows (lane per
 // row, 16 columns per matrix pass), quad (4 lanes per row, 32 columns per pass; default) or quad2
-// (4 lanes per row, 16 columns per pass).
+// (4 lanes per row, 16 columns per pass); grp / grp2 (k_sell_mv8g, 4 / 2 column blocks per pass).
+// One column block (m = 8): EIGMI_MV8_KERNEL1 = rows (k_sell_mv8) or grp (k_sell_mv8g, default:
+// 119 vs 131 us for the 7-point SpMM at 128^3, 221 vs 241 us on the 15-point P1 mass matrix).
 int mv8_kernel_choice()
 {
   static int v = [] {
     const char *e = std::getenv("EIGMI_MV8_KERNEL");
     if (e && std::string(e) == "rows") return 0;
     if (e && std::string(e) == "quad2") return 2;
+    if (e && std::string(e) == "grp") return 4;
+    if (e && std::string(e) == "grp2") return 5;
     return 1;
+  }();
+  return v;
+}
+
+static int mv8_single_choice()
+{
+  static int v = [] {
+    const char *e = std::getenv("EIGMI_MV8_KERNEL1");
+    if (e && std::string(e) == "rows") return 0;
+    return 4;
   }();
   return v;
 }
@@ -305,10 +448,47 @@ void sell_mv8(const eig_mat_s &A, i64 m, const double *X, double *Y, const doubl
   EIG_CHECK(A.R == 1, EIG_ERR_ARG, "multivector kernels need the R = 1 SELL image (unset EIGMI_SELL_R)");
   const int nblk = (int)(m / 8);
   const bool st = all_stencil(A);
-  // one column block: the lane-per-row kernel reads each 64-B X row with one lane (measured 139
-  // vs 188 us for the m = 8 SpMM at 128^3); wider blocks: the configured mapping (quad default)
-  const int kind = nblk == 1 ? 0 : mv8_kernel_choice();
-  if (kind == 0)
+  // one column block: grouped quad (k_sell_mv8g, MB = 1); wider blocks: the configured mapping
+  // (quad default: at m = 32 it beats grp / grp2, tools/spmm_sweep.py)
+  const int kind = nblk == 1 ? mv8_single_choice() : mv8_kernel_choice();
+  if (kind == 4 || kind == 5)
+  {
+    // grouped quad: MB = 1 (m = 8), 2 (grp2) or 4 (grp) column blocks per matrix pass
+    const int MBg = nblk == 1 ? 1 : (kind == 5 ? 2 : 4);
+    i64 gcap = (i64)A.ctx->num_cu * 4 / 2;
+    if (const char *e = std::getenv("EIGMI_MV8_GX")) gcap = std::max<i64>(8, std::atoll(e));
+    const i64 nunits = (A.nslices + 3) / 4;
+    const i64 gx = std::max<i64>(8, std::min<i64>(gcap, (nunits + 7) / 8 * 8) / 8 * 8);
+    const i64 prow = A.bandwidth > 0 ? A.bandwidth : std::max<i64>(1, A.nb_rows);
+    const i64 per = std::max<i64>(1, (prow + 8 * 256 - 1) / (8 * 256));
+    for (int b0 = 0; b0 < nblk; b0 += MBg)
+    {
+      const int nb = nblk - b0 < MBg ? nblk - b0 : MBg;
+#define EIGMI_GRP(MBV, STV)                                                                                      \
+  hipLaunchKernelGGL((k_sell_mv8g<MBV, 2, STV, EPI>), dim3((unsigned)gx), dim3(256), 0, s, A.nb_rows, A.nslices, \
+                     A.slice_ptr, A.val, A.col, A.st_delta, A.st_mask, X, Y, A.window, A.own_offset, b0, Bv, dinv, \
+                     omega, gamma, per)
+#define EIGMI_GRP_NB(STV)             \
+  switch (nb)                         \
+  {                                   \
+    case 1: EIGMI_GRP(1, STV); break; \
+    case 2: EIGMI_GRP(2, STV); break; \
+    case 3: EIGMI_GRP(3, STV); break; \
+    default: EIGMI_GRP(4, STV); break; \
+  }
+      if (st)
+      {
+        EIGMI_GRP_NB(true)
+      }
+      else
+      {
+        EIGMI_GRP_NB(false)
+      }
+#undef EIGMI_GRP_NB
+#undef EIGMI_GRP
+    }
+  }
+  else if (kind == 0)
   {
     constexpr int MB = 2;
     const int gx = grid_cap(A.nslices, 4, kStreamBlocks);
@@ -379,7 +559,9 @@ void sell_mv8(const eig_mat_s &A, i64 m, const double *X, double *Y, const doubl
 
 int sell_mv8_launches(i64 m)
 {
-  const int nblk = (int)(m / 8), per = (nblk > 1 && mv8_kernel_choice() == 1) ? 4 : 2;
+  const int nblk = (int)(m / 8);
+  if (nblk <= 1) return nblk;
+  const int kind = mv8_kernel_choice(), per = (kind == 1 || kind == 4) ? 4 : 2;
   return (nblk + per - 1) / per;
 }
 

@@ -49,6 +49,35 @@ def test_spmm_bitwise(ctx, m):
     assert np.array_equal(Y.get(), oracle.spmm_mv8(A, Qh, m))
 
 
+def _ragged(n=1000, seed=5):
+    """Irregular rows (0 to ~30 entries, n not a multiple of 64, an explicitly stored zero):
+    the explicit-column SELL image with padding."""
+    import scipy.sparse as sp
+    rng = np.random.default_rng(seed)
+    S = sp.random(n, n, density=0.012, random_state=rng, format="csr")
+    S = (S + sp.diags(rng.uniform(1, 2, n))).tocsr()
+    S.sort_indices()
+    S.data[3] = 0.0
+    return oracle.CSR(n, S.indptr.astype(np.int64), S.indices.astype(np.int32), S.data.copy())
+
+
+@pytest.mark.parametrize("m", [8, 16, 40])
+@pytest.mark.parametrize("which", ["ragged", "p1mass"])
+def test_spmm_bitwise_explicit_columns(ctx, m, which):
+    """Matrices without a stencil image (every mapping: the m = 8 single-block kernel and the
+    multi-block one) against the restated matmul_sparse_tallskinny_blocked, bitwise."""
+    if which == "ragged":
+        A = _ragged()
+    else:
+        K, Mm = oracle.p1_kuhn(7)
+        A = oracle.CSR(Mm.shape[0], Mm.indptr.astype(np.int64), Mm.indices.astype(np.int32), Mm.data.copy())
+    M = eigmi.Matrix.from_bcsr(ctx, A.rowptr, A.col, A.val)
+    Qh = oracle.random_mv8(A.n, m, 11)
+    Q, Y = ctx.array(Qh), ctx.zeros(A.n * m)
+    eigmi.spmm_mv8(M, m, Q, Y)
+    assert np.array_equal(Y.get(), oracle.spmm_mv8(A, Qh, m))
+
+
 def test_spmm_rejects_blocks_and_bad_m(ctx):
     A = oracle.q1elast(3)
     M = eigmi.Matrix.from_bcsr(ctx, A.rowptr, A.col, A.val, 3, 3)

@@ -107,14 +107,28 @@ def c2(ctx):
         emit(config="C2 3D Poisson 128^3", op=f"orthonormalize_blocked (MGS) m={m}", gpu_ms=round(tg * 1e3, 3),
              cpu_ms=round(tc * 1e3, 1), model_bytes=ob, model_GBs=round(ob / tg / 1e9, 1),
              model_GFLOPs=round(of / tg / 1e9, 1), speedup=round(tc / tg, 1))
-    # one StandardLargest iteration (SpMM + GS + SpMM + dots) at m = 8
+    # one StandardLargest iteration at m = 8, timed as the driver runs it (eigensolver.hh:78-96:
+    # SpMM, orthonormalize_blocked, SpMM, diagonal dots copied to the host for the stopping test);
+    # differencing whole solves of different lengths drowned the 10-iteration difference in the
+    # host generation of the random start block
+    m = 8
+    Q1, Q2, dp = ctx.array(oracle.random_mv8(n, m, 1)), ctx.zeros(n * m), ctx.zeros(m)
+    eigmi.orthonormalize_mv8(ctx, n, m, Q1)
+
+    def iteration():
+        eigmi.spmm_mv8(M, m, Q1, Q2)
+        eigmi.orthonormalize_mv8(ctx, n, m, Q2)
+        eigmi.spmm_mv8(M, m, Q2, Q1)
+        eigmi.dot_diag_mv8(ctx, n, m, Q2, Q1, dp)
+        dp.get()
+    iteration()
+    ctx.sync()
+    tg, _ = wall(iteration, 20)
     _, (_, _, it) = wall(lambda: eigmi.standard_largest(M, 0.0, 0.0, 2, 8, 123, want_evec=False))
-    tg1, _ = wall(lambda: eigmi.standard_largest(M, 0.0, 0.0, 2, 8, 123, want_evec=False))
-    tg11, _ = wall(lambda: eigmi.standard_largest(M, 0.0, 0.0, 12, 8, 123, want_evec=False))
     tc1, _ = wall(lambda: oracle.standard_largest(A, 0.0, 0.0, 2, 8, 123))
     tc2, _ = wall(lambda: oracle.standard_largest(A, 0.0, 0.0, 3, 8, 123))
-    emit(config="C2 3D Poisson 128^3", op="StandardLargest iteration m=8", gpu_ms_per_iter=round((tg11 - tg1) / 10 * 1e3, 3),
-         cpu_ms_per_iter=round((tc2 - tc1) * 1e3, 1), speedup=round((tc2 - tc1) / ((tg11 - tg1) / 10), 1))
+    emit(config="C2 3D Poisson 128^3", op="StandardLargest iteration m=8", gpu_ms_per_iter=round(tg * 1e3, 3),
+         cpu_ms_per_iter=round((tc2 - tc1) * 1e3, 1), speedup=round((tc2 - tc1) / tg, 1))
 
 
 def c3(ctx):

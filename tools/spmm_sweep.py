@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Sweep the window-layout SpMM / fused Chebyshev kernel mappings (EIGMI_MV8_KERNEL = rows | quad |
-quad2) on the C2 Poisson (7-pt, stencil image) and C5 P1 mass (15-pt, explicit columns) matrices.
+quad2; grp | grp2; one column block: rows1 | grp1) on the C2 Poisson (7-pt, stencil image) and C5 P1 mass (15-pt, explicit columns) matrices.
 Each mapping runs in its own child process (the choice is read once per process).  Prints one
 JSON line per (mapping, matrix, op) with the average launch-sequence time and algorithmic GB/s:
   SpMM m columns:  12 nnz + 4 (n+1) + 16 m n        Chebyshev step: 12 nnz + 4 (n+1) + 32 m n + 8 n
@@ -61,11 +61,15 @@ if __name__ == "__main__":
         sys.exit(0)
     N = int(os.environ.get("SWEEP_N", "160"))
     # SWEEP_CASES="quad:2048 quad:1024 quad2:4096" -- mapping[:workgroups in flight (EIGMI_MV8_GX)]
+    # single-block (m = 8) mappings: rows1 / grp1 (EIGMI_MV8_KERNEL1); SWEEP_M="8 32"
     cases = os.environ.get("SWEEP_CASES", "rows quad quad2").split()
-    for m in (32,):
+    for m in [int(x) for x in os.environ.get("SWEEP_M", "32").split()]:
         for case in cases:
             kind, _, gx = case.partition(":")
             env = dict(os.environ, EIGMI_MV8_KERNEL=kind)
+            k1 = {"rows1": "rows", "grp1": "grp"}.get(kind)
+            if k1:
+                env["EIGMI_MV8_KERNEL1"] = k1
             if gx:
                 env["EIGMI_MV8_GX"] = gx
             r = subprocess.run([sys.executable, __file__, "child", case, str(N), str(m)], env=env, timeout=600)
