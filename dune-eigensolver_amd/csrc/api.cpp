@@ -5,6 +5,8 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
+#include <mutex>
 #include <random>
 #include <thread>
 
@@ -710,6 +712,133 @@ void build_sell(eig_mat_s &A, i64 nb, const int64_t *rowptr, const int32_t *col,
   A.device_bytes = (ns + 1) * 8 + total * 4 + total * bb * 8 + (A.n_stencil_slices ? ns * (36 + C) : 0);
 }
 
+bool sym_enabled()
+{
+  const char *e = std::getenv("EIGMI_SYM");
+  return !(e && e[0] == '0');
+}
+
+// Symmetric band image (internal.h, eig_mat_s::sym_*) next to the SELL image, for square 1x1
+// matrices with at most kSymMaxOff distinct offsets whose stored mirror pairs are bitwise equal
+// and whose band arrays are smaller than the SELL values.  Pass 1 (rows in parallel) stores each
+// row's entries at d >= 0 in slot [j(d)][w]; pass 2 stores the entries at d < 0 in slot
+// [j(-d)][w + d], which only the mirror (row w + d, offset -d) of pass 1 can also own -- a set
+// slot with different bits rejects the image.  Ghost rows below the owned range (distributed)
+// get their slots from the owned rows' lower entries alone.  Silently skipped when not applicable.
+void build_sym(eig_mat_s &A, i64 nb, const int64_t *rowptr, const int32_t *col, const double *vals)
+{
+  if (A.br != 1 || A.bc != 1 || A.R != 1 || !sym_enabled() || nb == 0) return;
+  if (A.nb_cols != A.nb_rows_global) return;
+  const i64 row0 = A.row_begin;
+  // distinct offsets (per thread, then merged)
+  std::vector<i64> offs;
+  {
+    std::mutex mu;
+    bool ok = true;
+    parallel_slices(nb, [&](i64 r0, i64 r1) {
+      std::vector<i64> mine;
+      for (i64 r = r0; r < r1 && mine.size() <= (size_t)kSymMaxOff; ++r)
+        for (i64 p = rowptr[r]; p < rowptr[r + 1]; ++p)
+        {
+          const i64 d = (i64)col[p] - (row0 + r);
+          if (std::find(mine.begin(), mine.end(), d) == mine.end()) mine.push_back(d);
+        }
+      std::lock_guard<std::mutex> lk(mu);
+      if (mine.size() > (size_t)kSymMaxOff) ok = false;
+      for (i64 d : mine)
+        if (std::find(offs.begin(), offs.end(), d) == offs.end()) offs.push_back(d);
+    });
+    if (!ok || offs.size() > (size_t)kSymMaxOff || offs.empty()) return;
+  }
+  std::sort(offs.begin(), offs.end());
+  std::vector<i64> ups;
+  for (i64 d : offs)
+  {
+    if (d < INT32_MIN || d > INT32_MAX) return;
+    const i64 a = std::llabs(d);
+    if (std::find(ups.begin(), ups.end(), a) == ups.end()) ups.push_back(a);
+  }
+  std::sort(ups.begin(), ups.end());
+  const int nd = (int)offs.size(), nup = (int)ups.size();
+  const i64 ns = A.nslices, own = A.own_offset;
+  const i64 ld = ((std::max<i64>(A.window, own + ns * 64) + 63) / 64) * 64;
+  // only worth it when the band arrays are smaller than the SELL values the kernels would stream
+  if ((double)nup * (double)ld > 0.9 * (double)A.nnzb_padded) return;
+  auto jof = [&](i64 a) { return (int)(std::lower_bound(ups.begin(), ups.end(), a) - ups.begin()); };
+  std::vector<int> kj(nd);
+  for (int k = 0; k < nd; ++k) kj[k] = jof(std::llabs(offs[k]));
+  std::vector<double> U((size_t)nup * ld, 0.0);
+  std::vector<uint8_t> set((size_t)nup * ld, 0);
+  const int mb = nd <= 8 ? 1 : 4;
+  std::vector<uint8_t> m8(mb == 1 ? (size_t)ns * 64 : 0, 0);
+  std::vector<uint32_t> m32(mb == 4 ? (size_t)ns * 64 : 0, 0);
+  std::atomic<bool> good{true};
+  auto kof = [&](i64 d) { return (int)(std::lower_bound(offs.begin(), offs.end(), d) - offs.begin()); };
+  parallel_slices(nb, [&](i64 r0, i64 r1) {
+    for (i64 r = r0; r < r1; ++r)
+    {
+      uint32_t m = 0;
+      for (i64 p = rowptr[r]; p < rowptr[r + 1]; ++p)
+      {
+        const i64 d = (i64)col[p] - (row0 + r);
+        const int k = kof(d);
+        m |= 1u << k;
+        if (d >= 0)
+        {
+          const size_t q = (size_t)kj[k] * ld + (size_t)(own + r);
+          U[q] = vals[p];
+          set[q] = 1;
+        }
+      }
+      if (mb == 1) m8[r] = (uint8_t)m;
+      else m32[r] = m;
+    }
+  });
+  parallel_slices(nb, [&](i64 r0, i64 r1) {
+    for (i64 r = r0; r < r1 && good.load(std::memory_order_relaxed); ++r)
+      for (i64 p = rowptr[r]; p < rowptr[r + 1]; ++p)
+      {
+        const i64 d = (i64)col[p] - (row0 + r);
+        if (d >= 0) break;  // ascending columns: the rest are upper entries
+        const i64 x = own + r + d;
+        if (x < 0 || x >= ld)
+        {
+          good = false;
+          break;
+        }
+        const size_t q = (size_t)kj[kof(d)] * ld + (size_t)x;
+        if (set[q])
+        {
+          if (std::memcmp(&U[q], &vals[p], sizeof(double)) != 0)
+          {
+            good = false;
+            break;
+          }
+        }
+        else
+          U[q] = vals[p];
+      }
+  });
+  if (!good) return;
+  hipStream_t s = A.ctx->stream;
+  A.sym_val = dev_alloc<double>((size_t)nup * ld);
+  A.sym_mask = mb == 1 ? (void *)dev_alloc<uint8_t>(ns * 64) : (void *)dev_alloc<uint32_t>(ns * 64);
+  EIG_HIP(hipMemcpyAsync(A.sym_val, U.data(), (size_t)nup * ld * sizeof(double), hipMemcpyHostToDevice, s));
+  EIG_HIP(hipMemcpyAsync(A.sym_mask, mb == 1 ? (const void *)m8.data() : (const void *)m32.data(), ns * 64 * mb,
+                         hipMemcpyHostToDevice, s));
+  EIG_HIP(hipStreamSynchronize(s));
+  A.sym_mask_bytes = mb;
+  A.sym_nd = nd;
+  A.sym_nup = nup;
+  A.sym_ld = ld;
+  for (int k = 0; k < nd; ++k)
+  {
+    A.sym_off[k] = (i32)offs[k];
+    A.sym_dj[k] = kj[k];
+  }
+  A.device_bytes += (i64)nup * ld * 8 + ns * 64 * mb;
+}
+
 void validate_csr(i64 nb, i64 ncols, const int64_t *rowptr, const int32_t *col)
 {
   EIG_CHECK(rowptr[0] == 0, EIG_ERR_ARG, "rowptr[0] must be 0");
@@ -734,6 +863,8 @@ void destroy_mat(eig_mat_s *A)
   if (A->st_delta) (void)hipFree(A->st_delta);
   if (A->st_mask) (void)hipFree(A->st_mask);
   if (A->slice_list) (void)hipFree(A->slice_list);
+  if (A->sym_val) (void)hipFree(A->sym_val);
+  if (A->sym_mask) (void)hipFree(A->sym_mask);
   delete A;
 }
 
@@ -764,6 +895,7 @@ extern "C" int eig_mat_create_bcsr(eig_ctx_t ctx, int64_t nb_rows, int64_t nb_co
     try
     {
       build_sell(*A, nb_rows, rowptr, col, vals, 0);
+      build_sym(*A, nb_rows, rowptr, col, vals);
     }
     catch (...)
     {
@@ -808,6 +940,7 @@ extern "C" int eig_mat_create_bcsr_dist(eig_ctx_t ctx, int64_t nb_rows_global, i
     try
     {
       build_sell(*A, nb_local, rowptr, col, vals, wb_blk);
+      build_sym(*A, nb_local, rowptr, col, vals);
       // --- halo plan: allgather (row_begin, nb_local, cmin, cmax) of every rank ---
       std::vector<i64> mine = {row_begin, nb_local, cmin, cmax};
       std::vector<i64> all(4 * (size_t)P, 0);
@@ -939,6 +1072,7 @@ extern "C" int eig_mat_get_info(eig_mat_t A, eig_mat_info *info)
     info->device_bytes = A->device_bytes;
     info->stencil_slices = A->n_stencil_slices;
     info->rows_per_lane = A->R;
+    info->sym_offsets = A->sym_val ? A->sym_nd : 0;
   });
 }
 

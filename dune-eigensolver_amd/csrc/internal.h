@@ -52,6 +52,7 @@ constexpr int kStreamThreads = 256;
 constexpr int kMaxRedBlocks = 2048;
 constexpr int kMaxRedVals = 256;   // values reduced by one launch (e.g. a 16x16 Gram tile)
 constexpr int kNumTickets = 64;
+constexpr int kSymMaxOff = 32;   // offsets of the symmetric band image (eig_mat_s::sym_*)
 // One logical ticket = 8 shard counters (workgroup id mod 8, i.e. one per XCD group) + 1 top
 // counter, each on its own 128-B line: a single contended word serialises at ~88 agent atomics
 // per microsecond (MI355X_MICROARCH price list, row "dequeue"), i.e. ~23 us for 2048 workgroups.
@@ -172,6 +173,21 @@ struct eig_mat_s {
   eigmi::i32 *st_delta = nullptr;   // 8 * nslices
   uint8_t *st_mask = nullptr;       // nslices * C
   eigmi::i64 n_stencil_slices = 0;
+  // Symmetric band image (1x1 blocks, R = 1; api.cpp build_sym): when every row draws its columns
+  // from one global set of at most kSymMaxOff offsets d = col - row and every stored pair
+  // (r, r+d) / (r+d, r) is bitwise equal, the values live once, in nup = |{|d|}| window-indexed
+  // arrays: sym_val[j * sym_ld + x] = a(x, x + p_j) = a(x + p_j, x) for the j-th non-negative
+  // offset p_j.  Row w reads offset d >= 0 at [j(d)][w] and d < 0 at [j(-d)][w + d] (the mirrored
+  // upper entry); the per-row mask (bit k = row stores off[k], u8 when nd <= 8, else u32) gates
+  // the accumulation, so each row still sums exactly its own entries in ascending-column order.
+  // The SELL image above stays (SpMM, block and download paths use it).
+  double *sym_val = nullptr;
+  void *sym_mask = nullptr;         // nslices * 64 entries of sym_mask_bytes
+  int sym_mask_bytes = 0;
+  int sym_nd = 0, sym_nup = 0;
+  eigmi::i64 sym_ld = 0;
+  eigmi::i32 sym_off[eigmi::kSymMaxOff] = {};      // ascending offsets (ISTL column order)
+  eigmi::i32 sym_dj[eigmi::kSymMaxOff] = {};       // array index of |sym_off[k]|
   eigmi::i64 *slice_ptr = nullptr;  // nslices + 1
   eigmi::i32 *col = nullptr;        // nnzb_padded, window-local block columns, -1 = padding
   double *val = nullptr;            // nnzb_padded * br * bc

@@ -179,12 +179,35 @@ __global__ void k_shift_diag(i64 nbrows, i64 own_blk, const i64 *__restrict__ sl
       for (int d = 0; d < nd; ++d) val[(base + (i64)k * C) * bb + (i64)(d * bc + d) * C + l] += shift;
   }
 }
+// The symmetric band image's diagonal array (offset 0 = sym_off[k0]): rows whose mask has bit k0.
+template <class MT>
+__global__ void k_shift_sym(i64 nrows, i64 own, const MT *__restrict__ mask, int k0, double *__restrict__ diag,
+                            double shift)
+{
+  const i64 r = (i64)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= nrows) return;
+  if ((mask[r] >> k0) & 1u) diag[own + r] += shift;
+}
 void launch_shift_diag(eig_mat_s &A, double shift, hipStream_t s)
 {
   const i64 G = (A.nb_rows + 255) / 256;
   if (G == 0) return;
   hipLaunchKernelGGL(k_shift_diag, dim3((unsigned)G), dim3(256), 0, s, A.nb_rows, A.own_offset / A.bc, A.slice_ptr,
                      A.col, A.val, A.br, A.bc, 64 * A.R, shift);
+  if (A.sym_val)
+  {
+    int k0 = -1;
+    for (int k = 0; k < A.sym_nd; ++k)
+      if (A.sym_off[k] == 0) k0 = k;
+    if (k0 < 0) return;  // no row stores a diagonal entry
+    double *diag = A.sym_val + (i64)A.sym_dj[k0] * A.sym_ld;
+    if (A.sym_mask_bytes == 1)
+      hipLaunchKernelGGL(k_shift_sym<uint8_t>, dim3((unsigned)G), dim3(256), 0, s, A.nb_rows, A.own_offset,
+                         static_cast<const uint8_t *>(A.sym_mask), k0, diag, shift);
+    else
+      hipLaunchKernelGGL(k_shift_sym<uint32_t>, dim3((unsigned)G), dim3(256), 0, s, A.nb_rows, A.own_offset,
+                         static_cast<const uint32_t *>(A.sym_mask), k0, diag, shift);
+  }
 }
 
 // ---------------------------------------------------------------------------------------------

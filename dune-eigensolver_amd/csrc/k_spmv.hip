@@ -204,6 +204,17 @@ __device__ __forceinline__ void rows_dot_stencil(const double *__restrict__ val,
   }
 }
 
+// Symmetric band image (internal.h, eig_mat_s::sym_*): the stored diagonals of the upper triangle,
+// one window-indexed array each; the entry at offset -d of row w is the entry at +d of row w - d.
+struct SymImg {
+  const double *val;  // nup arrays of ld doubles
+  const void *mask;   // owned row r: bit k = row stores the entry at off[k] (u8 or u32 per row)
+  i64 ld;
+  int nd;                 // offsets, ascending = ISTL column order
+  i32 off[kSymMaxOff];
+  i32 dj[kSymMaxOff];     // array index of |off[k]|
+};
+
 struct SellB1 {
   const i64 *slice_ptr;
   const double *val;
@@ -214,7 +225,39 @@ struct SellB1 {
   i64 xlast;  // window length - 1 (gather clamp)
   int swz;    // XCD-aware chunk order (chunk_of)
   int nts;    // nontemporal stores of the step vectors (EIGMI_NT_STORE)
+  SymImg sym;
 };
+
+// Row r (window index w = own + r) of the symmetric band image, one row per lane.  Each offset is
+// one coalesced value load (at w for d >= 0, at w + d for d < 0: the mirrored upper entry, a
+// re-read of what rows d earlier streamed, served by L2 / MALL) plus one coalesced gather; the mask
+// gates the accumulation, so a row sums exactly its stored entries in ascending-column order
+// (bitwise BCRSMatrix::mv when the matrix is bitwise symmetric, which build_sym checks).
+template <class MT, class X>
+__device__ __forceinline__ void rows_dot_sym(const SymImg &S, i64 r, i64 w, const X &x, i64 xlast, double &acc)
+{
+  constexpr int KC = 4;
+  acc = 0.0;
+  const unsigned m = static_cast<const MT *>(S.mask)[r];
+  for (int k0 = 0; k0 < S.nd; k0 += KC)
+  {
+    double a[KC], xv[KC];
+#pragma unroll
+    for (int k = 0; k < KC; ++k)
+    {
+      const bool in = k0 + k < S.nd;
+      const int d = in ? S.off[k0 + k] : 0;
+      i64 g = w + d;
+      g = g < 0 ? 0 : (g > xlast ? xlast : g);
+      const i64 va = (i64)(in ? S.dj[k0 + k] : 0) * S.ld + (d < 0 ? g : w);
+      a[k] = in ? S.val[va] : 0.0;
+      xv[k] = in ? x(g) : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < KC; ++k)
+      if ((m >> (k0 + k)) & 1u) acc += a[k] * xv[k];
+  }
+}
 
 // Store of a streamed result vector entry: nontemporal (no L2 allocation) when A.nts.
 __device__ __forceinline__ void put(double *p, double v, int nts)
@@ -223,14 +266,27 @@ __device__ __forceinline__ void put(double *p, double v, int nts)
   else *p = v;
 }
 
-// Image modes: every slice explicit, every slice stencil, or mixed (per-slice wave-uniform branch).
-enum { kExplicit = 0, kStencil = 1, kMixed = 2 };
+// Image modes: every slice explicit, every slice stencil, or mixed (per-slice wave-uniform branch);
+// kSym8 / kSym32: the symmetric band image with u8 / u32 row masks (R = 1 only).
+enum { kExplicit = 0, kStencil = 1, kMixed = 2, kSym8 = 3, kSym32 = 4 };
 
 // Row sums of slice s for this lane's R rows.
 template <int R, int MODE, class X>
 __device__ __forceinline__ void slice_dot(const SellB1 &A, i64 s, const X &x, i64 own, int lane, double (&acc)[R])
 {
   constexpr int C = 64 * R;
+  if constexpr (MODE == kSym8 || MODE == kSym32)
+  {
+    if constexpr (R == 1)  // (the launchers pick these modes only for R = 1 images)
+    {
+      const i64 r = s * 64 + lane;
+      if constexpr (MODE == kSym8) rows_dot_sym<uint8_t>(A.sym, r, own + r, x, A.xlast, acc[0]);
+      else rows_dot_sym<uint32_t>(A.sym, r, own + r, x, A.xlast, acc[0]);
+    }
+    return;
+  }
+  else
+  {
   const i64 base = A.slice_ptr[s];
   const int width = (int)((A.slice_ptr[s + 1] - base) / C);
   const bool st = (MODE == kStencil) || (MODE == kMixed && A.st_width[s] > 0);
@@ -239,15 +295,38 @@ __device__ __forceinline__ void slice_dot(const SellB1 &A, i64 s, const X &x, i6
                         own + s * C + (i64)lane * R, A.xlast, acc);
   else
     rows_dot<R, X>(A.val, A.col, x, base, width, lane, acc);
+  }
 }
 
 static SellB1 sell_b1(const eig_mat_s &A)
 {
-  return SellB1{A.slice_ptr, A.val, A.col, A.st_width, A.st_delta, A.st_mask, A.window - 1, xcd_swizzle(), nt_store()};
+  SellB1 b{A.slice_ptr, A.val, A.col, A.st_width, A.st_delta, A.st_mask, A.window - 1, xcd_swizzle(), nt_store(), {}};
+  if (A.sym_val)
+  {
+    b.sym.val = A.sym_val;
+    b.sym.mask = A.sym_mask;
+    b.sym.ld = A.sym_ld;
+    b.sym.nd = A.sym_nd;
+    for (int k = 0; k < kSymMaxOff; ++k)
+    {
+      b.sym.off[k] = k < A.sym_nd ? A.sym_off[k] : 0;
+      b.sym.dj[k] = k < A.sym_nd ? A.sym_dj[k] : 0;
+    }
+  }
+  return b;
+}
+
+// EIGMI_SYM=0 keeps the SELL image for the scalar kernels even when a symmetric band image exists.
+// (read at every launch, like the other EIGMI_* kernel switches, so one upload can be A/B'd)
+static bool sym_kernels()
+{
+  const char *e = std::getenv("EIGMI_SYM");
+  return !(e && e[0] == '0');
 }
 
 static int image_mode(const eig_mat_s &A)
 {
+  if (A.sym_val && A.R == 1 && sym_kernels()) return A.sym_mask_bytes == 1 ? kSym8 : kSym32;
   if (A.n_stencil_slices == 0) return kExplicit;
   return A.n_stencil_slices == A.nslices ? kStencil : kMixed;
 }
@@ -480,6 +559,52 @@ __device__ __forceinline__ void fused_row_stencil(const SellB1 &A, i64 s, const 
   }
 }
 
+// Fused step, one row of the symmetric band image (rows_dot_sym with the (t, u) pair gathers); the
+// row's own (t, u) comes from the delta = 0 gather when the row pattern has it.
+template <class MT, int KC>
+__device__ __forceinline__ void fused_row_sym(const SymImg &S, i64 r, i64 w, i64 xl, const dpair *__restrict__ P,
+                                              double c, double &acc, double &tv, double &uv)
+{
+  acc = 0.0;
+  const unsigned m = static_cast<const MT *>(S.mask)[r];
+  bool centre = false;  // wave-uniform
+  for (int k0 = 0; k0 < S.nd; k0 += KC)
+  {
+    double a[KC];
+    dpair pr[KC];
+    int dk[KC];
+#pragma unroll
+    for (int k = 0; k < KC; ++k)
+    {
+      const bool in = k0 + k < S.nd;
+      const int d = in ? S.off[k0 + k] : 0;
+      dk[k] = d;
+      i64 g = w + d;
+      g = g < 0 ? 0 : (g > xl ? xl : g);
+      const i64 va = (i64)(in ? S.dj[k0 + k] : 0) * S.ld + (d < 0 ? g : w);
+      a[k] = in ? S.val[va] : 0.0;
+      pr[k] = in ? P[g] : dpair{0.0, 0.0};
+    }
+#pragma unroll
+    for (int k = 0; k < KC; ++k)
+    {
+      if (k0 + k < S.nd && dk[k] == 0)
+      {
+        tv = pr[k].x;
+        uv = pr[k].y;
+        centre = true;
+      }
+      if ((m >> (k0 + k)) & 1u) acc += a[k] * (pr[k].x - c * pr[k].y);
+    }
+  }
+  if (!centre)
+  {
+    const dpair pv = P[w > xl ? xl : w];
+    tv = pv.x;
+    uv = pv.y;
+  }
+}
+
 // W = waves per SIMD the register budget is sized for (W >= 8: stencil rows take 4 entries per
 // round to fit 64 VGPRs; EIGMI_FUSED_WAVES picks 4/5/6/8, see launch_lanczos_fused).
 template <int R, int MODE, int W>
@@ -518,7 +643,13 @@ __global__ __launch_bounds__(kStreamThreads, W) void k_lanczos_fused_b1(
     const i64 s = slices ? (i64)slices[first + it] : first + it;
     const i64 r0 = s * C + (i64)lane * R;
     double tv[R], uv[R], acc[R];
-    if (R == 1 && MODE != kExplicit && (MODE == kStencil || A.st_width[s] > 0))
+    if constexpr (MODE == kSym8 || MODE == kSym32)
+    {
+      if constexpr (R == 1)
+        fused_row_sym<typename std::conditional<MODE == kSym8, uint8_t, uint32_t>::type, (W >= 8 ? 4 : 8)>(
+            A.sym, r0, own + r0, A.xlast, P, c, acc[0], tv[0], uv[0]);
+    }
+    else if (R == 1 && MODE != kExplicit && (MODE == kStencil || A.st_width[s] > 0))
     {
       fused_row_stencil<(W >= 8 ? 4 : 8)>(A, s, P, c, own, lane, acc[0], tv[0], uv[0]);
     }
@@ -737,6 +868,8 @@ void launch_spmv(const eig_mat_s &A, const double *x, double *y, const i32 *slic
     const int m_ = image_mode(A);                                                                        \
     if (m_ == kExplicit) EIG_B1(R_, kExplicit)                                                           \
     else if (m_ == kStencil) EIG_B1(R_, kStencil)                                                        \
+    else if (m_ == kSym8) EIG_B1(R_, kSym8)                                                              \
+    else if (m_ == kSym32) EIG_B1(R_, kSym32)                                                            \
     else EIG_B1(R_, kMixed)                                                                              \
   }
   if (A.br == 1 && A.bc == 1)
@@ -772,6 +905,8 @@ void launch_lanczos_spmv(const eig_mat_s &A, const double *u, const double *up, 
     const int m_ = image_mode(A);                                                                            \
     if (m_ == kExplicit) EIG_LZ(R_, kExplicit);                                                              \
     else if (m_ == kStencil) EIG_LZ(R_, kStencil);                                                           \
+    else if (m_ == kSym8) EIG_LZ(R_, kSym8);                                                                 \
+    else if (m_ == kSym32) EIG_LZ(R_, kSym32);                                                               \
     else EIG_LZ(R_, kMixed);                                                                                 \
   }
   const int pm = k1_pipe_mode();
@@ -824,6 +959,8 @@ void launch_lanczos_fused(const eig_mat_s &A, const double *P, double *Pout, int
     const int m_ = image_mode(A);                                                                             \
     if (m_ == kExplicit) EIG_LFW(R_, kExplicit)                                                               \
     else if (m_ == kStencil) EIG_LFW(R_, kStencil)                                                            \
+    else if (m_ == kSym8) EIG_LFW(R_, kSym8)                                                                  \
+    else if (m_ == kSym32) EIG_LFW(R_, kSym32)                                                                \
     else EIG_LFW(R_, kMixed)                                                                                  \
   }
   if (A.R == 1) EIG_LFM(1)

@@ -47,7 +47,7 @@ class _MatInfo(ctypes.Structure):
                                               "nnzb_padded", "nslices")] + \
                [("br", ctypes.c_int), ("bc", ctypes.c_int)] + \
                [(k, ctypes.c_int64) for k in ("halo_recv", "halo_send", "device_bytes", "stencil_slices",
-                                              "rows_per_lane")]
+                                              "rows_per_lane", "sym_offsets")]
 
 
 class BlockTiming(ctypes.Structure):

@@ -130,6 +130,8 @@ typedef struct eig_mat_info {
   int64_t device_bytes; /* matrix image size in HBM */
   int64_t stencil_slices; /* slices read through per-slice column offsets + row masks */
   int64_t rows_per_lane;  /* R of the SELL-C image (C = 64 R) */
+  int64_t sym_offsets;    /* offsets of the symmetric band image (0 = none; the scalar SpMV and
+                             Lanczos kernels then read the upper-triangle band arrays) */
 } eig_mat_info;
 int eig_mat_get_info(eig_mat_t mat, eig_mat_info *info);
 

@@ -1,0 +1,134 @@
+"""GPU parity of the symmetric band image (internal.h eig_mat_s::sym_*, api.cpp build_sym).
+
+A square 1x1 matrix whose rows draw their columns from at most 32 offsets and whose stored mirror
+pairs are bitwise equal keeps its values once, in upper-triangle band arrays; the scalar SpMV and
+the Lanczos kernels read the lower entries through the mirrored upper slot.  Every row still sums
+its own stored entries in ascending-column order, so the bar stays BITWISE equality with the
+reference row loop (oracle.csr_mv = matmul_sparse_tallskinny_naive, kernels_cpp.hh:596-621)."""
+import os
+
+import numpy as np
+import pytest
+
+import eigmi
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def upload(ctx, A, sym=True):
+    old = os.environ.get("EIGMI_SYM")
+    os.environ["EIGMI_SYM"] = "1" if sym else "0"
+    try:
+        return eigmi.Matrix.from_bcsr(ctx, A.rowptr, A.col, A.val, A.br, A.bc)
+    finally:
+        if old is None:
+            del os.environ["EIGMI_SYM"]
+        else:
+            os.environ["EIGMI_SYM"] = old
+
+
+def band_matrix(n, offsets, seed, drop=0.0, symmetric=True):
+    """Random-valued band matrix on the given non-negative offsets (mirrored to negative ones).
+    `drop`: probability that an upper entry is stored without its mirror (a structurally
+    unsymmetric pattern whose stored pairs are still equal)."""
+    rng = np.random.default_rng(seed)
+    ups = {}
+    for p in offsets:
+        m = n - p
+        v = rng.standard_normal(m)
+        keep_lo = rng.random(m) >= drop
+        keep_up = rng.random(m) >= drop if p else np.ones(m, bool)
+        ups[p] = (v, keep_up, keep_lo)
+    rows = [[] for _ in range(n)]
+    for p, (v, ku, kl) in ups.items():
+        for i in range(n - p):
+            if ku[i]:
+                rows[i].append((i + p, v[i]))
+            if p and kl[i]:
+                rows[i + p].append((i, v[i] if symmetric else v[i] * (1 + 1e-15 * (i % 3 == 1))))
+    rowptr, col, val = [0], [], []
+    for r in rows:
+        r.sort()
+        col.extend(c for c, _ in r)
+        val.extend(x for _, x in r)
+        rowptr.append(len(col))
+    return oracle.CSR(n, np.array(rowptr, np.int64), np.array(col, np.int32), np.array(val, np.float64))
+
+
+def check_mv(ctx, A, expect_sym):
+    M = upload(ctx, A)
+    assert (M.info.sym_offsets > 0) == expect_sym
+    rng = np.random.default_rng(7)
+    for x in (rng.standard_normal(A.n), np.ones(A.n)):
+        y = M.mv_host(x)
+        ref = oracle.csr_mv(A, x)
+        assert np.array_equal(y, ref), f"max diff {np.abs(y - ref).max()}"
+    return M
+
+
+@pytest.mark.parametrize("N", [16, 33])
+def test_poisson_uses_sym_image_bitwise(ctx, N):
+    A = oracle.poisson3d(N)
+    M = check_mv(ctx, A, True)
+    assert M.info.sym_offsets == 7
+
+
+def test_2d_laplacians_bitwise(ctx):
+    check_mv(ctx, oracle.laplace2d(64), True)
+    check_mv(ctx, oracle.laplace2d(64, "neumann"), True)
+
+
+def test_random_symmetric_band_u8_mask(ctx):
+    check_mv(ctx, band_matrix(5000, [0, 1, 7, 130], 1), True)
+
+
+def test_structurally_unsymmetric_pattern(ctx):
+    """Pairs with one side missing: the slot carries the stored side, the mask hides the other."""
+    A = band_matrix(3001, [0, 1, 64, 200], 2, drop=0.3)
+    check_mv(ctx, A, True)
+
+
+def test_many_offsets_u32_mask(ctx):
+    """More than 8 offsets (here 2*12-1 = 23): 32-bit row masks."""
+    A = band_matrix(4100, [0, 1, 2, 3, 5, 8, 13, 21, 34, 55, 89, 144], 3, drop=0.1)
+    M = check_mv(ctx, A, True)
+    assert M.info.sym_offsets == 23
+
+
+def test_not_bitwise_symmetric_keeps_sell(ctx):
+    A = band_matrix(2000, [0, 1, 9], 4, symmetric=False)
+    check_mv(ctx, A, False)
+
+
+def test_wide_offsets_keep_sell(ctx):
+    A = band_matrix(600, list(range(0, 40)), 5)  # 79 offsets > 32
+    check_mv(ctx, A, False)
+
+
+def test_shift_diag_updates_band(ctx):
+    A = band_matrix(3000, [0, 1, 50], 6)
+    M = upload(ctx, A)
+    assert M.info.sym_offsets > 0
+    M.shift_diag(-0.625)
+    val = A.val.copy()
+    oracle.lib.orc_shift_diag(A.n, A.rowptr, A.col, val, -0.625)
+    B = oracle.CSR(A.nrows, A.rowptr, A.col, val)
+    x = np.random.default_rng(0).standard_normal(A.n)
+    assert np.array_equal(M.mv_host(x), oracle.csr_mv(B, x))
+
+
+@pytest.mark.parametrize("fused", [False, True])
+def test_lanczos_sym_equals_sell(ctx, fused):
+    """Same Krylov process through the band image and through the SELL image: per-row sums are
+    bitwise equal and both kernels run on the same grid, so alpha/beta agree to rounding of the
+    reductions (bitwise when the grids coincide)."""
+    A = oracle.poisson3d(24)
+    Ms, Mp = upload(ctx, A, True), upload(ctx, A, False)
+    assert Ms.info.sym_offsets == 7 and Mp.info.sym_offsets == 0
+    a1, b1, _ = eigmi.lanczos_run(Ms, 40, seed=123, fused=fused)
+    a2, b2, _ = eigmi.lanczos_run(Mp, 40, seed=123, fused=fused)
+    assert np.allclose(a1, a2, rtol=1e-12, atol=0) and np.allclose(b1, b2, rtol=1e-12, atol=0)
+    ra, rb = (oracle.lanczos_fused(A, oracle.random_vec(A.n, 123), 40) if fused
+              else oracle.lanczos(A, oracle.random_vec(A.n, 123), 40)[1:])
+    assert np.allclose(a1, ra, rtol=1e-11, atol=0) and np.allclose(b1, rb, rtol=1e-11, atol=0)

@@ -1,9 +1,9 @@
 #!/usr/bin/env python3
 """A/B of Lanczos step variants on one GPU, interleaved rounds in ONE process (guide rule 24).
 
-Variant spec "<fused|classic>[:swz0|swz1][:w4|w5|w6|w8][:nt0|nt1]": step form, XCD-aware chunk
+Variant spec "<fused|classic>[:swz0|swz1][:w4|w5|w6|w8][:nt0|nt1][:sym0|sym1]": step form, XCD-aware chunk
 order (EIGMI_XCD_SWIZZLE), register budget of the fused kernel (EIGMI_FUSED_WAVES), nontemporal
-stores of the step vectors (EIGMI_NT_STORE).  The environment is
+stores of the step vectors (EIGMI_NT_STORE), symmetric band image or SELL image (EIGMI_SYM).  The environment is
 read at every launch, so all variants share one matrix upload.  One JSON line per variant:
 median / min over rounds of the step time and of the dominant kernel's time.
 
@@ -23,9 +23,11 @@ import eigmi  # noqa: E402
 
 def parse(spec):
     parts = spec.split(":")
-    env = {"EIGMI_XCD_SWIZZLE": "0", "EIGMI_FUSED_WAVES": "8", "EIGMI_NT_STORE": "0"}
+    env = {"EIGMI_XCD_SWIZZLE": "0", "EIGMI_FUSED_WAVES": "8", "EIGMI_NT_STORE": "0", "EIGMI_SYM": "1"}
     for p in parts[1:]:
-        if p.startswith("nt"):
+        if p.startswith("sym"):
+            env["EIGMI_SYM"] = p[3:]
+        elif p.startswith("nt"):
             env["EIGMI_NT_STORE"] = p[2:]
         elif p.startswith("swz"):
             env["EIGMI_XCD_SWIZZLE"] = p[3:]
