@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
 """A/B of Lanczos step variants on one GPU, interleaved rounds in ONE process (guide rule 24).
 
-Variant spec "<fused|classic>[:swz0|swz1][:w4|w5|w6|w8][:nt0|nt1][:sym0|sym1]": step form, XCD-aware chunk
+Variant spec "<fused|classic>[:swz0|swz1][:w4|w5|w6|w8][:nt0|nt1][:sym0|sym1|sym2][:march0|march1]": step form, XCD-aware chunk
 order (EIGMI_XCD_SWIZZLE), register budget of the fused kernel (EIGMI_FUSED_WAVES), nontemporal
-stores of the step vectors (EIGMI_NT_STORE), symmetric band image or SELL image (EIGMI_SYM).  The environment is
+stores of the step vectors (EIGMI_NT_STORE), symmetric band image or SELL image (EIGMI_SYM), plane marching
+(EIGMI_MARCH).  The environment is
 read at every launch, so all variants share one matrix upload.  One JSON line per variant:
 median / min over rounds of the step time and of the dominant kernel's time.
 
@@ -23,9 +24,11 @@ import eigmi  # noqa: E402
 
 def parse(spec):
     parts = spec.split(":")
-    env = {"EIGMI_XCD_SWIZZLE": "0", "EIGMI_FUSED_WAVES": "8", "EIGMI_NT_STORE": "0", "EIGMI_SYM": "1"}
+    env = {"EIGMI_XCD_SWIZZLE": "0", "EIGMI_FUSED_WAVES": "8", "EIGMI_NT_STORE": "0", "EIGMI_SYM": "2", "EIGMI_MARCH": "1"}
     for p in parts[1:]:
-        if p.startswith("sym"):
+        if p.startswith("march"):
+            env["EIGMI_MARCH"] = p[5:]
+        elif p.startswith("sym"):
             env["EIGMI_SYM"] = p[3:]
         elif p.startswith("nt"):
             env["EIGMI_NT_STORE"] = p[2:]
