@@ -209,8 +209,11 @@ def main():
 
     # dominant kernel: the step kernel (fused) or the SpMV kernel (classic), HIP events on the
     # library stream around every launch of the timed region
-    kname = "k_lanczos_fused_b1" if fused else "k_lanczos_spmv_b1"
-    k1_bytes = eigmi.bytes_lanczos_fused(cnt, nnz_local) if fused else eigmi.bytes_lanczos_k1(cnt, nnz_local)
+    # algorithmic bytes per launch are those of the matrix image the kernel streams (DESIGN.md
+    # section 5): the symmetric band image moves 8 B per upper-band slot + a 1-B row mask, i.e.
+    # fewer bytes than the survey's CSR count (12 B per nonzero), which is reported beside it
+    kname, k1_bytes = M.lanczos_kernel_info(fused)
+    csr_bytes = eigmi.bytes_lanczos_fused(cnt, nnz_local) if fused else eigmi.bytes_lanczos_k1(cnt, nnz_local)
     k1_ms = tim.spmv_ms / K if tim.spmv_launches else None
     roofline = None
     if k1_ms:
@@ -219,12 +222,13 @@ def main():
         roofline = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": tr[0] if tr else None,
                     "traffic_source": tr[1] if tr else None,
-                    # measured HBM bytes / launch time: the stencil-slice image moves fewer bytes
-                    # than the CSR algorithmic count (column indices -> per-slice offsets + masks)
                     "traffic_GBs": round(tr[0] / (k1_ms * 1e-3) / 1e9, 1) if tr else None,
                     "traffic_frac": round(tr[0] / (k1_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if tr else None,
                     "kernel": kname, "bytes_per_launch": k1_bytes,
-                    "avg_launch_us": round(k1_ms * 1e3, 2)}
+                    "avg_launch_us": round(k1_ms * 1e3, 2),
+                    # the same launch priced at the survey's CSR byte count
+                    "csr_bytes_per_launch": csr_bytes,
+                    "csr_equiv_GBs": round(csr_bytes / (k1_ms * 1e-3) / 1e9, 1)}
     step_bytes = eigmi.bytes_lanczos_step(n, nnz_total)
     value = K / dt
     out = {
@@ -245,8 +249,9 @@ def main():
                    "N": N, "n": n, "nnz": nnz_total,
                    "parallelism": (f"row-partition z-slabs x{world} (RCCL halo, {ctx.comm_info()['allreduce']} "
                                    "allreduce)") if world > 1 else "single GPU"},
-        "step_hbm_gbs": round(step_bytes / (dt / K) / 1e9, 1),
-        "step_roofline_frac": round(step_bytes / (dt / K) / 1e9 / HBM_PEAK_GBS / max(world, 1), 4),
+        # SURVEY 8(d)'s CSR step bytes (12 nnz + 4(n+1) + 48 n) / step time: an equivalent rate, not
+        # HBM traffic (the band image streams fewer bytes; roofline.* prices the kernel's own bytes)
+        "step_csr_equiv_GBs": round(step_bytes / (dt / K) / 1e9, 1),
         "roofline": roofline,
         "spmv_hbm_gbs": roofline["achieved"] if roofline else None,
         # device time of the K steps: fused SpMV launches vs the rest (update kernel, allreduces)

@@ -1076,6 +1076,23 @@ extern "C" int eig_mat_get_info(eig_mat_t A, eig_mat_info *info)
   });
 }
 
+extern "C" int eig_lanczos_kernel_info(eig_mat_t A, int fused, char *name, int name_len, int64_t *bytes)
+{
+  return guard(A ? A->ctx : nullptr, [&] {
+    EIG_CHECK(A && bytes && (name || name_len == 0), EIG_ERR_ARG, "eig_lanczos_kernel_info: null argument");
+    std::string nm;
+    i64 b = 0;
+    lanczos_kernel_info(*A, fused != 0, nm, b);
+    *bytes = b;
+    if (name_len > 0)
+    {
+      const size_t k = std::min<size_t>(nm.size(), (size_t)name_len - 1);
+      std::memcpy(name, nm.data(), k);
+      name[k] = 0;
+    }
+  });
+}
+
 extern "C" int eig_mat_shift_diag(eig_mat_t A, double shift)
 {
   return guard(A ? A->ctx : nullptr, [&] {

@@ -225,6 +225,8 @@ void launch_lanczos_fused(const eig_mat_s &A, const double *P, double *Pout, int
                           const LanczosState &st, const i32 *slices, i64 first, i64 count, const double *carry,
                           double *out, int ticket, hipStream_t s, ReduceWS red);
 void launch_fused_tail(const LanczosState &st, int K, hipStream_t s);
+// Kernel a whole-matrix Lanczos step launch picks on this image, and its algorithmic bytes per launch.
+void lanczos_kernel_info(const eig_mat_s &A, bool fused, std::string &name, i64 &bytes);
 void launch_lanczos_spmv(const eig_mat_s &A, const double *u, const double *up, double *t, int j,
                          const LanczosState &st, const i32 *slices, i64 first, i64 count, double *dot_out,
                          double *beta_out, const double *carry, int ticket, hipStream_t s, ReduceWS red);

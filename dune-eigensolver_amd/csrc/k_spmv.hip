@@ -425,6 +425,8 @@ static int sym_kernels()
   return e && e[0] == '0' ? 0 : (e && e[0] == '1' ? 1 : 2);
 }
 
+static bool is_sym_mode(int mode) { return mode >= kSym8; }
+
 static int image_mode(const eig_mat_s &A)
 {
   const int sk = A.sym_val && A.R == 1 ? sym_kernels() : 0;
@@ -780,7 +782,121 @@ struct MarchPlan {
   int nseg;     // plane runs per column
 };
 
-template <class MT, int KC>
+// The rows of this wave's work item, in plane order: epi(r, w, acc, centre) gets each row's sum
+// and its own operand x[w] (raw: a double, or the (t, u) pair of the fused step).
+template <class MT, int KC, class X, class EPI>
+__device__ __forceinline__ void march_rows(const SellB1 &A, const MarchPlan &mp, i64 own, int lane, int wave,
+                                           const X &x, EPI &epi)
+{
+  typedef typename X::raw raw;
+  const SymImg &S = A.sym;
+  const i64 xl = A.xlast, D = mp.D, ldl = S.ld - 1;
+  const int nd = S.nd;
+  const double *UD = S.val + (i64)S.dj[nd - 1] * S.ld;
+  const double *U1 = S.val + (i64)S.j1 * S.ld;
+  const double *U0 = S.val + (i64)(S.j0 >= 0 ? S.j0 : 0) * S.ld;
+  const MT *mask = static_cast<const MT *>(S.mask);
+  const i64 item = swizzled_block(1) * kWaves + wave;
+  if (item >= (i64)mp.ncol * mp.nseg) return;
+  const i64 col = item % mp.ncol, seg = item / mp.ncol;
+  const i64 z0 = seg * mp.nplanes / mp.nseg, z1 = (seg + 1) * mp.nplanes / mp.nseg;
+  auto cx = [&](i64 g) { return g < 0 ? 0 : (g > xl ? xl : g); };
+  auto cv = [&](i64 g) { return g < 0 ? 0 : (g > ldl ? ldl : g); };
+  // carried operands: the -D operand, its mirrored value, and the centre
+  i64 w = own + col * 64 + lane + z0 * D;
+  raw pm = x.load(cx(w - D));
+  double amD = UD[cv(w - D)];
+  raw pcur = x.load(cx(w));
+  for (i64 z = z0; z < z1; ++z, w += D)
+  {
+    const i64 r = w - own;
+    const i64 wv = w > ldl ? ldl : w;
+    const unsigned m = r < mp.mrows ? (unsigned)mask[r] : 0u;
+    const double aD = UD[wv];
+    const raw pD = x.load(cx(w + D));
+    const double a0 = S.j0 >= 0 ? U0[wv] : 0.0;
+    const double ap = U1[wv];
+    raw el, er;
+    double ae = 0.0;
+    if (lane == 0)
+    {
+      el = x.load(cx(w - 1));
+      ae = U1[cv(w - 1)];
+    }
+    if (lane == 63) er = x.load(cx(w + 1));
+    double acc = 0.0;
+    if (m & 1u) acc += amD * x.val(pm);
+    sym_span<KC>(S, 1, S.klo, m, w, x, xl, acc);
+    raw pl = lane_shift<false>(pcur), pr = lane_shift<true>(pcur);
+    double am = lane_shift<false>(ap);
+    if (lane == 0)
+    {
+      pl = el;
+      am = ae;
+    }
+    if (lane == 63) pr = er;
+    if (S.km1 >= 0 && ((m >> S.km1) & 1u)) acc += am * x.val(pl);
+    if (S.k0 >= 0 && ((m >> S.k0) & 1u)) acc += a0 * x.val(pcur);
+    if (S.kp1 >= 0 && ((m >> S.kp1) & 1u)) acc += ap * x.val(pr);
+    sym_span<KC>(S, S.khi, nd - 1, m, w, x, xl, acc);
+    if ((m >> (nd - 1)) & 1u) acc += aD * x.val(pD);
+    epi(r, w, acc, pcur);
+    pm = pcur;
+    pcur = pD;
+    amD = aD;
+  }
+}
+
+// y[own + r] = (A x)[r] on the plane march (BCRSMatrix::mv; bitwise k_spmv_b1).
+template <class MT>
+__global__ __launch_bounds__(kStreamThreads, 8) void k_spmv_march(i64 nrows, i64 own, SellB1 A, MarchPlan mp,
+                                                                  const double *__restrict__ x,
+                                                                  double *__restrict__ y)
+{
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  auto epi = [&](i64 r, i64 w, double acc, double) {
+    if (r < nrows) y[w] = acc;
+  };
+  march_rows<MT, 2>(A, mp, own, lane, wave, XPlain{x}, epi);
+}
+
+// Classic Lanczos kernel 1 on the plane march (same per-row arithmetic as k_lanczos_spmv_b1; the
+// row's own u_j is the march's centre operand).
+template <class MT>
+__global__ __launch_bounds__(kStreamThreads, 8) void k_lanczos_spmv_march(
+    i64 nrows, i64 own, SellB1 A, MarchPlan mp, const double *__restrict__ u, const double *__restrict__ up,
+    double *__restrict__ t, int j, const double *__restrict__ nsum, double *__restrict__ dot_out,
+    double *__restrict__ beta_out, double *partials, unsigned *ticket)
+{
+  __shared__ double tot[1];
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const double beta = sqrt(nsum[j]);
+  const double sig = 1.0 / beta;
+  const double gam = (j > 0) ? beta * (1.0 / sqrt(nsum[j - 1])) : 0.0;
+  double d = 0.0;
+  auto epi = [&](i64 r, i64 w, double acc, double uv) {
+    if (r < nrows)
+    {
+      double ti = acc * sig;
+      if (j > 0) ti = ti - gam * up[w];
+      put(t + w, ti, A.nts);
+      d += ti * uv;
+    }
+  };
+  march_rows<MT, 2>(A, mp, own, lane, wave, XPlain{u}, epi);
+  double v[1] = {d};
+  if (grid_sum<1, kStreamThreads>(v, partials, ticket, tot))
+  {
+    if (threadIdx.x == 0)
+    {
+      dot_out[0] = tot[0];
+      if (beta_out) beta_out[0] = beta;
+    }
+  }
+}
+
+// Fused one-reduction step on the plane march (per-row arithmetic of k_lanczos_fused_b1).
+template <class MT>
 __global__ __launch_bounds__(kStreamThreads, 8) void k_lanczos_fused_march(
     i64 nrows, i64 own, SellB1 A, MarchPlan mp, const dpair *__restrict__ P, dpair *__restrict__ Pout, int k,
     double *__restrict__ nsum, double *__restrict__ alpha, double *__restrict__ beta, const double *__restrict__ red,
@@ -805,74 +921,20 @@ __global__ __launch_bounds__(kStreamThreads, 8) void k_lanczos_fused_march(
     else
       beta[0] = sqrt(nt);
   }
-  const XPair xc{P, c};
-  const SymImg &S = A.sym;
-  const i64 xl = A.xlast, D = mp.D, ldl = S.ld - 1;
-  const int nd = S.nd;
-  const double *UD = S.val + (i64)S.dj[nd - 1] * S.ld;
-  const double *U1 = S.val + (i64)S.j1 * S.ld;
-  const double *U0 = S.val + (i64)(S.j0 >= 0 ? S.j0 : 0) * S.ld;
-  const MT *mask = static_cast<const MT *>(S.mask);
-  const i64 item = swizzled_block(1) * kWaves + wave;
   double d = 0.0, q2 = 0.0, m2 = 0.0;
-  if (item < (i64)mp.ncol * mp.nseg)
-  {
-    const i64 col = item % mp.ncol, seg = item / mp.ncol;
-    const i64 z0 = seg * mp.nplanes / mp.nseg, z1 = (seg + 1) * mp.nplanes / mp.nseg;
-    auto clampx = [&](i64 g) { return g < 0 ? 0 : (g > xl ? xl : g); };
-    // carried operands: the -D pair, its mirrored value, and the centre pair
-    i64 w = own + col * 64 + lane + z0 * D;
-    dpair pm = P[clampx(w - D)];
-    double amD = UD[clampx(w - D) > ldl ? ldl : clampx(w - D)];
-    dpair pcur = P[clampx(w)];
-    for (i64 z = z0; z < z1; ++z, w += D)
+  auto epi = [&](i64 r, i64 w, double acc, dpair pc) {
+    if (r < nrows)
     {
-      const i64 r = w - own;
-      const i64 wv = w > ldl ? ldl : w;
-      const unsigned m = r < mp.mrows ? (unsigned)mask[r] : 0u;
-      const double aD = UD[wv];
-      const dpair pD = P[clampx(w + D)];
-      const double a0 = S.j0 >= 0 ? U0[wv] : 0.0;
-      const double ap = U1[wv];
-      dpair el, er;
-      double ae = 0.0;
-      if (lane == 0)
-      {
-        el = P[clampx(w - 1)];
-        ae = U1[clampx(w - 1) > ldl ? ldl : clampx(w - 1)];
-      }
-      if (lane == 63) er = P[clampx(w + 1)];
-      double acc = 0.0;
-      if (m & 1u) acc += amD * xc.val(pm);
-      sym_span<KC>(S, 1, S.klo, m, w, xc, xl, acc);
-      dpair pl = lane_shift<false>(pcur), pr = lane_shift<true>(pcur);
-      double am = lane_shift<false>(ap);
-      if (lane == 0)
-      {
-        pl = el;
-        am = ae;
-      }
-      if (lane == 63) pr = er;
-      if (S.km1 >= 0 && ((m >> S.km1) & 1u)) acc += am * xc.val(pl);
-      if (S.k0 >= 0 && ((m >> S.k0) & 1u)) acc += a0 * xc.val(pcur);
-      if (S.kp1 >= 0 && ((m >> S.kp1) & 1u)) acc += ap * xc.val(pr);
-      sym_span<KC>(S, S.khi, nd - 1, m, w, xc, xl, acc);
-      if ((m >> (nd - 1)) & 1u) acc += aD * xc.val(pD);
-      if (r < nrows)
-      {
-        const double uk = pcur.x - c * pcur.y;
-        double ti = acc * sig;
-        if (k > 0) ti = ti - gam * pcur.y;
-        Pout[w] = dpair{ti, uk};
-        d += ti * uk;
-        q2 += ti * ti;
-        m2 += uk * uk;
-      }
-      pm = pcur;
-      pcur = pD;
-      amD = aD;
+      const double uk = pc.x - c * pc.y;
+      double ti = acc * sig;
+      if (k > 0) ti = ti - gam * pc.y;
+      Pout[w] = dpair{ti, uk};
+      d += ti * uk;
+      q2 += ti * ti;
+      m2 += uk * uk;
     }
-  }
+  };
+  march_rows<MT, 2>(A, mp, own, lane, wave, XPair{P, c}, epi);
   double v[3] = {d, q2, m2};
   if (grid_sum<3, kStreamThreads>(v, partials, ticket, tot))
   {
@@ -1035,12 +1097,62 @@ static int grid_for_slices(K kernel, i64 count, int num_cu)
   return (int)(need < cap ? need : cap);
 }
 
+// EIGMI_MARCH=0 disables the plane-marching kernels.
+static bool march_enabled()
+{
+  const char *e = std::getenv("EIGMI_MARCH");
+  return !(e && e[0] == '0');
+}
+
+// Plane-marching plan for a whole-matrix launch on the lane-shift band image, or nseg = 0 when the
+// band does not qualify: symmetric offset set with off[0] = -D, off[nd-1] = +D, D a multiple of 64,
+// at least 4 planes.  Plane runs per column: enough items for one resident wave per SIMD slot
+// (8 per SIMD), at most kMaxRedBlocks workgroups.
+static MarchPlan march_plan(const eig_mat_s &A, int mode)
+{
+  MarchPlan mp{0, 0, 0, 0, 0};
+  if (mode != kSymN8 && mode != kSymN32) return mp;
+  if (!march_enabled() || A.sym_nd < 3) return mp;
+  const i64 D = A.sym_off[A.sym_nd - 1];
+  if (D <= 1 || D % 64 != 0 || A.sym_off[0] != -D) return mp;
+  const i64 nplanes = (A.nb_rows + D - 1) / D;
+  if (nplanes < 4) return mp;
+  const i64 ncol = D / 64;
+  const i64 resident = 8LL * 4 * A.ctx->num_cu;  // waves
+  i64 nseg = std::max<i64>(1, (resident + ncol - 1) / ncol);
+  nseg = std::min<i64>(nseg, nplanes);
+  while (nseg > 1 && (ncol * nseg + kWaves - 1) / kWaves > kMaxRedBlocks) --nseg;
+  if ((ncol * nseg + kWaves - 1) / kWaves > kMaxRedBlocks) return mp;
+  mp.D = D;
+  mp.nplanes = nplanes;
+  mp.mrows = A.nslices * 64;
+  mp.ncol = (int)ncol;
+  mp.nseg = (int)nseg;
+  return mp;
+}
+
 void launch_spmv(const eig_mat_s &A, const double *x, double *y, const i32 *slices, i64 first, i64 count,
                  hipStream_t s)
 {
   if (count <= 0) return;
   const int ncu = A.ctx->num_cu;
   double *yo = y + A.own_offset;
+  if (!slices && first == 0 && count == A.nslices && A.br == 1 && A.bc == 1)
+  {
+    const int mode = image_mode(A);
+    const MarchPlan mp = march_plan(A, mode);
+    if (mp.nseg > 0)
+    {
+      const unsigned G = (unsigned)((mp.ncol * (i64)mp.nseg + kWaves - 1) / kWaves);
+      if (mode == kSymN8)
+        hipLaunchKernelGGL(k_spmv_march<uint8_t>, dim3(G), dim3(kStreamThreads), 0, s, A.nb_rows, A.own_offset,
+                           sell_b1(A), mp, x, y);
+      else
+        hipLaunchKernelGGL(k_spmv_march<uint32_t>, dim3(G), dim3(kStreamThreads), 0, s, A.nb_rows, A.own_offset,
+                           sell_b1(A), mp, x, y);
+      return;
+    }
+  }
 #define EIG_BLK(R_, C_)                                                                                 \
   if (A.br == R_ && A.bc == C_)                                                                         \
   {                                                                                                     \
@@ -1089,6 +1201,22 @@ void launch_lanczos_spmv(const eig_mat_s &A, const double *u, const double *up, 
                          double *beta_out, const double *carry, int ticket, hipStream_t s, ReduceWS red)
 {
   EIG_CHECK(A.br == 1 && A.bc == 1, EIG_ERR_BLOCKSIZE, "Lanczos driver: 1x1 blocks only");
+  if (!slices && first == 0 && count == A.nslices && !carry)
+  {
+    const int mode = image_mode(A);
+    const MarchPlan mp = march_plan(A, mode);
+    if (mp.nseg > 0)
+    {
+      const unsigned G = (unsigned)((mp.ncol * (i64)mp.nseg + kWaves - 1) / kWaves);
+#define EIG_LZMARCH(MT_)                                                                                      \
+  hipLaunchKernelGGL(k_lanczos_spmv_march<MT_>, dim3(G), dim3(kStreamThreads), 0, s, A.nb_rows, A.own_offset, \
+                     sell_b1(A), mp, u, up, t, j, st.nsum, dot_out, beta_out, red.partials, red.ticket(ticket))
+      if (mode == kSymN8) EIG_LZMARCH(uint8_t);
+      else EIG_LZMARCH(uint32_t);
+#undef EIG_LZMARCH
+      return;
+    }
+  }
 #define EIG_LZ(R_, M_)                                                                                       \
   hipLaunchKernelGGL((k_lanczos_spmv_b1<R_, M_>),                                                           \
                      dim3(grid_for_slices(k_lanczos_spmv_b1<R_, M_>, count, A.ctx->num_cu)), dim3(kStreamThreads), \
@@ -1130,40 +1258,6 @@ static int fused_waves()
   return (w == 4 || w == 5 || w == 6) ? w : 8;
 }
 
-// EIGMI_MARCH=0 disables the plane-marching kernels.
-static bool march_enabled()
-{
-  const char *e = std::getenv("EIGMI_MARCH");
-  return !(e && e[0] == '0');
-}
-
-// Plane-marching plan for a whole-matrix launch on the lane-shift band image, or nseg = 0 when the
-// band does not qualify: symmetric offset set with off[0] = -D, off[nd-1] = +D, D a multiple of 64,
-// at least 4 planes.  Plane runs per column: enough items for one resident wave per SIMD slot
-// (8 per SIMD), at most kMaxRedBlocks workgroups.
-static MarchPlan march_plan(const eig_mat_s &A, int mode)
-{
-  MarchPlan mp{0, 0, 0, 0, 0};
-  if (mode != kSymN8 && mode != kSymN32) return mp;
-  if (!march_enabled() || A.sym_nd < 3) return mp;
-  const i64 D = A.sym_off[A.sym_nd - 1];
-  if (D <= 1 || D % 64 != 0 || A.sym_off[0] != -D) return mp;
-  const i64 nplanes = (A.nb_rows + D - 1) / D;
-  if (nplanes < 4) return mp;
-  const i64 ncol = D / 64;
-  const i64 resident = 8LL * 4 * A.ctx->num_cu;  // waves
-  i64 nseg = std::max<i64>(1, (resident + ncol - 1) / ncol);
-  nseg = std::min<i64>(nseg, nplanes);
-  while (nseg > 1 && (ncol * nseg + kWaves - 1) / kWaves > kMaxRedBlocks) --nseg;
-  if ((ncol * nseg + kWaves - 1) / kWaves > kMaxRedBlocks) return mp;
-  mp.D = D;
-  mp.nplanes = nplanes;
-  mp.mrows = A.nslices * 64;
-  mp.ncol = (int)ncol;
-  mp.nseg = (int)nseg;
-  return mp;
-}
-
 void launch_lanczos_fused(const eig_mat_s &A, const double *P, double *Pout, int k,
                           const LanczosState &st, const i32 *slices, i64 first, i64 count, const double *carry,
                           double *out, int ticket, hipStream_t s, ReduceWS red)
@@ -1177,7 +1271,7 @@ void launch_lanczos_fused(const eig_mat_s &A, const double *P, double *Pout, int
     {
       const unsigned G = (unsigned)((mp.ncol * (i64)mp.nseg + kWaves - 1) / kWaves);
 #define EIG_MARCH(MT_)                                                                                         \
-  hipLaunchKernelGGL((k_lanczos_fused_march<MT_, 2>), dim3(G), dim3(kStreamThreads), 0, s, A.nb_rows,          \
+  hipLaunchKernelGGL((k_lanczos_fused_march<MT_>), dim3(G), dim3(kStreamThreads), 0, s, A.nb_rows,          \
                      A.own_offset, sell_b1(A), mp, reinterpret_cast<const dpair *>(P),                          \
                      reinterpret_cast<dpair *>(Pout), k, st.nsum, st.alpha, st.beta, st.fred, out, red.partials, \
                      red.ticket(ticket))
@@ -1224,6 +1318,26 @@ void launch_lanczos_fused(const eig_mat_s &A, const double *P, double *Pout, int
 void launch_fused_tail(const LanczosState &st, int K, hipStream_t s)
 {
   hipLaunchKernelGGL(k_fused_tail, dim3(1), dim3(64), 0, s, st.nsum, st.alpha, st.beta, st.fred, K);
+}
+
+void lanczos_kernel_info(const eig_mat_s &A, bool fused, std::string &name, i64 &bytes)
+{
+  const i64 n = A.nb_rows, vec = fused ? 32 * n : 24 * n;  // fused: (t, u) pairs in + out; K1: x, u_{j-1}, t
+  const int mode = A.br == 1 && A.bc == 1 ? image_mode(A) : kExplicit;
+  if (is_sym_mode(mode))
+  {
+    bytes = 8 * (i64)A.sym_nup * n + (i64)A.sym_mask_bytes * n + vec;
+    // (distributed launches with a halo take the interior / boundary split, never the march)
+    const bool whole = !A.ctx->distributed() || (A.recvs.empty() && A.sends.empty());
+    const bool march = whole && march_plan(A, mode).nseg > 0 && (!fused || fused_waves() == 8);
+    name = fused ? (march ? "k_lanczos_fused_march" : "k_lanczos_fused_b1")
+                 : (march ? "k_lanczos_spmv_march" : "k_lanczos_spmv_b1");
+  }
+  else
+  {
+    bytes = 12 * A.nnzb + 4 * (n + 1) + vec;
+    name = fused ? "k_lanczos_fused_b1" : "k_lanczos_spmv_b1";
+  }
 }
 
 }  // namespace eigmi

@@ -97,6 +97,7 @@ SIGNATURES = {
     "eig_mat_destroy": (_int, [_vp]),
     "eig_mat_get_info": (_int, [_vp, ctypes.POINTER(_MatInfo)]),
     "eig_mat_shift_diag": (_int, [_vp, _dbl]),
+    "eig_lanczos_kernel_info": (_int, [_vp, _int, ctypes.c_char_p, _int, ctypes.POINTER(_i64)]),
     "eig_mv": (_int, [_vp, _vp, _vp]),
     "eig_mv_host": (_int, [_vp, _vp, _vp]),
     "eig_mv_timed": (_int, [_vp, _vp, _vp, _int, ctypes.POINTER(_dbl)]),
@@ -309,6 +310,14 @@ class Matrix:
         info = _MatInfo()
         ctx.check(lib.eig_mat_get_info(handle, ctypes.byref(info)))
         self.info = info
+
+    def lanczos_kernel_info(self, fused=True):
+        """-> (kernel name, algorithmic HBM bytes per launch) of a whole-matrix Lanczos step launch
+        on this image (eig_lanczos_kernel_info)."""
+        buf = ctypes.create_string_buffer(64)
+        b = _i64()
+        self.ctx.check(lib.eig_lanczos_kernel_info(self.h, int(bool(fused)), buf, 64, ctypes.byref(b)))
+        return buf.value.decode(), int(b.value)
 
     @classmethod
     def from_bcsr(cls, ctx, rowptr, col, vals, br=1, bc=1, ncols_blocks=None):

@@ -135,6 +135,12 @@ typedef struct eig_mat_info {
 } eig_mat_info;
 int eig_mat_get_info(eig_mat_t mat, eig_mat_info *info);
 
+/* Measurement helper: the kernel a whole-matrix Lanczos step launch uses on this matrix image
+ * (fused = 1: the one-reduction step; 0: the classic SpMV kernel K1) and its algorithmic HBM bytes
+ * per launch for that image: SELL/stencil images 12 nnz + 4(n+1) + vectors,
+ * the symmetric band image 8 nup n + mask bytes + vectors.  `name` gets at most name_len bytes. */
+int eig_lanczos_kernel_info(eig_mat_t mat, int fused, char *name, int name_len, int64_t *bytes);
+
 /* a13: A += shift*I on the diagonal of every diagonal block (eigensolver.hh:59-66). */
 int eig_mat_shift_diag(eig_mat_t mat, double shift);
 

@@ -132,3 +132,39 @@ def test_lanczos_sym_equals_sell(ctx, fused):
     ra, rb = (oracle.lanczos_fused(A, oracle.random_vec(A.n, 123), 40) if fused
               else oracle.lanczos(A, oracle.random_vec(A.n, 123), 40)[1:])
     assert np.allclose(a1, ra, rtol=1e-11, atol=0) and np.allclose(b1, rb, rtol=1e-11, atol=0)
+
+
+# ---- plane march (k_*_march): widest offset D a multiple of 64, rows marched plane by plane ----
+
+@pytest.mark.parametrize("n,offs,drop", [
+    (5000, [0, 1, 5, 128], 0.0),        # 39.06 planes: partial last plane
+    (4096, [0, 1, 64], 0.2),            # 2-D-like, structurally unsymmetric
+    (6000, [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 192], 0.1),  # 23 offsets: u32 masks
+    (3000, [0, 2, 64], 0.0),            # no +-1: band path without lane shifts, no march
+])
+def test_march_spmv_bitwise(ctx, n, offs, drop):
+    A = band_matrix(n, offs, 11, drop=drop)
+    M = check_mv(ctx, A, True)
+    name, _ = M.lanczos_kernel_info(fused=False)
+    assert name == ("k_lanczos_spmv_march" if 1 in offs else "k_lanczos_spmv_b1")
+
+
+def test_march_kernel_names_and_bytes(ctx):
+    A = oracle.poisson3d(16)
+    M = upload(ctx, A)
+    n = A.n
+    assert M.lanczos_kernel_info(True) == ("k_lanczos_fused_march", 8 * 4 * n + n + 32 * n)
+    assert M.lanczos_kernel_info(False) == ("k_lanczos_spmv_march", 8 * 4 * n + n + 24 * n)
+    P = upload(ctx, A, sym=False)
+    assert P.lanczos_kernel_info(True)[0] == "k_lanczos_fused_b1"
+
+
+@pytest.mark.parametrize("fused", [False, True])
+def test_march_lanczos_partial_plane(ctx, fused):
+    """Lanczos on a band matrix whose rows are not a whole number of planes, march vs SELL image."""
+    A = band_matrix(9000, [0, 1, 9, 128], 12)
+    Ms, Mp = upload(ctx, A, True), upload(ctx, A, False)
+    assert Ms.lanczos_kernel_info(fused)[0].endswith("_march")
+    a1, b1, _ = eigmi.lanczos_run(Ms, 30, seed=9, fused=fused)
+    a2, b2, _ = eigmi.lanczos_run(Mp, 30, seed=9, fused=fused)
+    assert np.allclose(a1, a2, rtol=1e-11, atol=1e-13) and np.allclose(b1, b2, rtol=1e-11, atol=1e-13)
