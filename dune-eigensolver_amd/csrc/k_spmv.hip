@@ -247,8 +247,8 @@ struct SymImg {
 // the mirrored upper entry, re-read from L2 / MALL after the rows d earlier streamed it) plus one
 // coalesced gather; the mask gates the accumulation.
 template <int KC, class X>
-__device__ __forceinline__ void sym_span(const SymImg &S, int kb, int ke, unsigned m, i64 w, const X &x, i64 xl,
-                                         double &acc)
+__device__ __forceinline__ void sym_span(const SymImg &S, int kb, int ke, unsigned m, i64 w, i64 wv, const X &x,
+                                         i64 xl, double &acc)
 {
   for (int k0 = kb; k0 < ke; k0 += KC)
   {
@@ -260,7 +260,7 @@ __device__ __forceinline__ void sym_span(const SymImg &S, int kb, int ke, unsign
       const int d = in ? S.off[k0 + k] : 0;
       i64 g = w + d;
       g = g < 0 ? 0 : (g > xl ? xl : g);
-      const i64 va = (i64)(in ? S.dj[k0 + k] : 0) * S.ld + (d < 0 ? g : w);
+      const i64 va = (i64)(in ? S.dj[k0 + k] : 0) * S.ld + (d < 0 ? g : wv);
       a[k] = in ? S.val[va] : 0.0;
       xv[k] = in ? x(g) : 0.0;
     }
@@ -286,7 +286,7 @@ __device__ __forceinline__ void row_sym(const SymImg &S, i64 r, i64 w, int lane,
   const i64 wc = w > xl ? xl : w;
   if constexpr (!NEAR)
   {
-    sym_span<KC>(S, 0, S.nd, m, w, x, xl, acc);
+    sym_span<KC>(S, 0, S.nd, m, w, w, x, xl, acc);
     centre = x.load(wc);
   }
   else
@@ -304,7 +304,7 @@ __device__ __forceinline__ void row_sym(const SymImg &S, i64 r, i64 w, int lane,
       ae = S.val[(i64)S.j1 * S.ld + wl];
     }
     if (lane == 63) er = x.load(wr);
-    sym_span<KC>(S, 0, S.klo, m, w, x, xl, acc);
+    sym_span<KC>(S, 0, S.klo, m, w, w, x, xl, acc);
     typename X::raw pl = lane_shift<false>(pc), pr = lane_shift<true>(pc);
     double am = lane_shift<false>(ap);
     if (lane == 0)
@@ -316,7 +316,7 @@ __device__ __forceinline__ void row_sym(const SymImg &S, i64 r, i64 w, int lane,
     if (S.km1 >= 0 && ((m >> S.km1) & 1u)) acc += am * x.val(pl);
     if (S.k0 >= 0 && ((m >> S.k0) & 1u)) acc += a0 * x.val(pc);
     if (S.kp1 >= 0 && ((m >> S.kp1) & 1u)) acc += ap * x.val(pr);
-    sym_span<KC>(S, S.khi, S.nd, m, w, x, xl, acc);
+    sym_span<KC>(S, S.khi, S.nd, m, w, w, x, xl, acc);
     centre = pc;
   }
 }
@@ -780,89 +780,160 @@ struct MarchPlan {
   i64 mrows;    // rows covered by the row mask (nslices * 64)
   int ncol;     // D / 64
   int nseg;     // plane runs per column
+  // first entries of the far spans (-D, -1) and (+1, +D): offset (0 = empty span) and band array
+  i32 dn, dq;
+  const double *Un, *Uq;
 };
 
 // The rows of this wave's work item, in plane order: epi(r, w, acc, centre) gets each row's sum
 // and its own operand x[w] (raw: a double, or the (t, u) pair of the fused step).
-template <class MT, int KC, class X, class EPI>
+// SPAN1 (VAR >= 2): each far span holds at most one offset (3-D 7-point, 2-D 5-point), so the
+// generic span loops are compiled out.
+// VAR 1: loads issued offset group by offset group (the far-negative span, then the far-positive
+// span after the near math); VAR 2: the first entry of both far spans is issued with the row's
+// streams, so a 7-point row waits once; VAR 3: VAR 2 + the next plane's streams (mask, the -D/+D
+// value and pair, the 0/+1 values) prefetched while this plane computes.
+template <class MT, int KC, int VAR, bool SPAN1, bool NT, class X, class EPI>
 __device__ __forceinline__ void march_rows(const SellB1 &A, const MarchPlan &mp, i64 own, int lane, int wave,
                                            const X &x, EPI &epi)
 {
   typedef typename X::raw raw;
+  // 32-bit row / window indices (window < 2^31, enforced at upload) keep the address math short
   const SymImg &S = A.sym;
-  const i64 xl = A.xlast, D = mp.D, ldl = S.ld - 1;
+  const int xl = (int)A.xlast, D = (int)mp.D, ldl = (int)(S.ld - 1), own32 = (int)own, mrows = (int)mp.mrows;
   const int nd = S.nd;
   const double *UD = S.val + (i64)S.dj[nd - 1] * S.ld;
   const double *U1 = S.val + (i64)S.j1 * S.ld;
   const double *U0 = S.val + (i64)(S.j0 >= 0 ? S.j0 : 0) * S.ld;
   const MT *mask = static_cast<const MT *>(S.mask);
-  const i64 item = swizzled_block(1) * kWaves + wave;
-  if (item >= (i64)mp.ncol * mp.nseg) return;
-  const i64 col = item % mp.ncol, seg = item / mp.ncol;
-  const i64 z0 = seg * mp.nplanes / mp.nseg, z1 = (seg + 1) * mp.nplanes / mp.nseg;
-  auto cx = [&](i64 g) { return g < 0 ? 0 : (g > xl ? xl : g); };
-  auto cv = [&](i64 g) { return g < 0 ? 0 : (g > ldl ? ldl : g); };
-  // carried operands: the -D operand, its mirrored value, and the centre
-  i64 w = own + col * 64 + lane + z0 * D;
-  raw pm = x.load(cx(w - D));
+  const int item = (int)swizzled_block(1) * kWaves + wave;
+  if (item >= mp.ncol * mp.nseg) return;
+  const int col = item % mp.ncol, seg = item / mp.ncol;
+  const int z0 = (int)(seg * mp.nplanes / mp.nseg), z1 = (int)((seg + 1) * mp.nplanes / mp.nseg);
+  auto cx = [&](int g) -> unsigned { return g < 0 ? 0u : (unsigned)(g > xl ? xl : g); };
+  auto cv = [&](int g) -> unsigned { return g < 0 ? 0u : (unsigned)(g > ldl ? ldl : g); };
+  const int kn0 = 1, kn1 = S.klo, kp0 = S.khi, kp1 = nd - 1;  // far spans (-D, -1) and (+1, +D)
+  struct Stream {
+    unsigned m;
+    double aD, a0, ap;
+    raw pD;
+  };
+  // streams read exactly once (the row mask, the 0 / +1 / +D band values): nontemporal loads keep
+  // them from evicting the (t, u) / band lines the neighbouring columns re-read from L2
+  auto ld1 = [&](const double *p, unsigned i) { return NT ? __builtin_nontemporal_load(p + i) : p[i]; };
+  auto load_stream = [&](int w, Stream &st) {
+    const int r = w - own32;
+    const unsigned wv = (unsigned)(w > ldl ? ldl : w);
+    if (NT)
+      st.m = r < mrows ? (unsigned)__builtin_nontemporal_load(mask + (unsigned)r) : 0u;
+    else
+      st.m = r < mrows ? (unsigned)mask[(unsigned)r] : 0u;
+    st.aD = ld1(UD, wv);
+    st.pD = x.load(cx(w + D));
+    st.a0 = S.j0 >= 0 ? ld1(U0, wv) : 0.0;
+    st.ap = ld1(U1, wv);
+  };
+  // carried operands: the -D operand (as its value x.val), its mirrored matrix entry, the centre
+  int w = own32 + col * 64 + lane + z0 * D;
+  double pmv = x.val(x.load(cx(w - D)));
   double amD = UD[cv(w - D)];
   raw pcur = x.load(cx(w));
-  for (i64 z = z0; z < z1; ++z, w += D)
+  Stream cur;
+  if (VAR == 3) load_stream(w, cur);
+  const bool edge = lane == 0 || lane == 63;
+  for (int z = z0; z < z1; ++z, w += D)
   {
-    const i64 r = w - own;
-    const i64 wv = w > ldl ? ldl : w;
-    const unsigned m = r < mp.mrows ? (unsigned)mask[r] : 0u;
-    const double aD = UD[wv];
-    const raw pD = x.load(cx(w + D));
-    const double a0 = S.j0 >= 0 ? U0[wv] : 0.0;
-    const double ap = U1[wv];
-    raw el, er;
+    const int r = w - own32;
+    const unsigned wv = (unsigned)(w > ldl ? ldl : w);
+    Stream nxt;
+    if (VAR != 3) load_stream(w, cur);
+    else if (z + 1 < z1) load_stream(w + D, nxt);
+    // lanes 0 / 63: the row across the wave edge (one load for both), and lane 0's mirrored -1 entry
+    raw eg;
     double ae = 0.0;
-    if (lane == 0)
+    if (edge) eg = x.load(cx(lane == 0 ? w - 1 : w + 1));
+    if (lane == 0) ae = U1[cv(w - 1)];
+    double an = 0.0, aq = 0.0;
+    raw xn, xq;
+    if (VAR >= 2)
     {
-      el = x.load(cx(w - 1));
-      ae = U1[cv(w - 1)];
+      if (mp.dn)
+      {
+        const unsigned g = cx(w + mp.dn);  // (negative offset: the mirrored slot at the gathered row)
+        an = mp.Un[g];
+        xn = x.load(g);
+      }
+      if (mp.dq)
+      {
+        aq = mp.Uq[wv];
+        xq = x.load(cx(w + mp.dq));
+      }
     }
-    if (lane == 63) er = x.load(cx(w + 1));
+    const unsigned m = cur.m;
     double acc = 0.0;
-    if (m & 1u) acc += amD * x.val(pm);
-    sym_span<KC>(S, 1, S.klo, m, w, x, xl, acc);
-    raw pl = lane_shift<false>(pcur), pr = lane_shift<true>(pcur);
-    double am = lane_shift<false>(ap);
-    if (lane == 0)
+    if (m & 1u) acc += amD * pmv;
+    if (VAR >= 2)
     {
-      pl = el;
-      am = ae;
+      if (mp.dn && ((m >> kn0) & 1u)) acc += an * x.val(xn);
+      if (!SPAN1) sym_span<KC>(S, kn0 + 1, kn1, m, w, wv, x, xl, acc);
     }
-    if (lane == 63) pr = er;
-    if (S.km1 >= 0 && ((m >> S.km1) & 1u)) acc += am * x.val(pl);
-    if (S.k0 >= 0 && ((m >> S.k0) & 1u)) acc += a0 * x.val(pcur);
-    if (S.kp1 >= 0 && ((m >> S.kp1) & 1u)) acc += ap * x.val(pr);
-    sym_span<KC>(S, S.khi, nd - 1, m, w, x, xl, acc);
-    if ((m >> (nd - 1)) & 1u) acc += aD * x.val(pD);
+    else
+      sym_span<KC>(S, kn0, kn1, m, w, wv, x, xl, acc);
+    // neighbours' operand VALUES shifted across lanes (x.val per lane, then moved: the same bits
+    // as evaluating x.val on the shifted raw operand, at half the registers for pairs)
+    const double vc = x.val(pcur);
+    double vl = lane_shift<false>(vc), vr = lane_shift<true>(vc);
+    double am = lane_shift<false>(cur.ap);
+    if (edge)
+    {
+      const double ve = x.val(eg);
+      if (lane == 0)
+      {
+        vl = ve;
+        am = ae;
+      }
+      else
+        vr = ve;
+    }
+    if (S.km1 >= 0 && ((m >> S.km1) & 1u)) acc += am * vl;
+    if (S.k0 >= 0 && ((m >> S.k0) & 1u)) acc += cur.a0 * vc;
+    if (S.kp1 >= 0 && ((m >> S.kp1) & 1u)) acc += cur.ap * vr;
+    if (VAR >= 2)
+    {
+      if (mp.dq && ((m >> kp0) & 1u)) acc += aq * x.val(xq);
+      if (!SPAN1) sym_span<KC>(S, kp0 + 1, kp1, m, w, wv, x, xl, acc);
+    }
+    else
+      sym_span<KC>(S, kp0, kp1, m, w, wv, x, xl, acc);
+    if ((m >> kp1) & 1u) acc += cur.aD * x.val(cur.pD);
     epi(r, w, acc, pcur);
-    pm = pcur;
-    pcur = pD;
-    amD = aD;
+    pmv = vc;
+    pcur = cur.pD;
+    amD = cur.aD;
+    if (VAR == 3) cur = nxt;
   }
 }
 
 // y[own + r] = (A x)[r] on the plane march (BCRSMatrix::mv; bitwise k_spmv_b1).
-template <class MT>
+template <class MT, int VAR>
 __global__ __launch_bounds__(kStreamThreads, 8) void k_spmv_march(i64 nrows, i64 own, SellB1 A, MarchPlan mp,
                                                                   const double *__restrict__ x,
                                                                   double *__restrict__ y)
 {
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  auto epi = [&](i64 r, i64 w, double acc, double) {
-    if (r < nrows) y[w] = acc;
+  auto epi = [&](int r, int w, double acc, double) {
+    if (r < nrows)
+    {
+      if ((VAR & 8) != 0) __builtin_nontemporal_store(acc, y + (unsigned)w);
+      else y[(unsigned)w] = acc;
+    }
   };
-  march_rows<MT, 2>(A, mp, own, lane, wave, XPlain{x}, epi);
+  march_rows<MT, 2, (VAR & 3), ((VAR & 4) != 0), ((VAR & 8) != 0)>(A, mp, own, lane, wave, XPlain{x}, epi);
 }
 
 // Classic Lanczos kernel 1 on the plane march (same per-row arithmetic as k_lanczos_spmv_b1; the
 // row's own u_j is the march's centre operand).
-template <class MT>
+template <class MT, int VAR>
 __global__ __launch_bounds__(kStreamThreads, 8) void k_lanczos_spmv_march(
     i64 nrows, i64 own, SellB1 A, MarchPlan mp, const double *__restrict__ u, const double *__restrict__ up,
     double *__restrict__ t, int j, const double *__restrict__ nsum, double *__restrict__ dot_out,
@@ -874,16 +945,16 @@ __global__ __launch_bounds__(kStreamThreads, 8) void k_lanczos_spmv_march(
   const double sig = 1.0 / beta;
   const double gam = (j > 0) ? beta * (1.0 / sqrt(nsum[j - 1])) : 0.0;
   double d = 0.0;
-  auto epi = [&](i64 r, i64 w, double acc, double uv) {
+  auto epi = [&](int r, int w, double acc, double uv) {
     if (r < nrows)
     {
       double ti = acc * sig;
-      if (j > 0) ti = ti - gam * up[w];
-      put(t + w, ti, A.nts);
+      if (j > 0) ti = ti - gam * up[(unsigned)w];
+      put(t + (unsigned)w, ti, A.nts | ((VAR & 8) != 0));
       d += ti * uv;
     }
   };
-  march_rows<MT, 2>(A, mp, own, lane, wave, XPlain{u}, epi);
+  march_rows<MT, 2, (VAR & 3), ((VAR & 4) != 0), ((VAR & 8) != 0)>(A, mp, own, lane, wave, XPlain{u}, epi);
   double v[1] = {d};
   if (grid_sum<1, kStreamThreads>(v, partials, ticket, tot))
   {
@@ -896,8 +967,8 @@ __global__ __launch_bounds__(kStreamThreads, 8) void k_lanczos_spmv_march(
 }
 
 // Fused one-reduction step on the plane march (per-row arithmetic of k_lanczos_fused_b1).
-template <class MT>
-__global__ __launch_bounds__(kStreamThreads, 8) void k_lanczos_fused_march(
+template <class MT, int VAR>
+__global__ __launch_bounds__(kStreamThreads, ((VAR & 3) == 3 ? 7 : 8)) void k_lanczos_fused_march(
     i64 nrows, i64 own, SellB1 A, MarchPlan mp, const dpair *__restrict__ P, dpair *__restrict__ Pout, int k,
     double *__restrict__ nsum, double *__restrict__ alpha, double *__restrict__ beta, const double *__restrict__ red,
     double *__restrict__ out, double *partials, unsigned *ticket)
@@ -922,19 +993,20 @@ __global__ __launch_bounds__(kStreamThreads, 8) void k_lanczos_fused_march(
       beta[0] = sqrt(nt);
   }
   double d = 0.0, q2 = 0.0, m2 = 0.0;
-  auto epi = [&](i64 r, i64 w, double acc, dpair pc) {
+  auto epi = [&](int r, int w, double acc, dpair pc) {
     if (r < nrows)
     {
       const double uk = pc.x - c * pc.y;
       double ti = acc * sig;
       if (k > 0) ti = ti - gam * pc.y;
-      Pout[w] = dpair{ti, uk};
+      if ((VAR & 8) != 0) __builtin_nontemporal_store(dpair{ti, uk}, Pout + (unsigned)w);
+      else Pout[(unsigned)w] = dpair{ti, uk};
       d += ti * uk;
       q2 += ti * ti;
       m2 += uk * uk;
     }
   };
-  march_rows<MT, 2>(A, mp, own, lane, wave, XPair{P, c}, epi);
+  march_rows<MT, 2, (VAR & 3), ((VAR & 4) != 0), ((VAR & 8) != 0)>(A, mp, own, lane, wave, XPair{P, c}, epi);
   double v[3] = {d, q2, m2};
   if (grid_sum<3, kStreamThreads>(v, partials, ticket, tot))
   {
@@ -1097,12 +1169,65 @@ static int grid_for_slices(K kernel, i64 count, int num_cu)
   return (int)(need < cap ? need : cap);
 }
 
-// EIGMI_MARCH=0 disables the plane-marching kernels.
-static bool march_enabled()
+// EIGMI_MARCH=0 disables the plane-marching kernels; 1 / 2 / 3 pick the load schedule (march_rows
+// VAR; default 2).
+// Default: 1 for the fused step (its pair operands make VAR 2 spill), 2 for SpMV and K1 (measured,
+// tools/lanczos_sweep.py).
+static int march_variant(bool fused = false)
 {
+  const int def = fused ? 1 : 2;
   const char *e = std::getenv("EIGMI_MARCH");
-  return !(e && e[0] == '0');
+  if (!e) return def;
+  return (e[0] >= '0' && e[0] <= '3') ? e[0] - '0' : def;
 }
+static bool march_enabled() { return march_variant() != 0; }
+// Nontemporal loads for the once-read streams of the march and nontemporal result stores (default;
+// EIGMI_MARCH_NT=0 turns them off): fused step -4 %, K1 -3 %, SpMV -14 % (tools/lanczos_sweep.py).
+static int march_nt()
+{
+  const char *e = std::getenv("EIGMI_MARCH_NT");
+  return (e && e[0] == '0') ? 0 : 1;
+}
+// Far spans of at most one offset each (u8-mask bands only: at most 8 offsets, so (-D, -1) and
+// (+1, +D) hold at most one offset each exactly when nd <= 7 with -1/0/+1 present).
+static bool march_span1(const eig_mat_s &A)
+{
+  int klo = A.sym_nd, khi = A.sym_nd;
+  for (int k = A.sym_nd - 1; k >= 0; --k)
+  {
+    if (A.sym_off[k] >= -1) klo = k;
+    if (A.sym_off[k] > 1) khi = k;
+  }
+  return A.sym_mask_bytes == 1 && klo - 1 <= 1 && (A.sym_nd - 1) - khi <= 1;
+}
+
+// Launch a march kernel template KERN<MT, VAR> for the image's mask width and the selected VAR.
+#define EIG_MARCH_LAUNCH(KERN, FUSED, MODE, G, ...)                                                           \
+  do {                                                                                                        \
+    const int v0_ = march_variant(FUSED), v_ = v0_ + (march_span1(A) && v0_ >= 2 ? 4 : 0) + 8 * march_nt();   \
+    if ((MODE) == kSymN8)                                                                                     \
+    {                                                                                                         \
+      if (v_ == 1) hipLaunchKernelGGL((KERN<uint8_t, 1>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);     \
+      else if (v_ == 3) hipLaunchKernelGGL((KERN<uint8_t, 3>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);\
+      else if (v_ == 6) hipLaunchKernelGGL((KERN<uint8_t, 6>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);\
+      else if (v_ == 7) hipLaunchKernelGGL((KERN<uint8_t, 7>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);\
+      else if (v_ == 9) hipLaunchKernelGGL((KERN<uint8_t, 9>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);\
+      else if (v_ == 11) hipLaunchKernelGGL((KERN<uint8_t, 11>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);\
+      else if (v_ == 14) hipLaunchKernelGGL((KERN<uint8_t, 14>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);\
+      else if (v_ == 15) hipLaunchKernelGGL((KERN<uint8_t, 15>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);\
+      else if (v_ == 10) hipLaunchKernelGGL((KERN<uint8_t, 10>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);\
+      else hipLaunchKernelGGL((KERN<uint8_t, 2>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);             \
+    }                                                                                                         \
+    else                                                                                                      \
+    {                                                                                                         \
+      if (v_ == 1) hipLaunchKernelGGL((KERN<uint32_t, 1>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);    \
+      else if (v_ == 3) hipLaunchKernelGGL((KERN<uint32_t, 3>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);\
+      else if (v_ == 9) hipLaunchKernelGGL((KERN<uint32_t, 9>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);\
+      else if (v_ == 11) hipLaunchKernelGGL((KERN<uint32_t, 11>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);\
+      else if (v_ == 10) hipLaunchKernelGGL((KERN<uint32_t, 10>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);\
+      else hipLaunchKernelGGL((KERN<uint32_t, 2>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);            \
+    }                                                                                                         \
+  } while (0)
 
 // Plane-marching plan for a whole-matrix launch on the lane-shift band image, or nseg = 0 when the
 // band does not qualify: symmetric offset set with off[0] = -D, off[nd-1] = +D, D a multiple of 64,
@@ -1110,7 +1235,7 @@ static bool march_enabled()
 // (8 per SIMD), at most kMaxRedBlocks workgroups.
 static MarchPlan march_plan(const eig_mat_s &A, int mode)
 {
-  MarchPlan mp{0, 0, 0, 0, 0};
+  MarchPlan mp{0, 0, 0, 0, 0, 0, 0, nullptr, nullptr};
   if (mode != kSymN8 && mode != kSymN32) return mp;
   if (!march_enabled() || A.sym_nd < 3) return mp;
   const i64 D = A.sym_off[A.sym_nd - 1];
@@ -1124,6 +1249,16 @@ static MarchPlan march_plan(const eig_mat_s &A, int mode)
   while (nseg > 1 && (ncol * nseg + kWaves - 1) / kWaves > kMaxRedBlocks) --nseg;
   if ((ncol * nseg + kWaves - 1) / kWaves > kMaxRedBlocks) return mp;
   mp.D = D;
+  int klo = A.sym_nd, khi = A.sym_nd;
+  for (int k = A.sym_nd - 1; k >= 0; --k)
+  {
+    if (A.sym_off[k] >= -1) klo = k;
+    if (A.sym_off[k] > 1) khi = k;
+  }
+  mp.dn = klo > 1 ? A.sym_off[1] : 0;
+  mp.Un = A.sym_val + (i64)(klo > 1 ? A.sym_dj[1] : 0) * A.sym_ld;
+  mp.dq = khi < A.sym_nd - 1 ? A.sym_off[khi] : 0;
+  mp.Uq = A.sym_val + (i64)(khi < A.sym_nd - 1 ? A.sym_dj[khi] : 0) * A.sym_ld;
   mp.nplanes = nplanes;
   mp.mrows = A.nslices * 64;
   mp.ncol = (int)ncol;
@@ -1144,12 +1279,7 @@ void launch_spmv(const eig_mat_s &A, const double *x, double *y, const i32 *slic
     if (mp.nseg > 0)
     {
       const unsigned G = (unsigned)((mp.ncol * (i64)mp.nseg + kWaves - 1) / kWaves);
-      if (mode == kSymN8)
-        hipLaunchKernelGGL(k_spmv_march<uint8_t>, dim3(G), dim3(kStreamThreads), 0, s, A.nb_rows, A.own_offset,
-                           sell_b1(A), mp, x, y);
-      else
-        hipLaunchKernelGGL(k_spmv_march<uint32_t>, dim3(G), dim3(kStreamThreads), 0, s, A.nb_rows, A.own_offset,
-                           sell_b1(A), mp, x, y);
+      EIG_MARCH_LAUNCH(k_spmv_march, false, mode, G, s, A.nb_rows, A.own_offset, sell_b1(A), mp, x, y);
       return;
     }
   }
@@ -1208,12 +1338,8 @@ void launch_lanczos_spmv(const eig_mat_s &A, const double *u, const double *up, 
     if (mp.nseg > 0)
     {
       const unsigned G = (unsigned)((mp.ncol * (i64)mp.nseg + kWaves - 1) / kWaves);
-#define EIG_LZMARCH(MT_)                                                                                      \
-  hipLaunchKernelGGL(k_lanczos_spmv_march<MT_>, dim3(G), dim3(kStreamThreads), 0, s, A.nb_rows, A.own_offset, \
-                     sell_b1(A), mp, u, up, t, j, st.nsum, dot_out, beta_out, red.partials, red.ticket(ticket))
-      if (mode == kSymN8) EIG_LZMARCH(uint8_t);
-      else EIG_LZMARCH(uint32_t);
-#undef EIG_LZMARCH
+      EIG_MARCH_LAUNCH(k_lanczos_spmv_march, false, mode, G, s, A.nb_rows, A.own_offset, sell_b1(A), mp, u, up, t, j,
+                       st.nsum, dot_out, beta_out, red.partials, red.ticket(ticket));
       return;
     }
   }
@@ -1270,14 +1396,9 @@ void launch_lanczos_fused(const eig_mat_s &A, const double *P, double *Pout, int
     if (mp.nseg > 0)
     {
       const unsigned G = (unsigned)((mp.ncol * (i64)mp.nseg + kWaves - 1) / kWaves);
-#define EIG_MARCH(MT_)                                                                                         \
-  hipLaunchKernelGGL((k_lanczos_fused_march<MT_>), dim3(G), dim3(kStreamThreads), 0, s, A.nb_rows,          \
-                     A.own_offset, sell_b1(A), mp, reinterpret_cast<const dpair *>(P),                          \
-                     reinterpret_cast<dpair *>(Pout), k, st.nsum, st.alpha, st.beta, st.fred, out, red.partials, \
-                     red.ticket(ticket))
-      if (mode == kSymN8) EIG_MARCH(uint8_t);
-      else EIG_MARCH(uint32_t);
-#undef EIG_MARCH
+      EIG_MARCH_LAUNCH(k_lanczos_fused_march, true, mode, G, s, A.nb_rows, A.own_offset, sell_b1(A), mp,
+                       reinterpret_cast<const dpair *>(P), reinterpret_cast<dpair *>(Pout), k, st.nsum, st.alpha,
+                       st.beta, st.fred, out, red.partials, red.ticket(ticket));
       return;
     }
   }

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """A/B of Lanczos step variants on one GPU, interleaved rounds in ONE process (guide rule 24).
 
-Variant spec "<fused|classic>[:swz0|swz1][:w4|w5|w6|w8][:nt0|nt1][:sym0|sym1|sym2][:march0|march1]": step form, XCD-aware chunk
+Variant spec "<fused|classic>[:swz0|swz1][:w4|w5|w6|w8][:nt0|nt1][:sym0|sym1|sym2][:march0|1|2|3][:mnt0|mnt1]": step form, XCD-aware chunk
 order (EIGMI_XCD_SWIZZLE), register budget of the fused kernel (EIGMI_FUSED_WAVES), nontemporal
 stores of the step vectors (EIGMI_NT_STORE), symmetric band image or SELL image (EIGMI_SYM), plane marching
 (EIGMI_MARCH).  The environment is
@@ -24,9 +24,11 @@ import eigmi  # noqa: E402
 
 def parse(spec):
     parts = spec.split(":")
-    env = {"EIGMI_XCD_SWIZZLE": "0", "EIGMI_FUSED_WAVES": "8", "EIGMI_NT_STORE": "0", "EIGMI_SYM": "2", "EIGMI_MARCH": "1"}
+    env = {"EIGMI_XCD_SWIZZLE": "0", "EIGMI_FUSED_WAVES": "8", "EIGMI_NT_STORE": "0", "EIGMI_SYM": "2", "EIGMI_MARCH": "d", "EIGMI_MARCH_NT": "1"}
     for p in parts[1:]:
-        if p.startswith("march"):
+        if p.startswith("mnt"):
+            env["EIGMI_MARCH_NT"] = p[3:]
+        elif p.startswith("march"):
             env["EIGMI_MARCH"] = p[5:]
         elif p.startswith("sym"):
             env["EIGMI_SYM"] = p[3:]
@@ -54,10 +56,18 @@ def main():
     M = eigmi.Matrix.from_bcsr(ctx, rp, c, v)
     specs = args.variants.split(",")
     res = {s: {"k_us": [], "step_us": []} for s in specs}
+    xy = None
     for _ in range(args.rounds):
         for spec in specs:
             fused, env = parse(spec)
             os.environ.update(env)
+            if spec.startswith("mv"):  # plain eig_mv (BCRSMatrix::mv) launches
+                if xy is None:
+                    xy = (ctx.array(np.random.default_rng(0).standard_normal(n)), ctx.zeros(n))
+                ms = M.mv_timed(xy[0], xy[1], args.steps)
+                res[spec]["k_us"].append(ms * 1e3)
+                res[spec]["step_us"].append(ms * 1e3)
+                continue
             ws = eigmi.LanczosWorkspace(M, args.steps + 2, seed=123, fused=fused)
             ws.step(2)
             t = ws.step(args.steps, timed=True)
@@ -66,7 +76,8 @@ def main():
             ws.close()
     for spec in specs:
         fused, _ = parse(spec)
-        kb = eigmi.bytes_lanczos_fused(n, nnz) if fused else eigmi.bytes_lanczos_k1(n, nnz)
+        kb = (eigmi.bytes_spmv(n, nnz) if spec.startswith("mv") else
+              eigmi.bytes_lanczos_fused(n, nnz) if fused else eigmi.bytes_lanczos_k1(n, nnz))
         r = res[spec]
         km = float(np.median(r["k_us"]))
         sm = float(np.median(r["step_us"]))
