@@ -863,6 +863,7 @@ void destroy_mat(eig_mat_s *A)
   if (A->st_delta) (void)hipFree(A->st_delta);
   if (A->st_mask) (void)hipFree(A->st_mask);
   if (A->slice_list) (void)hipFree(A->slice_list);
+  if (A->march_bnd) (void)hipFree(A->march_bnd);
   if (A->sym_val) (void)hipFree(A->sym_val);
   if (A->sym_mask) (void)hipFree(A->sym_mask);
   delete A;
@@ -1001,6 +1002,44 @@ extern "C" int eig_mat_create_bcsr_dist(eig_ctx_t ctx, int64_t nb_rows_global, i
       lst.insert(lst.end(), bound.begin(), bound.end());
       A->slice_list = dev_alloc<i32>(std::max<size_t>(lst.size(), 1));
       if (!lst.empty()) EIG_HIP(hipMemcpy(A->slice_list, lst.data(), lst.size() * sizeof(i32), hipMemcpyHostToDevice));
+      // plane-march split: the longest run of planes whose slices are all interior (>= 2 planes)
+      i64 D;
+      if (march_geometry(*A, D))
+      {
+        const i64 spp = D / 64, np = (nb_local + D - 1) / D;
+        std::vector<char> is_in(A->nslices, 0);
+        for (i32 q : inter) is_in[q] = 1;
+        i64 best0 = 0, best1 = 0;
+        for (i64 z = 0; z < np;)
+        {
+          auto plane_in = [&](i64 zz) {
+            for (i64 q = zz * spp; q < std::min(A->nslices, (zz + 1) * spp); ++q)
+              if (!is_in[q]) return false;
+            return true;
+          };
+          if (!plane_in(z))
+          {
+            ++z;
+            continue;
+          }
+          i64 e = z;
+          while (e < np && plane_in(e)) ++e;
+          if (e - z > best1 - best0) best0 = z, best1 = e;
+          z = e;
+        }
+        if (best1 - best0 >= 2)
+        {
+          std::vector<i32> bnd;
+          for (i64 q = 0; q < A->nslices; ++q)
+            if (q < best0 * spp || q >= best1 * spp) bnd.push_back((i32)q);
+          A->mz0 = best0;
+          A->mz1 = best1;
+          A->n_march_bnd = (i64)bnd.size();
+          A->march_bnd = dev_alloc<i32>(std::max<size_t>(bnd.size(), 1));
+          if (!bnd.empty())
+            EIG_HIP(hipMemcpy(A->march_bnd, bnd.data(), bnd.size() * sizeof(i32), hipMemcpyHostToDevice));
+        }
+      }
     }
     catch (...)
     {
@@ -1113,12 +1152,23 @@ void mv_device(eig_mat_s &A, double *x, double *y)
     launch_spmv(A, x, y, nullptr, 0, A.nslices, ctx->stream);
     return;
   }
+  // interior / boundary split: the interior planes on the plane march when it applies, else the
+  // interior slices
+  const bool mz = march_split_active(A);
+  auto interior = [&](hipStream_t s) {
+    if (mz) launch_spmv(A, x, y, &kMarchInteriorTag, 0, 0, s);
+    else launch_spmv(A, x, y, A.slice_list, 0, A.n_interior, s);
+  };
+  auto boundary = [&](hipStream_t s) {
+    if (mz) launch_spmv(A, x, y, A.march_bnd, 0, A.n_march_bnd, s);
+    else launch_spmv(A, x, y, A.slice_list, A.n_interior, A.n_boundary, s);
+  };
   if (ctx->loop)
   {
     // synchronous exchange, then the same interior / boundary launches as the RCCL path
     halo_exchange(A, x, ctx->stream);
-    launch_spmv(A, x, y, A.slice_list, 0, A.n_interior, ctx->stream);
-    launch_spmv(A, x, y, A.slice_list, A.n_interior, A.n_boundary, ctx->stream);
+    interior(ctx->stream);
+    boundary(ctx->stream);
     return;
   }
   hipEvent_t e0, e1;
@@ -1128,9 +1178,9 @@ void mv_device(eig_mat_s &A, double *x, double *y)
   EIG_HIP(hipStreamWaitEvent(ctx->comm_stream, e0, 0));
   halo_exchange(A, x, ctx->comm_stream);
   EIG_HIP(hipEventRecord(e1, ctx->comm_stream));
-  launch_spmv(A, x, y, A.slice_list, 0, A.n_interior, ctx->stream);
+  interior(ctx->stream);
   EIG_HIP(hipStreamWaitEvent(ctx->stream, e1, 0));
-  launch_spmv(A, x, y, A.slice_list, A.n_interior, A.n_boundary, ctx->stream);
+  boundary(ctx->stream);
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
 }

@@ -544,6 +544,15 @@ void halo_split(eig_mat_s &A, hipEvent_t e0, hipEvent_t e1, Halo halo, Launch la
     halo(ctx->comm_stream);
     EIG_HIP(hipEventRecord(e1, ctx->comm_stream));
   }
+  if (march_split_active(A))
+  {
+    // interior planes on the plane march (k_spmv.hip), every other slice after the exchange
+    const bool has_bd = A.n_march_bnd > 0;
+    launch(&kMarchInteriorTag, 0, 0, has_bd ? kPartFirst : kPartOnly);
+    if (!ctx->loop) EIG_HIP(hipStreamWaitEvent(s, e1, 0));
+    if (has_bd) launch(A.march_bnd, 0, A.n_march_bnd, kPartSecond);
+    return;
+  }
   const bool has_in = A.n_interior > 0, has_bd = A.n_boundary > 0;
   if (has_in) launch(A.slice_list, 0, A.n_interior, has_bd ? kPartFirst : kPartOnly);
   if (!ctx->loop) EIG_HIP(hipStreamWaitEvent(s, e1, 0));

@@ -188,6 +188,12 @@ struct eig_mat_s {
   eigmi::i64 sym_ld = 0;
   eigmi::i32 sym_off[eigmi::kSymMaxOff] = {};      // ascending offsets (ISTL column order)
   eigmi::i32 sym_dj[eigmi::kSymMaxOff] = {};       // array index of |sym_off[k]|
+  // Plane-march split of a distributed slab (k_spmv.hip march_plan): planes [mz0, mz1) have no
+  // ghost columns and are marched while the halo is in flight; march_bnd lists every slice outside
+  // them (the boundary launch after the exchange).  mz1 <= mz0: no split.
+  eigmi::i64 mz0 = 0, mz1 = 0;
+  eigmi::i32 *march_bnd = nullptr;
+  eigmi::i64 n_march_bnd = 0;
   eigmi::i64 *slice_ptr = nullptr;  // nslices + 1
   eigmi::i32 *col = nullptr;        // nnzb_padded, window-local block columns, -1 = padding
   double *val = nullptr;            // nnzb_padded * br * bc
@@ -225,6 +231,13 @@ void launch_lanczos_fused(const eig_mat_s &A, const double *P, double *Pout, int
                           const LanczosState &st, const i32 *slices, i64 first, i64 count, const double *carry,
                           double *out, int ticket, hipStream_t s, ReduceWS red);
 void launch_fused_tail(const LanczosState &st, int K, hipStream_t s);
+// Plane march (k_spmv.hip): band geometry (widest offset D) and whether the interior-plane split
+// launch applies now (split built at upload, image and EIGMI_* switches allow it).  Passing
+// slices == &kMarchInteriorTag to launch_spmv / launch_lanczos_spmv / launch_lanczos_fused marches
+// planes [A.mz0, A.mz1).
+bool march_geometry(const eig_mat_s &A, i64 &D);
+bool march_split_active(const eig_mat_s &A);
+extern const i32 kMarchInteriorTag;
 // Kernel a whole-matrix Lanczos step launch picks on this image, and its algorithmic bytes per launch.
 void lanczos_kernel_info(const eig_mat_s &A, bool fused, std::string &name, i64 &bytes);
 void launch_lanczos_spmv(const eig_mat_s &A, const double *u, const double *up, double *t, int j,

@@ -776,7 +776,8 @@ __global__ __launch_bounds__(kStreamThreads, W) void k_lanczos_fused_b1(
 // ---------------------------------------------------------------------------------------------
 struct MarchPlan {
   i64 D;        // rows per plane (the band's widest offset)
-  i64 nplanes;  // ceil(rows / D)
+  i64 zb;       // first plane marched
+  i64 nplanes;  // planes marched: zb .. zb + nplanes - 1 (whole launch: ceil(rows / D) from 0)
   i64 mrows;    // rows covered by the row mask (nslices * 64)
   int ncol;     // D / 64
   int nseg;     // plane runs per column
@@ -809,7 +810,7 @@ __device__ __forceinline__ void march_rows(const SellB1 &A, const MarchPlan &mp,
   const int item = (int)swizzled_block(1) * kWaves + wave;
   if (item >= mp.ncol * mp.nseg) return;
   const int col = item % mp.ncol, seg = item / mp.ncol;
-  const int z0 = (int)(seg * mp.nplanes / mp.nseg), z1 = (int)((seg + 1) * mp.nplanes / mp.nseg);
+  const int z0 = (int)(mp.zb + seg * mp.nplanes / mp.nseg), z1 = (int)(mp.zb + (seg + 1) * mp.nplanes / mp.nseg);
   auto cx = [&](int g) -> unsigned { return g < 0 ? 0u : (unsigned)(g > xl ? xl : g); };
   auto cv = [&](int g) -> unsigned { return g < 0 ? 0u : (unsigned)(g > ldl ? ldl : g); };
   const int kn0 = 1, kn1 = S.klo, kp0 = S.khi, kp1 = nd - 1;  // far spans (-D, -1) and (+1, +D)
@@ -1233,15 +1234,28 @@ static bool march_span1(const eig_mat_s &A)
 // band does not qualify: symmetric offset set with off[0] = -D, off[nd-1] = +D, D a multiple of 64,
 // at least 4 planes.  Plane runs per column: enough items for one resident wave per SIMD slot
 // (8 per SIMD), at most kMaxRedBlocks workgroups.
-static MarchPlan march_plan(const eig_mat_s &A, int mode)
+// Band geometry the march needs (independent of the EIGMI_* switches): widest offset D.
+bool march_geometry(const eig_mat_s &A, i64 &D)
 {
-  MarchPlan mp{0, 0, 0, 0, 0, 0, 0, nullptr, nullptr};
+  D = 0;
+  if (!A.sym_val || A.R != 1 || A.sym_nd < 3) return false;
+  bool near = false;
+  for (int k = 0; k < A.sym_nd; ++k) near = near || A.sym_off[k] == 1 || A.sym_off[k] == -1;
+  D = A.sym_off[A.sym_nd - 1];
+  return near && D > 1 && D % 64 == 0 && A.sym_off[0] == -D;
+}
+
+// [zb, ze): plane range of a split launch (the interior planes of a distributed slab); ze < 0 =
+// the whole matrix.
+static MarchPlan march_plan(const eig_mat_s &A, int mode, i64 zb = 0, i64 ze = -1)
+{
+  MarchPlan mp{0, 0, 0, 0, 0, 0, 0, 0, nullptr, nullptr};
   if (mode != kSymN8 && mode != kSymN32) return mp;
-  if (!march_enabled() || A.sym_nd < 3) return mp;
-  const i64 D = A.sym_off[A.sym_nd - 1];
-  if (D <= 1 || D % 64 != 0 || A.sym_off[0] != -D) return mp;
-  const i64 nplanes = (A.nb_rows + D - 1) / D;
-  if (nplanes < 4) return mp;
+  i64 D;
+  if (!march_enabled() || !march_geometry(A, D)) return mp;
+  if (ze < 0) ze = (A.nb_rows + D - 1) / D;
+  const i64 nplanes = ze - zb;
+  if (nplanes < 2 || (zb == 0 && nplanes < 4)) return mp;
   const i64 ncol = D / 64;
   const i64 resident = 8LL * 4 * A.ctx->num_cu;  // waves
   i64 nseg = std::max<i64>(1, (resident + ncol - 1) / ncol);
@@ -1259,6 +1273,7 @@ static MarchPlan march_plan(const eig_mat_s &A, int mode)
   mp.Un = A.sym_val + (i64)(klo > 1 ? A.sym_dj[1] : 0) * A.sym_ld;
   mp.dq = khi < A.sym_nd - 1 ? A.sym_off[khi] : 0;
   mp.Uq = A.sym_val + (i64)(khi < A.sym_nd - 1 ? A.sym_dj[khi] : 0) * A.sym_ld;
+  mp.zb = zb;
   mp.nplanes = nplanes;
   mp.mrows = A.nslices * 64;
   mp.ncol = (int)ncol;
@@ -1266,16 +1281,37 @@ static MarchPlan march_plan(const eig_mat_s &A, int mode)
   return mp;
 }
 
+const i32 kMarchInteriorTag = 0;
+
+bool march_split_active(const eig_mat_s &A)
+{
+  return A.mz1 > A.mz0 && march_plan(A, image_mode(A), A.mz0, A.mz1).nseg > 0;
+}
+
+// Plan for a launch: the whole matrix (slices == nullptr over all slices), the interior planes of a
+// distributed slab (slices == &kMarchInteriorTag), or none (nseg = 0: the slice kernels run).
+static MarchPlan launch_plan(const eig_mat_s &A, int mode, const i32 *slices, i64 first, i64 count)
+{
+  if (slices == &kMarchInteriorTag)
+  {
+    const MarchPlan mp = march_plan(A, mode, A.mz0, A.mz1);
+    EIG_CHECK(mp.nseg > 0, EIG_ERR_ARG, "interior-plane launch without a march plan");
+    return mp;
+  }
+  if (!slices && first == 0 && count == A.nslices) return march_plan(A, mode);
+  return MarchPlan{0, 0, 0, 0, 0, 0, 0, 0, nullptr, nullptr};
+}
+
 void launch_spmv(const eig_mat_s &A, const double *x, double *y, const i32 *slices, i64 first, i64 count,
                  hipStream_t s)
 {
-  if (count <= 0) return;
+  if (count <= 0 && slices != &kMarchInteriorTag) return;
   const int ncu = A.ctx->num_cu;
   double *yo = y + A.own_offset;
-  if (!slices && first == 0 && count == A.nslices && A.br == 1 && A.bc == 1)
+  if (A.br == 1 && A.bc == 1)
   {
     const int mode = image_mode(A);
-    const MarchPlan mp = march_plan(A, mode);
+    const MarchPlan mp = launch_plan(A, mode, slices, first, count);
     if (mp.nseg > 0)
     {
       const unsigned G = (unsigned)((mp.ncol * (i64)mp.nseg + kWaves - 1) / kWaves);
@@ -1331,10 +1367,10 @@ void launch_lanczos_spmv(const eig_mat_s &A, const double *u, const double *up, 
                          double *beta_out, const double *carry, int ticket, hipStream_t s, ReduceWS red)
 {
   EIG_CHECK(A.br == 1 && A.bc == 1, EIG_ERR_BLOCKSIZE, "Lanczos driver: 1x1 blocks only");
-  if (!slices && first == 0 && count == A.nslices && !carry)
+  if (!carry)
   {
     const int mode = image_mode(A);
-    const MarchPlan mp = march_plan(A, mode);
+    const MarchPlan mp = launch_plan(A, mode, slices, first, count);
     if (mp.nseg > 0)
     {
       const unsigned G = (unsigned)((mp.ncol * (i64)mp.nseg + kWaves - 1) / kWaves);
@@ -1389,10 +1425,10 @@ void launch_lanczos_fused(const eig_mat_s &A, const double *P, double *Pout, int
                           double *out, int ticket, hipStream_t s, ReduceWS red)
 {
   EIG_CHECK(A.br == 1 && A.bc == 1, EIG_ERR_BLOCKSIZE, "Lanczos driver: 1x1 blocks only");
-  if (!slices && first == 0 && count == A.nslices && !carry && fused_waves() == 8)
+  if (!carry && (fused_waves() == 8 || slices == &kMarchInteriorTag))
   {
     const int mode = image_mode(A);
-    const MarchPlan mp = march_plan(A, mode);
+    const MarchPlan mp = launch_plan(A, mode, slices, first, count);
     if (mp.nseg > 0)
     {
       const unsigned G = (unsigned)((mp.ncol * (i64)mp.nseg + kWaves - 1) / kWaves);
@@ -1450,7 +1486,8 @@ void lanczos_kernel_info(const eig_mat_s &A, bool fused, std::string &name, i64 
     bytes = 8 * (i64)A.sym_nup * n + (i64)A.sym_mask_bytes * n + vec;
     // (distributed launches with a halo take the interior / boundary split, never the march)
     const bool whole = !A.ctx->distributed() || (A.recvs.empty() && A.sends.empty());
-    const bool march = whole && march_plan(A, mode).nseg > 0 && (!fused || fused_waves() == 8);
+    const bool march = whole ? (march_plan(A, mode).nseg > 0 && (!fused || fused_waves() == 8))
+                             : march_split_active(A);
     name = fused ? (march ? "k_lanczos_fused_march" : "k_lanczos_fused_b1")
                  : (march ? "k_lanczos_spmv_march" : "k_lanczos_spmv_b1");
   }
