@@ -781,6 +781,7 @@ struct MarchPlan {
   i64 mrows;    // rows covered by the row mask (nslices * 64)
   int ncol;     // D / 64
   int nseg;     // plane runs per column
+  int wgs;      // y-line grouping stride (columns of the +N offset), 0 = consecutive columns
   // first entries of the far spans (-D, -1) and (+1, +D): offset (0 = empty span) and band array
   i32 dn, dq;
   const double *Un, *Uq;
@@ -792,8 +793,9 @@ struct MarchPlan {
 // generic span loops are compiled out.
 // VAR 1: loads issued offset group by offset group (the far-negative span, then the far-positive
 // span after the near math); VAR 2: the first entry of both far spans is issued with the row's
-// streams, so a 7-point row waits once; VAR 3: VAR 2 + the next plane's streams (mask, the -D/+D
-// value and pair, the 0/+1 values) prefetched while this plane computes.
+// streams, so a 7-point row waits once.  (Measured and dropped: prefetching the next plane's
+// streams, or its far-span operands, one iteration ahead -- both spill in the fused kernel and
+// gave nothing in the others.)
 template <class MT, int KC, int VAR, bool SPAN1, bool NT, class X, class EPI>
 __device__ __forceinline__ void march_rows(const SellB1 &A, const MarchPlan &mp, i64 own, int lane, int wave,
                                            const X &x, EPI &epi)
@@ -807,9 +809,25 @@ __device__ __forceinline__ void march_rows(const SellB1 &A, const MarchPlan &mp,
   const double *U1 = S.val + (i64)S.j1 * S.ld;
   const double *U0 = S.val + (i64)(S.j0 >= 0 ? S.j0 : 0) * S.ld;
   const MT *mask = static_cast<const MT *>(S.mask);
-  const int item = (int)swizzled_block(1) * kWaves + wave;
-  if (item >= mp.ncol * mp.nseg) return;
-  const int col = item % mp.ncol, seg = item / mp.ncol;
+  int col, seg;
+  if (mp.wgs)
+  {
+    // y-line groups: the workgroup's waves take columns c0, c0 + S, c0 + 2S, c0 + 3S (S = the +N
+    // offset in columns), so three of the four +-N neighbour pairs are the workgroup's own rows,
+    // kept in step by one barrier per plane (L1 / L2 hits instead of re-fetches)
+    const int L = (int)swizzled_block(1), per = mp.ncol / kWaves, S = mp.wgs;
+    seg = L / per;
+    if (seg >= mp.nseg) return;  // (whole workgroup)
+    const int blk = L % per;
+    col = (blk / S) * (kWaves * S) + blk % S + wave * S;
+  }
+  else
+  {
+    const int item = (int)swizzled_block(1) * kWaves + wave;
+    if (item >= mp.ncol * mp.nseg) return;
+    col = item % mp.ncol;
+    seg = item / mp.ncol;
+  }
   const int z0 = (int)(mp.zb + seg * mp.nplanes / mp.nseg), z1 = (int)(mp.zb + (seg + 1) * mp.nplanes / mp.nseg);
   auto cx = [&](int g) -> unsigned { return g < 0 ? 0u : (unsigned)(g > xl ? xl : g); };
   auto cv = [&](int g) -> unsigned { return g < 0 ? 0u : (unsigned)(g > ldl ? ldl : g); };
@@ -840,15 +858,12 @@ __device__ __forceinline__ void march_rows(const SellB1 &A, const MarchPlan &mp,
   double amD = UD[cv(w - D)];
   raw pcur = x.load(cx(w));
   Stream cur;
-  if (VAR == 3) load_stream(w, cur);
   const bool edge = lane == 0 || lane == 63;
   for (int z = z0; z < z1; ++z, w += D)
   {
     const int r = w - own32;
     const unsigned wv = (unsigned)(w > ldl ? ldl : w);
-    Stream nxt;
-    if (VAR != 3) load_stream(w, cur);
-    else if (z + 1 < z1) load_stream(w + D, nxt);
+    load_stream(w, cur);
     // lanes 0 / 63: the row across the wave edge (one load for both), and lane 0's mirrored -1 entry
     raw eg;
     double ae = 0.0;
@@ -911,7 +926,7 @@ __device__ __forceinline__ void march_rows(const SellB1 &A, const MarchPlan &mp,
     pmv = vc;
     pcur = cur.pD;
     amD = cur.aD;
-    if (VAR == 3) cur = nxt;
+    if (mp.wgs) __syncthreads();
   }
 }
 
@@ -969,7 +984,7 @@ __global__ __launch_bounds__(kStreamThreads, 8) void k_lanczos_spmv_march(
 
 // Fused one-reduction step on the plane march (per-row arithmetic of k_lanczos_fused_b1).
 template <class MT, int VAR>
-__global__ __launch_bounds__(kStreamThreads, ((VAR & 3) == 3 ? 7 : 8)) void k_lanczos_fused_march(
+__global__ __launch_bounds__(kStreamThreads, ((VAR & 32) ? 7 : 8)) void k_lanczos_fused_march(
     i64 nrows, i64 own, SellB1 A, MarchPlan mp, const dpair *__restrict__ P, dpair *__restrict__ Pout, int k,
     double *__restrict__ nsum, double *__restrict__ alpha, double *__restrict__ beta, const double *__restrict__ red,
     double *__restrict__ out, double *partials, unsigned *ticket)
@@ -1172,16 +1187,21 @@ static int grid_for_slices(K kernel, i64 count, int num_cu)
 
 // EIGMI_MARCH=0 disables the plane-marching kernels; 1 / 2 / 3 pick the load schedule (march_rows
 // VAR; default 2).
-// Default: 1 for the fused step (its pair operands make VAR 2 spill), 2 for SpMV and K1 (measured,
-// tools/lanczos_sweep.py).
-static int march_variant(bool fused = false)
+// Default 2 (measured, tools/lanczos_sweep.py).
+static int march_variant(bool = false)
 {
-  const int def = fused ? 1 : 2;
   const char *e = std::getenv("EIGMI_MARCH");
-  if (!e) return def;
-  return (e[0] >= '0' && e[0] <= '3') ? e[0] - '0' : def;
+  if (!e) return 2;
+  return (e[0] >= '0' && e[0] <= '2') ? e[0] - '0' : 2;
 }
 static bool march_enabled() { return march_variant() != 0; }
+// The fused march is compiled for 7 waves / SIMD (72 VGPRs; at 8 its pair operands spill): -5 %
+// (EIGMI_MARCH_W7=0: the 8-wave build, A/B).
+static int march_w7()
+{
+  const char *e = std::getenv("EIGMI_MARCH_W7");
+  return (e && e[0] == '0') ? 0 : 1;
+}
 // Nontemporal loads for the once-read streams of the march and nontemporal result stores (default;
 // EIGMI_MARCH_NT=0 turns them off): fused step -4 %, K1 -3 %, SpMV -14 % (tools/lanczos_sweep.py).
 static int march_nt()
@@ -1205,27 +1225,29 @@ static bool march_span1(const eig_mat_s &A)
 // Launch a march kernel template KERN<MT, VAR> for the image's mask width and the selected VAR.
 #define EIG_MARCH_LAUNCH(KERN, FUSED, MODE, G, ...)                                                           \
   do {                                                                                                        \
-    const int v0_ = march_variant(FUSED), v_ = v0_ + (march_span1(A) && v0_ >= 2 ? 4 : 0) + 8 * march_nt();   \
+    const int v0_ = march_variant(FUSED);                                                                     \
+    const int v_ = v0_ + (march_span1(A) && v0_ >= 2 ? 4 : 0) + 8 * march_nt() + ((FUSED) ? 32 * march_w7() : 0); \
     if ((MODE) == kSymN8)                                                                                     \
     {                                                                                                         \
       if (v_ == 1) hipLaunchKernelGGL((KERN<uint8_t, 1>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);     \
-      else if (v_ == 3) hipLaunchKernelGGL((KERN<uint8_t, 3>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);\
-      else if (v_ == 6) hipLaunchKernelGGL((KERN<uint8_t, 6>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);\
-      else if (v_ == 7) hipLaunchKernelGGL((KERN<uint8_t, 7>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);\
       else if (v_ == 9) hipLaunchKernelGGL((KERN<uint8_t, 9>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);\
-      else if (v_ == 11) hipLaunchKernelGGL((KERN<uint8_t, 11>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);\
+      else if (v_ == 41) hipLaunchKernelGGL((KERN<uint8_t, 41>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);\
+      else if (v_ == 6) hipLaunchKernelGGL((KERN<uint8_t, 6>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);\
       else if (v_ == 14) hipLaunchKernelGGL((KERN<uint8_t, 14>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);\
-      else if (v_ == 15) hipLaunchKernelGGL((KERN<uint8_t, 15>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);\
+      else if (v_ == 46) hipLaunchKernelGGL((KERN<uint8_t, 46>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);\
       else if (v_ == 10) hipLaunchKernelGGL((KERN<uint8_t, 10>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);\
+      else if (v_ == 42) hipLaunchKernelGGL((KERN<uint8_t, 42>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);\
+      else if (v_ == 38) hipLaunchKernelGGL((KERN<uint8_t, 38>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);\
       else hipLaunchKernelGGL((KERN<uint8_t, 2>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);             \
     }                                                                                                         \
     else                                                                                                      \
     {                                                                                                         \
       if (v_ == 1) hipLaunchKernelGGL((KERN<uint32_t, 1>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);    \
-      else if (v_ == 3) hipLaunchKernelGGL((KERN<uint32_t, 3>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);\
       else if (v_ == 9) hipLaunchKernelGGL((KERN<uint32_t, 9>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);\
-      else if (v_ == 11) hipLaunchKernelGGL((KERN<uint32_t, 11>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);\
+      else if (v_ == 41) hipLaunchKernelGGL((KERN<uint32_t, 41>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);\
       else if (v_ == 10) hipLaunchKernelGGL((KERN<uint32_t, 10>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);\
+      else if (v_ == 42) hipLaunchKernelGGL((KERN<uint32_t, 42>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);\
+      else if (v_ == 34) hipLaunchKernelGGL((KERN<uint32_t, 34>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);\
       else hipLaunchKernelGGL((KERN<uint32_t, 2>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);            \
     }                                                                                                         \
   } while (0)
@@ -1249,7 +1271,7 @@ bool march_geometry(const eig_mat_s &A, i64 &D)
 // the whole matrix.
 static MarchPlan march_plan(const eig_mat_s &A, int mode, i64 zb = 0, i64 ze = -1)
 {
-  MarchPlan mp{0, 0, 0, 0, 0, 0, 0, 0, nullptr, nullptr};
+  MarchPlan mp{0, 0, 0, 0, 0, 0, 0, 0, 0, nullptr, nullptr};
   if (mode != kSymN8 && mode != kSymN32) return mp;
   i64 D;
   if (!march_enabled() || !march_geometry(A, D)) return mp;
@@ -1260,6 +1282,8 @@ static MarchPlan march_plan(const eig_mat_s &A, int mode, i64 zb = 0, i64 ze = -
   const i64 resident = 8LL * 4 * A.ctx->num_cu;  // waves
   i64 nseg = std::max<i64>(1, (resident + ncol - 1) / ncol);
   nseg = std::min<i64>(nseg, nplanes);
+  if (const char *e = std::getenv("EIGMI_MARCH_SEG"))  // (A/B: plane runs per column)
+    if (std::atoi(e) > 0) nseg = std::min<i64>(std::atoi(e), nplanes);
   while (nseg > 1 && (ncol * nseg + kWaves - 1) / kWaves > kMaxRedBlocks) --nseg;
   if ((ncol * nseg + kWaves - 1) / kWaves > kMaxRedBlocks) return mp;
   mp.D = D;
@@ -1274,6 +1298,13 @@ static MarchPlan march_plan(const eig_mat_s &A, int mode, i64 zb = 0, i64 ze = -
   mp.dq = khi < A.sym_nd - 1 ? A.sym_off[khi] : 0;
   mp.Uq = A.sym_val + (i64)(khi < A.sym_nd - 1 ? A.sym_dj[khi] : 0) * A.sym_ld;
   mp.zb = zb;
+  {
+    // y-line grouping (EIGMI_MARCH_WG=1): the +N offset a multiple of 64 and the columns a whole
+    // number of 4-line groups
+    const char *e = std::getenv("EIGMI_MARCH_WG");
+    const i64 S = mp.dq > 0 && mp.dq % 64 == 0 ? mp.dq / 64 : 0;
+    mp.wgs = (e && e[0] == '1' && S > 0 && ncol % (kWaves * S) == 0) ? (int)S : 0;
+  }
   mp.nplanes = nplanes;
   mp.mrows = A.nslices * 64;
   mp.ncol = (int)ncol;
@@ -1299,7 +1330,7 @@ static MarchPlan launch_plan(const eig_mat_s &A, int mode, const i32 *slices, i6
     return mp;
   }
   if (!slices && first == 0 && count == A.nslices) return march_plan(A, mode);
-  return MarchPlan{0, 0, 0, 0, 0, 0, 0, 0, nullptr, nullptr};
+  return MarchPlan{0, 0, 0, 0, 0, 0, 0, 0, 0, nullptr, nullptr};
 }
 
 void launch_spmv(const eig_mat_s &A, const double *x, double *y, const i32 *slices, i64 first, i64 count,

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """A/B of Lanczos step variants on one GPU, interleaved rounds in ONE process (guide rule 24).
 
-Variant spec "<fused|classic>[:swz0|swz1][:w4|w5|w6|w8][:nt0|nt1][:sym0|sym1|sym2][:march0|1|2|3][:mnt0|mnt1]": step form, XCD-aware chunk
+Variant spec "<fused|classic>[:swz0|swz1][:w4|w5|w6|w8][:nt0|nt1][:sym0|sym1|sym2][:march0|1|2|3][:mnt0|mnt1][:wg0|wg1][:seg<k>][:m7|m8]": step form, XCD-aware chunk
 order (EIGMI_XCD_SWIZZLE), register budget of the fused kernel (EIGMI_FUSED_WAVES), nontemporal
 stores of the step vectors (EIGMI_NT_STORE), symmetric band image or SELL image (EIGMI_SYM), plane marching
 (EIGMI_MARCH).  The environment is
@@ -24,9 +24,16 @@ import eigmi  # noqa: E402
 
 def parse(spec):
     parts = spec.split(":")
-    env = {"EIGMI_XCD_SWIZZLE": "0", "EIGMI_FUSED_WAVES": "8", "EIGMI_NT_STORE": "0", "EIGMI_SYM": "2", "EIGMI_MARCH": "d", "EIGMI_MARCH_NT": "1"}
+    env = {"EIGMI_XCD_SWIZZLE": "0", "EIGMI_FUSED_WAVES": "8", "EIGMI_NT_STORE": "0", "EIGMI_SYM": "2", "EIGMI_MARCH": "d", "EIGMI_MARCH_NT": "1",
+           "EIGMI_MARCH_WG": "0", "EIGMI_MARCH_SEG": "0", "EIGMI_MARCH_W7": "1"}
     for p in parts[1:]:
-        if p.startswith("mnt"):
+        if p in ("m7", "m8"):
+            env["EIGMI_MARCH_W7"] = "1" if p == "m7" else "0"
+        elif p.startswith("wg"):
+            env["EIGMI_MARCH_WG"] = p[2:]
+        elif p.startswith("seg"):
+            env["EIGMI_MARCH_SEG"] = p[3:]
+        elif p.startswith("mnt"):
             env["EIGMI_MARCH_NT"] = p[3:]
         elif p.startswith("march"):
             env["EIGMI_MARCH"] = p[5:]
