@@ -1269,7 +1269,7 @@ bool march_geometry(const eig_mat_s &A, i64 &D)
 
 // [zb, ze): plane range of a split launch (the interior planes of a distributed slab); ze < 0 =
 // the whole matrix.
-static MarchPlan march_plan(const eig_mat_s &A, int mode, i64 zb = 0, i64 ze = -1)
+static MarchPlan march_plan(const eig_mat_s &A, int mode, i64 zb = 0, i64 ze = -1, bool fused = false)
 {
   MarchPlan mp{0, 0, 0, 0, 0, 0, 0, 0, 0, nullptr, nullptr};
   if (mode != kSymN8 && mode != kSymN32) return mp;
@@ -1282,6 +1282,10 @@ static MarchPlan march_plan(const eig_mat_s &A, int mode, i64 zb = 0, i64 ze = -
   const i64 resident = 8LL * 4 * A.ctx->num_cu;  // waves
   i64 nseg = std::max<i64>(1, (resident + ncol - 1) / ncol);
   nseg = std::min<i64>(nseg, nplanes);
+  // fused step on wide planes (>= 1024 columns: 3-D grids from 256^2 per plane) with few planes --
+  // the slab of one rank in a strong-scaling run: runs of >= 15 planes beat full occupancy
+  // (256 x 256 x 32 box: 2 runs 33.4 us vs 8 runs 37.8 us; at 256^3 the rule keeps 8 runs)
+  if (fused && ncol >= 1024) nseg = std::max<i64>(1, std::min<i64>(nseg, nplanes / 15));
   if (const char *e = std::getenv("EIGMI_MARCH_SEG"))  // (A/B: plane runs per column)
     if (std::atoi(e) > 0) nseg = std::min<i64>(std::atoi(e), nplanes);
   while (nseg > 1 && (ncol * nseg + kWaves - 1) / kWaves > kMaxRedBlocks) --nseg;
@@ -1321,15 +1325,16 @@ bool march_split_active(const eig_mat_s &A)
 
 // Plan for a launch: the whole matrix (slices == nullptr over all slices), the interior planes of a
 // distributed slab (slices == &kMarchInteriorTag), or none (nseg = 0: the slice kernels run).
-static MarchPlan launch_plan(const eig_mat_s &A, int mode, const i32 *slices, i64 first, i64 count)
+static MarchPlan launch_plan(const eig_mat_s &A, int mode, const i32 *slices, i64 first, i64 count,
+                             bool fused = false)
 {
   if (slices == &kMarchInteriorTag)
   {
-    const MarchPlan mp = march_plan(A, mode, A.mz0, A.mz1);
+    const MarchPlan mp = march_plan(A, mode, A.mz0, A.mz1, fused);
     EIG_CHECK(mp.nseg > 0, EIG_ERR_ARG, "interior-plane launch without a march plan");
     return mp;
   }
-  if (!slices && first == 0 && count == A.nslices) return march_plan(A, mode);
+  if (!slices && first == 0 && count == A.nslices) return march_plan(A, mode, 0, -1, fused);
   return MarchPlan{0, 0, 0, 0, 0, 0, 0, 0, 0, nullptr, nullptr};
 }
 
@@ -1459,7 +1464,7 @@ void launch_lanczos_fused(const eig_mat_s &A, const double *P, double *Pout, int
   if (!carry && (fused_waves() == 8 || slices == &kMarchInteriorTag))
   {
     const int mode = image_mode(A);
-    const MarchPlan mp = launch_plan(A, mode, slices, first, count);
+    const MarchPlan mp = launch_plan(A, mode, slices, first, count, true);
     if (mp.nseg > 0)
     {
       const unsigned G = (unsigned)((mp.ncol * (i64)mp.nseg + kWaves - 1) / kWaves);

@@ -54,11 +54,26 @@ def main():
     ap.add_argument("--variants", default="classic:swz0,classic:swz1,fused:swz0,fused:swz1")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--slab", type=int, default=0, help="N x N x slab box instead of the N^3 cube")
     args = ap.parse_args()
     ctx = eigmi.Context(0)
     N = args.N
-    n = N ** 3
-    rp, c, v = eigmi.gen_matrix(eigmi.GEN_POISSON3D, N)
+    if args.slab:
+        # one rank's share of an 8-way row partition: a standalone N x N x slab 7-point box
+        # (Dirichlet on all faces; no halo), to time the per-GPU compute of the strong-scaling runs
+        import scipy.sparse as sp
+        def lap1(k):
+            return sp.diags([-np.ones(k - 1), np.zeros(k), -np.ones(k - 1)], [-1, 0, 1])
+        Ix, Iz = sp.identity(N), sp.identity(args.slab)
+        A = (sp.kron(Iz, sp.kron(Ix, lap1(N))) + sp.kron(Iz, sp.kron(lap1(N), Ix)) +
+             sp.kron(lap1(args.slab), sp.kron(Ix, Ix))).tocsr()
+        A.setdiag(6.0)
+        A.sort_indices()
+        rp, c, v = A.indptr.astype(np.int64), A.indices.astype(np.int32), A.data.astype(np.float64)
+        n = A.shape[0]
+    else:
+        n = N ** 3
+        rp, c, v = eigmi.gen_matrix(eigmi.GEN_POISSON3D, N)
     nnz = int(rp[-1])
     M = eigmi.Matrix.from_bcsr(ctx, rp, c, v)
     specs = args.variants.split(",")
