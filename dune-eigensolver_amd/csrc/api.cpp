@@ -1112,6 +1112,8 @@ extern "C" int eig_mat_get_info(eig_mat_t A, eig_mat_info *info)
     info->stencil_slices = A->n_stencil_slices;
     info->rows_per_lane = A->R;
     info->sym_offsets = A->sym_val ? A->sym_nd : 0;
+    info->sym_arrays = A->sym_val ? A->sym_nup : 0;
+    info->sym_mask_bytes = A->sym_val ? A->sym_mask_bytes : 0;
   });
 }
 

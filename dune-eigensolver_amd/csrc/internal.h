@@ -235,9 +235,12 @@ void launch_fused_tail(const LanczosState &st, int K, hipStream_t s);
 // launch applies now (split built at upload, image and EIGMI_* switches allow it).  Passing
 // slices == &kMarchInteriorTag to launch_spmv / launch_lanczos_spmv / launch_lanczos_fused marches
 // planes [A.mz0, A.mz1).
-bool march_geometry(const eig_mat_s &A, i64 &D);
+bool march_geometry(const eig_mat_s &A, i64 &D, int chunk = 64);
 bool march_split_active(const eig_mat_s &A);
 extern const i32 kMarchInteriorTag;
+// a2 SpMM (kernels_cpp.hh:626-657) on the band-image plane march for 1x1 matrices whose band
+// qualifies; false (nothing launched) otherwise.  X, Y: window-layout multivectors, m % 8 == 0.
+bool launch_spmm_march(const eig_mat_s &A, i64 m, const double *X, double *Y, hipStream_t s);
 // Kernel a whole-matrix Lanczos step launch picks on this image, and its algorithmic bytes per launch.
 void lanczos_kernel_info(const eig_mat_s &A, bool fused, std::string &name, i64 &bytes);
 void launch_lanczos_spmv(const eig_mat_s &A, const double *u, const double *up, double *t, int j,

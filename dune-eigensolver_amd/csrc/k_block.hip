@@ -559,6 +559,7 @@ void sell_mv8(const eig_mat_s &A, i64 m, const double *X, double *Y, const doubl
 
 int sell_mv8_launches(i64 m)
 {
+  // (the Chebyshev step the caller counts never takes the march)
   const int nblk = (int)(m / 8);
   if (nblk <= 1) return nblk;
   const int kind = mv8_kernel_choice(), per = (kind == 1 || kind == 4) ? 4 : 2;
@@ -567,6 +568,8 @@ int sell_mv8_launches(i64 m)
 
 void launch_sell_mv8(const eig_mat_s &A, i64 m, const double *X, double *Y, hipStream_t s)
 {
+  // symmetric band image with a marchable band (3-D / 2-D stencils): k_spmm8_march (k_spmv.hip)
+  if (launch_spmm_march(A, m, X, Y, s)) return;
   sell_mv8<kStore>(A, m, X, Y, nullptr, nullptr, 0.0, 0.0, s);
 }
 

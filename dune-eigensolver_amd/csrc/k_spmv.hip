@@ -1030,6 +1030,116 @@ __global__ __launch_bounds__(kStreamThreads, ((VAR & 32) ? 7 : 8)) void k_lanczo
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// a2 SpMM Y = A X for one 8-column block of a MultiVector<double,8> (kernels_cpp.hh:626-657) on the
+// band-image plane march.  Lane = (row rq = lane >> 2 of a 16-row wave column, column pair
+// cp = lane & 3): every operand load of the wave reads 16 consecutive X rows = 1 KiB contiguous,
+// the 4 lanes of a row share the row's band values and mask byte (one cache line per wave).  The
+// wave marches its 16-row column through the planes like march_rows: the -D / centre operands are
+// carried, the +D operand loaded once; the +-1 operands (and the mirrored -1 value) come from the
+// lanes 4 apart by ds_bpermute (rows 0 / 15 of the wave load theirs); the +-N operands are L2 hits.
+// Per column, each row sums its stored entries in ascending-column order with separately rounded
+// products and sums: bitwise the reference loop.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ double lane_from(double v, int src_lane)
+{
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_ds_bpermute(src_lane << 2, (int)b);
+  const int hi = __builtin_amdgcn_ds_bpermute(src_lane << 2, (int)(b >> 32));
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+template <class MT>
+__global__ __launch_bounds__(kStreamThreads, 8) void k_spmm8_march(i64 nrows, i64 own, i64 ld, SellB1 A,
+                                                                   MarchPlan mp, const double *__restrict__ X,
+                                                                   double *__restrict__ Y)
+{
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int rq = lane >> 2, cp = lane & 3;
+  const SymImg &S = A.sym;
+  const int xl = (int)A.xlast, D = (int)mp.D, ldl = (int)(S.ld - 1), own32 = (int)own, mrows = (int)mp.mrows;
+  const int nd = S.nd;
+  const double *UD = S.val + (i64)S.dj[nd - 1] * S.ld;
+  const double *U1 = S.val + (i64)S.j1 * S.ld;
+  const double *U0 = S.val + (i64)(S.j0 >= 0 ? S.j0 : 0) * S.ld;
+  const MT *mask = static_cast<const MT *>(S.mask);
+  const int item = (int)swizzled_block(1) * kWaves + wave;
+  if (item >= mp.ncol * mp.nseg) return;
+  const int col = item % mp.ncol, seg = item / mp.ncol;
+  const int z0 = (int)(mp.zb + seg * mp.nplanes / mp.nseg), z1 = (int)(mp.zb + (seg + 1) * mp.nplanes / mp.nseg);
+  // column block blockIdx.y, column pair cp: row g's operand at Xb[g]
+  const dpair *Xb = reinterpret_cast<const dpair *>(X + (i64)blockIdx.y * ld * 8) + cp;
+  dpair *Yb = reinterpret_cast<dpair *>(Y + (i64)blockIdx.y * ld * 8) + cp;
+  auto xat = [&](int g) { return Xb[(unsigned)(g < 0 ? 0 : (g > xl ? xl : g)) * 4u]; };
+  auto cv = [&](int g) -> unsigned { return g < 0 ? 0u : (unsigned)(g > ldl ? ldl : g); };
+  auto fma2 = [](dpair acc, double a, dpair x) { return dpair{acc.x + a * x.x, acc.y + a * x.y}; };
+  const int kn0 = 1, kn1 = S.klo, kp0 = S.khi, kp1 = nd - 1;
+  const bool top = rq == 0, bot = rq == 15;
+  int w = own32 + col * 16 + rq + z0 * D;
+  dpair pm = xat(w - D);
+  double amD = UD[cv(w - D)];
+  dpair pcur = xat(w);
+  for (int z = z0; z < z1; ++z, w += D)
+  {
+    const int r = w - own32;
+    const unsigned wv = (unsigned)(w > ldl ? ldl : w);
+    const unsigned m = r < mrows ? (unsigned)__builtin_nontemporal_load(mask + (unsigned)r) : 0u;
+    const double aD = __builtin_nontemporal_load(UD + wv);
+    const dpair pD = xat(w + D);
+    const double a0 = S.j0 >= 0 ? __builtin_nontemporal_load(U0 + wv) : 0.0;
+    const double ap = __builtin_nontemporal_load(U1 + wv);
+    dpair eg;
+    double ae = 0.0;
+    if (top || bot) eg = xat(top ? w - 1 : w + 1);
+    if (top) ae = U1[cv(w - 1)];
+    double an = 0.0, aq = 0.0;
+    dpair xn, xq;
+    if (mp.dn)
+    {
+      const int g = w + mp.dn;
+      an = mp.Un[cv(g)];
+      xn = xat(g);
+    }
+    if (mp.dq)
+    {
+      aq = mp.Uq[wv];
+      xq = xat(w + mp.dq);
+    }
+    dpair acc{0.0, 0.0};
+    if (m & 1u) acc = fma2(acc, amD, pm);
+    if (mp.dn && ((m >> kn0) & 1u)) acc = fma2(acc, an, xn);
+    for (int k = kn0 + 1; k < kn1; ++k)  // (further far-negative offsets: generic gathers)
+      if ((m >> k) & 1u)
+      {
+        const int g = w + S.off[k];
+        acc = fma2(acc, S.val[(i64)S.dj[k] * S.ld + cv(g)], xat(g));
+      }
+    // rows w -/+ 1: lanes 4 apart (same column pair); the wave's first / last row loads its own
+    const int up = (lane - 4) & 63, dn = (lane + 4) & 63;
+    dpair pl{lane_from(pcur.x, up), lane_from(pcur.y, up)}, pr{lane_from(pcur.x, dn), lane_from(pcur.y, dn)};
+    double am = lane_from(ap, up);
+    if (top)
+    {
+      pl = eg;
+      am = ae;
+    }
+    if (bot) pr = eg;
+    if (S.km1 >= 0 && ((m >> S.km1) & 1u)) acc = fma2(acc, am, pl);
+    if (S.k0 >= 0 && ((m >> S.k0) & 1u)) acc = fma2(acc, a0, pcur);
+    if (S.kp1 >= 0 && ((m >> S.kp1) & 1u)) acc = fma2(acc, ap, pr);
+    if (mp.dq && ((m >> kp0) & 1u)) acc = fma2(acc, aq, xq);
+    for (int k = kp0 + 1; k < kp1; ++k)
+      if ((m >> k) & 1u) acc = fma2(acc, S.val[(i64)S.dj[k] * S.ld + wv], xat(w + S.off[k]));
+    if ((m >> kp1) & 1u) acc = fma2(acc, aD, pD);
+    if (r < nrows) __builtin_nontemporal_store(acc, Yb + (unsigned)w * 4u);
+    pm = pcur;
+    pcur = pD;
+    amD = aD;
+  }
+}
+
+bool launch_spmm_march(const eig_mat_s &A, i64 m, const double *X, double *Y, hipStream_t s);
+
 // After the last fused step K-1: alpha[K-1], nsum[K], beta[K] (same formulas as the prologue).
 __global__ void k_fused_tail(double *nsum, double *alpha, double *beta, const double *red, int K)
 {
@@ -1257,28 +1367,30 @@ static bool march_span1(const eig_mat_s &A)
 // at least 4 planes.  Plane runs per column: enough items for one resident wave per SIMD slot
 // (8 per SIMD), at most kMaxRedBlocks workgroups.
 // Band geometry the march needs (independent of the EIGMI_* switches): widest offset D.
-bool march_geometry(const eig_mat_s &A, i64 &D)
+bool march_geometry(const eig_mat_s &A, i64 &D, int chunk)
 {
   D = 0;
   if (!A.sym_val || A.R != 1 || A.sym_nd < 3) return false;
   bool near = false;
   for (int k = 0; k < A.sym_nd; ++k) near = near || A.sym_off[k] == 1 || A.sym_off[k] == -1;
   D = A.sym_off[A.sym_nd - 1];
-  return near && D > 1 && D % 64 == 0 && A.sym_off[0] == -D;
+  return near && D > 1 && D % chunk == 0 && A.sym_off[0] == -D;
 }
 
 // [zb, ze): plane range of a split launch (the interior planes of a distributed slab); ze < 0 =
 // the whole matrix.
-static MarchPlan march_plan(const eig_mat_s &A, int mode, i64 zb = 0, i64 ze = -1, bool fused = false)
+// chunk: rows per wave column (64 for the scalar kernels, 16 for the 8-column SpMM).
+static MarchPlan march_plan(const eig_mat_s &A, int mode, i64 zb = 0, i64 ze = -1, bool fused = false,
+                            int chunk = 64)
 {
   MarchPlan mp{0, 0, 0, 0, 0, 0, 0, 0, 0, nullptr, nullptr};
   if (mode != kSymN8 && mode != kSymN32) return mp;
   i64 D;
-  if (!march_enabled() || !march_geometry(A, D)) return mp;
+  if (!march_enabled() || !march_geometry(A, D, chunk)) return mp;
   if (ze < 0) ze = (A.nb_rows + D - 1) / D;
   const i64 nplanes = ze - zb;
   if (nplanes < 2 || (zb == 0 && nplanes < 4)) return mp;
-  const i64 ncol = D / 64;
+  const i64 ncol = D / chunk;
   const i64 resident = 8LL * 4 * A.ctx->num_cu;  // waves
   i64 nseg = std::max<i64>(1, (resident + ncol - 1) / ncol);
   nseg = std::min<i64>(nseg, nplanes);
@@ -1306,7 +1418,7 @@ static MarchPlan march_plan(const eig_mat_s &A, int mode, i64 zb = 0, i64 ze = -
     // y-line grouping (EIGMI_MARCH_WG=1): the +N offset a multiple of 64 and the columns a whole
     // number of 4-line groups
     const char *e = std::getenv("EIGMI_MARCH_WG");
-    const i64 S = mp.dq > 0 && mp.dq % 64 == 0 ? mp.dq / 64 : 0;
+    const i64 S = mp.dq > 0 && mp.dq % chunk == 0 ? mp.dq / chunk : 0;
     mp.wgs = (e && e[0] == '1' && S > 0 && ncol % (kWaves * S) == 0) ? (int)S : 0;
   }
   mp.nplanes = nplanes;
@@ -1511,6 +1623,23 @@ void launch_lanczos_fused(const eig_mat_s &A, const double *P, double *Pout, int
 void launch_fused_tail(const LanczosState &st, int K, hipStream_t s)
 {
   hipLaunchKernelGGL(k_fused_tail, dim3(1), dim3(64), 0, s, st.nsum, st.alpha, st.beta, st.fred, K);
+}
+
+bool launch_spmm_march(const eig_mat_s &A, i64 m, const double *X, double *Y, hipStream_t s)
+{
+  if (A.br != 1 || A.bc != 1 || m <= 0) return false;
+  const int mode = image_mode(A);
+  const MarchPlan mp = march_plan(A, mode, 0, -1, false, 16);
+  if (mp.nseg == 0) return false;
+  const unsigned G = (unsigned)((mp.ncol * (i64)mp.nseg + kWaves - 1) / kWaves);
+  const dim3 grid(G, (unsigned)(m / 8));
+  if (mode == kSymN8)
+    hipLaunchKernelGGL(k_spmm8_march<uint8_t>, grid, dim3(kStreamThreads), 0, s, A.nb_rows, A.own_offset, A.window,
+                       sell_b1(A), mp, X, Y);
+  else
+    hipLaunchKernelGGL(k_spmm8_march<uint32_t>, grid, dim3(kStreamThreads), 0, s, A.nb_rows, A.own_offset, A.window,
+                       sell_b1(A), mp, X, Y);
+  return true;
 }
 
 void lanczos_kernel_info(const eig_mat_s &A, bool fused, std::string &name, i64 &bytes)

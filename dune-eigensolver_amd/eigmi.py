@@ -47,7 +47,8 @@ class _MatInfo(ctypes.Structure):
                                               "nnzb_padded", "nslices")] + \
                [("br", ctypes.c_int), ("bc", ctypes.c_int)] + \
                [(k, ctypes.c_int64) for k in ("halo_recv", "halo_send", "device_bytes", "stencil_slices",
-                                              "rows_per_lane", "sym_offsets")]
+                                              "rows_per_lane", "sym_offsets", "sym_arrays",
+                                              "sym_mask_bytes")]
 
 
 class BlockTiming(ctypes.Structure):
@@ -728,6 +729,22 @@ def row_partition(n, nranks, rank, align=1):
 # Algorithmic byte models (DESIGN.md "Roofline accounting")
 def bytes_spmv(n, nnz):
     return 12 * nnz + 4 * (n + 1) + 16 * n
+
+
+def image_bytes(M, op, m=8):
+    """Algorithmic HBM bytes of one launch sequence on M's device image:
+    op "spmv" (y = A x) or "spmm" (m columns).  The symmetric band image streams 8 B per band slot
+    and the row mask once per 8-column block (the plane march); other images the SURVEY 8(d) CSR
+    count (12 B per nonzero + row pointers), which the SELL/stencil kernels stream at most."""
+    info = M.info
+    n, nnz = info.n, info.nnzb
+    band = info.sym_offsets > 0
+    mat = (8 * info.sym_arrays + info.sym_mask_bytes) * n if band else 12 * nnz + 4 * (n + 1)
+    if op == "spmv":
+        return mat + 16 * n
+    if op == "spmm":
+        return (m // 8 if band else 1) * mat + 16 * m * n
+    raise ValueError(op)
 
 
 def bytes_lanczos_step(n, nnz):

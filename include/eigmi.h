@@ -132,6 +132,8 @@ typedef struct eig_mat_info {
   int64_t rows_per_lane;  /* R of the SELL-C image (C = 64 R) */
   int64_t sym_offsets;    /* offsets of the symmetric band image (0 = none; the scalar SpMV and
                              Lanczos kernels then read the upper-triangle band arrays) */
+  int64_t sym_arrays;     /* band arrays (distinct |offset|), 8 B per row each */
+  int64_t sym_mask_bytes; /* row-mask bytes per row (1 or 4) */
 } eig_mat_info;
 int eig_mat_get_info(eig_mat_t mat, eig_mat_info *info);
 

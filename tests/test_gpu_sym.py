@@ -168,3 +168,25 @@ def test_march_lanczos_partial_plane(ctx, fused):
     a1, b1, _ = eigmi.lanczos_run(Ms, 30, seed=9, fused=fused)
     a2, b2, _ = eigmi.lanczos_run(Mp, 30, seed=9, fused=fused)
     assert np.allclose(a1, a2, rtol=1e-11, atol=1e-13) and np.allclose(b1, b2, rtol=1e-11, atol=1e-13)
+
+
+# ---- a2 SpMM on the band march (k_spmm8_march): 16-row wave columns, D a multiple of 16 ----
+
+@pytest.mark.parametrize("mat,m", [
+    ("poisson16", 8), ("poisson16", 24), ("laplace64", 16),
+    ("band_partial", 8),     # 5000 rows, D = 144: partial last plane
+    ("band_u32", 16),        # 23 offsets (u32 masks), structurally unsymmetric
+    ("band_no_pm1", 8),      # no +-1: not marched (row kernels)
+])
+def test_march_spmm_bitwise(ctx, mat, m):
+    A = {"poisson16": lambda: oracle.poisson3d(16),
+         "laplace64": lambda: oracle.laplace2d(64),
+         "band_partial": lambda: band_matrix(5000, [0, 1, 12, 144], 21),
+         "band_u32": lambda: band_matrix(3000, [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 48], 22, drop=0.1),
+         "band_no_pm1": lambda: band_matrix(3000, [0, 2, 64], 23)}[mat]()
+    M = upload(ctx, A)
+    assert M.info.sym_offsets > 0
+    Qh = oracle.random_mv8(A.n, m, 5)
+    Q, Y = ctx.array(Qh), ctx.zeros(A.n * m)
+    eigmi.spmm_mv8(M, m, Q, Y)
+    assert np.array_equal(Y.get(), oracle.spmm_mv8(A, Qh, m))
