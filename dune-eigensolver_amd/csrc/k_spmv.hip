@@ -1049,12 +1049,16 @@ __device__ __forceinline__ double lane_from(double v, int src_lane)
   return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
-template <class MT>
+// NBW column blocks per workgroup (1, 2, 4): the workgroup's waves take the same rows for NBW
+// blocks (block blockIdx.y * NBW + wave % NBW), so the band values and masks they stream are read
+// from HBM once per NBW blocks (the other waves' loads hit L1 / L2).
+template <class MT, int NBW>
 __global__ __launch_bounds__(kStreamThreads, 8) void k_spmm8_march(i64 nrows, i64 own, i64 ld, SellB1 A,
                                                                    MarchPlan mp, const double *__restrict__ X,
                                                                    double *__restrict__ Y)
 {
-  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63, wv_ = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wave = wv_ / NBW, qb = (int)blockIdx.y * NBW + wv_ % NBW;  // (row column, column block)
   const int rq = lane >> 2, cp = lane & 3;
   const SymImg &S = A.sym;
   const int xl = (int)A.xlast, D = (int)mp.D, ldl = (int)(S.ld - 1), own32 = (int)own, mrows = (int)mp.mrows;
@@ -1063,13 +1067,13 @@ __global__ __launch_bounds__(kStreamThreads, 8) void k_spmm8_march(i64 nrows, i6
   const double *U1 = S.val + (i64)S.j1 * S.ld;
   const double *U0 = S.val + (i64)(S.j0 >= 0 ? S.j0 : 0) * S.ld;
   const MT *mask = static_cast<const MT *>(S.mask);
-  const int item = (int)swizzled_block(1) * kWaves + wave;
+  const int item = (int)swizzled_block(1) * (kWaves / NBW) + wave;
   if (item >= mp.ncol * mp.nseg) return;
   const int col = item % mp.ncol, seg = item / mp.ncol;
   const int z0 = (int)(mp.zb + seg * mp.nplanes / mp.nseg), z1 = (int)(mp.zb + (seg + 1) * mp.nplanes / mp.nseg);
-  // column block blockIdx.y, column pair cp: row g's operand at Xb[g]
-  const dpair *Xb = reinterpret_cast<const dpair *>(X + (i64)blockIdx.y * ld * 8) + cp;
-  dpair *Yb = reinterpret_cast<dpair *>(Y + (i64)blockIdx.y * ld * 8) + cp;
+  // column block qb, column pair cp: row g's operand at Xb[g]
+  const dpair *Xb = reinterpret_cast<const dpair *>(X + (i64)qb * ld * 8) + cp;
+  dpair *Yb = reinterpret_cast<dpair *>(Y + (i64)qb * ld * 8) + cp;
   auto xat = [&](int g) { return Xb[(unsigned)(g < 0 ? 0 : (g > xl ? xl : g)) * 4u]; };
   auto cv = [&](int g) -> unsigned { return g < 0 ? 0u : (unsigned)(g > ldl ? ldl : g); };
   auto fma2 = [](dpair acc, double a, dpair x) { return dpair{acc.x + a * x.x, acc.y + a * x.y}; };
@@ -1631,14 +1635,33 @@ bool launch_spmm_march(const eig_mat_s &A, i64 m, const double *X, double *Y, hi
   const int mode = image_mode(A);
   const MarchPlan mp = march_plan(A, mode, 0, -1, false, 16);
   if (mp.nseg == 0) return false;
-  const unsigned G = (unsigned)((mp.ncol * (i64)mp.nseg + kWaves - 1) / kWaves);
-  const dim3 grid(G, (unsigned)(m / 8));
+  const i64 nblk = m / 8;
+  // one column block per workgroup: sharing the band stream between 2 / 4 blocks measured equal /
+  // 6 % slower (m = 32 at 256^3: 2716 / 2720 / 2894 us) -- the vector streams bound the launch
+  int nbw = 1;
+  if (const char *e = std::getenv("EIGMI_SPMM_NBW"))  // (A/B: column blocks per workgroup)
+  {
+    const int v = std::atoi(e);
+    if ((v == 1 || v == 2 || v == 4) && nblk % v == 0) nbw = v;
+  }
+  const i64 items = mp.ncol * (i64)mp.nseg, per = kWaves / nbw;
+  const dim3 grid((unsigned)((items + per - 1) / per), (unsigned)(nblk / nbw));
+#define EIG_SPMM(MT_, NB_)                                                                                      \
+  hipLaunchKernelGGL((k_spmm8_march<MT_, NB_>), grid, dim3(kStreamThreads), 0, s, A.nb_rows, A.own_offset, A.window, \
+                     sell_b1(A), mp, X, Y)
   if (mode == kSymN8)
-    hipLaunchKernelGGL(k_spmm8_march<uint8_t>, grid, dim3(kStreamThreads), 0, s, A.nb_rows, A.own_offset, A.window,
-                       sell_b1(A), mp, X, Y);
+  {
+    if (nbw == 4) EIG_SPMM(uint8_t, 4);
+    else if (nbw == 2) EIG_SPMM(uint8_t, 2);
+    else EIG_SPMM(uint8_t, 1);
+  }
   else
-    hipLaunchKernelGGL(k_spmm8_march<uint32_t>, grid, dim3(kStreamThreads), 0, s, A.nb_rows, A.own_offset, A.window,
-                       sell_b1(A), mp, X, Y);
+  {
+    if (nbw == 4) EIG_SPMM(uint32_t, 4);
+    else if (nbw == 2) EIG_SPMM(uint32_t, 2);
+    else EIG_SPMM(uint32_t, 1);
+  }
+#undef EIG_SPMM
   return true;
 }
 
