@@ -243,7 +243,7 @@ extern "C" int eig_device_count(int *count)
   });
 }
 
-extern "C" const char *eig_version(void) { return "eigmi 0.1 gfx950 (SELL-64 SpMV, MFMA f64 Gram, RCCL halo)"; }
+extern "C" const char *eig_version(void) { return "eigmi 0.2 gfx950 (band-image plane march SpMV / Lanczos / SpMM, SELL-64, MFMA f64 Gram, RCCL halo)"; }
 
 extern "C" int eig_ctx_create(int device, eig_ctx_t *out)
 {
