@@ -1134,6 +1134,18 @@ extern "C" int eig_lanczos_kernel_info(eig_mat_t A, int fused, char *name, int n
   });
 }
 
+extern "C" int eig_mat_kernel_info(eig_mat_t A, int op, char *name, int name_len)
+{
+  return guard(A ? A->ctx : nullptr, [&] {
+    EIG_CHECK(A && name && name_len > 0, EIG_ERR_ARG, "eig_mat_kernel_info: null argument");
+    EIG_CHECK(op >= EIG_OP_SPMV && op <= EIG_OP_CHEB8, EIG_ERR_ARG, "eig_mat_kernel_info: bad op");
+    const std::string nm = kernel_for(*A, op);
+    const size_t k = std::min<size_t>(nm.size(), (size_t)name_len - 1);
+    std::memcpy(name, nm.data(), k);
+    name[k] = 0;
+  });
+}
+
 extern "C" int eig_mat_shift_diag(eig_mat_t A, double shift)
 {
   return guard(A ? A->ctx : nullptr, [&] {

@@ -241,8 +241,13 @@ extern const i32 kMarchInteriorTag;
 // a2 SpMM (kernels_cpp.hh:626-657) on the band-image plane march for 1x1 matrices whose band
 // qualifies; false (nothing launched) otherwise.  X, Y: window-layout multivectors, m % 8 == 0.
 bool launch_spmm_march(const eig_mat_s &A, i64 m, const double *X, double *Y, hipStream_t s);
+// Chebyshev step (k_block.hip kCheb semantics) on the general band march; false when not applicable.
+bool launch_cheb_march(const eig_mat_s &M, i64 m, const double *Xk, double *Xold, const double *B, const double *dinv,
+                       double omega, double gamma, hipStream_t s);
 // Kernel a whole-matrix Lanczos step launch picks on this image, and its algorithmic bytes per launch.
 void lanczos_kernel_info(const eig_mat_s &A, bool fused, std::string &name, i64 &bytes);
+// Kernel family a whole-matrix launch of `op` (eig_mat_kernel_info's EIG_OP_*) picks on this image.
+std::string kernel_for(const eig_mat_s &A, int op);
 void launch_lanczos_spmv(const eig_mat_s &A, const double *u, const double *up, double *t, int j,
                          const LanczosState &st, const i32 *slices, i64 first, i64 count, double *dot_out,
                          double *beta_out, const double *carry, int ticket, hipStream_t s, ReduceWS red);

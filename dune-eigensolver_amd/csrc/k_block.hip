@@ -576,6 +576,8 @@ void launch_sell_mv8(const eig_mat_s &A, i64 m, const double *X, double *Y, hipS
 void launch_cheb_step(const eig_mat_s &M, i64 m, const double *Xk, double *Xold, const double *B, const double *dinv,
                       double omega, double gamma, hipStream_t s)
 {
+  // symmetric band image with a marchable band (the P1 mass matrix of config C5): k_spmm8_marchg
+  if (launch_cheb_march(M, m, Xk, Xold, B, dinv, omega, gamma, s)) return;
   sell_mv8<kCheb>(M, m, Xk, Xold, B, dinv, omega, gamma, s);
 }
 

@@ -1144,6 +1144,146 @@ __global__ __launch_bounds__(kStreamThreads, 8) void k_spmm8_march(i64 nrows, i6
 
 bool launch_spmm_march(const eig_mat_s &A, i64 m, const double *X, double *Y, hipStream_t s);
 
+// ---------------------------------------------------------------------------------------------
+// General band march for the 8-column SpMM and the fused Chebyshev step (k_spmm8_marchg).  The
+// carried offset P is the widest band offset that is a multiple of 16 with -P stored too (3-D P1
+// on the Kuhn split: P = N^2 + N); the others split into four spans of gathered offsets -- S1 below
+// -P, S2 in (-P, -1), S3 in (+1, +P), S4 above +P -- of at most kGSpan offsets each, loaded
+// predicated and unrolled (gathered operand + band value, the mirrored slot for negative offsets),
+// S1 / S2 with the row's streams and S3 / S4 after the near terms.  Accumulation in ascending
+// offset order: S1, -P, S2, -1, 0, +1, S3, +P, S4.  EPI = kStore: separately rounded products
+// and sums over the stored entries (bitwise the reference SpMM); kGCheb: fused multiply-adds and
+// the Chebyshev update of k_sell_mv8q's kCheb epilogue (tolerance-checked).
+// ---------------------------------------------------------------------------------------------
+constexpr int kGSpan = 3;
+enum { kGStore = 0, kGCheb = 1 };
+
+struct GSpans {
+  int kPm, kPp;                      // mask bits of -P / +P
+  int s1b, s1e, s2b, s2e, s3b, s3e, s4b, s4e;
+};
+
+template <class X>
+__device__ __forceinline__ void gspan_load(const SymImg &S, int kb, int ke, int w, unsigned wv, int xl, int ldl,
+                                           const X &xat, double (&a)[kGSpan], dpair (&x)[kGSpan])
+{
+#pragma unroll
+  for (int k = 0; k < kGSpan; ++k)
+  {
+    const bool in = kb + k < ke;
+    const int d = in ? S.off[kb + k] : 0;
+    int g = w + d;
+    g = g < 0 ? 0 : (g > xl ? xl : g);
+    const unsigned gv = (unsigned)(g > ldl ? ldl : g);
+    a[k] = in ? S.val[(i64)S.dj[kb + k] * S.ld + (d < 0 ? gv : wv)] : 0.0;
+    x[k] = in ? xat(g) : dpair{0.0, 0.0};
+  }
+}
+
+template <int EPI>
+__device__ __forceinline__ dpair gacc(dpair acc, double a, dpair x)
+{
+  if (EPI == kGStore) return dpair{acc.x + a * x.x, acc.y + a * x.y};
+  return dpair{__builtin_fma(a, x.x, acc.x), __builtin_fma(a, x.y, acc.y)};
+}
+
+template <int EPI>
+__device__ __forceinline__ void gspan_acc(int kb, int ke, unsigned m, const double (&a)[kGSpan],
+                                          const dpair (&x)[kGSpan], dpair &acc)
+{
+#pragma unroll
+  for (int k = 0; k < kGSpan; ++k)
+    if (kb + k < ke && ((m >> (kb + k)) & 1u)) acc = gacc<EPI>(acc, a[k], x[k]);
+}
+
+template <class MT, int EPI>
+__global__ __launch_bounds__(kStreamThreads, 6) void k_spmm8_marchg(
+    i64 nrows, i64 own, i64 ld, SellB1 A, MarchPlan mp, GSpans sp, const double *__restrict__ X,
+    double *__restrict__ Y, const double *__restrict__ Bv, const double *__restrict__ dinv, double omega,
+    double gamma)
+{
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int rq = lane >> 2, cp = lane & 3;
+  const SymImg &S = A.sym;
+  const int xl = (int)A.xlast, P = (int)mp.D, ldl = (int)(S.ld - 1), own32 = (int)own, mrows = (int)mp.mrows;
+  const double *UP = S.val + (i64)S.dj[sp.kPp] * S.ld;
+  const double *U1 = S.val + (i64)S.j1 * S.ld;
+  const double *U0 = S.val + (i64)(S.j0 >= 0 ? S.j0 : 0) * S.ld;
+  const MT *mask = static_cast<const MT *>(S.mask);
+  const int item = (int)swizzled_block(1) * kWaves + wave;
+  if (item >= mp.ncol * mp.nseg) return;
+  const int col = item % mp.ncol, seg = item / mp.ncol;
+  const int z0 = (int)(mp.zb + seg * mp.nplanes / mp.nseg), z1 = (int)(mp.zb + (seg + 1) * mp.nplanes / mp.nseg);
+  const i64 boff = (i64)blockIdx.y * ld * 8;
+  const dpair *Xb = reinterpret_cast<const dpair *>(X + boff) + cp;
+  dpair *Yb = reinterpret_cast<dpair *>(Y + boff) + cp;
+  const dpair *Bb = EPI == kGCheb ? reinterpret_cast<const dpair *>(Bv + boff) + cp : nullptr;
+  auto xat = [&](int g) { return Xb[(unsigned)(g < 0 ? 0 : (g > xl ? xl : g)) * 4u]; };
+  auto cv = [&](int g) -> unsigned { return g < 0 ? 0u : (unsigned)(g > ldl ? ldl : g); };
+  const bool top = rq == 0, bot = rq == 15;
+  int w = own32 + col * 16 + rq + z0 * P;
+  dpair pm = xat(w - P);
+  double amP = UP[cv(w - P)];
+  dpair pcur = xat(w);
+  for (int z = z0; z < z1; ++z, w += P)
+  {
+    const int r = w - own32;
+    const unsigned wv = (unsigned)(w > ldl ? ldl : w);
+    const unsigned m = r < mrows ? (unsigned)__builtin_nontemporal_load(mask + (unsigned)r) : 0u;
+    const double aP = __builtin_nontemporal_load(UP + wv);
+    const dpair pP = xat(w + P);
+    const double a0 = S.j0 >= 0 ? __builtin_nontemporal_load(U0 + wv) : 0.0;
+    const double ap = __builtin_nontemporal_load(U1 + wv);
+    dpair eg;
+    double ae = 0.0;
+    if (top || bot) eg = xat(top ? w - 1 : w + 1);
+    if (top) ae = U1[cv(w - 1)];
+    double a1[kGSpan], a2[kGSpan];
+    dpair x1[kGSpan], x2[kGSpan];
+    gspan_load(S, sp.s1b, sp.s1e, w, wv, xl, ldl, xat, a1, x1);
+    gspan_load(S, sp.s2b, sp.s2e, w, wv, xl, ldl, xat, a2, x2);
+    dpair acc{0.0, 0.0};
+    gspan_acc<EPI>(sp.s1b, sp.s1e, m, a1, x1, acc);
+    if ((m >> sp.kPm) & 1u) acc = gacc<EPI>(acc, amP, pm);
+    gspan_acc<EPI>(sp.s2b, sp.s2e, m, a2, x2, acc);
+    const int up = (lane - 4) & 63, dn = (lane + 4) & 63;
+    dpair pl{lane_from(pcur.x, up), lane_from(pcur.y, up)}, pr{lane_from(pcur.x, dn), lane_from(pcur.y, dn)};
+    double am = lane_from(ap, up);
+    if (top)
+    {
+      pl = eg;
+      am = ae;
+    }
+    if (bot) pr = eg;
+    if (S.km1 >= 0 && ((m >> S.km1) & 1u)) acc = gacc<EPI>(acc, am, pl);
+    if (S.k0 >= 0 && ((m >> S.k0) & 1u)) acc = gacc<EPI>(acc, a0, pcur);
+    if (S.kp1 >= 0 && ((m >> S.kp1) & 1u)) acc = gacc<EPI>(acc, ap, pr);
+    gspan_load(S, sp.s3b, sp.s3e, w, wv, xl, ldl, xat, a1, x1);
+    gspan_load(S, sp.s4b, sp.s4e, w, wv, xl, ldl, xat, a2, x2);
+    gspan_acc<EPI>(sp.s3b, sp.s3e, m, a1, x1, acc);
+    if ((m >> sp.kPp) & 1u) acc = gacc<EPI>(acc, aP, pP);
+    gspan_acc<EPI>(sp.s4b, sp.s4e, m, a2, x2, acc);
+    if (r < nrows)
+    {
+      if (EPI == kGStore)
+        __builtin_nontemporal_store(acc, Yb + (unsigned)w * 4u);
+      else
+      {
+        const double di = __builtin_nontemporal_load(dinv + r);
+        const dpair bb = __builtin_nontemporal_load(Bb + (unsigned)w * 4u);
+        const dpair xo = __builtin_nontemporal_load(Yb + (unsigned)w * 4u);
+        const double gd = gamma * di;
+        const double o0 = omega * (pcur.x + gd * (bb.x - acc.x) - xo.x) + xo.x;
+        const double o1 = omega * (pcur.y + gd * (bb.y - acc.y) - xo.y) + xo.y;
+        __builtin_nontemporal_store(dpair{o0, o1}, Yb + (unsigned)w * 4u);
+      }
+    }
+    pm = pcur;
+    pcur = pP;
+    amP = aP;
+  }
+}
+
 // After the last fused step K-1: alpha[K-1], nsum[K], beta[K] (same formulas as the prologue).
 __global__ void k_fused_tail(double *nsum, double *alpha, double *beta, const double *red, int K)
 {
@@ -1629,12 +1769,98 @@ void launch_fused_tail(const LanczosState &st, int K, hipStream_t s)
   hipLaunchKernelGGL(k_fused_tail, dim3(1), dim3(64), 0, s, st.nsum, st.alpha, st.beta, st.fred, K);
 }
 
+// General band geometry for k_spmm8_marchg: carried offset P (widest multiple of 16 with -P stored),
+// +-1 stored, every span at most kGSpan offsets.  False when the band does not qualify.
+static bool gspans(const eig_mat_s &A, i64 &P, GSpans &sp)
+{
+  if (!A.sym_val || A.R != 1 || A.sym_nd < 3) return false;
+  const int nd = A.sym_nd;
+  auto kof = [&](i64 d) {
+    for (int k = 0; k < nd; ++k)
+      if (A.sym_off[k] == d) return k;
+    return -1;
+  };
+  if (kof(1) < 0 || kof(-1) < 0) return false;
+  int klo = nd, khi = nd;
+  for (int k = nd - 1; k >= 0; --k)
+  {
+    if (A.sym_off[k] >= -1) klo = k;
+    if (A.sym_off[k] > 1) khi = k;
+  }
+  // candidates for P from the widest down; the first whose four spans fit
+  for (int kp = nd - 1; kp >= khi; --kp)
+  {
+    const i64 d = A.sym_off[kp];
+    if (d % 16 != 0 || kof(-d) < 0) continue;
+    sp.kPm = kof(-d);
+    sp.kPp = kp;
+    sp.s1b = 0, sp.s1e = sp.kPm;
+    sp.s2b = sp.kPm + 1, sp.s2e = klo;
+    sp.s3b = khi, sp.s3e = sp.kPp;
+    sp.s4b = sp.kPp + 1, sp.s4e = nd;
+    if (sp.s1e - sp.s1b <= kGSpan && sp.s2e - sp.s2b <= kGSpan && sp.s3e - sp.s3b <= kGSpan &&
+        sp.s4e - sp.s4b <= kGSpan)
+    {
+      P = d;
+      return true;
+    }
+  }
+  return false;
+}
+
+// EIGMI_MARCHG=0 disables the general-band march (SpMM of non-extreme carried bands, Chebyshev).
+static bool marchg_enabled()
+{
+  const char *e = std::getenv("EIGMI_MARCHG");
+  return march_enabled() && !(e && e[0] == '0');
+}
+
+template <int EPI>
+static bool launch_marchg(const eig_mat_s &A, i64 m, const double *X, double *Y, const double *Bv,
+                          const double *dinv, double omega, double gamma, hipStream_t s)
+{
+  if (A.br != 1 || A.bc != 1 || m <= 0 || !marchg_enabled()) return false;
+  const int mode = image_mode(A);
+  if (mode != kSymN8 && mode != kSymN32) return false;
+  i64 P;
+  GSpans sp;
+  if (!gspans(A, P, sp)) return false;
+  const i64 nplanes = (A.nb_rows + P - 1) / P;
+  if (nplanes < 4) return false;
+  const i64 ncol = P / 16;
+  const i64 resident = 6LL * 4 * A.ctx->num_cu;  // waves at the kernel's 6 waves / SIMD
+  i64 nseg = std::min<i64>(std::max<i64>(1, (resident + ncol - 1) / ncol), nplanes);
+  if (const char *e = std::getenv("EIGMI_MARCH_SEG"))
+    if (std::atoi(e) > 0) nseg = std::min<i64>(std::atoi(e), nplanes);
+  MarchPlan mp{0, 0, 0, 0, 0, 0, 0, 0, 0, nullptr, nullptr};
+  mp.D = P;
+  mp.zb = 0;
+  mp.nplanes = nplanes;
+  mp.mrows = A.nslices * 64;
+  mp.ncol = (int)ncol;
+  mp.nseg = (int)nseg;
+  const dim3 grid((unsigned)((ncol * nseg + kWaves - 1) / kWaves), (unsigned)(m / 8));
+  if (mode == kSymN8)
+    hipLaunchKernelGGL((k_spmm8_marchg<uint8_t, EPI>), grid, dim3(kStreamThreads), 0, s, A.nb_rows, A.own_offset,
+                       A.window, sell_b1(A), mp, sp, X, Y, Bv, dinv, omega, gamma);
+  else
+    hipLaunchKernelGGL((k_spmm8_marchg<uint32_t, EPI>), grid, dim3(kStreamThreads), 0, s, A.nb_rows, A.own_offset,
+                       A.window, sell_b1(A), mp, sp, X, Y, Bv, dinv, omega, gamma);
+  return true;
+}
+
+bool launch_cheb_march(const eig_mat_s &M, i64 m, const double *Xk, double *Xold, const double *B, const double *dinv,
+                       double omega, double gamma, hipStream_t s)
+{
+  return launch_marchg<kGCheb>(M, m, Xk, Xold, B, dinv, omega, gamma, s);
+}
+
 bool launch_spmm_march(const eig_mat_s &A, i64 m, const double *X, double *Y, hipStream_t s)
 {
   if (A.br != 1 || A.bc != 1 || m <= 0) return false;
   const int mode = image_mode(A);
   const MarchPlan mp = march_plan(A, mode, 0, -1, false, 16);
-  if (mp.nseg == 0) return false;
+  if (mp.nseg == 0) return launch_marchg<kGStore>(A, m, X, Y, nullptr, nullptr, 0.0, 0.0, s);
   const i64 nblk = m / 8;
   // one column block per workgroup: sharing the band stream between 2 / 4 blocks measured equal /
   // 6 % slower (m = 32 at 256^3: 2716 / 2720 / 2894 us) -- the vector streams bound the launch
@@ -1683,6 +1909,39 @@ void lanczos_kernel_info(const eig_mat_s &A, bool fused, std::string &name, i64 
   {
     bytes = 12 * A.nnzb + 4 * (n + 1) + vec;
     name = fused ? "k_lanczos_fused_b1" : "k_lanczos_spmv_b1";
+  }
+}
+
+std::string kernel_for(const eig_mat_s &A, int op)
+{
+  const bool b1 = A.br == 1 && A.bc == 1;
+  const int mode = b1 ? image_mode(A) : kExplicit;
+  const bool whole = !A.ctx->distributed() || (A.recvs.empty() && A.sends.empty());
+  std::string name;
+  i64 bytes;
+  switch (op)
+  {
+    case 0:
+      if (!b1) return "k_spmv_blk";
+      return (whole ? march_plan(A, mode).nseg > 0 : march_split_active(A)) ? "k_spmv_march" : "k_spmv_b1";
+    case 1:
+    case 2:
+      lanczos_kernel_info(A, op == 2, name, bytes);
+      return name;
+    case 3:
+    case 4:
+    {
+      if (!b1) return "none";
+      i64 P;
+      GSpans sp;
+      const bool g = marchg_enabled() && (mode == kSymN8 || mode == kSymN32) && gspans(A, P, sp) &&
+                     (A.nb_rows + P - 1) / P >= 4;
+      if (op == 3 && march_plan(A, mode, 0, -1, false, 16).nseg > 0) return "k_spmm8_march";
+      if (g) return op == 3 ? "k_spmm8_marchg" : "k_spmm8_marchg_cheb";
+      return op == 3 ? "k_sell_mv8" : "k_sell_mv8q_cheb";
+    }
+    default:
+      return "none";
   }
 }
 

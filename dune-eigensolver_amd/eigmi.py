@@ -99,6 +99,7 @@ SIGNATURES = {
     "eig_mat_get_info": (_int, [_vp, ctypes.POINTER(_MatInfo)]),
     "eig_mat_shift_diag": (_int, [_vp, _dbl]),
     "eig_lanczos_kernel_info": (_int, [_vp, _int, ctypes.c_char_p, _int, ctypes.POINTER(_i64)]),
+    "eig_mat_kernel_info": (_int, [_vp, _int, ctypes.c_char_p, _int]),
     "eig_mv": (_int, [_vp, _vp, _vp]),
     "eig_mv_host": (_int, [_vp, _vp, _vp]),
     "eig_mv_timed": (_int, [_vp, _vp, _vp, _int, ctypes.POINTER(_dbl)]),
@@ -311,6 +312,15 @@ class Matrix:
         info = _MatInfo()
         ctx.check(lib.eig_mat_get_info(handle, ctypes.byref(info)))
         self.info = info
+
+    OPS = {"spmv": 0, "k1": 1, "fused": 2, "spmm8": 3, "cheb8": 4}
+
+    def kernel(self, op):
+        """Kernel family a whole-matrix launch of `op` ("spmv", "k1", "fused", "spmm8", "cheb8")
+        picks on this image now (eig_mat_kernel_info)."""
+        buf = ctypes.create_string_buffer(64)
+        self.ctx.check(lib.eig_mat_kernel_info(self.h, self.OPS[op], buf, 64))
+        return buf.value.decode()
 
     def lanczos_kernel_info(self, fused=True):
         """-> (kernel name, algorithmic HBM bytes per launch) of a whole-matrix Lanczos step launch

@@ -142,6 +142,11 @@ int eig_mat_get_info(eig_mat_t mat, eig_mat_info *info);
  * per launch for that image: SELL/stencil images 12 nnz + 4(n+1) + vectors,
  * the symmetric band image 8 nup n + mask bytes + vectors.  `name` gets at most name_len bytes. */
 int eig_lanczos_kernel_info(eig_mat_t mat, int fused, char *name, int name_len, int64_t *bytes);
+/* Kernel family a whole-matrix launch of `op` picks on this matrix image now (the EIGMI_*
+ * environment switches included): EIG_OP_SPMV (eig_mv), EIG_OP_LANCZOS_K1, EIG_OP_LANCZOS_FUSED,
+ * EIG_OP_SPMM8 (eig_spmm_mv8, per 8-column block), EIG_OP_CHEB8 (eig_mass_solve_mv8's step). */
+enum { EIG_OP_SPMV = 0, EIG_OP_LANCZOS_K1 = 1, EIG_OP_LANCZOS_FUSED = 2, EIG_OP_SPMM8 = 3, EIG_OP_CHEB8 = 4 };
+int eig_mat_kernel_info(eig_mat_t mat, int op, char *name, int name_len);
 
 /* a13: A += shift*I on the diagonal of every diagonal block (eigensolver.hh:59-66). */
 int eig_mat_shift_diag(eig_mat_t mat, double shift);

@@ -190,3 +190,56 @@ def test_march_spmm_bitwise(ctx, mat, m):
     Q, Y = ctx.array(Qh), ctx.zeros(A.n * m)
     eigmi.spmm_mv8(M, m, Q, Y)
     assert np.array_equal(Y.get(), oracle.spmm_mv8(A, Qh, m))
+
+
+# ---- general band march (k_spmm8_marchg): carried offset P not the widest, spans S1..S4 ----
+
+def _p1(N, which):
+    K, Mm = oracle.p1_kuhn(N)
+    S = K if which == "K" else Mm
+    return oracle.CSR(S.shape[0], S.indptr.astype(np.int64), S.indices.astype(np.int32), S.data.copy())
+
+
+@pytest.mark.parametrize("mat,m", [
+    ("p1mass8", 8), ("p1mass8", 16), ("p1stiff8", 8), ("p1mass16", 8),
+    ("band_beyond", 8),   # offsets past the carried P = 32: spans S1 / S4 non-empty
+])
+def test_marchg_spmm_bitwise(ctx, mat, m):
+    A = {"p1mass8": lambda: _p1(8, "M"), "p1stiff8": lambda: _p1(8, "K"), "p1mass16": lambda: _p1(16, "M"),
+         "band_beyond": lambda: band_matrix(4000, [0, 1, 5, 32, 35, 40], 31, drop=0.05)}[mat]()
+    M = upload(ctx, A)
+    assert M.info.sym_offsets > 0
+    assert M.kernel("spmm8") == "k_spmm8_marchg"
+    Qh = oracle.random_mv8(A.n, m, 6)
+    Q, Y = ctx.array(Qh), ctx.zeros(A.n * m)
+    eigmi.spmm_mv8(M, m, Q, Y)
+    assert np.array_equal(Y.get(), oracle.spmm_mv8(A, Qh, m))
+
+
+@pytest.mark.parametrize("N,m", [(8, 8), (16, 32)])
+def test_marchg_chebyshev_matches_sell(ctx, N, m):
+    """The fused Chebyshev-Jacobi mass solve (config C5) on the general band march against the
+    SELL kernel (both fused multiply-adds in ascending offset order; tolerance: signed zeros)."""
+    A = _p1(N, "M")
+    M = upload(ctx, A)
+    assert M.kernel("cheb8") == "k_spmm8_marchg_cheb"
+    n = A.n
+    Bh = oracle.random_mv8(n, m, 8)
+    B = ctx.array(Bh)
+    X1, X2 = ctx.zeros(n * m), ctx.zeros(n * m)
+    eigmi.mass_solve_mv8(M, m, 12, B, X1)
+    old = os.environ.get("EIGMI_MARCHG")
+    os.environ["EIGMI_MARCHG"] = "0"
+    try:
+        assert M.kernel("cheb8") == "k_sell_mv8q_cheb"
+        eigmi.mass_solve_mv8(M, m, 12, B, X2)
+    finally:
+        if old is None:
+            del os.environ["EIGMI_MARCHG"]
+        else:
+            os.environ["EIGMI_MARCHG"] = old
+    a, b = X1.get(), X2.get()
+    assert np.allclose(a, b, rtol=1e-13, atol=1e-14 * np.abs(b).max())
+    # and the solve is a solve: M x ~ b (degree 12 Chebyshev, kappa(D^-1 M) <= 5: error ~ 2 0.38^12)
+    r = oracle.spmm_mv8(A, a, m) - Bh
+    assert np.linalg.norm(r) <= 1e-3 * np.linalg.norm(Bh)
