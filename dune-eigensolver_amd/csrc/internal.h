@@ -320,6 +320,16 @@ struct TrsvImage {
   double *uv = nullptr, *ud = nullptr;
   i32 *P = nullptr, *Q = nullptr;
   double *scale = nullptr;                // Rs[P[k]] (do_recip) or 1 / Rs[P[k]]
+  // Block-staged image (k_tsolve_staged, k_trsv.hip), per factor (0 = L, 1 = U) and 64-row block b:
+  // the entries outside the block as an ELL slab [k][r] (off1[b] .. + w1[b] * 64; column -1 =
+  // padding), the entries inside it as a dense 64 x 64 tile [t][r] (tile + b * 4096) + row masks.
+  i64 *off1[2] = {nullptr, nullptr};
+  i32 *w1[2] = {nullptr, nullptr};
+  double *v1[2] = {nullptr, nullptr};
+  i32 *c1[2] = {nullptr, nullptr};
+  double *tile[2] = {nullptr, nullptr};
+  unsigned long long *tmask[2] = {nullptr, nullptr};
+  bool staged = false;  // the factors fit k_tsolve_staged (k_trsv.hip)
 };
 void trsv_upload(eig_ctx_t ctx, i64 n, const std::vector<i64> &lrp, const std::vector<i32> &lc,
                  const std::vector<double> &lv, const std::vector<i64> &urp, const std::vector<i32> &uc,

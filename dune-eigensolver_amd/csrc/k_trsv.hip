@@ -26,6 +26,7 @@ namespace {
 constexpr int kTB = 64;       // rows per block
 constexpr int kTThreads = 512;  // 8 waves = the 8 columns of a column block
 constexpr int kRing = 3;        // solved blocks whose x stays in LDS for phase 1
+constexpr int kThreadsT = kTThreads;
 
 __global__ __launch_bounds__(256) void k_perm_scale(i64 n, int nblk, const i32 *__restrict__ P,
                                                     const double *__restrict__ scale, const double *__restrict__ Qin,
@@ -56,6 +57,12 @@ __global__ __launch_bounds__(256) void k_perm_out(i64 n, int nblk, const i32 *__
     for (int s = 0; s < 8; ++s) dst[s] = src[s];
   }
 }
+
+// Explicit global-address-space access (addrspace 1): a generic (flat) access would also count on
+// lgkmcnt, so every LDS wait of the solve loops would wait for it too.
+typedef __attribute__((address_space(1))) double gdouble;
+__device__ __forceinline__ double gld(const double *p) { return *(const gdouble *)p; }
+__device__ __forceinline__ void gst(double *p, double v) { *(gdouble *)p = v; }
 
 // Wave-uniform broadcast of lane t's double (two v_readlane_b32: scalar, no LDS crossbar).
 __device__ __forceinline__ double lane_bcast(double v, int t)
@@ -176,6 +183,175 @@ __global__ __launch_bounds__(kTThreads) void k_tsolve(i64 n, const i64 *__restri
   }
 }
 
+// Block-staged triangular solve (default when the factor fits it: at most kSlab outside-the-block
+// entries per row and every one within the kRing4 blocks solved last -- envelope factors of
+// bandwidth <= 256; other factors take k_tsolve).  Same per-row operation sequence as k_tsolve
+// (bitwise equal), but every global load of a block is coalesced and issued one block AHEAD: the
+// 512 threads load block b+1's ELL slab of outside-the-block entries ([k][r]: 64 rows per
+// instruction) and its dense in-block tile into registers during block b's register wavefront; at
+// staging the columns become ring indices, so phase 1 is LDS reads and selected subtractions
+// without per-entry branches.
+constexpr int kRing4 = 4;   // ring slots of the staged kernel (power of two)
+constexpr int kSlab = 128;  // slab entries per row staged at once (LDS: 96 KiB of slab + 32 KiB tile)
+
+struct Staged {
+  const i64 *off1;
+  const i32 *w1;
+  const double *v1;
+  const i32 *c1;
+  const double *tile;
+  const unsigned long long *tmask;
+};
+
+template <bool LOWER>
+__global__ __launch_bounds__(kTThreads) void k_tsolve_staged(i64 n, Staged F, const double *__restrict__ diag,
+                                                             const double *rhs, double *x)
+{
+  __shared__ double tile[kTB][kTB];  // tile[t][r]
+  __shared__ unsigned long long tmask[kTB];
+  __shared__ double sv[kSlab][kTB];  // slab chunk: value of entry k of row r
+  __shared__ i32 sc[kSlab][kTB];     // its column (-1: padding)
+  // x of the kRing4 most recently solved blocks, [slot][column c][row]: a phase-1 read by lane r
+  // of a banded row hits consecutive rows, i.e. distinct banks (a [row][c] layout would put the
+  // 64 lanes 64 B apart: 16-way bank conflicts)
+  __shared__ double ring[kRing4][8][kTB];
+  const int tid = threadIdx.x, r = tid & 63, c = tid >> 6;
+  const i64 cb = (i64)blockIdx.x * n * 8;
+  const double *R = rhs + cb;
+  double *X = x + cb;
+  const i64 nblocks = (n + kTB - 1) / kTB;
+  // prefetch registers: 8 tile doubles, 8 slab entries (value, column) per thread, one mask
+  constexpr int kQ = kSlab * kTB / kThreadsT;  // slab entries per thread per chunk
+  double pt[8], pv[kQ];
+  i32 pc[kQ];
+  unsigned long long pm = 0;
+  int pw = 0;
+  // one block's staging loads: all at fixed, block-indexed addresses (no dependent metadata load,
+  // no predicates), so they stay in flight until the next block's staging consumes them
+  auto prefetch = [&](i64 blk) {
+    const double *tg = F.tile + blk * (kTB * kTB);
+    const double *vg = F.v1 + blk * (kSlab * kTB);
+    const i32 *cg = F.c1 + blk * (kSlab * kTB);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) pt[q] = tg[q * kThreadsT + tid];
+#pragma unroll
+    for (int q = 0; q < kQ; ++q)
+    {
+      pv[q] = vg[q * kThreadsT + tid];  // entry k = q * 8 + c of row r
+      pc[q] = cg[q * kThreadsT + tid];
+    }
+    pm = F.tmask[blk * kTB + r];
+    pw = F.w1[blk];
+  };
+  prefetch(LOWER ? 0 : nblocks - 1);
+  for (i64 bi = 0; bi < nblocks; ++bi)
+  {
+    const i64 blk = LOWER ? bi : nblocks - 1 - bi;
+    const i64 bs = blk * kTB;
+    const i64 i = bs + r;
+    const bool valid = i < n;
+    double sum = valid ? gld(R + i * 8 + c) : 0.0;
+    const int w1 = pw;
+    // stage the prefetched block into LDS
+    const double dr = (!LOWER && valid) ? gld(diag + i) : 1.0;  // U pivot of row i
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+    {
+      const int e = q * kThreadsT + tid;
+      tile[e >> 6][e & 63] = pt[q];
+    }
+#pragma unroll
+    for (int q = 0; q < kQ; ++q)
+    {
+      const int e = q * kThreadsT + tid;
+      sv[e >> 6][e & 63] = pv[q];
+      // column -> its x in the ring: slot (block mod kRing4) * 512 + row (the column offset c * 64
+      // is added by the reading wave)
+      sc[e >> 6][e & 63] = pc[q] < 0 ? -1 : ((((pc[q] >> 6) & (kRing4 - 1)) << 9) | (pc[q] & 63));
+    }
+    if (c == 0) tmask[r] = pm;
+    __syncthreads();
+    // phase 1: the outside-the-block entries of row r in entry order (at most kSlab, all in the
+    // ring: the host admits a factor to this kernel only then), 8 per round: their LDS reads are
+    // issued before the 8 dependent subtractions; stored entries are selected, never branched on
+    const double *rf = &ring[0][c][0];
+    for (int kk = 0; kk < w1; kk += 8)
+    {
+      i32 ix[8];
+      double a[8], xv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+      {
+        ix[u] = sc[(kk + u) & (kSlab - 1)][r];  // ring index (slot * 512 + row) or -1
+        a[u] = sv[(kk + u) & (kSlab - 1)][r];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) xv[u] = rf[ix[u] < 0 ? 0 : ix[u]];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+      {
+        const double upd = sum - a[u] * xv[u];
+        sum = (kk + u < w1 && ix[u] >= 0) ? upd : sum;
+      }
+    }
+    // next block's staging loads fly during the wavefront and the end-of-block barrier
+    if (bi + 1 < nblocks) prefetch(LOWER ? blk + 1 : blk - 1);
+    // this lane's update mask: stored in-block entries in the columns solved before its row
+    const unsigned long long m = tmask[r] & (LOWER ? ((1ull << r) - 1ull) : ~((2ull << r) - 1ull));
+    const int nb = (int)((n - bs) < kTB ? (n - bs) : kTB);
+    // register wavefront, 8 steps per round: the round's tile entries are read from LDS before its
+    // chain of broadcasts, the round's 8 mask bits come from one 32-bit shift.  A lane's own row
+    // is final once the wavefront passes it (no later step updates it), so its x is read off its
+    // sum after the loop (U: sum / u_rr, the same division the broadcast step performs).
+    const int nb8 = (nb + 7) & ~7;
+    if (LOWER)
+    {
+      for (int t0 = 0; t0 < nb; t0 += 8)
+      {
+        double tv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) tv[u] = tile[(t0 + u) & 63][r];
+        const unsigned mr = (unsigned)(m >> t0);
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (t0 + u < nb)
+          {
+            const double xt = lane_bcast(sum, t0 + u);  // row bs + t is final
+            const double upd = sum - tv[u] * xt;
+            sum = ((mr >> u) & 1u) ? upd : sum;  // stored entries of rows below t only
+          }
+      }
+    }
+    else
+    {
+      for (int t0 = nb8 - 8; t0 >= 0; t0 -= 8)
+      {
+        double tv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) tv[u] = tile[(t0 + 7 - u) & 63][r];
+        const unsigned mr = (unsigned)(m >> t0);
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (t0 + 7 - u < nb)
+          {
+            const int t = t0 + 7 - u;
+            const double xt = lane_bcast(sum, t) / lane_bcast(dr, t);  // x = (rhs - sum u x) / u_tt
+            const double upd = sum - tv[u] * xt;
+            sum = ((mr >> (7 - u)) & 1u) ? upd : sum;  // stored entries of rows above t only
+          }
+      }
+    }
+    const double mine = LOWER ? sum : sum / dr;
+    if (valid) gst(X + i * 8 + c, mine);
+    ring[blk & (kRing4 - 1)][c][r] = mine;
+    // ring visible to the next block, LDS staging free for reuse: an LDS-only barrier (x is never
+    // re-read from global memory here), so the next block's staging loads stay in flight
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+    __builtin_amdgcn_s_barrier();
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  }
+}
+
 int grid256(i64 work)
 {
   i64 g = (work + 255) / 256;
@@ -218,6 +394,74 @@ void trsv_upload(eig_ctx_t ctx, i64 n, const std::vector<i64> &lrp, const std::v
     p32[k] = (i32)P[k];
     q32[k] = (i32)Q[k];
   }
+  // block-staged images (k_tsolve_staged): per 64-row block, the outside-the-block entries of each
+  // row as an ELL slab [k][r] in the row's own order, the inside entries as a dense tile [t][r]
+  auto stage = [&](int f, const std::vector<i64> &rp, const std::vector<i32> &cj, const std::vector<double> &cv,
+                   const std::vector<i64> &split) {
+    // slab: the first kSlab entries of every row at a fixed place (block b: b * kSlab * 64), the
+    // rest (rows wider than kSlab) in an overflow slab at off[b]
+    const i64 nblocks = (n + kTB - 1) / kTB;
+    std::vector<i64> off(nblocks + 1, 0);
+    std::vector<i32> w(std::max<i64>(nblocks, 1), 0);
+    const i64 fixed = nblocks * kSlab * kTB;
+    for (i64 b = 0; b < nblocks; ++b)
+    {
+      i64 mw = 0;
+      for (i64 i = b * kTB; i < std::min(n, b * kTB + kTB); ++i) mw = std::max(mw, split[i] - rp[i]);
+      w[b] = (i32)mw;
+      off[b + 1] = off[b] + std::max<i64>(mw - kSlab, 0) * kTB;
+    }
+    for (i64 b = 0; b <= nblocks; ++b) off[b] += fixed;
+    std::vector<double> v1(std::max<i64>(off[nblocks], 1), 0.0);
+    std::vector<i32> c1(std::max<i64>(off[nblocks], 1), -1);
+    std::vector<double> tl((size_t)std::max<i64>(nblocks, 1) * kTB * kTB, 0.0);
+    std::vector<unsigned long long> tm((size_t)std::max<i64>(nblocks, 1) * kTB, 0ull);
+    for (i64 b = 0; b < nblocks; ++b)
+      for (i64 i = b * kTB; i < std::min(n, b * kTB + kTB); ++i)
+      {
+        const i64 r = i - b * kTB;
+        for (i64 q = rp[i]; q < split[i]; ++q)
+        {
+          const i64 k = q - rp[i];
+          const i64 at = k < kSlab ? (b * kSlab + k) * kTB + r : off[b] + (k - kSlab) * kTB + r;
+          v1[at] = cv[q];
+          c1[at] = cj[q];
+        }
+        for (i64 q = split[i]; q < rp[i + 1]; ++q)
+        {
+          const i64 t = cj[q] - b * kTB;
+          tl[(size_t)b * kTB * kTB + t * kTB + r] = cv[q];
+          tm[(size_t)b * kTB + r] |= 1ull << t;
+        }
+      }
+    off.resize(nblocks);
+    img.off1[f] = upload(off);
+    img.w1[f] = upload(w);
+    img.v1[f] = upload(v1);
+    img.c1[f] = upload(c1);
+    img.tile[f] = upload(tl);
+    img.tmask[f] = upload(tm);
+  };
+  // admission to the staged kernel: <= kSlab outside entries per row, all within kRing4 blocks
+  auto fits = [&](const std::vector<i64> &rp, const std::vector<i32> &cj, const std::vector<i64> &split, bool lower) {
+    for (i64 i = 0; i < n; ++i)
+    {
+      if (split[i] - rp[i] > kSlab) return false;
+      const i64 blk = i / kTB;
+      for (i64 q = rp[i]; q < split[i]; ++q)
+      {
+        const i64 cb = cj[q] / kTB;
+        if (lower ? (cb < blk - kRing4) : (cb > blk + kRing4)) return false;
+      }
+    }
+    return true;
+  };
+  img.staged = fits(lrp, lc, ls, true) && fits(urp, uc, us, false);
+  if (img.staged)
+  {
+    stage(0, lrp, lc, lv, ls);
+    stage(1, urp, uc, uv, us);
+  }
   img.lrp = upload(lrp);
   img.lsplit = upload(ls);
   img.lc = upload(lc);
@@ -234,6 +478,10 @@ void trsv_upload(eig_ctx_t ctx, i64 n, const std::vector<i64> &lrp, const std::v
 
 void trsv_free(TrsvImage &img)
 {
+  for (int f = 0; f < 2; ++f)
+    for (void *p : {(void *)img.off1[f], (void *)img.w1[f], (void *)img.v1[f], (void *)img.c1[f], (void *)img.tile[f],
+                    (void *)img.tmask[f]})
+      if (p) (void)hipFree(p);
   for (void *p : {(void *)img.lrp, (void *)img.lsplit, (void *)img.lc, (void *)img.lv, (void *)img.urp,
                   (void *)img.usplit, (void *)img.uc, (void *)img.uv, (void *)img.ud, (void *)img.P, (void *)img.Q,
                   (void *)img.scale})
@@ -247,10 +495,23 @@ void launch_inverse_mv8(const TrsvImage &img, i64 m, double *Qin, double *Qout, 
   const int nblk = (int)(m / 8);
   // 1. Qout = P (R Qin)   2. Qin = L^-1 Qout   3. Qin = U^-1 Qin   4. Qout = Q Qin
   hipLaunchKernelGGL(k_perm_scale, dim3(grid256(n * nblk)), dim3(256), 0, s, n, nblk, img.P, img.scale, Qin, Qout);
-  hipLaunchKernelGGL(k_tsolve<true>, dim3(nblk), dim3(kTThreads), 0, s, n, img.lrp, img.lsplit, img.lc, img.lv,
-                     (const double *)nullptr, (const double *)Qout, Qin);
-  hipLaunchKernelGGL(k_tsolve<false>, dim3(nblk), dim3(kTThreads), 0, s, n, img.urp, img.usplit, img.uc, img.uv,
-                     (const double *)img.ud, (const double *)Qin, Qin);
+  const char *e = std::getenv("EIGMI_TRSV");  // "csr": the row-CSR kernel (A/B)
+  if (!img.staged || (e && std::string(e) == "csr"))
+  {
+    hipLaunchKernelGGL(k_tsolve<true>, dim3(nblk), dim3(kTThreads), 0, s, n, img.lrp, img.lsplit, img.lc, img.lv,
+                       (const double *)nullptr, (const double *)Qout, Qin);
+    hipLaunchKernelGGL(k_tsolve<false>, dim3(nblk), dim3(kTThreads), 0, s, n, img.urp, img.usplit, img.uc, img.uv,
+                       (const double *)img.ud, (const double *)Qin, Qin);
+  }
+  else
+  {
+    const Staged L{img.off1[0], img.w1[0], img.v1[0], img.c1[0], img.tile[0], img.tmask[0]};
+    const Staged U{img.off1[1], img.w1[1], img.v1[1], img.c1[1], img.tile[1], img.tmask[1]};
+    hipLaunchKernelGGL(k_tsolve_staged<true>, dim3(nblk), dim3(kTThreads), 0, s, n, L, (const double *)nullptr,
+                       (const double *)Qout, Qin);
+    hipLaunchKernelGGL(k_tsolve_staged<false>, dim3(nblk), dim3(kTThreads), 0, s, n, U, (const double *)img.ud,
+                       (const double *)Qin, Qin);
+  }
   hipLaunchKernelGGL(k_perm_out, dim3(grid256(n * nblk)), dim3(256), 0, s, n, nblk, img.Q, Qin, Qout);
   EIG_HIP(hipGetLastError());
 }

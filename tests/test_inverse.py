@@ -199,3 +199,30 @@ def test_generalized_inverse_pu_mass(ctx):
     f = oracle.LU(**factors(As))
     rev, _, rit = oracle.generalized_inverse(A, B, f, shift, reg, 1e-8, 200, 8, 123)
     assert it == rit and np.allclose(ev, rev, rtol=1e-10, atol=1e-12)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["laplace2d_64", "poisson3d_12", "poisson3d_20"])
+@pytest.mark.parametrize("kernel", ["staged", "csr"])
+def test_inverse_mv8_kernels_bitwise(ctx, name, kernel):
+    """Both triangular-solve kernels (k_tsolve_staged: envelope factors of bandwidth <= 256, the
+    default when the factor fits; k_tsolve: any factor) reproduce the reference arithmetic
+    bitwise.  poisson3d_20's RCM envelope reaches past 256 rows: it always takes k_tsolve."""
+    import os
+    A = {"laplace2d_64": lambda: oracle.laplace2d(64), "poisson3d_12": lambda: oracle.poisson3d(12),
+         "poisson3d_20": lambda: oracle.poisson3d(20)}[name]()
+    lu, f = _gpu_lu(ctx, A, "bcsr")
+    X = oracle.random_mv8(A.n, 16, 3)
+    ref_out, _ = oracle.inverse_mv8(f, X, 16)
+    old = os.environ.get("EIGMI_TRSV")
+    os.environ["EIGMI_TRSV"] = kernel
+    try:
+        din, dout = ctx.array(X), ctx.zeros(A.n * 16)
+        lu.inverse_mv8(16, din, dout)
+        assert np.array_equal(dout.get(), ref_out)
+    finally:
+        if old is None:
+            del os.environ["EIGMI_TRSV"]
+        else:
+            os.environ["EIGMI_TRSV"] = old
+    lu.close()
