@@ -24,7 +24,7 @@ def test_loopback_builds(loopback_bin):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("P,N", [(2, 16), (3, 24), (4, 32)])
+@pytest.mark.parametrize("P,N", [(2, 16), (3, 24), (4, 32), (8, 64)])
 def test_loopback_virtual_ranks(loopback_bin, P, N):
     r = subprocess.run([loopback_bin, str(P), str(N)], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "ALL OK" in r.stdout, r.stdout + r.stderr
