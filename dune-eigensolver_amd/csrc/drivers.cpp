@@ -2,7 +2,7 @@
 //   eig_standard_largest  StandardLargest subspace iteration (eigensolver.hh:28-112)
 //   eig_lanczos_run       the Lanczos three-term recurrence ARPACK's dsaupd runs around multMv
 //                         (arpack_geneo_wrapper.hh:257-279, :621-632) -- the benchmark unit
-//   eig_lanczos_solve     Lanczos with full (DGKS / CGS2) re-orthogonalisation + Ritz extraction
+//   eig_lanczos_solve     Lanczos with full DGKS re-orthogonalisation (ARPACK's conditional second pass) + Ritz extraction
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -955,6 +955,7 @@ extern "C" int eig_lanczos_solve(eig_mat_t A, int nev, int ncv, int which, unsig
     init_start(*A, V, nullptr, seed);
     LanczosBufs lb(ncv);
     DevBuf cb((size_t)(ncv + 8) * sizeof(double));
+    DevBuf gate(2 * sizeof(double));  // {||t||^2 after the first pass, before it}
     launch_nrm2sq(n, V + own, lb.st.nsum, 0, s, ctx->red);
     allreduce_sum(ctx, lb.st.nsum, 1, s);
     hipEvent_t h0, h1;
@@ -964,16 +965,26 @@ extern "C" int eig_lanczos_solve(eig_mat_t A, int nev, int ncv, int which, unsig
     {
       double *u = V + (i64)j * W, *up = j > 0 ? V + (i64)(j - 1) * W : V + (i64)j * W, *t = V + (i64)(j + 1) * W;
       lanczos_step(*A, u, up, t, j, lb, nullptr, 0, h0, h1);
-      // DGKS: two classical Gram-Schmidt passes against v_0..v_j (v_q = u_q / sqrt(nsum[q]))
+      // DGKS as ARPACK's dsaitr runs it: a classical Gram-Schmidt pass against v_0..v_j
+      // (v_q = u_q / sqrt(nsum[q])), then a second one only when the pass removed a large part
+      // of t (||t'|| <= 0.717 ||t||) -- decided on the device from the two norms (gated launches)
+      launch_nrm2sq(n, t + own, gate.d() + 1, 0, s, ctx->red);
+      allreduce_sum(ctx, gate.d() + 1, 1, s);
       for (int pass = 0; pass < 2; ++pass)
       {
+        const double *g = pass ? gate.d() : nullptr;
         for (int q0 = 0; q0 <= j; q0 += 8 * 48)
         {
           const int kq = std::min(j + 1 - q0, 8 * 48);
-          launch_gemv_t(n, kq, V + (i64)q0 * W + own, W, t + own, cb.d() + q0, 0, s, ctx->red);
+          launch_gemv_t(n, kq, V + (i64)q0 * W + own, W, t + own, cb.d() + q0, 0, s, ctx->red, g);
         }
-        allreduce_sum(ctx, cb.d(), j + 1, s);
-        launch_gemv_n_sub(n, j + 1, V + own, W, cb.d(), lb.st.nsum, t + own, s);
+        allreduce_sum(ctx, cb.d(), j + 1, s);  // (after a skipped pass: unused)
+        launch_gemv_n_sub(n, j + 1, V + own, W, cb.d(), lb.st.nsum, t + own, s, g);
+        if (pass == 0)
+        {
+          launch_nrm2sq(n, t + own, gate.d(), 0, s, ctx->red);
+          allreduce_sum(ctx, gate.d(), 1, s);
+        }
       }
       launch_nrm2sq(n, t + own, lb.st.nsum + j + 1, 0, s, ctx->red);
       allreduce_sum(ctx, lb.st.nsum + j + 1, 1, s);

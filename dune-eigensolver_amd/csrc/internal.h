@@ -280,11 +280,14 @@ void launch_max_offdiag(const double *S, i64 rows, i64 cols, bool upper_only, do
 
 // Column-major (b = 1) GEMV-type helpers for the Lanczos re-orthogonalisation:
 // c = V^T w (V: k columns of length ld, owned slice at off), w -= V c.
+// gate (device, nullable): {r, w} squared norms; the launch does nothing unless
+// r <= 0.717^2 w -- ARPACK's DGKS test for a second Gram-Schmidt pass (dsaitr: rnorm > 0.717 wnorm
+// means the first pass sufficed), evaluated on the device so no step synchronises with the host.
 void launch_gemv_t(i64 n, int k, const double *V, i64 ldv, const double *w, double *c, int ticket,
-                   hipStream_t s, ReduceWS red);
+                   hipStream_t s, ReduceWS red, const double *gate = nullptr);
 // w -= sum_q V_q * c[q] / (scale2 ? scale2[q] : 1)
 void launch_gemv_n_sub(i64 n, int k, const double *V, i64 ldv, const double *c, const double *scale2, double *w,
-                       hipStream_t s);
+                       hipStream_t s, const double *gate = nullptr);
 // y = sum_q V_q * c[q] / sqrt(nsum[q])   (Ritz vector assembly from an unnormalised basis)
 void launch_gemv_n_set(i64 n, int k, const double *V, i64 ldv, const double *c, const double *nsum, double *y,
                        hipStream_t s);

@@ -217,10 +217,18 @@ void launch_shift_diag(eig_mat_s &A, double shift, hipStream_t s)
 // ---------------------------------------------------------------------------------------------
 constexpr int kGemvBlocks = 512;
 
+constexpr double kDgks2 = 0.717 * 0.717;  // ARPACK dsaitr's DGKS threshold, squared
+
+__device__ __forceinline__ bool gated_off(const double *gate)
+{
+  return gate && !(gate[0] <= kDgks2 * gate[1]);
+}
+
 __global__ __launch_bounds__(kStreamThreads) void k_gemv_t(i64 n, int k, const double *__restrict__ V, i64 ldv,
                                                            const double *__restrict__ w, double *__restrict__ c,
-                                                           double *partials, unsigned *tickets)
+                                                           double *partials, unsigned *tickets, const double *gate)
 {
+  if (gated_off(gate)) return;  // (every block: the ticket is never touched)
   __shared__ double tot[8];
   const int c0 = blockIdx.y * 8;
   double acc[8];
@@ -241,7 +249,7 @@ __global__ __launch_bounds__(kStreamThreads) void k_gemv_t(i64 n, int k, const d
 }
 
 void launch_gemv_t(i64 n, int k, const double *V, i64 ldv, const double *w, double *c, int ticket, hipStream_t s,
-                   ReduceWS red)
+                   ReduceWS red, const double *gate)
 {
   const int tiles = (k + 7) / 8;
   EIG_CHECK(ticket + tiles <= kNumTickets, EIG_ERR_ARG, "gemv_t: too many column tiles for the ticket pool");
@@ -249,13 +257,14 @@ void launch_gemv_t(i64 n, int k, const double *V, i64 ldv, const double *w, doub
   if (G > kGemvBlocks) G = kGemvBlocks;
   EIG_CHECK((i64)G * tiles * 8 <= (i64)kMaxRedBlocks * kMaxRedVals, EIG_ERR_ARG, "gemv_t: partials overflow");
   hipLaunchKernelGGL(k_gemv_t, dim3(G, tiles), dim3(kStreamThreads), 0, s, n, k, V, ldv, w, c, red.partials,
-                     red.ticket(ticket));
+                     red.ticket(ticket), gate);
 }
 
 __global__ __launch_bounds__(kStreamThreads) void k_gemv_n(i64 n, int k, const double *__restrict__ V, i64 ldv,
                                                            const double *__restrict__ c, const double *__restrict__ sc,
-                                                           int mode, double *__restrict__ w)
+                                                           int mode, double *__restrict__ w, const double *gate)
 {
+  if (gated_off(gate)) return;
   // mode 0: w -= sum V_q c_q / sc_q (sc may be null)  ; mode 1: w = sum V_q c_q / sqrt(sc_q)
   __shared__ double coef[512];
   for (int q = threadIdx.x; q < k && q < 512; q += blockDim.x)
@@ -274,17 +283,19 @@ __global__ __launch_bounds__(kStreamThreads) void k_gemv_n(i64 n, int k, const d
   }
 }
 void launch_gemv_n_sub(i64 n, int k, const double *V, i64 ldv, const double *c, const double *scale2, double *w,
-                       hipStream_t s)
+                       hipStream_t s, const double *gate)
 {
   EIG_CHECK(k <= 512, EIG_ERR_ARG, "gemv_n: at most 512 basis vectors");
   if (k <= 0) return;
-  hipLaunchKernelGGL(k_gemv_n, dim3(stream_grid(n, 4)), dim3(kStreamThreads), 0, s, n, k, V, ldv, c, scale2, 0, w);
+  hipLaunchKernelGGL(k_gemv_n, dim3(stream_grid(n, 4)), dim3(kStreamThreads), 0, s, n, k, V, ldv, c, scale2, 0, w,
+                     gate);
 }
 void launch_gemv_n_set(i64 n, int k, const double *V, i64 ldv, const double *c, const double *nsum, double *y,
                        hipStream_t s)
 {
   EIG_CHECK(k <= 512, EIG_ERR_ARG, "gemv_n: at most 512 basis vectors");
-  hipLaunchKernelGGL(k_gemv_n, dim3(stream_grid(n, 4)), dim3(kStreamThreads), 0, s, n, k, V, ldv, c, nsum, 1, y);
+  hipLaunchKernelGGL(k_gemv_n, dim3(stream_grid(n, 4)), dim3(kStreamThreads), 0, s, n, k, V, ldv, c, nsum, 1, y,
+                     (const double *)nullptr);
 }
 
 // out = ||x - theta*y||^2
