@@ -333,6 +333,13 @@ struct TrsvImage {
   double *tile[2] = {nullptr, nullptr};
   unsigned long long *tmask[2] = {nullptr, nullptr};
   bool staged = false;  // the factors fit k_tsolve_staged (k_trsv.hip)
+  // Block-inverse image (k_binv_z / k_binv_chain, k_trsv.hip), per factor: the inverse of every
+  // 64 x 64 diagonal block, dinv + b * 4096 as [t][r], and G(b, d) = inv(D_b) T(b, d) for the
+  // coupling T(b, d) of block b to the block d before it (L) / after it (U), g + (b * gd + d - 1) * 4096
+  double *dinv[2] = {nullptr, nullptr};
+  double *g[2] = {nullptr, nullptr};
+  int gd[2] = {0, 0};
+  bool binv = false;
 };
 void trsv_upload(eig_ctx_t ctx, i64 n, const std::vector<i64> &lrp, const std::vector<i32> &lc,
                  const std::vector<double> &lv, const std::vector<i64> &urp, const std::vector<i32> &uc,

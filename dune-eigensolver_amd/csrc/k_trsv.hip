@@ -18,6 +18,8 @@
 //            entry in column bs + t -- a register wavefront, no barrier inside the block.
 // U runs the blocks bottom-up with t descending.  x of earlier blocks is re-read by the same
 // workgroup after a __syncthreads (workgroup-scope ordering).
+// Default where the factor fits the staged image: the block-inverse solve (k_binv_z +
+// k_binv_chain below; to rounding, not bitwise); EIGMI_TRSV=staged / csr keep the bitwise kernels.
 #include "internal.h"
 
 namespace eigmi {
@@ -193,6 +195,7 @@ __global__ __launch_bounds__(kTThreads) void k_tsolve(i64 n, const i64 *__restri
 // without per-entry branches.
 constexpr int kRing4 = 4;   // ring slots of the staged kernel (power of two)
 constexpr int kSlab = 128;  // slab entries per row staged at once (LDS: 96 KiB of slab + 32 KiB tile)
+constexpr i64 kBinvTiles = 2048;  // block-inverse image cap (64 x 64 double tiles, both factors)
 
 struct Staged {
   const i64 *off1;
@@ -352,6 +355,130 @@ __global__ __launch_bounds__(kTThreads) void k_tsolve_staged(i64 n, Staged F, co
   }
 }
 
+// Block-inverse solve (the default when the factor fits the staged image and the block-inverse
+// image is small enough; not bitwise: the products with inv(D_b) round differently from the
+// substitution, agreement with the reference arithmetic is to ~1e-15 relative).  With D_b the
+// 64 x 64 diagonal block b of the factor, T(b, d) its coupling to the block d away (d <= kRing4),
+// z_b = inv(D_b) y_b and G(b, d) = inv(D_b) T(b, d) (both built on the host at upload):
+//     x_b = z_b - sum_d G(b, d) x_(b -+ d).
+// z for all blocks is one parallel launch (k_binv_z); the chain over the blocks (k_binv_chain)
+// has no dependency inside a block, so a block costs a few dense 64 x 64 x 8 products and one
+// barrier instead of a 64-step register wavefront.
+//
+// k_binv_z: one workgroup per (64-row block, 8-column block); PERM: y = scale * Qin(P, :) (the
+// row scaling + permutation of the L solve), else y = Y.  Thread (r, s) forms the partial products
+// of row r over the columns t of slice s (8 t), the slices are summed in LDS in a fixed order.
+template <bool PERM>
+__global__ __launch_bounds__(kThreadsT) void k_binv_z(i64 n, const double *__restrict__ dinv, const i32 *__restrict__ P,
+                                                      const double *__restrict__ scale, const double *__restrict__ Y,
+                                                      double *__restrict__ Z)
+{
+  __shared__ double ys[kTB][8];
+  __shared__ double part[8][kTB][8];
+  const int tid = threadIdx.x, r = tid & 63, s = tid >> 6;
+  const i64 b = blockIdx.x, bs = b * kTB, cb = (i64)blockIdx.y * n * 8;
+  {
+    const int t = tid >> 3, c = tid & 7;
+    const i64 i = bs + t;
+    double v = 0.0;
+    if (i < n) v = PERM ? scale[i] * Y[cb + (i64)P[i] * 8 + c] : Y[cb + i * 8 + c];
+    ys[t][c] = v;
+  }
+  const double *D = dinv + b * (kTB * kTB);
+  double g[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) g[q] = D[(s * 8 + q) * kTB + r];
+  __syncthreads();
+  double acc[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) acc[c] = 0.0;
+#pragma unroll
+  for (int q = 0; q < 8; ++q)
+#pragma unroll
+    for (int c = 0; c < 8; ++c) acc[c] = fma(g[q], ys[s * 8 + q][c], acc[c]);
+#pragma unroll
+  for (int c = 0; c < 8; ++c) part[s][r][c] = acc[c];
+  __syncthreads();
+  const int t = tid >> 3, c = tid & 7;
+  double z = part[0][t][c];
+#pragma unroll
+  for (int q = 1; q < 8; ++q) z += part[q][t][c];
+  if (bs + t < n) Z[cb + (bs + t) * 8 + c] = z;
+}
+
+// k_binv_chain: one workgroup per 8-column block, the blocks in sequence (L top-down, U bottom-up).
+// Thread (r, s) multiplies the G entries of row r in slice s (prefetched one block ahead) with the
+// solved x rows of that slice, which wave s keeps in a private LDS ring (broadcast reads); the
+// partial sums of the 8 slices meet in LDS (double-buffered by block parity, so one barrier per
+// block), and lane (u, c) of wave s finishes x(row s*8+u, column c) = z - sum, the rows its wave
+// needs from this block later.  gd = number of coupled blocks (G tiles per block).
+template <bool LOWER>
+__global__ __launch_bounds__(kThreadsT) void k_binv_chain(i64 n, int gd, const double *__restrict__ G,
+                                                          const double *Z, double *X)
+{
+  __shared__ double part[2][8][kTB][8];
+  __shared__ double ring[8][kRing4][8][8];  // [wave s][slot][row u of slice s][column]
+  const int tid = threadIdx.x, r = tid & 63, s = tid >> 6;
+  const int u = r >> 3, c = r & 7;  // the reduction role of lane r
+  const i64 cb = (i64)blockIdx.x * n * 8;
+  const i64 nblocks = (n + kTB - 1) / kTB;
+#pragma unroll
+  for (int q = 0; q < kRing4; ++q) ring[s][q][u][c] = 0.0;
+  double pg[kRing4][8], pz = 0.0;
+  auto prefetch = [&](i64 blk) {
+    const double *gb = G + blk * gd * (kTB * kTB);
+#pragma unroll
+    for (int d = 0; d < kRing4; ++d)
+      if (d < gd)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) pg[d][q] = gb[d * (kTB * kTB) + (s * 8 + q) * kTB + r];
+    const i64 i = blk * kTB + s * 8 + u;
+    pz = i < n ? gld(Z + cb + i * 8 + c) : 0.0;
+  };
+  prefetch(LOWER ? 0 : nblocks - 1);
+  for (i64 bi = 0; bi < nblocks; ++bi)
+  {
+    const i64 blk = LOWER ? bi : nblocks - 1 - bi;
+    double g[kRing4][8];
+#pragma unroll
+    for (int d = 0; d < kRing4; ++d)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) g[d][q] = pg[d][q];
+    const double z = pz;
+    if (bi + 1 < nblocks) prefetch(LOWER ? blk + 1 : blk - 1);
+    double acc[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] = 0.0;
+#pragma unroll
+    for (int d = 0; d < kRing4; ++d)
+      if (d < gd && d < bi)  // block blk -+ (d + 1) exists and is solved
+      {
+        const i64 src = LOWER ? blk - (d + 1) : blk + (d + 1);
+        const double(*xr)[8] = ring[s][src & (kRing4 - 1)];
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+#pragma unroll
+          for (int k = 0; k < 8; ++k) acc[k] = fma(g[d][q], xr[q][k], acc[k]);
+      }
+    double(*pp)[kTB][8] = part[bi & 1];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) pp[s][r][k] = acc[k];
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): LDS-only barrier, the prefetch stays in flight
+    __builtin_amdgcn_s_barrier();
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    const int t = s * 8 + u;
+    double sum = pp[0][t][c];
+#pragma unroll
+    for (int q = 1; q < 8; ++q) sum += pp[q][t][c];
+    const double x = z - sum;
+    ring[s][blk & (kRing4 - 1)][u][c] = x;  // read back by this wave only (LDS is in order per wave)
+    const i64 i = blk * kTB + t;
+    if (i < n) gst(X + cb + i * 8 + c, x);
+    __builtin_amdgcn_wave_barrier();
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  }
+}
+
 int grid256(i64 work)
 {
   i64 g = (work + 255) / 256;
@@ -462,6 +589,96 @@ void trsv_upload(eig_ctx_t ctx, i64 n, const std::vector<i64> &lrp, const std::v
     stage(0, lrp, lc, lv, ls);
     stage(1, urp, uc, uv, us);
   }
+  // block-inverse images (k_binv_z / k_binv_chain) for factors that fit the staged kernel (every
+  // coupling within kRing4 blocks), when the tiles stay small (a 64 x 64 tile per diagonal block
+  // and per coupled block: at most kBinvTiles tiles, i.e. 64 MiB, and a few 1e8 host FMAs)
+  const i64 nblocks = (n + kTB - 1) / kTB;
+  auto coupled = [&](const std::vector<i64> &rp, const std::vector<i32> &cj, const std::vector<i64> &split,
+                     bool lower) {
+    int dm = 0;
+    for (i64 i = 0; i < n; ++i)
+      for (i64 q = rp[i]; q < split[i]; ++q)
+        dm = std::max<int>(dm, (int)(lower ? i / kTB - cj[q] / kTB : cj[q] / kTB - i / kTB));
+    return dm;
+  };
+  auto binv_image = [&](int f, const std::vector<i64> &rp, const std::vector<i32> &cj, const std::vector<double> &cv,
+                        const std::vector<i64> &split, const double *diag) {
+    const bool lower = diag == nullptr;
+    const int gd = img.gd[f];
+    const size_t T2 = (size_t)kTB * kTB;
+    std::vector<double> dinv((size_t)nblocks * T2, 0.0), gt((size_t)std::max<i64>(nblocks * gd, 1) * T2, 0.0);
+    std::vector<double> Db(T2), Di(T2), Tb(T2);
+    for (i64 b = 0; b < nblocks; ++b)
+    {
+      const i64 bs = b * kTB, nbr = std::min<i64>(kTB, n - bs);
+      // the diagonal block D[r][t] (rows past n: identity)
+      std::fill(Db.begin(), Db.end(), 0.0);
+      for (int r = 0; r < kTB; ++r) Db[r * kTB + r] = (r < nbr && !lower) ? diag[bs + r] : 1.0;
+      for (i64 r = 0; r < nbr; ++r)
+        for (i64 q = split[bs + r]; q < rp[bs + r + 1]; ++q) Db[r * kTB + (cj[q] - bs)] = cv[q];
+      // its inverse, column by column by substitution (lower: top-down, upper: bottom-up)
+      std::fill(Di.begin(), Di.end(), 0.0);
+      for (int j = 0; j < kTB; ++j)
+      {
+        if (lower)
+          for (int i = j; i < kTB; ++i)
+          {
+            double v = i == j ? 1.0 : 0.0;
+            for (int k = j; k < i; ++k) v -= Db[i * kTB + k] * Di[k * kTB + j];
+            Di[i * kTB + j] = v / Db[i * kTB + i];
+          }
+        else
+          for (int i = j; i >= 0; --i)
+          {
+            double v = i == j ? 1.0 : 0.0;
+            for (int k = i + 1; k <= j; ++k) v -= Db[i * kTB + k] * Di[k * kTB + j];
+            Di[i * kTB + j] = v / Db[i * kTB + i];
+          }
+      }
+      for (int r = 0; r < kTB; ++r)
+        for (int t = 0; t < kTB; ++t) dinv[b * T2 + (size_t)t * kTB + r] = Di[r * kTB + t];
+      // G(b, d) = inv(D_b) T(b, d), T(b, d)[r'][t] = the entry of row bs + r' in column t of block b -+ d
+      for (int d = 1; d <= gd; ++d)
+      {
+        const i64 src = lower ? b - d : b + d;
+        if (src < 0 || src >= nblocks) continue;
+        std::fill(Tb.begin(), Tb.end(), 0.0);
+        bool any = false;
+        for (i64 r = 0; r < nbr; ++r)
+          for (i64 q = rp[bs + r]; q < split[bs + r]; ++q)
+            if (cj[q] / kTB == src)
+            {
+              Tb[r * kTB + (cj[q] - src * kTB)] += cv[q];
+              any = true;
+            }
+        if (!any) continue;
+        double *gb = &gt[((size_t)b * gd + (d - 1)) * T2];
+        for (int rr = 0; rr < kTB; ++rr)  // G[:, t] += inv(D)[:, rr] T[rr][t]
+          for (int t = 0; t < kTB; ++t)
+          {
+            const double tv = Tb[rr * kTB + t];
+            if (tv == 0.0) continue;
+            for (int r = 0; r < kTB; ++r) gb[(size_t)t * kTB + r] += Di[r * kTB + rr] * tv;
+          }
+      }
+    }
+    img.dinv[f] = upload(dinv);
+    img.g[f] = upload(gt);
+  };
+  if (img.staged)
+  {
+    img.gd[0] = coupled(lrp, lc, ls, true);
+    img.gd[1] = coupled(urp, uc, us, false);
+    const i64 tiles = nblocks * (2 + img.gd[0] + img.gd[1]);
+    bool pivots = true;  // a zero U pivot leaves the reference's division to produce inf / nan
+    for (i64 i = 0; i < n; ++i) pivots = pivots && ud[i] != 0.0;
+    img.binv = pivots && tiles <= kBinvTiles && img.gd[0] <= kRing4 && img.gd[1] <= kRing4;
+    if (img.binv)
+    {
+      binv_image(0, lrp, lc, lv, ls, nullptr);
+      binv_image(1, urp, uc, uv, us, ud.data());
+    }
+  }
   img.lrp = upload(lrp);
   img.lsplit = upload(ls);
   img.lc = upload(lc);
@@ -480,7 +697,7 @@ void trsv_free(TrsvImage &img)
 {
   for (int f = 0; f < 2; ++f)
     for (void *p : {(void *)img.off1[f], (void *)img.w1[f], (void *)img.v1[f], (void *)img.c1[f], (void *)img.tile[f],
-                    (void *)img.tmask[f]})
+                    (void *)img.tmask[f], (void *)img.dinv[f], (void *)img.g[f]})
       if (p) (void)hipFree(p);
   for (void *p : {(void *)img.lrp, (void *)img.lsplit, (void *)img.lc, (void *)img.lv, (void *)img.urp,
                   (void *)img.usplit, (void *)img.uc, (void *)img.uv, (void *)img.ud, (void *)img.P, (void *)img.Q,
@@ -494,9 +711,29 @@ void launch_inverse_mv8(const TrsvImage &img, i64 m, double *Qin, double *Qout, 
   const i64 n = img.n;
   const int nblk = (int)(m / 8);
   // 1. Qout = P (R Qin)   2. Qin = L^-1 Qout   3. Qin = U^-1 Qin   4. Qout = Q Qin
+  // (block-inverse: Qout = inv(D) P R Qin, Qin = L^-1 chain, Qout = inv(D_U) Qin, Qin = U^-1 chain)
+  // EIGMI_TRSV: "csr" = the row-CSR kernel, "staged" = the block-staged kernel (both bitwise the
+  // reference arithmetic); default: the block-inverse solve when the factor has its image
+  const char *e = std::getenv("EIGMI_TRSV");
+  const std::string kind = e ? std::string(e) : std::string();
+  if (img.binv && kind != "csr" && kind != "staged")
+  {
+    const i64 nblocks = (n + kTB - 1) / kTB;
+    hipLaunchKernelGGL(k_binv_z<true>, dim3((unsigned)nblocks, nblk), dim3(kThreadsT), 0, s, n, (const double *)img.dinv[0],
+                       (const i32 *)img.P, (const double *)img.scale, (const double *)Qin, Qout);
+    hipLaunchKernelGGL(k_binv_chain<true>, dim3(nblk), dim3(kThreadsT), 0, s, n, img.gd[0], (const double *)img.g[0],
+                       (const double *)Qout, Qin);
+    hipLaunchKernelGGL(k_binv_z<false>, dim3((unsigned)nblocks, nblk), dim3(kThreadsT), 0, s, n,
+                       (const double *)img.dinv[1], (const i32 *)nullptr, (const double *)nullptr, (const double *)Qin,
+                       Qout);
+    hipLaunchKernelGGL(k_binv_chain<false>, dim3(nblk), dim3(kThreadsT), 0, s, n, img.gd[1], (const double *)img.g[1],
+                       (const double *)Qout, Qin);
+    hipLaunchKernelGGL(k_perm_out, dim3(grid256(n * nblk)), dim3(256), 0, s, n, nblk, img.Q, Qin, Qout);
+    EIG_HIP(hipGetLastError());
+    return;
+  }
   hipLaunchKernelGGL(k_perm_scale, dim3(grid256(n * nblk)), dim3(256), 0, s, n, nblk, img.P, img.scale, Qin, Qout);
-  const char *e = std::getenv("EIGMI_TRSV");  // "csr": the row-CSR kernel (A/B)
-  if (!img.staged || (e && std::string(e) == "csr"))
+  if (!img.staged || kind == "csr")
   {
     hipLaunchKernelGGL(k_tsolve<true>, dim3(nblk), dim3(kTThreads), 0, s, n, img.lrp, img.lsplit, img.lc, img.lv,
                        (const double *)nullptr, (const double *)Qout, Qin);
