@@ -374,7 +374,7 @@ __global__ __launch_bounds__(kThreadsT) void k_binv_z(i64 n, const double *__res
                                                       double *__restrict__ Z)
 {
   __shared__ double ys[kTB][8];
-  __shared__ double part[8][kTB][8];
+  __shared__ double part[8][kTB][9];  // rows padded to 9 doubles: lane r's stores on distinct banks
   const int tid = threadIdx.x, r = tid & 63, s = tid >> 6;
   const i64 b = blockIdx.x, bs = b * kTB, cb = (i64)blockIdx.y * n * 8;
   {
@@ -407,16 +407,19 @@ __global__ __launch_bounds__(kThreadsT) void k_binv_z(i64 n, const double *__res
 }
 
 // k_binv_chain: one workgroup per 8-column block, the blocks in sequence (L top-down, U bottom-up).
-// Thread (r, s) multiplies the G entries of row r in slice s (prefetched one block ahead) with the
-// solved x rows of that slice, which wave s keeps in a private LDS ring (broadcast reads); the
-// partial sums of the 8 slices meet in LDS (double-buffered by block parity, so one barrier per
-// block), and lane (u, c) of wave s finishes x(row s*8+u, column c) = z - sum, the rows its wave
-// needs from this block later.  gd = number of coupled blocks (G tiles per block).
-template <bool LOWER>
+// Thread (r, s) multiplies the G entries of row r in slice s with the solved x rows of that slice,
+// which wave s keeps in a private LDS ring (broadcast reads); the partial sums of the 8 slices meet
+// in LDS (double-buffered by block parity, so one barrier per block), and lane (u, c) of wave s
+// finishes x(row s*8+u, column c) = z - sum, the rows its wave needs from this block later.
+// GD = coupled blocks (G tiles per block, gd <= GD at run time).  The G tiles and z of the next PF
+// blocks are in flight in a register ring (PF buffers, the loop unrolled by PF so every buffer index
+// is static).  The partials' rows are padded to 9 doubles: lane r's 8 stores then fall on distinct
+// banks (a 64-B row stride put 8 lanes on each bank pair).
+template <bool LOWER, int GD, int PF>
 __global__ __launch_bounds__(kThreadsT) void k_binv_chain(i64 n, int gd, const double *__restrict__ G,
                                                           const double *Z, double *X)
 {
-  __shared__ double part[2][8][kTB][8];
+  __shared__ double part[2][8][kTB][9];
   __shared__ double ring[8][kRing4][8][8];  // [wave s][slot][row u of slice s][column]
   const int tid = threadIdx.x, r = tid & 63, s = tid >> 6;
   const int u = r >> 3, c = r & 7;  // the reduction role of lane r
@@ -424,59 +427,93 @@ __global__ __launch_bounds__(kThreadsT) void k_binv_chain(i64 n, int gd, const d
   const i64 nblocks = (n + kTB - 1) / kTB;
 #pragma unroll
   for (int q = 0; q < kRing4; ++q) ring[s][q][u][c] = 0.0;
-  double pg[kRing4][8], pz = 0.0;
-  auto prefetch = [&](i64 blk) {
+  double pg[PF][GD][8], pz[PF];
+  // tiles and z of the bi-th block solved.  Every load is unconditional (clamped block, tile and row
+  // indices; values past the end are never used or are masked at use), the loop runs a whole number
+  // of PF rounds (padded blocks compute but store nothing), and a buffer is refilled only once its
+  // old contents are dead (the tiles after the products, z after x): otherwise the compiler merges
+  // the loaded register into the loop-carried one with a copy right behind the load
+  // (s_waitcnt vmcnt(0)), which serialised the prefetch ring on the load latency.
+  auto fetch_g = [&](i64 bi, double (&g)[GD][8]) {
+    const i64 bc = bi < nblocks ? bi : nblocks - 1;
+    const i64 blk = LOWER ? bc : nblocks - 1 - bc;
     const double *gb = G + blk * gd * (kTB * kTB);
 #pragma unroll
-    for (int d = 0; d < kRing4; ++d)
-      if (d < gd)
+    for (int d = 0; d < GD; ++d)
+    {
+      const int dd = d < gd ? d : 0;  // (gd = 0: the one-tile placeholder buffer)
 #pragma unroll
-        for (int q = 0; q < 8; ++q) pg[d][q] = gb[d * (kTB * kTB) + (s * 8 + q) * kTB + r];
-    const i64 i = blk * kTB + s * 8 + u;
-    pz = i < n ? gld(Z + cb + i * 8 + c) : 0.0;
+      for (int q = 0; q < 8; ++q) g[d][q] = gb[dd * (kTB * kTB) + (s * 8 + q) * kTB + r];
+    }
   };
-  prefetch(LOWER ? 0 : nblocks - 1);
-  for (i64 bi = 0; bi < nblocks; ++bi)
+  auto fetch_z = [&](i64 bi, double &z) {
+    const i64 bc = bi < nblocks ? bi : nblocks - 1;
+    const i64 i = (LOWER ? bc : nblocks - 1 - bc) * kTB + s * 8 + u;
+    z = gld(Z + cb + (i < n ? i : n - 1) * 8 + c);
+  };
+#pragma unroll
+  for (int p = 0; p < PF; ++p)
   {
-    const i64 blk = LOWER ? bi : nblocks - 1 - bi;
-    double g[kRing4][8];
-#pragma unroll
-    for (int d = 0; d < kRing4; ++d)
-#pragma unroll
-      for (int q = 0; q < 8; ++q) g[d][q] = pg[d][q];
-    const double z = pz;
-    if (bi + 1 < nblocks) prefetch(LOWER ? blk + 1 : blk - 1);
-    double acc[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) acc[k] = 0.0;
-#pragma unroll
-    for (int d = 0; d < kRing4; ++d)
-      if (d < gd && d < bi)  // block blk -+ (d + 1) exists and is solved
-      {
-        const i64 src = LOWER ? blk - (d + 1) : blk + (d + 1);
-        const double(*xr)[8] = ring[s][src & (kRing4 - 1)];
-#pragma unroll
-        for (int q = 0; q < 8; ++q)
-#pragma unroll
-          for (int k = 0; k < 8; ++k) acc[k] = fma(g[d][q], xr[q][k], acc[k]);
-      }
-    double(*pp)[kTB][8] = part[bi & 1];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) pp[s][r][k] = acc[k];
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): LDS-only barrier, the prefetch stays in flight
-    __builtin_amdgcn_s_barrier();
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    const int t = s * 8 + u;
-    double sum = pp[0][t][c];
-#pragma unroll
-    for (int q = 1; q < 8; ++q) sum += pp[q][t][c];
-    const double x = z - sum;
-    ring[s][blk & (kRing4 - 1)][u][c] = x;  // read back by this wave only (LDS is in order per wave)
-    const i64 i = blk * kTB + t;
-    if (i < n) gst(X + cb + i * 8 + c, x);
-    __builtin_amdgcn_wave_barrier();
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    fetch_g(p, pg[p]);
+    fetch_z(p, pz[p]);
   }
+  const i64 nround = (nblocks + PF - 1) / PF * PF;
+  for (i64 b0 = 0; b0 < nround; b0 += PF)
+  {
+#pragma unroll
+    for (int p = 0; p < PF; ++p)
+    {
+      const i64 bi = b0 + p;
+      const bool live = bi < nblocks;  // (uniform)
+      const i64 blk = LOWER ? bi : nblocks - 1 - bi;
+      double acc[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] = 0.0;
+#pragma unroll
+      for (int d = 0; d < GD; ++d)
+        if (d < gd && d < bi)  // block blk -+ (d + 1) exists and is solved
+        {
+          const i64 src = LOWER ? blk - (d + 1) : blk + (d + 1);
+          const double(*xr)[8] = ring[s][src & (kRing4 - 1)];
+#pragma unroll
+          for (int q = 0; q < 8; ++q)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) acc[k] = fma(pg[p][d][q], xr[q][k], acc[k]);
+        }
+      fetch_g(bi + PF, pg[p]);  // the tiles of the block PF ahead
+      double(*pp)[kTB][9] = part[bi & 1];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) pp[s][r][k] = acc[k];
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): LDS-only barrier, the tile loads stay in flight
+      __builtin_amdgcn_s_barrier();
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      const int t = s * 8 + u;
+      double sum = pp[0][t][c];
+#pragma unroll
+      for (int q = 1; q < 8; ++q) sum += pp[q][t][c];
+      const i64 i = blk * kTB + t;
+      const bool own = live && i < n;
+      const double x = (own ? pz[p] : 0.0) - sum;  // rows past n: 0 (their G columns are zero)
+      ring[s][blk & (kRing4 - 1)][u][c] = x;  // read back by this wave only (LDS is in order per wave)
+      if (own) gst(X + cb + i * 8 + c, x);
+      fetch_z(bi + PF, pz[p]);
+      __builtin_amdgcn_wave_barrier();
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    }
+  }
+}
+
+template <bool LOWER>
+void launch_binv_chain(int gd, int nblk, i64 n, const double *G, const double *Z, double *X, hipStream_t s)
+{
+  // prefetch depth by register budget: PF x GD x 8 doubles per thread (512-thread workgroups: up to
+  // 256 VGPRs per lane)
+  if (gd <= 1)
+    hipLaunchKernelGGL((k_binv_chain<LOWER, 1, 4>), dim3(nblk), dim3(kThreadsT), 0, s, n, gd, G, Z, X);
+  else if (gd == 2)
+    hipLaunchKernelGGL((k_binv_chain<LOWER, 2, 3>), dim3(nblk), dim3(kThreadsT), 0, s, n, gd, G, Z, X);
+  else
+    hipLaunchKernelGGL((k_binv_chain<LOWER, 4, 2>), dim3(nblk), dim3(kThreadsT), 0, s, n, gd, G, Z, X);
 }
 
 int grid256(i64 work)
@@ -721,13 +758,11 @@ void launch_inverse_mv8(const TrsvImage &img, i64 m, double *Qin, double *Qout, 
     const i64 nblocks = (n + kTB - 1) / kTB;
     hipLaunchKernelGGL(k_binv_z<true>, dim3((unsigned)nblocks, nblk), dim3(kThreadsT), 0, s, n, (const double *)img.dinv[0],
                        (const i32 *)img.P, (const double *)img.scale, (const double *)Qin, Qout);
-    hipLaunchKernelGGL(k_binv_chain<true>, dim3(nblk), dim3(kThreadsT), 0, s, n, img.gd[0], (const double *)img.g[0],
-                       (const double *)Qout, Qin);
+    launch_binv_chain<true>(img.gd[0], nblk, n, img.g[0], Qout, Qin, s);
     hipLaunchKernelGGL(k_binv_z<false>, dim3((unsigned)nblocks, nblk), dim3(kThreadsT), 0, s, n,
                        (const double *)img.dinv[1], (const i32 *)nullptr, (const double *)nullptr, (const double *)Qin,
                        Qout);
-    hipLaunchKernelGGL(k_binv_chain<false>, dim3(nblk), dim3(kThreadsT), 0, s, n, img.gd[1], (const double *)img.g[1],
-                       (const double *)Qout, Qin);
+    launch_binv_chain<false>(img.gd[1], nblk, n, img.g[1], Qout, Qin, s);
     hipLaunchKernelGGL(k_perm_out, dim3(grid256(n * nblk)), dim3(256), 0, s, n, nblk, img.Q, Qin, Qout);
     EIG_HIP(hipGetLastError());
     return;

@@ -242,15 +242,18 @@ def test_generalized_inverse_pu_mass(ctx):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["laplace2d_64", "laplace2d_100", "poisson3d_12", "poisson3d_20"])
+@pytest.mark.parametrize("name", ["laplace2d_64", "laplace2d_100", "poisson3d_12", "poisson3d_16", "poisson3d_20"])
 @pytest.mark.parametrize("kernel", ["staged", "csr", None])
 def test_inverse_mv8_kernels(ctx, name, kernel):
     """The bitwise triangular-solve kernels (k_tsolve_staged: envelope factors of bandwidth <= 256;
     k_tsolve: any factor) reproduce the reference arithmetic bitwise; the default block-inverse
     solve (factors that fit the staged image) to BINV_RTOL.  poisson3d_20's RCM envelope reaches
-    past 256 rows: it always takes k_tsolve.  laplace2d_100: n = 10000, a ragged last block."""
+    past 256 rows: it always takes k_tsolve.  laplace2d_100: n = 10000, a ragged last block.  The
+    block-inverse chain's coupled-block counts: laplace2d_64 1, laplace2d_100 / poisson3d_12 2,
+    poisson3d_16 4 (RCM bandwidth 200)."""
     A = {"laplace2d_64": lambda: oracle.laplace2d(64), "laplace2d_100": lambda: oracle.laplace2d(100),
-         "poisson3d_12": lambda: oracle.poisson3d(12), "poisson3d_20": lambda: oracle.poisson3d(20)}[name]()
+         "poisson3d_12": lambda: oracle.poisson3d(12),
+         "poisson3d_16": lambda: oracle.poisson3d(16), "poisson3d_20": lambda: oracle.poisson3d(20)}[name]()
     lu, f = _gpu_lu(ctx, A, "bcsr")
     X = oracle.random_mv8(A.n, 16, 3)
     ref_out, _ = oracle.inverse_mv8(f, X, 16)
