@@ -457,6 +457,9 @@ __global__ __launch_bounds__(kThreadsT) void k_binv_chain(i64 n, int gd, const d
     fetch_g(p, pg[p]);
     fetch_z(p, pz[p]);
   }
+  // the prologue's loads complete before the loop: the loop header then sees only the latch's
+  // pending loads, and the first use of a round waits for its own tiles (vmcnt(N)), not vmcnt(0)
+  __builtin_amdgcn_s_waitcnt(0);
   const i64 nround = (nblocks + PF - 1) / PF * PF;
   for (i64 b0 = 0; b0 < nround; b0 += PF)
   {
