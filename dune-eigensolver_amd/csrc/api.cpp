@@ -1362,6 +1362,13 @@ void gram_device(eig_ctx_t ctx, i64 n, i64 m1, i64 m2, const double *Q1, const d
   allreduce_sum(ctx, G, m1 * m2, ctx->stream);
 }
 
+// EIGMI_MGS_SMALL=0 keeps the grid-wide MGS passes for small blocks too (A/B, tests)
+static bool mgs_small_disabled()
+{
+  const char *e = std::getenv("EIGMI_MGS_SMALL");
+  return e && e[0] == '0';
+}
+
 void orthonormalize_device(eig_ctx_t ctx, i64 n, i64 m, double *Q, int variant)
 {
   hipStream_t s = ctx->stream;
@@ -1373,7 +1380,10 @@ void orthonormalize_device(eig_ctx_t ctx, i64 n, i64 m, double *Q, int variant)
   for (i64 bk = 0; bk < m; bk += 8)
   {
     double *Qb = Q + bk * n;
-    if (variant == EIG_ORTHO_MGS)
+    if (variant == EIG_ORTHO_MGS && !ctx->distributed() && !mgs_small_disabled() && launch_mgs_small(n, Qb, s))
+    {
+    }
+    else if (variant == EIG_ORTHO_MGS)
     {
       for (int k = 0; k <= 8; ++k)
       {

@@ -273,6 +273,8 @@ void launch_gram_mv8(i64 n, i64 m1, i64 m2, const double *Q1, const double *Q2, 
                      hipStream_t s, ReduceWS red);
 // Block Gram-Schmidt building blocks, see k_mv8.hip.
 void launch_mgs_pass(i64 n, double *Qb, int k, double *S, int ticket, hipStream_t s, ReduceWS red);
+// Whole column MGS of one 8-column block in one workgroup (n <= 4096, one rank); false = not taken.
+bool launch_mgs_small(i64 n, double *Qb, hipStream_t s);
 void launch_apply_upper(i64 n, double *Qb, const double *U, hipStream_t s);
 void launch_cholqr_factor(const double *G, double *U, double *normmax, int flags, hipStream_t s);
 void launch_project(i64 n, i64 mrest, const double *Qk, double *Qrest, const double *S, hipStream_t s);

@@ -284,6 +284,96 @@ void launch_mgs_pass(i64 n, double *Qb, int k, double *Ssum, int ticket, hipStre
 }
 
 // ---------------------------------------------------------------------------------------------
+// The same column MGS for a small block (n <= 512 R rows, one rank), in ONE workgroup: the 512
+// threads keep their R rows in registers for all 8 passes, and each pass's sums meet in a
+// workgroup reduction (a xor-shuffle tree per wave, the 8 wave partials summed in wave order by
+// every thread), so the block is read and written once and the 9 grid-wide launches with their
+// reduction tails (10 us each at n = 4096, launch-bound) become one launch.  Per row the
+// operations are those of k_mgs_pass; only the sums' order differs (tolerance, as there).
+// ---------------------------------------------------------------------------------------------
+constexpr int kMgsSmallThreads = 512;
+
+template <int R>
+__global__ __launch_bounds__(kMgsSmallThreads) void k_mgs_small(i64 n, double *__restrict__ Qb)
+{
+  __shared__ double red[2][kMgsSmallThreads / 64][8];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  double q[R][8];
+#pragma unroll
+  for (int t = 0; t < R; ++t)
+  {
+    const i64 i = tid + (i64)t * kMgsSmallThreads;
+    const double2 *row = reinterpret_cast<const double2 *>(Qb + (i < n ? i : 0) * 8);
+#pragma unroll
+    for (int h = 0; h < 4; ++h)
+    {
+      const double2 v = i < n ? row[h] : make_double2(0.0, 0.0);
+      q[t][2 * h] = v.x;
+      q[t][2 * h + 1] = v.y;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k)
+  {
+    double acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.0;
+#pragma unroll
+    for (int t = 0; t < R; ++t)
+#pragma unroll
+      for (int j = k; j < 8; ++j) acc[j] += q[t][k] * q[t][j];  // (rows past n are zero)
+#pragma unroll
+    for (int j = k; j < 8; ++j)
+    {
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) acc[j] += __shfl_xor(acc[j], o, 64);
+      if (lane == 0) red[k & 1][wave][j] = acc[j];
+    }
+    __syncthreads();
+    double sk[8];
+#pragma unroll
+    for (int j = k; j < 8; ++j)
+    {
+      double v = red[k & 1][0][j];
+#pragma unroll
+      for (int w = 1; w < kMgsSmallThreads / 64; ++w) v += red[k & 1][w][j];
+      sk[j] = v;
+    }
+    // S[k][j] = s[k][j] / s[k][k] (j > k), S[k][k] = 1 / sqrt(s[k][k]) (kernels_cpp.hh:214-228)
+    const double skk = sk[k];
+#pragma unroll
+    for (int t = 0; t < R; ++t)
+    {
+#pragma unroll
+      for (int j = k + 1; j < 8; ++j) q[t][j] -= (sk[j] / skk) * q[t][k];
+      q[t][k] *= 1.0 / sqrt(skk);
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < R; ++t)
+  {
+    const i64 i = tid + (i64)t * kMgsSmallThreads;
+    if (i < n)
+    {
+      double2 *row = reinterpret_cast<double2 *>(Qb + i * 8);
+#pragma unroll
+      for (int h = 0; h < 4; ++h) row[h] = make_double2(q[t][2 * h], q[t][2 * h + 1]);
+    }
+  }
+}
+
+bool launch_mgs_small(i64 n, double *Qb, hipStream_t s)
+{
+  if (n <= 0 || n > 8 * kMgsSmallThreads) return false;
+  const dim3 g(1), b(kMgsSmallThreads);
+  if (n <= kMgsSmallThreads) hipLaunchKernelGGL(k_mgs_small<1>, g, b, 0, s, n, Qb);
+  else if (n <= 2 * kMgsSmallThreads) hipLaunchKernelGGL(k_mgs_small<2>, g, b, 0, s, n, Qb);
+  else if (n <= 4 * kMgsSmallThreads) hipLaunchKernelGGL(k_mgs_small<4>, g, b, 0, s, n, Qb);
+  else hipLaunchKernelGGL(k_mgs_small<8>, g, b, 0, s, n, Qb);
+  return true;
+}
+
+// ---------------------------------------------------------------------------------------------
 // CholQR factor of an 8x8 Gram (kernels_avx2.hh:185-252 / kernels_cpp.hh:474-526), one thread:
 // LU without pivoting, D = diag^-1/2, U = L^-T D.  flags & 1: take the UPPER triangle of G and
 // mirror it (B_orthonormalize_blocked :457-459), and fold max_{k<j} G[k][j] into *normmax.

@@ -115,7 +115,7 @@ def test_gram_mfma(ctx, n, m1, m2):
 
 
 @pytest.mark.parametrize("variant,name", [(eigmi.ORTHO_MGS, "mgs"), (eigmi.ORTHO_CHOLQR, "cholqr")])
-@pytest.mark.parametrize("n,m", [(4096, 8), (4096, 32), (5000, 16)])
+@pytest.mark.parametrize("n,m", [(4096, 8), (4096, 32), (5000, 16), (100, 8), (1000, 16), (2048, 8)])
 def test_orthonormalize_blocked(ctx, variant, name, n, m):
     Qh = oracle.random_mv8(n, m, 21)
     Q = ctx.array(Qh)
@@ -125,6 +125,20 @@ def test_orthonormalize_blocked(ctx, variant, name, n, m):
     assert np.abs(got.T @ got - np.eye(m)).max() < 1e-13
     # same thin QR as the reference algorithm: elementwise within 1e-12 (random, well conditioned)
     assert np.abs(got - ref).max() < 1e-12
+
+
+@pytest.mark.parametrize("n,m", [(3000, 16), (4096, 8), (513, 8)])
+def test_mgs_small_vs_grid(ctx, n, m, monkeypatch):
+    """n <= 4096 on one rank: the diagonal block's MGS runs in one workgroup (k_mgs_small); the
+    grid-wide passes (EIGMI_MGS_SMALL=0) do the same per-row operations, so the two agree to the
+    rounding of the sums' order."""
+    Qh = oracle.random_mv8(n, m, 5)
+    Qa, Qb = ctx.array(Qh), ctx.array(Qh)
+    eigmi.orthonormalize_mv8(ctx, n, m, Qa, eigmi.ORTHO_MGS)
+    monkeypatch.setenv("EIGMI_MGS_SMALL", "0")
+    eigmi.orthonormalize_mv8(ctx, n, m, Qb, eigmi.ORTHO_MGS)
+    a, b = Qa.get(), Qb.get()
+    assert np.all(np.isfinite(a)) and np.abs(a - b).max() < 1e-13
 
 
 def test_orthonormalize_naive(ctx):
