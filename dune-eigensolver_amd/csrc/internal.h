@@ -9,6 +9,7 @@
 #include <new>
 #include <stdexcept>
 #include <string>
+#include <memory>
 #include <vector>
 
 #include "../../include/eigmi.h"
@@ -335,6 +336,10 @@ struct TrsvImage {
   double *tile[2] = {nullptr, nullptr};
   unsigned long long *tmask[2] = {nullptr, nullptr};
   bool staged = false;  // the factors fit k_tsolve_staged (k_trsv.hip)
+  // the staged image is built on first use (EIGMI_TRSV=staged, or factors without the
+  // block-inverse image): host copies of the split factor rows until then
+  bool staged_built = false;
+  std::shared_ptr<struct TrsvHostRows> host;
   // Block-inverse image (k_binv_z / k_binv_chain, k_trsv.hip), per factor: the inverse of every
   // 64 x 64 diagonal block, dinv + b * 4096 as [t][r], and G(b, d) = inv(D_b) T(b, d) for the
   // coupling T(b, d) of block b to the block d before it (L) / after it (U), g + (b * gd + d - 1) * 4096
@@ -348,7 +353,7 @@ void trsv_upload(eig_ctx_t ctx, i64 n, const std::vector<i64> &lrp, const std::v
                  const std::vector<double> &uv, const std::vector<double> &ud, const std::vector<i64> &P,
                  const std::vector<i64> &Q, const std::vector<double> &scale, TrsvImage &img);
 void trsv_free(TrsvImage &img);
-void launch_inverse_mv8(const TrsvImage &img, i64 m, double *Qin, double *Qout, hipStream_t s);
+void launch_inverse_mv8(TrsvImage &img, i64 m, double *Qin, double *Qout, hipStream_t s);
 void lu_inverse_device(eig_lu_t lu, i64 m, double *Qin, double *Qout, hipStream_t s);
 i64 lu_size(eig_lu_t lu);
 

@@ -22,6 +22,9 @@
 // k_binv_chain below; to rounding, not bitwise); EIGMI_TRSV=staged / csr keep the bitwise kernels.
 #include "internal.h"
 
+#include <chrono>
+#include <cstdio>
+
 namespace eigmi {
 
 namespace {
@@ -535,32 +538,22 @@ T *upload(const std::vector<T> &h)
 }
 }  // namespace
 
-void trsv_upload(eig_ctx_t ctx, i64 n, const std::vector<i64> &lrp, const std::vector<i32> &lc,
-                 const std::vector<double> &lv, const std::vector<i64> &urp, const std::vector<i32> &uc,
-                 const std::vector<double> &uv, const std::vector<double> &ud, const std::vector<i64> &P,
-                 const std::vector<i64> &Q, const std::vector<double> &scale, TrsvImage &img)
+struct TrsvHostRows {
+  std::vector<i64> lrp;
+  std::vector<i32> lc;
+  std::vector<double> lv;
+  std::vector<i64> ls, urp;
+  std::vector<i32> uc;
+  std::vector<double> uv;
+  std::vector<i64> us;
+};
+
+namespace {
+// Build the block-staged images (k_tsolve_staged) from the host rows kept at upload.
+void build_staged(TrsvImage &img)
 {
-  (void)ctx;
-  img.n = n;
-  // split points: L row i -> first entry inside i's 64-row block; U row i (descending columns) ->
-  // first entry with a column inside the block
-  std::vector<i64> ls(n), us(n);
-  for (i64 i = 0; i < n; ++i)
-  {
-    const i64 bs = i / kTB * kTB, be = std::min(bs + kTB, n);
-    i64 k = lrp[i];
-    while (k < lrp[i + 1] && lc[k] < bs) ++k;
-    ls[i] = k;
-    k = urp[i];
-    while (k < urp[i + 1] && uc[k] >= be) ++k;
-    us[i] = k;
-  }
-  std::vector<i32> p32(n), q32(n);
-  for (i64 k = 0; k < n; ++k)
-  {
-    p32[k] = (i32)P[k];
-    q32[k] = (i32)Q[k];
-  }
+  const i64 n = img.n;
+  const TrsvHostRows &H = *img.host;
   // block-staged images (k_tsolve_staged): per 64-row block, the outside-the-block entries of each
   // row as an ELL slab [k][r] in the row's own order, the inside entries as a dense tile [t][r]
   auto stage = [&](int f, const std::vector<i64> &rp, const std::vector<i32> &cj, const std::vector<double> &cv,
@@ -609,6 +602,48 @@ void trsv_upload(eig_ctx_t ctx, i64 n, const std::vector<i64> &lrp, const std::v
     img.tile[f] = upload(tl);
     img.tmask[f] = upload(tm);
   };
+  stage(0, H.lrp, H.lc, H.lv, H.ls);
+  stage(1, H.urp, H.uc, H.uv, H.us);
+  img.staged_built = true;
+  img.host.reset();
+}
+}  // namespace
+
+void trsv_upload(eig_ctx_t ctx, i64 n, const std::vector<i64> &lrp, const std::vector<i32> &lc,
+                 const std::vector<double> &lv, const std::vector<i64> &urp, const std::vector<i32> &uc,
+                 const std::vector<double> &uv, const std::vector<double> &ud, const std::vector<i64> &P,
+                 const std::vector<i64> &Q, const std::vector<double> &scale, TrsvImage &img)
+{
+  (void)ctx;
+  img.n = n;
+  // EIGMI_TRACE_SETUP=1: phase times of the upload on stderr
+  const bool trace = std::getenv("EIGMI_TRACE_SETUP") != nullptr;
+  auto t_last = std::chrono::steady_clock::now();
+  auto phase = [&](const char *what) {
+    if (!trace) return;
+    const auto now = std::chrono::steady_clock::now();
+    fprintf(stderr, "trsv_upload %-10s %8.2f ms\n", what, std::chrono::duration<double, std::milli>(now - t_last).count());
+    t_last = now;
+  };
+  // split points: L row i -> first entry inside i's 64-row block; U row i (descending columns) ->
+  // first entry with a column inside the block
+  std::vector<i64> ls(n), us(n);
+  for (i64 i = 0; i < n; ++i)
+  {
+    const i64 bs = i / kTB * kTB, be = std::min(bs + kTB, n);
+    i64 k = lrp[i];
+    while (k < lrp[i + 1] && lc[k] < bs) ++k;
+    ls[i] = k;
+    k = urp[i];
+    while (k < urp[i + 1] && uc[k] >= be) ++k;
+    us[i] = k;
+  }
+  std::vector<i32> p32(n), q32(n);
+  for (i64 k = 0; k < n; ++k)
+  {
+    p32[k] = (i32)P[k];
+    q32[k] = (i32)Q[k];
+  }
   // admission to the staged kernel: <= kSlab outside entries per row, all within kRing4 blocks
   auto fits = [&](const std::vector<i64> &rp, const std::vector<i32> &cj, const std::vector<i64> &split, bool lower) {
     for (i64 i = 0; i < n; ++i)
@@ -623,12 +658,11 @@ void trsv_upload(eig_ctx_t ctx, i64 n, const std::vector<i64> &lrp, const std::v
     }
     return true;
   };
+  phase("split");
   img.staged = fits(lrp, lc, ls, true) && fits(urp, uc, us, false);
   if (img.staged)
-  {
-    stage(0, lrp, lc, lv, ls);
-    stage(1, urp, uc, uv, us);
-  }
+    img.host = std::make_shared<TrsvHostRows>(TrsvHostRows{lrp, lc, lv, ls, urp, uc, uv, us});
+  phase("staged");
   // block-inverse images (k_binv_z / k_binv_chain) for factors that fit the staged kernel (every
   // coupling within kRing4 blocks), when the tiles stay small (a 64 x 64 tile per diagonal block
   // and per coupled block: at most kBinvTiles tiles, i.e. 64 MiB, and a few 1e8 host FMAs)
@@ -647,6 +681,8 @@ void trsv_upload(eig_ctx_t ctx, i64 n, const std::vector<i64> &lrp, const std::v
     const int gd = img.gd[f];
     const size_t T2 = (size_t)kTB * kTB;
     std::vector<double> dinv((size_t)nblocks * T2, 0.0), gt((size_t)std::max<i64>(nblocks * gd, 1) * T2, 0.0);
+    // Di holds inv(D_b) by columns (Di[j * 64 + i] = inv(D)[i][j]): each column is one triangular
+    // solve with contiguous operands, and it is already the device layout of dinv ([t][r])
     std::vector<double> Db(T2), Di(T2), Tb(T2);
     for (i64 b = 0; b < nblocks; ++b)
     {
@@ -656,27 +692,29 @@ void trsv_upload(eig_ctx_t ctx, i64 n, const std::vector<i64> &lrp, const std::v
       for (int r = 0; r < kTB; ++r) Db[r * kTB + r] = (r < nbr && !lower) ? diag[bs + r] : 1.0;
       for (i64 r = 0; r < nbr; ++r)
         for (i64 q = split[bs + r]; q < rp[bs + r + 1]; ++q) Db[r * kTB + (cj[q] - bs)] = cv[q];
-      // its inverse, column by column by substitution (lower: top-down, upper: bottom-up)
+      // its inverse, column j = the solution of D x = e_j (lower: top-down, upper: bottom-up)
       std::fill(Di.begin(), Di.end(), 0.0);
       for (int j = 0; j < kTB; ++j)
       {
+        double *x = &Di[(size_t)j * kTB];
         if (lower)
           for (int i = j; i < kTB; ++i)
           {
+            const double *Dr = &Db[(size_t)i * kTB];
             double v = i == j ? 1.0 : 0.0;
-            for (int k = j; k < i; ++k) v -= Db[i * kTB + k] * Di[k * kTB + j];
-            Di[i * kTB + j] = v / Db[i * kTB + i];
+            for (int k = j; k < i; ++k) v -= Dr[k] * x[k];
+            x[i] = v / Dr[i];
           }
         else
           for (int i = j; i >= 0; --i)
           {
+            const double *Dr = &Db[(size_t)i * kTB];
             double v = i == j ? 1.0 : 0.0;
-            for (int k = i + 1; k <= j; ++k) v -= Db[i * kTB + k] * Di[k * kTB + j];
-            Di[i * kTB + j] = v / Db[i * kTB + i];
+            for (int k = i + 1; k <= j; ++k) v -= Dr[k] * x[k];
+            x[i] = v / Dr[i];
           }
       }
-      for (int r = 0; r < kTB; ++r)
-        for (int t = 0; t < kTB; ++t) dinv[b * T2 + (size_t)t * kTB + r] = Di[r * kTB + t];
+      std::copy(Di.begin(), Di.end(), dinv.begin() + (size_t)b * T2);
       // G(b, d) = inv(D_b) T(b, d), T(b, d)[r'][t] = the entry of row bs + r' in column t of block b -+ d
       for (int d = 1; d <= gd; ++d)
       {
@@ -693,13 +731,18 @@ void trsv_upload(eig_ctx_t ctx, i64 n, const std::vector<i64> &lrp, const std::v
             }
         if (!any) continue;
         double *gb = &gt[((size_t)b * gd + (d - 1)) * T2];
-        for (int rr = 0; rr < kTB; ++rr)  // G[:, t] += inv(D)[:, rr] T[rr][t]
+        for (int rr = 0; rr < kTB; ++rr)  // G[:, t] += inv(D)[:, rr] T[rr][t] (column rr of inv(D):
+        {                                 // rows rr.. (lower) / ..rr (upper) are its nonzeros)
+          const double *dcol = &Di[(size_t)rr * kTB];
+          const int r0 = lower ? rr : 0, r1 = lower ? kTB : rr + 1;
           for (int t = 0; t < kTB; ++t)
           {
             const double tv = Tb[rr * kTB + t];
             if (tv == 0.0) continue;
-            for (int r = 0; r < kTB; ++r) gb[(size_t)t * kTB + r] += Di[r * kTB + rr] * tv;
+            double *gcol = gb + (size_t)t * kTB;
+            for (int r = r0; r < r1; ++r) gcol[r] += dcol[r] * tv;
           }
+        }
       }
     }
     img.dinv[f] = upload(dinv);
@@ -719,6 +762,7 @@ void trsv_upload(eig_ctx_t ctx, i64 n, const std::vector<i64> &lrp, const std::v
       binv_image(1, urp, uc, uv, us, ud.data());
     }
   }
+  phase("binv");
   img.lrp = upload(lrp);
   img.lsplit = upload(ls);
   img.lc = upload(lc);
@@ -731,6 +775,7 @@ void trsv_upload(eig_ctx_t ctx, i64 n, const std::vector<i64> &lrp, const std::v
   img.P = upload(p32);
   img.Q = upload(q32);
   img.scale = upload(scale);
+  phase("csr");
 }
 
 void trsv_free(TrsvImage &img)
@@ -746,7 +791,7 @@ void trsv_free(TrsvImage &img)
   img = TrsvImage();
 }
 
-void launch_inverse_mv8(const TrsvImage &img, i64 m, double *Qin, double *Qout, hipStream_t s)
+void launch_inverse_mv8(TrsvImage &img, i64 m, double *Qin, double *Qout, hipStream_t s)
 {
   const i64 n = img.n;
   const int nblk = (int)(m / 8);
@@ -770,6 +815,7 @@ void launch_inverse_mv8(const TrsvImage &img, i64 m, double *Qin, double *Qout, 
     EIG_HIP(hipGetLastError());
     return;
   }
+  if (img.staged && !img.staged_built && kind != "csr") build_staged(img);
   hipLaunchKernelGGL(k_perm_scale, dim3(grid256(n * nblk)), dim3(256), 0, s, n, nblk, img.P, img.scale, Qin, Qout);
   if (!img.staged || kind == "csr")
   {
