@@ -326,6 +326,7 @@ struct TrsvImage {
   double *uv = nullptr, *ud = nullptr;
   i32 *P = nullptr, *Q = nullptr;
   double *scale = nullptr;                // Rs[P[k]] (do_recip) or 1 / Rs[P[k]]
+  void *arena = nullptr;                  // the one allocation holding lrp .. scale
   // Block-staged image (k_tsolve_staged, k_trsv.hip), per factor (0 = L, 1 = U) and 64-row block b:
   // the entries outside the block as an ELL slab [k][r] (off1[b] .. + w1[b] * 64; column -1 =
   // padding), the entries inside it as a dense 64 x 64 tile [t][r] (tile + b * 4096) + row masks.

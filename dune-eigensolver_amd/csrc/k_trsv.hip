@@ -23,6 +23,7 @@
 #include "internal.h"
 
 #include <chrono>
+#include <cstring>
 #include <cstdio>
 
 namespace eigmi {
@@ -763,18 +764,42 @@ void trsv_upload(eig_ctx_t ctx, i64 n, const std::vector<i64> &lrp, const std::v
     }
   }
   phase("binv");
-  img.lrp = upload(lrp);
-  img.lsplit = upload(ls);
-  img.lc = upload(lc);
-  img.lv = upload(lv);
-  img.urp = upload(urp);
-  img.usplit = upload(us);
-  img.uc = upload(uc);
-  img.uv = upload(uv);
-  img.ud = upload(ud);
-  img.P = upload(p32);
-  img.Q = upload(q32);
-  img.scale = upload(scale);
+  // the row-CSR factors, permutations and scaling: ONE device allocation and ONE copy (a dozen
+  // separate small hipMalloc + hipMemcpy calls cost ~1 ms each)
+  {
+    std::vector<std::pair<const void *, size_t>> parts = {
+        {lrp.data(), lrp.size() * 8}, {ls.data(), ls.size() * 8},   {lc.data(), lc.size() * 4},
+        {lv.data(), lv.size() * 8},   {urp.data(), urp.size() * 8}, {us.data(), us.size() * 8},
+        {uc.data(), uc.size() * 4},   {uv.data(), uv.size() * 8},   {ud.data(), ud.size() * 8},
+        {p32.data(), p32.size() * 4}, {q32.data(), q32.size() * 4}, {scale.data(), scale.size() * 8}};
+    std::vector<size_t> off(parts.size());
+    size_t total = 0;
+    for (size_t k = 0; k < parts.size(); ++k)
+    {
+      off[k] = total;
+      total += (std::max<size_t>(parts[k].second, 8) + 255) / 256 * 256;
+    }
+    std::vector<char> h(total, 0);
+    for (size_t k = 0; k < parts.size(); ++k)
+      if (parts[k].second) std::memcpy(h.data() + off[k], parts[k].first, parts[k].second);
+    void *d = nullptr;
+    EIG_HIP(hipMalloc(&d, total));
+    EIG_HIP(hipMemcpy(d, h.data(), total, hipMemcpyHostToDevice));
+    char *b = static_cast<char *>(d);
+    img.arena = d;
+    img.lrp = (i64 *)(b + off[0]);
+    img.lsplit = (i64 *)(b + off[1]);
+    img.lc = (i32 *)(b + off[2]);
+    img.lv = (double *)(b + off[3]);
+    img.urp = (i64 *)(b + off[4]);
+    img.usplit = (i64 *)(b + off[5]);
+    img.uc = (i32 *)(b + off[6]);
+    img.uv = (double *)(b + off[7]);
+    img.ud = (double *)(b + off[8]);
+    img.P = (i32 *)(b + off[9]);
+    img.Q = (i32 *)(b + off[10]);
+    img.scale = (double *)(b + off[11]);
+  }
   phase("csr");
 }
 
@@ -784,10 +809,7 @@ void trsv_free(TrsvImage &img)
     for (void *p : {(void *)img.off1[f], (void *)img.w1[f], (void *)img.v1[f], (void *)img.c1[f], (void *)img.tile[f],
                     (void *)img.tmask[f], (void *)img.dinv[f], (void *)img.g[f]})
       if (p) (void)hipFree(p);
-  for (void *p : {(void *)img.lrp, (void *)img.lsplit, (void *)img.lc, (void *)img.lv, (void *)img.urp,
-                  (void *)img.usplit, (void *)img.uc, (void *)img.uv, (void *)img.ud, (void *)img.P, (void *)img.Q,
-                  (void *)img.scale})
-    if (p) (void)hipFree(p);
+  if (img.arena) (void)hipFree(img.arena);  // (the row-CSR arrays live inside it)
   img = TrsvImage();
 }
 
