@@ -278,7 +278,11 @@ int eig_lu_destroy(eig_lu_t lu);
 /* Qout = A^-1 Qin for m columns (matmul_inverse_tallskinny_blocked, kernels_cpp.hh:660-755;
  * MultiVector<double,8> layout, n rows, single rank).  Qin is used as scratch (its contents afterwards are
  * unspecified), as the reference allows (kernels_cpp.hh:659).
- * Bitwise the reference's arithmetic when the L rows are stored in ascending column order. */
+ * Default: factors whose envelope fits (every coupling within 4 blocks of 64 rows; RCM envelope
+ * factors of bandwidth <= 256) take the block-inverse solve (products with the inverted 64 x 64
+ * diagonal blocks; within 1e-13 of the largest |entry| of the reference's result, not bitwise).
+ * Environment EIGMI_TRSV=staged / csr selects the substitution kernels, bitwise the reference's
+ * arithmetic when the L rows are stored in ascending column order (as are all other factors). */
 int eig_inverse_mv8(eig_lu_t lu, int64_t m, double *Qin, double *Qout);
 
 /* StandardInverse (eigensolver.hh:116-198): inverse subspace iteration for the nev smallest
