@@ -42,7 +42,7 @@ def cpu_baseline(N, rp, c, v, steps, gpu_alpha, fused):
     alpha, beta = np.zeros(steps), np.zeros(steps + 1)
     t0 = time.perf_counter()
     if fused:
-        oracle.lib.orc_lanczos_fused(n, rp, c, v, steps, u0, alpha, beta)
+        oracle.lib.orc_lanczos_fused(n, rp, c, v, steps, u0, alpha, beta, None)
     else:
         oracle.lib.orc_lanczos_rotating(n, rp, c, v, steps, u0, u1, u2, alpha, beta)
     dt = time.perf_counter() - t0
@@ -77,7 +77,7 @@ def cpu_replicas(N, steps, fused, threads):
         bar.wait()  # go
         if not err:
             if fused:
-                oracle.lib.orc_lanczos_fused(n, rp, c, v, steps, u0, alpha, beta)
+                oracle.lib.orc_lanczos_fused(n, rp, c, v, steps, u0, alpha, beta, None)
             else:
                 oracle.lib.orc_lanczos_rotating(n, rp, c, v, steps, u0, u1, u2, alpha, beta)
         bar.wait()  # done
@@ -204,6 +204,7 @@ def main():
     if W:
         ws.step(W)
     graph = False if eager else ws.capture(K, timed=kev and K2 == 0)
+    k0, L0 = ws.info()
     barrier()
     ctx.sync()
     t0 = time.perf_counter()
@@ -216,6 +217,11 @@ def main():
         tt = torch.tensor([dt], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
+    k1, L1 = ws.info()
+    # fused: a launch whose norm prediction is unsound repairs instead of stepping (k_spmv.hip
+    # fused_begin) and the workspace tops the launches up until K steps are done
+    repairs = (L1 - L0) - (k1 - k0)
+    region = region and repairs == 0
     if K2:
         # kernel timing pass (outside the timed region): K2 more steps, per-launch event nodes
         ws.capture(K2, timed=True)
@@ -283,6 +289,7 @@ def main():
                       "spmv": round(tim.total_ms if region else tim.spmv_ms, 3),
                       "rest": round(0.0 if region else tim.total_ms - tim.spmv_ms, 3)},
         "recurrence_finite": ok,
+        "fused_repairs": repairs if fused else None,
         "launch": "hipGraph replay of the K steps" if graph else "eager",
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -853,6 +853,25 @@ void validate_csr(i64 nb, i64 ncols, const int64_t *rowptr, const int32_t *col)
   }
 }
 
+// Diagonal share of the owned rows (global row = row_begin + r): sum of the stored diagonal
+// entries of the diagonal blocks and the number of scalar rows that store one.
+void diag_share(eig_mat_s &A, i64 nb, i64 row_begin, const int64_t *rowptr, const int32_t *col, const double *vals)
+{
+  const int br = A.br, bc = A.bc;
+  double s = 0.0;
+  i64 cnt = 0;
+  for (i64 r = 0; r < nb; ++r)
+    for (i64 p = rowptr[r]; p < rowptr[r + 1]; ++p)
+      if (col[p] == row_begin + r)
+        for (int i = 0; i < std::min(br, bc); ++i)
+        {
+          s += vals[p * br * bc + (i64)i * bc + i];
+          ++cnt;
+        }
+  A.diag_sum = s;
+  A.diag_count = cnt;
+}
+
 void destroy_mat(eig_mat_s *A)
 {
   if (!A) return;
@@ -897,6 +916,7 @@ extern "C" int eig_mat_create_bcsr(eig_ctx_t ctx, int64_t nb_rows, int64_t nb_co
     {
       build_sell(*A, nb_rows, rowptr, col, vals, 0);
       build_sym(*A, nb_rows, rowptr, col, vals);
+      diag_share(*A, nb_rows, 0, rowptr, col, vals);
     }
     catch (...)
     {
@@ -942,6 +962,7 @@ extern "C" int eig_mat_create_bcsr_dist(eig_ctx_t ctx, int64_t nb_rows_global, i
     {
       build_sell(*A, nb_local, rowptr, col, vals, wb_blk);
       build_sym(*A, nb_local, rowptr, col, vals);
+      diag_share(*A, nb_local, row_begin, rowptr, col, vals);
       // --- halo plan: allgather (row_begin, nb_local, cmin, cmax) of every rank ---
       std::vector<i64> mine = {row_begin, nb_local, cmin, cmax};
       std::vector<i64> all(4 * (size_t)P, 0);

@@ -502,9 +502,14 @@ namespace {
 
 struct LanczosBufs {
   DevBuf scal;
+  DevBuf ictl;
   LanczosState st;
   double *carry;
-  explicit LanczosBufs(int steps) : scal((size_t)(7 * (steps + 2) + 8) * sizeof(double))
+  // steps: logical steps; launches: fused launches (a step plus at most one repair each, plus the
+  // forced final repair)
+  explicit LanczosBufs(int steps, int launches = 0)
+      : scal((size_t)(4 * (steps + 2) + 5 * (launches + 2) + 8) * sizeof(double)),
+        ictl((size_t)2 * (launches + 2) * sizeof(int))
   {
     double *b = scal.d();
     st.dsum = b;
@@ -512,7 +517,10 @@ struct LanczosBufs {
     st.alpha = b + 2 * (steps + 2);
     st.beta = b + 3 * (steps + 2);
     st.fred = b + 4 * (steps + 2);
-    carry = b + 7 * (steps + 2);
+    st.aux = st.fred + 3 * (launches + 2);
+    carry = st.aux + 2 * (launches + 2);
+    st.mu2 = carry + 4;
+    st.ctl = static_cast<int *>(ictl.p);
   }
 };
 
@@ -589,12 +597,12 @@ void lanczos_step(eig_mat_s &A, double *u, double *up, double *t, int j, Lanczos
   mark(4);
 }
 
-// One fused step k (DESIGN.md "Fused step"): P = interleaved (t_{k-1}, u_{k-1}) pairs (window
-// layout, ghosts exchanged here), writes the pairs (t_k, u_k) into Pout; one allreduce of
-// (dsum_k, tsq_k, m_k).  Events as lanczos_step: ev[0] before, ev[1] after the kernel, ev[2..4]
-// after the allreduce.
-void lanczos_fused_step(eig_mat_s &A, double *P, double *Pout, int k, LanczosBufs &lb, hipEvent_t *ev, int nev,
-                        hipEvent_t halo_ev0, hipEvent_t halo_ev1, bool ev_external)
+// One fused launch L (k_spmv.hip "Fused one-reduction Lanczos step"; a step or a repair, decided
+// on the device): P = interleaved pairs of the previous launch (window layout, ghosts exchanged
+// here), the output pairs go to Pout; one allreduce of the launch's three sums.  Events as
+// lanczos_step: ev[0] before, ev[1] after the kernel, ev[2..4] after the allreduce.
+void lanczos_fused_step(eig_mat_s &A, double *P, double *Pout, int L, int force, LanczosBufs &lb, hipEvent_t *ev,
+                        int nev, hipEvent_t halo_ev0, hipEvent_t halo_ev1, bool ev_external)
 {
   eig_ctx_t ctx = A.ctx;
   hipStream_t s = ctx->stream;
@@ -602,12 +610,13 @@ void lanczos_fused_step(eig_mat_s &A, double *P, double *Pout, int k, LanczosBuf
     if (ev && i < nev)
       EIG_HIP(hipEventRecordWithFlags(ev[i], s, ev_external ? hipEventRecordExternal : hipEventRecordDefault));
   };
-  double *out = lb.st.fred + 3 * (i64)k;
+  double *out = lb.st.fred + 3 * (i64)L;
+  const FusedLaunch fl{lb.st, L, force};
   mark(0);
   halo_split(
       A, halo_ev0, halo_ev1, [&](hipStream_t hs) { halo_exchange(A, P, hs, nullptr, 2); },
       [&](const i32 *sl, i64 first, i64 count, int part) {
-        launch_lanczos_fused(A, P, Pout, k, lb.st, sl, first, count, part == kPartSecond ? lb.carry : nullptr,
+        launch_lanczos_fused(A, P, Pout, fl, sl, first, count, part == kPartSecond ? lb.carry : nullptr,
                              part == kPartFirst ? lb.carry : out, 0, s, ctx->red);
       });
   mark(1);
@@ -645,6 +654,8 @@ struct eig_lanczos_s {
   eig_mat_s *A = nullptr;
   int max_steps = 0, k = 0;
   bool fused = false;  // EIG_LANCZOS_FUSED: B = {P0, P1} (2-wide pair vectors); else B = {u_j rotation of 3}
+  // fused: launches issued (a repair is a launch, not a step) and the launch capacity
+  int L = 0, max_launches = 0;
   DevBuf *B[4] = {nullptr, nullptr, nullptr, nullptr};
   LanczosBufs *lb = nullptr;
   hipEvent_t h0 = nullptr, h1 = nullptr;
@@ -689,7 +700,8 @@ int events_per_step(int flags)
   return (flags & EIG_LANCZOS_TIME_DETAIL) ? 5 : (flags & EIG_LANCZOS_TIME_KERNELS) ? 2 : 0;
 }
 
-// ev = [beg, end, nps per step]; enqueues steps k .. k+steps-1 on the library stream.
+// ev = [beg, end, nps per step]; enqueues steps k .. k+steps-1 (fused: launches L .. L+steps-1) on
+// the library stream.
 void enqueue_steps(eig_lanczos_s &ws, int steps, int nps, hipEvent_t *ev, bool external)
 {
   eig_mat_s &A = *ws.A;
@@ -698,19 +710,65 @@ void enqueue_steps(eig_lanczos_s &ws, int steps, int nps, hipEvent_t *ev, bool e
   EIG_HIP(hipEventRecordWithFlags(ev[0], s, fl));
   for (int i = 0; i < steps; ++i)
   {
-    const int j = ws.k + i;
     hipEvent_t *e = nps ? ev + 2 + (size_t)nps * i : nullptr;
     if (ws.fused)
     {
-      lanczos_fused_step(A, ws.B[j & 1]->d(), ws.B[(j + 1) & 1]->d(), j, *ws.lb, e, nps, ws.h0, ws.h1, external);
+      const int L = ws.L + i;
+      lanczos_fused_step(A, ws.B[L & 1]->d(), ws.B[(L + 1) & 1]->d(), L, 0, *ws.lb, e, nps, ws.h0, ws.h1, external);
     }
     else
     {
+      const int j = ws.k + i;
       double *U[3] = {ws.B[0]->d(), ws.B[1]->d(), ws.B[2]->d()};
       lanczos_step(A, U[j % 3], U[(j + 2) % 3], U[(j + 1) % 3], j, *ws.lb, e, nps, ws.h0, ws.h1, external);
     }
   }
   EIG_HIP(hipEventRecordWithFlags(ev[1], s, fl));
+}
+
+// Fused workspace: control word of launch L (logical step, mode), read after a synchronisation.
+void fused_state(eig_lanczos_s &ws, int &j, int &mode)
+{
+  int c[2];
+  EIG_HIP(hipMemcpy(c, ws.lb->st.ctl + 2 * (i64)ws.L, sizeof(c), hipMemcpyDeviceToHost));
+  j = c[0];
+  mode = c[1];
+}
+
+void read_timing(const std::vector<hipEvent_t> &ev, int steps, int nps, eig_timing *timing, bool accumulate = false);
+std::vector<hipEvent_t> make_events(int steps, int nps);
+
+// After `launched` fused launches were enqueued for logical steps up to `target`: synchronise, then
+// top up with eager launches until the target step is reached (launches that repaired took no
+// step).  Extra batches add to `timing`.  Breakdown (u_j = 0) ends the recurrence at step j.
+void fused_settle(eig_lanczos_s &ws, int target, int nps, eig_timing *timing)
+{
+  eig_ctx_t ctx = ws.A->ctx;
+  for (;;)
+  {
+    int j, mode;
+    fused_state(ws, j, mode);
+    ws.k = j;
+    if (mode == kFusedModeHalt)
+      throw Error(EIG_ERR_BREAKDOWN, "Lanczos breakdown: invariant subspace after " + std::to_string(j) + " steps");
+    if (j >= target) return;
+    const int more = target - j;
+    EIG_CHECK(ws.L + more <= ws.max_launches, EIG_ERR_ARG, "fused Lanczos: launch capacity exhausted");
+    std::vector<hipEvent_t> ev = make_events(more, nps);
+    try
+    {
+      enqueue_steps(ws, more, nps, ev.data(), false);
+      EIG_HIP(hipStreamSynchronize(ctx->stream));
+      ws.L += more;
+      read_timing(ev, more, nps, timing, true);
+    }
+    catch (...)
+    {
+      for (auto &e : ev) (void)hipEventDestroy(e);
+      throw;
+    }
+    for (auto &e : ev) (void)hipEventDestroy(e);
+  }
 }
 
 std::vector<hipEvent_t> make_events(int steps, int nps)
@@ -720,13 +778,14 @@ std::vector<hipEvent_t> make_events(int steps, int nps)
   return ev;
 }
 
-void read_timing(const std::vector<hipEvent_t> &ev, int steps, int nps, eig_timing *timing)
+void read_timing(const std::vector<hipEvent_t> &ev, int steps, int nps, eig_timing *timing, bool accumulate)
 {
   if (!timing) return;
-  std::memset(timing, 0, sizeof(*timing));
+  if (!accumulate) std::memset(timing, 0, sizeof(*timing));
   float ms = 0.f;
   EIG_HIP(hipEventElapsedTime(&ms, ev[0], ev[1]));
-  timing->total_ms = ms;
+  timing->total_ms += ms;
+  timing->spmv_launches += steps;
   if (!nps) return;
   for (int i = 0; i < steps; ++i)
   {
@@ -741,7 +800,6 @@ void read_timing(const std::vector<hipEvent_t> &ev, int steps, int nps, eig_timi
     timing->comm_ms += b + d;
     timing->update_ms += c;
   }
-  timing->spmv_launches = steps;
 }
 
 }  // namespace
@@ -767,6 +825,8 @@ extern "C" int eig_lanczos_create_ex(eig_mat_t A, int max_steps, const double *u
       ws->A = A;
       ws->max_steps = max_steps;
       ws->fused = (flags & EIG_LANCZOS_FUSED) != 0;
+      // worst case: every step repaired, plus one forced repair per eig_lanczos_tridiag call
+      ws->max_launches = ws->fused ? 3 * max_steps + 8 : 0;
       const size_t wb = (size_t)A->window * sizeof(double);
       for (int i = 0; i < 3; ++i)
       {
@@ -776,13 +836,18 @@ extern "C" int eig_lanczos_create_ex(eig_mat_t A, int max_steps, const double *u
       }
       double *U0 = ws->fused ? ws->B[2]->d() : ws->B[0]->d();
       init_start(*A, U0, u0, seed);
-      ws->lb = new LanczosBufs(max_steps);
+      ws->lb = new LanczosBufs(max_steps, ws->max_launches);
       launch_nrm2sq(A->nb_rows, U0 + A->own_offset, ws->lb->st.nsum, 0, s, ctx->red);
       if (ws->fused)  // P0 = (u_0, 0) interleaved; the whole window (ghosts are refilled per step)
       {
         EIG_HIP(hipMemsetAsync(ws->B[0]->d(), 0, 2 * wb, s));
         EIG_HIP(hipMemcpy2DAsync(ws->B[0]->d(), 2 * sizeof(double), U0, sizeof(double), sizeof(double), A->window,
                                  hipMemcpyDeviceToDevice, s));
+        // launch 0 takes step 0; the shift mu = trace / n from every rank's diagonal share
+        EIG_HIP(hipMemsetAsync(ws->lb->st.ctl, 0, ws->lb->ictl.bytes(), s));
+        const double mu2[2] = {A->diag_sum, (double)A->nb_rows};
+        EIG_HIP(hipMemcpyAsync(ws->lb->st.mu2, mu2, sizeof(mu2), hipMemcpyHostToDevice, s));
+        allreduce_sum(ctx, ws->lb->st.mu2, 2, s);
       }
       allreduce_sum(ctx, ws->lb->st.nsum, 1, s);
       EIG_HIP(hipEventCreateWithFlags(&ws->h0, hipEventDisableTiming));
@@ -804,16 +869,19 @@ extern "C" int eig_lanczos_step(eig_lanczos_t ws, int steps, int flags, eig_timi
     EIG_CHECK(ws && steps >= 0, EIG_ERR_ARG, "eig_lanczos_step: bad argument");
     EIG_CHECK(ws->k + steps <= ws->max_steps, EIG_ERR_ARG, "eig_lanczos_step: more steps than max_steps");
     EIG_CHECK((flags & ~(EIG_LANCZOS_TIME_KERNELS | EIG_LANCZOS_TIME_DETAIL)) == 0, EIG_ERR_ARG, "eig_lanczos_step: unknown flag");
+    EIG_CHECK(!ws->fused || ws->L + steps <= ws->max_launches, EIG_ERR_ARG, "fused Lanczos: launch capacity exhausted");
     ws->drop_graph();  // a pending capture is for steps that are about to be taken eagerly
     eig_ctx_t ctx = ws->A->ctx;
     EIG_HIP(hipSetDevice(ctx->device));
     const int nps = events_per_step(flags);
+    const int target = ws->k + steps;
     std::vector<hipEvent_t> ev = make_events(steps, nps);
     try
     {
       enqueue_steps(*ws, steps, nps, ev.data(), false);
       EIG_HIP(hipStreamSynchronize(ctx->stream));
-      ws->k += steps;
+      if (ws->fused) ws->L += steps;
+      else ws->k += steps;
       read_timing(ev, steps, nps, timing);
     }
     catch (...)
@@ -822,6 +890,7 @@ extern "C" int eig_lanczos_step(eig_lanczos_t ws, int steps, int flags, eig_timi
       throw;
     }
     for (auto &e : ev) (void)hipEventDestroy(e);
+    if (ws->fused) fused_settle(*ws, target, nps, timing);
   });
 }
 
@@ -831,6 +900,7 @@ extern "C" int eig_lanczos_capture(eig_lanczos_t ws, int steps, int flags, int *
     EIG_CHECK(ws && steps > 0, EIG_ERR_ARG, "eig_lanczos_capture: bad argument");
     EIG_CHECK(ws->k + steps <= ws->max_steps, EIG_ERR_ARG, "eig_lanczos_capture: more steps than max_steps");
     EIG_CHECK((flags & ~(EIG_LANCZOS_TIME_KERNELS | EIG_LANCZOS_TIME_DETAIL)) == 0, EIG_ERR_ARG, "eig_lanczos_capture: unknown flag");
+    EIG_CHECK(!ws->fused || ws->L + steps <= ws->max_launches, EIG_ERR_ARG, "fused Lanczos: launch capacity exhausted");
     ws->drop_graph();
     eig_ctx_t ctx = ws->A->ctx;
     EIG_HIP(hipSetDevice(ctx->device));
@@ -882,14 +952,17 @@ extern "C" int eig_lanczos_replay(eig_lanczos_t ws, eig_timing *timing)
     hipStream_t s = ctx->stream;
     const int steps = ws->g_steps;
     const int nps = events_per_step(ws->g_flags);
+    const int target = ws->k + steps;
     if (ws->gexec)
       EIG_HIP(hipGraphLaunch(ws->gexec, s));
     else
       enqueue_steps(*ws, steps, nps, ws->g_ev.data(), false);
     EIG_HIP(hipStreamSynchronize(s));
-    ws->k += steps;
+    if (ws->fused) ws->L += steps;
+    else ws->k += steps;
     read_timing(ws->g_ev, steps, nps, timing);
     ws->drop_graph();
+    if (ws->fused) fused_settle(*ws, target, nps, timing);
   });
 }
 
@@ -899,8 +972,22 @@ extern "C" int eig_lanczos_tridiag(eig_lanczos_t ws, int *k, double *alpha_host,
     EIG_CHECK(ws, EIG_ERR_ARG, "eig_lanczos_tridiag: null workspace");
     eig_ctx_t ctx = ws->A->ctx;
     EIG_HIP(hipSetDevice(ctx->device));
+    EIG_HIP(hipStreamSynchronize(ctx->stream));
     if (ws->fused)
-      launch_fused_tail(ws->lb->st, ws->k, ctx->stream);
+    {
+      // alpha[k-1] and an EXACT beta[k]: a forced repair forms u_k and reduces its norm (the
+      // prediction is only used to scale a step, never reported), then the tail stores beta[k]
+      int j, mode;
+      fused_state(*ws, j, mode);
+      if (mode == kFusedModeStep && j > 0)
+      {
+        EIG_CHECK(ws->L + 1 <= ws->max_launches, EIG_ERR_ARG, "fused Lanczos: launch capacity exhausted");
+        lanczos_fused_step(*ws->A, ws->B[ws->L & 1]->d(), ws->B[(ws->L + 1) & 1]->d(), ws->L, 1, *ws->lb, nullptr, 0,
+                           ws->h0, ws->h1, false);
+        ++ws->L;
+      }
+      launch_fused_tail(ws->lb->st, ws->L, ctx->stream);
+    }
     else
       launch_beta_tail(ws->lb->st, ws->k, ctx->stream);
     EIG_HIP(hipStreamSynchronize(ctx->stream));
@@ -908,6 +995,15 @@ extern "C" int eig_lanczos_tridiag(eig_lanczos_t ws, int *k, double *alpha_host,
     if (alpha_host && ws->k > 0)
       EIG_HIP(hipMemcpy(alpha_host, ws->lb->st.alpha, ws->k * sizeof(double), hipMemcpyDeviceToHost));
     if (beta_host) EIG_HIP(hipMemcpy(beta_host, ws->lb->st.beta, (ws->k + 1) * sizeof(double), hipMemcpyDeviceToHost));
+  });
+}
+
+extern "C" int eig_lanczos_info(eig_lanczos_t ws, int *steps, int *launches)
+{
+  return guard(ws ? ws->A->ctx : nullptr, [&] {
+    EIG_CHECK(ws, EIG_ERR_ARG, "eig_lanczos_info: null workspace");
+    if (steps) *steps = ws->k;
+    if (launches) *launches = ws->fused ? ws->L : ws->k;
   });
 }
 

@@ -207,6 +207,10 @@ struct eig_mat_s {
   // max |global col - global row| over the stored blocks (block units): the far-neighbour distance
   // the XCD-aware gather kernels size their grid by (k_block.hip)
   eigmi::i64 bandwidth = 0;
+  // sum of the stored diagonal entries of the owned rows (trace share; shift_diag keeps it current)
+  // and how many rows store one: the fused Lanczos step's shift mu = trace / n
+  double diag_sum = 0.0;
+  eigmi::i64 diag_count = 0;
 };
 
 namespace eigmi {
@@ -225,13 +229,25 @@ struct LanczosState {
   double *nsum;   // nsum[j]  = ||u_j||^2 (local, then allreduced); nsum[0] from the start vector
   double *alpha;  // alpha[j]
   double *beta;   // beta[j]  = sqrt(nsum[j])
-  double *fred;   // fused step: fred[3k..3k+2] = (t_k . u_k, t_k . t_k, u_k . u_k) (local, then allreduced)
+  // fused step (k_spmv.hip "Fused one-reduction Lanczos step"), indexed by LAUNCH L (a repair is a
+  // launch that is not a step):
+  double *fred;   // fred[3L..3L+2] = (t . u, t . t, u . u) of launch L (local, then allreduced)
+  int *ctl;       // ctl[2L], ctl[2L+1] = logical step and mode at the start of launch L
+  double *aux;    // aux[2L], aux[2L+1] = (rn, rm) a repair hands to launch L
+  double *mu2;    // (sum of the diagonal, rows), allreduced: the step's shift mu = mu2[0] / mu2[1]
+};
+enum { kFusedModeStep = 0, kFusedModePost = 1, kFusedModeHalt = 2 };  // ctl[2L + 1]
+struct FusedLaunch {
+  LanczosState st;
+  int L;      // launch index
+  int force;  // repair regardless of the prediction (exact final beta, eig_lanczos_tridiag)
 };
 // P, Pout: interleaved (t, u) pair vectors in window layout (2 doubles per row).
-void launch_lanczos_fused(const eig_mat_s &A, const double *P, double *Pout, int k,
-                          const LanczosState &st, const i32 *slices, i64 first, i64 count, const double *carry,
-                          double *out, int ticket, hipStream_t s, ReduceWS red);
-void launch_fused_tail(const LanczosState &st, int K, hipStream_t s);
+void launch_lanczos_fused(const eig_mat_s &A, const double *P, double *Pout, const FusedLaunch &fl,
+                          const i32 *slices, i64 first, i64 count, const double *carry, double *out, int ticket,
+                          hipStream_t s, ReduceWS red);
+// beta / nsum of the current logical step after a repair launch (L = the next launch index)
+void launch_fused_tail(const LanczosState &st, int L, hipStream_t s);
 // Plane march (k_spmv.hip): band geometry (widest offset D) and whether the interior-plane split
 // launch applies now (split built at upload, image and EIGMI_* switches allow it).  Passing
 // slices == &kMarchInteriorTag to launch_spmv / launch_lanczos_spmv / launch_lanczos_fused marches

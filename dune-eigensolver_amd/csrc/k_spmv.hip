@@ -586,30 +586,168 @@ __global__ __launch_bounds__(kStreamThreads, min_waves<MODE>()) void k_lanczos_s
 }
 
 // ---------------------------------------------------------------------------------------------
-// Fused one-reduction Lanczos step (DESIGN.md "Fused step").  u_k = t_{k-1} - c u_{k-1} is formed
-// inside the gathers of the SpMV that needs it (XComb), and its squared norm is PREDICTED from the
-// previous step's reductions instead of being reduced before the SpMV:
+// Fused one-reduction Lanczos step.  u_k = t_{k-1} - c u_{k-1} is formed inside the
+// gathers of the SpMV that needs it (XPair), and its squared norm is PREDICTED from the previous
+// step's reductions instead of being reduced before the SpMV:
 //   c = dsum/m,  nt_k = tsq - c dsum       (m = measured ||u_{k-1}||^2, reduced when u_{k-1} was
 //                                             formed; using it keeps the prediction error at
 //                                             rounding level -- tsq - alpha^2 alone diverges)
-//   t_k = (A u_k) sig_k - gam_k u_{k-1},  sig_k = 1/sqrt(nt_k)
+//   t_k = ((A u_k) - mu u_k) sig_k - gam_k u_{k-1},  sig_k = 1/sqrt(nt_k)
 //   (dsum_k, tsq_k, m_k) = (t_k . u_k, t_k . t_k, u_k . u_k)   -> ONE allreduce of 3 doubles
-// P is the WINDOW buffer of the interleaved pairs (t_{k-1}, u_{k-1}) (ghosts exchanged); the pairs
-// (t_k, u_k) go to the owned rows of Pout.  Step 0: P = (u_0, 0), c = gam = 0.  out[0..2] receive the three sums (red + 3k,
-// or a carry slot for the interior half of a split step); red[3(k-1)..] are the previous step's
-// allreduced sums; block 0 stores nsum[k] = nt_k, alpha[k-1], beta[k].  Same formulas as
-// orc_lanczos_fused (oracle.cc).
+// Guard against cancellation (nt_k = ||t||^2 - (t.u)^2/||u||^2 loses digits when |alpha| >> beta):
+//  * the step runs on A - mu I, mu = trace(A)/n (a constant inside the spectrum): the Krylov space,
+//    beta and alpha - mu are unchanged, but |alpha - mu| stays of the order of the spectral width
+//    however far the operator is shifted (A + 1e6 I costs nothing extra);
+//  * when the prediction still keeps less than kFusedTau of tsq (nt <= tau tsq, incl. nt <= 0 and
+//    NaN), the launch REPAIRS instead of stepping: it forms u_k explicitly into the output pairs
+//    (u_k, u_{k-1}) and reduces its exact norm; the next launch then takes step k with c = 0 and
+//    the exact nt_k (the same per-row code: x - 0 y = x).  The decision is made on the device from
+//    the allreduced sums (identical on every rank), so no step synchronises with the host; the
+//    host tops the launch count up afterwards (drivers.cpp).  Launch L reads its logical step j
+//    and mode from ctl[2L], ctl[2L+1] and block 0 writes those of launch L+1.
+// Same formulas as orc_lanczos_fused (oracle.cc).
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ void fused_scalars(double nt_prev, double d, double q, double m, double &c,
-                                              double &alpha_prev, double &nt, double &beta, double &gam)
+constexpr double kFusedTau = 1e-2;
+enum { kFusedStep = 0, kFusedPost = 1, kFusedHalt = 2, kFusedRepair = 3, kFusedNoop = 4 };
+
+struct FusedArgs {
+  double *nsum, *alpha, *beta;  // per logical step
+  const double *fred;           // per launch: 3 allreduced sums
+  int *ctl;                     // per launch: (logical step j, mode) at its start
+  double *aux;                  // per launch: (rn, rm) handed from a repair to the next launch
+  const double *mu2;            // (sum of the diagonal, rows), allreduced: mu = mu2[0] / mu2[1]
+  int L;                        // launch index
+  int force;                    // 1: repair even if the prediction is sound (exact final beta)
+};
+
+struct FusedStep {
+  int j, act;
+  double c, nt, ap, bk, gam, sig, mu, rn, rm;
+};
+
+// Prologue of a fused launch (every thread; wave- and grid-uniform); block 0 / thread 0 stores the
+// step's scalars and the next launch's control word.  Returns the action.
+__device__ __forceinline__ FusedStep fused_begin(const FusedArgs &f)
 {
-  const double rn = sqrt(nt_prev);
-  const double rm = sqrt(m);
-  c = d / m;
-  alpha_prev = c * rn;
-  nt = q - c * d;
-  beta = sqrt(nt) * rn / rm;
-  gam = beta / rm;
+  FusedStep s;
+  s.j = f.ctl[2 * f.L];
+  const int mode = f.ctl[2 * f.L + 1];
+  s.mu = f.mu2[0] / f.mu2[1];
+  s.c = s.ap = s.bk = s.gam = s.rn = s.rm = 0.0;
+  s.nt = 1.0;
+  const int j = s.j;
+  if (mode == kFusedHalt) s.act = kFusedHalt;
+  else if (f.force && (j == 0 || mode != kFusedStep)) s.act = kFusedNoop;
+  else if (mode == kFusedPost)
+  {
+    const double mex = f.fred[3 * (f.L - 1) + 2];
+    s.rn = f.aux[2 * f.L];
+    s.rm = f.aux[2 * f.L + 1];
+    s.nt = mex;
+    if (!(mex > 0.0)) s.act = kFusedHalt;  // u_j = 0: invariant subspace
+    else
+    {
+      s.bk = sqrt(mex) * s.rn / s.rm;
+      s.gam = s.bk / s.rm;
+      s.act = kFusedPost;
+    }
+  }
+  else if (j == 0)
+  {
+    s.nt = f.nsum[0];
+    s.act = kFusedStep;
+  }
+  else
+  {
+    const double d = f.fred[3 * (f.L - 1)], q = f.fred[3 * (f.L - 1) + 1], m = f.fred[3 * (f.L - 1) + 2];
+    s.rn = sqrt(f.nsum[j - 1]);
+    s.rm = sqrt(m);
+    s.c = d / m;
+    s.ap = s.c * s.rn + s.mu;
+    s.nt = q - s.c * d;
+    if (f.force || !(s.nt > kFusedTau * q)) s.act = kFusedRepair;
+    else
+    {
+      s.bk = sqrt(s.nt) * s.rn / s.rm;
+      s.gam = s.bk / s.rm;
+      s.act = kFusedStep;
+    }
+  }
+  s.sig = 1.0 / sqrt(s.nt);
+  if (blockIdx.x == 0 && threadIdx.x == 0)  // (both launches of a split step store the same values)
+  {
+    int nj = j, nm = kFusedStep;
+    switch (s.act)
+    {
+      case kFusedStep:
+        if (j > 0)
+        {
+          f.nsum[j] = s.nt;
+          f.alpha[j - 1] = s.ap;
+          f.beta[j] = s.bk;
+        }
+        else
+          f.beta[0] = sqrt(s.nt);
+        nj = j + 1;
+        break;
+      case kFusedPost:
+        f.nsum[j] = s.nt;
+        f.beta[j] = s.bk;
+        nj = j + 1;
+        break;
+      case kFusedRepair:
+        f.alpha[j - 1] = s.ap;
+        f.aux[2 * f.L + 2] = s.rn;
+        f.aux[2 * f.L + 3] = s.rm;
+        nm = kFusedPost;
+        break;
+      case kFusedHalt:
+        if (mode == kFusedPost)
+        {
+          f.nsum[j] = 0.0;
+          f.beta[j] = 0.0;
+        }
+        nm = kFusedHalt;
+        break;
+      default:  // kFusedNoop
+        nm = mode;
+        if (mode == kFusedPost)
+        {
+          f.aux[2 * f.L + 2] = f.aux[2 * f.L];
+          f.aux[2 * f.L + 3] = f.aux[2 * f.L + 1];
+        }
+        break;
+    }
+    f.ctl[2 * f.L + 2] = nj;
+    f.ctl[2 * f.L + 3] = nm;
+  }
+  return s;
+}
+
+// Launch with nothing to compute (halted recurrence, or a forced repair with nothing to repair):
+// the reduction slot reads zero.
+// (The host forces a repair only after reading a stepping state, so kFusedNoop is defensive.)
+__device__ __forceinline__ void fused_idle(double *out)
+{
+  if (blockIdx.x == 0 && threadIdx.x < 3) out[threadIdx.x] = 0.0;
+}
+
+// Repair launch body for rows [r0, r1) (owned-row indices, grid-stride): u = t - c u_prev into the
+// output pair (u, u_prev), and ||u||^2.  The same mul-then-sub as the gathers (XPair), so the step
+// that follows multiplies exactly the u_k the unrepaired step would have formed.
+__device__ __forceinline__ double fused_repair_rows(i64 r0, i64 r1, i64 own, double c, const dpair *__restrict__ P,
+                                                    dpair *__restrict__ Pout)
+{
+  double m2 = 0.0;
+  const i64 stride = (i64)gridDim.x * blockDim.x;
+  for (i64 r = r0 + (i64)blockIdx.x * blockDim.x + threadIdx.x; r < r1; r += stride)
+  {
+    const dpair p = P[own + r];
+    const double u = p.x - c * p.y;
+    Pout[own + r] = dpair{u, p.y};
+    m2 += u * u;
+  }
+  return m2;
 }
 
 // Fused step, one stencil slice, one row per lane: gathers the (t, u) pairs at the slice's offsets
@@ -669,38 +807,56 @@ __device__ __forceinline__ void fused_row_stencil(const SellB1 &A, i64 s, const 
   }
 }
 
-// W = waves per SIMD the register budget is sized for (W >= 8: stencil rows take 4 entries per
-// round to fit 64 VGPRs; EIGMI_FUSED_WAVES picks 4/5/6/8, see launch_lanczos_fused).
-template <int R, int MODE, int W>
-__global__ __launch_bounds__(kStreamThreads, W) void k_lanczos_fused_b1(
+// Register budget for 8 waves / SIMD (W): stencil rows take 4 entries per round to fit 64 VGPRs
+// (measured: 5 waves with 8 entries per round and 6 waves were no faster).
+template <int R, int MODE>
+__global__ __launch_bounds__(kStreamThreads, 8) void k_lanczos_fused_b1(
     i64 nrows, i64 own, SellB1 A, const i32 *__restrict__ slices, i64 first, i64 count,
-    const dpair *__restrict__ P, dpair *__restrict__ Pout, int k, double *__restrict__ nsum, double *__restrict__ alpha,
-    double *__restrict__ beta, const double *__restrict__ red, double *__restrict__ out,
+    const dpair *__restrict__ P, dpair *__restrict__ Pout, FusedArgs fa, double *__restrict__ out,
     const double *__restrict__ carry, double *partials, unsigned *ticket)
 {
   constexpr int C = 64 * R;
+  constexpr int W = 8;
   __shared__ double tot[3];
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  double nt, c = 0.0, gam = 0.0, ap = 0.0, bk = 0.0;
-  if (k > 0)
-    fused_scalars(nsum[k - 1], red[3 * (k - 1)], red[3 * (k - 1) + 1], red[3 * (k - 1) + 2], c, ap, nt, bk, gam);
-  else
-    nt = nsum[0];
-  const double sig = 1.0 / sqrt(nt);
-  if (blockIdx.x == 0 && threadIdx.x == 0)  // (both launches of a split step store the same values)
+  const FusedStep fs = fused_begin(fa);
+  if (fs.act == kFusedHalt || fs.act == kFusedNoop)
   {
-    if (k > 0)
-    {
-      nsum[k] = nt;
-      alpha[k - 1] = ap;
-      beta[k] = bk;
-    }
-    else
-      beta[0] = sqrt(nt);
+    fused_idle(out);
+    return;
   }
-  const XPair xc{P, c};
+  const double c = fs.c, gam = fs.gam, sig = fs.sig, mu = fs.mu;
+  const int k = fs.j;
   i64 b, e;
   chunk_of(count, b, e, A.swz);
+  if (fs.act == kFusedRepair)
+  {
+    // this launch's rows: its slices (wave w of the chunk takes slice b + w, ...)
+    double m2 = 0.0;
+    for (i64 it = b + wave; it < e; it += kWaves)
+    {
+      const i64 s = slices ? (i64)slices[first + it] : first + it;
+#pragma unroll
+      for (int q = 0; q < R; ++q)
+      {
+        const i64 r = s * C + (i64)lane * R + q;
+        if (r < nrows)
+        {
+          const dpair p = P[own + r];
+          const double u = p.x - c * p.y;
+          Pout[own + r] = dpair{u, p.y};
+          m2 += u * u;
+        }
+      }
+    }
+    double v[3] = {0.0, 0.0, m2};
+    if (grid_sum<3, kStreamThreads>(v, partials, ticket, tot))
+    {
+      if (threadIdx.x < 3) out[threadIdx.x] = carry ? (carry[threadIdx.x] + tot[threadIdx.x]) : tot[threadIdx.x];
+    }
+    return;
+  }
+  const XPair xc{P, c};
   double d = 0.0, q2 = 0.0, m2 = 0.0;
   for (i64 it = b + wave; it < e; it += kWaves)
   {
@@ -743,7 +899,7 @@ __global__ __launch_bounds__(kStreamThreads, W) void k_lanczos_fused_b1(
       if (r < nrows)
       {
         const double uk = tv[q] - c * uv[q];
-        double ti = acc[q] * sig;
+        double ti = (acc[q] - mu * uk) * sig;
         if (k > 0) ti = ti - gam * uv[q];
         Pout[own + r] = dpair{ti, uk};
         d += ti * uk;
@@ -982,47 +1138,46 @@ __global__ __launch_bounds__(kStreamThreads, 8) void k_lanczos_spmv_march(
   }
 }
 
-// Fused one-reduction step on the plane march (per-row arithmetic of k_lanczos_fused_b1).
+// Fused one-reduction step on the plane march (per-row arithmetic of k_lanczos_fused_b1).  A repair
+// launch (fused_begin) takes the rows of the planes this launch marches.
 template <class MT, int VAR>
 __global__ __launch_bounds__(kStreamThreads, ((VAR & 32) ? 7 : 8)) void k_lanczos_fused_march(
-    i64 nrows, i64 own, SellB1 A, MarchPlan mp, const dpair *__restrict__ P, dpair *__restrict__ Pout, int k,
-    double *__restrict__ nsum, double *__restrict__ alpha, double *__restrict__ beta, const double *__restrict__ red,
+    i64 nrows, i64 own, SellB1 A, MarchPlan mp, const dpair *__restrict__ P, dpair *__restrict__ Pout, FusedArgs fa,
     double *__restrict__ out, double *partials, unsigned *ticket)
 {
   __shared__ double tot[3];
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  double nt, c = 0.0, gam = 0.0, ap_ = 0.0, bk = 0.0;
-  if (k > 0)
-    fused_scalars(nsum[k - 1], red[3 * (k - 1)], red[3 * (k - 1) + 1], red[3 * (k - 1) + 2], c, ap_, nt, bk, gam);
-  else
-    nt = nsum[0];
-  const double sig = 1.0 / sqrt(nt);
-  if (blockIdx.x == 0 && threadIdx.x == 0)
+  const FusedStep fs = fused_begin(fa);
+  if (fs.act == kFusedHalt || fs.act == kFusedNoop)
   {
-    if (k > 0)
-    {
-      nsum[k] = nt;
-      alpha[k - 1] = ap_;
-      beta[k] = bk;
-    }
-    else
-      beta[0] = sqrt(nt);
+    fused_idle(out);
+    return;
   }
+  const double c = fs.c, gam = fs.gam, sig = fs.sig, mu = fs.mu;
+  const int k = fs.j;
   double d = 0.0, q2 = 0.0, m2 = 0.0;
-  auto epi = [&](int r, int w, double acc, dpair pc) {
-    if (r < nrows)
-    {
-      const double uk = pc.x - c * pc.y;
-      double ti = acc * sig;
-      if (k > 0) ti = ti - gam * pc.y;
-      if ((VAR & 8) != 0) __builtin_nontemporal_store(dpair{ti, uk}, Pout + (unsigned)w);
-      else Pout[(unsigned)w] = dpair{ti, uk};
-      d += ti * uk;
-      q2 += ti * ti;
-      m2 += uk * uk;
-    }
-  };
-  march_rows<MT, 2, (VAR & 3), ((VAR & 4) != 0), ((VAR & 8) != 0)>(A, mp, own, lane, wave, XPair{P, c}, epi);
+  if (fs.act == kFusedRepair)
+  {
+    const i64 r0 = mp.zb * mp.D, r1 = std::min<i64>(nrows, (mp.zb + mp.nplanes) * mp.D);
+    m2 = fused_repair_rows(r0, r1, own, c, P, Pout);
+  }
+  else
+  {
+    auto epi = [&](int r, int w, double acc, dpair pc) {
+      if (r < nrows)
+      {
+        const double uk = pc.x - c * pc.y;
+        double ti = (acc - mu * uk) * sig;
+        if (k > 0) ti = ti - gam * pc.y;
+        if ((VAR & 8) != 0) __builtin_nontemporal_store(dpair{ti, uk}, Pout + (unsigned)w);
+        else Pout[(unsigned)w] = dpair{ti, uk};
+        d += ti * uk;
+        q2 += ti * ti;
+        m2 += uk * uk;
+      }
+    };
+    march_rows<MT, 2, (VAR & 3), ((VAR & 4) != 0), ((VAR & 8) != 0)>(A, mp, own, lane, wave, XPair{P, c}, epi);
+  }
   double v[3] = {d, q2, m2};
   if (grid_sum<3, kStreamThreads>(v, partials, ticket, tot))
   {
@@ -1284,19 +1439,20 @@ __global__ __launch_bounds__(kStreamThreads, 6) void k_spmm8_marchg(
   }
 }
 
-// After the last fused step K-1: alpha[K-1], nsum[K], beta[K] (same formulas as the prologue).
-__global__ void k_fused_tail(double *nsum, double *alpha, double *beta, const double *red, int K)
+// Final beta of a fused run (eig_lanczos_tridiag): after the forced repair launch L-1 (or a repair
+// the recurrence took itself), the exact ||u_j||^2 is in fred[3(L-1)+2] and (rn, rm) in aux[2L..]:
+// beta[j] = sqrt(mex) rn / rm, nsum[j] = mex -- the values the post-repair step would store.
+__global__ void k_fused_tail(double *nsum, double *beta, const double *fred, const int *ctl, const double *aux, int L)
 {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  if (K > 0)
+  const int j = ctl[2 * L], mode = ctl[2 * L + 1];
+  if (mode == kFusedPost)
   {
-    double c, ap, nt, bk, gam;
-    fused_scalars(nsum[K - 1], red[3 * (K - 1)], red[3 * (K - 1) + 1], red[3 * (K - 1) + 2], c, ap, nt, bk, gam);
-    alpha[K - 1] = ap;
-    nsum[K] = nt;
-    beta[K] = bk;
+    const double mex = fred[3 * (L - 1) + 2];
+    nsum[j] = mex;
+    beta[j] = mex > 0.0 ? sqrt(mex) * aux[2 * L] / aux[2 * L + 1] : 0.0;
   }
-  else
+  else if (j == 0)
     beta[0] = sqrt(nsum[0]);
 }
 
@@ -1703,21 +1859,13 @@ void launch_lanczos_spmv(const eig_mat_s &A, const double *u, const double *up, 
 #undef EIG_PIPE
 }
 
-static int fused_waves()
-{
-  const char *e = std::getenv("EIGMI_FUSED_WAVES");
-  // 8 (default): 4 entries per round, 59 VGPRs, 340 us at 256^3; 5: 8 entries per round, 83 VGPRs,
-  // 341-343 us; 6 spills (350 us)
-  const int w = e ? std::atoi(e) : 8;
-  return (w == 4 || w == 5 || w == 6) ? w : 8;
-}
-
-void launch_lanczos_fused(const eig_mat_s &A, const double *P, double *Pout, int k,
-                          const LanczosState &st, const i32 *slices, i64 first, i64 count, const double *carry,
-                          double *out, int ticket, hipStream_t s, ReduceWS red)
+void launch_lanczos_fused(const eig_mat_s &A, const double *P, double *Pout, const FusedLaunch &fl,
+                          const i32 *slices, i64 first, i64 count, const double *carry, double *out, int ticket,
+                          hipStream_t s, ReduceWS red)
 {
   EIG_CHECK(A.br == 1 && A.bc == 1, EIG_ERR_BLOCKSIZE, "Lanczos driver: 1x1 blocks only");
-  if (!carry && (fused_waves() == 8 || slices == &kMarchInteriorTag))
+  const FusedArgs fa{fl.st.nsum, fl.st.alpha, fl.st.beta, fl.st.fred, fl.st.ctl, fl.st.aux, fl.st.mu2, fl.L, fl.force};
+  if (!carry)
   {
     const int mode = image_mode(A);
     const MarchPlan mp = launch_plan(A, mode, slices, first, count, true);
@@ -1725,48 +1873,38 @@ void launch_lanczos_fused(const eig_mat_s &A, const double *P, double *Pout, int
     {
       const unsigned G = (unsigned)((mp.ncol * (i64)mp.nseg + kWaves - 1) / kWaves);
       EIG_MARCH_LAUNCH(k_lanczos_fused_march, true, mode, G, s, A.nb_rows, A.own_offset, sell_b1(A), mp,
-                       reinterpret_cast<const dpair *>(P), reinterpret_cast<dpair *>(Pout), k, st.nsum, st.alpha,
-                       st.beta, st.fred, out, red.partials, red.ticket(ticket));
+                       reinterpret_cast<const dpair *>(P), reinterpret_cast<dpair *>(Pout), fa, out, red.partials,
+                       red.ticket(ticket));
       return;
     }
   }
-#define EIG_LF(R_, M_, W_)                                                                                    \
-  hipLaunchKernelGGL((k_lanczos_fused_b1<R_, M_, W_>),                                                       \
-                     dim3(grid_for_slices(k_lanczos_fused_b1<R_, M_, W_>, count, A.ctx->num_cu)),             \
+#define EIG_LF(R_, M_)                                                                                        \
+  hipLaunchKernelGGL((k_lanczos_fused_b1<R_, M_>),                                                           \
+                     dim3(grid_for_slices(k_lanczos_fused_b1<R_, M_>, count, A.ctx->num_cu)),                 \
                      dim3(kStreamThreads), 0, s, A.nb_rows, A.own_offset, sell_b1(A), slices, first, count,      \
-                     reinterpret_cast<const dpair *>(P), reinterpret_cast<dpair *>(Pout), k, st.nsum, st.alpha,  \
-                     st.beta, st.fred, out, carry, red.partials,                                              \
-                     red.ticket(ticket))
-#define EIG_LFW(R_, M_)                                                                                       \
-  {                                                                                                           \
-    const int w_ = fused_waves();                                                                             \
-    if (w_ == 4) EIG_LF(R_, M_, 4);                                                                           \
-    else if (w_ == 5) EIG_LF(R_, M_, 5);                                                                      \
-    else if (w_ == 6) EIG_LF(R_, M_, 6);                                                                      \
-    else EIG_LF(R_, M_, 8);                                                                                   \
-  }
+                     reinterpret_cast<const dpair *>(P), reinterpret_cast<dpair *>(Pout), fa, out, carry,        \
+                     red.partials, red.ticket(ticket))
 #define EIG_LFM(R_)                                                                                           \
   {                                                                                                           \
     const int m_ = image_mode(A);                                                                             \
-    if (m_ == kExplicit) EIG_LFW(R_, kExplicit)                                                               \
-    else if (m_ == kStencil) EIG_LFW(R_, kStencil)                                                            \
-    else if (m_ == kSym8) EIG_LFW(R_, kSym8)                                                                  \
-    else if (m_ == kSym32) EIG_LFW(R_, kSym32)                                                                \
-    else if (m_ == kSymN8) EIG_LFW(R_, kSymN8)                                                                \
-    else if (m_ == kSymN32) EIG_LFW(R_, kSymN32)                                                                \
-    else EIG_LFW(R_, kMixed)                                                                                  \
+    if (m_ == kExplicit) EIG_LF(R_, kExplicit);                                                               \
+    else if (m_ == kStencil) EIG_LF(R_, kStencil);                                                            \
+    else if (m_ == kSym8) EIG_LF(R_, kSym8);                                                                  \
+    else if (m_ == kSym32) EIG_LF(R_, kSym32);                                                                \
+    else if (m_ == kSymN8) EIG_LF(R_, kSymN8);                                                                \
+    else if (m_ == kSymN32) EIG_LF(R_, kSymN32);                                                              \
+    else EIG_LF(R_, kMixed);                                                                                  \
   }
   if (A.R == 1) EIG_LFM(1)
   else if (A.R == 2) EIG_LFM(2)
   else EIG_LFM(4)
 #undef EIG_LFM
-#undef EIG_LFW
 #undef EIG_LF
 }
 
-void launch_fused_tail(const LanczosState &st, int K, hipStream_t s)
+void launch_fused_tail(const LanczosState &st, int L, hipStream_t s)
 {
-  hipLaunchKernelGGL(k_fused_tail, dim3(1), dim3(64), 0, s, st.nsum, st.alpha, st.beta, st.fred, K);
+  hipLaunchKernelGGL(k_fused_tail, dim3(1), dim3(64), 0, s, st.nsum, st.beta, st.fred, st.ctl, st.aux, L);
 }
 
 // General band geometry for k_spmm8_marchg: carried offset P (widest multiple of 16 with -P stored),
@@ -1900,7 +2038,7 @@ void lanczos_kernel_info(const eig_mat_s &A, bool fused, std::string &name, i64 
     bytes = 8 * (i64)A.sym_nup * n + (i64)A.sym_mask_bytes * n + vec;
     // (distributed launches with a halo take the interior / boundary split, never the march)
     const bool whole = !A.ctx->distributed() || (A.recvs.empty() && A.sends.empty());
-    const bool march = whole ? (march_plan(A, mode).nseg > 0 && (!fused || fused_waves() == 8))
+    const bool march = whole ? (march_plan(A, mode).nseg > 0)
                              : march_split_active(A);
     name = fused ? (march ? "k_lanczos_fused_march" : "k_lanczos_fused_b1")
                  : (march ? "k_lanczos_spmv_march" : "k_lanczos_spmv_b1");

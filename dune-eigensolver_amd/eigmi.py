@@ -123,6 +123,7 @@ SIGNATURES = {
     "eig_lanczos_step": (_int, [_vp, _int, _int, ctypes.POINTER(Timing)]),
     "eig_lanczos_tridiag": (_int, [_vp, ctypes.POINTER(_int), _vp, _vp]),
     "eig_lanczos_destroy": (_int, [_vp]),
+    "eig_lanczos_info": (_int, [_vp, ctypes.POINTER(_int), ctypes.POINTER(_int)]),
     "eig_lanczos_capture": (_int, [_vp, _int, _int, ctypes.POINTER(_int)]),
     "eig_lanczos_replay": (_int, [_vp, ctypes.POINTER(Timing)]),
     "eig_lu_create": (_int, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _int, ctypes.POINTER(_vp)]),
@@ -494,6 +495,12 @@ class LanczosWorkspace:
         t = Timing()
         self.A.ctx.check(lib.eig_lanczos_replay(self.h, ctypes.byref(t)))
         return t
+
+    def info(self):
+        """(logical steps taken, kernel launches issued); fused: launches - steps = repairs."""
+        k, L = _int(0), _int(0)
+        self.A.ctx.check(lib.eig_lanczos_info(self.h, ctypes.byref(k), ctypes.byref(L)))
+        return k.value, L.value
 
     def tridiag(self):
         k = _int(0)

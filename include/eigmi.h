@@ -213,10 +213,14 @@ typedef struct eig_timing {
 enum eig_lanczos_flags {
   EIG_LANCZOS_TIME_KERNELS = 1, /* HIP events around every fused SpMV launch (spmv_ms) */
   EIG_LANCZOS_TIME_DETAIL = 2,  /* + events after each allreduce and update (update_ms, comm_ms) */
-  /* One-reduction fused step: ||u_{k}||^2 = ||t_{k-1}||^2 - alpha_{k-1}^2, so u_k is formed inside
-   * the next SpMV's gathers and a step is ONE kernel + ONE allreduce of two doubles (4 window
-   * vectors instead of 3).  Same Krylov process; alpha/beta agree with the two-kernel form to
-   * rounding (cancellation only when beta_{k} << |alpha_{k-1}|). */
+  /* One-reduction fused step: u_k = t_{k-1} - c u_{k-1} is formed inside the next
+   * SpMV's gathers and its squared norm is predicted as ||t||^2 - (t.u)^2/||u||^2 from the three
+   * sums (t.u, t.t, u.u) the previous step reduced, so a step is ONE kernel + ONE allreduce of
+   * three doubles (2 pair vectors instead of 3 vectors).  Guarded: the step runs on A - mu I with
+   * mu = trace(A)/n (alpha reported unshifted), and a launch whose prediction keeps less than 1e-2
+   * of ||t||^2 repairs instead (forms u_k, reduces its exact norm; the next launch takes the step),
+   * decided on the device.  beta[k] of eig_lanczos_tridiag is always the exact ||u_k||.  Same
+   * Krylov process as the two-kernel step; alpha/beta agree with it to its own rounding spread. */
   EIG_LANCZOS_FUSED = 4
 };
 int eig_lanczos_run(eig_mat_t A, int steps, const double *u0, unsigned seed, int flags,
@@ -235,6 +239,9 @@ int eig_lanczos_create_ex(eig_mat_t A, int max_steps, const double *u0, unsigned
 int eig_lanczos_step(eig_lanczos_t ws, int steps, int flags, eig_timing *timing);
 int eig_lanczos_tridiag(eig_lanczos_t ws, int *k, double *alpha_host, double *beta_host);
 int eig_lanczos_destroy(eig_lanczos_t ws);
+/* Logical steps taken and kernel launches issued (fused: steps + repairs + forced final repairs;
+ * two-kernel: = steps). */
+int eig_lanczos_info(eig_lanczos_t ws, int *steps, int *launches);
 /* hipGraph form of eig_lanczos_step: capture the next `steps` steps (kernels, halo exchange,
  * allreduces; plus per-step kernel events when flags has EIG_LANCZOS_TIME_KERNELS) into one
  * graph and instantiate it -- nothing runs yet.  eig_lanczos_replay launches it once

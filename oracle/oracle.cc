@@ -765,72 +765,143 @@ void orc_lanczos_rotating(i64 n, const i64 *rowptr, const i32 *col, const double
   }
 }
 
-// One-reduction fused Lanczos step, the restatement of the GPU's fused step (k_lanczos_fused_b1;
-// DESIGN.md "Fused step").  The same Krylov process as orc_lanczos: u_k = t_{k-1} - c u_{k-1} is
-// formed right before the SpMV that needs it, and its squared norm is PREDICTED from the previous
-// step's reductions, nt_k = tsq - c dsum with c = dsum / m (m = the measured ||u_{k-1}||^2, reduced
-// in the step that formed u_{k-1}), so a step needs one reduction of (dsum, tsq, m).  Every scalar
-// formula is written exactly as fused_scalars() in k_spmv.hip evaluates it.
-static void fused_scalars(double nt_prev, double d, double q, double m, double &c, double &alpha_prev, double &nt,
-                          double &beta, double &gam)
-{
-  const double rn = std::sqrt(nt_prev);
-  const double rm = std::sqrt(m);
-  c = d / m;
-  alpha_prev = c * rn;
-  nt = q - c * d;
-  beta = std::sqrt(nt) * rn / rm;
-  gam = beta / rm;
-}
+// One-reduction fused Lanczos step, the restatement of the GPU's fused step (k_lanczos_fused_b1 /
+// k_lanczos_fused_march, fused_begin in k_spmv.hip).  The same Krylov process as
+// orc_lanczos: u_k = t_{k-1} - c u_{k-1} is formed right before the SpMV that needs it, and its
+// squared norm is PREDICTED from the previous step's reductions, nt_k = tsq - c dsum with
+// c = dsum / m (m = the measured ||u_{k-1}||^2), so a step needs one reduction of (dsum, tsq, m).
+// Guard: the step runs on A - mu I (mu = trace / n; alpha reported unshifted), and a launch whose
+// prediction keeps no more than kTau of tsq REPAIRS instead of stepping (u_k formed explicitly,
+// its exact norm reduced; the next launch takes step k with c = 0 and that norm).  The final beta
+// is always exact (a forced repair, as eig_lanczos_tridiag does).  Launch by launch, every scalar
+// formula is written exactly as the kernel prologue evaluates it.
+static const double kTau = 1e-2;
+enum { kStep = 0, kPost = 1, kHalt = 2, kRepair = 3 };
 
 void orc_lanczos_fused(i64 n, const i64 *rowptr, const i32 *col, const double *val, int steps, const double *u0,
-                       double *alpha, double *beta)
+                       double *alpha, double *beta, int *launches_out)
 {
+  double dsum = 0.0;
+  for (i64 i = 0; i < n; ++i)
+    for (i64 p = rowptr[i]; p < rowptr[i + 1]; ++p)
+      if (col[p] == i) dsum += val[p];
+  const double mu = dsum / (double)n;
   std::vector<double> T(u0, u0 + n), U(n, 0.0), Tn(n), Un(n), ux(n);
-  std::vector<double> nt(steps + 1), red(3 * (size_t)(steps > 0 ? steps : 1));
+  std::vector<double> nsum(steps + 2, 0.0);
   double s0 = 0.0;
   for (i64 i = 0; i < n; ++i) s0 += u0[i] * u0[i];
-  nt[0] = s0;
-  beta[0] = std::sqrt(s0);
-  for (int k = 0; k < steps; ++k)
-  {
-    double c = 0.0, gam = 0.0;
-    if (k > 0)
+  nsum[0] = s0;
+  double red[3] = {0.0, 0.0, 0.0}, aux[2] = {0.0, 0.0};
+  int j = 0, mode = kStep, L = 0;
+  auto launch = [&](bool force) {
+    double c = 0.0, nt = 1.0, ap = 0.0, bk = 0.0, gam = 0.0, rn = 0.0, rm = 0.0;
+    int act;
+    if (mode == kPost)
     {
-      double ap, bk;
-      fused_scalars(nt[k - 1], red[3 * (k - 1)], red[3 * (k - 1) + 1], red[3 * (k - 1) + 2], c, ap, nt[k], bk, gam);
-      alpha[k - 1] = ap;
-      beta[k] = bk;
+      const double mex = red[2];
+      rn = aux[0];
+      rm = aux[1];
+      nt = mex;
+      if (!(mex > 0.0)) act = kHalt;
+      else
+      {
+        bk = std::sqrt(mex) * rn / rm;
+        gam = bk / rm;
+        act = kPost;
+      }
     }
-    const double sig = 1.0 / std::sqrt(nt[k]);
+    else if (j == 0)
+    {
+      nt = nsum[0];
+      act = kStep;
+    }
+    else
+    {
+      const double d = red[0], q = red[1], m = red[2];
+      rn = std::sqrt(nsum[j - 1]);
+      rm = std::sqrt(m);
+      c = d / m;
+      ap = c * rn + mu;
+      nt = q - c * d;
+      if (force || !(nt > kTau * q)) act = kRepair;
+      else
+      {
+        bk = std::sqrt(nt) * rn / rm;
+        gam = bk / rm;
+        act = kStep;
+      }
+    }
+    const double sig = 1.0 / std::sqrt(nt);
+    ++L;
+    if (act == kHalt)
+    {
+      nsum[j] = 0.0;
+      beta[j] = 0.0;
+      mode = kHalt;
+      return;
+    }
+    if (act == kRepair)
+    {
+      alpha[j - 1] = ap;
+      aux[0] = rn;
+      aux[1] = rm;
+      double m2 = 0.0;
+      for (i64 i = 0; i < n; ++i)
+      {
+        const double u = T[i] - c * U[i];
+        T[i] = u;  // pairs (u_j, u_{j-1})
+        m2 += u * u;
+      }
+      red[0] = red[1] = 0.0;
+      red[2] = m2;
+      mode = kPost;
+      return;
+    }
+    if (act == kPost)
+    {
+      nsum[j] = nt;
+      beta[j] = bk;
+    }
+    else if (j > 0)
+    {
+      nsum[j] = nt;
+      alpha[j - 1] = ap;
+      beta[j] = bk;
+    }
+    else
+      beta[0] = std::sqrt(nt);
     for (i64 i = 0; i < n; ++i) ux[i] = T[i] - c * U[i];
     double d = 0.0, q = 0.0, m = 0.0;
     for (i64 i = 0; i < n; ++i)
     {
       double acc = 0.0;
       for (i64 p = rowptr[i]; p < rowptr[i + 1]; ++p) acc += val[p] * ux[col[p]];
-      double ti = acc * sig;
-      if (k > 0) ti = ti - gam * U[i];
+      double ti = (acc - mu * ux[i]) * sig;
+      if (j > 0) ti = ti - gam * U[i];
       Tn[i] = ti;
       Un[i] = ux[i];
       d += ti * ux[i];
       q += ti * ti;
       m += ux[i] * ux[i];
     }
-    red[3 * k] = d;
-    red[3 * k + 1] = q;
-    red[3 * k + 2] = m;
+    red[0] = d;
+    red[1] = q;
+    red[2] = m;
     std::swap(T, Tn);
     std::swap(U, Un);
-  }
-  if (steps > 0)
+    ++j;
+    mode = kStep;
+  };
+  beta[0] = std::sqrt(s0);
+  while (j < steps && mode != kHalt) launch(false);
+  if (mode == kStep && j > 0) launch(true);  // exact final beta (eig_lanczos_tridiag)
+  if (mode == kPost)
   {
-    double c, ap, bk, gam;
-    fused_scalars(nt[steps - 1], red[3 * (steps - 1)], red[3 * (steps - 1) + 1], red[3 * (steps - 1) + 2], c, ap,
-                  nt[steps], bk, gam);
-    alpha[steps - 1] = ap;
-    beta[steps] = bk;
+    const double mex = red[2];
+    nsum[j] = mex;
+    beta[j] = mex > 0.0 ? std::sqrt(mex) * aux[0] / aux[1] : 0.0;
   }
+  if (launches_out) *launches_out = L;
 }
 
 } // extern "C"

@@ -67,7 +67,7 @@ def _load():
                                     [ctypes.c_double, ctypes.c_double, ctypes.c_double, _int, _int, ctypes.c_uint,
                                      _f64p, _f64p]),
         "orc_lanczos_rotating": (None, [_i64, _i64p, _i32p, _f64p, _int, _f64p, _f64p, _f64p, _f64p, _f64p]),
-        "orc_lanczos_fused": (None, [_i64, _i64p, _i32p, _f64p, _int, _f64p, _f64p, _f64p]),
+        "orc_lanczos_fused": (None, [_i64, _i64p, _i32p, _f64p, _int, _f64p, _f64p, _f64p, ctypes.c_void_p]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -258,11 +258,17 @@ def lanczos(A, u0, k):
     return U.reshape(k + 1, A.n), alpha, beta
 
 
-def lanczos_fused(A, u0, k):
-    """The fused one-reduction recurrence (orc_lanczos_fused): alpha[k], beta[k+1]."""
+def lanczos_fused(A, u0, k, with_launches=False):
+    """The guarded fused one-reduction recurrence (orc_lanczos_fused): alpha[k], beta[k+1]
+    (beta[k] exact, as eig_lanczos_tridiag returns it); with_launches: also the launch count
+    (steps + repairs + the forced final repair)."""
     alpha = np.zeros(max(k, 1))
     beta = np.zeros(k + 1)
-    lib.orc_lanczos_fused(A.n, A.rowptr, A.col, A.val, k, np.ascontiguousarray(u0, dtype=np.float64), alpha, beta)
+    L = ctypes.c_int(0)
+    lib.orc_lanczos_fused(A.n, A.rowptr, A.col, A.val, k, np.ascontiguousarray(u0, dtype=np.float64), alpha, beta,
+                          ctypes.byref(L))
+    if with_launches:
+        return alpha[:k], beta, L.value
     return alpha[:k], beta
 
 

@@ -67,6 +67,28 @@ static void block_lanczos(eig_ctx_t ctx, int N, int64_t b, int64_t cnt, bool dis
   eig_mat_destroy(M);
 }
 
+// Guarded fused step with repairs (k_spmv.hip fused_begin): Poisson plus +100 on the diagonal of
+// 12 rows puts trace/n away from the bulk, so some launches repair instead of stepping; the
+// repair and the step after it run through the interior / boundary split with the carry.
+static const int kRsteps = 14;
+static void outliers(int N, int64_t b, Rows &r)
+{
+  const int64_t n = (int64_t)N * N * N, every = n / 12;
+  for (int64_t i = 0; i + 1 < (int64_t)r.rp.size(); ++i)
+    for (int64_t p = r.rp[i]; p < r.rp[i + 1]; ++p)
+      if (r.c[p] == b + i && (b + i) % every == 0) r.v[p] += 100.0;
+}
+static void fused_repair_run(eig_mat_t A, double *a, double *be, int *launches)
+{
+  eig_lanczos_t ws;
+  CK(eig_lanczos_create_ex(A, kRsteps, nullptr, 123, EIG_LANCZOS_FUSED, &ws));
+  CK(eig_lanczos_step(ws, kRsteps, 0, nullptr));
+  CK(eig_lanczos_tridiag(ws, nullptr, a, be));
+  int k = 0;
+  CK(eig_lanczos_info(ws, &k, launches));
+  CK(eig_lanczos_destroy(ws));
+}
+
 int main(int argc, char **argv)
 {
   const int P = argc > 1 ? std::atoi(argv[1]) : 3;
@@ -78,6 +100,10 @@ int main(int argc, char **argv)
   // ---- serial reference on one context
   std::vector<double> x(n), y_ser(n), a_ser(steps), b_ser(steps + 1), ev_ser(nev), fa_ser(steps), fb_ser(steps + 1);
   std::vector<double> bev_ser(kBnev);
+  std::vector<double> ra_ser(kRsteps), rb_ser(kRsteps + 1);
+  std::vector<std::vector<double>> ral(P, std::vector<double>(kRsteps)), rbe(P, std::vector<double>(kRsteps + 1));
+  int rl_ser = 0;
+  std::vector<int> rl(P, 0);
   std::vector<std::vector<double>> bev(P, std::vector<double>(kBnev));
   for (int64_t i = 0; i < n; ++i) x[i] = std::sin(0.37 * i) + 0.01 * (i % 7);
   {
@@ -90,6 +116,10 @@ int main(int argc, char **argv)
     CK(eig_lanczos_run(A, steps, nullptr, 123, 0, a_ser.data(), b_ser.data(), nullptr));
     CK(eig_lanczos_run(A, steps, nullptr, 123, EIG_LANCZOS_FUSED, fa_ser.data(), fb_ser.data(), nullptr));
     CK(eig_lanczos_solve(A, nev, ncv, EIG_WHICH_LA, 123, ev_ser.data(), nullptr, nullptr));
+    eig_mat_destroy(A);
+    outliers(N, 0, r);
+    CK(eig_mat_create_bcsr(ctx, n, n, 1, 1, r.rp.data(), r.c.data(), r.v.data(), &A));
+    fused_repair_run(A, ra_ser.data(), rb_ser.data(), &rl_ser);
     eig_mat_destroy(A);
     block_lanczos(ctx, N, 0, n, false, bev_ser.data());
     eig_ctx_destroy(ctx);
@@ -151,6 +181,13 @@ int main(int argc, char **argv)
                       std::memcmp(bg.data(), be[r].data(), (steps + 1) * 8) == 0;
       }
       CK(eig_lanczos_solve(A, nev, ncv, EIG_WHICH_LA, 123, ev[r].data(), nullptr, nullptr));
+      {
+        outliers(N, b, rows);
+        eig_mat_t B;
+        CK(eig_mat_create_bcsr_dist(ctx, n, b, cnt, 1, 1, rows.rp.data(), rows.c.data(), rows.v.data(), &B));
+        fused_repair_run(B, ral[r].data(), rbe[r].data(), &rl[r]);
+        eig_mat_destroy(B);
+      }
       block_lanczos(ctx, N, b, cnt, true, bev[r].data());
       eig_free(ctx, dx);
       eig_free(ctx, dy);
@@ -201,6 +238,21 @@ int main(int argc, char **argv)
       {
         std::printf("FAIL rank %d fused step %d: alpha %.17g/%.17g beta %.17g/%.17g\n", r, j, fal[r][j], fa_ser[j],
                     fbe[r][j + 1], fb_ser[j + 1]);
+        ++failures;
+        break;
+      }
+    if (rl[r] != rl_ser || rl_ser <= kRsteps + 1)
+    {
+      std::printf("FAIL rank %d: fused repair run took %d launches, serial %d (%d steps)\n", r, rl[r], rl_ser,
+                  kRsteps);
+      ++failures;
+    }
+    for (int j = 0; j < kRsteps; ++j)
+      if (std::fabs(ral[r][j] - ra_ser[j]) > 1e-10 * std::fabs(ra_ser[j]) ||
+          std::fabs(rbe[r][j + 1] - rb_ser[j + 1]) > 1e-10 * std::fabs(rb_ser[j + 1]))
+      {
+        std::printf("FAIL rank %d repaired fused step %d: alpha %.17g/%.17g beta %.17g/%.17g\n", r, j, ral[r][j],
+                    ra_ser[j], rbe[r][j + 1], rb_ser[j + 1]);
         ++failures;
         break;
       }
