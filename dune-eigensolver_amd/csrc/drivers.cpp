@@ -785,8 +785,8 @@ void read_timing(const std::vector<hipEvent_t> &ev, int steps, int nps, eig_timi
   float ms = 0.f;
   EIG_HIP(hipEventElapsedTime(&ms, ev[0], ev[1]));
   timing->total_ms += ms;
+  if (!nps) return;  // region events only: no per-launch kernel timing
   timing->spmv_launches += steps;
-  if (!nps) return;
   for (int i = 0; i < steps; ++i)
   {
     const hipEvent_t *e = &ev[2 + (size_t)nps * i];
