@@ -116,15 +116,16 @@ def committed_traffic(kernel, N, world):
     for p in glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json")):
         try:
             d = json.load(open(p))
-            line = d.get("bench_line_under_trace", {})
-            if line.get("config", {}).get("N") != N or line.get("n_gpus") != world:
+            line = d.get("bench_line_under_trace")
+            cfg = line.get("config") if isinstance(line, dict) else None
+            if not isinstance(cfg, dict) or cfg.get("N") != N or line.get("n_gpus") != world:
                 continue
             for name, k in d["kernels"].items():  # template instances: "eigmi::k_..._b1<1, 1>"
                 if name.split("<")[0] == "eigmi::" + kernel:
                     stamp = d.get("collected", os.path.getmtime(p))
                     if best is None or stamp > best[2]:
                         best = (k["hbm_bytes"], os.path.relpath(p, ROOT), stamp)
-        except (OSError, ValueError, KeyError):
+        except (OSError, ValueError, KeyError, TypeError, AttributeError):
             continue
     return best[:2] if best else None
 

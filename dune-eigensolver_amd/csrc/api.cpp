@@ -356,8 +356,7 @@ bool all_ranks(eig_ctx_t ctx, bool mine)
 void mailbox_setup_rccl(eig_ctx_t ctx)
 {
   const int P = ctx->nranks, me = ctx->rank;
-  const char *env = std::getenv("EIGMI_ALLREDUCE");
-  const bool want = P > 1 && P <= kMaxMailboxRanks && !(env && std::string(env) == "rccl");
+  const bool want = P > 1 && P <= kMaxMailboxRanks;
   if (!all_ranks(ctx, want)) return;
   std::vector<unsigned char> h((size_t)P * HIP_IPC_HANDLE_SIZE, 0);
   bool ok = true;
@@ -396,8 +395,14 @@ void mailbox_setup_rccl(eig_ctx_t ctx)
 
 extern "C" int eig_comm_init(eig_ctx_t ctx, int nranks, int rank, const unsigned char id[128])
 {
+  return eig_comm_init_ex(ctx, nranks, rank, id, 0);
+}
+
+extern "C" int eig_comm_init_ex(eig_ctx_t ctx, int nranks, int rank, const unsigned char id[128], int flags)
+{
   return guard(ctx, [&] {
     EIG_CHECK(ctx && id && nranks >= 1 && rank >= 0 && rank < nranks, EIG_ERR_ARG, "eig_comm_init: bad arguments");
+    EIG_CHECK((flags & ~EIG_COMM_MAILBOX) == 0, EIG_ERR_ARG, "eig_comm_init_ex: unknown flag");
     EIG_CHECK(!ctx->loop && !ctx->mbox, EIG_ERR_ARG, "context already has a transport");
     DeviceGuard dg(ctx->device);
     ncclUniqueId u;
@@ -405,7 +410,9 @@ extern "C" int eig_comm_init(eig_ctx_t ctx, int nranks, int rank, const unsigned
     EIG_NCCL(ncclCommInitRank(&ctx->comm, nranks, u, rank));
     ctx->nranks = nranks;
     ctx->rank = rank;
-    mailbox_setup_rccl(ctx);
+    // the mailbox allreduce only on request: it is validated between processes on one GPU
+    // (tests/test_mailbox_gpu.py), not yet across xGMI
+    if (flags & EIG_COMM_MAILBOX) mailbox_setup_rccl(ctx);
   });
 }
 
@@ -561,26 +568,6 @@ extern "C" int eig_memset(eig_ctx_t ctx, void *dst, int value, size_t bytes)
 // ============================================================================================
 namespace {
 
-// Rows per lane of the SELL image for 1x1 matrices (EIGMI_SELL_R overrides; 1, 2 or 4).
-int sell_rows_per_lane(int br, int bc)
-{
-  if (br != 1 || bc != 1) return 1;
-  int R = 1;  // measured best for the fused Lanczos kernel (tools/spmv_sweep.py)
-  if (const char *e = std::getenv("EIGMI_SELL_R"))
-  {
-    const int v = std::atoi(e);
-    if (v == 1 || v == 2 || v == 4) R = v;
-  }
-  return R;
-}
-
-// Build the SELL-C image (C = 64 R) of `nb` block rows (rowptr/col/vals on the host; columns are
-// shifted by col_shift into window-local block columns) and upload it.
-bool stencil_enabled()
-{
-  const char *e = std::getenv("EIGMI_STENCIL");
-  return !(e && e[0] == '0');
-}
 
 template <class F>
 void parallel_slices(i64 ns, F &&f)
@@ -603,10 +590,10 @@ void parallel_slices(i64 ns, F &&f)
 void build_sell(eig_mat_s &A, i64 nb, const int64_t *rowptr, const int32_t *col, const double *vals, i64 col_shift)
 {
   const int bb = A.br * A.bc;
-  A.R = sell_rows_per_lane(A.br, A.bc);
+  A.R = 1;  // one row per lane (2 / 4 measured slower for the fused Lanczos kernel)
   const i64 C = 64 * (i64)A.R;
   const i64 ns = (nb + C - 1) / C;
-  const bool try_stencil = (bb == 1) && stencil_enabled();
+  const bool try_stencil = (bb == 1) && !(A.kflags & EIG_MAT_NO_STENCIL);
   const i64 row0 = A.row_begin;
   std::vector<i32> swidth(ns, -1), sdelta(8 * (size_t)ns, 0);
   std::vector<i64> sp(ns + 1, 0), wdt(ns, 0);
@@ -712,11 +699,6 @@ void build_sell(eig_mat_s &A, i64 nb, const int64_t *rowptr, const int32_t *col,
   A.device_bytes = (ns + 1) * 8 + total * 4 + total * bb * 8 + (A.n_stencil_slices ? ns * (36 + C) : 0);
 }
 
-bool sym_enabled()
-{
-  const char *e = std::getenv("EIGMI_SYM");
-  return !(e && e[0] == '0');
-}
 
 // Symmetric band image (internal.h, eig_mat_s::sym_*) next to the SELL image, for square 1x1
 // matrices with at most kSymMaxOff distinct offsets whose stored mirror pairs are bitwise equal
@@ -727,7 +709,7 @@ bool sym_enabled()
 // get their slots from the owned rows' lower entries alone.  Silently skipped when not applicable.
 void build_sym(eig_mat_s &A, i64 nb, const int64_t *rowptr, const int32_t *col, const double *vals)
 {
-  if (A.br != 1 || A.bc != 1 || A.R != 1 || !sym_enabled() || nb == 0) return;
+  if (A.br != 1 || A.bc != 1 || (A.kflags & EIG_MAT_NO_BAND) || nb == 0) return;
   if (A.nb_cols != A.nb_rows_global) return;
   const i64 row0 = A.row_begin;
   // distinct offsets (per thread, then merged)
@@ -893,7 +875,15 @@ void destroy_mat(eig_mat_s *A)
 extern "C" int eig_mat_create_bcsr(eig_ctx_t ctx, int64_t nb_rows, int64_t nb_cols, int br, int bc,
                                    const int64_t *rowptr, const int32_t *col, const double *vals, eig_mat_t *out)
 {
+  return eig_mat_create_bcsr_ex(ctx, nb_rows, nb_cols, br, bc, rowptr, col, vals, 0, out);
+}
+
+extern "C" int eig_mat_create_bcsr_ex(eig_ctx_t ctx, int64_t nb_rows, int64_t nb_cols, int br, int bc,
+                                      const int64_t *rowptr, const int32_t *col, const double *vals, int flags,
+                                      eig_mat_t *out)
+{
   return guard(ctx, [&] {
+    EIG_CHECK((flags & ~EIG_MAT_FLAGS_ALL) == 0, EIG_ERR_ARG, "eig_mat_create_bcsr_ex: unknown flag");
     EIG_CHECK(ctx && out && rowptr && (rowptr[nb_rows] == 0 || (col && vals)), EIG_ERR_ARG,
               "eig_mat_create_bcsr: null argument");
     EIG_CHECK(nb_rows >= 0 && nb_cols >= 0, EIG_ERR_ARG, "eig_mat_create_bcsr: negative size");
@@ -903,6 +893,7 @@ extern "C" int eig_mat_create_bcsr(eig_ctx_t ctx, int64_t nb_rows, int64_t nb_co
     validate_csr(nb_rows, nb_cols, rowptr, col);
     auto *A = new eig_mat_s();
     A->ctx = ctx;
+    A->kflags = flags;
     A->br = br;
     A->bc = bc;
     A->nb_rows = A->nb_rows_global = nb_rows;
@@ -931,7 +922,15 @@ extern "C" int eig_mat_create_bcsr_dist(eig_ctx_t ctx, int64_t nb_rows_global, i
                                         int64_t nb_local, int br, int bc, const int64_t *rowptr, const int32_t *col,
                                         const double *vals, eig_mat_t *out)
 {
+  return eig_mat_create_bcsr_dist_ex(ctx, nb_rows_global, row_begin, nb_local, br, bc, rowptr, col, vals, 0, out);
+}
+
+extern "C" int eig_mat_create_bcsr_dist_ex(eig_ctx_t ctx, int64_t nb_rows_global, int64_t row_begin,
+                                           int64_t nb_local, int br, int bc, const int64_t *rowptr,
+                                           const int32_t *col, const double *vals, int flags, eig_mat_t *out)
+{
   return guard(ctx, [&] {
+    EIG_CHECK((flags & ~EIG_MAT_FLAGS_ALL) == 0, EIG_ERR_ARG, "eig_mat_create_bcsr_dist_ex: unknown flag");
     EIG_CHECK(ctx && out && rowptr, EIG_ERR_ARG, "eig_mat_create_bcsr_dist: null argument");
     EIG_CHECK(br == bc && br >= 1 && br <= 4, EIG_ERR_BLOCKSIZE, "distributed matrices need square blocks 1..4");
     EIG_CHECK(row_begin >= 0 && nb_local >= 0 && row_begin + nb_local <= nb_rows_global, EIG_ERR_SHAPE,
@@ -948,6 +947,7 @@ extern "C" int eig_mat_create_bcsr_dist(eig_ctx_t ctx, int64_t nb_rows_global, i
     const i64 wb_blk = plan[0], cmin = plan[3], cmax = plan[4];
     auto *A = new eig_mat_s();
     A->ctx = ctx;
+    A->kflags = flags;
     A->br = br;
     A->bc = bc;
     A->nb_rows = nb_local;
@@ -1383,15 +1383,11 @@ void gram_device(eig_ctx_t ctx, i64 n, i64 m1, i64 m2, const double *Q1, const d
   allreduce_sum(ctx, G, m1 * m2, ctx->stream);
 }
 
-// EIGMI_MGS_SMALL=0 keeps the grid-wide MGS passes for small blocks too (A/B, tests)
-static bool mgs_small_disabled()
-{
-  const char *e = std::getenv("EIGMI_MGS_SMALL");
-  return e && e[0] == '0';
-}
 
 void orthonormalize_device(eig_ctx_t ctx, i64 n, i64 m, double *Q, int variant)
 {
+  const int flags = variant & EIG_ORTHO_GRID;
+  variant &= ~EIG_ORTHO_GRID;
   hipStream_t s = ctx->stream;
   double *S = (double *)ctx_buffer(ctx, 3, 64 * sizeof(double));
   double *U = S + 0;  // reused: Ssum for MGS, Gram for CholQR
@@ -1401,7 +1397,7 @@ void orthonormalize_device(eig_ctx_t ctx, i64 n, i64 m, double *Q, int variant)
   for (i64 bk = 0; bk < m; bk += 8)
   {
     double *Qb = Q + bk * n;
-    if (variant == EIG_ORTHO_MGS && !ctx->distributed() && !mgs_small_disabled() && launch_mgs_small(n, Qb, s))
+    if (variant == EIG_ORTHO_MGS && !ctx->distributed() && !(flags & EIG_ORTHO_GRID) && launch_mgs_small(n, Qb, s))
     {
     }
     else if (variant == EIG_ORTHO_MGS)
@@ -1444,7 +1440,8 @@ extern "C" int eig_orthonormalize_mv8(eig_ctx_t ctx, int64_t n, int64_t m, doubl
 {
   return guard(ctx, [&] {
     EIG_CHECK(ctx && Q && n >= 0, EIG_ERR_ARG, "eig_orthonormalize_mv8: bad argument");
-    EIG_CHECK(variant == EIG_ORTHO_MGS || variant == EIG_ORTHO_CHOLQR, EIG_ERR_ARG, "unknown variant");
+    const int v = variant & ~EIG_ORTHO_GRID;
+    EIG_CHECK(v == EIG_ORTHO_MGS || v == EIG_ORTHO_CHOLQR, EIG_ERR_ARG, "unknown variant");
     EIG_MV8_CHECK(m);
     DeviceGuard dg(ctx->device);
     orthonormalize_device(ctx, n, m, Q, variant);

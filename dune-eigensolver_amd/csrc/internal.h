@@ -164,6 +164,9 @@ struct eig_mat_s {
   // r sits at slice_ptr[s] + k*C + r (cols) and (slice_ptr[s] + k*C)*br*bc + t*C + r (values,
   // t < br*bc).  Lane l of the slice's wavefront owns rows l R .. l R + R - 1.  R = 1 for blocks.
   int R = 1;
+  // kernel-image policy fixed at creation (eig_mat_create_bcsr_ex flags: EIG_MAT_NO_BAND,
+  // EIG_MAT_BAND_GATHER, EIG_MAT_NO_STENCIL, EIG_MAT_NO_MARCH)
+  int kflags = 0;
   // Stencil slices (1x1 blocks only): when every row of slice s draws its columns from one set of
   // at most 8 offsets delta = global col - global row (structured-grid / banded matrices), the
   // slice is read through st_delta[8 s + k] (ascending) and a per-row bit mask st_mask[r] (bit k
@@ -317,7 +320,6 @@ void launch_resid_sq(i64 n, const double *x, const double *y, double theta, doub
 // Window-layout multivector kernels (k_block.hip).  m columns (multiple of 8), leading dimension
 // = the matrix window, owned rows at own_offset.
 void launch_sell_mv8(const eig_mat_s &A, i64 m, const double *X, double *Y, hipStream_t s);
-int mv8_kernel_choice();
 int sell_mv8_launches(i64 m);  // kernel launches per launch_sell_mv8 / launch_cheb_step call
 void launch_cheb_step(const eig_mat_s &M, i64 m, const double *Xk, double *Xold, const double *B, const double *dinv,
                       double omega, double gamma, hipStream_t s);
@@ -353,7 +355,8 @@ struct TrsvImage {
   double *tile[2] = {nullptr, nullptr};
   unsigned long long *tmask[2] = {nullptr, nullptr};
   bool staged = false;  // the factors fit k_tsolve_staged (k_trsv.hip)
-  // the staged image is built on first use (EIGMI_TRSV=staged, or factors without the
+  int solver = 0;       // eig_lu_set_solver: EIG_TRSV_AUTO / _BLOCKINV / _STAGED / _CSR
+  // the staged image is built on first use (EIG_TRSV_STAGED, or factors without the
   // block-inverse image): host copies of the split factor rows until then
   bool staged_built = false;
   std::shared_ptr<struct TrsvHostRows> host;

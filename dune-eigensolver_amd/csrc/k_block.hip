@@ -1,8 +1,10 @@
 // k_block.hip -- window-layout MultiVector<double,8> kernels (gfx950) for the block methods:
 //
-//   k_sell_mv8        Y = A X over the SELL-64 image, row per lane, 8 columns per column block,
-//                     MB column blocks per matrix pass; epilogue kStore (plain SpMM, a2) or kCheb
-//                     (one Chebyshev-Jacobi step of the mass solve, fused into the SpMM)
+//   k_sell_mv8g       Y = A X over the SELL-64 image, one column block (m = 8): a wave per slice,
+//                     lane = column pair x 4 rows
+//   k_sell_mv8q       the same for m >= 16: 4 lanes per row, up to 4 column blocks per matrix pass;
+//                     epilogue kStore (plain SpMM, a2) or kCheb (one Chebyshev-Jacobi step of the
+//                     mass solve, fused into the SpMM)
 //   k_diag_inv        dinv[r] = 1 / a_rr
 //   k_cheb_init       X = gamma * dinv o B
 //   k_panel_gram_*    G = Q1^T Q2 for tall-skinny panels on MFMA (v_mfma_f64_16x16x4f64), two
@@ -32,114 +34,24 @@ static inline int grid_cap(i64 work, i64 per_block, int cap)
 }
 
 // ---------------------------------------------------------------------------------------------
-// SpMM over 64-row SELL slices (R = 1): lane l computes all 8 columns of slice row l for MB
-// column blocks b0 .. b0+nb-1; the slice's value / column (or offset + mask) streams are read once
-// per MB blocks, coalesced; each gathered X row is four 16-B loads.  Per column the row sum runs
-// over the stored entries in ascending-column order from 0.0 (bitwise the reference's
-// matmul_sparse_tallskinny_blocked, kernels_cpp.hh:644-655).
+// SpMM over 64-row SELL slices.  Per column the row sum runs over the stored entries in
+// ascending-column order from 0.0 (bitwise the reference's matmul_sparse_tallskinny_blocked,
+// kernels_cpp.hh:644-655).
 //
 // kCheb epilogue (Golub-Varga three-term Chebyshev semi-iteration for M x = b with the Jacobi
 // splitting): with acc = (M x_k)_r,
 //     x_{k+1}[r] = omega (x_k[r] + gamma dinv[r] (b[r] - acc) - x_{k-1}[r]) + x_{k-1}[r]
 // written in place over x_{k-1} (Xold); x_k is the gathered input X.
+// (Measured and dropped: a lane-per-row mapping with 16 columns per matrix pass -- 131 vs 119 us
+// for the 7-point SpMM at 128^3 -- and 2 column blocks per quad pass.)
 // ---------------------------------------------------------------------------------------------
 enum { kStore = 0, kCheb = 1 };
-
-template <int MB, bool STENCIL, int EPI>
-__global__ __launch_bounds__(256) void k_sell_mv8(i64 nrows, i64 nslices, const i64 *__restrict__ slice_ptr,
-                                                  const double *__restrict__ val, const i32 *__restrict__ col,
-                                                  const i32 *__restrict__ st_delta, const uint8_t *__restrict__ st_mask,
-                                                  const double *__restrict__ X, double *__restrict__ Y, i64 ld,
-                                                  i64 own, int b0, int nb, const double *__restrict__ Bv,
-                                                  const double *__restrict__ dinv, double omega, double gamma)
-{
-  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const i64 per = (nslices + gridDim.x - 1) / gridDim.x;
-  const i64 sb = (i64)blockIdx.x * per, se = sb + per < nslices ? sb + per : nslices;
-  for (i64 s = sb + wave; s < se; s += 4)
-  {
-    const i64 base = slice_ptr[s];
-    const int width = (int)((slice_ptr[s + 1] - base) >> 6);
-    const i64 r = s * 64 + lane;
-    unsigned m = 0;
-    if (STENCIL) m = st_mask[s * 64 + lane];
-    double acc[MB][8];
-#pragma unroll
-    for (int q = 0; q < MB; ++q)
-#pragma unroll
-      for (int jj = 0; jj < 8; ++jj) acc[q][jj] = 0.0;
-    for (int k = 0; k < width; ++k)
-    {
-      const double a = __builtin_nontemporal_load(val + base + k * 64 + lane);
-      i64 c;
-      bool ok;
-      if (STENCIL)
-      {
-        ok = (m >> k) & 1u;
-        c = own + r + st_delta[8 * s + k];  // window column = own + global row - row_begin + delta
-      }
-      else
-      {
-        const i32 cc = __builtin_nontemporal_load(col + base + k * 64 + lane);
-        ok = cc >= 0;
-        c = cc;
-      }
-      if (!ok) continue;
-#pragma unroll
-      for (int q = 0; q < MB; ++q)
-      {
-        if (q < nb)
-        {
-          const double2 *xr = reinterpret_cast<const double2 *>(X + ((i64)(b0 + q) * ld + c) * 8);
-#pragma unroll
-          for (int h = 0; h < 4; ++h)
-          {
-            const double2 xv = xr[h];
-            acc[q][2 * h] += a * xv.x;
-            acc[q][2 * h + 1] += a * xv.y;
-          }
-        }
-      }
-    }
-    if (r < nrows)
-    {
-      double di = 0.0;
-      if (EPI == kCheb) di = dinv[r];
-#pragma unroll
-      for (int q = 0; q < MB; ++q)
-        if (q < nb)
-        {
-          const i64 row = ((i64)(b0 + q) * ld + own + r) * 8;
-          double2 *yr = reinterpret_cast<double2 *>(Y + row);
-          if (EPI == kStore)
-          {
-#pragma unroll
-            for (int h = 0; h < 4; ++h) yr[h] = make_double2(acc[q][2 * h], acc[q][2 * h + 1]);
-          }
-          else
-          {
-            const double2 *xr = reinterpret_cast<const double2 *>(X + row);
-            const double2 *br = reinterpret_cast<const double2 *>(Bv + row);
-            const double gd = gamma * di;
-#pragma unroll
-            for (int h = 0; h < 4; ++h)
-            {
-              const double2 xk = xr[h], bb = br[h], xo = yr[h];
-              const double n0 = omega * (xk.x + gd * (bb.x - acc[q][2 * h]) - xo.x) + xo.x;
-              const double n1 = omega * (xk.y + gd * (bb.y - acc[q][2 * h + 1]) - xo.y) + xo.y;
-              yr[h] = make_double2(n0, n1);
-            }
-          }
-        }
-    }
-  }
-}
 
 // Quad mapping: 4 lanes per row (lane owns column pair 2 (l & 3), 2 (l & 3) + 1 of every column
 // block), 16 rows per wave, a workgroup (4 waves) per 64-row slice, MB column blocks per matrix
 // pass.  Entries are consumed U at a time: the U columns / values are loaded first, then all U * MB
 // 16-B gathers are issued before the multiply-adds (memory-level parallelism without holding
-// whole 64-B rows per lane).  Same per-column summation order as k_sell_mv8.
+// whole 64-B rows per lane).  Per column, ascending-column order from 0.0 as above.
 //
 // XCD-aware plane-slab schedule.  A unit is 16 W rows (W waves of 16 rows; W = 2: two units per
 // 64-row slice).  The rows are cut into "planes" of P8 units (P8 = the matrix bandwidth -- N^2
@@ -410,34 +322,6 @@ bool all_stencil(const eig_mat_s &A) { return A.n_stencil_slices == A.nslices &&
 
 }  // namespace
 
-// Kernel mapping for the window-layout SpMM / Chebyshev step: EIGMI_MV8_KERNEL = rows (lane per
-// row, 16 columns per matrix pass), quad (4 lanes per row, 32 columns per pass; default) or quad2
-// (4 lanes per row, 16 columns per pass); grp / grp2 (k_sell_mv8g, 4 / 2 column blocks per pass).
-// One column block (m = 8): EIGMI_MV8_KERNEL1 = rows (k_sell_mv8) or grp (k_sell_mv8g, default:
-// 119 vs 131 us for the 7-point SpMM at 128^3, 221 vs 241 us on the 15-point P1 mass matrix).
-int mv8_kernel_choice()
-{
-  static int v = [] {
-    const char *e = std::getenv("EIGMI_MV8_KERNEL");
-    if (e && std::string(e) == "rows") return 0;
-    if (e && std::string(e) == "quad2") return 2;
-    if (e && std::string(e) == "grp") return 4;
-    if (e && std::string(e) == "grp2") return 5;
-    return 1;
-  }();
-  return v;
-}
-
-static int mv8_single_choice()
-{
-  static int v = [] {
-    const char *e = std::getenv("EIGMI_MV8_KERNEL1");
-    if (e && std::string(e) == "rows") return 0;
-    return 4;
-  }();
-  return v;
-}
-
 namespace {
 template <int EPI>
 void sell_mv8(const eig_mat_s &A, i64 m, const double *X, double *Y, const double *Bv, const double *dinv,
@@ -445,83 +329,40 @@ void sell_mv8(const eig_mat_s &A, i64 m, const double *X, double *Y, const doubl
 {
   EIG_CHECK(A.br == 1 && A.bc == 1, EIG_ERR_BLOCKSIZE,
             "matmul_sparse_tallskinny_blocked: only implemented for FieldMatrix<..,1,1>");
-  EIG_CHECK(A.R == 1, EIG_ERR_ARG, "multivector kernels need the R = 1 SELL image (unset EIGMI_SELL_R)");
   const int nblk = (int)(m / 8);
   const bool st = all_stencil(A);
-  // one column block: grouped quad (k_sell_mv8g, MB = 1); wider blocks: the configured mapping
-  // (quad default: at m = 32 it beats grp / grp2, tools/spmm_sweep.py)
-  const int kind = nblk == 1 ? mv8_single_choice() : mv8_kernel_choice();
-  if (kind == 4 || kind == 5)
+  if (nblk == 1)
   {
-    // grouped quad: MB = 1 (m = 8), 2 (grp2) or 4 (grp) column blocks per matrix pass
-    const int MBg = nblk == 1 ? 1 : (kind == 5 ? 2 : 4);
-    i64 gcap = (i64)A.ctx->num_cu * 4 / 2;
-    if (const char *e = std::getenv("EIGMI_MV8_GX")) gcap = std::max<i64>(8, std::atoll(e));
+    // one column block: grouped quad (k_sell_mv8g, MB = 1): 119 vs 131 us for the lane-per-row
+    // mapping on the 7-point SpMM at 128^3, 221 vs 241 us on the 15-point P1 mass matrix
+    const i64 gcap = (i64)A.ctx->num_cu * 4 / 2;
     const i64 nunits = (A.nslices + 3) / 4;
     const i64 gx = std::max<i64>(8, std::min<i64>(gcap, (nunits + 7) / 8 * 8) / 8 * 8);
     const i64 prow = A.bandwidth > 0 ? A.bandwidth : std::max<i64>(1, A.nb_rows);
     const i64 per = std::max<i64>(1, (prow + 8 * 256 - 1) / (8 * 256));
-    for (int b0 = 0; b0 < nblk; b0 += MBg)
-    {
-      const int nb = nblk - b0 < MBg ? nblk - b0 : MBg;
-#define EIGMI_GRP(MBV, STV)                                                                                      \
-  hipLaunchKernelGGL((k_sell_mv8g<MBV, 2, STV, EPI>), dim3((unsigned)gx), dim3(256), 0, s, A.nb_rows, A.nslices, \
-                     A.slice_ptr, A.val, A.col, A.st_delta, A.st_mask, X, Y, A.window, A.own_offset, b0, Bv, dinv, \
+#define EIGMI_GRP(STV)                                                                                         \
+  hipLaunchKernelGGL((k_sell_mv8g<1, 2, STV, EPI>), dim3((unsigned)gx), dim3(256), 0, s, A.nb_rows, A.nslices, \
+                     A.slice_ptr, A.val, A.col, A.st_delta, A.st_mask, X, Y, A.window, A.own_offset, 0, Bv, dinv, \
                      omega, gamma, per)
-#define EIGMI_GRP_NB(STV)             \
-  switch (nb)                         \
-  {                                   \
-    case 1: EIGMI_GRP(1, STV); break; \
-    case 2: EIGMI_GRP(2, STV); break; \
-    case 3: EIGMI_GRP(3, STV); break; \
-    default: EIGMI_GRP(4, STV); break; \
-  }
-      if (st)
-      {
-        EIGMI_GRP_NB(true)
-      }
-      else
-      {
-        EIGMI_GRP_NB(false)
-      }
-#undef EIGMI_GRP_NB
+    if (st) EIGMI_GRP(true);
+    else EIGMI_GRP(false);
 #undef EIGMI_GRP
-    }
-  }
-  else if (kind == 0)
-  {
-    constexpr int MB = 2;
-    const int gx = grid_cap(A.nslices, 4, kStreamBlocks);
-    for (int b0 = 0; b0 < nblk; b0 += MB)
-    {
-      const int nb = nblk - b0 < MB ? nblk - b0 : MB;
-      if (st)
-        hipLaunchKernelGGL((k_sell_mv8<MB, true, EPI>), dim3(gx), dim3(256), 0, s, A.nb_rows, A.nslices, A.slice_ptr,
-                           A.val, A.col, A.st_delta, A.st_mask, X, Y, A.window, A.own_offset, b0, nb, Bv, dinv, omega,
-                           gamma);
-      else
-        hipLaunchKernelGGL((k_sell_mv8<MB, false, EPI>), dim3(gx), dim3(256), 0, s, A.nb_rows, A.nslices,
-                           A.slice_ptr, A.val, A.col, A.st_delta, A.st_mask, X, Y, A.window, A.own_offset, b0, nb, Bv,
-                           dinv, omega, gamma);
-    }
   }
   else
   {
-    // quad: 4 column blocks (32 columns) per matrix pass (quad2: 2), 4 entries in flight, 2-wave
-    // workgroups; grid from the XCD-aware schedule (k_sell_mv8q)
-    const int MBq = kind == 2 ? 2 : 4;
+    // quad: 4 column blocks (32 columns) per matrix pass, 4 entries in flight, 2-wave workgroups;
+    // grid from the XCD-aware schedule (k_sell_mv8q)
+    constexpr int MBq = 4;
     constexpr int W = 2;
     const i64 nunits = A.nslices * (4 / W);
     const i64 rows_per_unit = 16 * W;
     // resident 2-wave workgroups at the kernel's occupancy (4 waves / SIMD for MB = 4, 8 for MB = 2),
     // a multiple of 8 (one share per XCD)
-    const i64 resident = (i64)A.ctx->num_cu * 4 * (kind == 2 ? 8 : 4) / W;
+    const i64 resident = (i64)A.ctx->num_cu * 4 * 4 / W;
     // half the resident capacity: the plane-slab working set (front + the previous and next
     // planes' segments) then fits the XCD's 4 MiB L2 better (tools/spmm_sweep.py: -10 % time on
     // the 7-point SpMM / Chebyshev step at 224^3, equal on the 15-point P1 mass)
-    i64 gcap = resident / 2;
-    if (const char *e = std::getenv("EIGMI_MV8_GX"))  // experiment knob: workgroups in flight
-      gcap = std::max<i64>(8, std::atoll(e));
+    const i64 gcap = resident / 2;
     const i64 gx = std::max<i64>(8, std::min<i64>(gcap, (nunits + 7) / 8 * 8) / 8 * 8);
     // plane segment: bandwidth rows / 8, in units (at least 1); no bandwidth (diagonal): 1/8 of all
     const i64 prow = A.bandwidth > 0 ? A.bandwidth : std::max<i64>(1, A.nb_rows);
@@ -562,8 +403,7 @@ int sell_mv8_launches(i64 m)
   // (the Chebyshev step the caller counts never takes the march)
   const int nblk = (int)(m / 8);
   if (nblk <= 1) return nblk;
-  const int kind = mv8_kernel_choice(), per = (kind == 1 || kind == 4) ? 4 : 2;
-  return (nblk + per - 1) / per;
+  return (nblk + 3) / 4;
 }
 
 void launch_sell_mv8(const eig_mat_s &A, i64 m, const double *X, double *Y, hipStream_t s)

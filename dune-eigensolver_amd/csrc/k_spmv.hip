@@ -50,40 +50,27 @@ __device__ __forceinline__ i32 lane_geti(const typename Vec<R>::i &v, int q)
   else return v[q];
 }
 
-// Chunk order is XCD-aware: workgroups are dealt round-robin over the 8 XCDs (MI355X_MICROARCH
-// "Workgroup dispatch"), so workgroup b takes logical chunk swz(b) and each XCD walks ONE
-// contiguous eighth of the slices -- the stencil's +-plane neighbours of a workgroup's rows are
-// then the current rows of workgroups on the same XCD (its L2) instead of another XCD's.
-// Bijective for any grid size (the first G % 8 groups hold one workgroup more).  OFF by default:
-// measured (tools/lanczos_sweep.py, 256^3) +12 us on the two-kernel K1 and +24 us on the 8-wave
-// fused kernel -- the 256 MB MALL already serves the plane re-reads; EIGMI_XCD_SWIZZLE=1 enables.
-__device__ __forceinline__ i64 swizzled_block(int swz)
+// XCD-aware work-item order for the plane marches: workgroups are dealt round-robin over the 8 XCDs
+// (MI355X_MICROARCH "Workgroup dispatch"), so workgroup b takes logical item swizzled_block(b) and
+// each XCD walks ONE contiguous eighth of the items -- a column's +-plane neighbours then sit in
+// the same XCD's L2.  Bijective for any grid size (the first G % 8 groups hold one workgroup more).
+// (The slice kernels take plain contiguous chunks: measured faster there -- the 256 MB MALL
+// already serves their plane re-reads.)
+__device__ __forceinline__ i64 swizzled_block()
 {
   const int G = gridDim.x, bid = blockIdx.x;
-  if (!swz || G < 16) return bid;
+  if (G < 16) return bid;
   const int q = G >> 3, r = G & 7, x = bid & 7, i = bid >> 3;
   return (i64)(x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
 }
 
-__device__ __forceinline__ void chunk_of(i64 count, i64 &b, i64 &e, int swz = 0)
+__device__ __forceinline__ void chunk_of(i64 count, i64 &b, i64 &e)
 {
   const i64 G = gridDim.x;
   const i64 per = (count + G - 1) / G;
-  b = swizzled_block(swz) * per;
+  b = (i64)blockIdx.x * per;
   e = b + per;
   if (e > count) e = count;
-}
-
-static int nt_store()
-{
-  const char *e = std::getenv("EIGMI_NT_STORE");
-  return (e && e[0] == '1') ? 1 : 0;
-}
-
-static int xcd_swizzle()
-{
-  const char *e = std::getenv("EIGMI_XCD_SWIZZLE");
-  return (e && e[0] == '1') ? 1 : 0;
 }
 
 // Gathered operand x[g]: a plain vector, or the fused Lanczos step's u_k = t_{k-1} - c u_{k-1}
@@ -329,17 +316,8 @@ struct SellB1 {
   const i32 *st_delta;
   const uint8_t *st_mask;
   i64 xlast;  // window length - 1 (gather clamp)
-  int swz;    // XCD-aware chunk order (chunk_of)
-  int nts;    // nontemporal stores of the step vectors (EIGMI_NT_STORE)
   SymImg sym;
 };
-
-// Store of a streamed result vector entry: nontemporal (no L2 allocation) when A.nts.
-__device__ __forceinline__ void put(double *p, double v, int nts)
-{
-  if (nts) __builtin_nontemporal_store(v, p);
-  else *p = v;
-}
 
 // Image modes: every slice explicit, every slice stencil, or mixed (per-slice wave-uniform branch);
 // kSym8 / kSym32: the symmetric band image with u8 / u32 row masks (R = 1 only); kSymN8 / kSymN32:
@@ -388,7 +366,7 @@ __device__ __forceinline__ void slice_dot(const SellB1 &A, i64 s, const X &x, i6
 
 static SellB1 sell_b1(const eig_mat_s &A)
 {
-  SellB1 b{A.slice_ptr, A.val, A.col, A.st_width, A.st_delta, A.st_mask, A.window - 1, xcd_swizzle(), nt_store(), {}};
+  SellB1 b{A.slice_ptr, A.val, A.col, A.st_width, A.st_delta, A.st_mask, A.window - 1, {}};
   if (A.sym_val)
   {
     b.sym.val = A.sym_val;
@@ -416,20 +394,18 @@ static SellB1 sell_b1(const eig_mat_s &A)
   return b;
 }
 
-// EIGMI_SYM=0 keeps the SELL image for the scalar kernels even when a symmetric band image exists.
-// (read at every launch, like the other EIGMI_* kernel switches, so one upload can be A/B'd)
-// EIGMI_SYM=1 keeps the band image but takes every offset through its own gather (no lane shifts).
-static int sym_kernels()
+// Band-image kernels on this matrix: 0 = none (the SELL / stencil kernels: EIG_MAT_NO_BAND), 1 =
+// every offset through its own gather (EIG_MAT_BAND_GATHER), 2 = the lane-shift path (default).
+static int sym_kernels(const eig_mat_s &A)
 {
-  const char *e = std::getenv("EIGMI_SYM");
-  return e && e[0] == '0' ? 0 : (e && e[0] == '1' ? 1 : 2);
+  return (A.kflags & EIG_MAT_NO_BAND) ? 0 : (A.kflags & EIG_MAT_BAND_GATHER) ? 1 : 2;
 }
 
 static bool is_sym_mode(int mode) { return mode >= kSym8; }
 
 static int image_mode(const eig_mat_s &A)
 {
-  const int sk = A.sym_val && A.R == 1 ? sym_kernels() : 0;
+  const int sk = A.sym_val ? sym_kernels(A) : 0;
   if (sk)
   {
     bool near = false;  // offsets +-1 present: the lane-shift path applies
@@ -458,7 +434,7 @@ __global__ __launch_bounds__(kStreamThreads, min_waves<MODE>()) void k_spmv_b1(i
   // wave index through readfirstlane: the slice loop, slice_ptr loads and row bases stay scalar
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   i64 b, e;
-  chunk_of(count, b, e, A.swz);
+  chunk_of(count, b, e);
   for (i64 it = b + wave; it < e; it += kWaves)
   {
     const i64 s = slices ? (i64)slices[first + it] : first + it;
@@ -544,7 +520,7 @@ __global__ __launch_bounds__(kStreamThreads, min_waves<MODE>()) void k_lanczos_s
   const double sig = 1.0 / beta;
   const double gam = (j > 0) ? beta * (1.0 / sqrt(nsum[j - 1])) : 0.0;
   i64 b, e;
-  chunk_of(count, b, e, A.swz);
+  chunk_of(count, b, e);
   double d = 0.0;
   for (i64 it = b + wave; it < e; it += kWaves)
   {
@@ -569,7 +545,7 @@ __global__ __launch_bounds__(kStreamThreads, min_waves<MODE>()) void k_lanczos_s
       {
         double ti = acc[q] * sig;
         if (j > 0) ti = ti - gam * upv[q];
-        put(t + own + r, ti, A.nts);
+        t[own + r] = ti;
         d += ti * uv[q];
       }
     }
@@ -828,7 +804,7 @@ __global__ __launch_bounds__(kStreamThreads, 8) void k_lanczos_fused_b1(
   const double c = fs.c, gam = fs.gam, sig = fs.sig, mu = fs.mu;
   const int k = fs.j;
   i64 b, e;
-  chunk_of(count, b, e, A.swz);
+  chunk_of(count, b, e);
   if (fs.act == kFusedRepair)
   {
     // this launch's rows: its slices (wave w of the chunk takes slice b + w, ...)
@@ -937,7 +913,6 @@ struct MarchPlan {
   i64 mrows;    // rows covered by the row mask (nslices * 64)
   int ncol;     // D / 64
   int nseg;     // plane runs per column
-  int wgs;      // y-line grouping stride (columns of the +N offset), 0 = consecutive columns
   // first entries of the far spans (-D, -1) and (+1, +D): offset (0 = empty span) and band array
   i32 dn, dq;
   const double *Un, *Uq;
@@ -945,14 +920,13 @@ struct MarchPlan {
 
 // The rows of this wave's work item, in plane order: epi(r, w, acc, centre) gets each row's sum
 // and its own operand x[w] (raw: a double, or the (t, u) pair of the fused step).
-// SPAN1 (VAR >= 2): each far span holds at most one offset (3-D 7-point, 2-D 5-point), so the
-// generic span loops are compiled out.
-// VAR 1: loads issued offset group by offset group (the far-negative span, then the far-positive
-// span after the near math); VAR 2: the first entry of both far spans is issued with the row's
-// streams, so a 7-point row waits once.  (Measured and dropped: prefetching the next plane's
-// streams, or its far-span operands, one iteration ahead -- both spill in the fused kernel and
-// gave nothing in the others.)
-template <class MT, int KC, int VAR, bool SPAN1, bool NT, class X, class EPI>
+// The first entry of both far spans is issued with the row's streams, so a 7-point row waits
+// once.  SPAN1: each far span holds at most one offset (3-D 7-point, 2-D 5-point), so the generic
+// span loops are compiled out.  (Measured and dropped: issuing the far spans offset group by
+// offset group after the near math; prefetching the next plane's streams, or its far-span
+// operands, one iteration ahead -- both spill in the fused kernel and gave nothing in the others;
+// y-line workgroup grouping with a barrier per plane; temporal result stores.)
+template <class MT, int KC, bool SPAN1, class X, class EPI>
 __device__ __forceinline__ void march_rows(const SellB1 &A, const MarchPlan &mp, i64 own, int lane, int wave,
                                            const X &x, EPI &epi)
 {
@@ -965,25 +939,9 @@ __device__ __forceinline__ void march_rows(const SellB1 &A, const MarchPlan &mp,
   const double *U1 = S.val + (i64)S.j1 * S.ld;
   const double *U0 = S.val + (i64)(S.j0 >= 0 ? S.j0 : 0) * S.ld;
   const MT *mask = static_cast<const MT *>(S.mask);
-  int col, seg;
-  if (mp.wgs)
-  {
-    // y-line groups: the workgroup's waves take columns c0, c0 + S, c0 + 2S, c0 + 3S (S = the +N
-    // offset in columns), so three of the four +-N neighbour pairs are the workgroup's own rows,
-    // kept in step by one barrier per plane (L1 / L2 hits instead of re-fetches)
-    const int L = (int)swizzled_block(1), per = mp.ncol / kWaves, S = mp.wgs;
-    seg = L / per;
-    if (seg >= mp.nseg) return;  // (whole workgroup)
-    const int blk = L % per;
-    col = (blk / S) * (kWaves * S) + blk % S + wave * S;
-  }
-  else
-  {
-    const int item = (int)swizzled_block(1) * kWaves + wave;
-    if (item >= mp.ncol * mp.nseg) return;
-    col = item % mp.ncol;
-    seg = item / mp.ncol;
-  }
+  const int item = (int)swizzled_block() * kWaves + wave;
+  if (item >= mp.ncol * mp.nseg) return;
+  const int col = item % mp.ncol, seg = item / mp.ncol;
   const int z0 = (int)(mp.zb + seg * mp.nplanes / mp.nseg), z1 = (int)(mp.zb + (seg + 1) * mp.nplanes / mp.nseg);
   auto cx = [&](int g) -> unsigned { return g < 0 ? 0u : (unsigned)(g > xl ? xl : g); };
   auto cv = [&](int g) -> unsigned { return g < 0 ? 0u : (unsigned)(g > ldl ? ldl : g); };
@@ -995,14 +953,11 @@ __device__ __forceinline__ void march_rows(const SellB1 &A, const MarchPlan &mp,
   };
   // streams read exactly once (the row mask, the 0 / +1 / +D band values): nontemporal loads keep
   // them from evicting the (t, u) / band lines the neighbouring columns re-read from L2
-  auto ld1 = [&](const double *p, unsigned i) { return NT ? __builtin_nontemporal_load(p + i) : p[i]; };
+  auto ld1 = [&](const double *p, unsigned i) { return __builtin_nontemporal_load(p + i); };
   auto load_stream = [&](int w, Stream &st) {
     const int r = w - own32;
     const unsigned wv = (unsigned)(w > ldl ? ldl : w);
-    if (NT)
-      st.m = r < mrows ? (unsigned)__builtin_nontemporal_load(mask + (unsigned)r) : 0u;
-    else
-      st.m = r < mrows ? (unsigned)mask[(unsigned)r] : 0u;
+    st.m = r < mrows ? (unsigned)__builtin_nontemporal_load(mask + (unsigned)r) : 0u;
     st.aD = ld1(UD, wv);
     st.pD = x.load(cx(w + D));
     st.a0 = S.j0 >= 0 ? ld1(U0, wv) : 0.0;
@@ -1027,30 +982,22 @@ __device__ __forceinline__ void march_rows(const SellB1 &A, const MarchPlan &mp,
     if (lane == 0) ae = U1[cv(w - 1)];
     double an = 0.0, aq = 0.0;
     raw xn, xq;
-    if (VAR >= 2)
+    if (mp.dn)
     {
-      if (mp.dn)
-      {
-        const unsigned g = cx(w + mp.dn);  // (negative offset: the mirrored slot at the gathered row)
-        an = mp.Un[g];
-        xn = x.load(g);
-      }
-      if (mp.dq)
-      {
-        aq = mp.Uq[wv];
-        xq = x.load(cx(w + mp.dq));
-      }
+      const unsigned g = cx(w + mp.dn);  // (negative offset: the mirrored slot at the gathered row)
+      an = mp.Un[g];
+      xn = x.load(g);
+    }
+    if (mp.dq)
+    {
+      aq = mp.Uq[wv];
+      xq = x.load(cx(w + mp.dq));
     }
     const unsigned m = cur.m;
     double acc = 0.0;
     if (m & 1u) acc += amD * pmv;
-    if (VAR >= 2)
-    {
-      if (mp.dn && ((m >> kn0) & 1u)) acc += an * x.val(xn);
-      if (!SPAN1) sym_span<KC>(S, kn0 + 1, kn1, m, w, wv, x, xl, acc);
-    }
-    else
-      sym_span<KC>(S, kn0, kn1, m, w, wv, x, xl, acc);
+    if (mp.dn && ((m >> kn0) & 1u)) acc += an * x.val(xn);
+    if (!SPAN1) sym_span<KC>(S, kn0 + 1, kn1, m, w, wv, x, xl, acc);
     // neighbours' operand VALUES shifted across lanes (x.val per lane, then moved: the same bits
     // as evaluating x.val on the shifted raw operand, at half the registers for pairs)
     const double vc = x.val(pcur);
@@ -1070,42 +1017,32 @@ __device__ __forceinline__ void march_rows(const SellB1 &A, const MarchPlan &mp,
     if (S.km1 >= 0 && ((m >> S.km1) & 1u)) acc += am * vl;
     if (S.k0 >= 0 && ((m >> S.k0) & 1u)) acc += cur.a0 * vc;
     if (S.kp1 >= 0 && ((m >> S.kp1) & 1u)) acc += cur.ap * vr;
-    if (VAR >= 2)
-    {
-      if (mp.dq && ((m >> kp0) & 1u)) acc += aq * x.val(xq);
-      if (!SPAN1) sym_span<KC>(S, kp0 + 1, kp1, m, w, wv, x, xl, acc);
-    }
-    else
-      sym_span<KC>(S, kp0, kp1, m, w, wv, x, xl, acc);
+    if (mp.dq && ((m >> kp0) & 1u)) acc += aq * x.val(xq);
+    if (!SPAN1) sym_span<KC>(S, kp0 + 1, kp1, m, w, wv, x, xl, acc);
     if ((m >> kp1) & 1u) acc += cur.aD * x.val(cur.pD);
     epi(r, w, acc, pcur);
     pmv = vc;
     pcur = cur.pD;
     amD = cur.aD;
-    if (mp.wgs) __syncthreads();
   }
 }
 
 // y[own + r] = (A x)[r] on the plane march (BCRSMatrix::mv; bitwise k_spmv_b1).
-template <class MT, int VAR>
+template <class MT, bool SPAN1>
 __global__ __launch_bounds__(kStreamThreads, 8) void k_spmv_march(i64 nrows, i64 own, SellB1 A, MarchPlan mp,
                                                                   const double *__restrict__ x,
                                                                   double *__restrict__ y)
 {
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   auto epi = [&](int r, int w, double acc, double) {
-    if (r < nrows)
-    {
-      if ((VAR & 8) != 0) __builtin_nontemporal_store(acc, y + (unsigned)w);
-      else y[(unsigned)w] = acc;
-    }
+    if (r < nrows) __builtin_nontemporal_store(acc, y + (unsigned)w);
   };
-  march_rows<MT, 2, (VAR & 3), ((VAR & 4) != 0), ((VAR & 8) != 0)>(A, mp, own, lane, wave, XPlain{x}, epi);
+  march_rows<MT, 2, SPAN1>(A, mp, own, lane, wave, XPlain{x}, epi);
 }
 
 // Classic Lanczos kernel 1 on the plane march (same per-row arithmetic as k_lanczos_spmv_b1; the
 // row's own u_j is the march's centre operand).
-template <class MT, int VAR>
+template <class MT, bool SPAN1>
 __global__ __launch_bounds__(kStreamThreads, 8) void k_lanczos_spmv_march(
     i64 nrows, i64 own, SellB1 A, MarchPlan mp, const double *__restrict__ u, const double *__restrict__ up,
     double *__restrict__ t, int j, const double *__restrict__ nsum, double *__restrict__ dot_out,
@@ -1122,11 +1059,11 @@ __global__ __launch_bounds__(kStreamThreads, 8) void k_lanczos_spmv_march(
     {
       double ti = acc * sig;
       if (j > 0) ti = ti - gam * up[(unsigned)w];
-      put(t + (unsigned)w, ti, A.nts | ((VAR & 8) != 0));
+      __builtin_nontemporal_store(ti, t + (unsigned)w);
       d += ti * uv;
     }
   };
-  march_rows<MT, 2, (VAR & 3), ((VAR & 4) != 0), ((VAR & 8) != 0)>(A, mp, own, lane, wave, XPlain{u}, epi);
+  march_rows<MT, 2, SPAN1>(A, mp, own, lane, wave, XPlain{u}, epi);
   double v[1] = {d};
   if (grid_sum<1, kStreamThreads>(v, partials, ticket, tot))
   {
@@ -1139,9 +1076,10 @@ __global__ __launch_bounds__(kStreamThreads, 8) void k_lanczos_spmv_march(
 }
 
 // Fused one-reduction step on the plane march (per-row arithmetic of k_lanczos_fused_b1).  A repair
-// launch (fused_begin) takes the rows of the planes this launch marches.
-template <class MT, int VAR>
-__global__ __launch_bounds__(kStreamThreads, ((VAR & 32) ? 7 : 8)) void k_lanczos_fused_march(
+// launch (fused_begin) takes the rows of the planes this launch marches.  Built for 7 waves / SIMD
+// (72 VGPRs; at 8 the pair operands spill: -5 %).
+template <class MT, bool SPAN1>
+__global__ __launch_bounds__(kStreamThreads, 7) void k_lanczos_fused_march(
     i64 nrows, i64 own, SellB1 A, MarchPlan mp, const dpair *__restrict__ P, dpair *__restrict__ Pout, FusedArgs fa,
     double *__restrict__ out, double *partials, unsigned *ticket)
 {
@@ -1169,14 +1107,13 @@ __global__ __launch_bounds__(kStreamThreads, ((VAR & 32) ? 7 : 8)) void k_lanczo
         const double uk = pc.x - c * pc.y;
         double ti = (acc - mu * uk) * sig;
         if (k > 0) ti = ti - gam * pc.y;
-        if ((VAR & 8) != 0) __builtin_nontemporal_store(dpair{ti, uk}, Pout + (unsigned)w);
-        else Pout[(unsigned)w] = dpair{ti, uk};
+        __builtin_nontemporal_store(dpair{ti, uk}, Pout + (unsigned)w);
         d += ti * uk;
         q2 += ti * ti;
         m2 += uk * uk;
       }
     };
-    march_rows<MT, 2, (VAR & 3), ((VAR & 4) != 0), ((VAR & 8) != 0)>(A, mp, own, lane, wave, XPair{P, c}, epi);
+    march_rows<MT, 2, SPAN1>(A, mp, own, lane, wave, XPair{P, c}, epi);
   }
   double v[3] = {d, q2, m2};
   if (grid_sum<3, kStreamThreads>(v, partials, ticket, tot))
@@ -1204,16 +1141,15 @@ __device__ __forceinline__ double lane_from(double v, int src_lane)
   return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
-// NBW column blocks per workgroup (1, 2, 4): the workgroup's waves take the same rows for NBW
-// blocks (block blockIdx.y * NBW + wave % NBW), so the band values and masks they stream are read
-// from HBM once per NBW blocks (the other waves' loads hit L1 / L2).
-template <class MT, int NBW>
+// One column block per workgroup (blockIdx.y): sharing the band stream between 2 / 4 blocks measured
+// equal / 6 % slower (m = 32 at 256^3) -- the vector streams bound the launch.
+template <class MT>
 __global__ __launch_bounds__(kStreamThreads, 8) void k_spmm8_march(i64 nrows, i64 own, i64 ld, SellB1 A,
                                                                    MarchPlan mp, const double *__restrict__ X,
                                                                    double *__restrict__ Y)
 {
-  const int lane = threadIdx.x & 63, wv_ = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wave = wv_ / NBW, qb = (int)blockIdx.y * NBW + wv_ % NBW;  // (row column, column block)
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int qb = (int)blockIdx.y;  // column block
   const int rq = lane >> 2, cp = lane & 3;
   const SymImg &S = A.sym;
   const int xl = (int)A.xlast, D = (int)mp.D, ldl = (int)(S.ld - 1), own32 = (int)own, mrows = (int)mp.mrows;
@@ -1222,7 +1158,7 @@ __global__ __launch_bounds__(kStreamThreads, 8) void k_spmm8_march(i64 nrows, i6
   const double *U1 = S.val + (i64)S.j1 * S.ld;
   const double *U0 = S.val + (i64)(S.j0 >= 0 ? S.j0 : 0) * S.ld;
   const MT *mask = static_cast<const MT *>(S.mask);
-  const int item = (int)swizzled_block(1) * (kWaves / NBW) + wave;
+  const int item = (int)swizzled_block() * kWaves + wave;
   if (item >= mp.ncol * mp.nseg) return;
   const int col = item % mp.ncol, seg = item / mp.ncol;
   const int z0 = (int)(mp.zb + seg * mp.nplanes / mp.nseg), z1 = (int)(mp.zb + (seg + 1) * mp.nplanes / mp.nseg);
@@ -1365,7 +1301,10 @@ __global__ __launch_bounds__(kStreamThreads, 6) void k_spmm8_marchg(
   const double *U1 = S.val + (i64)S.j1 * S.ld;
   const double *U0 = S.val + (i64)(S.j0 >= 0 ? S.j0 : 0) * S.ld;
   const MT *mask = static_cast<const MT *>(S.mask);
-  const int item = (int)swizzled_block(1) * kWaves + wave;
+  // (Measured and dropped at 256^3, m = 32: the workgroup's 4 waves on the 4 column blocks of one
+  // item, so the band values / mask / D^-1 are fetched once per 4 blocks -- 6.62 vs 6.73 ms, with
+  // any number of plane runs per column; rocprof: L2 misses on the gathered X rows dominate.)
+  const int item = (int)swizzled_block() * kWaves + wave;
   if (item >= mp.ncol * mp.nseg) return;
   const int col = item % mp.ncol, seg = item / mp.ncol;
   const int z0 = (int)(mp.zb + seg * mp.nplanes / mp.nseg), z1 = (int)(mp.zb + (seg + 1) * mp.nplanes / mp.nseg);
@@ -1456,125 +1395,6 @@ __global__ void k_fused_tail(double *nsum, double *beta, const double *fred, con
     beta[0] = sqrt(nsum[0]);
 }
 
-// ---------------------------------------------------------------------------------------------
-// Software-pipelined Lanczos kernel 1 for all-stencil images, one row per lane (R = 1).  Per
-// slice iteration the wave issues, in this order: (1) the x gathers of the current slice (their
-// addresses need only the scalar offsets), (2) the value / mask / epilogue loads of the NEXT
-// slice, (3) the arithmetic of the current slice, which waits only for (1) -- vmcnt retires in
-// issue order, so (2) stays in flight behind the computation.  Same per-row arithmetic and
-// order as k_lanczos_spmv_b1 (bitwise identical results).
-// ---------------------------------------------------------------------------------------------
-struct StSlice {
-  double a[8];
-  unsigned m;
-  double upv, uv;
-};
-
-__device__ __forceinline__ void st_load(const SellB1 &A, i64 s, int w, int lane, i64 own, i64 nrows, int j,
-                                        const double *__restrict__ u, const double *__restrict__ up, StSlice &L)
-{
-  const double *vs = A.val + A.slice_ptr[s];  // wave-uniform base, 32-bit lane offsets
-#pragma unroll
-  for (int k = 0; k < 8; ++k) L.a[k] = (k < w) ? __builtin_nontemporal_load(vs + (k * 64 + lane)) : 0.0;
-  L.m = A.st_mask[s * 64 + lane];
-  const i64 r = s * 64 + lane;
-  const bool ok = r < nrows;
-  L.upv = (ok && j > 0) ? up[own + r] : 0.0;
-  L.uv = ok ? u[own + r] : 0.0;
-}
-
-template <int MINW>
-__global__ __launch_bounds__(kStreamThreads, MINW) void k_lanczos_spmv_st1_pipe(
-    i64 nrows, i64 own, SellB1 A, const i32 *__restrict__ slices, i64 first, i64 count,
-    const double *__restrict__ u, const double *__restrict__ up, double *__restrict__ t, int j,
-    const double *__restrict__ nsum, double *__restrict__ dot_out, double *__restrict__ beta_out,
-    const double *__restrict__ carry, double *partials, unsigned *ticket)
-{
-  __shared__ double tot[1];
-  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const double beta = sqrt(nsum[j]);
-  const double sig = 1.0 / beta;
-  const double gam = (j > 0) ? beta * (1.0 / sqrt(nsum[j - 1])) : 0.0;
-  i64 b, e;
-  chunk_of(count, b, e, A.swz);
-  double d = 0.0;
-  i64 it = b + wave;
-  StSlice cur;
-  i64 s = 0;
-  int w = 0;
-  if (it < e)
-  {
-    s = slices ? (i64)slices[first + it] : first + it;
-    w = A.st_width[s];
-    st_load(A, s, w, lane, own, nrows, j, u, up, cur);
-  }
-  for (; it < e; it += kWaves)
-  {
-    // (1) gathers of the current slice (32-bit window offsets: the window is < 2^31 entries)
-    const i32 *dl = A.st_delta + 8 * s;
-    const int xr = (int)(own + s * 64) + lane;
-    const int xl = (int)A.xlast;
-    double xv[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-    {
-      if (k < w)
-      {
-        int g = xr + dl[k];
-        g = g < 0 ? 0 : (g > xl ? xl : g);
-        xv[k] = u[g];
-      }
-      else
-        xv[k] = 0.0;
-    }
-    // (2) next slice's streams
-    const i64 itn = it + kWaves;
-    StSlice nxt;
-    i64 sn = s;
-    int wn = 0;
-    if (itn < e)
-    {
-      sn = slices ? (i64)slices[first + itn] : first + itn;
-      wn = A.st_width[sn];
-      st_load(A, sn, wn, lane, own, nrows, j, u, up, nxt);
-    }
-    // (3) current slice arithmetic (ascending offsets = ascending columns)
-    double acc = 0.0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-      if (k < w && ((cur.m >> k) & 1u)) acc += cur.a[k] * xv[k];
-    const i64 r = s * 64 + lane;
-    if (r < nrows)
-    {
-      double ti = acc * sig;
-      if (j > 0) ti = ti - gam * cur.upv;
-      t[own + r] = ti;
-      d += ti * cur.uv;
-    }
-    cur = nxt;
-    s = sn;
-    w = wn;
-  }
-  double v[1] = {d};
-  if (grid_sum<1, kStreamThreads>(v, partials, ticket, tot))
-  {
-    if (threadIdx.x == 0)
-    {
-      dot_out[0] = carry ? (carry[0] + tot[0]) : tot[0];
-      if (beta_out) beta_out[0] = beta;
-    }
-  }
-}
-
-// EIGMI_K1_PIPE: 0 = plain kernel (default: measured equal to 1 and faster than 2, see
-// tools/spmv_sweep.py), 1 = pipelined at 7 waves / SIMD, 2 = pipelined at 8 (spills)
-static int k1_pipe_mode()
-{
-  const char *e = std::getenv("EIGMI_K1_PIPE");
-  if (!e) return 0;
-  return e[0] == '0' ? 0 : (e[0] == '2' ? 2 : 1);
-}
-
 // Grid = min(work, resident workgroups): every workgroup takes one contiguous chunk, so a grid
 // larger than what the CUs hold at once would leave a tail of late chunks.
 template <class K>
@@ -1595,30 +1415,8 @@ static int grid_for_slices(K kernel, i64 count, int num_cu)
   return (int)(need < cap ? need : cap);
 }
 
-// EIGMI_MARCH=0 disables the plane-marching kernels; 1 / 2 / 3 pick the load schedule (march_rows
-// VAR; default 2).
-// Default 2 (measured, tools/lanczos_sweep.py).
-static int march_variant(bool = false)
-{
-  const char *e = std::getenv("EIGMI_MARCH");
-  if (!e) return 2;
-  return (e[0] >= '0' && e[0] <= '2') ? e[0] - '0' : 2;
-}
-static bool march_enabled() { return march_variant() != 0; }
-// The fused march is compiled for 7 waves / SIMD (72 VGPRs; at 8 its pair operands spill): -5 %
-// (EIGMI_MARCH_W7=0: the 8-wave build, A/B).
-static int march_w7()
-{
-  const char *e = std::getenv("EIGMI_MARCH_W7");
-  return (e && e[0] == '0') ? 0 : 1;
-}
-// Nontemporal loads for the once-read streams of the march and nontemporal result stores (default;
-// EIGMI_MARCH_NT=0 turns them off): fused step -4 %, K1 -3 %, SpMV -14 % (tools/lanczos_sweep.py).
-static int march_nt()
-{
-  const char *e = std::getenv("EIGMI_MARCH_NT");
-  return (e && e[0] == '0') ? 0 : 1;
-}
+// EIG_MAT_NO_MARCH: the plane-marching kernels are off for this matrix (the slice kernels run).
+static bool march_enabled(const eig_mat_s &A) { return (A.kflags & EIG_MAT_NO_MARCH) == 0; }
 // Far spans of at most one offset each (u8-mask bands only: at most 8 offsets, so (-D, -1) and
 // (+1, +D) hold at most one offset each exactly when nd <= 7 with -1/0/+1 present).
 static bool march_span1(const eig_mat_s &A)
@@ -1632,45 +1430,27 @@ static bool march_span1(const eig_mat_s &A)
   return A.sym_mask_bytes == 1 && klo - 1 <= 1 && (A.sym_nd - 1) - khi <= 1;
 }
 
-// Launch a march kernel template KERN<MT, VAR> for the image's mask width and the selected VAR.
-#define EIG_MARCH_LAUNCH(KERN, FUSED, MODE, G, ...)                                                           \
-  do {                                                                                                        \
-    const int v0_ = march_variant(FUSED);                                                                     \
-    const int v_ = v0_ + (march_span1(A) && v0_ >= 2 ? 4 : 0) + 8 * march_nt() + ((FUSED) ? 32 * march_w7() : 0); \
-    if ((MODE) == kSymN8)                                                                                     \
-    {                                                                                                         \
-      if (v_ == 1) hipLaunchKernelGGL((KERN<uint8_t, 1>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);     \
-      else if (v_ == 9) hipLaunchKernelGGL((KERN<uint8_t, 9>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);\
-      else if (v_ == 41) hipLaunchKernelGGL((KERN<uint8_t, 41>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);\
-      else if (v_ == 6) hipLaunchKernelGGL((KERN<uint8_t, 6>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);\
-      else if (v_ == 14) hipLaunchKernelGGL((KERN<uint8_t, 14>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);\
-      else if (v_ == 46) hipLaunchKernelGGL((KERN<uint8_t, 46>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);\
-      else if (v_ == 10) hipLaunchKernelGGL((KERN<uint8_t, 10>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);\
-      else if (v_ == 42) hipLaunchKernelGGL((KERN<uint8_t, 42>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);\
-      else if (v_ == 38) hipLaunchKernelGGL((KERN<uint8_t, 38>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);\
-      else hipLaunchKernelGGL((KERN<uint8_t, 2>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);             \
-    }                                                                                                         \
-    else                                                                                                      \
-    {                                                                                                         \
-      if (v_ == 1) hipLaunchKernelGGL((KERN<uint32_t, 1>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);    \
-      else if (v_ == 9) hipLaunchKernelGGL((KERN<uint32_t, 9>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);\
-      else if (v_ == 41) hipLaunchKernelGGL((KERN<uint32_t, 41>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);\
-      else if (v_ == 10) hipLaunchKernelGGL((KERN<uint32_t, 10>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);\
-      else if (v_ == 42) hipLaunchKernelGGL((KERN<uint32_t, 42>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);\
-      else if (v_ == 34) hipLaunchKernelGGL((KERN<uint32_t, 34>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);\
-      else hipLaunchKernelGGL((KERN<uint32_t, 2>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);            \
-    }                                                                                                         \
+// Launch a march kernel template KERN<MT, SPAN1> for the image's mask width (u8 masks only can
+// have single-offset far spans).
+#define EIG_MARCH_LAUNCH(KERN, MODE, G, ...)                                                               \
+  do {                                                                                                    \
+    if ((MODE) == kSymN8 && march_span1(A))                                                               \
+      hipLaunchKernelGGL((KERN<uint8_t, true>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);           \
+    else if ((MODE) == kSymN8)                                                                            \
+      hipLaunchKernelGGL((KERN<uint8_t, false>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);          \
+    else                                                                                                  \
+      hipLaunchKernelGGL((KERN<uint32_t, false>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);         \
   } while (0)
 
 // Plane-marching plan for a whole-matrix launch on the lane-shift band image, or nseg = 0 when the
 // band does not qualify: symmetric offset set with off[0] = -D, off[nd-1] = +D, D a multiple of 64,
 // at least 4 planes.  Plane runs per column: enough items for one resident wave per SIMD slot
 // (8 per SIMD), at most kMaxRedBlocks workgroups.
-// Band geometry the march needs (independent of the EIGMI_* switches): widest offset D.
+// Band geometry the march needs (independent of the matrix's kernel flags): widest offset D.
 bool march_geometry(const eig_mat_s &A, i64 &D, int chunk)
 {
   D = 0;
-  if (!A.sym_val || A.R != 1 || A.sym_nd < 3) return false;
+  if (!A.sym_val || A.sym_nd < 3) return false;
   bool near = false;
   for (int k = 0; k < A.sym_nd; ++k) near = near || A.sym_off[k] == 1 || A.sym_off[k] == -1;
   D = A.sym_off[A.sym_nd - 1];
@@ -1683,10 +1463,10 @@ bool march_geometry(const eig_mat_s &A, i64 &D, int chunk)
 static MarchPlan march_plan(const eig_mat_s &A, int mode, i64 zb = 0, i64 ze = -1, bool fused = false,
                             int chunk = 64)
 {
-  MarchPlan mp{0, 0, 0, 0, 0, 0, 0, 0, 0, nullptr, nullptr};
+  MarchPlan mp{};
   if (mode != kSymN8 && mode != kSymN32) return mp;
   i64 D;
-  if (!march_enabled() || !march_geometry(A, D, chunk)) return mp;
+  if (!march_enabled(A) || !march_geometry(A, D, chunk)) return mp;
   if (ze < 0) ze = (A.nb_rows + D - 1) / D;
   const i64 nplanes = ze - zb;
   if (nplanes < 2 || (zb == 0 && nplanes < 4)) return mp;
@@ -1698,8 +1478,6 @@ static MarchPlan march_plan(const eig_mat_s &A, int mode, i64 zb = 0, i64 ze = -
   // the slab of one rank in a strong-scaling run: runs of >= 15 planes beat full occupancy
   // (256 x 256 x 32 box: 2 runs 33.4 us vs 8 runs 37.8 us; at 256^3 the rule keeps 8 runs)
   if (fused && ncol >= 1024) nseg = std::max<i64>(1, std::min<i64>(nseg, nplanes / 15));
-  if (const char *e = std::getenv("EIGMI_MARCH_SEG"))  // (A/B: plane runs per column)
-    if (std::atoi(e) > 0) nseg = std::min<i64>(std::atoi(e), nplanes);
   while (nseg > 1 && (ncol * nseg + kWaves - 1) / kWaves > kMaxRedBlocks) --nseg;
   if ((ncol * nseg + kWaves - 1) / kWaves > kMaxRedBlocks) return mp;
   mp.D = D;
@@ -1714,13 +1492,6 @@ static MarchPlan march_plan(const eig_mat_s &A, int mode, i64 zb = 0, i64 ze = -
   mp.dq = khi < A.sym_nd - 1 ? A.sym_off[khi] : 0;
   mp.Uq = A.sym_val + (i64)(khi < A.sym_nd - 1 ? A.sym_dj[khi] : 0) * A.sym_ld;
   mp.zb = zb;
-  {
-    // y-line grouping (EIGMI_MARCH_WG=1): the +N offset a multiple of 64 and the columns a whole
-    // number of 4-line groups
-    const char *e = std::getenv("EIGMI_MARCH_WG");
-    const i64 S = mp.dq > 0 && mp.dq % chunk == 0 ? mp.dq / chunk : 0;
-    mp.wgs = (e && e[0] == '1' && S > 0 && ncol % (kWaves * S) == 0) ? (int)S : 0;
-  }
   mp.nplanes = nplanes;
   mp.mrows = A.nslices * 64;
   mp.ncol = (int)ncol;
@@ -1747,7 +1518,7 @@ static MarchPlan launch_plan(const eig_mat_s &A, int mode, const i32 *slices, i6
     return mp;
   }
   if (!slices && first == 0 && count == A.nslices) return march_plan(A, mode, 0, -1, fused);
-  return MarchPlan{0, 0, 0, 0, 0, 0, 0, 0, 0, nullptr, nullptr};
+  return MarchPlan{};
 }
 
 void launch_spmv(const eig_mat_s &A, const double *x, double *y, const i32 *slices, i64 first, i64 count,
@@ -1763,7 +1534,7 @@ void launch_spmv(const eig_mat_s &A, const double *x, double *y, const i32 *slic
     if (mp.nseg > 0)
     {
       const unsigned G = (unsigned)((mp.ncol * (i64)mp.nseg + kWaves - 1) / kWaves);
-      EIG_MARCH_LAUNCH(k_spmv_march, false, mode, G, s, A.nb_rows, A.own_offset, sell_b1(A), mp, x, y);
+      EIG_MARCH_LAUNCH(k_spmv_march, mode, G, s, A.nb_rows, A.own_offset, sell_b1(A), mp, x, y);
       return;
     }
   }
@@ -1794,14 +1565,11 @@ void launch_spmv(const eig_mat_s &A, const double *x, double *y, const i32 *slic
   }
   if (A.br == 1 && A.bc == 1)
   {
-    if (A.R == 1) EIG_B1M(1)
-    else if (A.R == 2) EIG_B1M(2)
-    else EIG_B1M(4)
+    EIG_B1M(1)
     return;
   }
 #undef EIG_B1M
 #undef EIG_B1
-  EIG_CHECK(A.R == 1, EIG_ERR_ARG, "block matrices use 64-row slices");
   EIG_BLK(1, 2) EIG_BLK(1, 3) EIG_BLK(1, 4)
   EIG_BLK(2, 1) EIG_BLK(2, 2) EIG_BLK(2, 3) EIG_BLK(2, 4)
   EIG_BLK(3, 1) EIG_BLK(3, 2) EIG_BLK(3, 3) EIG_BLK(3, 4)
@@ -1822,7 +1590,7 @@ void launch_lanczos_spmv(const eig_mat_s &A, const double *u, const double *up, 
     if (mp.nseg > 0)
     {
       const unsigned G = (unsigned)((mp.ncol * (i64)mp.nseg + kWaves - 1) / kWaves);
-      EIG_MARCH_LAUNCH(k_lanczos_spmv_march, false, mode, G, s, A.nb_rows, A.own_offset, sell_b1(A), mp, u, up, t, j,
+      EIG_MARCH_LAUNCH(k_lanczos_spmv_march, mode, G, s, A.nb_rows, A.own_offset, sell_b1(A), mp, u, up, t, j,
                        st.nsum, dot_out, beta_out, red.partials, red.ticket(ticket));
       return;
     }
@@ -1843,20 +1611,9 @@ void launch_lanczos_spmv(const eig_mat_s &A, const double *u, const double *up, 
     else if (m_ == kSymN32) EIG_LZ(R_, kSymN32);                                                               \
     else EIG_LZ(R_, kMixed);                                                                                 \
   }
-  const int pm = k1_pipe_mode();
-#define EIG_PIPE(W_)                                                                                            \
-  hipLaunchKernelGGL(k_lanczos_spmv_st1_pipe<W_>,                                                              \
-                     dim3(grid_for_slices(k_lanczos_spmv_st1_pipe<W_>, count, A.ctx->num_cu)), dim3(kStreamThreads), \
-                     0, s, A.nb_rows, A.own_offset, sell_b1(A), slices, first, count, u, up, t, j, st.nsum, dot_out, \
-                     beta_out, carry, red.partials, red.ticket(ticket))
-  if (A.R == 1 && image_mode(A) == kStencil && pm == 1) EIG_PIPE(7);
-  else if (A.R == 1 && image_mode(A) == kStencil && pm == 2) EIG_PIPE(8);
-  else if (A.R == 1) EIG_LZM(1)
-  else if (A.R == 2) EIG_LZM(2)
-  else EIG_LZM(4)
+  EIG_LZM(1)
 #undef EIG_LZM
 #undef EIG_LZ
-#undef EIG_PIPE
 }
 
 void launch_lanczos_fused(const eig_mat_s &A, const double *P, double *Pout, const FusedLaunch &fl,
@@ -1872,7 +1629,7 @@ void launch_lanczos_fused(const eig_mat_s &A, const double *P, double *Pout, con
     if (mp.nseg > 0)
     {
       const unsigned G = (unsigned)((mp.ncol * (i64)mp.nseg + kWaves - 1) / kWaves);
-      EIG_MARCH_LAUNCH(k_lanczos_fused_march, true, mode, G, s, A.nb_rows, A.own_offset, sell_b1(A), mp,
+      EIG_MARCH_LAUNCH(k_lanczos_fused_march, mode, G, s, A.nb_rows, A.own_offset, sell_b1(A), mp,
                        reinterpret_cast<const dpair *>(P), reinterpret_cast<dpair *>(Pout), fa, out, red.partials,
                        red.ticket(ticket));
       return;
@@ -1895,9 +1652,7 @@ void launch_lanczos_fused(const eig_mat_s &A, const double *P, double *Pout, con
     else if (m_ == kSymN32) EIG_LF(R_, kSymN32);                                                              \
     else EIG_LF(R_, kMixed);                                                                                  \
   }
-  if (A.R == 1) EIG_LFM(1)
-  else if (A.R == 2) EIG_LFM(2)
-  else EIG_LFM(4)
+  EIG_LFM(1)
 #undef EIG_LFM
 #undef EIG_LF
 }
@@ -1911,7 +1666,7 @@ void launch_fused_tail(const LanczosState &st, int L, hipStream_t s)
 // +-1 stored, every span at most kGSpan offsets.  False when the band does not qualify.
 static bool gspans(const eig_mat_s &A, i64 &P, GSpans &sp)
 {
-  if (!A.sym_val || A.R != 1 || A.sym_nd < 3) return false;
+  if (!A.sym_val || A.sym_nd < 3) return false;
   const int nd = A.sym_nd;
   auto kof = [&](i64 d) {
     for (int k = 0; k < nd; ++k)
@@ -1946,18 +1701,14 @@ static bool gspans(const eig_mat_s &A, i64 &P, GSpans &sp)
   return false;
 }
 
-// EIGMI_MARCHG=0 disables the general-band march (SpMM of non-extreme carried bands, Chebyshev).
-static bool marchg_enabled()
-{
-  const char *e = std::getenv("EIGMI_MARCHG");
-  return march_enabled() && !(e && e[0] == '0');
-}
+// The general-band march (SpMM of non-extreme carried bands, Chebyshev) is a plane march too.
+static bool marchg_enabled(const eig_mat_s &A) { return march_enabled(A); }
 
 template <int EPI>
 static bool launch_marchg(const eig_mat_s &A, i64 m, const double *X, double *Y, const double *Bv,
                           const double *dinv, double omega, double gamma, hipStream_t s)
 {
-  if (A.br != 1 || A.bc != 1 || m <= 0 || !marchg_enabled()) return false;
+  if (A.br != 1 || A.bc != 1 || m <= 0 || !marchg_enabled(A)) return false;
   const int mode = image_mode(A);
   if (mode != kSymN8 && mode != kSymN32) return false;
   i64 P;
@@ -1968,9 +1719,7 @@ static bool launch_marchg(const eig_mat_s &A, i64 m, const double *X, double *Y,
   const i64 ncol = P / 16;
   const i64 resident = 6LL * 4 * A.ctx->num_cu;  // waves at the kernel's 6 waves / SIMD
   i64 nseg = std::min<i64>(std::max<i64>(1, (resident + ncol - 1) / ncol), nplanes);
-  if (const char *e = std::getenv("EIGMI_MARCH_SEG"))
-    if (std::atoi(e) > 0) nseg = std::min<i64>(std::atoi(e), nplanes);
-  MarchPlan mp{0, 0, 0, 0, 0, 0, 0, 0, 0, nullptr, nullptr};
+  MarchPlan mp{};
   mp.D = P;
   mp.zb = 0;
   mp.nplanes = nplanes;
@@ -1999,33 +1748,14 @@ bool launch_spmm_march(const eig_mat_s &A, i64 m, const double *X, double *Y, hi
   const int mode = image_mode(A);
   const MarchPlan mp = march_plan(A, mode, 0, -1, false, 16);
   if (mp.nseg == 0) return launch_marchg<kGStore>(A, m, X, Y, nullptr, nullptr, 0.0, 0.0, s);
-  const i64 nblk = m / 8;
-  // one column block per workgroup: sharing the band stream between 2 / 4 blocks measured equal /
-  // 6 % slower (m = 32 at 256^3: 2716 / 2720 / 2894 us) -- the vector streams bound the launch
-  int nbw = 1;
-  if (const char *e = std::getenv("EIGMI_SPMM_NBW"))  // (A/B: column blocks per workgroup)
-  {
-    const int v = std::atoi(e);
-    if ((v == 1 || v == 2 || v == 4) && nblk % v == 0) nbw = v;
-  }
-  const i64 items = mp.ncol * (i64)mp.nseg, per = kWaves / nbw;
-  const dim3 grid((unsigned)((items + per - 1) / per), (unsigned)(nblk / nbw));
-#define EIG_SPMM(MT_, NB_)                                                                                      \
-  hipLaunchKernelGGL((k_spmm8_march<MT_, NB_>), grid, dim3(kStreamThreads), 0, s, A.nb_rows, A.own_offset, A.window, \
-                     sell_b1(A), mp, X, Y)
+  const i64 items = mp.ncol * (i64)mp.nseg;
+  const dim3 grid((unsigned)((items + kWaves - 1) / kWaves), (unsigned)(m / 8));
   if (mode == kSymN8)
-  {
-    if (nbw == 4) EIG_SPMM(uint8_t, 4);
-    else if (nbw == 2) EIG_SPMM(uint8_t, 2);
-    else EIG_SPMM(uint8_t, 1);
-  }
+    hipLaunchKernelGGL((k_spmm8_march<uint8_t>), grid, dim3(kStreamThreads), 0, s, A.nb_rows, A.own_offset, A.window,
+                       sell_b1(A), mp, X, Y);
   else
-  {
-    if (nbw == 4) EIG_SPMM(uint32_t, 4);
-    else if (nbw == 2) EIG_SPMM(uint32_t, 2);
-    else EIG_SPMM(uint32_t, 1);
-  }
-#undef EIG_SPMM
+    hipLaunchKernelGGL((k_spmm8_march<uint32_t>), grid, dim3(kStreamThreads), 0, s, A.nb_rows, A.own_offset, A.window,
+                       sell_b1(A), mp, X, Y);
   return true;
 }
 
@@ -2072,11 +1802,11 @@ std::string kernel_for(const eig_mat_s &A, int op)
       if (!b1) return "none";
       i64 P;
       GSpans sp;
-      const bool g = marchg_enabled() && (mode == kSymN8 || mode == kSymN32) && gspans(A, P, sp) &&
+      const bool g = marchg_enabled(A) && (mode == kSymN8 || mode == kSymN32) && gspans(A, P, sp) &&
                      (A.nb_rows + P - 1) / P >= 4;
       if (op == 3 && march_plan(A, mode, 0, -1, false, 16).nseg > 0) return "k_spmm8_march";
       if (g) return op == 3 ? "k_spmm8_marchg" : "k_spmm8_marchg_cheb";
-      return op == 3 ? "k_sell_mv8" : "k_sell_mv8q_cheb";
+      return op == 3 ? (b1 && A.nb_rows > 0 ? "k_sell_mv8g" : "none") : "k_sell_mv8q_cheb";
     }
     default:
       return "none";

@@ -819,11 +819,11 @@ void launch_inverse_mv8(TrsvImage &img, i64 m, double *Qin, double *Qout, hipStr
   const int nblk = (int)(m / 8);
   // 1. Qout = P (R Qin)   2. Qin = L^-1 Qout   3. Qin = U^-1 Qin   4. Qout = Q Qin
   // (block-inverse: Qout = inv(D) P R Qin, Qin = L^-1 chain, Qout = inv(D_U) Qin, Qin = U^-1 chain)
-  // EIGMI_TRSV: "csr" = the row-CSR kernel, "staged" = the block-staged kernel (both bitwise the
-  // reference arithmetic); default: the block-inverse solve when the factor has its image
-  const char *e = std::getenv("EIGMI_TRSV");
-  const std::string kind = e ? std::string(e) : std::string();
-  if (img.binv && kind != "csr" && kind != "staged")
+  // img.solver (eig_lu_set_solver): EIG_TRSV_CSR = the row-CSR kernel, EIG_TRSV_STAGED = the
+  // block-staged kernel (both bitwise the reference arithmetic); AUTO / BLOCKINV: the block-inverse
+  // solve when the factor has its image
+  const bool csr = img.solver == EIG_TRSV_CSR, staged = img.solver == EIG_TRSV_STAGED;
+  if (img.binv && !csr && !staged)
   {
     const i64 nblocks = (n + kTB - 1) / kTB;
     hipLaunchKernelGGL(k_binv_z<true>, dim3((unsigned)nblocks, nblk), dim3(kThreadsT), 0, s, n, (const double *)img.dinv[0],
@@ -837,9 +837,9 @@ void launch_inverse_mv8(TrsvImage &img, i64 m, double *Qin, double *Qout, hipStr
     EIG_HIP(hipGetLastError());
     return;
   }
-  if (img.staged && !img.staged_built && kind != "csr") build_staged(img);
+  if (img.staged && !img.staged_built && !csr) build_staged(img);
   hipLaunchKernelGGL(k_perm_scale, dim3(grid256(n * nblk)), dim3(256), 0, s, n, nblk, img.P, img.scale, Qin, Qout);
-  if (!img.staged || kind == "csr")
+  if (!img.staged || csr)
   {
     hipLaunchKernelGGL(k_tsolve<true>, dim3(nblk), dim3(kTThreads), 0, s, n, img.lrp, img.lsplit, img.lc, img.lv,
                        (const double *)nullptr, (const double *)Qout, Qin);

@@ -373,6 +373,17 @@ extern "C" int eig_lu_info(eig_lu_t lu, int64_t *n, int64_t *lnz, int64_t *unz, 
   });
 }
 
+extern "C" int eig_lu_set_solver(eig_lu_t lu, int kind)
+{
+  return guard(lu ? lu->ctx : nullptr, [&] {
+    EIG_CHECK(lu, EIG_ERR_ARG, "eig_lu_set_solver: null handle");
+    EIG_CHECK(kind >= EIG_TRSV_AUTO && kind <= EIG_TRSV_CSR, EIG_ERR_ARG, "eig_lu_set_solver: unknown solver");
+    EIG_CHECK(kind != EIG_TRSV_BLOCKINV || !lu->ctx || lu->img.binv, EIG_ERR_ARG,
+              "eig_lu_set_solver: these factors have no block-inverse image");
+    lu->img.solver = kind;
+  });
+}
+
 extern "C" int eig_lu_export(eig_lu_t lu, int64_t *Lp, int64_t *Lj, double *Lx, int64_t *Up, int64_t *Ui, double *Ux,
                              int64_t *P, int64_t *Q, double *Rs)
 {

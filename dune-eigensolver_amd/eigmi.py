@@ -14,6 +14,13 @@ LIB_PATH = os.path.join(_HERE, "lib", "libeigmi.so")
 
 EIG_OK, EIG_ERR_SHAPE, EIG_ERR_BLOCKSIZE, EIG_ERR_HIP, EIG_ERR_RCCL, EIG_ERR_BREAKDOWN, EIG_ERR_ARG, EIG_ERR_NODEVICE = range(8)
 ORTHO_MGS, ORTHO_CHOLQR = 0, 1
+ORTHO_GRID = 0x100  # or-ed into the variant: grid-wide MGS passes even for blocks one workgroup holds
+# matrix kernel-image flags (eig_mat_create_bcsr_ex)
+MAT_NO_BAND, MAT_BAND_GATHER, MAT_NO_STENCIL, MAT_NO_MARCH = 1, 2, 4, 8
+# triangular-solve kernels of an LU (eig_lu_set_solver)
+TRSV_AUTO, TRSV_BLOCKINV, TRSV_STAGED, TRSV_CSR = 0, 1, 2, 3
+TRSV_KINDS = {None: TRSV_AUTO, "auto": TRSV_AUTO, "blockinv": TRSV_BLOCKINV, "staged": TRSV_STAGED, "csr": TRSV_CSR}
+COMM_MAILBOX = 1
 WHICH_LA, WHICH_SA = 0, 1
 LANCZOS_TIME_KERNELS = 1
 LANCZOS_TIME_DETAIL = 2
@@ -78,6 +85,7 @@ SIGNATURES = {
     "eig_version": (ctypes.c_char_p, []),
     "eig_comm_unique_id": (_int, [ctypes.c_char_p]),
     "eig_comm_init": (_int, [_vp, _int, _int, ctypes.c_char_p]),
+    "eig_comm_init_ex": (_int, [_vp, _int, _int, ctypes.c_char_p, _int]),
     "eig_comm_allreduce_sum": (_int, [_vp, _vp, _i64]),
     "eig_comm_barrier": (_int, [_vp]),
     "eig_loopback_create": (_int, [_int, ctypes.POINTER(_vp)]),
@@ -95,6 +103,10 @@ SIGNATURES = {
     "eig_memset": (_int, [_vp, _vp, _int, ctypes.c_size_t]),
     "eig_mat_create_bcsr": (_int, [_vp, _i64, _i64, _int, _int, _vp, _vp, _vp, ctypes.POINTER(_vp)]),
     "eig_mat_create_bcsr_dist": (_int, [_vp, _i64, _i64, _i64, _int, _int, _vp, _vp, _vp, ctypes.POINTER(_vp)]),
+    "eig_mat_create_bcsr_ex": (_int, [_vp, _i64, _i64, _int, _int, _vp, _vp, _vp, _int, ctypes.POINTER(_vp)]),
+    "eig_mat_create_bcsr_dist_ex": (_int, [_vp, _i64, _i64, _i64, _int, _int, _vp, _vp, _vp, _int,
+                                           ctypes.POINTER(_vp)]),
+    "eig_lu_set_solver": (_int, [_vp, _int]),
     "eig_mat_destroy": (_int, [_vp]),
     "eig_mat_get_info": (_int, [_vp, ctypes.POINTER(_MatInfo)]),
     "eig_mat_shift_diag": (_int, [_vp, _dbl]),
@@ -225,8 +237,10 @@ class Context:
             raise EigError(rc, lib.eig_last_error(None).decode())
         return buf.raw
 
-    def comm_init(self, nranks, rank, uid):
-        self.check(lib.eig_comm_init(self.h, nranks, rank, uid))
+    def comm_init(self, nranks, rank, uid, mailbox=False):
+        """RCCL communicator (ncclAllReduce for dots); mailbox=True also sets up the xGMI mailbox
+        allreduce (eig_comm_init_ex, EIG_COMM_MAILBOX)."""
+        self.check(lib.eig_comm_init_ex(self.h, nranks, rank, uid, COMM_MAILBOX if mailbox else 0))
         self.nranks, self.rank = nranks, rank
 
     def barrier(self):
@@ -332,25 +346,27 @@ class Matrix:
         return buf.value.decode(), int(b.value)
 
     @classmethod
-    def from_bcsr(cls, ctx, rowptr, col, vals, br=1, bc=1, ncols_blocks=None):
+    def from_bcsr(cls, ctx, rowptr, col, vals, br=1, bc=1, ncols_blocks=None, flags=0):
+        """flags: MAT_NO_BAND | MAT_BAND_GATHER | MAT_NO_STENCIL | MAT_NO_MARCH (eig_mat_create_bcsr_ex)."""
         rowptr = np.ascontiguousarray(rowptr, np.int64)
         col = np.ascontiguousarray(col, np.int32)
         vals = np.ascontiguousarray(vals, np.float64)
         nb = rowptr.size - 1
         nbc = nb if ncols_blocks is None else ncols_blocks
         h = _vp()
-        ctx.check(lib.eig_mat_create_bcsr(ctx.h, nb, nbc, br, bc, _np_ptr(rowptr), _np_ptr(col), _np_ptr(vals),
-                                          ctypes.byref(h)))
+        ctx.check(lib.eig_mat_create_bcsr_ex(ctx.h, nb, nbc, br, bc, _np_ptr(rowptr), _np_ptr(col), _np_ptr(vals),
+                                             int(flags), ctypes.byref(h)))
         return cls(ctx, h)
 
     @classmethod
-    def from_rows(cls, ctx, nb_global, row_begin, rowptr, col, vals, br=1, bc=1):
+    def from_rows(cls, ctx, nb_global, row_begin, rowptr, col, vals, br=1, bc=1, flags=0):
         rowptr = np.ascontiguousarray(rowptr, np.int64)
         col = np.ascontiguousarray(col, np.int32)
         vals = np.ascontiguousarray(vals, np.float64)
         h = _vp()
-        ctx.check(lib.eig_mat_create_bcsr_dist(ctx.h, nb_global, row_begin, rowptr.size - 1, br, bc, _np_ptr(rowptr),
-                                               _np_ptr(col), _np_ptr(vals), ctypes.byref(h)))
+        ctx.check(lib.eig_mat_create_bcsr_dist_ex(ctx.h, nb_global, row_begin, rowptr.size - 1, br, bc,
+                                                  _np_ptr(rowptr), _np_ptr(col), _np_ptr(vals), int(flags),
+                                                  ctypes.byref(h)))
         return cls(ctx, h)
 
     def close(self):
@@ -595,6 +611,10 @@ class LU:
 
     def inverse_mv8(self, m, Qin, Qout):
         self.ctx.check(lib.eig_inverse_mv8(self.h, m, Qin.ptr, Qout.ptr))
+
+    def set_solver(self, kind):
+        """kind: None / "auto", "blockinv", "staged" or "csr" (eig_lu_set_solver)."""
+        self._check(lib.eig_lu_set_solver(self.h, TRSV_KINDS[kind]))
 
     def close(self):
         if self.h and (self.ctx is None or self.ctx.h):

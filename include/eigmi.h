@@ -65,6 +65,10 @@ const char *eig_version(void);
  * xGMI) and matrices created with eig_mat_create_bcsr_dist exchange halos. */
 int eig_comm_unique_id(unsigned char id[128]);
 int eig_comm_init(eig_ctx_t ctx, int nranks, int rank, const unsigned char id[128]);
+/* flags: EIG_COMM_MAILBOX = also set up the xGMI mailbox allreduce (below); default (0, and
+ * eig_comm_init): ncclAllReduce. */
+enum { EIG_COMM_MAILBOX = 1 };
+int eig_comm_init_ex(eig_ctx_t ctx, int nranks, int rank, const unsigned char id[128], int flags);
 int eig_comm_allreduce_sum(eig_ctx_t ctx, double *buf, int64_t count);
 /* In-process loopback transport for testing the distributed path on ONE device: create a hub for
  * nranks virtual ranks, give each rank its own host thread + context and attach it with
@@ -74,10 +78,10 @@ int eig_loopback_create(int nranks, void **hub);
 int eig_loopback_destroy(void *hub);
 int eig_comm_init_loopback(eig_ctx_t ctx, void *hub, int rank);
 int eig_comm_barrier(eig_ctx_t ctx);
-/* Allreduce transport.  With RCCL, eig_comm_init also sets up the xGMI mailbox allreduce (every
- * rank exports a small uncached mailbox through IPC; one launch stores this rank's values into
- * every peer's mailbox and sums all slots in rank order) for up to 16 ranks, validated and agreed
- * by all ranks, else ncclAllReduce stays in use; EIGMI_ALLREDUCE=rccl forces RCCL.
+/* Allreduce transport.  With RCCL and EIG_COMM_MAILBOX, eig_comm_init_ex also sets up the xGMI
+ * mailbox allreduce (every rank exports a small uncached mailbox through IPC; one launch stores
+ * this rank's values into every peer's mailbox and sums all slots in rank order) for up to 16
+ * ranks, validated and agreed by all ranks, else ncclAllReduce stays in use.
  * eig_comm_ipc_handle / eig_comm_ipc_open attach the mailbox alone (no RCCL; allreduce and dots
  * only -- distributed matrices need RCCL or loopback): every rank exports its handle, the
  * nranks x 64 bytes travel by any side channel (rank order), then every rank opens them. */
@@ -112,6 +116,26 @@ int eig_mat_create_bcsr(eig_ctx_t ctx, int64_t nb_rows, int64_t nb_cols, int br,
 int eig_mat_create_bcsr_dist(eig_ctx_t ctx, int64_t nb_rows_global, int64_t row_begin,
                              int64_t nb_rows_local, int br, int bc, const int64_t *rowptr_host,
                              const int32_t *col_host, const double *vals_host, eig_mat_t *mat);
+/* Kernel-image policy of a matrix, fixed at creation (the _ex variants; 0 = the default, which
+ * picks the fastest image the matrix admits).  These exist for A/B measurements and for the tests
+ * that pin every image against the oracle:
+ *   EIG_MAT_NO_BAND      no symmetric band image: the scalar kernels read the SELL / stencil image
+ *   EIG_MAT_BAND_GATHER  band image, but every offset through its own gather (no DPP lane shifts)
+ *   EIG_MAT_NO_STENCIL   SELL slices keep explicit column indices (no per-slice offsets + row masks)
+ *   EIG_MAT_NO_MARCH     no plane-marching kernels (band image: the row kernels) */
+enum {
+  EIG_MAT_NO_BAND = 1,
+  EIG_MAT_BAND_GATHER = 2,
+  EIG_MAT_NO_STENCIL = 4,
+  EIG_MAT_NO_MARCH = 8,
+  EIG_MAT_FLAGS_ALL = 15
+};
+int eig_mat_create_bcsr_ex(eig_ctx_t ctx, int64_t nb_rows, int64_t nb_cols, int br, int bc,
+                           const int64_t *rowptr_host, const int32_t *col_host, const double *vals_host, int flags,
+                           eig_mat_t *mat);
+int eig_mat_create_bcsr_dist_ex(eig_ctx_t ctx, int64_t nb_rows_global, int64_t row_begin,
+                                int64_t nb_rows_local, int br, int bc, const int64_t *rowptr_host,
+                                const int32_t *col_host, const double *vals_host, int flags, eig_mat_t *mat);
 int eig_mat_destroy(eig_mat_t mat);
 
 typedef struct eig_mat_info {
@@ -142,8 +166,8 @@ int eig_mat_get_info(eig_mat_t mat, eig_mat_info *info);
  * per launch for that image: SELL/stencil images 12 nnz + 4(n+1) + vectors,
  * the symmetric band image 8 nup n + mask bytes + vectors.  `name` gets at most name_len bytes. */
 int eig_lanczos_kernel_info(eig_mat_t mat, int fused, char *name, int name_len, int64_t *bytes);
-/* Kernel family a whole-matrix launch of `op` picks on this matrix image now (the EIGMI_*
- * environment switches included): EIG_OP_SPMV (eig_mv), EIG_OP_LANCZOS_K1, EIG_OP_LANCZOS_FUSED,
+/* Kernel family a whole-matrix launch of `op` picks on this matrix image (its creation flags
+ * included): EIG_OP_SPMV (eig_mv), EIG_OP_LANCZOS_K1, EIG_OP_LANCZOS_FUSED,
  * EIG_OP_SPMM8 (eig_spmm_mv8, per 8-column block), EIG_OP_CHEB8 (eig_mass_solve_mv8's step). */
 enum { EIG_OP_SPMV = 0, EIG_OP_LANCZOS_K1 = 1, EIG_OP_LANCZOS_FUSED = 2, EIG_OP_SPMM8 = 3, EIG_OP_CHEB8 = 4 };
 int eig_mat_kernel_info(eig_mat_t mat, int op, char *name, int name_len);
@@ -182,6 +206,9 @@ int eig_gram_mv8(eig_ctx_t ctx, int64_t n, int64_t m1, int64_t m2, const double 
  * EIG_ORTHO_CHOLQR = orthonormalize_avx2_b8_v2 / _neon_b8_v2 (kernels_avx2.hh:385-622): CholQR of
  *                    the diagonal block, one 8x8 projection per later block. */
 enum eig_ortho_variant { EIG_ORTHO_MGS = 0, EIG_ORTHO_CHOLQR = 1 };
+/* or-ed into `variant`: keep the grid-wide MGS passes even where one workgroup holds the block
+ * (n <= 4096 on one rank; the two do the same per-row operations -- A/B and tests) */
+enum { EIG_ORTHO_GRID = 0x100 };
 int eig_orthonormalize_mv8(eig_ctx_t ctx, int64_t n, int64_t m, double *Q, int variant);
 /* a8: orthonormalize_naive on a column-major (MultiVector<double,1>) block (kernels_cpp.hh:121-155). */
 int eig_orthonormalize_naive(eig_ctx_t ctx, int64_t n, int64_t m, double *Q);
@@ -278,6 +305,13 @@ int eig_lu_create(eig_ctx_t ctx, int64_t n, const int64_t *Lp, const int64_t *Lj
 int eig_lu_create_bcsr(eig_ctx_t ctx, int64_t nb_rows, int br, const int64_t *rowptr, const int32_t *col,
                        const double *vals, eig_lu_t *lu);
 int eig_lu_info(eig_lu_t lu, int64_t *n, int64_t *lnz, int64_t *unz, int *do_recip);
+/* Triangular-solve kernels eig_inverse_mv8 uses for these factors (default EIG_TRSV_AUTO: the
+ * block-inverse solve where the factors have its image, else the block-staged / row-CSR
+ * substitution).  EIG_TRSV_STAGED and EIG_TRSV_CSR are bitwise the reference arithmetic
+ * (matmul_inverse_tallskinny_blocked, kernels_cpp.hh:660-755); the block-inverse solve agrees to
+ * rounding. */
+enum { EIG_TRSV_AUTO = 0, EIG_TRSV_BLOCKINV = 1, EIG_TRSV_STAGED = 2, EIG_TRSV_CSR = 3 };
+int eig_lu_set_solver(eig_lu_t lu, int kind);
 /* Copy the factors out (sizes from eig_lu_info: Lp/Up n+1, Lj/Lx lnz, Ui/Ux unz, P/Q/Rs n). */
 int eig_lu_export(eig_lu_t lu, int64_t *Lp, int64_t *Lj, double *Lx, int64_t *Up, int64_t *Ui, double *Ux,
                   int64_t *P, int64_t *Q, double *Rs);

@@ -128,15 +128,14 @@ def test_orthonormalize_blocked(ctx, variant, name, n, m):
 
 
 @pytest.mark.parametrize("n,m", [(3000, 16), (4096, 8), (513, 8)])
-def test_mgs_small_vs_grid(ctx, n, m, monkeypatch):
+def test_mgs_small_vs_grid(ctx, n, m):
     """n <= 4096 on one rank: the diagonal block's MGS runs in one workgroup (k_mgs_small); the
-    grid-wide passes (EIGMI_MGS_SMALL=0) do the same per-row operations, so the two agree to the
+    grid-wide passes (variant | EIG_ORTHO_GRID) do the same per-row operations, so the two agree to the
     rounding of the sums' order."""
     Qh = oracle.random_mv8(n, m, 5)
     Qa, Qb = ctx.array(Qh), ctx.array(Qh)
     eigmi.orthonormalize_mv8(ctx, n, m, Qa, eigmi.ORTHO_MGS)
-    monkeypatch.setenv("EIGMI_MGS_SMALL", "0")
-    eigmi.orthonormalize_mv8(ctx, n, m, Qb, eigmi.ORTHO_MGS)
+    eigmi.orthonormalize_mv8(ctx, n, m, Qb, eigmi.ORTHO_MGS | eigmi.ORTHO_GRID)
     a, b = Qa.get(), Qb.get()
     assert np.all(np.isfinite(a)) and np.abs(a - b).max() < 1e-13
 

@@ -8,7 +8,6 @@ recurrence's own run-to-run spread beyond that (two classic runs whose start vec
 1e-16 already differ by ~6e-10 at sigma = 1e6 after 60 steps; tests/fused_ref.py); alpha to 1e-12
 relative throughout.  Both the plane-march kernel (band image) and the SELL row kernel run the
 guard; repairs and the halted (breakdown) state are exercised."""
-import os
 
 import numpy as np
 import pytest
@@ -21,15 +20,7 @@ pytestmark = pytest.mark.gpu
 
 
 def upload(ctx, A, band=True):
-    old = os.environ.get("EIGMI_SYM")
-    os.environ["EIGMI_SYM"] = "2" if band else "0"
-    try:
-        return eigmi.Matrix.from_bcsr(ctx, A.rowptr, A.col, A.val, A.br, A.bc)
-    finally:
-        if old is None:
-            del os.environ["EIGMI_SYM"]
-        else:
-            os.environ["EIGMI_SYM"] = old
+    return eigmi.Matrix.from_bcsr(ctx, A.rowptr, A.col, A.val, A.br, A.bc, flags=0 if band else eigmi.MAT_NO_BAND)
 
 
 def fused_run(M, steps, batches=1, graph=False):

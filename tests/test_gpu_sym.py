@@ -5,7 +5,6 @@ pairs are bitwise equal keeps its values once, in upper-triangle band arrays; th
 the Lanczos kernels read the lower entries through the mirrored upper slot.  Every row still sums
 its own stored entries in ascending-column order, so the bar stays BITWISE equality with the
 reference row loop (oracle.csr_mv = matmul_sparse_tallskinny_naive, kernels_cpp.hh:596-621)."""
-import os
 
 import numpy as np
 import pytest
@@ -16,16 +15,10 @@ import oracle
 pytestmark = pytest.mark.gpu
 
 
-def upload(ctx, A, sym=True):
-    old = os.environ.get("EIGMI_SYM")
-    os.environ["EIGMI_SYM"] = "1" if sym else "0"
-    try:
-        return eigmi.Matrix.from_bcsr(ctx, A.rowptr, A.col, A.val, A.br, A.bc)
-    finally:
-        if old is None:
-            del os.environ["EIGMI_SYM"]
-        else:
-            os.environ["EIGMI_SYM"] = old
+def upload(ctx, A, sym=True, flags=0):
+    """sym=False: no band image (eig_mat_create_bcsr_ex EIG_MAT_NO_BAND; the SELL kernels)."""
+    return eigmi.Matrix.from_bcsr(ctx, A.rowptr, A.col, A.val, A.br, A.bc,
+                                  flags=flags | (0 if sym else eigmi.MAT_NO_BAND))
 
 
 def band_matrix(n, offsets, seed, drop=0.0, symmetric=True):
@@ -228,16 +221,9 @@ def test_marchg_chebyshev_matches_sell(ctx, N, m):
     B = ctx.array(Bh)
     X1, X2 = ctx.zeros(n * m), ctx.zeros(n * m)
     eigmi.mass_solve_mv8(M, m, 12, B, X1)
-    old = os.environ.get("EIGMI_MARCHG")
-    os.environ["EIGMI_MARCHG"] = "0"
-    try:
-        assert M.kernel("cheb8") == "k_sell_mv8q_cheb"
-        eigmi.mass_solve_mv8(M, m, 12, B, X2)
-    finally:
-        if old is None:
-            del os.environ["EIGMI_MARCHG"]
-        else:
-            os.environ["EIGMI_MARCHG"] = old
+    Ms = upload(ctx, A, flags=eigmi.MAT_NO_MARCH)
+    assert Ms.kernel("cheb8") == "k_sell_mv8q_cheb"
+    eigmi.mass_solve_mv8(Ms, m, 12, B, X2)
     a, b = X1.get(), X2.get()
     assert np.allclose(a, b, rtol=1e-13, atol=1e-14 * np.abs(b).max())
     # and the solve is a solve: M x ~ b (degree 12 Chebyshev, kappa(D^-1 M) <= 5: error ~ 2 0.38^12)

@@ -104,26 +104,17 @@ def _gpu_lu(ctx, A, via="bcsr", recip=False):
 
 
 class trsv_kernel:
-    """EIGMI_TRSV for the duration of a block: "staged" / "csr" (bitwise kernels) or None (the
+    """eig_lu_set_solver for the duration of a block: "staged" / "csr" (bitwise kernels) or None (the
     default: the block-inverse solve where the factor has its image)."""
 
-    def __init__(self, kind):
-        self.kind = kind
+    def __init__(self, lu, kind):
+        self.lu, self.kind = lu, kind
 
     def __enter__(self):
-        import os
-        self.old = os.environ.get("EIGMI_TRSV")
-        if self.kind is None:
-            os.environ.pop("EIGMI_TRSV", None)
-        else:
-            os.environ["EIGMI_TRSV"] = self.kind
+        self.lu.set_solver(self.kind)
 
     def __exit__(self, *a):
-        import os
-        if self.old is None:
-            os.environ.pop("EIGMI_TRSV", None)
-        else:
-            os.environ["EIGMI_TRSV"] = self.old
+        self.lu.set_solver(None)
 
 
 # The block-inverse solve multiplies by inv(D_b) instead of substituting: agreement with the
@@ -144,7 +135,7 @@ def test_inverse_mv8_bitwise(ctx, name, m, via, kernel):
     X = oracle.random_mv8(n, m, 11)
     ref_out, ref_in = oracle.inverse_mv8(f, X, m)
     din, dout = ctx.array(X), ctx.zeros(n * m)
-    with trsv_kernel(kernel):
+    with trsv_kernel(lu, kernel):
         lu.inverse_mv8(m, din, dout)
     out = dout.get()
     if kernel == "staged":
@@ -165,7 +156,7 @@ def test_inverse_mv8_do_recip(ctx):
     X = oracle.random_mv8(A.n, 8, 2)
     ref_out, _ = oracle.inverse_mv8(f, X, 8)
     din, dout = ctx.array(X), ctx.zeros(A.n * 8)
-    with trsv_kernel("staged"):
+    with trsv_kernel(lu, "staged"):
         lu.inverse_mv8(8, din, dout)
     assert np.array_equal(dout.get(), ref_out)
     din = ctx.array(X)
@@ -257,7 +248,7 @@ def test_inverse_mv8_kernels(ctx, name, kernel):
     lu, f = _gpu_lu(ctx, A, "bcsr")
     X = oracle.random_mv8(A.n, 16, 3)
     ref_out, _ = oracle.inverse_mv8(f, X, 16)
-    with trsv_kernel(kernel):
+    with trsv_kernel(lu, kernel):
         din, dout = ctx.array(X), ctx.zeros(A.n * 16)
         lu.inverse_mv8(16, din, dout)
     out = dout.get()

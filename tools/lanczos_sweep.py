@@ -1,14 +1,16 @@
 #!/usr/bin/env python3
-"""A/B of Lanczos step variants on one GPU, interleaved rounds in ONE process (guide rule 24).
+"""A/B of Lanczos step / SpMV kernel images on one GPU, interleaved rounds in ONE process.
 
-Variant spec "<fused|classic>[:swz0|swz1][:w4|w5|w6|w8][:nt0|nt1][:sym0|sym1|sym2][:march0|1|2|3][:mnt0|mnt1][:wg0|wg1][:seg<k>][:m7|m8]": step form, XCD-aware chunk
-order (EIGMI_XCD_SWIZZLE), register budget of the fused kernel (EIGMI_FUSED_WAVES), nontemporal
-stores of the step vectors (EIGMI_NT_STORE), symmetric band image or SELL image (EIGMI_SYM), plane marching
-(EIGMI_MARCH).  The environment is
-read at every launch, so all variants share one matrix upload.  One JSON line per variant:
-median / min over rounds of the step time and of the dominant kernel's time.
+Variant spec "<fused|classic|mv>[:<image>]" with image one of
+    band     (default) symmetric band image, plane march where the band allows it
+    gather   band image, every offset through its own gather (EIG_MAT_BAND_GATHER)
+    nomarch  band image, row kernels (EIG_MAT_NO_MARCH)
+    sell     SELL-64 / stencil-slice image (EIG_MAT_NO_BAND)
+    explicit SELL-64 with explicit column indices only (EIG_MAT_NO_BAND | EIG_MAT_NO_STENCIL)
+Each image is uploaded once (eig_mat_create_bcsr_ex flags) and shared by its variants.  One JSON
+line per variant: median / min over rounds of the step time and of the dominant kernel's time.
 
-    python tools/lanczos_sweep.py --variants classic:swz0,classic:swz1,fused:swz1:w5
+    python tools/lanczos_sweep.py --variants fused,fused:sell,classic,mv,mv:explicit
 """
 import argparse
 import json
@@ -21,37 +23,19 @@ import numpy as np  # noqa: E402
 
 import eigmi  # noqa: E402
 
+IMAGES = {"band": 0, "gather": eigmi.MAT_BAND_GATHER, "nomarch": eigmi.MAT_NO_MARCH, "sell": eigmi.MAT_NO_BAND,
+          "explicit": eigmi.MAT_NO_BAND | eigmi.MAT_NO_STENCIL}
+
 
 def parse(spec):
     parts = spec.split(":")
-    env = {"EIGMI_XCD_SWIZZLE": "0", "EIGMI_FUSED_WAVES": "8", "EIGMI_NT_STORE": "0", "EIGMI_SYM": "2", "EIGMI_MARCH": "d", "EIGMI_MARCH_NT": "1",
-           "EIGMI_MARCH_WG": "0", "EIGMI_MARCH_SEG": "0", "EIGMI_MARCH_W7": "1"}
-    for p in parts[1:]:
-        if p in ("m7", "m8"):
-            env["EIGMI_MARCH_W7"] = "1" if p == "m7" else "0"
-        elif p.startswith("wg"):
-            env["EIGMI_MARCH_WG"] = p[2:]
-        elif p.startswith("seg"):
-            env["EIGMI_MARCH_SEG"] = p[3:]
-        elif p.startswith("mnt"):
-            env["EIGMI_MARCH_NT"] = p[3:]
-        elif p.startswith("march"):
-            env["EIGMI_MARCH"] = p[5:]
-        elif p.startswith("sym"):
-            env["EIGMI_SYM"] = p[3:]
-        elif p.startswith("nt"):
-            env["EIGMI_NT_STORE"] = p[2:]
-        elif p.startswith("swz"):
-            env["EIGMI_XCD_SWIZZLE"] = p[3:]
-        elif p.startswith("w"):
-            env["EIGMI_FUSED_WAVES"] = p[1:]
-    return parts[0] == "fused", env
+    return parts[0], IMAGES[parts[1] if len(parts) > 1 else "band"]
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--N", type=int, default=256)
-    ap.add_argument("--variants", default="classic:swz0,classic:swz1,fused:swz0,fused:swz1")
+    ap.add_argument("--variants", default="fused,fused:sell,classic,mv")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--slab", type=int, default=0, help="N x N x slab box instead of the N^3 cube")
@@ -62,6 +46,7 @@ def main():
         # one rank's share of an 8-way row partition: a standalone N x N x slab 7-point box
         # (Dirichlet on all faces; no halo), to time the per-GPU compute of the strong-scaling runs
         import scipy.sparse as sp
+
         def lap1(k):
             return sp.diags([-np.ones(k - 1), np.zeros(k), -np.ones(k - 1)], [-1, 0, 1])
         Ix, Iz = sp.identity(N), sp.identity(args.slab)
@@ -75,40 +60,47 @@ def main():
         n = N ** 3
         rp, c, v = eigmi.gen_matrix(eigmi.GEN_POISSON3D, N)
     nnz = int(rp[-1])
-    M = eigmi.Matrix.from_bcsr(ctx, rp, c, v)
     specs = args.variants.split(",")
+    mats = {}
+    for spec in specs:
+        fl = parse(spec)[1]
+        if fl not in mats:
+            mats[fl] = eigmi.Matrix.from_bcsr(ctx, rp, c, v, flags=fl)
     res = {s: {"k_us": [], "step_us": []} for s in specs}
     xy = None
     for _ in range(args.rounds):
         for spec in specs:
-            fused, env = parse(spec)
-            os.environ.update(env)
-            if spec.startswith("mv"):  # plain eig_mv (BCRSMatrix::mv) launches
+            op, fl = parse(spec)
+            M = mats[fl]
+            if op == "mv":  # plain eig_mv (BCRSMatrix::mv) launches
                 if xy is None:
                     xy = (ctx.array(np.random.default_rng(0).standard_normal(n)), ctx.zeros(n))
                 ms = M.mv_timed(xy[0], xy[1], args.steps)
                 res[spec]["k_us"].append(ms * 1e3)
                 res[spec]["step_us"].append(ms * 1e3)
                 continue
-            ws = eigmi.LanczosWorkspace(M, args.steps + 2, seed=123, fused=fused)
+            ws = eigmi.LanczosWorkspace(M, args.steps + 2, seed=123, fused=op == "fused")
             ws.step(2)
             t = ws.step(args.steps, timed=True)
             res[spec]["k_us"].append(t.spmv_ms / args.steps * 1e3)
             res[spec]["step_us"].append(t.total_ms / args.steps * 1e3)
             ws.close()
     for spec in specs:
-        fused, _ = parse(spec)
-        kb = (eigmi.bytes_spmv(n, nnz) if spec.startswith("mv") else
-              eigmi.bytes_lanczos_fused(n, nnz) if fused else eigmi.bytes_lanczos_k1(n, nnz))
+        op, fl = parse(spec)
+        M = mats[fl]
+        kb = (eigmi.bytes_spmv(n, nnz) if op == "mv" else
+              eigmi.bytes_lanczos_fused(n, nnz) if op == "fused" else eigmi.bytes_lanczos_k1(n, nnz))
         r = res[spec]
         km = float(np.median(r["k_us"]))
         sm = float(np.median(r["step_us"]))
-        print(json.dumps({"variant": spec, "kernel_us_med": round(km, 2), "kernel_us_min": round(min(r["k_us"]), 2),
-                          "kernel_GBs": round(kb / km / 1e3, 1), "step_us_med": round(sm, 2),
+        print(json.dumps({"variant": spec, "kernel": M.kernel({"mv": "spmv", "fused": "fused", "classic": "k1"}[op]),
+                          "kernel_us_med": round(km, 2), "kernel_us_min": round(min(r["k_us"]), 2),
+                          "kernel_csr_GBs": round(kb / km / 1e3, 1), "step_us_med": round(sm, 2),
                           "steps_per_s": round(1e6 / sm, 1),
                           "step_frac_survey_bytes": round(eigmi.bytes_lanczos_step(n, nnz) / sm / 1e3 / 8000, 4)}),
               flush=True)
-    M.close()
+    for M in mats.values():
+        M.close()
     ctx.close()
 
 
