@@ -1324,6 +1324,29 @@ extern "C" int eig_copy(eig_ctx_t ctx, int64_t n, const double *x, double *y)
   });
 }
 
+extern "C" int eig_stream_copy_timed(eig_ctx_t ctx, int64_t n, const double *x, double *y, int reps, int mode,
+                                     double *avg_ms)
+{
+  return guard(ctx, [&] {
+    EIG_CHECK(ctx && x && y && n >= 0 && reps >= 1 && avg_ms, EIG_ERR_ARG, "eig_stream_copy_timed: bad argument");
+    DeviceGuard dg(ctx->device);
+    hipStream_t s = ctx->stream;
+    hipEvent_t e0, e1;
+    EIG_HIP(hipEventCreate(&e0));
+    EIG_HIP(hipEventCreate(&e1));
+    launch_stream_copy(n, x, y, ctx->num_cu, s, mode);  // warm-up
+    EIG_HIP(hipEventRecord(e0, s));
+    for (int r = 0; r < reps; ++r) launch_stream_copy(n, x, y, ctx->num_cu, s, mode);
+    EIG_HIP(hipEventRecord(e1, s));
+    EIG_HIP(hipEventSynchronize(e1));
+    float ms = 0.f;
+    EIG_HIP(hipEventElapsedTime(&ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    *avg_ms = ms / reps;
+  });
+}
+
 // ============================================================================================
 // MultiVector<double,8>
 // ============================================================================================

@@ -323,3 +323,56 @@ void launch_resid_sq(i64 n, const double *x, const double *y, double theta, doub
 }
 
 }  // namespace eigmi
+
+namespace eigmi {
+// ---------------------------------------------------------------------------------------------
+// Stream copy y = x (the measured HBM peak the roofline fractions are also quoted against, SURVEY
+// 8(d)): 16 B per lane.  MODE (A/B, tools/copy_sweep.py): bit 0 = nontemporal loads / stores, bit 1
+// = one element per thread over a full grid (else a resident grid striding 4 elements per pass).
+// ---------------------------------------------------------------------------------------------
+typedef double dv2s __attribute__((ext_vector_type(2)));
+template <int MODE>
+__global__ __launch_bounds__(kStreamThreads) void k_stream_copy(i64 n2, const dv2s *__restrict__ x,
+                                                                dv2s *__restrict__ y)
+{
+  auto ld = [&](i64 i) { return (MODE & 1) ? __builtin_nontemporal_load(x + i) : x[i]; };
+  auto st = [&](i64 i, dv2s v) {
+    if (MODE & 1) __builtin_nontemporal_store(v, y + i);
+    else y[i] = v;
+  };
+  i64 i = (i64)blockIdx.x * kStreamThreads + threadIdx.x;
+  if (MODE & 2)
+  {
+    if (i < n2) st(i, ld(i));
+    return;
+  }
+  const i64 stride = (i64)gridDim.x * kStreamThreads;
+  for (; i + 3 * stride < n2; i += 4 * stride)
+  {
+    dv2s a[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) a[k] = ld(i + k * stride);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) st(i + k * stride, a[k]);
+  }
+  for (; i < n2; i += stride) st(i, ld(i));
+}
+
+void launch_stream_copy(i64 n, const double *x, double *y, int num_cu, hipStream_t s, int mode)
+{
+  const i64 n2 = n / 2;
+  const i64 full = (n2 + kStreamThreads - 1) / kStreamThreads;
+  const int G = (int)std::max<i64>(1, (mode & 2) ? full : std::min<i64>(full, (i64)num_cu * 8));
+  const dv2s *xv = reinterpret_cast<const dv2s *>(x);
+  dv2s *yv = reinterpret_cast<dv2s *>(y);
+  if (n2 > 0) switch (mode & 3)
+    {
+      case 0: hipLaunchKernelGGL(k_stream_copy<0>, dim3(G), dim3(kStreamThreads), 0, s, n2, xv, yv); break;
+      case 1: hipLaunchKernelGGL(k_stream_copy<1>, dim3(G), dim3(kStreamThreads), 0, s, n2, xv, yv); break;
+      case 2: hipLaunchKernelGGL(k_stream_copy<2>, dim3(G), dim3(kStreamThreads), 0, s, n2, xv, yv); break;
+      default: hipLaunchKernelGGL(k_stream_copy<3>, dim3(G), dim3(kStreamThreads), 0, s, n2, xv, yv); break;
+    }
+  if (n & 1) EIG_HIP(hipMemcpyAsync(y + n - 1, x + n - 1, sizeof(double), hipMemcpyDeviceToDevice, s));
+  EIG_HIP(hipGetLastError());
+}
+}  // namespace eigmi

@@ -21,6 +21,7 @@ MAT_NO_BAND, MAT_BAND_GATHER, MAT_NO_STENCIL, MAT_NO_MARCH = 1, 2, 4, 8
 TRSV_AUTO, TRSV_BLOCKINV, TRSV_STAGED, TRSV_CSR = 0, 1, 2, 3
 TRSV_KINDS = {None: TRSV_AUTO, "auto": TRSV_AUTO, "blockinv": TRSV_BLOCKINV, "staged": TRSV_STAGED, "csr": TRSV_CSR}
 COMM_MAILBOX = 1
+STREAM_COPY_MODE = 3  # eig_stream_copy_timed: nontemporal, full grid -- 6.70 TB/s vs 6.28 plain (tools/copy_sweep.py)
 WHICH_LA, WHICH_SA = 0, 1
 LANCZOS_TIME_KERNELS = 1
 LANCZOS_TIME_DETAIL = 2
@@ -107,6 +108,8 @@ SIGNATURES = {
     "eig_mat_create_bcsr_dist_ex": (_int, [_vp, _i64, _i64, _i64, _int, _int, _vp, _vp, _vp, _int,
                                            ctypes.POINTER(_vp)]),
     "eig_lu_set_solver": (_int, [_vp, _int]),
+    "eig_reorder_rcm": (_int, [_i64, _vp, _vp, _vp]),
+    "eig_permute_symmetric": (_int, [_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "eig_mat_destroy": (_int, [_vp]),
     "eig_mat_get_info": (_int, [_vp, ctypes.POINTER(_MatInfo)]),
     "eig_mat_shift_diag": (_int, [_vp, _dbl]),
@@ -120,6 +123,7 @@ SIGNATURES = {
     "eig_axpy": (_int, [_vp, _i64, _dbl, _vp, _vp]),
     "eig_scal": (_int, [_vp, _i64, _dbl, _vp]),
     "eig_copy": (_int, [_vp, _i64, _vp, _vp]),
+    "eig_stream_copy_timed": (_int, [_vp, _i64, _vp, _vp, _int, _int, ctypes.POINTER(_dbl)]),
     "eig_spmm_mv8": (_int, [_vp, _i64, _vp, _vp]),
     "eig_dot_diag_mv8": (_int, [_vp, _i64, _i64, _vp, _vp, _vp]),
     "eig_gram_mv8": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _vp]),
@@ -432,6 +436,18 @@ def scal(ctx, n, a, x):
 
 def copy(ctx, n, x, y):
     ctx.check(lib.eig_copy(ctx.h, n, x.ptr, y.ptr))
+
+
+def stream_copy_GBs(ctx, n=1 << 27, reps=20, mode=None):
+    """Measured HBM copy rate (eig_stream_copy_timed over n doubles, default 1 GiB each way): 16 n B per
+    launch / average launch time, in GB/s."""
+    x, y = ctx.zeros(n), ctx.zeros(n)
+    ms = _dbl(0)
+    ctx.check(lib.eig_stream_copy_timed(ctx.h, n, x.ptr, y.ptr, reps, STREAM_COPY_MODE if mode is None else mode,
+                                        ctypes.byref(ms)))
+    x.free()
+    y.free()
+    return 16.0 * n / (ms.value * 1e-3) / 1e9
 
 
 def spmm_mv8(A, m, Qin, Qout):
@@ -751,6 +767,42 @@ def mm_write(path, rowptr, col, vals, ncols_blocks=None, br=1, bc=1, symmetric=F
                           _np_ptr(col), _np_ptr(vals), int(symmetric))
     if rc != EIG_OK:
         raise EigError(rc, f"eig_mm_write({path})")
+
+
+def reorder_rcm(rowptr, col):
+    """Reverse Cuthill-McKee permutation of the symmetrised pattern (eig_reorder_rcm):
+    perm[k] = old row of new row k."""
+    rowptr = np.ascontiguousarray(rowptr, np.int64)
+    col = np.ascontiguousarray(col, np.int32)
+    perm = np.zeros(rowptr.size - 1, np.int64)
+    rc = lib.eig_reorder_rcm(rowptr.size - 1, _np_ptr(rowptr), _np_ptr(col), _np_ptr(perm))
+    if rc != EIG_OK:
+        raise EigError(rc, lib.eig_last_error(None).decode())
+    return perm
+
+
+def permute_symmetric(rowptr, col, vals, perm):
+    """B = P A P^T, B[k][l] = A[perm[k]][perm[l]], columns ascending (eig_permute_symmetric)."""
+    rowptr = np.ascontiguousarray(rowptr, np.int64)
+    col = np.ascontiguousarray(col, np.int32)
+    vals = np.ascontiguousarray(vals, np.float64)
+    perm = np.ascontiguousarray(perm, np.int64)
+    rp, c, v = np.zeros_like(rowptr), np.zeros_like(col), np.zeros_like(vals)
+    rc = lib.eig_permute_symmetric(rowptr.size - 1, _np_ptr(rowptr), _np_ptr(col), _np_ptr(vals), _np_ptr(perm),
+                                   _np_ptr(rp), _np_ptr(c), _np_ptr(v))
+    if rc != EIG_OK:
+        raise EigError(rc, lib.eig_last_error(None).decode())
+    return rp, c, v
+
+
+def scrambled_rcm(rowptr, col, vals, seed=123):
+    """The general-CSR bench / test matrix: a seeded random symmetric permutation
+    of A followed by reverse Cuthill-McKee -- nnz and symmetry kept, the constant-offset band and
+    the per-slice stencil structure gone, so the explicit-column SELL kernels run."""
+    p0 = np.random.default_rng(seed).permutation(rowptr.size - 1).astype(np.int64)
+    rp, c, v = permute_symmetric(rowptr, col, vals, p0)
+    p1 = reorder_rcm(rp, c)
+    return permute_symmetric(rp, c, v, p1)
 
 
 def row_partition(n, nranks, rank, align=1):

@@ -191,6 +191,12 @@ int eig_nrm2(eig_ctx_t ctx, int64_t n, const double *x, double *result);
 int eig_axpy(eig_ctx_t ctx, int64_t n, double a, const double *x, double *y);   /* y += a x */
 int eig_scal(eig_ctx_t ctx, int64_t n, double a, double *x);                    /* x *= a */
 int eig_copy(eig_ctx_t ctx, int64_t n, const double *x, double *y);
+/* Measurement helper: `reps` launches of a 16-B-per-lane nontemporal stream copy y = x (n doubles;
+ * 16 n bytes moved per launch) bracketed by HIP events; *avg_ms per launch.  The measured HBM peak
+ * the bench's roofline fractions are also quoted against.  mode: bit 0 nontemporal
+ * loads / stores, bit 1 one element per thread over a full grid (else a resident striding grid). */
+int eig_stream_copy_timed(eig_ctx_t ctx, int64_t n, const double *x, double *y, int reps, int mode,
+                          double *avg_ms);
 
 /* ---------------------------------------------------------------- MultiVector<double,8> ---- */
 /* a2: Qout = A Qin, m columns (m % 8 == 0), br = bc = 1 (kernels_cpp.hh:626-657). */
@@ -411,6 +417,14 @@ int eig_gen_matrix_rows(int kind, int N, int64_t row_begin, int64_t nrows, int64
                         int32_t *col, double *vals);
 
 /* ---------------------------------------------------------------- Matrix Market ---------- */
+/* Host reordering for imported (unstructured) matrices: reverse Cuthill-McKee of the symmetrised
+ * pattern of an n x n CSR matrix, perm[k] = old row of new row k (pseudo-peripheral start per
+ * component, neighbours by increasing degree); and B = P A P^T (B[k][l] = A[perm[k]][perm[l]]) with
+ * each row's columns ascending.  Output arrays sized like the input (rowptr n+1, col / vals nnz). */
+int eig_reorder_rcm(int64_t n, const int64_t *rowptr, const int32_t *col, int64_t *perm);
+int eig_permute_symmetric(int64_t n, const int64_t *rowptr, const int32_t *col, const double *vals,
+                          const int64_t *perm, int64_t *rowptr_out, int32_t *col_out, double *vals_out);
+
 /* Import / export of real matrices in Matrix Market coordinate form (the format
  * Dune::storeMatrixMarket writes), host-only.  Read: real | integer | pattern, general | symmetric
  * (mirrored), 1-based, duplicates summed, columns ascending; br > 1 groups the scalar entries into
