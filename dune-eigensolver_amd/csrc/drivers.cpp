@@ -320,18 +320,39 @@ void shifted_copy(eig_mat_s &A, eig_mat_s *B, double sigma, std::vector<i64> &rp
 
 }  // namespace
 
-extern "C" int eig_shift_invert_solve(eig_mat_t A, eig_mat_t B, eig_lu_t lu, double sigma, int nev, int ncv,
-                                      double tol, int maxit, unsigned seed, double *eval_host, double *evec_host,
-                                      int *restarts)
+namespace {
+
+void shift_invert_check(eig_mat_t A, eig_mat_t B)
 {
-  return guard(A ? A->ctx : nullptr, [&] {
-    EIG_CHECK(A && eval_host && nev > 0, EIG_ERR_ARG, "eig_shift_invert_solve: bad argument");
-    check_inverse_matrix(A, "computeGenSymShiftInvertMinMagnitude");
-    if (B)
-    {
-      check_inverse_matrix(B, "computeGenSymShiftInvertMinMagnitude");
-      EIG_CHECK(B->ctx == A->ctx && B->nb_rows == A->nb_rows, EIG_ERR_SHAPE, "shift-invert: A and B sizes differ");
-    }
+  check_inverse_matrix(A, "computeGenSymShiftInvertMinMagnitude");
+  if (B)
+  {
+    check_inverse_matrix(B, "computeGenSymShiftInvertMinMagnitude");
+    EIG_CHECK(B->ctx == A->ctx && B->nb_rows == A->nb_rows, EIG_ERR_SHAPE, "shift-invert: A and B sizes differ");
+  }
+}
+
+// The factorisation of A - sigma B (arpack_geneo_wrapper.hh:597-601): the caller's, or a host one.
+void shift_invert_factor(eig_mat_t A, eig_mat_t B, eig_lu_t lu, double sigma, LuRef &F)
+{
+  if (lu)
+    F.lu = lu;
+  else
+  {
+    std::vector<i64> rp;
+    std::vector<i32> c;
+    std::vector<double> v;
+    EIG_HIP(hipStreamSynchronize(A->ctx->stream));
+    shifted_copy(*A, B, sigma, rp, c, v);
+    factor_host(*A, rp, c, v, F);
+  }
+  EIG_CHECK(lu_size(F.lu) == A->nb_rows, EIG_ERR_SHAPE, "shift-invert: factorisation size differs from A");
+}
+
+// One computeGenSymShiftInvertMinMagnitude solve (ARSymGenEig 'S' mode, "LM") with the factors F.
+void shift_invert_core(eig_mat_t A, eig_mat_t B, const LuRef &F, double sigma, int nev, int ncv, double tol, int maxit,
+                       unsigned seed, double *eval_host, double *evec_host, int *restarts)
+{
     eig_ctx_t ctx = A->ctx;
     EIG_HIP(hipSetDevice(ctx->device));
     hipStream_t s = ctx->stream;
@@ -340,19 +361,6 @@ extern "C" int eig_shift_invert_solve(eig_mat_t A, eig_mat_t B, eig_lu_t lu, dou
     EIG_CHECK(nev < ncv && ncv <= n && ncv <= 500, EIG_ERR_ARG, "shift-invert: need nev < ncv <= min(n, 500)");
     if (tol <= 0.0) tol = 2.220446049250313e-16;  // tol = 0: machine precision (ARPACK)
     if (maxit <= 0) maxit = 100 * nev;            // maxit = 0: 100 nev (ARPACK++)
-    LuRef F;
-    if (lu)
-      F.lu = lu;
-    else
-    {
-      std::vector<i64> rp;
-      std::vector<i32> c;
-      std::vector<double> v;
-      EIG_HIP(hipStreamSynchronize(s));
-      shifted_copy(*A, B, sigma, rp, c, v);
-      factor_host(*A, rp, c, v, F);
-    }
-    EIG_CHECK(lu_size(F.lu) == n, EIG_ERR_SHAPE, "shift-invert: factorisation size differs from A");
     const int m = ncv;
     // basis V and BV (= B V; V itself when B is NULL), column-major, m + 1 vectors each
     DevBuf Vb((size_t)(m + 1) * n * 8), BVb(B ? (size_t)(m + 1) * n * 8 : 8), Wb(n * 8), BWb(n * 8), X8b(n * 64),
@@ -477,8 +485,12 @@ extern "C" int eig_shift_invert_solve(eig_mat_t A, eig_mat_t B, eig_lu_t lu, dou
     for (int i = 0; i < nev; ++i) eval_host[i] = lam[idx[i]];
     if (evec_host)
     {
-      // x = V y purified with the residual direction, x + (beta_m y_m / theta) v_m = OP(V y) / theta
-      // (ARPACK dseupd's purification for the spectral-transformation modes)
+      // purified Ritz vectors (ARPACK dseupd for the spectral-transformation modes): x = OP(V y) /
+      // theta = V y + (beta_m y_m / theta) v_m.  B = I: that linear combination.  Generalised: the
+      // operator applied explicitly to B V y = BV y, x = (A - sigma B)^-1 (BV y) / theta, then
+      // B-normalised -- with a singular B (the harness's partition-of-unity B) the basis picks up
+      // null(B) components through the projections that the B-inner products never see and that
+      // grow over thick restarts; OP maps into range(OP), where they cannot live.
       std::vector<double> coef(m + 1);
       for (int q = 0; q < nev; ++q)
       {
@@ -486,12 +498,69 @@ extern "C" int eig_shift_invert_solve(eig_mat_t A, eig_mat_t B, eig_lu_t lu, dou
         for (int i = 0; i < m; ++i) coef[i] = Y[(size_t)i * m + col];
         coef[m] = betam * Y[(size_t)(m - 1) * m + col] / th[col];
         EIG_HIP(hipMemcpyAsync(cd, coef.data(), (m + 1) * 8, hipMemcpyHostToDevice, s));
-        launch_gemv_n_set(n, m + 1, V, n, cd, nullptr, W, s);
+        if (!B)
+          launch_gemv_n_set(n, m + 1, V, n, cd, nullptr, W, s);
+        else
+        {
+          launch_gemv_n_set(n, m, BV, n, cd, nullptr, BW, s);
+          op(BW, W);
+          bmul(W, BW);
+          const double xb = dot(W, BW);
+          EIG_CHECK(xb > 0.0, EIG_ERR_BREAKDOWN, "shift-invert: purified Ritz vector has no B-norm");
+          launch_scal(n, 1.0 / std::sqrt(xb), W, s);
+        }
         EIG_HIP(hipMemcpyAsync(evec_host + (i64)q * n, W, n * 8, hipMemcpyDeviceToHost, s));
         EIG_HIP(hipStreamSynchronize(s));
       }
     }
     if (restarts) *restarts = nrestart;
+}
+
+}  // namespace
+
+extern "C" int eig_shift_invert_solve(eig_mat_t A, eig_mat_t B, eig_lu_t lu, double sigma, int nev, int ncv,
+                                      double tol, int maxit, unsigned seed, double *eval_host, double *evec_host,
+                                      int *restarts)
+{
+  return guard(A ? A->ctx : nullptr, [&] {
+    EIG_CHECK(A && eval_host && nev > 0, EIG_ERR_ARG, "eig_shift_invert_solve: bad argument");
+    shift_invert_check(A, B);
+    EIG_HIP(hipSetDevice(A->ctx->device));
+    LuRef F;
+    shift_invert_factor(A, B, lu, sigma, F);
+    shift_invert_core(A, B, F, sigma, nev, ncv, tol, maxit, seed, eval_host, evec_host, restarts);
+  });
+}
+
+// computeGenSymShiftInvertMinMagnitudeAdaptive (arpack_geneo_wrapper.hh:661-774): solve with nev =
+// initial_nev; while the largest returned eigenvalue is below `threshold` and nev < max_nev, grow
+// nev to min(max_nev, int(nev * 1.3)) (:770; the comment at :665 says 50 %, the code 1.3) and solve
+// again from the same start (ARPACK++'s default initial guess each pass).  One factorisation of
+// A - sigma B serves every pass.  ncv = 0 (auto) and maxit = nIterationsMax_ * nev as the reference.
+extern "C" int eig_shift_invert_adaptive(eig_mat_t A, eig_mat_t B, eig_lu_t lu, double sigma, double threshold,
+                                         int initial_nev, int max_nev, double tol, int maxit_per_nev, unsigned seed,
+                                         double *eval_host, double *evec_host, int *nev_out, int *passes)
+{
+  return guard(A ? A->ctx : nullptr, [&] {
+    EIG_CHECK(A && eval_host && nev_out && initial_nev > 0 && max_nev > 0, EIG_ERR_ARG,
+              "eig_shift_invert_adaptive: bad argument");
+    // (arpack_geneo_wrapper.hh:693-694: "initial_nev too large")
+    EIG_CHECK(initial_nev <= max_nev, EIG_ERR_ARG, "eig_shift_invert_adaptive: initial_nev too large");
+    shift_invert_check(A, B);
+    EIG_HIP(hipSetDevice(A->ctx->device));
+    LuRef F;
+    shift_invert_factor(A, B, lu, sigma, F);
+    int nev = initial_nev, pass = 0;
+    for (;;)
+    {
+      const int maxit = maxit_per_nev > 0 ? maxit_per_nev * nev : 0;
+      shift_invert_core(A, B, F, sigma, nev, 0, tol, maxit, seed, eval_host, evec_host, nullptr);
+      ++pass;
+      if (eval_host[nev - 1] >= threshold || nev >= max_nev) break;
+      nev = std::min(max_nev, (int)(nev * 1.3));
+    }
+    *nev_out = nev;
+    if (passes) *passes = pass;
   });
 }
 
@@ -1051,7 +1120,10 @@ extern "C" int eig_lanczos_solve(eig_mat_t A, int nev, int ncv, int which, unsig
     init_start(*A, V, nullptr, seed);
     LanczosBufs lb(ncv);
     DevBuf cb((size_t)(ncv + 8) * sizeof(double));
-    DevBuf gate(2 * sizeof(double));  // {||t||^2 after the first pass, before it}
+    // ||t||^2 after the passes, newest first: [n3, n2, n1, n0] (n0 before any); the gate of pass
+    // q is {n_q, n_(q-1)} = &ng[3 - q], as gated_off reads {after, before}
+    DevBuf gate(4 * sizeof(double));
+    double *ng = gate.d();
     launch_nrm2sq(n, V + own, lb.st.nsum, 0, s, ctx->red);
     allreduce_sum(ctx, lb.st.nsum, 1, s);
     hipEvent_t h0, h1;
@@ -1062,13 +1134,15 @@ extern "C" int eig_lanczos_solve(eig_mat_t A, int nev, int ncv, int which, unsig
       double *u = V + (i64)j * W, *up = j > 0 ? V + (i64)(j - 1) * W : V + (i64)j * W, *t = V + (i64)(j + 1) * W;
       lanczos_step(*A, u, up, t, j, lb, nullptr, 0, h0, h1);
       // DGKS as ARPACK's dsaitr runs it: a classical Gram-Schmidt pass against v_0..v_j
-      // (v_q = u_q / sqrt(nsum[q])), then a second one only when the pass removed a large part
-      // of t (||t'|| <= 0.717 ||t||) -- decided on the device from the two norms (gated launches)
-      launch_nrm2sq(n, t + own, gate.d() + 1, 0, s, ctx->red);
-      allreduce_sum(ctx, gate.d() + 1, 1, s);
-      for (int pass = 0; pass < 2; ++pass)
+      // (v_q = u_q / sqrt(nsum[q])); a correction pass only when the previous pass removed a large
+      // part of t (||t'|| <= 0.717 ||t||), at most two corrections; when the second one still
+      // fails the test, t = 0 (dsaitr: r = 0, rnorm = 0 -- an invariant subspace, T_j exact).
+      // Every decision is made on the device from the allreduced norms (gated launches).
+      launch_nrm2sq(n, t + own, ng + 3, 0, s, ctx->red);
+      allreduce_sum(ctx, ng + 3, 1, s);
+      for (int pass = 0; pass < 3; ++pass)
       {
-        const double *g = pass ? gate.d() : nullptr;
+        const double *g = pass ? ng + 3 - pass : nullptr;
         for (int q0 = 0; q0 <= j; q0 += 8 * 48)
         {
           const int kq = std::min(j + 1 - q0, 8 * 48);
@@ -1076,12 +1150,11 @@ extern "C" int eig_lanczos_solve(eig_mat_t A, int nev, int ncv, int which, unsig
         }
         allreduce_sum(ctx, cb.d(), j + 1, s);  // (after a skipped pass: unused)
         launch_gemv_n_sub(n, j + 1, V + own, W, cb.d(), lb.st.nsum, t + own, s, g);
-        if (pass == 0)
-        {
-          launch_nrm2sq(n, t + own, gate.d(), 0, s, ctx->red);
-          allreduce_sum(ctx, gate.d(), 1, s);
-        }
+        // ||t||^2 after this pass (a skipped pass leaves t, so n_q = n_(q-1) and the next gate is off)
+        launch_nrm2sq(n, t + own, ng + 2 - pass, 0, s, ctx->red);
+        allreduce_sum(ctx, ng + 2 - pass, 1, s);
       }
+      launch_zero_gated(n, t + own, ng, s);  // {n3, n2}: the second correction failed too
       launch_nrm2sq(n, t + own, lb.st.nsum + j + 1, 0, s, ctx->red);
       allreduce_sum(ctx, lb.st.nsum + j + 1, 1, s);
     }

@@ -312,6 +312,7 @@ void launch_gemv_t(i64 n, int k, const double *V, i64 ldv, const double *w, doub
 void launch_gemv_n_sub(i64 n, int k, const double *V, i64 ldv, const double *c, const double *scale2, double *w,
                        hipStream_t s, const double *gate = nullptr);
 // y = sum_q V_q * c[q] / sqrt(nsum[q])   (Ritz vector assembly from an unnormalised basis)
+void launch_zero_gated(i64 n, double *w, const double *gate, hipStream_t s);
 void launch_gemv_n_set(i64 n, int k, const double *V, i64 ldv, const double *c, const double *nsum, double *y,
                        hipStream_t s);
 // r = ||A y - theta y|| helper: out = ||x - theta*y||^2

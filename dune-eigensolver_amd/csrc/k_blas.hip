@@ -291,6 +291,16 @@ void launch_gemv_n_sub(i64 n, int k, const double *V, i64 ldv, const double *c, 
   hipLaunchKernelGGL(k_gemv_n, dim3(stream_grid(n, 4)), dim3(kStreamThreads), 0, s, n, k, V, ldv, c, scale2, 0, w,
                      gate);
 }
+// t = 0 when the gate is on (DGKS gave up: dsaitr's r = 0, rnorm = 0); returns at once otherwise
+__global__ __launch_bounds__(kStreamThreads) void k_zero_gated(i64 n, double *__restrict__ w, const double *gate)
+{
+  if (gated_off(gate)) return;
+  for (i64 i = (i64)blockIdx.x * kStreamThreads + threadIdx.x; i < n; i += (i64)gridDim.x * kStreamThreads) w[i] = 0.0;
+}
+void launch_zero_gated(i64 n, double *w, const double *gate, hipStream_t s)
+{
+  hipLaunchKernelGGL(k_zero_gated, dim3(stream_grid(n, 4)), dim3(kStreamThreads), 0, s, n, w, gate);
+}
 void launch_gemv_n_set(i64 n, int k, const double *V, i64 ldv, const double *c, const double *nsum, double *y,
                        hipStream_t s)
 {

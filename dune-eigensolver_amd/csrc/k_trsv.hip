@@ -22,9 +22,11 @@
 // k_binv_chain below; to rounding, not bitwise); EIGMI_TRSV=staged / csr keep the bitwise kernels.
 #include "internal.h"
 
+#include <atomic>
 #include <chrono>
 #include <cstring>
 #include <cstdio>
+#include <thread>
 
 namespace eigmi {
 
@@ -199,7 +201,13 @@ __global__ __launch_bounds__(kTThreads) void k_tsolve(i64 n, const i64 *__restri
 // without per-entry branches.
 constexpr int kRing4 = 4;   // ring slots of the staged kernel (power of two)
 constexpr int kSlab = 128;  // slab entries per row staged at once (LDS: 96 KiB of slab + 32 KiB tile)
-constexpr i64 kBinvTiles = 2048;  // block-inverse image cap (64 x 64 double tiles, both factors)
+// block-inverse image: at most kBinvMaxGD coupled blocks per factor (envelope bandwidth <= 512 rows)
+// and kBinvTiles 64 x 64 double tiles for both factors (1 GiB); a diagonal block whose estimated
+// condition max|D_b| max|inv(D_b)| 64 exceeds kBinvCond keeps the factors on the substitution
+// kernels (products with an inverse of an ill-conditioned block lose what substitution keeps)
+constexpr int kBinvMaxGD = 8;
+constexpr i64 kBinvTiles = 32768;
+constexpr double kBinvCond = 1e6;
 
 struct Staged {
   const i64 *off1;
@@ -367,7 +375,8 @@ __global__ __launch_bounds__(kTThreads) void k_tsolve_staged(i64 n, Staged F, co
 //     x_b = z_b - sum_d G(b, d) x_(b -+ d).
 // z for all blocks is one parallel launch (k_binv_z); the chain over the blocks (k_binv_chain)
 // has no dependency inside a block, so a block costs a few dense 64 x 64 x 8 products and one
-// barrier instead of a 64-step register wavefront.
+// barrier instead of a 64-step register wavefront.  Independent of the staged image: any factor
+// whose off-block entries lie within kBinvMaxGD blocks (the RCM envelope of a 200^2 grid: gd 7).
 //
 // k_binv_z: one workgroup per (64-row block, 8-column block); PERM: y = scale * Qin(P, :) (the
 // row scaling + permutation of the L solve), else y = Y.  Thread (r, s) forms the partial products
@@ -415,22 +424,24 @@ __global__ __launch_bounds__(kThreadsT) void k_binv_z(i64 n, const double *__res
 // which wave s keeps in a private LDS ring (broadcast reads); the partial sums of the 8 slices meet
 // in LDS (double-buffered by block parity, so one barrier per block), and lane (u, c) of wave s
 // finishes x(row s*8+u, column c) = z - sum, the rows its wave needs from this block later.
-// GD = coupled blocks (G tiles per block, gd <= GD at run time).  The G tiles and z of the next PF
+// GD = coupled blocks (G tiles per block, gd <= GD at run time), RING = ring slots (>= GD, power of
+// two).  The G tiles and z of the next PF
 // blocks are in flight in a register ring (PF buffers, the loop unrolled by PF so every buffer index
 // is static).  The partials' rows are padded to 9 doubles: lane r's 8 stores then fall on distinct
 // banks (a 64-B row stride put 8 lanes on each bank pair).
-template <bool LOWER, int GD, int PF>
+template <bool LOWER, int GD, int PF, int RING>
 __global__ __launch_bounds__(kThreadsT) void k_binv_chain(i64 n, int gd, const double *__restrict__ G,
                                                           const double *Z, double *X)
 {
+  static_assert(RING >= GD && (RING & (RING - 1)) == 0, "ring slots");
   __shared__ double part[2][8][kTB][9];
-  __shared__ double ring[8][kRing4][8][8];  // [wave s][slot][row u of slice s][column]
+  __shared__ double ring[8][RING][8][8];  // [wave s][slot][row u of slice s][column]
   const int tid = threadIdx.x, r = tid & 63, s = tid >> 6;
   const int u = r >> 3, c = r & 7;  // the reduction role of lane r
   const i64 cb = (i64)blockIdx.x * n * 8;
   const i64 nblocks = (n + kTB - 1) / kTB;
 #pragma unroll
-  for (int q = 0; q < kRing4; ++q) ring[s][q][u][c] = 0.0;
+  for (int q = 0; q < RING; ++q) ring[s][q][u][c] = 0.0;
   double pg[PF][GD][8], pz[PF];
   // tiles and z of the bi-th block solved.  Every load is unconditional (clamped block, tile and row
   // indices; values past the end are never used or are masked at use), the loop runs a whole number
@@ -481,7 +492,7 @@ __global__ __launch_bounds__(kThreadsT) void k_binv_chain(i64 n, int gd, const d
         if (d < gd && d < bi)  // block blk -+ (d + 1) exists and is solved
         {
           const i64 src = LOWER ? blk - (d + 1) : blk + (d + 1);
-          const double(*xr)[8] = ring[s][src & (kRing4 - 1)];
+          const double(*xr)[8] = ring[s][src & (RING - 1)];
 #pragma unroll
           for (int q = 0; q < 8; ++q)
 #pragma unroll
@@ -501,7 +512,7 @@ __global__ __launch_bounds__(kThreadsT) void k_binv_chain(i64 n, int gd, const d
       const i64 i = blk * kTB + t;
       const bool own = live && i < n;
       const double x = (own ? pz[p] : 0.0) - sum;  // rows past n: 0 (their G columns are zero)
-      ring[s][blk & (kRing4 - 1)][u][c] = x;  // read back by this wave only (LDS is in order per wave)
+      ring[s][blk & (RING - 1)][u][c] = x;  // read back by this wave only (LDS is in order per wave)
       if (own) gst(X + cb + i * 8 + c, x);
       fetch_z(bi + PF, pz[p]);
       __builtin_amdgcn_wave_barrier();
@@ -516,11 +527,13 @@ void launch_binv_chain(int gd, int nblk, i64 n, const double *G, const double *Z
   // prefetch depth by register budget: PF x GD x 8 doubles per thread (512-thread workgroups: up to
   // 256 VGPRs per lane)
   if (gd <= 1)
-    hipLaunchKernelGGL((k_binv_chain<LOWER, 1, 4>), dim3(nblk), dim3(kThreadsT), 0, s, n, gd, G, Z, X);
+    hipLaunchKernelGGL((k_binv_chain<LOWER, 1, 4, 4>), dim3(nblk), dim3(kThreadsT), 0, s, n, gd, G, Z, X);
   else if (gd == 2)
-    hipLaunchKernelGGL((k_binv_chain<LOWER, 2, 3>), dim3(nblk), dim3(kThreadsT), 0, s, n, gd, G, Z, X);
+    hipLaunchKernelGGL((k_binv_chain<LOWER, 2, 3, 4>), dim3(nblk), dim3(kThreadsT), 0, s, n, gd, G, Z, X);
+  else if (gd <= 4)
+    hipLaunchKernelGGL((k_binv_chain<LOWER, 4, 2, 4>), dim3(nblk), dim3(kThreadsT), 0, s, n, gd, G, Z, X);
   else
-    hipLaunchKernelGGL((k_binv_chain<LOWER, 4, 2>), dim3(nblk), dim3(kThreadsT), 0, s, n, gd, G, Z, X);
+    hipLaunchKernelGGL((k_binv_chain<LOWER, 8, 1, 8>), dim3(nblk), dim3(kThreadsT), 0, s, n, gd, G, Z, X);
 }
 
 int grid256(i64 work)
@@ -610,6 +623,20 @@ void build_staged(TrsvImage &img)
 }
 }  // namespace
 
+namespace {
+// f(b0, b1) over contiguous block ranges on up to 16 host threads
+template <class F>
+void parallel_blocks(i64 nb, F &&f)
+{
+  unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  if (nb < 32) nt = 1;
+  if (nt == 1) return f(0, nb);
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < nt; ++t) th.emplace_back([&, t] { f(nb * t / nt, nb * (t + 1) / nt); });
+  for (auto &t : th) t.join();
+}
+}  // namespace
+
 void trsv_upload(eig_ctx_t ctx, i64 n, const std::vector<i64> &lrp, const std::vector<i32> &lc,
                  const std::vector<double> &lv, const std::vector<i64> &urp, const std::vector<i32> &uc,
                  const std::vector<double> &uv, const std::vector<double> &ud, const std::vector<i64> &P,
@@ -661,12 +688,10 @@ void trsv_upload(eig_ctx_t ctx, i64 n, const std::vector<i64> &lrp, const std::v
   };
   phase("split");
   img.staged = fits(lrp, lc, ls, true) && fits(urp, uc, us, false);
-  if (img.staged)
-    img.host = std::make_shared<TrsvHostRows>(TrsvHostRows{lrp, lc, lv, ls, urp, uc, uv, us});
   phase("staged");
-  // block-inverse images (k_binv_z / k_binv_chain) for factors that fit the staged kernel (every
-  // coupling within kRing4 blocks), when the tiles stay small (a 64 x 64 tile per diagonal block
-  // and per coupled block: at most kBinvTiles tiles, i.e. 64 MiB, and a few 1e8 host FMAs)
+  // block-inverse images (k_binv_z / k_binv_chain) for factors whose every coupling lies within
+  // kBinvMaxGD blocks, when the tiles stay within kBinvTiles (a 64 x 64 tile per diagonal block and
+  // per coupled block) and every diagonal block is well conditioned
   const i64 nblocks = (n + kTB - 1) / kTB;
   auto coupled = [&](const std::vector<i64> &rp, const std::vector<i32> &cj, const std::vector<i64> &split,
                      bool lower) {
@@ -676,16 +701,20 @@ void trsv_upload(eig_ctx_t ctx, i64 n, const std::vector<i64> &lrp, const std::v
         dm = std::max<int>(dm, (int)(lower ? i / kTB - cj[q] / kTB : cj[q] / kTB - i / kTB));
     return dm;
   };
+  // returns false (nothing uploaded) when a diagonal block fails the conditioning test
   auto binv_image = [&](int f, const std::vector<i64> &rp, const std::vector<i32> &cj, const std::vector<double> &cv,
-                        const std::vector<i64> &split, const double *diag) {
+                        const std::vector<i64> &split, const double *diag) -> bool {
     const bool lower = diag == nullptr;
     const int gd = img.gd[f];
     const size_t T2 = (size_t)kTB * kTB;
     std::vector<double> dinv((size_t)nblocks * T2, 0.0), gt((size_t)std::max<i64>(nblocks * gd, 1) * T2, 0.0);
+    std::atomic<bool> ok{true};
+    // blocks are independent: threads over contiguous block ranges
+    parallel_blocks(nblocks, [&](i64 b0, i64 b1) {
     // Di holds inv(D_b) by columns (Di[j * 64 + i] = inv(D)[i][j]): each column is one triangular
     // solve with contiguous operands, and it is already the device layout of dinv ([t][r])
     std::vector<double> Db(T2), Di(T2), Tb(T2);
-    for (i64 b = 0; b < nblocks; ++b)
+    for (i64 b = b0; b < b1 && ok.load(std::memory_order_relaxed); ++b)
     {
       const i64 bs = b * kTB, nbr = std::min<i64>(kTB, n - bs);
       // the diagonal block D[r][t] (rows past n: identity)
@@ -714,6 +743,15 @@ void trsv_upload(eig_ctx_t ctx, i64 n, const std::vector<i64> &lrp, const std::v
             for (int k = i + 1; k <= j; ++k) v -= Dr[k] * x[k];
             x[i] = v / Dr[i];
           }
+      }
+      {
+        double dm = 0.0, im = 0.0;
+        for (size_t q = 0; q < T2; ++q)
+        {
+          dm = std::max(dm, std::fabs(Db[q]));
+          im = std::max(im, std::fabs(Di[q]));
+        }
+        if (!(dm * im * kTB <= kBinvCond)) ok = false;  // (NaN included)
       }
       std::copy(Di.begin(), Di.end(), dinv.begin() + (size_t)b * T2);
       // G(b, d) = inv(D_b) T(b, d), T(b, d)[r'][t] = the entry of row bs + r' in column t of block b -+ d
@@ -746,23 +784,35 @@ void trsv_upload(eig_ctx_t ctx, i64 n, const std::vector<i64> &lrp, const std::v
         }
       }
     }
+    });
+    if (!ok) return false;
     img.dinv[f] = upload(dinv);
     img.g[f] = upload(gt);
+    return true;
   };
-  if (img.staged)
   {
     img.gd[0] = coupled(lrp, lc, ls, true);
     img.gd[1] = coupled(urp, uc, us, false);
     const i64 tiles = nblocks * (2 + img.gd[0] + img.gd[1]);
     bool pivots = true;  // a zero U pivot leaves the reference's division to produce inf / nan
     for (i64 i = 0; i < n; ++i) pivots = pivots && ud[i] != 0.0;
-    img.binv = pivots && tiles <= kBinvTiles && img.gd[0] <= kRing4 && img.gd[1] <= kRing4;
+    img.binv = pivots && tiles <= kBinvTiles && img.gd[0] <= kBinvMaxGD && img.gd[1] <= kBinvMaxGD;
     if (img.binv)
     {
-      binv_image(0, lrp, lc, lv, ls, nullptr);
-      binv_image(1, urp, uc, uv, us, ud.data());
+      img.binv = binv_image(0, lrp, lc, lv, ls, nullptr) && binv_image(1, urp, uc, uv, us, ud.data());
+      if (!img.binv)
+        for (int f = 0; f < 2; ++f)
+        {
+          if (img.dinv[f]) (void)hipFree(img.dinv[f]);
+          if (img.g[f]) (void)hipFree(img.g[f]);
+          img.dinv[f] = img.g[f] = nullptr;
+        }
     }
   }
+  // host rows for a later build of the staged image: only when the staged kernel is the default
+  // (no block-inverse image); with one, EIG_TRSV_STAGED takes the row-CSR kernel (bitwise too)
+  if (img.staged && !img.binv)
+    img.host = std::make_shared<TrsvHostRows>(TrsvHostRows{lrp, lc, lv, ls, urp, uc, uv, us});
   phase("binv");
   // the row-CSR factors, permutations and scaling: ONE device allocation and ONE copy (a dozen
   // separate small hipMalloc + hipMemcpy calls cost ~1 ms each)
@@ -837,9 +887,9 @@ void launch_inverse_mv8(TrsvImage &img, i64 m, double *Qin, double *Qout, hipStr
     EIG_HIP(hipGetLastError());
     return;
   }
-  if (img.staged && !img.staged_built && !csr) build_staged(img);
+  if (img.staged && !img.staged_built && !csr && img.host) build_staged(img);
   hipLaunchKernelGGL(k_perm_scale, dim3(grid256(n * nblk)), dim3(256), 0, s, n, nblk, img.P, img.scale, Qin, Qout);
-  if (!img.staged || csr)
+  if (!img.staged_built || csr)
   {
     hipLaunchKernelGGL(k_tsolve<true>, dim3(nblk), dim3(kTThreads), 0, s, n, img.lrp, img.lsplit, img.lc, img.lv,
                        (const double *)nullptr, (const double *)Qout, Qin);

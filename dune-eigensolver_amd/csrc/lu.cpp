@@ -384,6 +384,21 @@ extern "C" int eig_lu_set_solver(eig_lu_t lu, int kind)
   });
 }
 
+extern "C" int eig_lu_solver_info(eig_lu_t lu, int *kind, int *coupled_l, int *coupled_u)
+{
+  return guard(lu ? lu->ctx : nullptr, [&] {
+    EIG_CHECK(lu && lu->ctx, EIG_ERR_ARG, "eig_lu_solver_info: null handle or host-only factors");
+    const TrsvImage &im = lu->img;
+    const bool csr = im.solver == EIG_TRSV_CSR, staged = im.solver == EIG_TRSV_STAGED;
+    if (kind)
+      *kind = (im.binv && !csr && !staged) ? EIG_TRSV_BLOCKINV
+              : (im.staged && !csr && (im.host || im.staged_built)) ? EIG_TRSV_STAGED
+                                                                    : EIG_TRSV_CSR;
+    if (coupled_l) *coupled_l = im.gd[0];
+    if (coupled_u) *coupled_u = im.gd[1];
+  });
+}
+
 extern "C" int eig_lu_export(eig_lu_t lu, int64_t *Lp, int64_t *Lj, double *Lx, int64_t *Up, int64_t *Ui, double *Ux,
                              int64_t *P, int64_t *Q, double *Rs)
 {

@@ -108,6 +108,9 @@ SIGNATURES = {
     "eig_mat_create_bcsr_dist_ex": (_int, [_vp, _i64, _i64, _i64, _int, _int, _vp, _vp, _vp, _int,
                                            ctypes.POINTER(_vp)]),
     "eig_lu_set_solver": (_int, [_vp, _int]),
+    "eig_lu_solver_info": (_int, [_vp, ctypes.POINTER(_int), ctypes.POINTER(_int), ctypes.POINTER(_int)]),
+    "eig_shift_invert_adaptive": (_int, [_vp, _vp, _vp, _dbl, _dbl, _int, _int, _dbl, _int, _u, _vp, _vp,
+                                         ctypes.POINTER(_int), ctypes.POINTER(_int)]),
     "eig_reorder_rcm": (_int, [_i64, _vp, _vp, _vp]),
     "eig_permute_symmetric": (_int, [_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "eig_mat_destroy": (_int, [_vp]),
@@ -628,6 +631,12 @@ class LU:
     def inverse_mv8(self, m, Qin, Qout):
         self.ctx.check(lib.eig_inverse_mv8(self.h, m, Qin.ptr, Qout.ptr))
 
+    def solver_info(self):
+        """-> (kernel in use: "blockinv" | "staged" | "csr", coupled blocks of L, of U)."""
+        k, gl, gu = _int(0), _int(0), _int(0)
+        self._check(lib.eig_lu_solver_info(self.h, ctypes.byref(k), ctypes.byref(gl), ctypes.byref(gu)))
+        return {TRSV_BLOCKINV: "blockinv", TRSV_STAGED: "staged", TRSV_CSR: "csr"}[k.value], gl.value, gu.value
+
     def set_solver(self, kind):
         """kind: None / "auto", "blockinv", "staged" or "csr" (eig_lu_set_solver)."""
         self._check(lib.eig_lu_set_solver(self.h, TRSV_KINDS[kind]))
@@ -672,6 +681,21 @@ def shift_invert_solve(A, nev, sigma=0.0, B=None, ncv=0, tol=0.0, maxit=0, seed=
                                            tol, maxit, seed, _np_ptr(ev), _np_ptr(evec) if want_evec else None,
                                            ctypes.byref(r)))
     return ev, (evec.reshape(nev, A.n) if want_evec else None), r.value
+
+
+def shift_invert_adaptive(A, threshold, initial_nev, max_nev, sigma=0.0, B=None, tol=0.0, maxit_per_nev=0, seed=123,
+                          lu=None, want_evec=True):
+    """computeGenSymShiftInvertMinMagnitudeAdaptive: every eigenvalue below `threshold` (nev grows x1.3
+    from initial_nev up to max_nev) -> (eigenvalues ascending, B-normalised vectors, passes)."""
+    ev = np.zeros(max_nev)
+    evec = np.zeros(max_nev * A.n) if want_evec else None
+    nv, ps = _int(0), _int(0)
+    A.ctx.check(lib.eig_shift_invert_adaptive(A.h, B.h if B is not None else None, lu.h if lu else None, sigma,
+                                              threshold, initial_nev, max_nev, tol, maxit_per_nev, seed, _np_ptr(ev),
+                                              _np_ptr(evec) if want_evec else None, ctypes.byref(nv),
+                                              ctypes.byref(ps)))
+    k = nv.value
+    return ev[:k], (evec[:k * A.n].reshape(k, A.n) if want_evec else None), ps.value
 
 
 class BlockLanczos:

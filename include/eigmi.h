@@ -318,6 +318,9 @@ int eig_lu_info(eig_lu_t lu, int64_t *n, int64_t *lnz, int64_t *unz, int *do_rec
  * rounding. */
 enum { EIG_TRSV_AUTO = 0, EIG_TRSV_BLOCKINV = 1, EIG_TRSV_STAGED = 2, EIG_TRSV_CSR = 3 };
 int eig_lu_set_solver(eig_lu_t lu, int kind);
+/* The kernels eig_inverse_mv8 runs now (*kind: EIG_TRSV_BLOCKINV / _STAGED / _CSR) and the coupled
+ * 64-row blocks of the L / U envelopes (the block-inverse chain takes up to 8). */
+int eig_lu_solver_info(eig_lu_t lu, int *kind, int *coupled_l, int *coupled_u);
 /* Copy the factors out (sizes from eig_lu_info: Lp/Up n+1, Lj/Lx lnz, Ui/Ux unz, P/Q/Rs n). */
 int eig_lu_export(eig_lu_t lu, int64_t *Lp, int64_t *Lj, double *Lx, int64_t *Up, int64_t *Ui, double *Ux,
                   int64_t *P, int64_t *Q, double *Rs);
@@ -356,6 +359,15 @@ int eig_generalized_inverse(eig_mat_t A, eig_mat_t B, eig_lu_t lu, double shift,
  * B-normalised, or NULL; *restarts: thick restarts taken. */
 int eig_shift_invert_solve(eig_mat_t A, eig_mat_t B, eig_lu_t lu, double sigma, int nev, int ncv, double tol,
                            int maxit, unsigned seed, double *eval_host, double *evec_host, int *restarts);
+/* computeGenSymShiftInvertMinMagnitudeAdaptive (arpack_geneo_wrapper.hh:661-774): every eigenvalue of
+ * the pencil below `threshold`, nev growing from initial_nev by x1.3 (the reference's code) up to
+ * max_nev (= the reference's x.size()); one factorisation of A - sigma B for all passes.  Outputs
+ * as eig_shift_invert_solve for the final nev (*nev_out; eval_host / evec_host sized for max_nev):
+ * ascending, the last one >= threshold unless nev reached max_nev.  maxit_per_nev: restarts allowed
+ * per eigenvalue (the reference's nIterationsMax_; <= 0: 100 nev). */
+int eig_shift_invert_adaptive(eig_mat_t A, eig_mat_t B, eig_lu_t lu, double sigma, double threshold, int initial_nev,
+                              int max_nev, double tol, int maxit_per_nev, unsigned seed, double *eval_host,
+                              double *evec_host, int *nev_out, int *passes);
 
 /* ---------------------------------------------------------------- block Lanczos (config C5) */
 /* Generalised symmetric-definite eigenproblem K x = lambda M x by block Lanczos in the M-inner

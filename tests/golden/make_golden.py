@@ -87,6 +87,22 @@ def geneo():
                         geneo_v=v[:, o], p1_N=8, p1_w=np.sort(pw))
 
 
+def geneo_adaptive():
+    """computeGenSymShiftInvertMinMagnitudeAdaptive (arpack_geneo_wrapper.hh:661-774) on the harness
+    pencil at N = 32: the 40 eigenvalues nearest sigma = -1e-3 from ARPACK (eigsh "LM", tol 1e-14),
+    ascending, and a threshold halfway between the 11th and 12th (distinct values; the 10th and 11th are
+    a double eigenvalue), so that nev = 4 grows 4 -> 5 -> 6 -> 7 -> 9 -> 11 -> 14 (x1.3, int) and stops
+    at 14 with ev[13] >= threshold."""
+    N, shift = 32, 1e-3
+    A = oracle.laplace2d(N, "neumann").to_scipy()
+    B = oracle.laplace2d(N, "pu", overlap=3).to_scipy()
+    w = np.sort(ssl.eigsh(A, k=40, M=B, sigma=-shift, which="LM", tol=1e-14, v0=np.ones(A.shape[0]),
+                          return_eigenvectors=False))
+    thr = 0.5 * (w[10] + w[11])
+    np.savez_compressed(os.path.join(HERE, "geneo_adaptive_arpack.npz"), N=N, shift=shift, w=w, threshold=thr,
+                        initial_nev=4, max_nev=40)
+
+
 def reference_run():
     rec = {
         "source": "SURVEY.md section 6 / BASELINE.md section 2: reference headers multivector.hh + kernels_cpp.hh + "
@@ -108,5 +124,6 @@ if __name__ == "__main__":
     poisson3d()
     q1elast()
     geneo()
+    geneo_adaptive()
     reference_run()
     print("golden fixtures written to", HERE)

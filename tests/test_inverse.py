@@ -150,6 +150,38 @@ def test_inverse_mv8_bitwise(ctx, name, m, via, kernel):
 
 
 @pytest.mark.gpu
+def test_inverse_mv8_interior_shift(ctx):
+    """factors of an interior shift (laplace2d(32) - sigma I, sigma between lambda_5 and
+    lambda_6) -- small U pivots.  Either the block-inverse image is refused for an ill-conditioned
+    diagonal block (kBinvCond) and the default is a bitwise substitution kernel, or its result stays
+    within 1e-11 of the reference arithmetic relative to max |x|."""
+    A = oracle.laplace2d(32)
+    N = 32
+    s1 = 4 * np.sin(np.arange(1, N + 1) * np.pi / (N + 1) / 2) ** 2
+    lam = np.sort((s1[:, None] + s1[None, :]).ravel())
+    sigma = 0.5 * (lam[5] + lam[6]) + 1e-3
+    A.val[A.col == np.repeat(np.arange(A.n), np.diff(A.rowptr))] -= sigma
+    lu, f = _gpu_lu(ctx, A, "bcsr")
+    X = oracle.random_mv8(A.n, 8, 4)
+    ref_out, _ = oracle.inverse_mv8(f, X, 8)
+    din, dout = ctx.array(X), ctx.zeros(A.n * 8)
+    lu.inverse_mv8(8, din, dout)
+    out = dout.get()
+    used, _, _ = lu.solver_info()
+    err = np.abs(out - ref_out).max() / np.abs(ref_out).max()
+    print(f"interior shift: kernel {used}, vs reference arithmetic {err:.2e}")
+    if used == "blockinv":
+        assert err <= 1e-11
+    else:
+        assert np.array_equal(out, ref_out)
+    with trsv_kernel(lu, "staged"):
+        din = ctx.array(X)
+        lu.inverse_mv8(8, din, dout)
+    assert np.array_equal(dout.get(), ref_out)
+    lu.close()
+
+
+@pytest.mark.gpu
 def test_inverse_mv8_do_recip(ctx):
     A = oracle.poisson3d(6)
     lu, f = _gpu_lu(ctx, A, "factors", recip=True)
@@ -233,7 +265,8 @@ def test_generalized_inverse_pu_mass(ctx):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["laplace2d_64", "laplace2d_100", "poisson3d_12", "poisson3d_16", "poisson3d_20"])
+@pytest.mark.parametrize("name", ["laplace2d_64", "laplace2d_100", "laplace2d_150", "poisson3d_12", "poisson3d_16",
+                                  "poisson3d_20", "laplace2d_200"])
 @pytest.mark.parametrize("kernel", ["staged", "csr", None])
 def test_inverse_mv8_kernels(ctx, name, kernel):
     """The bitwise triangular-solve kernels (k_tsolve_staged: envelope factors of bandwidth <= 256;
@@ -241,11 +274,18 @@ def test_inverse_mv8_kernels(ctx, name, kernel):
     solve (factors that fit the staged image) to BINV_RTOL.  poisson3d_20's RCM envelope reaches
     past 256 rows: it always takes k_tsolve.  laplace2d_100: n = 10000, a ragged last block.  The
     block-inverse chain's coupled-block counts: laplace2d_64 1, laplace2d_100 / poisson3d_12 2,
-    poisson3d_16 4 (RCM bandwidth 200)."""
+    poisson3d_16 4 (RCM bandwidth 200).  The block-inverse chain is independent of the staged image
+    (coupled distances 3 and up to 8 compared with the reference arithmetic):
+    laplace2d_150 3, poisson3d_20 and laplace2d_200 (the reference's ev.N, n = 40000) 5-8."""
     A = {"laplace2d_64": lambda: oracle.laplace2d(64), "laplace2d_100": lambda: oracle.laplace2d(100),
+         "laplace2d_150": lambda: oracle.laplace2d(150), "laplace2d_200": lambda: oracle.laplace2d(200),
          "poisson3d_12": lambda: oracle.poisson3d(12),
          "poisson3d_16": lambda: oracle.poisson3d(16), "poisson3d_20": lambda: oracle.poisson3d(20)}[name]()
     lu, f = _gpu_lu(ctx, A, "bcsr")
+    used, gl, gu = lu.solver_info()
+    print(f"{name}: default kernel {used}, coupled blocks L {gl} U {gu}")
+    if name in ("laplace2d_150", "laplace2d_200", "poisson3d_20"):
+        assert used == "blockinv" and max(gl, gu) >= 3
     X = oracle.random_mv8(A.n, 16, 3)
     ref_out, _ = oracle.inverse_mv8(f, X, 16)
     with trsv_kernel(lu, kernel):

@@ -96,3 +96,35 @@ def test_argument_errors(ctx):
     with pytest.raises(eigmi.EigShapeError):
         B = oracle.laplace2d(5, "identity")
         eigmi.shift_invert_solve(up(ctx, A), 2, sigma=0.1, B=up(ctx, B))  # sizes differ
+
+
+@pytest.mark.gpu
+def test_adaptive_threshold_vs_arpack(ctx, golden_dir):
+    """computeGenSymShiftInvertMinMagnitudeAdaptive (arpack_geneo_wrapper.hh:661-774) on the harness
+    pencil (Neumann A, PU-masked B, sigma = -1e-3) against ARPACK's 40 eigenvalues nearest sigma
+    (tests/golden/geneo_adaptive_arpack.npz): nev grows 4 -> 5 -> 6 -> 7 -> 9 -> 11 -> 14 (x1.3) and
+    stops when the largest returned eigenvalue reaches the threshold; every returned eigenvalue
+    within 1e-10 of ARPACK's."""
+    import os
+    g = np.load(os.path.join(golden_dir, "geneo_adaptive_arpack.npz"))
+    N, shift, w, thr = int(g["N"]), float(g["shift"]), g["w"], float(g["threshold"])
+    i0, mx = int(g["initial_nev"]), int(g["max_nev"])
+    # the reference loop replayed on ARPACK's eigenvalues
+    nev, passes = i0, 1
+    while w[nev - 1] < thr and nev < mx:
+        nev = min(mx, int(nev * 1.3))
+        passes += 1
+    assert (nev, passes) == (14, 7)
+    An, Bp = oracle.laplace2d(N, "neumann"), oracle.laplace2d(N, "pu", overlap=3)
+    dA = eigmi.Matrix.from_bcsr(ctx, An.rowptr, An.col, An.val)
+    dB = eigmi.Matrix.from_bcsr(ctx, Bp.rowptr, Bp.col, Bp.val)
+    ev, X, p = eigmi.shift_invert_adaptive(dA, thr, i0, mx, sigma=-shift, B=dB)
+    assert len(ev) == nev and p == passes
+    assert ev[-1] >= thr and np.all(ev[:-1] <= ev[1:])
+    assert np.max(np.abs(ev - w[:nev])) < 1e-10
+    check_vectors(An.to_scipy().toarray(), Bp.to_scipy().toarray(), ev, X)
+    # max_nev caps the growth; initial_nev > max_nev is the reference's "initial_nev too large"
+    ev2, _, p2 = eigmi.shift_invert_adaptive(dA, 10.0, 4, 6, sigma=-shift, B=dB, want_evec=False)
+    assert len(ev2) == 6 and p2 == 3 and np.max(np.abs(ev2 - w[:6])) < 1e-10
+    with pytest.raises(eigmi.EigError):
+        eigmi.shift_invert_adaptive(dA, 1.0, 8, 4, sigma=-shift, B=dB)
