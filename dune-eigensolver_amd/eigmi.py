@@ -10,7 +10,9 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libeigmi.so")
+# EIGMI_LIB_VARIANT=san loads the host-sanitizer build (make sanitize; tests/test_sanitize.py only)
+LIB_PATH = os.path.join(_HERE, "lib", "libeigmi_san.so" if os.environ.get("EIGMI_LIB_VARIANT") == "san"
+                        else "libeigmi.so")
 
 EIG_OK, EIG_ERR_SHAPE, EIG_ERR_BLOCKSIZE, EIG_ERR_HIP, EIG_ERR_RCCL, EIG_ERR_BREAKDOWN, EIG_ERR_ARG, EIG_ERR_NODEVICE = range(8)
 ORTHO_MGS, ORTHO_CHOLQR = 0, 1
