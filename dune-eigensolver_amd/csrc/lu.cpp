@@ -18,6 +18,10 @@
 #include <numeric>
 #include <vector>
 
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+
 #include "internal.h"
 
 using namespace eigmi;
@@ -105,6 +109,20 @@ std::vector<i64> rcm(i64 n, const std::vector<std::vector<i64>> &adj)
   }
   std::reverse(perm.begin(), perm.end());
   return perm;
+}
+
+// sum_t a[t] b[t] over a contiguous range with 8 independent partial sums, so the loop runs on
+// SIMD accumulators instead of one serial chain (the envelope LU is O(n bw^2) of these dot
+// products; its rounding is not part of any parity claim -- solves are checked against the
+// exported factors).  AVX2 clone where the host has it.
+__attribute__((target_clones("avx2", "default"))) double env_dot(const double *a, const double *b, i64 len)
+{
+  double s[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  i64 t = 0;
+  for (; t + 8 <= len; t += 8)
+    for (int q = 0; q < 8; ++q) s[q] += a[t + q] * b[t + q];
+  for (; t < len; ++t) s[0] += a[t] * b[t];
+  return ((s[0] + s[4]) + (s[1] + s[5])) + ((s[2] + s[6]) + (s[3] + s[7]));
 }
 
 }  // namespace
@@ -231,6 +249,15 @@ extern "C" int eig_lu_create_bcsr(eig_ctx_t ctx, int64_t nb_rows, int br, const 
     if (ctx) EIG_HIP(hipSetDevice(ctx->device));
     const i64 n = nb_rows * br;
     EIG_CHECK(n < (int64_t)INT32_MAX, EIG_ERR_SHAPE, "eig_lu_create_bcsr: too large");
+    // EIGMI_TRACE_SETUP=1: phase times on stderr (as trsv_upload)
+    const bool trace = std::getenv("EIGMI_TRACE_SETUP") != nullptr;
+    auto t_last = std::chrono::steady_clock::now();
+    auto phase = [&](const char *what) {
+      if (!trace) return;
+      const auto now = std::chrono::steady_clock::now();
+      fprintf(stderr, "lu_create  %-10s %8.2f ms\n", what, std::chrono::duration<double, std::milli>(now - t_last).count());
+      t_last = now;
+    };
     // scalar entries of the block matrix (zeros skipped, as umfpacktools.hh:66-93 does)
     std::vector<std::vector<std::pair<i64, double>>> rowsA(n);
     for (i64 rb = 0; rb < nb_rows; ++rb)
@@ -255,7 +282,9 @@ extern "C" int eig_lu_create_bcsr(eig_ctx_t ctx, int64_t nb_rows, int br, const 
       std::sort(a.begin(), a.end());
       a.erase(std::unique(a.begin(), a.end()), a.end());
     }
+    phase("rows+adj");
     std::vector<i64> perm = rcm(n, adj), inv(n);
+    phase("rcm");
     for (i64 k = 0; k < n; ++k) inv[perm[k]] = k;
     std::vector<double> Rs(n, 0.0);
     for (i64 i = 0; i < n; ++i)
@@ -288,6 +317,7 @@ extern "C" int eig_lu_create_bcsr(eig_ctx_t ctx, int64_t nb_rows, int br, const 
         else U[off[j] + (k - f[j])] = v;  // B[k][j], j > k: column j of U, row k
       }
     }
+    phase("scatter");
     auto Lat = [&](i64 r, i64 c) -> double & { return L[off[r] + (c - f[r])]; };
     auto Uat = [&](i64 r, i64 c) -> double & { return U[off[c] + (r - f[c])]; };  // r < c
     for (i64 k = 0; k < n; ++k)
@@ -295,47 +325,56 @@ extern "C" int eig_lu_create_bcsr(eig_ctx_t ctx, int64_t nb_rows, int br, const 
       // column k of U, rows f_k .. k-1
       for (i64 i = f[k]; i < k; ++i)
       {
-        double s = Uat(i, k);
-        for (i64 t = std::max(f[i], f[k]); t < i; ++t) s -= Lat(i, t) * Uat(t, k);
-        Uat(i, k) = s;
+        const i64 t0 = std::max(f[i], f[k]);
+        Uat(i, k) -= env_dot(&Lat(i, t0), &Uat(t0, k), i - t0);
       }
       // row k of L, columns f_k .. k-1
       for (i64 j = f[k]; j < k; ++j)
       {
-        double s = Lat(k, j);
-        for (i64 t = std::max(f[k], f[j]); t < j; ++t) s -= Lat(k, t) * Uat(t, j);
+        const i64 t0 = std::max(f[k], f[j]);
+        const double s = Lat(k, j) - env_dot(&Lat(k, t0), &Uat(t0, j), j - t0);
         EIG_CHECK(D[j] != 0.0, EIG_ERR_BREAKDOWN, "LU: zero pivot (matrix needs pivoting)");
         Lat(k, j) = s / D[j];
       }
-      double s = D[k];
-      for (i64 t = f[k]; t < k; ++t) s -= Lat(k, t) * Uat(t, k);
+      double s = D[k] - env_dot(&Lat(k, f[k]), &Uat(f[k], k), k - f[k]);
       EIG_CHECK(s != 0.0 && std::isfinite(s), EIG_ERR_BREAKDOWN, "LU: zero pivot (matrix needs pivoting)");
       D[k] = s;
     }
     // exported form: L rows ascending + unit diagonal last; U columns ascending + diagonal last
-    std::vector<i64> Lp(n + 1, 0), Lj, Up(n + 1, 0), Ui;
-    std::vector<double> Lx, Ux;
+    phase("factor");
+    std::vector<i64> Lp(n + 1, 0), Up(n + 1, 0);
     for (i64 k = 0; k < n; ++k)
     {
+      i64 cl = 1, cu = 1;  // + the unit / pivot diagonal
+      for (i64 j = f[k]; j < k; ++j) cl += Lat(k, j) != 0.0;
+      for (i64 i = f[k]; i < k; ++i) cu += Uat(i, k) != 0.0;
+      Lp[k + 1] = Lp[k] + cl;
+      Up[k + 1] = Up[k] + cu;
+    }
+    std::vector<i64> Lj(Lp[n]), Ui(Up[n]);
+    std::vector<double> Lx(Lp[n]), Ux(Up[n]);
+    for (i64 k = 0; k < n; ++k)
+    {
+      i64 q = Lp[k];
       for (i64 j = f[k]; j < k; ++j)
         if (Lat(k, j) != 0.0)
         {
-          Lj.push_back(j);
-          Lx.push_back(Lat(k, j));
+          Lj[q] = j;
+          Lx[q++] = Lat(k, j);
         }
-      Lj.push_back(k);
-      Lx.push_back(1.0);
-      Lp[k + 1] = (i64)Lj.size();
+      Lj[q] = k;
+      Lx[q] = 1.0;
+      q = Up[k];
       for (i64 i = f[k]; i < k; ++i)
         if (Uat(i, k) != 0.0)
         {
-          Ui.push_back(i);
-          Ux.push_back(Uat(i, k));
+          Ui[q] = i;
+          Ux[q++] = Uat(i, k);
         }
-      Ui.push_back(k);
-      Ux.push_back(D[k]);
-      Up[k + 1] = (i64)Ui.size();
+      Ui[q] = k;
+      Ux[q] = D[k];
     }
+    phase("export");
     auto *lu = new eig_lu_s();
     try
     {
@@ -352,6 +391,7 @@ extern "C" int eig_lu_create_bcsr(eig_ctx_t ctx, int64_t nb_rows, int br, const 
       lu->Q = perm;
       lu->Rs = std::move(Rs);
       if (ctx) build_device(*lu);  // ctx == NULL: host-only factors (export / tests)
+      phase("device");
     }
     catch (...)
     {
