@@ -23,6 +23,11 @@ struct eig_blanczos_s {
   eig_mat_s *K = nullptr, *M = nullptr;
   int b = 32, max_steps = 0, k = 0, degree = 36;
   double lmin = 0.5, lmax = 2.5;
+  // spectral transformation (eig_blanczos_create_si): Lanczos on OP = Ks^-1 M, Ks = K - sigma M,
+  // the inner solve by `degree` Chebyshev-Jacobi steps on Ks with D^-1 Ks in [lmin, lmax]
+  bool si = false;
+  eig_mat_s *Ks = nullptr;
+  double sigma = 0.0;
   i64 ld = 0, own = 0, n = 0;
   DevBuf *V = nullptr;                   // (max_steps + 1) * b columns, window layout
   DevBuf *W = nullptr, *Xa = nullptr, *Xb = nullptr, *MZ = nullptr;  // b columns each
@@ -40,6 +45,11 @@ struct eig_blanczos_s {
     delete small;
   }
 };
+
+namespace {
+// the matrix whose diagonal / Chebyshev solve the operator uses: M (M^-1 K) or Ks (shift-invert)
+eig_mat_s &solve_mat(eig_blanczos_s &w) { return w.si ? *w.Ks : *w.M; }
+}  // namespace
 
 namespace {
 
@@ -131,14 +141,15 @@ void check_pair(const eig_mat_s *K, const eig_mat_s *M)
 
 }  // namespace
 
-extern "C" int eig_blanczos_create(eig_mat_t K, eig_mat_t M, int block, int max_steps, int degree, double lmin,
-                                   double lmax, unsigned seed, eig_blanczos_t *out)
+namespace {
+void blanczos_create(eig_mat_t K, eig_mat_t M, eig_mat_t Ks, double sigma, int block, int max_steps, int degree,
+                     double lmin, double lmax, unsigned seed, eig_blanczos_t *out)
 {
-  return guard(K ? K->ctx : nullptr, [&] {
     EIG_CHECK(out && block >= 8 && block <= 32 && block % 8 == 0 && max_steps >= 1 && degree >= 1 && lmin > 0.0 &&
                   lmax > lmin,
               EIG_ERR_ARG, "eig_blanczos_create: block in {8,16,24,32}, max_steps >= 1, degree >= 1, 0 < lmin < lmax");
     check_pair(K, M);
+    if (Ks) check_pair(Ks, M);
     EIG_CHECK((i64)(max_steps + 1) * block <= K->nb_rows_global, EIG_ERR_SHAPE,
               "eig_blanczos_create: (max_steps + 1) * block exceeds the matrix size");
     eig_ctx_t ctx = K->ctx;
@@ -149,6 +160,9 @@ extern "C" int eig_blanczos_create(eig_mat_t K, eig_mat_t M, int block, int max_
     {
       w->K = K;
       w->M = M;
+      w->si = Ks != nullptr;
+      w->Ks = Ks;
+      w->sigma = sigma;
       w->b = block;
       w->max_steps = max_steps;
       w->degree = degree;
@@ -167,7 +181,7 @@ extern "C" int eig_blanczos_create(eig_mat_t K, eig_mat_t M, int block, int max_
       w->small = new DevBuf((size_t)(max_steps + 2) * block * block * sizeof(double) * 2);
       EIG_HIP(hipMemsetAsync(w->V->d(), 0, w->V->bytes(), s));
       for (DevBuf *d : {w->W, w->Xa, w->Xb, w->MZ}) EIG_HIP(hipMemsetAsync(d->d(), 0, d->bytes(), s));
-      launch_diag_inv(*M, w->dinv->d(), s);
+      launch_diag_inv(Ks ? *Ks : *M, w->dinv->d(), s);
       // start block: mt19937(seed) + normal(0,1) in MultiVector fill order (block, row, col) over
       // the GLOBAL rows (eigensolver.hh:49-55), this rank keeps its own rows
       {
@@ -194,6 +208,29 @@ extern "C" int eig_blanczos_create(eig_mat_t K, eig_mat_t M, int block, int max_
       throw;
     }
     *out = w;
+}
+}  // namespace
+
+extern "C" int eig_blanczos_create(eig_mat_t K, eig_mat_t M, int block, int max_steps, int degree, double lmin,
+                                   double lmax, unsigned seed, eig_blanczos_t *out)
+{
+  return guard(K ? K->ctx : nullptr, [&] {
+    blanczos_create(K, M, nullptr, 0.0, block, max_steps, degree, lmin, lmax, seed, out);
+  });
+}
+
+// Spectral transformation (shift-invert, ARPACK mode 3's operator, arpack_geneo_wrapper.hh:581-658):
+// Lanczos in the M-inner product on OP = (K - sigma M)^-1 M, whose largest |theta| are the pencil's
+// eigenvalues nearest sigma, lambda = sigma + 1 / theta -- the end of the spectrum GeneralizedInverse
+// (eigensolver.hh:204-351) returns.  Ks = K - sigma M is given by the caller (Ks = K for sigma = 0);
+// its solve is `degree` Chebyshev-Jacobi steps with the spectrum of diag(Ks)^-1 Ks in [lmin, lmax]
+// (reduction-free, like the mass solve).
+extern "C" int eig_blanczos_create_si(eig_mat_t K, eig_mat_t M, eig_mat_t Ks, double sigma, int block, int max_steps,
+                                      int degree, double lmin, double lmax, unsigned seed, eig_blanczos_t *out)
+{
+  return guard(K ? K->ctx : nullptr, [&] {
+    EIG_CHECK(Ks, EIG_ERR_ARG, "eig_blanczos_create_si: Ks = K - sigma M required (K itself for sigma = 0)");
+    blanczos_create(K, M, Ks, sigma, block, max_steps, degree, lmin, lmax, seed, out);
   });
 }
 
@@ -225,15 +262,29 @@ extern "C" int eig_blanczos_step(eig_blanczos_t w, int steps, eig_blanczos_timin
       hipEvent_t *e = &ev[(size_t)5 * i];
       double *Vj = w->V->d() + (size_t)j * bs;
       EIG_HIP(hipEventRecord(e[0], s));
-      // W = K V_j;  A_j = V_j^T W
-      halo_mv(*w->K, Vj, b, s);
-      launch_sell_mv8(*w->K, b, Vj, w->W->d(), s);
-      launch_panel_gram(ctx, n, ld, b, b, Vj + own * 8, w->W->d() + own * 8, Ad, s);
-      allreduce_sum(ctx, Ad, (i64)b * b, s);
-      EIG_HIP(hipEventRecord(e[1], s));
-      // Z = M^-1 W
-      double *Z = cheb_solve(*w->M, b, w->degree, w->lmin, w->lmax, w->W->d(), w->dinv->d(), w->Xa->d(), w->Xb->d(), s);
-      EIG_HIP(hipEventRecord(e[2], s));
+      double *Z;
+      if (!w->si)
+      {
+        // W = K V_j;  A_j = V_j^T W;  Z = M^-1 W
+        halo_mv(*w->K, Vj, b, s);
+        launch_sell_mv8(*w->K, b, Vj, w->W->d(), s);
+        launch_panel_gram(ctx, n, ld, b, b, Vj + own * 8, w->W->d() + own * 8, Ad, s);
+        allreduce_sum(ctx, Ad, (i64)b * b, s);
+        EIG_HIP(hipEventRecord(e[1], s));
+        Z = cheb_solve(*w->M, b, w->degree, w->lmin, w->lmax, w->W->d(), w->dinv->d(), w->Xa->d(), w->Xb->d(), s);
+        EIG_HIP(hipEventRecord(e[2], s));
+      }
+      else
+      {
+        // W = M V_j;  Z = Ks^-1 W = OP V_j;  A_j = V_j^T M Z = W^T Z
+        halo_mv(*w->M, Vj, b, s);
+        launch_sell_mv8(*w->M, b, Vj, w->W->d(), s);
+        EIG_HIP(hipEventRecord(e[1], s));
+        Z = cheb_solve(*w->Ks, b, w->degree, w->lmin, w->lmax, w->W->d(), w->dinv->d(), w->Xa->d(), w->Xb->d(), s);
+        launch_panel_gram(ctx, n, ld, b, b, w->W->d() + own * 8, Z + own * 8, Ad, s);
+        allreduce_sum(ctx, Ad, (i64)b * b, s);
+        EIG_HIP(hipEventRecord(e[2], s));
+      }
       // two CGS passes against V_0..V_j in the M-inner product: C = V^T (M Z), Z -= V C
       const i64 m1 = (i64)(j + 1) * b;
       for (int pass = 0; pass < 2; ++pass)
@@ -333,7 +384,22 @@ extern "C" int eig_blanczos_ritz(eig_blanczos_t w, int nev, int which, double *e
     std::vector<double> T = assemble_T(*w), th, S;
     sym_eig(N, T, th, S);
     std::vector<int> pick(nev);
-    for (int i = 0; i < nev; ++i) pick[i] = (which == EIG_WHICH_LA) ? N - 1 - i : i;
+    if (!w->si)
+      for (int i = 0; i < nev; ++i) pick[i] = (which == EIG_WHICH_LA) ? N - 1 - i : i;
+    else
+    {
+      // the nev Ritz values of OP of largest |theta| (eigenvalues nearest sigma), ordered by
+      // lambda = sigma + 1 / theta: ascending (SA) or descending (LA)
+      std::vector<int> ord(N);
+      for (int i = 0; i < N; ++i) ord[i] = i;
+      std::stable_sort(ord.begin(), ord.end(), [&](int a, int c) { return std::fabs(th[a]) > std::fabs(th[c]); });
+      ord.resize(nev);
+      for (int i = 0; i < N; ++i) th[i] = th[i] != 0.0 ? w->sigma + 1.0 / th[i] : HUGE_VAL;
+      std::stable_sort(ord.begin(), ord.end(), [&](int a, int c) {
+        return which == EIG_WHICH_SA ? th[a] < th[c] : th[a] > th[c];
+      });
+      pick = ord;
+    }
     for (int i = 0; i < nev; ++i) eval_host[i] = th[pick[i]];
     if (!evec_host && !resid_host) return;
     const i64 n = w->n, ld = w->ld, own = w->own;

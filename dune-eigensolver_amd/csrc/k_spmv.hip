@@ -1318,7 +1318,7 @@ template <class MT, int EPI>
 __global__ __launch_bounds__(kStreamThreads, 6) void k_spmm8_marchg(
     i64 nrows, i64 own, i64 ld, SellB1 A, MarchPlan mp, GSpans sp, const double *__restrict__ X,
     double *__restrict__ Y, const double *__restrict__ Bv, const double *__restrict__ dinv, double omega,
-    double gamma)
+    double gamma, int nblk, int pw)
 {
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int rq = lane >> 2, cp = lane & 3;
@@ -1331,11 +1331,9 @@ __global__ __launch_bounds__(kStreamThreads, 6) void k_spmm8_marchg(
   // (Measured and dropped at 256^3, m = 32: the workgroup's 4 waves on the 4 column blocks of one
   // item, so the band values / mask / D^-1 are fetched once per 4 blocks -- 6.62 vs 6.73 ms, with
   // any number of plane runs per column; rocprof: L2 misses on the gathered X rows dominate.)
-  const int item = (int)swizzled_block() * kWaves + wave;
-  if (item >= mp.ncol * mp.nseg) return;
-  const int col = item % mp.ncol, seg = item / mp.ncol;
+  auto march_item = [&](int col, int seg, int blk) {
   const int z0 = (int)(mp.zb + seg * mp.nplanes / mp.nseg), z1 = (int)(mp.zb + (seg + 1) * mp.nplanes / mp.nseg);
-  const i64 boff = (i64)blockIdx.y * ld * 8;
+  const i64 boff = (i64)blk * ld * 8;
   const dpair *Xb = reinterpret_cast<const dpair *>(X + boff) + cp;
   dpair *Yb = reinterpret_cast<dpair *>(Y + boff) + cp;
   const dpair *Bb = EPI == kGCheb ? reinterpret_cast<const dpair *>(Bv + boff) + cp : nullptr;
@@ -1402,6 +1400,24 @@ __global__ __launch_bounds__(kStreamThreads, 6) void k_spmm8_marchg(
     pm = pcur;
     pcur = pP;
     amP = aP;
+  }
+  };
+  if (pw == 0)
+  {
+    const int item = (int)swizzled_block() * kWaves + wave;
+    if (item >= mp.ncol * mp.nseg) return;
+    march_item(item % mp.ncol, item / mp.ncol, (int)blockIdx.y);
+    return;
+  }
+  // persistent: XCD x (workgroups b = x mod 8) owns columns [x ncol / 8, (x + 1) ncol / 8) and its
+  // waves walk that range block by block, plane run by plane run, consecutive columns together
+  const int x = (int)(blockIdx.x & 7), i = (int)(blockIdx.x >> 3), wx = (int)(gridDim.x >> 3);
+  const int c0 = mp.ncol * x / 8, nc = mp.ncol * (x + 1) / 8 - c0;
+  const int total = nc * mp.nseg * nblk;
+  for (int it = i * kWaves + wave; it < total; it += wx * kWaves)
+  {
+    const int colx = it % nc, rest = it / nc;
+    march_item(c0 + colx, rest % mp.nseg, rest / mp.nseg);
   }
 }
 
@@ -1753,13 +1769,17 @@ static bool launch_marchg(const eig_mat_s &A, i64 m, const double *X, double *Y,
   mp.mrows = A.nslices * 64;
   mp.ncol = (int)ncol;
   mp.nseg = (int)nseg;
-  const dim3 grid((unsigned)((ncol * nseg + kWaves - 1) / kWaves), (unsigned)(m / 8));
+  int pw = 0;  // persistent waves per XCD (0: one wave per item)
+  if (const char *e = std::getenv("EIGMI_EXP_PW")) pw = std::atoi(e) / kWaves * kWaves;
+  if (const char *e = std::getenv("EIGMI_EXP_NSEG")) mp.nseg = std::max(1, std::min((int)nplanes, std::atoi(e)));
+  const dim3 grid = pw > 0 ? dim3((unsigned)(8 * (pw / kWaves)), 1u)
+                           : dim3((unsigned)((ncol * mp.nseg + kWaves - 1) / kWaves), (unsigned)(m / 8));
   if (mode == kSymN8)
     hipLaunchKernelGGL((k_spmm8_marchg<uint8_t, EPI>), grid, dim3(kStreamThreads), 0, s, A.nb_rows, A.own_offset,
-                       A.window, sell_b1(A), mp, sp, X, Y, Bv, dinv, omega, gamma);
+                       A.window, sell_b1(A), mp, sp, X, Y, Bv, dinv, omega, gamma, (int)(m / 8), pw);
   else
     hipLaunchKernelGGL((k_spmm8_marchg<uint32_t, EPI>), grid, dim3(kStreamThreads), 0, s, A.nb_rows, A.own_offset,
-                       A.window, sell_b1(A), mp, sp, X, Y, Bv, dinv, omega, gamma);
+                       A.window, sell_b1(A), mp, sp, X, Y, Bv, dinv, omega, gamma, (int)(m / 8), pw);
   return true;
 }
 

@@ -158,6 +158,7 @@ SIGNATURES = {
                                        _int]),
     "eig_shift_invert_solve": (_int, [_vp, _vp, _vp, _dbl, _int, _int, _dbl, _int, _u, _vp, _vp, ctypes.POINTER(_int)]),
     "eig_blanczos_create": (_int, [_vp, _vp, _int, _int, _int, _dbl, _dbl, _u, ctypes.POINTER(_vp)]),
+    "eig_blanczos_create_si": (_int, [_vp, _vp, _vp, _dbl, _int, _int, _int, _dbl, _dbl, _u, ctypes.POINTER(_vp)]),
     "eig_blanczos_step": (_int, [_vp, _int, ctypes.POINTER(BlockTiming)]),
     "eig_blanczos_ritz": (_int, [_vp, _int, _int, _vp, _vp, _vp]),
     "eig_blanczos_tmatrix": (_int, [_vp, ctypes.POINTER(_int), _vp]),
@@ -703,10 +704,17 @@ def shift_invert_adaptive(A, threshold, initial_nev, max_nev, sigma=0.0, B=None,
 class BlockLanczos:
     """eig_blanczos_t: block Lanczos for K x = lambda M x (config C5), see include/eigmi.h."""
 
-    def __init__(self, K, M, block=32, max_steps=8, degree=36, lmin=0.5, lmax=2.5, seed=123):
+    def __init__(self, K, M, block=32, max_steps=8, degree=36, lmin=0.5, lmax=2.5, seed=123, Ks=None, sigma=0.0):
+        """Ks given: the spectral transformation (K - sigma M)^-1 M with Ks = K - sigma M and
+        (degree, lmin, lmax) the Chebyshev-Jacobi solve of Ks (eig_blanczos_create_si); otherwise
+        M^-1 K with (degree, lmin, lmax) the mass solve."""
         self.K, self.M, self.block = K, M, block
         h = _vp()
-        K.ctx.check(lib.eig_blanczos_create(K.h, M.h, block, max_steps, degree, lmin, lmax, seed, ctypes.byref(h)))
+        if Ks is None:
+            K.ctx.check(lib.eig_blanczos_create(K.h, M.h, block, max_steps, degree, lmin, lmax, seed, ctypes.byref(h)))
+        else:
+            K.ctx.check(lib.eig_blanczos_create_si(K.h, M.h, Ks.h, sigma, block, max_steps, degree, lmin, lmax, seed,
+                                                   ctypes.byref(h)))
         self.h = h
 
     def step(self, steps):

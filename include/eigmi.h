@@ -393,6 +393,14 @@ typedef struct eig_blanczos_timing {
 } eig_blanczos_timing;
 int eig_blanczos_create(eig_mat_t K, eig_mat_t M, int block, int max_steps, int degree, double lmin, double lmax,
                         unsigned seed, eig_blanczos_t *ws);
+/* Spectral transformation: the operator (K - sigma M)^-1 M (ARPACK mode 3, arpack_geneo_wrapper.hh:
+ * 581-658) for the end of the pencil nearest sigma -- the smallest eigenvalues GeneralizedInverse
+ * (eigensolver.hh:204-351) returns for sigma below the spectrum.  Ks = K - sigma M (K for sigma = 0),
+ * solved by `degree` Chebyshev-Jacobi steps with spec(diag(Ks)^-1 Ks) in [lmin, lmax].
+ * eig_blanczos_ritz then returns lambda = sigma + 1 / theta for the nev theta of largest |theta|,
+ * ascending (EIG_WHICH_SA) or descending (EIG_WHICH_LA). */
+int eig_blanczos_create_si(eig_mat_t K, eig_mat_t M, eig_mat_t Ks, double sigma, int block, int max_steps, int degree,
+                           double lmin, double lmax, unsigned seed, eig_blanczos_t *ws);
 int eig_blanczos_step(eig_blanczos_t ws, int steps, eig_blanczos_timing *timing);
 /* Ritz pairs of the k steps taken: eval_host[nev] (LA descending / SA ascending), evec_host: nev
  * owned-row vectors with y^T M y = 1 (or NULL), resid_host[nev]: ||K y - theta M y||_2 (or NULL). */

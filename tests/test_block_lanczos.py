@@ -164,3 +164,40 @@ def test_block_lanczos_argument_errors(ctx):
         eigmi.BlockLanczos(K, M, block=12, max_steps=2)
     with pytest.raises(eigmi.EigShapeError):
         eigmi.BlockLanczos(K, M, block=32, max_steps=2)  # (2+1)*32 > 64 rows
+
+
+def _cheb_degree(lmin, lmax, eps):
+    kappa = lmax / lmin
+    rho = (np.sqrt(kappa) - 1) / (np.sqrt(kappa) + 1)
+    return int(np.ceil(np.log(eps / 2) / np.log(rho)))
+
+
+@pytest.mark.gpu
+def test_shift_invert_smallest_p1(ctx):
+    """C5 at the end GeneralizedInverse returns (eigensolver.hh:204-351) -- the 4
+    smallest eigenvalues of the P1 pencil at N = 24 (n = 13824) through the spectral transformation
+    (K - sigma M)^-1 M, sigma = 0, inner Chebyshev-Jacobi K-solve (K = L7 / (N+1), so
+    spec(D^-1 K) = [2 sin^2(pi h / 2), 2 cos^2(pi h / 2)], h = 1 / (N + 1); degree for 1e-13).
+    Bar: within 1e-8 (relative) of ARPACK shift-invert (scipy eigsh sigma = 0) on the same pencil;
+    residuals ||K y - lambda M y|| <= 1e-5 lambda ||M y|| (the cluster 59.81 (double), 60.15: Ritz
+    vectors of a multiple eigenvalue converge as the square root of its Ritz value)."""
+    import scipy.sparse.linalg as ssl
+    N = 24
+    K, M = oracle.p1_kuhn(N)
+    h = 1.0 / (N + 1)
+    lmin, lmax = 2 * np.sin(np.pi * h / 2) ** 2, 2 * np.cos(np.pi * h / 2) ** 2
+    deg = _cheb_degree(lmin * 0.999, lmax * 1.001, 1e-13)
+    dK, dM = _upload(ctx, K), _upload(ctx, M)
+    bl = eigmi.BlockLanczos(dK, dM, block=32, max_steps=8, degree=deg, lmin=lmin * 0.999, lmax=lmax * 1.001,
+                            Ks=dK, sigma=0.0)
+    bl.step(8)
+    ev, Y, res = bl.ritz(4, eigmi.WHICH_SA, want_evec=True)
+    print('SI block Lanczos N=24:', ev, 'degree', deg)
+    ref = np.sort(ssl.eigsh(K, k=4, M=M, sigma=0.0, which="LM", tol=1e-14, v0=np.ones(K.shape[0]),
+                            return_eigenvectors=False))
+    assert np.all(np.diff(ev) >= 0)
+    assert np.max(np.abs(ev - ref) / ref) <= 1e-8, (ev, ref)
+    for lam, y in zip(ev, Y):
+        r = K @ y - lam * (M @ y)
+        assert np.linalg.norm(r) <= 1e-5 * lam * np.linalg.norm(M @ y)  # (a double eigenvalue: vectors ~ sqrt(eps_lambda))
+    bl.close()
