@@ -1318,7 +1318,7 @@ template <class MT, int EPI>
 __global__ __launch_bounds__(kStreamThreads, 6) void k_spmm8_marchg(
     i64 nrows, i64 own, i64 ld, SellB1 A, MarchPlan mp, GSpans sp, const double *__restrict__ X,
     double *__restrict__ Y, const double *__restrict__ Bv, const double *__restrict__ dinv, double omega,
-    double gamma, int nblk, int pw)
+    double gamma)
 {
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int rq = lane >> 2, cp = lane & 3;
@@ -1331,7 +1331,12 @@ __global__ __launch_bounds__(kStreamThreads, 6) void k_spmm8_marchg(
   // (Measured and dropped at 256^3, m = 32: the workgroup's 4 waves on the 4 column blocks of one
   // item, so the band values / mask / D^-1 are fetched once per 4 blocks -- 6.62 vs 6.73 ms, with
   // any number of plane runs per column; rocprof: L2 misses on the gathered X rows dominate.)
-  auto march_item = [&](int col, int seg, int blk) {
+  // (Measured and dropped: a persistent schedule with XCD-owned column ranges walked by 128-768
+  // resident waves per XCD -- slower at every count, 7.5-19.5 ms: the march is latency-bound per
+  // wave and wants full occupancy.)
+  const int item = (int)swizzled_block() * kWaves + wave;
+  if (item >= mp.ncol * mp.nseg) return;
+  const int col = item % mp.ncol, seg = item / mp.ncol, blk = (int)blockIdx.y;
   const int z0 = (int)(mp.zb + seg * mp.nplanes / mp.nseg), z1 = (int)(mp.zb + (seg + 1) * mp.nplanes / mp.nseg);
   const i64 boff = (i64)blk * ld * 8;
   const dpair *Xb = reinterpret_cast<const dpair *>(X + boff) + cp;
@@ -1400,24 +1405,6 @@ __global__ __launch_bounds__(kStreamThreads, 6) void k_spmm8_marchg(
     pm = pcur;
     pcur = pP;
     amP = aP;
-  }
-  };
-  if (pw == 0)
-  {
-    const int item = (int)swizzled_block() * kWaves + wave;
-    if (item >= mp.ncol * mp.nseg) return;
-    march_item(item % mp.ncol, item / mp.ncol, (int)blockIdx.y);
-    return;
-  }
-  // persistent: XCD x (workgroups b = x mod 8) owns columns [x ncol / 8, (x + 1) ncol / 8) and its
-  // waves walk that range block by block, plane run by plane run, consecutive columns together
-  const int x = (int)(blockIdx.x & 7), i = (int)(blockIdx.x >> 3), wx = (int)(gridDim.x >> 3);
-  const int c0 = mp.ncol * x / 8, nc = mp.ncol * (x + 1) / 8 - c0;
-  const int total = nc * mp.nseg * nblk;
-  for (int it = i * kWaves + wave; it < total; it += wx * kWaves)
-  {
-    const int colx = it % nc, rest = it / nc;
-    march_item(c0 + colx, rest % mp.nseg, rest / mp.nseg);
   }
 }
 
@@ -1769,17 +1756,13 @@ static bool launch_marchg(const eig_mat_s &A, i64 m, const double *X, double *Y,
   mp.mrows = A.nslices * 64;
   mp.ncol = (int)ncol;
   mp.nseg = (int)nseg;
-  int pw = 0;  // persistent waves per XCD (0: one wave per item)
-  if (const char *e = std::getenv("EIGMI_EXP_PW")) pw = std::atoi(e) / kWaves * kWaves;
-  if (const char *e = std::getenv("EIGMI_EXP_NSEG")) mp.nseg = std::max(1, std::min((int)nplanes, std::atoi(e)));
-  const dim3 grid = pw > 0 ? dim3((unsigned)(8 * (pw / kWaves)), 1u)
-                           : dim3((unsigned)((ncol * mp.nseg + kWaves - 1) / kWaves), (unsigned)(m / 8));
+  const dim3 grid((unsigned)((ncol * mp.nseg + kWaves - 1) / kWaves), (unsigned)(m / 8));
   if (mode == kSymN8)
     hipLaunchKernelGGL((k_spmm8_marchg<uint8_t, EPI>), grid, dim3(kStreamThreads), 0, s, A.nb_rows, A.own_offset,
-                       A.window, sell_b1(A), mp, sp, X, Y, Bv, dinv, omega, gamma, (int)(m / 8), pw);
+                       A.window, sell_b1(A), mp, sp, X, Y, Bv, dinv, omega, gamma);
   else
     hipLaunchKernelGGL((k_spmm8_marchg<uint32_t, EPI>), grid, dim3(kStreamThreads), 0, s, A.nb_rows, A.own_offset,
-                       A.window, sell_b1(A), mp, sp, X, Y, Bv, dinv, omega, gamma, (int)(m / 8), pw);
+                       A.window, sell_b1(A), mp, sp, X, Y, Bv, dinv, omega, gamma);
   return true;
 }
 

@@ -39,7 +39,7 @@ def main():
     res = {i: [] for i in range(len(variants))}
     for _ in range(args.rounds):
         for i, var in enumerate(variants):
-            for k in ("EIGMI_EXP_PW", "EIGMI_EXP_NSEG"):
+            for k in [k for k in os.environ if k.startswith("EIGMI_EXP_")]:
                 os.environ.pop(k, None)
             os.environ.update(var)
             ts = {}
