@@ -867,6 +867,7 @@ void destroy_mat(eig_mat_s *A)
   if (A->march_bnd) (void)hipFree(A->march_bnd);
   if (A->sym_val) (void)hipFree(A->sym_val);
   if (A->sym_mask) (void)hipFree(A->sym_mask);
+  if (A->box_val) (void)hipFree(A->box_val);
   delete A;
 }
 
@@ -1159,7 +1160,7 @@ extern "C" int eig_mat_kernel_info(eig_mat_t A, int op, char *name, int name_len
 {
   return guard(A ? A->ctx : nullptr, [&] {
     EIG_CHECK(A && name && name_len > 0, EIG_ERR_ARG, "eig_mat_kernel_info: null argument");
-    EIG_CHECK(op >= EIG_OP_SPMV && op <= EIG_OP_CHEB8, EIG_ERR_ARG, "eig_mat_kernel_info: bad op");
+    EIG_CHECK(op >= EIG_OP_SPMV && op <= EIG_OP_CHEB32, EIG_ERR_ARG, "eig_mat_kernel_info: bad op");
     const std::string nm = kernel_for(*A, op);
     const size_t k = std::min<size_t>(nm.size(), (size_t)name_len - 1);
     std::memcpy(name, nm.data(), k);

@@ -196,6 +196,13 @@ struct eig_mat_s {
   // ghost columns and are marched while the halo is in flight; march_bnd lists every slice outside
   // them (the boundary launch after the exchange).  mz1 <= mz0: no split.
   eigmi::i64 mz0 = 0, mz1 = 0;
+  // Box-stencil image for the 32-column SpMM / Chebyshev kernel (k_box.hip): box_state 0 = not
+  // examined yet, 1 = built, -1 = the band is not a 3-D box stencil; box_val[k n + r] = the entry of
+  // row r at sym_off[k]; grid nx x ny x nz; per offset its plane step and halo-tile row shift
+  int box_state = 0;
+  double *box_val = nullptr;
+  int box_nx = 0, box_ny = 0, box_nz = 0;
+  int box_dz[27] = {}, box_dxy[27] = {};
   eigmi::i32 *march_bnd = nullptr;
   eigmi::i64 n_march_bnd = 0;
   eigmi::i64 *slice_ptr = nullptr;  // nslices + 1
@@ -260,6 +267,11 @@ bool march_split_active(const eig_mat_s &A);
 extern const i32 kMarchInteriorTag;
 // a2 SpMM (kernels_cpp.hh:626-657) on the band-image plane march for 1x1 matrices whose band
 // qualifies; false (nothing launched) otherwise.  X, Y: window-layout multivectors, m % 8 == 0.
+bool box_prepare(const eig_mat_s &A);
+bool launch_box_spmm(const eig_mat_s &A, i64 m, const double *X, double *Y, hipStream_t s);
+bool launch_box_cheb(const eig_mat_s &M, i64 m, const double *Xk, double *Xold, const double *B, const double *dinv,
+                     double omega, double gamma, hipStream_t s);
+void box_invalidate(eig_mat_s &A);
 bool launch_spmm_march(const eig_mat_s &A, i64 m, const double *X, double *Y, hipStream_t s);
 // Chebyshev step (k_block.hip kCheb semantics) on the general band march; false when not applicable.
 bool launch_cheb_march(const eig_mat_s &M, i64 m, const double *Xk, double *Xold, const double *B, const double *dinv,

@@ -409,6 +409,8 @@ int sell_mv8_launches(i64 m)
 void launch_sell_mv8(const eig_mat_s &A, i64 m, const double *X, double *Y, hipStream_t s)
 {
   // symmetric band image with a marchable band (3-D / 2-D stencils): k_spmm8_march (k_spmv.hip)
+  // 3-D box stencils (7-point, P1 Kuhn), 32 columns per matrix pass: LDS-tiled plane march (k_box.hip)
+  if (launch_box_spmm(A, m, X, Y, s)) return;
   if (launch_spmm_march(A, m, X, Y, s)) return;
   sell_mv8<kStore>(A, m, X, Y, nullptr, nullptr, 0.0, 0.0, s);
 }
@@ -417,6 +419,7 @@ void launch_cheb_step(const eig_mat_s &M, i64 m, const double *Xk, double *Xold,
                       double omega, double gamma, hipStream_t s)
 {
   // symmetric band image with a marchable band (the P1 mass matrix of config C5): k_spmm8_marchg
+  if (launch_box_cheb(M, m, Xk, Xold, B, dinv, omega, gamma, s)) return;
   if (launch_cheb_march(M, m, Xk, Xold, B, dinv, omega, gamma, s)) return;
   sell_mv8<kCheb>(M, m, Xk, Xold, B, dinv, omega, gamma, s);
 }

@@ -1838,6 +1838,10 @@ std::string kernel_for(const eig_mat_s &A, int op)
       if (g) return op == 3 ? "k_spmm8_marchg" : "k_spmm8_marchg_cheb";
       return op == 3 ? (b1 && A.nb_rows > 0 ? "k_sell_mv8g" : "none") : "k_sell_mv8q_cheb";
     }
+    case 5:
+    case 6:
+      if (b1 && box_prepare(A)) return op == 5 ? "k_box_mv32" : "k_box_mv32_cheb";
+      return kernel_for(A, op - 2);
     default:
       return "none";
   }

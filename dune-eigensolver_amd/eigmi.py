@@ -338,7 +338,7 @@ class Matrix:
         ctx.check(lib.eig_mat_get_info(handle, ctypes.byref(info)))
         self.info = info
 
-    OPS = {"spmv": 0, "k1": 1, "fused": 2, "spmm8": 3, "cheb8": 4}
+    OPS = {"spmv": 0, "k1": 1, "fused": 2, "spmm8": 3, "cheb8": 4, "spmm32": 5, "cheb32": 6}
 
     def kernel(self, op):
         """Kernel family a whole-matrix launch of `op` ("spmv", "k1", "fused", "spmm8", "cheb8")

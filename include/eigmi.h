@@ -169,7 +169,8 @@ int eig_lanczos_kernel_info(eig_mat_t mat, int fused, char *name, int name_len, 
 /* Kernel family a whole-matrix launch of `op` picks on this matrix image (its creation flags
  * included): EIG_OP_SPMV (eig_mv), EIG_OP_LANCZOS_K1, EIG_OP_LANCZOS_FUSED,
  * EIG_OP_SPMM8 (eig_spmm_mv8, per 8-column block), EIG_OP_CHEB8 (eig_mass_solve_mv8's step). */
-enum { EIG_OP_SPMV = 0, EIG_OP_LANCZOS_K1 = 1, EIG_OP_LANCZOS_FUSED = 2, EIG_OP_SPMM8 = 3, EIG_OP_CHEB8 = 4 };
+enum { EIG_OP_SPMV = 0, EIG_OP_LANCZOS_K1 = 1, EIG_OP_LANCZOS_FUSED = 2, EIG_OP_SPMM8 = 3, EIG_OP_CHEB8 = 4,
+       EIG_OP_SPMM32 = 5, EIG_OP_CHEB32 = 6 /* m % 32 == 0: the 3-D box-stencil kernel where it applies */ };
 int eig_mat_kernel_info(eig_mat_t mat, int op, char *name, int name_len);
 
 /* a13: A += shift*I on the diagonal of every diagonal block (eigensolver.hh:59-66). */

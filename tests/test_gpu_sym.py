@@ -229,3 +229,68 @@ def test_marchg_chebyshev_matches_sell(ctx, N, m):
     # and the solve is a solve: M x ~ b (degree 12 Chebyshev, kappa(D^-1 M) <= 5: error ~ 2 0.38^12)
     r = oracle.spmm_mv8(A, a, m) - Bh
     assert np.linalg.norm(r) <= 1e-3 * np.linalg.norm(Bh)
+
+
+# ---- 3-D box stencils, 32 columns per pass (k_box.hip: LDS-tiled plane march, config C5) ----
+
+@pytest.mark.parametrize("mat,m", [
+    ("p1mass16", 32), ("p1stiff16", 32), ("p1mass20", 32),   # 20: ragged tiles in x and y
+    ("p1mass24", 64), ("poisson18", 32), ("poisson18", 96),
+])
+def test_box_spmm_bitwise(ctx, mat, m):
+    """The box kernel's SpMM (separately rounded products and sums, ascending offsets) is bitwise the
+    reference matmul_sparse_tallskinny_blocked (kernels_cpp.hh:626-657) restated in oracle.spmm_mv8."""
+    A = {"p1mass16": lambda: _p1(16, "M"), "p1stiff16": lambda: _p1(16, "K"), "p1mass20": lambda: _p1(20, "M"),
+         "p1mass24": lambda: _p1(24, "M"), "poisson18": lambda: oracle.poisson3d(18)}[mat]()
+    M = upload(ctx, A)
+    assert M.kernel("spmm32") == "k_box_mv32"
+    Qh = oracle.random_mv8(A.n, m, 7)
+    Q, Y = ctx.array(Qh), ctx.zeros(A.n * m)
+    eigmi.spmm_mv8(M, m, Q, Y)
+    assert np.array_equal(Y.get(), oracle.spmm_mv8(A, Qh, m))
+
+
+@pytest.mark.parametrize("N", [16, 20])
+def test_box_chebyshev_matches_sell(ctx, N):
+    """The fused Chebyshev-Jacobi step on the box kernel against the SELL kernel (both FMA in
+    ascending offset order: equal up to signed zeros / the rounding of the fused update)."""
+    A = _p1(N, "M")
+    M = upload(ctx, A)
+    assert M.kernel("cheb32") == "k_box_mv32_cheb"
+    Ms = upload(ctx, A, flags=eigmi.MAT_NO_MARCH)
+    assert Ms.kernel("cheb32") == "k_sell_mv8q_cheb"
+    n, m = A.n, 32
+    Bh = oracle.random_mv8(n, m, 9)
+    B = ctx.array(Bh)
+    X1, X2 = ctx.zeros(n * m), ctx.zeros(n * m)
+    eigmi.mass_solve_mv8(M, m, 20, B, X1)
+    eigmi.mass_solve_mv8(Ms, m, 20, B, X2)
+    a, b = X1.get(), X2.get()
+    assert np.allclose(a, b, rtol=1e-13, atol=1e-14 * np.abs(b).max())
+    r = oracle.spmm_mv8(A, a, m) - Bh
+    assert np.linalg.norm(r) <= 1e-6 * np.linalg.norm(Bh)
+
+
+def test_box_shift_rebuilds_image(ctx):
+    """eig_mat_shift_diag (A += sigma I) invalidates the box image; the next SpMM uses the new values."""
+    A = _p1(16, "K")
+    M = upload(ctx, A)
+    Qh = oracle.random_mv8(A.n, 32, 11)
+    Q, Y = ctx.array(Qh), ctx.zeros(A.n * 32)
+    eigmi.spmm_mv8(M, 32, Q, Y)
+    M.shift_diag(2.5)
+    eigmi.spmm_mv8(M, 32, Q, Y)
+    As = oracle.CSR(A.nrows, A.rowptr, A.col, A.val.copy())
+    As.val[As.col == np.repeat(np.arange(As.n), np.diff(As.rowptr))] += 2.5
+    assert np.array_equal(Y.get(), oracle.spmm_mv8(As, Qh, 32))
+
+
+def test_box_not_a_grid(ctx):
+    """A band that is not a 3-D box stencil (random offsets) keeps the band march / SELL kernels."""
+    A = band_matrix(4000, [0, 1, 5, 32, 35, 40], 31, drop=0.05)
+    M = upload(ctx, A)
+    assert M.kernel("spmm32") != "k_box_mv32"
+    Qh = oracle.random_mv8(A.n, 32, 12)
+    Q, Y = ctx.array(Qh), ctx.zeros(A.n * 32)
+    eigmi.spmm_mv8(M, 32, Q, Y)
+    assert np.array_equal(Y.get(), oracle.spmm_mv8(A, Qh, 32))

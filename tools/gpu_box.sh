@@ -1,0 +1,5 @@
+set -o pipefail
+O=gpurun_out/box
+mkdir -p $O
+timeout -k 10 400 python -u -m pytest tests/test_gpu_sym.py tests/test_block_lanczos.py -m gpu -x -v --timeout 200 --timeout-method thread > $O/tests.log 2>&1 || exit 1
+SWEEP="EIGMI_NOTHING=1" timeout -k 10 300 python -u tools/cheb_sweep.py --rounds 3 > $O/cheb.jsonl 2> $O/cheb.err || exit 1
