@@ -27,7 +27,6 @@ namespace {
 constexpr int kBoxTX = 16, kBoxTY = 8;                         // tile rows (x, y)
 constexpr int kBoxHX = kBoxTX + 2, kBoxHY = kBoxTY + 2;        // with the one-row halo
 constexpr int kBoxThreads = 1024;  // 16 waves: wave = (tile y, x half), lane = (x, 4-column quad)
-constexpr int kBoxLd = 34;                                     // LDS row stride in doubles (32 + pad)
 constexpr int kBoxChunks = kBoxHY * kBoxHX * 4 * 4;            // 16-B chunks of one plane (rows x blocks x 4)
 constexpr int kBoxRounds = (kBoxChunks + kBoxThreads - 1) / kBoxThreads;
 enum { kBoxStore = 0, kBoxCheb = 1 };
@@ -86,25 +85,30 @@ __global__ void k_box_check(i64 n, int nx, int ny, int nz, int nd, const i32 *__
 
 template <int EPI>
 __global__ __launch_bounds__(kBoxThreads) void k_box_mv32(BoxGeom g, i64 ld, const double *__restrict__ val,
-                                                             const uint32_t *__restrict__ mask32,
-                                                             const uint8_t *__restrict__ mask8,
-                                                             const double *__restrict__ X, double *__restrict__ Y,
-                                                             const double *__restrict__ Bv,
-                                                             const double *__restrict__ dinv, double omega,
-                                                             double gamma)
+                                                          const uint32_t *__restrict__ mask32,
+                                                          const uint8_t *__restrict__ mask8,
+                                                          const double *__restrict__ X, double *__restrict__ Y,
+                                                          const double *__restrict__ Bv,
+                                                          const double *__restrict__ dinv, double omega,
+                                                          double gamma)
 {
-  __shared__ double ring[3][kBoxHY * kBoxHX][kBoxLd];
+  // X of planes z-1, z, z+1 (tile + halo, 32 columns per row, 256-B rows; column c of an odd row
+  // at c ^ 2: the 16-B reads of lanes on adjacent rows then fall on distinct banks), and the
+  // plane's matrix values and row masks (staged once per plane, read by the 8 threads of a row)
+  __shared__ __attribute__((aligned(16))) double ring[3][kBoxHY * kBoxHX][32];
+  __shared__ double atile[kBoxMaxNd][kBoxTX * kBoxTY];
+  __shared__ unsigned mtile[kBoxTX * kBoxTY];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  // 8 threads per row (4 columns each): 16 waves = 4 per SIMD with the 147 KB ring (one workgroup
-  // per CU); lanes 8 apart read rows 272 B apart (the padded stride): conflict-free 32-B LDS reads
+  // 8 threads per row (4 columns each): 16 waves = 4 per SIMD with one workgroup per CU
   const int yi = wave >> 1, xi = (wave & 1) * 8 + (lane >> 3), cq = lane & 7, blk = cq >> 1, c4 = (cq & 1) * 4;
   const int item = (int)blockIdx.x;
   const int tile = item % (g.ntx * g.nty), seg = item / (g.ntx * g.nty);
   const int x0 = (tile % g.ntx) * kBoxTX, y0 = (tile / g.ntx) * kBoxTY;
   const int z0 = seg * g.nz / g.nseg, z1 = (seg + 1) * g.nz / g.nseg;
   const i64 n = (i64)g.P * g.nz;
-  // load plane zz of the tile (+ halo) into ring slot zz mod 3: 16-B chunks, consecutive threads
-  // on consecutive chunks of one (line, block) segment of 18 rows x 64 B
+  auto swz = [](int row, int col) { return col ^ ((row & 1) << 1); };
+  // X plane zz of the tile + halo into ring slot zz mod 3: 16-B chunks, consecutive threads on
+  // consecutive chunks of one (line, block) segment of 18 rows x 64 B
   dv2b pre[kBoxRounds];
   auto fetch = [&](int zz) {
 #pragma unroll
@@ -128,63 +132,99 @@ __global__ __launch_bounds__(kBoxThreads) void k_box_mv32(BoxGeom g, i64 ld, con
       if (c < kBoxChunks)
       {
         const int q = c & 3, hx = (c >> 2) % kBoxHX, rest = (c >> 2) / kBoxHX, b = rest & 3, hy = rest >> 2;
-        *reinterpret_cast<dv2b *>(&ring[sl][hy * kBoxHX + hx][b * 8 + q * 2]) = pre[i];
+        const int hr = hy * kBoxHX + hx;
+        *reinterpret_cast<dv2b *>(&ring[sl][hr][swz(hr, b * 8 + q * 2)]) = pre[i];
       }
     }
   };
+  // the plane's matrix values / masks: thread t stages (row t % 128, offsets t / 128 + 8 j)
+  constexpr int kRows = kBoxTX * kBoxTY, kVal = (kBoxMaxNd * kRows + kBoxThreads - 1) / kBoxThreads;
+  const int srow = tid % kRows, sk0 = tid / kRows;
+  const int sx = x0 + (srow % kBoxTX), sy = y0 + (srow / kBoxTX);
+  const bool sown = sx < g.nx && sy < g.ny;
+  double vpre[kVal];
+  unsigned mpre = 0u;
+  auto fetch_vals = [&](int zz) {
+    const i64 r = sown && zz < z1 ? (i64)sx + (i64)g.nx * sy + (i64)g.P * zz : -1;
+#pragma unroll
+    for (int j = 0; j < kVal; ++j)
+    {
+      const int k = sk0 + j * (kBoxThreads / kRows);
+      vpre[j] = (r >= 0 && k < g.nd) ? __builtin_nontemporal_load(val + (i64)k * n + r) : 0.0;
+    }
+    if (sk0 == 0) mpre = r >= 0 ? (mask32 ? mask32[r] : (unsigned)mask8[r]) : 0u;
+  };
+  auto store_vals = [&]() {
+#pragma unroll
+    for (int j = 0; j < kVal; ++j)
+    {
+      const int k = sk0 + j * (kBoxThreads / kRows);
+      if (k < kBoxMaxNd) atile[k][srow] = vpre[j];
+    }
+    if (sk0 == 0) mtile[srow] = mpre;
+  };
+  const int x = x0 + xi, y = y0 + yi;
+  const bool own = x < g.nx && y < g.ny;
+  const int trow = yi * kBoxTX + xi;            // this thread's row in the tile
+  const int hrow = (yi + 1) * kBoxHX + xi + 1;  // ... and in the halo tile
+  // this thread's Chebyshev operands of plane zz (B, x_{k-1}, gamma / a_rr), one plane ahead
+  dv2b bb[2] = {}, xo[2] = {}, bn[2] = {}, xn[2] = {};
+  double gd = 0.0, gn = 0.0;
+  auto fetch_cheb = [&](int zz, dv2b (&b2)[2], dv2b (&x2)[2], double &gg) {
+    if (EPI != kBoxCheb || !own || zz >= z1) return;
+    const i64 r = (i64)x + (i64)g.nx * y + (i64)g.P * zz;
+    const double *br = Bv + (i64)blk * ld * 8 + r * 8 + c4, *yr = Y + (i64)blk * ld * 8 + r * 8 + c4;
+    gg = gamma * __builtin_nontemporal_load(dinv + r);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+    {
+      b2[j] = __builtin_nontemporal_load(reinterpret_cast<const dv2b *>(br) + j);
+      x2[j] = __builtin_nontemporal_load(reinterpret_cast<const dv2b *>(yr) + j);
+    }
+  };
+  // prologue: X planes z0 - 1 .. z0 + 1, the values of plane z0, the Chebyshev operands of z0
   fetch(z0 - 1);
   store(z0 - 1);
   fetch(z0);
   store(z0);
   fetch(z0 + 1);
   store(z0 + 1);
-  const int x = x0 + xi, y = y0 + yi;
-  const bool own = x < g.nx && y < g.ny;
-  const int hrow = (yi + 1) * kBoxHX + xi + 1;  // this thread's row in the halo tile
+  fetch_vals(z0);
+  store_vals();
+  fetch_cheb(z0, bb, xo, gd);
   for (int z = z0; z < z1; ++z)
   {
-    __syncthreads();  // planes z - 1, z, z + 1 are in the ring
-    // this plane's streams first (row mask, every offset's value -- the box image holds 0.0 where
-    // the row stores none -- and the Chebyshev operands), then the next X plane, all in flight
-    // before the LDS products
-    const i64 r = own ? (i64)x + (i64)g.nx * y + (i64)g.P * z : 0;
-    const unsigned m = own ? (mask32 ? mask32[r] : (unsigned)mask8[r]) : 0u;
-    double a[kBoxMaxNd];
-#pragma unroll
-    for (int k = 0; k < kBoxMaxNd; ++k) a[k] = k < g.nd ? val[(i64)k * n + r] : 0.0;
-    double *yr = Y + (i64)blk * ld * 8 + r * 8 + c4;
-    dv2b bb[2], xo[2];
-    double gd = 0.0;
-    if (EPI == kBoxCheb)
-    {
-      const double *br = Bv + (i64)blk * ld * 8 + r * 8 + c4;
-      gd = gamma * __builtin_nontemporal_load(dinv + r);
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-      {
-        bb[j] = __builtin_nontemporal_load(reinterpret_cast<const dv2b *>(br) + j);
-        xo[j] = __builtin_nontemporal_load(reinterpret_cast<const dv2b *>(yr) + j);
-      }
-    }
+    __syncthreads();  // ring holds planes z - 1, z, z + 1; atile / mtile plane z
+    // in flight during the products: the next plane's values and operands, X of plane z + 2
+    fetch_vals(z + 1);
+    fetch_cheb(z + 1, bn, xn, gn);
     fetch(z + 2);
+    const unsigned m = own ? mtile[trow] : 0u;
     double acc[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[j] = 0.0;
-#pragma unroll
-    for (int k = 0; k < kBoxMaxNd; ++k)
+    // (partially unrolled: a full unroll hoists all 15 offsets' LDS reads and spills)
+#pragma unroll 4
+    for (int k = 0; k < g.nd; ++k)
     {
-      if (k >= g.nd || !((m >> k) & 1u)) continue;
-      const int sl = (((z + g.dz[k]) % 3) + 3) % 3;
-      const double *xr = &ring[sl][hrow + g.dxy[k]][blk * 8 + c4];
+      if (!((m >> k) & 1u)) continue;
+      const double a = atile[k][trow];
+      const int sl = (((z + g.dz[k]) % 3) + 3) % 3, hr = hrow + g.dxy[k];
+      // two 16-B LDS reads (ds_read_b128)
+      const dv2b p0 = *reinterpret_cast<const dv2b *>(&ring[sl][hr][swz(hr, blk * 8 + c4)]);
+      const dv2b p1 = *reinterpret_cast<const dv2b *>(&ring[sl][hr][swz(hr, blk * 8 + c4 + 2)]);
+      const double xr[4] = {p0.x, p0.y, p1.x, p1.y};
 #pragma unroll
       for (int j = 0; j < 4; ++j)
       {
-        if (EPI == kBoxStore) acc[j] = acc[j] + a[k] * xr[j];
-        else acc[j] = __builtin_fma(a[k], xr[j], acc[j]);
+        if (EPI == kBoxStore) acc[j] = acc[j] + a * xr[j];
+        else acc[j] = __builtin_fma(a, xr[j], acc[j]);
       }
     }
     if (own)
     {
+      const i64 r = (i64)x + (i64)g.nx * y + (i64)g.P * z;
+      double *yr = Y + (i64)blk * ld * 8 + r * 8 + c4;
       if (EPI == kBoxStore)
       {
 #pragma unroll
@@ -192,7 +232,10 @@ __global__ __launch_bounds__(kBoxThreads) void k_box_mv32(BoxGeom g, i64 ld, con
       }
       else
       {
-        const double *xc = &ring[((z % 3) + 3) % 3][hrow][blk * 8 + c4];
+        const int sl = ((z % 3) + 3) % 3;
+        const dv2b c0 = *reinterpret_cast<const dv2b *>(&ring[sl][hrow][swz(hrow, blk * 8 + c4)]);
+        const dv2b c1 = *reinterpret_cast<const dv2b *>(&ring[sl][hrow][swz(hrow, blk * 8 + c4 + 2)]);
+        const double xc[4] = {c0.x, c0.y, c1.x, c1.y};
 #pragma unroll
         for (int j = 0; j < 2; ++j)
         {
@@ -202,8 +245,16 @@ __global__ __launch_bounds__(kBoxThreads) void k_box_mv32(BoxGeom g, i64 ld, con
         }
       }
     }
-    __syncthreads();  // everyone is done with slot (z - 1) mod 3
+    __syncthreads();  // everyone is done with slot (z - 1) mod 3 and with atile
     store(z + 2);
+    store_vals();
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+    {
+      bb[j] = bn[j];
+      xo[j] = xn[j];
+    }
+    gd = gn;
   }
 }
 
