@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""Summarise a rocprofv3 run laid out as <dir>/{trace,fetch,write,sq} (tools/prof_c5.sh,
+tools/prof_box.sh) into profiles/<tag>_pmc_summary.json: per kernel FETCH_SIZE x 2 x 1024 +
+WRITE_SIZE x 1024 bytes per launch (MI355X_MICROARCH gfx950 correction), trace average, SQ / TCC
+counters.
+    python tools/summarize_pmc_dirs.py gpurun_out/prof_c5 r02c_c5 "C5 P1 Kuhn K/M 256^3" [bench.json]"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def name(k):
+    # "void eigmi::(anonymous namespace)::k_box_mv32<1>(...)" -> "eigmi::k_box_mv32<1>"
+    k = k.replace("void ", "").replace("(anonymous namespace)::", "")
+    return k.split("(")[0]
+
+
+def pmc(base, d):
+    agg = collections.defaultdict(lambda: collections.defaultdict(list))
+    for f in glob.glob(os.path.join(base, d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            agg[name(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return agg
+
+
+def main(base, tag, config, line=None):
+    stats = {}
+    for f in glob.glob(os.path.join(base, "trace", "*kernel_stats.csv")):
+        for r in csv.DictReader(open(f)):
+            stats[name(r["Name"])] = (float(r["AverageNs"]), int(r["Calls"]))
+    F, W, S = pmc(base, "fetch"), pmc(base, "write"), pmc(base, "sq")
+    out = {"tag": tag, "collected": time.time(), "config": config,
+           "units": "bytes per launch: FETCH_SIZE x 2 x 1024 + WRITE_SIZE x 1024 (MI355X_MICROARCH gfx950 correction)",
+           "kernels": {}}
+    for k in sorted(set(F) | set(W)):
+        f = sum(F[k]["FETCH_SIZE"]) / len(F[k]["FETCH_SIZE"]) * 2048 if F[k]["FETCH_SIZE"] else 0.0
+        w = sum(W[k]["WRITE_SIZE"]) / len(W[k]["WRITE_SIZE"]) * 1024 if W[k]["WRITE_SIZE"] else 0.0
+        e = {"fetch_bytes": round(f), "write_bytes": round(w), "hbm_bytes": round(f + w),
+             "avg_ns_trace": stats.get(k, (None, None))[0], "calls": stats.get(k, (None, None))[1]}
+        for c, v in S.get(k, {}).items():
+            e[c] = sum(v) / len(v)
+        if "TCC_HIT_sum" in e:
+            e["tcc_hit_rate"] = e["TCC_HIT_sum"] / max(1.0, e["TCC_HIT_sum"] + e["TCC_MISS_sum"])
+        out["kernels"][k] = e
+    if line and os.path.exists(line):
+        out["bench_line_under_trace"] = json.loads(open(line).read().strip().splitlines()[-1])
+    dst = os.path.join(ROOT, "profiles", f"{tag}_pmc_summary.json")
+    json.dump(out, open(dst, "w"), indent=1)
+    for k, e in out["kernels"].items():
+        if e["avg_ns_trace"]:
+            print(k, e["hbm_bytes"] / 1e9, "GB", e["avg_ns_trace"] / 1e3, "us")
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:])
