@@ -130,6 +130,10 @@ def committed_traffic(kernel, N, world):
     return best[:2] if best else None
 
 
+VARIANT_NAME = {"fused": "fused one-reduction step", "pipelined": "pipelined one-reduction step",
+                "classic": "SpMV + update kernels"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -144,9 +148,13 @@ def main():
     ap.add_argument("--no-kernel-events", action="store_true", help="skip per-kernel HIP events")
     ap.add_argument("--kernel-events", choices=["auto", "per-launch"], default="auto",
                     help="auto: region events at N=1 for the fused step, per-launch events otherwise")
-    ap.add_argument("--variant", choices=["fused", "classic"], default="fused",
+    ap.add_argument("--variant", choices=["auto", "fused", "pipelined", "classic"], default="auto",
                     help="fused: one kernel + one 3-value allreduce per step (EIG_LANCZOS_FUSED); "
-                         "classic: SpMV kernel + update kernel, two allreduces")
+                         "pipelined: SpMV on t_{k-1} overlapping the previous step's allreduce + a row "
+                         "kernel (EIG_LANCZOS_PIPELINED); classic: SpMV kernel + update kernel, two "
+                         "allreduces; auto: fused on one GPU, on N > 1 the faster of fused / pipelined "
+                         "in a short timed trial before the timed region (all ranks agree)")
+    ap.add_argument("--trial-steps", type=int, default=40, help="steps per variant of the auto trial (N > 1)")
     ap.add_argument("--launch", choices=["auto", "graph", "eager"], default="auto",
                     help="timed steps as one hipGraph replay or launched one by one; auto = graph when "
                          "N > 1 (host-bound halo/allreduce calls), eager at N = 1 (measured faster there)")
@@ -186,7 +194,40 @@ def main():
     nnz_local = int(rp[-1])
 
     K, W = args.steps, args.warmup
-    fused = args.variant == "fused"
+
+    def max_over_ranks(x):
+        if dist is None:
+            return x
+        import torch
+        tt = torch.tensor([x], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        return float(tt.item())
+
+    # N > 1: the per-step allreduce sits on the fused step's critical path; the pipelined step hides
+    # it behind the next SpMV at 56 B/row of extra row traffic.  Which wins depends on the
+    # allreduce latency over xGMI, so the auto variant measures both (graph replays, max over ranks)
+    variant = args.variant
+    trial = None
+    if variant == "auto":
+        variant = "fused"
+        if world > 1:
+            trial = {}
+            for var in ("fused", "pipelined"):
+                tw = eigmi.LanczosWorkspace(M, 5 + args.trial_steps, seed=123, fused=var == "fused",
+                                            pipelined=var == "pipelined")
+                tw.step(5)
+                tw.capture(args.trial_steps)
+                barrier()
+                ctx.sync()
+                t0 = time.perf_counter()
+                tw.replay()
+                ctx.sync()
+                barrier()
+                trial[var] = round(max_over_ranks(time.perf_counter() - t0) / args.trial_steps * 1e3, 4)
+                tw.close()
+            variant = min(trial, key=trial.get)
+    fused = variant in ("fused", "pipelined")
+    pipelined = variant == "pipelined"
     # the K timed steps are captured as one hipGraph before the clock starts (kernels, halo
     # send/recv, allreduces, per-kernel events as graph nodes) and replayed once inside it
     # One GPU, fused step: the timed region has exactly one kernel launch per step, so the two
@@ -194,14 +235,14 @@ def main():
     # region / K = average launch duration including the inter-launch gap (a conservative kernel
     # time).  Per-launch events there would add an event packet between consecutive kernels
     # (measured: 4590 vs 4830 steps/s).  Two-kernel steps keep per-kernel events.
-    region = world == 1 and fused and args.kernel_events != "per-launch"
+    region = world == 1 and variant == "fused" and args.kernel_events != "per-launch"
     kev = not args.no_kernel_events and not region
     eager = args.launch == "eager" or (args.launch == "auto" and world == 1)
     # graph replay (the N > 1 default): the timed graph carries no per-launch events; a second,
     # short graph with per-launch event nodes is replayed after the timed region for the kernel
     # timing, so the event packets do not sit between the timed kernels
     K2 = min(K, 20) if kev and not eager else 0
-    ws = eigmi.LanczosWorkspace(M, W + K + K2, seed=123, fused=fused)
+    ws = eigmi.LanczosWorkspace(M, W + K + K2, seed=123, fused=variant == "fused", pipelined=pipelined)
     if W:
         ws.step(W)
     graph = False if eager else ws.capture(K, timed=kev and K2 == 0)
@@ -212,12 +253,7 @@ def main():
     tim = ws.step(K, timed=kev) if eager else ws.replay()
     ctx.sync()
     barrier()
-    dt = time.perf_counter() - t0
-    if dist is not None:
-        import torch
-        tt = torch.tensor([dt], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
+    dt = max_over_ranks(time.perf_counter() - t0)
     k1, L1 = ws.info()
     # fused: a launch whose norm prediction is unsound repairs instead of stepping (k_spmv.hip
     # fused_begin) and the workspace tops the launches up until K steps are done
@@ -240,6 +276,12 @@ def main():
     # fewer bytes than the survey's CSR count (12 B per nonzero), which is reported beside it
     kname, k1_bytes = M.lanczos_kernel_info(fused)
     csr_bytes = eigmi.bytes_lanczos_fused(cnt, nnz_local) if fused else eigmi.bytes_lanczos_k1(cnt, nnz_local)
+    if pipelined:
+        # timed launch = the SpMV of t_{k-1} (eig_mv's kernel) + the row kernel (32 B read + 24 B
+        # written per row)
+        kname = M.kernel("spmv") + "+k_lanczos_pipe"
+        k1_bytes = eigmi.image_bytes(M, "spmv") + 56 * cnt
+        csr_bytes = eigmi.bytes_spmv(cnt, nnz_local) + 56 * cnt
     k1_ms = (tim_k.spmv_ms / tim_k.spmv_launches if tim_k.spmv_launches else
              (tim.total_ms / K if region and K else None))
     roofline = None
@@ -299,7 +341,7 @@ def main():
         "dtype": "f64",
         "data": "synthetic (generated 7-point Poisson matrix, mt19937 seed-123 start vector)",
         "config": {"workload": f"3D Poisson 7-pt {N}^3 Lanczos 3-term step, no re-orthogonalisation"
-                               f" ({'fused one-reduction step' if fused else 'SpMV + update kernels'})",
+                               f" ({VARIANT_NAME[variant]})",
                    "N": N, "n": n, "nnz": nnz_total,
                    "parallelism": (f"row-partition z-slabs x{world} (RCCL halo, {ctx.comm_info()['allreduce']} "
                                    "allreduce)") if world > 1 else "single GPU"},
@@ -316,6 +358,9 @@ def main():
                       "rest": round(0.0 if region else tim.total_ms - tim.spmv_ms, 3)},
         "recurrence_finite": ok,
         "fused_repairs": repairs if fused else None,
+        "variant": variant,
+        # auto at N > 1: ms per step of each one-reduction variant in the trial (max over ranks)
+        "variant_trial_ms": trial,
         "launch": "hipGraph replay of the K steps" if graph else "eager",
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -93,6 +93,22 @@ void allreduce_sum(eig_ctx_t ctx, double *buf, i64 count, hipStream_t s)
   EIG_NCCL(ncclAllReduce(buf, buf, (size_t)count, ncclDouble, ncclSum, ctx->comm, s));
 }
 
+bool allreduce_overlaps(eig_ctx_t ctx)
+{
+  return ctx->distributed() && !ctx->loop && ((ctx->mbox && ctx->mbox->ready) || ctx->comm_red);
+}
+
+void allreduce_sum_red(eig_ctx_t ctx, double *buf, i64 count, hipStream_t s)
+{
+  EIG_CHECK(allreduce_overlaps(ctx), EIG_ERR_ARG, "allreduce_sum_red: no concurrent allreduce transport");
+  if (ctx->mbox && ctx->mbox->ready)
+  {
+    allreduce_sum(ctx, buf, count, s);
+    return;
+  }
+  EIG_NCCL(ncclAllReduce(buf, buf, (size_t)count, ncclDouble, ncclSum, ctx->comm_red, s));
+}
+
 // ---------------------------------------------------------------------------------------------
 // xGMI mailbox (k_comm.hip).  prepare: allocate my uncached mailbox + state and export it;
 // open: map every peer's mailbox; validate: one allreduce of rank+1 must give P(P+1)/2 exactly.
@@ -259,6 +275,7 @@ extern "C" int eig_ctx_create(int device, eig_ctx_t *out)
     {
       EIG_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
       EIG_HIP(hipStreamCreateWithFlags(&ctx->comm_stream, hipStreamNonBlocking));
+      EIG_HIP(hipStreamCreateWithFlags(&ctx->red_stream, hipStreamNonBlocking));
       hipDeviceProp_t prop;
       EIG_HIP(hipGetDeviceProperties(&prop, device));
       ctx->num_cu = prop.multiProcessorCount;
@@ -283,6 +300,7 @@ extern "C" int eig_ctx_destroy(eig_ctx_t ctx)
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   mailbox_free(ctx);
+  if (ctx->comm_red) (void)ncclCommDestroy(ctx->comm_red);
   if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
   ctx->loop = nullptr;  // the hub is owned by eig_loopback_create / _destroy
   for (auto &e : ctx->pool)
@@ -292,6 +310,7 @@ extern "C" int eig_ctx_destroy(eig_ctx_t ctx)
   if (ctx->scratch) (void)hipFree(ctx->scratch);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   if (ctx->comm_stream) (void)hipStreamDestroy(ctx->comm_stream);
+  if (ctx->red_stream) (void)hipStreamDestroy(ctx->red_stream);
   delete ctx;
   return EIG_OK;
 }
@@ -410,6 +429,10 @@ extern "C" int eig_comm_init_ex(eig_ctx_t ctx, int nranks, int rank, const unsig
     EIG_NCCL(ncclCommInitRank(&ctx->comm, nranks, u, rank));
     ctx->nranks = nranks;
     ctx->rank = rank;
+    // second communicator (same ranks, same order) for allreduces that overlap the halo exchange;
+    // collective, so every rank either has it or none does
+    if (nranks > 1 && ncclCommSplit(ctx->comm, 0, rank, &ctx->comm_red, nullptr) != ncclSuccess)
+      ctx->comm_red = nullptr;
     // the mailbox allreduce only on request: it is validated between processes on one GPU
     // (tests/test_mailbox_gpu.py), not yet across xGMI
     if (flags & EIG_COMM_MAILBOX) mailbox_setup_rccl(ctx);

@@ -723,6 +723,10 @@ struct eig_lanczos_s {
   eig_mat_s *A = nullptr;
   int max_steps = 0, k = 0;
   bool fused = false;  // EIG_LANCZOS_FUSED: B = {P0, P1} (2-wide pair vectors); else B = {u_j rotation of 3}
+  // EIG_LANCZOS_PIPELINED (implies fused launch accounting): B = {T, UZ pairs, S}; hp = after the
+  // row kernel (main stream), ha = after its allreduce (red_stream, when that overlaps)
+  bool pipe = false;
+  hipEvent_t hp = nullptr, ha = nullptr;
   // fused: launches issued (a repair is a launch, not a step) and the launch capacity
   int L = 0, max_launches = 0;
   DevBuf *B[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -750,6 +754,8 @@ struct eig_lanczos_s {
     delete lb;
     if (h0) (void)hipEventDestroy(h0);
     if (h1) (void)hipEventDestroy(h1);
+    if (hp) (void)hipEventDestroy(hp);
+    if (ha) (void)hipEventDestroy(ha);
   }
 };
 
@@ -769,6 +775,54 @@ int events_per_step(int flags)
   return (flags & EIG_LANCZOS_TIME_DETAIL) ? 5 : (flags & EIG_LANCZOS_TIME_KERNELS) ? 2 : 0;
 }
 
+// Pipelined launch L (k_spmv.hip k_lanczos_pipe): S = A t_{k-1} -- interior planes
+// while the halo of T is exchanged, boundary planes after it -- needs nothing from launch L-1's
+// allreduce, which is still running on red_stream; only the row kernel waits for it.  Its sums
+// then go out on red_stream while launch L+1's SpMV computes.  Without a concurrent transport (one
+// rank, loopback) the allreduce runs in line.  wait_prev: launch L-1 was enqueued in the same batch
+// (its allreduce event was recorded there; a batch starts after a join).  Events as
+// lanczos_fused_step (ev[1]: after the row kernel).
+void lanczos_pipe_step(eig_lanczos_s &ws, int L, int force, bool wait_prev, hipEvent_t *ev, int nev,
+                       bool ev_external)
+{
+  eig_mat_s &A = *ws.A;
+  eig_ctx_t ctx = A.ctx;
+  hipStream_t s = ctx->stream;
+  auto mark = [&](int i) {
+    if (ev && i < nev)
+      EIG_HIP(hipEventRecordWithFlags(ev[i], s, ev_external ? hipEventRecordExternal : hipEventRecordDefault));
+  };
+  double *T = ws.B[0]->d(), *UZ = ws.B[1]->d(), *S = ws.B[2]->d();
+  double *out = ws.lb->st.fred + 3 * (i64)L;
+  const bool ovl = allreduce_overlaps(ctx);
+  mark(0);
+  halo_split(
+      A, ws.h0, ws.h1, [&](hipStream_t hs) { halo_exchange(A, T, hs); },
+      [&](const i32 *sl, i64 first, i64 count, int) { launch_spmv(A, T, S, sl, first, count, s); });
+  if (ovl && wait_prev) EIG_HIP(hipStreamWaitEvent(s, ws.ha, 0));  // launch L-1's sums are in
+  launch_lanczos_pipe(A, T, UZ, S, FusedLaunch{ws.lb->st, L, force}, out, s, ctx->red);
+  mark(1);
+  if (ovl)
+  {
+    EIG_HIP(hipEventRecord(ws.hp, s));
+    EIG_HIP(hipStreamWaitEvent(ctx->red_stream, ws.hp, 0));
+    allreduce_sum_red(ctx, out, 3, ctx->red_stream);
+    EIG_HIP(hipEventRecord(ws.ha, ctx->red_stream));
+  }
+  else
+    allreduce_sum(ctx, out, 3, s);
+  mark(2);
+  mark(3);
+  mark(4);
+}
+
+// The library stream waits for the last pipelined allreduce (joins red_stream back, e.g. before a
+// synchronisation or the end of a graph capture).
+void pipe_join(eig_lanczos_s &ws)
+{
+  if (ws.pipe && allreduce_overlaps(ws.A->ctx)) EIG_HIP(hipStreamWaitEvent(ws.A->ctx->stream, ws.ha, 0));
+}
+
 // ev = [beg, end, nps per step]; enqueues steps k .. k+steps-1 (fused: launches L .. L+steps-1) on
 // the library stream.
 void enqueue_steps(eig_lanczos_s &ws, int steps, int nps, hipEvent_t *ev, bool external)
@@ -780,7 +834,9 @@ void enqueue_steps(eig_lanczos_s &ws, int steps, int nps, hipEvent_t *ev, bool e
   for (int i = 0; i < steps; ++i)
   {
     hipEvent_t *e = nps ? ev + 2 + (size_t)nps * i : nullptr;
-    if (ws.fused)
+    if (ws.pipe)
+      lanczos_pipe_step(ws, ws.L + i, 0, i > 0, e, nps, external);
+    else if (ws.fused)
     {
       const int L = ws.L + i;
       lanczos_fused_step(A, ws.B[L & 1]->d(), ws.B[(L + 1) & 1]->d(), L, 0, *ws.lb, e, nps, ws.h0, ws.h1, external);
@@ -792,6 +848,7 @@ void enqueue_steps(eig_lanczos_s &ws, int steps, int nps, hipEvent_t *ev, bool e
       lanczos_step(A, U[j % 3], U[(j + 2) % 3], U[(j + 1) % 3], j, *ws.lb, e, nps, ws.h0, ws.h1, external);
     }
   }
+  if (steps > 0) pipe_join(ws);
   EIG_HIP(hipEventRecordWithFlags(ev[1], s, fl));
 }
 
@@ -883,7 +940,10 @@ extern "C" int eig_lanczos_create_ex(eig_mat_t A, int max_steps, const double *u
 {
   return guard(A ? A->ctx : nullptr, [&] {
     EIG_CHECK(A && out && max_steps >= 0, EIG_ERR_ARG, "eig_lanczos_create: bad argument");
-    EIG_CHECK((flags & ~EIG_LANCZOS_FUSED) == 0, EIG_ERR_ARG, "eig_lanczos_create_ex: unknown flag");
+    EIG_CHECK((flags & ~(EIG_LANCZOS_FUSED | EIG_LANCZOS_PIPELINED)) == 0, EIG_ERR_ARG,
+              "eig_lanczos_create_ex: unknown flag");
+    EIG_CHECK((flags & (EIG_LANCZOS_FUSED | EIG_LANCZOS_PIPELINED)) != (EIG_LANCZOS_FUSED | EIG_LANCZOS_PIPELINED),
+              EIG_ERR_ARG, "eig_lanczos_create_ex: FUSED and PIPELINED are exclusive");
     check_lanczos_matrix(A);
     eig_ctx_t ctx = A->ctx;
     EIG_HIP(hipSetDevice(ctx->device));
@@ -893,25 +953,31 @@ extern "C" int eig_lanczos_create_ex(eig_mat_t A, int max_steps, const double *u
     {
       ws->A = A;
       ws->max_steps = max_steps;
-      ws->fused = (flags & EIG_LANCZOS_FUSED) != 0;
+      ws->pipe = (flags & EIG_LANCZOS_PIPELINED) != 0;
+      ws->fused = ws->pipe || (flags & EIG_LANCZOS_FUSED) != 0;
       // worst case: every step repaired, plus one forced repair per eig_lanczos_tridiag call
       ws->max_launches = ws->fused ? 3 * max_steps + 8 : 0;
       const size_t wb = (size_t)A->window * sizeof(double);
       for (int i = 0; i < 3; ++i)
       {
-        // fused: B[0], B[1] = pair vectors (2 doubles per row), B[2] = start vector scratch
-        ws->B[i] = new DevBuf(ws->fused && i < 2 ? 2 * wb : wb);
+        // fused: B[0], B[1] = pair vectors (2 doubles per row), B[2] = start vector scratch;
+        // pipelined: B[0] = T (t_0 = u_0), B[1] = (u, z) pairs, B[2] = S
+        const bool pair = ws->pipe ? i == 1 : (ws->fused && i < 2);
+        ws->B[i] = new DevBuf(pair ? 2 * wb : wb);
         if (i) EIG_HIP(hipMemsetAsync(ws->B[i]->d(), 0, ws->B[i]->bytes(), s));
       }
-      double *U0 = ws->fused ? ws->B[2]->d() : ws->B[0]->d();
+      double *U0 = ws->pipe ? ws->B[0]->d() : ws->fused ? ws->B[2]->d() : ws->B[0]->d();
       init_start(*A, U0, u0, seed);
       ws->lb = new LanczosBufs(max_steps, ws->max_launches);
       launch_nrm2sq(A->nb_rows, U0 + A->own_offset, ws->lb->st.nsum, 0, s, ctx->red);
       if (ws->fused)  // P0 = (u_0, 0) interleaved; the whole window (ghosts are refilled per step)
       {
-        EIG_HIP(hipMemsetAsync(ws->B[0]->d(), 0, 2 * wb, s));
-        EIG_HIP(hipMemcpy2DAsync(ws->B[0]->d(), 2 * sizeof(double), U0, sizeof(double), sizeof(double), A->window,
-                                 hipMemcpyDeviceToDevice, s));
+        if (!ws->pipe)
+        {
+          EIG_HIP(hipMemsetAsync(ws->B[0]->d(), 0, 2 * wb, s));
+          EIG_HIP(hipMemcpy2DAsync(ws->B[0]->d(), 2 * sizeof(double), U0, sizeof(double), sizeof(double),
+                                   A->window, hipMemcpyDeviceToDevice, s));
+        }
         // launch 0 takes step 0; the shift mu = trace / n from every rank's diagonal share
         EIG_HIP(hipMemsetAsync(ws->lb->st.ctl, 0, ws->lb->ictl.bytes(), s));
         const double mu2[2] = {A->diag_sum, (double)A->nb_rows};
@@ -921,6 +987,8 @@ extern "C" int eig_lanczos_create_ex(eig_mat_t A, int max_steps, const double *u
       allreduce_sum(ctx, ws->lb->st.nsum, 1, s);
       EIG_HIP(hipEventCreateWithFlags(&ws->h0, hipEventDisableTiming));
       EIG_HIP(hipEventCreateWithFlags(&ws->h1, hipEventDisableTiming));
+      EIG_HIP(hipEventCreateWithFlags(&ws->hp, hipEventDisableTiming));
+      EIG_HIP(hipEventCreateWithFlags(&ws->ha, hipEventDisableTiming));
       EIG_HIP(hipStreamSynchronize(s));
     }
     catch (...)
@@ -1051,8 +1119,14 @@ extern "C" int eig_lanczos_tridiag(eig_lanczos_t ws, int *k, double *alpha_host,
       if (mode == kFusedModeStep && j > 0)
       {
         EIG_CHECK(ws->L + 1 <= ws->max_launches, EIG_ERR_ARG, "fused Lanczos: launch capacity exhausted");
-        lanczos_fused_step(*ws->A, ws->B[ws->L & 1]->d(), ws->B[(ws->L + 1) & 1]->d(), ws->L, 1, *ws->lb, nullptr, 0,
-                           ws->h0, ws->h1, false);
+        if (ws->pipe)
+        {
+          lanczos_pipe_step(*ws, ws->L, 1, false, nullptr, 0, false);
+          pipe_join(*ws);
+        }
+        else
+          lanczos_fused_step(*ws->A, ws->B[ws->L & 1]->d(), ws->B[(ws->L + 1) & 1]->d(), ws->L, 1, *ws->lb, nullptr,
+                             0, ws->h0, ws->h1, false);
         ++ws->L;
       }
       launch_fused_tail(ws->lb->st, ws->L, ctx->stream);
@@ -1089,9 +1163,10 @@ extern "C" int eig_lanczos_run(eig_mat_t A, int steps, const double *u0, unsigne
                                double *beta_host, eig_timing *timing)
 {
   eig_lanczos_t ws = nullptr;
-  int rc = eig_lanczos_create_ex(A, steps, u0, seed, flags & EIG_LANCZOS_FUSED, &ws);
+  const int kind = EIG_LANCZOS_FUSED | EIG_LANCZOS_PIPELINED;
+  int rc = eig_lanczos_create_ex(A, steps, u0, seed, flags & kind, &ws);
   if (rc != EIG_OK) return rc;
-  rc = eig_lanczos_step(ws, steps, flags & ~EIG_LANCZOS_FUSED, timing);
+  rc = eig_lanczos_step(ws, steps, flags & ~kind, timing);
   if (rc == EIG_OK) rc = eig_lanczos_tridiag(ws, nullptr, alpha_host, beta_host);
   eig_lanczos_destroy(ws);
   return rc;

@@ -121,12 +121,16 @@ struct eig_ctx_s {
   int device = 0;
   hipStream_t stream = nullptr;      // compute stream
   hipStream_t comm_stream = nullptr; // halo exchange stream
+  hipStream_t red_stream = nullptr;  // allreduce stream of the pipelined Lanczos step (drivers.cpp)
   std::string last_error;
   eigmi::ReduceWS red;
   double *scratch = nullptr;         // small device scalars (reduction results)
   int num_cu = 256;
   // RCCL
   ncclComm_t comm = nullptr;
+  // split of `comm` for the pipelined step's allreduce on red_stream, concurrent with the halo
+  // exchange on comm_stream (two streams never share a communicator); nullptr: no overlap
+  ncclComm_t comm_red = nullptr;
   eigmi::LoopHub *loop = nullptr;    // in-process loopback transport (tests), exclusive with comm
   eigmi::MailboxHost *mbox = nullptr; // xGMI mailbox allreduce (with RCCL, or alone for tests)
   int nranks = 1, rank = 0;
@@ -256,6 +260,11 @@ struct FusedLaunch {
 void launch_lanczos_fused(const eig_mat_s &A, const double *P, double *Pout, const FusedLaunch &fl,
                           const i32 *slices, i64 first, i64 count, const double *carry, double *out, int ticket,
                           hipStream_t s, ReduceWS red);
+// Pipelined step, row half (k_lanczos_pipe): T = t (window layout, updated in place), UZ = (u, z)
+// pairs (window layout, 2 doubles per row), S = A t of this launch (window layout); the three sums
+// of launch fl.L to `out`.
+void launch_lanczos_pipe(const eig_mat_s &A, double *T, double *UZ, const double *S, const FusedLaunch &fl,
+                         double *out, hipStream_t s, ReduceWS red);
 // beta / nsum of the current logical step after a repair launch (L = the next launch index)
 void launch_fused_tail(const LanczosState &st, int L, hipStream_t s);
 // Plane march (k_spmv.hip): band geometry (widest offset D) and whether the interior-plane split
@@ -410,6 +419,11 @@ void b_orthonormalize_device(eig_mat_s &B, i64 m, double *Q, double *norm);
 // Host CSR copy of a single-rank matrix's device image (rows in ISTL order, padding dropped).
 void mat_download_bcsr(const eig_mat_s &A, std::vector<i64> &rowptr, std::vector<i32> &col, std::vector<double> &vals);
 void allreduce_sum(eig_ctx_t ctx, double *buf, i64 count, hipStream_t s);
+// Whether allreduce_sum_red can run on ctx->red_stream concurrently with the compute and halo
+// streams (RCCL with the split communicator, or the mailbox); false for one rank / loopback.
+bool allreduce_overlaps(eig_ctx_t ctx);
+// allreduce_sum on the split communicator (or the mailbox), for ctx->red_stream.
+void allreduce_sum_red(eig_ctx_t ctx, double *buf, i64 count, hipStream_t s);
 void *ctx_buffer(eig_ctx_t ctx, int slot, size_t bytes);
 void host_random_normal(i64 count, unsigned seed, double *out);
 

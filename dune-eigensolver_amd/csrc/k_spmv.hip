@@ -1150,6 +1150,89 @@ __global__ __launch_bounds__(kStreamThreads, 7) void k_lanczos_fused_march(
 }
 
 // ---------------------------------------------------------------------------------------------
+// Pipelined one-reduction step, row half (restatement orc_lanczos_pipelined).  The
+// step's SpMV multiplies t_{k-1} (S = A t_{k-1}, a plain eig_mv launch), which needs no scalar of the
+// previous launch, so on N GPUs it runs while that launch's 3-value allreduce is in flight.  This
+// kernel then applies the scalars (fused_begin: the same modes, prediction and repairs as the fused
+// step) row by row:
+//   u_k = t_{k-1} - c u_{k-1},  z_k = S - c z_{k-1}  (= A u_k),  t_k = (z_k - mu u_k) sig - gam u_{k-1}
+// T (t) is updated in place; UZ holds the (u, z) pairs.  A repair writes T = u_k and keeps UZ (the
+// launch after it has c = 0: u = T, z = S = A u_k exactly).  Bytes: 32 B read + 24 B written per row.
+// Rows [0, n) are owned rows (pointers already offset to the owned part).
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kStreamThreads) void k_lanczos_pipe(i64 n, double *__restrict__ T,
+                                                                 dpair *__restrict__ UZ,
+                                                                 const double *__restrict__ S, FusedArgs fa,
+                                                                 double *__restrict__ out, double *partials,
+                                                                 unsigned *ticket)
+{
+  __shared__ double tot[3];
+  const FusedStep fs = fused_begin(fa);
+  if (fs.act == kFusedHalt || fs.act == kFusedNoop)
+  {
+    fused_idle(out);
+    return;
+  }
+  const double c = fs.c, gam = fs.gam, sig = fs.sig, mu = fs.mu;
+  const bool k0 = fs.j > 0;
+  const i64 stride = (i64)gridDim.x * kStreamThreads;
+  double d = 0.0, q2 = 0.0, m2 = 0.0;
+  if (fs.act == kFusedRepair)
+  {
+    for (i64 i = (i64)blockIdx.x * kStreamThreads + threadIdx.x; i < n; i += stride)
+    {
+      const double u = T[i] - c * UZ[i].x;
+      T[i] = u;
+      m2 += u * u;
+    }
+  }
+  else
+  {
+    auto row = [&](double t, double s, dpair uz, double &tn, dpair &uzn) {
+      const double u = t - c * uz.x;
+      const double z = s - c * uz.y;
+      double ti = (z - mu * u) * sig;
+      if (k0) ti = ti - gam * uz.x;
+      tn = ti;
+      uzn = dpair{u, z};
+      d += ti * u;
+      q2 += ti * ti;
+      m2 += u * u;
+    };
+    // two rows per lane: 16-B loads of T and S, two 16-B (u, z) pairs (4 items in flight per lane
+    // with all loads issued first measured no faster: the launch is HBM-bound at 56 B per row)
+    const i64 n2 = n >> 1;
+    double2 *T2 = reinterpret_cast<double2 *>(T);
+    const double2 *S2 = reinterpret_cast<const double2 *>(S);
+    for (i64 i = (i64)blockIdx.x * kStreamThreads + threadIdx.x; i < n2; i += stride)
+    {
+      const double2 t = T2[i], s = S2[i];
+      const dpair a = UZ[2 * i], b = UZ[2 * i + 1];
+      double2 tn;
+      dpair an, bn;
+      row(t.x, s.x, a, tn.x, an);
+      row(t.y, s.y, b, tn.y, bn);
+      T2[i] = tn;
+      UZ[2 * i] = an;
+      UZ[2 * i + 1] = bn;
+    }
+    if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0)
+    {
+      double tn;
+      dpair zn;
+      row(T[n - 1], S[n - 1], UZ[n - 1], tn, zn);
+      T[n - 1] = tn;
+      UZ[n - 1] = zn;
+    }
+  }
+  double v[3] = {d, q2, m2};
+  if (grid_sum<3, kStreamThreads>(v, partials, ticket, tot))
+  {
+    if (threadIdx.x < 3) out[threadIdx.x] = tot[threadIdx.x];
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // a2 SpMM Y = A X for one 8-column block of a MultiVector<double,8> (kernels_cpp.hh:626-657) on the
 // band-image plane march.  Lane = (row rq = lane >> 2 of a 16-row wave column, column pair
 // cp = lane & 3): every operand load of the wave reads 16 consecutive X rows = 1 KiB contiguous,
@@ -1685,6 +1768,20 @@ void launch_lanczos_fused(const eig_mat_s &A, const double *P, double *Pout, con
   EIG_LFM(1)
 #undef EIG_LFM
 #undef EIG_LF
+}
+
+void launch_lanczos_pipe(const eig_mat_s &A, double *T, double *UZ, const double *S, const FusedLaunch &fl,
+                         double *out, hipStream_t s, ReduceWS red)
+{
+  EIG_CHECK(A.br == 1 && A.bc == 1, EIG_ERR_BLOCKSIZE, "Lanczos driver: 1x1 blocks only");
+  const i64 n = A.nb_rows, own = A.own_offset;
+  EIG_CHECK((own & 1) == 0 && (((uintptr_t)T | (uintptr_t)UZ | (uintptr_t)S) & 15) == 0, EIG_ERR_ARG,
+            "pipelined Lanczos: vectors must be 16-B aligned");
+  const FusedArgs fa{fl.st.nsum, fl.st.alpha, fl.st.beta, fl.st.fred, fl.st.ctl, fl.st.aux, fl.st.mu2, fl.L, fl.force};
+  const i64 per = 2LL * kStreamThreads;
+  const int G = (int)std::max<i64>(1, std::min<i64>(kStreamBlocks, (n + per - 1) / per));
+  hipLaunchKernelGGL(k_lanczos_pipe, dim3(G), dim3(kStreamThreads), 0, s, n, T + own,
+                     reinterpret_cast<dpair *>(UZ) + own, S + own, fa, out, red.partials, red.ticket(0));
 }
 
 void launch_fused_tail(const LanczosState &st, int L, hipStream_t s)

@@ -28,6 +28,7 @@ WHICH_LA, WHICH_SA = 0, 1
 LANCZOS_TIME_KERNELS = 1
 LANCZOS_TIME_DETAIL = 2
 LANCZOS_FUSED = 4
+LANCZOS_PIPELINED = 8
 IPC_HANDLE_BYTES = 64
 ALLREDUCE_KINDS = {0: "none", 1: "rccl", 2: "xgmi-mailbox", 3: "loopback"}
 
@@ -493,13 +494,18 @@ def standard_largest(A, shift, tol, maxiter, nev, seed=123, want_evec=True, verb
     return ev, (evec.reshape(nev, A.n) if want_evec else None), it.value
 
 
-def lanczos_run(A, steps, u0=None, seed=123, timed=False, fused=False):
-    """fused: the one-reduction single-kernel step (EIG_LANCZOS_FUSED) instead of K1 + K2."""
+def _lflags(fused, pipelined):
+    return (LANCZOS_PIPELINED if pipelined else LANCZOS_FUSED if fused else 0)
+
+
+def lanczos_run(A, steps, u0=None, seed=123, timed=False, fused=False, pipelined=False):
+    """fused: the one-reduction single-kernel step (EIG_LANCZOS_FUSED) instead of K1 + K2;
+    pipelined: the one-reduction step with the SpMV on t_{k-1} (EIG_LANCZOS_PIPELINED)."""
     alpha = np.zeros(max(steps, 1))
     beta = np.zeros(steps + 1)
     t = Timing()
     A.ctx.check(lib.eig_lanczos_run(A.h, steps, u0.ptr if u0 is not None else None, seed,
-                                    _tflags(timed) | (LANCZOS_FUSED if fused else 0), _np_ptr(alpha), _np_ptr(beta),
+                                    _tflags(timed) | _lflags(fused, pipelined), _np_ptr(alpha), _np_ptr(beta),
                                     ctypes.byref(t)))
     return alpha[:steps], beta, t
 
@@ -508,12 +514,13 @@ class LanczosWorkspace:
     """eig_lanczos_t: the three-term recurrence as a persistent workspace (setup outside any
     timed region; step() advances and returns the eig_timing of that batch)."""
 
-    def __init__(self, A, max_steps, u0=None, seed=123, fused=False):
+    def __init__(self, A, max_steps, u0=None, seed=123, fused=False, pipelined=False):
         self.A = A
-        self.fused = fused
+        self.fused = fused or pipelined
+        self.pipelined = pipelined
         h = _vp()
         A.ctx.check(lib.eig_lanczos_create_ex(A.h, max_steps, u0.ptr if u0 is not None else None, seed,
-                                              LANCZOS_FUSED if fused else 0, ctypes.byref(h)))
+                                              _lflags(fused, pipelined), ctypes.byref(h)))
         self.h = h
 
     def step(self, steps, timed=False):

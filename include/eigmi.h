@@ -255,7 +255,14 @@ enum eig_lanczos_flags {
    * of ||t||^2 repairs instead (forms u_k, reduces its exact norm; the next launch takes the step),
    * decided on the device.  beta[k] of eig_lanczos_tridiag is always the exact ||u_k||.  Same
    * Krylov process as the two-kernel step; alpha/beta agree with it to its own rounding spread. */
-  EIG_LANCZOS_FUSED = 4
+  EIG_LANCZOS_FUSED = 4,
+  /* Pipelined one-reduction step, for N > 1 ranks: the same scalars, guard and
+   * repairs as EIG_LANCZOS_FUSED, but a step's SpMV multiplies t_{k-1} (S = A t_{k-1}, an eig_mv
+   * launch that needs no scalar of the previous step) and a row kernel forms u_k = t_{k-1} - c u_{k-1},
+   * z_k = S - c z_{k-1} (= A u_k) and t_k; so the previous step's 3-value allreduce (second RCCL
+   * communicator, its own stream) overlaps the SpMV and the halo of t (8 B per row, not 16).
+   * Costs 56 B per row more than the fused step on one GPU.  Exclusive with EIG_LANCZOS_FUSED. */
+  EIG_LANCZOS_PIPELINED = 8
 };
 int eig_lanczos_run(eig_mat_t A, int steps, const double *u0, unsigned seed, int flags,
                     double *alpha_host, double *beta_host, eig_timing *timing);
@@ -267,7 +274,7 @@ int eig_lanczos_run(eig_mat_t A, int steps, const double *u0, unsigned seed, int
  * done so far.  No host synchronisation happens inside a step batch. */
 typedef struct eig_lanczos_s *eig_lanczos_t;
 int eig_lanczos_create(eig_mat_t A, int max_steps, const double *u0, unsigned seed, eig_lanczos_t *ws);
-/* flags: 0 (two-kernel step, as eig_lanczos_create) or EIG_LANCZOS_FUSED. */
+/* flags: 0 (two-kernel step, as eig_lanczos_create), EIG_LANCZOS_FUSED or EIG_LANCZOS_PIPELINED. */
 int eig_lanczos_create_ex(eig_mat_t A, int max_steps, const double *u0, unsigned seed, int flags,
                           eig_lanczos_t *ws);
 int eig_lanczos_step(eig_lanczos_t ws, int steps, int flags, eig_timing *timing);

@@ -778,15 +778,16 @@ void orc_lanczos_rotating(i64 n, const i64 *rowptr, const i32 *col, const double
 static const double kTau = 1e-2;
 enum { kStep = 0, kPost = 1, kHalt = 2, kRepair = 3 };
 
-void orc_lanczos_fused(i64 n, const i64 *rowptr, const i32 *col, const double *val, int steps, const double *u0,
-                       double *alpha, double *beta, int *launches_out)
+// pipe = false: orc_lanczos_fused; pipe = true: orc_lanczos_pipelined (below).
+static void lanczos_onered(i64 n, const i64 *rowptr, const i32 *col, const double *val, int steps, const double *u0,
+                           double *alpha, double *beta, int *launches_out, bool pipe)
 {
   double dsum = 0.0;
   for (i64 i = 0; i < n; ++i)
     for (i64 p = rowptr[i]; p < rowptr[i + 1]; ++p)
       if (col[p] == i) dsum += val[p];
   const double mu = dsum / (double)n;
-  std::vector<double> T(u0, u0 + n), U(n, 0.0), Tn(n), Un(n), ux(n);
+  std::vector<double> T(u0, u0 + n), U(n, 0.0), Tn(n), Un(n), ux(n), Z(n, 0.0), S(n);
   std::vector<double> nsum(steps + 2, 0.0);
   double s0 = 0.0;
   for (i64 i = 0; i < n; ++i) s0 += u0[i] * u0[i];
@@ -794,6 +795,13 @@ void orc_lanczos_fused(i64 n, const i64 *rowptr, const i32 *col, const double *v
   double red[3] = {0.0, 0.0, 0.0}, aux[2] = {0.0, 0.0};
   int j = 0, mode = kStep, L = 0;
   auto launch = [&](bool force) {
+    if (pipe)  // S = A t_{k-1}: needs no scalar of the previous launch (issued before its allreduce)
+      for (i64 i = 0; i < n; ++i)
+      {
+        double acc = 0.0;
+        for (i64 p = rowptr[i]; p < rowptr[i + 1]; ++p) acc += val[p] * T[col[p]];
+        S[i] = acc;
+      }
     double c = 0.0, nt = 1.0, ap = 0.0, bk = 0.0, gam = 0.0, rn = 0.0, rm = 0.0;
     int act;
     if (mode == kPost)
@@ -875,7 +883,13 @@ void orc_lanczos_fused(i64 n, const i64 *rowptr, const i32 *col, const double *v
     for (i64 i = 0; i < n; ++i)
     {
       double acc = 0.0;
-      for (i64 p = rowptr[i]; p < rowptr[i + 1]; ++p) acc += val[p] * ux[col[p]];
+      if (pipe)
+      {
+        acc = S[i] - c * Z[i];  // z_k = A u_k = A t_{k-1} - c A u_{k-1}
+        Z[i] = acc;
+      }
+      else
+        for (i64 p = rowptr[i]; p < rowptr[i + 1]; ++p) acc += val[p] * ux[col[p]];
       double ti = (acc - mu * ux[i]) * sig;
       if (j > 0) ti = ti - gam * U[i];
       Tn[i] = ti;
@@ -902,6 +916,24 @@ void orc_lanczos_fused(i64 n, const i64 *rowptr, const i32 *col, const double *v
     beta[j] = mex > 0.0 ? std::sqrt(mex) * aux[0] / aux[1] : 0.0;
   }
   if (launches_out) *launches_out = L;
+}
+
+void orc_lanczos_fused(i64 n, const i64 *rowptr, const i32 *col, const double *val, int steps, const double *u0,
+                       double *alpha, double *beta, int *launches_out)
+{
+  lanczos_onered(n, rowptr, col, val, steps, u0, alpha, beta, launches_out, false);
+}
+
+// Pipelined one-reduction step, the restatement of the GPU's pipelined step (k_lanczos_pipe in
+// k_spmv.hip): the same scalars, modes and repairs as orc_lanczos_fused, but the SpMV of
+// a launch multiplies t_{k-1} -- a vector that does not depend on the previous launch's reductions,
+// so on N GPUs it overlaps that launch's allreduce -- and A u_k is recovered by the recurrence
+// z_k = A t_{k-1} - c z_{k-1} (z_{k-1} = A u_{k-1}, carried per row).  A repair keeps Z; the launch
+// after it has c = 0, so z = A u_k exactly.
+void orc_lanczos_pipelined(i64 n, const i64 *rowptr, const i32 *col, const double *val, int steps, const double *u0,
+                           double *alpha, double *beta, int *launches_out)
+{
+  lanczos_onered(n, rowptr, col, val, steps, u0, alpha, beta, launches_out, true);
 }
 
 } // extern "C"

@@ -68,6 +68,7 @@ def _load():
                                      _f64p, _f64p]),
         "orc_lanczos_rotating": (None, [_i64, _i64p, _i32p, _f64p, _int, _f64p, _f64p, _f64p, _f64p, _f64p]),
         "orc_lanczos_fused": (None, [_i64, _i64p, _i32p, _f64p, _int, _f64p, _f64p, _f64p, ctypes.c_void_p]),
+        "orc_lanczos_pipelined": (None, [_i64, _i64p, _i32p, _f64p, _int, _f64p, _f64p, _f64p, ctypes.c_void_p]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -258,14 +259,16 @@ def lanczos(A, u0, k):
     return U.reshape(k + 1, A.n), alpha, beta
 
 
-def lanczos_fused(A, u0, k, with_launches=False):
+def lanczos_fused(A, u0, k, with_launches=False, pipelined=False):
     """The guarded fused one-reduction recurrence (orc_lanczos_fused): alpha[k], beta[k+1]
     (beta[k] exact, as eig_lanczos_tridiag returns it); with_launches: also the launch count
-    (steps + repairs + the forced final repair)."""
+    (steps + repairs + the forced final repair).  pipelined: orc_lanczos_pipelined (the SpMV of
+    a launch multiplies t_{k-1}; A u_k by the z recurrence)."""
     alpha = np.zeros(max(k, 1))
     beta = np.zeros(k + 1)
     L = ctypes.c_int(0)
-    lib.orc_lanczos_fused(A.n, A.rowptr, A.col, A.val, k, np.ascontiguousarray(u0, dtype=np.float64), alpha, beta,
+    f = lib.orc_lanczos_pipelined if pipelined else lib.orc_lanczos_fused
+    f(A.n, A.rowptr, A.col, A.val, k, np.ascontiguousarray(u0, dtype=np.float64), alpha, beta,
                           ctypes.byref(L))
     if with_launches:
         return alpha[:k], beta, L.value

@@ -78,10 +78,10 @@ static void outliers(int N, int64_t b, Rows &r)
     for (int64_t p = r.rp[i]; p < r.rp[i + 1]; ++p)
       if (r.c[p] == b + i && (b + i) % every == 0) r.v[p] += 100.0;
 }
-static void fused_repair_run(eig_mat_t A, double *a, double *be, int *launches)
+static void fused_repair_run(eig_mat_t A, double *a, double *be, int *launches, int kind = EIG_LANCZOS_FUSED)
 {
   eig_lanczos_t ws;
-  CK(eig_lanczos_create_ex(A, kRsteps, nullptr, 123, EIG_LANCZOS_FUSED, &ws));
+  CK(eig_lanczos_create_ex(A, kRsteps, nullptr, 123, kind, &ws));
   CK(eig_lanczos_step(ws, kRsteps, 0, nullptr));
   CK(eig_lanczos_tridiag(ws, nullptr, a, be));
   int k = 0;
@@ -100,7 +100,13 @@ int main(int argc, char **argv)
   // ---- serial reference on one context
   std::vector<double> x(n), y_ser(n), a_ser(steps), b_ser(steps + 1), ev_ser(nev), fa_ser(steps), fb_ser(steps + 1);
   std::vector<double> bev_ser(kBnev);
-  std::vector<double> ra_ser(kRsteps), rb_ser(kRsteps + 1);
+  std::vector<double> ra_ser(kRsteps), rb_ser(kRsteps + 1), pra_ser(kRsteps), prb_ser(kRsteps + 1);
+  // pipelined step (EIG_LANCZOS_PIPELINED: SpMV on t_{k-1} while the previous allreduce runs)
+  std::vector<double> pa_ser(steps), pb_ser(steps + 1);
+  std::vector<std::vector<double>> pal(P, std::vector<double>(steps)), pbe(P, std::vector<double>(steps + 1));
+  std::vector<std::vector<double>> pral(P, std::vector<double>(kRsteps)), prbe(P, std::vector<double>(kRsteps + 1));
+  int prl_ser = 0;
+  std::vector<int> prl(P, 0);
   std::vector<std::vector<double>> ral(P, std::vector<double>(kRsteps)), rbe(P, std::vector<double>(kRsteps + 1));
   int rl_ser = 0;
   std::vector<int> rl(P, 0);
@@ -115,11 +121,13 @@ int main(int argc, char **argv)
     CK(eig_mv_host(A, x.data(), y_ser.data()));
     CK(eig_lanczos_run(A, steps, nullptr, 123, 0, a_ser.data(), b_ser.data(), nullptr));
     CK(eig_lanczos_run(A, steps, nullptr, 123, EIG_LANCZOS_FUSED, fa_ser.data(), fb_ser.data(), nullptr));
+    CK(eig_lanczos_run(A, steps, nullptr, 123, EIG_LANCZOS_PIPELINED, pa_ser.data(), pb_ser.data(), nullptr));
     CK(eig_lanczos_solve(A, nev, ncv, EIG_WHICH_LA, 123, ev_ser.data(), nullptr, nullptr));
     eig_mat_destroy(A);
     outliers(N, 0, r);
     CK(eig_mat_create_bcsr(ctx, n, n, 1, 1, r.rp.data(), r.c.data(), r.v.data(), &A));
     fused_repair_run(A, ra_ser.data(), rb_ser.data(), &rl_ser);
+    fused_repair_run(A, pra_ser.data(), prb_ser.data(), &prl_ser, EIG_LANCZOS_PIPELINED);
     eig_mat_destroy(A);
     block_lanczos(ctx, N, 0, n, false, bev_ser.data());
     eig_ctx_destroy(ctx);
@@ -167,6 +175,7 @@ int main(int argc, char **argv)
       // Lanczos recurrence and solver
       CK(eig_lanczos_run(A, steps, nullptr, 123, EIG_LANCZOS_TIME_KERNELS, al[r].data(), be[r].data(), nullptr));
       CK(eig_lanczos_run(A, steps, nullptr, 123, EIG_LANCZOS_FUSED, fal[r].data(), fbe[r].data(), nullptr));
+      CK(eig_lanczos_run(A, steps, nullptr, 123, EIG_LANCZOS_PIPELINED, pal[r].data(), pbe[r].data(), nullptr));
       {
         // capture/replay: the loopback transport cannot be captured, replay must take the same steps eagerly
         std::vector<double> ag(steps), bg(steps + 1);
@@ -186,6 +195,7 @@ int main(int argc, char **argv)
         eig_mat_t B;
         CK(eig_mat_create_bcsr_dist(ctx, n, b, cnt, 1, 1, rows.rp.data(), rows.c.data(), rows.v.data(), &B));
         fused_repair_run(B, ral[r].data(), rbe[r].data(), &rl[r]);
+        fused_repair_run(B, pral[r].data(), prbe[r].data(), &prl[r], EIG_LANCZOS_PIPELINED);
         eig_mat_destroy(B);
       }
       block_lanczos(ctx, N, b, cnt, true, bev[r].data());
@@ -238,6 +248,30 @@ int main(int argc, char **argv)
       {
         std::printf("FAIL rank %d fused step %d: alpha %.17g/%.17g beta %.17g/%.17g\n", r, j, fal[r][j], fa_ser[j],
                     fbe[r][j + 1], fb_ser[j + 1]);
+        ++failures;
+        break;
+      }
+    for (int j = 0; j < steps; ++j)
+      if (std::fabs(pal[r][j] - pa_ser[j]) > 1e-12 * std::fabs(pa_ser[j]) ||
+          std::fabs(pbe[r][j + 1] - pb_ser[j + 1]) > 1e-12 * std::fabs(pb_ser[j + 1]) ||
+          std::fabs(pa_ser[j] - a_ser[j]) > 1e-11 * std::fabs(a_ser[j]) ||
+          std::fabs(pb_ser[j + 1] - b_ser[j + 1]) > 1e-11 * std::fabs(b_ser[j + 1]))
+      {
+        std::printf("FAIL rank %d pipelined step %d: alpha %.17g/%.17g/%.17g beta %.17g/%.17g/%.17g\n", r, j,
+                    pal[r][j], pa_ser[j], a_ser[j], pbe[r][j + 1], pb_ser[j + 1], b_ser[j + 1]);
+        ++failures;
+        break;
+      }
+    if (prl[r] != prl_ser || prl_ser <= kRsteps + 1)
+    {
+      std::printf("FAIL rank %d: pipelined repair run took %d launches, serial %d\n", r, prl[r], prl_ser);
+      ++failures;
+    }
+    for (int j = 0; j < kRsteps; ++j)
+      if (std::fabs(pral[r][j] - pra_ser[j]) > 1e-10 * std::fabs(pra_ser[j]) ||
+          std::fabs(prbe[r][j + 1] - prb_ser[j + 1]) > 1e-10 * std::fabs(prb_ser[j + 1]))
+      {
+        std::printf("FAIL rank %d repaired pipelined step %d\n", r, j);
         ++failures;
         break;
       }

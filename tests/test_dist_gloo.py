@@ -26,7 +26,106 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, N, steps, q):
+def _pipelined(rank, cnt, own, wlen, rp, cl, v, b, full0, steps, halo, oracle):
+    """Per-rank pipelined one-reduction recurrence (orc_lanczos_pipelined / k_lanczos_pipe,
+    DESIGN.md 6): launch L computes S = A t_{k-1} after the halo of T while launch L-1's three sums
+    are still being allreduced (gloo async_op, waited only before the row update); the row update
+    applies the scalars (fused_begin's modes: step, repair, post) and issues its own allreduce.
+    Returns alpha[steps], beta[steps + 1] (final beta exact: the forced repair)."""
+    import torch
+    import torch.distributed as dist
+    STEP, POST, HALT, REPAIR = 0, 1, 2, 3
+    diag = 0.0
+    for i in range(cnt):
+        for p in range(rp[i], rp[i + 1]):
+            if cl[p] == own + i:
+                diag += v[p]
+    mu2 = torch.tensor([diag, float(cnt)], dtype=torch.float64)
+    dist.all_reduce(mu2)
+    mu = float(mu2[0] / mu2[1])
+    T = np.zeros(wlen)
+    T[own:own + cnt] = full0[b:b + cnt]
+    U, Z = np.zeros(cnt), np.zeros(cnt)
+    t0 = torch.tensor([float(np.dot(T[own:own + cnt], T[own:own + cnt]))], dtype=torch.float64)
+    dist.all_reduce(t0)
+    nsum = [0.0] * (steps + 2)
+    nsum[0] = float(t0.item())
+    alpha, beta = np.zeros(steps), np.zeros(steps + 1)
+    beta[0] = np.sqrt(nsum[0])
+    st = {"j": 0, "mode": STEP, "red": np.zeros(3), "aux": (0.0, 0.0), "pend": None}
+
+    def launch(force):
+        halo(T)
+        S = np.zeros(cnt)
+        oracle.lib.orc_csr_mv(cnt, rp, cl, v, T, S)
+        if st["pend"] is not None:  # launch L-1's allreduce completes only now
+            st["pend"][0].wait()
+            st["red"] = st["pend"][1].numpy().copy()
+            st["pend"] = None
+        j, mode, (d, q, m) = st["j"], st["mode"], st["red"]
+        c = ap = bk = gam = rn = rm = 0.0
+        nt = 1.0
+        if mode == POST:
+            rn, rm = st["aux"]
+            nt = m
+            act = HALT if not m > 0.0 else POST
+            if act == POST:
+                bk = np.sqrt(m) * rn / rm
+                gam = bk / rm
+        elif j == 0:
+            nt, act = nsum[0], STEP
+        else:
+            rn, rm = np.sqrt(nsum[j - 1]), np.sqrt(m)
+            c = d / m
+            ap = c * rn + mu
+            nt = q - c * d
+            if force or not nt > 1e-2 * q:
+                act = REPAIR
+            else:
+                bk = np.sqrt(nt) * rn / rm
+                gam = bk / rm
+                act = STEP
+        sig = 1.0 / np.sqrt(nt)
+        t = T[own:own + cnt]
+        if act == HALT:
+            st["mode"] = HALT
+            return
+        if act == REPAIR:
+            alpha[j - 1] = ap
+            st["aux"] = (rn, rm)
+            u = t - c * U
+            T[own:own + cnt] = u
+            sums = [0.0, 0.0, float(np.dot(u, u))]
+            st["mode"] = POST
+        else:
+            if act == POST:
+                nsum[j], beta[j] = nt, bk
+            elif j > 0:
+                nsum[j], alpha[j - 1], beta[j] = nt, ap, bk
+            u = t - c * U
+            z = S - c * Z
+            tn = (z - mu * u) * sig
+            if j > 0:
+                tn = tn - gam * U
+            T[own:own + cnt] = tn
+            U[:], Z[:] = u, z
+            sums = [float(np.dot(tn, u)), float(np.dot(tn, tn)), float(np.dot(u, u))]
+            st["j"], st["mode"] = j + 1, STEP
+        r = torch.tensor(sums, dtype=torch.float64)
+        st["pend"] = (dist.all_reduce(r, async_op=True), r)
+
+    while st["j"] < steps and st["mode"] != HALT:
+        launch(False)
+    if st["mode"] == STEP and st["j"] > 0:
+        launch(True)
+    st["pend"][0].wait()
+    m = float(st["pend"][1][2])
+    rn, rm = st["aux"]
+    beta[st["j"]] = np.sqrt(m) * rn / rm
+    return alpha, beta
+
+
+def _worker(rank, world, port, N, steps, q, variant="classic"):
     import sys
     sys.path.insert(0, os.path.join(ROOT, "dune-eigensolver_amd"))
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -68,6 +167,10 @@ def _worker(rank, world, port, N, steps, q):
             return float(t.item())
 
         full0 = oracle.random_vec(n, 123)
+        if variant == "pipelined":
+            alpha, beta = _pipelined(rank, cnt, own, wlen, rp, cl, v, b, full0, steps, halo, oracle)
+            q.put((rank, alpha, beta, [(p, cnt_) for p, _, cnt_ in recvs]))
+            return
         U = [np.zeros(wlen) for _ in range(3)]
         U[0][own:own + cnt] = full0[b:b + cnt]
         nsum = [allreduce(float(np.dot(U[0][own:own + cnt], U[0][own:own + cnt])))]
@@ -96,8 +199,12 @@ def _worker(rank, world, port, N, steps, q):
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("variant", ["classic", "pipelined"])
 @pytest.mark.parametrize("world", [2, 3])
-def test_distributed_lanczos_matches_serial_oracle(world):
+def test_distributed_lanczos_matches_serial_oracle(world, variant):
+    """classic: two allreduces per step, vs orc_lanczos.  pipelined: the allreduce of launch L
+    overlaps launch L+1's halo + SpMV (async gloo), vs the serial restatement orc_lanczos_pipelined
+    (1e-12) and the classic recurrence (1e-11, the fused/classic spread of test_oracle)."""
     import sys
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
@@ -105,7 +212,7 @@ def test_distributed_lanczos_matches_serial_oracle(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, N, steps, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, N, steps, q, variant)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=180) for _ in range(world)]
@@ -113,10 +220,18 @@ def test_distributed_lanczos_matches_serial_oracle(world):
         p.join(timeout=60)
         assert p.exitcode == 0
     A = oracle.poisson3d(N)
-    _, ra, rb = oracle.lanczos(A, oracle.random_vec(A.n, 123), steps)
+    u0 = oracle.random_vec(A.n, 123)
+    _, ra, rb = oracle.lanczos(A, u0, steps)
+    if variant == "pipelined":
+        pa, pb = oracle.lanczos_fused(A, u0, steps, pipelined=True)
     for rank, alpha, beta, recv in res:
-        assert np.allclose(alpha, ra, rtol=1e-12), rank
-        assert np.allclose(beta, rb, rtol=1e-12), rank
+        if variant == "pipelined":
+            assert np.allclose(alpha, pa, rtol=1e-12, atol=0), rank
+            assert np.allclose(beta, pb, rtol=1e-12, atol=0), rank
+            assert np.allclose(alpha, ra, rtol=1e-11, atol=0) and np.allclose(beta, rb, rtol=1e-11, atol=0), rank
+        else:
+            assert np.allclose(alpha, ra, rtol=1e-12), rank
+            assert np.allclose(beta, rb, rtol=1e-12), rank
         peers = sorted(p for p, _ in recv)
         assert peers == [x for x in (rank - 1, rank + 1) if 0 <= x < world]
         assert all(c == N * N for _, c in recv)  # one z-plane per neighbour

@@ -7,7 +7,10 @@ the reference CPU path's Lanczos step) to 1e-12 relative for |sigma| <= 1e4, and
 recurrence's own run-to-run spread beyond that (two classic runs whose start vectors differ by
 1e-16 already differ by ~6e-10 at sigma = 1e6 after 60 steps; tests/fused_ref.py); alpha to 1e-12
 relative throughout.  Both the plane-march kernel (band image) and the SELL row kernel run the
-guard; repairs and the halted (breakdown) state are exercised."""
+guard; repairs and the halted (breakdown) state are exercised.  The pipelined step
+(EIG_LANCZOS_PIPELINED: SpMV on t_{k-1}, A u_k by the z recurrence; k_lanczos_pipe) runs the same
+guard and is held to the same bars against the classic recurrence and its own restatement
+(orc_lanczos_pipelined)."""
 
 import numpy as np
 import pytest
@@ -23,8 +26,8 @@ def upload(ctx, A, band=True):
     return eigmi.Matrix.from_bcsr(ctx, A.rowptr, A.col, A.val, A.br, A.bc, flags=0 if band else eigmi.MAT_NO_BAND)
 
 
-def fused_run(M, steps, batches=1, graph=False):
-    ws = eigmi.LanczosWorkspace(M, steps, seed=123, fused=True)
+def fused_run(M, steps, batches=1, graph=False, pipe=False):
+    ws = eigmi.LanczosWorkspace(M, steps, seed=123, fused=not pipe, pipelined=pipe)
     try:
         per = steps // batches
         done = 0
@@ -45,17 +48,21 @@ def fused_run(M, steps, batches=1, graph=False):
 KERNEL = {True: "k_lanczos_fused_march", False: "k_lanczos_fused_b1"}
 
 
+PIPE = pytest.mark.parametrize("pipe", [False, True], ids=["fused", "pipelined"])
+
+
+@PIPE
 @pytest.mark.parametrize("band", [True, False], ids=["march", "sell"])
 @pytest.mark.parametrize("mat", ["p3d_16", "c1"])
 @pytest.mark.parametrize("sigma", [1e2, 1e4, 1e6, -1e6])
-def test_fused_shifted_operator_vs_classic(ctx, band, mat, sigma):
+def test_fused_shifted_operator_vs_classic(ctx, band, mat, sigma, pipe):
     A = shifted(oracle.poisson3d(16) if mat == "p3d_16" else oracle.laplace2d(64), sigma)
     M = upload(ctx, A, band)
     assert M.lanczos_kernel_info(True)[0] == KERNEL[band]
-    a, b, L = fused_run(M, 60)
+    a, b, L = fused_run(M, 60, pipe=pipe)
     u0 = oracle.random_vec(A.n, 123)
     ca, cb = classic(A, u0, 60)
-    oa, ob, oL = oracle.lanczos_fused(A, u0, 60, with_launches=True)
+    oa, ob, oL = oracle.lanczos_fused(A, u0, 60, with_launches=True, pipelined=pipe)
     assert L == oL == 61  # 60 steps + the forced final repair (no prediction failed)
     tol = max(1e-12, 4 * classic_spread(A, u0, 60, cb))
     assert np.all(np.abs(a - ca) <= 1e-12 * np.abs(ca))
@@ -65,8 +72,9 @@ def test_fused_shifted_operator_vs_classic(ctx, band, mat, sigma):
         assert np.all(np.abs(b - cb) <= 1e-12 * np.abs(cb))
 
 
+@PIPE
 @pytest.mark.parametrize("band", [True, False], ids=["march", "sell"])
-def test_fused_repair_launches(ctx, band):
+def test_fused_repair_launches(ctx, band, pipe):
     """Outliers (+100 on 12 diagonal entries) make some predictions unsound: those launches
     repair, the step after each runs with c = 0 and the exact norm.  Same decisions and values as
     the oracle restatement; in batches (top-up launches after each batch) and as replayed graphs
@@ -74,28 +82,29 @@ def test_fused_repair_launches(ctx, band):
     A0 = oracle.poisson3d(16)
     A = shifted(A0, 0.0, range(0, A0.n, A0.n // 12), 1e2)
     M = upload(ctx, A, band)
-    a, b, L = fused_run(M, 16)
+    a, b, L = fused_run(M, 16, pipe=pipe)
     u0 = oracle.random_vec(A.n, 123)
     ca, cb = classic(A, u0, 16)
-    oa, ob, oL = oracle.lanczos_fused(A, u0, 16, with_launches=True)
+    oa, ob, oL = oracle.lanczos_fused(A, u0, 16, with_launches=True, pipelined=pipe)
     assert L == oL and L > 17
     tol = max(1e-12, 4 * classic_spread(A, u0, 16, cb))
     assert np.all(np.abs(a - ca) <= tol * np.abs(ca)) and np.all(np.abs(b - cb) <= tol * np.abs(cb))
     assert np.all(np.abs(a - oa) <= tol * np.abs(oa)) and np.all(np.abs(b - ob) <= tol * np.abs(ob))
     for batches, graph in ((4, False), (3, True)):
-        a2, b2, L2 = fused_run(M, 16, batches, graph)
+        a2, b2, L2 = fused_run(M, 16, batches, graph, pipe)
         assert np.array_equal(a2, a) and np.array_equal(b2, b)
     # long run with large outliers: chaotic without re-orthogonalisation, compared through the
     # converged top Ritz value
     A = shifted(A0, 0.0, range(0, A0.n, A0.n // 12), 1e5)
     M = upload(ctx, A, band)
-    a, b, L = fused_run(M, 60)
+    a, b, L = fused_run(M, 60, pipe=pipe)
     ca, cb = classic(A, u0, 60)
     assert L > 70
     assert abs(top_ritz(a, b) - top_ritz(ca, cb)) <= 1e-12 * top_ritz(ca, cb)
 
 
-def test_fused_breakdown_halts(ctx):
+@PIPE
+def test_fused_breakdown_halts(ctx, pipe):
     """u0 an eigenvector of a diagonal matrix: u_1 = 0 exactly; the repair launch reduces
     ||u_1|| = 0, the recurrence halts (EIG_ERR_BREAKDOWN) with beta[1] = 0, alpha[0] exact."""
     n = 256
@@ -105,7 +114,7 @@ def test_fused_breakdown_halts(ctx):
     e = np.zeros(n)
     e[5] = 2.0
     u0.upload(e)
-    ws = eigmi.LanczosWorkspace(M, 8, u0=u0, fused=True)
+    ws = eigmi.LanczosWorkspace(M, 8, u0=u0, fused=not pipe, pipelined=pipe)
     with pytest.raises(eigmi.EigError) as ei:
         ws.step(8)
     assert ei.value.code == 5  # EIG_ERR_BREAKDOWN

@@ -122,8 +122,9 @@ def test_lanczos_oracle_ritz_values_converge(golden_dir):
     assert abs(w[0] - g["sa_w"][0]) < 1e-6
 
 
+@pytest.mark.parametrize("pipe", [False, True], ids=["fused", "pipelined"])
 @pytest.mark.parametrize("mat", ["c1", "p3d_20"])
-def test_lanczos_fused_oracle_matches_two_reduction_form(mat, golden_dir):
+def test_lanczos_fused_oracle_matches_two_reduction_form(mat, pipe, golden_dir):
     """The one-reduction recurrence (orc_lanczos_fused) is the same Krylov process: alpha/beta
     agree with orc_lanczos to rounding over 40 and 100 steps (measured <= 2e-12; two runs of
     the classic form whose start vectors differ by 1e-16 differ by as much), and its Ritz values
@@ -132,19 +133,20 @@ def test_lanczos_fused_oracle_matches_two_reduction_form(mat, golden_dir):
     u0 = oracle.random_vec(A.n, 123)
     for k in (40, 100):
         _, a, b = oracle.lanczos(A, u0, k)
-        fa, fb = oracle.lanczos_fused(A, u0, k)
+        fa, fb = oracle.lanczos_fused(A, u0, k, pipelined=pipe)
         assert np.allclose(fa, a, rtol=1e-11, atol=0) and np.allclose(fb, b, rtol=1e-11, atol=0)
     if mat == "c1":
-        fa, fb = oracle.lanczos_fused(A, u0, 300)
+        fa, fb = oracle.lanczos_fused(A, u0, 300, pipelined=pipe)
         T = np.diag(fa) + np.diag(fb[1:-1], 1) + np.diag(fb[1:-1], -1)
         w = np.linalg.eigvalsh(T)
         g = np.load(os.path.join(golden_dir, "c1_arpack.npz"))
         assert abs(w[-1] - g["la_w"][0]) < 1e-10
 
 
+@pytest.mark.parametrize("pipe", [False, True], ids=["fused", "pipelined"])
 @pytest.mark.parametrize("mat", ["p3d_16", "c1"])
 @pytest.mark.parametrize("sigma", [0.0, 1e2, 1e4, 1e6, -1e6])
-def test_lanczos_fused_shifted_operator(mat, sigma):
+def test_lanczos_fused_shifted_operator(mat, sigma, pipe):
     """the fused step's predicted norm ||t||^2 - (t.u)^2/||u||^2 cancels when
     alpha >> beta (A + sigma I, eigensolver.hh:59-66, arpack_geneo_wrapper.hh:600-601): the
     unguarded form was off by 9e-2 in beta at sigma = 1e6.  The guarded step (shift by
@@ -155,7 +157,7 @@ def test_lanczos_fused_shifted_operator(mat, sigma):
     A = shifted(A0, sigma)
     u0 = oracle.random_vec(A.n, 123)
     ca, cb = classic(A, u0, 60)
-    fa, fb, L = oracle.lanczos_fused(A, u0, 60, with_launches=True)
+    fa, fb, L = oracle.lanczos_fused(A, u0, 60, with_launches=True, pipelined=pipe)
     tol = max(1e-12, 4 * classic_spread(A, u0, 60, cb))
     if abs(sigma) <= 1e4:  # the verdict's 1e-12 (the classic spread is <= 4e-13 here)
         assert np.all(np.abs(fb - cb) <= 1e-12 * np.abs(cb))
@@ -165,7 +167,8 @@ def test_lanczos_fused_shifted_operator(mat, sigma):
     assert L == 61
 
 
-def test_lanczos_fused_repair_path():
+@pytest.mark.parametrize("pipe", [False, True], ids=["fused", "pipelined"])
+def test_lanczos_fused_repair_path(pipe):
     """Outlier rows (diagonal + add on 12 rows) put trace/n away from the bulk of the spectrum, so
     |alpha - mu| >> beta at some steps: those launches repair (form u_k, reduce its exact norm)
     and the recurrence still follows the classic one to its own spread.  (A 12-fold outlier makes
@@ -176,19 +179,20 @@ def test_lanczos_fused_repair_path():
     A = shifted(A0, 0.0, rows, 1e2)
     u0 = oracle.random_vec(A.n, 123)
     ca, cb = classic(A, u0, 16)
-    fa, fb, L = oracle.lanczos_fused(A, u0, 16, with_launches=True)
+    fa, fb, L = oracle.lanczos_fused(A, u0, 16, with_launches=True, pipelined=pipe)
     assert L > 17, "expected repair launches"
     tol = max(1e-12, 4 * classic_spread(A, u0, 16, cb))
     assert np.all(np.abs(fa - ca) <= tol * np.abs(ca))
     assert np.all(np.abs(fb - cb) <= tol * np.abs(cb))
     A = shifted(A0, 0.0, rows, 1e5)
     ca, cb = classic(A, u0, 60)
-    fa, fb, L = oracle.lanczos_fused(A, u0, 60, with_launches=True)
+    fa, fb, L = oracle.lanczos_fused(A, u0, 60, with_launches=True, pipelined=pipe)
     assert L > 70
     assert abs(top_ritz(fa, fb) - top_ritz(ca, cb)) <= 1e-12 * top_ritz(ca, cb)
 
 
-def test_lanczos_fused_breakdown():
+@pytest.mark.parametrize("pipe", [False, True], ids=["fused", "pipelined"])
+def test_lanczos_fused_breakdown(pipe):
     """u0 = an eigenvector: u_1 = 0 exactly, the repair finds ||u_1|| = 0 and the recurrence
     halts with beta[1] = 0 (what the classic form computes)."""
     n = 64
@@ -196,7 +200,7 @@ def test_lanczos_fused_breakdown():
     A = oracle.CSR(n, rp, np.arange(n, dtype=np.int32), np.arange(1.0, n + 1.0))
     u0 = np.zeros(n)
     u0[5] = 2.0
-    fa, fb, L = oracle.lanczos_fused(A, u0, 4, with_launches=True)
+    fa, fb, L = oracle.lanczos_fused(A, u0, 4, with_launches=True, pipelined=pipe)
     assert fb[0] == 2.0 and fa[0] == 6.0 and fb[1] == 0.0
     assert L == 3  # step 0, the repair, the halted launch
 

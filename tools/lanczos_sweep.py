@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """A/B of Lanczos step / SpMV kernel images on one GPU, interleaved rounds in ONE process.
 
-Variant spec "<fused|classic|mv>[:<image>]" with image one of
+Variant spec "<fused|pipelined|classic|mv>[:<image>]" with image one of
     band     (default) symmetric band image, plane march where the band allows it
     gather   band image, every offset through its own gather (EIG_MAT_BAND_GATHER)
     nomarch  band image, row kernels (EIG_MAT_NO_MARCH)
@@ -79,7 +79,8 @@ def main():
                 res[spec]["k_us"].append(ms * 1e3)
                 res[spec]["step_us"].append(ms * 1e3)
                 continue
-            ws = eigmi.LanczosWorkspace(M, args.steps + 2, seed=123, fused=op == "fused")
+            ws = eigmi.LanczosWorkspace(M, args.steps + 2, seed=123, fused=op == "fused",
+                                        pipelined=op == "pipelined")
             ws.step(2)
             t = ws.step(args.steps, timed=True)
             res[spec]["k_us"].append(t.spmv_ms / args.steps * 1e3)
@@ -89,11 +90,13 @@ def main():
         op, fl = parse(spec)
         M = mats[fl]
         kb = (eigmi.bytes_spmv(n, nnz) if op == "mv" else
+              eigmi.bytes_spmv(n, nnz) + 56 * n if op == "pipelined" else
               eigmi.bytes_lanczos_fused(n, nnz) if op == "fused" else eigmi.bytes_lanczos_k1(n, nnz))
         r = res[spec]
         km = float(np.median(r["k_us"]))
         sm = float(np.median(r["step_us"]))
-        print(json.dumps({"variant": spec, "kernel": M.kernel({"mv": "spmv", "fused": "fused", "classic": "k1"}[op]),
+        print(json.dumps({"variant": spec, "kernel": M.kernel({"mv": "spmv", "fused": "fused", "pipelined": "spmv",
+                                                             "classic": "k1"}[op]),
                           "kernel_us_med": round(km, 2), "kernel_us_min": round(min(r["k_us"]), 2),
                           "kernel_csr_GBs": round(kb / km / 1e3, 1), "step_us_med": round(sm, 2),
                           "steps_per_s": round(1e6 / sm, 1),
