@@ -1462,7 +1462,19 @@ void orthonormalize_device(eig_ctx_t ctx, i64 n, i64 m, double *Q, int variant)
       launch_apply_upper(n, Qb, U2, s);
     }
     const i64 mrest = m - bk - 8;
-    if (mrest > 0)
+    if (mrest > 0 && variant == EIG_ORTHO_CHOLQR_SPLIT)
+    {
+      // orthonormalize_avx2_b8 (kernels_avx2.hh:255-381): columns 0-3 of Q_bk first, then 4-7
+      // against the updated later blocks.  Each half is the full 8 x mrest Gram with the other
+      // half's rows zeroed: those add 0 * q_k, which leaves every entry exactly as it was.
+      for (int h = 0; h < 2; ++h)
+      {
+        gram_device(ctx, n, 8, mrest, Qb, Qb + 8 * n, Sg);
+        EIG_HIP(hipMemsetAsync(Sg + (h ? 0 : 4 * mrest), 0, (size_t)4 * mrest * sizeof(double), s));
+        launch_project(n, mrest, Qb, Qb + 8 * n, Sg, s);
+      }
+    }
+    else if (mrest > 0)
     {
       gram_device(ctx, n, 8, mrest, Qb, Qb + 8 * n, Sg);
       launch_project(n, mrest, Qb, Qb + 8 * n, Sg, s);
@@ -1488,7 +1500,8 @@ extern "C" int eig_orthonormalize_mv8(eig_ctx_t ctx, int64_t n, int64_t m, doubl
   return guard(ctx, [&] {
     EIG_CHECK(ctx && Q && n >= 0, EIG_ERR_ARG, "eig_orthonormalize_mv8: bad argument");
     const int v = variant & ~EIG_ORTHO_GRID;
-    EIG_CHECK(v == EIG_ORTHO_MGS || v == EIG_ORTHO_CHOLQR, EIG_ERR_ARG, "unknown variant");
+    EIG_CHECK(v == EIG_ORTHO_MGS || v == EIG_ORTHO_CHOLQR || v == EIG_ORTHO_CHOLQR_SPLIT, EIG_ERR_ARG,
+              "unknown variant");
     EIG_MV8_CHECK(m);
     DeviceGuard dg(ctx->device);
     orthonormalize_device(ctx, n, m, Q, variant);

@@ -15,7 +15,7 @@ LIB_PATH = os.path.join(_HERE, "lib", "libeigmi_san.so" if os.environ.get("EIGMI
                         else "libeigmi.so")
 
 EIG_OK, EIG_ERR_SHAPE, EIG_ERR_BLOCKSIZE, EIG_ERR_HIP, EIG_ERR_RCCL, EIG_ERR_BREAKDOWN, EIG_ERR_ARG, EIG_ERR_NODEVICE = range(8)
-ORTHO_MGS, ORTHO_CHOLQR = 0, 1
+ORTHO_MGS, ORTHO_CHOLQR, ORTHO_CHOLQR_SPLIT = 0, 1, 2
 ORTHO_GRID = 0x100  # or-ed into the variant: grid-wide MGS passes even for blocks one workgroup holds
 # matrix kernel-image flags (eig_mat_create_bcsr_ex)
 MAT_NO_BAND, MAT_BAND_GATHER, MAT_NO_STENCIL, MAT_NO_MARCH = 1, 2, 4, 8

@@ -211,8 +211,11 @@ int eig_gram_mv8(eig_ctx_t ctx, int64_t n, int64_t m1, int64_t m2, const double 
  * EIG_ORTHO_MGS    = orthonormalize_blocked (kernels_cpp.hh:180-351): diagonal block by column MGS,
  *                    later blocks by one block-CGS pass.
  * EIG_ORTHO_CHOLQR = orthonormalize_avx2_b8_v2 / _neon_b8_v2 (kernels_avx2.hh:385-622): CholQR of
- *                    the diagonal block, one 8x8 projection per later block. */
-enum eig_ortho_variant { EIG_ORTHO_MGS = 0, EIG_ORTHO_CHOLQR = 1 };
+ *                    the diagonal block, one 8x8 projection per later block.
+ * EIG_ORTHO_CHOLQR_SPLIT = orthonormalize_avx2_b8 (kernels_avx2.hh:64-381): the same CholQR of the
+ *                    diagonal block, later blocks projected in two halves (columns 0-3, then 4-7
+ *                    against the updated block). */
+enum eig_ortho_variant { EIG_ORTHO_MGS = 0, EIG_ORTHO_CHOLQR = 1, EIG_ORTHO_CHOLQR_SPLIT = 2 };
 /* or-ed into `variant`: keep the grid-wide MGS passes even where one workgroup holds the block
  * (n <= 4096 on one rank; the two do the same per-row operations -- A/B and tests) */
 enum { EIG_ORTHO_GRID = 0x100 };

@@ -391,6 +391,40 @@ void orc_orthonormalize_cholqr_mv8(i64 n, i64 m, double *q)
   }
 }
 
+// a10, split-half order: orthonormalize_avx2_b8 (kernels_avx2.hh:64-381): the same CholQR of the
+// diagonal block, but every later block is projected in two halves -- S1 = Q_bk[:, 0:4]^T Q_bj,
+// Q_bj -= Q_bk[:, 0:4] S1, then S2 = Q_bk[:, 4:8]^T Q_bj (the UPDATED block), Q_bj -= Q_bk[:, 4:8] S2
+// (:255-381).  (FMA in the SIMD code; separately rounded here.)
+void orc_orthonormalize_cholqr_split_mv8(i64 n, i64 m, double *q)
+{
+  for (i64 bk = 0; bk < m; bk += 8)
+  {
+    double *qb = q + n * bk;
+    double s[8][8], U[8][8];
+    std::memset(s, 0, sizeof s);
+    for (i64 i = 0; i < n; ++i)
+      for (int k = 0; k < 8; ++k)
+        for (int j = 0; j < 8; ++j) s[k][j] += qb[i * 8 + k] * qb[i * 8 + j];
+    cholqr_factor(s, U);
+    apply_upper(n, qb, U);
+    for (i64 bj = bk + 8; bj < m; bj += 8)
+    {
+      double *qj = q + n * bj;
+      for (int h = 0; h < 8; h += 4)
+      {
+        double S[4][8];
+        std::memset(S, 0, sizeof S);
+        for (i64 i = 0; i < n; ++i)
+          for (int k = 0; k < 4; ++k)
+            for (int j = 0; j < 8; ++j) S[k][j] += qb[i * 8 + h + k] * qj[i * 8 + j];
+        for (i64 i = 0; i < n; ++i)
+          for (int k = 0; k < 4; ++k)
+            for (int j = 0; j < 8; ++j) qj[i * 8 + j] -= S[k][j] * qb[i * 8 + h + k];
+      }
+    }
+  }
+}
+
 // a11: B_orthonormalize_blocked (kernels_cpp.hh:356-591); returns max off-diagonal "R" entry.
 double orc_b_orthonormalize_mv8(i64 n, i64 m, const i64 *rowptr, const i32 *col, const double *val, double *q)
 {

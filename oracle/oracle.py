@@ -47,6 +47,7 @@ def _load():
         "orc_orthonormalize_naive": (None, [_i64, _i64, _f64p]),
         "orc_orthonormalize_mv8": (None, [_i64, _i64, _f64p]),
         "orc_orthonormalize_cholqr_mv8": (None, [_i64, _i64, _f64p]),
+        "orc_orthonormalize_cholqr_split_mv8": (None, [_i64, _i64, _f64p]),
         "orc_b_orthonormalize_mv8": (ctypes.c_double, [_i64, _i64, _i64p, _i32p, _f64p, _f64p]),
         "orc_flops_orthonormalize": (ctypes.c_double, [_int, _int]),
         "orc_bytes_orthonormalize_naive": (ctypes.c_double, [_int, _int]),
@@ -175,6 +176,8 @@ def orthonormalize_mv8(Q, n, m, variant="mgs"):
         lib.orc_orthonormalize_mv8(n, m, Q)
     elif variant == "cholqr":
         lib.orc_orthonormalize_cholqr_mv8(n, m, Q)
+    elif variant == "cholqr_split":
+        lib.orc_orthonormalize_cholqr_split_mv8(n, m, Q)
     else:
         raise ValueError(variant)
     return Q

@@ -114,7 +114,8 @@ def test_gram_mfma(ctx, n, m1, m2):
     assert np.all(np.abs(G.get().reshape(m1, m2) - ref) <= bound)
 
 
-@pytest.mark.parametrize("variant,name", [(eigmi.ORTHO_MGS, "mgs"), (eigmi.ORTHO_CHOLQR, "cholqr")])
+@pytest.mark.parametrize("variant,name", [(eigmi.ORTHO_MGS, "mgs"), (eigmi.ORTHO_CHOLQR, "cholqr"),
+                                          (eigmi.ORTHO_CHOLQR_SPLIT, "cholqr_split")])
 @pytest.mark.parametrize("n,m", [(4096, 8), (4096, 32), (5000, 16), (100, 8), (1000, 16), (2048, 8)])
 def test_orthonormalize_blocked(ctx, variant, name, n, m):
     Qh = oracle.random_mv8(n, m, 21)
@@ -125,6 +126,26 @@ def test_orthonormalize_blocked(ctx, variant, name, n, m):
     assert np.abs(got.T @ got - np.eye(m)).max() < 1e-13
     # same thin QR as the reference algorithm: elementwise within 1e-12 (random, well conditioned)
     assert np.abs(got - ref).max() < 1e-12
+
+
+def test_cholqr_split_half_order(ctx):
+    """orthonormalize_avx2_b8 (kernels_avx2.hh:255-381) projects a later block with columns 0-3 of
+    the diagonal block, then 4-7 against the updated block; _v2 (:385-622) in one 8x8 step.  On a
+    second block that is nearly a combination of the first (1e-7 noise) the two orders differ at
+    ~5e-9; the device split variant follows the split restatement 10x more closely than that."""
+    n, m = 3000, 16
+    rng = np.random.default_rng(1)
+    X = rng.standard_normal((n, m))
+    X[:, 8:] = X[:, :8] @ rng.standard_normal((8, 8)) + 1e-7 * rng.standard_normal((n, 8))
+    Qh = oracle.cols_to_mv(X)
+    split = oracle.mv_to_cols(oracle.orthonormalize_mv8(Qh, n, m, "cholqr_split"), n, m)
+    single = oracle.mv_to_cols(oracle.orthonormalize_mv8(Qh, n, m, "cholqr"), n, m)
+    Q = ctx.array(Qh)
+    eigmi.orthonormalize_mv8(ctx, n, m, Q, eigmi.ORTHO_CHOLQR_SPLIT)
+    got = oracle.mv_to_cols(Q.get(), n, m)
+    gap = np.abs(split - single).max()
+    assert gap > 1e-10
+    assert np.abs(got - split).max() < 0.1 * gap
 
 
 @pytest.mark.parametrize("n,m", [(3000, 16), (4096, 8), (513, 8)])

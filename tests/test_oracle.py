@@ -46,7 +46,7 @@ def test_standard_largest_matches_recorded_reference_run(golden_dir):
 
 
 @pytest.mark.parametrize("m", [8, 16, 32])
-@pytest.mark.parametrize("variant", ["mgs", "cholqr"])
+@pytest.mark.parametrize("variant", ["mgs", "cholqr", "cholqr_split"])
 def test_orthonormalize_blocked(m, variant):
     n = 1000
     Q = oracle.random_mv8(n, m, 7)

@@ -23,7 +23,7 @@ def t(f, reps=3):
 
 
 ctx = eigmi.Context(0)
-N = 64
+N = int(sys.argv[1]) if len(sys.argv) > 1 else 64
 A = oracle.laplace2d(N)
 th, _ = t(lambda: eigmi.LU.from_bcsr(None, A.rowptr, A.col, A.val))
 td, lu = t(lambda: eigmi.LU.from_bcsr(ctx, A.rowptr, A.col, A.val))
