@@ -1,8 +1,11 @@
 // dense.cpp -- small dense host linear algebra of the Krylov drivers: the tridiagonal QL
 // eigensolver (Lanczos), Householder reduction of a dense symmetric matrix (block Lanczos'
-// block-tridiagonal T), Cholesky and triangular inverse (CholQR of 8..32-column blocks).
+// block-tridiagonal T), Cholesky and triangular inverse (CholQR of 8..32-column blocks), and the
+// general real eigenproblem of the Arnoldi drivers' projected matrix (Hessenberg reduction, the
+// Francis double-shift QR, inverse-iteration eigenvectors).
 #include <algorithm>
 #include <cmath>
+#include <complex>
 #include <numeric>
 #include <vector>
 
@@ -190,6 +193,282 @@ void tri_upper_inv(int n, const double *R, double *Rinv)
       Rinv[(size_t)i * n + c] = s / R[(size_t)i * n + i];
     }
   }
+}
+
+// ---------------------------------------------------------------------------------------------
+// General real eigenproblem of the Arnoldi drivers' m x m projected matrix (m <= a few hundred).
+// Eigenvalues: Gaussian-elimination reduction to upper Hessenberg form (a similarity with row
+// pivoting), then the Francis double-shift QR iteration (the EISPACK hqr algorithm: deflation on
+// negligible subdiagonals, exceptional shifts at iterations 10 and 20).  Eigenvectors: two steps of
+// inverse iteration with the ORIGINAL matrix in complex arithmetic (LU with partial pivoting; a
+// zero pivot is replaced by eps ||G||), unit 2-norm, phase such that the largest entry is real.
+// ---------------------------------------------------------------------------------------------
+namespace {
+
+void hess_reduce(int n, std::vector<double> &a)  // row-major, in place; entries below the subdiagonal zeroed
+{
+  auto A = [&](int i, int j) -> double & { return a[(size_t)i * n + j]; };
+  for (int m = 1; m < n - 1; ++m)
+  {
+    double x = 0.0;
+    int piv = m;
+    for (int j = m; j < n; ++j)
+      if (std::fabs(A(j, m - 1)) > std::fabs(x))
+      {
+        x = A(j, m - 1);
+        piv = j;
+      }
+    if (piv != m)
+    {
+      for (int j = m - 1; j < n; ++j) std::swap(A(piv, j), A(m, j));
+      for (int j = 0; j < n; ++j) std::swap(A(j, piv), A(j, m));
+    }
+    if (x != 0.0)
+      for (int i = m + 1; i < n; ++i)
+      {
+        double y = A(i, m - 1);
+        if (y == 0.0) continue;
+        y /= x;
+        A(i, m - 1) = y;
+        for (int j = m; j < n; ++j) A(i, j) -= y * A(m, j);
+        for (int j = 0; j < n; ++j) A(j, m) += y * A(j, i);
+      }
+  }
+  for (int i = 2; i < n; ++i)
+    for (int j = 0; j < i - 1; ++j) A(i, j) = 0.0;
+}
+
+// Eigenvalues of the upper Hessenberg matrix a (destroyed).  False when an eigenvalue needed more
+// than 60 iterations.
+bool hess_eigvals(int n, std::vector<double> &a, std::vector<std::complex<double>> &w)
+{
+  // 1-based accessor (the algorithm's natural indexing)
+  auto A = [&](int i, int j) -> double & { return a[(size_t)(i - 1) * n + (j - 1)]; };
+  auto sgn = [](double x, double y) { return y >= 0.0 ? std::fabs(x) : -std::fabs(x); };
+  w.assign(n, {0.0, 0.0});
+  double anorm = 0.0;
+  for (int i = 1; i <= n; ++i)
+    for (int j = std::max(i - 1, 1); j <= n; ++j) anorm += std::fabs(A(i, j));
+  int nn = n, l = 1;
+  double t = 0.0, x, y, z, wv, p = 0, q = 0, r = 0, s, u, v;
+  while (nn >= 1)
+  {
+    int its = 0;
+    do
+    {
+      for (l = nn; l >= 2; --l)
+      {
+        s = std::fabs(A(l - 1, l - 1)) + std::fabs(A(l, l));
+        if (s == 0.0) s = anorm;
+        if (std::fabs(A(l, l - 1)) + s == s)
+        {
+          A(l, l - 1) = 0.0;
+          break;
+        }
+      }
+      x = A(nn, nn);
+      if (l == nn)
+      {
+        w[nn - 1] = {x + t, 0.0};
+        --nn;
+      }
+      else
+      {
+        y = A(nn - 1, nn - 1);
+        wv = A(nn, nn - 1) * A(nn - 1, nn);
+        if (l == nn - 1)
+        {
+          p = 0.5 * (y - x);
+          q = p * p + wv;
+          z = std::sqrt(std::fabs(q));
+          x += t;
+          if (q >= 0.0)
+          {
+            z = p + sgn(z, p);
+            const double a2 = x + z, a1 = z != 0.0 ? x - wv / z : x + z;
+            w[nn - 2] = {a2, 0.0};
+            w[nn - 1] = {a1, 0.0};
+          }
+          else
+          {
+            w[nn - 2] = {x + p, -z};
+            w[nn - 1] = {x + p, z};
+          }
+          nn -= 2;
+        }
+        else
+        {
+          if (its == 60) return false;
+          if (its == 10 || its == 20)
+          {
+            t += x;
+            for (int i = 1; i <= nn; ++i) A(i, i) -= x;
+            s = std::fabs(A(nn, nn - 1)) + std::fabs(A(nn - 1, nn - 2));
+            y = x = 0.75 * s;
+            wv = -0.4375 * s * s;
+          }
+          ++its;
+          int m;
+          for (m = nn - 2; m >= l; --m)
+          {
+            z = A(m, m);
+            r = x - z;
+            s = y - z;
+            p = (r * s - wv) / A(m + 1, m) + A(m, m + 1);
+            q = A(m + 1, m + 1) - z - r - s;
+            r = A(m + 2, m + 1);
+            s = std::fabs(p) + std::fabs(q) + std::fabs(r);
+            p /= s;
+            q /= s;
+            r /= s;
+            if (m == l) break;
+            u = std::fabs(A(m, m - 1)) * (std::fabs(q) + std::fabs(r));
+            v = std::fabs(p) * (std::fabs(A(m - 1, m - 1)) + std::fabs(z) + std::fabs(A(m + 1, m + 1)));
+            if (u + v == v) break;
+          }
+          for (int i = m + 2; i <= nn; ++i)
+          {
+            A(i, i - 2) = 0.0;
+            if (i != m + 2) A(i, i - 3) = 0.0;
+          }
+          for (int k = m; k <= nn - 1; ++k)
+          {
+            if (k != m)
+            {
+              p = A(k, k - 1);
+              q = A(k + 1, k - 1);
+              r = 0.0;
+              if (k != nn - 1) r = A(k + 2, k - 1);
+              if ((x = std::fabs(p) + std::fabs(q) + std::fabs(r)) != 0.0)
+              {
+                p /= x;
+                q /= x;
+                r /= x;
+              }
+            }
+            if ((s = sgn(std::sqrt(p * p + q * q + r * r), p)) != 0.0)
+            {
+              if (k == m)
+              {
+                if (l != m) A(k, k - 1) = -A(k, k - 1);
+              }
+              else
+                A(k, k - 1) = -s * x;
+              p += s;
+              x = p / s;
+              y = q / s;
+              z = r / s;
+              q /= p;
+              r /= p;
+              for (int j = k; j <= nn; ++j)
+              {
+                p = A(k, j) + q * A(k + 1, j);
+                if (k != nn - 1)
+                {
+                  p += r * A(k + 2, j);
+                  A(k + 2, j) -= p * z;
+                }
+                A(k + 1, j) -= p * y;
+                A(k, j) -= p * x;
+              }
+              const int mmin = nn < k + 3 ? nn : k + 3;
+              for (int i = l; i <= mmin; ++i)
+              {
+                p = x * A(i, k) + y * A(i, k + 1);
+                if (k != nn - 1)
+                {
+                  p += z * A(i, k + 2);
+                  A(i, k + 2) -= p * r;
+                }
+                A(i, k + 1) -= p * q;
+                A(i, k) -= p;
+              }
+            }
+          }
+        }
+      }
+    } while (l < nn - 1);
+  }
+  return true;
+}
+
+// Eigenvector of the real matrix g (row-major n x n) for the eigenvalue theta.
+void inverse_iteration(int n, const std::vector<double> &g, std::complex<double> theta,
+                       std::vector<std::complex<double>> &y)
+{
+  typedef std::complex<double> C;
+  double gn = 0.0;
+  for (double v : g) gn = std::max(gn, std::fabs(v));
+  const double tiny = std::max(gn, 1e-300) * 2.220446049250313e-16;
+  std::vector<C> M((size_t)n * n);
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) M[(size_t)i * n + j] = g[(size_t)i * n + j] - (i == j ? theta : C(0.0));
+  std::vector<int> piv(n);
+  for (int k = 0; k < n; ++k)
+  {
+    int pk = k;
+    for (int i = k + 1; i < n; ++i)
+      if (std::abs(M[(size_t)i * n + k]) > std::abs(M[(size_t)pk * n + k])) pk = i;
+    piv[k] = pk;
+    if (pk != k)
+      for (int j = 0; j < n; ++j) std::swap(M[(size_t)k * n + j], M[(size_t)pk * n + j]);
+    if (std::abs(M[(size_t)k * n + k]) < tiny) M[(size_t)k * n + k] = tiny;
+    const C d = M[(size_t)k * n + k];
+    for (int i = k + 1; i < n; ++i)
+    {
+      const C f = M[(size_t)i * n + k] / d;
+      M[(size_t)i * n + k] = f;
+      if (f != C(0.0))
+        for (int j = k + 1; j < n; ++j) M[(size_t)i * n + j] -= f * M[(size_t)k * n + j];
+    }
+  }
+  y.assign(n, C(1.0));
+  for (int i = 0; i < n; ++i) y[i] += C(0.0, 1e-3 * (i % 7));  // generic start (not orthogonal to any vector)
+  for (int it = 0; it < 3; ++it)
+  {
+    for (int k = 0; k < n; ++k)
+      if (piv[k] != k) std::swap(y[k], y[piv[k]]);
+    for (int i = 0; i < n; ++i)
+      for (int k = 0; k < i; ++k) y[i] -= M[(size_t)i * n + k] * y[k];
+    for (int i = n - 1; i >= 0; --i)
+    {
+      for (int k = i + 1; k < n; ++k) y[i] -= M[(size_t)i * n + k] * y[k];
+      y[i] /= M[(size_t)i * n + i];
+    }
+    double nrm = 0.0;
+    int big = 0;
+    for (int i = 0; i < n; ++i)
+    {
+      nrm += std::norm(y[i]);
+      if (std::abs(y[i]) > std::abs(y[big])) big = i;
+    }
+    const C ph = std::abs(y[big]) > 0.0 ? std::conj(y[big]) / std::abs(y[big]) : C(1.0);
+    nrm = std::sqrt(nrm);
+    for (auto &v : y) v = v * ph / nrm;
+  }
+}
+
+}  // namespace
+
+bool gen_eig(int n, const std::vector<double> &g, std::vector<std::complex<double>> &w,
+             std::vector<std::complex<double>> &Y)
+{
+  std::vector<double> h = g;
+  hess_reduce(n, h);
+  if (!hess_eigvals(n, h, w)) return false;
+  Y.assign((size_t)n * n, 0.0);
+  std::vector<std::complex<double>> y;
+  for (int j = 0; j < n; ++j)
+  {
+    if (j > 0 && w[j].imag() != 0.0 && w[j] == std::conj(w[j - 1]))
+    {
+      for (int i = 0; i < n; ++i) Y[(size_t)i * n + j] = std::conj(Y[(size_t)i * n + j - 1]);
+      continue;
+    }
+    inverse_iteration(n, g, w[j], y);
+    for (int i = 0; i < n; ++i) Y[(size_t)i * n + j] = y[i];
+  }
+  return true;
 }
 
 }  // namespace eigmi

@@ -4,6 +4,7 @@
 //                         (arpack_geneo_wrapper.hh:257-279, :621-632) -- the benchmark unit
 //   eig_lanczos_solve     Lanczos with full DGKS re-orthogonalisation (ARPACK's conditional second pass) + Ritz extraction
 #include <algorithm>
+#include <complex>
 #include <cmath>
 #include <cstring>
 #include <numeric>
@@ -557,10 +558,288 @@ extern "C" int eig_shift_invert_adaptive(eig_mat_t A, eig_mat_t B, eig_lu_t lu, 
       shift_invert_core(A, B, F, sigma, nev, 0, tol, maxit, seed, eval_host, evec_host, nullptr);
       ++pass;
       if (eval_host[nev - 1] >= threshold || nev >= max_nev) break;
-      nev = std::min(max_nev, (int)(nev * 1.3));
+      // (:770; for nev <= 3, int(nev * 1.3) == nev and the reference would solve the same problem
+      // forever -- there nev grows by one instead; from nev = 4 on the sequences are identical)
+      nev = std::min(max_nev, std::max(nev + 1, (int)(nev * 1.3)));
     }
     *nev_out = nev;
     if (passes) *passes = pass;
+  });
+}
+
+// ============================================================================================
+// Non-symmetric modes (arpack_geneo_wrapper.hh:428-578): computeStdNonSymMinMagnitude
+// (ARNonSymStdEig on OP = (A - sigma B)^-1 B, "LM", lambda = sigma + 1 / Re(nu)) and
+// computeGenNonSymShiftInvertMinMagnitude (ARNonSymGenEig, real shift-invert mode: the same OP in
+// the B-inner product, lambda = sigma + 1 / nu).  ARPACK's dnaupd restarts implicitly with exact
+// shifts; here the restart is Stewart's Krylov-Schur in its eigenvector-basis form: the projected
+// matrix G of the Krylov decomposition  OP V = V G + f c^T  has its wanted eigenvectors (real and
+// imaginary parts of complex pairs) orthonormalised into Z (m x kk); span(Z) is G-invariant, so
+// OP (V Z) = (V Z)(Z^T G Z) + f (Z^T c)^T is again a Krylov decomposition, extended by Arnoldi
+// steps (CGS2 in the chosen inner product) back to m vectors.  The same wanted Ritz values as
+// ARPACK's restart filter (the polynomial with the unwanted Ritz values as roots annihilates the
+// complement of span(Z)); convergence: ||f|| |c^T y| <= tol |nu| (dnaupd's Ritz estimate).
+// ============================================================================================
+namespace {
+
+void arnoldi_core(eig_mat_t A, eig_mat_t B, const LuRef &F, double sigma, int nev, int ncv, double tol, int maxit,
+                  unsigned seed, bool gen, double *eval_re, double *eval_im, double *evec_host, int *restarts)
+{
+  typedef std::complex<double> C;
+  eig_ctx_t ctx = A->ctx;
+  EIG_HIP(hipSetDevice(ctx->device));
+  hipStream_t s = ctx->stream;
+  const i64 n = A->nb_rows;
+  if (ncv <= 0) ncv = (int)std::min<i64>(n, std::max(2 * nev + 1, 20));  // ARPACK++ ncv = 0 (auto)
+  EIG_CHECK(nev + 2 <= ncv && ncv <= n && ncv <= 500, EIG_ERR_ARG, "Arnoldi: need nev + 2 <= ncv <= min(n, 500)");
+  if (tol <= 0.0) tol = 2.220446049250313e-16;
+  if (maxit <= 0) maxit = 100 * nev;
+  const int m = ncv;
+  const bool bip = gen && B;  // B-inner product
+  DevBuf Vb((size_t)(m + 1) * n * 8), BVb(bip ? (size_t)(m + 1) * n * 8 : 8), Wb(n * 8), BWb(n * 8), X8b(n * 64),
+      Y8b(n * 64), Tb((size_t)2 * (m + 1) * n * 8), cb((size_t)(m + 8) * 8 * 2);
+  double *V = Vb.d(), *BV = bip ? BVb.d() : Vb.d(), *W = Wb.d(), *BW = BWb.d(), *X8 = X8b.d(), *Y8 = Y8b.d();
+  double *cd = cb.d(), *sc = cd + m + 8;
+  EIG_HIP(hipMemsetAsync(X8, 0, n * 64, s));
+  auto bmul = [&](const double *x, double *y) {  // y = B x
+    if (B) launch_spmv(*B, x, y, nullptr, 0, B->nslices, s);
+    else if (y != x) EIG_HIP(hipMemcpyAsync(y, x, n * 8, hipMemcpyDeviceToDevice, s));
+  };
+  auto dot = [&](const double *x, const double *y) {
+    launch_dot(n, x, y, sc, 0, s, ctx->red);
+    double h = 0.0;
+    EIG_HIP(hipMemcpyAsync(&h, sc, 8, hipMemcpyDeviceToHost, s));
+    EIG_HIP(hipStreamSynchronize(s));
+    return h;
+  };
+  auto solve = [&](const double *bx, double *y) {  // y = (A - sigma B)^-1 bx
+    EIG_HIP(hipMemcpy2DAsync(X8, 64, bx, 8, 8, n, hipMemcpyDeviceToDevice, s));
+    lu_inverse_device(F.lu, 8, X8, Y8, s);
+    EIG_HIP(hipMemcpy2DAsync(y, 8, Y8, 64, 8, n, hipMemcpyDeviceToDevice, s));
+  };
+  auto norm_in = [&](double *x, double *bx) {  // ||x|| in the driver's inner product; bx = B x (bip)
+    if (bip) bmul(x, bx);
+    return std::sqrt(std::max(0.0, dot(x, bip ? bx : x)));
+  };
+  // start vector: mt19937(seed) normal numbers; the generalised mode puts it into range(OP) first
+  // (dgetv0 for mode 3)
+  {
+    std::vector<double> h(n);
+    host_random_normal(n, seed, h.data());
+    EIG_HIP(hipMemcpyAsync(W, h.data(), n * 8, hipMemcpyHostToDevice, s));
+    if (gen)
+    {
+      bmul(W, BW);
+      solve(BW, V);
+    }
+    else
+      EIG_HIP(hipMemcpyAsync(V, W, n * 8, hipMemcpyDeviceToDevice, s));
+    const double nb = norm_in(V, BV);
+    EIG_CHECK(nb > 0.0, EIG_ERR_BREAKDOWN, "Arnoldi: zero start vector");
+    launch_scal(n, 1.0 / nb, V, s);
+    if (bip) launch_scal(n, 1.0 / nb, BV, s);
+  }
+  std::vector<double> G((size_t)m * m, 0.0), cvec, ctot(m + 1), ch(m + 1);
+  std::vector<C> w, Y;
+  std::vector<int> ord(m);
+  double beta = 0.0;
+  int k = 0, nrestart = 0;
+  for (;;)
+  {
+    // extend the Krylov decomposition from k to m vectors (Arnoldi steps)
+    for (int j = k; j < m; ++j)
+    {
+      if (j > 0)
+        for (int i = 0; i < j; ++i) G[(size_t)j * m + i] = beta * cvec[i];
+      double *vj = V + (i64)j * n;
+      bmul(vj, BW);
+      solve(BW, W);  // W = OP v_j (the reverse-communication product)
+      std::fill(ctot.begin(), ctot.end(), 0.0);
+      for (int pass = 0; pass < 2; ++pass)  // CGS2 against v_0 .. v_j in the inner product
+      {
+        launch_gemv_t(n, j + 1, BV, n, W, cd, 0, s, ctx->red);
+        launch_gemv_n_sub(n, j + 1, V, n, cd, nullptr, W, s);
+        EIG_HIP(hipMemcpyAsync(ch.data(), cd, (j + 1) * 8, hipMemcpyDeviceToHost, s));
+        EIG_HIP(hipStreamSynchronize(s));
+        for (int i = 0; i <= j; ++i) ctot[i] += ch[i];
+      }
+      for (int i = 0; i <= j; ++i) G[(size_t)i * m + j] = ctot[i];
+      beta = norm_in(W, BW);
+      double hn = 0.0;
+      for (int i = 0; i <= j; ++i) hn = std::max(hn, std::fabs(ctot[i]));
+      EIG_CHECK(beta > 1e-14 * hn, EIG_ERR_BREAKDOWN,
+                "Arnoldi: invariant subspace reached (choose ncv < n or another seed)");
+      double *vn = V + (i64)(j + 1) * n;
+      EIG_HIP(hipMemcpyAsync(vn, W, n * 8, hipMemcpyDeviceToDevice, s));
+      launch_scal(n, 1.0 / beta, vn, s);
+      if (bip)
+      {
+        double *bvn = BV + (i64)(j + 1) * n;
+        EIG_HIP(hipMemcpyAsync(bvn, BW, n * 8, hipMemcpyDeviceToDevice, s));
+        launch_scal(n, 1.0 / beta, bvn, s);
+      }
+      cvec.assign(j + 1, 0.0);
+      cvec[j] = 1.0;
+    }
+    EIG_CHECK(gen_eig(m, G, w, Y), EIG_ERR_BREAKDOWN, "Arnoldi: QR iteration of the projected matrix failed");
+    // "LM": largest |nu| first (conjugate partners keep their relative order)
+    std::iota(ord.begin(), ord.end(), 0);
+    std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return std::abs(w[a]) > std::abs(w[b]); });
+    auto resid = [&](int q) {
+      C r = 0.0;
+      for (int i = 0; i < m; ++i) r += cvec[i] * Y[(size_t)i * m + q];
+      return beta * std::abs(r);
+    };
+    bool conv = true;
+    for (int i = 0; i < nev; ++i)
+      if (resid(ord[i]) > tol * std::abs(w[ord[i]])) conv = false;
+    if (conv || nrestart >= maxit) break;
+    // Krylov-Schur restart: kk wanted vectors, never splitting a conjugate pair
+    int kk = std::min(m - 2, nev + (m - nev) / 2);
+    if (w[ord[kk - 1]].imag() != 0.0 && w[ord[kk]] == std::conj(w[ord[kk - 1]])) ++kk;
+    if (kk > m - 1) kk -= 2;
+    std::vector<double> Z((size_t)m * kk, 0.0);  // row-major m x kk
+    {
+      int col = 0;
+      std::vector<char> used(m, 0);
+      for (int q = 0; q < kk && col < kk; ++q)
+      {
+        const int e = ord[q];
+        if (used[e]) continue;
+        used[e] = 1;
+        for (int i = 0; i < m; ++i) Z[(size_t)i * kk + col] = Y[(size_t)i * m + e].real();
+        ++col;
+        if (w[e].imag() != 0.0 && col < kk)
+        {
+          for (int i = 0; i < m; ++i) Z[(size_t)i * kk + col] = Y[(size_t)i * m + e].imag();
+          ++col;
+          for (int q2 = q + 1; q2 < m; ++q2)
+            if (w[ord[q2]] == std::conj(w[e]))
+            {
+              used[ord[q2]] = 1;
+              break;
+            }
+        }
+      }
+      kk = col;
+      for (int c = 0; c < kk; ++c)  // MGS, twice
+        for (int pass = 0; pass < 2; ++pass)
+        {
+          for (int p = 0; p < c; ++p)
+          {
+            double d = 0.0;
+            for (int i = 0; i < m; ++i) d += Z[(size_t)i * kk + p] * Z[(size_t)i * kk + c];
+            for (int i = 0; i < m; ++i) Z[(size_t)i * kk + c] -= d * Z[(size_t)i * kk + p];
+          }
+          double nr = 0.0;
+          for (int i = 0; i < m; ++i) nr += Z[(size_t)i * kk + c] * Z[(size_t)i * kk + c];
+          nr = std::sqrt(nr);
+          EIG_CHECK(nr > 0.0, EIG_ERR_BREAKDOWN, "Arnoldi: dependent Ritz vectors at restart");
+          for (int i = 0; i < m; ++i) Z[(size_t)i * kk + c] /= nr;
+        }
+    }
+    // G <- Z^T G Z, c <- Z^T c; V <- V Z, v_kk <- v_m
+    std::vector<double> GZ((size_t)m * kk, 0.0), Gn((size_t)m * m, 0.0), cn(kk, 0.0);
+    for (int i = 0; i < m; ++i)
+      for (int q = 0; q < kk; ++q)
+      {
+        double a = 0.0;
+        for (int l = 0; l < m; ++l) a += G[(size_t)i * m + l] * Z[(size_t)l * kk + q];
+        GZ[(size_t)i * kk + q] = a;
+      }
+    for (int p = 0; p < kk; ++p)
+    {
+      for (int q = 0; q < kk; ++q)
+      {
+        double a = 0.0;
+        for (int i = 0; i < m; ++i) a += Z[(size_t)i * kk + p] * GZ[(size_t)i * kk + q];
+        Gn[(size_t)p * m + q] = a;
+      }
+      for (int i = 0; i < m; ++i) cn[p] += Z[(size_t)i * kk + p] * cvec[i];
+    }
+    G.swap(Gn);
+    cvec = cn;
+    double *Tmp = Tb.d();
+    std::vector<double> coef(m);
+    for (int q = 0; q < kk; ++q)
+    {
+      for (int i = 0; i < m; ++i) coef[i] = Z[(size_t)i * kk + q];
+      EIG_HIP(hipMemcpyAsync(cd, coef.data(), m * 8, hipMemcpyHostToDevice, s));
+      launch_gemv_n_set(n, m, V, n, cd, nullptr, Tmp + (i64)q * n, s);
+      if (bip) launch_gemv_n_set(n, m, BV, n, cd, nullptr, Tmp + (i64)(kk + q) * n, s);
+      EIG_HIP(hipStreamSynchronize(s));
+    }
+    EIG_HIP(hipMemcpyAsync(V, Tmp, (size_t)kk * n * 8, hipMemcpyDeviceToDevice, s));
+    EIG_HIP(hipMemcpyAsync(V + (i64)kk * n, V + (i64)m * n, n * 8, hipMemcpyDeviceToDevice, s));
+    if (bip)
+    {
+      EIG_HIP(hipMemcpyAsync(BV, Tmp + (i64)kk * n, (size_t)kk * n * 8, hipMemcpyDeviceToDevice, s));
+      EIG_HIP(hipMemcpyAsync(BV + (i64)kk * n, BV + (i64)m * n, n * 8, hipMemcpyDeviceToDevice, s));
+    }
+    k = kk;
+    ++nrestart;
+  }
+  // eigenvalues of the original problem, ascending by real part (:484-498, :556-571)
+  std::vector<C> lam(nev);
+  for (int i = 0; i < nev; ++i)
+  {
+    const C nu = w[ord[i]];
+    lam[i] = gen ? C(sigma) + 1.0 / nu : C(sigma + 1.0 / nu.real(), (C(sigma) + 1.0 / nu).imag());
+  }
+  std::vector<int> idx(nev);
+  std::iota(idx.begin(), idx.end(), 0);
+  std::stable_sort(idx.begin(), idx.end(), [&](int a, int b) { return lam[a].real() < lam[b].real(); });
+  for (int i = 0; i < nev; ++i)
+  {
+    eval_re[i] = lam[idx[i]].real();
+    if (eval_im) eval_im[i] = lam[idx[i]].imag();
+  }
+  if (evec_host)
+  {
+    // x = V y, unit 2-norm as a complex vector; ARPACK's raw storage of a conjugate pair: the real
+    // part for the member with Im(nu) > 0, the imaginary part for its partner
+    std::vector<double> coef(m);
+    for (int q = 0; q < nev; ++q)
+    {
+      const int e = ord[idx[q]];
+      const bool cplx = w[e].imag() != 0.0;
+      int ey = e;
+      if (cplx && w[e].imag() < 0.0)
+        for (int i = 0; i < m; ++i)
+          if (w[i] == std::conj(w[e])) ey = i;
+      double nr2 = 0.0;
+      for (int part = 0; part < (cplx ? 2 : 1); ++part)
+      {
+        for (int i = 0; i < m; ++i)
+          coef[i] = part == 0 ? Y[(size_t)i * m + ey].real() : Y[(size_t)i * m + ey].imag();
+        EIG_HIP(hipMemcpyAsync(cd, coef.data(), m * 8, hipMemcpyHostToDevice, s));
+        launch_gemv_n_set(n, m, V, n, cd, nullptr, part == 0 ? W : BW, s);
+        nr2 += dot(part == 0 ? W : BW, part == 0 ? W : BW);
+      }
+      double *x = (cplx && w[e].imag() < 0.0) ? BW : W;
+      launch_scal(n, 1.0 / std::sqrt(nr2), x, s);
+      EIG_HIP(hipMemcpyAsync(evec_host + (i64)q * n, x, n * 8, hipMemcpyDeviceToHost, s));
+      EIG_HIP(hipStreamSynchronize(s));
+    }
+  }
+  if (restarts) *restarts = nrestart;
+}
+
+}  // namespace
+
+extern "C" int eig_arnoldi_shift_invert(eig_mat_t A, eig_mat_t B, eig_lu_t lu, double sigma, int nev, int ncv,
+                                        double tol, int maxit, unsigned seed, int mode, double *eval_re,
+                                        double *eval_im, double *evec_host, int *restarts)
+{
+  return guard(A ? A->ctx : nullptr, [&] {
+    EIG_CHECK(A && eval_re && nev > 0, EIG_ERR_ARG, "eig_arnoldi_shift_invert: bad argument");
+    EIG_CHECK(mode == EIG_ARNOLDI_STD || mode == EIG_ARNOLDI_GEN, EIG_ERR_ARG, "eig_arnoldi_shift_invert: bad mode");
+    shift_invert_check(A, B);
+    EIG_HIP(hipSetDevice(A->ctx->device));
+    LuRef F;
+    shift_invert_factor(A, B, lu, sigma, F);
+    arnoldi_core(A, B, F, sigma, nev, ncv, tol, maxit, seed, mode == EIG_ARNOLDI_GEN, eval_re, eval_im, evec_host,
+                 restarts);
   });
 }
 

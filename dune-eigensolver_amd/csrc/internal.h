@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <complex>
 #include <condition_variable>
 #include <cstdint>
 #include <mutex>
@@ -407,6 +408,11 @@ void householder_tridiag(int n, std::vector<double> A, std::vector<double> &d, s
 void sym_eig(int n, const std::vector<double> &A, std::vector<double> &w, std::vector<double> &Z);
 bool chol_upper(int n, const double *G, double *R);
 void tri_upper_inv(int n, const double *R, double *Rinv);
+// General real n x n matrix g (row-major): eigenvalues w and unit eigenvectors Y (column j of the
+// row-major n x n Y belongs to w[j]; conjugate pairs adjacent).  False when the QR iteration
+// did not converge.
+bool gen_eig(int n, const std::vector<double> &g, std::vector<std::complex<double>> &w,
+             std::vector<std::complex<double>> &Y);
 
 // ---- helpers in api.cpp --------------------------------------------------------------------
 // Ghost entries of window vector x (and x2 when given) from their owners.

@@ -114,6 +114,8 @@ SIGNATURES = {
     "eig_lu_solver_info": (_int, [_vp, ctypes.POINTER(_int), ctypes.POINTER(_int), ctypes.POINTER(_int)]),
     "eig_shift_invert_adaptive": (_int, [_vp, _vp, _vp, _dbl, _dbl, _int, _int, _dbl, _int, _u, _vp, _vp,
                                          ctypes.POINTER(_int), ctypes.POINTER(_int)]),
+    "eig_arnoldi_shift_invert": (_int, [_vp, _vp, _vp, _dbl, _int, _int, _dbl, _int, _u, _int, _vp, _vp, _vp,
+                                        ctypes.POINTER(_int)]),
     "eig_reorder_rcm": (_int, [_i64, _vp, _vp, _vp]),
     "eig_permute_symmetric": (_int, [_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "eig_mat_destroy": (_int, [_vp]),
@@ -706,6 +708,24 @@ def shift_invert_adaptive(A, threshold, initial_nev, max_nev, sigma=0.0, B=None,
                                               ctypes.byref(ps)))
     k = nv.value
     return ev[:k], (evec[:k * A.n].reshape(k, A.n) if want_evec else None), ps.value
+
+
+ARNOLDI_STD, ARNOLDI_GEN = 0, 1
+
+
+def arnoldi_shift_invert(A, nev, sigma=0.0, B=None, mode="std", ncv=0, tol=0.0, maxit=0, seed=123, lu=None,
+                         want_evec=True):
+    """computeStdNonSymMinMagnitude (mode "std") / computeGenNonSymShiftInvertMinMagnitude (mode
+    "gen"): (eigenvalues ascending by real part as a complex array, eigenvectors in ARPACK's raw
+    storage or None, restarts)."""
+    er, ei = np.zeros(nev), np.zeros(nev)
+    evec = np.zeros(nev * A.n) if want_evec else None
+    r = _int(0)
+    A.ctx.check(lib.eig_arnoldi_shift_invert(A.h, B.h if B is not None else None, lu.h if lu else None, sigma, nev,
+                                             ncv, tol, maxit, seed, ARNOLDI_GEN if mode == "gen" else ARNOLDI_STD,
+                                             _np_ptr(er), _np_ptr(ei), _np_ptr(evec) if want_evec else None,
+                                             ctypes.byref(r)))
+    return er + 1j * ei, (evec.reshape(nev, A.n) if want_evec else None), r.value
 
 
 class BlockLanczos:

@@ -372,13 +372,33 @@ int eig_shift_invert_solve(eig_mat_t A, eig_mat_t B, eig_lu_t lu, double sigma, 
                            int maxit, unsigned seed, double *eval_host, double *evec_host, int *restarts);
 /* computeGenSymShiftInvertMinMagnitudeAdaptive (arpack_geneo_wrapper.hh:661-774): every eigenvalue of
  * the pencil below `threshold`, nev growing from initial_nev by x1.3 (the reference's code) up to
- * max_nev (= the reference's x.size()); one factorisation of A - sigma B for all passes.  Outputs
+ * max_nev (= the reference's x.size(); at nev <= 3, where int(nev * 1.3) == nev would repeat the same
+ * solve forever in the reference, by one); one factorisation of A - sigma B for all passes.  Outputs
  * as eig_shift_invert_solve for the final nev (*nev_out; eval_host / evec_host sized for max_nev):
  * ascending, the last one >= threshold unless nev reached max_nev.  maxit_per_nev: restarts allowed
  * per eigenvalue (the reference's nIterationsMax_; <= 0: 100 nev). */
 int eig_shift_invert_adaptive(eig_mat_t A, eig_mat_t B, eig_lu_t lu, double sigma, double threshold, int initial_nev,
                               int max_nev, double tol, int maxit_per_nev, unsigned seed, double *eval_host,
                               double *evec_host, int *nev_out, int *passes);
+/* Non-symmetric modes (arpack_geneo_wrapper.hh:428-578), nev eigenvalues of A x = lambda B x nearest
+ * sigma ("LM" on OP = (A - sigma B)^-1 B, B = NULL: identity), by Arnoldi with Krylov-Schur restarts
+ * (CGS2 per step; the projected matrix's eigenproblem on the host):
+ *   EIG_ARNOLDI_STD = computeStdNonSymMinMagnitude (:428-499, ARNonSymStdEig): Euclidean inner
+ *                     product, lambda = sigma + 1 / Re(nu) (the reference unshifts the real part);
+ *   EIG_ARNOLDI_GEN = computeGenNonSymShiftInvertMinMagnitude (:502-578, ARNonSymGenEig, real
+ *                     shift-invert mode): B-inner product, start vector in range(OP), lambda =
+ *                     sigma + 1 / nu.
+ * eval_re[nev] ascending (both modes sort by the real part, :484-498 / :556-571), eval_im[nev] (or
+ * NULL) the imaginary parts; evec_host nev x n (or NULL): unit 2-norm eigenvectors, for a complex
+ * conjugate pair ARPACK's raw storage (the real part of the eigenvector of the member with
+ * Im nu > 0, the imaginary part for its partner).  ncv = 0: min(n, max(2 nev + 1, 20)) (needs
+ * nev + 2 <= ncv); tol = 0: machine precision; maxit = 0: 100 nev restarts.  Converged when
+ * ||f|| |c^T y_i| <= tol |nu_i| for the nev wanted Ritz pairs.  The LU of A - sigma B is computed on
+ * the host unless `lu` is given. */
+enum { EIG_ARNOLDI_STD = 0, EIG_ARNOLDI_GEN = 1 };
+int eig_arnoldi_shift_invert(eig_mat_t A, eig_mat_t B, eig_lu_t lu, double sigma, int nev, int ncv, double tol,
+                             int maxit, unsigned seed, int mode, double *eval_re, double *eval_im, double *evec_host,
+                             int *restarts);
 
 /* ---------------------------------------------------------------- block Lanczos (config C5) */
 /* Generalised symmetric-definite eigenproblem K x = lambda M x by block Lanczos in the M-inner

@@ -14,7 +14,10 @@
 //                                     exposing UMFPackFactorizedMatrix's public factor arrays;
 //   * eigmi::ShiftInvertOperator      APP_BCRSMatMul_GeneralizedShiftInvertMode's multMv =
 //                                     (A - sigma B)^-1 v and multMvB = B v (arpack_geneo_wrapper.hh:
-//                                     225-285), and computeGenSymShiftInvertMinMagnitude (:581-658);
+//                                     225-285), and computeGenSymShiftInvertMinMagnitude (:581-658),
+//                                     its Adaptive variant (:661-774) and the non-symmetric modes
+//                                     computeStdNonSymMinMagnitude / computeGenNonSymShiftInvert-
+//                                     MinMagnitude (:428-578);
 //   * free functions with the reference kernel names and MultiVector signatures
 //     (matmul_sparse_tallskinny_blocked, matmul_inverse_tallskinny_blocked,
 //     dot_products_diagonal_blocked, dot_products_all_blocked, orthonormalize_blocked,
@@ -510,6 +513,72 @@ void computeGenSymShiftInvertMinMagnitude(const Matrix &A, const Matrix &B, doub
     double *dst = &x[i][0][0];  // BlockVector<FieldVector<double,k>>: contiguous scalars
     for (std::size_t r = 0; r < n; ++r) dst[r] = vec[(std::size_t)i * n + r];
   }
+}
+
+// computeGenSymShiftInvertMinMagnitudeAdaptive (arpack_geneo_wrapper.hh:661-774): every eigenpair
+// below `threshold`, starting from initial_nev; x.size() is the most the caller accepts (the
+// reference's x is resized to the number found, as here).
+template <class BlockVector>
+void computeGenSymShiftInvertMinMagnitudeAdaptive(const Matrix &A, const Matrix &B, double epsilon, double threshold,
+                                                  std::vector<BlockVector> &x, std::vector<double> &lambda,
+                                                  double sigma, int initial_nev, int maxit_per_nev = 0)
+{
+  const int max_nev = (int)x.size();
+  const std::size_t n = (std::size_t)A.info().n;
+  std::vector<double> ev(max_nev), vec((std::size_t)max_nev * n);
+  int nev = 0, passes = 0;
+  check(eig_shift_invert_adaptive(A.get(), B.get(), nullptr, sigma, threshold, initial_nev, max_nev, epsilon,
+                                  maxit_per_nev, 123, ev.data(), vec.data(), &nev, &passes),
+        A.ctx());
+  x.resize(nev);
+  lambda.assign(ev.begin(), ev.begin() + nev);
+  for (int i = 0; i < nev; ++i)
+  {
+    const eig_mat_info inf = A.info();
+    x[i].resize((std::size_t)(inf.n / inf.br));  // block rows
+    double *dst = &x[i][0][0];
+    for (std::size_t r = 0; r < n; ++r) dst[r] = vec[(std::size_t)i * n + r];
+  }
+}
+
+// computeStdNonSymMinMagnitude (:428-499) / computeGenNonSymShiftInvertMinMagnitude (:502-578):
+// x.size() eigenpairs nearest sigma of the (possibly non-symmetric) pencil, real parts ascending;
+// a complex pair's vectors in ARPACK's raw storage (real part, imaginary part).
+namespace detail {
+template <class BlockVector>
+void nonsym(const Matrix &A, const Matrix &B, double epsilon, std::vector<BlockVector> &x,
+            std::vector<double> &lambda, double sigma, int mode, int maxit)
+{
+  const int nev = (int)x.size();
+  const std::size_t n = (std::size_t)A.info().n;
+  std::vector<double> er(nev), ei(nev), vec((std::size_t)nev * n);
+  int restarts = 0;
+  check(eig_arnoldi_shift_invert(A.get(), B.get(), nullptr, sigma, nev, 0, epsilon, maxit, 123, mode, er.data(),
+                                 ei.data(), vec.data(), &restarts),
+        A.ctx());
+  if (lambda.size() < (std::size_t)nev) lambda.resize(nev);
+  for (int i = 0; i < nev; ++i)
+  {
+    lambda[i] = er[i];
+    double *dst = &x[i][0][0];
+    for (std::size_t r = 0; r < n; ++r) dst[r] = vec[(std::size_t)i * n + r];
+  }
+}
+}  // namespace detail
+
+template <class BlockVector>
+void computeStdNonSymMinMagnitude(const Matrix &A, const Matrix &B, double epsilon, std::vector<BlockVector> &x,
+                                  std::vector<double> &lambda, double sigma, int maxit = 0)
+{
+  detail::nonsym(A, B, epsilon, x, lambda, sigma, EIG_ARNOLDI_STD, maxit);
+}
+
+template <class BlockVector>
+void computeGenNonSymShiftInvertMinMagnitude(const Matrix &A, const Matrix &B, double epsilon,
+                                             std::vector<BlockVector> &x, std::vector<double> &lambda, double sigma,
+                                             int maxit = 0)
+{
+  detail::nonsym(A, B, epsilon, x, lambda, sigma, EIG_ARNOLDI_GEN, maxit);
 }
 
 }  // namespace eigmi

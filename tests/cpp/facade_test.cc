@@ -321,6 +321,20 @@ int main(int argc, char **argv)
     std::vector<double> lam(4);
     eigmi::computeGenSymShiftInvertMinMagnitude(dA16, dI16, 1e-14, xs, lam, 0.0);
     for (int i = 0; i < 4; ++i) EXPECT(std::fabs(lam[i] - exact[i]) < 1e-10);
+    // 9) the adaptive variant (every eigenvalue below a threshold between exact[2] and exact[3]) and
+    // the non-symmetric modes on the same (symmetric) pencil
+    std::vector<std::vector<std::array<double, 1>>> xa(8);
+    std::vector<double> la;
+    eigmi::computeGenSymShiftInvertMinMagnitudeAdaptive(dA16, dI16, 1e-14, 0.5 * (exact[2] + exact[3]), xa, la, 0.0, 2);
+    EXPECT(la.size() >= 3 && xa.size() == la.size() && xa[0].size() == n16);
+    for (int i = 0; i < 3 && i < (int)la.size(); ++i) EXPECT(std::fabs(la[i] - exact[i]) < 1e-10);
+    for (int mode = 0; mode < 2; ++mode)
+    {
+      std::vector<double> ln(4);
+      if (mode == 0) eigmi::computeStdNonSymMinMagnitude(dA16, dI16, 1e-13, xs, ln, 0.0);
+      else eigmi::computeGenNonSymShiftInvertMinMagnitude(dA16, dI16, 1e-13, xs, ln, 0.0);
+      for (int i = 0; i < 4; ++i) EXPECT(std::fabs(ln[i] - exact[i]) < 1e-10);
+    }
   }
 
   std::printf(failures ? "FAILED %d\n" : "ALL OK\n", failures);

@@ -103,6 +103,52 @@ def geneo_adaptive():
                         initial_nev=4, max_nev=40)
 
 
+def convdiff(N, pe=40.0):
+    """Non-symmetric test operator (no reference fixture exists for the non-symmetric modes): 2-D
+    Dirichlet 5-point Laplacian on an N x N grid plus a rotating convection field b = pe (-(y - 1/2),
+    x - 1/2), central differences -- complex eigenvalue pairs near the bottom of the spectrum.  And
+    an SPD B on the same 5-point pattern (the reference's A - sigma B needs pattern(B) within
+    pattern(A), arpack_geneo_wrapper.hh:599-600): (M1 kron I + I kron M1) / 2, M1 = tridiag(1, 4, 1) / 6."""
+    import scipy.sparse as sp
+    h = 1.0 / (N + 1)
+    L1 = sp.diags([-np.ones(N - 1), 2 * np.ones(N), -np.ones(N - 1)], [-1, 0, 1])
+    D1 = sp.diags([-np.ones(N - 1), np.ones(N - 1)], [-1, 1]) * (0.5 * h)  # h^2 * d/dx (central)
+    I = sp.identity(N)
+    xs = (np.arange(N) + 1) * h
+    X, Y = np.meshgrid(xs, xs, indexing="xy")  # row index = y, column = x: unknown = y * N + x
+    bx, by = -pe * (Y - 0.5).ravel(), pe * (X - 0.5).ravel()
+    A = sp.kron(I, L1) + sp.kron(L1, I) + sp.diags(bx) @ sp.kron(I, D1) + sp.diags(by) @ sp.kron(D1, I)
+    M1 = sp.diags([np.ones(N - 1), 4 * np.ones(N), np.ones(N - 1)], [-1, 0, 1]) / 6.0
+    B = (sp.kron(M1, I) + sp.kron(I, M1)) * 0.5
+    A, B = A.tocsr(), B.tocsr()
+    A.sort_indices()
+    B.sort_indices()
+    return A, B
+
+
+def nonsym():
+    """ARPACK's non-symmetric driver (scipy eigs = dnaupd/dneupd, real shift-invert mode 3,
+    "LM") for the non-symmetric modes computeStdNonSymMinMagnitude / computeGenNonSymShiftInvert-
+    MinMagnitude (arpack_geneo_wrapper.hh:428-578): the rotating convection-diffusion operator at
+    N = 24 (n = 576) standard (sigma = 0, nev = 6) and against the SPD B (sigma = 0.1, nev = 6), and
+    the harness GenEO pencil (symmetric, real spectrum) through eigs at sigma = -1e-3, nev = 4."""
+    N = 24
+    A, B = convdiff(N)
+    w_std = ssl.eigs(A, k=6, sigma=0.0, which="LM", tol=1e-14, v0=np.ones(A.shape[0]), return_eigenvectors=False)
+    w_gen = ssl.eigs(A, k=6, M=B, sigma=0.1, which="LM", tol=1e-14, v0=np.ones(A.shape[0]),
+                     return_eigenvectors=False)
+    Ng, shift = 32, 1e-3
+    Ag = oracle.laplace2d(Ng, "neumann").to_scipy()
+    Bg = oracle.laplace2d(Ng, "pu", overlap=3).to_scipy()
+    w_geneo = ssl.eigs(Ag, k=4, M=Bg, sigma=-shift, which="LM", tol=1e-14, v0=np.ones(Ag.shape[0]),
+                       return_eigenvectors=False)
+    srt = lambda w: w[np.lexsort((w.imag, w.real))]  # noqa: E731
+    np.savez_compressed(os.path.join(HERE, "nonsym_arpack.npz"), N=N, A_indptr=A.indptr, A_indices=A.indices,
+                        A_data=A.data, B_indptr=B.indptr, B_indices=B.indices, B_data=B.data,
+                        w_std=srt(w_std), w_gen=srt(w_gen), sigma_gen=0.1, geneo_N=Ng, geneo_shift=shift,
+                        w_geneo=srt(w_geneo))
+
+
 def reference_run():
     rec = {
         "source": "SURVEY.md section 6 / BASELINE.md section 2: reference headers multivector.hh + kernels_cpp.hh + "
@@ -125,5 +171,6 @@ if __name__ == "__main__":
     q1elast()
     geneo()
     geneo_adaptive()
+    nonsym()
     reference_run()
     print("golden fixtures written to", HERE)

@@ -59,6 +59,22 @@ def test_orthonormalize_blocked(m, variant):
     assert np.abs(q - X).max() < 1e-12
 
 
+def test_cholqr_split_half_order_differs():
+    """orthonormalize_avx2_b8's split-half projection (kernels_avx2.hh:255-381) and _v2's single
+    8x8 projection differ by rounding: measurably (~5e-9) when a later block is nearly a combination
+    of the diagonal block, and both keep orthonormality to the same level."""
+    n, m = 3000, 16
+    rng = np.random.default_rng(1)
+    X = rng.standard_normal((n, m))
+    X[:, 8:] = X[:, :8] @ rng.standard_normal((8, 8)) + 1e-7 * rng.standard_normal((n, 8))
+    Q = oracle.cols_to_mv(X)
+    a = oracle.mv_to_cols(oracle.orthonormalize_mv8(Q, n, m, "cholqr"), n, m)
+    b = oracle.mv_to_cols(oracle.orthonormalize_mv8(Q, n, m, "cholqr_split"), n, m)
+    assert 1e-10 < np.abs(a - b).max() < 1e-6
+    for Y in (a, b):
+        assert np.abs(Y.T @ Y - np.eye(m)).max() < 1e-6
+
+
 def test_orthonormalize_naive_matches_blocked_span():
     n, m = 500, 8
     Q = oracle.random_mv8(n, m, 3)
