@@ -279,8 +279,9 @@ extern const i32 kMarchInteriorTag;
 // qualifies; false (nothing launched) otherwise.  X, Y: window-layout multivectors, m % 8 == 0.
 bool box_prepare(const eig_mat_s &A);
 bool launch_box_spmm(const eig_mat_s &A, i64 m, const double *X, double *Y, hipStream_t s);
+// Xnew: x_{k+1} into a third buffer (nullptr: in place over Xold)
 bool launch_box_cheb(const eig_mat_s &M, i64 m, const double *Xk, double *Xold, const double *B, const double *dinv,
-                     double omega, double gamma, hipStream_t s);
+                     double omega, double gamma, hipStream_t s, double *Xnew = nullptr);
 void box_invalidate(eig_mat_s &A);
 bool launch_spmm_march(const eig_mat_s &A, i64 m, const double *X, double *Y, hipStream_t s);
 // Chebyshev step (k_block.hip kCheb semantics) on the general band march; false when not applicable.

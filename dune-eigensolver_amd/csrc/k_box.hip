@@ -88,6 +88,7 @@ __global__ __launch_bounds__(kBoxThreads) void k_box_mv32(BoxGeom g, i64 ld, con
                                                           const uint32_t *__restrict__ mask32,
                                                           const uint8_t *__restrict__ mask8,
                                                           const double *__restrict__ X, double *__restrict__ Y,
+                                                          const double *__restrict__ Xold,
                                                           const double *__restrict__ Bv,
                                                           const double *__restrict__ dinv, double omega,
                                                           double gamma)
@@ -101,6 +102,8 @@ __global__ __launch_bounds__(kBoxThreads) void k_box_mv32(BoxGeom g, i64 ld, con
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   // 8 threads per row (4 columns each): 16 waves = 4 per SIMD with one workgroup per CU
   const int yi = wave >> 1, xi = (wave & 1) * 8 + (lane >> 3), cq = lane & 7, blk = cq >> 1, c4 = (cq & 1) * 4;
+  // item = (tile, z run) in dispatch order (an XCD-contiguous item map -- workgroup b on XCD b % 8
+  // taking one run of adjacent tiles -- measured no faster)
   const int item = (int)blockIdx.x;
   const int tile = item % (g.ntx * g.nty), seg = item / (g.ntx * g.nty);
   const int x0 = (tile % g.ntx) * kBoxTX, y0 = (tile / g.ntx) * kBoxTY;
@@ -119,8 +122,10 @@ __global__ __launch_bounds__(kBoxThreads) void k_box_mv32(BoxGeom g, i64 ld, con
       const int x = x0 + hx - 1, y = y0 + hy - 1;
       const bool ok = c < kBoxChunks && zz >= 0 && zz < g.nz && x >= 0 && x < g.nx && y >= 0 && y < g.ny;
       const i64 row = ok ? (i64)x + (i64)g.nx * y + (i64)g.P * zz : 0;
-      pre[i] = ok ? __builtin_nontemporal_load(reinterpret_cast<const dv2b *>(X + (i64)b * ld * 8 + row * 8) + q)
-                  : dv2b{0.0, 0.0};
+      // plain loads: a plane's rows are also the halo of the neighbouring tiles (nontemporal X
+      // loads measured the same, 4.21 vs 4.23 ms, in one interleaved run)
+      const dv2b *src = reinterpret_cast<const dv2b *>(X + (i64)b * ld * 8 + row * 8) + q;
+      pre[i] = ok ? *src : dv2b{0.0, 0.0};
     }
   };
   auto store = [&](int zz) {
@@ -173,7 +178,7 @@ __global__ __launch_bounds__(kBoxThreads) void k_box_mv32(BoxGeom g, i64 ld, con
   auto fetch_cheb = [&](int zz, dv2b (&b2)[2], dv2b (&x2)[2], double &gg) {
     if (EPI != kBoxCheb || !own || zz >= z1) return;
     const i64 r = (i64)x + (i64)g.nx * y + (i64)g.P * zz;
-    const double *br = Bv + (i64)blk * ld * 8 + r * 8 + c4, *yr = Y + (i64)blk * ld * 8 + r * 8 + c4;
+    const double *br = Bv + (i64)blk * ld * 8 + r * 8 + c4, *yr = Xold + (i64)blk * ld * 8 + r * 8 + c4;
     gg = gamma * __builtin_nontemporal_load(dinv + r);
 #pragma unroll
     for (int j = 0; j < 2; ++j)
@@ -352,8 +357,8 @@ bool box_prepare(const eig_mat_s &Ac)
 
 // Y = A X (EPI store) or the Chebyshev step into Xold (EPI cheb) for m % 32 == 0 columns on the box
 // kernel; false when the matrix has no box geometry (the caller takes the band march).
-static bool launch_box(const eig_mat_s &A, i64 m, const double *X, double *Y, const double *Bv, const double *dinv,
-                       double omega, double gamma, bool cheb, hipStream_t s)
+static bool launch_box(const eig_mat_s &A, i64 m, const double *X, double *Y, const double *Xold, const double *Bv,
+                       const double *dinv, double omega, double gamma, bool cheb, hipStream_t s)
 {
   if (m <= 0 || m % 32 != 0 || !box_prepare(A)) return false;
   BoxGeom g;
@@ -380,11 +385,12 @@ static bool launch_box(const eig_mat_s &A, i64 m, const double *X, double *Y, co
     const i64 off = c0 * ld;  // 4 column blocks of ld rows x 8
     if (cheb)
       hipLaunchKernelGGL(k_box_mv32<kBoxCheb>, dim3((unsigned)(tiles * g.nseg)), dim3(kBoxThreads), 0, s, g, ld,
-                         (const double *)A.box_val, m32, m8, X + off, Y + off, Bv + off, dinv, omega, gamma);
+                         (const double *)A.box_val, m32, m8, X + off, Y + off, Xold + off, Bv + off, dinv, omega,
+                         gamma);
     else
       hipLaunchKernelGGL(k_box_mv32<kBoxStore>, dim3((unsigned)(tiles * g.nseg)), dim3(kBoxThreads), 0, s, g, ld,
                          (const double *)A.box_val, m32, m8, X + off, Y + off, (const double *)nullptr,
-                         (const double *)nullptr, 0.0, 0.0);
+                         (const double *)nullptr, (const double *)nullptr, 0.0, 0.0);
   }
   EIG_HIP(hipGetLastError());
   return true;
@@ -392,13 +398,13 @@ static bool launch_box(const eig_mat_s &A, i64 m, const double *X, double *Y, co
 
 bool launch_box_spmm(const eig_mat_s &A, i64 m, const double *X, double *Y, hipStream_t s)
 {
-  return launch_box(A, m, X, Y, nullptr, nullptr, 0.0, 0.0, false, s);
+  return launch_box(A, m, X, Y, nullptr, nullptr, nullptr, 0.0, 0.0, false, s);
 }
 
 bool launch_box_cheb(const eig_mat_s &M, i64 m, const double *Xk, double *Xold, const double *B, const double *dinv,
-                     double omega, double gamma, hipStream_t s)
+                     double omega, double gamma, hipStream_t s, double *Xnew)
 {
-  return launch_box(M, m, Xk, Xold, B, dinv, omega, gamma, true, s);
+  return launch_box(M, m, Xk, Xnew ? Xnew : Xold, Xold, B, dinv, omega, gamma, true, s);
 }
 
 }  // namespace eigmi

@@ -25,7 +25,7 @@ def main():
     ap.add_argument("--m", type=int, default=32)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--dlo", type=int, default=2)
-    ap.add_argument("--dhi", type=int, default=10)
+    ap.add_argument("--dhi", type=int, default=34)
     args = ap.parse_args()
     ctx = eigmi.Context(0)
     N, m = args.N, args.m
