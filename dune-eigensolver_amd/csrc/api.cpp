@@ -891,6 +891,8 @@ void destroy_mat(eig_mat_s *A)
   if (A->sym_val) (void)hipFree(A->sym_val);
   if (A->sym_mask) (void)hipFree(A->sym_mask);
   if (A->box_val) (void)hipFree(A->box_val);
+  if (A->box_ctab) (void)hipFree(A->box_ctab);
+  if (A->box_cmask) (void)hipFree(A->box_cmask);
   delete A;
 }
 

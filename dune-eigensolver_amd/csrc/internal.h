@@ -207,7 +207,13 @@ struct eig_mat_s {
   int box_state = 0;
   double *box_val = nullptr;
   int box_nx = 0, box_ny = 0, box_nz = 0;
-  int box_dz[27] = {}, box_dxy[27] = {};
+  int box_dz[27] = {}, box_dxy[27] = {}, box_dx[27] = {}, box_dy[27] = {};
+  // Row classes (k_box.hip k_boxc_mv8): when every row's stored entries equal those of its
+  // geometric class representative (27 classes: first / interior / last position in x, y and z),
+  // box_ctab holds per class the nd values and 1 / a_rr (slot 15), box_cmask the row mask, and the
+  // class kernels read no matrix stream at all (box_val is then freed)
+  double *box_ctab = nullptr;
+  unsigned *box_cmask = nullptr;
   eigmi::i32 *march_bnd = nullptr;
   eigmi::i64 n_march_bnd = 0;
   eigmi::i64 *slice_ptr = nullptr;  // nslices + 1

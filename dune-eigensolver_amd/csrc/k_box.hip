@@ -263,6 +263,169 @@ __global__ __launch_bounds__(kBoxThreads) void k_box_mv32(BoxGeom g, i64 ld, con
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Row-class box kernels.  On a box grid whose matrix has constant entries per geometric class
+// (first / interior / last position along x, y and z: 27 classes -- the generators' 7-point Poisson
+// and P1 Kuhn K / M, any constant-coefficient stencil with its boundary rows), a row's stored
+// entries are those of its class representative.  The class table (27 x (nd values + 1 / a_rr),
+// 27 masks) sits in LDS, so the SpMM and the Chebyshev step stream only the vectors: no box image,
+// no band values, no row masks, no D^-1.  8 columns (one MultiVector block, 64-B rows) per
+// workgroup (blockIdx.y = column block): 4 lanes per row, 16 consecutive x rows per wave, every
+// vector access a 1-KiB contiguous run; a 32 x 8 tile with a one-row halo, 3 planes in LDS
+// (3 x 340 rows x 64 B = 65 KiB: two workgroups per CU).  Entries summed in ascending-column order
+// per row and column: kBoxStore bitwise the reference SpMM, kBoxCheb with FMA (as k_box_mv32).
+// ---------------------------------------------------------------------------------------------
+constexpr int kCTX = 32, kCTY = 8, kCHX = kCTX + 2, kCHY = kCTY + 2;
+constexpr int kCThreads = 1024;
+constexpr int kCChunks = kCHY * kCHX * 4;  // 16-B chunks of one plane (tile + halo, 8 columns)
+constexpr int kCRounds = (kCChunks + kCThreads - 1) / kCThreads;
+constexpr int kBoxClasses = 27;
+constexpr int kCStride = 16;  // doubles per class: nd <= 15 values, then 1 / a_rr
+
+__device__ __forceinline__ int box_cls1(int v, int nv) { return v == 0 ? 0 : (v == nv - 1 ? 2 : 1); }
+
+// bad |= 1 when a row's mask or a stored entry differs from its class's (bitwise).
+__global__ void k_boxc_check(i64 n, int nx, int ny, int nd, const double *__restrict__ val,
+                             const void *__restrict__ mask, int mask_bytes, const double *__restrict__ ctab,
+                             const unsigned *__restrict__ cmask, unsigned *__restrict__ bad)
+{
+  for (i64 r = (i64)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (i64)gridDim.x * blockDim.x)
+  {
+    const int x = (int)(r % nx), y = (int)((r / nx) % ny);
+    const i64 z = r / ((i64)nx * ny), nz = n / ((i64)nx * ny);
+    const int c = (z == 0 ? 0 : (z == nz - 1 ? 2 : 1)) * 9 + box_cls1(y, ny) * 3 + box_cls1(x, nx);
+    const unsigned m = mask_bytes == 1 ? static_cast<const uint8_t *>(mask)[r] : static_cast<const uint32_t *>(mask)[r];
+    bool ok = m == cmask[c];
+    for (int k = 0; k < nd && ok; ++k)
+      if ((m >> k) & 1u)
+        ok = __double_as_longlong(val[(i64)k * n + r]) == __double_as_longlong(ctab[c * kCStride + k]);
+    if (!ok) atomicOr(bad, 1u);
+  }
+}
+
+// out[c * (kCStride + 1) + k] = val[k n + rep[c]] (k < nd), out[c * (kCStride + 1) + kCStride] = mask
+__global__ void k_boxc_gather(i64 n, int nd, const double *__restrict__ val, const void *__restrict__ mask,
+                              int mask_bytes, const i64 *__restrict__ rep, double *__restrict__ out)
+{
+  const int c = blockIdx.x, k = threadIdx.x;
+  const i64 r = rep[c];
+  if (k < nd) out[c * (kCStride + 1) + k] = val[(i64)k * n + r];
+  if (k == kCStride)
+    out[c * (kCStride + 1) + k] = (double)(mask_bytes == 1 ? static_cast<const uint8_t *>(mask)[r]
+                                                           : static_cast<const uint32_t *>(mask)[r]);
+}
+
+template <int EPI>
+__global__ __launch_bounds__(kCThreads) void k_boxc_mv8(BoxGeom g, i64 ld, const double *__restrict__ ctab,
+                                                        const unsigned *__restrict__ cmask,
+                                                        const double *__restrict__ X, double *__restrict__ Y,
+                                                        const double *__restrict__ Xold,
+                                                        const double *__restrict__ Bv, double omega, double gamma)
+{
+  __shared__ __attribute__((aligned(16))) dv2b ring[3][kCHY * kCHX][4];
+  __shared__ double ct[kBoxClasses][kCStride];
+  __shared__ unsigned cm[kBoxClasses];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  for (int i = tid; i < kBoxClasses * kCStride; i += kCThreads) ct[i / kCStride][i % kCStride] = ctab[i];
+  if (tid < kBoxClasses) cm[tid] = cmask[tid];
+  const i64 boff = (i64)blockIdx.y * ld * 8;  // column block
+  const dv2b *Xb = reinterpret_cast<const dv2b *>(X + boff);
+  dv2b *Yb = reinterpret_cast<dv2b *>(Y + boff);
+  const dv2b *Ob = reinterpret_cast<const dv2b *>(Xold ? Xold + boff : nullptr);
+  const dv2b *Bb = reinterpret_cast<const dv2b *>(Bv ? Bv + boff : nullptr);
+  const int item = (int)blockIdx.x;
+  const int tile = item % (g.ntx * g.nty), seg = item / (g.ntx * g.nty);
+  const int x0 = (tile % g.ntx) * kCTX, y0 = (tile / g.ntx) * kCTY;
+  const int z0 = seg * g.nz / g.nseg, z1 = (seg + 1) * g.nz / g.nseg;
+  // X plane zz of the tile + halo (8 columns, 64-B rows) into ring slot zz mod 3
+  dv2b pre[kCRounds];
+  auto fetch = [&](int zz) {
+#pragma unroll
+    for (int i = 0; i < kCRounds; ++i)
+    {
+      const int c = tid + i * kCThreads, q = c & 3, hr = c >> 2, hx = hr % kCHX, hy = hr / kCHX;
+      const int x = x0 + hx - 1, y = y0 + hy - 1;
+      const bool ok = c < kCChunks && zz >= 0 && zz < g.nz && x >= 0 && x < g.nx && y >= 0 && y < g.ny;
+      const i64 row = ok ? (i64)x + (i64)g.nx * y + (i64)g.P * zz : 0;
+      pre[i] = ok ? Xb[row * 4 + q] : dv2b{0.0, 0.0};
+    }
+  };
+  auto store = [&](int zz) {
+    const int sl = ((zz % 3) + 3) % 3;
+#pragma unroll
+    for (int i = 0; i < kCRounds; ++i)
+    {
+      const int c = tid + i * kCThreads;
+      if (c < kCChunks) ring[sl][c >> 2][c & 3] = pre[i];
+    }
+  };
+  // this thread: row (x0 + xi, y0 + yi), column pair cp; a wave = 16 consecutive x rows
+  const int xi = (wave & 1) * 16 + (lane >> 2), yi = wave >> 1, cp = lane & 3;
+  const int x = x0 + xi, y = y0 + yi;
+  const bool own = x < g.nx && y < g.ny;
+  const int hrow = (yi + 1) * kCHX + xi + 1;
+  const int cxy = (own ? box_cls1(y, g.ny) * 3 + box_cls1(x, g.nx) : 0);
+  dv2b bb = {}, xo = {}, bn = {}, xn = {};
+  auto fetch_cheb = [&](int zz, dv2b &b2, dv2b &x2) {
+    if (EPI != kBoxCheb || !own || zz >= z1) return;
+    const i64 r = (i64)x + (i64)g.nx * y + (i64)g.P * zz;
+    b2 = __builtin_nontemporal_load(Bb + r * 4 + cp);
+    x2 = __builtin_nontemporal_load(Ob + r * 4 + cp);
+  };
+  fetch(z0 - 1);
+  store(z0 - 1);
+  fetch(z0);
+  store(z0);
+  fetch(z0 + 1);
+  store(z0 + 1);
+  fetch_cheb(z0, bb, xo);
+  for (int z = z0; z < z1; ++z)
+  {
+    __syncthreads();  // ring holds planes z - 1, z, z + 1 (and the class table)
+    fetch_cheb(z + 1, bn, xn);
+    fetch(z + 2);
+    const int cls = (z == 0 ? 0 : (z == g.nz - 1 ? 2 : 1)) * 9 + cxy;
+    const unsigned m = own ? cm[cls] : 0u;
+    dv2b acc = {0.0, 0.0};
+#pragma unroll 4
+    for (int k = 0; k < g.nd; ++k)
+    {
+      if (!((m >> k) & 1u)) continue;
+      const double a = ct[cls][k];
+      const int sl = (((z + g.dz[k]) % 3) + 3) % 3;
+      const dv2b xv = ring[sl][hrow + g.dxy[k]][cp];
+      if (EPI == kBoxStore)
+      {
+        acc.x = acc.x + a * xv.x;
+        acc.y = acc.y + a * xv.y;
+      }
+      else
+      {
+        acc.x = __builtin_fma(a, xv.x, acc.x);
+        acc.y = __builtin_fma(a, xv.y, acc.y);
+      }
+    }
+    if (own)
+    {
+      const i64 r = (i64)x + (i64)g.nx * y + (i64)g.P * z;
+      if (EPI == kBoxStore)
+        __builtin_nontemporal_store(acc, Yb + r * 4 + cp);
+      else
+      {
+        const dv2b xc = ring[((z % 3) + 3) % 3][hrow][cp];
+        const double gd = gamma * ct[cls][kCStride - 1];
+        const double o0 = omega * (xc.x + gd * (bb.x - acc.x) - xo.x) + xo.x;
+        const double o1 = omega * (xc.y + gd * (bb.y - acc.y) - xo.y) + xo.y;
+        __builtin_nontemporal_store(dv2b{o0, o1}, Yb + r * 4 + cp);
+      }
+    }
+    __syncthreads();  // everyone is done with slot (z - 1) mod 3
+    store(z + 2);
+    bb = bn;
+    xo = xn;
+  }
+}
 }  // namespace
 
 void box_invalidate(eig_mat_s &A)
@@ -274,7 +437,73 @@ void box_invalidate(eig_mat_s &A)
     A.device_bytes -= (i64)A.sym_nd * A.nb_rows * (i64)sizeof(double);
   }
   A.box_val = nullptr;
+  if (A.box_ctab)
+  {
+    (void)hipStreamSynchronize(A.ctx->stream);
+    (void)hipFree(A.box_ctab);
+    (void)hipFree(A.box_cmask);
+  }
+  A.box_ctab = nullptr;
+  A.box_cmask = nullptr;
   A.box_state = 0;
+}
+
+// Row classes of a box image (k_boxc_mv8): the 27 representatives' entries and masks to the host,
+// 1 / a_rr per class, then every row checked bitwise against its class on the device; on success
+// A.box_ctab / box_cmask are set.  Needs a stored diagonal in every class.
+static void box_classes(eig_mat_s &A, i64 nx, i64 ny, i64 nz)
+{
+  if (nx < 3 || ny < 3 || nz < 3 || A.sym_nd >= kCStride || (A.kflags & EIG_MAT_NO_CLASS)) return;
+  int k0 = -1;
+  for (int k = 0; k < A.sym_nd; ++k)
+    if (A.sym_off[k] == 0) k0 = k;
+  if (k0 < 0) return;
+  hipStream_t s = A.ctx->stream;
+  const i64 n = A.nb_rows;
+  std::vector<i64> rep(kBoxClasses);
+  auto pos = [](int c, i64 nv) { return c == 0 ? (i64)0 : (c == 1 ? (i64)1 : nv - 1); };
+  for (int c = 0; c < kBoxClasses; ++c)
+    rep[c] = pos(c % 3, nx) + nx * pos((c / 3) % 3, ny) + nx * ny * pos(c / 9, nz);
+  DevBuf drep(kBoxClasses * sizeof(i64)), dout((size_t)kBoxClasses * (kCStride + 1) * sizeof(double));
+  EIG_HIP(hipMemcpyAsync(drep.p, rep.data(), kBoxClasses * sizeof(i64), hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(k_boxc_gather, dim3(kBoxClasses), dim3(64), 0, s, n, A.sym_nd, (const double *)A.box_val,
+                     (const void *)A.sym_mask, A.sym_mask_bytes, (const i64 *)drep.p, dout.d());
+  std::vector<double> h((size_t)kBoxClasses * (kCStride + 1));
+  EIG_HIP(hipMemcpyAsync(h.data(), dout.p, h.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+  EIG_HIP(hipStreamSynchronize(s));
+  std::vector<double> ctab((size_t)kBoxClasses * kCStride, 0.0);
+  std::vector<unsigned> cmask(kBoxClasses);
+  for (int c = 0; c < kBoxClasses; ++c)
+  {
+    const unsigned m = (unsigned)h[(size_t)c * (kCStride + 1) + kCStride];
+    cmask[c] = m;
+    if (!((m >> k0) & 1u)) return;
+    for (int k = 0; k < A.sym_nd; ++k)
+      if ((m >> k) & 1u) ctab[(size_t)c * kCStride + k] = h[(size_t)c * (kCStride + 1) + k];
+    // the same IEEE division k_diag_inv performs on the row's diagonal
+    ctab[(size_t)c * kCStride + kCStride - 1] = 1.0 / ctab[(size_t)c * kCStride + k0];
+  }
+  double *dct = nullptr;
+  unsigned *dcm = nullptr;
+  EIG_HIP(hipMalloc(&dct, ctab.size() * sizeof(double)));
+  EIG_HIP(hipMalloc(&dcm, (kBoxClasses + 1) * sizeof(unsigned)));
+  EIG_HIP(hipMemcpyAsync(dct, ctab.data(), ctab.size() * sizeof(double), hipMemcpyHostToDevice, s));
+  EIG_HIP(hipMemcpyAsync(dcm, cmask.data(), kBoxClasses * sizeof(unsigned), hipMemcpyHostToDevice, s));
+  unsigned *bad = dcm + kBoxClasses;
+  EIG_HIP(hipMemsetAsync(bad, 0, sizeof(unsigned), s));
+  hipLaunchKernelGGL(k_boxc_check, dim3(2048), dim3(256), 0, s, n, (int)nx, (int)ny, A.sym_nd,
+                     (const double *)A.box_val, (const void *)A.sym_mask, A.sym_mask_bytes, dct, dcm, bad);
+  unsigned hb = 1;
+  EIG_HIP(hipMemcpyAsync(&hb, bad, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+  EIG_HIP(hipStreamSynchronize(s));
+  if (hb)
+  {
+    (void)hipFree(dct);
+    (void)hipFree(dcm);
+    return;
+  }
+  A.box_ctab = dct;
+  A.box_cmask = dcm;
 }
 
 // Box-stencil geometry of a band image and its device box image (built on first use and cached on
@@ -342,6 +571,7 @@ bool box_prepare(const eig_mat_s &Ac)
     EIG_HIP(hipStreamSynchronize(s));
     A.box_val = val;
   }
+  box_classes(A, nx, ny, nz);
   A.box_nx = (int)nx;
   A.box_ny = (int)ny;
   A.box_nz = (int)nz;
@@ -349,8 +579,17 @@ bool box_prepare(const eig_mat_s &Ac)
   {
     A.box_dz[k] = dz[k];
     A.box_dxy[k] = dy[k] * kBoxHX + dx[k];
+    A.box_dx[k] = dx[k];
+    A.box_dy[k] = dy[k];
   }
-  A.device_bytes += (i64)A.sym_nd * n * (i64)sizeof(double);
+  if (A.box_ctab)
+  {
+    // the class kernels read no box image
+    EIG_HIP(hipFree(A.box_val));
+    A.box_val = nullptr;
+  }
+  else
+    A.device_bytes += (i64)A.sym_nd * n * (i64)sizeof(double);
   A.box_state = 1;
   return true;
 }
@@ -361,6 +600,37 @@ static bool launch_box(const eig_mat_s &A, i64 m, const double *X, double *Y, co
                        const double *dinv, double omega, double gamma, bool cheb, hipStream_t s)
 {
   if (m <= 0 || m % 32 != 0 || !box_prepare(A)) return false;
+  if (A.box_ctab)
+  {
+    // row-class kernels: one launch, blockIdx.y = column block; z runs for ~2 rounds of the
+    // resident workgroups (2 per CU)
+    BoxGeom g;
+    g.nx = A.box_nx;
+    g.ny = A.box_ny;
+    g.nz = A.box_nz;
+    g.P = g.nx * g.ny;
+    g.ntx = (g.nx + kCTX - 1) / kCTX;
+    g.nty = (g.ny + kCTY - 1) / kCTY;
+    const i64 per_seg = (i64)g.ntx * g.nty * (m / 8);
+    const i64 want = 4LL * A.ctx->num_cu;
+    g.nseg = (int)std::max<i64>(1, std::min<i64>(g.nz / 8, (want + per_seg - 1) / per_seg));
+    g.nd = A.sym_nd;
+    for (int k = 0; k < 27; ++k)
+    {
+      g.dz[k] = k < A.sym_nd ? A.box_dz[k] : 0;
+      g.dxy[k] = k < A.sym_nd ? A.box_dy[k] * kCHX + A.box_dx[k] : 0;
+    }
+    const dim3 grid((unsigned)(g.ntx * g.nty * g.nseg), (unsigned)(m / 8));
+    if (cheb)
+      hipLaunchKernelGGL(k_boxc_mv8<kBoxCheb>, grid, dim3(kCThreads), 0, s, g, A.window,
+                         (const double *)A.box_ctab, (const unsigned *)A.box_cmask, X, Y, Xold, Bv, omega, gamma);
+    else
+      hipLaunchKernelGGL(k_boxc_mv8<kBoxStore>, grid, dim3(kCThreads), 0, s, g, A.window,
+                         (const double *)A.box_ctab, (const unsigned *)A.box_cmask, X, Y, (const double *)nullptr,
+                         (const double *)nullptr, 0.0, 0.0);
+    EIG_HIP(hipGetLastError());
+    return true;
+  }
   BoxGeom g;
   g.nx = A.box_nx;
   g.ny = A.box_ny;

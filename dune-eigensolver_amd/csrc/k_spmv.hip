@@ -1937,7 +1937,11 @@ std::string kernel_for(const eig_mat_s &A, int op)
     }
     case 5:
     case 6:
-      if (b1 && box_prepare(A)) return op == 5 ? "k_box_mv32" : "k_box_mv32_cheb";
+      if (b1 && box_prepare(A))
+      {
+        if (A.box_ctab) return op == 5 ? "k_boxc_mv8" : "k_boxc_mv8_cheb";  // row-class image
+        return op == 5 ? "k_box_mv32" : "k_box_mv32_cheb";
+      }
       return kernel_for(A, op - 2);
     default:
       return "none";

@@ -18,7 +18,7 @@ EIG_OK, EIG_ERR_SHAPE, EIG_ERR_BLOCKSIZE, EIG_ERR_HIP, EIG_ERR_RCCL, EIG_ERR_BRE
 ORTHO_MGS, ORTHO_CHOLQR, ORTHO_CHOLQR_SPLIT = 0, 1, 2
 ORTHO_GRID = 0x100  # or-ed into the variant: grid-wide MGS passes even for blocks one workgroup holds
 # matrix kernel-image flags (eig_mat_create_bcsr_ex)
-MAT_NO_BAND, MAT_BAND_GATHER, MAT_NO_STENCIL, MAT_NO_MARCH = 1, 2, 4, 8
+MAT_NO_BAND, MAT_BAND_GATHER, MAT_NO_STENCIL, MAT_NO_MARCH, MAT_NO_CLASS = 1, 2, 4, 8, 16
 # triangular-solve kernels of an LU (eig_lu_set_solver)
 TRSV_AUTO, TRSV_BLOCKINV, TRSV_STAGED, TRSV_CSR = 0, 1, 2, 3
 TRSV_KINDS = {None: TRSV_AUTO, "auto": TRSV_AUTO, "blockinv": TRSV_BLOCKINV, "staged": TRSV_STAGED, "csr": TRSV_CSR}
@@ -360,7 +360,8 @@ class Matrix:
 
     @classmethod
     def from_bcsr(cls, ctx, rowptr, col, vals, br=1, bc=1, ncols_blocks=None, flags=0):
-        """flags: MAT_NO_BAND | MAT_BAND_GATHER | MAT_NO_STENCIL | MAT_NO_MARCH (eig_mat_create_bcsr_ex)."""
+        """flags: MAT_NO_BAND | MAT_BAND_GATHER | MAT_NO_STENCIL | MAT_NO_MARCH | MAT_NO_CLASS
+        (eig_mat_create_bcsr_ex)."""
         rowptr = np.ascontiguousarray(rowptr, np.int64)
         col = np.ascontiguousarray(col, np.int32)
         vals = np.ascontiguousarray(vals, np.float64)

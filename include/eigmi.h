@@ -122,13 +122,16 @@ int eig_mat_create_bcsr_dist(eig_ctx_t ctx, int64_t nb_rows_global, int64_t row_
  *   EIG_MAT_NO_BAND      no symmetric band image: the scalar kernels read the SELL / stencil image
  *   EIG_MAT_BAND_GATHER  band image, but every offset through its own gather (no DPP lane shifts)
  *   EIG_MAT_NO_STENCIL   SELL slices keep explicit column indices (no per-slice offsets + row masks)
- *   EIG_MAT_NO_MARCH     no plane-marching kernels (band image: the row kernels) */
+ *   EIG_MAT_NO_MARCH     no plane-marching kernels (band image: the row kernels)
+ *   EIG_MAT_NO_CLASS     the 32-column box kernels keep the box image even when every row's entries
+ *                        equal those of its geometric class (row-class image, k_box.hip) */
 enum {
   EIG_MAT_NO_BAND = 1,
   EIG_MAT_BAND_GATHER = 2,
   EIG_MAT_NO_STENCIL = 4,
   EIG_MAT_NO_MARCH = 8,
-  EIG_MAT_FLAGS_ALL = 15
+  EIG_MAT_NO_CLASS = 16,
+  EIG_MAT_FLAGS_ALL = 31
 };
 int eig_mat_create_bcsr_ex(eig_ctx_t ctx, int64_t nb_rows, int64_t nb_cols, int br, int bc,
                            const int64_t *rowptr_host, const int32_t *col_host, const double *vals_host, int flags,

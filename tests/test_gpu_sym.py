@@ -233,30 +233,53 @@ def test_marchg_chebyshev_matches_sell(ctx, N, m):
 
 # ---- 3-D box stencils, 32 columns per pass (k_box.hip: LDS-tiled plane march, config C5) ----
 
+def _perturbed(A, rows=(1000, 2345)):
+    """A with the symmetric pair of entries (i, i + 1) / (i + 1, i) scaled by 1.01 for i in rows: still
+    a box stencil with a bitwise-symmetric band, but rows i, i + 1 leave their geometric class."""
+    v = A.val.copy()
+    for i in rows:
+        for r, c in ((i, i + 1), (i + 1, i)):
+            p = A.rowptr[r] + int(np.nonzero(A.col[A.rowptr[r]:A.rowptr[r + 1]] == c)[0][0])
+            v[p] *= 1.01
+    return oracle.CSR(A.n, A.rowptr, A.col, v)
+
+
+BOX_CLASS = {"p1mass16": True, "p1stiff16": True, "p1mass20": True, "p1mass24": True, "poisson18": True,
+             "p1mass16var": False, "poisson18var": False}
+
+
 @pytest.mark.parametrize("mat,m", [
     ("p1mass16", 32), ("p1stiff16", 32), ("p1mass20", 32),   # 20: ragged tiles in x and y
     ("p1mass24", 64), ("poisson18", 32), ("poisson18", 96),
+    ("p1mass16var", 32), ("poisson18var", 64),  # not class-constant: the full box image kernel
 ])
 def test_box_spmm_bitwise(ctx, mat, m):
-    """The box kernel's SpMM (separately rounded products and sums, ascending offsets) is bitwise the
-    reference matmul_sparse_tallskinny_blocked (kernels_cpp.hh:626-657) restated in oracle.spmm_mv8."""
+    """The box kernels' SpMM (separately rounded products and sums, ascending offsets) is bitwise the
+    reference matmul_sparse_tallskinny_blocked (kernels_cpp.hh:626-657) restated in oracle.spmm_mv8:
+    the row-class kernel (k_boxc_mv8: constant entries per geometric class, values from LDS) and,
+    for matrices whose rows leave their class, the box-image kernel (k_box_mv32)."""
     A = {"p1mass16": lambda: _p1(16, "M"), "p1stiff16": lambda: _p1(16, "K"), "p1mass20": lambda: _p1(20, "M"),
-         "p1mass24": lambda: _p1(24, "M"), "poisson18": lambda: oracle.poisson3d(18)}[mat]()
+         "p1mass24": lambda: _p1(24, "M"), "poisson18": lambda: oracle.poisson3d(18),
+         "p1mass16var": lambda: _perturbed(_p1(16, "M")),
+         "poisson18var": lambda: _perturbed(oracle.poisson3d(18))}[mat]()
     M = upload(ctx, A)
-    assert M.kernel("spmm32") == "k_box_mv32"
+    assert M.kernel("spmm32") == ("k_boxc_mv8" if BOX_CLASS[mat] else "k_box_mv32")
     Qh = oracle.random_mv8(A.n, m, 7)
     Q, Y = ctx.array(Qh), ctx.zeros(A.n * m)
     eigmi.spmm_mv8(M, m, Q, Y)
     assert np.array_equal(Y.get(), oracle.spmm_mv8(A, Qh, m))
 
 
-@pytest.mark.parametrize("N", [16, 20])
-def test_box_chebyshev_matches_sell(ctx, N):
-    """The fused Chebyshev-Jacobi step on the box kernel against the SELL kernel (both FMA in
-    ascending offset order: equal up to signed zeros / the rounding of the fused update)."""
+@pytest.mark.parametrize("N,var", [(16, False), (20, False), (16, True)])
+def test_box_chebyshev_matches_sell(ctx, N, var):
+    """The fused Chebyshev-Jacobi step on the box kernels (row-class and, var: box image) against the
+    SELL kernel (all FMA in ascending offset order: equal up to signed zeros / the rounding of the
+    fused update)."""
     A = _p1(N, "M")
+    if var:
+        A = _perturbed(A)
     M = upload(ctx, A)
-    assert M.kernel("cheb32") == "k_box_mv32_cheb"
+    assert M.kernel("cheb32") == ("k_box_mv32_cheb" if var else "k_boxc_mv8_cheb")
     Ms = upload(ctx, A, flags=eigmi.MAT_NO_MARCH)
     assert Ms.kernel("cheb32") == "k_sell_mv8q_cheb"
     n, m = A.n, 32
@@ -269,6 +292,19 @@ def test_box_chebyshev_matches_sell(ctx, N):
     assert np.allclose(a, b, rtol=1e-13, atol=1e-14 * np.abs(b).max())
     r = oracle.spmm_mv8(A, a, m) - Bh
     assert np.linalg.norm(r) <= 1e-6 * np.linalg.norm(Bh)
+
+
+@pytest.mark.parametrize("mat", ["p1mass16", "poisson18"])
+def test_box_no_class_flag(ctx, mat):
+    """EIG_MAT_NO_CLASS keeps the box-image kernel on a class-constant matrix; both kernels give the
+    reference SpMM bitwise."""
+    A = _p1(16, "M") if mat == "p1mass16" else oracle.poisson3d(18)
+    M = upload(ctx, A, flags=eigmi.MAT_NO_CLASS)
+    assert M.kernel("spmm32") == "k_box_mv32"
+    Qh = oracle.random_mv8(A.n, 32, 13)
+    Q, Y = ctx.array(Qh), ctx.zeros(A.n * 32)
+    eigmi.spmm_mv8(M, 32, Q, Y)
+    assert np.array_equal(Y.get(), oracle.spmm_mv8(A, Qh, 32))
 
 
 def test_box_shift_rebuilds_image(ctx):
@@ -289,7 +325,7 @@ def test_box_not_a_grid(ctx):
     """A band that is not a 3-D box stencil (random offsets) keeps the band march / SELL kernels."""
     A = band_matrix(4000, [0, 1, 5, 32, 35, 40], 31, drop=0.05)
     M = upload(ctx, A)
-    assert M.kernel("spmm32") != "k_box_mv32"
+    assert M.kernel("spmm32") not in ("k_box_mv32", "k_boxc_mv8")
     Qh = oracle.random_mv8(A.n, 32, 12)
     Q, Y = ctx.array(Qh), ctx.zeros(A.n * 32)
     eigmi.spmm_mv8(M, 32, Q, Y)

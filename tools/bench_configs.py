@@ -243,16 +243,28 @@ def c5(ctx):
     t = bl.step(steps)
     ev, _, res = bl.ritz(4, eigmi.WHICH_LA, want_resid=False)
     cols = b // (t.cheb_launches // (steps * (degree - 1)))  # columns per launch
-    # per launch: matrix + (gather x_k, read x_{k-1}, read b, write x_{k+1}) per column + dinv
-    cheb_bytes = 12 * nnz + 4 * (n + 1) + 32 * cols * n + 8 * n
+    # per launch, SURVEY 8(d) CSR count: matrix + (gather x_k, read x_{k-1}, read b, write x_{k+1}) per
+    # column + dinv; and the bytes of the image the launch streams: the row-class kernel reads no
+    # matrix data (class table in LDS, 1 / a_rr included), the box-image kernel one array per offset
+    csr_bytes = 12 * nnz + 4 * (n + 1) + 32 * cols * n + 8 * n
+    kname = M.kernel("cheb32")
+    info = M.info
+    if kname == "k_boxc_mv8_cheb":
+        cheb_bytes = 32 * cols * n
+    elif kname == "k_box_mv32_cheb":
+        cheb_bytes = (8 * (2 * info.sym_arrays - 1) + info.sym_mask_bytes + 8) * n + 32 * cols * n
+    else:
+        cheb_bytes = csr_bytes
     cheb_us = t.cheb_ms / t.cheb_launches * 1e3
     emit(config=f"C5 P1 Kuhn K/M {N}^3, block Lanczos k={b}", op=f"block step (Chebyshev degree {degree}, CGS2, CholQR2)",
          block_steps_per_s=round(steps / (t.total_ms * 1e-3), 3), ms_per_step=round(t.total_ms / steps, 2),
          kspmm_ms=round(t.kspmm_ms / steps, 2), cheb_ms=round(t.cheb_ms / steps, 2),
          orth_ms=round(t.orth_ms / steps, 2), norm_ms=round(t.norm_ms / steps, 2),
-         cheb_kernel_us=round(cheb_us, 1), cheb_bytes_per_launch=cheb_bytes,
+         cheb_kernel=kname, cheb_kernel_us=round(cheb_us, 1), cheb_bytes_per_launch=cheb_bytes,
          cheb_GBs=round(cheb_bytes / (cheb_us * 1e-6) / 1e9, 1),
-         cheb_frac=round(cheb_bytes / (cheb_us * 1e-6) / 1e9 / PEAK, 4), nnz=nnz, setup_s=round(setup_s, 1),
+         cheb_frac=round(cheb_bytes / (cheb_us * 1e-6) / 1e9 / PEAK, 4),
+         cheb_csr_bytes=csr_bytes, cheb_csr_equiv_GBs=round(csr_bytes / (cheb_us * 1e-6) / 1e9, 1),
+         nnz=nnz, setup_s=round(setup_s, 1),
          top_ritz=[float(x) for x in ev], steps_taken=steps + warm)
     bl.close()
 

@@ -50,7 +50,7 @@ def main():
                 eigmi.mass_solve_mv8(M, m, d, B, X)
                 ts[d] = time.perf_counter() - t0
             res[i].append((ts[args.dhi] - ts[args.dlo]) / (args.dhi - args.dlo))
-    byt = 12 * nnz + 4 * (n + 1) + (32 * m + 8) * n
+    byt = 12 * nnz + 4 * (n + 1) + (32 * m + 8) * n  # SURVEY 8(d) CSR count (the row-class kernel: 32 m n)
     for i, var in enumerate(variants):
         t = float(np.median(res[i]))
         print(json.dumps({"variant": var, "N": N, "m": m, "kernel": M.kernel("cheb8"), "launch_ms": round(t * 1e3, 3),
