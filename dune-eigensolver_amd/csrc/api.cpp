@@ -95,7 +95,10 @@ void allreduce_sum(eig_ctx_t ctx, double *buf, i64 count, hipStream_t s)
 
 bool allreduce_overlaps(eig_ctx_t ctx)
 {
-  return ctx->distributed() && !ctx->loop && ((ctx->mbox && ctx->mbox->ready) || ctx->comm_red);
+  const bool ovl = ctx->distributed() && !ctx->loop && ((ctx->mbox && ctx->mbox->ready) || ctx->comm_red);
+  // the reduction stream exists only where it is used (every stream takes a hardware queue)
+  if (ovl && !ctx->red_stream) EIG_HIP(hipStreamCreateWithFlags(&ctx->red_stream, hipStreamNonBlocking));
+  return ovl;
 }
 
 void allreduce_sum_red(eig_ctx_t ctx, double *buf, i64 count, hipStream_t s)
@@ -275,7 +278,6 @@ extern "C" int eig_ctx_create(int device, eig_ctx_t *out)
     {
       EIG_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
       EIG_HIP(hipStreamCreateWithFlags(&ctx->comm_stream, hipStreamNonBlocking));
-      EIG_HIP(hipStreamCreateWithFlags(&ctx->red_stream, hipStreamNonBlocking));
       hipDeviceProp_t prop;
       EIG_HIP(hipGetDeviceProperties(&prop, device));
       ctx->num_cu = prop.multiProcessorCount;

@@ -375,7 +375,10 @@ struct TrsvImage {
   double *uv = nullptr, *ud = nullptr;
   i32 *P = nullptr, *Q = nullptr;
   double *scale = nullptr;                // Rs[P[k]] (do_recip) or 1 / Rs[P[k]]
-  void *arena = nullptr;                  // the one allocation holding lrp .. scale
+  void *arena = nullptr;                  // the one allocation holding P, Q, scale
+  void *arena_rows = nullptr;             // the one allocation holding lrp .. ud (when `rows`)
+  bool rows = false;                      // the row-CSR factors are on the device
+  hipStream_t stream = nullptr;           // the owning context's stream (uploads)
   // Block-staged image (k_tsolve_staged, k_trsv.hip), per factor (0 = L, 1 = U) and 64-row block b:
   // the entries outside the block as an ELL slab [k][r] (off1[b] .. + w1[b] * 64; column -1 =
   // padding), the entries inside it as a dense 64 x 64 tile [t][r] (tile + b * 4096) + row masks.
@@ -399,6 +402,9 @@ struct TrsvImage {
   int gd[2] = {0, 0};
   bool binv = false;
 };
+void trsv_upload_rows(TrsvImage &img, const std::vector<i64> &lrp, const std::vector<i32> &lc,
+                      const std::vector<double> &lv, const std::vector<i64> &urp, const std::vector<i32> &uc,
+                      const std::vector<double> &uv, const std::vector<double> &ud);
 void trsv_upload(eig_ctx_t ctx, i64 n, const std::vector<i64> &lrp, const std::vector<i32> &lc,
                  const std::vector<double> &lv, const std::vector<i64> &urp, const std::vector<i32> &uc,
                  const std::vector<double> &uv, const std::vector<double> &ud, const std::vector<i64> &P,

@@ -543,11 +543,15 @@ int grid256(i64 work)
 }
 
 template <class T>
-T *upload(const std::vector<T> &h)
+T *upload(const std::vector<T> &h, hipStream_t stream)
 {
   void *p = nullptr;
   EIG_HIP(hipMalloc(&p, std::max<size_t>(h.size(), 1) * sizeof(T)));
-  if (!h.empty()) EIG_HIP(hipMemcpy(p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
+  if (!h.empty())
+  {
+    EIG_HIP(hipMemcpyAsync(p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice, stream));
+    EIG_HIP(hipStreamSynchronize(stream));
+  }
   return static_cast<T *>(p);
 }
 }  // namespace
@@ -609,12 +613,12 @@ void build_staged(TrsvImage &img)
         }
       }
     off.resize(nblocks);
-    img.off1[f] = upload(off);
-    img.w1[f] = upload(w);
-    img.v1[f] = upload(v1);
-    img.c1[f] = upload(c1);
-    img.tile[f] = upload(tl);
-    img.tmask[f] = upload(tm);
+    img.off1[f] = upload(off, img.stream);
+    img.w1[f] = upload(w, img.stream);
+    img.v1[f] = upload(v1, img.stream);
+    img.c1[f] = upload(c1, img.stream);
+    img.tile[f] = upload(tl, img.stream);
+    img.tmask[f] = upload(tm, img.stream);
   };
   stage(0, H.lrp, H.lc, H.lv, H.ls);
   stage(1, H.urp, H.uc, H.uv, H.us);
@@ -637,25 +641,14 @@ void parallel_blocks(i64 nb, F &&f)
 }
 }  // namespace
 
-void trsv_upload(eig_ctx_t ctx, i64 n, const std::vector<i64> &lrp, const std::vector<i32> &lc,
-                 const std::vector<double> &lv, const std::vector<i64> &urp, const std::vector<i32> &uc,
-                 const std::vector<double> &uv, const std::vector<double> &ud, const std::vector<i64> &P,
-                 const std::vector<i64> &Q, const std::vector<double> &scale, TrsvImage &img)
+namespace {
+// split points: L row i -> first entry inside i's 64-row block; U row i (descending columns) ->
+// first entry with a column inside the block
+void row_splits(i64 n, const std::vector<i64> &lrp, const std::vector<i32> &lc, const std::vector<i64> &urp,
+                const std::vector<i32> &uc, std::vector<i64> &ls, std::vector<i64> &us)
 {
-  (void)ctx;
-  img.n = n;
-  // EIGMI_TRACE_SETUP=1: phase times of the upload on stderr
-  const bool trace = std::getenv("EIGMI_TRACE_SETUP") != nullptr;
-  auto t_last = std::chrono::steady_clock::now();
-  auto phase = [&](const char *what) {
-    if (!trace) return;
-    const auto now = std::chrono::steady_clock::now();
-    fprintf(stderr, "trsv_upload %-10s %8.2f ms\n", what, std::chrono::duration<double, std::milli>(now - t_last).count());
-    t_last = now;
-  };
-  // split points: L row i -> first entry inside i's 64-row block; U row i (descending columns) ->
-  // first entry with a column inside the block
-  std::vector<i64> ls(n), us(n);
+  ls.resize(n);
+  us.resize(n);
   for (i64 i = 0; i < n; ++i)
   {
     const i64 bs = i / kTB * kTB, be = std::min(bs + kTB, n);
@@ -666,6 +659,84 @@ void trsv_upload(eig_ctx_t ctx, i64 n, const std::vector<i64> &lrp, const std::v
     while (k < urp[i + 1] && uc[k] >= be) ++k;
     us[i] = k;
   }
+}
+
+// Host arrays into ONE device allocation with ONE copy (a dozen separate small hipMalloc + hipMemcpy
+// calls cost ~1 ms each); returns the allocation and the device address of every part.
+void *upload_parts(const std::vector<std::pair<const void *, size_t>> &parts, std::vector<char *> &at,
+                   hipStream_t stream)
+{
+  std::vector<size_t> off(parts.size());
+  size_t total = 0;
+  for (size_t k = 0; k < parts.size(); ++k)
+  {
+    off[k] = total;
+    total += (std::max<size_t>(parts[k].second, 8) + 255) / 256 * 256;
+  }
+  std::vector<char> h(total, 0);
+  for (size_t k = 0; k < parts.size(); ++k)
+    if (parts[k].second) std::memcpy(h.data() + off[k], parts[k].first, parts[k].second);
+  void *d = nullptr;
+  const bool trace = std::getenv("EIGMI_TRACE_SETUP") != nullptr;
+  auto t0 = std::chrono::steady_clock::now();
+  EIG_HIP(hipMalloc(&d, total));
+  auto t1 = std::chrono::steady_clock::now();
+  EIG_HIP(hipMemcpyAsync(d, h.data(), total, hipMemcpyHostToDevice, stream));
+  EIG_HIP(hipStreamSynchronize(stream));
+  auto t2 = std::chrono::steady_clock::now();
+  if (trace)
+    fprintf(stderr, "upload_parts %zu B: malloc %.2f ms, memcpy %.2f ms\n", total,
+            std::chrono::duration<double, std::milli>(t1 - t0).count(),
+            std::chrono::duration<double, std::milli>(t2 - t1).count());
+  at.resize(parts.size());
+  for (size_t k = 0; k < parts.size(); ++k) at[k] = static_cast<char *>(d) + off[k];
+  return d;
+}
+}  // namespace
+
+// The row-CSR factors the substitution kernels read (k_tsolve, and the U diagonal of the staged one).
+void trsv_upload_rows(TrsvImage &img, const std::vector<i64> &lrp, const std::vector<i32> &lc,
+                      const std::vector<double> &lv, const std::vector<i64> &urp, const std::vector<i32> &uc,
+                      const std::vector<double> &uv, const std::vector<double> &ud)
+{
+  if (img.rows) return;
+  std::vector<i64> ls, us;
+  row_splits(img.n, lrp, lc, urp, uc, ls, us);
+  std::vector<char *> at;
+  img.arena_rows = upload_parts({{lrp.data(), lrp.size() * 8}, {ls.data(), ls.size() * 8}, {lc.data(), lc.size() * 4},
+                                 {lv.data(), lv.size() * 8}, {urp.data(), urp.size() * 8}, {us.data(), us.size() * 8},
+                                 {uc.data(), uc.size() * 4}, {uv.data(), uv.size() * 8}, {ud.data(), ud.size() * 8}},
+                                at, img.stream);
+  img.lrp = (i64 *)at[0];
+  img.lsplit = (i64 *)at[1];
+  img.lc = (i32 *)at[2];
+  img.lv = (double *)at[3];
+  img.urp = (i64 *)at[4];
+  img.usplit = (i64 *)at[5];
+  img.uc = (i32 *)at[6];
+  img.uv = (double *)at[7];
+  img.ud = (double *)at[8];
+  img.rows = true;
+}
+
+void trsv_upload(eig_ctx_t ctx, i64 n, const std::vector<i64> &lrp, const std::vector<i32> &lc,
+                 const std::vector<double> &lv, const std::vector<i64> &urp, const std::vector<i32> &uc,
+                 const std::vector<double> &uv, const std::vector<double> &ud, const std::vector<i64> &P,
+                 const std::vector<i64> &Q, const std::vector<double> &scale, TrsvImage &img)
+{
+  img.n = n;
+  img.stream = ctx ? ctx->stream : nullptr;
+  // EIGMI_TRACE_SETUP=1: phase times of the upload on stderr
+  const bool trace = std::getenv("EIGMI_TRACE_SETUP") != nullptr;
+  auto t_last = std::chrono::steady_clock::now();
+  auto phase = [&](const char *what) {
+    if (!trace) return;
+    const auto now = std::chrono::steady_clock::now();
+    fprintf(stderr, "trsv_upload %-10s %8.2f ms\n", what, std::chrono::duration<double, std::milli>(now - t_last).count());
+    t_last = now;
+  };
+  std::vector<i64> ls, us;
+  row_splits(n, lrp, lc, urp, uc, ls, us);
   std::vector<i32> p32(n), q32(n);
   for (i64 k = 0; k < n; ++k)
   {
@@ -786,8 +857,8 @@ void trsv_upload(eig_ctx_t ctx, i64 n, const std::vector<i64> &lrp, const std::v
     }
     });
     if (!ok) return false;
-    img.dinv[f] = upload(dinv);
-    img.g[f] = upload(gt);
+    img.dinv[f] = upload(dinv, img.stream);
+    img.g[f] = upload(gt, img.stream);
     return true;
   };
   {
@@ -814,42 +885,18 @@ void trsv_upload(eig_ctx_t ctx, i64 n, const std::vector<i64> &lrp, const std::v
   if (img.staged && !img.binv)
     img.host = std::make_shared<TrsvHostRows>(TrsvHostRows{lrp, lc, lv, ls, urp, uc, uv, us});
   phase("binv");
-  // the row-CSR factors, permutations and scaling: ONE device allocation and ONE copy (a dozen
-  // separate small hipMalloc + hipMemcpy calls cost ~1 ms each)
+  // permutations and scaling (every solve); the row-CSR factors only where a substitution kernel
+  // is the default -- with the block-inverse image they are uploaded when eig_lu_set_solver asks
+  // for EIG_TRSV_STAGED / _CSR (lu.cpp rebuilds them from the factors it keeps)
   {
-    std::vector<std::pair<const void *, size_t>> parts = {
-        {lrp.data(), lrp.size() * 8}, {ls.data(), ls.size() * 8},   {lc.data(), lc.size() * 4},
-        {lv.data(), lv.size() * 8},   {urp.data(), urp.size() * 8}, {us.data(), us.size() * 8},
-        {uc.data(), uc.size() * 4},   {uv.data(), uv.size() * 8},   {ud.data(), ud.size() * 8},
-        {p32.data(), p32.size() * 4}, {q32.data(), q32.size() * 4}, {scale.data(), scale.size() * 8}};
-    std::vector<size_t> off(parts.size());
-    size_t total = 0;
-    for (size_t k = 0; k < parts.size(); ++k)
-    {
-      off[k] = total;
-      total += (std::max<size_t>(parts[k].second, 8) + 255) / 256 * 256;
-    }
-    std::vector<char> h(total, 0);
-    for (size_t k = 0; k < parts.size(); ++k)
-      if (parts[k].second) std::memcpy(h.data() + off[k], parts[k].first, parts[k].second);
-    void *d = nullptr;
-    EIG_HIP(hipMalloc(&d, total));
-    EIG_HIP(hipMemcpy(d, h.data(), total, hipMemcpyHostToDevice));
-    char *b = static_cast<char *>(d);
-    img.arena = d;
-    img.lrp = (i64 *)(b + off[0]);
-    img.lsplit = (i64 *)(b + off[1]);
-    img.lc = (i32 *)(b + off[2]);
-    img.lv = (double *)(b + off[3]);
-    img.urp = (i64 *)(b + off[4]);
-    img.usplit = (i64 *)(b + off[5]);
-    img.uc = (i32 *)(b + off[6]);
-    img.uv = (double *)(b + off[7]);
-    img.ud = (double *)(b + off[8]);
-    img.P = (i32 *)(b + off[9]);
-    img.Q = (i32 *)(b + off[10]);
-    img.scale = (double *)(b + off[11]);
+    std::vector<char *> at;
+    img.arena = upload_parts({{p32.data(), p32.size() * 4}, {q32.data(), q32.size() * 4},
+                              {scale.data(), scale.size() * 8}}, at, img.stream);
+    img.P = (i32 *)at[0];
+    img.Q = (i32 *)at[1];
+    img.scale = (double *)at[2];
   }
+  if (!img.binv) trsv_upload_rows(img, lrp, lc, lv, urp, uc, uv, ud);
   phase("csr");
 }
 
@@ -859,7 +906,8 @@ void trsv_free(TrsvImage &img)
     for (void *p : {(void *)img.off1[f], (void *)img.w1[f], (void *)img.v1[f], (void *)img.c1[f], (void *)img.tile[f],
                     (void *)img.tmask[f], (void *)img.dinv[f], (void *)img.g[f]})
       if (p) (void)hipFree(p);
-  if (img.arena) (void)hipFree(img.arena);  // (the row-CSR arrays live inside it)
+  if (img.arena) (void)hipFree(img.arena);
+  if (img.arena_rows) (void)hipFree(img.arena_rows);  // (the row-CSR arrays live inside it)
   img = TrsvImage();
 }
 
@@ -887,6 +935,7 @@ void launch_inverse_mv8(TrsvImage &img, i64 m, double *Qin, double *Qout, hipStr
     EIG_HIP(hipGetLastError());
     return;
   }
+  EIG_CHECK(img.rows, EIG_ERR_ARG, "triangular solve: row factors not on the device (eig_lu_set_solver uploads them)");
   if (img.staged && !img.staged_built && !csr && img.host) build_staged(img);
   hipLaunchKernelGGL(k_perm_scale, dim3(grid256(n * nblk)), dim3(256), 0, s, n, nblk, img.P, img.scale, Qin, Qout);
   if (!img.staged_built || csr)

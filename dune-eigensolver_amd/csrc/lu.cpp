@@ -145,32 +145,56 @@ struct eig_lu_s {
 
 namespace {
 
-void build_device(eig_lu_s &lu)
+// The factors in the row form the device solves read: L rows without the unit diagonal (ascending
+// columns), U rows without the diagonal (descending columns) and the U diagonal.
+void factor_rows(const eig_lu_s &lu, std::vector<i64> &lrp, std::vector<i32> &lc, std::vector<double> &lv,
+                 std::vector<i64> &urp, std::vector<i32> &uc, std::vector<double> &uv, std::vector<double> &ud)
 {
   const i64 n = lu.n;
   // L rows: the reference subtracts entries Lp[i] .. Lp[i+1]-2 in stored order (the last entry is
   // the unit diagonal, kernels_cpp.hh:716-722).  Stored order is kept when ascending; otherwise the
   // row is sorted by column (then equal to the reference to rounding, not bitwise).
-  std::vector<i64> lrp(n + 1, 0), urp(n + 1, 0);
-  std::vector<i32> lc, uc;
-  std::vector<double> lv, uv, ud(n);
+  lrp.assign(n + 1, 0);
+  urp.assign(n + 1, 0);
+  lc.clear();
+  lv.clear();
+  ud.assign(n, 0.0);
+  // L: rows copied as stored when ascending (the usual case), else through a sorted copy
+  lc.reserve(lu.Lx.size());
+  lv.reserve(lu.Lx.size());
+  std::vector<std::pair<i64, double>> e;
   for (i64 i = 0; i < n; ++i)
   {
-    std::vector<std::pair<i64, double>> e;
-    for (i64 k = lu.Lp[i]; k < lu.Lp[i + 1] - 1; ++k) e.push_back({lu.Lj[k], lu.Lx[k]});
-    std::stable_sort(e.begin(), e.end(), [](const auto &a, const auto &b) { return a.first < b.first; });
-    for (auto &p : e)
+    const i64 b = lu.Lp[i], t = lu.Lp[i + 1] - 1;  // (the last entry is the unit diagonal)
+    bool sorted = true;
+    for (i64 k = b; k < t; ++k)
     {
-      EIG_CHECK(p.first >= 0 && p.first < i, EIG_ERR_ARG, "L factor: entry not strictly below the diagonal");
-      lc.push_back((i32)p.first);
-      lv.push_back(p.second);
+      EIG_CHECK(lu.Lj[k] >= 0 && lu.Lj[k] < i, EIG_ERR_ARG, "L factor: entry not strictly below the diagonal");
+      if (k > b && lu.Lj[k] < lu.Lj[k - 1]) sorted = false;
+    }
+    if (sorted)
+      for (i64 k = b; k < t; ++k)
+      {
+        lc.push_back((i32)lu.Lj[k]);
+        lv.push_back(lu.Lx[k]);
+      }
+    else
+    {
+      e.clear();
+      for (i64 k = b; k < t; ++k) e.push_back({lu.Lj[k], lu.Lx[k]});
+      std::stable_sort(e.begin(), e.end(), [](const auto &a, const auto &c) { return a.first < c.first; });
+      for (auto &q : e)
+      {
+        lc.push_back((i32)q.first);
+        lv.push_back(q.second);
+      }
     }
     lrp[i + 1] = (i64)lc.size();
   }
   // U: column j holds rows Ui[Up[j] .. Up[j+1]-2] above the diagonal Ux[Up[j+1]-1]; the reference's
   // push loop (kernels_cpp.hh:730-745) updates row i with columns j in DECREASING order, which is
-  // the order the pull form below uses -- bitwise whatever the order inside a column.
-  std::vector<std::vector<std::pair<i64, double>>> rows(n);
+  // the order the pull form below uses -- bitwise whatever the order inside a column.  Transposed
+  // by a counting sort over the columns in descending order (rows come out descending).
   for (i64 j = 0; j < n; ++j)
   {
     EIG_CHECK(lu.Up[j + 1] > lu.Up[j], EIG_ERR_ARG, "U factor: empty column");
@@ -178,21 +202,31 @@ void build_device(eig_lu_s &lu)
     for (i64 k = lu.Up[j]; k < lu.Up[j + 1] - 1; ++k)
     {
       EIG_CHECK(lu.Ui[k] >= 0 && lu.Ui[k] < j, EIG_ERR_ARG, "U factor: entry not strictly above the diagonal");
-      rows[lu.Ui[k]].push_back({j, lu.Ux[k]});
+      ++urp[lu.Ui[k] + 1];
     }
   }
-  for (i64 i = 0; i < n; ++i)
+  for (i64 i = 0; i < n; ++i) urp[i + 1] += urp[i];
+  uc.resize((size_t)urp[n]);
+  uv.resize((size_t)urp[n]);
   {
-    auto &e = rows[i];
-    std::stable_sort(e.begin(), e.end(), [](const auto &a, const auto &b) { return a.first > b.first; });
-    for (auto &p : e)
-    {
-      uc.push_back((i32)p.first);
-      uv.push_back(p.second);
-    }
-    urp[i + 1] = (i64)uc.size();
-    std::vector<std::pair<i64, double>>().swap(e);
+    std::vector<i64> next(urp.begin(), urp.end() - 1);
+    for (i64 j = n - 1; j >= 0; --j)
+      for (i64 k = lu.Up[j]; k < lu.Up[j + 1] - 1; ++k)
+      {
+        const i64 at = next[lu.Ui[k]]++;
+        uc[at] = (i32)j;
+        uv[at] = lu.Ux[k];
+      }
   }
+}
+
+void build_device(eig_lu_s &lu)
+{
+  const i64 n = lu.n;
+  std::vector<i64> lrp, urp;
+  std::vector<i32> lc, uc;
+  std::vector<double> lv, uv, ud;
+  factor_rows(lu, lrp, lc, lv, urp, uc, uv, ud);
   std::vector<i64> P(lu.P), Q(lu.Q);
   std::vector<double> scale(n);
   for (i64 k = 0; k < n; ++k)
@@ -420,6 +454,16 @@ extern "C" int eig_lu_set_solver(eig_lu_t lu, int kind)
     EIG_CHECK(kind >= EIG_TRSV_AUTO && kind <= EIG_TRSV_CSR, EIG_ERR_ARG, "eig_lu_set_solver: unknown solver");
     EIG_CHECK(kind != EIG_TRSV_BLOCKINV || !lu->ctx || lu->img.binv, EIG_ERR_ARG,
               "eig_lu_set_solver: these factors have no block-inverse image");
+    if ((kind == EIG_TRSV_STAGED || kind == EIG_TRSV_CSR) && lu->ctx && !lu->img.rows)
+    {
+      // the substitution kernels read the row factors, not uploaded next to a block-inverse image
+      EIG_HIP(hipSetDevice(lu->ctx->device));
+      std::vector<i64> lrp, urp;
+      std::vector<i32> lc, uc;
+      std::vector<double> lv, uv, ud;
+      factor_rows(*lu, lrp, lc, lv, urp, uc, uv, ud);
+      trsv_upload_rows(lu->img, lrp, lc, lv, urp, uc, uv, ud);
+    }
     lu->img.solver = kind;
   });
 }
