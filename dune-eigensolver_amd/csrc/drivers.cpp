@@ -1234,6 +1234,7 @@ extern "C" int eig_lanczos_create_ex(eig_mat_t A, int max_steps, const double *u
       ws->max_steps = max_steps;
       ws->pipe = (flags & EIG_LANCZOS_PIPELINED) != 0;
       ws->fused = ws->pipe || (flags & EIG_LANCZOS_FUSED) != 0;
+      if (ws->pipe) (void)allreduce_overlaps(ctx);  // creates the reduction stream before any capture
       // worst case: every step repaired, plus one forced repair per eig_lanczos_tridiag call
       ws->max_launches = ws->fused ? 3 * max_steps + 8 : 0;
       const size_t wb = (size_t)A->window * sizeof(double);
