@@ -599,7 +599,7 @@ bool box_prepare(const eig_mat_s &Ac)
 static bool launch_box(const eig_mat_s &A, i64 m, const double *X, double *Y, const double *Xold, const double *Bv,
                        const double *dinv, double omega, double gamma, bool cheb, hipStream_t s)
 {
-  if (m <= 0 || m % 32 != 0 || !box_prepare(A)) return false;
+  if (m <= 0 || m % 8 != 0 || !box_prepare(A)) return false;
   if (A.box_ctab)
   {
     // row-class kernels: one launch, blockIdx.y = column block; z runs for ~2 rounds of the
@@ -631,6 +631,7 @@ static bool launch_box(const eig_mat_s &A, i64 m, const double *X, double *Y, co
     EIG_HIP(hipGetLastError());
     return true;
   }
+  if (m % 32 != 0) return false;  // the box-image kernel takes 32 columns per pass
   BoxGeom g;
   g.nx = A.box_nx;
   g.ny = A.box_ny;

@@ -1925,6 +1925,8 @@ std::string kernel_for(const eig_mat_s &A, int op)
       return name;
     case 3:
     case 4:
+      // 3-D box stencils whose rows are class-constant: the row-class kernels for any m % 8 == 0
+      if (b1 && box_prepare(A) && A.box_ctab) return op == 3 ? "k_boxc_mv8" : "k_boxc_mv8_cheb";
     {
       if (!b1) return "none";
       i64 P;

@@ -885,7 +885,8 @@ def bytes_spmv(n, nnz):
 def image_bytes(M, op, m=8):
     """Algorithmic HBM bytes of one launch sequence on M's device image:
     op "spmv" (y = A x) or "spmm" (m columns).  The symmetric band image streams 8 B per band slot
-    and the row mask once per 8-column block (the plane march); other images the SURVEY 8(d) CSR
+    and the row mask once per 8-column block (the plane march); the row-class image (3-D box
+    stencils with class-constant rows) no matrix data at all; other images the SURVEY 8(d) CSR
     count (12 B per nonzero + row pointers), which the SELL/stencil kernels stream at most."""
     info = M.info
     n, nnz = info.n, info.nnzb
@@ -894,6 +895,8 @@ def image_bytes(M, op, m=8):
     if op == "spmv":
         return mat + 16 * n
     if op == "spmm":
+        if M.kernel("spmm8") == "k_boxc_mv8":  # row-class image: the class table lives in LDS
+            return 16 * m * n
         return (m // 8 if band else 1) * mat + 16 * m * n
     raise ValueError(op)
 

@@ -177,8 +177,9 @@ def test_march_spmm_bitwise(ctx, mat, m):
          "band_partial": lambda: band_matrix(5000, [0, 1, 12, 144], 21),
          "band_u32": lambda: band_matrix(3000, [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 48], 22, drop=0.1),
          "band_no_pm1": lambda: band_matrix(3000, [0, 2, 64], 23)}[mat]()
-    M = upload(ctx, A)
+    M = upload(ctx, A, flags=eigmi.MAT_NO_CLASS)  # (the 3-D box grids would take the row-class kernel)
     assert M.info.sym_offsets > 0
+    assert M.kernel("spmm8") != "k_boxc_mv8"
     Qh = oracle.random_mv8(A.n, m, 5)
     Q, Y = ctx.array(Qh), ctx.zeros(A.n * m)
     eigmi.spmm_mv8(M, m, Q, Y)
@@ -200,7 +201,7 @@ def _p1(N, which):
 def test_marchg_spmm_bitwise(ctx, mat, m):
     A = {"p1mass8": lambda: _p1(8, "M"), "p1stiff8": lambda: _p1(8, "K"), "p1mass16": lambda: _p1(16, "M"),
          "band_beyond": lambda: band_matrix(4000, [0, 1, 5, 32, 35, 40], 31, drop=0.05)}[mat]()
-    M = upload(ctx, A)
+    M = upload(ctx, A, flags=eigmi.MAT_NO_CLASS)
     assert M.info.sym_offsets > 0
     assert M.kernel("spmm8") == "k_spmm8_marchg"
     Qh = oracle.random_mv8(A.n, m, 6)
@@ -214,7 +215,7 @@ def test_marchg_chebyshev_matches_sell(ctx, N, m):
     """The fused Chebyshev-Jacobi mass solve (config C5) on the general band march against the
     SELL kernel (both fused multiply-adds in ascending offset order; tolerance: signed zeros)."""
     A = _p1(N, "M")
-    M = upload(ctx, A)
+    M = upload(ctx, A, flags=eigmi.MAT_NO_CLASS)
     assert M.kernel("cheb8") == "k_spmm8_marchg_cheb"
     n = A.n
     Bh = oracle.random_mv8(n, m, 8)
@@ -265,6 +266,20 @@ def test_box_spmm_bitwise(ctx, mat, m):
     M = upload(ctx, A)
     assert M.kernel("spmm32") == ("k_boxc_mv8" if BOX_CLASS[mat] else "k_box_mv32")
     Qh = oracle.random_mv8(A.n, m, 7)
+    Q, Y = ctx.array(Qh), ctx.zeros(A.n * m)
+    eigmi.spmm_mv8(M, m, Q, Y)
+    assert np.array_equal(Y.get(), oracle.spmm_mv8(A, Qh, m))
+
+
+@pytest.mark.parametrize("mat,m", [("poisson16", 8), ("poisson16", 24), ("p1mass16", 8), ("p1stiff20", 16)])
+def test_boxc_spmm_any_8_columns(ctx, mat, m):
+    """The row-class kernel serves any multiple of 8 columns (one MultiVector block per workgroup):
+    bitwise the reference SpMM (kernels_cpp.hh:626-657)."""
+    A = {"poisson16": lambda: oracle.poisson3d(16), "p1mass16": lambda: _p1(16, "M"),
+         "p1stiff20": lambda: _p1(20, "K")}[mat]()
+    M = upload(ctx, A)
+    assert M.kernel("spmm8") == "k_boxc_mv8"
+    Qh = oracle.random_mv8(A.n, m, 19)
     Q, Y = ctx.array(Qh), ctx.zeros(A.n * m)
     eigmi.spmm_mv8(M, m, Q, Y)
     assert np.array_equal(Y.get(), oracle.spmm_mv8(A, Qh, m))
