@@ -517,20 +517,264 @@ void shift_invert_core(eig_mat_t A, eig_mat_t B, const LuRef &F, double sigma, i
     if (restarts) *restarts = nrestart;
 }
 
+// Block variant (EIG_SI_BLOCK, the default where the basis fits): the same OP, the same wanted
+// pairs and the same B-inner product, by block Lanczos with Krylov-Schur (thick) restarts on p
+// columns at once.  Why: one application of OP is the block-inverse triangular solve, a chain over
+// the factor's 64-row blocks that one workgroup walks per 8 columns -- latency-bound, so p = 16
+// columns cost what one column costs (two chains side by side), and a block Krylov space reaches
+// the wanted pairs in a fraction of the applications the one-vector recurrence needs (nev = 8 on
+// the 200^2 GenEO pencil: 44 applications -> 8).  Basis V (c columns, MultiVector<double,8>
+// blocks) and BV = B V; per block step, with V_a the last p columns:
+//     W = OP(B V_a);  H = (B V)^T W, W -= V H  (twice: CGS2 in the B-inner product);
+//     W = F R (CholQR2 in the B-inner product);  T(:, a) = H, T(next, a) = R.
+// Rayleigh-Ritz on T; the residual of Ritz pair i is ||R y_i(a)|| (V_next is B-orthonormal), so the
+// convergence test is ||R y_i(a)|| <= tol |theta_i|.  Restart: U = V Y(:, kept) (kk Ritz vectors of
+// largest |theta|), T = diag(theta_kept) coupled to F by C = R Y(a, kept) -- again a block Krylov
+// decomposition OP [U F] = [U F] T + ..., extended from F.  Eigenvectors purified like the one-vector
+// path: x = OP(B V y) / theta, B-normalised (one block solve for all of them).
+struct SiBlockShape {
+  int nw, p, kk, cmax;
+};
+
+SiBlockShape si_block_shape(int nev, int ncv)
+{
+  SiBlockShape g;
+  g.nw = (nev + 7) / 8 * 8;
+  g.p = std::max(16, g.nw);
+  g.kk = (nev + (nev + 1) / 2 + 7) / 8 * 8;
+  g.cmax = std::max(g.kk + 3 * g.p, (ncv + 7) / 8 * 8);
+  return g;
+}
+
+void shift_invert_block_core(eig_mat_t A, eig_mat_t B, const LuRef &F, double sigma, int nev, int ncv, double tol,
+                             int maxit, unsigned seed, double *eval_host, double *evec_host, int *restarts)
+{
+  eig_ctx_t ctx = A->ctx;
+  EIG_HIP(hipSetDevice(ctx->device));
+  hipStream_t s = ctx->stream;
+  const i64 n = A->nb_rows;
+  const SiBlockShape g = si_block_shape(nev, ncv);
+  const int p = g.p, kk = g.kk, cmax = g.cmax, cap = cmax + p;
+  EIG_CHECK(nev < n && cap <= n, EIG_ERR_ARG, "shift-invert (block): the block basis does not fit n");
+  if (tol <= 0.0) tol = 2.220446049250313e-16;
+  if (maxit <= 0) maxit = 100 * nev;
+  const int wk = std::max(kk, g.nw);
+  DevBuf Vb((size_t)cap * n * 8), BVb(B ? (size_t)cap * n * 8 : 8), W1b((size_t)p * n * 8), W2b((size_t)p * n * 8),
+      BWb((size_t)p * n * 8), Ub((size_t)wk * n * 8), Hb((size_t)cap * std::max(p, wk) * 8);
+  double *V = Vb.d(), *BV = B ? BVb.d() : V, *W = W1b.d(), *Wt = W2b.d(), *BW = BWb.d(), *U = Ub.d(), *dH = Hb.d();
+  auto bmul = [&](const double *x, double *y, int cols) {  // y = B x (cols columns)
+    if (B) launch_spmm_mv8(*B, cols, x, y, s);
+    else if (y != x) EIG_HIP(hipMemcpyAsync(y, x, (size_t)cols * n * 8, hipMemcpyDeviceToDevice, s));
+  };
+  // y (q columns) = x (px columns) M, M px x q row-major on the host
+  std::vector<double> mneg;
+  auto mul_small = [&](const double *x, int px, const std::vector<double> &M, int q, double *y) {
+    mneg.resize((size_t)px * q);
+    for (size_t k = 0; k < mneg.size(); ++k) mneg[k] = -M[k];
+    EIG_HIP(hipMemcpyAsync(dH, mneg.data(), mneg.size() * 8, hipMemcpyHostToDevice, s));
+    EIG_HIP(hipMemsetAsync(y, 0, (size_t)q * n * 8, s));
+    for (int i = 0; i < px / 8; ++i) launch_project(n, q, x + (i64)i * 8 * n, y, dH + (size_t)i * 8 * q, s);
+    EIG_HIP(hipStreamSynchronize(s));  // (mneg is reused by the next call)
+  };
+  // OP on p columns: y = (A - sigma B)^-1 bx (bx is consumed as the solve's scratch)
+  auto op = [&](double *bx, double *y, int cols) { lu_inverse_device(F.lu, cols, bx, y, s); };
+  // W (p columns, scratch Wt) -> B-orthonormal F at dst / bdst with W = F R; false on a rank loss
+  std::vector<double> G((size_t)p * p), R((size_t)p * p), Ri((size_t)p * p), Rtot((size_t)p * p);
+  auto bortho = [&](double *dst, double *bdst) -> bool {
+    std::fill(Rtot.begin(), Rtot.end(), 0.0);
+    for (int i = 0; i < p; ++i) Rtot[(size_t)i * p + i] = 1.0;
+    for (int pass = 0; pass < 2; ++pass)
+    {
+      double *bw = B ? BW : W;
+      bmul(W, bw, p);
+      launch_gram_mv8(n, p, p, W, bw, dH, 0, s, ctx->red);
+      EIG_HIP(hipMemcpyAsync(G.data(), dH, G.size() * 8, hipMemcpyDeviceToHost, s));
+      EIG_HIP(hipStreamSynchronize(s));
+      for (int i = 0; i < p; ++i)
+        for (int j = i + 1; j < p; ++j) G[(size_t)j * p + i] = G[(size_t)i * p + j];
+      if (!chol_upper(p, G.data(), R.data())) return false;
+      tri_upper_inv(p, R.data(), Ri.data());
+      mul_small(W, p, Ri, p, Wt);
+      std::swap(W, Wt);
+      std::vector<double> Rn((size_t)p * p, 0.0);  // Rtot = R Rtot
+      for (int i = 0; i < p; ++i)
+        for (int k = i; k < p; ++k)
+          for (int j = k; j < p; ++j) Rn[(size_t)i * p + j] += R[(size_t)i * p + k] * Rtot[(size_t)k * p + j];
+      Rtot.swap(Rn);
+    }
+    EIG_HIP(hipMemcpyAsync(dst, W, (size_t)p * n * 8, hipMemcpyDeviceToDevice, s));
+    bmul(dst, bdst, p);
+    return true;
+  };
+  // start block: normal numbers put into the range of OP (dgetv0 for the generalised modes), then
+  // B-orthonormalised
+  {
+    std::vector<double> h((size_t)p * n);
+    host_random_normal((i64)p * n, seed, h.data());
+    EIG_HIP(hipMemcpyAsync(Wt, h.data(), h.size() * 8, hipMemcpyHostToDevice, s));
+    bmul(Wt, BW, p);
+    op(BW, W, p);
+    EIG_HIP(hipStreamSynchronize(s));  // (h)
+    EIG_CHECK(bortho(V, BV), EIG_ERR_BREAKDOWN, "shift-invert (block): start block is rank deficient");
+  }
+  std::vector<double> T((size_t)cap * cap, 0.0), th, Y, Hh, Ht;
+  int c = p, nrestart = 0;
+  std::vector<int> ord;
+  for (;;)
+  {
+    // extend: apply OP to the active block V(:, c - p .. c) until the basis holds cmax columns
+    for (;;)
+    {
+      const int a = c - p;
+      EIG_HIP(hipMemcpyAsync(BW, BV + (i64)a * n, (size_t)p * n * 8, hipMemcpyDeviceToDevice, s));
+      op(BW, W, p);
+      Ht.assign((size_t)c * p, 0.0);
+      for (int pass = 0; pass < 2; ++pass)  // CGS2 against V(:, 0 .. c) in the B-inner product
+      {
+        launch_gram_mv8(n, c, p, BV, W, dH, 0, s, ctx->red);
+        for (int i = 0; i < c / 8; ++i) launch_project(n, p, V + (i64)i * 8 * n, W, dH + (size_t)i * 8 * p, s);
+        Hh.resize((size_t)c * p);
+        EIG_HIP(hipMemcpyAsync(Hh.data(), dH, Hh.size() * 8, hipMemcpyDeviceToHost, s));
+        EIG_HIP(hipStreamSynchronize(s));
+        for (size_t k = 0; k < Hh.size(); ++k) Ht[k] += Hh[k];
+      }
+      for (int i = 0; i < c; ++i)
+        for (int j = 0; j < p; ++j) T[(size_t)i * cap + a + j] = T[(size_t)(a + j) * cap + i] = Ht[(size_t)i * p + j];
+      EIG_CHECK(bortho(V + (i64)c * n, BV + (i64)c * n), EIG_ERR_BREAKDOWN,
+                "shift-invert (block): invariant subspace reached (choose another seed or the one-vector solver)");
+      if (c + p > cmax) break;  // V(:, c .. c + p) is the residual block F, Rtot its coupling
+      for (int i = 0; i < p; ++i)
+        for (int j = 0; j < p; ++j)
+          T[(size_t)(c + i) * cap + a + j] = T[(size_t)(a + j) * cap + c + i] = Rtot[(size_t)i * p + j];
+      c += p;
+    }
+    const int a = c - p;
+    std::vector<double> Tc((size_t)c * c);
+    for (int i = 0; i < c; ++i)
+      for (int j = 0; j < c; ++j) Tc[(size_t)i * c + j] = T[(size_t)i * cap + j];
+    sym_eig(c, Tc, th, Y);  // Y[i * c + j]: component i of Ritz vector j
+    // "LM" on OP: the Ritz values of largest magnitude (eigenvalues of the pencil nearest sigma)
+    ord.resize(c);
+    std::iota(ord.begin(), ord.end(), 0);
+    std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return std::fabs(th[x]) > std::fabs(th[y]); });
+    // coupling of the Ritz vectors to F: C(:, j) = R y_j(a .. a + p)
+    auto coupling = [&](int j, int i) {
+      double v = 0.0;
+      for (int k = i; k < p; ++k) v += Rtot[(size_t)i * p + k] * Y[(size_t)(a + k) * c + j];
+      return v;
+    };
+    bool conv = true;
+    for (int q = 0; q < nev && conv; ++q)
+    {
+      double r2 = 0.0;
+      for (int i = 0; i < p; ++i)
+      {
+        const double v = coupling(ord[q], i);
+        r2 += v * v;
+      }
+      if (std::sqrt(r2) > tol * std::fabs(th[ord[q]])) conv = false;
+    }
+    if (conv || nrestart >= maxit) break;
+    // thick restart: U = V Y(:, kept), F moves behind it, T = diag(theta_kept) + the coupling C
+    {
+      std::vector<double> Ysel((size_t)c * kk);
+      for (int r = 0; r < c; ++r)
+        for (int q = 0; q < kk; ++q) Ysel[(size_t)r * kk + q] = Y[(size_t)r * c + ord[q]];
+      mul_small(V, c, Ysel, kk, U);
+      EIG_HIP(hipMemcpyAsync(V, U, (size_t)kk * n * 8, hipMemcpyDeviceToDevice, s));
+      EIG_HIP(hipMemcpyAsync(V + (i64)kk * n, V + (i64)c * n, (size_t)p * n * 8, hipMemcpyDeviceToDevice, s));
+      if (B)
+      {
+        EIG_HIP(hipMemcpyAsync(BV + (i64)kk * n, BV + (i64)c * n, (size_t)p * n * 8, hipMemcpyDeviceToDevice, s));
+        bmul(V, BV, kk);
+      }
+      std::fill(T.begin(), T.end(), 0.0);
+      for (int q = 0; q < kk; ++q)
+      {
+        T[(size_t)q * cap + q] = th[ord[q]];
+        for (int i = 0; i < p; ++i) T[(size_t)(kk + i) * cap + q] = T[(size_t)q * cap + kk + i] = coupling(ord[q], i);
+      }
+      c = kk + p;
+      ++nrestart;
+    }
+  }
+  // eigenpairs of the pencil: lambda = sigma + 1 / theta, ascending (:636-648)
+  std::vector<int> idx(nev);
+  std::iota(idx.begin(), idx.end(), 0);
+  std::vector<double> lam(nev);
+  for (int q = 0; q < nev; ++q) lam[q] = sigma + 1.0 / th[ord[q]];
+  std::stable_sort(idx.begin(), idx.end(), [&](int x, int y) { return lam[x] < lam[y]; });
+  for (int q = 0; q < nev; ++q) eval_host[q] = lam[idx[q]];
+  if (evec_host)
+  {
+    const int nw = g.nw;
+    std::vector<double> Ysel((size_t)c * nw, 0.0);
+    for (int q = 0; q < nev; ++q)
+    {
+      const int j = ord[idx[q]];
+      for (int r = 0; r < c; ++r) Ysel[(size_t)r * nw + q] = Y[(size_t)r * c + j] / th[j];
+    }
+    mul_small(BV, c, Ysel, nw, U);  // B V y / theta
+    op(U, W, nw);                   // x = OP(B V y) / theta
+    double *bw = B ? BW : W;
+    bmul(W, bw, nw);
+    launch_dot_diag_mv8(n, nw, W, bw, dH, 0, s, ctx->red);
+    std::vector<double> xb(nw), h((size_t)nw * n);
+    EIG_HIP(hipMemcpyAsync(xb.data(), dH, nw * 8, hipMemcpyDeviceToHost, s));
+    EIG_HIP(hipMemcpyAsync(h.data(), W, h.size() * 8, hipMemcpyDeviceToHost, s));
+    EIG_HIP(hipStreamSynchronize(s));
+    for (int q = 0; q < nev; ++q)
+    {
+      EIG_CHECK(xb[q] > 0.0, EIG_ERR_BREAKDOWN, "shift-invert: purified Ritz vector has no B-norm");
+      const double sc = 1.0 / std::sqrt(xb[q]);
+      for (i64 i = 0; i < n; ++i) evec_host[(i64)q * n + i] = sc * h[((i64)(q / 8) * n + i) * 8 + q % 8];
+    }
+  }
+  if (restarts) *restarts = nrestart;
+}
+
+// EIG_SI_AUTO: the block solver where its basis (cmax + p columns) is at most a quarter of n
+bool si_use_block(i64 n, int nev, int ncv, int flags)
+{
+  if (flags & EIG_SI_SINGLE) return false;
+  if (flags & EIG_SI_BLOCK) return true;
+  const SiBlockShape g = si_block_shape(nev, ncv);
+  return (i64)(g.cmax + g.p) * 4 <= n;
+}
+
+void shift_invert_run(eig_mat_t A, eig_mat_t B, const LuRef &F, double sigma, int nev, int ncv, double tol, int maxit,
+                      unsigned seed, double *eval_host, double *evec_host, int *restarts, int flags)
+{
+  if (si_use_block(A->nb_rows, nev, ncv, flags))
+    shift_invert_block_core(A, B, F, sigma, nev, ncv, tol, maxit, seed, eval_host, evec_host, restarts);
+  else
+    shift_invert_core(A, B, F, sigma, nev, ncv, tol, maxit, seed, eval_host, evec_host, restarts);
+}
+
 }  // namespace
+
+extern "C" int eig_shift_invert_solve_ex(eig_mat_t A, eig_mat_t B, eig_lu_t lu, double sigma, int nev, int ncv,
+                                         double tol, int maxit, unsigned seed, double *eval_host, double *evec_host,
+                                         int *restarts, int flags)
+{
+  return guard(A ? A->ctx : nullptr, [&] {
+    EIG_CHECK(A && eval_host && nev > 0, EIG_ERR_ARG, "eig_shift_invert_solve: bad argument");
+    EIG_CHECK((flags & ~(EIG_SI_SINGLE | EIG_SI_BLOCK)) == 0 && flags != (EIG_SI_SINGLE | EIG_SI_BLOCK), EIG_ERR_ARG,
+              "eig_shift_invert_solve_ex: unknown flags");
+    shift_invert_check(A, B);
+    EIG_HIP(hipSetDevice(A->ctx->device));
+    LuRef F;
+    shift_invert_factor(A, B, lu, sigma, F);
+    shift_invert_run(A, B, F, sigma, nev, ncv, tol, maxit, seed, eval_host, evec_host, restarts, flags);
+  });
+}
 
 extern "C" int eig_shift_invert_solve(eig_mat_t A, eig_mat_t B, eig_lu_t lu, double sigma, int nev, int ncv,
                                       double tol, int maxit, unsigned seed, double *eval_host, double *evec_host,
                                       int *restarts)
 {
-  return guard(A ? A->ctx : nullptr, [&] {
-    EIG_CHECK(A && eval_host && nev > 0, EIG_ERR_ARG, "eig_shift_invert_solve: bad argument");
-    shift_invert_check(A, B);
-    EIG_HIP(hipSetDevice(A->ctx->device));
-    LuRef F;
-    shift_invert_factor(A, B, lu, sigma, F);
-    shift_invert_core(A, B, F, sigma, nev, ncv, tol, maxit, seed, eval_host, evec_host, restarts);
-  });
+  return eig_shift_invert_solve_ex(A, B, lu, sigma, nev, ncv, tol, maxit, seed, eval_host, evec_host, restarts,
+                                   EIG_SI_AUTO);
 }
 
 // computeGenSymShiftInvertMinMagnitudeAdaptive (arpack_geneo_wrapper.hh:661-774): solve with nev =
@@ -555,7 +799,7 @@ extern "C" int eig_shift_invert_adaptive(eig_mat_t A, eig_mat_t B, eig_lu_t lu, 
     for (;;)
     {
       const int maxit = maxit_per_nev > 0 ? maxit_per_nev * nev : 0;
-      shift_invert_core(A, B, F, sigma, nev, 0, tol, maxit, seed, eval_host, evec_host, nullptr);
+      shift_invert_run(A, B, F, sigma, nev, 0, tol, maxit, seed, eval_host, evec_host, nullptr, EIG_SI_AUTO);
       ++pass;
       if (eval_host[nev - 1] >= threshold || nev >= max_nev) break;
       // (:770; for nev <= 3, int(nev * 1.3) == nev and the reference would solve the same problem

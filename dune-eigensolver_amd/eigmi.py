@@ -160,6 +160,8 @@ SIGNATURES = {
     "eig_generalized_inverse": (_int, [_vp, _vp, _vp, _dbl, _dbl, _dbl, _int, _int, _u, _vp, _vp, ctypes.POINTER(_int),
                                        _int]),
     "eig_shift_invert_solve": (_int, [_vp, _vp, _vp, _dbl, _int, _int, _dbl, _int, _u, _vp, _vp, ctypes.POINTER(_int)]),
+    "eig_shift_invert_solve_ex": (_int, [_vp, _vp, _vp, _dbl, _int, _int, _dbl, _int, _u, _vp, _vp,
+                                         ctypes.POINTER(_int), _int]),
     "eig_blanczos_create": (_int, [_vp, _vp, _int, _int, _int, _dbl, _dbl, _u, ctypes.POINTER(_vp)]),
     "eig_blanczos_create_si": (_int, [_vp, _vp, _vp, _dbl, _int, _int, _int, _dbl, _dbl, _u, ctypes.POINTER(_vp)]),
     "eig_blanczos_step": (_int, [_vp, _int, ctypes.POINTER(BlockTiming)]),
@@ -685,14 +687,20 @@ def generalized_inverse(A, B, shift, reg, tol, maxiter, nev, seed=123, lu=None, 
     return ev, (evec.reshape(nev, A.n) if want_evec else None), it.value
 
 
-def shift_invert_solve(A, nev, sigma=0.0, B=None, ncv=0, tol=0.0, maxit=0, seed=123, lu=None, want_evec=True):
-    """computeGenSymShiftInvertMinMagnitude: (eigenvalues ascending, B-normalised vectors, restarts)."""
+SI_AUTO, SI_SINGLE, SI_BLOCK = 0, 1, 2
+_SI_METHODS = {"auto": SI_AUTO, "single": SI_SINGLE, "block": SI_BLOCK}
+
+
+def shift_invert_solve(A, nev, sigma=0.0, B=None, ncv=0, tol=0.0, maxit=0, seed=123, lu=None, want_evec=True,
+                       method="auto"):
+    """computeGenSymShiftInvertMinMagnitude: (eigenvalues ascending, B-normalised vectors, restarts).
+    method: "auto" | "single" (one-vector thick-restart Lanczos) | "block" (block Krylov-Schur)."""
     ev = np.zeros(nev)
     evec = np.zeros(nev * A.n) if want_evec else None
     r = _int(0)
-    A.ctx.check(lib.eig_shift_invert_solve(A.h, B.h if B is not None else None, lu.h if lu else None, sigma, nev, ncv,
-                                           tol, maxit, seed, _np_ptr(ev), _np_ptr(evec) if want_evec else None,
-                                           ctypes.byref(r)))
+    A.ctx.check(lib.eig_shift_invert_solve_ex(A.h, B.h if B is not None else None, lu.h if lu else None, sigma, nev,
+                                              ncv, tol, maxit, seed, _np_ptr(ev), _np_ptr(evec) if want_evec else None,
+                                              ctypes.byref(r), _SI_METHODS[method]))
     return ev, (evec.reshape(nev, A.n) if want_evec else None), r.value
 
 

@@ -373,6 +373,21 @@ int eig_generalized_inverse(eig_mat_t A, eig_mat_t B, eig_lu_t lu, double shift,
  * B-normalised, or NULL; *restarts: thick restarts taken. */
 int eig_shift_invert_solve(eig_mat_t A, eig_mat_t B, eig_lu_t lu, double sigma, int nev, int ncv, double tol,
                            int maxit, unsigned seed, double *eval_host, double *evec_host, int *restarts);
+/* The same with the Krylov method chosen.  EIG_SI_SINGLE: the one-vector thick-restart Lanczos
+ * above (ARPACK's dsaupd recurrence; one OP application per basis vector).  EIG_SI_BLOCK: block
+ * Lanczos with Krylov-Schur restarts on p = max(16, 8 ceil(nev / 8)) columns -- one OP application
+ * is a latency-bound block-inverse chain per 8 columns that costs about the same for 16 columns as
+ * for one, so the block space reaches the wanted pairs in far fewer applications; the same wanted
+ * pairs, B-inner product, convergence test (||R y_i|| <= tol |theta_i|, R the residual block's
+ * coupling) and purified vectors; ncv = a lower bound on the search dimension; *restarts counts block
+ * restarts.  EIG_SI_AUTO (0, what eig_shift_invert_solve and eig_shift_invert_adaptive use): the block
+ * method when its basis (at most ~4 p + 1.5 nev columns) is at most n / 4, else the one-vector one. */
+#define EIG_SI_AUTO 0
+#define EIG_SI_SINGLE 1
+#define EIG_SI_BLOCK 2
+int eig_shift_invert_solve_ex(eig_mat_t A, eig_mat_t B, eig_lu_t lu, double sigma, int nev, int ncv, double tol,
+                              int maxit, unsigned seed, double *eval_host, double *evec_host, int *restarts,
+                              int flags);
 /* computeGenSymShiftInvertMinMagnitudeAdaptive (arpack_geneo_wrapper.hh:661-774): every eigenvalue of
  * the pencil below `threshold`, nev growing from initial_nev by x1.3 (the reference's code) up to
  * max_nev (= the reference's x.size(); at nev <= 3, where int(nev * 1.3) == nev would repeat the same

@@ -35,43 +35,51 @@ def check_vectors(As, Bs, ev, X, tol=1e-8):
     assert np.abs(G - np.eye(len(ev))).max() <= 1e-10
 
 
-def test_c1_standard_smallest(ctx):
+METHODS = ["single", "block"]
+
+
+@pytest.mark.parametrize("method", METHODS)
+def test_c1_standard_smallest(ctx, method):
     d = np.load(os.path.join(GOLD, "c1_arpack.npz"))
     A = oracle.laplace2d(64)
-    ev, X, restarts = eigmi.shift_invert_solve(up(ctx, A), 4, sigma=0.0)
+    ev, X, restarts = eigmi.shift_invert_solve(up(ctx, A), 4, sigma=0.0, method=method)
     assert np.allclose(ev, d["sa_w"], rtol=0, atol=1e-10)
     assert np.allclose(ev, np.sort(d["analytic"])[:4], rtol=0, atol=1e-10)
     check_vectors(A.to_scipy().toarray(), None, ev, X)
 
 
-def test_poisson3d_smallest(ctx):
+@pytest.mark.parametrize("method", METHODS)
+def test_poisson3d_smallest(ctx, method):
     d = np.load(os.path.join(GOLD, "poisson3d_16_arpack.npz"))
     A = oracle.poisson3d(16)
-    ev, _, _ = eigmi.shift_invert_solve(up(ctx, A), 4, sigma=0.0, want_evec=False)
+    ev, _, _ = eigmi.shift_invert_solve(up(ctx, A), 4, sigma=0.0, want_evec=False, method=method)
     assert np.allclose(ev, d["sa_w"], rtol=1e-11, atol=0)
 
 
-def test_geneo_pencil(ctx):
+@pytest.mark.parametrize("method", METHODS)
+def test_geneo_pencil(ctx, method):
     """The reference harness's ARPACK experiment, src/dune-eigensolver.cc:508-512."""
     d = np.load(os.path.join(GOLD, "geneo_arpack.npz"))
     N, shift = int(d["geneo_N"]), float(d["geneo_shift"])
     A, B = oracle.laplace2d(N, "neumann"), oracle.laplace2d(N, "pu", overlap=3)
-    ev, X, _ = eigmi.shift_invert_solve(up(ctx, A), 4, sigma=-shift, B=up(ctx, B))
+    ev, X, _ = eigmi.shift_invert_solve(up(ctx, A), 4, sigma=-shift, B=up(ctx, B), method=method)
     assert np.allclose(ev, d["geneo_w"], rtol=0, atol=1e-10)
     check_vectors(A.to_scipy().toarray(), B.to_scipy().toarray(), ev, X)
 
 
-def test_p1_pencil(ctx):
+@pytest.mark.parametrize("method", METHODS)
+def test_p1_pencil(ctx, method):
     d = np.load(os.path.join(GOLD, "geneo_arpack.npz"))
     K, M = oracle.p1_kuhn(int(d["p1_N"]))
     dK = eigmi.Matrix.from_bcsr(ctx, K.indptr.astype(np.int64), K.indices.astype(np.int32), K.data)
     dM = eigmi.Matrix.from_bcsr(ctx, M.indptr.astype(np.int64), M.indices.astype(np.int32), M.data)
-    ev, X, _ = eigmi.shift_invert_solve(dK, 6, sigma=0.0, B=dM)
+    ev, X, _ = eigmi.shift_invert_solve(dK, 6, sigma=0.0, B=dM, method=method)
     assert np.allclose(ev, d["p1_w"], rtol=1e-11, atol=0)
     check_vectors(K.toarray(), M.toarray(), ev, X)
 
 
-def test_given_factors_and_interior_shift(ctx):
+@pytest.mark.parametrize("method", METHODS)
+def test_given_factors_and_interior_shift(ctx, method):
     """Factors passed in (of A - sigma I, like the wrapper's ashiftb, :599-604) give the same
     answer; a shift inside the spectrum selects the eigenvalues nearest sigma."""
     A = oracle.laplace2d(24)
@@ -83,10 +91,24 @@ def test_given_factors_and_interior_shift(ctx):
     d = {k: v for k, v in d.items()}
     lu = eigmi.LU.from_factors(ctx, **d)
     dA = up(ctx, A)
-    ev1, _, _ = eigmi.shift_invert_solve(dA, 6, sigma=sigma, lu=lu, want_evec=False)
-    ev2, _, _ = eigmi.shift_invert_solve(dA, 6, sigma=sigma, want_evec=False)
+    ev1, _, _ = eigmi.shift_invert_solve(dA, 6, sigma=sigma, lu=lu, want_evec=False, method=method)
+    ev2, X, _ = eigmi.shift_invert_solve(dA, 6, sigma=sigma, method=method)
     nearest = np.sort(exact[np.argsort(np.abs(exact - sigma))[:6]])
     assert np.allclose(ev1, nearest, rtol=0, atol=1e-10) and np.allclose(ev2, nearest, rtol=0, atol=1e-10)
+    check_vectors(A.to_scipy().toarray(), None, ev2, X)  # (negative theta: eigenvalues below sigma)
+
+
+def test_block_method_arguments(ctx):
+    """EIG_SI_BLOCK needs its basis (cmax + p columns) inside n; both method flags at once is an error."""
+    A = oracle.laplace2d(6)
+    with pytest.raises(eigmi.EigError):
+        eigmi.shift_invert_solve(up(ctx, A), 4, sigma=0.0, method="block")  # n = 36 < 72 columns
+    ev, _, _ = eigmi.shift_invert_solve(up(ctx, A), 4, sigma=0.0, want_evec=False)  # auto: one-vector
+    assert np.allclose(ev, np.sort(oracle.eig_laplace2d(6))[:4], rtol=0, atol=1e-10)
+    with pytest.raises(eigmi.EigError):
+        A2 = up(ctx, A)
+        A2.ctx.check(eigmi.lib.eig_shift_invert_solve_ex(A2.h, None, None, 0.0, 4, 0, 0.0, 0, 1,
+                                                         eigmi._np_ptr(np.zeros(4)), None, None, 3))
 
 
 def test_argument_errors(ctx):
