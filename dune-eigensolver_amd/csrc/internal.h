@@ -410,6 +410,14 @@ void trsv_upload(eig_ctx_t ctx, i64 n, const std::vector<i64> &lrp, const std::v
                  const std::vector<double> &uv, const std::vector<double> &ud, const std::vector<i64> &P,
                  const std::vector<i64> &Q, const std::vector<double> &scale, TrsvImage &img);
 void trsv_free(TrsvImage &img);
+void trsv_attach_perm(eig_ctx_t ctx, i64 n, const std::vector<i64> &P, const std::vector<i64> &Q,
+                      const std::vector<double> &scale, TrsvImage &img);
+// Device band LU of B = (R^-1 A)[perm, perm] (k_band.hip) + its block-inverse image in img; the
+// band ([b][d + gd] 64 x 64 column-major tiles) is returned in *band_out.  false: a diagonal tile
+// failed the conditioning test (img untouched, the band still returned).
+bool band_lu_device(eig_ctx_t ctx, i64 n, int gd, const std::vector<i64> &rp, const std::vector<i32> &cj,
+                    const std::vector<double> &cv, const std::vector<i32> &inv, const std::vector<double> &rs,
+                    TrsvImage &img, double **band_out);
 void launch_inverse_mv8(TrsvImage &img, i64 m, double *Qin, double *Qout, hipStream_t s);
 void lu_inverse_device(eig_lu_t lu, i64 m, double *Qin, double *Qout, hipStream_t s);
 i64 lu_size(eig_lu_t lu);

@@ -900,6 +900,27 @@ void trsv_upload(eig_ctx_t ctx, i64 n, const std::vector<i64> &lrp, const std::v
   phase("csr");
 }
 
+// The permutations and scaling every solve applies, for an image whose block-inverse tiles were
+// built on the device (band_lu_device, k_band.hip).
+void trsv_attach_perm(eig_ctx_t ctx, i64 n, const std::vector<i64> &P, const std::vector<i64> &Q,
+                      const std::vector<double> &scale, TrsvImage &img)
+{
+  img.n = n;
+  img.stream = ctx->stream;
+  std::vector<i32> p32(n), q32(n);
+  for (i64 k = 0; k < n; ++k)
+  {
+    p32[k] = (i32)P[k];
+    q32[k] = (i32)Q[k];
+  }
+  std::vector<char *> at;
+  img.arena = upload_parts({{p32.data(), p32.size() * 4}, {q32.data(), q32.size() * 4}, {scale.data(), scale.size() * 8}},
+                           at, img.stream);
+  img.P = (i32 *)at[0];
+  img.Q = (i32 *)at[1];
+  img.scale = (double *)at[2];
+}
+
 void trsv_free(TrsvImage &img)
 {
   for (int f = 0; f < 2; ++f)

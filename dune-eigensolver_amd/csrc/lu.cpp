@@ -28,6 +28,11 @@ using namespace eigmi;
 
 namespace {
 
+// device band factorisation admission: coupled 64-row blocks (the block-inverse chain's limit) and
+// band + image tiles (2 GiB of 64 x 64 double tiles)
+constexpr i64 kBandMaxGD = 8;
+constexpr i64 kBandMaxTiles = 65536;
+
 // Reverse Cuthill-McKee on the symmetrised pattern; per connected component a BFS from a
 // pseudo-peripheral node, neighbours visited by increasing degree.  perm[k] = old index of new k.
 std::vector<i64> rcm(i64 n, const std::vector<std::vector<i64>> &adj)
@@ -137,9 +142,16 @@ struct eig_lu_s {
   // device image (k_trsv.hip): L rows without the unit diagonal, ascending columns; U rows
   // (transposed from the columns) without the diagonal, DESCENDING columns; U diagonal
   TrsvImage img;
+  // device-factored (band_lu_device): the band of 64 x 64 tiles, the envelope starts f and the block
+  // bandwidth; the host copy above is filled from the band on first request (host_ready)
+  double *band = nullptr;
+  int band_gd = 0;
+  std::vector<i64> f;
+  bool host_ready = true;
   ~eig_lu_s()
   {
     if (ctx) trsv_free(img);
+    if (band) (void)hipFree(band);
   }
 };
 
@@ -218,6 +230,61 @@ void factor_rows(const eig_lu_s &lu, std::vector<i64> &lrp, std::vector<i32> &lc
         uv[at] = lu.Ux[k];
       }
   }
+}
+
+// The exported form from the device band: L rows over the envelope [f_k, k) with the unit diagonal
+// last, U columns over [f_k, k) with the pivot last; exact zeros dropped (the host factor's rule).
+void ensure_host(eig_lu_s &lu)
+{
+  if (lu.host_ready) return;
+  const i64 n = lu.n, nb = (n + 63) / 64;
+  const int gd = lu.band_gd;
+  std::vector<double> h((size_t)nb * (2 * gd + 1) * 4096);
+  EIG_HIP(hipSetDevice(lu.ctx->device));
+  EIG_HIP(hipMemcpyAsync(h.data(), lu.band, h.size() * 8, hipMemcpyDeviceToHost, lu.ctx->stream));
+  EIG_HIP(hipStreamSynchronize(lu.ctx->stream));
+  auto at = [&](i64 r, i64 c) { return h[((size_t)(r >> 6) * (2 * gd + 1) + ((c >> 6) - (r >> 6)) + gd) * 4096 +
+                                         (size_t)(c & 63) * 64 + (r & 63)]; };
+  const std::vector<i64> &f = lu.f;
+  std::vector<i64> Lp(n + 1, 0), Up(n + 1, 0);
+  for (i64 k = 0; k < n; ++k)
+  {
+    i64 cl = 1, cu = 1;
+    for (i64 j = f[k]; j < k; ++j) cl += at(k, j) != 0.0;
+    for (i64 i = f[k]; i < k; ++i) cu += at(i, k) != 0.0;
+    Lp[k + 1] = Lp[k] + cl;
+    Up[k + 1] = Up[k] + cu;
+  }
+  std::vector<i64> Lj(Lp[n]), Ui(Up[n]);
+  std::vector<double> Lx(Lp[n]), Ux(Up[n]);
+  for (i64 k = 0; k < n; ++k)
+  {
+    i64 q = Lp[k];
+    for (i64 j = f[k]; j < k; ++j)
+      if (at(k, j) != 0.0)
+      {
+        Lj[q] = j;
+        Lx[q++] = at(k, j);
+      }
+    Lj[q] = k;
+    Lx[q] = 1.0;
+    q = Up[k];
+    for (i64 i = f[k]; i < k; ++i)
+      if (at(i, k) != 0.0)
+      {
+        Ui[q] = i;
+        Ux[q++] = at(i, k);
+      }
+    Ui[q] = k;
+    Ux[q] = at(k, k);
+  }
+  lu.Lp = std::move(Lp);
+  lu.Lj = std::move(Lj);
+  lu.Lx = std::move(Lx);
+  lu.Up = std::move(Up);
+  lu.Ui = std::move(Ui);
+  lu.Ux = std::move(Ux);
+  lu.host_ready = true;
 }
 
 void build_device(eig_lu_s &lu)
@@ -334,6 +401,66 @@ extern "C" int eig_lu_create_bcsr(eig_ctx_t ctx, int64_t nb_rows, int br, const 
       for (i64 v : adj[perm[k]]) m = std::min(m, inv[v]);
       f[k] = m;
     }
+    // device factorisation (k_band.hip) when the envelope fits a band of at most kBandMaxGD coupled
+    // 64-row blocks: the band LU and the block-inverse image on the GPU, the exported form built
+    // from the band only when asked for (eig_lu_info / _export / _set_solver staged or csr)
+    {
+      i64 gdm = 0;
+      for (i64 k = 0; k < n; ++k) gdm = std::max(gdm, k / 64 - f[k] / 64);
+      const i64 nb = (n + 63) / 64;
+      if (ctx && gdm <= kBandMaxGD && nb * (4 * gdm + 3) <= kBandMaxTiles)
+      {
+        std::vector<i64> rp(n + 1, 0);
+        for (i64 i = 0; i < n; ++i) rp[i + 1] = rp[i] + (i64)rowsA[i].size();
+        std::vector<i32> cj(rp[n]), inv32(n);
+        std::vector<double> cv(rp[n]);
+        for (i64 i = 0; i < n; ++i)
+        {
+          i64 q = rp[i];
+          for (auto &e : rowsA[i])
+          {
+            cj[q] = (i32)e.first;
+            cv[q++] = e.second;
+          }
+          inv32[i] = (i32)inv[i];
+        }
+        phase("csr");
+        auto *lu = new eig_lu_s();
+        try
+        {
+          lu->ctx = ctx;
+          lu->n = n;
+          lu->do_recip = 0;
+          lu->P = perm;
+          lu->Q = perm;
+          lu->f = f;
+          lu->band_gd = (int)gdm;
+          lu->host_ready = false;
+          const bool ok = band_lu_device(ctx, n, (int)gdm, rp, cj, cv, inv32, Rs, lu->img, &lu->band);
+          phase("band");
+          std::vector<double> scale(n);
+          for (i64 k = 0; k < n; ++k) scale[k] = 1.0 / Rs[perm[k]];  // kernels_cpp.hh:683-705
+          lu->Rs = std::move(Rs);
+          if (ok)
+            trsv_attach_perm(ctx, n, lu->P, lu->Q, scale, lu->img);
+          else
+          {
+            // a diagonal tile too ill-conditioned for the block-inverse image: the host image path
+            // (substitution kernels) on the downloaded factors
+            ensure_host(*lu);
+            build_device(*lu);
+          }
+          phase("device");
+        }
+        catch (...)
+        {
+          delete lu;
+          throw;
+        }
+        *out = lu;
+        return;
+      }
+    }
     std::vector<i64> off(n + 1, 0);  // envelope storage: row k of L / column k of U over [f_k, k)
     for (i64 k = 0; k < n; ++k) off[k + 1] = off[k] + (k - f[k]);
     const i64 env = off[n];
@@ -440,6 +567,7 @@ extern "C" int eig_lu_info(eig_lu_t lu, int64_t *n, int64_t *lnz, int64_t *unz, 
 {
   return guard(lu ? lu->ctx : nullptr, [&] {
     EIG_CHECK(lu, EIG_ERR_ARG, "eig_lu_info: null handle");
+    ensure_host(*lu);
     if (n) *n = lu->n;
     if (lnz) *lnz = lu->Lp[lu->n];
     if (unz) *unz = lu->Up[lu->n];
@@ -458,6 +586,7 @@ extern "C" int eig_lu_set_solver(eig_lu_t lu, int kind)
     {
       // the substitution kernels read the row factors, not uploaded next to a block-inverse image
       EIG_HIP(hipSetDevice(lu->ctx->device));
+      ensure_host(*lu);
       std::vector<i64> lrp, urp;
       std::vector<i32> lc, uc;
       std::vector<double> lv, uv, ud;
@@ -488,6 +617,7 @@ extern "C" int eig_lu_export(eig_lu_t lu, int64_t *Lp, int64_t *Lj, double *Lx, 
 {
   return guard(lu ? lu->ctx : nullptr, [&] {
     EIG_CHECK(lu && Lp && Lj && Lx && Up && Ui && Ux && P && Q && Rs, EIG_ERR_ARG, "eig_lu_export: null argument");
+    ensure_host(*lu);
     std::copy(lu->Lp.begin(), lu->Lp.end(), Lp);
     std::copy(lu->Lj.begin(), lu->Lj.end(), Lj);
     std::copy(lu->Lx.begin(), lu->Lx.end(), Lx);

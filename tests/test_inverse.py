@@ -299,3 +299,50 @@ def test_inverse_mv8_kernels(ctx, name, kernel):
     else:
         assert np.array_equal(out, ref_out)
     lu.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["laplace2d_16", "poisson3d_8", "q1elast_4", "neumann2d_12", "laplace2d_100",
+                                  "poisson3d_16", "tiny_5"])
+def test_device_band_factors_match_host(ctx, name):
+    """eig_lu_create_bcsr with a context factors on the device (k_band.hip: band LU of 64 x 64 tiles +
+    the block-inverse image built from the tiles).  Its exported factors carry the host envelope LU's
+    pattern, permutations and scaling exactly and its values to rounding (same no-pivoting
+    elimination, different operation order): 1e-12 of the largest |entry| per factor, the same
+    pattern where no entry cancels exactly.  Rows past n
+    in the last block (laplace2d_100: n = 10000; tiny_5: n = 25 < 64) are identity padding."""
+    A = {"laplace2d_100": lambda: oracle.laplace2d(100), "poisson3d_16": lambda: oracle.poisson3d(16),
+         "tiny_5": lambda: oracle.laplace2d(5)}.get(name, CASES.get(name))()
+    if name.startswith("neumann"):
+        A.val[A.col == np.repeat(np.arange(A.n), np.diff(A.rowptr))] += 0.5
+    host = eigmi.LU.from_bcsr(None, A.rowptr, A.col, A.val, A.br).export()
+    lu = eigmi.LU.from_bcsr(ctx, A.rowptr, A.col, A.val, A.br)
+    used, gl, gu = lu.solver_info()
+    dev = lu.export()
+    for k in ("P", "Q", "Rs"):
+        assert np.array_equal(dev[k], host[k]), k
+    # (entries that cancel to exactly 0.0 in one operation order may be ~1e-17 in the other -- the
+    # 3 x 3 elasticity blocks have such -- so the factors are compared as matrices, not patterns)
+    import scipy.sparse as sp
+    n = A.n
+
+    def mats(d):
+        L = sp.csr_matrix((d["Lx"], d["Lj"], d["Lp"]), shape=(n, n))
+        U = sp.csc_matrix((d["Ux"], d["Ui"], d["Up"]), shape=(n, n))
+        return L, U
+
+    (Ld, Ud), (Lh, Uh) = mats(dev), mats(host)
+    assert abs(Ld - Lh).max() <= 1e-12 * abs(Lh).max()
+    assert abs(Ud - Uh).max() <= 1e-12 * abs(Uh).max()
+    if not name.startswith("q1elast"):
+        for k in ("Lp", "Lj", "Up", "Ui"):
+            assert np.array_equal(dev[k], host[k]), k
+    # the solve on the device-built image vs the reference arithmetic on the exported factors
+    X = oracle.random_mv8(A.n, 8, 5)
+    ref_out, _ = oracle.inverse_mv8(oracle.LU(**dev), X, 8)
+    din, dout = ctx.array(X), ctx.zeros(A.n * 8)
+    lu.inverse_mv8(8, din, dout)
+    err = np.abs(dout.get() - ref_out).max() / np.abs(ref_out).max()
+    print(f"{name}: kernel {used} (coupled {gl}/{gu}), device image vs reference arithmetic {err:.2e}")
+    assert used == "blockinv" and err <= BINV_RTOL
+    lu.close()
