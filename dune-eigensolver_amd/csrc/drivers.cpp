@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <complex>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <string>
@@ -541,7 +542,7 @@ SiBlockShape si_block_shape(int nev, int ncv)
   SiBlockShape g;
   g.nw = (nev + 7) / 8 * 8;
   g.p = std::max(16, g.nw);
-  g.kk = (nev + (nev + 1) / 2 + 7) / 8 * 8;
+  g.kk = std::max((nev + (nev + 1) / 2 + 7) / 8 * 8, 3 * g.p);
   g.cmax = std::max(g.kk + 3 * g.p, (ncv + 7) / 8 * 8);
   return g;
 }
@@ -609,47 +610,36 @@ void shift_invert_block_core(eig_mat_t A, eig_mat_t B, const LuRef &F, double si
   // start block: normal numbers put into the range of OP (dgetv0 for the generalised modes), then
   // B-orthonormalised
   {
-    std::vector<double> h((size_t)p * n);
-    host_random_normal((i64)p * n, seed, h.data());
-    EIG_HIP(hipMemcpyAsync(Wt, h.data(), h.size() * 8, hipMemcpyHostToDevice, s));
+    launch_fill_normal((i64)p * n, seed, Wt, s);
     bmul(Wt, BW, p);
     op(BW, W, p);
-    EIG_HIP(hipStreamSynchronize(s));  // (h)
     EIG_CHECK(bortho(V, BV), EIG_ERR_BREAKDOWN, "shift-invert (block): start block is rank deficient");
   }
-  std::vector<double> T((size_t)cap * cap, 0.0), th, Y, Hh, Ht;
+  std::vector<double> T((size_t)cap * cap, 0.0), th, Y, Hh, Ht, Tc;
   int c = p, nrestart = 0;
   std::vector<int> ord;
   for (;;)
   {
-    // extend: apply OP to the active block V(:, c - p .. c) until the basis holds cmax columns
-    for (;;)
-    {
-      const int a = c - p;
-      EIG_HIP(hipMemcpyAsync(BW, BV + (i64)a * n, (size_t)p * n * 8, hipMemcpyDeviceToDevice, s));
-      op(BW, W, p);
-      Ht.assign((size_t)c * p, 0.0);
-      for (int pass = 0; pass < 2; ++pass)  // CGS2 against V(:, 0 .. c) in the B-inner product
-      {
-        launch_gram_mv8(n, c, p, BV, W, dH, 0, s, ctx->red);
-        for (int i = 0; i < c / 8; ++i) launch_project(n, p, V + (i64)i * 8 * n, W, dH + (size_t)i * 8 * p, s);
-        Hh.resize((size_t)c * p);
-        EIG_HIP(hipMemcpyAsync(Hh.data(), dH, Hh.size() * 8, hipMemcpyDeviceToHost, s));
-        EIG_HIP(hipStreamSynchronize(s));
-        for (size_t k = 0; k < Hh.size(); ++k) Ht[k] += Hh[k];
-      }
-      for (int i = 0; i < c; ++i)
-        for (int j = 0; j < p; ++j) T[(size_t)i * cap + a + j] = T[(size_t)(a + j) * cap + i] = Ht[(size_t)i * p + j];
-      EIG_CHECK(bortho(V + (i64)c * n, BV + (i64)c * n), EIG_ERR_BREAKDOWN,
-                "shift-invert (block): invariant subspace reached (choose another seed or the one-vector solver)");
-      if (c + p > cmax) break;  // V(:, c .. c + p) is the residual block F, Rtot its coupling
-      for (int i = 0; i < p; ++i)
-        for (int j = 0; j < p; ++j)
-          T[(size_t)(c + i) * cap + a + j] = T[(size_t)(a + j) * cap + c + i] = Rtot[(size_t)i * p + j];
-      c += p;
-    }
+    // apply OP to the active block V(:, a .. c), project, B-orthonormalise: F = V(:, c .. c + p)
     const int a = c - p;
-    std::vector<double> Tc((size_t)c * c);
+    EIG_HIP(hipMemcpyAsync(BW, BV + (i64)a * n, (size_t)p * n * 8, hipMemcpyDeviceToDevice, s));
+    op(BW, W, p);
+    Ht.assign((size_t)c * p, 0.0);
+    for (int pass = 0; pass < 2; ++pass)  // CGS2 against V(:, 0 .. c) in the B-inner product
+    {
+      launch_gram_mv8(n, c, p, BV, W, dH, 0, s, ctx->red);
+      for (int i = 0; i < c / 8; ++i) launch_project(n, p, V + (i64)i * 8 * n, W, dH + (size_t)i * 8 * p, s);
+      Hh.resize((size_t)c * p);
+      EIG_HIP(hipMemcpyAsync(Hh.data(), dH, Hh.size() * 8, hipMemcpyDeviceToHost, s));
+      EIG_HIP(hipStreamSynchronize(s));
+      for (size_t k = 0; k < Hh.size(); ++k) Ht[k] += Hh[k];
+    }
+    for (int i = 0; i < c; ++i)
+      for (int j = 0; j < p; ++j) T[(size_t)i * cap + a + j] = T[(size_t)(a + j) * cap + i] = Ht[(size_t)i * p + j];
+    EIG_CHECK(bortho(V + (i64)c * n, BV + (i64)c * n), EIG_ERR_BREAKDOWN,
+              "shift-invert (block): invariant subspace reached (choose another seed or the one-vector solver)");
+    // Rayleigh-Ritz on the c columns, every application: stop as soon as the wanted pairs converged
+    Tc.resize((size_t)c * c);
     for (int i = 0; i < c; ++i)
       for (int j = 0; j < c; ++j) Tc[(size_t)i * c + j] = T[(size_t)i * cap + j];
     sym_eig(c, Tc, th, Y);  // Y[i * c + j]: component i of Ritz vector j
@@ -663,7 +653,7 @@ void shift_invert_block_core(eig_mat_t A, eig_mat_t B, const LuRef &F, double si
       for (int k = i; k < p; ++k) v += Rtot[(size_t)i * p + k] * Y[(size_t)(a + k) * c + j];
       return v;
     };
-    bool conv = true;
+    bool conv = c >= std::min(nev + 1, cmax);
     for (int q = 0; q < nev && conv; ++q)
     {
       double r2 = 0.0;
@@ -674,7 +664,17 @@ void shift_invert_block_core(eig_mat_t A, eig_mat_t B, const LuRef &F, double si
       }
       if (std::sqrt(r2) > tol * std::fabs(th[ord[q]])) conv = false;
     }
-    if (conv || nrestart >= maxit) break;
+    if (conv) break;
+    if (c + p <= cmax)
+    {
+      // F joins the basis: T(c .. c + p, a .. c) = R
+      for (int i = 0; i < p; ++i)
+        for (int j = 0; j < p; ++j)
+          T[(size_t)(c + i) * cap + a + j] = T[(size_t)(a + j) * cap + c + i] = Rtot[(size_t)i * p + j];
+      c += p;
+      continue;
+    }
+    if (nrestart >= maxit) break;
     // thick restart: U = V Y(:, kept), F moves behind it, T = diag(theta_kept) + the coupling C
     {
       std::vector<double> Ysel((size_t)c * kk);

@@ -310,6 +310,7 @@ void launch_nrm2sq(i64 n, const double *x, double *out, int ticket, hipStream_t 
 void launch_axpy(i64 n, double a, const double *x, double *y, hipStream_t s);
 void launch_axpy_dev(i64 n, const double *a, double scale, const double *x, double *y, hipStream_t s);
 void launch_scal(i64 n, double a, double *x, hipStream_t s);
+void launch_fill_normal(i64 n, unsigned seed, double *x, hipStream_t s);  // counter-based N(0, 1)
 void launch_stream_copy(i64 n, const double *x, double *y, int num_cu, hipStream_t s, int mode);
 void launch_scal_dev(i64 n, const double *a, bool reciprocal_sqrt, double *x, hipStream_t s);
 void launch_sqrt_inplace(double *v, int count, hipStream_t s);

@@ -130,6 +130,31 @@ void launch_axpy_dev(i64 n, const double *a, double scale, const double *x, doub
   hipLaunchKernelGGL(k_axpy, dim3(stream_grid(n, 4)), dim3(kStreamThreads), 0, s, n, 0.0, a, scale, x, y);
 }
 
+// x[i] = standard normal numbers from a counter-based generator (splitmix64 of (seed, i), Box-Muller):
+// start blocks of the block Krylov drivers, generated where they are used
+__device__ __forceinline__ unsigned long long splitmix64(unsigned long long z)
+{
+  z += 0x9e3779b97f4a7c15ull;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+__global__ __launch_bounds__(kStreamThreads) void k_fill_normal(i64 n, unsigned long long seed, double *__restrict__ x)
+{
+  for (i64 i = (i64)blockIdx.x * kStreamThreads + threadIdx.x; i < n; i += (i64)gridDim.x * kStreamThreads)
+  {
+    const unsigned long long a = splitmix64(seed ^ splitmix64(2 * (unsigned long long)i));
+    const unsigned long long b = splitmix64(seed ^ splitmix64(2 * (unsigned long long)i + 1));
+    const double u1 = ((double)(a >> 11) + 0.5) * 0x1.0p-53, u2 = (double)(b >> 11) * 0x1.0p-53;
+    x[i] = sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
+  }
+}
+void launch_fill_normal(i64 n, unsigned seed, double *x, hipStream_t s)
+{
+  hipLaunchKernelGGL(k_fill_normal, dim3(stream_grid(n, 1)), dim3(kStreamThreads), 0, s, n,
+                     0x5eedull * 0x100000001ull + (unsigned long long)seed, x);
+}
+
 // x *= a ; or x *= 1/sqrt(*a_dev) (normalise by a device-resident squared norm)
 __global__ __launch_bounds__(kStreamThreads) void k_scal(i64 n, double a, const double *a_dev, int rsqrt_mode,
                                                          double *__restrict__ x)
