@@ -62,7 +62,7 @@ __global__ __launch_bounds__(64) void k_band_pad(i64 n, int gd, double *band)
 // One block step's panels.  Workgroup w < G (G = max(gd, 1)): tall panel [D; A(b+1+w, b)];
 // w >= G: wide panel [D, A(b, b+1+w-G)].  Threads 0..63 hold row t of D in registers, threads
 // 64..127 row t-64 of the tall tile or column t-64 of the wide tile.  Elimination step k (unrolled:
-// every register index is static): the rows below k take the multiplier l = v[k] / p(k) against
+// every register index is static): the rows below k take the multiplier l = v[k] (1 / p(k)) against
 // the pivot row p published in LDS, store it in v[k] and subtract l p from their columns > k; the
 // wide tile's columns apply the previous step's multipliers (x_i -= l_i x_(k-1), i >= k: the
 // forward substitution with L_bb, one step behind); the row that becomes the next pivot publishes
@@ -75,6 +75,7 @@ __global__ __launch_bounds__(kPanelThreads) void k_band_panel(i64 b, i64 nb, int
 {
   __shared__ double prow[2][kB];
   __shared__ double lcol[2][kB];
+  __shared__ double prcp[2];  // 1 / pivot
   const int G = gd > 0 ? gd : 1;
   const int w = blockIdx.x, t = threadIdx.x;
   const bool tall = w < G;
@@ -107,6 +108,7 @@ __global__ __launch_bounds__(kPanelThreads) void k_band_panel(i64 b, i64 nb, int
   {
 #pragma unroll
     for (int c = 0; c < kB; ++c) prow[0][c] = v[c];
+    prcp[0] = 1.0 / v[0];
   }
   __syncthreads();
 #pragma unroll
@@ -115,17 +117,18 @@ __global__ __launch_bounds__(kPanelThreads) void k_band_panel(i64 b, i64 nb, int
     const double *pr = prow[k & 1];
     if ((drow && q > k) || xrow)
     {
-      const double l = v[k] / pr[k];
+      const double l = v[k] * prcp[k & 1];
       v[k] = l;
 #pragma unroll
-      for (int c = k + 1; c < kB; ++c) v[c] -= l * pr[c];
+      for (int c = k + 1; c < kB; ++c) v[c] = fma(-l, pr[c], v[c]);
       if (drow)
       {
         lcol[k & 1][q] = l;
         if (q == k + 1)
         {
 #pragma unroll
-          for (int c = 0; c < kB; ++c) prow[(k + 1) & 1][c] = v[c];
+          for (int c = k + 1; c < kB; ++c) prow[(k + 1) & 1][c] = v[c];
+          prcp[(k + 1) & 1] = 1.0 / v[k + 1];
         }
       }
     }
@@ -134,7 +137,7 @@ __global__ __launch_bounds__(kPanelThreads) void k_band_panel(i64 b, i64 nb, int
       const double *lc = lcol[(k - 1) & 1];
       const double xk = v[k - 1];
 #pragma unroll
-      for (int i = k; i < kB; ++i) v[i] -= lc[i] * xk;
+      for (int i = k; i < kB; ++i) v[i] = fma(-lc[i], xk, v[i]);
     }
     if (w == 0 && t == 0)
     {
