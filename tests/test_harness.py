@@ -107,3 +107,15 @@ def test_mgs_performance_row(ini):
     out = run(ini, "-run", "mgs")
     row = [l for l in out.splitlines() if l.startswith("P_n_m_i_iblocked_perfn_perfb_perfv")][0].split()[1:]
     assert row[:3] == ["1", "2000", "16"] and all(float(x) > 0 for x in row[3:])
+
+
+@pytest.mark.gpu
+def test_smallest_reference_default_size(ini):
+    """The smallest-eigenvalue experiment at the reference's default size (src/dune-eigensolver.ini:
+    ev.N = 200, n = 40000): GeneralizedInverse and the shift-invert (ARPACK-mode) solve of the GenEO
+    pencil on device-factored LU (k_band.hip) agree, and ARPACK-mode at tol with itself at 1e-14."""
+    out = run(ini, "-run", "smallest", "-ev.N", "200", "-ev.tol", "1e-8")
+    row = [l for l in out.splitlines() if l.startswith("N_M_TOL_RASERROR_ARPERROR_TIMERATIO_ARPACKITER")][0]
+    f = [float(x) for x in row.split(" ", 1)[1].replace("\\\\", "").split("&")]
+    assert int(f[0]) == 40000 and int(f[1]) == 4
+    assert f[3] < 1e-6 and f[4] < 1e-6

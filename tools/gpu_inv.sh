@@ -1,10 +1,10 @@
-#!/bin/bash
-# Inverse-row check on one GPU: the factor-apply / inverse-driver tests, the INV bench lines with
-# the default (block-inverse) and the bitwise staged kernel, and a kernel trace of the default.
-set -e
-mkdir -p gpurun_out/inv
-export PYTHONPATH=$PWD/dune-eigensolver_amd:$PWD:$PYTHONPATH
-timeout -k 10 300 python -u -m pytest -x -v -s --timeout 120 --timeout-method thread -m gpu tests/test_inverse.py tests/test_shift_invert.py > gpurun_out/inv/pytest.log 2>&1
-timeout -k 10 200 python -u tools/bench_configs.py inv > gpurun_out/inv/default.jsonl 2> gpurun_out/inv/default.err
-cd /tmp && export TMPDIR=/tmp
-timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/inv/prof -o inv -- python3 $GRAFT_REPO_ROOT/tools/bench_configs.py inv > $GRAFT_REPO_ROOT/gpurun_out/inv/prof.log 2>&1
+# INV rows (tools/bench_configs.py inv) at 64^2 and the reference's default 200^2, and the harness
+# smallest experiment at ev.N = 200
+set -o pipefail
+O=gpurun_out/inv
+mkdir -p $O
+timeout -k 10 300 python -u -m pytest tests/test_harness.py -x -v -m gpu --timeout 200 --timeout-method thread > $O/harness.log 2>&1 || { tail -30 $O/harness.log; exit 1; }
+tail -2 $O/harness.log
+EIGMI_INV_N=64 timeout -k 10 300 python -u tools/bench_configs.py inv > $O/inv64.jsonl 2> $O/inv64.err || { tail $O/inv64.err; exit 1; }
+EIGMI_INV_N=200 timeout -k 10 600 python -u tools/bench_configs.py inv > $O/inv200.jsonl 2> $O/inv200.err || { tail $O/inv200.err; exit 1; }
+cat $O/inv64.jsonl $O/inv200.jsonl
