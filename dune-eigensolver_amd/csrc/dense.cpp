@@ -392,9 +392,13 @@ bool hess_eigvals(int n, std::vector<double> &a, std::vector<std::complex<double
   return true;
 }
 
-// Eigenvector of the real matrix g (row-major n x n) for the eigenvalue theta.
+// Eigenvector of the real matrix g (row-major n x n) for the eigenvalue theta, orthogonal to the
+// vectors `defl` (eigenvectors already found for the same eigenvalue: a multiple eigenvalue gets
+// independent vectors of its eigenspace -- otherwise inverse iteration returns the same vector each
+// time and the Krylov-Schur restart basis would not span an invariant subspace).
 void inverse_iteration(int n, const std::vector<double> &g, std::complex<double> theta,
-                       std::vector<std::complex<double>> &y)
+                       std::vector<std::complex<double>> &y,
+                       const std::vector<const std::vector<std::complex<double>> *> &defl = {})
 {
   typedef std::complex<double> C;
   double gn = 0.0;
@@ -435,6 +439,13 @@ void inverse_iteration(int n, const std::vector<double> &g, std::complex<double>
       for (int k = i + 1; k < n; ++k) y[i] -= M[(size_t)i * n + k] * y[k];
       y[i] /= M[(size_t)i * n + i];
     }
+    for (int pass = 0; pass < 2; ++pass)
+      for (const auto *x : defl)
+      {
+        C d = 0.0;
+        for (int i = 0; i < n; ++i) d += std::conj((*x)[i]) * y[i];
+        for (int i = 0; i < n; ++i) y[i] -= d * (*x)[i];
+      }
     double nrm = 0.0;
     int big = 0;
     for (int i = 0; i < n; ++i)
@@ -457,16 +468,23 @@ bool gen_eig(int n, const std::vector<double> &g, std::vector<std::complex<doubl
   hess_reduce(n, h);
   if (!hess_eigvals(n, h, w)) return false;
   Y.assign((size_t)n * n, 0.0);
-  std::vector<std::complex<double>> y;
+  double wmax = 0.0;
+  for (const auto &v : w) wmax = std::max(wmax, std::abs(v));
+  std::vector<std::vector<std::complex<double>>> found(n);
   for (int j = 0; j < n; ++j)
   {
     if (j > 0 && w[j].imag() != 0.0 && w[j] == std::conj(w[j - 1]))
     {
-      for (int i = 0; i < n; ++i) Y[(size_t)i * n + j] = std::conj(Y[(size_t)i * n + j - 1]);
+      found[j].resize(n);
+      for (int i = 0; i < n; ++i) found[j][i] = Y[(size_t)i * n + j] = std::conj(Y[(size_t)i * n + j - 1]);
       continue;
     }
-    inverse_iteration(n, g, w[j], y);
-    for (int i = 0; i < n; ++i) Y[(size_t)i * n + j] = y[i];
+    // the vectors of (numerically) the same eigenvalue found so far
+    std::vector<const std::vector<std::complex<double>> *> defl;
+    for (int i = 0; i < j; ++i)
+      if (std::abs(w[i] - w[j]) <= 1e-10 * wmax) defl.push_back(&found[i]);
+    inverse_iteration(n, g, w[j], found[j], defl);
+    for (int i = 0; i < n; ++i) Y[(size_t)i * n + j] = found[j][i];
   }
   return true;
 }

@@ -265,7 +265,15 @@ int main(int argc, char **argv)
     auto Fu = eigmi::Factorization::from_umfpack(ctx, u);
     MV8 R2 = Rc, Z2(n16, 8);
     eigmi::matmul_inverse_tallskinny_blocked(Z2, Fu, R2);
-    EXPECT(std::memcmp(Z2.p.data(), Z.p.data(), Z.p.size() * 8) == 0);
+    // (F's block-inverse image was built on the device from its band factors, Fu's on the host
+    // from the exported arrays: the same factors, images that round differently)
+    double zmax = 0.0, zd = 0.0;
+    for (std::size_t q = 0; q < Z.p.size(); ++q)
+    {
+      zmax = std::max(zmax, std::fabs(Z.p[q]));
+      zd = std::max(zd, std::fabs(Z2.p[q] - Z.p[q]));
+    }
+    EXPECT(zd <= 1e-13 * zmax);
   }
   bool threw2 = false;
   try
@@ -333,7 +341,16 @@ int main(int argc, char **argv)
       std::vector<double> ln(4);
       if (mode == 0) eigmi::computeStdNonSymMinMagnitude(dA16, dI16, 1e-13, xs, ln, 0.0);
       else eigmi::computeGenNonSymShiftInvertMinMagnitude(dA16, dI16, 1e-13, xs, ln, 0.0);
-      for (int i = 0; i < 4; ++i) EXPECT(std::fabs(ln[i] - exact[i]) < 1e-10);
+      // a one-vector Krylov space holds ONE vector of a multiple eigenspace in exact arithmetic (the
+      // Laplacian's lambda_2 = lambda_3); the second copy enters through rounding alone (in ARPACK
+      // too), so only the simple leading values and membership in the spectrum are required
+      EXPECT(std::fabs(ln[0] - exact[0]) < 1e-10 && std::fabs(ln[1] - exact[1]) < 1e-10);
+      for (int i = 0; i < 4; ++i)
+      {
+        double dmin = 1e300;
+        for (double e : exact) dmin = std::min(dmin, std::fabs(ln[i] - e));
+        EXPECT(dmin < 1e-10);
+      }
     }
   }
 
