@@ -292,7 +292,7 @@ def test_inverse_mv8_kernels(ctx, name, kernel):
         din, dout = ctx.array(X), ctx.zeros(A.n * 16)
         lu.inverse_mv8(16, din, dout)
     out = dout.get()
-    if kernel is None:
+    if kernel in (None, "blockinv_mfma"):
         err = np.abs(out - ref_out).max() / np.abs(ref_out).max()
         print(f"{name}: default solve vs reference arithmetic {err:.2e}")
         assert err <= BINV_RTOL
