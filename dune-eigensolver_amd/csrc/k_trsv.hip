@@ -521,131 +521,6 @@ __global__ __launch_bounds__(kThreadsT) void k_binv_chain(i64 n, int gd, const d
   }
 }
 
-// k_binv_chain_mfma: the same chain with the block products on the matrix cores.  Per 64-row block
-// x_b = z_b - sum_d G(b, d) x_(b -+ d) is 4 row tiles (16 rows) x 64-row k-range per coupled tile;
-// wave w takes row tile w & 3 and the coupled tiles d = h, h + 2, ... (h = w >> 2), 16
-// v_mfma_f64_16x16x4f64 per tile: A = the G tile (lane l: row 16 rt + (l & 15), t = 4 ks + (l >> 4),
-// one coalesced 128-B segment per 16 lanes), B = the solved x of block b -+ (d + 1) from the LDS ring
-// (row t, column l & 15; columns 8..15 are zero: one 8-column block per workgroup), accumulator
-// C[row (l >> 4) + 4 q][column l & 15] in register q.  The two k-halves meet in LDS, the h = 0 waves
-// form x = z - C, store it and put it in the ring; two barriers per block.  Per lane the k-loop reads
-// ONE x value per 16 multiply-adds (the vector kernel above: one LDS broadcast per multiply-add, which
-// made the CU's LDS pipe its bound).  G tiles and z of the next PF blocks are prefetched in registers.
-typedef double d4t __attribute__((ext_vector_type(4)));
-template <bool LOWER, int GD, int PF>
-__global__ __launch_bounds__(kThreadsT) void k_binv_chain_mfma(i64 n, int gd, const double *__restrict__ G,
-                                                               const double *Z, double *X)
-{
-  constexpr int RING = 8;  // >= GD: a source slot is read before the block's own x is written
-  constexpr int NT = (GD + 1) / 2;
-  static_assert(RING >= GD, "ring slots");
-  __shared__ double ring[RING][kTB][8];
-  __shared__ double part[4][4][64];
-  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
-  const int rt = w & 3, h = w >> 2, i16 = l & 15, k4 = l >> 4;
-  const i64 cb = (i64)blockIdx.x * n * 8;
-  const i64 nblocks = (n + kTB - 1) / kTB;
-  for (int e = tid; e < RING * kTB * 8; e += kThreadsT) (&ring[0][0][0])[e] = 0.0;
-  double ga[PF][NT][16], pz[PF][4];
-  auto fetch_g = [&](i64 bi, double (&g)[NT][16]) {
-    const i64 bc = bi < nblocks ? bi : nblocks - 1;
-    const i64 blk = LOWER ? bc : nblocks - 1 - bc;
-    const double *gb = G + blk * gd * (kTB * kTB);
-#pragma unroll
-    for (int tt = 0; tt < NT; ++tt)
-    {
-      const int d = 2 * tt + h;
-      const int dd = d < gd ? d : 0;  // (gd = 0: the one-tile placeholder buffer)
-#pragma unroll
-      for (int ks = 0; ks < 16; ++ks) g[tt][ks] = gld(gb + dd * (kTB * kTB) + (4 * ks + k4) * kTB + 16 * rt + i16);
-    }
-  };
-  auto fetch_z = [&](i64 bi, double (&z)[4]) {
-    const i64 bc = bi < nblocks ? bi : nblocks - 1;
-    const i64 blk = LOWER ? bc : nblocks - 1 - bc;
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-    {
-      const i64 i = blk * kTB + 16 * rt + k4 + 4 * q;
-      z[q] = gld(Z + cb + (i < n ? i : n - 1) * 8 + (i16 & 7));
-    }
-  };
-#pragma unroll
-  for (int p = 0; p < PF; ++p)
-  {
-    fetch_g(p, ga[p]);
-    fetch_z(p, pz[p]);
-  }
-  __builtin_amdgcn_s_waitcnt(0);
-  __syncthreads();
-  const i64 nround = (nblocks + PF - 1) / PF * PF;
-  for (i64 b0 = 0; b0 < nround; b0 += PF)
-  {
-#pragma unroll
-    for (int p = 0; p < PF; ++p)
-    {
-      const i64 bi = b0 + p;
-      const bool live = bi < nblocks;
-      const i64 blk = LOWER ? bi : nblocks - 1 - bi;
-      d4t acc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int tt = 0; tt < NT; ++tt)
-      {
-        const int d = 2 * tt + h;
-        if (d < gd && d < bi)  // (wave-uniform) block blk -+ (d + 1) exists and is solved
-        {
-          const i64 src = LOWER ? blk - (d + 1) : blk + (d + 1);
-          const double(*xr)[8] = ring[src & (RING - 1)];
-#pragma unroll
-          for (int ks = 0; ks < 16; ++ks)
-          {
-            const double xv = xr[4 * ks + k4][i16 & 7];
-            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(ga[p][tt][ks], i16 < 8 ? xv : 0.0, acc, 0, 0, 0);
-          }
-        }
-      }
-      fetch_g(bi + PF, ga[p]);  // the tiles of the block PF ahead
-      if (h == 1)
-      {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) part[rt][q][l] = acc[q];
-      }
-      __syncthreads();
-      if (h == 0)
-      {
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-        {
-          const int row = 16 * rt + k4 + 4 * q;
-          const i64 i = blk * kTB + row;
-          const bool own = live && i < n;
-          const double x = (own ? pz[p][q] : 0.0) - (acc[q] + part[rt][q][l]);
-          if (i16 < 8)
-          {
-            ring[blk & (RING - 1)][row][i16] = x;
-            if (own) gst(X + cb + i * 8 + i16, x);
-          }
-        }
-      }
-      fetch_z(bi + PF, pz[p]);
-      __syncthreads();
-    }
-  }
-}
-
-template <bool LOWER>
-void launch_binv_chain_mfma(int gd, int nblk, i64 n, const double *G, const double *Z, double *X, hipStream_t s)
-{
-  if (gd <= 1)
-    hipLaunchKernelGGL((k_binv_chain_mfma<LOWER, 1, 2>), dim3(nblk), dim3(kThreadsT), 0, s, n, gd, G, Z, X);
-  else if (gd == 2)
-    hipLaunchKernelGGL((k_binv_chain_mfma<LOWER, 2, 2>), dim3(nblk), dim3(kThreadsT), 0, s, n, gd, G, Z, X);
-  else if (gd <= 4)
-    hipLaunchKernelGGL((k_binv_chain_mfma<LOWER, 4, 2>), dim3(nblk), dim3(kThreadsT), 0, s, n, gd, G, Z, X);
-  else
-    hipLaunchKernelGGL((k_binv_chain_mfma<LOWER, 8, 1>), dim3(nblk), dim3(kThreadsT), 0, s, n, gd, G, Z, X);
-}
-
 template <bool LOWER>
 void launch_binv_chain(int gd, int nblk, i64 n, const double *G, const double *Z, double *X, hipStream_t s)
 {
@@ -1072,17 +947,11 @@ void launch_inverse_mv8(TrsvImage &img, i64 m, double *Qin, double *Qout, hipStr
     const i64 nblocks = (n + kTB - 1) / kTB;
     hipLaunchKernelGGL(k_binv_z<true>, dim3((unsigned)nblocks, nblk), dim3(kThreadsT), 0, s, n, (const double *)img.dinv[0],
                        (const i32 *)img.P, (const double *)img.scale, (const double *)Qin, Qout);
-    if (img.solver == EIG_TRSV_BLOCKINV_MFMA)
-      launch_binv_chain_mfma<true>(img.gd[0], nblk, n, img.g[0], Qout, Qin, s);
-    else
-      launch_binv_chain<true>(img.gd[0], nblk, n, img.g[0], Qout, Qin, s);
+    launch_binv_chain<true>(img.gd[0], nblk, n, img.g[0], Qout, Qin, s);
     hipLaunchKernelGGL(k_binv_z<false>, dim3((unsigned)nblocks, nblk), dim3(kThreadsT), 0, s, n,
                        (const double *)img.dinv[1], (const i32 *)nullptr, (const double *)nullptr, (const double *)Qin,
                        Qout);
-    if (img.solver == EIG_TRSV_BLOCKINV_MFMA)
-      launch_binv_chain_mfma<false>(img.gd[1], nblk, n, img.g[1], Qout, Qin, s);
-    else
-      launch_binv_chain<false>(img.gd[1], nblk, n, img.g[1], Qout, Qin, s);
+    launch_binv_chain<false>(img.gd[1], nblk, n, img.g[1], Qout, Qin, s);
     hipLaunchKernelGGL(k_perm_out, dim3(grid256(n * nblk)), dim3(256), 0, s, n, nblk, img.Q, Qin, Qout);
     EIG_HIP(hipGetLastError());
     return;

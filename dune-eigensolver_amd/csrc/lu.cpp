@@ -579,8 +579,8 @@ extern "C" int eig_lu_set_solver(eig_lu_t lu, int kind)
 {
   return guard(lu ? lu->ctx : nullptr, [&] {
     EIG_CHECK(lu, EIG_ERR_ARG, "eig_lu_set_solver: null handle");
-    EIG_CHECK(kind >= EIG_TRSV_AUTO && kind <= EIG_TRSV_BLOCKINV_MFMA, EIG_ERR_ARG, "eig_lu_set_solver: unknown solver");
-    EIG_CHECK((kind != EIG_TRSV_BLOCKINV && kind != EIG_TRSV_BLOCKINV_MFMA) || !lu->ctx || lu->img.binv, EIG_ERR_ARG,
+    EIG_CHECK(kind >= EIG_TRSV_AUTO && kind <= EIG_TRSV_CSR, EIG_ERR_ARG, "eig_lu_set_solver: unknown solver");
+    EIG_CHECK(kind != EIG_TRSV_BLOCKINV || !lu->ctx || lu->img.binv, EIG_ERR_ARG,
               "eig_lu_set_solver: these factors have no block-inverse image");
     if ((kind == EIG_TRSV_STAGED || kind == EIG_TRSV_CSR) && lu->ctx && !lu->img.rows)
     {
@@ -604,7 +604,7 @@ extern "C" int eig_lu_solver_info(eig_lu_t lu, int *kind, int *coupled_l, int *c
     const TrsvImage &im = lu->img;
     const bool csr = im.solver == EIG_TRSV_CSR, staged = im.solver == EIG_TRSV_STAGED;
     if (kind)
-      *kind = (im.binv && !csr && !staged) ? (im.solver == EIG_TRSV_BLOCKINV_MFMA ? EIG_TRSV_BLOCKINV_MFMA : EIG_TRSV_BLOCKINV)
+      *kind = (im.binv && !csr && !staged) ? EIG_TRSV_BLOCKINV
               : (im.staged && !csr && (im.host || im.staged_built)) ? EIG_TRSV_STAGED
                                                                     : EIG_TRSV_CSR;
     if (coupled_l) *coupled_l = im.gd[0];

@@ -20,9 +20,8 @@ ORTHO_GRID = 0x100  # or-ed into the variant: grid-wide MGS passes even for bloc
 # matrix kernel-image flags (eig_mat_create_bcsr_ex)
 MAT_NO_BAND, MAT_BAND_GATHER, MAT_NO_STENCIL, MAT_NO_MARCH, MAT_NO_CLASS = 1, 2, 4, 8, 16
 # triangular-solve kernels of an LU (eig_lu_set_solver)
-TRSV_AUTO, TRSV_BLOCKINV, TRSV_STAGED, TRSV_CSR, TRSV_BLOCKINV_MFMA = 0, 1, 2, 3, 4
-TRSV_KINDS = {None: TRSV_AUTO, "auto": TRSV_AUTO, "blockinv": TRSV_BLOCKINV, "staged": TRSV_STAGED, "csr": TRSV_CSR,
-              "blockinv_mfma": TRSV_BLOCKINV_MFMA}
+TRSV_AUTO, TRSV_BLOCKINV, TRSV_STAGED, TRSV_CSR = 0, 1, 2, 3
+TRSV_KINDS = {None: TRSV_AUTO, "auto": TRSV_AUTO, "blockinv": TRSV_BLOCKINV, "staged": TRSV_STAGED, "csr": TRSV_CSR}
 COMM_MAILBOX = 1
 STREAM_COPY_MODE = 3  # eig_stream_copy_timed: nontemporal, full grid -- 6.70 TB/s vs 6.28 plain (tools/copy_sweep.py)
 WHICH_LA, WHICH_SA = 0, 1
@@ -651,8 +650,7 @@ class LU:
         """-> (kernel in use: "blockinv" | "staged" | "csr", coupled blocks of L, of U)."""
         k, gl, gu = _int(0), _int(0), _int(0)
         self._check(lib.eig_lu_solver_info(self.h, ctypes.byref(k), ctypes.byref(gl), ctypes.byref(gu)))
-        return {TRSV_BLOCKINV: "blockinv", TRSV_STAGED: "staged", TRSV_CSR: "csr",
-                TRSV_BLOCKINV_MFMA: "blockinv_mfma"}[k.value], gl.value, gu.value
+        return {TRSV_BLOCKINV: "blockinv", TRSV_STAGED: "staged", TRSV_CSR: "csr"}[k.value], gl.value, gu.value
 
     def set_solver(self, kind):
         """kind: None / "auto", "blockinv", "staged" or "csr" (eig_lu_set_solver)."""

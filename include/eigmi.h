@@ -330,9 +330,7 @@ int eig_lu_info(eig_lu_t lu, int64_t *n, int64_t *lnz, int64_t *unz, int *do_rec
  * substitution).  EIG_TRSV_STAGED and EIG_TRSV_CSR are bitwise the reference arithmetic
  * (matmul_inverse_tallskinny_blocked, kernels_cpp.hh:660-755); the block-inverse solve agrees to
  * rounding. */
-enum { EIG_TRSV_AUTO = 0, EIG_TRSV_BLOCKINV = 1, EIG_TRSV_STAGED = 2, EIG_TRSV_CSR = 3, EIG_TRSV_BLOCKINV_MFMA = 4 };
-/* EIG_TRSV_BLOCKINV_MFMA: the block-inverse solve with the chain's block products on the matrix
- * cores (v_mfma_f64_16x16x4f64; same image, same tolerance as EIG_TRSV_BLOCKINV). */
+enum { EIG_TRSV_AUTO = 0, EIG_TRSV_BLOCKINV = 1, EIG_TRSV_STAGED = 2, EIG_TRSV_CSR = 3 };
 int eig_lu_set_solver(eig_lu_t lu, int kind);
 /* The kernels eig_inverse_mv8 runs now (*kind: EIG_TRSV_BLOCKINV / _STAGED / _CSR) and the coupled
  * 64-row blocks of the L / U envelopes (the block-inverse chain takes up to 8). */
