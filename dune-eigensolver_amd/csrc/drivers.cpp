@@ -638,7 +638,17 @@ void shift_invert_block_core(eig_mat_t A, eig_mat_t B, const LuRef &F, double si
       for (int j = 0; j < p; ++j) T[(size_t)i * cap + a + j] = T[(size_t)(a + j) * cap + i] = Ht[(size_t)i * p + j];
     EIG_CHECK(bortho(V + (i64)c * n, BV + (i64)c * n), EIG_ERR_BREAKDOWN,
               "shift-invert (block): invariant subspace reached (choose another seed or the one-vector solver)");
-    // Rayleigh-Ritz on the c columns, every application: stop as soon as the wanted pairs converged
+    // Rayleigh-Ritz on the c columns: at the end of the first cycle, then after every application
+    // (stop as soon as the wanted pairs converged).  Inside the first cycle the wanted pairs have not
+    // converged in any run seen, and the host eigen-solve of T costs O(c^3) (~1-2 ms at c = 64-96).
+    if (nrestart == 0 && c + p <= cmax)
+    {
+      for (int i = 0; i < p; ++i)
+        for (int j = 0; j < p; ++j)
+          T[(size_t)(c + i) * cap + a + j] = T[(size_t)(a + j) * cap + c + i] = Rtot[(size_t)i * p + j];
+      c += p;
+      continue;
+    }
     Tc.resize((size_t)c * c);
     for (int i = 0; i < c; ++i)
       for (int j = 0; j < c; ++j) Tc[(size_t)i * c + j] = T[(size_t)i * cap + j];
