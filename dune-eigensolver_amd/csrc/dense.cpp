@@ -28,6 +28,11 @@ void tridiag_eig(int k, std::vector<double> &d, std::vector<double> e, std::vect
   }
   e.resize(k, 0.0);
   if (k > 0) e[k - 1] = 0.0;
+  // the rotations act on pairs of columns of Z: work on Zt = Z^T (row i of Zt = column i of Z), so
+  // each rotation updates two contiguous rows (the column-strided form was cache-bound at k ~ 100)
+  std::vector<double> Zt((size_t)k * k);
+  for (int q = 0; q < k; ++q)
+    for (int i = 0; i < k; ++i) Zt[(size_t)i * k + q] = Z[(size_t)q * k + i];
   const double eps = 2.220446049250313e-16;
   for (int l = 0; l < k; ++l)
   {
@@ -63,11 +68,12 @@ void tridiag_eig(int k, std::vector<double> &d, std::vector<double> e, std::vect
           r = (d[i] - g) * s + 2.0 * c * b;
           d[i + 1] = g + (p = s * r);
           g = c * r - b;
+          double *__restrict__ zi = &Zt[(size_t)i * k], *__restrict__ zi1 = &Zt[(size_t)(i + 1) * k];
           for (int q = 0; q < k; ++q)
           {
-            f = Z[(size_t)q * k + i + 1];
-            Z[(size_t)q * k + i + 1] = s * Z[(size_t)q * k + i] + c * f;
-            Z[(size_t)q * k + i] = c * Z[(size_t)q * k + i] - s * f;
+            const double fz = zi1[q];
+            zi1[q] = s * zi[q] + c * fz;
+            zi[q] = c * zi[q] - s * fz;
           }
         }
         if (r == 0.0 && i >= l) continue;
@@ -81,14 +87,14 @@ void tridiag_eig(int k, std::vector<double> &d, std::vector<double> e, std::vect
   std::vector<int> idx(k);
   std::iota(idx.begin(), idx.end(), 0);
   std::sort(idx.begin(), idx.end(), [&](int a, int b) { return d[a] < d[b]; });
-  std::vector<double> d2(k), Z2((size_t)k * k);
+  std::vector<double> d2(k);
   for (int j = 0; j < k; ++j)
   {
     d2[j] = d[idx[j]];
-    for (int q = 0; q < k; ++q) Z2[(size_t)q * k + j] = Z[(size_t)q * k + idx[j]];
+    const double *zc = &Zt[(size_t)idx[j] * k];
+    for (int q = 0; q < k; ++q) Z[(size_t)q * k + j] = zc[q];
   }
   d.swap(d2);
-  Z.swap(Z2);
 }
 
 
@@ -98,6 +104,25 @@ void tridiag_eig(int k, std::vector<double> &d, std::vector<double> e, std::vect
 // accumulated reflectors.  Reflector k: v zeroes A[k+2.., k]; the trailing block is updated as
 // A <- A - v w^T - w v^T with p = tau A v, w = p - (tau/2)(v^T p) v, tau = 2 / v^T v.
 // ---------------------------------------------------------------------------------------------
+namespace {
+// sum_j a[j] b[j] with 4 independent partial sums (vectorisable; the strict-order single
+// accumulator kept these O(n^3) loops scalar)
+inline double dot4(const double *a, const double *b, int m)
+{
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+  int j = 0;
+  for (; j + 4 <= m; j += 4)
+  {
+    s0 += a[j] * b[j];
+    s1 += a[j + 1] * b[j + 1];
+    s2 += a[j + 2] * b[j + 2];
+    s3 += a[j + 3] * b[j + 3];
+  }
+  for (; j < m; ++j) s0 += a[j] * b[j];
+  return (s0 + s1) + (s2 + s3);
+}
+}  // namespace
+
 void householder_tridiag(int n, std::vector<double> A, std::vector<double> &d, std::vector<double> &e,
                          std::vector<double> &Q)
 {
@@ -120,13 +145,7 @@ void householder_tridiag(int n, std::vector<double> A, std::vector<double> &d, s
     for (int i = 0; i < m; ++i) vv += v[i] * v[i];
     if (vv == 0.0) continue;  // column already reduced
     const double tau = 2.0 / vv;
-    for (int i = 0; i < m; ++i)
-    {
-      double s = 0.0;
-      const double *row = &A[(size_t)(k + 1 + i) * n + k + 1];
-      for (int j = 0; j < m; ++j) s += row[j] * v[j];
-      p[i] = tau * s;
-    }
+    for (int i = 0; i < m; ++i) p[i] = tau * dot4(&A[(size_t)(k + 1 + i) * n + k + 1], v.data(), m);
     double vp = 0.0;
     for (int i = 0; i < m; ++i) vp += v[i] * p[i];
     for (int i = 0; i < m; ++i) w[i] = p[i] - 0.5 * tau * vp * v[i];
@@ -142,9 +161,7 @@ void householder_tridiag(int n, std::vector<double> A, std::vector<double> &d, s
     for (int r = 0; r < n; ++r)
     {
       double *qr = &Q[(size_t)r * n + k + 1];
-      double s = 0.0;
-      for (int j = 0; j < m; ++j) s += qr[j] * v[j];
-      s *= tau;
+      const double s = tau * dot4(qr, v.data(), m);
       for (int j = 0; j < m; ++j) qr[j] -= s * v[j];
     }
   }
