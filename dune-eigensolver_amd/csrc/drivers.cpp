@@ -557,6 +557,8 @@ void shift_invert_block_core(eig_mat_t A, eig_mat_t B, const LuRef &F, double si
   const SiBlockShape g = si_block_shape(nev, ncv);
   const int p = g.p, kk = g.kk, cmax = g.cmax, cap = cmax + p;
   EIG_CHECK(nev < n && cap <= n, EIG_ERR_ARG, "shift-invert (block): the block basis does not fit n");
+  EIG_CHECK(((cmax + 15) / 16) * ((p + 15) / 16) <= kNumTickets, EIG_ERR_ARG,
+            "shift-invert (block): nev too large for the block method (use EIG_SI_SINGLE)");
   if (tol <= 0.0) tol = 2.220446049250313e-16;
   if (maxit <= 0) maxit = 100 * nev;
   const int wk = std::max(kk, g.nw);
@@ -749,7 +751,8 @@ bool si_use_block(i64 n, int nev, int ncv, int flags)
   if (flags & EIG_SI_SINGLE) return false;
   if (flags & EIG_SI_BLOCK) return true;
   const SiBlockShape g = si_block_shape(nev, ncv);
-  return (i64)(g.cmax + g.p) * 4 <= n;
+  // the basis within n / 4, and the projection Gram (cmax x p) within the reduction tickets
+  return (i64)(g.cmax + g.p) * 4 <= n && ((g.cmax + 15) / 16) * ((g.p + 15) / 16) <= kNumTickets;
 }
 
 void shift_invert_run(eig_mat_t A, eig_mat_t B, const LuRef &F, double sigma, int nev, int ncv, double tol, int maxit,
