@@ -105,6 +105,8 @@ def test_block_method_arguments(ctx):
         eigmi.shift_invert_solve(up(ctx, A), 4, sigma=0.0, method="block")  # n = 36 < 72 columns
     ev, _, _ = eigmi.shift_invert_solve(up(ctx, A), 4, sigma=0.0, want_evec=False)  # auto: one-vector
     assert np.allclose(ev, np.sort(oracle.eig_laplace2d(6))[:4], rtol=0, atol=1e-10)
+    with pytest.raises(eigmi.EigError):  # nev = 60: the projection Gram exceeds the reduction tickets
+        eigmi.shift_invert_solve(up(ctx, oracle.laplace2d(64)), 60, sigma=0.0, method="block")
     with pytest.raises(eigmi.EigError):
         A2 = up(ctx, A)
         A2.ctx.check(eigmi.lib.eig_shift_invert_solve_ex(A2.h, None, None, 0.0, 4, 0, 0.0, 0, 1,
