@@ -381,7 +381,9 @@ int eig_shift_invert_solve(eig_mat_t A, eig_mat_t B, eig_lu_t lu, double sigma, 
  * pairs, B-inner product, convergence test (||R y_i|| <= tol |theta_i|, R the residual block's
  * coupling) and purified vectors; ncv = a lower bound on the search dimension; *restarts counts block
  * restarts.  EIG_SI_AUTO (0, what eig_shift_invert_solve and eig_shift_invert_adaptive use): the block
- * method when its basis (at most ~4 p + 1.5 nev columns) is at most n / 4, else the one-vector one. */
+ * method when its basis (at most ~4 p + 1.5 nev columns) is at most n / 4 and its projection Gram
+ * (basis x p, in 16 x 16 tiles) fits the 64 device reduction slots, else the one-vector one;
+ * EIG_SI_BLOCK with an nev past that limit returns EIG_ERR_ARG. */
 #define EIG_SI_AUTO 0
 #define EIG_SI_SINGLE 1
 #define EIG_SI_BLOCK 2
