@@ -107,10 +107,11 @@ def cpu_model():
     return None
 
 
-def committed_traffic(kernel, N, world):
-    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
+def committed_traffic(kernel, N, world, build):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summaries
     (profiles/<tag>_pmc_summary.json, FETCH_SIZE x2 + WRITE_SIZE, KiB -> B; tools/profile_round.sh)
-    taken on the same configuration; None when no matching profile exists."""
+    taken on the same configuration: the newest one profiled on this build (eigmi.build_id()) when
+    there is one, else the newest of any build; (bytes, source, same_build) or None."""
     import glob
     best = None
     for p in glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json")):
@@ -122,12 +123,13 @@ def committed_traffic(kernel, N, world):
                 continue
             for name, k in d["kernels"].items():  # template instances: "eigmi::k_..._b1<1, 1>"
                 if name.split("<")[0] == "eigmi::" + kernel:
-                    stamp = d.get("collected", os.path.getmtime(p))
+                    same = d.get("build") is not None and d.get("build") == build
+                    stamp = (same, d.get("collected", os.path.getmtime(p)))
                     if best is None or stamp > best[2]:
                         best = (k["hbm_bytes"], os.path.relpath(p, ROOT), stamp)
         except (OSError, ValueError, KeyError, TypeError, AttributeError):
             continue
-    return best[:2] if best else None
+    return (best[0], best[1], best[2][0]) if best else None
 
 
 VARIANT_NAME = {"fused": "fused one-reduction step", "pipelined": "pipelined one-reduction step",
@@ -194,6 +196,7 @@ def main():
     nnz_local = int(rp[-1])
 
     K, W = args.steps, args.warmup
+    build = eigmi.build_id()
 
     def max_over_ranks(x):
         if dist is None:
@@ -213,7 +216,11 @@ def main():
         if world > 1:
             trial = {}
             for var in ("fused", "pipelined"):
-                ms = float("inf")
+                # every call below may already have queued a halo exchange or an allreduce on the
+                # other ranks when it fails here, so a failing rank cannot rejoin them at a barrier:
+                # it exits non-zero at once and the launcher tears the job down on every rank
+                # (a refused hipGraph capture is no failure: replay() then runs the steps eagerly)
+                tw = None
                 try:
                     tw = eigmi.LanczosWorkspace(M, 5 + args.trial_steps, seed=123, fused=var == "fused",
                                                 pipelined=var == "pipelined")
@@ -225,14 +232,16 @@ def main():
                     tw.replay()
                     ctx.sync()
                     ms = (time.perf_counter() - t0) / args.trial_steps * 1e3
-                    tw.close()
-                except eigmi.EigError as e:  # a variant that fails on this transport is not chosen
-                    print(f"bench: {var} trial failed on rank {rank}: {e}", file=sys.stderr, flush=True)
+                except eigmi.EigError as e:
+                    print(f"bench: {var} trial failed on rank {rank}: {e}; stopping every rank", file=sys.stderr,
+                          flush=True)
+                    os._exit(3)
+                finally:
+                    if tw is not None:
+                        tw.close()
                 barrier()
                 trial[var] = round(max_over_ranks(ms), 4)
             variant = min(trial, key=trial.get)
-            if trial[variant] == float("inf"):
-                raise SystemExit("bench: neither one-reduction variant ran at N > 1")
     fused = variant in ("fused", "pipelined")
     pipelined = variant == "pipelined"
     # the K timed steps are captured as one hipGraph before the clock starts (kernels, halo
@@ -294,10 +303,11 @@ def main():
     roofline = None
     if k1_ms:
         ach = k1_bytes / (k1_ms * 1e-3) / 1e9
-        tr = committed_traffic(kname, N, world)
+        tr = committed_traffic(kname, N, world, build)
         roofline = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": tr[0] if tr else None,
                     "traffic_source": tr[1] if tr else None,
+                    "traffic_same_build": tr[2] if tr else None,
                     "traffic_GBs": round(tr[0] / (k1_ms * 1e-3) / 1e9, 1) if tr else None,
                     "traffic_frac": round(tr[0] / (k1_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if tr else None,
                     "kernel": kname, "bytes_per_launch": k1_bytes,
@@ -369,6 +379,7 @@ def main():
         # auto at N > 1: ms per step of each one-reduction variant in the trial (max over ranks)
         "variant_trial_ms": ({k: (v if v != float("inf") else None) for k, v in trial.items()} if trial else None),
         "launch": "hipGraph replay of the K steps" if graph else "eager",
+        "build": build,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cv, cdt, rel = cpu_baseline(N, rp, c, v, args.cpu_steps, alpha, fused)

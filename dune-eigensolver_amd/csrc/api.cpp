@@ -62,7 +62,7 @@ void *ctx_buffer(eig_ctx_t ctx, int slot, size_t bytes)
 
 void allreduce_sum(eig_ctx_t ctx, double *buf, i64 count, hipStream_t s)
 {
-  if (!ctx->distributed() || count <= 0) return;
+  if (!ctx->collectives() || count <= 0) return;
   if (ctx->mbox && ctx->mbox->ready)
   {
     for (i64 off = 0; off < count; off += kMailboxVals)
@@ -91,11 +91,12 @@ void allreduce_sum(eig_ctx_t ctx, double *buf, i64 count, hipStream_t s)
     return;
   }
   EIG_NCCL(ncclAllReduce(buf, buf, (size_t)count, ncclDouble, ncclSum, ctx->comm, s));
+  ++ctx->n_ar;
 }
 
 bool allreduce_overlaps(eig_ctx_t ctx)
 {
-  const bool ovl = ctx->distributed() && !ctx->loop && ((ctx->mbox && ctx->mbox->ready) || ctx->comm_red);
+  const bool ovl = ctx->collectives() && !ctx->loop && ((ctx->mbox && ctx->mbox->ready) || ctx->comm_red);
   // the reduction stream exists only where it is used (every stream takes a hardware queue)
   if (ovl && !ctx->red_stream) EIG_HIP(hipStreamCreateWithFlags(&ctx->red_stream, hipStreamNonBlocking));
   return ovl;
@@ -110,6 +111,7 @@ void allreduce_sum_red(eig_ctx_t ctx, double *buf, i64 count, hipStream_t s)
     return;
   }
   EIG_NCCL(ncclAllReduce(buf, buf, (size_t)count, ncclDouble, ncclSum, ctx->comm_red, s));
+  ++ctx->n_ar_red;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -236,6 +238,8 @@ void halo_exchange(const eig_mat_s &A, double *x, hipStream_t s, double *x2, int
     if (x2) EIG_NCCL(ncclSend(x2 + r.offset * w, (size_t)(r.count * w), ncclDouble, r.peer, ctx->comm, s));
   }
   EIG_NCCL(ncclGroupEnd());
+  ++ctx->n_halo;
+  ctx->n_p2p += (long long)(A.recvs.size() + A.sends.size()) * (x2 ? 2 : 1);
 }
 
 // eigensolver.hh:49-55 generator (libstdc++ mt19937 + normal_distribution, bitwise the
@@ -423,7 +427,7 @@ extern "C" int eig_comm_init_ex(eig_ctx_t ctx, int nranks, int rank, const unsig
 {
   return guard(ctx, [&] {
     EIG_CHECK(ctx && id && nranks >= 1 && rank >= 0 && rank < nranks, EIG_ERR_ARG, "eig_comm_init: bad arguments");
-    EIG_CHECK((flags & ~EIG_COMM_MAILBOX) == 0, EIG_ERR_ARG, "eig_comm_init_ex: unknown flag");
+    EIG_CHECK((flags & ~(EIG_COMM_MAILBOX | EIG_COMM_ALWAYS)) == 0, EIG_ERR_ARG, "eig_comm_init_ex: unknown flag");
     EIG_CHECK(!ctx->loop && !ctx->mbox, EIG_ERR_ARG, "context already has a transport");
     DeviceGuard dg(ctx->device);
     ncclUniqueId u;
@@ -431,10 +435,19 @@ extern "C" int eig_comm_init_ex(eig_ctx_t ctx, int nranks, int rank, const unsig
     EIG_NCCL(ncclCommInitRank(&ctx->comm, nranks, u, rank));
     ctx->nranks = nranks;
     ctx->rank = rank;
-    // second communicator (same ranks, same order) for allreduces that overlap the halo exchange;
-    // collective, so every rank either has it or none does
-    if (nranks > 1 && ncclCommSplit(ctx->comm, 0, rank, &ctx->comm_red, nullptr) != ncclSuccess)
-      ctx->comm_red = nullptr;
+    ctx->comm_always = (flags & EIG_COMM_ALWAYS) != 0;
+    // second communicator (same ranks, same order) for allreduces that overlap the halo exchange.
+    // A rank whose split fails makes every rank drop it (all_ranks), so all ranks agree on
+    // allreduce_overlaps() and run the pipelined step's allreduce on the same communicator.
+    if (nranks > 1 || ctx->comm_always)
+    {
+      if (ncclCommSplit(ctx->comm, 0, rank, &ctx->comm_red, nullptr) != ncclSuccess) ctx->comm_red = nullptr;
+      if (!all_ranks(ctx, ctx->comm_red != nullptr) && ctx->comm_red)
+      {
+        (void)ncclCommDestroy(ctx->comm_red);
+        ctx->comm_red = nullptr;
+      }
+    }
     // the mailbox allreduce only on request: it is validated between processes on one GPU
     // (tests/test_mailbox_gpu.py), not yet across xGMI
     if (flags & EIG_COMM_MAILBOX) mailbox_setup_rccl(ctx);
@@ -471,7 +484,7 @@ extern "C" int eig_comm_info(eig_ctx_t ctx, int *nranks, int *rank, int *allredu
     if (nranks) *nranks = ctx->nranks;
     if (rank) *rank = ctx->rank;
     if (allreduce)
-      *allreduce = !ctx->distributed()                 ? EIG_AR_NONE
+      *allreduce = !ctx->collectives()                 ? EIG_AR_NONE
                    : (ctx->mbox && ctx->mbox->ready)   ? EIG_AR_MAILBOX
                    : ctx->loop                         ? EIG_AR_LOOPBACK
                                                        : EIG_AR_RCCL;
@@ -485,6 +498,17 @@ extern "C" int eig_comm_info(eig_ctx_t ctx, int *nranks, int *rank, int *allredu
         EIG_HIP(hipMemcpy(mailbox_errors, ctx->mbox->dev.err, sizeof(int), hipMemcpyDeviceToHost));
       }
     }
+  });
+}
+
+extern "C" int eig_comm_counters(eig_ctx_t ctx, int64_t out[4])
+{
+  return guard(ctx, [&] {
+    EIG_CHECK(ctx && out, EIG_ERR_ARG, "eig_comm_counters: null argument");
+    out[0] = ctx->n_ar;
+    out[1] = ctx->n_ar_red;
+    out[2] = ctx->n_halo;
+    out[3] = ctx->n_p2p;
   });
 }
 

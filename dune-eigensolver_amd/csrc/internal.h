@@ -135,7 +135,11 @@ struct eig_ctx_s {
   eigmi::LoopHub *loop = nullptr;    // in-process loopback transport (tests), exclusive with comm
   eigmi::MailboxHost *mbox = nullptr; // xGMI mailbox allreduce (with RCCL, or alone for tests)
   int nranks = 1, rank = 0;
+  long long n_ar = 0, n_ar_red = 0, n_halo = 0, n_p2p = 0;  // eig_comm_counters
+  bool comm_always = false;          // EIG_COMM_ALWAYS: collectives through `comm` even at one rank
   bool distributed() const { return nranks > 1 && (comm || loop || (mbox && mbox->ready)); }
+  // whether allreduces go through a transport (distributed, or a forced one-rank RCCL communicator)
+  bool collectives() const { return distributed() || (comm_always && comm); }
   // reusable device buffers for drivers (grown on demand)
   std::vector<std::pair<void *, size_t>> pool;
 };

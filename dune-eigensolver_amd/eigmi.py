@@ -23,6 +23,7 @@ MAT_NO_BAND, MAT_BAND_GATHER, MAT_NO_STENCIL, MAT_NO_MARCH, MAT_NO_CLASS = 1, 2,
 TRSV_AUTO, TRSV_BLOCKINV, TRSV_STAGED, TRSV_CSR = 0, 1, 2, 3
 TRSV_KINDS = {None: TRSV_AUTO, "auto": TRSV_AUTO, "blockinv": TRSV_BLOCKINV, "staged": TRSV_STAGED, "csr": TRSV_CSR}
 COMM_MAILBOX = 1
+COMM_ALWAYS = 2  # collectives through RCCL even at one rank (eig_comm_init_ex)
 STREAM_COPY_MODE = 3  # eig_stream_copy_timed: nontemporal, full grid -- 6.70 TB/s vs 6.28 plain (tools/copy_sweep.py)
 WHICH_LA, WHICH_SA = 0, 1
 LANCZOS_TIME_KERNELS = 1
@@ -99,6 +100,7 @@ SIGNATURES = {
     "eig_comm_ipc_open": (_int, [_vp, ctypes.c_char_p]),
     "eig_comm_info": (_int, [_vp, ctypes.POINTER(_int), ctypes.POINTER(_int), ctypes.POINTER(_int),
                              ctypes.POINTER(_int)]),
+    "eig_comm_counters": (_int, [_vp, ctypes.POINTER(_i64)]),
     "eig_malloc": (_int, [_vp, ctypes.c_size_t, ctypes.POINTER(_vp)]),
     "eig_free": (_int, [_vp, _vp]),
     "eig_memcpy_h2d": (_int, [_vp, _vp, _vp, ctypes.c_size_t]),
@@ -200,6 +202,21 @@ def load():
 lib = load()
 
 
+def build_id():
+    """Identity of the kernel sources the loaded library was built from: sha1 over csrc/ (the .hip
+    kernels, host .cpp and headers) -- bench lines and committed PMC summaries carry it, so a
+    summary is matched to the build it measured."""
+    import hashlib
+    h = hashlib.sha1()
+    src = os.path.join(_HERE, "csrc")
+    for f in sorted(os.listdir(src)):
+        if f.endswith((".hip", ".cpp", ".h")):
+            h.update(f.encode())
+            with open(os.path.join(src, f), "rb") as fh:
+                h.update(fh.read())
+    return h.hexdigest()[:12]
+
+
 def _np_ptr(a):
     return a.ctypes.data_as(_vp)
 
@@ -252,11 +269,19 @@ class Context:
             raise EigError(rc, lib.eig_last_error(None).decode())
         return buf.raw
 
-    def comm_init(self, nranks, rank, uid, mailbox=False):
+    def comm_init(self, nranks, rank, uid, mailbox=False, always=False):
         """RCCL communicator (ncclAllReduce for dots); mailbox=True also sets up the xGMI mailbox
-        allreduce (eig_comm_init_ex, EIG_COMM_MAILBOX)."""
-        self.check(lib.eig_comm_init_ex(self.h, nranks, rank, uid, COMM_MAILBOX if mailbox else 0))
+        allreduce (eig_comm_init_ex, EIG_COMM_MAILBOX); always=True routes the collectives through
+        RCCL even at nranks == 1 (EIG_COMM_ALWAYS: the one-GPU rehearsal of the transport)."""
+        flags = (COMM_MAILBOX if mailbox else 0) | (COMM_ALWAYS if always else 0)
+        self.check(lib.eig_comm_init_ex(self.h, nranks, rank, uid, flags))
         self.nranks, self.rank = nranks, rank
+
+    def comm_counters(self):
+        """Collectives the library has enqueued on its communicators (eig_comm_counters)."""
+        v = (_i64 * 4)()
+        self.check(lib.eig_comm_counters(self.h, v))
+        return {"allreduce": v[0], "allreduce_split": v[1], "halo_groups": v[2], "p2p": v[3]}
 
     def barrier(self):
         self.check(lib.eig_comm_barrier(self.h))

@@ -66,8 +66,12 @@ const char *eig_version(void);
 int eig_comm_unique_id(unsigned char id[128]);
 int eig_comm_init(eig_ctx_t ctx, int nranks, int rank, const unsigned char id[128]);
 /* flags: EIG_COMM_MAILBOX = also set up the xGMI mailbox allreduce (below); default (0, and
- * eig_comm_init): ncclAllReduce. */
-enum { EIG_COMM_MAILBOX = 1 };
+ * eig_comm_init): ncclAllReduce.  EIG_COMM_ALWAYS = route every collective of the drivers through
+ * the communicator even at nranks == 1 (ncclAllReduce on the main and on the split communicator,
+ * inside hipGraph captures too) instead of skipping it: a one-GPU rehearsal of the transport whose
+ * results must be bitwise those of the run without a communicator.  Kernel choices stay those of a
+ * single rank. */
+enum { EIG_COMM_MAILBOX = 1, EIG_COMM_ALWAYS = 2 };
 int eig_comm_init_ex(eig_ctx_t ctx, int nranks, int rank, const unsigned char id[128], int flags);
 int eig_comm_allreduce_sum(eig_ctx_t ctx, double *buf, int64_t count);
 /* In-process loopback transport for testing the distributed path on ONE device: create a hub for
@@ -87,6 +91,11 @@ int eig_comm_barrier(eig_ctx_t ctx);
  * nranks x 64 bytes travel by any side channel (rank order), then every rank opens them. */
 #define EIG_IPC_HANDLE_BYTES 64
 enum eig_allreduce_kind { EIG_AR_NONE = 0, EIG_AR_RCCL = 1, EIG_AR_MAILBOX = 2, EIG_AR_LOOPBACK = 3 };
+/* Collectives the library has enqueued on its RCCL communicators since eig_comm_init (a captured
+ * hipGraph counts once, at capture): out[0] = ncclAllReduce on the main communicator, out[1] =
+ * ncclAllReduce on the split one (the pipelined step's overlapped allreduce), out[2] = halo groups
+ * (ncclGroupStart .. End), out[3] = ncclSend + ncclRecv calls inside them. */
+int eig_comm_counters(eig_ctx_t ctx, int64_t out[4]);
 int eig_comm_ipc_handle(eig_ctx_t ctx, int nranks, int rank, unsigned char handle[EIG_IPC_HANDLE_BYTES]);
 int eig_comm_ipc_open(eig_ctx_t ctx, const unsigned char *handles);
 /* nranks / rank / the allreduce in use (eig_allreduce_kind) / mailbox timeouts so far (syncs). */

@@ -50,6 +50,7 @@ def main(src, tag):
         p = os.path.join(src, fn)
         if os.path.exists(p):
             out["bench_line_under_trace"] = json.loads(open(p).read().strip().splitlines()[-1])
+            out["build"] = out["bench_line_under_trace"].get("build")  # eigmi.build_id() of the profiled library
     with open(os.path.join(dst, f"{tag}_pmc_summary.json"), "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out["kernels"], indent=1))
