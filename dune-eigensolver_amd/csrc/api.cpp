@@ -1437,20 +1437,18 @@ namespace eigmi {
 // G (m1 x m2 row-major) = Q1^T Q2, tiled so that one launch stays within the ticket pool.
 void gram_device(eig_ctx_t ctx, i64 n, i64 m1, i64 m2, const double *Q1, const double *Q2, double *G)
 {
-  // one launch per group of 16-column output tiles that fits 48 tickets
-  const i64 ti = (m1 + 15) / 16, tj = (m2 + 15) / 16;
-  if (ti * tj <= 48)
+  if (gram_mv8_chunks(m1, m2) <= 48)
   {
     launch_gram_mv8(n, m1, m2, Q1, Q2, G, 0, ctx->stream, ctx->red);
   }
   else
   {
-    // row panels of Q1 (16 columns each) against all of Q2 in chunks; write into a temp then scatter
-    EIG_CHECK(tj <= 48, EIG_ERR_ARG, "gram: Q2 too wide (> 768 columns)");
-    double *tmp = (double *)ctx_buffer(ctx, 2, (size_t)16 * m2 * sizeof(double));
-    for (i64 r = 0; r < m1; r += 16)
+    // row panels of Q1 (32 columns each) against all of Q2; write into a temp then scatter
+    EIG_CHECK(gram_mv8_chunks(32, m2) <= 48, EIG_ERR_ARG, "gram: Q2 too wide (> 1536 columns)");
+    double *tmp = (double *)ctx_buffer(ctx, 2, (size_t)32 * m2 * sizeof(double));
+    for (i64 r = 0; r < m1; r += 32)
     {
-      const i64 mr = std::min<i64>(16, m1 - r);
+      const i64 mr = std::min<i64>(32, m1 - r);
       launch_gram_mv8(n, mr, m2, Q1 + r * n, Q2, tmp, 0, ctx->stream, ctx->red);
       EIG_HIP(hipMemcpyAsync(G + r * m2, tmp, mr * m2 * sizeof(double), hipMemcpyDeviceToDevice, ctx->stream));
     }

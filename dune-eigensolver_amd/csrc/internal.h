@@ -326,6 +326,7 @@ void launch_dot_diag_mv8(i64 n, i64 m, const double *Q1, const double *Q2, doubl
                          hipStream_t s, ReduceWS red);
 void launch_gram_mv8(i64 n, i64 m1, i64 m2, const double *Q1, const double *Q2, double *G, int ticket,
                      hipStream_t s, ReduceWS red);
+int gram_mv8_chunks(i64 m1, i64 m2);  // tickets one launch_gram_mv8 takes
 // Block Gram-Schmidt building blocks, see k_mv8.hip.
 void launch_mgs_pass(i64 n, double *Qb, int k, double *S, int ticket, hipStream_t s, ReduceWS red);
 // Whole column MGS of one 8-column block in one workgroup (n <= 4096, one rank); false = not taken.

@@ -5,6 +5,8 @@
 // column block b of an n x m multivector is n rows of 8 contiguous doubles (64 B) starting at
 // Q + b*8*n.  Kernels keep the reference's per-element operation order wherever the result is
 // not a reduction, so SpMM / projections are bitwise the reference arithmetic on equal inputs.
+#include <algorithm>
+
 #include "internal.h"
 #include "reduce_dev.h"
 
@@ -136,82 +138,168 @@ void launch_dot_diag_mv8(i64 n, i64 m, const double *Q1, const double *Q2, doubl
 }
 
 // ---------------------------------------------------------------------------------------------
-// a6: G = Q1^T Q2 on MFMA (v_mfma_f64_16x16x4f64), one 16x16 output tile per grid.y.
-// Lane l supplies A[i = l&15][k = l>>4] = Q1(row r0+k, c1 + i) and B[k][j = l&15] = Q2(row r0+k,
-// c2 + j); the f64 accumulator holds C[row (l>>4) + 4 q][col l&15] in register q.  Columns past
-// m1 / m2 read as zero (an m = 8 Gram uses the top-left 8x8 quadrant).  Per workgroup the 4
-// waves' tiles are summed in LDS, then across workgroups in block order (deterministic).
+// a6: G = Q1^T Q2 on MFMA (dot_products_all_blocked, kernels_cpp.hh:58-96), v_mfma_f64_16x16x4f64.
+//
+// One MultiVector column block is 8 columns wide, the MFMA tile 16: instead of padding half the
+// lanes, a tile takes 8 ROWS of one block -- lane l (k = l>>4, i = l&15) supplies
+// A[i][k] = Q1(8g + k + 4 (i>>3), i & 7) and B[k][j] = Q2(8g + k + 4 (j>>3), j & 7), so one 8-B load
+// per lane reads 8 whole 64-B rows (512 contiguous bytes) and every loaded value is used.  The
+// products with i>>3 == j>>3 are the two 8x8 quadrants on the tile diagonal (rows 8g..8g+3 and
+// 8g+4..8g+7); G's 8x8 block is their sum (the off-diagonal quadrants are discarded).
+// A workgroup takes NB1 blocks of Q1 x NB2 blocks of Q2 for its row range (every operand loaded
+// once for NB2 / NB1 MFMAs: NB1 x NB2 independent accumulator chains), U 8-row groups per wave
+// iteration with all loads issued before the MFMAs.  grid.y = chunks of the block grid (each
+// panel streams once per chunk of the other).  Reduction: quadrants folded by a lane shuffle,
+// the 4 waves summed in LDS, then grid_sum2 (two-level, deterministic).
 // ---------------------------------------------------------------------------------------------
 constexpr int kGramThreads = 256;
 
-__device__ __forceinline__ double mv8_at(const double *Q, i64 n, i64 r, i64 c) { return Q[((c >> 3) * n + r) * 8 + (c & 7)]; }
-
-__global__ __launch_bounds__(kGramThreads) void k_gram_mv8(i64 n, i64 m1, i64 m2, const double *__restrict__ Q1,
-                                                           const double *__restrict__ Q2, double *__restrict__ G,
-                                                           int tiles_j, double *partials, unsigned *tickets)
+template <int NB1, int NB2, int U>
+__global__ __launch_bounds__(kGramThreads) void k_gram_mv8(i64 n, int nb1, int nb2, int nby2,
+                                                           const double *__restrict__ Q1, const double *__restrict__ Q2,
+                                                           double *__restrict__ G, double *partials, unsigned *tickets)
 {
-  __shared__ double sh[kGramThreads / 64][256];
-  __shared__ unsigned s_last;
+  constexpr int E = NB1 * NB2 * 64;
+  constexpr int W = kGramThreads / 64;
+  __shared__ double sh[W][E];
+  __shared__ double tot[E];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int ti = blockIdx.y / tiles_j, tj = blockIdx.y % tiles_j;
-  const i64 c1 = (i64)ti * 16 + (lane & 15), c2 = (i64)tj * 16 + (lane & 15);
-  const bool ok1 = c1 < m1, ok2 = c2 < m2;
-  const int kk = lane >> 4;
-  d4 acc = {0.0, 0.0, 0.0, 0.0};
-  // rows in groups of 4 (one MFMA), 4 groups per wave iteration
-  const i64 ngroups = (n + 3) / 4;
-  const i64 wstride = (i64)gridDim.x * (kGramThreads / 64);
-  for (i64 g = (i64)blockIdx.x * (kGramThreads / 64) + wave; g < ngroups; g += wstride)
+  const int cy1 = blockIdx.y / nby2, cy2 = blockIdx.y % nby2;
+  const int k = lane >> 4, i = lane & 15;
+  const int rl = k + 4 * (i >> 3);  // row inside the 8-row group
+  const double *a[NB1];
+  const double *b[NB2];
+  bool aok[NB1], bok[NB2];
+#pragma unroll
+  for (int t = 0; t < NB1; ++t)
   {
-    const i64 r = g * 4 + kk;
-    const bool rok = r < n;
-    const double a = (ok1 && rok) ? mv8_at(Q1, n, r, c1) : 0.0;
-    const double b = (ok2 && rok) ? mv8_at(Q2, n, r, c2) : 0.0;
-    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+    const int blk = cy1 * NB1 + t;
+    aok[t] = blk < nb1;
+    a[t] = Q1 + (i64)(aok[t] ? blk : 0) * n * 8 + (i & 7);
   }
-  // tile element (row, col) = (kk + 4 q, lane & 15)
 #pragma unroll
-  for (int q = 0; q < 4; ++q) sh[wave][(kk + 4 * q) * 16 + (lane & 15)] = acc[q];
-  __syncthreads();
-  const int t = threadIdx.x;  // 256 threads = 256 tile elements
-  double bsum = 0.0;
-#pragma unroll
-  for (int w = 0; w < kGramThreads / 64; ++w) bsum += sh[w][t];
-  double *part = partials + (size_t)blockIdx.y * gridDim.x * 256;
-  st_sc1(&part[(size_t)blockIdx.x * 256 + t], bsum);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (t == 0)
+  for (int u = 0; u < NB2; ++u)
   {
-    s_last = ticket_arrive(tickets + (size_t)blockIdx.y * kTicketStride, blockIdx.x, gridDim.x) ? 1u : 0u;
+    const int blk = cy2 * NB2 + u;
+    bok[u] = blk < nb2;
+    b[u] = Q2 + (i64)(bok[u] ? blk : 0) * n * 8 + (i & 7);
+  }
+  d4 acc[NB1][NB2];
+#pragma unroll
+  for (int t = 0; t < NB1; ++t)
+#pragma unroll
+    for (int u = 0; u < NB2; ++u) acc[t][u] = d4{0.0, 0.0, 0.0, 0.0};
+  const i64 ng = (n + 7) >> 3;
+  const i64 ws = (i64)gridDim.x * W;
+  for (i64 g0 = (i64)blockIdx.x * W + wave; g0 < ng; g0 += U * ws)
+  {
+    double av[U][NB1], bv[U][NB2];
+#pragma unroll
+    for (int v = 0; v < U; ++v)
+    {
+      const i64 r = (g0 + v * ws) * 8 + rl;
+      const bool ok = r < n;  // (also false for groups past ng)
+      const i64 rr = ok ? r : 0;
+#pragma unroll
+      for (int t = 0; t < NB1; ++t) av[v][t] = a[t][rr * 8];
+#pragma unroll
+      for (int u = 0; u < NB2; ++u) bv[v][u] = b[u][rr * 8];
+#pragma unroll
+      for (int t = 0; t < NB1; ++t) av[v][t] = (ok && aok[t]) ? av[v][t] : 0.0;
+#pragma unroll
+      for (int u = 0; u < NB2; ++u) bv[v][u] = (ok && bok[u]) ? bv[v][u] : 0.0;
+    }
+#pragma unroll
+    for (int v = 0; v < U; ++v)
+#pragma unroll
+      for (int t = 0; t < NB1; ++t)
+#pragma unroll
+        for (int u = 0; u < NB2; ++u)
+          acc[t][u] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[v][t], bv[v][u], acc[t][u], 0, 0, 0);
+  }
+  // lane holds C[k + 4q][i]; for i < 8 and q < 2, C[k + 4q][i] + C[k + 4q + 8][i + 8] (lane + 8,
+  // register q + 2) is G(k + 4q, i) of this block pair
+#pragma unroll
+  for (int t = 0; t < NB1; ++t)
+#pragma unroll
+    for (int u = 0; u < NB2; ++u)
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+      {
+        const double hi = __shfl_down(acc[t][u][q + 2], 8, 64);
+        if (i < 8) sh[wave][(t * NB2 + u) * 64 + (k + 4 * q) * 8 + i] = acc[t][u][q] + hi;
+      }
+  __syncthreads();
+  for (int e = threadIdx.x; e < E; e += kGramThreads)
+  {
+    double v = sh[0][e];
+#pragma unroll
+    for (int w = 1; w < W; ++w) v += sh[w][e];
+    tot[e] = v;
   }
   __syncthreads();
-  if (!s_last) return;
-  double tot = 0.0;
-  for (unsigned b0 = 0; b0 < gridDim.x; b0 += 16)
+  const size_t ny = gridDim.y;
+  double *part = partials + (size_t)blockIdx.y * gridDim.x * E;
+  double *spart = partials + ny * gridDim.x * E + (size_t)blockIdx.y * 8 * E;
+  if (!grid_sum2<kGramThreads>(tot, E, part, spart, tickets + (size_t)blockIdx.y * kTicketStride, blockIdx.x,
+                               gridDim.x, sh[0]))
+    return;
+  const i64 m2 = (i64)nb2 * 8;
+  for (int e = threadIdx.x; e < E; e += kGramThreads)
   {
-    double v[16];  // 16 independent sc1 loads in flight, then the adds in block order
-#pragma unroll
-    for (int u = 0; u < 16; ++u) v[u] = (b0 + u < gridDim.x) ? ld_sc1(&part[(size_t)(b0 + u) * 256 + t]) : 0.0;
-#pragma unroll
-    for (int u = 0; u < 16; ++u) tot += v[u];
+    const int tu = e >> 6, t = tu / NB2, u = tu % NB2, row = (e >> 3) & 7, col = e & 7;
+    if (cy1 * NB1 + t < nb1 && cy2 * NB2 + u < nb2) G[((i64)(cy1 * NB1 + t) * 8 + row) * m2 + (i64)(cy2 * NB2 + u) * 8 + col] = sh[0][e];
   }
-  const int row = t >> 4, cl = t & 15;
-  const i64 gi = (i64)ti * 16 + row, gj = (i64)tj * 16 + cl;
-  if (gi < m1 && gj < m2) G[gi * m2 + gj] = tot;
-  if (t == 0) ticket_reset(tickets + (size_t)blockIdx.y * kTicketStride);
+}
+
+namespace {
+template <int NB1, int NB2>
+void gram_launch(i64 n, int nb1, int nb2, const double *Q1, const double *Q2, double *G, int ticket, hipStream_t s,
+                 ReduceWS red)
+{
+  constexpr int U = (NB1 + NB2) <= 2 ? 8 : (NB1 + NB2) <= 4 ? 4 : 2;
+  constexpr int E = NB1 * NB2 * 64;
+  const int ny1 = (nb1 + NB1 - 1) / NB1, ny2 = (nb2 + NB2 - 1) / NB2, ny = ny1 * ny2;
+  EIG_CHECK(ticket + ny <= kNumTickets, EIG_ERR_ARG, "gram_mv8: too many output chunks");
+  const i64 ng = (n + 7) / 8;
+  // about 2 resident workgroups per CU, at least one U-group batch per wave
+  i64 gx = std::min<i64>(512, std::max<i64>(1, (ng + 4 * U - 1) / (4 * U)));
+  while ((gx * ny + 8 * ny) * E > (i64)kMaxRedBlocks * kMaxRedVals && gx > 1) gx /= 2;
+  hipLaunchKernelGGL((k_gram_mv8<NB1, NB2, U>), dim3((unsigned)gx, (unsigned)ny), dim3(kGramThreads), 0, s, n, nb1,
+                     nb2, ny2, Q1, Q2, G, red.partials, red.ticket(ticket));
+}
+}  // namespace
+
+int gram_mv8_chunks(i64 m1, i64 m2)
+{
+  const i64 nb1 = m1 / 8, nb2 = m2 / 8;
+  const i64 NB1 = nb1 >= 4 ? 4 : nb1 >= 2 ? 2 : 1, NB2 = nb2 >= 4 ? 4 : std::max<i64>(1, nb2);
+  return (int)(((nb1 + NB1 - 1) / NB1) * ((nb2 + NB2 - 1) / NB2));
 }
 
 void launch_gram_mv8(i64 n, i64 m1, i64 m2, const double *Q1, const double *Q2, double *G, int ticket,
                      hipStream_t s, ReduceWS red)
 {
-  const int tiles_i = (int)((m1 + 15) / 16), tiles_j = (int)((m2 + 15) / 16);
-  const int tiles = tiles_i * tiles_j;
-  EIG_CHECK(tiles >= 1 && ticket + tiles <= kNumTickets, EIG_ERR_ARG, "gram_mv8: too many output tiles");
-  int gx = grid_for((n + 3) / 4, 4 * 8, 256);
-  while ((i64)gx * tiles * 256 > (i64)kMaxRedBlocks * kMaxRedVals && gx > 1) gx /= 2;
-  hipLaunchKernelGGL(k_gram_mv8, dim3(gx, tiles), dim3(kGramThreads), 0, s, n, m1, m2, Q1, Q2, G, tiles_j,
-                     red.partials, red.ticket(ticket));
+  EIG_CHECK(m1 > 0 && m2 > 0 && m1 % 8 == 0 && m2 % 8 == 0, EIG_ERR_ARG, "gram_mv8: m1, m2 multiples of 8");
+  const int nb1 = (int)(m1 / 8), nb2 = (int)(m2 / 8);
+  const int NB1 = nb1 >= 4 ? 4 : nb1 >= 2 ? 2 : 1;
+  const int NB2 = nb2 >= 4 ? 4 : nb2;
+  switch (NB1 * 8 + NB2)
+  {
+    case 9: gram_launch<1, 1>(n, nb1, nb2, Q1, Q2, G, ticket, s, red); break;
+    case 10: gram_launch<1, 2>(n, nb1, nb2, Q1, Q2, G, ticket, s, red); break;
+    case 11: gram_launch<1, 3>(n, nb1, nb2, Q1, Q2, G, ticket, s, red); break;
+    case 12: gram_launch<1, 4>(n, nb1, nb2, Q1, Q2, G, ticket, s, red); break;
+    case 17: gram_launch<2, 1>(n, nb1, nb2, Q1, Q2, G, ticket, s, red); break;
+    case 18: gram_launch<2, 2>(n, nb1, nb2, Q1, Q2, G, ticket, s, red); break;
+    case 19: gram_launch<2, 3>(n, nb1, nb2, Q1, Q2, G, ticket, s, red); break;
+    case 20: gram_launch<2, 4>(n, nb1, nb2, Q1, Q2, G, ticket, s, red); break;
+    case 33: gram_launch<4, 1>(n, nb1, nb2, Q1, Q2, G, ticket, s, red); break;
+    case 34: gram_launch<4, 2>(n, nb1, nb2, Q1, Q2, G, ticket, s, red); break;
+    case 35: gram_launch<4, 3>(n, nb1, nb2, Q1, Q2, G, ticket, s, red); break;
+    default: gram_launch<4, 4>(n, nb1, nb2, Q1, Q2, G, ticket, s, red); break;
+  }
+  EIG_HIP(hipGetLastError());
 }
 
 // ---------------------------------------------------------------------------------------------

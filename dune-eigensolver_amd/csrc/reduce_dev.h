@@ -143,4 +143,61 @@ __device__ bool grid_sum_n(double (&v)[NV], double *partials, unsigned *ticket, 
   return true;
 }
 
+// Two-level grid reduction of E values per workgroup (vals: the workgroup's block sums, in LDS).
+// The ticket's shards double as reduction groups: the workgroup completing shard s (members
+// bid = s, s + 8, ...) sums the shard's partials in bid order into spart[s]; the workgroup
+// completing the top sums the <= 8 shard sums in shard order into out (LDS) and returns true.
+// Deterministic like grid_sum_n, but the tail reads nblk / 8 partials per element in 8 workgroups
+// at once instead of nblk in one.  part: >= nblk E doubles, spart: >= 8 E doubles.
+template <int NT>
+__device__ bool grid_sum2(const double *vals, int E, double *part, double *spart, unsigned *t, unsigned bid,
+                          unsigned nblk, double *out)
+{
+  __shared__ unsigned s_flag;
+  for (int e = threadIdx.x; e < E; e += NT) st_sc1(&part[(size_t)bid * E + e], vals[e]);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  constexpr unsigned L = 32;
+  const unsigned shard = bid & 7u;
+  const unsigned shard_n = nblk / 8u + ((shard < nblk % 8u) ? 1u : 0u);
+  const unsigned nshards = nblk < 8u ? nblk : 8u;
+  if (threadIdx.x == 0)
+    s_flag = __hip_atomic_fetch_add(t + shard * L, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == shard_n - 1u;
+  __syncthreads();
+  if (!s_flag) return false;
+  for (int e = threadIdx.x; e < E; e += NT)
+  {
+    double acc = 0.0;
+    for (unsigned j0 = 0; j0 < shard_n; j0 += 16)
+    {
+      double v[16];  // 16 independent sc1 loads in flight, then the adds in bid order
+#pragma unroll
+      for (int u = 0; u < 16; ++u)
+        v[u] = (j0 + u < shard_n) ? ld_sc1(&part[(size_t)(shard + 8u * (j0 + u)) * E + e]) : 0.0;
+#pragma unroll
+      for (int u = 0; u < 16; ++u) acc += v[u];
+    }
+    st_sc1(&spart[(size_t)shard * E + e], acc);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    s_flag = __hip_atomic_fetch_add(t + 8u * L, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nshards - 1u;
+  __syncthreads();
+  if (!s_flag) return false;
+  for (int e = threadIdx.x; e < E; e += NT)
+  {
+    double v[8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) v[s] = (unsigned)s < nshards ? ld_sc1(&spart[(size_t)s * E + e]) : 0.0;
+    double acc = 0.0;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) acc += v[s];
+    out[e] = acc;
+  }
+  if (threadIdx.x == 0) ticket_reset(t);
+  __syncthreads();
+  return true;
+}
+
 }  // namespace eigmi

@@ -146,6 +146,40 @@ def c2(ctx):
          cpu_ms_per_iter=round((tc2 - tc1) * 1e3, 1), speedup=round((tc2 - tc1) / tg, 1))
 
 
+def gram(ctx):
+    """a6 panel Gram G = Q1^T Q2 (k_gram_mv8) and a9 orthonormalize_blocked at C2 size (n = 128^3):
+    per call, 50 back-to-back calls between two synchronisations; algorithmic bytes 8 n (m1 + m2)."""
+    n = int(os.environ.get("EIGMI_GRAM_N", str(128 ** 3)))
+    reps = 50
+    for m1, m2 in ((8, 8), (8, 16), (8, 24), (32, 32)):
+        Q1, Q2, G = ctx.array(oracle.random_mv8(n, m1, 1)), ctx.array(oracle.random_mv8(n, m2, 2)), ctx.zeros(m1 * m2)
+        eigmi.gram_mv8(ctx, n, m1, m2, Q1, Q2, G)
+        ctx.sync()
+        tg = min(wall(lambda: (eigmi.gram_mv8(ctx, n, m1, m2, Q1, Q2, G), None), reps)[0] for _ in range(3))
+        ctx.sync()
+        b = 8 * n * (m1 + m2)
+        emit(config=f"gram n={n}", op=f"gram_mv8 m1={m1} m2={m2}", us=round(tg * 1e6, 2), algorithmic_bytes=b,
+             GBs=round(b / tg / 1e9, 1), frac=round(b / tg / 1e9 / PEAK, 4))
+        Q1.free(), Q2.free(), G.free()
+    for m in (8, 32):
+        Qh = oracle.random_mv8(n, m, 1)
+        Q = ctx.array(Qh)
+
+        def ortho():
+            Q.upload(Qh)
+            ctx.sync()
+            t0 = time.perf_counter()
+            eigmi.orthonormalize_mv8(ctx, n, m, Q)
+            ctx.sync()
+            return time.perf_counter() - t0
+        ortho()
+        tg = min(ortho() for _ in range(5))
+        ob = eigmi.lib.eig_bytes_orthonormalize_blocked(n, m, 8)
+        emit(config=f"gram n={n}", op=f"orthonormalize_blocked (MGS) m={m}", gpu_ms=round(tg * 1e3, 3),
+             model_bytes=ob, model_GBs=round(ob / tg / 1e9, 1))
+        Q.free()
+
+
 def c3(ctx):
     N = 64
     rp, c, v = eigmi.gen_matrix(eigmi.GEN_Q1ELAST3D, N)

@@ -1,0 +1,10 @@
+#!/bin/bash
+# a6 Gram / a9 orthonormalize: parity tests, then the C2-size timing under a kernel trace.
+set -o pipefail
+TAG=${TAG:-r03b}
+OUT=gpurun_out/gram_$TAG
+mkdir -p $OUT
+timeout -k 10 300 python -u -m pytest tests/test_gpu_blas_mv8.py tests/test_gpu_drivers.py -q -s --timeout 120 --timeout-method thread > $OUT/tests.log 2>&1 && \
+cd /tmp && export TMPDIR=/tmp && cd - > /dev/null && \
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o trace -- \
+  python3 tools/bench_configs.py gram > $OUT/gram.jsonl 2> $OUT/gram.err
