@@ -212,7 +212,10 @@ def main():
     variant = args.variant
     trial = None
     if variant == "auto":
-        variant = "fused"
+        # one rank: EIG_LANCZOS_AUTO's choice for this image (fused where the pair gathers hit cache)
+        tw = eigmi.LanczosWorkspace(M, 1, seed=123, fused="auto")
+        variant = tw.variant
+        tw.close()
         if world > 1:
             trial = {}
             for var in ("fused", "pipelined"):

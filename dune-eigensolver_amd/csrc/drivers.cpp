@@ -1476,11 +1476,12 @@ extern "C" int eig_lanczos_create_ex(eig_mat_t A, int max_steps, const double *u
 {
   return guard(A ? A->ctx : nullptr, [&] {
     EIG_CHECK(A && out && max_steps >= 0, EIG_ERR_ARG, "eig_lanczos_create: bad argument");
-    EIG_CHECK((flags & ~(EIG_LANCZOS_FUSED | EIG_LANCZOS_PIPELINED)) == 0, EIG_ERR_ARG,
+    EIG_CHECK((flags & ~(EIG_LANCZOS_FUSED | EIG_LANCZOS_PIPELINED | EIG_LANCZOS_AUTO)) == 0, EIG_ERR_ARG,
               "eig_lanczos_create_ex: unknown flag");
-    EIG_CHECK((flags & (EIG_LANCZOS_FUSED | EIG_LANCZOS_PIPELINED)) != (EIG_LANCZOS_FUSED | EIG_LANCZOS_PIPELINED),
-              EIG_ERR_ARG, "eig_lanczos_create_ex: FUSED and PIPELINED are exclusive");
+    EIG_CHECK(__builtin_popcount(flags & (EIG_LANCZOS_FUSED | EIG_LANCZOS_PIPELINED | EIG_LANCZOS_AUTO)) <= 1,
+              EIG_ERR_ARG, "eig_lanczos_create_ex: FUSED, PIPELINED and AUTO are exclusive");
     check_lanczos_matrix(A);
+    if (flags & EIG_LANCZOS_AUTO) flags = fused_step_pays(*A) ? EIG_LANCZOS_FUSED : 0;
     eig_ctx_t ctx = A->ctx;
     EIG_HIP(hipSetDevice(ctx->device));
     hipStream_t s = ctx->stream;
@@ -1565,6 +1566,29 @@ extern "C" int eig_lanczos_step(eig_lanczos_t ws, int steps, int flags, eig_timi
     }
     for (auto &e : ev) (void)hipEventDestroy(e);
     if (ws->fused) fused_settle(*ws, target, nps, timing);
+  });
+}
+
+extern "C" int eig_lanczos_ws_info(eig_lanczos_t ws, int *variant, char *name, int name_len, int64_t *bytes)
+{
+  return guard(ws ? ws->A->ctx : nullptr, [&] {
+    EIG_CHECK(ws, EIG_ERR_ARG, "eig_lanczos_ws_info: null workspace");
+    if (variant) *variant = ws->pipe ? EIG_LANCZOS_PIPELINED : ws->fused ? EIG_LANCZOS_FUSED : 0;
+    std::string nm;
+    i64 b = 0;
+    if (ws->pipe)
+    {
+      nm = kernel_for(*ws->A, EIG_OP_SPMV) + "+k_lanczos_pipe";
+      b = 0;  // (two launches per step: see bench.py)
+    }
+    else
+      lanczos_kernel_info(*ws->A, ws->fused, nm, b);
+    if (name && name_len > 0)
+    {
+      std::strncpy(name, nm.c_str(), (size_t)name_len - 1);
+      name[name_len - 1] = 0;
+    }
+    if (bytes) *bytes = b;
   });
 }
 

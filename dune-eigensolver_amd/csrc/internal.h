@@ -299,6 +299,9 @@ bool launch_cheb_march(const eig_mat_s &M, i64 m, const double *Xk, double *Xold
                        double omega, double gamma, hipStream_t s);
 // Kernel a whole-matrix Lanczos step launch picks on this image, and its algorithmic bytes per launch.
 void lanczos_kernel_info(const eig_mat_s &A, bool fused, std::string &name, i64 &bytes);
+// Whether the fused step's (t, u) pair gathers are mostly cache hits on this image (band image or
+// stencil slices), i.e. whether EIG_LANCZOS_AUTO takes the fused step.
+bool fused_step_pays(const eig_mat_s &A);
 // Kernel family a whole-matrix launch of `op` (eig_mat_kernel_info's EIG_OP_*) picks on this image.
 std::string kernel_for(const eig_mat_s &A, int op);
 void launch_lanczos_spmv(const eig_mat_s &A, const double *u, const double *up, double *t, int j,

@@ -1907,6 +1907,13 @@ void lanczos_kernel_info(const eig_mat_s &A, bool fused, std::string &name, i64 
   }
 }
 
+bool fused_step_pays(const eig_mat_s &A)
+{
+  if (A.br != 1 || A.bc != 1) return false;
+  const int mode = image_mode(A);
+  return is_sym_mode(mode) || 2 * A.n_stencil_slices >= A.nslices;
+}
+
 std::string kernel_for(const eig_mat_s &A, int op)
 {
   const bool b1 = A.br == 1 && A.bc == 1;

@@ -30,6 +30,7 @@ LANCZOS_TIME_KERNELS = 1
 LANCZOS_TIME_DETAIL = 2
 LANCZOS_FUSED = 4
 LANCZOS_PIPELINED = 8
+LANCZOS_AUTO = 16
 IPC_HANDLE_BYTES = 64
 ALLREDUCE_KINDS = {0: "none", 1: "rccl", 2: "xgmi-mailbox", 3: "loopback"}
 
@@ -151,6 +152,7 @@ SIGNATURES = {
     "eig_lanczos_destroy": (_int, [_vp]),
     "eig_lanczos_info": (_int, [_vp, ctypes.POINTER(_int), ctypes.POINTER(_int)]),
     "eig_lanczos_capture": (_int, [_vp, _int, _int, ctypes.POINTER(_int)]),
+    "eig_lanczos_ws_info": (_int, [_vp, ctypes.POINTER(_int), ctypes.c_char_p, _int, ctypes.POINTER(_i64)]),
     "eig_lanczos_replay": (_int, [_vp, ctypes.POINTER(Timing)]),
     "eig_lu_create": (_int, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _int, ctypes.POINTER(_vp)]),
     "eig_lu_create_bcsr": (_int, [_vp, _i64, _int, _vp, _vp, _vp, ctypes.POINTER(_vp)]),
@@ -525,7 +527,10 @@ def standard_largest(A, shift, tol, maxiter, nev, seed=123, want_evec=True, verb
 
 
 def _lflags(fused, pipelined):
-    return (LANCZOS_PIPELINED if pipelined else LANCZOS_FUSED if fused else 0)
+    """fused: True / False / "auto" (EIG_LANCZOS_AUTO: fused where the image makes it pay)."""
+    if pipelined:
+        return LANCZOS_PIPELINED
+    return LANCZOS_AUTO if fused == "auto" else LANCZOS_FUSED if fused else 0
 
 
 def lanczos_run(A, steps, u0=None, seed=123, timed=False, fused=False, pipelined=False):
@@ -546,12 +551,21 @@ class LanczosWorkspace:
 
     def __init__(self, A, max_steps, u0=None, seed=123, fused=False, pipelined=False):
         self.A = A
-        self.fused = fused or pipelined
-        self.pipelined = pipelined
         h = _vp()
         A.ctx.check(lib.eig_lanczos_create_ex(A.h, max_steps, u0.ptr if u0 is not None else None, seed,
                                               _lflags(fused, pipelined), ctypes.byref(h)))
         self.h = h
+        self.variant, self.kernel, self.kernel_bytes = self.ws_info()
+        self.fused = self.variant in ("fused", "pipelined")
+        self.pipelined = self.variant == "pipelined"
+
+    def ws_info(self):
+        """(variant: "classic" | "fused" | "pipelined", step kernel, its algorithmic bytes per launch)."""
+        v, b = _int(0), _i64(0)
+        name = ctypes.create_string_buffer(96)
+        self.A.ctx.check(lib.eig_lanczos_ws_info(self.h, ctypes.byref(v), name, 96, ctypes.byref(b)))
+        return ({0: "classic", LANCZOS_FUSED: "fused", LANCZOS_PIPELINED: "pipelined"}[v.value],
+                name.value.decode(), b.value)
 
     def step(self, steps, timed=False):
         t = Timing()

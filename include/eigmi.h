@@ -277,7 +277,13 @@ enum eig_lanczos_flags {
    * z_k = S - c z_{k-1} (= A u_k) and t_k; so the previous step's 3-value allreduce (second RCCL
    * communicator, its own stream) overlaps the SpMV and the halo of t (8 B per row, not 16).
    * Costs 56 B per row more than the fused step on one GPU.  Exclusive with EIG_LANCZOS_FUSED. */
-  EIG_LANCZOS_PIPELINED = 8
+  EIG_LANCZOS_PIPELINED = 8,
+  /* Pick per matrix image at creation: EIG_LANCZOS_FUSED where its pair gathers are cache hits (the
+   * symmetric band image, or a stencil-sliced SELL image), else the two-kernel step (a scattered
+   * general matrix: the fused step gathers 16-B (t, u) pairs at every column, twice the classic
+   * step's gather bytes -- 634 vs 427 us per step at 256^3 scrambled + RCM).
+   * eig_lanczos_ws_info reports the choice. */
+  EIG_LANCZOS_AUTO = 16
 };
 int eig_lanczos_run(eig_mat_t A, int steps, const double *u0, unsigned seed, int flags,
                     double *alpha_host, double *beta_host, eig_timing *timing);
@@ -298,6 +304,10 @@ int eig_lanczos_destroy(eig_lanczos_t ws);
 /* Logical steps taken and kernel launches issued (fused: steps + repairs + forced final repairs;
  * two-kernel: = steps). */
 int eig_lanczos_info(eig_lanczos_t ws, int *steps, int *launches);
+/* The recurrence the workspace runs (*variant: 0 two-kernel, EIG_LANCZOS_FUSED or
+ * EIG_LANCZOS_PIPELINED, after EIG_LANCZOS_AUTO resolved it), its step kernel (name, at most
+ * name_len bytes) and that kernel's algorithmic bytes per launch (as eig_lanczos_kernel_info). */
+int eig_lanczos_ws_info(eig_lanczos_t ws, int *variant, char *name, int name_len, int64_t *bytes);
 /* hipGraph form of eig_lanczos_step: capture the next `steps` steps (kernels, halo exchange,
  * allreduces; plus per-step kernel events when flags has EIG_LANCZOS_TIME_KERNELS) into one
  * graph and instantiate it -- nothing runs yet.  eig_lanczos_replay launches it once

@@ -71,3 +71,28 @@ def test_general_mv_bitwise_256(ctx):
     x = np.random.default_rng(11).standard_normal(A.n)
     assert np.array_equal(M.mv_host(x), oracle.csr_mv(A, x))
     M.close()
+
+
+def test_lanczos_auto_picks_per_image(ctx, s64):
+    """EIG_LANCZOS_AUTO: the scrambled matrix takes the two-kernel step (its
+    16-B pair gathers would double the gather bytes), the 7-point band image the fused step; the
+    recurrence is then bitwise the explicitly requested one."""
+    M = eigmi.Matrix.from_bcsr(ctx, s64.rowptr, s64.col, s64.val)
+    ws = eigmi.LanczosWorkspace(M, 30, seed=123, fused="auto")
+    assert ws.variant == "classic" and ws.kernel == "k_lanczos_spmv_b1"
+    ws.step(30)
+    a, b = ws.tridiag()
+    ws.close()
+    ref = eigmi.LanczosWorkspace(M, 30, seed=123)
+    ref.step(30)
+    ra, rb = ref.tridiag()
+    ref.close()
+    assert np.array_equal(a, ra) and np.array_equal(b, rb)
+    M.close()
+    P = oracle.poisson3d(32)
+    Mp = eigmi.Matrix.from_bcsr(ctx, P.rowptr, P.col, P.val)
+    ws = eigmi.LanczosWorkspace(Mp, 30, seed=123, fused="auto")
+    assert ws.variant == "fused" and ws.kernel == Mp.lanczos_kernel_info(True)[0]
+    assert ws.kernel_bytes == Mp.lanczos_kernel_info(True)[1]
+    ws.close()
+    Mp.close()
