@@ -501,6 +501,15 @@ extern "C" int eig_comm_info(eig_ctx_t ctx, int *nranks, int *rank, int *allredu
   });
 }
 
+extern "C" int eig_mat_tune(eig_mat_t A, int key, int value)
+{
+  return guard(A ? A->ctx : nullptr, [&] {
+    EIG_CHECK(A && value >= 0, EIG_ERR_ARG, "eig_mat_tune: bad argument");
+    EIG_CHECK(key == EIG_TUNE_MARCH_RUNS, EIG_ERR_ARG, "eig_mat_tune: unknown key");
+    A->tune_march_runs = value;
+  });
+}
+
 extern "C" int eig_comm_counters(eig_ctx_t ctx, int64_t out[4])
 {
   return guard(ctx, [&] {

@@ -1113,7 +1113,7 @@ struct LanczosBufs {
   // steps: logical steps; launches: fused launches (a step plus at most one repair each, plus the
   // forced final repair)
   explicit LanczosBufs(int steps, int launches = 0)
-      : scal((size_t)(4 * (steps + 2) + 5 * (launches + 2) + 8) * sizeof(double)),
+      : scal((size_t)(4 * (steps + 2) + 6 * (launches + 2) + 8) * sizeof(double)),
         ictl((size_t)2 * (launches + 2) * sizeof(int))
   {
     double *b = scal.d();
@@ -1125,6 +1125,7 @@ struct LanczosBufs {
     st.aux = st.fred + 3 * (launches + 2);
     carry = st.aux + 2 * (launches + 2);
     st.mu2 = carry + 4;
+    st.pn = st.mu2 + 4;
     st.ctl = static_cast<int *>(ictl.p);
   }
 };

@@ -205,6 +205,7 @@ struct eig_mat_s {
   // ghost columns and are marched while the halo is in flight; march_bnd lists every slice outside
   // them (the boundary launch after the exchange).  mz1 <= mz0: no split.
   eigmi::i64 mz0 = 0, mz1 = 0;
+  int tune_march_runs = 0;  // eig_mat_tune(EIG_TUNE_MARCH_RUNS): plane runs per column, 0 = automatic
   // Box-stencil image for the 32-column SpMM / Chebyshev kernel (k_box.hip): box_state 0 = not
   // examined yet, 1 = built, -1 = the band is not a 3-D box stencil; box_val[k n + r] = the entry of
   // row r at sym_off[k]; grid nx x ny x nz; per offset its plane step and halo-tile row shift
@@ -260,6 +261,8 @@ struct LanczosState {
   int *ctl;       // ctl[2L], ctl[2L+1] = logical step and mode at the start of launch L
   double *aux;    // aux[2L], aux[2L+1] = (rn, rm) a repair hands to launch L
   double *mu2;    // (sum of the diagonal, rows), allreduced: the step's shift mu = mu2[0] / mu2[1]
+  double *pn;     // pn[L] = nsum[j - 1] for launch L at step j (written by launch L - 1), so a launch's
+                  // prologue loads are independent of each other (one memory round trip)
 };
 enum { kFusedModeStep = 0, kFusedModePost = 1, kFusedModeHalt = 2 };  // ctl[2L + 1]
 struct FusedLaunch {
@@ -330,6 +333,9 @@ void launch_dot_diag_mv8(i64 n, i64 m, const double *Q1, const double *Q2, doubl
 void launch_gram_mv8(i64 n, i64 m1, i64 m2, const double *Q1, const double *Q2, double *G, int ticket,
                      hipStream_t s, ReduceWS red);
 int gram_mv8_chunks(i64 m1, i64 m2);  // tickets one launch_gram_mv8 takes
+// The same Gram on window-layout panels (column blocks ld rows apart, pointers at owned row 0).
+void launch_gram_panel(eig_ctx_t ctx, i64 n, i64 ld, i64 m1, i64 m2, const double *Q1, const double *Q2, double *G,
+                       hipStream_t s);
 // Block Gram-Schmidt building blocks, see k_mv8.hip.
 void launch_mgs_pass(i64 n, double *Qb, int k, double *S, int ticket, hipStream_t s, ReduceWS red);
 // Whole column MGS of one 8-column block in one workgroup (n <= 4096, one rank); false = not taken.
@@ -369,6 +375,8 @@ void launch_cheb_init(i64 n, i64 ld, i64 own, i64 m, const double *B, const doub
 // G (m1 x m2, row-major, device) = Q1^T Q2 over n rows; Q1, Q2 address owned row 0 (pointer + 8 own).
 void launch_panel_gram(eig_ctx_t ctx, i64 n, i64 ld, i64 m1, i64 m2, const double *Q1, const double *Q2, double *G,
                        hipStream_t s);
+void launch_panel_gram_2stage(eig_ctx_t ctx, i64 n, i64 ld, i64 m1, i64 m2, const double *Q1, const double *Q2,
+                              double *G, hipStream_t s);
 // Y = beta Y + alpha Q S over n rows (owned-row pointers), m2 <= 32.
 void launch_panel_update(i64 n, i64 ldq, i64 ldy, i64 m1, i64 m2, const double *Q, const double *S, double alpha,
                          double beta, double *Y, hipStream_t s);

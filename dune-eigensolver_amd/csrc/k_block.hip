@@ -616,8 +616,17 @@ void panel_gram(eig_ctx_t ctx, i64 n, i64 ld, i64 m1, i64 m2, const double *Q1, 
 }
 }  // namespace
 
+// The block Lanczos panel products run on the a6 Gram kernel (k_mv8.hip launch_gram_panel: paired
+// 16-column tiles, one launch with its deterministic two-level reduction); the two-launch form
+// above (k_panel_gram_part + k_panel_gram_reduce) is kept as launch_panel_gram_2stage for A/B.
 void launch_panel_gram(eig_ctx_t ctx, i64 n, i64 ld, i64 m1, i64 m2, const double *Q1, const double *Q2, double *G,
                        hipStream_t s)
+{
+  launch_gram_panel(ctx, n, ld, m1, m2, Q1, Q2, G, s);
+}
+
+void launch_panel_gram_2stage(eig_ctx_t ctx, i64 n, i64 ld, i64 m1, i64 m2, const double *Q1, const double *Q2,
+                              double *G, hipStream_t s)
 {
   if (m1 <= 32)
     panel_gram<2, 2>(ctx, n, ld, m1, m2, Q1, Q2, G, s);

@@ -140,95 +140,111 @@ void launch_dot_diag_mv8(i64 n, i64 m, const double *Q1, const double *Q2, doubl
 // ---------------------------------------------------------------------------------------------
 // a6: G = Q1^T Q2 on MFMA (dot_products_all_blocked, kernels_cpp.hh:58-96), v_mfma_f64_16x16x4f64.
 //
-// One MultiVector column block is 8 columns wide, the MFMA tile 16: instead of padding half the
-// lanes, a tile takes 8 ROWS of one block -- lane l (k = l>>4, i = l&15) supplies
-// A[i][k] = Q1(8g + k + 4 (i>>3), i & 7) and B[k][j] = Q2(8g + k + 4 (j>>3), j & 7), so one 8-B load
-// per lane reads 8 whole 64-B rows (512 contiguous bytes) and every loaded value is used.  The
-// products with i>>3 == j>>3 are the two 8x8 quadrants on the tile diagonal (rows 8g..8g+3 and
-// 8g+4..8g+7); G's 8x8 block is their sum (the off-diagonal quadrants are discarded).
-// A workgroup takes NB1 blocks of Q1 x NB2 blocks of Q2 for its row range (every operand loaded
-// once for NB2 / NB1 MFMAs: NB1 x NB2 independent accumulator chains), U 8-row groups per wave
-// iteration with all loads issued before the MFMAs.  grid.y = chunks of the block grid (each
-// panel streams once per chunk of the other).  Reduction: quadrants folded by a lane shuffle,
-// the 4 waves summed in LDS, then grid_sum2 (two-level, deterministic).
+// The MFMA tile is 16 columns wide, a MultiVector column block 8.  Two operand forms, neither with
+// padding lanes (lane l: k = l>>4, i = l&15; one 8-B load per lane and operand, 512 contiguous
+// bytes per wave instruction):
+//  * doubled rows (DR = 1; any block count): a "unit" is ONE block and a tile takes 8 ROWS,
+//    A[i][k] = Q1(8g + k + 4 (i>>3), i & 7), B[k][j] = Q2(8g + k + 4 (j>>3), j & 7); the products
+//    with i>>3 == j>>3 are the two 8x8 quadrants on the tile diagonal (rows 8g..8g+3 and
+//    8g+4..8g+7) and the block of G is their sum (the off-diagonal quadrants are discarded);
+//  * paired blocks (DR = 0; even block counts): a unit is TWO blocks side by side and a tile takes
+//    4 rows, A[i][k] = Q1(4g + k, 16 u + i) -- the whole 16 x 16 tile is output.
+// A workgroup takes T1 units of Q1 x T2 units of Q2 over its rows (each operand loaded once for
+// T2 / T1 MFMAs: T1 x T2 independent accumulator chains), U row groups per wave iteration with all
+// loads issued before the MFMAs; grid.y = chunks of the unit grid (each panel streams once per
+// chunk of the other).  Column blocks sit ld rows apart (ld = n for a plain MultiVector, the
+// window for the block Lanczos panels).  Reduction: (DR) quadrants folded by a lane shuffle, the 4
+// waves summed in LDS, then grid_sum2 across workgroups (two-level, deterministic).
 // ---------------------------------------------------------------------------------------------
 constexpr int kGramThreads = 256;
 
-template <int NB1, int NB2, int U>
-__global__ __launch_bounds__(kGramThreads) void k_gram_mv8(i64 n, int nb1, int nb2, int nby2,
+template <int DR, int T1, int T2, int U>
+__global__ __launch_bounds__(kGramThreads) void k_gram_mv8(i64 n, i64 ld1, i64 ld2, int nb1, int nb2, int nby2,
                                                            const double *__restrict__ Q1, const double *__restrict__ Q2,
                                                            double *__restrict__ G, double *partials, unsigned *tickets)
 {
-  constexpr int E = NB1 * NB2 * 64;
+  constexpr int TE = DR ? 64 : 256;  // output elements per unit pair
+  constexpr int E = T1 * T2 * TE;
   constexpr int W = kGramThreads / 64;
+  constexpr int RG = DR ? 8 : 4;     // rows per group (one MFMA per unit pair)
   __shared__ double sh[W][E];
   __shared__ double tot[E];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int cy1 = blockIdx.y / nby2, cy2 = blockIdx.y % nby2;
   const int k = lane >> 4, i = lane & 15;
-  const int rl = k + 4 * (i >> 3);  // row inside the 8-row group
-  const double *a[NB1];
-  const double *b[NB2];
-  bool aok[NB1], bok[NB2];
+  const int rl = DR ? k + 4 * (i >> 3) : k;  // row inside the group
+  const double *a[T1];
+  const double *b[T2];
+  bool aok[T1], bok[T2];
 #pragma unroll
-  for (int t = 0; t < NB1; ++t)
+  for (int t = 0; t < T1; ++t)
   {
-    const int blk = cy1 * NB1 + t;
+    const int blk = DR ? cy1 * T1 + t : 2 * (cy1 * T1 + t) + (i >> 3);
     aok[t] = blk < nb1;
-    a[t] = Q1 + (i64)(aok[t] ? blk : 0) * n * 8 + (i & 7);
+    a[t] = Q1 + (aok[t] ? blk : 0) * ld1 * 8 + (i & 7);
   }
 #pragma unroll
-  for (int u = 0; u < NB2; ++u)
+  for (int u = 0; u < T2; ++u)
   {
-    const int blk = cy2 * NB2 + u;
+    const int blk = DR ? cy2 * T2 + u : 2 * (cy2 * T2 + u) + (i >> 3);
     bok[u] = blk < nb2;
-    b[u] = Q2 + (i64)(bok[u] ? blk : 0) * n * 8 + (i & 7);
+    b[u] = Q2 + (bok[u] ? blk : 0) * ld2 * 8 + (i & 7);
   }
-  d4 acc[NB1][NB2];
+  d4 acc[T1][T2];
 #pragma unroll
-  for (int t = 0; t < NB1; ++t)
+  for (int t = 0; t < T1; ++t)
 #pragma unroll
-    for (int u = 0; u < NB2; ++u) acc[t][u] = d4{0.0, 0.0, 0.0, 0.0};
-  const i64 ng = (n + 7) >> 3;
+    for (int u = 0; u < T2; ++u) acc[t][u] = d4{0.0, 0.0, 0.0, 0.0};
+  const i64 ng = (n + RG - 1) / RG;
   const i64 ws = (i64)gridDim.x * W;
   for (i64 g0 = (i64)blockIdx.x * W + wave; g0 < ng; g0 += U * ws)
   {
-    double av[U][NB1], bv[U][NB2];
+    double av[U][T1], bv[U][T2];
 #pragma unroll
     for (int v = 0; v < U; ++v)
     {
-      const i64 r = (g0 + v * ws) * 8 + rl;
+      const i64 r = (g0 + v * ws) * RG + rl;
       const bool ok = r < n;  // (also false for groups past ng)
       const i64 rr = ok ? r : 0;
 #pragma unroll
-      for (int t = 0; t < NB1; ++t) av[v][t] = a[t][rr * 8];
+      for (int t = 0; t < T1; ++t) av[v][t] = a[t][rr * 8];
 #pragma unroll
-      for (int u = 0; u < NB2; ++u) bv[v][u] = b[u][rr * 8];
+      for (int u = 0; u < T2; ++u) bv[v][u] = b[u][rr * 8];
 #pragma unroll
-      for (int t = 0; t < NB1; ++t) av[v][t] = (ok && aok[t]) ? av[v][t] : 0.0;
+      for (int t = 0; t < T1; ++t) av[v][t] = (ok && aok[t]) ? av[v][t] : 0.0;
 #pragma unroll
-      for (int u = 0; u < NB2; ++u) bv[v][u] = (ok && bok[u]) ? bv[v][u] : 0.0;
+      for (int u = 0; u < T2; ++u) bv[v][u] = (ok && bok[u]) ? bv[v][u] : 0.0;
     }
 #pragma unroll
     for (int v = 0; v < U; ++v)
 #pragma unroll
-      for (int t = 0; t < NB1; ++t)
+      for (int t = 0; t < T1; ++t)
 #pragma unroll
-        for (int u = 0; u < NB2; ++u)
+        for (int u = 0; u < T2; ++u)
           acc[t][u] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[v][t], bv[v][u], acc[t][u], 0, 0, 0);
   }
-  // lane holds C[k + 4q][i]; for i < 8 and q < 2, C[k + 4q][i] + C[k + 4q + 8][i + 8] (lane + 8,
-  // register q + 2) is G(k + 4q, i) of this block pair
+  // lane holds C[k + 4q][i] of each tile
 #pragma unroll
-  for (int t = 0; t < NB1; ++t)
+  for (int t = 0; t < T1; ++t)
 #pragma unroll
-    for (int u = 0; u < NB2; ++u)
-#pragma unroll
-      for (int q = 0; q < 2; ++q)
+    for (int u = 0; u < T2; ++u)
+    {
+      if constexpr (DR)
       {
-        const double hi = __shfl_down(acc[t][u][q + 2], 8, 64);
-        if (i < 8) sh[wave][(t * NB2 + u) * 64 + (k + 4 * q) * 8 + i] = acc[t][u][q] + hi;
+        // for i < 8, q < 2: C[k + 4q][i] + C[k + 4q + 8][i + 8] (lane + 8, register q + 2)
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+        {
+          const double hi = __shfl_down(acc[t][u][q + 2], 8, 64);
+          if (i < 8) sh[wave][(t * T2 + u) * 64 + (k + 4 * q) * 8 + i] = acc[t][u][q] + hi;
+        }
       }
+      else
+      {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) sh[wave][(t * T2 + u) * 256 + (k + 4 * q) * 16 + i] = acc[t][u][q];
+      }
+    }
   __syncthreads();
   for (int e = threadIdx.x; e < E; e += kGramThreads)
   {
@@ -244,62 +260,107 @@ __global__ __launch_bounds__(kGramThreads) void k_gram_mv8(i64 n, int nb1, int n
   if (!grid_sum2<kGramThreads>(tot, E, part, spart, tickets + (size_t)blockIdx.y * kTicketStride, blockIdx.x,
                                gridDim.x, sh[0]))
     return;
-  const i64 m2 = (i64)nb2 * 8;
+  const i64 m1 = (i64)nb1 * 8, m2 = (i64)nb2 * 8;
   for (int e = threadIdx.x; e < E; e += kGramThreads)
   {
-    const int tu = e >> 6, t = tu / NB2, u = tu % NB2, row = (e >> 3) & 7, col = e & 7;
-    if (cy1 * NB1 + t < nb1 && cy2 * NB2 + u < nb2) G[((i64)(cy1 * NB1 + t) * 8 + row) * m2 + (i64)(cy2 * NB2 + u) * 8 + col] = sh[0][e];
+    const int tu = e / TE, t = tu / T2, u = tu % T2, el = e % TE;
+    const int TW = DR ? 8 : 16;  // tile width in G
+    const i64 row = (i64)(cy1 * T1 + t) * TW + el / TW, col = (i64)(cy2 * T2 + u) * TW + el % TW;
+    if (row < m1 && col < m2) G[row * m2 + col] = sh[0][e];
   }
 }
 
 namespace {
-template <int NB1, int NB2>
-void gram_launch(i64 n, int nb1, int nb2, const double *Q1, const double *Q2, double *G, int ticket, hipStream_t s,
-                 ReduceWS red)
+struct GramShape {
+  int dr, t1, t2, ny1, ny2;
+};
+// Operand form and unit tiling of an m1 x m2 Gram: paired blocks when both block counts are even
+// (full tiles), doubled rows otherwise; up to 4 x 4 units (doubled) or 4 x 2 pairs per workgroup.
+GramShape gram_shape(i64 m1, i64 m2)
 {
-  constexpr int U = (NB1 + NB2) <= 2 ? 8 : (NB1 + NB2) <= 4 ? 4 : 2;
-  constexpr int E = NB1 * NB2 * 64;
-  const int ny1 = (nb1 + NB1 - 1) / NB1, ny2 = (nb2 + NB2 - 1) / NB2, ny = ny1 * ny2;
-  EIG_CHECK(ticket + ny <= kNumTickets, EIG_ERR_ARG, "gram_mv8: too many output chunks");
-  const i64 ng = (n + 7) / 8;
-  // about 2 resident workgroups per CU, at least one U-group batch per wave
-  i64 gx = std::min<i64>(512, std::max<i64>(1, (ng + 4 * U - 1) / (4 * U)));
-  while ((gx * ny + 8 * ny) * E > (i64)kMaxRedBlocks * kMaxRedVals && gx > 1) gx /= 2;
-  hipLaunchKernelGGL((k_gram_mv8<NB1, NB2, U>), dim3((unsigned)gx, (unsigned)ny), dim3(kGramThreads), 0, s, n, nb1,
-                     nb2, ny2, Q1, Q2, G, red.partials, red.ticket(ticket));
+  const int nb1 = (int)(m1 / 8), nb2 = (int)(m2 / 8);
+  GramShape g;
+  g.dr = (nb1 % 2 || nb2 % 2) ? 1 : 0;
+  const int u1 = g.dr ? nb1 : nb1 / 2, u2 = g.dr ? nb2 : nb2 / 2;
+  if (g.dr)
+  {
+    g.t1 = u1 >= 4 ? 4 : u1 >= 2 ? 2 : 1;
+    g.t2 = u2 >= 4 ? 4 : std::max(1, u2);
+  }
+  else
+  {
+    g.t2 = u2 >= 2 ? 2 : 1;
+    g.t1 = u1 >= 4 ? 4 : u1 >= 2 ? 2 : 1;
+  }
+  g.ny1 = (u1 + g.t1 - 1) / g.t1;
+  g.ny2 = (u2 + g.t2 - 1) / g.t2;
+  return g;
+}
+
+template <int DR, int T1, int T2>
+void gram_launch(i64 n, i64 ld1, i64 ld2, int nb1, int nb2, const GramShape &gs, const double *Q1, const double *Q2,
+                 double *G, unsigned *tickets, double *partials, i64 cap, hipStream_t s)
+{
+  constexpr int U = (T1 + T2) <= 2 ? 8 : (T1 + T2) <= 4 ? 4 : 2;
+  constexpr int E = T1 * T2 * (DR ? 64 : 256);
+  const int ny = gs.ny1 * gs.ny2;
+  const i64 ng = (n + (DR ? 7 : 3)) / (DR ? 8 : 4);
+  // about 4 resident workgroups per CU, at least one U-group batch per wave
+  i64 gx = std::min<i64>(1024, std::max<i64>(1, (ng + 4 * U - 1) / (4 * U)));
+  while ((gx * ny + 8 * ny) * E > cap && gx > 1) gx /= 2;
+  EIG_CHECK((gx * ny + 8 * ny) * E <= cap, EIG_ERR_ARG, "gram: output too large for the reduction workspace");
+  hipLaunchKernelGGL((k_gram_mv8<DR, T1, T2, U>), dim3((unsigned)gx, (unsigned)ny), dim3(kGramThreads), 0, s, n, ld1,
+                     ld2, nb1, nb2, gs.ny2, Q1, Q2, G, partials, tickets);
+}
+
+void gram_dispatch(i64 n, i64 ld1, i64 ld2, i64 m1, i64 m2, const double *Q1, const double *Q2, double *G,
+                   unsigned *tickets, double *partials, i64 cap, hipStream_t s)
+{
+  EIG_CHECK(m1 > 0 && m2 > 0 && m1 % 8 == 0 && m2 % 8 == 0, EIG_ERR_ARG, "gram_mv8: m1, m2 multiples of 8");
+  const int nb1 = (int)(m1 / 8), nb2 = (int)(m2 / 8);
+  const GramShape gs = gram_shape(m1, m2);
+#define EIG_GRAM(D_, A_, B_)                                                                           \
+  if (gs.dr == D_ && gs.t1 == A_ && gs.t2 == B_)                                                       \
+  {                                                                                                    \
+    gram_launch<D_, A_, B_>(n, ld1, ld2, nb1, nb2, gs, Q1, Q2, G, tickets, partials, cap, s);          \
+    EIG_HIP(hipGetLastError());                                                                        \
+    return;                                                                                            \
+  }
+  EIG_GRAM(1, 1, 1) EIG_GRAM(1, 1, 2) EIG_GRAM(1, 1, 3) EIG_GRAM(1, 1, 4)
+  EIG_GRAM(1, 2, 1) EIG_GRAM(1, 2, 2) EIG_GRAM(1, 2, 3) EIG_GRAM(1, 2, 4)
+  EIG_GRAM(1, 4, 1) EIG_GRAM(1, 4, 2) EIG_GRAM(1, 4, 3) EIG_GRAM(1, 4, 4)
+  EIG_GRAM(0, 1, 1) EIG_GRAM(0, 1, 2) EIG_GRAM(0, 2, 1) EIG_GRAM(0, 2, 2) EIG_GRAM(0, 4, 1) EIG_GRAM(0, 4, 2)
+#undef EIG_GRAM
+  throw Error(EIG_ERR_ARG, "gram: no kernel for this shape");
 }
 }  // namespace
 
 int gram_mv8_chunks(i64 m1, i64 m2)
 {
-  const i64 nb1 = m1 / 8, nb2 = m2 / 8;
-  const i64 NB1 = nb1 >= 4 ? 4 : nb1 >= 2 ? 2 : 1, NB2 = nb2 >= 4 ? 4 : std::max<i64>(1, nb2);
-  return (int)(((nb1 + NB1 - 1) / NB1) * ((nb2 + NB2 - 1) / NB2));
+  const GramShape gs = gram_shape(m1, m2);
+  return gs.ny1 * gs.ny2;
 }
 
 void launch_gram_mv8(i64 n, i64 m1, i64 m2, const double *Q1, const double *Q2, double *G, int ticket,
                      hipStream_t s, ReduceWS red)
 {
-  EIG_CHECK(m1 > 0 && m2 > 0 && m1 % 8 == 0 && m2 % 8 == 0, EIG_ERR_ARG, "gram_mv8: m1, m2 multiples of 8");
-  const int nb1 = (int)(m1 / 8), nb2 = (int)(m2 / 8);
-  const int NB1 = nb1 >= 4 ? 4 : nb1 >= 2 ? 2 : 1;
-  const int NB2 = nb2 >= 4 ? 4 : nb2;
-  switch (NB1 * 8 + NB2)
-  {
-    case 9: gram_launch<1, 1>(n, nb1, nb2, Q1, Q2, G, ticket, s, red); break;
-    case 10: gram_launch<1, 2>(n, nb1, nb2, Q1, Q2, G, ticket, s, red); break;
-    case 11: gram_launch<1, 3>(n, nb1, nb2, Q1, Q2, G, ticket, s, red); break;
-    case 12: gram_launch<1, 4>(n, nb1, nb2, Q1, Q2, G, ticket, s, red); break;
-    case 17: gram_launch<2, 1>(n, nb1, nb2, Q1, Q2, G, ticket, s, red); break;
-    case 18: gram_launch<2, 2>(n, nb1, nb2, Q1, Q2, G, ticket, s, red); break;
-    case 19: gram_launch<2, 3>(n, nb1, nb2, Q1, Q2, G, ticket, s, red); break;
-    case 20: gram_launch<2, 4>(n, nb1, nb2, Q1, Q2, G, ticket, s, red); break;
-    case 33: gram_launch<4, 1>(n, nb1, nb2, Q1, Q2, G, ticket, s, red); break;
-    case 34: gram_launch<4, 2>(n, nb1, nb2, Q1, Q2, G, ticket, s, red); break;
-    case 35: gram_launch<4, 3>(n, nb1, nb2, Q1, Q2, G, ticket, s, red); break;
-    default: gram_launch<4, 4>(n, nb1, nb2, Q1, Q2, G, ticket, s, red); break;
-  }
-  EIG_HIP(hipGetLastError());
+  EIG_CHECK(ticket + gram_mv8_chunks(m1, m2) <= kNumTickets, EIG_ERR_ARG, "gram_mv8: too many output chunks");
+  gram_dispatch(n, n, n, m1, m2, Q1, Q2, G, red.ticket(ticket), red.partials, (i64)kMaxRedBlocks * kMaxRedVals, s);
+}
+
+// Window-layout panels (block Lanczos, blanczos.cpp): column blocks ld rows apart; partials in a
+// context buffer sized for the launch, tickets from the context pool (the panel products run alone
+// on the stream, like every other reduction)
+void launch_gram_panel(eig_ctx_t ctx, i64 n, i64 ld, i64 m1, i64 m2, const double *Q1, const double *Q2, double *G,
+                       hipStream_t s)
+{
+  const int chunks = gram_mv8_chunks(m1, m2);
+  EIG_CHECK(chunks <= kNumTickets, EIG_ERR_ARG, "panel gram: too many output chunks");
+  const GramShape gs = gram_shape(m1, m2);
+  const i64 E = (i64)gs.t1 * gs.t2 * (gs.dr ? 64 : 256);
+  const i64 cap = (1024 + 8) * (i64)chunks * E;
+  double *part = (double *)ctx_buffer(ctx, 8, (size_t)cap * sizeof(double));  // slot 8: panel partials
+  gram_dispatch(n, ld, ld, m1, m2, Q1, Q2, G, ctx->red.ticket(0), part, cap, s);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -559,45 +620,53 @@ void launch_apply_upper(i64 n, double *Qb, const double *U, hipStream_t s)
 // ---------------------------------------------------------------------------------------------
 // Later-block projection (kernels_cpp.hh:335-348): Q_rest(i, j) -= sum_k S[k][j] Q_k(i, k), k
 // ascending, element by element in the reference order.  S is 8 x mrest row-major (the Gram
-// Q_k^T Q_rest).  One thread per (row, column block of Q_rest).
+// Q_k^T Q_rest).  One thread per row: Q_k's row is loaded once and every later block is updated in
+// turn, so S is read with wave-uniform addresses (scalar loads, SGPR operands).
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kStreamThreads) void k_project(i64 n, i64 mrest, const double *__restrict__ Qk,
+__global__ __launch_bounds__(kStreamThreads) void k_project(i64 n, int nb, const double *__restrict__ Qk,
                                                             double *__restrict__ Qrest, const double *__restrict__ S)
 {
-  const int nb = (int)(mrest / 8);
-  const i64 total = n * nb;
-  for (i64 idx = (i64)blockIdx.x * kStreamThreads + threadIdx.x; idx < total; idx += (i64)gridDim.x * kStreamThreads)
+  const int mrest = nb * 8;
+  for (i64 i = (i64)blockIdx.x * kStreamThreads + threadIdx.x; i < n; i += (i64)gridDim.x * kStreamThreads)
   {
-    const int b = (int)(idx / n);
-    const i64 i = idx - (i64)b * n;
-    double qk[8], qj[8];
+    double qk[8];
     const double2 *rk = reinterpret_cast<const double2 *>(Qk + i * 8);
-    double2 *rj = reinterpret_cast<double2 *>(Qrest + ((i64)b * n + i) * 8);
 #pragma unroll
     for (int h = 0; h < 4; ++h)
     {
-      const double2 x = rk[h], y = rj[h];
+      const double2 x = rk[h];
       qk[2 * h] = x.x;
       qk[2 * h + 1] = x.y;
-      qj[2 * h] = y.x;
-      qj[2 * h + 1] = y.y;
     }
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
+    for (int b = 0; b < nb; ++b)
     {
+      double qj[8];
+      double2 *rj = reinterpret_cast<double2 *>(Qrest + ((i64)b * n + i) * 8);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) qj[j] -= S[k * mrest + b * 8 + j] * qk[k];
+      for (int h = 0; h < 4; ++h)
+      {
+        const double2 y = rj[h];
+        qj[2 * h] = y.x;
+        qj[2 * h + 1] = y.y;
+      }
+      const double *Sb = S + b * 8;
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+      {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) qj[j] -= Sb[k * mrest + j] * qk[k];
+      }
+#pragma unroll
+      for (int h = 0; h < 4; ++h) rj[h] = make_double2(qj[2 * h], qj[2 * h + 1]);
     }
-#pragma unroll
-    for (int h = 0; h < 4; ++h) rj[h] = make_double2(qj[2 * h], qj[2 * h + 1]);
   }
 }
 
 void launch_project(i64 n, i64 mrest, const double *Qk, double *Qrest, const double *S, hipStream_t s)
 {
   if (mrest <= 0) return;
-  hipLaunchKernelGGL(k_project, dim3(grid_for(n * (mrest / 8), kStreamThreads * 4, kStreamBlocks)),
-                     dim3(kStreamThreads), 0, s, n, mrest, Qk, Qrest, S);
+  hipLaunchKernelGGL(k_project, dim3(grid_for(n, kStreamThreads * 2, kStreamBlocks)), dim3(kStreamThreads), 0, s, n,
+                     (int)(mrest / 8), Qk, Qrest, S);
 }
 
 // *normmax = max(*normmax, max over S (rows x cols, row-major) [strict upper triangle only]).

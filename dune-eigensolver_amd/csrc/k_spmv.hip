@@ -619,6 +619,7 @@ struct FusedArgs {
   int *ctl;                     // per launch: (logical step j, mode) at its start
   double *aux;                  // per launch: (rn, rm) handed from a repair to the next launch
   const double *mu2;            // (sum of the diagonal, rows), allreduced: mu = mu2[0] / mu2[1]
+  double *pn;                   // per launch: nsum[j - 1] of its step (LanczosState::pn)
   int L;                        // launch index
   int force;                    // 1: repair even if the prediction is sound (exact final beta)
 };
@@ -633,9 +634,15 @@ struct FusedStep {
 __device__ __forceinline__ FusedStep fused_begin(const FusedArgs &f)
 {
   FusedStep s;
-  s.j = f.ctl[2 * f.L];
-  const int mode = f.ctl[2 * f.L + 1];
-  s.mu = f.mu2[0] / f.mu2[1];
+  // every operand the prologue may need, loaded together (addresses depend on L only: one memory
+  // round trip before the launch's streams start, instead of ctl -> nsum[j - 1])
+  const int cj = f.ctl[2 * f.L], mode = f.ctl[2 * f.L + 1];
+  const double mu0 = f.mu2[0], mu1 = f.mu2[1];
+  const int Lp = f.L > 0 ? f.L - 1 : 0;
+  const double fd = f.fred[3 * Lp], fq = f.fred[3 * Lp + 1], fm = f.fred[3 * Lp + 2];
+  const double ax0 = f.aux[2 * f.L], ax1 = f.aux[2 * f.L + 1], pnl = f.pn[f.L], ns0 = f.nsum[0];
+  s.j = cj;
+  s.mu = mu0 / mu1;
   s.c = s.ap = s.bk = s.gam = s.rn = s.rm = 0.0;
   s.nt = 1.0;
   const int j = s.j;
@@ -643,9 +650,9 @@ __device__ __forceinline__ FusedStep fused_begin(const FusedArgs &f)
   else if (f.force && (j == 0 || mode != kFusedStep)) s.act = kFusedNoop;
   else if (mode == kFusedPost)
   {
-    const double mex = f.fred[3 * (f.L - 1) + 2];
-    s.rn = f.aux[2 * f.L];
-    s.rm = f.aux[2 * f.L + 1];
+    const double mex = fm;
+    s.rn = ax0;
+    s.rm = ax1;
     s.nt = mex;
     if (!(mex > 0.0)) s.act = kFusedHalt;  // u_j = 0: invariant subspace
     else
@@ -657,13 +664,13 @@ __device__ __forceinline__ FusedStep fused_begin(const FusedArgs &f)
   }
   else if (j == 0)
   {
-    s.nt = f.nsum[0];
+    s.nt = ns0;
     s.act = kFusedStep;
   }
   else
   {
-    const double d = f.fred[3 * (f.L - 1)], q = f.fred[3 * (f.L - 1) + 1], m = f.fred[3 * (f.L - 1) + 2];
-    s.rn = sqrt(f.nsum[j - 1]);
+    const double d = fd, q = fq, m = fm;
+    s.rn = sqrt(pnl);
     s.rm = sqrt(m);
     s.c = d / m;
     s.ap = s.c * s.rn + s.mu;
@@ -723,6 +730,9 @@ __device__ __forceinline__ FusedStep fused_begin(const FusedArgs &f)
     }
     f.ctl[2 * f.L + 2] = nj;
     f.ctl[2 * f.L + 3] = nm;
+    // nsum[j' - 1] for the next launch: the norm this launch fixed (step / post: nsum[j]); otherwise
+    // the logical step does not advance and the value carries over
+    f.pn[f.L + 1] = (s.act == kFusedStep || s.act == kFusedPost) ? s.nt : pnl;
   }
   return s;
 }
@@ -1584,13 +1594,16 @@ static MarchPlan march_plan(const eig_mat_s &A, int mode, i64 zb = 0, i64 ze = -
   const i64 nplanes = ze - zb;
   if (nplanes < 2 || (zb == 0 && nplanes < 4)) return mp;
   const i64 ncol = D / chunk;
-  const i64 resident = 8LL * 4 * A.ctx->num_cu;  // waves
-  i64 nseg = std::max<i64>(1, (resident + ncol - 1) / ncol);
+  // one work item per resident wave slot: the fused kernel is built for 7 waves / SIMD, the others
+  // for 8 (launch bounds); items beyond the resident slots would run as a second, thin round
+  const i64 resident = (fused ? 7LL : 8LL) * 4 * A.ctx->num_cu;  // waves
+  i64 nseg = std::max<i64>(1, resident / ncol);
   nseg = std::min<i64>(nseg, nplanes);
   // fused step on wide planes (>= 1024 columns: 3-D grids from 256^2 per plane) with few planes --
   // the slab of one rank in a strong-scaling run: runs of >= 15 planes beat full occupancy
-  // (256 x 256 x 32 box: 2 runs 33.4 us vs 8 runs 37.8 us; at 256^3 the rule keeps 8 runs)
+  // (256 x 256 x 32 box: 2 runs 33.4 us vs 8 runs 37.8 us; at 256^3 the rule keeps 7 runs)
   if (fused && ncol >= 1024) nseg = std::max<i64>(1, std::min<i64>(nseg, nplanes / 15));
+  if (A.tune_march_runs > 0) nseg = std::min<i64>(A.tune_march_runs, nplanes);  // eig_mat_tune
   while (nseg > 1 && (ncol * nseg + kWaves - 1) / kWaves > kMaxRedBlocks) --nseg;
   if ((ncol * nseg + kWaves - 1) / kWaves > kMaxRedBlocks) return mp;
   mp.D = D;
@@ -1734,7 +1747,8 @@ void launch_lanczos_fused(const eig_mat_s &A, const double *P, double *Pout, con
                           hipStream_t s, ReduceWS red)
 {
   EIG_CHECK(A.br == 1 && A.bc == 1, EIG_ERR_BLOCKSIZE, "Lanczos driver: 1x1 blocks only");
-  const FusedArgs fa{fl.st.nsum, fl.st.alpha, fl.st.beta, fl.st.fred, fl.st.ctl, fl.st.aux, fl.st.mu2, fl.L, fl.force};
+  const FusedArgs fa{fl.st.nsum, fl.st.alpha, fl.st.beta, fl.st.fred, fl.st.ctl, fl.st.aux, fl.st.mu2, fl.st.pn, fl.L,
+                     fl.force};
   if (!carry)
   {
     const int mode = image_mode(A);
@@ -1777,7 +1791,8 @@ void launch_lanczos_pipe(const eig_mat_s &A, double *T, double *UZ, const double
   const i64 n = A.nb_rows, own = A.own_offset;
   EIG_CHECK((own & 1) == 0 && (((uintptr_t)T | (uintptr_t)UZ | (uintptr_t)S) & 15) == 0, EIG_ERR_ARG,
             "pipelined Lanczos: vectors must be 16-B aligned");
-  const FusedArgs fa{fl.st.nsum, fl.st.alpha, fl.st.beta, fl.st.fred, fl.st.ctl, fl.st.aux, fl.st.mu2, fl.L, fl.force};
+  const FusedArgs fa{fl.st.nsum, fl.st.alpha, fl.st.beta, fl.st.fred, fl.st.ctl, fl.st.aux, fl.st.mu2, fl.st.pn, fl.L,
+                     fl.force};
   const i64 per = 2LL * kStreamThreads;
   const int G = (int)std::max<i64>(1, std::min<i64>(kStreamBlocks, (n + per - 1) / per));
   hipLaunchKernelGGL(k_lanczos_pipe, dim3(G), dim3(kStreamThreads), 0, s, n, T + own,

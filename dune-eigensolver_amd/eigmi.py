@@ -124,6 +124,7 @@ SIGNATURES = {
     "eig_mat_destroy": (_int, [_vp]),
     "eig_mat_get_info": (_int, [_vp, ctypes.POINTER(_MatInfo)]),
     "eig_mat_shift_diag": (_int, [_vp, _dbl]),
+    "eig_mat_tune": (_int, [_vp, _int, _int]),
     "eig_lanczos_kernel_info": (_int, [_vp, _int, ctypes.c_char_p, _int, ctypes.POINTER(_i64)]),
     "eig_mat_kernel_info": (_int, [_vp, _int, ctypes.c_char_p, _int]),
     "eig_mv": (_int, [_vp, _vp, _vp]),
@@ -451,6 +452,10 @@ class Matrix:
         y = np.zeros(self.info.n)
         self.ctx.check(lib.eig_mv_host(self.h, _np_ptr(x), _np_ptr(y)))
         return y
+
+    def tune(self, march_runs=0):
+        """eig_mat_tune(EIG_TUNE_MARCH_RUNS): plane runs per column of the plane-march kernels (0 = auto)."""
+        self.ctx.check(lib.eig_mat_tune(self.h, 1, int(march_runs)))
 
     def shift_diag(self, shift):
         self.ctx.check(lib.eig_mat_shift_diag(self.h, shift))

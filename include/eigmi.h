@@ -185,6 +185,13 @@ enum { EIG_OP_SPMV = 0, EIG_OP_LANCZOS_K1 = 1, EIG_OP_LANCZOS_FUSED = 2, EIG_OP_
        EIG_OP_SPMM32 = 5, EIG_OP_CHEB32 = 6 /* m % 32 == 0: the 3-D box-stencil kernel where it applies */ };
 int eig_mat_kernel_info(eig_mat_t mat, int op, char *name, int name_len);
 
+/* Measurement / tuning override of a launch parameter the library otherwise derives from the
+ * image and the device (no environment switches): EIG_TUNE_MARCH_RUNS = plane runs per 64-row column
+ * of the plane-march kernels (value 0 = automatic: one work item per resident wave slot).  Results
+ * are unchanged except for the summation order of the step's reductions. */
+enum { EIG_TUNE_MARCH_RUNS = 1 };
+int eig_mat_tune(eig_mat_t mat, int key, int value);
+
 /* a13: A += shift*I on the diagonal of every diagonal block (eigensolver.hh:59-66). */
 int eig_mat_shift_diag(eig_mat_t mat, double shift);
 

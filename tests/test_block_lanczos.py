@@ -57,7 +57,8 @@ def _upload(ctx, A):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n,m1,m2", [(1000, 32, 32), (5003, 96, 32), (777, 8, 16), (20000, 160, 24)])
+@pytest.mark.parametrize("n,m1,m2", [(1000, 32, 32), (5003, 96, 32), (777, 8, 16), (20000, 160, 24),
+                                     (300007, 96, 32), (4097, 48, 16), (3, 16, 16)])
 def test_panel_gram(ctx, n, m1, m2):
     rng = np.random.default_rng(n)
     Q1, Q2 = rng.standard_normal((n, m1)), rng.standard_normal((n, m2))

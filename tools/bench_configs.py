@@ -155,11 +155,37 @@ def gram(ctx):
         Q1, Q2, G = ctx.array(oracle.random_mv8(n, m1, 1)), ctx.array(oracle.random_mv8(n, m2, 2)), ctx.zeros(m1 * m2)
         eigmi.gram_mv8(ctx, n, m1, m2, Q1, Q2, G)
         ctx.sync()
-        tg = min(wall(lambda: (eigmi.gram_mv8(ctx, n, m1, m2, Q1, Q2, G), None), reps)[0] for _ in range(3))
-        ctx.sync()
+        def batch():
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                eigmi.gram_mv8(ctx, n, m1, m2, Q1, Q2, G)
+            ctx.sync()
+            return (time.perf_counter() - t0) / reps
+        tg = min(batch() for _ in range(3))
         b = 8 * n * (m1 + m2)
         emit(config=f"gram n={n}", op=f"gram_mv8 m1={m1} m2={m2}", us=round(tg * 1e6, 2), algorithmic_bytes=b,
              GBs=round(b / tg / 1e9, 1), frac=round(b / tg / 1e9 / PEAK, 4))
+        Q1.free(), Q2.free(), G.free()
+    # block Lanczos panel products at C5 size (n = 256^3, eig_panel_gram_mv8: V^T (M Z) of CGS, k = 32)
+    nc5 = int(os.environ.get("EIGMI_GRAM_N5", str(256 ** 3)))
+    for m1, m2 in ((32, 32), (96, 32), (256, 32)):
+        Q1, Q2, G = ctx.zeros(nc5 * m1), ctx.zeros(nc5 * m2), ctx.zeros(m1 * m2)
+        # (timing only: a constant byte pattern, 0x3F3F... = 4.8e-4 per entry, instead of host random numbers)
+        eigmi.lib.eig_memset(ctx.h, Q1.ptr, 0x3F, nc5 * m1 * 8)
+        eigmi.lib.eig_memset(ctx.h, Q2.ptr, 0x3F, nc5 * m2 * 8)
+        eigmi.panel_gram_mv8(ctx, nc5, m1, m2, Q1, Q2, G)
+        ctx.sync()
+
+        def batch5():
+            t0 = time.perf_counter()
+            for _ in range(5):
+                eigmi.panel_gram_mv8(ctx, nc5, m1, m2, Q1, Q2, G)
+            ctx.sync()
+            return (time.perf_counter() - t0) / 5
+        tg = min(batch5() for _ in range(3))
+        b = 8 * nc5 * (m1 + m2)
+        emit(config=f"panel gram n={nc5}", op=f"panel_gram_mv8 m1={m1} m2={m2}", us=round(tg * 1e6, 2),
+             algorithmic_bytes=b, GBs=round(b / tg / 1e9, 1), frac=round(b / tg / 1e9 / PEAK, 4))
         Q1.free(), Q2.free(), G.free()
     for m in (8, 32):
         Qh = oracle.random_mv8(n, m, 1)
