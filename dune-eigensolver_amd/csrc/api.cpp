@@ -501,6 +501,15 @@ extern "C" int eig_comm_info(eig_ctx_t ctx, int *nranks, int *rank, int *allredu
   });
 }
 
+extern "C" int eig_fill_normal(eig_ctx_t ctx, int64_t count, unsigned seed, double *x)
+{
+  return guard(ctx, [&] {
+    EIG_CHECK(ctx && x && count >= 0, EIG_ERR_ARG, "eig_fill_normal: bad argument");
+    DeviceGuard dg(ctx->device);
+    if (count > 0) launch_fill_normal(count, seed, x, ctx->stream);
+  });
+}
+
 extern "C" int eig_mat_tune(eig_mat_t A, int key, int value)
 {
   return guard(A ? A->ctx : nullptr, [&] {

@@ -28,6 +28,10 @@ struct eig_blanczos_s {
   bool si = false;
   eig_mat_s *Ks = nullptr;
   double sigma = 0.0;
+  // multigrid inner solve (eig_blanczos_create_si_mg): `cycles` V-cycle iterations instead of the
+  // Chebyshev-Jacobi solve
+  eig_mg_s *mg = nullptr;
+  int cycles = 0;
   i64 ld = 0, own = 0, n = 0;
   DevBuf *V = nullptr;                   // (max_steps + 1) * b columns, window layout
   DevBuf *W = nullptr, *Xa = nullptr, *Xb = nullptr, *Xc = nullptr, *MZ = nullptr;  // b columns each
@@ -69,6 +73,9 @@ void halo_mv(const eig_mat_s &A, double *X, i64 m, hipStream_t s)
 // Xc (optional third buffer): on the box kernel x_{k+1} goes to a buffer of its own instead of over
 // the x_{k-1} it reads (interleaved A/B at 256^3: 4.23 vs 4.28 ms per launch; box-to-box spread of
 // the same launch is 4.2-4.8 ms).
+}  // namespace
+
+namespace eigmi {
 double *cheb_solve(eig_mat_s &M, i64 m, int degree, double lmin, double lmax, const double *Bv, const double *dinv,
                    double *Xa, double *Xb, double *Xc, hipStream_t s)
 {
@@ -99,7 +106,9 @@ double *cheb_solve(eig_mat_s &M, i64 m, int degree, double lmin, double lmax, co
   }
   return Xa;
 }
+}  // namespace eigmi
 
+namespace {
 double *dptr(DevBuf *b) { return b->d(); }
 
 // Z (b columns) = Vdst R with Vdst M-orthonormal (CholQR twice); R (b x b upper, row-major) on
@@ -118,8 +127,13 @@ void mcholqr2(eig_blanczos_s &w, double *Z, double *Vdst, std::vector<double> &R
   for (int i = 0; i < b; ++i) Rtot[(size_t)i * b + i] = 1.0;
   for (int pass = 0; pass < 2; ++pass)
   {
-    halo_mv(M, Z, b, s);
-    launch_sell_mv8(M, b, Z, dptr(w.MZ), s);
+    // pass 1 reuses M Z: the first pass updated it with the same triangular factor as Z (row-local,
+    // M (Z R^-1) = (M Z) R^-1 up to rounding), so one M SpMM per CholQR2 instead of two
+    if (pass == 0)
+    {
+      halo_mv(M, Z, b, s);
+      launch_sell_mv8(M, b, Z, dptr(w.MZ), s);
+    }
     launch_panel_gram(ctx, n, ld, b, b, Z + own * 8, dptr(w.MZ) + own * 8, Gd, s);
     allreduce_sum(ctx, Gd, (i64)b * b, s);
     EIG_HIP(hipMemcpyAsync(G.data(), Gd, G.size() * sizeof(double), hipMemcpyDeviceToHost, s));
@@ -131,6 +145,7 @@ void mcholqr2(eig_blanczos_s &w, double *Z, double *Vdst, std::vector<double> &R
     tri_upper_inv(b, R.data(), Ri.data());
     EIG_HIP(hipMemcpyAsync(Sd, Ri.data(), Ri.size() * sizeof(double), hipMemcpyHostToDevice, s));
     launch_panel_update(n, ld, ld, b, b, Z + own * 8, Sd, 1.0, 0.0, (pass == 1 ? Vdst : Z) + own * 8, s);
+    if (pass == 0) launch_panel_update(n, ld, ld, b, b, dptr(w.MZ) + own * 8, Sd, 1.0, 0.0, dptr(w.MZ) + own * 8, s);
     // Rtot <- R Rtot
     for (int i = 0; i < b; ++i)
       for (int j = 0; j < b; ++j)
@@ -159,7 +174,8 @@ void check_pair(const eig_mat_s *K, const eig_mat_s *M)
 
 namespace {
 void blanczos_create(eig_mat_t K, eig_mat_t M, eig_mat_t Ks, double sigma, int block, int max_steps, int degree,
-                     double lmin, double lmax, unsigned seed, eig_blanczos_t *out)
+                     double lmin, double lmax, unsigned seed, eig_blanczos_t *out, eig_mg_t mg = nullptr,
+                     int cycles = 0)
 {
     EIG_CHECK(out && block >= 8 && block <= 32 && block % 8 == 0 && max_steps >= 1 && degree >= 1 && lmin > 0.0 &&
                   lmax > lmin,
@@ -179,6 +195,8 @@ void blanczos_create(eig_mat_t K, eig_mat_t M, eig_mat_t Ks, double sigma, int b
       w->si = Ks != nullptr;
       w->Ks = Ks;
       w->sigma = sigma;
+      w->mg = mg;
+      w->cycles = cycles;
       w->b = block;
       w->max_steps = max_steps;
       w->degree = degree;
@@ -251,6 +269,18 @@ extern "C" int eig_blanczos_create_si(eig_mat_t K, eig_mat_t M, eig_mat_t Ks, do
   });
 }
 
+// The same with the Ks solve by `cycles` multigrid V-cycle iterations (mg.cpp; mg built on Ks).
+extern "C" int eig_blanczos_create_si_mg(eig_mat_t K, eig_mat_t M, eig_mat_t Ks, double sigma, eig_mg_t mg, int cycles,
+                                         int block, int max_steps, unsigned seed, eig_blanczos_t *out)
+{
+  return guard(K ? K->ctx : nullptr, [&] {
+    EIG_CHECK(Ks && mg && cycles >= 1, EIG_ERR_ARG, "eig_blanczos_create_si_mg: Ks, mg and cycles >= 1 required");
+    EIG_CHECK(mg_matrix(*mg) == Ks && block <= mg_max_cols(*mg), EIG_ERR_ARG,
+              "eig_blanczos_create_si_mg: mg must be built on Ks with max_cols >= block");
+    blanczos_create(K, M, Ks, sigma, block, max_steps, 1, 0.5, 2.5, seed, out, mg, cycles);
+  });
+}
+
 extern "C" int eig_blanczos_step(eig_blanczos_t w, int steps, eig_blanczos_timing *timing)
 {
   return guard(w ? w->K->ctx : nullptr, [&] {
@@ -298,8 +328,14 @@ extern "C" int eig_blanczos_step(eig_blanczos_t w, int steps, eig_blanczos_timin
         halo_mv(*w->M, Vj, b, s);
         launch_sell_mv8(*w->M, b, Vj, w->W->d(), s);
         EIG_HIP(hipEventRecord(e[1], s));
-        Z = cheb_solve(*w->Ks, b, w->degree, w->lmin, w->lmax, w->W->d(), w->dinv->d(), w->Xa->d(), w->Xb->d(),
-                       w->Xc->d(), s);
+        if (w->mg)
+        {
+          mg_apply(*w->mg, b, w->W->d(), w->Xa->d(), w->cycles);
+          Z = w->Xa->d();
+        }
+        else
+          Z = cheb_solve(*w->Ks, b, w->degree, w->lmin, w->lmax, w->W->d(), w->dinv->d(), w->Xa->d(), w->Xb->d(),
+                         w->Xc->d(), s);
         launch_panel_gram(ctx, n, ld, b, b, w->W->d() + own * 8, Z + own * 8, Ad, s);
         allreduce_sum(ctx, Ad, (i64)b * b, s);
         EIG_HIP(hipEventRecord(e[2], s));
@@ -308,9 +344,17 @@ extern "C" int eig_blanczos_step(eig_blanczos_t w, int steps, eig_blanczos_timin
       const i64 m1 = (i64)(j + 1) * b;
       for (int pass = 0; pass < 2; ++pass)
       {
-        halo_mv(*w->M, Z, b, s);
-        launch_sell_mv8(*w->M, b, Z, w->MZ->d(), s);
-        launch_panel_gram(ctx, n, ld, m1, b, w->V->d() + own * 8, w->MZ->d() + own * 8, Cd, s);
+        // first pass of the M^-1 K operator: M Z = M (M^-1 W) = W to the mass solve's accuracy
+        // (2 rho^degree), so W stands in for the M SpMM
+        const double *MZ = w->MZ->d();
+        if (pass == 0 && !w->si)
+          MZ = w->W->d();
+        else
+        {
+          halo_mv(*w->M, Z, b, s);
+          launch_sell_mv8(*w->M, b, Z, w->MZ->d(), s);
+        }
+        launch_panel_gram(ctx, n, ld, m1, b, w->V->d() + own * 8, MZ + own * 8, Cd, s);
         allreduce_sum(ctx, Cd, m1 * b, s);
         launch_panel_update(n, ld, ld, m1, b, w->V->d() + own * 8, Cd, -1.0, 1.0, Z + own * 8, s);
       }

@@ -951,34 +951,52 @@ void arnoldi_core(eig_mat_t A, eig_mat_t B, const LuRef &F, double sigma, int ne
     for (int i = 0; i < nev; ++i)
       if (resid(ord[i]) > tol * std::abs(w[ord[i]])) conv = false;
     if (conv || nrestart >= maxit) break;
-    // Krylov-Schur restart: kk wanted vectors, never splitting a conjugate pair
-    int kk = std::min(m - 2, nev + (m - nev) / 2);
-    if (w[ord[kk - 1]].imag() != 0.0 && w[ord[kk]] == std::conj(w[ord[kk - 1]])) ++kk;
-    if (kk > m - 1) kk -= 2;
-    std::vector<double> Z((size_t)m * kk, 0.0);  // row-major m x kk
+    // Krylov-Schur restart: about nev + (m - nev) / 2 wanted vectors, never splitting a conjugate
+    // pair.  The kept set is built from whole units in "LM" order -- a real Ritz value (one column)
+    // or a conjugate pair (real and imaginary part: two columns; its partner is looked up by value,
+    // wherever the sort put it) -- so span(Z) is G-invariant whatever the ordering of equal moduli.
+    const int target = std::min(m - 2, nev + (m - nev) / 2);
+    std::vector<std::pair<int, bool>> units;  // (eigenvalue index, complex pair)
+    int kk = 0;
     {
-      int col = 0;
       std::vector<char> used(m, 0);
-      for (int q = 0; q < kk && col < kk; ++q)
+      for (int q = 0; q < m && kk < target; ++q)
       {
         const int e = ord[q];
         if (used[e]) continue;
         used[e] = 1;
-        for (int i = 0; i < m; ++i) Z[(size_t)i * kk + col] = Y[(size_t)i * m + e].real();
-        ++col;
-        if (w[e].imag() != 0.0 && col < kk)
+        const bool cplx = w[e].imag() != 0.0;
+        if (cplx)
         {
-          for (int i = 0; i < m; ++i) Z[(size_t)i * kk + col] = Y[(size_t)i * m + e].imag();
-          ++col;
-          for (int q2 = q + 1; q2 < m; ++q2)
-            if (w[ord[q2]] == std::conj(w[e]))
+          int partner = -1;
+          for (int q2 = 0; q2 < m; ++q2)
+            if (!used[ord[q2]] && w[ord[q2]] == std::conj(w[e]))
             {
-              used[ord[q2]] = 1;
+              partner = ord[q2];
               break;
             }
+          EIG_CHECK(partner >= 0, EIG_ERR_BREAKDOWN, "Arnoldi: complex Ritz value without its conjugate");
+          used[partner] = 1;
+          if (kk + 2 > m - 1) break;  // a pair that does not fit is dropped whole
+        }
+        units.push_back({e, cplx});
+        kk += cplx ? 2 : 1;
+      }
+    }
+    EIG_CHECK(kk >= 1, EIG_ERR_BREAKDOWN, "Arnoldi: no Ritz vector to keep at restart");
+    std::vector<double> Z((size_t)m * kk, 0.0);  // row-major m x kk
+    {
+      int col = 0;
+      for (auto &u : units)
+      {
+        for (int i = 0; i < m; ++i) Z[(size_t)i * kk + col] = Y[(size_t)i * m + u.first].real();
+        ++col;
+        if (u.second)
+        {
+          for (int i = 0; i < m; ++i) Z[(size_t)i * kk + col] = Y[(size_t)i * m + u.first].imag();
+          ++col;
         }
       }
-      kk = col;
       for (int c = 0; c < kk; ++c)  // MGS, twice
         for (int pass = 0; pass < 2; ++pass)
         {
@@ -1013,6 +1031,21 @@ void arnoldi_core(eig_mat_t A, eig_mat_t B, const LuRef &F, double sigma, int ne
         Gn[(size_t)p * m + q] = a;
       }
       for (int i = 0; i < m; ++i) cn[p] += Z[(size_t)i * kk + p] * cvec[i];
+    }
+    {
+      // the restarted decomposition is a Krylov decomposition only if span(Z) is G-invariant:
+      // ||G Z - Z (Z^T G Z)|| small relative to ||G||
+      double gmax = 0.0, rmax = 0.0;
+      for (double g : G) gmax = std::max(gmax, std::fabs(g));
+      for (int i = 0; i < m; ++i)
+        for (int q = 0; q < kk; ++q)
+        {
+          double a = GZ[(size_t)i * kk + q];
+          for (int p = 0; p < kk; ++p) a -= Z[(size_t)i * kk + p] * Gn[(size_t)p * m + q];
+          rmax = std::max(rmax, std::fabs(a));
+        }
+      EIG_CHECK(rmax <= 1e-6 * std::max(gmax, 1e-300), EIG_ERR_BREAKDOWN,
+                "Arnoldi: restart subspace is not invariant under the projected matrix");
     }
     G.swap(Gn);
     cvec = cn;

@@ -118,6 +118,8 @@ void launch_mailbox_allreduce(double *buf, int count, const Mailbox &mb, unsigne
 
 }  // namespace eigmi
 
+struct eig_mg_s;  // mg.cpp
+
 struct eig_ctx_s {
   int device = 0;
   hipStream_t stream = nullptr;      // compute stream
@@ -377,6 +379,14 @@ void launch_panel_gram(eig_ctx_t ctx, i64 n, i64 ld, i64 m1, i64 m2, const doubl
                        hipStream_t s);
 void launch_panel_gram_2stage(eig_ctx_t ctx, i64 n, i64 ld, i64 m1, i64 m2, const double *Q1, const double *Q2,
                               double *G, hipStream_t s);
+// Chebyshev-Jacobi semi-iteration for M X = Bv (degree steps on the spectrum bounds [lmin, lmax]
+// of diag(M)^-1 M, from X = 0; blanczos.cpp): returns the buffer (Xa, Xb or Xc) holding x_degree.
+double *cheb_solve(eig_mat_s &M, i64 m, int degree, double lmin, double lmax, const double *Bv, const double *dinv,
+                   double *Xa, double *Xb, double *Xc, hipStream_t s);
+// Geometric multigrid inner solve (mg.cpp): X = S_cycles B on the level-0 matrix's window layout.
+void mg_apply(eig_mg_s &mg, i64 m, const double *B, double *X, int cycles);
+eig_mat_s *mg_matrix(const eig_mg_s &mg);
+int mg_max_cols(const eig_mg_s &mg);
 // Y = beta Y + alpha Q S over n rows (owned-row pointers), m2 <= 32.
 void launch_panel_update(i64 n, i64 ldq, i64 ldy, i64 m1, i64 m2, const double *Q, const double *S, double alpha,
                          double beta, double *Y, hipStream_t s);

@@ -90,6 +90,9 @@ __global__ __launch_bounds__(64 * W) void k_sell_mv8q(i64 nrows, i64 nslices, co
     const i64 base = slice_ptr[s];
     const int width = (int)((slice_ptr[s + 1] - base) >> 6);
     const i64 r = s * 64 + ri;
+    // entries that are not stored gather the row's own element; padding rows of the last slice
+    // (r >= nrows) the last owned row's, so no gather leaves the window (tiny matrices: n < 64)
+    const i64 rs = r < nrows ? r : nrows - 1;
     unsigned m = 0;
     if (STENCIL) m = st_mask[s * 64 + ri];
     double2 acc[MB];
@@ -112,13 +115,13 @@ __global__ __launch_bounds__(64 * W) void k_sell_mv8q(i64 nrows, i64 nslices, co
         if (STENCIL)
         {
           okk[u] = (k0 + u < width) && ((m >> (k0 + u)) & 1u);
-          c[u] = own + r + (okk[u] ? st_delta[8 * s + k] : 0);
+          c[u] = okk[u] ? own + r + st_delta[8 * s + k] : own + rs;
         }
         else
         {
           const i32 ci = __builtin_nontemporal_load(col + base + k * 64 + ri);
           okk[u] = (k0 + u < width) && ci >= 0;
-          c[u] = okk[u] ? (i64)ci : own + r;
+          c[u] = okk[u] ? (i64)ci : own + rs;
         }
       }
       double2 xv[U][MB];
@@ -246,17 +249,18 @@ __global__ __launch_bounds__(256) void k_sell_mv8g(i64 nrows, i64 nslices, const
         {
           const int ri = rq + 16 * h;
           const i64 r = s * 64 + ri;
+          const i64 rs = r < nrows ? r : nrows - 1;  // (padding rows: see k_sell_mv8q)
           a[u][h] = __builtin_nontemporal_load(val + base + k * 64 + ri);
           if (STENCIL)
           {
             okk[u][h] = (k0 + u < width) && ((m[h] >> (k0 + u)) & 1u);
-            c[u][h] = own + r + (okk[u][h] ? dl : 0);
+            c[u][h] = okk[u][h] ? own + r + dl : own + rs;
           }
           else
           {
             const i32 ci = __builtin_nontemporal_load(col + base + k * 64 + ri);
             okk[u][h] = (k0 + u < width) && ci >= 0;
-            c[u][h] = okk[u][h] ? (i64)ci : own + r;
+            c[u][h] = okk[u][h] ? (i64)ci : own + rs;
           }
         }
       }

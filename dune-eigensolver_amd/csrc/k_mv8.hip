@@ -159,7 +159,7 @@ void launch_dot_diag_mv8(i64 n, i64 m, const double *Q1, const double *Q2, doubl
 constexpr int kGramThreads = 256;
 
 template <int DR, int T1, int T2, int U>
-__global__ __launch_bounds__(kGramThreads) void k_gram_mv8(i64 n, i64 ld1, i64 ld2, int nb1, int nb2, int nby2,
+__global__ __launch_bounds__(kGramThreads) void k_gram_mv8(i64 n, i64 ld1, i64 ld2, int nb1, int nb2, int ny2, int ny,
                                                            const double *__restrict__ Q1, const double *__restrict__ Q2,
                                                            double *__restrict__ G, double *partials, unsigned *tickets)
 {
@@ -170,7 +170,14 @@ __global__ __launch_bounds__(kGramThreads) void k_gram_mv8(i64 n, i64 ld1, i64 l
   __shared__ double sh[W][E];
   __shared__ double tot[E];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int cy1 = blockIdx.y / nby2, cy2 = blockIdx.y % nby2;
+  // 1-D grid of gx * ny workgroups (gx a multiple of 8), XCD-aware: workgroups are dealt round-robin
+  // over the 8 XCDs, so b, b + 8, b + 16, ... share an XCD; they take the ny output chunks of ONE row
+  // range (chunk fastest), run together and read each operand panel's rows once from HBM -- the
+  // other chunks' re-reads of it are hits in that XCD's L2
+  const int bq = blockIdx.x >> 3;
+  const int cy = bq % ny, bx = (bq / ny) * 8 + (blockIdx.x & 7);
+  const int gxw = gridDim.x / ny;  // workgroups per chunk
+  const int cy1 = cy / ny2, cy2 = cy % ny2;
   const int k = lane >> 4, i = lane & 15;
   const int rl = DR ? k + 4 * (i >> 3) : k;  // row inside the group
   const double *a[T1];
@@ -196,8 +203,8 @@ __global__ __launch_bounds__(kGramThreads) void k_gram_mv8(i64 n, i64 ld1, i64 l
 #pragma unroll
     for (int u = 0; u < T2; ++u) acc[t][u] = d4{0.0, 0.0, 0.0, 0.0};
   const i64 ng = (n + RG - 1) / RG;
-  const i64 ws = (i64)gridDim.x * W;
-  for (i64 g0 = (i64)blockIdx.x * W + wave; g0 < ng; g0 += U * ws)
+  const i64 ws = (i64)gxw * W;
+  for (i64 g0 = (i64)bx * W + wave; g0 < ng; g0 += U * ws)
   {
     double av[U][T1], bv[U][T2];
 #pragma unroll
@@ -254,12 +261,9 @@ __global__ __launch_bounds__(kGramThreads) void k_gram_mv8(i64 n, i64 ld1, i64 l
     tot[e] = v;
   }
   __syncthreads();
-  const size_t ny = gridDim.y;
-  double *part = partials + (size_t)blockIdx.y * gridDim.x * E;
-  double *spart = partials + ny * gridDim.x * E + (size_t)blockIdx.y * 8 * E;
-  if (!grid_sum2<kGramThreads>(tot, E, part, spart, tickets + (size_t)blockIdx.y * kTicketStride, blockIdx.x,
-                               gridDim.x, sh[0]))
-    return;
+  double *part = partials + (size_t)cy * gxw * E;
+  double *spart = partials + (size_t)ny * gxw * E + (size_t)cy * 8 * E;
+  if (!grid_sum2<kGramThreads>(tot, E, part, spart, tickets + (size_t)cy * kTicketStride, bx, gxw, sh[0])) return;
   const i64 m1 = (i64)nb1 * 8, m2 = (i64)nb2 * 8;
   for (int e = threadIdx.x; e < E; e += kGramThreads)
   {
@@ -281,19 +285,13 @@ GramShape gram_shape(i64 m1, i64 m2)
   const int nb1 = (int)(m1 / 8), nb2 = (int)(m2 / 8);
   GramShape g;
   g.dr = (nb1 % 2 || nb2 % 2) ? 1 : 0;
-  const int u1 = g.dr ? nb1 : nb1 / 2, u2 = g.dr ? nb2 : nb2 / 2;
-  if (g.dr)
-  {
-    g.t1 = u1 >= 4 ? 4 : u1 >= 2 ? 2 : 1;
-    g.t2 = u2 >= 4 ? 4 : std::max(1, u2);
-  }
-  else
-  {
-    g.t2 = u2 >= 2 ? 2 : 1;
-    g.t1 = u1 >= 4 ? 4 : u1 >= 2 ? 2 : 1;
-  }
-  g.ny1 = (u1 + g.t1 - 1) / g.t1;
-  g.ny2 = (u2 + g.t2 - 1) / g.t2;
+  const int u1 = std::max(1, g.dr ? nb1 : nb1 / 2), u2 = std::max(1, g.dr ? nb2 : nb2 / 2);
+  // at most 4 x 4 units (doubled) / 4 x 2 pairs per workgroup, chunks of equal size
+  const int max1 = 4, max2 = g.dr ? 4 : 2;
+  g.ny1 = (u1 + max1 - 1) / max1;
+  g.ny2 = (u2 + max2 - 1) / max2;
+  g.t1 = (u1 + g.ny1 - 1) / g.ny1;
+  g.t2 = (u2 + g.ny2 - 1) / g.ny2;
   return g;
 }
 
@@ -305,12 +303,14 @@ void gram_launch(i64 n, i64 ld1, i64 ld2, int nb1, int nb2, const GramShape &gs,
   constexpr int E = T1 * T2 * (DR ? 64 : 256);
   const int ny = gs.ny1 * gs.ny2;
   const i64 ng = (n + (DR ? 7 : 3)) / (DR ? 8 : 4);
-  // about 4 resident workgroups per CU, at least one U-group batch per wave
-  i64 gx = std::min<i64>(1024, std::max<i64>(1, (ng + 4 * U - 1) / (4 * U)));
-  while ((gx * ny + 8 * ny) * E > cap && gx > 1) gx /= 2;
+  // about 4 resident workgroups per CU in all, at least one U-group batch per wave; gx a multiple
+  // of 8 (the kernel's XCD mapping)
+  i64 gx = std::min<i64>(std::max<i64>(8, 1024 / ny), std::max<i64>(1, (ng + 4 * U - 1) / (4 * U)));
+  gx = (gx + 7) / 8 * 8;
+  while ((gx * ny + 8 * ny) * E > cap && gx > 8) gx -= 8;
   EIG_CHECK((gx * ny + 8 * ny) * E <= cap, EIG_ERR_ARG, "gram: output too large for the reduction workspace");
-  hipLaunchKernelGGL((k_gram_mv8<DR, T1, T2, U>), dim3((unsigned)gx, (unsigned)ny), dim3(kGramThreads), 0, s, n, ld1,
-                     ld2, nb1, nb2, gs.ny2, Q1, Q2, G, partials, tickets);
+  hipLaunchKernelGGL((k_gram_mv8<DR, T1, T2, U>), dim3((unsigned)(gx * ny)), dim3(kGramThreads), 0, s, n, ld1, ld2,
+                     nb1, nb2, gs.ny2, ny, Q1, Q2, G, partials, tickets);
 }
 
 void gram_dispatch(i64 n, i64 ld1, i64 ld2, i64 m1, i64 m2, const double *Q1, const double *Q2, double *G,
@@ -328,8 +328,10 @@ void gram_dispatch(i64 n, i64 ld1, i64 ld2, i64 m1, i64 m2, const double *Q1, co
   }
   EIG_GRAM(1, 1, 1) EIG_GRAM(1, 1, 2) EIG_GRAM(1, 1, 3) EIG_GRAM(1, 1, 4)
   EIG_GRAM(1, 2, 1) EIG_GRAM(1, 2, 2) EIG_GRAM(1, 2, 3) EIG_GRAM(1, 2, 4)
+  EIG_GRAM(1, 3, 1) EIG_GRAM(1, 3, 2) EIG_GRAM(1, 3, 3) EIG_GRAM(1, 3, 4)
   EIG_GRAM(1, 4, 1) EIG_GRAM(1, 4, 2) EIG_GRAM(1, 4, 3) EIG_GRAM(1, 4, 4)
-  EIG_GRAM(0, 1, 1) EIG_GRAM(0, 1, 2) EIG_GRAM(0, 2, 1) EIG_GRAM(0, 2, 2) EIG_GRAM(0, 4, 1) EIG_GRAM(0, 4, 2)
+  EIG_GRAM(0, 1, 1) EIG_GRAM(0, 1, 2) EIG_GRAM(0, 2, 1) EIG_GRAM(0, 2, 2) EIG_GRAM(0, 3, 1) EIG_GRAM(0, 3, 2)
+  EIG_GRAM(0, 4, 1) EIG_GRAM(0, 4, 2)
 #undef EIG_GRAM
   throw Error(EIG_ERR_ARG, "gram: no kernel for this shape");
 }
@@ -358,7 +360,7 @@ void launch_gram_panel(eig_ctx_t ctx, i64 n, i64 ld, i64 m1, i64 m2, const doubl
   EIG_CHECK(chunks <= kNumTickets, EIG_ERR_ARG, "panel gram: too many output chunks");
   const GramShape gs = gram_shape(m1, m2);
   const i64 E = (i64)gs.t1 * gs.t2 * (gs.dr ? 64 : 256);
-  const i64 cap = (1024 + 8) * (i64)chunks * E;
+  const i64 cap = (std::max<i64>(8, 1024 / chunks) + 8 + 8) * (i64)chunks * E;
   double *part = (double *)ctx_buffer(ctx, 8, (size_t)cap * sizeof(double));  // slot 8: panel partials
   gram_dispatch(n, ld, ld, m1, m2, Q1, Q2, G, ctx->red.ticket(0), part, cap, s);
 }

@@ -341,6 +341,53 @@ extern "C" int eig_lu_create(eig_ctx_t ctx, int64_t n, const int64_t *Lp, const 
   });
 }
 
+namespace {
+// The device band LU factors without pivoting (k_band.hip) where UMFPACK, the reference's factoriser,
+// pivots.  Growth through the coupled tiles is not bounded a priori, so after factoring: one solve of
+// 8 right-hand sides and the componentwise backward error max |A x - b| / (|A| |x| + |b|) on the host
+// (Oettli-Prager); above 1e-9 the factors are rejected (EIG_ERR_BREAKDOWN) instead of returning a
+// solve that silently lost its digits.
+void check_backward_error(eig_lu_s &lu, const std::vector<std::vector<std::pair<i64, double>>> &rowsA)
+{
+  const i64 n = lu.n;
+  if (n == 0) return;
+  hipStream_t s = lu.ctx->stream;
+  std::vector<double> b((size_t)n * 8), x((size_t)n * 8);
+  u64 h = 0x9e3779b97f4a7c15ull;
+  for (auto &v : b)
+  {
+    h ^= h >> 33;
+    h *= 0xff51afd7ed558ccdull;
+    h ^= h >> 29;
+    v = (double)(h >> 11) * (2.0 / 9007199254740992.0) - 1.0;
+  }
+  DevBuf din(b.size() * sizeof(double)), dout(b.size() * sizeof(double));
+  EIG_HIP(hipMemcpyAsync(din.d(), b.data(), b.size() * sizeof(double), hipMemcpyHostToDevice, s));
+  launch_inverse_mv8(lu.img, 8, din.d(), dout.d(), s);
+  EIG_HIP(hipMemcpyAsync(x.data(), dout.d(), x.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+  EIG_HIP(hipStreamSynchronize(s));
+  EIG_HIP(hipMemcpyAsync(din.d(), b.data(), b.size() * sizeof(double), hipMemcpyHostToDevice, s));  // (restore)
+  double worst = 0.0;
+  for (i64 i = 0; i < n; ++i)
+    for (int j = 0; j < 8; ++j)
+    {
+      double r = -b[(size_t)i * 8 + j], d = std::fabs(b[(size_t)i * 8 + j]);
+      for (auto &e : rowsA[i])
+      {
+        const double t = e.second * x[(size_t)e.first * 8 + j];
+        r += t;
+        d += std::fabs(t);
+      }
+      if (!std::isfinite(r)) worst = HUGE_VAL;
+      else if (d > 0.0) worst = std::max(worst, std::fabs(r) / d);
+    }
+  EIG_HIP(hipStreamSynchronize(s));
+  if (!(worst <= 1e-9))
+    throw Error(EIG_ERR_BREAKDOWN, "LU without pivoting: backward error " + std::to_string(worst) +
+                                       " of a test solve exceeds 1e-9 (the matrix needs pivoting)");
+}
+}  // namespace
+
 extern "C" int eig_lu_create_bcsr(eig_ctx_t ctx, int64_t nb_rows, int br, const int64_t *rowptr, const int32_t *col,
                                   const double *vals, eig_lu_t *out)
 {
@@ -451,6 +498,8 @@ extern "C" int eig_lu_create_bcsr(eig_ctx_t ctx, int64_t nb_rows, int br, const 
             build_device(*lu);
           }
           phase("device");
+          check_backward_error(*lu, rowsA);
+          phase("check");
         }
         catch (...)
         {

@@ -125,6 +125,7 @@ SIGNATURES = {
     "eig_mat_get_info": (_int, [_vp, ctypes.POINTER(_MatInfo)]),
     "eig_mat_shift_diag": (_int, [_vp, _dbl]),
     "eig_mat_tune": (_int, [_vp, _int, _int]),
+    "eig_fill_normal": (_int, [_vp, _i64, _u, _vp]),
     "eig_lanczos_kernel_info": (_int, [_vp, _int, ctypes.c_char_p, _int, ctypes.POINTER(_i64)]),
     "eig_mat_kernel_info": (_int, [_vp, _int, ctypes.c_char_p, _int]),
     "eig_mv": (_int, [_vp, _vp, _vp]),
@@ -170,6 +171,12 @@ SIGNATURES = {
     "eig_blanczos_create": (_int, [_vp, _vp, _int, _int, _int, _dbl, _dbl, _u, ctypes.POINTER(_vp)]),
     "eig_blanczos_create_si": (_int, [_vp, _vp, _vp, _dbl, _int, _int, _int, _dbl, _dbl, _u, ctypes.POINTER(_vp)]),
     "eig_blanczos_step": (_int, [_vp, _int, ctypes.POINTER(BlockTiming)]),
+    "eig_mg_create": (_int, [_vp, _int, _int, _int, _int, _int, _dbl, ctypes.POINTER(_vp)]),
+    "eig_mg_info": (_int, [_vp, ctypes.POINTER(_int), ctypes.POINTER(_i64), ctypes.POINTER(_int),
+                           ctypes.POINTER(_dbl)]),
+    "eig_mg_solve": (_int, [_vp, _i64, _vp, _vp, _int, ctypes.POINTER(_dbl)]),
+    "eig_mg_destroy": (_int, [_vp]),
+    "eig_blanczos_create_si_mg": (_int, [_vp, _vp, _vp, _dbl, _vp, _int, _int, _int, _u, ctypes.POINTER(_vp)]),
     "eig_blanczos_ritz": (_int, [_vp, _int, _int, _vp, _vp, _vp]),
     "eig_blanczos_tmatrix": (_int, [_vp, ctypes.POINTER(_int), _vp]),
     "eig_blanczos_destroy": (_int, [_vp]),
@@ -781,16 +788,55 @@ def arnoldi_shift_invert(A, nev, sigma=0.0, B=None, mode="std", ncv=0, tol=0.0, 
     return er + 1j * ei, (evec.reshape(nev, A.n) if want_evec else None), r.value
 
 
+class Multigrid:
+    """eig_mg_t: geometric multigrid on a box-grid matrix (include/eigmi.h eig_mg_create)."""
+
+    def __init__(self, A, dims, max_cols=32, smooth_degree=2, smooth_ratio=10.0):
+        self.A = A
+        h = _vp()
+        A.ctx.check(lib.eig_mg_create(A.h, dims[0], dims[1], dims[2], max_cols, smooth_degree, smooth_ratio,
+                                      ctypes.byref(h)))
+        self.h = h
+
+    def info(self):
+        lv, cr, cd, lm = _int(0), _i64(0), _int(0), _dbl(0)
+        self.A.ctx.check(lib.eig_mg_info(self.h, ctypes.byref(lv), ctypes.byref(cr), ctypes.byref(cd), ctypes.byref(lm)))
+        return {"levels": lv.value, "coarse_rows": cr.value, "coarse_degree": cd.value, "lmax_fine": lm.value}
+
+    def solve(self, m, B, X, cycles, resid=False):
+        """X = S_cycles B (device MultiVector buffers); returns max_j ||B - A X|| / ||B|| when resid."""
+        r = _dbl(0)
+        self.A.ctx.check(lib.eig_mg_solve(self.h, m, B.ptr, X.ptr, cycles, ctypes.byref(r) if resid else None))
+        return r.value if resid else None
+
+    def close(self):
+        if self.h and self.A.h and self.A.ctx.h:
+            lib.eig_mg_destroy(self.h)
+        self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class BlockLanczos:
     """eig_blanczos_t: block Lanczos for K x = lambda M x (config C5), see include/eigmi.h."""
 
-    def __init__(self, K, M, block=32, max_steps=8, degree=36, lmin=0.5, lmax=2.5, seed=123, Ks=None, sigma=0.0):
+    def __init__(self, K, M, block=32, max_steps=8, degree=36, lmin=0.5, lmax=2.5, seed=123, Ks=None, sigma=0.0,
+                 mg=None, cycles=0):
         """Ks given: the spectral transformation (K - sigma M)^-1 M with Ks = K - sigma M and
-        (degree, lmin, lmax) the Chebyshev-Jacobi solve of Ks (eig_blanczos_create_si); otherwise
+        (degree, lmin, lmax) the Chebyshev-Jacobi solve of Ks (eig_blanczos_create_si), or with
+        mg (a Multigrid on Ks) `cycles` multigrid iterations (eig_blanczos_create_si_mg); otherwise
         M^-1 K with (degree, lmin, lmax) the mass solve."""
         self.K, self.M, self.block = K, M, block
+        self.mg = mg
         h = _vp()
-        if Ks is None:
+        if mg is not None:
+            K.ctx.check(lib.eig_blanczos_create_si_mg(K.h, M.h, Ks.h, sigma, mg.h, cycles, block, max_steps, seed,
+                                                      ctypes.byref(h)))
+        elif Ks is None:
             K.ctx.check(lib.eig_blanczos_create(K.h, M.h, block, max_steps, degree, lmin, lmax, seed, ctypes.byref(h)))
         else:
             K.ctx.check(lib.eig_blanczos_create_si(K.h, M.h, Ks.h, sigma, block, max_steps, degree, lmin, lmax, seed,

@@ -247,6 +247,9 @@ int eig_b_orthonormalize_mv8(eig_mat_t B, int64_t m, double *Q, double *norm);
 /* eigensolver.hh:49-55 start block: mt19937(seed) + normal_distribution(0,1), fill order
  * (block, row, col); generated on the host (bitwise the reference's numbers), uploaded. */
 int eig_random_mv8(eig_ctx_t ctx, int64_t n, int64_t m, unsigned seed, double *Q);
+/* x[0..count) = N(0,1) numbers from a counter-based generator on the device (seeded; NOT the
+ * reference's mt19937 sequence -- for synthetic workloads and measurements). */
+int eig_fill_normal(eig_ctx_t ctx, int64_t count, unsigned seed, double *x);
 
 /* ---------------------------------------------------------------- drivers ------------------ */
 /* a12: StandardLargest (eigensolver.hh:28-112) on the device.  Mutates the matrix when
@@ -478,6 +481,28 @@ int eig_blanczos_create(eig_mat_t K, eig_mat_t M, int block, int max_steps, int 
  * ascending (EIG_WHICH_SA) or descending (EIG_WHICH_LA). */
 int eig_blanczos_create_si(eig_mat_t K, eig_mat_t M, eig_mat_t Ks, double sigma, int block, int max_steps, int degree,
                            double lmin, double lmax, unsigned seed, eig_blanczos_t *ws);
+/* Geometric multigrid for a matrix on an nx x ny x nz box grid (lexicographic rows k = (z ny + y) nx
+ * + x; 1x1 blocks, one rank; every entry within one grid step per direction, e.g. the 7-point and P1
+ * Kuhn stencils): coarse grids keep the nodes of odd index per direction, trilinear P, Galerkin
+ * P^T A P on the host (27-point, bitwise symmetric), Chebyshev-Jacobi smoothing of degree
+ * smooth_degree on [lmax / smooth_ratio, lmax] (lmax = Gershgorin bound of diag(A)^-1 A), the
+ * coarsest level (<= 64 rows) solved to 1e-15 by Chebyshev on its exact spectrum.  max_cols: the
+ * widest multivector a solve takes (workspace: 6 x rows x max_cols doubles per level). */
+typedef struct eig_mg_s *eig_mg_t;
+int eig_mg_create(eig_mat_t A, int nx, int ny, int nz, int max_cols, int smooth_degree, double smooth_ratio,
+                  eig_mg_t *mg);
+int eig_mg_info(eig_mg_t mg, int *levels, int64_t *coarse_rows, int *coarse_degree, double *lmax_fine);
+/* X = S B, m columns (window layout = plain MultiVector<double,8> on one rank), S = `cycles`
+ * stationary iterations x += V (b - A x) from x = 0 with V one symmetric V-cycle: a fixed symmetric
+ * linear operator (no inner products inside).  resid_host (or NULL): max over the columns of
+ * ||B - A X|| / ||B|| afterwards (a measurement; synchronous either way). */
+int eig_mg_solve(eig_mg_t mg, int64_t m, const double *B, double *X, int cycles, double *resid_host);
+int eig_mg_destroy(eig_mg_t mg);
+/* eig_blanczos_create_si with the Ks solve by `cycles` multigrid iterations (mg built on Ks with
+ * max_cols >= block) instead of Chebyshev-Jacobi -- the smallest end of the pencil at 256^3, where
+ * kappa(diag(K)^-1 K) ~ 2.7e4 would need ~2,500 Chebyshev steps per application. */
+int eig_blanczos_create_si_mg(eig_mat_t K, eig_mat_t M, eig_mat_t Ks, double sigma, eig_mg_t mg, int cycles, int block,
+                              int max_steps, unsigned seed, eig_blanczos_t *ws);
 int eig_blanczos_step(eig_blanczos_t ws, int steps, eig_blanczos_timing *timing);
 /* Ritz pairs of the k steps taken: eval_host[nev] (LA descending / SA ascending), evec_host: nev
  * owned-row vectors with y^T M y = 1 (or NULL), resid_host[nev]: ||K y - theta M y||_2 (or NULL). */

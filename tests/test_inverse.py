@@ -346,3 +346,23 @@ def test_device_band_factors_match_host(ctx, name):
     print(f"{name}: kernel {used} (coupled {gl}/{gu}), device image vs reference arithmetic {err:.2e}")
     assert used == "blockinv" and err <= BINV_RTOL
     lu.close()
+
+
+@pytest.mark.gpu
+def test_device_lu_rejects_factors_that_need_pivoting(ctx):
+    """the device band LU does not pivot (UMFPACK, the reference's factoriser,
+    does).  A matrix whose every unpivoted elimination order meets a tiny pivot (3x3 blocks with
+    1e-13 on the diagonal and ones elsewhere: well conditioned, eigenvalues 2 and -1) must be
+    rejected by the backward-error check (EIG_ERR_BREAKDOWN), not solved to garbage."""
+    import scipy.sparse as sp
+    blk = np.ones((3, 3)) - np.eye(3) + 1e-13 * np.eye(3)
+    A = sp.block_diag([blk] * 200).tocsr()
+    A.sort_indices()
+    with pytest.raises(eigmi.EigError) as e:
+        eigmi.LU.from_bcsr(ctx, A.indptr.astype(np.int64), A.indices.astype(np.int32), A.data.copy())
+    assert e.value.code in (eigmi.EIG_ERR_BREAKDOWN,), str(e.value)
+    # a well-pivoted matrix of the same pattern passes the check
+    good = sp.block_diag([4 * np.eye(3) - (np.ones((3, 3)) - np.eye(3))] * 200).tocsr()
+    good.sort_indices()
+    lu = eigmi.LU.from_bcsr(ctx, good.indptr.astype(np.int64), good.indices.astype(np.int32), good.data.copy())
+    lu.close()

@@ -1,0 +1,72 @@
+#!/bin/bash
+# GPU-box task runner (run through gpurun from the repo root): one script, one subcommand per
+# measurement, outputs under gpurun_out/<TAG>/.  Every GPU step has its own time limit; the first
+# failing step ends the call (no retries).
+#
+#   TAG=r03x bash tools/gpu.sh <task> [<task> ...]
+#
+# tasks:
+#   tests[:<file,file>]  pytest -m gpu (all, or the listed tests/ files)       -> tests.log
+#   smoke                __graft_entry__.smoke()                              -> smoke.log
+#   bench                python bench.py (the driver's default line)          -> bench.json
+#   profile              rocprofv3 kernel trace + FETCH / WRITE PMC passes of the bench (tools/profile_round.sh)
+#   configs              tools/bench_configs.py c1 c2 c3, c5 (256^3), inv (64^2, 200^2)  -> cfg_*.jsonl
+#   gram                 a6 / a9 / panel-Gram timings under a kernel trace    -> gram.jsonl, gram_trace/
+#   c5 | c5si            block Lanczos 256^3: largest end / smallest end (multigrid solve)  -> c5*.jsonl
+#   latency              fused step vs eig_mv across sizes and slabs, plane-run counts  -> latency.jsonl
+#   pipe                 fused vs pipelined on one rank's slab and the cube   -> pipe.jsonl
+#   csr                  general (scrambled + RCM) 256^3 matrix: SpMV / Lanczos kernels  -> csr.jsonl
+set -o pipefail
+TAG=${TAG:-scratch}
+O=gpurun_out/$TAG
+mkdir -p "$O"
+prof_env() { cd /tmp && export TMPDIR=/tmp && cd - > /dev/null; }
+sweep() { timeout -k 10 150 python3 tools/lanczos_sweep.py "$@" --rounds 3 --steps 40 >> "$O/latency.jsonl"; }
+
+run_task() {
+  case "$1" in
+    tests)
+      timeout -k 10 1500 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > "$O/tests.log" 2>&1 ;;
+    tests:*)
+      local files
+      files=$(echo "${1#tests:}" | tr ',' ' ' | sed 's#\([^ ]*\)#tests/\1#g')
+      timeout -k 10 900 python -u -m pytest $files -m gpu -x -v -s --timeout 300 --timeout-method thread > "$O/tests.log" 2>&1 ;;
+    smoke)
+      timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 ;;
+    bench)
+      timeout -k 10 400 python bench.py > "$O/bench.json" 2> "$O/bench.err" ;;
+    profile)
+      bash tools/profile_round.sh "$TAG" > "$O/profile.log" 2>&1 ;;
+    configs)
+      timeout -k 10 300 python -u tools/bench_configs.py c1 c2 c3 > "$O/cfg_c123.jsonl" 2> "$O/cfg_c123.err" && \
+      EIGMI_C5_N=256 timeout -k 10 300 python -u tools/bench_configs.py c5 > "$O/cfg_c5.jsonl" 2> "$O/cfg_c5.err" && \
+      EIGMI_INV_N=64 timeout -k 10 300 python -u tools/bench_configs.py inv > "$O/cfg_inv64.jsonl" 2> "$O/cfg_inv64.err" && \
+      EIGMI_INV_N=200 timeout -k 10 400 python -u tools/bench_configs.py inv > "$O/cfg_inv200.jsonl" 2> "$O/cfg_inv200.err" ;;
+    gram)
+      prof_env
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/gram_trace" -o trace -- \
+        python3 tools/bench_configs.py gram > "$O/gram.jsonl" 2> "$O/gram.err" ;;
+    c5)
+      EIGMI_C5_N=256 timeout -k 10 300 python -u tools/bench_configs.py c5 > "$O/c5.jsonl" 2> "$O/c5.err" ;;
+    c5si)
+      EIGMI_C5_N=256 timeout -k 10 600 python -u tools/bench_configs.py c5si > "$O/c5si.jsonl" 2> "$O/c5si.err" ;;
+    latency)
+      sweep --N 128 --variants fused,fused@32,fused@28,fused@16,fused@12,mv,mv@16 && \
+      sweep --N 256 --variants fused,fused@8,fused@7,fused@6,fused@4,mv,mv@7 && \
+      sweep --N 256 --slab 32 --variants fused,fused@1,fused@4,fused@7,mv && \
+      sweep --N 256 --slab 16 --variants fused,fused@2,fused@4,fused@7,mv && \
+      sweep --N 64 --variants fused,mv ;;
+    pipe)
+      timeout -k 10 200 python -u tools/lanczos_sweep.py --slab 32 --variants fused,pipelined,mv --rounds 5 > "$O/pipe.jsonl" 2>&1 && \
+      timeout -k 10 200 python -u tools/lanczos_sweep.py --variants fused,pipelined,mv --rounds 3 >> "$O/pipe.jsonl" 2>&1 ;;
+    csr)
+      timeout -k 10 400 python -u tools/csr_general.py > "$O/csr.jsonl" 2> "$O/csr.err" ;;
+    *)
+      echo "unknown task $1" >&2; return 2 ;;
+  esac
+}
+
+for t in "$@"; do
+  echo "[gpu.sh] $t" >&2
+  run_task "$t" || { echo "[gpu.sh] task $t failed (status $?)" >&2; exit 1; }
+done
