@@ -40,11 +40,12 @@ def cpu_baseline(N, rp, c, v, steps, gpu_alpha, fused):
     u0, u1, u2 = np.zeros(n), np.zeros(n), np.zeros(n)
     oracle.lib.orc_random_vec(n, 123, u0)
     alpha, beta = np.zeros(steps), np.zeros(steps + 1)
+    fast = oracle.fast_lib()  # -O3 -march=x86-64-v3 build of the restatement (oracle/Makefile)
     t0 = time.perf_counter()
     if fused:
-        oracle.lib.orc_lanczos_fused(n, rp, c, v, steps, u0, alpha, beta, None)
+        fast.orc_lanczos_fused(n, rp, c, v, steps, u0, alpha, beta, None)
     else:
-        oracle.lib.orc_lanczos_rotating(n, rp, c, v, steps, u0, u1, u2, alpha, beta)
+        fast.orc_lanczos_rotating(n, rp, c, v, steps, u0, u1, u2, alpha, beta)
     dt = time.perf_counter() - t0
     k = min(steps, len(gpu_alpha))
     rel = float(np.max(np.abs(alpha[:k] - gpu_alpha[:k]) / np.abs(alpha[:k]))) if k else None
@@ -76,10 +77,11 @@ def cpu_replicas(N, steps, fused, threads):
         bar.wait()  # all replicas built
         bar.wait()  # go
         if not err:
+            fast = oracle.fast_lib()
             if fused:
-                oracle.lib.orc_lanczos_fused(n, rp, c, v, steps, u0, alpha, beta, None)
+                fast.orc_lanczos_fused(n, rp, c, v, steps, u0, alpha, beta, None)
             else:
-                oracle.lib.orc_lanczos_rotating(n, rp, c, v, steps, u0, u1, u2, alpha, beta)
+                fast.orc_lanczos_rotating(n, rp, c, v, steps, u0, u1, u2, alpha, beta)
         bar.wait()  # done
 
     ts = [threading.Thread(target=replica) for _ in range(threads)]
@@ -388,7 +390,8 @@ def main():
         cv, cdt, rel = cpu_baseline(N, rp, c, v, args.cpu_steps, alpha, fused)
         out["cpu_baseline"] = {"value": round(cv, 4), "unit": "iters/s", "cores": 1, "kind": "port",
                                "sample": f"{args.cpu_steps} Lanczos steps on the same {N}^3 matrix and start "
-                                         f"vector, oracle/oracle.cc single thread ({cdt:.1f} s)",
+                                         f"vector, oracle/oracle.cc built -O3 -march=x86-64-v3 "
+                                         f"(liboracle_fast.so), single thread ({cdt:.1f} s)",
                                "alpha_max_rel_diff_vs_gpu": rel, "cpu_model": cpu_model()}
         P = args.cpu_replicas
         usable = len(os.sched_getaffinity(0))

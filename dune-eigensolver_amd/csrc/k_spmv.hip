@@ -1594,15 +1594,19 @@ static MarchPlan march_plan(const eig_mat_s &A, int mode, i64 zb = 0, i64 ze = -
   const i64 nplanes = ze - zb;
   if (nplanes < 2 || (zb == 0 && nplanes < 4)) return mp;
   const i64 ncol = D / chunk;
-  // one work item per resident wave slot: the fused kernel is built for 7 waves / SIMD, the others
-  // for 8 (launch bounds); items beyond the resident slots would run as a second, thin round
-  const i64 resident = (fused ? 7LL : 8LL) * 4 * A.ctx->num_cu;  // waves
-  i64 nseg = std::max<i64>(1, resident / ncol);
+  // about one work item per resident wave slot (8 per SIMD)
+  const i64 resident = 8LL * 4 * A.ctx->num_cu;  // waves
+  i64 nseg = std::max<i64>(1, (resident + ncol - 1) / ncol);
   nseg = std::min<i64>(nseg, nplanes);
-  // fused step on wide planes (>= 1024 columns: 3-D grids from 256^2 per plane) with few planes --
-  // the slab of one rank in a strong-scaling run: runs of >= 15 planes beat full occupancy
-  // (256 x 256 x 32 box: 2 runs 33.4 us vs 8 runs 37.8 us; at 256^3 the rule keeps 7 runs)
-  if (fused && ncol >= 1024) nseg = std::max<i64>(1, std::min<i64>(nseg, nplanes / 15));
+  // the fused step prefers longer plane runs (fewer fronts in the XCDs' L2 at once) wherever the
+  // grid is small; measured with eig_mat_tune sweeps (tools/gpu.sh latency, profiles/r03h_latency):
+  //  * wide planes (>= 1024 columns: 256^2 per plane): 256^3 8 runs 220.8 us (7: 224.6, 6: 232.5,
+  //    4: 267.3); one rank's 256^2 x 32 slab 2 runs 33.7 us (4: 35.5, 7: 36.7, 1: 47.3); the 16-plane
+  //    slab 2 runs 21.7 us (1: 28.3, 4: 23.9, 7: 26.2)  ->  nplanes / 32 runs, at least 2, at most 8
+  //  * narrower planes (128^3: 256 columns): 12 runs 34.9 us (16: 35.5, 28: 36.5, 32: 36.7)  ->
+  //    runs of >= 10 planes
+  if (fused && ncol >= 1024) nseg = std::min<i64>(nplanes / 2 > 0 ? nplanes / 2 : 1, std::max<i64>(2, std::min<i64>(8, nplanes / 32)));
+  else if (fused) nseg = std::max<i64>(1, std::min<i64>(nseg, nplanes / 10));
   if (A.tune_march_runs > 0) nseg = std::min<i64>(A.tune_march_runs, nplanes);  // eig_mat_tune
   while (nseg > 1 && (ncol * nseg + kWaves - 1) / kWaves > kMaxRedBlocks) --nseg;
   if ((ncol * nseg + kWaves - 1) / kWaves > kMaxRedBlocks) return mp;

@@ -24,10 +24,10 @@ def build():
     subprocess.check_call(["make", "-s", "-C", _HERE])
 
 
-def _load():
-    if not os.path.exists(_LIB) or os.path.getmtime(_LIB) < os.path.getmtime(os.path.join(_HERE, "oracle.cc")):
+def _load(path=_LIB):
+    if not os.path.exists(path) or os.path.getmtime(path) < os.path.getmtime(os.path.join(_HERE, "oracle.cc")):
         build()
-    lib = ctypes.CDLL(_LIB)
+    lib = ctypes.CDLL(path)
     sig = {
         "orc_laplace2d_nnz": (_i64, [_int]),
         "orc_laplace2d": (None, [_int, _i64p, _i32p, _f64p]),
@@ -79,6 +79,16 @@ def _load():
 
 
 lib = _load()
+_fast = None
+
+
+def fast_lib():
+    """liboracle_fast.so: the same restatement built -O3 -march=x86-64-v3 (FMA contraction on) -- the
+    CPU baseline bench.py times; never used as a parity checker."""
+    global _fast
+    if _fast is None:
+        _fast = _load(os.path.join(_HERE, "liboracle_fast.so"))
+    return _fast
 
 
 class CSR:
