@@ -45,7 +45,7 @@ static inline int grid_cap(i64 work, i64 per_block, int cap)
 // (Measured and dropped: a lane-per-row mapping with 16 columns per matrix pass -- 131 vs 119 us
 // for the 7-point SpMM at 128^3 -- and 2 column blocks per quad pass.)
 // ---------------------------------------------------------------------------------------------
-enum { kStore = 0, kCheb = 1 };
+enum { kStore = 0, kCheb = 1, kResid = 2 };  // kResid: Y = B - A X (multigrid residual)
 
 // Quad mapping: 4 lanes per row (lane owns column pair 2 (l & 3), 2 (l & 3) + 1 of every column
 // block), 16 rows per wave, a workgroup (4 waves) per 64-row slice, MB column blocks per matrix
@@ -129,7 +129,7 @@ __global__ __launch_bounds__(64 * W) void k_sell_mv8q(i64 nrows, i64 nslices, co
       for (int u = 0; u < U; ++u)
 #pragma unroll
         for (int q = 0; q < MB; ++q) xv[u][q] = *reinterpret_cast<const double2 *>(Xc + ((i64)q * ld + c[u]) * 8);
-      if (EPI == kStore)
+      if (EPI == kStore || EPI == kResid)
       {
         // bitwise the reference: separately rounded products and sums over stored entries only
 #pragma unroll
@@ -175,6 +175,12 @@ __global__ __launch_bounds__(64 * W) void k_sell_mv8q(i64 nrows, i64 nslices, co
         {
           o0 = acc[q].x;
           o1 = acc[q].y;
+        }
+        else if (EPI == kResid)
+        {
+          const dv2 bb = __builtin_nontemporal_load(reinterpret_cast<const dv2 *>(Bv + at));
+          o0 = bb.x - acc[q].x;
+          o1 = bb.y - acc[q].y;
         }
         else
         {
@@ -279,7 +285,7 @@ __global__ __launch_bounds__(256) void k_sell_mv8g(i64 nrows, i64 nslices, const
 #pragma unroll
           for (int q = 0; q < MB; ++q)
           {
-            if (EPI == kStore)
+            if (EPI == kStore || EPI == kResid)
             {
               const double tx = acc[h][q].x + a[u][h] * xv[u][h][q].x, ty = acc[h][q].y + a[u][h] * xv[u][h][q].y;
               acc[h][q].x = okk[u][h] ? tx : acc[h][q].x;
@@ -306,6 +312,12 @@ __global__ __launch_bounds__(256) void k_sell_mv8g(i64 nrows, i64 nslices, const
         const i64 at = ((i64)(b0 + q) * ld + own + r) * 8 + 2 * cp;
         double *yr = Y + at;
         double o0 = acc[h][q].x, o1 = acc[h][q].y;
+        if (EPI == kResid)
+        {
+          const dv2 bb = __builtin_nontemporal_load(reinterpret_cast<const dv2 *>(Bv + at));
+          o0 = bb.x - o0;
+          o1 = bb.y - o1;
+        }
         if (EPI == kCheb)
         {
           const double2 xk = *reinterpret_cast<const double2 *>(X + at);
@@ -417,6 +429,13 @@ void launch_sell_mv8(const eig_mat_s &A, i64 m, const double *X, double *Y, hipS
   if (launch_box_spmm(A, m, X, Y, s)) return;
   if (launch_spmm_march(A, m, X, Y, s)) return;
   sell_mv8<kStore>(A, m, X, Y, nullptr, nullptr, 0.0, 0.0, s);
+}
+
+void launch_resid_mv8(const eig_mat_s &A, i64 m, const double *X, const double *B, double *R, hipStream_t s)
+{
+  // R = B - A X; R may be B (each row reads its own B entry before writing it), never X
+  if (launch_box_resid(A, m, X, B, R, s)) return;
+  sell_mv8<kResid>(A, m, X, R, B, nullptr, 0.0, 0.0, s);
 }
 
 void launch_cheb_step(const eig_mat_s &M, i64 m, const double *Xk, double *Xold, const double *B, const double *dinv,

@@ -29,7 +29,7 @@ constexpr int kBoxHX = kBoxTX + 2, kBoxHY = kBoxTY + 2;        // with the one-r
 constexpr int kBoxThreads = 1024;  // 16 waves: wave = (tile y, x half), lane = (x, 4-column quad)
 constexpr int kBoxChunks = kBoxHY * kBoxHX * 4 * 4;            // 16-B chunks of one plane (rows x blocks x 4)
 constexpr int kBoxRounds = (kBoxChunks + kBoxThreads - 1) / kBoxThreads;
-enum { kBoxStore = 0, kBoxCheb = 1 };
+enum { kBoxStore = 0, kBoxCheb = 1, kBoxResid = 2 };  // kBoxResid: Y = B - A X (multigrid residual)
 constexpr int kBoxMaxNd = 15;  // offsets the kernel holds in registers (P1 Kuhn: 15, 7-point: 7)
 
 typedef double dv2b __attribute__((ext_vector_type(2)));
@@ -176,16 +176,16 @@ __global__ __launch_bounds__(kBoxThreads) void k_box_mv32(BoxGeom g, i64 ld, con
   dv2b bb[2] = {}, xo[2] = {}, bn[2] = {}, xn[2] = {};
   double gd = 0.0, gn = 0.0;
   auto fetch_cheb = [&](int zz, dv2b (&b2)[2], dv2b (&x2)[2], double &gg) {
-    if (EPI != kBoxCheb || !own || zz >= z1) return;
+    if (EPI == kBoxStore || !own || zz >= z1) return;
     const i64 r = (i64)x + (i64)g.nx * y + (i64)g.P * zz;
-    const double *br = Bv + (i64)blk * ld * 8 + r * 8 + c4, *yr = Xold + (i64)blk * ld * 8 + r * 8 + c4;
+    const double *br = Bv + (i64)blk * ld * 8 + r * 8 + c4;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) b2[j] = __builtin_nontemporal_load(reinterpret_cast<const dv2b *>(br) + j);
+    if (EPI != kBoxCheb) return;
+    const double *yr = Xold + (i64)blk * ld * 8 + r * 8 + c4;
     gg = gamma * __builtin_nontemporal_load(dinv + r);
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
-    {
-      b2[j] = __builtin_nontemporal_load(reinterpret_cast<const dv2b *>(br) + j);
-      x2[j] = __builtin_nontemporal_load(reinterpret_cast<const dv2b *>(yr) + j);
-    }
+    for (int j = 0; j < 2; ++j) x2[j] = __builtin_nontemporal_load(reinterpret_cast<const dv2b *>(yr) + j);
   };
   // prologue: X planes z0 - 1 .. z0 + 1, the values of plane z0, the Chebyshev operands of z0
   fetch(z0 - 1);
@@ -234,6 +234,12 @@ __global__ __launch_bounds__(kBoxThreads) void k_box_mv32(BoxGeom g, i64 ld, con
       {
 #pragma unroll
         for (int j = 0; j < 4; j += 2) __builtin_nontemporal_store(dv2b{acc[j], acc[j + 1]}, reinterpret_cast<dv2b *>(yr + j));
+      }
+      else if (EPI == kBoxResid)
+      {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          __builtin_nontemporal_store(dv2b{bb[j].x - acc[2 * j], bb[j].y - acc[2 * j + 1]}, reinterpret_cast<dv2b *>(yr) + j);
       }
       else
       {
@@ -368,10 +374,10 @@ __global__ __launch_bounds__(kCThreads) void k_boxc_mv8(BoxGeom g, i64 ld, const
   const int cxy = (own ? box_cls1(y, g.ny) * 3 + box_cls1(x, g.nx) : 0);
   dv2b bb = {}, xo = {}, bn = {}, xn = {};
   auto fetch_cheb = [&](int zz, dv2b &b2, dv2b &x2) {
-    if (EPI != kBoxCheb || !own || zz >= z1) return;
+    if (EPI == kBoxStore || !own || zz >= z1) return;
     const i64 r = (i64)x + (i64)g.nx * y + (i64)g.P * zz;
     b2 = __builtin_nontemporal_load(Bb + r * 4 + cp);
-    x2 = __builtin_nontemporal_load(Ob + r * 4 + cp);
+    if (EPI == kBoxCheb) x2 = __builtin_nontemporal_load(Ob + r * 4 + cp);
   };
   fetch(z0 - 1);
   store(z0 - 1);
@@ -411,6 +417,8 @@ __global__ __launch_bounds__(kCThreads) void k_boxc_mv8(BoxGeom g, i64 ld, const
       const i64 r = (i64)x + (i64)g.nx * y + (i64)g.P * z;
       if (EPI == kBoxStore)
         __builtin_nontemporal_store(acc, Yb + r * 4 + cp);
+      else if (EPI == kBoxResid)
+        __builtin_nontemporal_store(dv2b{bb.x - acc.x, bb.y - acc.y}, Yb + r * 4 + cp);
       else
       {
         const dv2b xc = ring[((z % 3) + 3) % 3][hrow][cp];
@@ -597,7 +605,7 @@ bool box_prepare(const eig_mat_s &Ac)
 // Y = A X (EPI store) or the Chebyshev step into Xold (EPI cheb) for m % 32 == 0 columns on the box
 // kernel; false when the matrix has no box geometry (the caller takes the band march).
 static bool launch_box(const eig_mat_s &A, i64 m, const double *X, double *Y, const double *Xold, const double *Bv,
-                       const double *dinv, double omega, double gamma, bool cheb, hipStream_t s)
+                       const double *dinv, double omega, double gamma, int epi, hipStream_t s)
 {
   if (m <= 0 || m % 8 != 0 || !box_prepare(A)) return false;
   if (A.box_ctab)
@@ -621,9 +629,13 @@ static bool launch_box(const eig_mat_s &A, i64 m, const double *X, double *Y, co
       g.dxy[k] = k < A.sym_nd ? A.box_dy[k] * kCHX + A.box_dx[k] : 0;
     }
     const dim3 grid((unsigned)(g.ntx * g.nty * g.nseg), (unsigned)(m / 8));
-    if (cheb)
+    if (epi == kBoxCheb)
       hipLaunchKernelGGL(k_boxc_mv8<kBoxCheb>, grid, dim3(kCThreads), 0, s, g, A.window,
                          (const double *)A.box_ctab, (const unsigned *)A.box_cmask, X, Y, Xold, Bv, omega, gamma);
+    else if (epi == kBoxResid)
+      hipLaunchKernelGGL(k_boxc_mv8<kBoxResid>, grid, dim3(kCThreads), 0, s, g, A.window,
+                         (const double *)A.box_ctab, (const unsigned *)A.box_cmask, X, Y, (const double *)nullptr, Bv,
+                         0.0, 0.0);
     else
       hipLaunchKernelGGL(k_boxc_mv8<kBoxStore>, grid, dim3(kCThreads), 0, s, g, A.window,
                          (const double *)A.box_ctab, (const unsigned *)A.box_cmask, X, Y, (const double *)nullptr,
@@ -654,10 +666,14 @@ static bool launch_box(const eig_mat_s &A, i64 m, const double *X, double *Y, co
   for (i64 c0 = 0; c0 < m; c0 += 32)
   {
     const i64 off = c0 * ld;  // 4 column blocks of ld rows x 8
-    if (cheb)
+    if (epi == kBoxCheb)
       hipLaunchKernelGGL(k_box_mv32<kBoxCheb>, dim3((unsigned)(tiles * g.nseg)), dim3(kBoxThreads), 0, s, g, ld,
                          (const double *)A.box_val, m32, m8, X + off, Y + off, Xold + off, Bv + off, dinv, omega,
                          gamma);
+    else if (epi == kBoxResid)
+      hipLaunchKernelGGL(k_box_mv32<kBoxResid>, dim3((unsigned)(tiles * g.nseg)), dim3(kBoxThreads), 0, s, g, ld,
+                         (const double *)A.box_val, m32, m8, X + off, Y + off, (const double *)nullptr, Bv + off,
+                         (const double *)nullptr, 0.0, 0.0);
     else
       hipLaunchKernelGGL(k_box_mv32<kBoxStore>, dim3((unsigned)(tiles * g.nseg)), dim3(kBoxThreads), 0, s, g, ld,
                          (const double *)A.box_val, m32, m8, X + off, Y + off, (const double *)nullptr,
@@ -669,13 +685,18 @@ static bool launch_box(const eig_mat_s &A, i64 m, const double *X, double *Y, co
 
 bool launch_box_spmm(const eig_mat_s &A, i64 m, const double *X, double *Y, hipStream_t s)
 {
-  return launch_box(A, m, X, Y, nullptr, nullptr, nullptr, 0.0, 0.0, false, s);
+  return launch_box(A, m, X, Y, nullptr, nullptr, nullptr, 0.0, 0.0, kBoxStore, s);
+}
+
+bool launch_box_resid(const eig_mat_s &A, i64 m, const double *X, const double *B, double *R, hipStream_t s)
+{
+  return launch_box(A, m, X, R, nullptr, B, nullptr, 0.0, 0.0, kBoxResid, s);
 }
 
 bool launch_box_cheb(const eig_mat_s &M, i64 m, const double *Xk, double *Xold, const double *B, const double *dinv,
                      double omega, double gamma, hipStream_t s, double *Xnew)
 {
-  return launch_box(M, m, Xk, Xnew ? Xnew : Xold, Xold, B, dinv, omega, gamma, true, s);
+  return launch_box(M, m, Xk, Xnew ? Xnew : Xold, Xold, B, dinv, omega, gamma, kBoxCheb, s);
 }
 
 }  // namespace eigmi

@@ -367,7 +367,7 @@ void launch_gram_panel(eig_ctx_t ctx, i64 n, i64 ld, i64 m1, i64 m2, const doubl
 
 // ---------------------------------------------------------------------------------------------
 // a9 diagonal block, fused column MGS (kernels_cpp.hh:202-229).  Pass k (0..8) over the n x 8
-// block Qb, one thread per row.  Ssum (8x8) holds the RAW sums s[k][j] = q_k . q_j of each pass
+// block Qb, four lanes per row.  Ssum (8x8) holds the RAW sums s[k][j] = q_k . q_j of each pass
 // (so a distributed run can allreduce them between passes); pass k first finalises row k-1
 // exactly like the reference,  S[k-1][j] = s/s[k-1][k-1] (j > k-1), S[k-1][k-1] = 1/sqrt(s),
 // then applies it:  q_j -= S[k-1][j] q_{k-1} (j > k-1), q_{k-1} *= S[k-1][k-1], and (k < 8)
@@ -377,51 +377,48 @@ __global__ __launch_bounds__(kStreamThreads) void k_mgs_pass(i64 n, double *__re
                                                              double *__restrict__ Ssum, double *partials,
                                                              unsigned *ticket)
 {
+  // quad mapping: 4 lanes per row, lane ql holds columns 2 ql, 2 ql + 1 (one 16-B load: a wave
+  // instruction reads 16 whole 64-B rows); the pivot columns are broadcast inside the quad
   __shared__ double tot[8];
-  double sp[8];
+  const int ql = threadIdx.x & 3;
+  const int c0 = 2 * ql, c1 = c0 + 1;
+  const int qbase = (threadIdx.x & 63) & ~3;
+  double sp0 = 0.0, sp1 = 0.0;  // this lane's S[k-1][c] (0 for c < k-1, 1/sqrt for c = k-1)
+  const int kp = k - 1;
   if (k > 0)
   {
-    const int kp = k - 1;
     const double skk = Ssum[kp * 8 + kp];
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      sp[j] = (j > kp) ? Ssum[kp * 8 + j] / skk : ((j == kp) ? 1.0 / sqrt(skk) : 0.0);
+    sp0 = (c0 > kp) ? Ssum[kp * 8 + c0] / skk : ((c0 == kp) ? 1.0 / sqrt(skk) : 0.0);
+    sp1 = (c1 > kp) ? Ssum[kp * 8 + c1] / skk : ((c1 == kp) ? 1.0 / sqrt(skk) : 0.0);
   }
-  double acc[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) acc[j] = 0.0;
-  for (i64 i = (i64)blockIdx.x * kStreamThreads + threadIdx.x; i < n; i += (i64)gridDim.x * kStreamThreads)
+  double a0 = 0.0, a1 = 0.0;
+  const i64 stride = (i64)gridDim.x * (kStreamThreads / 4);
+  for (i64 i = ((i64)blockIdx.x * kStreamThreads + threadIdx.x) >> 2; i < n; i += stride)
   {
-    double q[8];
-    double2 *row = reinterpret_cast<double2 *>(Qb + i * 8);
-#pragma unroll
-    for (int h = 0; h < 4; ++h)
-    {
-      const double2 v = row[h];
-      q[2 * h] = v.x;
-      q[2 * h + 1] = v.y;
-    }
+    double2 *row = reinterpret_cast<double2 *>(Qb + i * 8) + ql;
+    double2 v = *row;
     if (k > 0)
     {
-      const int kp = k - 1;
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (j > kp) q[j] -= sp[j] * q[kp];
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (j == kp) q[j] *= sp[kp];
-#pragma unroll
-      for (int h = 0; h < 4; ++h) row[h] = make_double2(q[2 * h], q[2 * h + 1]);
+      // q_j -= S[kp][j] q_kp (j > kp) with the OLD q_kp, then q_kp *= S[kp][kp]
+      const double qkp = __shfl((kp & 1) ? v.y : v.x, qbase + (kp >> 1), 64);
+      if (c0 > kp) v.x -= sp0 * qkp;
+      if (c1 > kp) v.y -= sp1 * qkp;
+      if (c0 == kp) v.x *= sp0;
+      if (c1 == kp) v.y *= sp1;
+      *row = v;
     }
     if (k < 8)
     {
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (j >= k) acc[j] += q[k] * q[j];
+      const double qk = __shfl((k & 1) ? v.y : v.x, qbase + (k >> 1), 64);
+      if (c0 >= k) a0 += qk * v.x;
+      if (c1 >= k) a1 += qk * v.y;
     }
   }
   if (k >= 8) return;
-  if (grid_sum<8, kStreamThreads>(acc, partials, ticket, tot))
+  double vals[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) vals[j] = (j == c0) ? a0 : ((j == c1) ? a1 : 0.0);
+  if (grid_sum<8, kStreamThreads>(vals, partials, ticket, tot))
   {
     if (threadIdx.x < 8) Ssum[k * 8 + threadIdx.x] = (threadIdx.x >= (unsigned)k) ? tot[threadIdx.x] : 0.0;
   }
@@ -429,7 +426,7 @@ __global__ __launch_bounds__(kStreamThreads) void k_mgs_pass(i64 n, double *__re
 
 void launch_mgs_pass(i64 n, double *Qb, int k, double *Ssum, int ticket, hipStream_t s, ReduceWS red)
 {
-  const int G = grid_for(n, kStreamThreads * 4, 1024);
+  const int G = grid_for(n * 4, kStreamThreads * 4, 1024);
   hipLaunchKernelGGL(k_mgs_pass, dim3(G), dim3(kStreamThreads), 0, s, n, Qb, k, Ssum, red.partials,
                      red.ticket(ticket));
 }

@@ -44,7 +44,7 @@ struct MgLevel {
   double lmax = 2.0;                          // Gershgorin bound of D^-1 A
   double clo = 0.0, chi = 0.0;                // coarsest: exact spectrum bounds of D^-1 A
   int cdeg = 0;                               // coarsest: Chebyshev degree
-  DevBuf *dinv = nullptr, *B = nullptr, *X = nullptr, *T = nullptr, *C[3] = {nullptr, nullptr, nullptr};
+  DevBuf *dinv = nullptr, *B = nullptr, *T = nullptr, *Z = nullptr, *C[4] = {nullptr, nullptr, nullptr, nullptr};
 };
 
 struct eig_mg_s {
@@ -56,7 +56,7 @@ struct eig_mg_s {
   {
     for (auto &L : lev)
     {
-      for (DevBuf *b : {L.dinv, L.B, L.X, L.T, L.C[0], L.C[1], L.C[2]}) delete b;
+      for (DevBuf *b : {L.dinv, L.B, L.T, L.Z, L.C[0], L.C[1], L.C[2], L.C[3]}) delete b;
       if (L.own && L.A) eig_mat_destroy(L.A);
     }
   }
@@ -223,42 +223,43 @@ void spectrum_bounds(const HostCsr &A, i64 n, double &lo, double &hi)
   EIG_CHECK(lo > 0.0, EIG_ERR_BREAKDOWN, "multigrid: the coarsest operator is not positive definite");
 }
 
-void alloc_level(MgLevel &L, int m)
+void alloc_level(MgLevel &L, int m, hipStream_t s)
 {
   const size_t bytes = (size_t)std::max<i64>(L.n, 1) * m * sizeof(double);
   L.dinv = new DevBuf((size_t)std::max<i64>(L.n, 1) * sizeof(double));
   L.B = new DevBuf(bytes);
-  L.X = new DevBuf(bytes);
   L.T = new DevBuf(bytes);
+  L.Z = new DevBuf(bytes);  // a zero block: x_0 of the Chebyshev smoothers (cheb_solve)
+  EIG_HIP(hipMemsetAsync(L.Z->d(), 0, bytes, s));
   for (auto &c : L.C) c = new DevBuf(bytes);
 }
 
-// x (output) = V_l b: the V-cycle on level l (all buffers n_l x m, ld = n_l)
-void vcycle(eig_mg_s &mg, size_t l, i64 m, const double *b, double *x)
+// V_l b: the V-cycle on level l (all buffers n_l x m, ld = n_l); returns the level buffer (one of
+// C[0..3]) that holds the result.  Residuals come from the SpMM's residual epilogue (T = b - A x in
+// one pass), the smoothers start from the level's zero block, and the smoothed iterate stays where
+// cheb_solve left it (the post-smoother takes the three other C buffers).
+double *vcycle(eig_mg_s &mg, size_t l, i64 m, const double *b)
 {
   MgLevel &L = mg.lev[l];
   hipStream_t s = mg.ctx->stream;
-  const size_t bytes = (size_t)L.n * m * sizeof(double);
+  double *C[4] = {L.C[0]->d(), L.C[1]->d(), L.C[2]->d(), L.C[3]->d()};
   if (l + 1 == mg.lev.size())
-  {
-    const double *p = cheb_solve(*L.A, m, L.cdeg, L.clo, L.chi, b, L.dinv->d(), L.C[0]->d(), L.C[1]->d(), L.C[2]->d(), s);
-    EIG_HIP(hipMemcpyAsync(x, p, bytes, hipMemcpyDeviceToDevice, s));
-    return;
-  }
+    return cheb_solve(*L.A, m, L.cdeg, L.clo, L.chi, b, L.dinv->d(), C[0], C[1], C[2], s, L.Z->d());
   MgLevel &Cl = mg.lev[l + 1];
   const double lo = L.lmax / mg.ratio, hi = L.lmax;
-  const double *p = cheb_solve(*L.A, m, mg.nu, lo, hi, b, L.dinv->d(), L.C[0]->d(), L.C[1]->d(), L.C[2]->d(), s);
-  EIG_HIP(hipMemcpyAsync(x, p, bytes, hipMemcpyDeviceToDevice, s));
+  double *x = cheb_solve(*L.A, m, mg.nu, lo, hi, b, L.dinv->d(), C[0], C[1], C[2], s, L.Z->d());
   double *T = L.T->d();
-  launch_sell_mv8(*L.A, m, x, T, s);
-  launch_mv8_axpby(L.n, m, L.n, 1.0, b, -1.0, T, s);  // T = b - A x
+  launch_resid_mv8(*L.A, m, x, b, T, s);  // T = b - A x
   launch_mg_restrict(L.dim, Cl.dim, m, L.n, Cl.n, T, Cl.B->d(), s);
-  vcycle(mg, l + 1, m, Cl.B->d(), Cl.X->d());
-  launch_mg_prolong_add(L.dim, Cl.dim, m, L.n, Cl.n, Cl.X->d(), x, s);
-  launch_sell_mv8(*L.A, m, x, T, s);
-  launch_mv8_axpby(L.n, m, L.n, 1.0, b, -1.0, T, s);  // T = b - A x
-  p = cheb_solve(*L.A, m, mg.nu, lo, hi, T, L.dinv->d(), L.C[0]->d(), L.C[1]->d(), L.C[2]->d(), s);
+  const double *xc = vcycle(mg, l + 1, m, Cl.B->d());
+  launch_mg_prolong_add(L.dim, Cl.dim, m, L.n, Cl.n, xc, x, s);
+  launch_resid_mv8(*L.A, m, x, b, T, s);  // T = b - A x
+  double *q[3];
+  for (int i = 0, j = 0; i < 4; ++i)
+    if (C[i] != x) q[j++] = C[i];
+  const double *p = cheb_solve(*L.A, m, mg.nu, lo, hi, T, L.dinv->d(), q[0], q[1], q[2], s, L.Z->d());
   launch_mv8_axpby(L.n, m, L.n, 1.0, p, 1.0, x, s);  // x += post-smoothing correction
+  return x;
 }
 
 }  // namespace
@@ -273,19 +274,19 @@ void mg_apply(eig_mg_s &mg, i64 m, const double *B, double *X, int cycles)
   EIG_CHECK(m > 0 && m % 8 == 0 && m <= mg.max_cols && cycles >= 1, EIG_ERR_ARG,
             "multigrid solve: 8 <= m <= max_cols (multiple of 8), cycles >= 1");
   const size_t bytes = (size_t)L.n * m * sizeof(double);
-  double *R = L.B->d(), *E = L.X->d(), *T = L.T->d();
-  EIG_HIP(hipMemcpyAsync(R, B, bytes, hipMemcpyDeviceToDevice, s));
+  double *R = L.B->d();
+  const double *rhs = B;  // residual of the current iterate (B itself before the first correction)
   for (int it = 0; it < cycles; ++it)
   {
-    vcycle(mg, 0, m, R, E);
+    const double *E = vcycle(mg, 0, m, rhs);
     if (it == 0)
       EIG_HIP(hipMemcpyAsync(X, E, bytes, hipMemcpyDeviceToDevice, s));
     else
       launch_mv8_axpby(L.n, m, L.n, 1.0, E, 1.0, X, s);
     if (it + 1 < cycles)
     {
-      launch_sell_mv8(*L.A, m, E, T, s);
-      launch_mv8_axpby(L.n, m, L.n, -1.0, T, 1.0, R, s);  // r -= A e
+      launch_resid_mv8(*L.A, m, E, rhs, R, s);  // r -= A e (in place after the first iteration)
+      rhs = R;
     }
   }
 }
@@ -329,7 +330,7 @@ extern "C" int eig_mg_create(eig_mat_t A, int nx, int ny, int nz, int max_cols, 
       {
         MgLevel &F = mg->lev.back();
         F.lmax = gershgorin(h, F.n);
-        alloc_level(F, max_cols);
+        alloc_level(F, max_cols, s);
         launch_diag_inv(*F.A, F.dinv->d(), s);
         const bool last = F.n <= 64 || F.dim[0] < 3 || F.dim[1] < 3 || F.dim[2] < 3;
         if (last)
@@ -391,8 +392,7 @@ extern "C" int eig_mg_solve(eig_mg_t mg, int64_t m, const double *B, double *X, 
       MgLevel &L = mg->lev[0];
       double *T = L.T->d();
       double *dp = (double *)ctx_buffer(ctx, 9, (size_t)2 * m * sizeof(double));
-      launch_sell_mv8(*L.A, m, X, T, s);
-      launch_mv8_axpby(L.n, m, L.n, 1.0, B, -1.0, T, s);
+      launch_resid_mv8(*L.A, m, X, B, T, s);
       launch_dot_diag_mv8(L.n, m, T, T, dp, 0, s, ctx->red);
       launch_dot_diag_mv8(L.n, m, B, B, dp + m, 0, s, ctx->red);
       std::vector<double> h((size_t)2 * m);

@@ -50,9 +50,16 @@ def test_mg_ref_hierarchy_is_symmetric_galerkin():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kind,N,m", [("p1", 12, 8), ("p1", 24, 32), ("poisson7", 20, 16), ("p1", 17, 8)])
+@pytest.mark.parametrize("kind,N,m", [("p1", 12, 8), ("p1", 24, 32), ("poisson7", 20, 16), ("p1", 17, 8),
+                                      ("p1var", 24, 32), ("p1var", 18, 24)])
 def test_mg_solve_matches_restatement(ctx, kind, N, m):
-    K = oracle.p1_kuhn(N)[0] if kind == "p1" else poisson7(N)
+    """p1var: K + a random positive diagonal -- rows no longer equal their geometric class, so the
+    fine level runs the box-image kernels (k_box_mv32) instead of the row-class ones."""
+    if kind == "p1var":
+        K = oracle.p1_kuhn(N)[0]
+        K = (K + sp.diags(np.random.default_rng(N).uniform(0.0, 0.1, K.shape[0]) / (N + 1))).tocsr()
+    else:
+        K = oracle.p1_kuhn(N)[0] if kind == "p1" else poisson7(N)
     n = K.shape[0]
     dK = _upload(ctx, K)
     mg = eigmi.Multigrid(dK, (N, N, N), max_cols=32, smooth_degree=2, smooth_ratio=5.0)
