@@ -159,6 +159,9 @@ def main():
                          "allreduces; auto: fused on one GPU, on N > 1 the faster of fused / pipelined "
                          "in a short timed trial before the timed region (all ranks agree)")
     ap.add_argument("--trial-steps", type=int, default=40, help="steps per variant of the auto trial (N > 1)")
+    ap.add_argument("--comm-self", action="store_true",
+                    help="one GPU: attach a one-rank RCCL communicator with EIG_COMM_ALWAYS, so every step's "
+                         "allreduce runs through ncclAllReduce (the transport's per-step cost without xGMI)")
     ap.add_argument("--launch", choices=["auto", "graph", "eager"], default="auto",
                     help="timed steps as one hipGraph replay or launched one by one; auto = graph when "
                          "N > 1 (host-bound halo/allreduce calls), eager at N = 1 (measured faster there)")
@@ -179,6 +182,8 @@ def main():
 
     # EIGMI_FORCE_DEVICE pins every rank to one device (RCCL path rehearsal on a 1-GPU box)
     ctx = eigmi.Context(int(os.environ.get("EIGMI_FORCE_DEVICE", local)))
+    if world == 1 and args.comm_self:
+        ctx.comm_init(1, 0, eigmi.Context.unique_id(), always=True)
     if world > 1:
         import torch
         uid = eigmi.Context.unique_id() if rank == 0 else bytes(128)
@@ -366,7 +371,8 @@ def main():
                                f" ({VARIANT_NAME[variant]})",
                    "N": N, "n": n, "nnz": nnz_total,
                    "parallelism": (f"row-partition z-slabs x{world} (RCCL halo, {ctx.comm_info()['allreduce']} "
-                                   "allreduce)") if world > 1 else "single GPU"},
+                                   "allreduce)") if world > 1 else
+                                  ("single GPU, one-rank RCCL allreduce per step" if args.comm_self else "single GPU")},
         # SURVEY 8(d)'s CSR step bytes (12 nnz + 4(n+1) + 48 n) / step time: an equivalent rate, not
         # HBM traffic (the band image streams fewer bytes; roofline.* prices the kernel's own bytes)
         "step_csr_equiv_GBs": round(step_bytes / (dt / K) / 1e9, 1),

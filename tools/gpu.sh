@@ -16,6 +16,7 @@
 #   latency              fused step vs eig_mv across sizes and slabs, plane-run counts  -> latency.jsonl
 #   pipe                 fused vs pipelined on one rank's slab and the cube   -> pipe.jsonl
 #   csr                  general (scrambled + RCM) 256^3 matrix: SpMV / Lanczos kernels  -> csr.jsonl
+#   commself             bench.py with and without a one-rank RCCL allreduce per step (eager / graph, 128^3 / 256^3)
 set -o pipefail
 TAG=${TAG:-scratch}
 O=gpurun_out/$TAG
@@ -59,6 +60,13 @@ run_task() {
     pipe)
       timeout -k 10 200 python -u tools/lanczos_sweep.py --slab 32 --variants fused,pipelined,mv --rounds 5 > "$O/pipe.jsonl" 2>&1 && \
       timeout -k 10 200 python -u tools/lanczos_sweep.py --variants fused,pipelined,mv --rounds 3 >> "$O/pipe.jsonl" 2>&1 ;;
+    commself)
+      for L in eager graph; do
+        for N in 128 256; do
+          timeout -k 10 300 python bench.py --N $N --no-cpu-baseline --launch $L --comm-self >> "$O/commself.jsonl" 2>> "$O/commself.err" && \
+          timeout -k 10 300 python bench.py --N $N --no-cpu-baseline --launch $L >> "$O/commself.jsonl" 2>> "$O/commself.err" || return 1
+        done
+      done ;;
     csr)
       timeout -k 10 400 python -u tools/csr_general.py > "$O/csr.jsonl" 2> "$O/csr.err" ;;
     *)
