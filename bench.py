@@ -166,6 +166,11 @@ def main():
                     help="timed steps as one hipGraph replay or launched one by one; auto = graph when "
                          "N > 1 (host-bound halo/allreduce calls), eager at N = 1 (measured faster there)")
     args = ap.parse_args()
+    # stdout carries exactly one JSON line: native libraries that write to fd 1 (RCCL prints its
+    # version banner there at communicator creation) are sent to stderr, the line goes to the saved fd
+    sys.stdout.flush()
+    out_fd = os.dup(1)
+    os.dup2(2, 1)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -413,7 +418,7 @@ def main():
                           f"{N}^3 matrix (the reference's numthreads mode, .cc:754-760) ({pdt:.1f} s)",
                 "cap": f"{P} of {usable} visible cores (nproc {os.cpu_count()}): the box allots 16 CPUs per GPU"}
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        os.write(out_fd, (json.dumps(out) + "\n").encode())
     ws.close()
     M.close()
     ctx.close()

@@ -77,7 +77,7 @@ void halo_mv(const eig_mat_s &A, double *X, i64 m, hipStream_t s)
 
 namespace eigmi {
 double *cheb_solve(eig_mat_s &M, i64 m, int degree, double lmin, double lmax, const double *Bv, const double *dinv,
-                   double *Xa, double *Xb, double *Xc, hipStream_t s, const double *zero)
+                   double *Xa, double *Xb, double *Xc, hipStream_t s)
 {
   const i64 n = M.nb_rows, ld = M.window, own = M.own_offset;
   const double gamma = 2.0 / (lmin + lmax), mu = (lmax - lmin) / (lmax + lmin);
@@ -85,16 +85,16 @@ double *cheb_solve(eig_mat_s &M, i64 m, int degree, double lmin, double lmax, co
   if (degree <= 1) return Xa;
   double omega = 1.0;
   const bool oop = Xc && m % 32 == 0 && box_prepare(M);
-  // x_0 = 0: a caller-held zero block stands in for it where the step writes a third buffer
-  if (!(oop && zero)) EIG_HIP(hipMemsetAsync(Xb, 0, (size_t)ld * m * sizeof(double), s));
+  // x_0 = 0: the box kernel (a third output buffer) takes it as "not read"; the in-place kernels
+  // read a cleared buffer
+  if (!oop) EIG_HIP(hipMemsetAsync(Xb, 0, (size_t)ld * m * sizeof(double), s));
   for (int k = 1; k < degree; ++k)
   {
     omega = (k == 1) ? 1.0 / (1.0 - 0.5 * mu * mu) : 1.0 / (1.0 - 0.25 * mu * mu * omega);
     halo_mv(M, Xa, m, s);
     if (oop)
     {
-      double *old = (k == 1 && zero) ? const_cast<double *>(zero) : Xb;  // (only read in this form)
-      launch_box_cheb(M, m, Xa, old, Bv, dinv, omega, gamma, s, Xc);  // Xc = x_{k+1}
+      launch_box_cheb(M, m, Xa, k == 1 ? nullptr : Xb, Bv, dinv, omega, gamma, s, Xc);  // Xc = x_{k+1}
       double *t = Xb;
       Xb = Xa;
       Xa = Xc;

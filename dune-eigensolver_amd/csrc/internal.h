@@ -294,7 +294,7 @@ extern const i32 kMarchInteriorTag;
 // qualifies; false (nothing launched) otherwise.  X, Y: window-layout multivectors, m % 8 == 0.
 bool box_prepare(const eig_mat_s &A);
 bool launch_box_spmm(const eig_mat_s &A, i64 m, const double *X, double *Y, hipStream_t s);
-// Xnew: x_{k+1} into a third buffer (nullptr: in place over Xold)
+// Xnew: x_{k+1} into a third buffer (nullptr: in place over Xold); Xold nullptr (with Xnew): x_{k-1} = 0
 bool launch_box_cheb(const eig_mat_s &M, i64 m, const double *Xk, double *Xold, const double *B, const double *dinv,
                      double omega, double gamma, hipStream_t s, double *Xnew = nullptr);
 void box_invalidate(eig_mat_s &A);
@@ -384,10 +384,8 @@ void launch_panel_gram_2stage(eig_ctx_t ctx, i64 n, i64 ld, i64 m1, i64 m2, cons
                               double *G, hipStream_t s);
 // Chebyshev-Jacobi semi-iteration for M X = Bv (degree steps on the spectrum bounds [lmin, lmax]
 // of diag(M)^-1 M, from X = 0; blanczos.cpp): returns the buffer (Xa, Xb or Xc) holding x_degree.
-// zero (optional): a zero block of the same shape, used as x_0 instead of clearing Xb where the step
-// writes a third buffer (3-D box stencils, m % 32 == 0).
 double *cheb_solve(eig_mat_s &M, i64 m, int degree, double lmin, double lmax, const double *Bv, const double *dinv,
-                   double *Xa, double *Xb, double *Xc, hipStream_t s, const double *zero = nullptr);
+                   double *Xa, double *Xb, double *Xc, hipStream_t s);
 // Geometric multigrid inner solve (mg.cpp): X = S_cycles B on the level-0 matrix's window layout.
 void mg_apply(eig_mg_s &mg, i64 m, const double *B, double *X, int cycles);
 eig_mat_s *mg_matrix(const eig_mg_s &mg);

@@ -182,8 +182,9 @@ __global__ __launch_bounds__(kBoxThreads) void k_box_mv32(BoxGeom g, i64 ld, con
 #pragma unroll
     for (int j = 0; j < 2; ++j) b2[j] = __builtin_nontemporal_load(reinterpret_cast<const dv2b *>(br) + j);
     if (EPI != kBoxCheb) return;
-    const double *yr = Xold + (i64)blk * ld * 8 + r * 8 + c4;
     gg = gamma * __builtin_nontemporal_load(dinv + r);
+    if (!Xold) return;  // x_{k-1} = 0 (the first step from a zero start): not read
+    const double *yr = Xold + (i64)blk * ld * 8 + r * 8 + c4;
 #pragma unroll
     for (int j = 0; j < 2; ++j) x2[j] = __builtin_nontemporal_load(reinterpret_cast<const dv2b *>(yr) + j);
   };
@@ -377,7 +378,7 @@ __global__ __launch_bounds__(kCThreads) void k_boxc_mv8(BoxGeom g, i64 ld, const
     if (EPI == kBoxStore || !own || zz >= z1) return;
     const i64 r = (i64)x + (i64)g.nx * y + (i64)g.P * zz;
     b2 = __builtin_nontemporal_load(Bb + r * 4 + cp);
-    if (EPI == kBoxCheb) x2 = __builtin_nontemporal_load(Ob + r * 4 + cp);
+    if (EPI == kBoxCheb && Ob) x2 = __builtin_nontemporal_load(Ob + r * 4 + cp);  // (null: x_{k-1} = 0)
   };
   fetch(z0 - 1);
   store(z0 - 1);
@@ -668,8 +669,8 @@ static bool launch_box(const eig_mat_s &A, i64 m, const double *X, double *Y, co
     const i64 off = c0 * ld;  // 4 column blocks of ld rows x 8
     if (epi == kBoxCheb)
       hipLaunchKernelGGL(k_box_mv32<kBoxCheb>, dim3((unsigned)(tiles * g.nseg)), dim3(kBoxThreads), 0, s, g, ld,
-                         (const double *)A.box_val, m32, m8, X + off, Y + off, Xold + off, Bv + off, dinv, omega,
-                         gamma);
+                         (const double *)A.box_val, m32, m8, X + off, Y + off, Xold ? Xold + off : nullptr, Bv + off,
+                         dinv, omega, gamma);
     else if (epi == kBoxResid)
       hipLaunchKernelGGL(k_box_mv32<kBoxResid>, dim3((unsigned)(tiles * g.nseg)), dim3(kBoxThreads), 0, s, g, ld,
                          (const double *)A.box_val, m32, m8, X + off, Y + off, (const double *)nullptr, Bv + off,
@@ -696,6 +697,7 @@ bool launch_box_resid(const eig_mat_s &A, i64 m, const double *X, const double *
 bool launch_box_cheb(const eig_mat_s &M, i64 m, const double *Xk, double *Xold, const double *B, const double *dinv,
                      double omega, double gamma, hipStream_t s, double *Xnew)
 {
+  EIG_CHECK(Xold || Xnew, EIG_ERR_ARG, "box Chebyshev step: x_{k-1} = 0 needs a separate output buffer");
   return launch_box(M, m, Xk, Xnew ? Xnew : Xold, Xold, B, dinv, omega, gamma, kBoxCheb, s);
 }
 

@@ -44,7 +44,7 @@ struct MgLevel {
   double lmax = 2.0;                          // Gershgorin bound of D^-1 A
   double clo = 0.0, chi = 0.0;                // coarsest: exact spectrum bounds of D^-1 A
   int cdeg = 0;                               // coarsest: Chebyshev degree
-  DevBuf *dinv = nullptr, *B = nullptr, *T = nullptr, *Z = nullptr, *C[4] = {nullptr, nullptr, nullptr, nullptr};
+  DevBuf *dinv = nullptr, *B = nullptr, *T = nullptr, *C[4] = {nullptr, nullptr, nullptr, nullptr};
 };
 
 struct eig_mg_s {
@@ -56,7 +56,7 @@ struct eig_mg_s {
   {
     for (auto &L : lev)
     {
-      for (DevBuf *b : {L.dinv, L.B, L.T, L.Z, L.C[0], L.C[1], L.C[2], L.C[3]}) delete b;
+      for (DevBuf *b : {L.dinv, L.B, L.T, L.C[0], L.C[1], L.C[2], L.C[3]}) delete b;
       if (L.own && L.A) eig_mat_destroy(L.A);
     }
   }
@@ -229,14 +229,13 @@ void alloc_level(MgLevel &L, int m, hipStream_t s)
   L.dinv = new DevBuf((size_t)std::max<i64>(L.n, 1) * sizeof(double));
   L.B = new DevBuf(bytes);
   L.T = new DevBuf(bytes);
-  L.Z = new DevBuf(bytes);  // a zero block: x_0 of the Chebyshev smoothers (cheb_solve)
-  EIG_HIP(hipMemsetAsync(L.Z->d(), 0, bytes, s));
   for (auto &c : L.C) c = new DevBuf(bytes);
+  (void)s;
 }
 
 // V_l b: the V-cycle on level l (all buffers n_l x m, ld = n_l); returns the level buffer (one of
 // C[0..3]) that holds the result.  Residuals come from the SpMM's residual epilogue (T = b - A x in
-// one pass), the smoothers start from the level's zero block, and the smoothed iterate stays where
+// one pass), the smoothers' zero start is not read (box kernels), and the smoothed iterate stays where
 // cheb_solve left it (the post-smoother takes the three other C buffers).
 double *vcycle(eig_mg_s &mg, size_t l, i64 m, const double *b)
 {
@@ -244,10 +243,10 @@ double *vcycle(eig_mg_s &mg, size_t l, i64 m, const double *b)
   hipStream_t s = mg.ctx->stream;
   double *C[4] = {L.C[0]->d(), L.C[1]->d(), L.C[2]->d(), L.C[3]->d()};
   if (l + 1 == mg.lev.size())
-    return cheb_solve(*L.A, m, L.cdeg, L.clo, L.chi, b, L.dinv->d(), C[0], C[1], C[2], s, L.Z->d());
+    return cheb_solve(*L.A, m, L.cdeg, L.clo, L.chi, b, L.dinv->d(), C[0], C[1], C[2], s);
   MgLevel &Cl = mg.lev[l + 1];
   const double lo = L.lmax / mg.ratio, hi = L.lmax;
-  double *x = cheb_solve(*L.A, m, mg.nu, lo, hi, b, L.dinv->d(), C[0], C[1], C[2], s, L.Z->d());
+  double *x = cheb_solve(*L.A, m, mg.nu, lo, hi, b, L.dinv->d(), C[0], C[1], C[2], s);
   double *T = L.T->d();
   launch_resid_mv8(*L.A, m, x, b, T, s);  // T = b - A x
   launch_mg_restrict(L.dim, Cl.dim, m, L.n, Cl.n, T, Cl.B->d(), s);
@@ -257,7 +256,7 @@ double *vcycle(eig_mg_s &mg, size_t l, i64 m, const double *b)
   double *q[3];
   for (int i = 0, j = 0; i < 4; ++i)
     if (C[i] != x) q[j++] = C[i];
-  const double *p = cheb_solve(*L.A, m, mg.nu, lo, hi, T, L.dinv->d(), q[0], q[1], q[2], s, L.Z->d());
+  const double *p = cheb_solve(*L.A, m, mg.nu, lo, hi, T, L.dinv->d(), q[0], q[1], q[2], s);
   launch_mv8_axpby(L.n, m, L.n, 1.0, p, 1.0, x, s);  // x += post-smoothing correction
   return x;
 }
