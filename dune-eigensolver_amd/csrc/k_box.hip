@@ -323,8 +323,33 @@ __global__ void k_boxc_gather(i64 n, int nd, const double *__restrict__ val, con
                                                            : static_cast<const uint32_t *>(mask)[r]);
 }
 
-template <int EPI>
-__global__ __launch_bounds__(kCThreads) void k_boxc_mv8(BoxGeom g, i64 ld, const double *__restrict__ ctab,
+// Compile-time box stencils: SHAPE has bit (dz + 1) 9 + (dy + 1) 3 + (dx + 1) for every stored offset;
+// the k-th set bit in that (lexicographic = ascending offset) order is the image's offset k.
+constexpr unsigned kShape7 = (1u << 4) | (1u << 10) | (1u << 12) | (1u << 13) | (1u << 14) | (1u << 16) | (1u << 22);
+// P1 on the Kuhn split: all offsets whose nonzero components share one sign
+constexpr unsigned kShapeKuhn = (1u << 0) | (1u << 1) | (1u << 3) | (1u << 4) | (1u << 9) | (1u << 10) | (1u << 12) |
+                                (1u << 13) | (1u << 14) | (1u << 16) | (1u << 17) | (1u << 22) | (1u << 23) |
+                                (1u << 25) | (1u << 26);
+struct BoxShapeTab {
+  int nd;
+  int dz[27], dy[27], dx[27];
+};
+constexpr BoxShapeTab box_shape_tab(unsigned shape)
+{
+  BoxShapeTab t{};
+  for (int b = 0; b < 27; ++b)
+    if ((shape >> b) & 1u)
+    {
+      t.dz[t.nd] = b / 9 - 1;
+      t.dy[t.nd] = (b / 3) % 3 - 1;
+      t.dx[t.nd] = b % 3 - 1;
+      ++t.nd;
+    }
+  return t;
+}
+
+template <int EPI, unsigned SHAPE>
+__global__ __launch_bounds__(kCThreads, 8) void k_boxc_mv8(BoxGeom g, i64 ld, const double *__restrict__ ctab,
                                                         const unsigned *__restrict__ cmask,
                                                         const double *__restrict__ X, double *__restrict__ Y,
                                                         const double *__restrict__ Xold,
@@ -394,23 +419,62 @@ __global__ __launch_bounds__(kCThreads) void k_boxc_mv8(BoxGeom g, i64 ld, const
     fetch(z + 2);
     const int cls = (z == 0 ? 0 : (z == g.nz - 1 ? 2 : 1)) * 9 + cxy;
     const unsigned m = own ? cm[cls] : 0u;
+    // ring slots of planes z - 1, z, z + 1 (scalar)
+    const int s0 = z % 3, sm = s0 == 0 ? 2 : s0 - 1, sp = s0 == 2 ? 0 : s0 + 1;
     dv2b acc = {0.0, 0.0};
-#pragma unroll 4
-    for (int k = 0; k < g.nd; ++k)
-    {
-      if (!((m >> k) & 1u)) continue;
-      const double a = ct[cls][k];
-      const int sl = (((z + g.dz[k]) % 3) + 3) % 3;
-      const dv2b xv = ring[sl][hrow + g.dxy[k]][cp];
+    // stored entry k: a * x, summed in ascending offset order; an offset the row does not store is
+    // dropped by a select (the class entry is 0 there, but 0 * inf would not be)
+    auto add = [&](bool on, double a, dv2b xv) {
       if (EPI == kBoxStore)
       {
-        acc.x = acc.x + a * xv.x;
-        acc.y = acc.y + a * xv.y;
+        const double s0v = acc.x + a * xv.x, s1v = acc.y + a * xv.y;
+        acc.x = on ? s0v : acc.x;
+        acc.y = on ? s1v : acc.y;
       }
       else
       {
-        acc.x = __builtin_fma(a, xv.x, acc.x);
-        acc.y = __builtin_fma(a, xv.y, acc.y);
+        const double f0 = __builtin_fma(a, xv.x, acc.x), f1 = __builtin_fma(a, xv.y, acc.y);
+        acc.x = on ? f0 : acc.x;
+        acc.y = on ? f1 : acc.y;
+      }
+    };
+    if constexpr (SHAPE != 0)
+    {
+      // compile-time stencil on a geometric mask (box_geomask): every offset of the shape is summed,
+      // in ascending order; one the row does not store has a zero class entry and points at a zero
+      // halo row, and +0 added to a sum that starts at +0 changes nothing -- the same sums as with
+      // the mask.  LDS offsets are immediates off three per-plane slot bases.
+      constexpr BoxShapeTab T = box_shape_tab(SHAPE);
+      constexpr int kGroup = EPI == kBoxCheb ? 2 : 4;  // (the Chebyshev step holds 4 more vectors)
+      // ring index (dv2b units) of the (-1, -1) neighbour in the three slots, made opaque to the
+      // compiler: otherwise it hoists base + offset for every offset out of the plane loop (one
+      // live VGPR per offset and slot, ~110 VGPRs: one workgroup per CU instead of two)
+      constexpr int kSlot = kCHY * kCHX * 4;
+      const dv2b *r0 = &ring[0][0][0];
+      int pz[3];
+      pz[0] = sm * kSlot + (hrow - kCHX - 1) * 4 + cp;
+      pz[1] = s0 * kSlot + (hrow - kCHX - 1) * 4 + cp;
+      pz[2] = sp * kSlot + (hrow - kCHX - 1) * 4 + cp;
+      asm volatile("" : "+v"(pz[0]), "+v"(pz[1]), "+v"(pz[2]));
+      const double *crow = &ct[cls][0];
+#pragma unroll
+      for (int k = 0; k < T.nd; ++k)
+      {
+        add(true, crow[k], r0[pz[T.dz[k] + 1] + ((T.dy[k] + 1) * kCHX + T.dx[k] + 1) * 4]);
+        // the next group's LDS reads wait for this group's sums (kGroup reads in flight; without it
+        // the scheduler issues all of them at once and needs ~77 VGPRs: one workgroup per CU)
+        if ((k + 1) % kGroup == 0 && k + 1 < T.nd)
+          asm volatile("" : "+v"(pz[0]), "+v"(pz[1]), "+v"(pz[2]) : "v"(acc.x), "v"(acc.y));
+      }
+    }
+    else
+    {
+#pragma unroll 4
+      for (int k = 0; k < g.nd; ++k)
+      {
+        if (!((m >> k) & 1u)) continue;
+        const int sl = g.dz[k] < 0 ? sm : (g.dz[k] > 0 ? sp : s0);
+        add(true, ct[cls][k], ring[sl][hrow + g.dxy[k]][cp]);
       }
     }
     if (own)
@@ -422,7 +486,7 @@ __global__ __launch_bounds__(kCThreads) void k_boxc_mv8(BoxGeom g, i64 ld, const
         __builtin_nontemporal_store(dv2b{bb.x - acc.x, bb.y - acc.y}, Yb + r * 4 + cp);
       else
       {
-        const dv2b xc = ring[((z % 3) + 3) % 3][hrow][cp];
+        const dv2b xc = ring[s0][hrow][cp];
         const double gd = gamma * ct[cls][kCStride - 1];
         const double o0 = omega * (xc.x + gd * (bb.x - acc.x) - xo.x) + xo.x;
         const double o1 = omega * (xc.y + gd * (bb.y - acc.y) - xo.y) + xo.y;
@@ -454,13 +518,15 @@ void box_invalidate(eig_mat_s &A)
   }
   A.box_ctab = nullptr;
   A.box_cmask = nullptr;
+  A.box_geomask = false;
   A.box_state = 0;
 }
 
 // Row classes of a box image (k_boxc_mv8): the 27 representatives' entries and masks to the host,
 // 1 / a_rr per class, then every row checked bitwise against its class on the device; on success
 // A.box_ctab / box_cmask are set.  Needs a stored diagonal in every class.
-static void box_classes(eig_mat_s &A, i64 nx, i64 ny, i64 nz)
+static void box_classes(eig_mat_s &A, i64 nx, i64 ny, i64 nz, const std::vector<i32> &dx, const std::vector<i32> &dy,
+                        const std::vector<i32> &dz)
 {
   if (nx < 3 || ny < 3 || nz < 3 || A.sym_nd >= kCStride || (A.kflags & EIG_MAT_NO_CLASS)) return;
   int k0 = -1;
@@ -513,6 +579,15 @@ static void box_classes(eig_mat_s &A, i64 nx, i64 ny, i64 nz)
   }
   A.box_ctab = dct;
   A.box_cmask = dcm;
+  // class position along an axis: 0 first, 1 interior, 2 last; offset d leaves the grid from the
+  // first position when d < 0, from the last when d > 0
+  auto leaves = [](int pos, int d) { return (pos == 0 && d < 0) || (pos == 2 && d > 0); };
+  bool geo = true;
+  for (int c = 0; c < kBoxClasses; ++c)
+    for (int k = 0; k < A.sym_nd; ++k)
+      if (!((cmask[c] >> k) & 1u) && !(leaves(c % 3, dx[k]) || leaves((c / 3) % 3, dy[k]) || leaves(c / 9, dz[k])))
+        geo = false;
+  A.box_geomask = geo;
 }
 
 // Box-stencil geometry of a band image and its device box image (built on first use and cached on
@@ -580,7 +655,7 @@ bool box_prepare(const eig_mat_s &Ac)
     EIG_HIP(hipStreamSynchronize(s));
     A.box_val = val;
   }
-  box_classes(A, nx, ny, nz);
+  box_classes(A, nx, ny, nz, dx, dy, dz);
   A.box_nx = (int)nx;
   A.box_ny = (int)ny;
   A.box_nz = (int)nz;
@@ -630,17 +705,32 @@ static bool launch_box(const eig_mat_s &A, i64 m, const double *X, double *Y, co
       g.dxy[k] = k < A.sym_nd ? A.box_dy[k] * kCHX + A.box_dx[k] : 0;
     }
     const dim3 grid((unsigned)(g.ntx * g.nty * g.nseg), (unsigned)(m / 8));
-    if (epi == kBoxCheb)
-      hipLaunchKernelGGL(k_boxc_mv8<kBoxCheb>, grid, dim3(kCThreads), 0, s, g, A.window,
-                         (const double *)A.box_ctab, (const unsigned *)A.box_cmask, X, Y, Xold, Bv, omega, gamma);
-    else if (epi == kBoxResid)
-      hipLaunchKernelGGL(k_boxc_mv8<kBoxResid>, grid, dim3(kCThreads), 0, s, g, A.window,
-                         (const double *)A.box_ctab, (const unsigned *)A.box_cmask, X, Y, (const double *)nullptr, Bv,
-                         0.0, 0.0);
+    // the stencil's shape: compile-time kernels for the 7-point and the Kuhn 15-point stencils,
+    // a runtime offset loop for any other
+    unsigned shape = 0;
+    for (int k = 0; k < A.sym_nd; ++k)
+      shape |= 1u << ((A.box_dz[k] + 1) * 9 + (A.box_dy[k] + 1) * 3 + (A.box_dx[k] + 1));
+    auto go = [&](auto shape_tag) {
+      constexpr unsigned S = decltype(shape_tag)::value;
+      const double *ct = (const double *)A.box_ctab;
+      const unsigned *cm = (const unsigned *)A.box_cmask;
+      if (epi == kBoxCheb)
+        hipLaunchKernelGGL((k_boxc_mv8<kBoxCheb, S>), grid, dim3(kCThreads), 0, s, g, A.window, ct, cm, X, Y, Xold,
+                           Bv, omega, gamma);
+      else if (epi == kBoxResid)
+        hipLaunchKernelGGL((k_boxc_mv8<kBoxResid, S>), grid, dim3(kCThreads), 0, s, g, A.window, ct, cm, X, Y,
+                           (const double *)nullptr, Bv, 0.0, 0.0);
+      else
+        hipLaunchKernelGGL((k_boxc_mv8<kBoxStore, S>), grid, dim3(kCThreads), 0, s, g, A.window, ct, cm, X, Y,
+                           (const double *)nullptr, (const double *)nullptr, 0.0, 0.0);
+    };
+    // (the image's offsets ascend, i.e. run in the shape's bit order: box_prepare builds them so)
+    if (A.box_geomask && shape == kShape7 && A.sym_nd == 7)
+      go(std::integral_constant<unsigned, kShape7>{});
+    else if (A.box_geomask && shape == kShapeKuhn && A.sym_nd == 15)
+      go(std::integral_constant<unsigned, kShapeKuhn>{});
     else
-      hipLaunchKernelGGL(k_boxc_mv8<kBoxStore>, grid, dim3(kCThreads), 0, s, g, A.window,
-                         (const double *)A.box_ctab, (const unsigned *)A.box_cmask, X, Y, (const double *)nullptr,
-                         (const double *)nullptr, 0.0, 0.0);
+      go(std::integral_constant<unsigned, 0u>{});
     EIG_HIP(hipGetLastError());
     return true;
   }

@@ -345,3 +345,77 @@ def test_box_not_a_grid(ctx):
     Q, Y = ctx.array(Qh), ctx.zeros(A.n * 32)
     eigmi.spmm_mv8(M, 32, Q, Y)
     assert np.array_equal(Y.get(), oracle.spmm_mv8(A, Qh, 32))
+
+
+def _box_stencil(N, stencil, drop_xfirst_z=False):
+    """Symmetric constant-coefficient box stencil on an N^3 grid, Dirichlet truncation: stencil maps
+    (dz, dy, dx) -> value (with (-dz, -dy, -dx) the same value).  drop_xfirst_z: rows on the x = 0
+    face do not couple along z (an in-grid offset their class does not store)."""
+    import scipy.sparse as sp
+    n = N ** 3
+    r = np.arange(n)
+    x, y, z = r % N, (r // N) % N, r // (N * N)
+    rows, cols, vals = [], [], []
+    for (dz, dy, dx), v in stencil.items():
+        ok = (x + dx >= 0) & (x + dx < N) & (y + dy >= 0) & (y + dy < N) & (z + dz >= 0) & (z + dz < N)
+        if drop_xfirst_z and dz != 0:
+            ok &= x != 0
+        rows.append(r[ok])
+        cols.append(r[ok] + dz * N * N + dy * N + dx)
+        vals.append(np.full(int(ok.sum()), v))
+    S = sp.csr_matrix((np.concatenate(vals), (np.concatenate(rows), np.concatenate(cols))), shape=(n, n))
+    S.sort_indices()
+    return oracle.CSR(n, S.indptr.astype(np.int64), S.indices.astype(np.int32), S.data.copy())
+
+
+_P7 = {(0, 0, 0): 6.0, (1, 0, 0): -1.0, (-1, 0, 0): -1.0, (0, 1, 0): -1.0, (0, -1, 0): -1.0,
+       (0, 0, 1): -1.0, (0, 0, -1): -1.0}
+
+
+@pytest.mark.parametrize("kind", ["hole", "nine"])
+def test_boxc_runtime_offsets(ctx, kind):
+    """The row-class kernels take the compile-time stencil (7-point, Kuhn 15-point: no masks, every
+    offset summed with the zero class entries) only when every offset a class does not store points
+    out of the grid; otherwise -- hole: x = 0 rows drop their in-grid z couplings -- and for other
+    shapes -- nine: the 7-point plus one face diagonal -- the runtime offset loop with the row masks.
+    All bitwise the reference SpMM; the Chebyshev step equal to the SELL kernel to rounding."""
+    st = dict(_P7)
+    if kind == "nine":
+        st[(0, 1, 1)] = st[(0, -1, -1)] = -0.25
+        st[(0, 0, 0)] = 6.5
+    A = _box_stencil(17, st, drop_xfirst_z=(kind == "hole"))
+    M = upload(ctx, A)
+    assert M.kernel("spmm32") == "k_boxc_mv8"
+    for m in (8, 32):
+        Qh = oracle.random_mv8(A.n, m, 23)
+        Q, Y = ctx.array(Qh), ctx.zeros(A.n * m)
+        eigmi.spmm_mv8(M, m, Q, Y)
+        assert np.array_equal(Y.get(), oracle.spmm_mv8(A, Qh, m))
+    Ms = upload(ctx, A, flags=eigmi.MAT_NO_MARCH)
+    Bh = oracle.random_mv8(A.n, 32, 29)
+    B = ctx.array(Bh)
+    X1, X2 = ctx.zeros(A.n * 32), ctx.zeros(A.n * 32)
+    lo, hi = 0.1, 2.0  # (the two kernels run the same recurrence; convergence is not the point)
+    eigmi.mass_solve_mv8(M, 32, 12, B, X1, lo, hi)
+    eigmi.mass_solve_mv8(Ms, 32, 12, B, X2, lo, hi)
+    a, b = X1.get(), X2.get()
+    assert np.allclose(a, b, rtol=1e-13, atol=1e-14 * np.abs(b).max()), np.abs(a - b).max()
+
+
+def test_boxc_compile_time_stencils(ctx):
+    """The 7-point and Kuhn 15-point stencils with zero (not absent) boundary entries: the
+    compile-time kernels sum the shape's offsets with zero class entries -- bitwise the reference,
+    which skips absent entries (a sum starting at +0 is unchanged by adding +-0) -- also when X holds
+    exact zeros and negative values next to the faces."""
+    for A in (oracle.poisson3d(16), _p1(16, "K")):
+        M = upload(ctx, A)
+        assert M.kernel("spmm32") == "k_boxc_mv8"
+        Qh = oracle.random_mv8(A.n, 32, 31)
+        Qh[::7] = 0.0
+        Qh[1::11] = -0.0
+        Q, Y = ctx.array(Qh), ctx.zeros(A.n * 32)
+        eigmi.spmm_mv8(M, 32, Q, Y)
+        ref = oracle.spmm_mv8(A, Qh, 32)
+        got = Y.get()
+        assert np.array_equal(got, ref)
+        assert np.array_equal(np.signbit(got), np.signbit(ref))

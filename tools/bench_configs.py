@@ -334,6 +334,43 @@ def c5(ctx):
     bl.close()
 
 
+def boxk(ctx):
+    """Row-class box kernels alone at 256^3, m = 32 (the C5 / multigrid fine-level launches): the
+    SpMM Y = K X (k_boxc_mv8<kBoxStore>, 2 vector streams = 16 m n bytes) and the mass solve's
+    Chebyshev step (kBoxCheb, 4 streams = 32 m n bytes) from the difference of two solve degrees."""
+    N = int(os.environ.get("EIGMI_C5_N", "256"))
+    b, n, reps = 32, N ** 3, 20
+    rk, ck, vk = eigmi.gen_matrix(eigmi.GEN_P1STIFF3D, N)
+    K = eigmi.Matrix.from_bcsr(ctx, rk, ck, vk)
+    del rk, ck, vk
+    rm, cm, vm = eigmi.gen_matrix(eigmi.GEN_P1MASS3D, N)
+    M = eigmi.Matrix.from_bcsr(ctx, rm, cm, vm)
+    del rm, cm, vm
+    X, Y = ctx.zeros(n * b), ctx.zeros(n * b)
+    ctx.check(eigmi.lib.eig_fill_normal(ctx.h, n * b, 5, X.ptr))
+    eigmi.spmm_mv8(K, b, X, Y)
+    ctx.sync()
+
+    def spmm():
+        for _ in range(reps):
+            eigmi.spmm_mv8(K, b, X, Y)
+        ctx.sync()
+    ts, _ = wall(spmm)
+    ts /= reps
+    emit(config=f"P1 K {N}^3 m={b}", op="SpMM (row-class kBoxStore)", kernel=K.kernel("spmm32"), us=round(ts * 1e6, 1),
+         bytes=16 * b * n, frac=round(16 * b * n / ts / 1e9 / PEAK, 4))
+    d0, d1 = 2, 22
+    eigmi.mass_solve_mv8(M, b, d0, X, Y)
+    ctx.sync()
+    t0, _ = wall(lambda: (eigmi.mass_solve_mv8(M, b, d0, X, Y), ctx.sync()), 5)
+    t1, _ = wall(lambda: (eigmi.mass_solve_mv8(M, b, d1, X, Y), ctx.sync()), 5)
+    tc = (t1 - t0) / (d1 - d0)
+    emit(config=f"P1 M {N}^3 m={b}", op="Chebyshev step (row-class kBoxCheb)", kernel=M.kernel("cheb32"),
+         us=round(tc * 1e6, 1), bytes=32 * b * n, frac=round(32 * b * n / tc / 1e9 / PEAK, 4))
+    X.free(), Y.free()
+    K.close(), M.close()
+
+
 def c5si(ctx):
     """C5 at the end GeneralizedInverse returns (eigensolver.hh:204-351): the smallest eigenvalues
     of the P1 pencil by block Lanczos on K^-1 M (sigma = 0) with the K solve by multigrid

@@ -11,9 +11,9 @@ for line in open(os.path.join(O, "variants.txt")):
     i, v = line.split(maxsplit=1)
     t = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
          for f in glob.glob(f"{O}/t{i}/**/*kernel_trace.csv", recursive=True) for r in csv.DictReader(open(f))
-         if ("k_box_mv32<1>" in r["Kernel_Name"] or "k_boxc_mv8<1>" in r["Kernel_Name"])]
+         if ("k_box_mv32<1>" in r["Kernel_Name"] or "k_boxc_mv8<1," in r["Kernel_Name"])]
     w = [float(r["Counter_Value"]) for f in glob.glob(f"{O}/w{i}/**/*counter_collection.csv", recursive=True)
-         for r in csv.DictReader(open(f)) if ("k_box_mv32<1>" in r["Kernel_Name"] or "k_boxc_mv8<1>" in r["Kernel_Name"])]
+         for r in csv.DictReader(open(f)) if ("k_box_mv32<1>" in r["Kernel_Name"] or "k_boxc_mv8<1," in r["Kernel_Name"])]
     t.sort()
     print(v.strip(), "launch_ms", round(t[len(t) // 2] / 1e6, 3) if t else None,
           "write_GB", round(sum(w) / len(w) * 1024 / 1e9, 3) if w else None)

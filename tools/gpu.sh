@@ -13,6 +13,7 @@
 #   configs              tools/bench_configs.py c1 c2 c3, c5 (256^3), inv (64^2, 200^2)  -> cfg_*.jsonl
 #   gram                 a6 / a9 / panel-Gram timings under a kernel trace    -> gram.jsonl, gram_trace/
 #   grampmc              FETCH_SIZE / WRITE_SIZE passes over the gram timings -> grampmc/{fetch,write}
+#   boxk                 row-class box kernels alone (SpMM, Chebyshev step) at 256^3 under a kernel trace -> boxk.jsonl, boxk_trace/
 #   c5 | c5si            block Lanczos 256^3: largest end / smallest end (multigrid solve)  -> c5*.jsonl
 #   latency              fused step vs eig_mv across sizes and slabs, plane-run counts  -> latency.jsonl
 #   pipe                 fused vs pipelined on one rank's slab and the cube   -> pipe.jsonl
@@ -57,6 +58,10 @@ run_task() {
         python3 tools/bench_configs.py gram > /dev/null 2> "$O/grampmc_f.err" && \
       timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/grampmc/write" -o pmc -- \
         python3 tools/bench_configs.py gram > /dev/null 2> "$O/grampmc_w.err" ;;
+    boxk)
+      prof_env
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/boxk_trace" -o trace -- \
+        python3 tools/bench_configs.py boxk > "$O/boxk.jsonl" 2> "$O/boxk.err" ;;
     c5)
       EIGMI_C5_N=256 timeout -k 10 300 python -u tools/bench_configs.py c5 > "$O/c5.jsonl" 2> "$O/c5.err" ;;
     c5si)
