@@ -221,8 +221,8 @@ struct eig_mat_s {
   // class kernels read no matrix stream at all (box_val is then freed)
   double *box_ctab = nullptr;
   unsigned *box_cmask = nullptr;
-  // every offset a class does not store points out of the grid (its halo row is 0): the kernels
-  // with a compile-time stencil then sum all offsets with the zero class entries, no masks
+  // every offset a row does not store points out of the grid (its halo row is 0): the kernels with
+  // a compile-time stencil then sum all offsets with the zero image / class entries, no masks
   bool box_geomask = false;
   eigmi::i32 *march_bnd = nullptr;
   eigmi::i64 n_march_bnd = 0;

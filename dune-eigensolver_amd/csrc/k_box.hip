@@ -44,6 +44,31 @@ struct BoxGeom {
   int dz[27], dxy[27];
 };
 
+// Compile-time box stencils: SHAPE has bit (dz + 1) 9 + (dy + 1) 3 + (dx + 1) for every stored offset;
+// the k-th set bit in that (lexicographic = ascending offset) order is the image's offset k.
+constexpr unsigned kShape7 = (1u << 4) | (1u << 10) | (1u << 12) | (1u << 13) | (1u << 14) | (1u << 16) | (1u << 22);
+// P1 on the Kuhn split: all offsets whose nonzero components share one sign
+constexpr unsigned kShapeKuhn = (1u << 0) | (1u << 1) | (1u << 3) | (1u << 4) | (1u << 9) | (1u << 10) | (1u << 12) |
+                                (1u << 13) | (1u << 14) | (1u << 16) | (1u << 17) | (1u << 22) | (1u << 23) |
+                                (1u << 25) | (1u << 26);
+struct BoxShapeTab {
+  int nd;
+  int dz[27], dy[27], dx[27];
+};
+constexpr BoxShapeTab box_shape_tab(unsigned shape)
+{
+  BoxShapeTab t{};
+  for (int b = 0; b < 27; ++b)
+    if ((shape >> b) & 1u)
+    {
+      t.dz[t.nd] = b / 9 - 1;
+      t.dy[t.nd] = (b / 3) % 3 - 1;
+      t.dx[t.nd] = b % 3 - 1;
+      ++t.nd;
+    }
+  return t;
+}
+
 // Box image of the band: val[k * n + r] = a(r, r + off[k]) (0 where row r does not store it).
 __global__ void k_box_image(i64 n, i64 ld, int nd, const i32 *__restrict__ off, const i32 *__restrict__ dj,
                             const double *__restrict__ sym, const void *__restrict__ mask, int mask_bytes,
@@ -65,25 +90,32 @@ __global__ void k_box_image(i64 n, i64 ld, int nd, const i32 *__restrict__ off, 
   }
 }
 
-// Geometry check: every stored entry of row r stays inside the grid (no x / y / z wrap-around).
+// Geometry check: every stored entry of row r stays inside the grid (no x / y / z wrap-around),
+// else bad |= 1; a row that does not store an offset staying inside the grid sets bad |= 2 (the
+// masks are then not the geometric ones: box_geomask stays false).
 __global__ void k_box_check(i64 n, int nx, int ny, int nz, int nd, const i32 *__restrict__ dx,
                             const i32 *__restrict__ dy, const i32 *__restrict__ dzz, const void *__restrict__ mask,
                             int mask_bytes, unsigned *__restrict__ bad)
 {
+  unsigned b = 0u;
   for (i64 r = (i64)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (i64)gridDim.x * blockDim.x)
   {
     const unsigned m = mask_bytes == 1 ? static_cast<const uint8_t *>(mask)[r] : static_cast<const uint32_t *>(mask)[r];
     const int x = (int)(r % nx), y = (int)((r / nx) % ny), z = (int)(r / ((i64)nx * ny));
     for (int k = 0; k < nd; ++k)
+    {
+      const int X = x + dx[k], Y = y + dy[k], Z = z + dzz[k];
+      const bool inside = X >= 0 && X < nx && Y >= 0 && Y < ny && Z >= 0 && Z < nz;
       if ((m >> k) & 1u)
-      {
-        const int X = x + dx[k], Y = y + dy[k], Z = z + dzz[k];
-        if (X < 0 || X >= nx || Y < 0 || Y >= ny || Z < 0 || Z >= nz) atomicOr(bad, 1u);
-      }
+        b |= inside ? 0u : 1u;
+      else
+        b |= inside ? 2u : 0u;
+    }
   }
+  if (b) atomicOr(bad, b);
 }
 
-template <int EPI>
+template <int EPI, unsigned SHAPE>
 __global__ __launch_bounds__(kBoxThreads) void k_box_mv32(BoxGeom g, i64 ld, const double *__restrict__ val,
                                                           const uint32_t *__restrict__ mask32,
                                                           const uint8_t *__restrict__ mask8,
@@ -157,7 +189,7 @@ __global__ __launch_bounds__(kBoxThreads) void k_box_mv32(BoxGeom g, i64 ld, con
       const int k = sk0 + j * (kBoxThreads / kRows);
       vpre[j] = (r >= 0 && k < g.nd) ? __builtin_nontemporal_load(val + (i64)k * n + r) : 0.0;
     }
-    if (sk0 == 0) mpre = r >= 0 ? (mask32 ? mask32[r] : (unsigned)mask8[r]) : 0u;
+    if (SHAPE == 0 && sk0 == 0) mpre = r >= 0 ? (mask32 ? mask32[r] : (unsigned)mask8[r]) : 0u;
   };
   auto store_vals = [&]() {
 #pragma unroll
@@ -205,26 +237,63 @@ __global__ __launch_bounds__(kBoxThreads) void k_box_mv32(BoxGeom g, i64 ld, con
     fetch_vals(z + 1);
     fetch_cheb(z + 1, bn, xn, gn);
     fetch(z + 2);
-    const unsigned m = own ? mtile[trow] : 0u;
     double acc[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[j] = 0.0;
-    // (partially unrolled: a full unroll hoists all 15 offsets' LDS reads and spills)
-#pragma unroll 4
-    for (int k = 0; k < g.nd; ++k)
-    {
-      if (!((m >> k) & 1u)) continue;
-      const double a = atile[k][trow];
-      const int sl = (((z + g.dz[k]) % 3) + 3) % 3, hr = hrow + g.dxy[k];
-      // two 16-B LDS reads (ds_read_b128)
-      const dv2b p0 = *reinterpret_cast<const dv2b *>(&ring[sl][hr][swz(hr, blk * 8 + c4)]);
-      const dv2b p1 = *reinterpret_cast<const dv2b *>(&ring[sl][hr][swz(hr, blk * 8 + c4 + 2)]);
+    auto add = [&](double a, dv2b p0, dv2b p1) {
       const double xr[4] = {p0.x, p0.y, p1.x, p1.y};
 #pragma unroll
       for (int j = 0; j < 4; ++j)
       {
         if (EPI == kBoxStore) acc[j] = acc[j] + a * xr[j];
         else acc[j] = __builtin_fma(a, xr[j], acc[j]);
+      }
+    };
+    const int s0 = z % 3, sm = s0 == 0 ? 2 : s0 - 1, sp = s0 == 2 ? 0 : s0 + 1;
+    if constexpr (SHAPE != 0)
+    {
+      // compile-time stencil on geometric masks (box_geomask; as k_boxc_mv8): all offsets summed, an
+      // unstored one with its zero image entry against a zero halo row -- the masked sums bitwise.
+      // The swizzle of a row depends on its parity only, i.e. on the offset's dx, dy (compile time).
+      constexpr BoxShapeTab T = box_shape_tab(SHAPE);
+      constexpr int kGroup = 2;
+      const int hb0 = hrow - kBoxHX - 1;  // (-1, -1) neighbour in the halo tile
+      const double *rg = &ring[0][0][0];
+      int pz[3];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) pz[q] = (q == 0 ? sm : q == 1 ? s0 : sp) * (kBoxHY * kBoxHX * 32) + hb0 * 32;
+      const int par = hb0 & 1;  // parity of the (-1, -1) neighbour's halo row
+      const int cA = blk * 8 + c4;
+      // column offsets of the two 16-B reads for a row of the (-1, -1) neighbour's parity and the other
+      const int e0 = swz(par, cA), e1 = swz(par, cA + 2), o0 = swz(par ^ 1, cA), o1 = swz(par ^ 1, cA + 2);
+      asm volatile("" : "+v"(pz[0]), "+v"(pz[1]), "+v"(pz[2]));
+#pragma unroll
+      for (int k = 0; k < T.nd; ++k)
+      {
+        const int dr = (T.dy[k] + 1) * kBoxHX + T.dx[k] + 1;  // halo-row shift from (-1, -1)
+        const int base = pz[T.dz[k] + 1] + dr * 32;
+        const bool odd = dr & 1;
+        const dv2b p0 = *reinterpret_cast<const dv2b *>(rg + base + (odd ? o0 : e0));
+        const dv2b p1 = *reinterpret_cast<const dv2b *>(rg + base + (odd ? o1 : e1));
+        add(atile[k][trow], p0, p1);
+        // (the next group's reads wait for these sums: a bounded number of LDS reads in flight)
+        if ((k + 1) % kGroup == 0 && k + 1 < T.nd)
+          asm volatile("" : "+v"(pz[0]), "+v"(pz[1]), "+v"(pz[2]) : "v"(acc[0]), "v"(acc[1]), "v"(acc[2]), "v"(acc[3]));
+      }
+    }
+    else
+    {
+      const unsigned m = own ? mtile[trow] : 0u;
+      // (partially unrolled: a full unroll hoists all 15 offsets' LDS reads and spills)
+#pragma unroll 4
+      for (int k = 0; k < g.nd; ++k)
+      {
+        if (!((m >> k) & 1u)) continue;
+        const double a = atile[k][trow];
+        const int sl = g.dz[k] < 0 ? sm : (g.dz[k] > 0 ? sp : s0), hr = hrow + g.dxy[k];
+        // two 16-B LDS reads (ds_read_b128)
+        add(a, *reinterpret_cast<const dv2b *>(&ring[sl][hr][swz(hr, blk * 8 + c4)]),
+            *reinterpret_cast<const dv2b *>(&ring[sl][hr][swz(hr, blk * 8 + c4 + 2)]));
       }
     }
     if (own)
@@ -323,30 +392,6 @@ __global__ void k_boxc_gather(i64 n, int nd, const double *__restrict__ val, con
                                                            : static_cast<const uint32_t *>(mask)[r]);
 }
 
-// Compile-time box stencils: SHAPE has bit (dz + 1) 9 + (dy + 1) 3 + (dx + 1) for every stored offset;
-// the k-th set bit in that (lexicographic = ascending offset) order is the image's offset k.
-constexpr unsigned kShape7 = (1u << 4) | (1u << 10) | (1u << 12) | (1u << 13) | (1u << 14) | (1u << 16) | (1u << 22);
-// P1 on the Kuhn split: all offsets whose nonzero components share one sign
-constexpr unsigned kShapeKuhn = (1u << 0) | (1u << 1) | (1u << 3) | (1u << 4) | (1u << 9) | (1u << 10) | (1u << 12) |
-                                (1u << 13) | (1u << 14) | (1u << 16) | (1u << 17) | (1u << 22) | (1u << 23) |
-                                (1u << 25) | (1u << 26);
-struct BoxShapeTab {
-  int nd;
-  int dz[27], dy[27], dx[27];
-};
-constexpr BoxShapeTab box_shape_tab(unsigned shape)
-{
-  BoxShapeTab t{};
-  for (int b = 0; b < 27; ++b)
-    if ((shape >> b) & 1u)
-    {
-      t.dz[t.nd] = b / 9 - 1;
-      t.dy[t.nd] = (b / 3) % 3 - 1;
-      t.dx[t.nd] = b % 3 - 1;
-      ++t.nd;
-    }
-  return t;
-}
 
 template <int EPI, unsigned SHAPE>
 __global__ __launch_bounds__(kCThreads, 8) void k_boxc_mv8(BoxGeom g, i64 ld, const double *__restrict__ ctab,
@@ -525,8 +570,7 @@ void box_invalidate(eig_mat_s &A)
 // Row classes of a box image (k_boxc_mv8): the 27 representatives' entries and masks to the host,
 // 1 / a_rr per class, then every row checked bitwise against its class on the device; on success
 // A.box_ctab / box_cmask are set.  Needs a stored diagonal in every class.
-static void box_classes(eig_mat_s &A, i64 nx, i64 ny, i64 nz, const std::vector<i32> &dx, const std::vector<i32> &dy,
-                        const std::vector<i32> &dz)
+static void box_classes(eig_mat_s &A, i64 nx, i64 ny, i64 nz)
 {
   if (nx < 3 || ny < 3 || nz < 3 || A.sym_nd >= kCStride || (A.kflags & EIG_MAT_NO_CLASS)) return;
   int k0 = -1;
@@ -579,15 +623,6 @@ static void box_classes(eig_mat_s &A, i64 nx, i64 ny, i64 nz, const std::vector<
   }
   A.box_ctab = dct;
   A.box_cmask = dcm;
-  // class position along an axis: 0 first, 1 interior, 2 last; offset d leaves the grid from the
-  // first position when d < 0, from the last when d > 0
-  auto leaves = [](int pos, int d) { return (pos == 0 && d < 0) || (pos == 2 && d > 0); };
-  bool geo = true;
-  for (int c = 0; c < kBoxClasses; ++c)
-    for (int k = 0; k < A.sym_nd; ++k)
-      if (!((cmask[c] >> k) & 1u) && !(leaves(c % 3, dx[k]) || leaves((c / 3) % 3, dy[k]) || leaves(c / 9, dz[k])))
-        geo = false;
-  A.box_geomask = geo;
 }
 
 // Box-stencil geometry of a band image and its device box image (built on first use and cached on
@@ -639,7 +674,8 @@ bool box_prepare(const eig_mat_s &Ac)
     unsigned hb = 0;
     EIG_HIP(hipMemcpyAsync(&hb, bad, sizeof(unsigned), hipMemcpyDeviceToHost, s));
     EIG_HIP(hipStreamSynchronize(s));
-    if (hb) return false;
+    if (hb & 1u) return false;
+    A.box_geomask = !(hb & 2u);
   }
   // the box image: one array per offset
   {
@@ -655,7 +691,7 @@ bool box_prepare(const eig_mat_s &Ac)
     EIG_HIP(hipStreamSynchronize(s));
     A.box_val = val;
   }
-  box_classes(A, nx, ny, nz, dx, dy, dz);
+  box_classes(A, nx, ny, nz);
   A.box_nx = (int)nx;
   A.box_ny = (int)ny;
   A.box_nz = (int)nz;
@@ -754,22 +790,34 @@ static bool launch_box(const eig_mat_s &A, i64 m, const double *X, double *Y, co
   const uint32_t *m32 = A.sym_mask_bytes == 4 ? static_cast<const uint32_t *>(A.sym_mask) : nullptr;
   const uint8_t *m8 = A.sym_mask_bytes == 1 ? static_cast<const uint8_t *>(A.sym_mask) : nullptr;
   const i64 ld = A.window;
-  for (i64 c0 = 0; c0 < m; c0 += 32)
-  {
-    const i64 off = c0 * ld;  // 4 column blocks of ld rows x 8
-    if (epi == kBoxCheb)
-      hipLaunchKernelGGL(k_box_mv32<kBoxCheb>, dim3((unsigned)(tiles * g.nseg)), dim3(kBoxThreads), 0, s, g, ld,
-                         (const double *)A.box_val, m32, m8, X + off, Y + off, Xold ? Xold + off : nullptr, Bv + off,
-                         dinv, omega, gamma);
-    else if (epi == kBoxResid)
-      hipLaunchKernelGGL(k_box_mv32<kBoxResid>, dim3((unsigned)(tiles * g.nseg)), dim3(kBoxThreads), 0, s, g, ld,
-                         (const double *)A.box_val, m32, m8, X + off, Y + off, (const double *)nullptr, Bv + off,
-                         (const double *)nullptr, 0.0, 0.0);
-    else
-      hipLaunchKernelGGL(k_box_mv32<kBoxStore>, dim3((unsigned)(tiles * g.nseg)), dim3(kBoxThreads), 0, s, g, ld,
-                         (const double *)A.box_val, m32, m8, X + off, Y + off, (const double *)nullptr,
-                         (const double *)nullptr, (const double *)nullptr, 0.0, 0.0);
-  }
+  unsigned shape = 0;
+  for (int k = 0; k < A.sym_nd; ++k)
+    shape |= 1u << ((A.box_dz[k] + 1) * 9 + (A.box_dy[k] + 1) * 3 + (A.box_dx[k] + 1));
+  auto go = [&](auto shape_tag) {
+    constexpr unsigned S = decltype(shape_tag)::value;
+    for (i64 c0 = 0; c0 < m; c0 += 32)
+    {
+      const i64 off = c0 * ld;  // 4 column blocks of ld rows x 8
+      const dim3 grid((unsigned)(tiles * g.nseg));
+      if (epi == kBoxCheb)
+        hipLaunchKernelGGL((k_box_mv32<kBoxCheb, S>), grid, dim3(kBoxThreads), 0, s, g, ld, (const double *)A.box_val,
+                           m32, m8, X + off, Y + off, Xold ? Xold + off : nullptr, Bv + off, dinv, omega, gamma);
+      else if (epi == kBoxResid)
+        hipLaunchKernelGGL((k_box_mv32<kBoxResid, S>), grid, dim3(kBoxThreads), 0, s, g, ld, (const double *)A.box_val,
+                           m32, m8, X + off, Y + off, (const double *)nullptr, Bv + off, (const double *)nullptr, 0.0,
+                           0.0);
+      else
+        hipLaunchKernelGGL((k_box_mv32<kBoxStore, S>), grid, dim3(kBoxThreads), 0, s, g, ld, (const double *)A.box_val,
+                           m32, m8, X + off, Y + off, (const double *)nullptr, (const double *)nullptr,
+                           (const double *)nullptr, 0.0, 0.0);
+    }
+  };
+  if (A.box_geomask && shape == kShape7 && A.sym_nd == 7)
+    go(std::integral_constant<unsigned, kShape7>{});
+  else if (A.box_geomask && shape == kShapeKuhn && A.sym_nd == 15)
+    go(std::integral_constant<unsigned, kShapeKuhn>{});
+  else
+    go(std::integral_constant<unsigned, 0u>{});
   EIG_HIP(hipGetLastError());
   return true;
 }

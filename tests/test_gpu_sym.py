@@ -372,20 +372,23 @@ _P7 = {(0, 0, 0): 6.0, (1, 0, 0): -1.0, (-1, 0, 0): -1.0, (0, 1, 0): -1.0, (0, -
        (0, 0, 1): -1.0, (0, 0, -1): -1.0}
 
 
-@pytest.mark.parametrize("kind", ["hole", "nine"])
-def test_boxc_runtime_offsets(ctx, kind):
+@pytest.mark.parametrize("kind,var", [("hole", False), ("nine", False), ("hole", True), ("nine", True)])
+def test_boxc_runtime_offsets(ctx, kind, var):
     """The row-class kernels take the compile-time stencil (7-point, Kuhn 15-point: no masks, every
     offset summed with the zero class entries) only when every offset a class does not store points
     out of the grid; otherwise -- hole: x = 0 rows drop their in-grid z couplings -- and for other
     shapes -- nine: the 7-point plus one face diagonal -- the runtime offset loop with the row masks.
-    All bitwise the reference SpMM; the Chebyshev step equal to the SELL kernel to rounding."""
+    var: two rows leave their class -- the box-image kernel (k_box_mv32), same rule.  All bitwise
+    the reference SpMM; the Chebyshev step equal to the SELL kernel to rounding."""
     st = dict(_P7)
     if kind == "nine":
         st[(0, 1, 1)] = st[(0, -1, -1)] = -0.25
         st[(0, 0, 0)] = 6.5
     A = _box_stencil(17, st, drop_xfirst_z=(kind == "hole"))
+    if var:
+        A = _perturbed(A, rows=(1000, 2344))  # (x = 14, 15 on the 17-grid: the pair (i, i + 1) exists)
     M = upload(ctx, A)
-    assert M.kernel("spmm32") == "k_boxc_mv8"
+    assert M.kernel("spmm32") == ("k_box_mv32" if var else "k_boxc_mv8")
     for m in (8, 32):
         Qh = oracle.random_mv8(A.n, m, 23)
         Q, Y = ctx.array(Qh), ctx.zeros(A.n * m)

@@ -339,13 +339,21 @@ def boxk(ctx):
     SpMM Y = K X (k_boxc_mv8<kBoxStore>, 2 vector streams = 16 m n bytes) and the mass solve's
     Chebyshev step (kBoxCheb, 4 streams = 32 m n bytes) from the difference of two solve degrees."""
     N = int(os.environ.get("EIGMI_C5_N", "256"))
+    var = os.environ.get("EIGMI_BOXK_VAR", "0") == "1"
     b, n, reps = 32, N ** 3, 20
-    rk, ck, vk = eigmi.gen_matrix(eigmi.GEN_P1STIFF3D, N)
-    K = eigmi.Matrix.from_bcsr(ctx, rk, ck, vk)
-    del rk, ck, vk
-    rm, cm, vm = eigmi.gen_matrix(eigmi.GEN_P1MASS3D, N)
-    M = eigmi.Matrix.from_bcsr(ctx, rm, cm, vm)
-    del rm, cm, vm
+
+    def load(kind):
+        r, c, v = eigmi.gen_matrix(kind, N)
+        if var:
+            # variable coefficients: a random positive diagonal term per row (the rows leave their
+            # geometric class, so the box-image kernel runs; the pattern stays the same)
+            rows = np.repeat(np.arange(n, dtype=np.int64), np.diff(r))
+            diag = np.nonzero(c == rows)[0]
+            v[diag] *= 1.0 + 0.01 * np.random.default_rng(1).random(n)
+            del rows, diag
+        return eigmi.Matrix.from_bcsr(ctx, r, c, v)
+    K = load(eigmi.GEN_P1STIFF3D)
+    M = load(eigmi.GEN_P1MASS3D)
     X, Y = ctx.zeros(n * b), ctx.zeros(n * b)
     ctx.check(eigmi.lib.eig_fill_normal(ctx.h, n * b, 5, X.ptr))
     eigmi.spmm_mv8(K, b, X, Y)
@@ -357,7 +365,7 @@ def boxk(ctx):
         ctx.sync()
     ts, _ = wall(spmm)
     ts /= reps
-    emit(config=f"P1 K {N}^3 m={b}", op="SpMM (row-class kBoxStore)", kernel=K.kernel("spmm32"), us=round(ts * 1e6, 1),
+    emit(config=f"P1 K {N}^3 m={b}" + (" (variable diagonal)" if var else ""), op="SpMM (kBoxStore)", kernel=K.kernel("spmm32"), us=round(ts * 1e6, 1),
          bytes=16 * b * n, frac=round(16 * b * n / ts / 1e9 / PEAK, 4))
     d0, d1 = 2, 22
     eigmi.mass_solve_mv8(M, b, d0, X, Y)
@@ -365,8 +373,15 @@ def boxk(ctx):
     t0, _ = wall(lambda: (eigmi.mass_solve_mv8(M, b, d0, X, Y), ctx.sync()), 5)
     t1, _ = wall(lambda: (eigmi.mass_solve_mv8(M, b, d1, X, Y), ctx.sync()), 5)
     tc = (t1 - t0) / (d1 - d0)
-    emit(config=f"P1 M {N}^3 m={b}", op="Chebyshev step (row-class kBoxCheb)", kernel=M.kernel("cheb32"),
-         us=round(tc * 1e6, 1), bytes=32 * b * n, frac=round(32 * b * n / tc / 1e9 / PEAK, 4))
+    # vectors only for the row-class kernels; the box image adds its nd value arrays (+ D^-1 for the
+    # Chebyshev step) per row
+    img_s = 0 if K.kernel("spmm32") == "k_boxc_mv8" else 15 * 8 * n
+    img_c = 0 if M.kernel("cheb32") == "k_boxc_mv8_cheb" else 15 * 8 * n + 8 * n
+    emit(config=f"P1 K {N}^3 m={b}" + (" (variable diagonal)" if var else ""), op="SpMM bytes incl. image",
+         bytes=16 * b * n + img_s, frac=round((16 * b * n + img_s) / ts / 1e9 / PEAK, 4))
+    emit(config=f"P1 M {N}^3 m={b}" + (" (variable diagonal)" if var else ""), op="Chebyshev step (kBoxCheb)",
+         kernel=M.kernel("cheb32"), us=round(tc * 1e6, 1), bytes=32 * b * n + img_c,
+         frac=round((32 * b * n + img_c) / tc / 1e9 / PEAK, 4))
     X.free(), Y.free()
     K.close(), M.close()
 

@@ -61,7 +61,9 @@ run_task() {
     boxk)
       prof_env
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/boxk_trace" -o trace -- \
-        python3 tools/bench_configs.py boxk > "$O/boxk.jsonl" 2> "$O/boxk.err" ;;
+        python3 tools/bench_configs.py boxk > "$O/boxk.jsonl" 2> "$O/boxk.err" && \
+      EIGMI_BOXK_VAR=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/boxkvar_trace" -o trace -- \
+        python3 tools/bench_configs.py boxk >> "$O/boxk.jsonl" 2>> "$O/boxk.err" ;;
     c5)
       EIGMI_C5_N=256 timeout -k 10 300 python -u tools/bench_configs.py c5 > "$O/c5.jsonl" 2> "$O/c5.err" ;;
     c5si)
