@@ -15,6 +15,7 @@
 #   grampmc              FETCH_SIZE / WRITE_SIZE passes over the gram timings -> grampmc/{fetch,write}
 #   boxk                 row-class box kernels alone (SpMM, Chebyshev step) at 256^3 under a kernel trace -> boxk.jsonl, boxk_trace/
 #   c5 | c5si            block Lanczos 256^3: largest end / smallest end (multigrid solve)  -> c5*.jsonl
+#   c5trace              both under a kernel trace                            -> c5_trace/, c5si_trace/
 #   latency              fused step vs eig_mv across sizes and slabs, plane-run counts  -> latency.jsonl
 #   pipe                 fused vs pipelined on one rank's slab and the cube   -> pipe.jsonl
 #   csr                  general (scrambled + RCM) 256^3 matrix: SpMV / Lanczos kernels  -> csr.jsonl
@@ -68,6 +69,13 @@ run_task() {
       EIGMI_C5_N=256 timeout -k 10 300 python -u tools/bench_configs.py c5 > "$O/c5.jsonl" 2> "$O/c5.err" ;;
     c5si)
       EIGMI_C5_N=256 timeout -k 10 600 python -u tools/bench_configs.py c5si > "$O/c5si.jsonl" 2> "$O/c5si.err" ;;
+    c5trace)
+      # C5 block steps (both ends) under a kernel trace: the per-kernel split of a block step
+      prof_env
+      EIGMI_C5_N=256 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/c5_trace" -o trace -- \
+        python3 tools/bench_configs.py c5 > "$O/c5t.jsonl" 2> "$O/c5t.err" && \
+      EIGMI_C5_N=256 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/c5si_trace" -o trace -- \
+        python3 tools/bench_configs.py c5si > "$O/c5sit.jsonl" 2> "$O/c5sit.err" ;;
     latency)
       sweep --N 128 --variants fused,fused@32,fused@28,fused@16,fused@12,mv,mv@16 && \
       sweep --N 256 --variants fused,fused@8,fused@7,fused@6,fused@4,mv,mv@7 && \
