@@ -81,16 +81,40 @@ double *cheb_solve(eig_mat_s &M, i64 m, int degree, double lmin, double lmax, co
 {
   const i64 n = M.nb_rows, ld = M.window, own = M.own_offset;
   const double gamma = 2.0 / (lmin + lmax), mu = (lmax - lmin) / (lmax + lmin);
+  double omega = 1.0 / (1.0 - 0.5 * mu * mu);  // omega_1
+  // Row-class image (one rank): x_1 = gamma D^-1 b is never stored -- the first step forms it while
+  // b's planes enter the LDS ring (x_2 straight from b), the second forms x_{k-1} = x_1 from the
+  // row's b.  Same arithmetic as the k_cheb_init + box-step chain below.
+  if (degree >= 2 && Xc && !M.ctx->distributed() && launch_box_cheb_first(M, m, Bv, omega, gamma, Xa, s))
+  {
+    if (degree == 2) return Xa;
+    omega = 1.0 / (1.0 - 0.25 * mu * mu * omega);
+    EIG_CHECK(launch_box_cheb_second(M, m, Xa, Bv, omega, gamma, Xc, s), EIG_ERR_ARG,
+              "Chebyshev: second row-class step refused");
+    double *x2 = Xa;
+    Xa = Xc;  // x_3
+    Xc = Xb;
+    Xb = x2;
+    for (int k = 3; k < degree; ++k)
+    {
+      omega = 1.0 / (1.0 - 0.25 * mu * mu * omega);
+      launch_box_cheb(M, m, Xa, Xb, Bv, dinv, omega, gamma, s, Xc);  // Xc = x_{k+1}
+      double *t = Xb;
+      Xb = Xa;
+      Xa = Xc;
+      Xc = t;
+    }
+    return Xa;
+  }
   launch_cheb_init(n, ld, own, m, Bv, dinv, gamma, Xa, s);
   if (degree <= 1) return Xa;
-  double omega = 1.0;
   const bool oop = Xc && m % 32 == 0 && box_prepare(M);
   // x_0 = 0: the box kernel (a third output buffer) takes it as "not read"; the in-place kernels
   // read a cleared buffer
   if (!oop) EIG_HIP(hipMemsetAsync(Xb, 0, (size_t)ld * m * sizeof(double), s));
   for (int k = 1; k < degree; ++k)
   {
-    omega = (k == 1) ? 1.0 / (1.0 - 0.5 * mu * mu) : 1.0 / (1.0 - 0.25 * mu * mu * omega);
+    if (k > 1) omega = 1.0 / (1.0 - 0.25 * mu * mu * omega);
     halo_mv(M, Xa, m, s);
     if (oop)
     {

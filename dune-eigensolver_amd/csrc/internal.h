@@ -302,6 +302,10 @@ bool launch_box_cheb(const eig_mat_s &M, i64 m, const double *Xk, double *Xold, 
                      double omega, double gamma, hipStream_t s, double *Xnew = nullptr);
 void box_invalidate(eig_mat_s &A);
 bool launch_box_resid(const eig_mat_s &A, i64 m, const double *X, const double *B, double *R, hipStream_t s);
+bool launch_box_cheb_first(const eig_mat_s &M, i64 m, const double *B, double omega, double gamma, double *Y,
+                           hipStream_t s);
+bool launch_box_cheb_second(const eig_mat_s &M, i64 m, const double *X2, const double *B, double omega, double gamma,
+                            double *Y, hipStream_t s);
 // R = B - A X for window-layout multivectors (m % 8 == 0); R may alias B, not X.
 void launch_resid_mv8(const eig_mat_s &A, i64 m, const double *X, const double *B, double *R, hipStream_t s);
 bool launch_spmm_march(const eig_mat_s &A, i64 m, const double *X, double *Y, hipStream_t s);

@@ -29,7 +29,11 @@ constexpr int kBoxHX = kBoxTX + 2, kBoxHY = kBoxTY + 2;        // with the one-r
 constexpr int kBoxThreads = 1024;  // 16 waves: wave = (tile y, x half), lane = (x, 4-column quad)
 constexpr int kBoxChunks = kBoxHY * kBoxHX * 4 * 4;            // 16-B chunks of one plane (rows x blocks x 4)
 constexpr int kBoxRounds = (kBoxChunks + kBoxThreads - 1) / kBoxThreads;
-enum { kBoxStore = 0, kBoxCheb = 1, kBoxResid = 2 };  // kBoxResid: Y = B - A X (multigrid residual)
+// kBoxResid: Y = B - A X (multigrid residual).  Row-class kernel only: kBoxChebFirst, the first
+// Chebyshev step from x_0 = 0 with x_1 = gamma D^-1 b formed while b's planes enter the ring, and
+// kBoxChebSecond, the second step with x_{k-1} = x_1 = gamma D^-1 b formed from the row's b (x_1 is
+// never stored: two vector passes less per solve)
+enum { kBoxStore = 0, kBoxCheb = 1, kBoxResid = 2, kBoxChebFirst = 3, kBoxChebSecond = 4 };
 constexpr int kBoxMaxNd = 15;  // offsets the kernel holds in registers (P1 Kuhn: 15, 7-point: 7)
 
 typedef double dv2b __attribute__((ext_vector_type(2)));
@@ -415,7 +419,9 @@ __global__ __launch_bounds__(kCThreads, 8) void k_boxc_mv8(BoxGeom g, i64 ld, co
   const int tile = item % (g.ntx * g.nty), seg = item / (g.ntx * g.nty);
   const int x0 = (tile % g.ntx) * kCTX, y0 = (tile / g.ntx) * kCTY;
   const int z0 = seg * g.nz / g.nseg, z1 = (seg + 1) * g.nz / g.nseg;
-  // X plane zz of the tile + halo (8 columns, 64-B rows) into ring slot zz mod 3
+  constexpr bool cheb = EPI == kBoxCheb || EPI == kBoxChebFirst || EPI == kBoxChebSecond;
+  // X plane zz of the tile + halo (8 columns, 64-B rows) into ring slot zz mod 3 (kBoxChebFirst: X is
+  // b, and the ring takes x_1 = (gamma / a_rr) b with the row's class diagonal, as k_cheb_init)
   dv2b pre[kCRounds];
   auto fetch = [&](int zz) {
 #pragma unroll
@@ -434,7 +440,18 @@ __global__ __launch_bounds__(kCThreads, 8) void k_boxc_mv8(BoxGeom g, i64 ld, co
     for (int i = 0; i < kCRounds; ++i)
     {
       const int c = tid + i * kCThreads;
-      if (c < kCChunks) ring[sl][c >> 2][c & 3] = pre[i];
+      if (c < kCChunks)
+      {
+        dv2b v = pre[i];
+        if constexpr (EPI == kBoxChebFirst)
+        {
+          const int hr = c >> 2, xx = x0 + hr % kCHX - 1, yy = y0 + hr / kCHX - 1;
+          const int zc = zz <= 0 ? 0 : (zz >= g.nz - 1 ? 2 : 1);
+          const double gr = gamma * ct[zc * 9 + box_cls1(yy, g.ny) * 3 + box_cls1(xx, g.nx)][kCStride - 1];
+          v = dv2b{gr * v.x, gr * v.y};  // (outside rows: 0 either way)
+        }
+        ring[sl][c >> 2][c & 3] = v;
+      }
     }
   };
   // this thread: row (x0 + xi, y0 + yi), column pair cp; a wave = 16 consecutive x rows
@@ -447,7 +464,10 @@ __global__ __launch_bounds__(kCThreads, 8) void k_boxc_mv8(BoxGeom g, i64 ld, co
   auto fetch_cheb = [&](int zz, dv2b &b2, dv2b &x2) {
     if (EPI == kBoxStore || !own || zz >= z1) return;
     const i64 r = (i64)x + (i64)g.nx * y + (i64)g.P * zz;
-    b2 = __builtin_nontemporal_load(Bb + r * 4 + cp);
+    if constexpr (EPI == kBoxChebFirst)
+      b2 = Bb[r * 4 + cp];  // (the plane just went through the ring: an L2 hit)
+    else
+      b2 = __builtin_nontemporal_load(Bb + r * 4 + cp);
     if (EPI == kBoxCheb && Ob) x2 = __builtin_nontemporal_load(Ob + r * 4 + cp);  // (null: x_{k-1} = 0)
   };
   fetch(z0 - 1);
@@ -490,7 +510,7 @@ __global__ __launch_bounds__(kCThreads, 8) void k_boxc_mv8(BoxGeom g, i64 ld, co
       // halo row, and +0 added to a sum that starts at +0 changes nothing -- the same sums as with
       // the mask.  LDS offsets are immediates off three per-plane slot bases.
       constexpr BoxShapeTab T = box_shape_tab(SHAPE);
-      constexpr int kGroup = EPI == kBoxCheb ? 2 : 4;  // (the Chebyshev step holds 4 more vectors)
+      constexpr int kGroup = cheb ? 2 : 4;  // (the Chebyshev step holds 4 more vectors)
       // ring index (dv2b units) of the (-1, -1) neighbour in the three slots, made opaque to the
       // compiler: otherwise it hoists base + offset for every offset out of the plane loop (one
       // live VGPR per offset and slot, ~110 VGPRs: one workgroup per CU instead of two)
@@ -533,6 +553,7 @@ __global__ __launch_bounds__(kCThreads, 8) void k_boxc_mv8(BoxGeom g, i64 ld, co
       {
         const dv2b xc = ring[s0][hrow][cp];
         const double gd = gamma * ct[cls][kCStride - 1];
+        if constexpr (EPI == kBoxChebSecond) xo = dv2b{gd * bb.x, gd * bb.y};  // x_1 (k_cheb_init's product)
         const double o0 = omega * (xc.x + gd * (bb.x - acc.x) - xo.x) + xo.x;
         const double o1 = omega * (xc.y + gd * (bb.y - acc.y) - xo.y) + xo.y;
         __builtin_nontemporal_store(dv2b{o0, o1}, Yb + r * 4 + cp);
@@ -720,6 +741,7 @@ static bool launch_box(const eig_mat_s &A, i64 m, const double *X, double *Y, co
                        const double *dinv, double omega, double gamma, int epi, hipStream_t s)
 {
   if (m <= 0 || m % 8 != 0 || !box_prepare(A)) return false;
+  if ((epi == kBoxChebFirst || epi == kBoxChebSecond) && !A.box_ctab) return false;  // (row-class only)
   if (A.box_ctab)
   {
     // row-class kernels: one launch, blockIdx.y = column block; z runs for ~2 rounds of the
@@ -753,6 +775,12 @@ static bool launch_box(const eig_mat_s &A, i64 m, const double *X, double *Y, co
       if (epi == kBoxCheb)
         hipLaunchKernelGGL((k_boxc_mv8<kBoxCheb, S>), grid, dim3(kCThreads), 0, s, g, A.window, ct, cm, X, Y, Xold,
                            Bv, omega, gamma);
+      else if (epi == kBoxChebFirst)
+        hipLaunchKernelGGL((k_boxc_mv8<kBoxChebFirst, S>), grid, dim3(kCThreads), 0, s, g, A.window, ct, cm, X, Y,
+                           (const double *)nullptr, Bv, omega, gamma);
+      else if (epi == kBoxChebSecond)
+        hipLaunchKernelGGL((k_boxc_mv8<kBoxChebSecond, S>), grid, dim3(kCThreads), 0, s, g, A.window, ct, cm, X, Y,
+                           (const double *)nullptr, Bv, omega, gamma);
       else if (epi == kBoxResid)
         hipLaunchKernelGGL((k_boxc_mv8<kBoxResid, S>), grid, dim3(kCThreads), 0, s, g, A.window, ct, cm, X, Y,
                            (const double *)nullptr, Bv, 0.0, 0.0);
@@ -837,6 +865,21 @@ bool launch_box_cheb(const eig_mat_s &M, i64 m, const double *Xk, double *Xold, 
 {
   EIG_CHECK(Xold || Xnew, EIG_ERR_ARG, "box Chebyshev step: x_{k-1} = 0 needs a separate output buffer");
   return launch_box(M, m, Xk, Xnew ? Xnew : Xold, Xold, B, dinv, omega, gamma, kBoxCheb, s);
+}
+
+// The first Chebyshev step from x_0 = 0, x_1 = gamma D^-1 B never stored: Y = x_2 straight from B
+// (row-class image only; false otherwise -- the caller then runs k_cheb_init and launch_box_cheb).
+bool launch_box_cheb_first(const eig_mat_s &M, i64 m, const double *B, double omega, double gamma, double *Y,
+                           hipStream_t s)
+{
+  return launch_box(M, m, B, Y, nullptr, B, nullptr, omega, gamma, kBoxChebFirst, s);
+}
+
+// The second step, x_3 from x_2 = X2 and x_1 = gamma D^-1 B (formed per row, not read): Y = x_3.
+bool launch_box_cheb_second(const eig_mat_s &M, i64 m, const double *X2, const double *B, double omega, double gamma,
+                            double *Y, hipStream_t s)
+{
+  return launch_box(M, m, X2, Y, nullptr, B, nullptr, omega, gamma, kBoxChebSecond, s);
 }
 
 }  // namespace eigmi
