@@ -35,135 +35,142 @@ __device__ __forceinline__ void add_row(double (&acc)[8], const double *p, doubl
 
 }  // namespace
 
+// Thread layout of the transfers: a workgroup takes 64 consecutive x of one grid line (y, z) and
+// one 8-column block (blockIdx.y); thread t handles x = x0 + t / 4 and the 16-B quarter t % 4 of
+// that 64-B row, so a wave's accesses are 1-KiB contiguous runs.  The line and x chunk come from
+// blockIdx.x (scalar), no per-element 64-bit division.
+constexpr int kMgRows = 64;
+
 // Bc(I) = sum over the fine 3 x 3 x 3 block around 2 I + 1 of w_x w_y w_z Rf(i)  (w = 1 at the
 // centre, 1/2 at +-1 per direction), z, y, x ascending
-__global__ __launch_bounds__(256) void k_mg_restrict(int fx, int fy, int fz, int cx, int cy, int cz, int nblk, i64 ldf,
-                                                     i64 ldc, const double *__restrict__ Rf, double *__restrict__ Bc)
+__global__ __launch_bounds__(256) void k_mg_restrict(int fx, int fy, int fz, int cx, int cy, int cz, i64 ldf, i64 ldc,
+                                                     const double *__restrict__ Rf, double *__restrict__ Bc)
 {
-  const i64 nc = (i64)cx * cy * cz, total = nc * nblk;
-  for (i64 idx = (i64)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (i64)gridDim.x * 256)
+  const int xb = (cx + kMgRows - 1) / kMgRows, line = (int)blockIdx.x / xb;
+  const int X = ((int)blockIdx.x - line * xb) * kMgRows + (int)(threadIdx.x >> 2), q = threadIdx.x & 3;
+  const int Y = line % cy, Z = line / cy;
+  if (X >= cx || Z >= cz) return;
+  const double *base = Rf + (i64)blockIdx.y * ldf * 8 + q * 2;
+  double a0 = 0.0, a1 = 0.0;
+  for (int dz = -1; dz <= 1; ++dz)
   {
-    const i64 b = idx / nc, I = idx - b * nc;
-    const int X = (int)(I % cx), Y = (int)((I / cx) % cy), Z = (int)(I / ((i64)cx * cy));
-    double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    const double *base = Rf + b * ldf * 8;
-    for (int dz = -1; dz <= 1; ++dz)
+    const int z = 2 * Z + 1 + dz;
+    if (z < 0 || z >= fz) continue;
+    const double wz = dz ? 0.5 : 1.0;
+    for (int dy = -1; dy <= 1; ++dy)
     {
-      const int z = 2 * Z + 1 + dz;
-      if (z < 0 || z >= fz) continue;
-      const double wz = dz ? 0.5 : 1.0;
-      for (int dy = -1; dy <= 1; ++dy)
+      const int y = 2 * Y + 1 + dy;
+      if (y < 0 || y >= fy) continue;
+      const double wzy = wz * (dy ? 0.5 : 1.0);
+      const double *lp = base + ((i64)z * fy + y) * fx * 8;
+#pragma unroll
+      for (int dx = -1; dx <= 1; ++dx)
       {
-        const int y = 2 * Y + 1 + dy;
-        if (y < 0 || y >= fy) continue;
-        const double wzy = wz * (dy ? 0.5 : 1.0);
-        for (int dx = -1; dx <= 1; ++dx)
-        {
-          const int x = 2 * X + 1 + dx;
-          if (x < 0 || x >= fx) continue;
-          add_row(acc, base + (((i64)z * fy + y) * fx + x) * 8, wzy * (dx ? 0.5 : 1.0));
-        }
+        const int x = 2 * X + 1 + dx;
+        if (x < 0 || x >= fx) continue;
+        const double w = wzy * (dx ? 0.5 : 1.0);
+        const double2 v = *reinterpret_cast<const double2 *>(lp + (i64)x * 8);
+        a0 += w * v.x;
+        a1 += w * v.y;
       }
     }
-    double2 *dst = reinterpret_cast<double2 *>(Bc + (b * ldc + I) * 8);
-#pragma unroll
-    for (int h = 0; h < 4; ++h) dst[h] = make_double2(acc[2 * h], acc[2 * h + 1]);
   }
+  *reinterpret_cast<double2 *>(Bc + ((i64)blockIdx.y * ldc + ((i64)Z * cy + Y) * cx + X) * 8 + q * 2) =
+      make_double2(a0, a1);
 }
 
 // Xf(i) += sum over the coarse nodes of i of w_x w_y w_z Xc(J)  (z, y, x ascending)
-__global__ __launch_bounds__(256) void k_mg_prolong_add(int fx, int fy, int fz, int cx, int cy, int cz, int nblk,
-                                                        i64 ldf, i64 ldc, const double *__restrict__ Xc,
+__global__ __launch_bounds__(256) void k_mg_prolong_add(int fx, int fy, int fz, int cx, int cy, int cz, i64 ldf,
+                                                        i64 ldc, const double *__restrict__ Xc,
                                                         double *__restrict__ Xf)
 {
-  const i64 nf = (i64)fx * fy * fz, total = nf * nblk;
-  for (i64 idx = (i64)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (i64)gridDim.x * 256)
-  {
-    const i64 b = idx / nf, i = idx - b * nf;
-    const int x = (int)(i % fx), y = (int)((i / fx) % fy), z = (int)(i / ((i64)fx * fy));
-    // per direction: coarse indices c0 (weight w0) and c1 (weight w1; -1 = none)
-    auto split = [](int f, int nc, int &c0, int &c1, double &w0) {
-      if (f & 1)
-      {
-        c0 = (f - 1) >> 1;
-        c1 = -1;
-        w0 = 1.0;
-      }
-      else
-      {
-        c0 = (f >> 1) - 1;
-        c1 = (f >> 1) < nc ? (f >> 1) : -1;
-        w0 = 0.5;
-      }
-    };
-    int zc[2], yc[2], xc[2];
-    double wz, wy, wx;
-    split(z, cz, zc[0], zc[1], wz);
-    split(y, cy, yc[0], yc[1], wy);
-    split(x, cx, xc[0], xc[1], wx);
-    double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    const double *base = Xc + b * ldc * 8;
-    for (int a = 0; a < 2; ++a)
+  const int xb = (fx + kMgRows - 1) / kMgRows, line = (int)blockIdx.x / xb;
+  const int x = ((int)blockIdx.x - line * xb) * kMgRows + (int)(threadIdx.x >> 2), q = threadIdx.x & 3;
+  const int y = line % fy, z = line / fy;
+  if (x >= fx || z >= fz) return;
+  // per direction: coarse indices c0 (weight w0) and c1 (weight w0; -1 = none)
+  auto split = [](int f, int nc, int &c0, int &c1, double &w0) {
+    if (f & 1)
     {
-      if (zc[a] < 0) continue;
-      for (int c = 0; c < 2; ++c)
-      {
-        if (yc[c] < 0) continue;
-        for (int e = 0; e < 2; ++e)
-        {
-          if (xc[e] < 0) continue;
-          add_row(acc, base + (((i64)zc[a] * cy + yc[c]) * cx + xc[e]) * 8, wz * wy * wx);
-        }
-      }
+      c0 = (f - 1) >> 1;
+      c1 = -1;
+      w0 = 1.0;
     }
-    double2 *dst = reinterpret_cast<double2 *>(Xf + (b * ldf + i) * 8);
-#pragma unroll
-    for (int h = 0; h < 4; ++h)
+    else
     {
-      const double2 v = dst[h];
-      dst[h] = make_double2(v.x + acc[2 * h], v.y + acc[2 * h + 1]);
+      c0 = (f >> 1) - 1;
+      c1 = (f >> 1) < nc ? (f >> 1) : -1;
+      w0 = 0.5;
+    }
+  };
+  int zc[2], yc[2], xc[2];
+  double wz, wy, wx;
+  split(z, cz, zc[0], zc[1], wz);
+  split(y, cy, yc[0], yc[1], wy);
+  split(x, cx, xc[0], xc[1], wx);
+  const double w = wz * wy * wx;
+  const double *base = Xc + (i64)blockIdx.y * ldc * 8 + q * 2;
+  double a0 = 0.0, a1 = 0.0;
+  for (int a = 0; a < 2; ++a)
+  {
+    if (zc[a] < 0) continue;
+    for (int c = 0; c < 2; ++c)
+    {
+      if (yc[c] < 0) continue;
+      for (int e = 0; e < 2; ++e)
+      {
+        if (xc[e] < 0) continue;
+        const double2 v = *reinterpret_cast<const double2 *>(base + (((i64)zc[a] * cy + yc[c]) * cx + xc[e]) * 8);
+        a0 += w * v.x;
+        a1 += w * v.y;
+      }
     }
   }
+  double2 *dst = reinterpret_cast<double2 *>(Xf + ((i64)blockIdx.y * ldf + ((i64)z * fy + y) * fx + x) * 8 + q * 2);
+  const double2 v = *dst;
+  *dst = make_double2(v.x + a0, v.y + a1);
 }
 
-// Y = a X + b Y over the n owned rows of m columns (window layout, pointers at owned row 0)
-__global__ __launch_bounds__(256) void k_mv8_axpby(i64 n, int nblk, i64 ld, double a, const double *__restrict__ X,
-                                                   double b, double *__restrict__ Y)
+// Y = a X + b Y over the n owned rows of m columns (window layout, pointers at owned row 0);
+// blockIdx.y = column block, 16-B pieces
+__global__ __launch_bounds__(256) void k_mv8_axpby(i64 n, i64 ld, double a, const double *__restrict__ X, double b,
+                                                   double *__restrict__ Y)
 {
-  const i64 total = n * nblk * 4;  // 16-B pieces
+  const i64 off = (i64)blockIdx.y * ld * 8, total = n * 4;
+  const double2 *xs = reinterpret_cast<const double2 *>(X + off);
+  double2 *ys = reinterpret_cast<double2 *>(Y + off);
   for (i64 idx = (i64)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (i64)gridDim.x * 256)
   {
-    const i64 row = idx >> 2, blk = row / n, r = row - blk * n;
-    const i64 at = (blk * ld + r) * 8 + (idx & 3) * 2;
-    const double2 x = *reinterpret_cast<const double2 *>(X + at);
-    double2 *y = reinterpret_cast<double2 *>(Y + at);
-    const double2 v = *y;
-    *y = make_double2(a * x.x + b * v.x, a * x.y + b * v.y);
+    const double2 x = xs[idx];
+    const double2 v = ys[idx];
+    ys[idx] = make_double2(a * x.x + b * v.x, a * x.y + b * v.y);
   }
 }
 
 void launch_mg_restrict(const int *fdim, const int *cdim, i64 m, i64 ldf, i64 ldc, const double *Rf, double *Bc,
                         hipStream_t s)
 {
-  const i64 nc = (i64)cdim[0] * cdim[1] * cdim[2];
-  hipLaunchKernelGGL(k_mg_restrict, dim3(grid_cap(nc * (m / 8), 256, kStreamBlocks)), dim3(256), 0, s, fdim[0],
-                     fdim[1], fdim[2], cdim[0], cdim[1], cdim[2], (int)(m / 8), ldf, ldc, Rf, Bc);
+  const i64 blocks = (i64)((cdim[0] + kMgRows - 1) / kMgRows) * cdim[1] * cdim[2];
+  EIG_CHECK(blocks < (1LL << 31), EIG_ERR_SHAPE, "multigrid restriction: grid too large");
+  hipLaunchKernelGGL(k_mg_restrict, dim3((unsigned)blocks, (unsigned)(m / 8)), dim3(256), 0, s, fdim[0], fdim[1],
+                     fdim[2], cdim[0], cdim[1], cdim[2], ldf, ldc, Rf, Bc);
   EIG_HIP(hipGetLastError());
 }
 
 void launch_mg_prolong_add(const int *fdim, const int *cdim, i64 m, i64 ldf, i64 ldc, const double *Xc, double *Xf,
                            hipStream_t s)
 {
-  const i64 nf = (i64)fdim[0] * fdim[1] * fdim[2];
-  hipLaunchKernelGGL(k_mg_prolong_add, dim3(grid_cap(nf * (m / 8), 256, kStreamBlocks)), dim3(256), 0, s, fdim[0],
-                     fdim[1], fdim[2], cdim[0], cdim[1], cdim[2], (int)(m / 8), ldf, ldc, Xc, Xf);
+  const i64 blocks = (i64)((fdim[0] + kMgRows - 1) / kMgRows) * fdim[1] * fdim[2];
+  EIG_CHECK(blocks < (1LL << 31), EIG_ERR_SHAPE, "multigrid prolongation: grid too large");
+  hipLaunchKernelGGL(k_mg_prolong_add, dim3((unsigned)blocks, (unsigned)(m / 8)), dim3(256), 0, s, fdim[0], fdim[1],
+                     fdim[2], cdim[0], cdim[1], cdim[2], ldf, ldc, Xc, Xf);
   EIG_HIP(hipGetLastError());
 }
 
 void launch_mv8_axpby(i64 n, i64 m, i64 ld, double a, const double *X, double b, double *Y, hipStream_t s)
 {
-  hipLaunchKernelGGL(k_mv8_axpby, dim3(grid_cap(n * (m / 8) * 4, 256, kStreamBlocks)), dim3(256), 0, s, n,
-                     (int)(m / 8), ld, a, X, b, Y);
+  hipLaunchKernelGGL(k_mv8_axpby, dim3(grid_cap(n * 4, 256, 4 * kStreamBlocks / (int)(m / 8) + 1), (unsigned)(m / 8)),
+                     dim3(256), 0, s, n, ld, a, X, b, Y);
   EIG_HIP(hipGetLastError());
 }
 
