@@ -410,6 +410,7 @@ __global__ __launch_bounds__(kCThreads, 8) void k_boxc_mv8(BoxGeom g, i64 ld, co
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   for (int i = tid; i < kBoxClasses * kCStride; i += kCThreads) ct[i / kCStride][i % kCStride] = ctab[i];
   if (tid < kBoxClasses) cm[tid] = cmask[tid];
+  if constexpr (EPI == kBoxChebFirst) __syncthreads();  // the prologue's ring stores read the class table
   const i64 boff = (i64)blockIdx.y * ld * 8;  // column block
   const dv2b *Xb = reinterpret_cast<const dv2b *>(X + boff);
   dv2b *Yb = reinterpret_cast<dv2b *>(Y + boff);

@@ -422,3 +422,23 @@ def test_boxc_compile_time_stencils(ctx):
         got = Y.get()
         assert np.array_equal(got, ref)
         assert np.array_equal(np.signbit(got), np.signbit(ref))
+
+
+def test_box_chebyshev_first_step_after_other_class_table(ctx):
+    """The first Chebyshev step (x_1 = gamma D^-1 b formed as b enters the LDS ring) reads the class
+    table in its prologue: right after a row-class SpMM on another matrix (whose table the CU's LDS
+    still holds) a degree-2 and a degree-3 solve of the mass matrix equal the SELL kernel's."""
+    K, Mh = _p1(16, "K"), _p1(16, "M")
+    dK, dM = upload(ctx, K), upload(ctx, Mh)
+    dMs = upload(ctx, Mh, flags=eigmi.MAT_NO_MARCH)
+    n, m = Mh.n, 32
+    Bh = oracle.random_mv8(n, m, 41)
+    B, Y = ctx.array(Bh), ctx.zeros(n * m)
+    X1, X2 = ctx.zeros(n * m), ctx.zeros(n * m)
+    for degree in (2, 3):
+        eigmi.spmm_mv8(dK, m, B, Y)  # another class table through the same kernel's LDS
+        eigmi.mass_solve_mv8(dM, m, degree, B, X1)
+        eigmi.mass_solve_mv8(dMs, m, degree, B, X2)
+        a, b = X1.get(), X2.get()
+        assert np.all(np.isfinite(a))
+        assert np.allclose(a, b, rtol=1e-13, atol=1e-14 * np.abs(b).max()), (degree, np.abs(a - b).max())

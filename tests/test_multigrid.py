@@ -89,6 +89,7 @@ def test_mg_converges_and_is_symmetric(ctx):
     dB, dX = _mv(ctx, B), ctx.zeros(n * m)
     r = [mg.solve(m, dB, dX, c, resid=True) for c in (2, 6, 14)]
     print("multigrid residual after 2 / 6 / 14 iterations:", r)
+    assert np.all(np.isfinite(r)) and r[0] < 0.05, r  # (2 iterations at ~0.1 each)
     rho = (r[1] / r[0]) ** 0.25
     assert rho < 0.2, rho
     assert r[2] <= 1e-12
