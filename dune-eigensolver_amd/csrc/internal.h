@@ -304,6 +304,8 @@ void box_invalidate(eig_mat_s &A);
 bool launch_box_resid(const eig_mat_s &A, i64 m, const double *X, const double *B, double *R, hipStream_t s);
 bool launch_box_cheb_first(const eig_mat_s &M, i64 m, const double *B, double omega, double gamma, double *Y,
                            hipStream_t s);
+bool launch_box_cheb_first_add(const eig_mat_s &M, i64 m, const double *B, double omega, double gamma, double *Y,
+                               hipStream_t s);
 bool launch_box_cheb_second(const eig_mat_s &M, i64 m, const double *X2, const double *B, double omega, double gamma,
                             double *Y, hipStream_t s);
 // R = B - A X for window-layout multivectors (m % 8 == 0); R may alias B, not X.

@@ -33,8 +33,11 @@ constexpr int kBoxRounds = (kBoxChunks + kBoxThreads - 1) / kBoxThreads;
 // Chebyshev step from x_0 = 0 with x_1 = gamma D^-1 b formed while b's planes enter the ring, and
 // kBoxChebSecond, the second step with x_{k-1} = x_1 = gamma D^-1 b formed from the row's b (x_1 is
 // never stored: two vector passes less per solve)
-enum { kBoxStore = 0, kBoxCheb = 1, kBoxResid = 2, kBoxChebFirst = 3, kBoxChebSecond = 4 };
-constexpr int kBoxMaxNd = 15;  // offsets the kernel holds in registers (P1 Kuhn: 15, 7-point: 7)
+// kBoxChebFirstAdd: kBoxChebFirst added into Y (Y += x_2: a degree-2 smoother's correction applied
+// in place, the multigrid post-smoother)
+enum { kBoxStore = 0, kBoxCheb = 1, kBoxResid = 2, kBoxChebFirst = 3, kBoxChebSecond = 4, kBoxChebFirstAdd = 5 };
+constexpr int kBoxMaxNd = 15;  // offsets of the box-image kernel's LDS value tile (P1 Kuhn: 15, 7-point: 7)
+constexpr int kBoxClassMaxNd = 27;  // offsets of the row-class kernels (27: Galerkin coarse operators)
 
 typedef double dv2b __attribute__((ext_vector_type(2)));
 
@@ -51,6 +54,7 @@ struct BoxGeom {
 // Compile-time box stencils: SHAPE has bit (dz + 1) 9 + (dy + 1) 3 + (dx + 1) for every stored offset;
 // the k-th set bit in that (lexicographic = ascending offset) order is the image's offset k.
 constexpr unsigned kShape7 = (1u << 4) | (1u << 10) | (1u << 12) | (1u << 13) | (1u << 14) | (1u << 16) | (1u << 22);
+constexpr unsigned kShape27 = (1u << 27) - 1u;  // full box (Galerkin coarse operators)
 // P1 on the Kuhn split: all offsets whose nonzero components share one sign
 constexpr unsigned kShapeKuhn = (1u << 0) | (1u << 1) | (1u << 3) | (1u << 4) | (1u << 9) | (1u << 10) | (1u << 12) |
                                 (1u << 13) | (1u << 14) | (1u << 16) | (1u << 17) | (1u << 22) | (1u << 23) |
@@ -361,7 +365,7 @@ constexpr int kCThreads = 1024;
 constexpr int kCChunks = kCHY * kCHX * 4;  // 16-B chunks of one plane (tile + halo, 8 columns)
 constexpr int kCRounds = (kCChunks + kCThreads - 1) / kCThreads;
 constexpr int kBoxClasses = 27;
-constexpr int kCStride = 16;  // doubles per class: nd <= 15 values, then 1 / a_rr
+constexpr int kCStride = 28;  // doubles per class: nd <= 27 values, then 1 / a_rr
 
 __device__ __forceinline__ int box_cls1(int v, int nv) { return v == 0 ? 0 : (v == nv - 1 ? 2 : 1); }
 
@@ -410,7 +414,8 @@ __global__ __launch_bounds__(kCThreads, 8) void k_boxc_mv8(BoxGeom g, i64 ld, co
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   for (int i = tid; i < kBoxClasses * kCStride; i += kCThreads) ct[i / kCStride][i % kCStride] = ctab[i];
   if (tid < kBoxClasses) cm[tid] = cmask[tid];
-  if constexpr (EPI == kBoxChebFirst) __syncthreads();  // the prologue's ring stores read the class table
+  if constexpr (EPI == kBoxChebFirst || EPI == kBoxChebFirstAdd)
+    __syncthreads();  // the prologue's ring stores read the class table
   const i64 boff = (i64)blockIdx.y * ld * 8;  // column block
   const dv2b *Xb = reinterpret_cast<const dv2b *>(X + boff);
   dv2b *Yb = reinterpret_cast<dv2b *>(Y + boff);
@@ -420,7 +425,8 @@ __global__ __launch_bounds__(kCThreads, 8) void k_boxc_mv8(BoxGeom g, i64 ld, co
   const int tile = item % (g.ntx * g.nty), seg = item / (g.ntx * g.nty);
   const int x0 = (tile % g.ntx) * kCTX, y0 = (tile / g.ntx) * kCTY;
   const int z0 = seg * g.nz / g.nseg, z1 = (seg + 1) * g.nz / g.nseg;
-  constexpr bool cheb = EPI == kBoxCheb || EPI == kBoxChebFirst || EPI == kBoxChebSecond;
+  constexpr bool first = EPI == kBoxChebFirst || EPI == kBoxChebFirstAdd;
+  constexpr bool cheb = EPI == kBoxCheb || first || EPI == kBoxChebSecond;
   // X plane zz of the tile + halo (8 columns, 64-B rows) into ring slot zz mod 3 (kBoxChebFirst: X is
   // b, and the ring takes x_1 = (gamma / a_rr) b with the row's class diagonal, as k_cheb_init)
   dv2b pre[kCRounds];
@@ -444,7 +450,7 @@ __global__ __launch_bounds__(kCThreads, 8) void k_boxc_mv8(BoxGeom g, i64 ld, co
       if (c < kCChunks)
       {
         dv2b v = pre[i];
-        if constexpr (EPI == kBoxChebFirst)
+        if constexpr (first)
         {
           const int hr = c >> 2, xx = x0 + hr % kCHX - 1, yy = y0 + hr / kCHX - 1;
           const int zc = zz <= 0 ? 0 : (zz >= g.nz - 1 ? 2 : 1);
@@ -465,7 +471,7 @@ __global__ __launch_bounds__(kCThreads, 8) void k_boxc_mv8(BoxGeom g, i64 ld, co
   auto fetch_cheb = [&](int zz, dv2b &b2, dv2b &x2) {
     if (EPI == kBoxStore || !own || zz >= z1) return;
     const i64 r = (i64)x + (i64)g.nx * y + (i64)g.P * zz;
-    if constexpr (EPI == kBoxChebFirst)
+    if constexpr (first)
       b2 = Bb[r * 4 + cp];  // (the plane just went through the ring: an L2 hit)
     else
       b2 = __builtin_nontemporal_load(Bb + r * 4 + cp);
@@ -555,8 +561,14 @@ __global__ __launch_bounds__(kCThreads, 8) void k_boxc_mv8(BoxGeom g, i64 ld, co
         const dv2b xc = ring[s0][hrow][cp];
         const double gd = gamma * ct[cls][kCStride - 1];
         if constexpr (EPI == kBoxChebSecond) xo = dv2b{gd * bb.x, gd * bb.y};  // x_1 (k_cheb_init's product)
-        const double o0 = omega * (xc.x + gd * (bb.x - acc.x) - xo.x) + xo.x;
-        const double o1 = omega * (xc.y + gd * (bb.y - acc.y) - xo.y) + xo.y;
+        double o0 = omega * (xc.x + gd * (bb.x - acc.x) - xo.x) + xo.x;
+        double o1 = omega * (xc.y + gd * (bb.y - acc.y) - xo.y) + xo.y;
+        if constexpr (EPI == kBoxChebFirstAdd)
+        {
+          const dv2b yv = Yb[r * 4 + cp];  // (the row's own: read-modify-write by this thread only)
+          o0 = yv.x + o0;
+          o1 = yv.y + o1;
+        }
         __builtin_nontemporal_store(dv2b{o0, o1}, Yb + r * 4 + cp);
       }
     }
@@ -655,31 +667,51 @@ bool box_prepare(const eig_mat_s &Ac)
   if (A.box_state != 0) return A.box_state > 0;
   A.box_state = -1;
   if (!A.sym_val || A.br != 1 || A.bc != 1 || A.ctx->distributed() || (A.kflags & EIG_MAT_NO_MARCH)) return false;
-  if (A.sym_nd > kBoxMaxNd || A.nb_rows != A.nb_rows_global || A.window != A.nb_rows) return false;
-  // Nx = the smallest offset > 1, P = the smallest offset > Nx + 1
-  i64 nx = 0, P = 0;
+  if (A.sym_nd > kBoxClassMaxNd || A.nb_rows != A.nb_rows_global || A.window != A.nb_rows) return false;
+  // Grid from the offsets: Nx is the smallest offset > 1 (+1 when the stencil has the (0, +1, -1)
+  // neighbour, d = Nx - 1), P = Nx Ny the smallest offset past Nx + 1 (+ 0, 1, Nx - 1, Nx or Nx + 1
+  // for the neighbours with dz = 1 and dy, dx < 0 .. dy = 1); every offset must be a P + b Nx + c
+  // with a, b, c in {-1, 0, 1}
+  i64 s1 = 0;
   for (int k = 0; k < A.sym_nd; ++k)
-    if (A.sym_off[k] > 1 && (nx == 0 || A.sym_off[k] < nx)) nx = A.sym_off[k];
-  for (int k = 0; k < A.sym_nd; ++k)
-    if (nx > 0 && A.sym_off[k] > nx + 1 && (P == 0 || A.sym_off[k] < P)) P = A.sym_off[k];
-  if (nx < kBoxTX || P == 0 || P % nx != 0 || A.nb_rows % P != 0) return false;
-  const i64 ny = P / nx, nz = A.nb_rows / P;
-  if (ny < kBoxTY || nz < 3 || nz > (1 << 24)) return false;
+    if (A.sym_off[k] > 1 && (s1 == 0 || A.sym_off[k] < s1)) s1 = A.sym_off[k];
   std::vector<i32> dx(A.sym_nd), dy(A.sym_nd), dz(A.sym_nd);
-  for (int k = 0; k < A.sym_nd; ++k)
+  auto decompose = [&](i64 nxc, i64 Pc) {
+    for (int k = 0; k < A.sym_nd; ++k)
+    {
+      const i64 d = A.sym_off[k];
+      bool found = false;
+      for (int a = -1; a <= 1 && !found; ++a)
+        for (int b = -1; b <= 1 && !found; ++b)
+          for (int c = -1; c <= 1 && !found; ++c)
+            if (a * Pc + b * nxc + c == d)
+            {
+              dz[k] = a, dy[k] = b, dx[k] = c;
+              found = true;
+            }
+      if (!found) return false;
+    }
+    return true;
+  };
+  i64 nx = 0, P = 0;
+  for (i64 nxc : {s1, s1 + 1})
   {
-    const i64 d = A.sym_off[k];
-    bool found = false;
-    for (int a = -1; a <= 1 && !found; ++a)
-      for (int b = -1; b <= 1 && !found; ++b)
-        for (int c = -1; c <= 1 && !found; ++c)
-          if (a * P + b * nx + c == d)
-          {
-            dz[k] = a, dy[k] = b, dx[k] = c;
-            found = true;
-          }
-    if (!found) return false;
+    if (nxc < kBoxTX || P) continue;
+    i64 t = 0;
+    for (int k = 0; k < A.sym_nd; ++k)
+      if (A.sym_off[k] > nxc + 1 && (t == 0 || A.sym_off[k] < t)) t = A.sym_off[k];
+    if (t == 0) continue;
+    for (i64 Pc : {t, t + 1, t + nxc - 1, t + nxc, t + nxc + 1})
+      if (!P && Pc % nxc == 0 && A.nb_rows % Pc == 0 && Pc / nxc >= kBoxTY && decompose(nxc, Pc))
+      {
+        nx = nxc;
+        P = Pc;
+      }
   }
+  if (!P) return false;
+  const i64 ny = P / nx, nz = A.nb_rows / P;
+  if (nz < 3 || nz > (1 << 24)) return false;
+  decompose(nx, P);
   hipStream_t s = A.ctx->stream;
   const i64 n = A.nb_rows;
   // wrap-around check on the device (rows on a face storing an entry across it)
@@ -724,11 +756,12 @@ bool box_prepare(const eig_mat_s &Ac)
     A.box_dx[k] = dx[k];
     A.box_dy[k] = dy[k];
   }
-  if (A.box_ctab)
+  if (A.box_ctab || A.sym_nd > kBoxMaxNd)
   {
-    // the class kernels read no box image
+    // the class kernels read no box image; past kBoxMaxNd offsets there is no box-image kernel
     EIG_HIP(hipFree(A.box_val));
     A.box_val = nullptr;
+    if (!A.box_ctab) return false;  // (box_state stays -1)
   }
   else
     A.device_bytes += (i64)A.sym_nd * n * (i64)sizeof(double);
@@ -742,7 +775,8 @@ static bool launch_box(const eig_mat_s &A, i64 m, const double *X, double *Y, co
                        const double *dinv, double omega, double gamma, int epi, hipStream_t s)
 {
   if (m <= 0 || m % 8 != 0 || !box_prepare(A)) return false;
-  if ((epi == kBoxChebFirst || epi == kBoxChebSecond) && !A.box_ctab) return false;  // (row-class only)
+  if ((epi == kBoxChebFirst || epi == kBoxChebSecond || epi == kBoxChebFirstAdd) && !A.box_ctab)
+    return false;  // (row-class only)
   if (A.box_ctab)
   {
     // row-class kernels: one launch, blockIdx.y = column block; z runs for ~2 rounds of the
@@ -779,6 +813,9 @@ static bool launch_box(const eig_mat_s &A, i64 m, const double *X, double *Y, co
       else if (epi == kBoxChebFirst)
         hipLaunchKernelGGL((k_boxc_mv8<kBoxChebFirst, S>), grid, dim3(kCThreads), 0, s, g, A.window, ct, cm, X, Y,
                            (const double *)nullptr, Bv, omega, gamma);
+      else if (epi == kBoxChebFirstAdd)
+        hipLaunchKernelGGL((k_boxc_mv8<kBoxChebFirstAdd, S>), grid, dim3(kCThreads), 0, s, g, A.window, ct, cm, X, Y,
+                           (const double *)nullptr, Bv, omega, gamma);
       else if (epi == kBoxChebSecond)
         hipLaunchKernelGGL((k_boxc_mv8<kBoxChebSecond, S>), grid, dim3(kCThreads), 0, s, g, A.window, ct, cm, X, Y,
                            (const double *)nullptr, Bv, omega, gamma);
@@ -794,6 +831,8 @@ static bool launch_box(const eig_mat_s &A, i64 m, const double *X, double *Y, co
       go(std::integral_constant<unsigned, kShape7>{});
     else if (A.box_geomask && shape == kShapeKuhn && A.sym_nd == 15)
       go(std::integral_constant<unsigned, kShapeKuhn>{});
+    else if (A.box_geomask && shape == kShape27 && A.sym_nd == 27)
+      go(std::integral_constant<unsigned, kShape27>{});
     else
       go(std::integral_constant<unsigned, 0u>{});
     EIG_HIP(hipGetLastError());
@@ -874,6 +913,13 @@ bool launch_box_cheb_first(const eig_mat_s &M, i64 m, const double *B, double om
                            hipStream_t s)
 {
   return launch_box(M, m, B, Y, nullptr, B, nullptr, omega, gamma, kBoxChebFirst, s);
+}
+
+// Y += x_2 of the degree-2 solve from B (the same x_2 as launch_box_cheb_first, added in place).
+bool launch_box_cheb_first_add(const eig_mat_s &M, i64 m, const double *B, double omega, double gamma, double *Y,
+                               hipStream_t s)
+{
+  return launch_box(M, m, B, Y, nullptr, B, nullptr, omega, gamma, kBoxChebFirstAdd, s);
 }
 
 // The second step, x_3 from x_2 = X2 and x_1 = gamma D^-1 B (formed per row, not read): Y = x_3.

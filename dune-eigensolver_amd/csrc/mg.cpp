@@ -253,11 +253,15 @@ double *vcycle(eig_mg_s &mg, size_t l, i64 m, const double *b)
   const double *xc = vcycle(mg, l + 1, m, Cl.B->d());
   launch_mg_prolong_add(L.dim, Cl.dim, m, L.n, Cl.n, xc, x, s);
   launch_resid_mv8(*L.A, m, x, b, T, s);  // T = b - A x
+  // x += post-smoothing correction: a degree-2 smoother on the row-class image adds its x_2 in
+  // place (cheb_solve's first step, its gamma and omega_1)
+  const double gamma = 2.0 / (lo + hi), mu = (hi - lo) / (hi + lo);
+  if (mg.nu == 2 && launch_box_cheb_first_add(*L.A, m, T, 1.0 / (1.0 - 0.5 * mu * mu), gamma, x, s)) return x;
   double *q[3];
   for (int i = 0, j = 0; i < 4; ++i)
     if (C[i] != x) q[j++] = C[i];
   const double *p = cheb_solve(*L.A, m, mg.nu, lo, hi, T, L.dinv->d(), q[0], q[1], q[2], s);
-  launch_mv8_axpby(L.n, m, L.n, 1.0, p, 1.0, x, s);  // x += post-smoothing correction
+  launch_mv8_axpby(L.n, m, L.n, 1.0, p, 1.0, x, s);
   return x;
 }
 

@@ -372,7 +372,8 @@ _P7 = {(0, 0, 0): 6.0, (1, 0, 0): -1.0, (-1, 0, 0): -1.0, (0, 1, 0): -1.0, (0, -
        (0, 0, 1): -1.0, (0, 0, -1): -1.0}
 
 
-@pytest.mark.parametrize("kind,var", [("hole", False), ("nine", False), ("hole", True), ("nine", True)])
+@pytest.mark.parametrize("kind,var", [("hole", False), ("nine", False), ("hole", True), ("nine", True),
+                                      ("full27", False)])
 def test_boxc_runtime_offsets(ctx, kind, var):
     """The row-class kernels take the compile-time stencil (7-point, Kuhn 15-point: no masks, every
     offset summed with the zero class entries) only when every offset a class does not store points
@@ -381,6 +382,9 @@ def test_boxc_runtime_offsets(ctx, kind, var):
     var: two rows leave their class -- the box-image kernel (k_box_mv32), same rule.  All bitwise
     the reference SpMM; the Chebyshev step equal to the SELL kernel to rounding."""
     st = dict(_P7)
+    if kind == "full27":  # every box offset (a Galerkin coarse operator's shape): compile-time 27-point
+        st = {(a, b, c): (-0.05 if (a, b, c) != (0, 0, 0) else 2.0) for a in (-1, 0, 1) for b in (-1, 0, 1)
+              for c in (-1, 0, 1)}
     if kind == "nine":
         st[(0, 1, 1)] = st[(0, -1, -1)] = -0.25
         st[(0, 0, 0)] = 6.5

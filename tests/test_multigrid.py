@@ -51,7 +51,8 @@ def test_mg_ref_hierarchy_is_symmetric_galerkin():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("kind,N,m", [("p1", 12, 8), ("p1", 24, 32), ("poisson7", 20, 16), ("p1", 17, 8),
-                                      ("p1var", 24, 32), ("p1var", 18, 24)])
+                                      ("p1var", 24, 32), ("p1var", 18, 24),
+                                      ("p1", 32, 16)])  # 32: the 16^3 Galerkin level on the 27-point class kernel
 def test_mg_solve_matches_restatement(ctx, kind, N, m):
     """p1var: K + a random positive diagonal -- rows no longer equal their geometric class, so the
     fine level runs the box-image kernels (k_box_mv32) instead of the row-class ones."""
