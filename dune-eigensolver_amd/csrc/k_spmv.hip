@@ -1153,7 +1153,7 @@ __global__ __launch_bounds__(kStreamThreads, 7) void k_lanczos_fused_march(
     march_rows<MT, 2, SPAN1>(A, mp, own, lane, wave, XPair{P, c}, epi);
   }
   double v[3] = {d, q2, m2};
-  if (grid_sum<3, kStreamThreads>(v, partials, ticket, tot))
+  if (grid_sum<3, kStreamThreads, 8>(v, partials, ticket, tot))
   {
     if (threadIdx.x < 3) out[threadIdx.x] = tot[threadIdx.x];
   }
@@ -1604,9 +1604,11 @@ static MarchPlan march_plan(const eig_mat_s &A, int mode, i64 zb = 0, i64 ze = -
   //    4: 267.3); one rank's 256^2 x 32 slab 2 runs 33.7 us (4: 35.5, 7: 36.7, 1: 47.3); the 16-plane
   //    slab 2 runs 21.7 us (1: 28.3, 4: 23.9, 7: 26.2)  ->  nplanes / 32 runs, at least 2, at most 8
   //  * narrower planes (128^3: 256 columns): 12 runs 34.9 us (16: 35.5, 28: 36.5, 32: 36.7)  ->
-  //    runs of >= 10 planes
+  //    runs of >= 10 planes, as long as that leaves a quarter of the resident slots busy (64^3, 64
+  //    columns: 6 runs of 10 planes took 20.1 us, 64 runs of one plane 13.3)
   if (fused && ncol >= 1024) nseg = std::min<i64>(nplanes / 2 > 0 ? nplanes / 2 : 1, std::max<i64>(2, std::min<i64>(8, nplanes / 32)));
-  else if (fused) nseg = std::max<i64>(1, std::min<i64>(nseg, nplanes / 10));
+  else if (fused)
+    nseg = std::min(nseg, std::max<i64>({1, nplanes / 10, (resident / 4 + ncol - 1) / ncol}));
   if (A.tune_march_runs > 0) nseg = std::min<i64>(A.tune_march_runs, nplanes);  // eig_mat_tune
   while (nseg > 1 && (ncol * nseg + kWaves - 1) / kWaves > kMaxRedBlocks) --nseg;
   if ((ncol * nseg + kWaves - 1) / kWaves > kMaxRedBlocks) return mp;

@@ -80,19 +80,21 @@ __device__ __forceinline__ void block_sum(double (&v)[NV], double (&out)[NV])
 
 // Grid-wide sum.  Returns true in every thread of the LAST workgroup; there tot[0..NV) (LDS,
 // visible to all its threads) holds the grid totals.  partials: >= gridDim.x*NV doubles.
-template <int NV, int NT>
+// U: partials per thread and value loaded in one round of the last workgroup's sum (a kernel with
+// registers to spare passes 8: the fused march step's 2048 x 3 partials in one round)
+template <int NV, int NT, int U = (NV <= 2 ? 8 : 2)>
 __device__ bool grid_sum_n(double (&v)[NV], double *partials, unsigned *ticket, double *tot, unsigned bid,
                            unsigned nblk);
 
-template <int NV, int NT>
+template <int NV, int NT, int U = (NV <= 2 ? 8 : 2)>
 __device__ __forceinline__ bool grid_sum(double (&v)[NV], double *partials, unsigned *ticket, double *tot)
 {
-  return grid_sum_n<NV, NT>(v, partials, ticket, tot, blockIdx.x, gridDim.x);
+  return grid_sum_n<NV, NT, U>(v, partials, ticket, tot, blockIdx.x, gridDim.x);
 }
 
 // Same with an explicit reduction group: `nblk` workgroups with ids `bid` share one ticket and
 // partials[0 .. nblk*NV) (used by 2-D grids that run several independent reductions).
-template <int NV, int NT>
+template <int NV, int NT, int U>
 __device__ bool grid_sum_n(double (&v)[NV], double *partials, unsigned *ticket, double *tot, unsigned bid,
                            unsigned nblk)
 {
@@ -115,7 +117,6 @@ __device__ bool grid_sum_n(double (&v)[NV], double *partials, unsigned *ticket, 
   double acc[NV];
 #pragma unroll
   for (int i = 0; i < NV; ++i) acc[i] = 0.0;
-  constexpr int U = NV <= 2 ? 8 : 2;
   for (unsigned b0 = threadIdx.x; b0 < nblk; b0 += NT * U)
   {
     double vals[U][NV];

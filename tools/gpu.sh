@@ -81,7 +81,7 @@ run_task() {
       sweep --N 256 --variants fused,fused@8,fused@7,fused@6,fused@4,mv,mv@7 && \
       sweep --N 256 --slab 32 --variants fused,fused@1,fused@4,fused@7,mv && \
       sweep --N 256 --slab 16 --variants fused,fused@2,fused@4,fused@7,mv && \
-      sweep --N 64 --variants fused,mv ;;
+      sweep --N 64 --variants fused,fused@64,fused@32,fused@16,mv ;;
     pipe)
       timeout -k 10 200 python -u tools/lanczos_sweep.py --slab 32 --variants fused,pipelined,mv --rounds 5 > "$O/pipe.jsonl" 2>&1 && \
       timeout -k 10 200 python -u tools/lanczos_sweep.py --variants fused,pipelined,mv --rounds 3 >> "$O/pipe.jsonl" 2>&1 ;;
