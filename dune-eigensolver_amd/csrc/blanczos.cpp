@@ -37,6 +37,7 @@ struct eig_blanczos_s {
   DevBuf *W = nullptr, *Xa = nullptr, *Xb = nullptr, *Xc = nullptr, *MZ = nullptr;  // b columns each
   DevBuf *dinv = nullptr;                // 1 / diag(M), owned rows
   DevBuf *small = nullptr;               // Gram / coefficient panels
+  DevBuf *chol = nullptr;                // CholQR on the device: R, Rtot (b x b each) and a flag
   std::vector<double> A, B;              // host: A_j (b x b), B_{j+1} (b x b, upper) per step
   ~eig_blanczos_s()
   {
@@ -48,6 +49,7 @@ struct eig_blanczos_s {
     delete MZ;
     delete dinv;
     delete small;
+    delete chol;
   }
 };
 
@@ -138,7 +140,9 @@ namespace {
 double *dptr(DevBuf *b) { return b->d(); }
 
 // Z (b columns) = Vdst R with Vdst M-orthonormal (CholQR twice); R (b x b upper, row-major) on
-// the host.  Vdst may equal Z.
+// the host.  Vdst may equal Z.  The b x b factorisations run on the device (k_chol_small: the host
+// chol_upper / tri_upper_inv arithmetic), so the two passes queue without a host round trip; one
+// synchronisation at the end brings R and the breakdown flag back.
 void mcholqr2(eig_blanczos_s &w, double *Z, double *Vdst, std::vector<double> &Rtot)
 {
   eig_mat_s &M = *w.M;
@@ -148,9 +152,9 @@ void mcholqr2(eig_blanczos_s &w, double *Z, double *Vdst, std::vector<double> &R
   const i64 n = w.n, ld = w.ld, own = w.own;
   double *Gd = w.small->d();
   double *Sd = Gd + (size_t)b * b;
-  std::vector<double> G((size_t)b * b), R((size_t)b * b), Ri((size_t)b * b), T((size_t)b * b);
-  Rtot.assign((size_t)b * b, 0.0);
-  for (int i = 0; i < b; ++i) Rtot[(size_t)i * b + i] = 1.0;
+  double *Rd = w.chol->d(), *Rt = Rd + (size_t)b * b;
+  int *flag = reinterpret_cast<int *>(Rt + (size_t)b * b);
+  EIG_HIP(hipMemsetAsync(flag, 0, sizeof(int), s));
   for (int pass = 0; pass < 2; ++pass)
   {
     // pass 1 reuses M Z: the first pass updated it with the same triangular factor as Z (row-local,
@@ -162,27 +166,17 @@ void mcholqr2(eig_blanczos_s &w, double *Z, double *Vdst, std::vector<double> &R
     }
     launch_panel_gram(ctx, n, ld, b, b, Z + own * 8, dptr(w.MZ) + own * 8, Gd, s);
     allreduce_sum(ctx, Gd, (i64)b * b, s);
-    EIG_HIP(hipMemcpyAsync(G.data(), Gd, G.size() * sizeof(double), hipMemcpyDeviceToHost, s));
-    EIG_HIP(hipStreamSynchronize(s));
-    for (int i = 0; i < b; ++i)
-      for (int j = i + 1; j < b; ++j) G[(size_t)i * b + j] = G[(size_t)j * b + i] = 0.5 * (G[(size_t)i * b + j] + G[(size_t)j * b + i]);
-    EIG_CHECK(chol_upper(b, G.data(), R.data()), EIG_ERR_BREAKDOWN,
-              "block Lanczos: M-Gram of the new block is not positive definite (Krylov space exhausted)");
-    tri_upper_inv(b, R.data(), Ri.data());
-    EIG_HIP(hipMemcpyAsync(Sd, Ri.data(), Ri.size() * sizeof(double), hipMemcpyHostToDevice, s));
+    launch_chol_small(b, pass, Gd, Rd, Sd, Rt, flag, s);  // Sd = R^-1, Rt <- R Rt
     launch_panel_update(n, ld, ld, b, b, Z + own * 8, Sd, 1.0, 0.0, (pass == 1 ? Vdst : Z) + own * 8, s);
     if (pass == 0) launch_panel_update(n, ld, ld, b, b, dptr(w.MZ) + own * 8, Sd, 1.0, 0.0, dptr(w.MZ) + own * 8, s);
-    // Rtot <- R Rtot
-    for (int i = 0; i < b; ++i)
-      for (int j = 0; j < b; ++j)
-      {
-        double acc = 0.0;
-        for (int q = i; q <= j; ++q) acc += R[(size_t)i * b + q] * Rtot[(size_t)q * b + j];
-        T[(size_t)i * b + j] = acc;
-      }
-    Rtot = T;
-    EIG_HIP(hipStreamSynchronize(s));  // Ri's host buffer is reused next pass
   }
+  Rtot.assign((size_t)b * b, 0.0);
+  int hflag = 0;
+  EIG_HIP(hipMemcpyAsync(Rtot.data(), Rt, Rtot.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+  EIG_HIP(hipMemcpyAsync(&hflag, flag, sizeof(int), hipMemcpyDeviceToHost, s));
+  EIG_HIP(hipStreamSynchronize(s));
+  EIG_CHECK(!hflag, EIG_ERR_BREAKDOWN,
+            "block Lanczos: M-Gram of the new block is not positive definite (Krylov space exhausted)");
 }
 
 void check_pair(const eig_mat_s *K, const eig_mat_s *M)
@@ -240,6 +234,7 @@ void blanczos_create(eig_mat_t K, eig_mat_t M, eig_mat_t Ks, double sigma, int b
       w->MZ = new DevBuf(blk);
       w->dinv = new DevBuf((size_t)std::max<i64>(w->n, 1) * sizeof(double));
       w->small = new DevBuf((size_t)(max_steps + 2) * block * block * sizeof(double) * 2);
+      w->chol = new DevBuf((size_t)2 * block * block * sizeof(double) + 64);
       EIG_HIP(hipMemsetAsync(w->V->d(), 0, w->V->bytes(), s));
       for (DevBuf *d : {w->W, w->Xa, w->Xb, w->MZ}) EIG_HIP(hipMemsetAsync(d->d(), 0, d->bytes(), s));
       launch_diag_inv(Ks ? *Ks : *M, w->dinv->d(), s);

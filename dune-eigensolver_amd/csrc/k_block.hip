@@ -716,6 +716,89 @@ __global__ __launch_bounds__(256) void k_panel_update(i64 n, i64 ldq, i64 ldy, i
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// CholQR's small factorisation on the device (block Lanczos, blanczos.cpp mcholqr2): one workgroup
+// takes the b x b M-Gram G (b <= 32), symmetrises it, factors G = R^T R (upper R), inverts R and
+// folds R into the running product Rtot <- R Rtot (pass 0: Rtot = I).  The same operations in the
+// same order as the host chol_upper / tri_upper_inv (dense.cpp) and mcholqr2's product -- each
+// entry's sum sequential in one thread, correctly rounded sqrt and division, no contraction -- so
+// the factors are the host's bit for bit.  A non-positive pivot sets *flag (the caller reports
+// EIG_ERR_BREAKDOWN at its next synchronisation).  Row-major b x b everywhere.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_chol_small(int b, int pass, const double *__restrict__ G, double *R,
+                                                    double *Ri, double *Rtot, int *flag)
+{
+  __shared__ double g[32][32], r[32][32], ri[32][32], rt[32][32];
+  const int t = threadIdx.x;
+  for (int e = t; e < b * b; e += 256)
+  {
+    const int i = e / b, j = e % b;
+    g[i][j] = G[e];
+    r[i][j] = 0.0;
+    ri[i][j] = 0.0;
+    rt[i][j] = pass == 0 ? (i == j ? 1.0 : 0.0) : Rtot[e];
+  }
+  __syncthreads();
+  for (int e = t; e < b * b; e += 256)
+  {
+    const int i = e / b, j = e % b;
+    if (i < j)  // (each pair read and written by its i < j thread only)
+    {
+      const double v = 0.5 * (g[i][j] + g[j][i]);
+      g[i][j] = v;
+      g[j][i] = v;
+    }
+  }
+  __syncthreads();
+  for (int j = 0; j < b; ++j)
+  {
+    if (t == 0)
+    {
+      double s = g[j][j];
+      for (int k = 0; k < j; ++k) s -= r[k][j] * r[k][j];
+      if (!(s > 0.0)) *flag = 1;
+      r[j][j] = sqrt(s);
+    }
+    __syncthreads();
+    const double rjj = r[j][j];
+    for (int i = j + 1 + t; i < b; i += 256)
+    {
+      double u = g[j][i];
+      for (int k = 0; k < j; ++k) u -= r[k][j] * r[k][i];
+      r[j][i] = u / rjj;
+    }
+    __syncthreads();
+  }
+  if (t < b)  // column c = t of R^-1, back substitution
+  {
+    const int c = t;
+    for (int i = c; i >= 0; --i)
+    {
+      double s = (i == c) ? 1.0 : 0.0;
+      for (int k = i + 1; k <= c; ++k) s -= r[i][k] * ri[k][c];
+      ri[i][c] = s / r[i][i];
+    }
+  }
+  __syncthreads();
+  for (int e = t; e < b * b; e += 256)
+  {
+    const int i = e / b, j = e % b;
+    double acc = 0.0;
+    for (int q = i; q <= j; ++q) acc += r[i][q] * rt[q][j];
+    R[e] = r[i][j];
+    Ri[e] = ri[i][j];
+    Rtot[e] = acc;
+  }
+}
+
+void launch_chol_small(int b, int pass, const double *G, double *R, double *Ri, double *Rtot, int *flag,
+                       hipStream_t s)
+{
+  EIG_CHECK(b >= 1 && b <= 32, EIG_ERR_ARG, "chol_small: b <= 32");
+  hipLaunchKernelGGL(k_chol_small, dim3(1), dim3(256), 0, s, b, pass, G, R, Ri, Rtot, flag);
+  EIG_HIP(hipGetLastError());
+}
+
 void launch_panel_update(i64 n, i64 ldq, i64 ldy, i64 m1, i64 m2, const double *Q, const double *S, double alpha,
                          double beta, double *Y, hipStream_t s)
 {
