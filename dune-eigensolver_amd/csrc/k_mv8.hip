@@ -167,8 +167,7 @@ __global__ __launch_bounds__(kGramThreads) void k_gram_mv8(i64 n, i64 ld1, i64 l
   constexpr int E = T1 * T2 * TE;
   constexpr int W = kGramThreads / 64;
   constexpr int RG = DR ? 8 : 4;     // rows per group (one MFMA per unit pair)
-  __shared__ double sh[W][E];
-  __shared__ double tot[E];
+  __shared__ double red[E];  // the workgroup's sum of its waves' tiles, then the grid total
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   // 1-D grid of gx * ny workgroups (gx a multiple of 8), XCD-aware: workgroups are dealt round-robin
   // over the 8 XCDs, so b, b + 8, b + 16, ... share an XCD; they take the ny output chunks of ONE row
@@ -230,47 +229,51 @@ __global__ __launch_bounds__(kGramThreads) void k_gram_mv8(i64 n, i64 ld1, i64 l
         for (int u = 0; u < T2; ++u)
           acc[t][u] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[v][t], bv[v][u], acc[t][u], 0, 0, 0);
   }
-  // lane holds C[k + 4q][i] of each tile
-#pragma unroll
-  for (int t = 0; t < T1; ++t)
-#pragma unroll
-    for (int u = 0; u < T2; ++u)
-    {
-      if constexpr (DR)
-      {
-        // for i < 8, q < 2: C[k + 4q][i] + C[k + 4q + 8][i + 8] (lane + 8, register q + 2)
-#pragma unroll
-        for (int q = 0; q < 2; ++q)
-        {
-          const double hi = __shfl_down(acc[t][u][q + 2], 8, 64);
-          if (i < 8) sh[wave][(t * T2 + u) * 64 + (k + 4 * q) * 8 + i] = acc[t][u][q] + hi;
-        }
-      }
-      else
-      {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) sh[wave][(t * T2 + u) * 256 + (k + 4 * q) * 16 + i] = acc[t][u][q];
-      }
-    }
-  __syncthreads();
-  for (int e = threadIdx.x; e < E; e += kGramThreads)
+  // lane holds C[k + 4q][i] of each tile.  The waves add their tiles into one LDS image in wave
+  // order (((w0 + w1) + w2) + w3: a fixed order, E doubles of LDS instead of W E)
+  for (int w = 0; w < W; ++w)
   {
-    double v = sh[0][e];
+    if (wave == w)
+    {
 #pragma unroll
-    for (int w = 1; w < W; ++w) v += sh[w][e];
-    tot[e] = v;
+      for (int t = 0; t < T1; ++t)
+#pragma unroll
+        for (int u = 0; u < T2; ++u)
+        {
+          if constexpr (DR)
+          {
+            // for i < 8, q < 2: C[k + 4q][i] + C[k + 4q + 8][i + 8] (lane + 8, register q + 2)
+#pragma unroll
+            for (int q = 0; q < 2; ++q)
+            {
+              const double hi = __shfl_down(acc[t][u][q + 2], 8, 64);
+              const int e = (t * T2 + u) * 64 + (k + 4 * q) * 8 + i;
+              if (i < 8) red[e] = w == 0 ? acc[t][u][q] + hi : red[e] + (acc[t][u][q] + hi);
+            }
+          }
+          else
+          {
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+            {
+              const int e = (t * T2 + u) * 256 + (k + 4 * q) * 16 + i;
+              red[e] = w == 0 ? acc[t][u][q] : red[e] + acc[t][u][q];
+            }
+          }
+        }
+    }
+    __syncthreads();
   }
-  __syncthreads();
   double *part = partials + (size_t)cy * gxw * E;
   double *spart = partials + (size_t)ny * gxw * E + (size_t)cy * 8 * E;
-  if (!grid_sum2<kGramThreads>(tot, E, part, spart, tickets + (size_t)cy * kTicketStride, bx, gxw, sh[0])) return;
+  if (!grid_sum2<kGramThreads>(red, E, part, spart, tickets + (size_t)cy * kTicketStride, bx, gxw, red)) return;
   const i64 m1 = (i64)nb1 * 8, m2 = (i64)nb2 * 8;
   for (int e = threadIdx.x; e < E; e += kGramThreads)
   {
     const int tu = e / TE, t = tu / T2, u = tu % T2, el = e % TE;
     const int TW = DR ? 8 : 16;  // tile width in G
     const i64 row = (i64)(cy1 * T1 + t) * TW + el / TW, col = (i64)(cy2 * T2 + u) * TW + el % TW;
-    if (row < m1 && col < m2) G[row * m2 + col] = sh[0][e];
+    if (row < m1 && col < m2) G[row * m2 + col] = red[e];
   }
 }
 
