@@ -562,6 +562,7 @@ extern "C" int eig_mass_solve_mv8(eig_mat_t M, int64_t m, int degree, double lmi
               "eig_mass_solve_mv8: bad argument");
     EIG_CHECK(M->br == 1 && M->bc == 1 && M->nb_rows_global == M->nb_cols, EIG_ERR_BLOCKSIZE,
               "eig_mass_solve_mv8: square FieldMatrix<double,1,1> only");
+    EIG_CHECK(X != B, EIG_ERR_ARG, "eig_mass_solve_mv8: X must not alias B (B is read by every step)");
     eig_ctx_t ctx = M->ctx;
     EIG_HIP(hipSetDevice(ctx->device));
     hipStream_t s = ctx->stream;

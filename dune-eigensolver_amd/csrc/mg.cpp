@@ -385,6 +385,7 @@ extern "C" int eig_mg_solve(eig_mg_t mg, int64_t m, const double *B, double *X, 
 {
   return guard(mg ? mg->ctx : nullptr, [&] {
     EIG_CHECK(mg && B && X, EIG_ERR_ARG, "eig_mg_solve: null argument");
+    EIG_CHECK(X != B, EIG_ERR_ARG, "eig_mg_solve: X must not alias B");
     eig_ctx_t ctx = mg->ctx;
     EIG_HIP(hipSetDevice(ctx->device));
     hipStream_t s = ctx->stream;

@@ -510,7 +510,8 @@ int eig_blanczos_ritz(eig_blanczos_t ws, int nev, int which, double *eval_host, 
 /* The block tridiagonal T (dim = steps * block; T_host dim x dim row-major, or NULL for the size). */
 int eig_blanczos_tmatrix(eig_blanczos_t ws, int *dim, double *T_host);
 int eig_blanczos_destroy(eig_blanczos_t ws);
-/* X = M^-1 B for m columns (window layout) by `degree` Chebyshev-Jacobi steps (the operator's solve). */
+/* X = M^-1 B for m columns (window layout) by `degree` Chebyshev-Jacobi steps (the operator's solve);
+ * X must not alias B (EIG_ERR_ARG). */
 int eig_mass_solve_mv8(eig_mat_t M, int64_t m, int degree, double lmin, double lmax, const double *B, double *X);
 /* Tall-skinny panel kernels on n-row MultiVector<double,8> buffers (single rank):
  * Y = beta Y + alpha Q S (Q n x m1, S m1 x m2 row-major device, m2 in {8,16,24,32}; Y may be Q), and

@@ -138,3 +138,17 @@ def test_shift_invert_smallest_p1_multigrid(ctx):
         assert np.linalg.norm(r) <= 1e-5 * lam * np.linalg.norm(M @ y)
     bl.close()
     mg.close()
+
+
+@pytest.mark.gpu
+def test_solves_reject_aliased_output(ctx):
+    """The multigrid and mass solves read B in every iteration / step: X == B is refused."""
+    K, M = oracle.p1_kuhn(6)
+    dK, dM = _upload(ctx, K), _upload(ctx, M)
+    mg = eigmi.Multigrid(dK, (6, 6, 6), max_cols=8)
+    B = _mv(ctx, np.ones((K.shape[0], 8)))
+    with pytest.raises(eigmi.EigError):
+        mg.solve(8, B, B, 2)
+    with pytest.raises(eigmi.EigError):
+        eigmi.mass_solve_mv8(dM, 8, 4, B, B)
+    mg.close()
