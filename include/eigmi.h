@@ -495,7 +495,7 @@ int eig_mg_info(eig_mg_t mg, int *levels, int64_t *coarse_rows, int *coarse_degr
 /* X = S B, m columns (window layout = plain MultiVector<double,8> on one rank), S = `cycles`
  * stationary iterations x += V (b - A x) from x = 0 with V one symmetric V-cycle: a fixed symmetric
  * linear operator (no inner products inside).  resid_host (or NULL): max over the columns of
- * ||B - A X|| / ||B|| afterwards (a measurement; synchronous either way). */
+ * ||B - A X|| / ||B|| afterwards (a measurement; synchronous either way).  X must not alias B. */
 int eig_mg_solve(eig_mg_t mg, int64_t m, const double *B, double *X, int cycles, double *resid_host);
 int eig_mg_destroy(eig_mg_t mg);
 /* eig_blanczos_create_si with the Ks solve by `cycles` multigrid iterations (mg built on Ks with
