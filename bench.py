@@ -224,7 +224,7 @@ def main():
     variant = args.variant
     trial = None
     if variant == "auto":
-        # one rank: EIG_LANCZOS_AUTO's choice for this image (fused where the pair gathers hit cache)
+        # one rank: EIG_LANCZOS_AUTO's choice for this image (the fused step on a 1x1 image)
         tw = eigmi.LanczosWorkspace(M, 1, seed=123, fused="auto")
         variant = tw.variant
         tw.close()

@@ -822,8 +822,15 @@ __device__ __forceinline__ void fused_row_stencil(const SellB1 &A, i64 s, const 
 
 // Register budget for 8 waves / SIMD (W): stencil rows take 4 entries per round to fit 64 VGPRs
 // (measured: 5 waves with 8 entries per round and 6 waves were no faster).
+// (explicit-column and mixed images: 6 waves / SIMD; at 8 their row loops spill 36 / 46 VGPRs to
+// scratch, whose write-back is the write traffic PMC showed beyond the pair stores)
+template <int MODE>
+constexpr int fused_b1_waves()
+{
+  return (MODE == kExplicit || MODE == kMixed) ? 6 : 8;
+}
 template <int R, int MODE>
-__global__ __launch_bounds__(kStreamThreads, 8) void k_lanczos_fused_b1(
+__global__ __launch_bounds__(kStreamThreads, fused_b1_waves<MODE>()) void k_lanczos_fused_b1(
     i64 nrows, i64 own, SellB1 A, const i32 *__restrict__ slices, i64 first, i64 count,
     const dpair *__restrict__ P, dpair *__restrict__ Pout, FusedArgs fa, double *__restrict__ out,
     const double *__restrict__ carry, double *partials, unsigned *ticket)
@@ -1928,12 +1935,12 @@ void lanczos_kernel_info(const eig_mat_s &A, bool fused, std::string &name, i64 
   }
 }
 
-bool fused_step_pays(const eig_mat_s &A)
-{
-  if (A.br != 1 || A.bc != 1) return false;
-  const int mode = image_mode(A);
-  return is_sym_mode(mode) || 2 * A.n_stencil_slices >= A.nslices;
-}
+// EIG_LANCZOS_AUTO: the fused step on every 1x1 image.  (Round 3 took the two-kernel step on
+// scattered images while k_lanczos_fused_b1 spilled 36-46 VGPRs there -- 634 vs 427 us on the
+// scrambled + RCM 256^3 Poisson, the spill write-back being the 3.5x write excess PMC showed; at 6
+// waves / SIMD without the spills it runs 408 us, step 415 vs 436 us, PMC 0.97x of the CSR bytes:
+// profiles/r03ah_csr*.)
+bool fused_step_pays(const eig_mat_s &A) { return A.br == 1 && A.bc == 1; }
 
 std::string kernel_for(const eig_mat_s &A, int op)
 {

@@ -539,7 +539,7 @@ def standard_largest(A, shift, tol, maxiter, nev, seed=123, want_evec=True, verb
 
 
 def _lflags(fused, pipelined):
-    """fused: True / False / "auto" (EIG_LANCZOS_AUTO: fused where the image makes it pay)."""
+    """fused: True / False / "auto" (EIG_LANCZOS_AUTO: fused on every 1x1 image)."""
     if pipelined:
         return LANCZOS_PIPELINED
     return LANCZOS_AUTO if fused == "auto" else LANCZOS_FUSED if fused else 0

@@ -288,11 +288,10 @@ enum eig_lanczos_flags {
    * communicator, its own stream) overlaps the SpMV and the halo of t (8 B per row, not 16).
    * Costs 56 B per row more than the fused step on one GPU.  Exclusive with EIG_LANCZOS_FUSED. */
   EIG_LANCZOS_PIPELINED = 8,
-  /* Pick per matrix image at creation: EIG_LANCZOS_FUSED where its pair gathers are cache hits (the
-   * symmetric band image, or a stencil-sliced SELL image), else the two-kernel step (a scattered
-   * general matrix: the fused step gathers 16-B (t, u) pairs at every column, twice the classic
-   * step's gather bytes -- 634 vs 427 us per step at 256^3 scrambled + RCM).
-   * eig_lanczos_ws_info reports the choice. */
+  /* Pick per matrix at creation: EIG_LANCZOS_FUSED for every 1x1 (scalar) matrix image -- band,
+   * stencil or scattered (256^3 scrambled + RCM: 415 us per fused step vs 436 for the two-kernel
+   * step) -- the two-kernel step for blocked images.  eig_lanczos_ws_info reports the
+   * choice. */
   EIG_LANCZOS_AUTO = 16
 };
 int eig_lanczos_run(eig_mat_t A, int steps, const double *u0, unsigned seed, int flags,

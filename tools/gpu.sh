@@ -19,6 +19,7 @@
 #   latency              fused step vs eig_mv across sizes and slabs, plane-run counts  -> latency.jsonl
 #   pipe                 fused vs pipelined on one rank's slab and the cube   -> pipe.jsonl
 #   csr                  general (scrambled + RCM) 256^3 matrix: SpMV / Lanczos kernels  -> csr.jsonl
+#   csrpmc               the same under a kernel trace and FETCH_SIZE / WRITE_SIZE passes -> csrpmc/
 #   commself             bench.py with and without a one-rank RCCL allreduce per step (eager / graph, 128^3 / 256^3)
 set -o pipefail
 TAG=${TAG:-scratch}
@@ -94,6 +95,15 @@ run_task() {
       done ;;
     csr)
       timeout -k 10 400 python -u tools/csr_general.py > "$O/csr.jsonl" 2> "$O/csr.err" ;;
+    csrpmc)
+      # the general-matrix kernels under a kernel trace and FETCH_SIZE / WRITE_SIZE passes
+      prof_env
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/csrpmc/trace" -o trace -- \
+        python3 tools/csr_general.py --reps 10 --steps 20 > "$O/csrpmc.jsonl" 2> "$O/csrpmc_t.err" && \
+      timeout -s KILL 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/csrpmc/fetch" -o pmc -- \
+        python3 tools/csr_general.py --reps 10 --steps 20 > /dev/null 2> "$O/csrpmc_f.err" && \
+      timeout -s KILL 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/csrpmc/write" -o pmc -- \
+        python3 tools/csr_general.py --reps 10 --steps 20 > /dev/null 2> "$O/csrpmc_w.err" ;;
     *)
       echo "unknown task $1" >&2; return 2 ;;
   esac
