@@ -823,11 +823,13 @@ __device__ __forceinline__ void fused_row_stencil(const SellB1 &A, i64 s, const 
 // Register budget for 8 waves / SIMD (W): stencil rows take 4 entries per round to fit 64 VGPRs
 // (measured: 5 waves with 8 entries per round and 6 waves were no faster).
 // (explicit-column and mixed images: 6 waves / SIMD; at 8 their row loops spill 36 / 46 VGPRs to
-// scratch, whose write-back is the write traffic PMC showed beyond the pair stores)
+// scratch, whose write-back is the write traffic PMC showed beyond the pair stores.  Stencil
+// images: 7 (at 8: 20 B of scratch per lane; 3-D Poisson 256^3 on the SELL stencil image 353.2 ->
+// 333.3 us, tools/stencil_fused.py)
 template <int MODE>
 constexpr int fused_b1_waves()
 {
-  return (MODE == kExplicit || MODE == kMixed) ? 6 : 8;
+  return (MODE == kExplicit || MODE == kMixed) ? 6 : MODE == kStencil ? 7 : 8;
 }
 template <int R, int MODE>
 __global__ __launch_bounds__(kStreamThreads, fused_b1_waves<MODE>()) void k_lanczos_fused_b1(
