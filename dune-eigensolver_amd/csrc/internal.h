@@ -302,6 +302,8 @@ bool launch_box_cheb(const eig_mat_s &M, i64 m, const double *Xk, double *Xold, 
                      double omega, double gamma, hipStream_t s, double *Xnew = nullptr);
 void box_invalidate(eig_mat_s &A);
 bool launch_box_resid(const eig_mat_s &A, i64 m, const double *X, const double *B, double *R, hipStream_t s);
+bool launch_box_resid_acc(const eig_mat_s &A, i64 m, const double *E, const double *B, double *R, double *Xacc,
+                          bool copy, hipStream_t s);
 bool launch_box_cheb_first(const eig_mat_s &M, i64 m, const double *B, double omega, double gamma, double *Y,
                            hipStream_t s);
 bool launch_box_cheb_first_add(const eig_mat_s &M, i64 m, const double *B, double omega, double gamma, double *Y,

@@ -35,7 +35,18 @@ constexpr int kBoxRounds = (kBoxChunks + kBoxThreads - 1) / kBoxThreads;
 // never stored: two vector passes less per solve)
 // kBoxChebFirstAdd: kBoxChebFirst added into Y (Y += x_2: a degree-2 smoother's correction applied
 // in place, the multigrid post-smoother)
-enum { kBoxStore = 0, kBoxCheb = 1, kBoxResid = 2, kBoxChebFirst = 3, kBoxChebSecond = 4, kBoxChebFirstAdd = 5 };
+// kBoxResidCopy / kBoxResidAcc: kBoxResid that also sets / adds the input block into a second
+// output (Xold's slot): the multigrid outer iteration's X = E or X += E beside r = b - A E
+enum {
+  kBoxStore = 0,
+  kBoxCheb = 1,
+  kBoxResid = 2,
+  kBoxChebFirst = 3,
+  kBoxChebSecond = 4,
+  kBoxChebFirstAdd = 5,
+  kBoxResidCopy = 6,
+  kBoxResidAcc = 7
+};
 constexpr int kBoxMaxNd = 15;  // offsets of the box-image kernel's LDS value tile (P1 Kuhn: 15, 7-point: 7)
 constexpr int kBoxClassMaxNd = 27;  // offsets of the row-class kernels (27: Galerkin coarse operators)
 
@@ -554,8 +565,21 @@ __global__ __launch_bounds__(kCThreads, 8) void k_boxc_mv8(BoxGeom g, i64 ld, co
       const i64 r = (i64)x + (i64)g.nx * y + (i64)g.P * z;
       if (EPI == kBoxStore)
         __builtin_nontemporal_store(acc, Yb + r * 4 + cp);
-      else if (EPI == kBoxResid)
+      else if (EPI == kBoxResid || EPI == kBoxResidCopy || EPI == kBoxResidAcc)
+      {
         __builtin_nontemporal_store(dv2b{bb.x - acc.x, bb.y - acc.y}, Yb + r * 4 + cp);
+        if constexpr (EPI != kBoxResid)
+        {
+          dv2b *Xs = const_cast<dv2b *>(Ob);  // (the row's own: read-modify-write by this thread only)
+          dv2b v = ring[s0][hrow][cp];
+          if constexpr (EPI == kBoxResidAcc)
+          {
+            const dv2b xa = Xs[r * 4 + cp];
+            v = dv2b{xa.x + v.x, xa.y + v.y};
+          }
+          Xs[r * 4 + cp] = v;
+        }
+      }
       else
       {
         const dv2b xc = ring[s0][hrow][cp];
@@ -775,8 +799,7 @@ static bool launch_box(const eig_mat_s &A, i64 m, const double *X, double *Y, co
                        const double *dinv, double omega, double gamma, int epi, hipStream_t s)
 {
   if (m <= 0 || m % 8 != 0 || !box_prepare(A)) return false;
-  if ((epi == kBoxChebFirst || epi == kBoxChebSecond || epi == kBoxChebFirstAdd) && !A.box_ctab)
-    return false;  // (row-class only)
+  if (epi >= kBoxChebFirst && !A.box_ctab) return false;  // (row-class only)
   if (A.box_ctab)
   {
     // row-class kernels: one launch, blockIdx.y = column block; z runs for ~2 rounds of the
@@ -816,6 +839,12 @@ static bool launch_box(const eig_mat_s &A, i64 m, const double *X, double *Y, co
       else if (epi == kBoxChebFirstAdd)
         hipLaunchKernelGGL((k_boxc_mv8<kBoxChebFirstAdd, S>), grid, dim3(kCThreads), 0, s, g, A.window, ct, cm, X, Y,
                            (const double *)nullptr, Bv, omega, gamma);
+      else if (epi == kBoxResidCopy)
+        hipLaunchKernelGGL((k_boxc_mv8<kBoxResidCopy, S>), grid, dim3(kCThreads), 0, s, g, A.window, ct, cm, X, Y,
+                           Xold, Bv, 0.0, 0.0);
+      else if (epi == kBoxResidAcc)
+        hipLaunchKernelGGL((k_boxc_mv8<kBoxResidAcc, S>), grid, dim3(kCThreads), 0, s, g, A.window, ct, cm, X, Y,
+                           Xold, Bv, 0.0, 0.0);
       else if (epi == kBoxChebSecond)
         hipLaunchKernelGGL((k_boxc_mv8<kBoxChebSecond, S>), grid, dim3(kCThreads), 0, s, g, A.window, ct, cm, X, Y,
                            (const double *)nullptr, Bv, omega, gamma);
@@ -898,6 +927,13 @@ bool launch_box_spmm(const eig_mat_s &A, i64 m, const double *X, double *Y, hipS
 bool launch_box_resid(const eig_mat_s &A, i64 m, const double *X, const double *B, double *R, hipStream_t s)
 {
   return launch_box(A, m, X, R, nullptr, B, nullptr, 0.0, 0.0, kBoxResid, s);
+}
+
+// R = B - A E and Xacc = E (copy) or Xacc += E (row-class image only; false otherwise).
+bool launch_box_resid_acc(const eig_mat_s &A, i64 m, const double *E, const double *B, double *R, double *Xacc,
+                          bool copy, hipStream_t s)
+{
+  return launch_box(A, m, E, R, Xacc, B, nullptr, 0.0, 0.0, copy ? kBoxResidCopy : kBoxResidAcc, s);
 }
 
 bool launch_box_cheb(const eig_mat_s &M, i64 m, const double *Xk, double *Xold, const double *B, const double *dinv,

@@ -282,13 +282,21 @@ void mg_apply(eig_mg_s &mg, i64 m, const double *B, double *X, int cycles)
   for (int it = 0; it < cycles; ++it)
   {
     const double *E = vcycle(mg, 0, m, rhs);
+    // r -= A e (in place after the first iteration) and X = E / X += E: one pass on the row-class
+    // image (the residual kernel's epilogue also writes X), a copy or axpby and the residual
+    // otherwise
+    if (it + 1 < cycles && launch_box_resid_acc(*L.A, m, E, rhs, R, X, it == 0, s))
+    {
+      rhs = R;
+      continue;
+    }
     if (it == 0)
       EIG_HIP(hipMemcpyAsync(X, E, bytes, hipMemcpyDeviceToDevice, s));
     else
       launch_mv8_axpby(L.n, m, L.n, 1.0, E, 1.0, X, s);
     if (it + 1 < cycles)
     {
-      launch_resid_mv8(*L.A, m, E, rhs, R, s);  // r -= A e (in place after the first iteration)
+      launch_resid_mv8(*L.A, m, E, rhs, R, s);
       rhs = R;
     }
   }
