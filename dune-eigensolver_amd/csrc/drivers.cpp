@@ -400,7 +400,15 @@ void shift_invert_core(eig_mat_t A, eig_mat_t B, const LuRef &F, double sigma, i
       launch_scal(n, 1.0 / nb, V, s);
       if (B) launch_scal(n, 1.0 / nb, BV, s);
     }
-    std::vector<double> T((size_t)m * m, 0.0), ctot(m + 1), ch(m + 1), th, Y;
+    std::vector<double> T((size_t)m * m, 0.0), ctot(m + 1), th, Y;
+    // per step j of an extension: the two CGS passes' coefficients (m + 1 each) and (w, B w), kept on
+    // the device and read back once per extension -- the steps queue without a host round trip (the
+    // host sums and scalars are those the step-by-step loop computed; a breakdown is reported after
+    // the extension, with the same error)
+    const i64 cstride = 2 * (i64)(m + 1) + 1;
+    DevBuf coefb((size_t)m * cstride * 8);
+    double *coef = coefb.d();
+    std::vector<double> coefh((size_t)m * cstride);
     int k = 0, nrestart = 0;
     double betam = 0.0;
     std::vector<int> want;
@@ -411,32 +419,40 @@ void shift_invert_core(eig_mat_t A, eig_mat_t B, const LuRef &F, double sigma, i
       for (int j = k; j < m; ++j)
       {
         double *bvj = BV + (i64)j * n;
+        double *cj = coef + (i64)j * cstride;
         // w = (A - sigma B)^-1 (B v_j): the reverse-communication product of ARSymGenEig 'S' mode
         op(bvj, W);
-        std::fill(ctot.begin(), ctot.end(), 0.0);
         for (int pass = 0; pass < 2; ++pass)  // DGKS / CGS2 against v_0 .. v_j in the B-inner product
         {
-          launch_gemv_t(n, j + 1, BV, n, W, cd, 0, s, ctx->red);
-          launch_gemv_n_sub(n, j + 1, V, n, cd, nullptr, W, s);
-          EIG_HIP(hipMemcpyAsync(ch.data(), cd, (j + 1) * 8, hipMemcpyDeviceToHost, s));
-          EIG_HIP(hipStreamSynchronize(s));
-          for (int i = 0; i <= j; ++i) ctot[i] += ch[i];
+          launch_gemv_t(n, j + 1, BV, n, W, cj + pass * (m + 1), 0, s, ctx->red);
+          launch_gemv_n_sub(n, j + 1, V, n, cj + pass * (m + 1), nullptr, W, s);
         }
-        for (int i = 0; i <= j; ++i) T[(size_t)i * m + j] = T[(size_t)j * m + i] = ctot[i];
         bmul(W, BW);
-        const double beta = std::sqrt(std::max(0.0, dot(W, BW)));
+        launch_dot(n, W, BW, cj + 2 * (m + 1), 0, s, ctx->red);  // beta_j^2
+        double *vn = V + (i64)(j + 1) * n, *bvn = BV + (i64)(j + 1) * n;
+        EIG_HIP(hipMemcpyAsync(vn, W, n * 8, hipMemcpyDeviceToDevice, s));
+        launch_scal_dev(n, cj + 2 * (m + 1), true, vn, s);  // 1 / sqrt(beta_j^2)
+        if (B)
+        {
+          EIG_HIP(hipMemcpyAsync(bvn, BW, n * 8, hipMemcpyDeviceToDevice, s));
+          launch_scal_dev(n, cj + 2 * (m + 1), true, bvn, s);
+        }
+      }
+      EIG_HIP(hipMemcpyAsync(coefh.data() + (size_t)k * cstride, coef + (i64)k * cstride,
+                             (size_t)(m - k) * cstride * 8, hipMemcpyDeviceToHost, s));
+      EIG_HIP(hipStreamSynchronize(s));
+      for (int j = k; j < m; ++j)
+      {
+        const double *ch = coefh.data() + (size_t)j * cstride;
+        std::fill(ctot.begin(), ctot.end(), 0.0);
+        for (int pass = 0; pass < 2; ++pass)
+          for (int i = 0; i <= j; ++i) ctot[i] += ch[pass * (m + 1) + i];
+        for (int i = 0; i <= j; ++i) T[(size_t)i * m + j] = T[(size_t)j * m + i] = ctot[i];
+        const double beta = std::sqrt(std::max(0.0, ch[2 * (m + 1)]));
         double tn = 0.0;
         for (int i = 0; i <= j; ++i) tn = std::max(tn, std::fabs(ctot[i]));
         EIG_CHECK(beta > 1e-14 * tn, EIG_ERR_BREAKDOWN,
                   "shift-invert Lanczos: invariant subspace reached (choose ncv < n or another seed)");
-        double *vn = V + (i64)(j + 1) * n, *bvn = BV + (i64)(j + 1) * n;
-        EIG_HIP(hipMemcpyAsync(vn, W, n * 8, hipMemcpyDeviceToDevice, s));
-        launch_scal(n, 1.0 / beta, vn, s);
-        if (B)
-        {
-          EIG_HIP(hipMemcpyAsync(bvn, BW, n * 8, hipMemcpyDeviceToDevice, s));
-          launch_scal(n, 1.0 / beta, bvn, s);
-        }
         if (j + 1 < m) T[(size_t)(j + 1) * m + j] = T[(size_t)j * m + (j + 1)] = beta;
         betam = beta;
       }
@@ -547,6 +563,25 @@ SiBlockShape si_block_shape(int nev, int ncv)
   return g;
 }
 
+// the block method's reductions within the context's tickets: the projection Gram (cmax x p, partials
+// in a buffer sized for the launch), the CholQR Gram (p x p) and the purified vectors' B-norms
+// (the projection Gram goes in row slices of 64 when it is larger: see gram_rows)
+bool si_block_fits(const SiBlockShape &g)
+{
+  return gram_mv8_chunks(64, g.p) <= kNumTickets && gram_mv8_chunks(g.p, g.p) <= kNumTickets &&
+         g.nw / 8 <= kNumTickets;
+}
+
+// H (c x p, row i at H + i p) = Q1(:, 0 .. c)^T Q2: one launch where its output chunks fit the
+// tickets, else row slices (each a multiple of 64 rows) in stream order
+void gram_rows(eig_ctx_t ctx, i64 n, int c, int p, const double *Q1, const double *Q2, double *H, hipStream_t s)
+{
+  int rc = c;
+  while (gram_mv8_chunks(rc, p) > kNumTickets) rc = std::max(64, (rc / 2 + 63) / 64 * 64);
+  for (int r0 = 0; r0 < c; r0 += rc)
+    launch_gram_panel(ctx, n, n, std::min(rc, c - r0), p, Q1 + (i64)r0 * n, Q2, H + (size_t)r0 * p, s);
+}
+
 void shift_invert_block_core(eig_mat_t A, eig_mat_t B, const LuRef &F, double sigma, int nev, int ncv, double tol,
                              int maxit, unsigned seed, double *eval_host, double *evec_host, int *restarts)
 {
@@ -557,8 +592,7 @@ void shift_invert_block_core(eig_mat_t A, eig_mat_t B, const LuRef &F, double si
   const SiBlockShape g = si_block_shape(nev, ncv);
   const int p = g.p, kk = g.kk, cmax = g.cmax, cap = cmax + p;
   EIG_CHECK(nev < n && cap <= n, EIG_ERR_ARG, "shift-invert (block): the block basis does not fit n");
-  EIG_CHECK(((cmax + 15) / 16) * ((p + 15) / 16) <= kNumTickets, EIG_ERR_ARG,
-            "shift-invert (block): nev too large for the block method (use EIG_SI_SINGLE)");
+  EIG_CHECK(si_block_fits(g), EIG_ERR_ARG, "shift-invert (block): nev too large for the block method (use EIG_SI_SINGLE)");
   if (tol <= 0.0) tol = 2.220446049250313e-16;
   if (maxit <= 0) maxit = 100 * nev;
   const int wk = std::max(kk, g.nw);
@@ -590,7 +624,7 @@ void shift_invert_block_core(eig_mat_t A, eig_mat_t B, const LuRef &F, double si
     {
       double *bw = B ? BW : W;
       bmul(W, bw, p);
-      launch_gram_mv8(n, p, p, W, bw, dH, 0, s, ctx->red);
+      launch_gram_panel(ctx, n, n, p, p, W, bw, dH, s);
       EIG_HIP(hipMemcpyAsync(G.data(), dH, G.size() * 8, hipMemcpyDeviceToHost, s));
       EIG_HIP(hipStreamSynchronize(s));
       for (int i = 0; i < p; ++i)
@@ -629,7 +663,7 @@ void shift_invert_block_core(eig_mat_t A, eig_mat_t B, const LuRef &F, double si
     Ht.assign((size_t)c * p, 0.0);
     for (int pass = 0; pass < 2; ++pass)  // CGS2 against V(:, 0 .. c) in the B-inner product
     {
-      launch_gram_mv8(n, c, p, BV, W, dH, 0, s, ctx->red);
+      gram_rows(ctx, n, c, p, BV, W, dH, s);
       for (int i = 0; i < c / 8; ++i) launch_project(n, p, V + (i64)i * 8 * n, W, dH + (size_t)i * 8 * p, s);
       Hh.resize((size_t)c * p);
       EIG_HIP(hipMemcpyAsync(Hh.data(), dH, Hh.size() * 8, hipMemcpyDeviceToHost, s));
@@ -751,8 +785,8 @@ bool si_use_block(i64 n, int nev, int ncv, int flags)
   if (flags & EIG_SI_SINGLE) return false;
   if (flags & EIG_SI_BLOCK) return true;
   const SiBlockShape g = si_block_shape(nev, ncv);
-  // the basis within n / 4, and the projection Gram (cmax x p) within the reduction tickets
-  return (i64)(g.cmax + g.p) * 4 <= n && ((g.cmax + 15) / 16) * ((g.p + 15) / 16) <= kNumTickets;
+  // the basis within n / 4, and the reductions within the tickets
+  return (i64)(g.cmax + g.p) * 4 <= n && si_block_fits(g);
 }
 
 void shift_invert_run(eig_mat_t A, eig_mat_t B, const LuRef &F, double sigma, int nev, int ncv, double tol, int maxit,
@@ -896,7 +930,13 @@ void arnoldi_core(eig_mat_t A, eig_mat_t B, const LuRef &F, double sigma, int ne
     launch_scal(n, 1.0 / nb, V, s);
     if (bip) launch_scal(n, 1.0 / nb, BV, s);
   }
-  std::vector<double> G((size_t)m * m, 0.0), cvec, ctot(m + 1), ch(m + 1);
+  std::vector<double> G((size_t)m * m, 0.0), cvec, ctot(m + 1);
+  // per step j: the two CGS passes' coefficients and the squared norm of the new vector, on the
+  // device; one read-back per extension (as shift_invert_core)
+  const i64 cstride = 2 * (i64)(m + 1) + 1;
+  DevBuf coefb((size_t)m * cstride * 8);
+  double *coef = coefb.d();
+  std::vector<double> coefh((size_t)m * cstride);
   std::vector<C> w, Y;
   std::vector<int> ord(m);
   double beta = 0.0;
@@ -906,35 +946,44 @@ void arnoldi_core(eig_mat_t A, eig_mat_t B, const LuRef &F, double sigma, int ne
     // extend the Krylov decomposition from k to m vectors (Arnoldi steps)
     for (int j = k; j < m; ++j)
     {
-      if (j > 0)
-        for (int i = 0; i < j; ++i) G[(size_t)j * m + i] = beta * cvec[i];
       double *vj = V + (i64)j * n;
+      double *cj = coef + (i64)j * cstride;
       bmul(vj, BW);
       solve(BW, W);  // W = OP v_j (the reverse-communication product)
-      std::fill(ctot.begin(), ctot.end(), 0.0);
       for (int pass = 0; pass < 2; ++pass)  // CGS2 against v_0 .. v_j in the inner product
       {
-        launch_gemv_t(n, j + 1, BV, n, W, cd, 0, s, ctx->red);
-        launch_gemv_n_sub(n, j + 1, V, n, cd, nullptr, W, s);
-        EIG_HIP(hipMemcpyAsync(ch.data(), cd, (j + 1) * 8, hipMemcpyDeviceToHost, s));
-        EIG_HIP(hipStreamSynchronize(s));
-        for (int i = 0; i <= j; ++i) ctot[i] += ch[i];
+        launch_gemv_t(n, j + 1, BV, n, W, cj + pass * (m + 1), 0, s, ctx->red);
+        launch_gemv_n_sub(n, j + 1, V, n, cj + pass * (m + 1), nullptr, W, s);
       }
-      for (int i = 0; i <= j; ++i) G[(size_t)i * m + j] = ctot[i];
-      beta = norm_in(W, BW);
-      double hn = 0.0;
-      for (int i = 0; i <= j; ++i) hn = std::max(hn, std::fabs(ctot[i]));
-      EIG_CHECK(beta > 1e-14 * hn, EIG_ERR_BREAKDOWN,
-                "Arnoldi: invariant subspace reached (choose ncv < n or another seed)");
+      if (bip) bmul(W, BW);
+      launch_dot(n, W, bip ? BW : W, cj + 2 * (m + 1), 0, s, ctx->red);  // beta_j^2
       double *vn = V + (i64)(j + 1) * n;
       EIG_HIP(hipMemcpyAsync(vn, W, n * 8, hipMemcpyDeviceToDevice, s));
-      launch_scal(n, 1.0 / beta, vn, s);
+      launch_scal_dev(n, cj + 2 * (m + 1), true, vn, s);
       if (bip)
       {
         double *bvn = BV + (i64)(j + 1) * n;
         EIG_HIP(hipMemcpyAsync(bvn, BW, n * 8, hipMemcpyDeviceToDevice, s));
-        launch_scal(n, 1.0 / beta, bvn, s);
+        launch_scal_dev(n, cj + 2 * (m + 1), true, bvn, s);
       }
+    }
+    EIG_HIP(hipMemcpyAsync(coefh.data() + (size_t)k * cstride, coef + (i64)k * cstride,
+                           (size_t)(m - k) * cstride * 8, hipMemcpyDeviceToHost, s));
+    EIG_HIP(hipStreamSynchronize(s));
+    for (int j = k; j < m; ++j)
+    {
+      if (j > 0)
+        for (int i = 0; i < j; ++i) G[(size_t)j * m + i] = beta * cvec[i];
+      const double *ch = coefh.data() + (size_t)j * cstride;
+      std::fill(ctot.begin(), ctot.end(), 0.0);
+      for (int pass = 0; pass < 2; ++pass)
+        for (int i = 0; i <= j; ++i) ctot[i] += ch[pass * (m + 1) + i];
+      for (int i = 0; i <= j; ++i) G[(size_t)i * m + j] = ctot[i];
+      beta = std::sqrt(std::max(0.0, ch[2 * (m + 1)]));
+      double hn = 0.0;
+      for (int i = 0; i <= j; ++i) hn = std::max(hn, std::fabs(ctot[i]));
+      EIG_CHECK(beta > 1e-14 * hn, EIG_ERR_BREAKDOWN,
+                "Arnoldi: invariant subspace reached (choose ncv < n or another seed)");
       cvec.assign(j + 1, 0.0);
       cvec[j] = 1.0;
     }

@@ -105,12 +105,27 @@ def test_block_method_arguments(ctx):
         eigmi.shift_invert_solve(up(ctx, A), 4, sigma=0.0, method="block")  # n = 36 < 72 columns
     ev, _, _ = eigmi.shift_invert_solve(up(ctx, A), 4, sigma=0.0, want_evec=False)  # auto: one-vector
     assert np.allclose(ev, np.sort(oracle.eig_laplace2d(6))[:4], rtol=0, atol=1e-10)
-    with pytest.raises(eigmi.EigError):  # nev = 60: the projection Gram exceeds the reduction tickets
-        eigmi.shift_invert_solve(up(ctx, oracle.laplace2d(64)), 60, sigma=0.0, method="block")
+    with pytest.raises(eigmi.EigError):  # nev = 264: the CholQR Gram (264 x 264) exceeds the tickets
+        eigmi.shift_invert_solve(up(ctx, oracle.laplace2d(64)), 264, sigma=0.0, method="block")
     with pytest.raises(eigmi.EigError):
         A2 = up(ctx, A)
         A2.ctx.check(eigmi.lib.eig_shift_invert_solve_ex(A2.h, None, None, 0.0, 4, 0, 0.0, 0, 1,
                                                          eigmi._np_ptr(np.zeros(4)), None, None, 3))
+
+
+@pytest.mark.parametrize("method,nev", [("auto", 60), ("block", 100)])
+def test_large_nev_block(ctx, method, nev):
+    """Large nev on the block method, with its Grams' partials in a buffer sized for the launch:
+    nev = 60 (p = 64, a 384-column basis; EIG_SI_AUTO takes the block method) and nev = 100 (p = 104,
+    624 columns: the projection Gram goes in row slices).  Eigenvalues against the analytic
+    spectrum, vectors through their residual and orthonormality."""
+    A = oracle.laplace2d(64)
+    ev, X, _ = eigmi.shift_invert_solve(up(ctx, A), nev, sigma=0.0, method=method)
+    assert np.allclose(ev, np.sort(oracle.eig_laplace2d(64))[:nev], rtol=0, atol=1e-10)
+    As = A.to_scipy()
+    R = (As @ X.T) - X.T * ev[None, :]
+    assert np.abs(R).max() <= 1e-8 * 8.0
+    assert np.abs(X @ X.T - np.eye(nev)).max() <= 1e-10
 
 
 def test_argument_errors(ctx):
