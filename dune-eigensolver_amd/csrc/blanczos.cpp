@@ -155,20 +155,38 @@ void mcholqr2(eig_blanczos_s &w, double *Z, double *Vdst, std::vector<double> &R
   double *Rd = w.chol->d(), *Rt = Rd + (size_t)b * b;
   int *flag = reinterpret_cast<int *>(Rt + (size_t)b * b);
   EIG_HIP(hipMemsetAsync(flag, 0, sizeof(int), s));
-  for (int pass = 0; pass < 2; ++pass)
+  if (b == 32)
   {
-    // pass 1 reuses M Z: the first pass updated it with the same triangular factor as Z (row-local,
-    // M (Z R^-1) = (M Z) R^-1 up to rounding), so one M SpMM per CholQR2 instead of two
-    if (pass == 0)
-    {
-      halo_mv(M, Z, b, s);
-      launch_sell_mv8(M, b, Z, dptr(w.MZ), s);
-    }
+    // Z <- Z R0^-1 and the second pass's Gram (Z R0^-1)^T (M Z R0^-1) in one pass over Z and M Z
+    // (k_cholqr_fold): M Z R0^-1 is never stored, Z R0^-1 is not read back
+    halo_mv(M, Z, b, s);
+    launch_sell_mv8(M, b, Z, dptr(w.MZ), s);
     launch_panel_gram(ctx, n, ld, b, b, Z + own * 8, dptr(w.MZ) + own * 8, Gd, s);
     allreduce_sum(ctx, Gd, (i64)b * b, s);
-    launch_chol_small(b, pass, Gd, Rd, Sd, Rt, flag, s);  // Sd = R^-1, Rt <- R Rt
-    launch_panel_update(n, ld, ld, b, b, Z + own * 8, Sd, 1.0, 0.0, (pass == 1 ? Vdst : Z) + own * 8, s);
-    if (pass == 0) launch_panel_update(n, ld, ld, b, b, dptr(w.MZ) + own * 8, Sd, 1.0, 0.0, dptr(w.MZ) + own * 8, s);
+    launch_chol_small(b, 0, Gd, Rd, Sd, Rt, flag, s);
+    launch_cholqr_fold(ctx, n, ld, Z + own * 8, dptr(w.MZ) + own * 8, Sd, Gd, s);
+    allreduce_sum(ctx, Gd, (i64)b * b, s);
+    launch_chol_small(b, 1, Gd, Rd, Sd, Rt, flag, s);
+    launch_panel_update(n, ld, ld, b, b, Z + own * 8, Sd, 1.0, 0.0, Vdst + own * 8, s);
+  }
+  else
+  {
+    for (int pass = 0; pass < 2; ++pass)
+    {
+      // pass 1 reuses M Z: the first pass updated it with the same triangular factor as Z (row-local,
+      // M (Z R^-1) = (M Z) R^-1 up to rounding), so one M SpMM per CholQR2 instead of two
+      if (pass == 0)
+      {
+        halo_mv(M, Z, b, s);
+        launch_sell_mv8(M, b, Z, dptr(w.MZ), s);
+      }
+      launch_panel_gram(ctx, n, ld, b, b, Z + own * 8, dptr(w.MZ) + own * 8, Gd, s);
+      allreduce_sum(ctx, Gd, (i64)b * b, s);
+      launch_chol_small(b, pass, Gd, Rd, Sd, Rt, flag, s);  // Sd = R^-1, Rt <- R Rt
+      launch_panel_update(n, ld, ld, b, b, Z + own * 8, Sd, 1.0, 0.0, (pass == 1 ? Vdst : Z) + own * 8, s);
+      if (pass == 0)
+        launch_panel_update(n, ld, ld, b, b, dptr(w.MZ) + own * 8, Sd, 1.0, 0.0, dptr(w.MZ) + own * 8, s);
+    }
   }
   Rtot.assign((size_t)b * b, 0.0);
   int hflag = 0;
@@ -333,11 +351,9 @@ extern "C" int eig_blanczos_step(eig_blanczos_t w, int steps, eig_blanczos_timin
       double *Z;
       if (!w->si)
       {
-        // W = K V_j;  A_j = V_j^T W;  Z = M^-1 W
+        // W = K V_j;  Z = M^-1 W;  A_j = V_j^T W is block j of the first CGS pass's V^T W below
         halo_mv(*w->K, Vj, b, s);
         launch_sell_mv8(*w->K, b, Vj, w->W->d(), s);
-        launch_panel_gram(ctx, n, ld, b, b, Vj + own * 8, w->W->d() + own * 8, Ad, s);
-        allreduce_sum(ctx, Ad, (i64)b * b, s);
         EIG_HIP(hipEventRecord(e[1], s));
         Z = cheb_solve(*w->M, b, w->degree, w->lmin, w->lmax, w->W->d(), w->dinv->d(), w->Xa->d(), w->Xb->d(),
                        w->Xc->d(), s);
@@ -377,6 +393,8 @@ extern "C" int eig_blanczos_step(eig_blanczos_t w, int steps, eig_blanczos_timin
         }
         launch_panel_gram(ctx, n, ld, m1, b, w->V->d() + own * 8, MZ + own * 8, Cd, s);
         allreduce_sum(ctx, Cd, m1 * b, s);
+        if (pass == 0 && !w->si)  // A_j = V_j^T W: rows j b .. (j + 1) b of C
+          EIG_HIP(hipMemcpyAsync(Ad, Cd + (size_t)j * b * b, (size_t)b * b * sizeof(double), hipMemcpyDeviceToDevice, s));
         launch_panel_update(n, ld, ld, m1, b, w->V->d() + own * 8, Cd, -1.0, 1.0, Z + own * 8, s);
       }
       EIG_HIP(hipEventRecord(e[3], s));

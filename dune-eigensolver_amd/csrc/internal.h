@@ -401,9 +401,12 @@ double *cheb_solve(eig_mat_s &M, i64 m, int degree, double lmin, double lmax, co
 void mg_apply(eig_mg_s &mg, i64 m, const double *B, double *X, int cycles);
 eig_mat_s *mg_matrix(const eig_mg_s &mg);
 int mg_max_cols(const eig_mg_s &mg);
-// Y = beta Y + alpha Q S over n rows (owned-row pointers), m2 <= 32.
+// CholQR2's middle step, b = 32: Z <- Z S, G = (Z S)^T (MZ S) (k_block.hip; partials in context slot 8)
+void launch_cholqr_fold(eig_ctx_t ctx, i64 n, i64 ld, double *Z, const double *MZ, const double *S, double *G,
+                        hipStream_t s);
 void launch_chol_small(int b, int pass, const double *G, double *R, double *Ri, double *Rtot, int *flag,
                        hipStream_t s);
+// Y = beta Y + alpha Q S over n rows (owned-row pointers), m2 <= 32.
 void launch_panel_update(i64 n, i64 ldq, i64 ldy, i64 m1, i64 m2, const double *Q, const double *S, double alpha,
                          double beta, double *Y, hipStream_t s);
 

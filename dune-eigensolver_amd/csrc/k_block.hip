@@ -11,6 +11,8 @@
 //                     deterministic stages (per-workgroup partials, then a fixed-order sum)
 //   k_panel_update    Y = beta Y + alpha Q S (Q: n x m1, S: m1 x m2 with m2 <= 32), FMA with S
 //                     in scalar registers
+//   k_cholqr_fold     CholQR2's middle step for 32 columns: Z <- Z S and G = (Z S)^T (MZ S) in one
+//                     pass, MFMA for both products
 //
 // Window layout: column block b of a multivector with leading dimension ld (the matrix window)
 // is ld rows of 8 contiguous doubles at Q + 8 b ld; owned row r sits at window row own + r.  On
@@ -20,6 +22,7 @@
 #include <string>
 
 #include "internal.h"
+#include "reduce_dev.h"
 
 namespace eigmi {
 
@@ -796,6 +799,134 @@ void launch_chol_small(int b, int pass, const double *G, double *R, double *Ri, 
 {
   EIG_CHECK(b >= 1 && b <= 32, EIG_ERR_ARG, "chol_small: b <= 32");
   hipLaunchKernelGGL(k_chol_small, dim3(1), dim3(256), 0, s, b, pass, G, R, Ri, Rtot, flag);
+  EIG_HIP(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------------------------
+// CholQR2's middle step fused (blanczos.cpp mcholqr2, b = 32 columns = 4 blocks): with S = R^-1 of
+// the first pass (upper triangular, row-major 32 x 32), Z <- Z' = Z S and G = Z'^T (MZ S) in ONE
+// pass over Z and MZ -- MZ S (the first pass's update of M Z) is never stored, and Z' is not read
+// back for the second Gram.  Both products on v_mfma_f64_16x16x4f64, 16 rows per wave iteration:
+//  * transform: lane (k, i) loads row i's columns 2k, 2k + 1 of each 8-column block (a 16-B load;
+//    one wave instruction reads 16 whole 64-B rows) and the MFMA h of block kb takes inner index
+//    k -> column 8 kb + 2 k + h, with B[k][j] = S[8 kb + 2 k + h][16 t + j] held in registers for
+//    the whole launch.  S is upper triangular, so output columns 0..15 need blocks 0 and 1 only;
+//  * the transform's output layout (lane (k, i), register q: row k + 4 q, column 16 t + i) is the
+//    Gram MFMA's operand layout for the row group q, so Z' and MZ' go from the accumulators into
+//    the Gram MFMAs without any exchange; Z' is stored from the same registers (in place: a wave
+//    reads its 16 rows completely before it writes them).
+// The Gram sums are reduced as k_gram_mv8's: waves in order into one LDS image, then grid_sum2.
+// Not bitwise the two-launch form (the MFMA's four-term products round differently from
+// k_panel_update's FMA chain); the block Lanczos results are checked against scipy.
+// ---------------------------------------------------------------------------------------------
+constexpr int kFoldThreads = 256;
+
+__global__ __launch_bounds__(kFoldThreads) void k_cholqr_fold(i64 n, i64 ld, double *Z, const double *__restrict__ MZ,
+                                                              const double *__restrict__ S, double *__restrict__ G,
+                                                              double *partials, unsigned *tickets)
+{
+  constexpr int E = 4 * 256;  // the 2 x 2 tiles of 16 x 16
+  __shared__ double red[E];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int k = lane >> 4, i = lane & 15;
+  double sb[4][2][2];
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) sb[kb][h][t] = S[(8 * kb + 2 * k + h) * 32 + 16 * t + i];
+  d4 acc[2][2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) acc[t][u] = d4{0.0, 0.0, 0.0, 0.0};
+  const i64 ntile = (n + 15) / 16;
+  const i64 ws = (i64)gridDim.x * (kFoldThreads / 64);
+  for (i64 tile = (i64)blockIdx.x * (kFoldThreads / 64) + wave; tile < ntile; tile += ws)
+  {
+    const i64 r = tile * 16 + i;
+    const bool ok = r < n;
+    const i64 rr = ok ? r : 0;
+    dv2 zv[4], mv[4];
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+    {
+      zv[kb] = *reinterpret_cast<const dv2 *>(Z + ((i64)kb * ld + rr) * 8 + 2 * k);
+      mv[kb] = *reinterpret_cast<const dv2 *>(MZ + ((i64)kb * ld + rr) * 8 + 2 * k);
+    }
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+    {
+      zv[kb] = ok ? zv[kb] : dv2{0.0, 0.0};
+      mv[kb] = ok ? mv[kb] : dv2{0.0, 0.0};
+    }
+    d4 zt[2], mt[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) zt[t] = mt[t] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+          if (t == 1 || kb < 2)
+          {
+            zt[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(zv[kb][h], sb[kb][h][t], zt[t], 0, 0, 0);
+            mt[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(mv[kb][h], sb[kb][h][t], mt[t], 0, 0, 0);
+          }
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+      {
+        const i64 row = tile * 16 + 4 * q + k;
+        if (row < n) Z[((i64)(2 * t + (i >> 3)) * ld + row) * 8 + (i & 7)] = zt[t][q];
+      }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) acc[t][u] = __builtin_amdgcn_mfma_f64_16x16x4f64(zt[t][q], mt[u][q], acc[t][u], 0, 0, 0);
+  }
+  for (int w = 0; w < kFoldThreads / 64; ++w)
+  {
+    if (wave == w)
+    {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+          {
+            const int e = (t * 2 + u) * 256 + (k + 4 * q) * 16 + i;
+            red[e] = w == 0 ? acc[t][u][q] : red[e] + acc[t][u][q];
+          }
+    }
+    __syncthreads();
+  }
+  if (!grid_sum2<kFoldThreads>(red, E, partials, partials + (size_t)gridDim.x * E, tickets, blockIdx.x, gridDim.x,
+                               red))
+    return;
+  for (int e = threadIdx.x; e < E; e += kFoldThreads)
+  {
+    const int tu = e / 256, t = tu / 2, u = tu % 2, el = e % 256;
+    G[(16 * t + el / 16) * 32 + 16 * u + el % 16] = red[e];
+  }
+}
+
+void launch_cholqr_fold(eig_ctx_t ctx, i64 n, i64 ld, double *Z, const double *MZ, const double *S, double *G,
+                        hipStream_t s)
+{
+  constexpr int E = 4 * 256;
+  const i64 ntile = (n + 15) / 16;
+  // two workgroups per CU (122 VGPRs + 48 AGPRs: two waves per SIMD)
+  const int gx = (int)std::max<i64>(1, std::min<i64>(512, (ntile + 3) / 4));
+  double *part = (double *)ctx_buffer(ctx, 8, (size_t)(gx + 8) * E * sizeof(double));
+  hipLaunchKernelGGL(k_cholqr_fold, dim3(gx), dim3(kFoldThreads), 0, s, n, ld, Z, MZ, S, G, part,
+                     ctx->red.ticket(0));
   EIG_HIP(hipGetLastError());
 }
 
