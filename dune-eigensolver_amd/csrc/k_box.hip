@@ -802,8 +802,10 @@ static bool launch_box(const eig_mat_s &A, i64 m, const double *X, double *Y, co
   if (epi >= kBoxChebFirst && !A.box_ctab) return false;  // (row-class only)
   if (A.box_ctab)
   {
-    // row-class kernels: one launch, blockIdx.y = column block; z runs for ~2 rounds of the
-    // resident workgroups (2 per CU)
+    // row-class kernels: one launch, blockIdx.y = column block.  z runs of about 32 planes (a run
+    // re-reads two halo planes, so shorter runs cost bytes; longer ones balance worse), but at least
+    // one workgroup per CU on small grids and no run shorter than 8 planes (EIG_TUNE_BOX_SEGS sweeps,
+    // profiles/r03aw_box_segs.jsonl: 128^3 m = 8 55.3 -> 46.8 us, 256^3 m = 32 1554 -> 1500 us)
     BoxGeom g;
     g.nx = A.box_nx;
     g.ny = A.box_ny;
@@ -812,8 +814,9 @@ static bool launch_box(const eig_mat_s &A, i64 m, const double *X, double *Y, co
     g.ntx = (g.nx + kCTX - 1) / kCTX;
     g.nty = (g.ny + kCTY - 1) / kCTY;
     const i64 per_seg = (i64)g.ntx * g.nty * (m / 8);
-    const i64 want = 4LL * A.ctx->num_cu;
-    g.nseg = (int)std::max<i64>(1, std::min<i64>(g.nz / 8, (want + per_seg - 1) / per_seg));
+    const i64 fill = std::min<i64>(g.nz / 8, (A.ctx->num_cu + per_seg - 1) / per_seg);
+    g.nseg = (int)std::max<i64>({1, (g.nz + 31) / 32, fill});
+    if (A.tune_box_segs > 0) g.nseg = std::min(g.nz, A.tune_box_segs);
     g.nd = A.sym_nd;
     for (int k = 0; k < 27; ++k)
     {
@@ -878,6 +881,7 @@ static bool launch_box(const eig_mat_s &A, i64 m, const double *X, double *Y, co
   // z runs: enough tiles x runs for two rounds of the 256 CUs (one 147 KB workgroup per CU)
   const int tiles = g.ntx * g.nty;
   g.nseg = std::max(1, std::min(g.nz / 8, (2 * A.ctx->num_cu + tiles - 1) / tiles));
+  if (A.tune_box_segs > 0) g.nseg = std::min(g.nz, A.tune_box_segs);
   g.nd = A.sym_nd;
   for (int k = 0; k < 27; ++k)
   {

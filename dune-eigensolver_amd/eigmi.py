@@ -460,9 +460,12 @@ class Matrix:
         self.ctx.check(lib.eig_mv_host(self.h, _np_ptr(x), _np_ptr(y)))
         return y
 
-    def tune(self, march_runs=0):
-        """eig_mat_tune(EIG_TUNE_MARCH_RUNS): plane runs per column of the plane-march kernels (0 = auto)."""
+    def tune(self, march_runs=0, box_segs=None):
+        """eig_mat_tune: EIG_TUNE_MARCH_RUNS = plane runs per column of the plane-march kernels,
+        EIG_TUNE_BOX_SEGS = z segments per tile column of the box kernels (0 = automatic)."""
         self.ctx.check(lib.eig_mat_tune(self.h, 1, int(march_runs)))
+        if box_segs is not None:
+            self.ctx.check(lib.eig_mat_tune(self.h, 2, int(box_segs)))
 
     def shift_diag(self, shift):
         self.ctx.check(lib.eig_mat_shift_diag(self.h, shift))

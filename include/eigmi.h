@@ -187,9 +187,11 @@ int eig_mat_kernel_info(eig_mat_t mat, int op, char *name, int name_len);
 
 /* Measurement / tuning override of a launch parameter the library otherwise derives from the
  * image and the device (no environment switches): EIG_TUNE_MARCH_RUNS = plane runs per 64-row column
- * of the plane-march kernels (value 0 = automatic: one work item per resident wave slot).  Results
- * are unchanged except for the summation order of the step's reductions. */
-enum { EIG_TUNE_MARCH_RUNS = 1 };
+ * of the plane-march kernels (value 0 = automatic: one work item per resident wave slot);
+ * EIG_TUNE_BOX_SEGS = z segments per tile column of the 3-D box kernels (0 = automatic; results
+ * bitwise unchanged, every row's sum is formed in one place).  Results are otherwise unchanged except
+ * for the summation order of the step's reductions. */
+enum { EIG_TUNE_MARCH_RUNS = 1, EIG_TUNE_BOX_SEGS = 2 };
 int eig_mat_tune(eig_mat_t mat, int key, int value);
 
 /* a13: A += shift*I on the diagonal of every diagonal block (eigensolver.hh:59-66). */

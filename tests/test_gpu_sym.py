@@ -309,6 +309,38 @@ def test_box_chebyshev_matches_sell(ctx, N, var):
     assert np.linalg.norm(r) <= 1e-6 * np.linalg.norm(Bh)
 
 
+@pytest.mark.parametrize("mat,var", [("p1mass20", False), ("poisson18", False), ("p1mass16", True)])
+def test_box_segments_bitwise(ctx, mat, var):
+    """EIG_TUNE_BOX_SEGS (z segments per tile column) changes where a row is computed, never how:
+    SpMM, residual-free Chebyshev solves of degree 2 / 3 / 7 (first / second / later step epilogues)
+    are bitwise those of the automatic choice for 1 .. nz segments (ragged segment lengths included)."""
+    A = {"p1mass20": lambda: _p1(20, "M"), "poisson18": lambda: oracle.poisson3d(18),
+         "p1mass16": lambda: _p1(16, "M")}[mat]()
+    if var:
+        A = _perturbed(A)
+    M = upload(ctx, A)
+    n, m = A.n, 32
+    nz = round(n ** (1 / 3))
+    Qh = oracle.random_mv8(n, m, 23)
+    Q, Y = ctx.array(Qh), ctx.zeros(n * m)
+    ref = {}
+    for segs in (0, 1, 2, 3, 5, nz):
+        M.tune(box_segs=segs)
+        eigmi.spmm_mv8(M, m, Q, Y)
+        out = {"spmm": Y.get()}
+        if mat.startswith("p1"):
+            for d in (2, 3, 7):
+                eigmi.mass_solve_mv8(M, m, d, Q, Y)
+                out[d] = Y.get()
+        if segs == 0:
+            ref = out
+            assert np.array_equal(out["spmm"], oracle.spmm_mv8(A, Qh, m))
+        else:
+            for k in ref:
+                assert np.array_equal(out[k], ref[k]), (segs, k)
+    M.tune(box_segs=0)
+
+
 @pytest.mark.parametrize("mat", ["p1mass16", "poisson18"])
 def test_box_no_class_flag(ctx, mat):
     """EIG_MAT_NO_CLASS keeps the box-image kernel on a class-constant matrix; both kernels give the

@@ -11,6 +11,7 @@
 #   bench                python bench.py (the driver's default line)          -> bench.json
 #   profile              rocprofv3 kernel trace + FETCH / WRITE PMC passes of the bench (tools/profile_round.sh)
 #   configs              tools/bench_configs.py c1 c2 c3, c5 (256^3), inv (64^2, 200^2)  -> cfg_*.jsonl
+#   boxsegs              box kernels' z segments per tile column swept (tools/box_segs.py) -> box_segs.jsonl
 #   inv                  the inverse-mode configs alone (64^2, 200^2)        -> cfg_inv*.jsonl
 #   gram                 a6 / a9 / panel-Gram timings under a kernel trace    -> gram.jsonl, gram_trace/
 #   grampmc              FETCH_SIZE / WRITE_SIZE passes over the gram timings -> grampmc/{fetch,write}
@@ -48,6 +49,8 @@ run_task() {
       EIGMI_C5_N=256 timeout -k 10 300 python -u tools/bench_configs.py c5 > "$O/cfg_c5.jsonl" 2> "$O/cfg_c5.err" && \
       EIGMI_INV_N=64 timeout -k 10 300 python -u tools/bench_configs.py inv > "$O/cfg_inv64.jsonl" 2> "$O/cfg_inv64.err" && \
       EIGMI_INV_N=200 timeout -k 10 400 python -u tools/bench_configs.py inv > "$O/cfg_inv200.jsonl" 2> "$O/cfg_inv200.err" ;;
+    boxsegs)
+      timeout -k 10 400 python -u tools/box_segs.py 128 256 > "$O/box_segs.jsonl" 2> "$O/box_segs.err" ;;
     inv)
       EIGMI_INV_N=64 timeout -k 10 300 python -u tools/bench_configs.py inv > "$O/cfg_inv64.jsonl" 2> "$O/cfg_inv64.err" && \
       EIGMI_INV_N=200 timeout -k 10 400 python -u tools/bench_configs.py inv > "$O/cfg_inv200.jsonl" 2> "$O/cfg_inv200.err" ;;
