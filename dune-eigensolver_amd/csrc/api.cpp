@@ -872,6 +872,51 @@ void build_sym(eig_mat_s &A, i64 nb, const int64_t *rowptr, const int32_t *col, 
       }
   });
   if (!good) return;
+  // uniform band: one value per array over every stored entry (the symmetric pairs are equal bit
+  // for bit already, so the lower entries need no separate check)
+  {
+    std::mutex mu;
+    std::vector<double> uc(nup, 0.0);
+    std::vector<char> seen(nup, 0);
+    bool uni = true;
+    parallel_slices(nb, [&](i64 r0, i64 r1) {
+      std::vector<double> v(nup, 0.0);
+      std::vector<char> sn(nup, 0);
+      bool ok = true;
+      for (i64 r = r0; r < r1 && ok; ++r)
+        for (i64 p = rowptr[r]; p < rowptr[r + 1]; ++p)
+        {
+          const i64 d = (i64)col[p] - (row0 + r);
+          if (d < 0) continue;
+          const int j = kj[kof(d)];
+          if (!sn[j])
+          {
+            sn[j] = 1;
+            v[j] = vals[p];
+          }
+          else if (std::memcmp(&v[j], &vals[p], sizeof(double)) != 0)
+          {
+            ok = false;
+            break;
+          }
+        }
+      std::lock_guard<std::mutex> lk(mu);
+      uni = uni && ok;
+      for (int j = 0; j < nup && uni; ++j)
+        if (sn[j])
+        {
+          if (!seen[j])
+          {
+            seen[j] = 1;
+            uc[j] = v[j];
+          }
+          else if (std::memcmp(&uc[j], &v[j], sizeof(double)) != 0)
+            uni = false;
+        }
+    });
+    A.sym_uniform = uni;
+    for (int j = 0; j < nup; ++j) A.sym_uc[j] = uni ? uc[j] : 0.0;
+  }
   hipStream_t s = A.ctx->stream;
   A.sym_val = dev_alloc<double>((size_t)nup * ld);
   A.sym_mask = mb == 1 ? (void *)dev_alloc<uint8_t>(ns * 64) : (void *)dev_alloc<uint32_t>(ns * 64);
@@ -1208,6 +1253,7 @@ extern "C" int eig_mat_get_info(eig_mat_t A, eig_mat_info *info)
     info->sym_offsets = A->sym_val ? A->sym_nd : 0;
     info->sym_arrays = A->sym_val ? A->sym_nup : 0;
     info->sym_mask_bytes = A->sym_val ? A->sym_mask_bytes : 0;
+    info->sym_uniform = (A->sym_val && A->sym_uniform && !(A->kflags & EIG_MAT_NO_UNIFORM)) ? 1 : 0;
   });
 }
 

@@ -203,6 +203,11 @@ struct eig_mat_s {
   eigmi::i64 sym_ld = 0;
   eigmi::i32 sym_off[eigmi::kSymMaxOff] = {};      // ascending offsets (ISTL column order)
   eigmi::i32 sym_dj[eigmi::kSymMaxOff] = {};       // array index of |sym_off[k]|
+  // Uniform band (constant-coefficient stencils): every stored entry of band array j has the value
+  // sym_uc[j] bit for bit, so the plane-march kernels take the values from their arguments and
+  // stream the row mask and the vectors only (the arrays stay for the other kernels)
+  bool sym_uniform = false;
+  double sym_uc[eigmi::kSymMaxOff] = {};
   // Plane-march split of a distributed slab (k_spmv.hip march_plan): planes [mz0, mz1) have no
   // ghost columns and are marched while the halo is in flight; march_bnd lists every slice outside
   // them (the boundary launch after the exchange).  mz1 <= mz0: no split.

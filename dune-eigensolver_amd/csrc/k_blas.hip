@@ -228,6 +228,7 @@ void launch_shift_diag(eig_mat_s &A, double shift, hipStream_t s)
       if (A.sym_off[k] == 0) k0 = k;
     if (k0 < 0) return;  // no row stores a diagonal entry
     double *diag = A.sym_val + (i64)A.sym_dj[k0] * A.sym_ld;
+    A.sym_uc[A.sym_dj[k0]] += shift;  // (k_shift_sym's addition: a uniform diagonal stays uniform)
     if (A.sym_mask_bytes == 1)
       hipLaunchKernelGGL(k_shift_sym<uint8_t>, dim3((unsigned)G), dim3(256), 0, s, A.nb_rows, A.own_offset,
                          static_cast<const uint8_t *>(A.sym_mask), k0, diag, shift);

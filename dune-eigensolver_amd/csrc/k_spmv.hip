@@ -962,6 +962,9 @@ struct MarchPlan {
   // first entries of the far spans (-D, -1) and (+1, +D): offset (0 = empty span) and band array
   i32 dn, dq;
   const double *Un, *Uq;
+  // uniform band (eig_mat_s::sym_uniform): the band values of the +D, 0, +1, far-span (dn / dq)
+  // arrays, taken instead of the array loads by the UNI kernels
+  double cD, c0, c1, cn, cq;
 };
 
 // The rows of this wave's work item, in plane order: epi(r, w, acc, centre) gets each row's sum
@@ -972,10 +975,16 @@ struct MarchPlan {
 // offset group after the near math; prefetching the next plane's streams, or its far-span
 // operands, one iteration ahead -- both spill in the fused kernel and gave nothing in the others;
 // y-line workgroup grouping with a barrier per plane; temporal result stores.)
-template <class MT, int KC, bool SPAN1, class X, class EPI>
+// UNI (uniform band, SPAN1 only): the band values come from the plan's constants -- the values the
+// arrays hold at every slot the mask admits -- so only the row mask and the operands are streamed;
+// the same products and sums in the same order, bit for bit.  (Measured and dropped for UNI: issuing
+// plane z + 1's mask / gathers / edge operand before plane z's arithmetic -- 256^3 fused step 145 vs
+// 137 us at the 7 waves / SIMD it needs, 128^3 28.0 vs 30.7: profiles/r03bc_latency.jsonl.)
+template <class MT, int KC, bool SPAN1, bool UNI, class X, class EPI>
 __device__ __forceinline__ void march_rows(const SellB1 &A, const MarchPlan &mp, i64 own, int lane, int wave,
                                            const X &x, EPI &epi)
 {
+  static_assert(!UNI || SPAN1, "uniform-band march: far spans of at most one offset");
   typedef typename X::raw raw;
   // 32-bit row / window indices (window < 2^31, enforced at upload) keep the address math short
   const SymImg &S = A.sym;
@@ -1004,15 +1013,24 @@ __device__ __forceinline__ void march_rows(const SellB1 &A, const MarchPlan &mp,
     const int r = w - own32;
     const unsigned wv = (unsigned)(w > ldl ? ldl : w);
     st.m = r < mrows ? (unsigned)__builtin_nontemporal_load(mask + (unsigned)r) : 0u;
-    st.aD = ld1(UD, wv);
     st.pD = x.load(cx(w + D));
-    st.a0 = S.j0 >= 0 ? ld1(U0, wv) : 0.0;
-    st.ap = ld1(U1, wv);
+    if constexpr (UNI)
+    {
+      st.aD = mp.cD;
+      st.a0 = mp.c0;
+      st.ap = mp.c1;
+    }
+    else
+    {
+      st.aD = ld1(UD, wv);
+      st.a0 = S.j0 >= 0 ? ld1(U0, wv) : 0.0;
+      st.ap = ld1(U1, wv);
+    }
   };
   // carried operands: the -D operand (as its value x.val), its mirrored matrix entry, the centre
   int w = own32 + col * 64 + lane + z0 * D;
   double pmv = x.val(x.load(cx(w - D)));
-  double amD = UD[cv(w - D)];
+  double amD = UNI ? mp.cD : UD[cv(w - D)];
   raw pcur = x.load(cx(w));
   Stream cur;
   const bool edge = lane == 0 || lane == 63;
@@ -1025,18 +1043,18 @@ __device__ __forceinline__ void march_rows(const SellB1 &A, const MarchPlan &mp,
     raw eg;
     double ae = 0.0;
     if (edge) eg = x.load(cx(lane == 0 ? w - 1 : w + 1));
-    if (lane == 0) ae = U1[cv(w - 1)];
+    if (lane == 0) ae = UNI ? mp.c1 : U1[cv(w - 1)];
     double an = 0.0, aq = 0.0;
     raw xn, xq;
     if (mp.dn)
     {
       const unsigned g = cx(w + mp.dn);  // (negative offset: the mirrored slot at the gathered row)
-      an = mp.Un[g];
+      an = UNI ? mp.cn : mp.Un[g];
       xn = x.load(g);
     }
     if (mp.dq)
     {
-      aq = mp.Uq[wv];
+      aq = UNI ? mp.cq : mp.Uq[wv];
       xq = x.load(cx(w + mp.dq));
     }
     const unsigned m = cur.m;
@@ -1074,7 +1092,7 @@ __device__ __forceinline__ void march_rows(const SellB1 &A, const MarchPlan &mp,
 }
 
 // y[own + r] = (A x)[r] on the plane march (BCRSMatrix::mv; bitwise k_spmv_b1).
-template <class MT, bool SPAN1>
+template <class MT, bool SPAN1, bool UNI>
 __global__ __launch_bounds__(kStreamThreads, 8) void k_spmv_march(i64 nrows, i64 own, SellB1 A, MarchPlan mp,
                                                                   const double *__restrict__ x,
                                                                   double *__restrict__ y)
@@ -1083,12 +1101,12 @@ __global__ __launch_bounds__(kStreamThreads, 8) void k_spmv_march(i64 nrows, i64
   auto epi = [&](int r, int w, double acc, double) {
     if (r < nrows) __builtin_nontemporal_store(acc, y + (unsigned)w);
   };
-  march_rows<MT, 2, SPAN1>(A, mp, own, lane, wave, XPlain{x}, epi);
+  march_rows<MT, 2, SPAN1, UNI>(A, mp, own, lane, wave, XPlain{x}, epi);
 }
 
 // Classic Lanczos kernel 1 on the plane march (same per-row arithmetic as k_lanczos_spmv_b1; the
 // row's own u_j is the march's centre operand).
-template <class MT, bool SPAN1>
+template <class MT, bool SPAN1, bool UNI>
 __global__ __launch_bounds__(kStreamThreads, 8) void k_lanczos_spmv_march(
     i64 nrows, i64 own, SellB1 A, MarchPlan mp, const double *__restrict__ u, const double *__restrict__ up,
     double *__restrict__ t, int j, const double *__restrict__ nsum, double *__restrict__ dot_out,
@@ -1109,7 +1127,7 @@ __global__ __launch_bounds__(kStreamThreads, 8) void k_lanczos_spmv_march(
       d += ti * uv;
     }
   };
-  march_rows<MT, 2, SPAN1>(A, mp, own, lane, wave, XPlain{u}, epi);
+  march_rows<MT, 2, SPAN1, UNI>(A, mp, own, lane, wave, XPlain{u}, epi);
   double v[1] = {d};
   if (grid_sum<1, kStreamThreads>(v, partials, ticket, tot))
   {
@@ -1124,8 +1142,8 @@ __global__ __launch_bounds__(kStreamThreads, 8) void k_lanczos_spmv_march(
 // Fused one-reduction step on the plane march (per-row arithmetic of k_lanczos_fused_b1).  A repair
 // launch (fused_begin) takes the rows of the planes this launch marches.  Built for 7 waves / SIMD
 // (72 VGPRs; at 8 the pair operands spill: -5 %).
-template <class MT, bool SPAN1>
-__global__ __launch_bounds__(kStreamThreads, 7) void k_lanczos_fused_march(
+template <class MT, bool SPAN1, bool UNI>
+__global__ __launch_bounds__(kStreamThreads, UNI ? 8 : 7) void k_lanczos_fused_march(
     i64 nrows, i64 own, SellB1 A, MarchPlan mp, const dpair *__restrict__ P, dpair *__restrict__ Pout, FusedArgs fa,
     double *__restrict__ out, double *partials, unsigned *ticket)
 {
@@ -1159,7 +1177,7 @@ __global__ __launch_bounds__(kStreamThreads, 7) void k_lanczos_fused_march(
         m2 += uk * uk;
       }
     };
-    march_rows<MT, 2, SPAN1>(A, mp, own, lane, wave, XPair{P, c}, epi);
+    march_rows<MT, 2, SPAN1, UNI>(A, mp, own, lane, wave, XPair{P, c}, epi);
   }
   double v[3] = {d, q2, m2};
   if (grid_sum<3, kStreamThreads, 8>(v, partials, ticket, tot))
@@ -1551,6 +1569,9 @@ static int grid_for_slices(K kernel, i64 count, int num_cu)
 static bool march_enabled(const eig_mat_s &A) { return (A.kflags & EIG_MAT_NO_MARCH) == 0; }
 // Far spans of at most one offset each (u8-mask bands only: at most 8 offsets, so (-D, -1) and
 // (+1, +D) hold at most one offset each exactly when nd <= 7 with -1/0/+1 present).
+// Uniform band values in the march kernels' arguments (EIG_MAT_NO_UNIFORM keeps the array loads).
+static bool march_uniform(const eig_mat_s &A) { return A.sym_uniform && !(A.kflags & EIG_MAT_NO_UNIFORM); }
+
 static bool march_span1(const eig_mat_s &A)
 {
   int klo = A.sym_nd, khi = A.sym_nd;
@@ -1566,12 +1587,14 @@ static bool march_span1(const eig_mat_s &A)
 // have single-offset far spans).
 #define EIG_MARCH_LAUNCH(KERN, MODE, G, ...)                                                               \
   do {                                                                                                    \
-    if ((MODE) == kSymN8 && march_span1(A))                                                               \
-      hipLaunchKernelGGL((KERN<uint8_t, true>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);           \
+    if ((MODE) == kSymN8 && march_span1(A) && march_uniform(A))                                           \
+      hipLaunchKernelGGL((KERN<uint8_t, true, true>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);     \
+    else if ((MODE) == kSymN8 && march_span1(A))                                                          \
+      hipLaunchKernelGGL((KERN<uint8_t, true, false>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);    \
     else if ((MODE) == kSymN8)                                                                            \
-      hipLaunchKernelGGL((KERN<uint8_t, false>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);          \
+      hipLaunchKernelGGL((KERN<uint8_t, false, false>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);   \
     else                                                                                                  \
-      hipLaunchKernelGGL((KERN<uint32_t, false>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);         \
+      hipLaunchKernelGGL((KERN<uint32_t, false, false>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);  \
   } while (0)
 
 // Plane-marching plan for a whole-matrix launch on the lane-shift band image, or nseg = 0 when the
@@ -1632,6 +1655,21 @@ static MarchPlan march_plan(const eig_mat_s &A, int mode, i64 zb = 0, i64 ze = -
   mp.Un = A.sym_val + (i64)(klo > 1 ? A.sym_dj[1] : 0) * A.sym_ld;
   mp.dq = khi < A.sym_nd - 1 ? A.sym_off[khi] : 0;
   mp.Uq = A.sym_val + (i64)(khi < A.sym_nd - 1 ? A.sym_dj[khi] : 0) * A.sym_ld;
+  if (A.sym_uniform)
+  {
+    const int kD = A.sym_nd - 1;
+    int kz = -1, k1 = -1;
+    for (int k = 0; k < A.sym_nd; ++k)
+    {
+      if (A.sym_off[k] == 0) kz = k;
+      if (A.sym_off[k] == 1) k1 = k;
+    }
+    mp.cD = A.sym_uc[A.sym_dj[kD]];
+    mp.c0 = kz >= 0 ? A.sym_uc[A.sym_dj[kz]] : 0.0;
+    mp.c1 = k1 >= 0 ? A.sym_uc[A.sym_dj[k1]] : 0.0;
+    mp.cn = klo > 1 ? A.sym_uc[A.sym_dj[1]] : 0.0;
+    mp.cq = khi < A.sym_nd - 1 ? A.sym_uc[A.sym_dj[khi]] : 0.0;
+  }
   mp.zb = zb;
   mp.nplanes = nplanes;
   mp.mrows = A.nslices * 64;
@@ -1927,6 +1965,8 @@ void lanczos_kernel_info(const eig_mat_s &A, bool fused, std::string &name, i64 
     const bool whole = !A.ctx->distributed() || (A.recvs.empty() && A.sends.empty());
     const bool march = whole ? (march_plan(A, mode).nseg > 0)
                              : march_split_active(A);
+    // the uniform-band march streams the row mask and the vectors only
+    if (march && mode == kSymN8 && march_span1(A) && march_uniform(A)) bytes = (i64)A.sym_mask_bytes * n + vec;
     name = fused ? (march ? "k_lanczos_fused_march" : "k_lanczos_fused_b1")
                  : (march ? "k_lanczos_spmv_march" : "k_lanczos_spmv_b1");
   }

@@ -18,7 +18,7 @@ EIG_OK, EIG_ERR_SHAPE, EIG_ERR_BLOCKSIZE, EIG_ERR_HIP, EIG_ERR_RCCL, EIG_ERR_BRE
 ORTHO_MGS, ORTHO_CHOLQR, ORTHO_CHOLQR_SPLIT = 0, 1, 2
 ORTHO_GRID = 0x100  # or-ed into the variant: grid-wide MGS passes even for blocks one workgroup holds
 # matrix kernel-image flags (eig_mat_create_bcsr_ex)
-MAT_NO_BAND, MAT_BAND_GATHER, MAT_NO_STENCIL, MAT_NO_MARCH, MAT_NO_CLASS = 1, 2, 4, 8, 16
+MAT_NO_BAND, MAT_BAND_GATHER, MAT_NO_STENCIL, MAT_NO_MARCH, MAT_NO_CLASS, MAT_NO_UNIFORM = 1, 2, 4, 8, 16, 32
 # triangular-solve kernels of an LU (eig_lu_set_solver)
 TRSV_AUTO, TRSV_BLOCKINV, TRSV_STAGED, TRSV_CSR = 0, 1, 2, 3
 TRSV_KINDS = {None: TRSV_AUTO, "auto": TRSV_AUTO, "blockinv": TRSV_BLOCKINV, "staged": TRSV_STAGED, "csr": TRSV_CSR}
@@ -61,7 +61,7 @@ class _MatInfo(ctypes.Structure):
                [("br", ctypes.c_int), ("bc", ctypes.c_int)] + \
                [(k, ctypes.c_int64) for k in ("halo_recv", "halo_send", "device_bytes", "stencil_slices",
                                               "rows_per_lane", "sym_offsets", "sym_arrays",
-                                              "sym_mask_bytes")]
+                                              "sym_mask_bytes", "sym_uniform")]
 
 
 class BlockTiming(ctypes.Structure):
@@ -397,7 +397,7 @@ class Matrix:
 
     @classmethod
     def from_bcsr(cls, ctx, rowptr, col, vals, br=1, bc=1, ncols_blocks=None, flags=0):
-        """flags: MAT_NO_BAND | MAT_BAND_GATHER | MAT_NO_STENCIL | MAT_NO_MARCH | MAT_NO_CLASS
+        """flags: MAT_NO_BAND | MAT_BAND_GATHER | MAT_NO_STENCIL | MAT_NO_MARCH | MAT_NO_CLASS | MAT_NO_UNIFORM
         (eig_mat_create_bcsr_ex)."""
         rowptr = np.ascontiguousarray(rowptr, np.int64)
         col = np.ascontiguousarray(col, np.int32)
@@ -986,7 +986,8 @@ def bytes_spmv(n, nnz):
 def image_bytes(M, op, m=8):
     """Algorithmic HBM bytes of one launch sequence on M's device image:
     op "spmv" (y = A x) or "spmm" (m columns).  The symmetric band image streams 8 B per band slot
-    and the row mask once per 8-column block (the plane march); the row-class image (3-D box
+    and the row mask once per 8-column block (the plane march; a uniform band only the mask in the
+    scalar march); the row-class image (3-D box
     stencils with class-constant rows) no matrix data at all; other images the SURVEY 8(d) CSR
     count (12 B per nonzero + row pointers), which the SELL/stencil kernels stream at most."""
     info = M.info
@@ -994,6 +995,8 @@ def image_bytes(M, op, m=8):
     band = info.sym_offsets > 0
     mat = (8 * info.sym_arrays + info.sym_mask_bytes) * n if band else 12 * nnz + 4 * (n + 1)
     if op == "spmv":
+        if band and info.sym_uniform and M.kernel("spmv") == "k_spmv_march":
+            return info.sym_mask_bytes * n + 16 * n  # uniform band: the values ride in the arguments
         return mat + 16 * n
     if op == "spmm":
         if M.kernel("spmm8") == "k_boxc_mv8":  # row-class image: the class table lives in LDS

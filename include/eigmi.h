@@ -133,14 +133,17 @@ int eig_mat_create_bcsr_dist(eig_ctx_t ctx, int64_t nb_rows_global, int64_t row_
  *   EIG_MAT_NO_STENCIL   SELL slices keep explicit column indices (no per-slice offsets + row masks)
  *   EIG_MAT_NO_MARCH     no plane-marching kernels (band image: the row kernels)
  *   EIG_MAT_NO_CLASS     the 32-column box kernels keep the box image even when every row's entries
- *                        equal those of its geometric class (row-class image, k_box.hip) */
+ *                        equal those of its geometric class (row-class image, k_box.hip)
+ *   EIG_MAT_NO_UNIFORM   the plane-march kernels load the band values even when every stored entry
+ *                        of each band diagonal has one value (constant-coefficient stencils) */
 enum {
   EIG_MAT_NO_BAND = 1,
   EIG_MAT_BAND_GATHER = 2,
   EIG_MAT_NO_STENCIL = 4,
   EIG_MAT_NO_MARCH = 8,
   EIG_MAT_NO_CLASS = 16,
-  EIG_MAT_FLAGS_ALL = 31
+  EIG_MAT_NO_UNIFORM = 32,
+  EIG_MAT_FLAGS_ALL = 63
 };
 int eig_mat_create_bcsr_ex(eig_ctx_t ctx, int64_t nb_rows, int64_t nb_cols, int br, int bc,
                            const int64_t *rowptr_host, const int32_t *col_host, const double *vals_host, int flags,
@@ -170,6 +173,9 @@ typedef struct eig_mat_info {
                              Lanczos kernels then read the upper-triangle band arrays) */
   int64_t sym_arrays;     /* band arrays (distinct |offset|), 8 B per row each */
   int64_t sym_mask_bytes; /* row-mask bytes per row (1 or 4) */
+  int64_t sym_uniform;    /* 1: every stored entry of each band diagonal has one value (constant-
+                             coefficient stencil): the plane-march kernels stream the row mask and
+                             the vectors only (EIG_MAT_NO_UNIFORM: 0) */
 } eig_mat_info;
 int eig_mat_get_info(eig_mat_t mat, eig_mat_info *info);
 

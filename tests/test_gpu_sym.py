@@ -144,12 +144,48 @@ def test_march_spmv_bitwise(ctx, n, offs, drop):
 
 def test_march_kernel_names_and_bytes(ctx):
     A = oracle.poisson3d(16)
-    M = upload(ctx, A)
     n = A.n
+    # constant coefficients: the uniform-band march streams the row mask and the vectors only
+    M = upload(ctx, A)
+    assert M.lanczos_kernel_info(True) == ("k_lanczos_fused_march", n + 32 * n)
+    assert M.lanczos_kernel_info(False) == ("k_lanczos_spmv_march", n + 24 * n)
+    M = upload(ctx, A, flags=eigmi.MAT_NO_UNIFORM)
     assert M.lanczos_kernel_info(True) == ("k_lanczos_fused_march", 8 * 4 * n + n + 32 * n)
     assert M.lanczos_kernel_info(False) == ("k_lanczos_spmv_march", 8 * 4 * n + n + 24 * n)
+    B = upload(ctx, band_matrix(5000, [0, 1, 5, 128], 11))  # random values: not uniform
+    assert B.lanczos_kernel_info(True) == ("k_lanczos_fused_march", 8 * 4 * 5000 + 5000 + 32 * 5000)
     P = upload(ctx, A, sym=False)
     assert P.lanczos_kernel_info(True)[0] == "k_lanczos_fused_b1"
+
+
+@pytest.mark.parametrize("mat", ["poisson16", "poisson24", "laplace64", "laplace64neu"])
+def test_uniform_band_march_bitwise(ctx, mat):
+    """Constant-coefficient stencils (every stored entry of a band diagonal one value): the march
+    kernels take the values from their arguments instead of the band arrays.  eig_mv is bitwise the
+    reference row loop; the classic and the fused Lanczos recurrences give alpha / beta bitwise equal
+    to the array-loading kernels (EIG_MAT_NO_UNIFORM: same grid, same per-row sums), also after
+    A += sigma I (the diagonal constant follows the shift).  The Neumann Laplacian's boundary rows
+    have another diagonal value: not uniform, the arrays are loaded."""
+    A = {"poisson16": lambda: oracle.poisson3d(16), "poisson24": lambda: oracle.poisson3d(24),
+         "laplace64": lambda: oracle.laplace2d(64), "laplace64neu": lambda: oracle.laplace2d(64, "neumann")}[mat]()
+    uniform = mat != "laplace64neu"
+    M = check_mv(ctx, A, True)
+    R = upload(ctx, A, flags=eigmi.MAT_NO_UNIFORM)
+    n = A.n
+    assert M.info.sym_uniform == int(uniform) and R.info.sym_uniform == 0
+    assert M.lanczos_kernel_info(True)[1] == (n + 32 * n if uniform else R.lanczos_kernel_info(True)[1])
+    for shift in (None, 0.375):
+        if shift is not None:
+            M.shift_diag(shift)
+            R.shift_diag(shift)
+            val = A.val.copy()
+            oracle.lib.orc_shift_diag(A.n, A.rowptr, A.col, val, shift)
+            x = np.random.default_rng(3).standard_normal(n)
+            assert np.array_equal(M.mv_host(x), oracle.csr_mv(oracle.CSR(A.nrows, A.rowptr, A.col, val), x))
+        for fused in (False, True):
+            a1, b1, _ = eigmi.lanczos_run(M, 30, seed=5, fused=fused)
+            a2, b2, _ = eigmi.lanczos_run(R, 30, seed=5, fused=fused)
+            assert np.array_equal(a1, a2) and np.array_equal(b1, b2), (shift, fused)
 
 
 @pytest.mark.parametrize("fused", [False, True])
