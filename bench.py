@@ -375,7 +375,10 @@ def main():
         "config": {"workload": f"3D Poisson 7-pt {N}^3 Lanczos 3-term step, no re-orthogonalisation"
                                f" ({VARIANT_NAME[variant]})",
                    "N": N, "n": n, "nnz": nnz_total,
-                   "matrix_image": ("uniform band (constant coefficients: the 7 band values in the kernel "
+                   "matrix_image": ("uniform band on a grid (constant coefficients: the 7 band values in the "
+                                    "kernel arguments, row masks from the grid coordinates; the (t, u) pairs "
+                                    "streamed)" if M.info.sym_uniform == 2 else
+                                    "uniform band (constant coefficients: the 7 band values in the kernel "
                                     "arguments, 1-B row mask + (t, u) pairs streamed)" if M.info.sym_uniform else
                                     "symmetric band arrays + row mask" if M.info.sym_offsets else "SELL / CSR"),
                    "parallelism": (f"row-partition z-slabs x{world} (RCCL halo, {ctx.comm_info()['allreduce']} "

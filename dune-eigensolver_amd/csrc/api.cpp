@@ -917,6 +917,45 @@ void build_sym(eig_mat_s &A, i64 nb, const int64_t *rowptr, const int32_t *col, 
     A.sym_uniform = uni;
     for (int j = 0; j < nup; ++j) A.sym_uc[j] = uni ? uc[j] : 0.0;
   }
+  // geometric masks: a whole grid on one rank whose rows store exactly their in-grid neighbours
+  A.sym_geo = false;
+  if (A.sym_uniform && mb == 1 && row0 == 0 && nb == A.nb_rows_global && offs.front() == -offs.back() &&
+      (nd == 7 || nd == 5))
+  {
+    const i64 D = offs.back();
+    const i64 nx = nd == 7 ? offs[5] : D;
+    bool shape = D > 1 && nx > 1 && D % nx == 0 && nb % D == 0 && (nd == 5 || (offs[4] == 1 && offs[2] == -1 &&
+                                                                                 offs[1] == -nx && nx < D));
+    if (nd == 5) shape = shape && offs[1] == -1 && offs[3] == 1;
+    if (shape)
+    {
+      const i64 ny = D / nx, nz = nb / D;
+      std::atomic<bool> same{true};
+      parallel_slices(nb, [&](i64 r0, i64 r1) {
+        for (i64 r = r0; r < r1 && same.load(std::memory_order_relaxed); ++r)
+        {
+          const i64 x = r % nx, y = (r / nx) % ny, z = r / D;
+          unsigned e = 0;
+          int k = 0;
+          e |= (z > 0 ? 1u : 0u) << k++;
+          if (nd == 7) e |= (y > 0 ? 1u : 0u) << k++;
+          e |= (x > 0 ? 1u : 0u) << k++;
+          e |= 1u << k++;
+          e |= (x < nx - 1 ? 1u : 0u) << k++;
+          if (nd == 7) e |= (y < ny - 1 ? 1u : 0u) << k++;
+          e |= (z < nz - 1 ? 1u : 0u) << k++;
+          if (e != m8[r]) same = false;
+        }
+      });
+      if (same && nx <= INT32_MAX && ny <= INT32_MAX && nz <= INT32_MAX)
+      {
+        A.sym_geo = true;
+        A.sym_gx = (int)nx;
+        A.sym_gy = (int)ny;
+        A.sym_gz = (int)nz;
+      }
+    }
+  }
   hipStream_t s = A.ctx->stream;
   A.sym_val = dev_alloc<double>((size_t)nup * ld);
   A.sym_mask = mb == 1 ? (void *)dev_alloc<uint8_t>(ns * 64) : (void *)dev_alloc<uint32_t>(ns * 64);
@@ -1253,7 +1292,9 @@ extern "C" int eig_mat_get_info(eig_mat_t A, eig_mat_info *info)
     info->sym_offsets = A->sym_val ? A->sym_nd : 0;
     info->sym_arrays = A->sym_val ? A->sym_nup : 0;
     info->sym_mask_bytes = A->sym_val ? A->sym_mask_bytes : 0;
-    info->sym_uniform = (A->sym_val && A->sym_uniform && !(A->kflags & EIG_MAT_NO_UNIFORM)) ? 1 : 0;
+    info->sym_uniform = (A->sym_val && A->sym_uniform && !(A->kflags & EIG_MAT_NO_UNIFORM))
+                            ? (A->sym_geo && !A->ctx->distributed() ? 2 : 1)
+                            : 0;
   });
 }
 

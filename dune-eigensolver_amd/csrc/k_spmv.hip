@@ -965,6 +965,10 @@ struct MarchPlan {
   // uniform band (eig_mat_s::sym_uniform): the band values of the +D, 0, +1, far-span (dn / dq)
   // arrays, taken instead of the array loads by the UNI kernels
   double cD, c0, c1, cn, cq;
+  // geometric row masks (eig_mat_s::sym_geo, uniform bands only): the nx x ny x nz grid whose
+  // in-grid neighbours are exactly the stored entries -- the march derives each row's mask from
+  // its coordinates instead of loading it
+  int gx, gy, gz;
 };
 
 // The rows of this wave's work item, in plane order: epi(r, w, acc, centre) gets each row's sum
@@ -980,11 +984,12 @@ struct MarchPlan {
 // the same products and sums in the same order, bit for bit.  (Measured and dropped for UNI: issuing
 // plane z + 1's mask / gathers / edge operand before plane z's arithmetic -- 256^3 fused step 145 vs
 // 137 us at the 7 waves / SIMD it needs, 128^3 28.0 vs 30.7: profiles/r03bc_latency.jsonl.)
-template <class MT, int KC, bool SPAN1, bool UNI, class X, class EPI>
+template <class MT, int KC, bool SPAN1, int UNI, class X, class EPI>
 __device__ __forceinline__ void march_rows(const SellB1 &A, const MarchPlan &mp, i64 own, int lane, int wave,
                                            const X &x, EPI &epi)
 {
   static_assert(!UNI || SPAN1, "uniform-band march: far spans of at most one offset");
+  constexpr bool GEO = UNI == 2;
   typedef typename X::raw raw;
   // 32-bit row / window indices (window < 2^31, enforced at upload) keep the address math short
   const SymImg &S = A.sym;
@@ -1001,6 +1006,22 @@ __device__ __forceinline__ void march_rows(const SellB1 &A, const MarchPlan &mp,
   auto cx = [&](int g) -> unsigned { return g < 0 ? 0u : (unsigned)(g > xl ? xl : g); };
   auto cv = [&](int g) -> unsigned { return g < 0 ? 0u : (unsigned)(g > ldl ? ldl : g); };
   const int kn0 = 1, kn1 = S.klo, kp0 = S.khi, kp1 = nd - 1;  // far spans (-D, -1) and (+1, +D)
+  // GEO: the lane's row keeps its (x, y) in every plane; bit k of the mask = the neighbour at
+  // off[k] lies in the grid (verified row by row at upload)
+  unsigned gxy = 0;
+  if constexpr (GEO)
+  {
+    const int pr = col * 64 + lane, gxc = pr % mp.gx, gyc = pr / mp.gx;
+    // offsets ascending: -D, (-nx), -1, 0, +1, (+nx), +D -- the far-span bits only when present
+    unsigned b = 0;
+    int k = 1;
+    if (mp.dn) b |= (gyc > 0 ? 1u : 0u) << k++;
+    b |= (gxc > 0 ? 1u : 0u) << k++;
+    b |= 1u << k++;
+    b |= (gxc < mp.gx - 1 ? 1u : 0u) << k++;
+    if (mp.dq) b |= (gyc < mp.gy - 1 ? 1u : 0u) << k++;
+    gxy = b;
+  }
   struct Stream {
     unsigned m;
     double aD, a0, ap;
@@ -1009,10 +1030,13 @@ __device__ __forceinline__ void march_rows(const SellB1 &A, const MarchPlan &mp,
   // streams read exactly once (the row mask, the 0 / +1 / +D band values): nontemporal loads keep
   // them from evicting the (t, u) / band lines the neighbouring columns re-read from L2
   auto ld1 = [&](const double *p, unsigned i) { return __builtin_nontemporal_load(p + i); };
-  auto load_stream = [&](int w, Stream &st) {
+  auto load_stream = [&](int w, int z, Stream &st) {
     const int r = w - own32;
     const unsigned wv = (unsigned)(w > ldl ? ldl : w);
-    st.m = r < mrows ? (unsigned)__builtin_nontemporal_load(mask + (unsigned)r) : 0u;
+    if constexpr (GEO)
+      st.m = gxy | (z > 0 ? 1u : 0u) | (z < mp.gz - 1 ? 1u << kp1 : 0u);  // (z: the wave's plane)
+    else
+      st.m = r < mrows ? (unsigned)__builtin_nontemporal_load(mask + (unsigned)r) : 0u;
     st.pD = x.load(cx(w + D));
     if constexpr (UNI)
     {
@@ -1038,7 +1062,7 @@ __device__ __forceinline__ void march_rows(const SellB1 &A, const MarchPlan &mp,
   {
     const int r = w - own32;
     const unsigned wv = (unsigned)(w > ldl ? ldl : w);
-    load_stream(w, cur);
+    load_stream(w, z, cur);
     // lanes 0 / 63: the row across the wave edge (one load for both), and lane 0's mirrored -1 entry
     raw eg;
     double ae = 0.0;
@@ -1092,7 +1116,7 @@ __device__ __forceinline__ void march_rows(const SellB1 &A, const MarchPlan &mp,
 }
 
 // y[own + r] = (A x)[r] on the plane march (BCRSMatrix::mv; bitwise k_spmv_b1).
-template <class MT, bool SPAN1, bool UNI>
+template <class MT, bool SPAN1, int UNI>
 __global__ __launch_bounds__(kStreamThreads, 8) void k_spmv_march(i64 nrows, i64 own, SellB1 A, MarchPlan mp,
                                                                   const double *__restrict__ x,
                                                                   double *__restrict__ y)
@@ -1106,7 +1130,7 @@ __global__ __launch_bounds__(kStreamThreads, 8) void k_spmv_march(i64 nrows, i64
 
 // Classic Lanczos kernel 1 on the plane march (same per-row arithmetic as k_lanczos_spmv_b1; the
 // row's own u_j is the march's centre operand).
-template <class MT, bool SPAN1, bool UNI>
+template <class MT, bool SPAN1, int UNI>
 __global__ __launch_bounds__(kStreamThreads, 8) void k_lanczos_spmv_march(
     i64 nrows, i64 own, SellB1 A, MarchPlan mp, const double *__restrict__ u, const double *__restrict__ up,
     double *__restrict__ t, int j, const double *__restrict__ nsum, double *__restrict__ dot_out,
@@ -1142,7 +1166,7 @@ __global__ __launch_bounds__(kStreamThreads, 8) void k_lanczos_spmv_march(
 // Fused one-reduction step on the plane march (per-row arithmetic of k_lanczos_fused_b1).  A repair
 // launch (fused_begin) takes the rows of the planes this launch marches.  Built for 7 waves / SIMD
 // (72 VGPRs; at 8 the pair operands spill: -5 %).
-template <class MT, bool SPAN1, bool UNI>
+template <class MT, bool SPAN1, int UNI>
 __global__ __launch_bounds__(kStreamThreads, UNI ? 8 : 7) void k_lanczos_fused_march(
     i64 nrows, i64 own, SellB1 A, MarchPlan mp, const dpair *__restrict__ P, dpair *__restrict__ Pout, FusedArgs fa,
     double *__restrict__ out, double *partials, unsigned *ticket)
@@ -1570,7 +1594,13 @@ static bool march_enabled(const eig_mat_s &A) { return (A.kflags & EIG_MAT_NO_MA
 // Far spans of at most one offset each (u8-mask bands only: at most 8 offsets, so (-D, -1) and
 // (+1, +D) hold at most one offset each exactly when nd <= 7 with -1/0/+1 present).
 // Uniform band values in the march kernels' arguments (EIG_MAT_NO_UNIFORM keeps the array loads).
-static bool march_uniform(const eig_mat_s &A) { return A.sym_uniform && !(A.kflags & EIG_MAT_NO_UNIFORM); }
+// 0 = the arrays, 1 = uniform values + loaded row masks, 2 = uniform values + geometric row masks
+// (a whole-matrix launch on one rank: the grid coordinates are those of the global rows).
+static int march_uniform(const eig_mat_s &A)
+{
+  if (!A.sym_uniform || (A.kflags & EIG_MAT_NO_UNIFORM)) return 0;
+  return A.sym_geo && !A.ctx->distributed() ? 2 : 1;
+}
 
 static bool march_span1(const eig_mat_s &A)
 {
@@ -1587,14 +1617,16 @@ static bool march_span1(const eig_mat_s &A)
 // have single-offset far spans).
 #define EIG_MARCH_LAUNCH(KERN, MODE, G, ...)                                                               \
   do {                                                                                                    \
-    if ((MODE) == kSymN8 && march_span1(A) && march_uniform(A))                                           \
-      hipLaunchKernelGGL((KERN<uint8_t, true, true>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);     \
+    if ((MODE) == kSymN8 && march_span1(A) && march_uniform(A) == 2)                                      \
+      hipLaunchKernelGGL((KERN<uint8_t, true, 2>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);        \
+    else if ((MODE) == kSymN8 && march_span1(A) && march_uniform(A) == 1)                                 \
+      hipLaunchKernelGGL((KERN<uint8_t, true, 1>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);        \
     else if ((MODE) == kSymN8 && march_span1(A))                                                          \
-      hipLaunchKernelGGL((KERN<uint8_t, true, false>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);    \
+      hipLaunchKernelGGL((KERN<uint8_t, true, 0>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);        \
     else if ((MODE) == kSymN8)                                                                            \
-      hipLaunchKernelGGL((KERN<uint8_t, false, false>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);   \
+      hipLaunchKernelGGL((KERN<uint8_t, false, 0>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);       \
     else                                                                                                  \
-      hipLaunchKernelGGL((KERN<uint32_t, false, false>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);  \
+      hipLaunchKernelGGL((KERN<uint32_t, false, 0>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);      \
   } while (0)
 
 // Plane-marching plan for a whole-matrix launch on the lane-shift band image, or nseg = 0 when the
@@ -1638,7 +1670,8 @@ static MarchPlan march_plan(const eig_mat_s &A, int mode, i64 zb = 0, i64 ze = -
   //  * narrower planes (128^3: 256 columns): 12 runs 34.9 us (16: 35.5, 28: 36.5, 32: 36.7)  ->
   //    runs of >= 10 planes, as long as that leaves a quarter of the resident slots busy (64^3, 64
   //    columns: 6 runs of 10 planes took 20.1 us, 64 runs of one plane 13.3)
-  if (fused && ncol >= 1024) nseg = std::min<i64>(nplanes / 2 > 0 ? nplanes / 2 : 1, std::max<i64>(2, std::min<i64>(8, nplanes / 32)));
+  //  * (round 3, uniform-band march: 256^3 6 runs 129.8-134.0 us, 8 runs 133.6-137.1: at most 6)
+  if (fused && ncol >= 1024) nseg = std::min<i64>(nplanes / 2 > 0 ? nplanes / 2 : 1, std::max<i64>(2, std::min<i64>(6, nplanes / 32)));
   else if (fused)
     nseg = std::min(nseg, std::max<i64>({1, nplanes / 10, (resident / 4 + ncol - 1) / ncol}));
   if (A.tune_march_runs > 0) nseg = std::min<i64>(A.tune_march_runs, nplanes);  // eig_mat_tune
@@ -1669,6 +1702,9 @@ static MarchPlan march_plan(const eig_mat_s &A, int mode, i64 zb = 0, i64 ze = -
     mp.c1 = k1 >= 0 ? A.sym_uc[A.sym_dj[k1]] : 0.0;
     mp.cn = klo > 1 ? A.sym_uc[A.sym_dj[1]] : 0.0;
     mp.cq = khi < A.sym_nd - 1 ? A.sym_uc[A.sym_dj[khi]] : 0.0;
+    mp.gx = A.sym_gx;
+    mp.gy = A.sym_gy;
+    mp.gz = A.sym_gz;
   }
   mp.zb = zb;
   mp.nplanes = nplanes;
@@ -1966,7 +2002,8 @@ void lanczos_kernel_info(const eig_mat_s &A, bool fused, std::string &name, i64 
     const bool march = whole ? (march_plan(A, mode).nseg > 0)
                              : march_split_active(A);
     // the uniform-band march streams the row mask and the vectors only
-    if (march && mode == kSymN8 && march_span1(A) && march_uniform(A)) bytes = (i64)A.sym_mask_bytes * n + vec;
+    if (march && mode == kSymN8 && march_span1(A) && march_uniform(A))
+      bytes = (march_uniform(A) == 2 ? 0 : (i64)A.sym_mask_bytes * n) + vec;
     name = fused ? (march ? "k_lanczos_fused_march" : "k_lanczos_fused_b1")
                  : (march ? "k_lanczos_spmv_march" : "k_lanczos_spmv_b1");
   }

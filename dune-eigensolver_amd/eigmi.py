@@ -996,7 +996,8 @@ def image_bytes(M, op, m=8):
     mat = (8 * info.sym_arrays + info.sym_mask_bytes) * n if band else 12 * nnz + 4 * (n + 1)
     if op == "spmv":
         if band and info.sym_uniform and M.kernel("spmv") == "k_spmv_march":
-            return info.sym_mask_bytes * n + 16 * n  # uniform band: the values ride in the arguments
+            # uniform band: the values ride in the arguments (2: the row masks are geometric too)
+            return (0 if info.sym_uniform == 2 else info.sym_mask_bytes * n) + 16 * n
         return mat + 16 * n
     if op == "spmm":
         if M.kernel("spmm8") == "k_boxc_mv8":  # row-class image: the class table lives in LDS

@@ -175,7 +175,9 @@ typedef struct eig_mat_info {
   int64_t sym_mask_bytes; /* row-mask bytes per row (1 or 4) */
   int64_t sym_uniform;    /* 1: every stored entry of each band diagonal has one value (constant-
                              coefficient stencil): the plane-march kernels stream the row mask and
-                             the vectors only (EIG_MAT_NO_UNIFORM: 0) */
+                             the vectors only; 2: besides, the rows form a grid whose rows store
+                             exactly their in-grid neighbours, and the march derives the row masks
+                             from the coordinates (vectors only); EIG_MAT_NO_UNIFORM: 0 */
 } eig_mat_info;
 int eig_mat_get_info(eig_mat_t mat, eig_mat_info *info);
 

@@ -145,10 +145,11 @@ def test_march_spmv_bitwise(ctx, n, offs, drop):
 def test_march_kernel_names_and_bytes(ctx):
     A = oracle.poisson3d(16)
     n = A.n
-    # constant coefficients: the uniform-band march streams the row mask and the vectors only
+    # constant coefficients on a grid: the uniform-band march streams the vectors only (values in
+    # the arguments, row masks from the coordinates)
     M = upload(ctx, A)
-    assert M.lanczos_kernel_info(True) == ("k_lanczos_fused_march", n + 32 * n)
-    assert M.lanczos_kernel_info(False) == ("k_lanczos_spmv_march", n + 24 * n)
+    assert M.lanczos_kernel_info(True) == ("k_lanczos_fused_march", 32 * n)
+    assert M.lanczos_kernel_info(False) == ("k_lanczos_spmv_march", 24 * n)
     M = upload(ctx, A, flags=eigmi.MAT_NO_UNIFORM)
     assert M.lanczos_kernel_info(True) == ("k_lanczos_fused_march", 8 * 4 * n + n + 32 * n)
     assert M.lanczos_kernel_info(False) == ("k_lanczos_spmv_march", 8 * 4 * n + n + 24 * n)
@@ -158,22 +159,36 @@ def test_march_kernel_names_and_bytes(ctx):
     assert P.lanczos_kernel_info(True)[0] == "k_lanczos_fused_b1"
 
 
-@pytest.mark.parametrize("mat", ["poisson16", "poisson24", "laplace64", "laplace64neu"])
+def _drop_pair(A, i, d=1):
+    """A without the symmetric pair (i, i + d) / (i + d, i): still a uniform band, but row masks that
+    are no longer those of the grid."""
+    keep = np.ones(A.val.size, bool)
+    for r, c in ((i, i + d), (i + d, i)):
+        keep[A.rowptr[r] + int(np.nonzero(A.col[A.rowptr[r]:A.rowptr[r + 1]] == c)[0][0])] = False
+    counts = np.diff(A.rowptr) - np.add.reduceat(~keep, A.rowptr[:-1]).astype(np.int64)
+    rp = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+    return oracle.CSR(A.n, rp, A.col[keep].copy(), A.val[keep].copy())
+
+
+@pytest.mark.parametrize("mat", ["poisson16", "poisson24", "laplace64", "laplace64neu", "poisson16hole"])
 def test_uniform_band_march_bitwise(ctx, mat):
     """Constant-coefficient stencils (every stored entry of a band diagonal one value): the march
-    kernels take the values from their arguments instead of the band arrays.  eig_mv is bitwise the
+    kernels take the values from their arguments instead of the band arrays, and on a grid whose
+    rows store exactly their in-grid neighbours the row masks from the coordinates (poisson16hole:
+    one pair missing, so the loaded masks).  eig_mv is bitwise the
     reference row loop; the classic and the fused Lanczos recurrences give alpha / beta bitwise equal
     to the array-loading kernels (EIG_MAT_NO_UNIFORM: same grid, same per-row sums), also after
     A += sigma I (the diagonal constant follows the shift).  The Neumann Laplacian's boundary rows
     have another diagonal value: not uniform, the arrays are loaded."""
     A = {"poisson16": lambda: oracle.poisson3d(16), "poisson24": lambda: oracle.poisson3d(24),
-         "laplace64": lambda: oracle.laplace2d(64), "laplace64neu": lambda: oracle.laplace2d(64, "neumann")}[mat]()
-    uniform = mat != "laplace64neu"
+         "laplace64": lambda: oracle.laplace2d(64), "laplace64neu": lambda: oracle.laplace2d(64, "neumann"),
+         "poisson16hole": lambda: _drop_pair(oracle.poisson3d(16), 1000)}[mat]()
+    kind = {"laplace64neu": 0, "poisson16hole": 1}.get(mat, 2)  # 2: uniform values + grid masks
     M = check_mv(ctx, A, True)
     R = upload(ctx, A, flags=eigmi.MAT_NO_UNIFORM)
     n = A.n
-    assert M.info.sym_uniform == int(uniform) and R.info.sym_uniform == 0
-    assert M.lanczos_kernel_info(True)[1] == (n + 32 * n if uniform else R.lanczos_kernel_info(True)[1])
+    assert M.info.sym_uniform == kind and R.info.sym_uniform == 0
+    assert M.lanczos_kernel_info(True)[1] == {0: R.lanczos_kernel_info(True)[1], 1: n + 32 * n, 2: 32 * n}[kind]
     for shift in (None, 0.375):
         if shift is not None:
             M.shift_diag(shift)

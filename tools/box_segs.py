@@ -17,15 +17,26 @@ def main():
     Np = int(sys.argv[1]) if len(sys.argv) > 1 else 128
     Nk = int(sys.argv[2]) if len(sys.argv) > 2 else 256
     ctx = eigmi.Context(0)
-    for kind, N, ms, name in ((eigmi.GEN_POISSON3D, Np, (8, 32), "Poisson"), (eigmi.GEN_P1STIFF3D, Nk, (32,), "P1 K")):
+    var = os.environ.get("EIGMI_BOXSEG_VAR", "0") == "1"
+    cases = ((eigmi.GEN_POISSON3D, Np, (8, 32), "Poisson"), (eigmi.GEN_P1STIFF3D, Nk, (32,), "P1 K"))
+    if var:
+        # variable coefficients (a random positive diagonal term per row): the box-image kernel
+        cases = ((eigmi.GEN_P1STIFF3D, Nk, (32,), "P1 K var"), (eigmi.GEN_P1MASS3D, Nk, (32,), "P1 M var"))
+    for kind, N, ms, name in cases:
         n = N ** 3
         r, c, v = eigmi.gen_matrix(kind, N)
+        if var:
+            import numpy as np
+            rows = np.repeat(np.arange(n, dtype=np.int64), np.diff(r))
+            diag = np.nonzero(c == rows)[0]
+            v[diag] *= 1.0 + 0.01 * np.random.default_rng(1).random(n)
+            del rows, diag
         A = eigmi.Matrix.from_bcsr(ctx, r, c, v)
         del r, c, v
         for m in ms:
             X, Y = ctx.zeros(n * m), ctx.zeros(n * m)
             ctx.check(eigmi.lib.eig_fill_normal(ctx.h, n * m, 5, X.ptr))
-            for segs in (0, 1, 2, 4, 8, 12, 16, 24, 32):
+            for segs in (0, 1, 2, 3, 4, 6, 8, 12, 16, 24, 32):
                 if segs > N:
                     continue
                 A.tune(box_segs=segs)
@@ -48,6 +59,8 @@ def main():
             A.tune(box_segs=0)
             X.free(), Y.free()
         A.close()
+    if var:
+        return
     # Chebyshev step of the mass solve, 256^3, m = 32 (difference of two solve degrees)
     N = Nk
     n, m = N ** 3, 32

@@ -19,6 +19,8 @@
 #   c5 | c5si            block Lanczos 256^3: largest end / smallest end (multigrid solve)  -> c5*.jsonl
 #   c5trace              both under a kernel trace                            -> c5_trace/, c5si_trace/
 #   latency              fused step vs eig_mv across sizes and slabs, plane-run counts  -> latency.jsonl
+#   march256             fused step / eig_mv plane-run sweep at 256^3 and 128^3  -> latency.jsonl
+#   sqpmc                SQ wave-cycle buckets and TA busy of the bench (PMC)   -> sqpmc/
 #   pipe                 fused vs pipelined on one rank's slab and the cube   -> pipe.jsonl
 #   csr                  general (scrambled + RCM) 256^3 matrix: SpMV / Lanczos kernels  -> csr.jsonl
 #   csrpmc               the same under a kernel trace and FETCH_SIZE / WRITE_SIZE passes -> csrpmc/
@@ -51,6 +53,8 @@ run_task() {
       EIGMI_INV_N=200 timeout -k 10 400 python -u tools/bench_configs.py inv > "$O/cfg_inv200.jsonl" 2> "$O/cfg_inv200.err" ;;
     boxsegs)
       timeout -k 10 400 python -u tools/box_segs.py 128 256 > "$O/box_segs.jsonl" 2> "$O/box_segs.err" ;;
+    boxsegsvar)
+      EIGMI_BOXSEG_VAR=1 timeout -k 10 400 python -u tools/box_segs.py 128 256 > "$O/box_segs_var.jsonl" 2> "$O/box_segs_var.err" ;;
     inv)
       EIGMI_INV_N=64 timeout -k 10 300 python -u tools/bench_configs.py inv > "$O/cfg_inv64.jsonl" 2> "$O/cfg_inv64.err" && \
       EIGMI_INV_N=200 timeout -k 10 400 python -u tools/bench_configs.py inv > "$O/cfg_inv200.jsonl" 2> "$O/cfg_inv200.err" ;;
@@ -90,6 +94,16 @@ run_task() {
       sweep --N 256 --slab 32 --variants fused,fused@1,fused@4,fused@7,mv && \
       sweep --N 256 --slab 16 --variants fused,fused@2,fused@4,fused@7,mv && \
       sweep --N 64 --variants fused,fused@64,fused@32,fused@16,mv ;;
+    march256)
+      sweep --N 256 --variants fused,fused@16,fused@12,fused@8,fused@6,fused@4,mv && \
+      sweep --N 128 --variants fused,fused@24,fused@12,fused@8,fused@4,mv ;;
+    sqpmc)
+      # where the fused march's wave cycles go (SQ counters) and how busy the texture-address path is
+      prof_env
+      timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_VMEM --output-format csv -d "$O/sqpmc/sq" -o pmc -- \
+        python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline > /dev/null 2> "$O/sqpmc_sq.err" && \
+      timeout -s KILL 120 rocprofv3 --pmc TA_TA_BUSY_sum TA_BUSY_avr --output-format csv -d "$O/sqpmc/ta" -o pmc -- \
+        python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline > /dev/null 2> "$O/sqpmc_ta.err" ;;
     pipe)
       timeout -k 10 200 python -u tools/lanczos_sweep.py --slab 32 --variants fused,pipelined,mv --rounds 5 > "$O/pipe.jsonl" 2>&1 && \
       timeout -k 10 200 python -u tools/lanczos_sweep.py --variants fused,pipelined,mv --rounds 3 >> "$O/pipe.jsonl" 2>&1 ;;
