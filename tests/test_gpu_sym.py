@@ -159,6 +159,19 @@ def test_march_kernel_names_and_bytes(ctx):
     assert P.lanczos_kernel_info(True)[0] == "k_lanczos_fused_b1"
 
 
+def _box_poisson(nx, ny, nz):
+    """7-point Poisson (6 on the diagonal, -1 to each in-grid neighbour) on an nx x ny x nz box."""
+    import scipy.sparse as sp
+
+    def lap(k):
+        return sp.diags([-np.ones(k - 1), 2 * np.ones(k), -np.ones(k - 1)], [-1, 0, 1])
+    I = [sp.identity(k) for k in (nx, ny, nz)]
+    L = (sp.kron(sp.kron(I[2], I[1]), lap(nx)) + sp.kron(sp.kron(I[2], lap(ny)), I[0]) +
+         sp.kron(sp.kron(lap(nz), I[1]), I[0])).tocsr()
+    L.sort_indices()
+    return oracle.CSR(L.shape[0], L.indptr.astype(np.int64), L.indices.astype(np.int32), L.data.astype(np.float64))
+
+
 def _drop_pair(A, i, d=1):
     """A without the symmetric pair (i, i + d) / (i + d, i): still a uniform band, but row masks that
     are no longer those of the grid."""
@@ -170,7 +183,8 @@ def _drop_pair(A, i, d=1):
     return oracle.CSR(A.n, rp, A.col[keep].copy(), A.val[keep].copy())
 
 
-@pytest.mark.parametrize("mat", ["poisson16", "poisson24", "laplace64", "laplace64neu", "poisson16hole"])
+@pytest.mark.parametrize("mat", ["poisson16", "poisson24", "poisson32x16", "laplace64", "laplace64neu",
+                                 "poisson16hole"])
 def test_uniform_band_march_bitwise(ctx, mat):
     """Constant-coefficient stencils (every stored entry of a band diagonal one value): the march
     kernels take the values from their arguments instead of the band arrays, and on a grid whose
@@ -182,7 +196,8 @@ def test_uniform_band_march_bitwise(ctx, mat):
     have another diagonal value: not uniform, the arrays are loaded."""
     A = {"poisson16": lambda: oracle.poisson3d(16), "poisson24": lambda: oracle.poisson3d(24),
          "laplace64": lambda: oracle.laplace2d(64), "laplace64neu": lambda: oracle.laplace2d(64, "neumann"),
-         "poisson16hole": lambda: _drop_pair(oracle.poisson3d(16), 1000)}[mat]()
+         "poisson16hole": lambda: _drop_pair(oracle.poisson3d(16), 1000),
+         "poisson32x16": lambda: _box_poisson(32, 16, 20)}[mat]()
     kind = {"laplace64neu": 0, "poisson16hole": 1}.get(mat, 2)  # 2: uniform values + grid masks
     M = check_mv(ctx, A, True)
     R = upload(ctx, A, flags=eigmi.MAT_NO_UNIFORM)
