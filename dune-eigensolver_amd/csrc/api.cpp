@@ -917,24 +917,26 @@ void build_sym(eig_mat_s &A, i64 nb, const int64_t *rowptr, const int32_t *col, 
     A.sym_uniform = uni;
     for (int j = 0; j < nup; ++j) A.sym_uc[j] = uni ? uc[j] : 0.0;
   }
-  // geometric masks: a whole grid on one rank whose rows store exactly their in-grid neighbours
+  // geometric masks: a grid whose rows store exactly their in-grid neighbours -- the whole grid on
+  // one rank, or a rank's slab of whole planes (row0 and nb multiples of the plane size D; z is
+  // the global plane, so the slab's first / last planes keep their ghost-plane bits)
   A.sym_geo = false;
-  if (A.sym_uniform && mb == 1 && row0 == 0 && nb == A.nb_rows_global && offs.front() == -offs.back() &&
-      (nd == 7 || nd == 5))
+  if (A.sym_uniform && mb == 1 && offs.front() == -offs.back() && (nd == 7 || nd == 5))
   {
     const i64 D = offs.back();
     const i64 nx = nd == 7 ? offs[5] : D;
-    bool shape = D > 1 && nx > 1 && D % nx == 0 && nb % D == 0 && (nd == 5 || (offs[4] == 1 && offs[2] == -1 &&
-                                                                                 offs[1] == -nx && nx < D));
+    bool shape = D > 1 && nx > 1 && D % nx == 0 && nb % D == 0 && row0 % D == 0 && A.nb_rows_global % D == 0 &&
+                 (nd == 5 || (offs[4] == 1 && offs[2] == -1 && offs[1] == -nx && nx < D));
     if (nd == 5) shape = shape && offs[1] == -1 && offs[3] == 1;
     if (shape)
     {
-      const i64 ny = D / nx, nz = nb / D;
+      const i64 ny = D / nx, nz = A.nb_rows_global / D;
       std::atomic<bool> same{true};
       parallel_slices(nb, [&](i64 r0, i64 r1) {
         for (i64 r = r0; r < r1 && same.load(std::memory_order_relaxed); ++r)
         {
-          const i64 x = r % nx, y = (r / nx) % ny, z = r / D;
+          const i64 g = row0 + r;
+          const i64 x = g % nx, y = (g / nx) % ny, z = g / D;
           unsigned e = 0;
           int k = 0;
           e |= (z > 0 ? 1u : 0u) << k++;
@@ -953,6 +955,7 @@ void build_sym(eig_mat_s &A, i64 nb, const int64_t *rowptr, const int32_t *col, 
         A.sym_gx = (int)nx;
         A.sym_gy = (int)ny;
         A.sym_gz = (int)nz;
+        A.sym_gz0 = (int)(row0 / D);
       }
     }
   }
@@ -1293,7 +1296,7 @@ extern "C" int eig_mat_get_info(eig_mat_t A, eig_mat_info *info)
     info->sym_arrays = A->sym_val ? A->sym_nup : 0;
     info->sym_mask_bytes = A->sym_val ? A->sym_mask_bytes : 0;
     info->sym_uniform = (A->sym_val && A->sym_uniform && !(A->kflags & EIG_MAT_NO_UNIFORM))
-                            ? (A->sym_geo && !A->ctx->distributed() ? 2 : 1)
+                            ? (A->sym_geo ? 2 : 1)
                             : 0;
   });
 }

@@ -212,7 +212,7 @@ struct eig_mat_s {
   // -D, -nx, -1, 0, 1, nx, D with D = nx ny, or the 2-D -D, -1, 0, 1, D with D = nx) and every row
   // stores exactly its in-grid neighbours; the march derives the masks from the coordinates
   bool sym_geo = false;
-  int sym_gx = 0, sym_gy = 0, sym_gz = 0;
+  int sym_gx = 0, sym_gy = 0, sym_gz = 0, sym_gz0 = 0;  // grid (global planes) and this rank's first plane
   // Plane-march split of a distributed slab (k_spmv.hip march_plan): planes [mz0, mz1) have no
   // ghost columns and are marched while the halo is in flight; march_bnd lists every slice outside
   // them (the boundary launch after the exchange).  mz1 <= mz0: no split.

@@ -967,8 +967,8 @@ struct MarchPlan {
   double cD, c0, c1, cn, cq;
   // geometric row masks (eig_mat_s::sym_geo, uniform bands only): the nx x ny x nz grid whose
   // in-grid neighbours are exactly the stored entries -- the march derives each row's mask from
-  // its coordinates instead of loading it
-  int gx, gy, gz;
+  // its coordinates instead of loading it; gz0 = the global plane of the rank's first row
+  int gx, gy, gz, gz0;
 };
 
 // The rows of this wave's work item, in plane order: epi(r, w, acc, centre) gets each row's sum
@@ -1034,7 +1034,10 @@ __device__ __forceinline__ void march_rows(const SellB1 &A, const MarchPlan &mp,
     const int r = w - own32;
     const unsigned wv = (unsigned)(w > ldl ? ldl : w);
     if constexpr (GEO)
-      st.m = gxy | (z > 0 ? 1u : 0u) | (z < mp.gz - 1 ? 1u << kp1 : 0u);  // (z: the wave's plane)
+    {
+      const int zg = z + mp.gz0;  // (z: the wave's plane on this rank)
+      st.m = gxy | (zg > 0 ? 1u : 0u) | (zg < mp.gz - 1 ? 1u << kp1 : 0u);
+    }
     else
       st.m = r < mrows ? (unsigned)__builtin_nontemporal_load(mask + (unsigned)r) : 0u;
     st.pD = x.load(cx(w + D));
@@ -1595,11 +1598,11 @@ static bool march_enabled(const eig_mat_s &A) { return (A.kflags & EIG_MAT_NO_MA
 // (+1, +D) hold at most one offset each exactly when nd <= 7 with -1/0/+1 present).
 // Uniform band values in the march kernels' arguments (EIG_MAT_NO_UNIFORM keeps the array loads).
 // 0 = the arrays, 1 = uniform values + loaded row masks, 2 = uniform values + geometric row masks
-// (a whole-matrix launch on one rank: the grid coordinates are those of the global rows).
+// (the grid coordinates of the global rows: a rank's slab starts at global plane sym_gz0).
 static int march_uniform(const eig_mat_s &A)
 {
   if (!A.sym_uniform || (A.kflags & EIG_MAT_NO_UNIFORM)) return 0;
-  return A.sym_geo && !A.ctx->distributed() ? 2 : 1;
+  return A.sym_geo ? 2 : 1;
 }
 
 static bool march_span1(const eig_mat_s &A)
@@ -1705,6 +1708,7 @@ static MarchPlan march_plan(const eig_mat_s &A, int mode, i64 zb = 0, i64 ze = -
     mp.gx = A.sym_gx;
     mp.gy = A.sym_gy;
     mp.gz = A.sym_gz;
+    mp.gz0 = A.sym_gz0;
   }
   mp.zb = zb;
   mp.nplanes = nplanes;

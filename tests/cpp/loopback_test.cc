@@ -140,7 +140,7 @@ int main(int argc, char **argv)
   std::vector<std::vector<double>> fal(P, std::vector<double>(steps)), fbe(P, std::vector<double>(steps + 1));
   std::vector<std::vector<double>> y(P), al(P, std::vector<double>(steps)), be(P, std::vector<double>(steps + 1)),
       ev(P, std::vector<double>(nev));
-  std::vector<int64_t> rb(P), rc(P), halo(P);
+  std::vector<int64_t> rb(P), rc(P), halo(P), uni(P);
   std::vector<double> dots(P);
   std::vector<std::thread> th;
   for (int r = 0; r < P; ++r)
@@ -159,6 +159,7 @@ int main(int argc, char **argv)
       eig_mat_info info;
       CK(eig_mat_get_info(A, &info));
       halo[r] = info.halo_recv;
+      uni[r] = info.sym_uniform;
       // y = A x through window vectors
       double *dx, *dy, *dd;
       CK(eig_malloc(ctx, info.window * 8, (void **)&dx));
@@ -303,6 +304,13 @@ int main(int argc, char **argv)
         ++failures;
       }
   }
+  // every rank's slab of whole planes takes the geometric-mask march (global plane coordinates)
+  for (int r = 0; r < P; ++r)
+    if (uni[r] != 2)
+    {
+      std::printf("FAIL rank %d: sym_uniform %lld, expected 2 (geometric row masks)\n", r, (long long)uni[r]);
+      ++failures;
+    }
   std::printf(failures ? "FAILED %d\n" : "ALL OK (P=%d, N=%d)\n", failures ? failures : P, N);
   return failures ? 1 : 0;
 }

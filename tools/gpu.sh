@@ -19,6 +19,7 @@
 #   c5 | c5si            block Lanczos 256^3: largest end / smallest end (multigrid solve)  -> c5*.jsonl
 #   c5trace              both under a kernel trace                            -> c5_trace/, c5si_trace/
 #   latency              fused step vs eig_mv across sizes and slabs, plane-run counts  -> latency.jsonl
+#   marchcopy            the march streams alone (tools/march_copy.hip)       -> march_copy.jsonl
 #   march256             fused step / eig_mv plane-run sweep at 256^3 and 128^3  -> latency.jsonl
 #   sqpmc                SQ wave-cycle buckets and TA busy of the bench (PMC)   -> sqpmc/
 #   pipe                 fused vs pipelined on one rank's slab and the cube   -> pipe.jsonl
@@ -94,6 +95,10 @@ run_task() {
       sweep --N 256 --slab 32 --variants fused,fused@1,fused@4,fused@7,mv && \
       sweep --N 256 --slab 16 --variants fused,fused@2,fused@4,fused@7,mv && \
       sweep --N 64 --variants fused,fused@64,fused@32,fused@16,mv ;;
+    marchcopy)
+      # the march's streams without the matrix (tools/march_copy.hip, built on the CPU host)
+      timeout -k 10 120 tools/march_copy 256 > "$O/march_copy.jsonl" && \
+      timeout -k 10 60 tools/march_copy 128 >> "$O/march_copy.jsonl" ;;
     march256)
       sweep --N 256 --variants fused,fused@16,fused@12,fused@8,fused@6,fused@4,mv && \
       sweep --N 128 --variants fused,fused@24,fused@12,fused@8,fused@4,mv ;;

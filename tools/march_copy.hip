@@ -1,0 +1,174 @@
+// What bounds the plane march at 256^3?  Access-pattern microbenchmark (no matrix, no
+// reductions): the fused Lanczos step's HBM streams -- read the (t, u) pair vector once, write one
+// pair vector -- issued in the patterns the march kernels use, timed with HIP events.
+//
+//   hipcc -O3 --offload-arch=gfx950 tools/march_copy.hip -o tools/march_copy && tools/march_copy
+//
+// One JSON line per (pattern, plane runs): GB/s = 2 * n * 16 B / kernel time.
+//   linear     grid-stride 16-B copy (the reference rate)
+//   march      a wave owns a 64-row column of a plane run: load the +D pair, carry it, store the
+//              centre (the march's stream structure, one load in flight per wave)
+//   march_g    march + the two +-nx gathers of the same plane (L2 hits when the neighbour column
+//              passed first)
+//   march_pf   march with the +D pair loaded one plane ahead (two loads in flight per wave)
+//   march_2c   two columns per wave (columns c and c + ncol / 2 interleaved: two independent loads)
+//   march_t    march with temporal stores
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#include <algorithm>
+
+#define CK(x)                                                                   \
+  do {                                                                          \
+    hipError_t e_ = (x);                                                        \
+    if (e_ != hipSuccess) {                                                     \
+      std::fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      std::exit(1);                                                             \
+    }                                                                           \
+  } while (0)
+
+typedef double dpair __attribute__((ext_vector_type(2)));
+constexpr int kThreads = 256, kW = kThreads / 64;
+
+__device__ __forceinline__ int swz()
+{
+  const int G = gridDim.x, bid = blockIdx.x;
+  if (G < 16) return bid;
+  const int q = G >> 3, r = G & 7, x = bid & 7, i = bid >> 3;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
+}
+
+__global__ __launch_bounds__(kThreads) void k_linear(int n, const dpair *__restrict__ P, dpair *__restrict__ Q)
+{
+  const int stride = gridDim.x * kThreads;
+  for (int i = blockIdx.x * kThreads + threadIdx.x; i < n; i += stride)
+  {
+    dpair v = __builtin_nontemporal_load(P + i);
+    __builtin_nontemporal_store(v, Q + i);
+  }
+}
+
+// MODE 0 march, 1 march + gathers, 2 prefetch, 3 temporal stores
+template <int MODE>
+__global__ __launch_bounds__(kThreads, 8) void k_march(int n, int D, int nx, int ncol, int nseg, int nplanes,
+                                                       const dpair *__restrict__ P, dpair *__restrict__ Q)
+{
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int item = swz() * kW + wave;
+  if (item >= ncol * nseg) return;
+  const int col = item % ncol, seg = item / ncol;
+  const int z0 = seg * nplanes / nseg, z1 = (seg + 1) * nplanes / nseg;
+  const int last = n - 1;
+  auto cl = [&](int g) { return g < 0 ? 0 : (g > last ? last : g); };
+  int w = col * 64 + lane + z0 * D;
+  dpair cur = P[cl(w)];
+  dpair nxt;
+  if (MODE == 2) nxt = P[cl(w + D)];
+  for (int z = z0; z < z1; ++z, w += D)
+  {
+    dpair pd;
+    if (MODE == 2)
+    {
+      pd = nxt;
+      nxt = P[cl(w + 2 * D)];
+    }
+    else
+      pd = P[cl(w + D)];
+    dpair o = cur;
+    if (MODE == 1)
+    {
+      const dpair a = P[cl(w - nx)], b = P[cl(w + nx)];
+      o.x += a.x + b.x;
+      o.y += a.y + b.y;
+    }
+    o.x += pd.x * 1e-300;
+    if (MODE == 3)
+      Q[w] = o;
+    else
+      __builtin_nontemporal_store(o, Q + w);
+    cur = pd;
+  }
+}
+
+// two columns per wave: c and c + ncol / 2 (ncol even)
+__global__ __launch_bounds__(kThreads, 8) void k_march2(int n, int D, int ncol, int nseg, int nplanes,
+                                                        const dpair *__restrict__ P, dpair *__restrict__ Q)
+{
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int h = ncol / 2;
+  const int item = swz() * kW + wave;
+  if (item >= h * nseg) return;
+  const int col = item % h, seg = item / h;
+  const int z0 = seg * nplanes / nseg, z1 = (seg + 1) * nplanes / nseg;
+  const int last = n - 1;
+  auto cl = [&](int g) { return g < 0 ? 0 : (g > last ? last : g); };
+  int w = col * 64 + lane + z0 * D;
+  const int o2 = h * 64;
+  dpair c0 = P[cl(w)], c1 = P[cl(w + o2)];
+  for (int z = z0; z < z1; ++z, w += D)
+  {
+    const dpair p0 = P[cl(w + D)], p1 = P[cl(w + o2 + D)];
+    dpair a = c0, b = c1;
+    a.x += p0.x * 1e-300;
+    b.x += p1.x * 1e-300;
+    __builtin_nontemporal_store(a, Q + w);
+    __builtin_nontemporal_store(b, Q + w + o2);
+    c0 = p0;
+    c1 = p1;
+  }
+}
+
+int main(int argc, char **argv)
+{
+  const int N = argc > 1 ? std::atoi(argv[1]) : 256;
+  const int n = N * N * N, D = N * N, nx = N, ncol = D / 64;
+  if (D % 64 != 0 || (ncol & 1)) return 2;
+  dpair *P, *Q;
+  CK(hipMalloc(&P, (size_t)n * sizeof(dpair)));
+  CK(hipMalloc(&Q, (size_t)n * sizeof(dpair)));
+  CK(hipMemset(P, 0, (size_t)n * sizeof(dpair)));
+  CK(hipMemset(Q, 0, (size_t)n * sizeof(dpair)));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  const double bytes = 2.0 * n * sizeof(dpair);
+  auto time = [&](auto launch) {
+    for (int i = 0; i < 3; ++i) launch();
+    CK(hipDeviceSynchronize());
+    std::vector<float> t;
+    for (int i = 0; i < 20; ++i)
+    {
+      CK(hipEventRecord(e0));
+      launch();
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      t.push_back(ms);
+    }
+    std::sort(t.begin(), t.end());
+    return (double)t[t.size() / 2] * 1e3;  // median us
+  };
+  auto out = [&](const char *pat, int nseg, double us) {
+    std::printf("{\"pattern\": \"%s\", \"N\": %d, \"runs\": %d, \"us\": %.2f, \"GBs\": %.1f}\n", pat, N, nseg, us,
+                bytes / us * 1e-3);
+    std::fflush(stdout);
+  };
+  for (int g : {1024, 2048, 4096, 8192})
+    out("linear", g, time([&] { k_linear<<<g, kThreads>>>(n, P, Q); }));
+  for (int nseg : {4, 6, 8, 12, 16, 32})
+  {
+    const int items = ncol * nseg, G = (items + kW - 1) / kW;
+    out("march", nseg, time([&] { k_march<0><<<G, kThreads>>>(n, D, nx, ncol, nseg, N, P, Q); }));
+    out("march_g", nseg, time([&] { k_march<1><<<G, kThreads>>>(n, D, nx, ncol, nseg, N, P, Q); }));
+    out("march_pf", nseg, time([&] { k_march<2><<<G, kThreads>>>(n, D, nx, ncol, nseg, N, P, Q); }));
+    out("march_t", nseg, time([&] { k_march<3><<<G, kThreads>>>(n, D, nx, ncol, nseg, N, P, Q); }));
+    const int G2 = (ncol / 2 * nseg + kW - 1) / kW;
+    out("march_2c", nseg, time([&] { k_march2<<<G2, kThreads>>>(n, D, ncol, nseg, N, P, Q); }));
+  }
+  CK(hipGetLastError());
+  CK(hipFree(P));
+  CK(hipFree(Q));
+  return 0;
+}
