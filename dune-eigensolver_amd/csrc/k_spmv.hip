@@ -106,6 +106,7 @@ __device__ __forceinline__ void slice_sweep(i64 count, int wave, i64 &it0, i64 &
 struct XPlain {
   const double *__restrict__ x;
   typedef double raw;
+  __device__ __forceinline__ const void *ptr() const { return x; }
   __device__ __forceinline__ double operator()(i64 g) const { return x[g]; }
   __device__ __forceinline__ raw load(i64 g) const { return x[g]; }
   __device__ __forceinline__ double val(raw v) const { return v; }
@@ -116,6 +117,7 @@ struct XPair {
   const dpair *__restrict__ p;
   double c;
   typedef dpair raw;
+  __device__ __forceinline__ const void *ptr() const { return p; }
   __device__ __forceinline__ double operator()(i64 g) const
   {
     const dpair v = p[g];
@@ -969,7 +971,218 @@ struct MarchPlan {
   // in-grid neighbours are exactly the stored entries -- the march derives each row's mask from
   // its coordinates instead of loading it; gz0 = the global plane of the rank's first row
   int gx, gy, gz, gz0;
+  int uni;  // the march variant the launch takes (march_uniform: 0 arrays, 1 loaded masks, 2..9 geometric)
 };
+
+// Geometric uniform-band march with the +D operand loaded PF + 1 planes ahead (UNI = 2 + PF;
+// eig_mat_tune(EIG_TUNE_MARCH_PREFETCH)).  The plain march waits for every load of plane z --
+// including the +D pair that only arrives from HBM -- and, at the loop head, for the store of
+// plane z - 1 (one vmcnt counter, in order), so a wave has one plane's memory in flight.  Here the
+// plane's loads are issued gathers first, prefetch last, so the waits for the L2 gathers leave the
+// prefetch in flight; the prefetch slots rotate through a loop unrolled PF + 1 times (no register
+// moves of in-flight loads); the edge operand is loaded by every lane (lanes 1..62 fetch lane 0's,
+// one cache line) so no divergent branch merges pending loads; and there is no row test (a
+// geometric image covers whole planes: every marched row exists).  Products, sums and their order
+// are those of march_rows<UNI = 2>: bitwise the same results.
+template <int PF, bool PG, class X, class EPI>
+__device__ __forceinline__ void march_rows_geo(const SellB1 &A, const MarchPlan &mp, i64 own, int lane, int wave,
+                                               const X &x, EPI &epi)
+{
+  typedef typename X::raw raw;
+  const SymImg &S = A.sym;
+  const int xl = (int)A.xlast, D = (int)mp.D, own32 = (int)own;
+  const int nd = S.nd;
+  const int item = (int)swizzled_block() * kWaves + wave;
+  if (item >= mp.ncol * mp.nseg) return;
+  const int col = item % mp.ncol, seg = item / mp.ncol;
+  const int z0 = (int)(mp.zb + seg * mp.nplanes / mp.nseg), z1 = (int)(mp.zb + (seg + 1) * mp.nplanes / mp.nseg);
+  auto cx = [&](int g) -> unsigned { return g < 0 ? 0u : (unsigned)(g > xl ? xl : g); };
+  const int kn0 = 1, kp0 = S.khi, kp1 = nd - 1;
+  unsigned gxy = 0;
+  {
+    const int pr = col * 64 + lane, gxc = pr % mp.gx, gyc = pr / mp.gx;
+    unsigned b = 0;
+    int k = 1;
+    if (mp.dn) b |= (gyc > 0 ? 1u : 0u) << k++;
+    b |= (gxc > 0 ? 1u : 0u) << k++;
+    b |= 1u << k++;
+    b |= (gxc < mp.gx - 1 ? 1u : 0u) << k++;
+    if (mp.dq) b |= (gyc < mp.gy - 1 ? 1u : 0u) << k++;
+    gxy = b;
+  }
+  int w = own32 + col * 64 + lane + z0 * D;
+  const int eoff = lane == 63 ? 1 : -1 - lane;  // lane 63: row w + 1; the others: lane 0's row w - 1
+  // slots: plane z's pair (the centre), z + 1 (the +D operand), ..., z + PF + 1 (in flight); body k
+  // of a trip reads slots k and k + 1 and loads into slot k + PF + 1 (mod PF + 2): no slot is copied
+  constexpr int NS = PF + 2;
+  struct Gath {
+    raw eg, xn, xq;
+  };
+  auto gather = [&](int wg, Gath &g) {
+    g.eg = x.load(cx(wg + eoff));
+    if (mp.dn) g.xn = x.load(cx(wg + mp.dn));
+    if (mp.dq) g.xq = x.load(cx(wg + mp.dq));
+  };
+  double pmv = x.val(x.load(cx(w - D)));
+  raw sl[NS];
+  Gath gs[2];
+#pragma unroll
+  for (int k = 0; k <= PF; ++k) sl[k] = x.load(cx(w + k * D));
+  if constexpr (PG) gather(w, gs[0]);
+  // PG: plane z + 1's gathers are issued in body z (before its prefetch), so the wait for them in
+  // body z + 1 leaves the loads of body z + 1 in flight as well
+  auto body = [&](int z, const raw &pcur, const raw &pd, raw &pf, Gath &gc, Gath &gn) {
+    if constexpr (PG)
+      gather(w + D, gn);
+    else
+      gather(w, gc);
+    pf = x.load(cx(w + (PF + 1) * D));
+    const int zg = z + mp.gz0;
+    const unsigned m = gxy | (zg > 0 ? 1u : 0u) | (zg < mp.gz - 1 ? 1u << kp1 : 0u);
+    double acc = 0.0;
+    if (m & 1u) acc += mp.cD * pmv;
+    if (mp.dn && ((m >> kn0) & 1u)) acc += mp.cn * x.val(gc.xn);
+    const double vc = x.val(pcur);
+    double vl = lane_shift<false>(vc), vr = lane_shift<true>(vc);
+    const double ve = x.val(gc.eg);
+    if (lane == 0) vl = ve;
+    if (lane == 63) vr = ve;
+    if (S.km1 >= 0 && ((m >> S.km1) & 1u)) acc += mp.c1 * vl;
+    if (S.k0 >= 0 && ((m >> S.k0) & 1u)) acc += mp.c0 * vc;
+    if (S.kp1 >= 0 && ((m >> S.kp1) & 1u)) acc += mp.c1 * vr;
+    if (mp.dq && ((m >> kp0) & 1u)) acc += mp.cq * x.val(gc.xq);
+    if ((m >> kp1) & 1u) acc += mp.cD * x.val(pd);
+    epi(w - own32, w, acc, pcur);
+    pmv = vc;
+    w += D;
+  };
+  // (NS bodies per trip; with PG the gather sets alternate, so NS must be even)
+  static_assert(!PG || NS % 2 == 0, "gather prefetch: an even number of bodies per trip");
+  int z = z0;
+  for (; z + NS - 1 < z1; z += NS)
+  {
+#pragma unroll
+    for (int k = 0; k < NS; ++k)
+      body(z + k, sl[k], sl[(k + 1) % NS], sl[(k + PF + 1) % NS], gs[PG ? k & 1 : 0], gs[PG ? (k + 1) & 1 : 1]);
+  }
+#pragma unroll
+  for (int k = 0; k < NS - 1; ++k)
+    if (z + k < z1)
+      body(z + k, sl[k], sl[(k + 1) % NS], sl[(k + PF + 1) % NS], gs[PG ? k & 1 : 0], gs[PG ? (k + 1) & 1 : 1]);
+}
+
+// Raw buffer loads (32-bit byte offset, hardware range check: an offset at or past the descriptor's
+// byte count, or any offset through a zero-record descriptor, returns 0 without a memory access).
+__device__ __forceinline__ void bload(__amdgpu_buffer_rsrc_t r, unsigned off, dpair &v)
+{
+  v = __builtin_bit_cast(dpair, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
+}
+__device__ __forceinline__ void bload(__amdgpu_buffer_rsrc_t r, unsigned off, double &v)
+{
+  v = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0));
+}
+// lane l takes v of lane l - 1 (NEXT = false) or l + 1; the lane without a source keeps `old`
+template <bool NEXT>
+__device__ __forceinline__ double lane_shift_or(double v, double old)
+{
+  return __builtin_amdgcn_update_dpp(old, v, NEXT ? 0x130 : 0x138, 0xf, 0xf, false);
+}
+
+// Geometric uniform-band march without row masks or selects (UNI 7..9; grids whose x extent is a
+// multiple of 64, so each wave's 64 rows share one y line and one plane, and windows under 2 GiB).
+// Every stored offset of a row is its in-grid neighbour (verified at upload), so the only missing
+// terms are at the grid faces -- and a missing neighbour's operand is made EXACTLY zero instead of
+// being masked out: the -nx / +nx gathers of a wave on the first / last y line go through a
+// zero-record buffer descriptor (wave-uniform choice), the +D operand of the last global plane too
+// (plane-uniform), the -D operand of the first global plane is set to 0, and the lane-0 / lane-63
+// edge operand of a wave at x = 0 / x = nx - 1 is an out-of-range offset (the other 62 lanes'
+// edge loads are out of range as well: no traffic).  The value of a zero pair is +0 and the band
+// constant times it is +-0; acc starts at +0 and can never become -0 under round-to-nearest, so
+// acc + (+-0) == acc bit for bit (also for Inf / NaN acc): each row's sum, term order and rounding
+// are those of march_rows<UNI = 2> -- bitwise the same results -- with ~half its VALU work (no
+// mask bits, selects or 64-bit address clamps).  Prefetch slots as in march_rows_geo.
+template <int PF, bool PG, class X, class EPI>
+__device__ __forceinline__ void march_rows_geo2(const SellB1 &A, const MarchPlan &mp, i64 own, int lane, int wave,
+                                                const X &x, EPI &epi)
+{
+  typedef typename X::raw raw;
+  constexpr unsigned SZ = sizeof(raw);
+  const int D = (int)mp.D, own32 = (int)own;
+  const int item = (int)swizzled_block() * kWaves + wave;
+  if (item >= mp.ncol * mp.nseg) return;
+  const int col = item % mp.ncol, seg = item / mp.ncol;
+  const int z0 = (int)(mp.zb + seg * mp.nplanes / mp.nseg), z1 = (int)(mp.zb + (seg + 1) * mp.nplanes / mp.nseg);
+  const unsigned nbytes = (unsigned)(A.xlast + 1) * SZ;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(x.ptr()), 0, (int)nbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t r0 = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(x.ptr()), 0, 0, 0x00020000);
+  // the wave's line: first x and its y (wave-uniform)
+  const int x0 = (col * 64) % mp.gx, yw = (col * 64) / mp.gx;
+  // (2-D grids have no +-nx offsets: both gathers read zeros through r0, and cn = cq = 0, so
+  // their terms add +-0 -- no branch around a load in the loop)
+  const __amdgpu_buffer_rsrc_t rn = mp.dn && yw > 0 ? rs : r0, rq = mp.dq && yw < mp.gy - 1 ? rs : r0;
+  constexpr unsigned kOut = 0x80000000u;  // + any window offset (< 2 GiB): past the byte count
+  const unsigned eoff = lane == 0 ? (x0 > 0 ? 0u - SZ : kOut) : lane == 63 ? (x0 + 64 < mp.gx ? SZ : kOut) : kOut;
+  const unsigned dnb = (unsigned)mp.dn * SZ, dqb = (unsigned)mp.dq * SZ, Db = (unsigned)D * SZ;
+  int w = own32 + col * 64 + lane + z0 * D;
+  unsigned vo = (unsigned)w * SZ;
+  const int zg0 = z0 + mp.gz0;
+  constexpr int NS = PF + 2;
+  struct Gath {
+    raw eg, xn, xq;
+  };
+  auto gather = [&](unsigned v, Gath &g) {
+    bload(rs, v + eoff, g.eg);
+    bload(rn, v + dnb, g.xn);
+    bload(rq, v + dqb, g.xq);
+  };
+  double pmv = 0.0;
+  if (zg0 > 0)
+  {
+    raw t;
+    bload(rs, vo - Db, t);
+    pmv = x.val(t);
+  }
+  raw sl[NS];
+  bload(rs, vo, sl[0]);
+#pragma unroll
+  for (int k = 1; k <= PF; ++k) bload(zg0 + k < mp.gz ? rs : r0, vo + (unsigned)k * Db, sl[k]);
+  Gath gs[2];
+  if constexpr (PG) gather(vo, gs[0]);
+  auto body = [&](int z, const raw &pcur, const raw &pd, raw &pf, Gath &gc, Gath &gn) {
+    if constexpr (PG)
+      gather(vo + Db, gn);
+    else
+      gather(vo, gc);
+    const int zg = z + mp.gz0;
+    bload(zg + PF + 1 < mp.gz ? rs : r0, vo + (unsigned)(PF + 1) * Db, pf);
+    double acc = 0.0;
+    acc += mp.cD * pmv;
+    acc += mp.cn * x.val(gc.xn);
+    const double vc = x.val(pcur), ve = x.val(gc.eg);
+    const double vl = lane_shift_or<false>(vc, ve), vr = lane_shift_or<true>(vc, ve);
+    acc += mp.c1 * vl;
+    acc += mp.c0 * vc;
+    acc += mp.c1 * vr;
+    acc += mp.cq * x.val(gc.xq);
+    acc += mp.cD * x.val(pd);
+    epi(w - own32, w, acc, pcur);
+    pmv = vc;
+    w += D;
+    vo += Db;
+  };
+  static_assert(!PG || NS % 2 == 0, "gather prefetch: an even number of bodies per trip");
+  int z = z0;
+  for (; z + NS - 1 < z1; z += NS)
+  {
+#pragma unroll
+    for (int k = 0; k < NS; ++k)
+      body(z + k, sl[k], sl[(k + 1) % NS], sl[(k + PF + 1) % NS], gs[PG ? k & 1 : 0], gs[PG ? (k + 1) & 1 : 1]);
+  }
+#pragma unroll
+  for (int k = 0; k < NS - 1; ++k)
+    if (z + k < z1)
+      body(z + k, sl[k], sl[(k + 1) % NS], sl[(k + PF + 1) % NS], gs[PG ? k & 1 : 0], gs[PG ? (k + 1) & 1 : 1]);
+}
 
 // The rows of this wave's work item, in plane order: epi(r, w, acc, centre) gets each row's sum
 // and its own operand x[w] (raw: a double, or the (t, u) pair of the fused step).
@@ -989,6 +1202,15 @@ __device__ __forceinline__ void march_rows(const SellB1 &A, const MarchPlan &mp,
                                            const X &x, EPI &epi)
 {
   static_assert(!UNI || SPAN1, "uniform-band march: far spans of at most one offset");
+  if constexpr (UNI >= 3)
+  {
+    // 3, 4, 5: +D operand 1, 2, 3 planes ahead; 6: 3 planes ahead and the gathers one plane ahead
+    if constexpr (UNI >= 7)  // 7, 8, 9: march_rows_geo2 with the prefetches of 3, 4, 6
+      march_rows_geo2<UNI == 9 ? 2 : UNI - 7, UNI == 9>(A, mp, own, lane, wave, x, epi);
+    else
+      march_rows_geo<UNI == 6 ? 2 : UNI - 3, UNI == 6>(A, mp, own, lane, wave, x, epi);
+    return;
+  }
   constexpr bool GEO = UNI == 2;
   typedef typename X::raw raw;
   // 32-bit row / window indices (window < 2^31, enforced at upload) keep the address math short
@@ -1126,7 +1348,7 @@ __global__ __launch_bounds__(kStreamThreads, 8) void k_spmv_march(i64 nrows, i64
 {
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   auto epi = [&](int r, int w, double acc, double) {
-    if (r < nrows) __builtin_nontemporal_store(acc, y + (unsigned)w);
+    if (UNI >= 3 || r < nrows) __builtin_nontemporal_store(acc, y + (unsigned)w);  // (geometric: whole planes)
   };
   march_rows<MT, 2, SPAN1, UNI>(A, mp, own, lane, wave, XPlain{x}, epi);
 }
@@ -1169,8 +1391,14 @@ __global__ __launch_bounds__(kStreamThreads, 8) void k_lanczos_spmv_march(
 // Fused one-reduction step on the plane march (per-row arithmetic of k_lanczos_fused_b1).  A repair
 // launch (fused_begin) takes the rows of the planes this launch marches.  Built for 7 waves / SIMD
 // (72 VGPRs; at 8 the pair operands spill: -5 %).
+// resident waves per SIMD the fused march kernels are built for (registers: no spills)
+constexpr int march_fused_waves(int uni)
+{
+  return uni == 6 || uni == 9 ? 4 : uni == 5 ? 5 : uni == 4 || uni == 8 ? 6 : uni == 3 || uni == 7 ? 7 : uni ? 8 : 7;
+}
+
 template <class MT, bool SPAN1, int UNI>
-__global__ __launch_bounds__(kStreamThreads, UNI ? 8 : 7) void k_lanczos_fused_march(
+__global__ __launch_bounds__(kStreamThreads, march_fused_waves(UNI)) void k_lanczos_fused_march(
     i64 nrows, i64 own, SellB1 A, MarchPlan mp, const dpair *__restrict__ P, dpair *__restrict__ Pout, FusedArgs fa,
     double *__restrict__ out, double *partials, unsigned *ticket)
 {
@@ -1193,7 +1421,7 @@ __global__ __launch_bounds__(kStreamThreads, UNI ? 8 : 7) void k_lanczos_fused_m
   else
   {
     auto epi = [&](int r, int w, double acc, dpair pc) {
-      if (r < nrows)
+      if (UNI >= 3 || r < nrows)  // (geometric images cover whole planes: no row test)
       {
         const double uk = pc.x - c * pc.y;
         double ti = (acc - mu * uk) * sig;
@@ -1598,11 +1826,29 @@ static bool march_enabled(const eig_mat_s &A) { return (A.kflags & EIG_MAT_NO_MA
 // (+1, +D) hold at most one offset each exactly when nd <= 7 with -1/0/+1 present).
 // Uniform band values in the march kernels' arguments (EIG_MAT_NO_UNIFORM keeps the array loads).
 // 0 = the arrays, 1 = uniform values + loaded row masks, 2 = uniform values + geometric row masks
-// (the grid coordinates of the global rows: a rank's slab starts at global plane sym_gz0).
-static int march_uniform(const eig_mat_s &A)
+// (the grid coordinates of the global rows: a rank's slab starts at global plane sym_gz0);
+// 3 / 4 / 5: geometric, march_rows_geo with the +D operand 1 / 2 / 3 planes ahead, 6: 3 planes
+// ahead and the gathers 1 plane ahead (eig_mat_tune(EIG_TUNE_MARCH_PREFETCH) = 1 forces 2, 2..5
+// force 3..6; 0 = kGeoAuto).
+// 7 / 8 / 9: march_rows_geo2 (no masks or selects; x extent a multiple of 64, window < 2 GiB) with
+// the prefetches of 3 / 4 / 6 (tune values 6..8); a geo2 request on a grid that does not qualify
+// takes the corresponding march_rows_geo variant.
+// Automatic choice (measured: profiles/r03bj_latency.jsonl, tools/gpu.sh prefetch): geo2 where the
+// grid allows it -- the fused step with the +D operand one plane ahead (8) up to 128 planes per
+// launch (128^3: 25.2 us vs 30.3 for the plain march; one rank's 256^2 x 32 slab: 24.3 vs 34.5),
+// without prefetch (7) on deeper grids (256^3: 126.0 us at 8 plane runs vs 131.6); eig_mv and the
+// classic K1 without prefetch (7; eig_mv 256^3 46.1 us vs 59.4, 128^3 8.0 vs 12.1).  Grids geo2 does
+// not take: march_rows_geo with the +D operand two planes ahead (4).
+static int march_uniform(const eig_mat_s &A, bool fused = false, i64 nplanes = 0)
 {
   if (!A.sym_uniform || (A.kflags & EIG_MAT_NO_UNIFORM)) return 0;
-  return A.sym_geo ? 2 : 1;
+  if (!A.sym_geo) return 1;
+  const bool geo2 = A.sym_gx % 64 == 0 && A.window * 16 < (i64(1) << 31);
+  int u = A.tune_march_prefetch > 0 ? 1 + A.tune_march_prefetch
+          : geo2                    ? (fused && nplanes <= 128 ? 8 : 7)
+                                    : 4;
+  if (u >= 7 && !geo2) u = u == 9 ? 6 : u - 4;
+  return u;
 }
 
 static bool march_span1(const eig_mat_s &A)
@@ -1620,9 +1866,23 @@ static bool march_span1(const eig_mat_s &A)
 // have single-offset far spans).
 #define EIG_MARCH_LAUNCH(KERN, MODE, G, ...)                                                               \
   do {                                                                                                    \
-    if ((MODE) == kSymN8 && march_span1(A) && march_uniform(A) == 2)                                      \
+    if ((MODE) == kSymN8 && march_span1(A) && mp.uni == 9)                                      \
+      hipLaunchKernelGGL((KERN<uint8_t, true, 9>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);        \
+    else if ((MODE) == kSymN8 && march_span1(A) && mp.uni == 8)                                 \
+      hipLaunchKernelGGL((KERN<uint8_t, true, 8>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);        \
+    else if ((MODE) == kSymN8 && march_span1(A) && mp.uni == 7)                                 \
+      hipLaunchKernelGGL((KERN<uint8_t, true, 7>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);        \
+    else if ((MODE) == kSymN8 && march_span1(A) && mp.uni == 6)                                 \
+      hipLaunchKernelGGL((KERN<uint8_t, true, 6>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);        \
+    else if ((MODE) == kSymN8 && march_span1(A) && mp.uni == 5)                                 \
+      hipLaunchKernelGGL((KERN<uint8_t, true, 5>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);        \
+    else if ((MODE) == kSymN8 && march_span1(A) && mp.uni == 4)                                 \
+      hipLaunchKernelGGL((KERN<uint8_t, true, 4>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);        \
+    else if ((MODE) == kSymN8 && march_span1(A) && mp.uni == 3)                                 \
+      hipLaunchKernelGGL((KERN<uint8_t, true, 3>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);        \
+    else if ((MODE) == kSymN8 && march_span1(A) && mp.uni == 2)                                 \
       hipLaunchKernelGGL((KERN<uint8_t, true, 2>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);        \
-    else if ((MODE) == kSymN8 && march_span1(A) && march_uniform(A) == 1)                                 \
+    else if ((MODE) == kSymN8 && march_span1(A) && mp.uni == 1)                                 \
       hipLaunchKernelGGL((KERN<uint8_t, true, 1>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);        \
     else if ((MODE) == kSymN8 && march_span1(A))                                                          \
       hipLaunchKernelGGL((KERN<uint8_t, true, 0>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);        \
@@ -1674,7 +1934,10 @@ static MarchPlan march_plan(const eig_mat_s &A, int mode, i64 zb = 0, i64 ze = -
   //    runs of >= 10 planes, as long as that leaves a quarter of the resident slots busy (64^3, 64
   //    columns: 6 runs of 10 planes took 20.1 us, 64 runs of one plane 13.3)
   //  * (round 3, uniform-band march: 256^3 6 runs 129.8-134.0 us, 8 runs 133.6-137.1: at most 6)
-  if (fused && ncol >= 1024) nseg = std::min<i64>(nplanes / 2 > 0 ? nplanes / 2 : 1, std::max<i64>(2, std::min<i64>(6, nplanes / 32)));
+  const int uni = march_uniform(A, fused, nplanes);
+  if (fused && ncol >= 1024)
+    nseg = std::min<i64>(nplanes / 2 > 0 ? nplanes / 2 : 1,
+                         std::max<i64>(2, std::min<i64>(uni == 7 ? 8 : 6, nplanes / 32)));
   else if (fused)
     nseg = std::min(nseg, std::max<i64>({1, nplanes / 10, (resident / 4 + ncol - 1) / ncol}));
   if (A.tune_march_runs > 0) nseg = std::min<i64>(A.tune_march_runs, nplanes);  // eig_mat_tune
@@ -1710,6 +1973,7 @@ static MarchPlan march_plan(const eig_mat_s &A, int mode, i64 zb = 0, i64 ze = -
     mp.gz = A.sym_gz;
     mp.gz0 = A.sym_gz0;
   }
+  mp.uni = uni;
   mp.zb = zb;
   mp.nplanes = nplanes;
   mp.mrows = A.nslices * 64;
@@ -2007,7 +2271,7 @@ void lanczos_kernel_info(const eig_mat_s &A, bool fused, std::string &name, i64 
                              : march_split_active(A);
     // the uniform-band march streams the row mask and the vectors only
     if (march && mode == kSymN8 && march_span1(A) && march_uniform(A))
-      bytes = (march_uniform(A) == 2 ? 0 : (i64)A.sym_mask_bytes * n) + vec;
+      bytes = (march_uniform(A) >= 2 ? 0 : (i64)A.sym_mask_bytes * n) + vec;
     name = fused ? (march ? "k_lanczos_fused_march" : "k_lanczos_fused_b1")
                  : (march ? "k_lanczos_spmv_march" : "k_lanczos_spmv_b1");
   }

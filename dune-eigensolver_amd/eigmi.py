@@ -460,12 +460,16 @@ class Matrix:
         self.ctx.check(lib.eig_mv_host(self.h, _np_ptr(x), _np_ptr(y)))
         return y
 
-    def tune(self, march_runs=0, box_segs=None):
+    def tune(self, march_runs=0, box_segs=None, march_prefetch=None):
         """eig_mat_tune: EIG_TUNE_MARCH_RUNS = plane runs per column of the plane-march kernels,
-        EIG_TUNE_BOX_SEGS = z segments per tile column of the box kernels (0 = automatic)."""
+        EIG_TUNE_BOX_SEGS = z segments per tile column of the box kernels, EIG_TUNE_MARCH_PREFETCH =
+        the geometric march variant (1 plain, 2-4 the +D operand 1-3 planes ahead, 5 + gathers one
+        plane ahead; 0 = automatic)."""
         self.ctx.check(lib.eig_mat_tune(self.h, 1, int(march_runs)))
         if box_segs is not None:
             self.ctx.check(lib.eig_mat_tune(self.h, 2, int(box_segs)))
+        if march_prefetch is not None:
+            self.ctx.check(lib.eig_mat_tune(self.h, 3, int(march_prefetch)))
 
     def shift_diag(self, shift):
         self.ctx.check(lib.eig_mat_shift_diag(self.h, shift))

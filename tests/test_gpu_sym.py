@@ -544,3 +544,31 @@ def test_box_chebyshev_first_step_after_other_class_table(ctx):
         a, b = X1.get(), X2.get()
         assert np.all(np.isfinite(a))
         assert np.allclose(a, b, rtol=1e-13, atol=1e-14 * np.abs(b).max()), (degree, np.abs(a - b).max())
+
+
+@pytest.mark.parametrize("mat", ["poisson16", "poisson24", "laplace64", "poisson32x16"])
+def test_geometric_march_prefetch_bitwise(ctx, mat):
+    """The geometric march variants (eig_mat_tune EIG_TUNE_MARCH_PREFETCH: 1 = plain march_rows, 2-4 =
+    march_rows_geo with the +D operand 1-3 planes ahead, 5 = plus the gathers one plane ahead; 6-8 =
+    march_rows_geo2: no masks or selects, missing neighbours read as exact zeros) only reorder loads
+    or add exact zeros: eig_mv bitwise the reference row loop, classic and fused Lanczos alpha / beta
+    bitwise equal to the plain march at the same plane runs -- including runs whose plane counts leave
+    every remainder of the unrolled loop (1, 2, 3, 5 and 7 runs)."""
+    A = {"poisson16": lambda: oracle.poisson3d(16), "poisson24": lambda: oracle.poisson3d(24),
+         "laplace64": lambda: oracle.laplace2d(64), "poisson32x16": lambda: _box_poisson(32, 16, 20)}[mat]()
+    M = check_mv(ctx, A, True)
+    assert M.info.sym_uniform == 2
+    x = np.random.default_rng(11).standard_normal(A.n)
+    ref_mv = oracle.csr_mv(A, x)
+    for runs in (0, 1, 2, 3, 5, 7):
+        base = {}
+        for pf in (1, 2, 3, 4, 5, 6, 7, 8):
+            M.tune(runs, march_prefetch=pf)
+            assert np.array_equal(M.mv_host(x), ref_mv), (runs, pf)
+            for fused in (False, True):
+                a, b, _ = eigmi.lanczos_run(M, 25, seed=7, fused=fused)
+                if pf == 1:
+                    base[fused] = (a, b)
+                else:
+                    assert np.array_equal(a, base[fused][0]) and np.array_equal(b, base[fused][1]), (runs, pf, fused)
+    M.tune(0, march_prefetch=0)

@@ -20,6 +20,7 @@
 #   c5trace              both under a kernel trace                            -> c5_trace/, c5si_trace/
 #   latency              fused step vs eig_mv across sizes and slabs, plane-run counts  -> latency.jsonl
 #   marchcopy            the march streams alone (tools/march_copy.hip)       -> march_copy.jsonl
+#   prefetch             geometric march prefetch variants x plane runs (256^3, 128^3, slab) -> latency.jsonl
 #   march256             fused step / eig_mv plane-run sweep at 256^3 and 128^3  -> latency.jsonl
 #   sqpmc                SQ wave-cycle buckets and TA busy of the bench (PMC)   -> sqpmc/
 #   pipe                 fused vs pipelined on one rank's slab and the cube   -> pipe.jsonl
@@ -99,6 +100,12 @@ run_task() {
       # the march's streams without the matrix (tools/march_copy.hip, built on the CPU host)
       timeout -k 10 120 tools/march_copy 256 > "$O/march_copy.jsonl" && \
       timeout -k 10 60 tools/march_copy 128 >> "$O/march_copy.jsonl" ;;
+    prefetch)
+      # geometric march variants (eig_mat_tune EIG_TUNE_MARCH_PREFETCH #1..#5) x plane runs
+      sweep --N 256 --variants fused@6#1,fused@6#6,fused@8#6,fused@6#7,fused@4#8,fused@8#7,fused@4#5,mv#1,mv#5,mv#6,mv#7,mv#8 && \
+      sweep --N 128 --variants fused#1,fused#5,fused#6,fused#7,fused#8,fused@16#7,fused@6#8,mv#1,mv#5,mv#6,mv#7 && \
+      sweep --N 256 --slab 32 --variants fused#1,fused#5,fused#6,fused#7,fused#8,mv#5,mv#6,mv#7 && \
+      sweep --N 256 --slab 16 --variants fused#1,fused#5,fused#7,fused#8 ;;
     march256)
       sweep --N 256 --variants fused,fused@16,fused@12,fused@8,fused@6,fused@4,mv && \
       sweep --N 128 --variants fused,fused@24,fused@12,fused@8,fused@4,mv ;;

@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """A/B of Lanczos step / SpMV kernel images on one GPU, interleaved rounds in ONE process.
 
-Variant spec "<fused|pipelined|classic|mv>[:<image>][@<runs>]" (runs: plane runs per column of the
-march kernels, eig_mat_tune; default automatic) with image one of
+Variant spec "<fused|pipelined|classic|mv>[:<image>][@<runs>][#<pf>]" (runs: plane runs per column of
+the march kernels, pf: the geometric march variant, eig_mat_tune; default automatic) with image one of
     band     (default) symmetric band image, plane march where the band allows it
     gather   band image, every offset through its own gather (EIG_MAT_BAND_GATHER)
     nomarch  band image, row kernels (EIG_MAT_NO_MARCH)
@@ -29,10 +29,12 @@ IMAGES = {"band": 0, "gather": eigmi.MAT_BAND_GATHER, "nomarch": eigmi.MAT_NO_MA
 
 
 def parse(spec):
-    """"op[:image][@runs]" -> (op, image flags, plane runs per column (0 = automatic))."""
+    """"op[:image][@runs][#pf]" -> (op, image flags, plane runs per column (0 = automatic),
+    geometric march variant (eig_mat_tune EIG_TUNE_MARCH_PREFETCH; 0 = automatic))."""
+    spec, _, pf = spec.partition("#")
     spec, _, runs = spec.partition("@")
     parts = spec.split(":")
-    return parts[0], IMAGES[parts[1] if len(parts) > 1 else "band"], int(runs or 0)
+    return parts[0], IMAGES[parts[1] if len(parts) > 1 else "band"], int(runs or 0), int(pf or 0)
 
 
 def main():
@@ -73,9 +75,9 @@ def main():
     xy = None
     for _ in range(args.rounds):
         for spec in specs:
-            op, fl, runs = parse(spec)
+            op, fl, runs, pf = parse(spec)
             M = mats[fl]
-            M.tune(runs)
+            M.tune(runs, march_prefetch=pf)
             if op == "mv":  # plain eig_mv (BCRSMatrix::mv) launches
                 if xy is None:
                     xy = (ctx.array(np.random.default_rng(0).standard_normal(n)), ctx.zeros(n))
@@ -91,9 +93,9 @@ def main():
             res[spec]["step_us"].append(t.total_ms / args.steps * 1e3)
             ws.close()
     for spec in specs:
-        op, fl, runs = parse(spec)
+        op, fl, runs, pf = parse(spec)
         M = mats[fl]
-        M.tune(runs)
+        M.tune(runs, march_prefetch=pf)
         kb = (eigmi.bytes_spmv(n, nnz) if op == "mv" else
               eigmi.bytes_spmv(n, nnz) + 56 * n if op == "pipelined" else
               eigmi.bytes_lanczos_fused(n, nnz) if op == "fused" else eigmi.bytes_lanczos_k1(n, nnz))

@@ -13,6 +13,8 @@
 //   march_pf   march with the +D pair loaded one plane ahead (two loads in flight per wave)
 //   march_2c   two columns per wave (columns c and c + ncol / 2 interleaved: two independent loads)
 //   march_t    march with temporal stores
+//   *_pp       ping-pong: consecutive launches swap the input and output vectors, as the Lanczos
+//              step does (its output pairs are the next step's input)
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
@@ -133,14 +135,16 @@ int main(int argc, char **argv)
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   const double bytes = 2.0 * n * sizeof(dpair);
+  int rep = 0;  // ping-pong launches read P on even reps, Q on odd ones
   auto time = [&](auto launch) {
-    for (int i = 0; i < 3; ++i) launch();
+    for (int i = 0; i < 3; ++i, ++rep) launch();
     CK(hipDeviceSynchronize());
     std::vector<float> t;
     for (int i = 0; i < 20; ++i)
     {
       CK(hipEventRecord(e0));
       launch();
+      ++rep;
       CK(hipEventRecord(e1));
       CK(hipEventSynchronize(e1));
       float ms;
@@ -157,6 +161,16 @@ int main(int argc, char **argv)
   };
   for (int g : {1024, 2048, 4096, 8192})
     out("linear", g, time([&] { k_linear<<<g, kThreads>>>(n, P, Q); }));
+  auto src = [&] { return rep & 1 ? Q : P; };
+  auto dst = [&] { return rep & 1 ? P : Q; };
+  out("linear_pp", 2048, time([&] { k_linear<<<2048, kThreads>>>(n, src(), dst()); }));
+  for (int nseg : {6, 8})
+  {
+    const int items = ncol * nseg, G = (items + kW - 1) / kW;
+    out("march_pp", nseg, time([&] { k_march<0><<<G, kThreads>>>(n, D, nx, ncol, nseg, N, src(), dst()); }));
+    out("march_g_pp", nseg, time([&] { k_march<1><<<G, kThreads>>>(n, D, nx, ncol, nseg, N, src(), dst()); }));
+    out("march_t_pp", nseg, time([&] { k_march<3><<<G, kThreads>>>(n, D, nx, ncol, nseg, N, src(), dst()); }));
+  }
   for (int nseg : {4, 6, 8, 12, 16, 32})
   {
     const int items = ncol * nseg, G = (items + kW - 1) / kW;
