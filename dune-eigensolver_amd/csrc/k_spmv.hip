@@ -1101,9 +1101,15 @@ __device__ __forceinline__ double lane_shift_or(double v, double old)
 // acc + (+-0) == acc bit for bit (also for Inf / NaN acc): each row's sum, term order and rounding
 // are those of march_rows<UNI = 2> -- bitwise the same results -- with ~half its VALU work (no
 // mask bits, selects or 64-bit address clamps).  Prefetch slots as in march_rows_geo.
-template <int PF, bool PG, class X, class EPI>
+// pre(x): called once the wave's first loads are in flight (the fused step's scalar prologue runs
+// under them; it sets x's scalars); false = the launch does not march (the loads are dropped).
+struct MarchNoPre {
+  template <class X>
+  __device__ __forceinline__ bool operator()(X &) const { return true; }
+};
+template <int PF, bool PG, class X, class EPI, class PRE>
 __device__ __forceinline__ void march_rows_geo2(const SellB1 &A, const MarchPlan &mp, i64 own, int lane, int wave,
-                                                const X &x, EPI &epi)
+                                                X x, EPI &epi, PRE &pre)
 {
   typedef typename X::raw raw;
   constexpr unsigned SZ = sizeof(raw);
@@ -1135,19 +1141,16 @@ __device__ __forceinline__ void march_rows_geo2(const SellB1 &A, const MarchPlan
     bload(rn, v + dnb, g.xn);
     bload(rq, v + dqb, g.xq);
   };
-  double pmv = 0.0;
-  if (zg0 > 0)
-  {
-    raw t;
-    bload(rs, vo - Db, t);
-    pmv = x.val(t);
-  }
+  raw pm{};
+  if (zg0 > 0) bload(rs, vo - Db, pm);  // (plane 0 of the grid: no -D neighbour)
   raw sl[NS];
   bload(rs, vo, sl[0]);
 #pragma unroll
   for (int k = 1; k <= PF; ++k) bload(zg0 + k < mp.gz ? rs : r0, vo + (unsigned)k * Db, sl[k]);
   Gath gs[2];
   if constexpr (PG) gather(vo, gs[0]);
+  if (!pre(x)) return;
+  double pmv = zg0 > 0 ? x.val(pm) : 0.0;
   auto body = [&](int z, const raw &pcur, const raw &pd, raw &pf, Gath &gc, Gath &gn) {
     if constexpr (PG)
       gather(vo + Db, gn);
@@ -1197,16 +1200,16 @@ __device__ __forceinline__ void march_rows_geo2(const SellB1 &A, const MarchPlan
 // the same products and sums in the same order, bit for bit.  (Measured and dropped for UNI: issuing
 // plane z + 1's mask / gathers / edge operand before plane z's arithmetic -- 256^3 fused step 145 vs
 // 137 us at the 7 waves / SIMD it needs, 128^3 28.0 vs 30.7: profiles/r03bc_latency.jsonl.)
-template <class MT, int KC, bool SPAN1, int UNI, class X, class EPI>
+template <class MT, int KC, bool SPAN1, int UNI, class X, class EPI, class PRE = MarchNoPre>
 __device__ __forceinline__ void march_rows(const SellB1 &A, const MarchPlan &mp, i64 own, int lane, int wave,
-                                           const X &x, EPI &epi)
+                                           const X &x, EPI &epi, PRE &&pre = PRE{})
 {
   static_assert(!UNI || SPAN1, "uniform-band march: far spans of at most one offset");
   if constexpr (UNI >= 3)
   {
     // 3, 4, 5: +D operand 1, 2, 3 planes ahead; 6: 3 planes ahead and the gathers one plane ahead
     if constexpr (UNI >= 7)  // 7, 8, 9: march_rows_geo2 with the prefetches of 3, 4, 6
-      march_rows_geo2<UNI == 9 ? 2 : UNI - 7, UNI == 9>(A, mp, own, lane, wave, x, epi);
+      march_rows_geo2<UNI == 9 ? 2 : UNI - 7, UNI == 9>(A, mp, own, lane, wave, x, epi, pre);
     else
       march_rows_geo<UNI == 6 ? 2 : UNI - 3, UNI == 6>(A, mp, own, lane, wave, x, epi);
     return;
@@ -1404,6 +1407,47 @@ __global__ __launch_bounds__(kStreamThreads, march_fused_waves(UNI)) void k_lanc
 {
   __shared__ double tot[3];
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  double d = 0.0, q2 = 0.0, m2 = 0.0;
+  if constexpr (UNI >= 7)
+  {
+    // geo2: the scalar prologue runs while the wave's first plane loads are in flight (the march
+    // calls `pre` after issuing them); waves without a work item run it after the march returns
+    FusedStep fs{};
+    bool begun = false;
+    auto epi = [&](int, int w, double acc, dpair pc) {
+      const double uk = pc.x - fs.c * pc.y;
+      double ti = (acc - fs.mu * uk) * fs.sig;
+      if (fs.j > 0) ti = ti - fs.gam * pc.y;
+      __builtin_nontemporal_store(dpair{ti, uk}, Pout + (unsigned)w);
+      d += ti * uk;
+      q2 += ti * ti;
+      m2 += uk * uk;
+    };
+    auto pre = [&](XPair &x) {
+      fs = fused_begin(fa);
+      begun = true;
+      x.c = fs.c;
+      return fs.act == kFusedStep || fs.act == kFusedPost;
+    };
+    march_rows<MT, 2, SPAN1, UNI>(A, mp, own, lane, wave, XPair{P, 0.0}, epi, pre);
+    if (!begun) fs = fused_begin(fa);
+    if (fs.act == kFusedHalt || fs.act == kFusedNoop)
+    {
+      fused_idle(out);
+      return;
+    }
+    if (fs.act == kFusedRepair)
+    {
+      const i64 r0 = mp.zb * mp.D, r1 = std::min<i64>(nrows, (mp.zb + mp.nplanes) * mp.D);
+      m2 = fused_repair_rows(r0, r1, own, fs.c, P, Pout);
+    }
+    double v[3] = {d, q2, m2};
+    if (grid_sum<3, kStreamThreads, 8>(v, partials, ticket, tot))
+    {
+      if (threadIdx.x < 3) out[threadIdx.x] = tot[threadIdx.x];
+    }
+    return;
+  }
   const FusedStep fs = fused_begin(fa);
   if (fs.act == kFusedHalt || fs.act == kFusedNoop)
   {
@@ -1412,7 +1456,6 @@ __global__ __launch_bounds__(kStreamThreads, march_fused_waves(UNI)) void k_lanc
   }
   const double c = fs.c, gam = fs.gam, sig = fs.sig, mu = fs.mu;
   const int k = fs.j;
-  double d = 0.0, q2 = 0.0, m2 = 0.0;
   if (fs.act == kFusedRepair)
   {
     const i64 r0 = mp.zb * mp.D, r1 = std::min<i64>(nrows, (mp.zb + mp.nplanes) * mp.D);
@@ -1938,8 +1981,8 @@ static MarchPlan march_plan(const eig_mat_s &A, int mode, i64 zb = 0, i64 ze = -
   if (fused && ncol >= 1024)
     nseg = std::min<i64>(nplanes / 2 > 0 ? nplanes / 2 : 1,
                          std::max<i64>(2, std::min<i64>(uni == 7 ? 8 : 6, nplanes / 32)));
-  else if (fused)
-    nseg = std::min(nseg, std::max<i64>({1, nplanes / 10, (resident / 4 + ncol - 1) / ncol}));
+  else if (fused)  // (geo2 marches: runs of >= 16 planes -- 128^3 8 runs 24.3 us, 12: 25.3, 16: 26.4)
+    nseg = std::min(nseg, std::max<i64>({1, nplanes / (uni >= 7 ? 16 : 10), (resident / 4 + ncol - 1) / ncol}));
   if (A.tune_march_runs > 0) nseg = std::min<i64>(A.tune_march_runs, nplanes);  // eig_mat_tune
   while (nseg > 1 && (ncol * nseg + kWaves - 1) / kWaves > kMaxRedBlocks) --nseg;
   if ((ncol * nseg + kWaves - 1) / kWaves > kMaxRedBlocks) return mp;

@@ -21,6 +21,7 @@
 #   latency              fused step vs eig_mv across sizes and slabs, plane-run counts  -> latency.jsonl
 #   marchcopy            the march streams alone (tools/march_copy.hip)       -> march_copy.jsonl
 #   prefetch             geometric march prefetch variants x plane runs (256^3, 128^3, slab) -> latency.jsonl
+#   slabruns             plane runs on the per-rank slabs and 128^3 with the geo2 variants -> latency.jsonl
 #   march256             fused step / eig_mv plane-run sweep at 256^3 and 128^3  -> latency.jsonl
 #   sqpmc                SQ wave-cycle buckets and TA busy of the bench (PMC)   -> sqpmc/
 #   pipe                 fused vs pipelined on one rank's slab and the cube   -> pipe.jsonl
@@ -106,6 +107,11 @@ run_task() {
       sweep --N 128 --variants fused#1,fused#5,fused#6,fused#7,fused#8,fused@16#7,fused@6#8,mv#1,mv#5,mv#6,mv#7 && \
       sweep --N 256 --slab 32 --variants fused#1,fused#5,fused#6,fused#7,fused#8,mv#5,mv#6,mv#7 && \
       sweep --N 256 --slab 16 --variants fused#1,fused#5,fused#7,fused#8 ;;
+    slabruns)
+      # plane runs per column on the per-rank slabs and C2 with the geo2 variants
+      sweep --N 256 --slab 32 --variants fused@2#7,fused@4#7,fused@8#7,fused@16#7,fused@2#8,fused@4#8,fused@8#8,fused@16#8 && \
+      sweep --N 256 --slab 16 --variants fused@2#7,fused@4#7,fused@8#7,fused@16#7,fused@2#8,fused@4#8 && \
+      sweep --N 128 --variants fused@4#8,fused@8#8,fused@12#8,fused@16#8,fused@32#8,fused@8#7,fused@16#7,fused@32#7 ;;
     march256)
       sweep --N 256 --variants fused,fused@16,fused@12,fused@8,fused@6,fused@4,mv && \
       sweep --N 128 --variants fused,fused@24,fused@12,fused@8,fused@4,mv ;;
