@@ -972,7 +972,19 @@ struct MarchPlan {
   // its coordinates instead of loading it; gz0 = the global plane of the rank's first row
   int gx, gy, gz, gz0;
   int uni;  // the march variant the launch takes (march_uniform: 0 arrays, 1 loaded masks, 2..9 geometric)
+  // results stored with plain (MALL-allocating) stores instead of nontemporal ones: the vectors of a
+  // small grid stay in the 256 MB memory-side cache for the next launch (geo2 kernels)
+  int tstore;
 };
+// store helper of the geo2 epilogues: temporal when the plan says the vectors fit the MALL
+template <class T>
+__device__ __forceinline__ void march_store(const MarchPlan &mp, T v, T *p)
+{
+  if (mp.tstore)
+    *p = v;
+  else
+    __builtin_nontemporal_store(v, p);
+}
 
 // Geometric uniform-band march with the +D operand loaded PF + 1 planes ahead (UNI = 2 + PF;
 // eig_mat_tune(EIG_TUNE_MARCH_PREFETCH)).  The plain march waits for every load of plane z --
@@ -1351,7 +1363,10 @@ __global__ __launch_bounds__(kStreamThreads, 8) void k_spmv_march(i64 nrows, i64
 {
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   auto epi = [&](int r, int w, double acc, double) {
-    if (UNI >= 3 || r < nrows) __builtin_nontemporal_store(acc, y + (unsigned)w);  // (geometric: whole planes)
+    if constexpr (UNI >= 7)
+      march_store(mp, acc, y + (unsigned)w);  // (geometric: whole planes)
+    else if (UNI >= 3 || r < nrows)
+      __builtin_nontemporal_store(acc, y + (unsigned)w);
   };
   march_rows<MT, 2, SPAN1, UNI>(A, mp, own, lane, wave, XPlain{x}, epi);
 }
@@ -1418,7 +1433,7 @@ __global__ __launch_bounds__(kStreamThreads, march_fused_waves(UNI)) void k_lanc
       const double uk = pc.x - fs.c * pc.y;
       double ti = (acc - fs.mu * uk) * fs.sig;
       if (fs.j > 0) ti = ti - fs.gam * pc.y;
-      __builtin_nontemporal_store(dpair{ti, uk}, Pout + (unsigned)w);
+      march_store(mp, dpair{ti, uk}, Pout + (unsigned)w);
       d += ti * uk;
       q2 += ti * ti;
       m2 += uk * uk;
@@ -1876,20 +1891,18 @@ static bool march_enabled(const eig_mat_s &A) { return (A.kflags & EIG_MAT_NO_MA
 // 7 / 8 / 9: march_rows_geo2 (no masks or selects; x extent a multiple of 64, window < 2 GiB) with
 // the prefetches of 3 / 4 / 6 (tune values 6..8); a geo2 request on a grid that does not qualify
 // takes the corresponding march_rows_geo variant.
-// Automatic choice (measured: profiles/r03bj_latency.jsonl, tools/gpu.sh prefetch): geo2 where the
-// grid allows it -- the fused step with the +D operand one plane ahead (8) up to 128 planes per
-// launch (128^3: 25.2 us vs 30.3 for the plain march; one rank's 256^2 x 32 slab: 24.3 vs 34.5),
-// without prefetch (7) on deeper grids (256^3: 126.0 us at 8 plane runs vs 131.6); eig_mv and the
-// classic K1 without prefetch (7; eig_mv 256^3 46.1 us vs 59.4, 128^3 8.0 vs 12.1).  Grids geo2 does
-// not take: march_rows_geo with the +D operand two planes ahead (4).
+// Automatic choice (measured: profiles/r03bj_march_variants.jsonl, r03bn_*, r03bp_*; tools/gpu.sh
+// prefetch): geo2 without prefetch (7) where the grid allows it -- fused step 256^3 125.8 us at 8
+// plane runs (plain march 130.0), 128^3 20.1 us (plain 30.2; with the MALL-resident plain stores,
+// MarchPlan::tstore), one rank's 256^2 x 32 slab 20.5 us (plain 34.5); eig_mv 256^3 46.1 us (plain
+// 59.4), 128^3 8.0 (12.1).  The prefetching geo2 variants (8, 9) are within a few per cent either
+// way.  Grids geo2 does not take: march_rows_geo with the +D operand two planes ahead (4).
 static int march_uniform(const eig_mat_s &A, bool fused = false, i64 nplanes = 0)
 {
   if (!A.sym_uniform || (A.kflags & EIG_MAT_NO_UNIFORM)) return 0;
   if (!A.sym_geo) return 1;
   const bool geo2 = A.sym_gx % 64 == 0 && A.window * 16 < (i64(1) << 31);
-  int u = A.tune_march_prefetch > 0 ? 1 + A.tune_march_prefetch
-          : geo2                    ? (fused && nplanes <= 128 ? 8 : 7)
-                                    : 4;
+  int u = A.tune_march_prefetch > 0 ? 1 + A.tune_march_prefetch : geo2 ? 7 : 4;
   if (u >= 7 && !geo2) u = u == 9 ? 6 : u - 4;
   return u;
 }
@@ -2017,6 +2030,13 @@ static MarchPlan march_plan(const eig_mat_s &A, int mode, i64 zb = 0, i64 ze = -
     mp.gz0 = A.sym_gz0;
   }
   mp.uni = uni;
+  // measured (tools/march_copy.hip *_pp, profiles/r03bo_march_copy.jsonl): the step's ping-pong at
+  // 128^3 (2 x 32 MB of pairs) 12.9 us with plain stores vs 17.6 us nontemporal; at 256^3 (2 x 268
+  // MB) no difference either way -- plain stores where every vector a launch touches fits in half
+  // of the 256 MB MALL
+  // fused step only (eig_mv's y, written repeatedly beside the same x, measured slower: 128^3 9.6 vs
+  // 8.0 us)
+  mp.tstore = fused && uni >= 7 && A.window * 16 * 3 <= (i64(128) << 20);
   mp.zb = zb;
   mp.nplanes = nplanes;
   mp.mrows = A.nslices * 64;

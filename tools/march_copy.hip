@@ -51,7 +51,8 @@ __global__ __launch_bounds__(kThreads) void k_linear(int n, const dpair *__restr
   }
 }
 
-// MODE 0 march, 1 march + gathers, 2 prefetch, 3 temporal stores
+// MODE 0 march, 1 march + gathers, 2 prefetch, 3 temporal stores; 4 / 5: modes 0 / 3 marching the
+// planes in descending order (each run from its last plane to its first)
 template <int MODE>
 __global__ __launch_bounds__(kThreads, 8) void k_march(int n, int D, int nx, int ncol, int nseg, int nplanes,
                                                        const dpair *__restrict__ P, dpair *__restrict__ Q)
@@ -63,6 +64,23 @@ __global__ __launch_bounds__(kThreads, 8) void k_march(int n, int D, int nx, int
   const int z0 = seg * nplanes / nseg, z1 = (seg + 1) * nplanes / nseg;
   const int last = n - 1;
   auto cl = [&](int g) { return g < 0 ? 0 : (g > last ? last : g); };
+  if (MODE >= 4)
+  {
+    int w = col * 64 + lane + (z1 - 1) * D;
+    dpair cur = P[cl(w)];
+    for (int z = z1 - 1; z >= z0; --z, w -= D)
+    {
+      const dpair pd = P[cl(w - D)];
+      dpair o = cur;
+      o.x += pd.x * 1e-300;
+      if (MODE == 5)
+        Q[w] = o;
+      else
+        __builtin_nontemporal_store(o, Q + w);
+      cur = pd;
+    }
+    return;
+  }
   int w = col * 64 + lane + z0 * D;
   dpair cur = P[cl(w)];
   dpair nxt;
@@ -167,6 +185,20 @@ int main(int argc, char **argv)
   for (int nseg : {6, 8})
   {
     const int items = ncol * nseg, G = (items + kW - 1) / kW;
+    // alternating direction: odd launches march down, so they start on the planes the previous
+    // launch wrote last (what a memory-side cache still holds)
+    out("march_alt_pp", nseg, time([&] {
+      if (rep & 1)
+        k_march<4><<<G, kThreads>>>(n, D, nx, ncol, nseg, N, src(), dst());
+      else
+        k_march<0><<<G, kThreads>>>(n, D, nx, ncol, nseg, N, src(), dst());
+    }));
+    out("march_alt_t_pp", nseg, time([&] {
+      if (rep & 1)
+        k_march<5><<<G, kThreads>>>(n, D, nx, ncol, nseg, N, src(), dst());
+      else
+        k_march<3><<<G, kThreads>>>(n, D, nx, ncol, nseg, N, src(), dst());
+    }));
     out("march_pp", nseg, time([&] { k_march<0><<<G, kThreads>>>(n, D, nx, ncol, nseg, N, src(), dst()); }));
     out("march_g_pp", nseg, time([&] { k_march<1><<<G, kThreads>>>(n, D, nx, ncol, nseg, N, src(), dst()); }));
     out("march_t_pp", nseg, time([&] { k_march<3><<<G, kThreads>>>(n, D, nx, ncol, nseg, N, src(), dst()); }));
