@@ -572,3 +572,21 @@ def test_geometric_march_prefetch_bitwise(ctx, mat):
                 else:
                     assert np.array_equal(a, base[fused][0]) and np.array_equal(b, base[fused][1]), (runs, pf, fused)
     M.tune(0, march_prefetch=0)
+
+
+@pytest.mark.parametrize("N", [64, 128])
+def test_geo2_grids_vs_oracle(ctx, N):
+    """The automatic geometric march on grids whose x extent is a multiple of 64 (geo2: raw buffer
+    loads, missing neighbours read as exact zeros) -- and, at these sizes, the fused step's plain
+    (MALL-resident) stores: eig_mv bitwise the reference row loop, the fused and classic recurrences
+    vs their restatements (rtol 1e-12)."""
+    A = oracle.poisson3d(N)
+    M = check_mv(ctx, A, True)
+    assert M.info.sym_uniform == 2
+    assert M.lanczos_kernel_info(True)[0] == "k_lanczos_fused_march"
+    fa, fb, _ = eigmi.lanczos_run(M, 20, seed=123, fused=True)
+    qa, qb = oracle.lanczos_fused(A, oracle.random_vec(A.n, 123), 20)
+    assert np.allclose(fa, qa, rtol=1e-12) and np.allclose(fb, qb, rtol=1e-12)
+    ca, cb, _ = eigmi.lanczos_run(M, 20, seed=123)
+    _, ra, rb = oracle.lanczos(A, oracle.random_vec(A.n, 123), 20)
+    assert np.allclose(ca, ra, rtol=1e-12) and np.allclose(cb, rb, rtol=1e-12)
