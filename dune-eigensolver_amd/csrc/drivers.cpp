@@ -1417,7 +1417,7 @@ void lanczos_pipe_step(eig_lanczos_s &ws, int L, int force, bool wait_prev, hipE
   mark(0);
   halo_split(
       A, ws.h0, ws.h1, [&](hipStream_t hs) { halo_exchange(A, T, hs); },
-      [&](const i32 *sl, i64 first, i64 count, int) { launch_spmv(A, T, S, sl, first, count, s); });
+      [&](const i32 *sl, i64 first, i64 count, int) { launch_spmv(A, T, S, sl, first, count, s, true); });
   if (ovl && wait_prev) EIG_HIP(hipStreamWaitEvent(s, ws.ha, 0));  // launch L-1's sums are in
   launch_lanczos_pipe(A, T, UZ, S, FusedLaunch{ws.lb->st, L, force}, out, s, ctx->red);
   mark(1);

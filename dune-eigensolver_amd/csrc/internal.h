@@ -264,7 +264,7 @@ namespace eigmi {
 // SpMV over the SELL image: y[own_offset + r] = (A x)[r] for the slices [first, first+count) of
 // `slices` (or all slices when slices == nullptr).
 void launch_spmv(const eig_mat_s &A, const double *x, double *y, const i32 *slices, i64 first, i64 count,
-                 hipStream_t s);
+                 hipStream_t s, bool keep = false);
 
 // Lanczos fused kernels (see DESIGN.md "Lanczos step").  Device scalar arrays live in `st`.
 struct LanczosState {

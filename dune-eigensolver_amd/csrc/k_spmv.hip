@@ -2068,7 +2068,7 @@ static MarchPlan launch_plan(const eig_mat_s &A, int mode, const i32 *slices, i6
 }
 
 void launch_spmv(const eig_mat_s &A, const double *x, double *y, const i32 *slices, i64 first, i64 count,
-                 hipStream_t s)
+                 hipStream_t s, bool keep)
 {
   if (count <= 0 && slices != &kMarchInteriorTag) return;
   const int ncu = A.ctx->num_cu;
@@ -2076,7 +2076,10 @@ void launch_spmv(const eig_mat_s &A, const double *x, double *y, const i32 *slic
   if (A.br == 1 && A.bc == 1)
   {
     const int mode = image_mode(A);
-    const MarchPlan mp = launch_plan(A, mode, slices, first, count);
+    MarchPlan mp = launch_plan(A, mode, slices, first, count);
+    // keep: y is read by the very next launch (the pipelined step's S) -- plain stores on grids
+    // whose vectors fit the MALL, as the fused step's (MarchPlan::tstore)
+    if (keep && mp.uni >= 7 && A.window * 16 * 3 <= (i64(128) << 20)) mp.tstore = 1;
     if (mp.nseg > 0)
     {
       const unsigned G = (unsigned)((mp.ncol * (i64)mp.nseg + kWaves - 1) / kWaves);
