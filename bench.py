@@ -159,6 +159,8 @@ def main():
                          "allreduces; auto: fused on one GPU, on N > 1 the faster of fused / pipelined "
                          "in a short timed trial before the timed region (all ranks agree)")
     ap.add_argument("--trial-steps", type=int, default=40, help="steps per variant of the auto trial (N > 1)")
+    ap.add_argument("--rehearse-trial", action="store_true",
+                    help="run the N > 1 auto trial (variant x launch) on one GPU too (rehearsal of that path)")
     ap.add_argument("--comm-self", action="store_true",
                     help="one GPU: attach a one-rank RCCL communicator with EIG_COMM_ALWAYS, so every step's "
                          "allreduce runs through ncclAllReduce (the transport's per-step cost without xGMI)")
@@ -228,25 +230,35 @@ def main():
         tw = eigmi.LanczosWorkspace(M, 1, seed=123, fused="auto")
         variant = tw.variant
         tw.close()
-        if world > 1:
+        if world > 1 or args.rehearse_trial:
             trial = {}
             for var in ("fused", "pipelined"):
                 # every call below may already have queued a halo exchange or an allreduce on the
                 # other ranks when it fails here, so a failing rank cannot rejoin them at a barrier:
                 # it exits non-zero at once and the launcher tears the job down on every rank
                 # (a refused hipGraph capture is no failure: replay() then runs the steps eagerly)
+                # --launch auto also times the eager loop: a hipGraph replay adds a few us per kernel
+                # node on this stack (one GPU, 128^3 fused step: 22.2 us per step replayed vs 18.3
+                # eager, profiles/r03bx_*), which can outweigh the host's per-step enqueue cost
+                launches = ("graph", "eager") if args.launch == "auto" else (args.launch,)
                 tw = None
+                ms = {}
                 try:
-                    tw = eigmi.LanczosWorkspace(M, 5 + args.trial_steps, seed=123, fused=var == "fused",
-                                                pipelined=var == "pipelined")
+                    tw = eigmi.LanczosWorkspace(M, 5 + len(launches) * args.trial_steps, seed=123,
+                                                fused=var == "fused", pipelined=var == "pipelined")
                     tw.step(5)
-                    tw.capture(args.trial_steps)
-                    barrier()
-                    ctx.sync()
-                    t0 = time.perf_counter()
-                    tw.replay()
-                    ctx.sync()
-                    ms = (time.perf_counter() - t0) / args.trial_steps * 1e3
+                    for la in launches:
+                        if la == "graph":
+                            tw.capture(args.trial_steps)
+                        barrier()
+                        ctx.sync()
+                        t0 = time.perf_counter()
+                        if la == "graph":
+                            tw.replay()
+                        else:
+                            tw.step(args.trial_steps)
+                        ctx.sync()
+                        ms[la] = (time.perf_counter() - t0) / args.trial_steps * 1e3
                 except eigmi.EigError as e:
                     print(f"bench: {var} trial failed on rank {rank}: {e}; stopping every rank", file=sys.stderr,
                           flush=True)
@@ -255,8 +267,12 @@ def main():
                     if tw is not None:
                         tw.close()
                 barrier()
-                trial[var] = round(max_over_ranks(ms), 4)
-            variant = min(trial, key=trial.get)
+                for la in launches:
+                    trial[f"{var}/{la}"] = round(max_over_ranks(ms[la]), 4)
+            best = min(trial, key=trial.get)
+            variant = best.split("/")[0]
+            if args.launch == "auto":
+                args.launch = best.split("/")[1]
     fused = variant in ("fused", "pipelined")
     pipelined = variant == "pipelined"
     # the K timed steps are captured as one hipGraph before the clock starts (kernels, halo
