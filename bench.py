@@ -225,6 +225,7 @@ def main():
     # allreduce latency over xGMI, so the auto variant measures both (graph replays, max over ranks)
     variant = args.variant
     trial = None
+    halo_mode = "split"
     if variant == "auto":
         # one rank: EIG_LANCZOS_AUTO's choice for this image (the fused step on a 1x1 image)
         tw = eigmi.LanczosWorkspace(M, 1, seed=123, fused="auto")
@@ -232,7 +233,12 @@ def main():
         tw.close()
         if world > 1 or args.rehearse_trial:
             trial = {}
-            for var in ("fused", "pipelined"):
+            # halo: "split" = interior planes during the exchange + a boundary launch (the default),
+            # "whole" = the exchange first, then one launch (EIG_TUNE_HALO; no second launch's fixed
+            # cost) -- N > 1 only, one GPU has no halo
+            halos = ("split", "whole") if world > 1 else ("split",)
+            for var, halo in [(v, h) for v in ("fused", "pipelined") for h in halos]:
+                M.tune(0, halo_whole=int(halo == "whole"))
                 # every call below may already have queued a halo exchange or an allreduce on the
                 # other ranks when it fails here, so a failing rank cannot rejoin them at a barrier:
                 # it exits non-zero at once and the launcher tears the job down on every rank
@@ -268,11 +274,13 @@ def main():
                         tw.close()
                 barrier()
                 for la in launches:
-                    trial[f"{var}/{la}"] = round(max_over_ranks(ms[la]), 4)
+                    trial[f"{var}/{la}/{halo}"] = round(max_over_ranks(ms[la]), 4)
             best = min(trial, key=trial.get)
-            variant = best.split("/")[0]
+            variant, best_launch, best_halo = best.split("/")
             if args.launch == "auto":
-                args.launch = best.split("/")[1]
+                args.launch = best_launch
+            M.tune(0, halo_whole=int(best_halo == "whole"))
+            halo_mode = best_halo
     fused = variant in ("fused", "pipelined")
     pipelined = variant == "pipelined"
     # the K timed steps are captured as one hipGraph before the clock starts (kernels, halo
@@ -397,8 +405,8 @@ def main():
                                     "uniform band (constant coefficients: the 7 band values in the kernel "
                                     "arguments, 1-B row mask + (t, u) pairs streamed)" if M.info.sym_uniform else
                                     "symmetric band arrays + row mask" if M.info.sym_offsets else "SELL / CSR"),
-                   "parallelism": (f"row-partition z-slabs x{world} (RCCL halo, {ctx.comm_info()['allreduce']} "
-                                   "allreduce)") if world > 1 else
+                   "parallelism": (f"row-partition z-slabs x{world} (RCCL halo, {halo_mode} launch, "
+                                   f"{ctx.comm_info()['allreduce']} allreduce)") if world > 1 else
                                   ("single GPU, one-rank RCCL allreduce per step" if args.comm_self else "single GPU")},
         # SURVEY 8(d)'s CSR step bytes (12 nnz + 4(n+1) + 48 n) / step time: an equivalent rate, not
         # HBM traffic (the band image streams fewer bytes; roofline.* prices the kernel's own bytes)

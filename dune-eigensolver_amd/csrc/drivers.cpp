@@ -1240,6 +1240,13 @@ void halo_split(eig_mat_s &A, hipEvent_t e0, hipEvent_t e1, Halo halo, Launch la
     halo(ctx->comm_stream);
     EIG_HIP(hipEventRecord(e1, ctx->comm_stream));
   }
+  if (A.tune_halo_whole)
+  {
+    // EIG_TUNE_HALO = 1: wait for the exchange, then one launch over every owned row
+    if (!ctx->loop) EIG_HIP(hipStreamWaitEvent(s, e1, 0));
+    launch(nullptr, 0, A.nslices, kPartOnly);
+    return;
+  }
   if (march_split_active(A))
   {
     // interior planes on the plane march (k_spmv.hip), every other slice after the exchange

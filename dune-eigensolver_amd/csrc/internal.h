@@ -218,6 +218,7 @@ struct eig_mat_s {
   // them (the boundary launch after the exchange).  mz1 <= mz0: no split.
   eigmi::i64 mz0 = 0, mz1 = 0;
   int tune_march_runs = 0;  // eig_mat_tune(EIG_TUNE_MARCH_RUNS): plane runs per column, 0 = automatic
+  int tune_halo_whole = 0;      // eig_mat_tune(EIG_TUNE_HALO): 1 = exchange first, then one whole launch
   int tune_march_prefetch = 0;  // eig_mat_tune(EIG_TUNE_MARCH_PREFETCH): geometric march variant, 0 = automatic
   int tune_box_segs = 0;    // eig_mat_tune(EIG_TUNE_BOX_SEGS): z segments per box tile column, 0 = automatic
   // Box-stencil image for the 32-column SpMM / Chebyshev kernel (k_box.hip): box_state 0 = not

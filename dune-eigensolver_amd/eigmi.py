@@ -460,7 +460,7 @@ class Matrix:
         self.ctx.check(lib.eig_mv_host(self.h, _np_ptr(x), _np_ptr(y)))
         return y
 
-    def tune(self, march_runs=0, box_segs=None, march_prefetch=None):
+    def tune(self, march_runs=0, box_segs=None, march_prefetch=None, halo_whole=None):
         """eig_mat_tune: EIG_TUNE_MARCH_RUNS = plane runs per column of the plane-march kernels,
         EIG_TUNE_BOX_SEGS = z segments per tile column of the box kernels, EIG_TUNE_MARCH_PREFETCH =
         the geometric march variant (1 plain, 2-4 the +D operand 1-3 planes ahead, 5 + gathers one
@@ -470,6 +470,8 @@ class Matrix:
             self.ctx.check(lib.eig_mat_tune(self.h, 2, int(box_segs)))
         if march_prefetch is not None:
             self.ctx.check(lib.eig_mat_tune(self.h, 3, int(march_prefetch)))
+        if halo_whole is not None:  # EIG_TUNE_HALO: distributed steps, exchange first + one launch
+            self.ctx.check(lib.eig_mat_tune(self.h, 4, int(halo_whole)))
 
     def shift_diag(self, shift):
         self.ctx.check(lib.eig_mat_shift_diag(self.h, shift))

@@ -199,7 +199,11 @@ int eig_mat_kernel_info(eig_mat_t mat, int op, char *name, int name_len);
  * EIG_TUNE_BOX_SEGS = z segments per tile column of the 3-D box kernels (0 = automatic; results
  * bitwise unchanged, every row's sum is formed in one place).  Results are otherwise unchanged except
  * for the summation order of the step's reductions. */
-enum { EIG_TUNE_MARCH_RUNS = 1, EIG_TUNE_BOX_SEGS = 2, EIG_TUNE_MARCH_PREFETCH = 3 };
+enum { EIG_TUNE_MARCH_RUNS = 1, EIG_TUNE_BOX_SEGS = 2, EIG_TUNE_MARCH_PREFETCH = 3, EIG_TUNE_HALO = 4 };
+/* EIG_TUNE_HALO (distributed Lanczos steps): 0 = the interior planes run while the halo is in flight
+ * and the boundary planes after it (two launches, the default); 1 = the exchange first, then ONE
+ * launch over all owned rows (no second launch's fixed cost; the exchange is exposed).  The step's
+ * sums are then formed in another (fixed) order. */
 /* EIG_TUNE_MARCH_PREFETCH (geometric uniform-band images, eig_mat_info.sym_uniform = 2): 1 = the
  * plain march, 2 / 3 / 4 = the +D operand loaded 1 / 2 / 3 planes ahead, 5 = 3 planes ahead and the
  * neighbour gathers 1 plane ahead; 6 / 7 / 8 = the variants of 2 / 3 / 5 without row masks or

@@ -141,6 +141,9 @@ int main(int argc, char **argv)
   std::vector<std::vector<double>> y(P), al(P, std::vector<double>(steps)), be(P, std::vector<double>(steps + 1)),
       ev(P, std::vector<double>(nev));
   std::vector<int64_t> rb(P), rc(P), halo(P), uni(P);
+  // EIG_TUNE_HALO = 1 (exchange first, one launch): fused and pipelined recurrences
+  std::vector<std::vector<double>> wfal(P, std::vector<double>(steps)), wfbe(P, std::vector<double>(steps + 1)),
+      wpal(P, std::vector<double>(steps)), wpbe(P, std::vector<double>(steps + 1));
   std::vector<double> dots(P);
   std::vector<std::thread> th;
   for (int r = 0; r < P; ++r)
@@ -177,6 +180,10 @@ int main(int argc, char **argv)
       CK(eig_lanczos_run(A, steps, nullptr, 123, EIG_LANCZOS_TIME_KERNELS, al[r].data(), be[r].data(), nullptr));
       CK(eig_lanczos_run(A, steps, nullptr, 123, EIG_LANCZOS_FUSED, fal[r].data(), fbe[r].data(), nullptr));
       CK(eig_lanczos_run(A, steps, nullptr, 123, EIG_LANCZOS_PIPELINED, pal[r].data(), pbe[r].data(), nullptr));
+      CK(eig_mat_tune(A, EIG_TUNE_HALO, 1));
+      CK(eig_lanczos_run(A, steps, nullptr, 123, EIG_LANCZOS_FUSED, wfal[r].data(), wfbe[r].data(), nullptr));
+      CK(eig_lanczos_run(A, steps, nullptr, 123, EIG_LANCZOS_PIPELINED, wpal[r].data(), wpbe[r].data(), nullptr));
+      CK(eig_mat_tune(A, EIG_TUNE_HALO, 0));
       {
         // capture/replay: the loopback transport cannot be captured, replay must take the same steps eagerly
         std::vector<double> ag(steps), bg(steps + 1);
@@ -249,6 +256,16 @@ int main(int argc, char **argv)
       {
         std::printf("FAIL rank %d fused step %d: alpha %.17g/%.17g beta %.17g/%.17g\n", r, j, fal[r][j], fa_ser[j],
                     fbe[r][j + 1], fb_ser[j + 1]);
+        ++failures;
+        break;
+      }
+    for (int j = 0; j < steps; ++j)
+      if (std::fabs(wfal[r][j] - fa_ser[j]) > 1e-12 * std::fabs(fa_ser[j]) ||
+          std::fabs(wfbe[r][j + 1] - fb_ser[j + 1]) > 1e-12 * std::fabs(fb_ser[j + 1]) ||
+          std::fabs(wpal[r][j] - pa_ser[j]) > 1e-12 * std::fabs(pa_ser[j]) ||
+          std::fabs(wpbe[r][j + 1] - pb_ser[j + 1]) > 1e-12 * std::fabs(pb_ser[j + 1]))
+      {
+        std::printf("FAIL rank %d whole-launch (EIG_TUNE_HALO) step %d\n", r, j);
         ++failures;
         break;
       }
