@@ -238,7 +238,7 @@ def main():
             # cost) -- N > 1 only, one GPU has no halo
             halos = ("split", "whole") if world > 1 else ("split",)
             for var, halo in [(v, h) for v in ("fused", "pipelined") for h in halos]:
-                M.tune(0, halo_whole=int(halo == "whole"))
+                M.tune(halo_whole=int(halo == "whole"))
                 # every call below may already have queued a halo exchange or an allreduce on the
                 # other ranks when it fails here, so a failing rank cannot rejoin them at a barrier:
                 # it exits non-zero at once and the launcher tears the job down on every rank
@@ -279,7 +279,7 @@ def main():
             variant, best_launch, best_halo = best.split("/")
             if args.launch == "auto":
                 args.launch = best_launch
-            M.tune(0, halo_whole=int(best_halo == "whole"))
+            M.tune(halo_whole=int(best_halo == "whole"))
             halo_mode = best_halo
     fused = variant in ("fused", "pipelined")
     pipelined = variant == "pipelined"

@@ -518,7 +518,7 @@ extern "C" int eig_mat_tune(eig_mat_t A, int key, int value)
                   key == EIG_TUNE_HALO,
               EIG_ERR_ARG, "eig_mat_tune: unknown key");
     EIG_CHECK(key != EIG_TUNE_HALO || value <= 1, EIG_ERR_ARG, "eig_mat_tune: halo mode 0 / 1");
-    EIG_CHECK(key != EIG_TUNE_MARCH_PREFETCH || value <= 8, EIG_ERR_ARG, "eig_mat_tune: march variant 0..8");
+    EIG_CHECK(key != EIG_TUNE_MARCH_PREFETCH || value <= 10, EIG_ERR_ARG, "eig_mat_tune: march variant 0..10");
     if (key == EIG_TUNE_MARCH_RUNS)
       A->tune_march_runs = value;
     else if (key == EIG_TUNE_MARCH_PREFETCH)
@@ -880,8 +880,9 @@ void build_sym(eig_mat_s &A, i64 nb, const int64_t *rowptr, const int32_t *col, 
       }
   });
   if (!good) return;
-  // uniform band: one value per array over every stored entry (the symmetric pairs are equal bit
-  // for bit already, so the lower entries need no separate check)
+  // uniform band: one value per array over every stored entry, lower entries included (a lower entry
+  // whose mirror is not stored on this rank -- a ghost row's coupling, or a one-sided pattern -- was
+  // never compared in the mirror pass, and the uniform march kernels take the array's constant for it)
   {
     std::mutex mu;
     std::vector<double> uc(nup, 0.0);
@@ -895,7 +896,6 @@ void build_sym(eig_mat_s &A, i64 nb, const int64_t *rowptr, const int32_t *col, 
         for (i64 p = rowptr[r]; p < rowptr[r + 1]; ++p)
         {
           const i64 d = (i64)col[p] - (row0 + r);
-          if (d < 0) continue;
           const int j = kj[kof(d)];
           if (!sn[j])
           {
@@ -927,9 +927,11 @@ void build_sym(eig_mat_s &A, i64 nb, const int64_t *rowptr, const int32_t *col, 
   }
   // geometric masks: a grid whose rows store exactly their in-grid neighbours -- the whole grid on
   // one rank, or a rank's slab of whole planes (row0 and nb multiples of the plane size D; z is
-  // the global plane, so the slab's first / last planes keep their ghost-plane bits)
+  // the global plane, so the slab's first / last planes keep their ghost-plane bits).  A property of
+  // the pattern alone: the uniform marches take the values from their arguments, the value march
+  // (march variant 10) streams them from the band arrays.
   A.sym_geo = false;
-  if (A.sym_uniform && mb == 1 && offs.front() == -offs.back() && (nd == 7 || nd == 5))
+  if (mb == 1 && offs.front() == -offs.back() && (nd == 7 || nd == 5))
   {
     const i64 D = offs.back();
     const i64 nx = nd == 7 ? offs[5] : D;
@@ -1306,6 +1308,8 @@ extern "C" int eig_mat_get_info(eig_mat_t A, eig_mat_info *info)
     info->sym_uniform = (A->sym_val && A->sym_uniform && !(A->kflags & EIG_MAT_NO_UNIFORM))
                             ? (A->sym_geo ? 2 : 1)
                             : 0;
+    info->sym_geo = A->sym_val && A->sym_geo ? 1 : 0;
+    info->march_variant = march_variant(*A, true);
   });
 }
 

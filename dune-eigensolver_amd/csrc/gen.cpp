@@ -12,6 +12,10 @@
 //           nodes, h = 1/(N+1), Dirichlet nodes eliminated, 15-point edge pattern   (config C5)
 //   kind 7  3-D P1 consistent mass M on the same mesh and the SAME 15-point pattern (config C5;
 //           the reference assumes pattern(A) contains pattern(B), eigensolver.hh:202-203)
+//   kind 8  3-D 7-point variable-coefficient diffusion (finite volumes, Dirichlet): the 7-point
+//           pattern of kind 4 with a positive conductance kappa(e) in [0.5, 1.5) per grid edge e
+//           (a hash of the edge, so a(k, q) = a(q, k) = -kappa bit for bit) and the diagonal
+//           the sum of the six face conductances (boundary faces included): SPD, no two rows equal
 #include <cmath>
 #include <cstdint>
 #include <cstdlib>
@@ -95,6 +99,17 @@ int gen_p1_row(bool mass, int N, i64 k, int32_t *cols, double *vals)
   return cnt;
 }
 
+// kind 8: the conductance of the edge from node k along axis a (0 x, 1 y, 2 z) to its + neighbour;
+// boundary faces of the grid hash with side 1 (the - face of node k) so every face has its own value
+inline double kappa(i64 k, int a, int side)
+{
+  uint64_t h = (uint64_t)k * 6u + (uint64_t)a * 2u + (uint64_t)side + 0x9e3779b97f4a7c15ull;
+  h = (h ^ (h >> 30)) * 0xbf58476d1ce4e5b9ull;
+  h = (h ^ (h >> 27)) * 0x94d049bb133111ebull;
+  h ^= h >> 31;
+  return 0.5 + (double)(h >> 11) * 0x1.0p-53;
+}
+
 // Entries of global block row k; returns the count.  cols/vals may be null (count only).
 int gen_row(int kind, int N, int overlap, i64 k, int32_t *cols, double *vals)
 {
@@ -141,6 +156,27 @@ int gen_row(int kind, int N, int overlap, i64 k, int32_t *cols, double *vals)
     if (z < N - 1) put(k + NN, -1.0);
     return c;
   }
+  if (kind == 8)
+  {
+    const i64 st[3] = {1, (i64)N, NN};
+    const int co[3] = {x, y, z};
+    // faces -z, -y, -x, +x, +y, +z: the - face of node k is the + edge of k - st[a] (or a boundary face)
+    double kf[6];
+    for (int a = 0; a < 3; ++a)
+    {
+      kf[2 - a] = co[a] > 0 ? kappa(k - st[a], a, 0) : kappa(k, a, 1);
+      kf[3 + a] = kappa(k, a, 0);
+    }
+    const double d = ((((kf[0] + kf[1]) + kf[2]) + kf[3]) + kf[4]) + kf[5];
+    if (z > 0) put(k - NN, -kf[0]);
+    if (y > 0) put(k - N, -kf[1]);
+    if (x > 0) put(k - 1, -kf[2]);
+    put(k, d);
+    if (x < N - 1) put(k + 1, -kf[3]);
+    if (y < N - 1) put(k + N, -kf[4]);
+    if (z < N - 1) put(k + NN, -kf[5]);
+    return c;
+  }
   if (kind == 5)
   {
     static const double C[9] = {2, 1, 0, 1, 2, 1, 0, 1, 2};
@@ -164,13 +200,14 @@ int gen_row(int kind, int N, int overlap, i64 k, int32_t *cols, double *vals)
 }
 
 i64 nrows_of(int kind, int N) { return (kind <= 3) ? (i64)N * N : (i64)N * N * N; }
+constexpr int kGenKinds = 9;
 int blk_of(int kind) { return kind == 5 ? 9 : 1; }
 
 }  // namespace
 
 extern "C" int64_t eig_gen_nnzb_rows(int kind, int N, int64_t row_begin, int64_t nrows)
 {
-  if (kind < 0 || kind > 7 || N <= 0) return -1;
+  if (kind < 0 || kind >= kGenKinds || N <= 0) return -1;
   i64 s = 0;
   for (i64 k = row_begin; k < row_begin + nrows; ++k) s += gen_row(kind, N, 0, k, nullptr, nullptr);
   return s;
@@ -179,7 +216,7 @@ extern "C" int64_t eig_gen_nnzb_rows(int kind, int N, int64_t row_begin, int64_t
 extern "C" int64_t eig_gen_nnzb(int kind, int N)
 {
   if (kind == 0 || kind == 1 || kind == 2 || kind == 3) return (i64)5 * N * N - 4 * (i64)N;
-  if (kind == 4) return (i64)7 * N * N * N - (i64)6 * N * N;
+  if (kind == 4 || kind == 8) return (i64)7 * N * N * N - (i64)6 * N * N;
   if (kind == 5)
   {
     const i64 t = 3 * (i64)N - 2;
@@ -196,7 +233,7 @@ extern "C" int64_t eig_gen_nnzb(int kind, int N)
 extern "C" int eig_gen_matrix_rows(int kind, int N, int64_t row_begin, int64_t nrows, int64_t *rowptr, int32_t *col,
                                    double *vals)
 {
-  if (kind < 0 || kind > 7 || N <= 0 || !rowptr || !col || !vals) return EIG_ERR_ARG;
+  if (kind < 0 || kind >= kGenKinds || N <= 0 || !rowptr || !col || !vals) return EIG_ERR_ARG;
   if (row_begin < 0 || row_begin + nrows > nrows_of(kind, N)) return EIG_ERR_SHAPE;
   const int bb = blk_of(kind);
   i64 p = 0;
@@ -211,7 +248,7 @@ extern "C" int eig_gen_matrix_rows(int kind, int N, int64_t row_begin, int64_t n
 
 extern "C" int eig_gen_matrix(int kind, int N, int overlap, int64_t *rowptr, int32_t *col, double *vals)
 {
-  if (kind < 0 || kind > 7 || N <= 0 || !rowptr || !col || !vals) return EIG_ERR_ARG;
+  if (kind < 0 || kind >= kGenKinds || N <= 0 || !rowptr || !col || !vals) return EIG_ERR_ARG;
   const int bb = blk_of(kind);
   const i64 n = nrows_of(kind, N);
   i64 p = 0;

@@ -208,9 +208,11 @@ struct eig_mat_s {
   // stream the row mask and the vectors only (the arrays stay for the other kernels)
   bool sym_uniform = false;
   double sym_uc[eigmi::kSymMaxOff] = {};
-  // Geometric row masks (uniform bands on one rank): the rows form an nx x ny x nz grid (offsets
-  // -D, -nx, -1, 0, 1, nx, D with D = nx ny, or the 2-D -D, -1, 0, 1, D with D = nx) and every row
-  // stores exactly its in-grid neighbours; the march derives the masks from the coordinates
+  // Geometric row masks (a property of the pattern; one rank's whole grid or a slab of whole
+  // planes): the rows form an nx x ny x nz grid (offsets -D, -nx, -1, 0, 1, nx, D with D = nx ny, or
+  // the 2-D -D, -1, 0, 1, D with D = nx) and every row stores exactly its in-grid neighbours; the
+  // march derives the masks from the coordinates (uniform bands: values from the arguments; other
+  // bands: the value march streams the band arrays, k_spmv.hip march variant 10)
   bool sym_geo = false;
   int sym_gx = 0, sym_gy = 0, sym_gz = 0, sym_gz0 = 0;  // grid (global planes) and this rank's first plane
   // Plane-march split of a distributed slab (k_spmv.hip march_plan): planes [mz0, mz1) have no
@@ -305,6 +307,7 @@ void launch_fused_tail(const LanczosState &st, int L, hipStream_t s);
 // planes [A.mz0, A.mz1).
 bool march_geometry(const eig_mat_s &A, i64 &D, int chunk = 64);
 bool march_split_active(const eig_mat_s &A);
+int march_variant(const eig_mat_s &A, bool fused);
 extern const i32 kMarchInteriorTag;
 // a2 SpMM (kernels_cpp.hh:626-657) on the band-image plane march for 1x1 matrices whose band
 // qualifies; false (nothing launched) otherwise.  X, Y: window-layout multivectors, m % 8 == 0.
@@ -331,8 +334,8 @@ bool launch_cheb_march(const eig_mat_s &M, i64 m, const double *Xk, double *Xold
                        double omega, double gamma, hipStream_t s);
 // Kernel a whole-matrix Lanczos step launch picks on this image, and its algorithmic bytes per launch.
 void lanczos_kernel_info(const eig_mat_s &A, bool fused, std::string &name, i64 &bytes);
-// Whether the fused step's (t, u) pair gathers are mostly cache hits on this image (band image or
-// stencil slices), i.e. whether EIG_LANCZOS_AUTO takes the fused step.
+// Whether EIG_LANCZOS_AUTO takes the fused step on this image: every 1x1 image (round 3: without
+// register spills the fused step beats the two-kernel step on scattered images too).
 bool fused_step_pays(const eig_mat_s &A);
 // Kernel family a whole-matrix launch of `op` (eig_mat_kernel_info's EIG_OP_*) picks on this image.
 std::string kernel_for(const eig_mat_s &A, int op);

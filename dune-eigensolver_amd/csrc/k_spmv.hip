@@ -1119,7 +1119,16 @@ struct MarchNoPre {
   template <class X>
   __device__ __forceinline__ bool operator()(X &) const { return true; }
 };
-template <int PF, bool PG, class X, class EPI, class PRE>
+// VAL (march variants 10 / 11: geometric bands whose values are not uniform): the band values are
+// streamed from the symmetric band arrays instead -- the +D / 0 / +1 / +nx values of each row once
+// (nontemporal), the mirrored -D value carried from the previous plane in a register, the mirrored
+// -1 value by the same lane shift as the operands (lane 0 loads its own), the mirrored -nx value
+// re-read at row w - nx (the +nx array, streamed 4 columns earlier on the same XCD: an L2 hit).
+// A missing neighbour's value reads as 0.0 (its slot is unset, or the same zero-record / out-of-range
+// load as its operand) and its operand as exactly zero, so its product is +-0 and the row's sum is
+// that of the masked march bit for bit.  VAL = 2 (variant 11) issues the next plane's value streams
+// one plane ahead (the last plane of a run issues none).
+template <int PF, bool PG, int VAL, class X, class EPI, class PRE>
 __device__ __forceinline__ void march_rows_geo2(const SellB1 &A, const MarchPlan &mp, i64 own, int lane, int wave,
                                                 X x, EPI &epi, PRE &pre)
 {
@@ -1153,50 +1162,103 @@ __device__ __forceinline__ void march_rows_geo2(const SellB1 &A, const MarchPlan
     bload(rn, v + dnb, g.xn);
     bload(rq, v + dqb, g.xq);
   };
+  // VAL: one descriptor per band array (8-B slots, window-indexed like the operands); vv = w * 8
+  const SymImg &S = A.sym;
+  const unsigned vbytes = (unsigned)S.ld * 8u;
+  auto arr = [&](int j, bool on) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(S.val + (i64)(j >= 0 ? j : 0) * S.ld), 0,
+                                             on && j >= 0 ? (int)vbytes : 0, 0x00020000);
+  };
+  const __amdgpu_buffer_rsrc_t vD = arr(S.dj[S.nd - 1], VAL), v0 = arr(S.j0, VAL), v1 = arr(S.j1, VAL),
+                               vq = arr(S.dj[S.khi], VAL && mp.dq), vn = arr(S.dj[S.khi], VAL && mp.dn && yw > 0);
+  const unsigned eov = lane == 0 && x0 > 0 ? 0u - 8u : kOut;  // lane 0: the mirrored -1 value at w - 1
+  const unsigned dnv = (unsigned)mp.dn * 8u, Dv = (unsigned)D * 8u;
+  unsigned vv = (unsigned)w * 8u;
+  struct Vals {
+    double aD, a0, ap, aq, an, ae;
+  };
+  const __amdgpu_buffer_rsrc_t vz = arr(0, false);
+  auto vload = [&](unsigned o, Vals &v, bool on) {  // on: wave-uniform (false: zeros, no traffic)
+    v.aD = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(on ? vD : vz, (int)o, 0, 2));
+    v.a0 = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(on ? v0 : vz, (int)o, 0, 2));
+    v.ap = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(on ? v1 : vz, (int)o, 0, 2));
+    v.aq = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(on ? vq : vz, (int)o, 0, 0));
+    v.an = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(on ? vn : vz, (int)(o + dnv), 0, 0));
+    v.ae = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(on ? v1 : vz, (int)(o + eov), 0, 0));
+  };
+  constexpr bool VPF = VAL == 2;  // value streams one plane ahead
+  Vals vs[2];
+  double amD = 0.0;  // VAL: the mirrored -D value (the +D value of the row below)
   raw pm{};
-  if (zg0 > 0) bload(rs, vo - Db, pm);  // (plane 0 of the grid: no -D neighbour)
+  if (zg0 > 0)
+  {
+    bload(rs, vo - Db, pm);  // (plane 0 of the grid: no -D neighbour)
+    if constexpr (VAL) amD = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(vD, (int)(vv - Dv), 0, 0));
+  }
   raw sl[NS];
   bload(rs, vo, sl[0]);
 #pragma unroll
   for (int k = 1; k <= PF; ++k) bload(zg0 + k < mp.gz ? rs : r0, vo + (unsigned)k * Db, sl[k]);
   Gath gs[2];
   if constexpr (PG) gather(vo, gs[0]);
+  if constexpr (VPF) vload(vv, vs[0], true);
   if (!pre(x)) return;
   double pmv = zg0 > 0 ? x.val(pm) : 0.0;
-  auto body = [&](int z, const raw &pcur, const raw &pd, raw &pf, Gath &gc, Gath &gn) {
+  auto body = [&](int z, const raw &pcur, const raw &pd, raw &pf, Gath &gc, Gath &gn, Vals &vc_, Vals &vn_) {
     if constexpr (PG)
       gather(vo + Db, gn);
     else
       gather(vo, gc);
+    if constexpr (VAL == 1) vload(vv, vc_, true);
     const int zg = z + mp.gz0;
     bload(zg + PF + 1 < mp.gz ? rs : r0, vo + (unsigned)(PF + 1) * Db, pf);
+    if constexpr (VPF) vload(vv + Dv, vn_, z + 1 < z1);
     double acc = 0.0;
-    acc += mp.cD * pmv;
-    acc += mp.cn * x.val(gc.xn);
     const double vc = x.val(pcur), ve = x.val(gc.eg);
     const double vl = lane_shift_or<false>(vc, ve), vr = lane_shift_or<true>(vc, ve);
-    acc += mp.c1 * vl;
-    acc += mp.c0 * vc;
-    acc += mp.c1 * vr;
-    acc += mp.cq * x.val(gc.xq);
-    acc += mp.cD * x.val(pd);
+    if constexpr (VAL)
+    {
+      const double am = lane_shift_or<false>(vc_.ap, vc_.ae);
+      acc += amD * pmv;
+      acc += vc_.an * x.val(gc.xn);
+      acc += am * vl;
+      acc += vc_.a0 * vc;
+      acc += vc_.ap * vr;
+      acc += vc_.aq * x.val(gc.xq);
+      acc += vc_.aD * x.val(pd);
+      amD = vc_.aD;
+    }
+    else
+    {
+      acc += mp.cD * pmv;
+      acc += mp.cn * x.val(gc.xn);
+      acc += mp.c1 * vl;
+      acc += mp.c0 * vc;
+      acc += mp.c1 * vr;
+      acc += mp.cq * x.val(gc.xq);
+      acc += mp.cD * x.val(pd);
+    }
     epi(w - own32, w, acc, pcur);
     pmv = vc;
     w += D;
     vo += Db;
+    vv += Dv;
   };
   static_assert(!PG || NS % 2 == 0, "gather prefetch: an even number of bodies per trip");
+  static_assert(!VPF || NS % 2 == 0, "value prefetch: an even number of bodies per trip");
   int z = z0;
   for (; z + NS - 1 < z1; z += NS)
   {
 #pragma unroll
     for (int k = 0; k < NS; ++k)
-      body(z + k, sl[k], sl[(k + 1) % NS], sl[(k + PF + 1) % NS], gs[PG ? k & 1 : 0], gs[PG ? (k + 1) & 1 : 1]);
+      body(z + k, sl[k], sl[(k + 1) % NS], sl[(k + PF + 1) % NS], gs[PG ? k & 1 : 0], gs[PG ? (k + 1) & 1 : 1],
+           vs[VPF ? k & 1 : 0], vs[VPF ? (k + 1) & 1 : 1]);
   }
 #pragma unroll
   for (int k = 0; k < NS - 1; ++k)
     if (z + k < z1)
-      body(z + k, sl[k], sl[(k + 1) % NS], sl[(k + PF + 1) % NS], gs[PG ? k & 1 : 0], gs[PG ? (k + 1) & 1 : 1]);
+      body(z + k, sl[k], sl[(k + 1) % NS], sl[(k + PF + 1) % NS], gs[PG ? k & 1 : 0], gs[PG ? (k + 1) & 1 : 1],
+           vs[VPF ? k & 1 : 0], vs[VPF ? (k + 1) & 1 : 1]);
 }
 
 // The rows of this wave's work item, in plane order: epi(r, w, acc, centre) gets each row's sum
@@ -1220,8 +1282,10 @@ __device__ __forceinline__ void march_rows(const SellB1 &A, const MarchPlan &mp,
   if constexpr (UNI >= 3)
   {
     // 3, 4, 5: +D operand 1, 2, 3 planes ahead; 6: 3 planes ahead and the gathers one plane ahead
-    if constexpr (UNI >= 7)  // 7, 8, 9: march_rows_geo2 with the prefetches of 3, 4, 6
-      march_rows_geo2<UNI == 9 ? 2 : UNI - 7, UNI == 9>(A, mp, own, lane, wave, x, epi, pre);
+    if constexpr (UNI >= 10)  // 10, 11: the value march (band arrays streamed), 11 one plane ahead
+      march_rows_geo2<0, false, UNI - 9>(A, mp, own, lane, wave, x, epi, pre);
+    else if constexpr (UNI >= 7)  // 7, 8, 9: march_rows_geo2 with the prefetches of 3, 4, 6
+      march_rows_geo2<UNI == 9 ? 2 : UNI - 7, UNI == 9, 0>(A, mp, own, lane, wave, x, epi, pre);
     else
       march_rows_geo<UNI == 6 ? 2 : UNI - 3, UNI == 6>(A, mp, own, lane, wave, x, epi);
     return;
@@ -1412,7 +1476,8 @@ __global__ __launch_bounds__(kStreamThreads, 8) void k_lanczos_spmv_march(
 // resident waves per SIMD the fused march kernels are built for (registers: no spills)
 constexpr int march_fused_waves(int uni)
 {
-  return uni == 6 || uni == 9 ? 4 : uni == 5 ? 5 : uni == 4 || uni == 8 ? 6 : uni == 3 || uni == 7 ? 7 : uni ? 8 : 7;
+  return uni == 11 ? 5 : uni == 10 ? 6 : uni == 6 || uni == 9 ? 4 : uni == 5 ? 5 : uni == 4 || uni == 8 ? 6
+       : uni == 3 || uni == 7 ? 7 : uni ? 8 : 7;
 }
 
 template <class MT, bool SPAN1, int UNI>
@@ -1880,6 +1945,17 @@ static int grid_for_slices(K kernel, i64 count, int num_cu)
 
 // EIG_MAT_NO_MARCH: the plane-marching kernels are off for this matrix (the slice kernels run).
 static bool march_enabled(const eig_mat_s &A) { return (A.kflags & EIG_MAT_NO_MARCH) == 0; }
+static bool march_span1(const eig_mat_s &A)
+{
+  int klo = A.sym_nd, khi = A.sym_nd;
+  for (int k = A.sym_nd - 1; k >= 0; --k)
+  {
+    if (A.sym_off[k] >= -1) klo = k;
+    if (A.sym_off[k] > 1) khi = k;
+  }
+  return A.sym_mask_bytes == 1 && klo - 1 <= 1 && (A.sym_nd - 1) - khi <= 1;
+}
+
 // Far spans of at most one offset each (u8-mask bands only: at most 8 offsets, so (-D, -1) and
 // (+1, +D) hold at most one offset each exactly when nd <= 7 with -1/0/+1 present).
 // Uniform band values in the march kernels' arguments (EIG_MAT_NO_UNIFORM keeps the array loads).
@@ -1897,32 +1973,33 @@ static bool march_enabled(const eig_mat_s &A) { return (A.kflags & EIG_MAT_NO_MA
 // MarchPlan::tstore), one rank's 256^2 x 32 slab 20.5 us (plain 34.5); eig_mv 256^3 46.1 us (plain
 // 59.4), 128^3 8.0 (12.1).  The prefetching geo2 variants (8, 9) are within a few per cent either
 // way.  Grids geo2 does not take: march_rows_geo with the +D operand two planes ahead (4).
+// 10 / 11: bands that are not uniform (or EIG_MAT_NO_UNIFORM) on a geo2 grid: the value march
+// (march_rows_geo2<VAL>: the band arrays streamed, masks from the coordinates), 11 with the value
+// streams and the +D operand one plane ahead (tune values 9 / 10; 1 = the plain masked march).
 static int march_uniform(const eig_mat_s &A, bool fused = false, i64 nplanes = 0)
 {
-  if (!A.sym_uniform || (A.kflags & EIG_MAT_NO_UNIFORM)) return 0;
+  const bool geo2 = A.sym_geo && A.sym_gx % 64 == 0 && A.window * 16 < (i64(1) << 31);
+  if (!A.sym_uniform || (A.kflags & EIG_MAT_NO_UNIFORM))
+  {
+    if (!geo2 || !march_span1(A) || A.sym_ld * 8 >= (i64(1) << 31) || A.tune_march_prefetch == 1) return 0;
+    return A.tune_march_prefetch == 10 ? 11 : 10;
+  }
   if (!A.sym_geo) return 1;
-  const bool geo2 = A.sym_gx % 64 == 0 && A.window * 16 < (i64(1) << 31);
   int u = A.tune_march_prefetch > 0 ? 1 + A.tune_march_prefetch : geo2 ? 7 : 4;
   if (u >= 7 && !geo2) u = u == 9 ? 6 : u - 4;
   return u;
 }
 
-static bool march_span1(const eig_mat_s &A)
-{
-  int klo = A.sym_nd, khi = A.sym_nd;
-  for (int k = A.sym_nd - 1; k >= 0; --k)
-  {
-    if (A.sym_off[k] >= -1) klo = k;
-    if (A.sym_off[k] > 1) khi = k;
-  }
-  return A.sym_mask_bytes == 1 && klo - 1 <= 1 && (A.sym_nd - 1) - khi <= 1;
-}
 
 // Launch a march kernel template KERN<MT, SPAN1> for the image's mask width (u8 masks only can
 // have single-offset far spans).
 #define EIG_MARCH_LAUNCH(KERN, MODE, G, ...)                                                               \
   do {                                                                                                    \
-    if ((MODE) == kSymN8 && march_span1(A) && mp.uni == 9)                                      \
+    if ((MODE) == kSymN8 && march_span1(A) && mp.uni == 11)                                               \
+      hipLaunchKernelGGL((KERN<uint8_t, true, 11>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);       \
+    else if ((MODE) == kSymN8 && march_span1(A) && mp.uni == 10)                                          \
+      hipLaunchKernelGGL((KERN<uint8_t, true, 10>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);       \
+    else if ((MODE) == kSymN8 && march_span1(A) && mp.uni == 9)                                      \
       hipLaunchKernelGGL((KERN<uint8_t, true, 9>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);        \
     else if ((MODE) == kSymN8 && march_span1(A) && mp.uni == 8)                                 \
       hipLaunchKernelGGL((KERN<uint8_t, true, 8>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);        \
@@ -1993,7 +2070,7 @@ static MarchPlan march_plan(const eig_mat_s &A, int mode, i64 zb = 0, i64 ze = -
   const int uni = march_uniform(A, fused, nplanes);
   if (fused && ncol >= 1024)
     nseg = std::min<i64>(nplanes / 2 > 0 ? nplanes / 2 : 1,
-                         std::max<i64>(2, std::min<i64>(uni == 7 ? 8 : 6, nplanes / 32)));
+                         std::max<i64>(2, std::min<i64>(uni == 7 || uni >= 10 ? 8 : 6, nplanes / 32)));
   else if (fused)  // (geo2 marches: runs of >= 16 planes -- 128^3 8 runs 24.3 us, 12: 25.3, 16: 26.4)
     nseg = std::min(nseg, std::max<i64>({1, nplanes / (uni >= 7 ? 16 : 10), (resident / 4 + ncol - 1) / ncol}));
   if (A.tune_march_runs > 0) nseg = std::min<i64>(A.tune_march_runs, nplanes);  // eig_mat_tune
@@ -2010,6 +2087,13 @@ static MarchPlan march_plan(const eig_mat_s &A, int mode, i64 zb = 0, i64 ze = -
   mp.Un = A.sym_val + (i64)(klo > 1 ? A.sym_dj[1] : 0) * A.sym_ld;
   mp.dq = khi < A.sym_nd - 1 ? A.sym_off[khi] : 0;
   mp.Uq = A.sym_val + (i64)(khi < A.sym_nd - 1 ? A.sym_dj[khi] : 0) * A.sym_ld;
+  if (A.sym_geo)
+  {
+    mp.gx = A.sym_gx;
+    mp.gy = A.sym_gy;
+    mp.gz = A.sym_gz;
+    mp.gz0 = A.sym_gz0;
+  }
   if (A.sym_uniform)
   {
     const int kD = A.sym_nd - 1;
@@ -2024,10 +2108,6 @@ static MarchPlan march_plan(const eig_mat_s &A, int mode, i64 zb = 0, i64 ze = -
     mp.c1 = k1 >= 0 ? A.sym_uc[A.sym_dj[k1]] : 0.0;
     mp.cn = klo > 1 ? A.sym_uc[A.sym_dj[1]] : 0.0;
     mp.cq = khi < A.sym_nd - 1 ? A.sym_uc[A.sym_dj[khi]] : 0.0;
-    mp.gx = A.sym_gx;
-    mp.gy = A.sym_gy;
-    mp.gz = A.sym_gz;
-    mp.gz0 = A.sym_gz0;
   }
   mp.uni = uni;
   // measured (tools/march_copy.hip *_pp, profiles/r03bo_march_copy.jsonl): the step's ping-pong at
@@ -2043,6 +2123,14 @@ static MarchPlan march_plan(const eig_mat_s &A, int mode, i64 zb = 0, i64 ze = -
   mp.ncol = (int)ncol;
   mp.nseg = (int)nseg;
   return mp;
+}
+
+// eig_mat_info.march_variant: the variant a whole-matrix launch takes, -1 when it does not march
+int march_variant(const eig_mat_s &A, bool fused)
+{
+  if (A.br != 1 || A.bc != 1) return -1;
+  const MarchPlan mp = march_plan(A, image_mode(A), 0, -1, fused);
+  return mp.nseg > 0 ? mp.uni : -1;
 }
 
 const i32 kMarchInteriorTag = 0;
@@ -2335,9 +2423,13 @@ void lanczos_kernel_info(const eig_mat_s &A, bool fused, std::string &name, i64 
     const bool whole = !A.ctx->distributed() || (A.recvs.empty() && A.sends.empty());
     const bool march = whole ? (march_plan(A, mode).nseg > 0)
                              : march_split_active(A);
-    // the uniform-band march streams the row mask and the vectors only
-    if (march && mode == kSymN8 && march_span1(A) && march_uniform(A))
-      bytes = (march_uniform(A) >= 2 ? 0 : (i64)A.sym_mask_bytes * n) + vec;
+    // the uniform-band march streams the row mask and the vectors only; the value march (10, 11)
+    // the band arrays and the vectors (geometric masks: no mask stream)
+    const int mv = march && mode == kSymN8 && march_span1(A) ? march_uniform(A) : 0;
+    if (mv >= 10)
+      bytes = 8 * (i64)A.sym_nup * n + vec;
+    else if (mv)
+      bytes = (mv >= 2 ? 0 : (i64)A.sym_mask_bytes * n) + vec;
     name = fused ? (march ? "k_lanczos_fused_march" : "k_lanczos_fused_b1")
                  : (march ? "k_lanczos_spmv_march" : "k_lanczos_spmv_b1");
   }

@@ -42,7 +42,8 @@ def _tflags(timed):
     return LANCZOS_TIME_KERNELS if timed else 0
 
 
-GEN_LAPLACE2D, GEN_NEUMANN2D, GEN_PU2D, GEN_IDENTITY2D, GEN_POISSON3D, GEN_Q1ELAST3D, GEN_P1STIFF3D, GEN_P1MASS3D = range(8)
+GEN_LAPLACE2D, GEN_NEUMANN2D, GEN_PU2D, GEN_IDENTITY2D, GEN_POISSON3D, GEN_Q1ELAST3D, GEN_P1STIFF3D, GEN_P1MASS3D, \
+    GEN_VARCOEF3D = range(9)
 
 
 class EigError(RuntimeError):
@@ -61,7 +62,8 @@ class _MatInfo(ctypes.Structure):
                [("br", ctypes.c_int), ("bc", ctypes.c_int)] + \
                [(k, ctypes.c_int64) for k in ("halo_recv", "halo_send", "device_bytes", "stencil_slices",
                                               "rows_per_lane", "sym_offsets", "sym_arrays",
-                                              "sym_mask_bytes", "sym_uniform")]
+                                              "sym_mask_bytes", "sym_uniform", "sym_geo",
+                                              "march_variant")]
 
 
 class BlockTiming(ctypes.Structure):
@@ -460,12 +462,13 @@ class Matrix:
         self.ctx.check(lib.eig_mv_host(self.h, _np_ptr(x), _np_ptr(y)))
         return y
 
-    def tune(self, march_runs=0, box_segs=None, march_prefetch=None, halo_whole=None):
-        """eig_mat_tune: EIG_TUNE_MARCH_RUNS = plane runs per column of the plane-march kernels,
-        EIG_TUNE_BOX_SEGS = z segments per tile column of the box kernels, EIG_TUNE_MARCH_PREFETCH =
-        the geometric march variant (1 plain, 2-4 the +D operand 1-3 planes ahead, 5 + gathers one
-        plane ahead; 0 = automatic)."""
-        self.ctx.check(lib.eig_mat_tune(self.h, 1, int(march_runs)))
+    def tune(self, march_runs=None, box_segs=None, march_prefetch=None, halo_whole=None):
+        """eig_mat_tune, only for the keys given (None leaves a key as it is): EIG_TUNE_MARCH_RUNS =
+        plane runs per column of the plane-march kernels, EIG_TUNE_BOX_SEGS = z segments per tile
+        column of the box kernels, EIG_TUNE_MARCH_PREFETCH = the geometric march variant (eigmi.h;
+        0 = automatic), EIG_TUNE_HALO = distributed steps: exchange first + one launch."""
+        if march_runs is not None:
+            self.ctx.check(lib.eig_mat_tune(self.h, 1, int(march_runs)))
         if box_segs is not None:
             self.ctx.check(lib.eig_mat_tune(self.h, 2, int(box_segs)))
         if march_prefetch is not None:
@@ -1001,9 +1004,13 @@ def image_bytes(M, op, m=8):
     band = info.sym_offsets > 0
     mat = (8 * info.sym_arrays + info.sym_mask_bytes) * n if band else 12 * nnz + 4 * (n + 1)
     if op == "spmv":
-        if band and info.sym_uniform and M.kernel("spmv") == "k_spmv_march":
-            # uniform band: the values ride in the arguments (2: the row masks are geometric too)
-            return (0 if info.sym_uniform == 2 else info.sym_mask_bytes * n) + 16 * n
+        if band and M.kernel("spmv") == "k_spmv_march":
+            v = info.march_variant
+            if v >= 10:  # the value march: band arrays streamed, geometric masks (no mask stream)
+                return 8 * info.sym_arrays * n + 16 * n
+            if v >= 1:
+                # uniform band: the values ride in the arguments (2..9: the row masks are geometric too)
+                return (0 if v >= 2 else info.sym_mask_bytes * n) + 16 * n
         return mat + 16 * n
     if op == "spmm":
         if M.kernel("spmm8") == "k_boxc_mv8":  # row-class image: the class table lives in LDS

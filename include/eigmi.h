@@ -178,6 +178,12 @@ typedef struct eig_mat_info {
                              the vectors only; 2: besides, the rows form a grid whose rows store
                              exactly their in-grid neighbours, and the march derives the row masks
                              from the coordinates (vectors only); EIG_MAT_NO_UNIFORM: 0 */
+  int64_t sym_geo;        /* 1: the rows form a grid whose rows store exactly their in-grid
+                             neighbours (geometric row masks; a property of the pattern, any values) */
+  int64_t march_variant;  /* plane-march variant of a whole-matrix fused Lanczos launch (-1: no
+                             march, the row kernels): 0 band arrays + loaded masks, 1 uniform values +
+                             loaded masks, 2..9 uniform values + geometric masks, 10 / 11 band arrays
+                             streamed + geometric masks (the value march; 11 one plane ahead) */
 } eig_mat_info;
 int eig_mat_get_info(eig_mat_t mat, eig_mat_info *info);
 
@@ -208,8 +214,10 @@ enum { EIG_TUNE_MARCH_RUNS = 1, EIG_TUNE_BOX_SEGS = 2, EIG_TUNE_MARCH_PREFETCH =
  * plain march, 2 / 3 / 4 = the +D operand loaded 1 / 2 / 3 planes ahead, 5 = 3 planes ahead and the
  * neighbour gathers 1 plane ahead; 6 / 7 / 8 = the variants of 2 / 3 / 5 without row masks or
  * selects (missing neighbours read as exact zeros; grids whose x extent is a multiple of 64);
- * 0 = automatic.  Bitwise
- * the same results for every value. */
+ * on geometric bands whose values are not uniform (or EIG_MAT_NO_UNIFORM): 1 = the plain masked
+ * march on the band arrays, 9 = the value march (eig_mat_info.march_variant 10: the band arrays
+ * streamed, masks from the coordinates), 10 = the same with the value streams one plane ahead (11);
+ * 0 = automatic.  Bitwise the same results for every value. */
 int eig_mat_tune(eig_mat_t mat, int key, int value);
 
 /* a13: A += shift*I on the diagonal of every diagonal block (eigensolver.hh:59-66). */
@@ -550,7 +558,9 @@ double eig_bytes_orthonormalize_blocked(int64_t n, int64_t m, int b);
  *   2 2-D partition-of-unity B (.cc:124-143)       3 2-D identity pattern (.cc:145-156)
  *   4 3-D Poisson 7-pt N^3                          5 3-D Q1 "elasticity" L_Q1 (x) C, 3x3 blocks
  *   6 3-D P1 stiffness K, Kuhn 6-tet split, N^3     7 3-D P1 consistent mass M, same 15-pt pattern
- *     interior nodes, h = 1/(N+1) (config C5)            (pattern(K) == pattern(M), config C5) */
+ *     interior nodes, h = 1/(N+1) (config C5)            (pattern(K) == pattern(M), config C5)
+ *   8 3-D 7-pt variable-coefficient diffusion N^3: kind 4's pattern, a hashed conductance in
+ *     [0.5, 1.5) per grid edge (bitwise symmetric), diagonal = the six face conductances' sum */
 int64_t eig_gen_nnzb(int kind, int N);
 int eig_gen_matrix(int kind, int N, int overlap, int64_t *rowptr, int32_t *col, double *vals);
 /* Rows [row_begin, row_begin + nrows) of the same matrix (for eig_mat_create_bcsr_dist). */

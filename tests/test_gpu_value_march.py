@@ -1,0 +1,177 @@
+"""The value-streaming plane march (k_spmv.hip march_rows_geo2<VAL>, march variants 10 / 11): the
+BCRSMatrix::mv / Lanczos step kernels on a geometric 7-point (or 5-point) band whose values are NOT
+constant, so every stored value is read from the symmetric band arrays in HBM on every launch
+(the reference reads every stored value per call: kernels_cpp.hh:611-617, arpack_geneo_wrapper.hh:275).
+
+Bar: eig_mv BITWISE the reference row loop (oracle.csr_mv = matmul_sparse_tallskinny_naive,
+kernels_cpp.hh:596-621); the classic and fused Lanczos alpha / beta BITWISE equal to the plain
+masked march (variant 0: same rows per wave, same reduction order) at every plane-run count, and
+within 1e-12 (relative) of the oracle's restated recurrences.  The matrices: eig_gen kind 8 (a hashed
+conductance per grid edge), 7-point Poisson with EIG_MAT_NO_UNIFORM, and random symmetric boxes."""
+import numpy as np
+import pytest
+
+import eigmi
+import oracle
+
+
+def varcoef(N):
+    rp, c, v = eigmi.gen_matrix(eigmi.GEN_VARCOEF3D, N)
+    return oracle.CSR(N ** 3, rp, c, v)
+
+
+def test_varcoef_generator_properties():
+    """kind 8: the 7-point pattern of kind 4, bitwise symmetric, off-diagonals in (-1.5, -0.5],
+    diagonally dominant rows (strictly on the Dirichlet faces), no two grid edges alike."""
+    N = 12
+    A = varcoef(N)
+    P = oracle.poisson3d(N)
+    assert np.array_equal(A.rowptr, P.rowptr) and np.array_equal(A.col, P.col)
+    import scipy.sparse as sp
+    S = sp.csr_matrix((A.val, A.col, A.rowptr), shape=(A.n, A.n))
+    assert (S != S.T).nnz == 0
+    r = np.repeat(np.arange(A.n), np.diff(A.rowptr))
+    off = A.val[A.col != r]
+    assert off.max() <= -0.5 and off.min() > -1.5
+    assert len(np.unique(off)) > 0.45 * off.size  # each grid edge its own value (stored twice)
+    d = A.val[A.col == r]
+    rowabs = np.bincount(r, weights=np.abs(A.val)) - d
+    assert np.all(d >= rowabs * (1 - 1e-15)) and np.count_nonzero(d > rowabs + 0.4) == N ** 3 - (N - 2) ** 3
+    # the distributed generator produces the same rows
+    rp2, c2, v2 = eigmi.gen_rows(eigmi.GEN_VARCOEF3D, N, 5 * N * N, 3 * N * N)
+    lo, hi = A.rowptr[5 * N * N], A.rowptr[8 * N * N]
+    assert np.array_equal(v2, A.val[lo:hi]) and np.array_equal(c2, A.col[lo:hi])
+
+
+def _box_random(nx, ny, nz, seed):
+    """Random symmetric 7-point values on an nx x ny x nz box (positive diagonal, one random value per
+    grid edge)."""
+    import scipy.sparse as sp
+    rng = np.random.default_rng(seed)
+    n = nx * ny * nz
+    idx = np.arange(n)
+    x, y, z = idx % nx, (idx // nx) % ny, idx // (nx * ny)
+    rows, cols, vals = [idx], [idx], [6.0 + rng.random(n)]
+    for step, ok in ((1, x < nx - 1), (nx, y < ny - 1), (nx * ny, z < nz - 1)):
+        i = idx[ok]
+        w = -0.5 - rng.random(i.size)
+        rows += [i, i + step]
+        cols += [i + step, i]
+        vals += [w, w]
+    S = sp.csr_matrix((np.concatenate(vals), (np.concatenate(rows), np.concatenate(cols))), shape=(n, n))
+    S.sort_indices()
+    return oracle.CSR(n, S.indptr.astype(np.int64), S.indices.astype(np.int32), S.data.astype(np.float64))
+
+
+MATS = {
+    "varcoef64": lambda: (varcoef(64), 0),
+    "poisson64_arrays": lambda: (oracle.poisson3d(64), eigmi.MAT_NO_UNIFORM),
+    "box64x16x20": lambda: (_box_random(64, 16, 20, 3), 0),
+    "box128x3x9": lambda: (_box_random(128, 3, 9, 4), 0),
+}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mat", list(MATS))
+def test_value_march_bitwise(ctx, mat):
+    A, flags = MATS[mat]()
+    M = eigmi.Matrix.from_bcsr(ctx, A.rowptr, A.col, A.val, flags=flags)
+    info = M.info
+    assert info.sym_geo == 1 and info.sym_uniform == 0 and info.march_variant == 10
+    n = A.n
+    assert M.lanczos_kernel_info(True) == ("k_lanczos_fused_march", 8 * info.sym_arrays * n + 32 * n)
+    assert eigmi.image_bytes(M, "spmv") == 8 * info.sym_arrays * n + 16 * n
+    x = np.random.default_rng(11).standard_normal(n)
+    ref = oracle.csr_mv(A, x)
+    for runs in (0, 1, 2, 3, 5, 7):
+        base = {}
+        for pf in (1, 9, 10):  # 1: the plain masked march on the arrays; 9 / 10: variants 10 / 11
+            M.tune(runs, march_prefetch=pf)
+            assert M.info.march_variant == {1: 0, 9: 10, 10: 11}[pf]
+            assert np.array_equal(M.mv_host(x), ref), (runs, pf)
+            for fused in (False, True):
+                a, b, _ = eigmi.lanczos_run(M, 25, seed=7, fused=fused)
+                if pf == 1:
+                    base[fused] = (a, b)
+                else:
+                    assert np.array_equal(a, base[fused][0]) and np.array_equal(b, base[fused][1]), (runs, pf, fused)
+    M.tune(0, march_prefetch=0)
+    fa, fb, _ = eigmi.lanczos_run(M, 20, seed=123, fused=True)
+    qa, qb = oracle.lanczos_fused(A, oracle.random_vec(n, 123), 20)
+    assert np.allclose(fa, qa, rtol=1e-12, atol=0) and np.allclose(fb, qb, rtol=1e-12, atol=0)
+    ca, cb, _ = eigmi.lanczos_run(M, 20, seed=123)
+    _, ra, rb = oracle.lanczos(A, oracle.random_vec(n, 123), 20)
+    assert np.allclose(ca, ra, rtol=1e-12, atol=0) and np.allclose(cb, rb, rtol=1e-12, atol=0)
+
+
+@pytest.mark.gpu
+def test_value_march_after_shift(ctx):
+    """A += sigma I updates the band arrays the value march streams (StandardLargest's shift,
+    eigensolver.hh:59-66): eig_mv bitwise the shifted reference matrix."""
+    A = varcoef(64)
+    M = eigmi.Matrix.from_bcsr(ctx, A.rowptr, A.col, A.val)
+    assert M.info.march_variant == 10
+    M.shift_diag(-2.375)
+    val = A.val.copy()
+    oracle.lib.orc_shift_diag(A.n, A.rowptr, A.col, val, -2.375)
+    x = np.random.default_rng(2).standard_normal(A.n)
+    assert np.array_equal(M.mv_host(x), oracle.csr_mv(oracle.CSR(A.nrows, A.rowptr, A.col, val), x))
+
+
+@pytest.mark.gpu
+def test_lower_only_entry_not_uniform(ctx):
+    """A constant band whose one LOWER entry (its mirror not stored: a one-sided pattern) has another
+    value must not be taken as a uniform band (the uniform march would use the array's constant for
+    it).  Row 1000 of the 16^3 Poisson keeps (1000, 999) = -2.5 while (999, 1000) is dropped."""
+    P = oracle.poisson3d(16)
+    keep = np.ones(P.val.size, bool)
+    r = 999
+    keep[P.rowptr[r] + int(np.nonzero(P.col[P.rowptr[r]:P.rowptr[r + 1]] == 1000)[0][0])] = False
+    val = P.val.copy()
+    val[P.rowptr[1000] + int(np.nonzero(P.col[P.rowptr[1000]:P.rowptr[1001]] == 999)[0][0])] = -2.5
+    counts = np.diff(P.rowptr) - np.add.reduceat(~keep, P.rowptr[:-1]).astype(np.int64)
+    rp = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+    A = oracle.CSR(P.n, rp, P.col[keep].copy(), val[keep].copy())
+    M = eigmi.Matrix.from_bcsr(ctx, A.rowptr, A.col, A.val)
+    assert M.info.sym_offsets == 7 and M.info.sym_uniform == 0
+    x = np.random.default_rng(5).standard_normal(A.n)
+    assert np.array_equal(M.mv_host(x), oracle.csr_mv(A, x))
+
+
+@pytest.fixture(scope="module")
+def v256(ctx):
+    N = 256
+    rp, c, v = eigmi.gen_matrix(eigmi.GEN_VARCOEF3D, N)
+    M = eigmi.Matrix.from_bcsr(ctx, rp, c, v)
+    return N, M, oracle.CSR(N ** 3, rp, c, v)
+
+
+@pytest.mark.gpu
+def test_value_march_256_bitwise(ctx, v256):
+    """Configuration size (C4's grid, variable coefficients): eig_mv bitwise the oracle row loop."""
+    N, M, A = v256
+    assert M.info.march_variant == 10
+    x = np.random.default_rng(9).standard_normal(N ** 3)
+    assert np.array_equal(M.mv_host(x), oracle.csr_mv(A, x))
+
+
+@pytest.mark.gpu
+def test_value_march_256_lanczos(ctx, v256):
+    """The benchmark step on the value-streaming image at 256^3: 3 fused steps vs orc_lanczos_fused
+    and 4 classic steps vs orc_lanczos_rotating (rtol 1e-12), then 30 fused GPU steps against the
+    two-kernel GPU recurrence (rtol 1e-11)."""
+    N, M, A = v256
+    n = N ** 3
+    U0 = np.zeros(n)
+    oracle.lib.orc_random_vec(n, 123, U0)
+    fa, fb, _ = eigmi.lanczos_run(M, 3, seed=123, fused=True)
+    ra, rb = oracle.lanczos_fused(A, U0, 3)
+    assert np.allclose(fa, ra, rtol=1e-12, atol=0) and np.allclose(fb, rb, rtol=1e-12, atol=0)
+    ca, cb, _ = eigmi.lanczos_run(M, 4, seed=123)
+    u1, u2 = np.zeros(n), np.zeros(n)
+    qa, qb = np.zeros(4), np.zeros(5)
+    oracle.lib.orc_lanczos_rotating(n, A.rowptr, A.col, A.val, 4, U0, u1, u2, qa, qb)
+    assert np.allclose(ca, qa, rtol=1e-12, atol=0) and np.allclose(cb, qb, rtol=1e-12, atol=0)
+    fa, fb, _ = eigmi.lanczos_run(M, 30, seed=123, fused=True)
+    ca, cb, _ = eigmi.lanczos_run(M, 30, seed=123)
+    assert np.allclose(fa, ca, rtol=1e-11) and np.allclose(fb, cb, rtol=1e-11)

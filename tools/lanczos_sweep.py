@@ -4,6 +4,7 @@
 Variant spec "<fused|pipelined|classic|mv>[:<image>][@<runs>][#<pf>]" (runs: plane runs per column of
 the march kernels, pf: the geometric march variant, eig_mat_tune; default automatic) with image one of
     band     (default) symmetric band image, plane march where the band allows it
+    arrays   band image with the values streamed from the band arrays (EIG_MAT_NO_UNIFORM)
     gather   band image, every offset through its own gather (EIG_MAT_BAND_GATHER)
     nomarch  band image, row kernels (EIG_MAT_NO_MARCH)
     sell     SELL-64 / stencil-slice image (EIG_MAT_NO_BAND)
@@ -24,7 +25,7 @@ import numpy as np  # noqa: E402
 
 import eigmi  # noqa: E402
 
-IMAGES = {"band": 0, "gather": eigmi.MAT_BAND_GATHER, "nomarch": eigmi.MAT_NO_MARCH, "sell": eigmi.MAT_NO_BAND,
+IMAGES = {"band": 0, "arrays": eigmi.MAT_NO_UNIFORM, "gather": eigmi.MAT_BAND_GATHER, "nomarch": eigmi.MAT_NO_MARCH, "sell": eigmi.MAT_NO_BAND,
           "explicit": eigmi.MAT_NO_BAND | eigmi.MAT_NO_STENCIL}
 
 
@@ -44,6 +45,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--slab", type=int, default=0, help="N x N x slab box instead of the N^3 cube")
+    ap.add_argument("--matrix", choices=["poisson", "varcoef"], default="poisson",
+                    help="7-point Poisson (eig_gen kind 4) or the variable-coefficient 7-point (kind 8)")
     args = ap.parse_args()
     ctx = eigmi.Context(0)
     N = args.N
@@ -63,7 +66,7 @@ def main():
         n = A.shape[0]
     else:
         n = N ** 3
-        rp, c, v = eigmi.gen_matrix(eigmi.GEN_POISSON3D, N)
+        rp, c, v = eigmi.gen_matrix(eigmi.GEN_VARCOEF3D if args.matrix == "varcoef" else eigmi.GEN_POISSON3D, N)
     nnz = int(rp[-1])
     specs = args.variants.split(",")
     mats = {}
@@ -102,7 +105,13 @@ def main():
         r = res[spec]
         km = float(np.median(r["k_us"]))
         sm = float(np.median(r["step_us"]))
-        print(json.dumps({"variant": spec, "kernel": M.kernel({"mv": "spmv", "fused": "fused", "pipelined": "spmv",
+        info = M.info
+        ib = eigmi.image_bytes(M, "spmv") + (16 * n if op == "fused" else 0)  # bytes the image streams
+        print(json.dumps({"variant": spec, "matrix": args.matrix, "march_variant": info.march_variant,
+                          "image_bytes": ib if op in ("mv", "fused") else None,
+                          "image_frac": round(ib / (float(np.median(res[spec]["k_us"])) * 1e3) / 8000, 4)
+                          if op in ("mv", "fused") else None,
+                          "kernel": M.kernel({"mv": "spmv", "fused": "fused", "pipelined": "spmv",
                                                              "classic": "k1"}[op]),
                           "kernel_us_med": round(km, 2), "kernel_us_min": round(min(r["k_us"]), 2),
                           "kernel_csr_GBs": round(kb / km / 1e3, 1), "step_us_med": round(sm, 2),
