@@ -3,10 +3,17 @@
 256^3 DoF (BASELINE.json metric), fp64, 1..8 MI355X.
 
 One "step" = one Lanczos three-term-recurrence iteration (no re-orthogonalisation) of the whole
-256^3 problem: the fused SpMV kernel (t = A u sig - gam u_prev, t.u) + the fused update kernel
-(u_next = t - alpha sig u, ||u_next||^2), plus at N > 1 the one-plane RCCL halo exchange and two
-one-double allreduces.  The matrix is row-partitioned in z-slabs (strong scaling: the total work
-is fixed as N grows).
+256^3 problem: by default the fused one-reduction step (one kernel: t = A u sig - gam u_prev and the
+step's three sums), plus at N > 1 the one-plane RCCL halo exchange and one 3-value
+allreduce.  The matrix is row-partitioned in z-slabs (strong scaling: the total work is fixed as N
+grows).
+
+The timed image reads every stored matrix value from HBM on every step, as BCRSMatrix::mv does
+(kernels_cpp.hh:611-617): `--image arrays` (default) = the symmetric band arrays (EIG_MAT_NO_UNIFORM:
+the 4 upper diagonals, 32 B per row, lower entries through the mirrored slots).  At N = 1 the line
+also carries the same step on the SELL / CSR image (`csr`: values + column structure) and the
+constant-coefficient shortcut (`stencil_shortcut`: band values in the kernel arguments, no matrix
+bytes) -- side numbers, never `value` or `roofline`.
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 --master-port P \
@@ -52,23 +59,21 @@ def cpu_baseline(N, rp, c, v, steps, gpu_alpha, fused):
     return steps / dt, dt, rel
 
 
-def cpu_replicas(N, steps, fused, threads):
+def cpu_replicas(N, rp0, c0, v0, steps, fused, threads):
     """SURVEY 8(d) CPU baseline (ii): the reference's own parallel mode (src/dune-eigensolver.cc:
     754-760, aggregate as at :292-294) -- `threads` independent replicas of the single-thread solve,
-    each on its own copy of the matrix and vectors, started together behind a barrier; value =
-    replicas x steps / wall time.  ctypes drops the GIL, so the replicas run in parallel."""
+    each on its own copy of the matrix (rp0, c0, v0) and vectors, started together behind a barrier;
+    value = replicas x steps / wall time.  ctypes drops the GIL, so the replicas run in parallel."""
     import threading
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # noqa: E402  (checker / baseline only)
     n = N ** 3
-    nnz = int(oracle.lib.orc_poisson3d_nnz(N))
     bar = threading.Barrier(threads + 1)
     err = []
 
     def replica():
         try:
-            rp, c, v = np.zeros(n + 1, np.int64), np.zeros(nnz, np.int32), np.zeros(nnz)
-            oracle.lib.orc_poisson3d(N, rp, c, v)
+            rp, c, v = rp0.copy(), c0.copy(), v0.copy()
             u0, u1, u2 = np.zeros(n), np.zeros(n), np.zeros(n)
             oracle.lib.orc_random_vec(n, 123, u0)
             alpha, beta = np.zeros(steps), np.zeros(steps + 1)
@@ -109,11 +114,12 @@ def cpu_model():
     return None
 
 
-def committed_traffic(kernel, N, world, build):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summaries
-    (profiles/<tag>_pmc_summary.json, FETCH_SIZE x2 + WRITE_SIZE, KiB -> B; tools/profile_round.sh)
-    taken on the same configuration: the newest one profiled on this build (eigmi.build_id()) when
-    there is one, else the newest of any build; (bytes, source, same_build) or None."""
+def committed_traffic(kernel, N, world, build, image):
+    """HBM bytes per launch of `kernel` (a template instance "k_...<...>" matches exactly, a bare name
+    any instance) from the committed rocprofv3 PMC summaries (profiles/<tag>_pmc_summary.json,
+    FETCH_SIZE x2 + WRITE_SIZE, KiB -> B; tools/profile_round.sh) taken on the same configuration and
+    matrix image: the newest one profiled on this build (eigmi.build_id()) when there is one, else the
+    newest of any build; (bytes, source, same_build) or None."""
     import glob
     best = None
     for p in glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json")):
@@ -123,8 +129,10 @@ def committed_traffic(kernel, N, world, build):
             cfg = line.get("config") if isinstance(line, dict) else None
             if not isinstance(cfg, dict) or cfg.get("N") != N or line.get("n_gpus") != world:
                 continue
+            if cfg.get("image", "uniform") != image:
+                continue
             for name, k in d["kernels"].items():  # template instances: "eigmi::k_..._b1<1, 1>"
-                if name.split("<")[0] == "eigmi::" + kernel:
+                if (name == "eigmi::" + kernel) if "<" in kernel else (name.split("<")[0] == "eigmi::" + kernel):
                     same = d.get("build") is not None and d.get("build") == build
                     stamp = (same, d.get("collected", os.path.getmtime(p)))
                     if best is None or stamp > best[2]:
@@ -136,6 +144,60 @@ def committed_traffic(kernel, N, world, build):
 
 VARIANT_NAME = {"fused": "fused one-reduction step", "pipelined": "pipelined one-reduction step",
                 "classic": "SpMV + update kernels"}
+# matrix images (eig_mat_create_bcsr_ex flags)
+IMAGES = {"arrays": eigmi.MAT_NO_UNIFORM, "csr": eigmi.MAT_NO_BAND, "uniform": 0}
+
+
+def image_name(M):
+    """What the step kernel streams on this image (config.matrix_image)."""
+    info = M.info
+    v = info.march_variant
+    if info.sym_offsets == 0:
+        return "SELL-64 / CSR image (values + column structure: stencil slices keep offsets + a 1-B row mask)"
+    if v >= 10:
+        return (f"symmetric band arrays streamed every step ({info.sym_arrays} upper diagonals, "
+                f"{8 * info.sym_arrays} B per row; lower entries through the mirrored slots; row masks from "
+                f"the grid coordinates; the (t, u) pairs streamed)")
+    if v >= 2:
+        return ("uniform band on a grid (constant coefficients: the band values in the kernel arguments, row "
+                "masks from the grid coordinates; the (t, u) pairs streamed -- reads no matrix bytes)")
+    if v == 1:
+        return "uniform band (band values in the kernel arguments, 1-B row mask + (t, u) pairs streamed)"
+    return "symmetric band arrays + 1-B row mask streamed every step"
+
+
+def kernel_instance(M, kname):
+    """The template instance of a march kernel (as rocprofv3 names it), else the bare name."""
+    info = M.info
+    if kname.endswith("_march") and info.march_variant >= 0 and info.sym_mask_bytes == 1 and info.sym_offsets <= 7:
+        return f"{kname}<unsigned char, true, {info.march_variant}>"
+    return kname
+
+
+def side_image(ctx, rp, c, v, image, steps, n, nnz):
+    """N = 1 side measurement: the same fused step on another image of the same matrix (K eager steps,
+    region events: one launch per step), priced at the bytes that image streams and at SURVEY 8(d)'s
+    CSR step bytes."""
+    M = eigmi.Matrix.from_bcsr(ctx, rp, c, v, flags=IMAGES[image])
+    try:
+        ws = eigmi.LanczosWorkspace(M, steps + 5, seed=123, fused=True)
+        ws.step(5)
+        ctx.sync()
+        t0 = time.perf_counter()
+        tim = ws.step(steps)
+        ctx.sync()
+        dt = time.perf_counter() - t0
+        kname, kb = M.lanczos_kernel_info(True)
+        ws.close()
+        us = tim.total_ms / steps * 1e3
+        sb = eigmi.bytes_lanczos_step(n, nnz)
+        return {"image": image, "matrix_image": image_name(M), "kernel": kernel_instance(M, kname),
+                "value": round(steps / dt, 3), "unit": "iters/s", "ms_per_step": round(dt / steps * 1e3, 4),
+                "avg_launch_us": round(us, 2), "bytes_per_launch": kb,
+                "achieved_GBs": round(kb / us / 1e3, 1), "frac": round(kb / us / 1e3 / HBM_PEAK_GBS, 4),
+                "survey_step_bytes": sb, "survey_step_GBs": round(sb / (dt / steps) / 1e9, 1)}
+    finally:
+        M.close()
 
 
 def main():
@@ -144,6 +206,15 @@ def main():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--N", type=int, default=256, help="grid points per axis (n = N^3)")
+    ap.add_argument("--matrix", choices=["poisson", "varcoef"], default="poisson",
+                    help="poisson: the 7-point Poisson matrix of the metric (eig_gen kind 4); varcoef: the "
+                         "same pattern with a hashed conductance per grid edge (kind 8)")
+    ap.add_argument("--image", choices=list(IMAGES), default="arrays",
+                    help="matrix image of the timed step: arrays = symmetric band arrays streamed every step "
+                         "(EIG_MAT_NO_UNIFORM), csr = SELL / CSR image (EIG_MAT_NO_BAND), uniform = the "
+                         "constant-coefficient shortcut (band values in the kernel arguments, no matrix bytes)")
+    ap.add_argument("--side-steps", type=int, default=50,
+                    help="N = 1: steps of the csr / stencil_shortcut side measurements (0 = skip them)")
     ap.add_argument("--cpu-steps", type=int, default=160, help="Lanczos steps of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-replicas", type=int, default=None,
@@ -201,12 +272,13 @@ def main():
     N = args.N
     n = N ** 3
     b, cnt = eigmi.row_partition(n, world, rank, align=N * N)
-    rp, c, v = eigmi.gen_rows(eigmi.GEN_POISSON3D, N, b, cnt)
+    gkind = eigmi.GEN_VARCOEF3D if args.matrix == "varcoef" else eigmi.GEN_POISSON3D
+    rp, c, v = eigmi.gen_rows(gkind, N, b, cnt)
     if world > 1:
-        M = eigmi.Matrix.from_rows(ctx, n, b, rp, c, v)
+        M = eigmi.Matrix.from_rows(ctx, n, b, rp, c, v, flags=IMAGES[args.image])
     else:
-        M = eigmi.Matrix.from_bcsr(ctx, rp, c, v)
-    nnz_total = int(eigmi.lib.eig_gen_nnzb(eigmi.GEN_POISSON3D, N))
+        M = eigmi.Matrix.from_bcsr(ctx, rp, c, v, flags=IMAGES[args.image])
+    nnz_total = int(eigmi.lib.eig_gen_nnzb(gkind, N))
     nnz_local = int(rp[-1])
 
     K, W = args.steps, args.warmup
@@ -342,14 +414,14 @@ def main():
     roofline = None
     if k1_ms:
         ach = k1_bytes / (k1_ms * 1e-3) / 1e9
-        tr = committed_traffic(kname, N, world, build)
+        tr = committed_traffic(kernel_instance(M, kname), N, world, build, args.image)
         roofline = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": tr[0] if tr else None,
                     "traffic_source": tr[1] if tr else None,
                     "traffic_same_build": tr[2] if tr else None,
                     "traffic_GBs": round(tr[0] / (k1_ms * 1e-3) / 1e9, 1) if tr else None,
                     "traffic_frac": round(tr[0] / (k1_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if tr else None,
-                    "kernel": kname, "bytes_per_launch": k1_bytes,
+                    "kernel": kernel_instance(M, kname), "bytes_per_launch": k1_bytes,
                     "avg_launch_us": round(k1_ms * 1e3, 2),
                     "launch_timing": ("region events / K (one launch per step; includes the inter-launch gap)"
                                       if region else
@@ -376,6 +448,12 @@ def main():
                 "csr_bytes": cb, "csr_equiv_GBs": round(cb / (mv_ms * 1e-3) / 1e9, 1)}
         x.free()
         y.free()
+    sides = {}
+    if rank == 0 and world == 1 and args.side_steps > 0:
+        # the same step on the other images of the same matrix (side numbers: never value / roofline)
+        for img, key in (("csr", "csr"), ("uniform", "stencil_shortcut")):
+            if img != args.image:
+                sides[key] = side_image(ctx, rp, c, v, img, args.side_steps, n, nnz_total)
     if rank == 0:
         copy_GBs = eigmi.stream_copy_GBs(ctx)
         if spmv:
@@ -395,16 +473,13 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (generated 7-point Poisson matrix, mt19937 seed-123 start vector)",
-        "config": {"workload": f"3D Poisson 7-pt {N}^3 Lanczos 3-term step, no re-orthogonalisation"
-                               f" ({VARIANT_NAME[variant]})",
-                   "N": N, "n": n, "nnz": nnz_total,
-                   "matrix_image": ("uniform band on a grid (constant coefficients: the 7 band values in the "
-                                    "kernel arguments, row masks from the grid coordinates; the (t, u) pairs "
-                                    "streamed)" if M.info.sym_uniform == 2 else
-                                    "uniform band (constant coefficients: the 7 band values in the kernel "
-                                    "arguments, 1-B row mask + (t, u) pairs streamed)" if M.info.sym_uniform else
-                                    "symmetric band arrays + row mask" if M.info.sym_offsets else "SELL / CSR"),
+        "data": ("synthetic (generated 7-point Poisson matrix" if args.matrix == "poisson" else
+                 "synthetic (generated variable-coefficient 7-point matrix, eig_gen kind 8") +
+                ", mt19937 seed-123 start vector)",
+        "config": {"workload": f"3D {'Poisson' if args.matrix == 'poisson' else 'variable-coefficient'} 7-pt "
+                               f"{N}^3 Lanczos 3-term step, no re-orthogonalisation ({VARIANT_NAME[variant]})",
+                   "N": N, "n": n, "nnz": nnz_total, "matrix": args.matrix, "image": args.image,
+                   "matrix_image": image_name(M),
                    "parallelism": (f"row-partition z-slabs x{world} (RCCL halo, {halo_mode} launch, "
                                    f"{ctx.comm_info()['allreduce']} allreduce)") if world > 1 else
                                   ("single GPU, one-rank RCCL allreduce per step" if args.comm_self else "single GPU")},
@@ -415,6 +490,9 @@ def main():
         "spmv_hbm_gbs": roofline["achieved"] if roofline else None,
         # eig_mv alone (y = A x on the same image, 20 launches x 3, best average), beside the step
         "spmv": spmv,
+        # N = 1: the same fused step on the SELL / CSR image (SURVEY 8(d)'s CSR bytes are what it streams at
+        # most) and on the constant-coefficient shortcut (no matrix bytes) -- side numbers only
+        **sides,
         # device time of the K steps: fused SpMV launches vs the rest (update kernel, allreduces)
         "device_ms": {"total": round(tim.total_ms, 3),
                       "spmv": round(tim.total_ms if region else tim.spmv_ms, 3),
@@ -441,7 +519,7 @@ def main():
             # machine), and each replica holds its own 1.9 GB matrix + vectors
             P = min(16, usable)
         if P > 0:
-            pv, pdt = cpu_replicas(N, args.cpu_replica_steps, fused, P)
+            pv, pdt = cpu_replicas(N, rp, c, v, args.cpu_replica_steps, fused, P)
             out["cpu_baseline"]["replicas"] = {
                 "value": round(pv, 4) if pv else None, "unit": "iters/s", "cores": P,
                 "sample": f"{P} concurrent replicas x {args.cpu_replica_steps} steps, each on its own "

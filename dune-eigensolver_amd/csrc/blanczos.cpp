@@ -32,6 +32,7 @@ struct eig_blanczos_s {
   // Chebyshev-Jacobi solve
   eig_mg_s *mg = nullptr;
   int cycles = 0;
+  long long cholqr_recomputed = 0;  // CholQR2 second passes that recomputed M Z (ill-conditioned blocks)
   i64 ld = 0, own = 0, n = 0;
   DevBuf *V = nullptr;                   // (max_steps + 1) * b columns, window layout
   DevBuf *W = nullptr, *Xa = nullptr, *Xb = nullptr, *Xc = nullptr, *MZ = nullptr;  // b columns each
@@ -139,6 +140,9 @@ double *cheb_solve(eig_mat_s &M, i64 m, int degree, double lmin, double lmax, co
 namespace {
 double *dptr(DevBuf *b) { return b->d(); }
 
+// R0 diagonal spread beyond which CholQR2's second pass recomputes M Z instead of reusing (M Z) R0^-1
+constexpr double kCholQrReuseCond = 1e4;
+
 // Z (b columns) = Vdst R with Vdst M-orthonormal (CholQR twice); R (b x b upper, row-major) on
 // the host.  Vdst may equal Z.  The b x b factorisations run on the device (k_chol_small: the host
 // chol_upper / tri_upper_inv arithmetic), so the two passes queue without a host round trip; one
@@ -155,39 +159,49 @@ void mcholqr2(eig_blanczos_s &w, double *Z, double *Vdst, std::vector<double> &R
   double *Rd = w.chol->d(), *Rt = Rd + (size_t)b * b;
   int *flag = reinterpret_cast<int *>(Rt + (size_t)b * b);
   EIG_HIP(hipMemsetAsync(flag, 0, sizeof(int), s));
-  if (b == 32)
+  halo_mv(M, Z, b, s);
+  launch_sell_mv8(M, b, Z, dptr(w.MZ), s);
+  launch_panel_gram(ctx, n, ld, b, b, Z + own * 8, dptr(w.MZ) + own * 8, Gd, s);
+  allreduce_sum(ctx, Gd, (i64)b * b, s);
+  launch_chol_small(b, 0, Gd, Rd, Sd, Rt, flag, s);  // Sd = R0^-1, Rt = R0
+  // The second pass may reuse M Z updated by the same factor (row-local: M (Z R0^-1) = (M Z) R0^-1 up
+  // to rounding) instead of a second M SpMM -- but that rounding gap is ~eps cond(Z), so for an
+  // ill-conditioned block the second pass would no longer restore M-orthonormality to ~eps (CholQR2's
+  // guarantee).  R0's diagonal decides (one small read-back): beyond kCholQrReuseCond the second pass
+  // recomputes M (Z R0^-1).
+  std::vector<double> r0((size_t)b * b);
+  EIG_HIP(hipMemcpyAsync(r0.data(), Rd, r0.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+  EIG_HIP(hipStreamSynchronize(s));
+  double dmax = 0.0, dmin = HUGE_VAL;
+  for (int i = 0; i < b; ++i)
+  {
+    const double d = std::fabs(r0[(size_t)i * b + i]);
+    dmax = std::max(dmax, d);
+    dmin = std::min(dmin, d);
+  }
+  const bool reuse = dmin > 0.0 && dmax <= kCholQrReuseCond * dmin;
+  w.cholqr_recomputed += !reuse;
+  if (reuse && b == 32)
   {
     // Z <- Z R0^-1 and the second pass's Gram (Z R0^-1)^T (M Z R0^-1) in one pass over Z and M Z
     // (k_cholqr_fold): M Z R0^-1 is never stored, Z R0^-1 is not read back
-    halo_mv(M, Z, b, s);
-    launch_sell_mv8(M, b, Z, dptr(w.MZ), s);
-    launch_panel_gram(ctx, n, ld, b, b, Z + own * 8, dptr(w.MZ) + own * 8, Gd, s);
-    allreduce_sum(ctx, Gd, (i64)b * b, s);
-    launch_chol_small(b, 0, Gd, Rd, Sd, Rt, flag, s);
     launch_cholqr_fold(ctx, n, ld, Z + own * 8, dptr(w.MZ) + own * 8, Sd, Gd, s);
-    allreduce_sum(ctx, Gd, (i64)b * b, s);
-    launch_chol_small(b, 1, Gd, Rd, Sd, Rt, flag, s);
-    launch_panel_update(n, ld, ld, b, b, Z + own * 8, Sd, 1.0, 0.0, Vdst + own * 8, s);
   }
   else
   {
-    for (int pass = 0; pass < 2; ++pass)
+    launch_panel_update(n, ld, ld, b, b, Z + own * 8, Sd, 1.0, 0.0, Z + own * 8, s);
+    if (reuse)
+      launch_panel_update(n, ld, ld, b, b, dptr(w.MZ) + own * 8, Sd, 1.0, 0.0, dptr(w.MZ) + own * 8, s);
+    else
     {
-      // pass 1 reuses M Z: the first pass updated it with the same triangular factor as Z (row-local,
-      // M (Z R^-1) = (M Z) R^-1 up to rounding), so one M SpMM per CholQR2 instead of two
-      if (pass == 0)
-      {
-        halo_mv(M, Z, b, s);
-        launch_sell_mv8(M, b, Z, dptr(w.MZ), s);
-      }
-      launch_panel_gram(ctx, n, ld, b, b, Z + own * 8, dptr(w.MZ) + own * 8, Gd, s);
-      allreduce_sum(ctx, Gd, (i64)b * b, s);
-      launch_chol_small(b, pass, Gd, Rd, Sd, Rt, flag, s);  // Sd = R^-1, Rt <- R Rt
-      launch_panel_update(n, ld, ld, b, b, Z + own * 8, Sd, 1.0, 0.0, (pass == 1 ? Vdst : Z) + own * 8, s);
-      if (pass == 0)
-        launch_panel_update(n, ld, ld, b, b, dptr(w.MZ) + own * 8, Sd, 1.0, 0.0, dptr(w.MZ) + own * 8, s);
+      halo_mv(M, Z, b, s);
+      launch_sell_mv8(M, b, Z, dptr(w.MZ), s);
     }
+    launch_panel_gram(ctx, n, ld, b, b, Z + own * 8, dptr(w.MZ) + own * 8, Gd, s);
   }
+  allreduce_sum(ctx, Gd, (i64)b * b, s);
+  launch_chol_small(b, 1, Gd, Rd, Sd, Rt, flag, s);  // Sd = R1^-1, Rt <- R1 R0
+  launch_panel_update(n, ld, ld, b, b, Z + own * 8, Sd, 1.0, 0.0, Vdst + own * 8, s);
   Rtot.assign((size_t)b * b, 0.0);
   int hflag = 0;
   EIG_HIP(hipMemcpyAsync(Rtot.data(), Rt, Rtot.size() * sizeof(double), hipMemcpyDeviceToHost, s));

@@ -7,7 +7,8 @@
 // Galerkin operator A_c = P^T A P computed on the host from the fine rows (27-point coarse
 // stencils; any fine stencil within +-1 node per direction), mirrored so that every coarse matrix
 // is bitwise symmetric (it then takes the band / box images of the device upload).  Levels stop at
-// <= 64 rows or a direction < 3 nodes.
+// <= 64 rows or a direction < 3 nodes; grids whose coarsest level would exceed kMgMaxCoarse rows (flat
+// grids: a direction runs out first) are refused.
 //
 // Solve (device, no reductions): X = S_k B with S_k = sum_{i<k} (I - V A)^i V, i.e. `cycles`
 // stationary iterations x += V (b - A x) from x = 0, V one symmetric V-cycle:
@@ -63,6 +64,9 @@ struct eig_mg_s {
 };
 
 namespace {
+
+// largest coarsest level whose D^-1/2 A D^-1/2 spectrum is computed densely on the host
+constexpr i64 kMgMaxCoarse = 1024;
 
 // Host CSR of one level (rows ascending columns).
 struct HostCsr {
@@ -320,6 +324,22 @@ extern "C" int eig_mg_create(eig_mat_t A, int nx, int ny, int nz, int max_cols, 
     EIG_CHECK(!A->ctx->distributed() && A->nb_rows == A->nb_cols && A->window == A->nb_rows, EIG_ERR_ARG,
               "eig_mg_create: square single-rank matrix required");
     EIG_CHECK((i64)nx * ny * nz == A->nb_rows, EIG_ERR_SHAPE, "eig_mg_create: nx * ny * nz must equal the rows");
+    {
+      // the coarsest level is solved through a dense host eigenvalue problem (spectrum_bounds): coarsening
+      // halves every direction and stops at a direction below 3 nodes, so a flat grid (e.g. nz = 1, or
+      // 256 x 256 x 4) would end far above 64 rows -- refuse it instead of an O(n^3) dense solve
+      int d[3] = {nx, ny, nz};
+      i64 n = A->nb_rows;
+      while (n > 64 && d[0] >= 3 && d[1] >= 3 && d[2] >= 3)
+      {
+        for (int &x : d) x /= 2;
+        n = (i64)d[0] * d[1] * d[2];
+      }
+      EIG_CHECK(n <= kMgMaxCoarse, EIG_ERR_ARG,
+                "eig_mg_create: the grid coarsens only to " + std::to_string(n) + " rows (a direction falls below 3 "
+                "nodes first; at most " + std::to_string(kMgMaxCoarse) + " rows are solved densely): semi-"
+                "coarsening of flat grids is not implemented");
+    }
     eig_ctx_t ctx = A->ctx;
     EIG_HIP(hipSetDevice(ctx->device));
     hipStream_t s = ctx->stream;

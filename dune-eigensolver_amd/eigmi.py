@@ -376,9 +376,14 @@ class Matrix:
 
     def __init__(self, ctx, handle):
         self.ctx, self.h = ctx, handle
+        self.info  # noqa: B018  (validates the handle)
+
+    @property
+    def info(self):
+        """eig_mat_get_info, queried now (tuning and shifts change the march variant / uniformity)."""
         info = _MatInfo()
-        ctx.check(lib.eig_mat_get_info(handle, ctypes.byref(info)))
-        self.info = info
+        self.ctx.check(lib.eig_mat_get_info(self.h, ctypes.byref(info)))
+        return info
 
     OPS = {"spmv": 0, "k1": 1, "fused": 2, "spmm8": 3, "cheb8": 4, "spmm32": 5, "cheb32": 6}
 

@@ -89,6 +89,139 @@ static void fused_repair_run(eig_mat_t A, double *a, double *be, int *launches, 
   CK(eig_lanczos_destroy(ws));
 }
 
+// Value-streaming images (k_spmv.hip march variants 10 / 11 where the grid allows) and the uniform-
+// band check across rank interfaces: (a) the variable-coefficient 7-point matrix (eig_gen kind 8);
+// (b) the Poisson matrix whose z couplings across plane pz (rows of planes pz - 1 / pz, both mirror
+// entries) are -2: every rank's own upper entries are still one constant per diagonal, but the
+// lower entries of rank r's first plane that point at its ghost rows are not, so no
+// rank may take the uniform march.  SpMV bitwise and the fused recurrence (split and whole halo
+// launches) within 1e-12 of the single-rank run.
+static void iface(int N, int64_t b, Rows &r, int64_t pz)
+{
+  const int64_t D = (int64_t)N * N;
+  for (int64_t i = 0; i + 1 < (int64_t)r.rp.size(); ++i)
+  {
+    const int64_t g = b + i;
+    for (int64_t p = r.rp[i]; p < r.rp[i + 1]; ++p)
+      if ((g / D == pz && r.c[p] == g - D) || (g / D == pz - 1 && r.c[p] == g + D)) r.v[p] = -2.0;
+  }
+}
+struct ValRun {
+  std::vector<double> y, fa, fb, wa, wb;
+  int64_t variant = -1, uniform = -1;
+};
+static void value_run(eig_ctx_t ctx, int N, int64_t b, int64_t cnt, bool dist, int kind, int64_t pz,
+                      const std::vector<double> &x, int steps, ValRun &o)
+{
+  const int64_t n = (int64_t)N * N * N;
+  Rows r = gen(N, b, cnt, kind);
+  if (pz > 0) iface(N, b, r, pz);
+  eig_mat_t A;
+  if (dist)
+    CK(eig_mat_create_bcsr_dist(ctx, n, b, cnt, 1, 1, r.rp.data(), r.c.data(), r.v.data(), &A));
+  else
+    CK(eig_mat_create_bcsr(ctx, n, n, 1, 1, r.rp.data(), r.c.data(), r.v.data(), &A));
+  eig_mat_info info;
+  CK(eig_mat_get_info(A, &info));
+  o.variant = info.march_variant;
+  o.uniform = info.sym_uniform;
+  double *dx, *dy;
+  CK(eig_malloc(ctx, info.window * 8, (void **)&dx));
+  CK(eig_malloc(ctx, info.window * 8, (void **)&dy));
+  CK(eig_memset(ctx, dx, 0, info.window * 8));
+  CK(eig_memcpy_h2d(ctx, dx + info.own_offset, x.data() + b, cnt * 8));
+  CK(eig_mv(A, dx, dy));
+  o.y.resize(cnt);
+  CK(eig_memcpy_d2h(ctx, o.y.data(), dy + info.own_offset, cnt * 8));
+  eig_free(ctx, dx);
+  eig_free(ctx, dy);
+  o.fa.resize(steps);
+  o.fb.resize(steps + 1);
+  CK(eig_lanczos_run(A, steps, nullptr, 123, EIG_LANCZOS_FUSED, o.fa.data(), o.fb.data(), nullptr));
+  o.wa = o.fa;
+  o.wb = o.fb;
+  if (dist)
+  {
+    CK(eig_mat_tune(A, EIG_TUNE_HALO, 1));
+    CK(eig_lanczos_run(A, steps, nullptr, 123, EIG_LANCZOS_FUSED, o.wa.data(), o.wb.data(), nullptr));
+  }
+  eig_mat_destroy(A);
+}
+static int value_images(int P, int N, const std::vector<double> &x)
+{
+  const int64_t n = (int64_t)N * N * N;
+  const int steps = 25;
+  int failures = 0;
+  for (int cs = 0; cs < 2; ++cs)
+  {
+    const int kind = cs == 0 ? 8 : 4;
+    const int64_t pz = cs == 0 ? 0 : N / P;  // the first plane of rank 1
+    ValRun ser;
+    {
+      eig_ctx_t ctx;
+      CK(eig_ctx_create(0, &ctx));
+      value_run(ctx, N, 0, n, false, kind, pz, x, steps, ser);
+      eig_ctx_destroy(ctx);
+    }
+    void *hub;
+    CK(eig_loopback_create(P, &hub));
+    std::vector<ValRun> out(P);
+    std::vector<int64_t> rb(P), rc(P);
+    std::vector<std::thread> th;
+    for (int r = 0; r < P; ++r)
+      th.emplace_back([&, r] {
+        eig_ctx_t ctx;
+        CK(eig_ctx_create(0, &ctx));
+        CK(eig_comm_init_loopback(ctx, hub, r));
+        const int64_t p0 = (int64_t)N * r / P, p1 = (int64_t)N * (r + 1) / P;
+        rb[r] = p0 * N * N;
+        rc[r] = (p1 - p0) * N * N;
+        value_run(ctx, N, rb[r], rc[r], true, kind, pz, x, steps, out[r]);
+        eig_ctx_destroy(ctx);
+      });
+    for (auto &t : th) t.join();
+    eig_loopback_destroy(hub);
+    const char *nm = cs == 0 ? "variable-coefficient" : "interface-coupling";
+    if (ser.uniform != 0)
+    {
+      std::printf("FAIL %s serial: sym_uniform %lld, expected 0\n", nm, (long long)ser.uniform);
+      ++failures;
+    }
+    for (int r = 0; r < P; ++r)
+    {
+      if (std::memcmp(out[r].y.data(), ser.y.data() + rb[r], rc[r] * 8) != 0)
+      {
+        std::printf("FAIL %s rank %d: distributed SpMV not bitwise the serial one\n", nm, r);
+        ++failures;
+      }
+      // (b): ranks 0 and 1 hold the modified couplings; uniform ranks further away are fine
+      if (cs == 0 ? out[r].uniform != 0 : (r <= 1 && out[r].uniform != 0))
+      {
+        std::printf("FAIL %s rank %d: sym_uniform %lld, expected 0\n", nm, r, (long long)out[r].uniform);
+        ++failures;
+      }
+      if (cs == 0 && N % 64 == 0 && out[r].variant != 10 && out[r].variant != -1)
+      {
+        std::printf("FAIL %s rank %d: march variant %lld, expected the value march (10)\n", nm, r,
+                    (long long)out[r].variant);
+        ++failures;
+      }
+      for (int j = 0; j < steps; ++j)
+        if (std::fabs(out[r].fa[j] - ser.fa[j]) > 1e-12 * std::fabs(ser.fa[j]) ||
+            std::fabs(out[r].fb[j + 1] - ser.fb[j + 1]) > 1e-12 * std::fabs(ser.fb[j + 1]) ||
+            std::fabs(out[r].wa[j] - ser.fa[j]) > 1e-12 * std::fabs(ser.fa[j]) ||
+            std::fabs(out[r].wb[j + 1] - ser.fb[j + 1]) > 1e-12 * std::fabs(ser.fb[j + 1]))
+        {
+          std::printf("FAIL %s rank %d fused step %d: alpha %.17g/%.17g/%.17g\n", nm, r, j, out[r].fa[j],
+                      out[r].wa[j], ser.fa[j]);
+          ++failures;
+          break;
+        }
+    }
+  }
+  return failures;
+}
+
 int main(int argc, char **argv)
 {
   const int P = argc > 1 ? std::atoi(argv[1]) : 3;
@@ -321,6 +454,7 @@ int main(int argc, char **argv)
         ++failures;
       }
   }
+  failures += value_images(P, N, x);
   // every rank's slab of whole planes takes the geometric-mask march (global plane coordinates)
   for (int r = 0; r < P; ++r)
     if (uni[r] != 2)

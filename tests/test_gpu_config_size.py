@@ -1,0 +1,69 @@
+"""Kernel parity at configuration size (SURVEY 8(d) C2 / C3 sizes), beside the small-case tests in
+test_gpu_blas_mv8.py / test_gpu_spmv.py:
+
+* orthonormalize_blocked (kernels_cpp.hh:180-351) on n = 128^3, m = 32 -- the MGS diagonal block and
+  both CholQR variants (orthonormalize_avx2_b8 / _v2, kernels_avx2.hh:60-622) -- vs the restatements
+  orc_orthonormalize_mv8 / _cholqr_ / _cholqr_split_, elementwise within 1e-12;
+* B_orthonormalize_blocked (kernels_cpp.hh:356-591) with n = 1024^2 rows (the 2-D Dirichlet
+  Laplacian as B), m = 24, vs orc_b_orthonormalize_mv8 within 1e-12, and its returned norm;
+* config C3: the Q1 3x3-block BCRSMatrix::mv at 64^3 block rows (262,144 x 3x3, nnzb 6,859,000),
+  BITWISE the restated row loop (the block order of BCRSMatrix::mv; kernels_cpp.hh:611-617 per entry).
+Random well-conditioned start blocks (mt19937 / normal, the reference's generator) as everywhere."""
+import numpy as np
+import pytest
+
+import eigmi
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("variant,name", [(eigmi.ORTHO_MGS, "mgs"), (eigmi.ORTHO_CHOLQR, "cholqr"),
+                                          (eigmi.ORTHO_CHOLQR_SPLIT, "cholqr_split")])
+def test_orthonormalize_blocked_128cubed(ctx, variant, name):
+    n, m = 128 ** 3, 32
+    Qh = oracle.random_mv8(n, m, 21)
+    Q = ctx.array(Qh)
+    eigmi.orthonormalize_mv8(ctx, n, m, Q, variant)
+    got = Q.get()
+    Q.free()
+    ref = oracle.orthonormalize_mv8(Qh, n, m, name)
+    diff = np.abs(got - ref).max()
+    G = oracle.gram_mv8(got, got, n, m)
+    orth = np.abs(G - np.eye(m)).max()
+    print(f"orthonormalize_blocked {name} n={n} m={m}: |Q - Q_ref| = {diff:.3e}, |Q^T Q - I| = {orth:.3e}")
+    assert diff < 1e-12
+    assert orth < 1e-13
+
+
+def test_b_orthonormalize_1m_rows(ctx):
+    N, m = 1024, 24
+    B = oracle.laplace2d(N)
+    n = B.n
+    Qh = oracle.random_mv8(n, m, 77)
+    MB = eigmi.Matrix.from_bcsr(ctx, B.rowptr, B.col, B.val)
+    Q, norm = ctx.array(Qh), ctx.zeros(1)
+    eigmi.b_orthonormalize_mv8(MB, m, Q, norm)
+    got = Q.get()
+    refQ, refnorm = oracle.b_orthonormalize_mv8(B, Qh, n, m)
+    diff = np.abs(got - refQ).max()
+    # Q^T B Q from the oracle's own SpMM + Gram
+    BQ = oracle.spmm_mv8(B, got, m)
+    orth = np.abs(oracle.gram_mv8(got, BQ, n, m) - np.eye(m)).max()
+    print(f"B-orthonormalize n={n} m={m}: |Q - Q_ref| = {diff:.3e}, |Q^T B Q - I| = {orth:.3e}, "
+          f"norm {norm.get(1)[0]:.6e} vs {refnorm:.6e}")
+    assert diff < 1e-12
+    assert orth < 1e-10
+    assert abs(norm.get(1)[0] - refnorm) <= 1e-12 * abs(refnorm)
+    MB.close()
+
+
+def test_q1elast_64_spmv_bitwise(ctx):
+    A = oracle.q1elast(64)
+    assert A.nrows == 64 ** 3 and int(A.rowptr[-1]) == 6859000
+    M = eigmi.Matrix.from_bcsr(ctx, A.rowptr, A.col, A.val, 3, 3)
+    rng = np.random.default_rng(64)
+    for x in (rng.standard_normal(A.n), np.ones(A.n)):
+        y = M.mv_host(x)
+        assert np.array_equal(y, oracle.csr_mv(A, x))
+    M.close()

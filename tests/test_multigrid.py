@@ -117,6 +117,25 @@ def test_mg_rejects_bad_grids(ctx):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("dims", [(128, 128, 1), (64, 64, 4)])
+def test_mg_refuses_flat_grids(ctx, dims):
+    """A direction below 3 nodes stops the coarsening: a flat grid would leave a coarsest level of
+    thousands of rows for the dense host eigensolve -- refused with EIG_ERR_ARG at once."""
+    import time
+    nx, ny, nz = dims
+    L = [sp.diags([-np.ones(k - 1), 2 * np.ones(k), -np.ones(k - 1)], [-1, 0, 1]) for k in (nx, ny, nz)]
+    I = [sp.identity(k) for k in (nx, ny, nz)]
+    A = (sp.kron(sp.kron(I[2], I[1]), L[0]) + sp.kron(sp.kron(I[2], L[1]), I[0]) +
+         sp.kron(sp.kron(L[2], I[1]), I[0]) + 0.1 * sp.identity(nx * ny * nz)).tocsr()
+    dA = _upload(ctx, A)
+    t0 = time.perf_counter()
+    with pytest.raises(eigmi.EigError) as e:
+        eigmi.Multigrid(dA, dims)
+    assert e.value.code == eigmi.EIG_ERR_ARG and "semi-coarsening" in str(e.value)
+    assert time.perf_counter() - t0 < 5.0
+
+
+@pytest.mark.gpu
 def test_shift_invert_smallest_p1_multigrid(ctx):
     """As test_block_lanczos.py::test_shift_invert_smallest_p1, with the K solve by 14 multigrid
     iterations (residual ~1e-13) instead of ~240 Chebyshev-Jacobi steps."""

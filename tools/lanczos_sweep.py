@@ -61,6 +61,12 @@ def main():
         A = (sp.kron(Iz, sp.kron(Ix, lap1(N))) + sp.kron(Iz, sp.kron(lap1(N), Ix)) +
              sp.kron(lap1(args.slab), sp.kron(Ix, Ix))).tocsr()
         A.setdiag(6.0)
+        if args.matrix == "varcoef":
+            # a random conductance per grid edge (symmetric), diagonal 6 + U(0, 1): no uniform band
+            rng = np.random.default_rng(5)
+            U = sp.triu(A, k=1).tocoo()
+            U.data = -0.5 - rng.random(U.nnz)
+            A = (U + U.T + sp.diags(6.0 + rng.random(A.shape[0]))).tocsr()
         A.sort_indices()
         rp, c, v = A.indptr.astype(np.int64), A.indices.astype(np.int32), A.data.astype(np.float64)
         n = A.shape[0]
