@@ -969,6 +969,71 @@ void build_sym(eig_mat_s &A, i64 nb, const int64_t *rowptr, const int32_t *col, 
       }
     }
   }
+  // box-geometric masks (general 27-point box subsets, e.g. the P1 Kuhn 15-point stencil): decompose the
+  // offsets as a D + b nx + c -- nx the smallest offset > 1 (or that + 1 when (0, 1, -1) is stored), D
+  // the smallest offset past nx + 1 (or that + 1, + nx - 1, + nx, + nx + 1) -- then check row by row
+  A.sym_box27 = 0;
+  if (!A.sym_geo && nd >= 3 && nd <= 27 && offs.front() == -offs.back())
+  {
+    i64 s1 = 0;
+    for (i64 d : offs)
+      if (d > 1 && (s1 == 0 || d < s1)) s1 = d;
+    std::vector<int> bx(nd), by(nd), bz(nd);
+    auto decompose = [&](i64 nxc, i64 Dc) {
+      for (int k = 0; k < nd; ++k)
+      {
+        bool found = false;
+        for (int a = -1; a <= 1 && !found; ++a)
+          for (int b2 = -1; b2 <= 1 && !found; ++b2)
+            for (int c = -1; c <= 1 && !found; ++c)
+              if (a * Dc + b2 * nxc + c == offs[k]) bz[k] = a, by[k] = b2, bx[k] = c, found = true;
+        if (!found) return false;
+      }
+      return true;
+    };
+    i64 gnx = 0, gD = 0;
+    for (i64 nxc : {s1, s1 + 1})
+    {
+      if (nxc < 3 || gD) continue;
+      i64 t = 0;
+      for (i64 d : offs)
+        if (d > nxc + 1 && (t == 0 || d < t)) t = d;
+      if (t == 0) continue;
+      for (i64 Dc : {t, t + 1, t + nxc - 1, t + nxc, t + nxc + 1})
+        if (!gD && Dc % nxc == 0 && Dc / nxc >= 3 && A.nb_rows_global % Dc == 0 && nb % Dc == 0 && row0 % Dc == 0 &&
+            decompose(nxc, Dc))
+          gnx = nxc, gD = Dc;
+    }
+    if (gD && A.nb_rows_global / gD >= 3 && gnx <= INT32_MAX && gD / gnx <= INT32_MAX &&
+        A.nb_rows_global / gD <= INT32_MAX)
+    {
+      decompose(gnx, gD);
+      const i64 gny = gD / gnx, gnz = A.nb_rows_global / gD;
+      std::atomic<bool> same{true};
+      parallel_slices(nb, [&](i64 r0, i64 r1) {
+        for (i64 r = r0; r < r1 && same.load(std::memory_order_relaxed); ++r)
+        {
+          const i64 g = row0 + r;
+          const i64 x = g % gnx, y = (g / gnx) % gny, z = g / gD;
+          uint32_t e = 0;
+          for (int k = 0; k < nd; ++k)
+          {
+            const i64 xx = x + bx[k], yy = y + by[k], zz = z + bz[k];
+            if (xx >= 0 && xx < gnx && yy >= 0 && yy < gny && zz >= 0 && zz < gnz) e |= 1u << k;
+          }
+          if (e != (mb == 1 ? (uint32_t)m8[r] : m32[r])) same = false;
+        }
+      });
+      if (same)
+      {
+        for (int k = 0; k < nd; ++k) A.sym_box27 |= 1u << ((bz[k] + 1) * 9 + (by[k] + 1) * 3 + (bx[k] + 1));
+        A.sym_gx = (int)gnx;
+        A.sym_gy = (int)gny;
+        A.sym_gz = (int)gnz;
+        A.sym_gz0 = (int)(row0 / gD);
+      }
+    }
+  }
   hipStream_t s = A.ctx->stream;
   A.sym_val = dev_alloc<double>((size_t)nup * ld);
   A.sym_mask = mb == 1 ? (void *)dev_alloc<uint8_t>(ns * 64) : (void *)dev_alloc<uint32_t>(ns * 64);

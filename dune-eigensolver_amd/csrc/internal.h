@@ -215,6 +215,12 @@ struct eig_mat_s {
   // bands: the value march streams the band arrays, k_spmv.hip march variant 10)
   bool sym_geo = false;
   int sym_gx = 0, sym_gy = 0, sym_gz = 0, sym_gz0 = 0;  // grid (global planes) and this rank's first plane
+  // Box-geometric masks (api.cpp build_sym): offsets inside the 27-point box a D + b nx + c (a, b, c in
+  // {-1, 0, 1}) of an nx x ny x nz grid, every row storing exactly its in-grid neighbours among them
+  // (sym_geo's 5 / 7-point grids excluded); sym_box27 = bit (a + 1) 9 + (b + 1) 3 + (c + 1) per stored
+  // offset; grid in sym_gx / gy / gz / gz0.  The box marches (k_spmv.hip, e.g. the P1 Kuhn 15-point
+  // stencil of config C5) derive the masks from the coordinates
+  unsigned sym_box27 = 0;
   // Plane-march split of a distributed slab (k_spmv.hip march_plan): planes [mz0, mz1) have no
   // ghost columns and are marched while the halo is in flight; march_bnd lists every slice outside
   // them (the boundary launch after the exchange).  mz1 <= mz0: no split.

@@ -975,6 +975,9 @@ struct MarchPlan {
   // results stored with plain (MALL-allocating) stores instead of nontemporal ones: the vectors of a
   // small grid stay in the 256 MB memory-side cache for the next launch (geo2 kernels)
   int tstore;
+  // box marches (variant 12): band array of the upper offset at 27-box position (a+1) 9 + (b+1) 3 + (c+1),
+  // -1 when the stencil does not store it
+  signed char kj[27];
 };
 // store helper of the geo2 epilogues: temporal when the plan says the vectors fit the MALL
 template <class T>
@@ -1261,6 +1264,142 @@ __device__ __forceinline__ void march_rows_geo2(const SellB1 &A, const MarchPlan
            vs[VPF ? k & 1 : 0], vs[VPF ? (k + 1) & 1 : 1]);
 }
 
+// Box march for the P1 Kuhn 15-point stencil (march variant 12; config C5's K and M, any values): the
+// band's offsets are a D + b nx + c with (a, b, c) in the Kuhn edge set {0, +-e_i, +-(e_i + e_j),
+// +-(1, 1, 1)} and every row stores exactly its in-grid neighbours among them (eig_mat_s::sym_box27,
+// checked at upload).  A wave owns 64 consecutive x of one grid line (nx a multiple of 64) and marches
+// z, keeping the operand lines it needs in registers as values x.val (the fused step's u_k):
+//   plane z - 1: lines y - 1, y        plane z: y - 1, y, y + 1        plane z + 1: y, y + 1
+// each line with one edge register (lane 0: the row at x0 - 1, lane 63: x0 + 64; DPP lane shifts take
+// it as the "old" operand).  Per plane only plane z + 1's three lines are loaded (y: the stream, y +- 1:
+// gathers the neighbouring columns streamed, L2 hits); the rest are carried (z + 1 -> z -> z - 1).
+// Values: the row's 8 upper band arrays streamed once (0, +1, +nx, +nx+1, +D, +D+1, +D+nx, +D+nx+1);
+// the mirrored lower entries from the rows below: -1 by the lane shift of the +1 stream, -D / -D-1
+// carried from the previous plane's +D / +D+1 streams, -nx / -nx-1 / -D-nx / -D-nx-1 gathered at line
+// y - 1 (planes z and z - 1).  Missing neighbours read as exact zeros (zero-record descriptors for
+// lines / planes outside the grid, out-of-range edge offsets at x = 0 / nx - 1), so each row sums its
+// stored entries in ascending-column order bit for bit as the reference row loop.
+constexpr unsigned kKuhn15 = (1u << 0) | (1u << 1) | (1u << 3) | (1u << 4) | (1u << 9) | (1u << 10) | (1u << 12) |
+                             (1u << 13) | (1u << 14) | (1u << 16) | (1u << 17) | (1u << 22) | (1u << 23) |
+                             (1u << 25) | (1u << 26);
+template <class X, class EPI, class PRE>
+__device__ __forceinline__ void march_rows_kuhn(const SellB1 &A, const MarchPlan &mp, i64 own, int lane, int wave,
+                                                X x, EPI &epi, PRE &pre)
+{
+  typedef typename X::raw raw;
+  constexpr unsigned SZ = sizeof(raw);
+  constexpr unsigned kOut = 0x80000000u;
+  const int D = (int)mp.D, own32 = (int)own, gx = mp.gx;
+  const int item = (int)swizzled_block() * kWaves + wave;
+  if (item >= mp.ncol * mp.nseg) return;
+  const int col = item % mp.ncol, seg = item / mp.ncol;
+  const int z0 = (int)(mp.zb + seg * mp.nplanes / mp.nseg), z1 = (int)(mp.zb + (seg + 1) * mp.nplanes / mp.nseg);
+  const unsigned nbytes = (unsigned)(A.xlast + 1) * SZ;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(x.ptr()), 0, (int)nbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t r0 = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(x.ptr()), 0, 0, 0x00020000);
+  const int x0 = (col * 64) % gx, yw = (col * 64) / gx;
+  const __amdgpu_buffer_rsrc_t rm = yw > 0 ? rs : r0, rp = yw < mp.gy - 1 ? rs : r0;  // lines y - 1, y + 1
+  const unsigned eoff = lane == 0 ? (x0 > 0 ? 0u - SZ : kOut) : lane == 63 ? (x0 + 64 < gx ? SZ : kOut) : kOut;
+  const unsigned nxb = (unsigned)gx * SZ, Db = (unsigned)D * SZ;
+  int w = own32 + col * 64 + lane + z0 * D;
+  unsigned vo = (unsigned)w * SZ;
+  const int zg0 = z0 + mp.gz0;
+  // value arrays (8-B window-indexed slots): one descriptor per upper array, zero-record where absent
+  const SymImg &S = A.sym;
+  const unsigned vbytes = (unsigned)S.ld * 8u;
+  auto arr = [&](int pos, bool on) {
+    const int j = mp.kj[pos];
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(S.val + (i64)(j >= 0 ? j : 0) * S.ld), 0,
+                                             on && j >= 0 ? (int)vbytes : 0, 0x00020000);
+  };
+  const __amdgpu_buffer_rsrc_t a0d = arr(13, true), a1d = arr(14, true), aNd = arr(16, true), aN1d = arr(17, true),
+                               aDd = arr(22, true), aD1d = arr(23, true), aDNd = arr(25, true), aDN1d = arr(26, true),
+                               aNm = arr(16, yw > 0), aN1m = arr(17, yw > 0), vz = arr(13, false);
+  const unsigned eov = lane == 0 && x0 > 0 ? 0u - 8u : kOut;  // lane 0: the value slot at x0 - 1
+  const unsigned nxv = (unsigned)gx * 8u, Dv = (unsigned)D * 8u;
+  unsigned vv = (unsigned)w * 8u;
+  auto ld8 = [&](__amdgpu_buffer_rsrc_t r, unsigned o) {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (int)o, 0, 0));
+  };
+  auto ld8nt = [&](__amdgpu_buffer_rsrc_t r, unsigned o) {  // once-read streams: nontemporal
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (int)o, 0, 2));
+  };
+  // operand lines: raw loads first (the fused prologue sets x.c meanwhile), values after
+  const bool below = zg0 > 0;
+  raw rAm, rAme, rA0, rA0e, rBm, rBme, rB0, rB0e, rBp, rBpe;
+  {
+    const __amdgpu_buffer_rsrc_t p0 = below ? rs : r0, pm = below ? rm : r0;
+    bload(pm, vo - Db - nxb, rAm);
+    bload(pm, vo - Db - nxb + eoff, rAme);
+    bload(p0, vo - Db, rA0);
+    bload(p0, vo - Db + eoff, rA0e);
+  }
+  bload(rm, vo - nxb, rBm);
+  bload(rm, vo - nxb + eoff, rBme);
+  bload(rs, vo, rB0);
+  bload(rs, vo + eoff, rB0e);
+  bload(rp, vo + nxb, rBp);
+  bload(rp, vo + nxb + eoff, rBpe);
+  double aDp = below ? ld8(aDd, vv - Dv) : 0.0, aD1p = below ? ld8(aD1d, vv - Dv) : 0.0,
+         aD1pe = below ? ld8(aD1d, vv - Dv + eov) : 0.0;
+  if (!pre(x)) return;
+  double Am = x.val(rAm), Ame = x.val(rAme), A0 = x.val(rA0), A0e = x.val(rA0e), Bm = x.val(rBm), Bme = x.val(rBme),
+         Bp = x.val(rBp), Bpe = x.val(rBpe);
+  double B0 = x.val(rB0), B0e = x.val(rB0e);
+  raw pB0 = rB0;
+  for (int z = z0; z < z1; ++z)
+  {
+    const int zg = z + mp.gz0;
+    const bool up = zg + 1 < mp.gz, dn = zg > 0;
+    raw rC0, rC0e, rCp, rCpe, rCm, rCme;
+    {
+      const __amdgpu_buffer_rsrc_t q0 = up ? rs : r0, qp = up ? rp : r0, qm = up ? rm : r0;
+      bload(q0, vo + Db, rC0);
+      bload(q0, vo + Db + eoff, rC0e);
+      bload(qp, vo + Db + nxb, rCp);
+      bload(qp, vo + Db + nxb + eoff, rCpe);
+      bload(qm, vo + Db - nxb, rCm);
+      bload(qm, vo + Db - nxb + eoff, rCme);
+    }
+    // the row's upper values (once-read streams nontemporal; +nx.. arrays are re-read by line y + 1)
+    const double a0 = ld8nt(a0d, vv), a1 = ld8nt(a1d, vv), aN = ld8(aNd, vv), aN1 = ld8(aN1d, vv),
+                 aD = ld8nt(aDd, vv), aD1 = ld8nt(aD1d, vv), aDN = ld8(aDNd, vv), aDN1 = ld8(aDN1d, vv);
+    const double a1e = ld8(a1d, vv + eov), aD1e = ld8(aD1d, vv + eov);
+    // mirrored lower entries at line y - 1 (plane z: -nx, -nx-1; plane z - 1: -D-nx, -D-nx-1)
+    const double aNl = ld8(aNm, vv - nxv), aN1l = ld8(aN1m, vv - nxv), aN1le = ld8(aN1m, vv - nxv + eov);
+    const __amdgpu_buffer_rsrc_t dnm = dn && yw > 0 ? aDNd : vz, dn1m = dn && yw > 0 ? aDN1d : vz;
+    const double aDNl = ld8(dnm, vv - Dv - nxv), aDN1l = ld8(dn1m, vv - Dv - nxv),
+                 aDN1le = ld8(dn1m, vv - Dv - nxv + eov);
+    const double C0 = x.val(rC0), C0e = x.val(rC0e), Cp = x.val(rCp), Cpe = x.val(rCpe);
+    double acc = 0.0;
+    acc += lane_shift_or<false>(aDN1l, aDN1le) * lane_shift_or<false>(Am, Ame);  // (-1, -1, -1)
+    acc += aDNl * Am;                                                            // (-1, -1,  0)
+    acc += lane_shift_or<false>(aD1p, aD1pe) * lane_shift_or<false>(A0, A0e);    // (-1,  0, -1)
+    acc += aDp * A0;                                                             // (-1,  0,  0)
+    acc += lane_shift_or<false>(aN1l, aN1le) * lane_shift_or<false>(Bm, Bme);    // ( 0, -1, -1)
+    acc += aNl * Bm;                                                             // ( 0, -1,  0)
+    acc += lane_shift_or<false>(a1, a1e) * lane_shift_or<false>(B0, B0e);        // ( 0,  0, -1)
+    acc += a0 * B0;                                                              // ( 0,  0,  0)
+    acc += a1 * lane_shift_or<true>(B0, B0e);                                    // ( 0,  0, +1)
+    acc += aN * Bp;                                                              // ( 0, +1,  0)
+    acc += aN1 * lane_shift_or<true>(Bp, Bpe);                                   // ( 0, +1, +1)
+    acc += aD * C0;                                                              // (+1,  0,  0)
+    acc += aD1 * lane_shift_or<true>(C0, C0e);                                   // (+1,  0, +1)
+    acc += aDN * Cp;                                                             // (+1, +1,  0)
+    acc += aDN1 * lane_shift_or<true>(Cp, Cpe);                                  // (+1, +1, +1)
+    epi(w - own32, w, acc, pB0);
+    // carry z + 1 -> z -> z - 1
+    Am = Bm, Ame = Bme, A0 = B0, A0e = B0e;
+    Bm = x.val(rCm), Bme = x.val(rCme);
+    B0 = C0, B0e = C0e, pB0 = rC0;
+    Bp = Cp, Bpe = Cpe;
+    aDp = aD, aD1p = aD1, aD1pe = aD1e;
+    w += D;
+    vo += Db;
+    vv += Dv;
+  }
+}
+
 // The rows of this wave's work item, in plane order: epi(r, w, acc, centre) gets each row's sum
 // and its own operand x[w] (raw: a double, or the (t, u) pair of the fused step).
 // The first entry of both far spans is issued with the row's streams, so a 7-point row waits
@@ -1278,8 +1417,13 @@ template <class MT, int KC, bool SPAN1, int UNI, class X, class EPI, class PRE =
 __device__ __forceinline__ void march_rows(const SellB1 &A, const MarchPlan &mp, i64 own, int lane, int wave,
                                            const X &x, EPI &epi, PRE &&pre = PRE{})
 {
-  static_assert(!UNI || SPAN1, "uniform-band march: far spans of at most one offset");
-  if constexpr (UNI >= 3)
+  static_assert(!UNI || SPAN1 || UNI == 12, "uniform-band march: far spans of at most one offset");
+  if constexpr (UNI == 12)
+  {
+    march_rows_kuhn(A, mp, own, lane, wave, x, epi, pre);
+    return;
+  }
+  else if constexpr (UNI >= 3)
   {
     // 3, 4, 5: +D operand 1, 2, 3 planes ahead; 6: 3 planes ahead and the gathers one plane ahead
     if constexpr (UNI >= 10)  // 10, 11: the value march (band arrays streamed), 11 one plane ahead
@@ -1420,8 +1564,11 @@ __device__ __forceinline__ void march_rows(const SellB1 &A, const MarchPlan &mp,
 }
 
 // y[own + r] = (A x)[r] on the plane march (BCRSMatrix::mv; bitwise k_spmv_b1).
+// resident waves per SIMD of the eig_mv / K1 march kernels (the box march holds ~90 VGPRs)
+constexpr int march_mv_waves(int uni) { return uni == 12 ? 5 : 8; }
+
 template <class MT, bool SPAN1, int UNI>
-__global__ __launch_bounds__(kStreamThreads, 8) void k_spmv_march(i64 nrows, i64 own, SellB1 A, MarchPlan mp,
+__global__ __launch_bounds__(kStreamThreads, march_mv_waves(UNI)) void k_spmv_march(i64 nrows, i64 own, SellB1 A, MarchPlan mp,
                                                                   const double *__restrict__ x,
                                                                   double *__restrict__ y)
 {
@@ -1438,7 +1585,7 @@ __global__ __launch_bounds__(kStreamThreads, 8) void k_spmv_march(i64 nrows, i64
 // Classic Lanczos kernel 1 on the plane march (same per-row arithmetic as k_lanczos_spmv_b1; the
 // row's own u_j is the march's centre operand).
 template <class MT, bool SPAN1, int UNI>
-__global__ __launch_bounds__(kStreamThreads, 8) void k_lanczos_spmv_march(
+__global__ __launch_bounds__(kStreamThreads, march_mv_waves(UNI)) void k_lanczos_spmv_march(
     i64 nrows, i64 own, SellB1 A, MarchPlan mp, const double *__restrict__ u, const double *__restrict__ up,
     double *__restrict__ t, int j, const double *__restrict__ nsum, double *__restrict__ dot_out,
     double *__restrict__ beta_out, double *partials, unsigned *ticket)
@@ -1476,7 +1623,7 @@ __global__ __launch_bounds__(kStreamThreads, 8) void k_lanczos_spmv_march(
 // resident waves per SIMD the fused march kernels are built for (registers: no spills)
 constexpr int march_fused_waves(int uni)
 {
-  return uni == 11 ? 5 : uni == 10 ? 6 : uni == 6 || uni == 9 ? 4 : uni == 5 ? 5 : uni == 4 || uni == 8 ? 6
+  return uni == 12 ? 5 : uni == 11 ? 5 : uni == 10 ? 6 : uni == 6 || uni == 9 ? 4 : uni == 5 ? 5 : uni == 4 || uni == 8 ? 6
        : uni == 3 || uni == 7 ? 7 : uni ? 8 : 7;
 }
 
@@ -1976,8 +2123,15 @@ static bool march_span1(const eig_mat_s &A)
 // 10 / 11: bands that are not uniform (or EIG_MAT_NO_UNIFORM) on a geo2 grid: the value march
 // (march_rows_geo2<VAL>: the band arrays streamed, masks from the coordinates), 11 with the value
 // streams and the +D operand one plane ahead (tune values 9 / 10; 1 = the plain masked march).
+// 12: the P1 Kuhn box march (march_rows_kuhn; eig_mat_s::sym_box27 == kKuhn15, one rank).
+static bool march_kuhn(const eig_mat_s &A)
+{
+  return A.sym_box27 == kKuhn15 && A.sym_nd == 15 && !A.ctx->distributed() && A.sym_gx % 64 == 0 &&
+         A.window * 16 < (i64(1) << 31) && A.sym_ld * 8 < (i64(1) << 31) && A.tune_march_prefetch != 1;
+}
 static int march_uniform(const eig_mat_s &A, bool fused = false, i64 nplanes = 0)
 {
+  if (march_kuhn(A)) return 12;
   const bool geo2 = A.sym_geo && A.sym_gx % 64 == 0 && A.window * 16 < (i64(1) << 31);
   if (!A.sym_uniform || (A.kflags & EIG_MAT_NO_UNIFORM))
   {
@@ -1995,7 +2149,9 @@ static int march_uniform(const eig_mat_s &A, bool fused = false, i64 nplanes = 0
 // have single-offset far spans).
 #define EIG_MARCH_LAUNCH(KERN, MODE, G, ...)                                                               \
   do {                                                                                                    \
-    if ((MODE) == kSymN8 && march_span1(A) && mp.uni == 11)                                               \
+    if (mp.uni == 12)                                                                                     \
+      hipLaunchKernelGGL((KERN<uint32_t, false, 12>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);     \
+    else if ((MODE) == kSymN8 && march_span1(A) && mp.uni == 11)                                          \
       hipLaunchKernelGGL((KERN<uint8_t, true, 11>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);       \
     else if ((MODE) == kSymN8 && march_span1(A) && mp.uni == 10)                                          \
       hipLaunchKernelGGL((KERN<uint8_t, true, 10>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);       \
@@ -2049,7 +2205,8 @@ static MarchPlan march_plan(const eig_mat_s &A, int mode, i64 zb = 0, i64 ze = -
   MarchPlan mp{};
   if (mode != kSymN8 && mode != kSymN32) return mp;
   i64 D;
-  if (!march_enabled(A) || !march_geometry(A, D, chunk)) return mp;
+  const bool kuhn = chunk == 64 && march_kuhn(A);
+  if (!march_enabled(A) || !(kuhn ? (D = (i64)A.sym_gx * A.sym_gy) > 0 : march_geometry(A, D, chunk))) return mp;
   if (ze < 0) ze = (A.nb_rows + D - 1) / D;
   const i64 nplanes = ze - zb;
   if (nplanes < 2 || (zb == 0 && nplanes < 4)) return mp;
@@ -2087,7 +2244,16 @@ static MarchPlan march_plan(const eig_mat_s &A, int mode, i64 zb = 0, i64 ze = -
   mp.Un = A.sym_val + (i64)(klo > 1 ? A.sym_dj[1] : 0) * A.sym_ld;
   mp.dq = khi < A.sym_nd - 1 ? A.sym_off[khi] : 0;
   mp.Uq = A.sym_val + (i64)(khi < A.sym_nd - 1 ? A.sym_dj[khi] : 0) * A.sym_ld;
-  if (A.sym_geo)
+  for (int q = 0; q < 27; ++q) mp.kj[q] = -1;
+  if (kuhn)
+  {
+    // band array of each upper box offset a D + b nx + c
+    for (int k = 0; k < A.sym_nd; ++k)
+      for (int q = 13; q < 27; ++q)
+        if ((i64)(q / 9 - 1) * D + (i64)((q / 3) % 3 - 1) * A.sym_gx + (q % 3 - 1) == A.sym_off[k])
+          mp.kj[q] = (signed char)A.sym_dj[k];
+  }
+  if (A.sym_geo || kuhn)
   {
     mp.gx = A.sym_gx;
     mp.gy = A.sym_gy;
@@ -2425,7 +2591,7 @@ void lanczos_kernel_info(const eig_mat_s &A, bool fused, std::string &name, i64 
                              : march_split_active(A);
     // the uniform-band march streams the row mask and the vectors only; the value march (10, 11)
     // the band arrays and the vectors (geometric masks: no mask stream)
-    const int mv = march && mode == kSymN8 && march_span1(A) ? march_uniform(A) : 0;
+    const int mv = march && ((mode == kSymN8 && march_span1(A)) || march_kuhn(A)) ? march_uniform(A) : 0;
     if (mv >= 10)
       bytes = 8 * (i64)A.sym_nup * n + vec;
     else if (mv)

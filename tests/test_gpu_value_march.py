@@ -175,3 +175,37 @@ def test_value_march_256_lanczos(ctx, v256):
     fa, fb, _ = eigmi.lanczos_run(M, 30, seed=123, fused=True)
     ca, cb, _ = eigmi.lanczos_run(M, 30, seed=123)
     assert np.allclose(fa, ca, rtol=1e-11) and np.allclose(fb, cb, rtol=1e-11)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,N", [(eigmi.GEN_P1STIFF3D, 64), (eigmi.GEN_P1MASS3D, 64), (eigmi.GEN_P1STIFF3D, 128)])
+def test_kuhn_box_march(ctx, kind, N):
+    """The P1 Kuhn 15-point box march (march variant 12, config C5's K and M): eig_mv bitwise the
+    reference row loop; the fused and classic recurrences within 1e-12 of their restatements and of
+    the row kernels (EIG_TUNE_MARCH_PREFETCH = 1: no march) at every plane-run count."""
+    rp, c, v = eigmi.gen_matrix(kind, N)
+    A = oracle.CSR(N ** 3, rp, c, v)
+    M = eigmi.Matrix.from_bcsr(ctx, rp, c, v)
+    info = M.info
+    assert info.sym_offsets == 15 and info.march_variant == 12, (info.sym_offsets, info.march_variant)
+    n = A.n
+    assert M.lanczos_kernel_info(True) == ("k_lanczos_fused_march", 8 * info.sym_arrays * n + 32 * n)
+    x = np.random.default_rng(13).standard_normal(n)
+    ref = oracle.csr_mv(A, x)
+    assert np.array_equal(M.mv_host(x), ref)
+    M.tune(march_prefetch=1)  # row kernels
+    assert M.info.march_variant == -1
+    assert np.array_equal(M.mv_host(x), ref)
+    base = {f: eigmi.lanczos_run(M, 25, seed=7, fused=f)[:2] for f in (False, True)}
+    M.tune(march_prefetch=0)
+    for runs in (0, 1, 3, 7):
+        M.tune(runs)
+        assert np.array_equal(M.mv_host(x), ref), runs
+        for fused in (False, True):
+            a, b, _ = eigmi.lanczos_run(M, 25, seed=7, fused=fused)
+            assert np.allclose(a, base[fused][0], rtol=1e-12, atol=0) and \
+                np.allclose(b, base[fused][1], rtol=1e-12, atol=0), (runs, fused)
+    M.tune(0)
+    fa, fb, _ = eigmi.lanczos_run(M, 15, seed=123, fused=True)
+    qa, qb = oracle.lanczos_fused(A, oracle.random_vec(n, 123), 15)
+    assert np.allclose(fa, qa, rtol=1e-12, atol=0) and np.allclose(fb, qb, rtol=1e-12, atol=0)

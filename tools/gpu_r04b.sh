@@ -6,3 +6,5 @@ timeout -k 10 300 python3 tools/lanczos_sweep.py --N 256 --matrix varcoef --vari
 cat $O/latency.jsonl
 timeout -k 10 200 python3 tools/lanczos_sweep.py --N 256 --slab 32 --matrix varcoef --variants fused,fused@1,fused@4,fused#1,fused#10,pipelined,mv --rounds 3 --steps 40 > $O/slab.jsonl 2>> $O/sweep.err || exit 1
 cat $O/slab.jsonl
+timeout -k 10 300 python3 tools/lanczos_sweep.py --N 256 --matrix p1k --variants fused,fused@6,fused@12,fused#1,mv,mv#1 --rounds 3 --steps 30 > $O/p1k.jsonl 2>> $O/sweep.err || exit 1
+cat $O/p1k.jsonl

@@ -45,8 +45,9 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--slab", type=int, default=0, help="N x N x slab box instead of the N^3 cube")
-    ap.add_argument("--matrix", choices=["poisson", "varcoef"], default="poisson",
-                    help="7-point Poisson (eig_gen kind 4) or the variable-coefficient 7-point (kind 8)")
+    ap.add_argument("--matrix", choices=["poisson", "varcoef", "p1k", "p1m"], default="poisson",
+                    help="7-point Poisson (eig_gen kind 4), the variable-coefficient 7-point (kind 8), or the P1 "
+                         "Kuhn stiffness / mass (kinds 6 / 7, config C5's 15-point K and M)")
     args = ap.parse_args()
     ctx = eigmi.Context(0)
     N = args.N
@@ -72,7 +73,8 @@ def main():
         n = A.shape[0]
     else:
         n = N ** 3
-        rp, c, v = eigmi.gen_matrix(eigmi.GEN_VARCOEF3D if args.matrix == "varcoef" else eigmi.GEN_POISSON3D, N)
+        rp, c, v = eigmi.gen_matrix({"poisson": eigmi.GEN_POISSON3D, "varcoef": eigmi.GEN_VARCOEF3D,
+                                     "p1k": eigmi.GEN_P1STIFF3D, "p1m": eigmi.GEN_P1MASS3D}[args.matrix], N)
     nnz = int(rp[-1])
     specs = args.variants.split(",")
     mats = {}
