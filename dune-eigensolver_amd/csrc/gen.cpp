@@ -12,6 +12,9 @@
 //           nodes, h = 1/(N+1), Dirichlet nodes eliminated, 15-point edge pattern   (config C5)
 //   kind 7  3-D P1 consistent mass M on the same mesh and the SAME 15-point pattern (config C5;
 //           the reference assumes pattern(A) contains pattern(B), eigensolver.hh:202-203)
+//   kind 9, 10  the P1 K / M of kinds 6 / 7 with a coefficient c_e in [0.5, 1.5) per tetrahedron
+//           (hashed; contributions summed in element order: bitwise symmetric) -- config C5's
+//           variable-coefficient realism variant (no two rows alike: the box-image kernels run)
 //   kind 8  3-D 7-point variable-coefficient diffusion (finite volumes, Dirichlet): the 7-point
 //           pattern of kind 4 with a positive conductance kappa(e) in [0.5, 1.5) per grid edge e
 //           (a hash of the edge, so a(k, q) = a(q, k) = -kappa bit for bit) and the diagonal
@@ -36,13 +39,21 @@ inline double m1(int d) { return d == 0 ? 4.0 / 6.0 : 1.0 / 6.0; }
 // Laplacian (h/6) [1 -1 0 0; -1 2 -1 0; 0 -1 2 -1; 0 0 -1 1] and every element mass is
 // (h^3/120)(1 + delta_ab).  Edges are +-e_i, +-(e_i + e_j), +-(1,1,1): 14 neighbours + self.
 const int kPerm[6][3] = {{0, 1, 2}, {0, 2, 1}, {1, 0, 2}, {1, 2, 0}, {2, 0, 1}, {2, 1, 0}};
-int gen_p1_row(bool mass, int N, i64 k, int32_t *cols, double *vals)
+inline double kappa(i64 k, int a, int side);
+// variable coefficients (kinds 9 / 10): element e = (cube corner, tetrahedron) scales its stiffness /
+// mass by c_e in [0.5, 1.5) (a hash of e); an entry's element contributions are summed in ascending
+// element order, so a(k, q) and a(q, k) round identically (bitwise symmetric)
+int gen_p1_row(bool mass, int N, i64 k, int32_t *cols, double *vals, bool var = false)
 {
   const i64 NN = (i64)N * N;
   const int P[3] = {(int)(k % N) + 1, (int)((k / N) % N) + 1, (int)(k / NN) + 1};  // grid coords 1..N
   const double h = 1.0 / (N + 1);
   double acc[27] = {0.0};
   bool nb[27] = {false};
+  // var: per slot the (element, contribution) pairs, summed in element order below
+  int64_t eid[27][24];
+  double ev[27][24];
+  int ne[27] = {0};
   static const double path[4][4] = {{1, -1, 0, 0}, {-1, 2, -1, 0}, {0, -1, 2, -1}, {0, 0, -1, 1}};
   const double ks = h / 6.0, ms = h * h * h / 120.0;
   for (int dz = 0; dz <= 1; ++dz)
@@ -68,11 +79,32 @@ int gen_p1_row(bool mass, int N, i64 k, int32_t *cols, double *vals)
             for (int a = 0; a < 3; ++a) interior = interior && v[b][a] >= 1 && v[b][a] <= N;
             if (!interior) continue;
             const int slot = ((v[b][2] - P[2] + 1) * 3 + (v[b][1] - P[1] + 1)) * 3 + (v[b][0] - P[0] + 1);
-            acc[slot] += mass ? ms * (me == b ? 2.0 : 1.0) : ks * path[me][b];
+            const double cv = mass ? ms * (me == b ? 2.0 : 1.0) : ks * path[me][b];
+            if (var)
+            {
+              const int64_t e = (((int64_t)c[2] * (N + 1) + c[1]) * (N + 1) + c[0]) * 6 + t;
+              eid[slot][ne[slot]] = e;
+              ev[slot][ne[slot]++] = kappa(e, mass ? 1 : 0, 1) * cv;
+            }
+            else
+              acc[slot] += cv;
             nb[slot] = true;
           }
         }
       }
+  if (var)
+    for (int sl = 0; sl < 27; ++sl)
+    {
+      for (int i = 1; i < ne[sl]; ++i)  // insertion sort by element
+        for (int j = i; j > 0 && eid[sl][j - 1] > eid[sl][j]; --j)
+        {
+          std::swap(eid[sl][j - 1], eid[sl][j]);
+          std::swap(ev[sl][j - 1], ev[sl][j]);
+        }
+      double a = 0.0;
+      for (int i = 0; i < ne[sl]; ++i) a += ev[sl][i];
+      acc[sl] = a;
+    }
   // the 14 edge neighbours + self that exist (interior), in ascending global column
   int32_t cc[27];
   double vv[27];
@@ -196,11 +228,12 @@ int gen_row(int kind, int N, int overlap, i64 k, int32_t *cols, double *vals)
     return c;
   }
   if (kind == 6 || kind == 7) return gen_p1_row(kind == 7, N, k, cols, vals);
+  if (kind == 9 || kind == 10) return gen_p1_row(kind == 10, N, k, cols, vals, true);
   return -1;
 }
 
 i64 nrows_of(int kind, int N) { return (kind <= 3) ? (i64)N * N : (i64)N * N * N; }
-constexpr int kGenKinds = 9;
+constexpr int kGenKinds = 11;
 int blk_of(int kind) { return kind == 5 ? 9 : 1; }
 
 }  // namespace
@@ -222,7 +255,7 @@ extern "C" int64_t eig_gen_nnzb(int kind, int N)
     const i64 t = 3 * (i64)N - 2;
     return t * t * t;
   }
-  if (kind == 6 || kind == 7)
+  if (kind == 6 || kind == 7 || kind == 9 || kind == 10)
   {
     const i64 n = N, m = N - 1;
     return n * n * n + 6 * n * n * m + 6 * n * m * m + 2 * m * m * m;

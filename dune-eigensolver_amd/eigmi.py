@@ -43,7 +43,7 @@ def _tflags(timed):
 
 
 GEN_LAPLACE2D, GEN_NEUMANN2D, GEN_PU2D, GEN_IDENTITY2D, GEN_POISSON3D, GEN_Q1ELAST3D, GEN_P1STIFF3D, GEN_P1MASS3D, \
-    GEN_VARCOEF3D = range(9)
+    GEN_VARCOEF3D, GEN_P1STIFF3D_VAR, GEN_P1MASS3D_VAR = range(11)
 
 
 class EigError(RuntimeError):

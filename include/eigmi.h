@@ -560,7 +560,9 @@ double eig_bytes_orthonormalize_blocked(int64_t n, int64_t m, int b);
  *   6 3-D P1 stiffness K, Kuhn 6-tet split, N^3     7 3-D P1 consistent mass M, same 15-pt pattern
  *     interior nodes, h = 1/(N+1) (config C5)            (pattern(K) == pattern(M), config C5)
  *   8 3-D 7-pt variable-coefficient diffusion N^3: kind 4's pattern, a hashed conductance in
- *     [0.5, 1.5) per grid edge (bitwise symmetric), diagonal = the six face conductances' sum */
+ *     [0.5, 1.5) per grid edge (bitwise symmetric), diagonal = the six face conductances' sum
+ *   9 / 10 the P1 K / M of kinds 6 / 7 with a hashed coefficient in [0.5, 1.5) per tetrahedron
+ *     (bitwise symmetric; the C5 variable-coefficient variant) */
 int64_t eig_gen_nnzb(int kind, int N);
 int eig_gen_matrix(int kind, int N, int overlap, int64_t *rowptr, int32_t *col, double *vals);
 /* Rows [row_begin, row_begin + nrows) of the same matrix (for eig_mat_create_bcsr_dist). */

@@ -43,6 +43,27 @@ def test_varcoef_generator_properties():
     assert np.array_equal(v2, A.val[lo:hi]) and np.array_equal(c2, A.col[lo:hi])
 
 
+@pytest.mark.parametrize("kind,base", [(eigmi.GEN_P1STIFF3D_VAR, eigmi.GEN_P1STIFF3D),
+                                       (eigmi.GEN_P1MASS3D_VAR, eigmi.GEN_P1MASS3D)])
+def test_p1_varcoef_generator(kind, base):
+    """kinds 9 / 10: the P1 Kuhn pattern of kinds 6 / 7, bitwise symmetric (element contributions summed
+    in element order), SPD, and no longer class-constant (values vary row to row)."""
+    import scipy.sparse as sp
+    N = 9
+    r, c, v = eigmi.gen_matrix(kind, N)
+    r0, c0, v0 = eigmi.gen_matrix(base, N)
+    assert np.array_equal(r, r0) and np.array_equal(c, c0)
+    S = sp.csr_matrix((v, c, r), shape=(N ** 3, N ** 3))
+    assert (S != S.T).nnz == 0
+    assert np.linalg.eigvalsh(S.toarray()).min() > 0
+    ratio = v / np.where(v0 == 0, 1, v0)
+    assert ratio[v0 != 0].min() >= 0.5 - 1e-12 and ratio[v0 != 0].max() < 1.5
+    assert len(np.unique(np.round(ratio[v0 != 0], 12))) > 100
+    # the distributed generator produces the same rows
+    r2, c2, v2 = eigmi.gen_rows(kind, N, 2 * N * N, 3 * N * N)
+    assert np.array_equal(v2, v[r[2 * N * N]:r[5 * N * N]])
+
+
 def _box_random(nx, ny, nz, seed):
     """Random symmetric 7-point values on an nx x ny x nz box (positive diagonal, one random value per
     grid edge)."""

@@ -290,18 +290,30 @@ def inv(ctx):
                   "scipy: SuperLU)")
 
 
+def c5_var():
+    """EIGMI_C5_VAR=1: the variable-coefficient P1 K / M (eig_gen kinds 9 / 10, a coefficient per
+    tetrahedron) uploaded with EIG_MAT_NO_CLASS -- every launch streams its box image."""
+    return os.environ.get("EIGMI_C5_VAR", "0") == "1"
+
+
+def c5_mats(ctx, N):
+    var = c5_var()
+    fl = eigmi.MAT_NO_CLASS if var else 0
+    rk, ck, vk = eigmi.gen_matrix(eigmi.GEN_P1STIFF3D_VAR if var else eigmi.GEN_P1STIFF3D, N)
+    K = eigmi.Matrix.from_bcsr(ctx, rk, ck, vk, flags=fl)
+    del rk, ck, vk
+    rm, cm, vm = eigmi.gen_matrix(eigmi.GEN_P1MASS3D_VAR if var else eigmi.GEN_P1MASS3D, N)
+    nnz = int(rm[-1])
+    M = eigmi.Matrix.from_bcsr(ctx, rm, cm, vm, flags=fl)
+    return K, M, nnz
+
+
 def c5(ctx):
     N = int(os.environ.get("EIGMI_C5_N", "256"))
     steps, warm, b, degree = 3, 1, 32, 36
     n = N ** 3
     t0 = time.perf_counter()
-    rk, ck, vk = eigmi.gen_matrix(eigmi.GEN_P1STIFF3D, N)
-    K = eigmi.Matrix.from_bcsr(ctx, rk, ck, vk)
-    del rk, ck, vk
-    rm, cm, vm = eigmi.gen_matrix(eigmi.GEN_P1MASS3D, N)
-    nnz = int(rm[-1])
-    M = eigmi.Matrix.from_bcsr(ctx, rm, cm, vm)
-    del rm, cm, vm
+    K, M, nnz = c5_mats(ctx, N)
     bl = eigmi.BlockLanczos(K, M, block=b, max_steps=steps + warm, degree=degree, seed=123)
     setup_s = time.perf_counter() - t0
     bl.step(warm)
@@ -321,7 +333,8 @@ def c5(ctx):
     else:
         cheb_bytes = csr_bytes
     cheb_us = t.cheb_ms / t.cheb_launches * 1e3
-    emit(config=f"C5 P1 Kuhn K/M {N}^3, block Lanczos k={b}", op=f"block step (Chebyshev degree {degree}, CGS2, CholQR2)",
+    emit(config=f"C5 P1 Kuhn K/M {N}^3, block Lanczos k={b}" + (" (variable coefficients, box image)" if c5_var() else ""),
+         op=f"block step (Chebyshev degree {degree}, CGS2, CholQR2)",
          block_steps_per_s=round(steps / (t.total_ms * 1e-3), 3), ms_per_step=round(t.total_ms / steps, 2),
          kspmm_ms=round(t.kspmm_ms / steps, 2), cheb_ms=round(t.cheb_ms / steps, 2),
          orth_ms=round(t.orth_ms / steps, 2), norm_ms=round(t.norm_ms / steps, 2),
@@ -343,17 +356,12 @@ def boxk(ctx):
     b, n, reps = 32, N ** 3, 20
 
     def load(kind):
+        # variable coefficients: a coefficient per tetrahedron (eig_gen kinds 9 / 10; the rows leave
+        # their geometric class, so the box-image kernel runs; the pattern stays the same)
         r, c, v = eigmi.gen_matrix(kind, N)
-        if var:
-            # variable coefficients: a random positive diagonal term per row (the rows leave their
-            # geometric class, so the box-image kernel runs; the pattern stays the same)
-            rows = np.repeat(np.arange(n, dtype=np.int64), np.diff(r))
-            diag = np.nonzero(c == rows)[0]
-            v[diag] *= 1.0 + 0.01 * np.random.default_rng(1).random(n)
-            del rows, diag
-        return eigmi.Matrix.from_bcsr(ctx, r, c, v)
-    K = load(eigmi.GEN_P1STIFF3D)
-    M = load(eigmi.GEN_P1MASS3D)
+        return eigmi.Matrix.from_bcsr(ctx, r, c, v, flags=eigmi.MAT_NO_CLASS if var else 0)
+    K = load(eigmi.GEN_P1STIFF3D_VAR if var else eigmi.GEN_P1STIFF3D)
+    M = load(eigmi.GEN_P1MASS3D_VAR if var else eigmi.GEN_P1MASS3D)
     X, Y = ctx.zeros(n * b), ctx.zeros(n * b)
     ctx.check(eigmi.lib.eig_fill_normal(ctx.h, n * b, 5, X.ptr))
     eigmi.spmm_mv8(K, b, X, Y)
@@ -365,7 +373,7 @@ def boxk(ctx):
         ctx.sync()
     ts, _ = wall(spmm)
     ts /= reps
-    emit(config=f"P1 K {N}^3 m={b}" + (" (variable diagonal)" if var else ""), op="SpMM (kBoxStore)", kernel=K.kernel("spmm32"), us=round(ts * 1e6, 1),
+    emit(config=f"P1 K {N}^3 m={b}" + (" (variable coefficients)" if var else ""), op="SpMM (kBoxStore)", kernel=K.kernel("spmm32"), us=round(ts * 1e6, 1),
          bytes=16 * b * n, frac=round(16 * b * n / ts / 1e9 / PEAK, 4))
     d0, d1 = 2, 22
     eigmi.mass_solve_mv8(M, b, d0, X, Y)
@@ -377,9 +385,9 @@ def boxk(ctx):
     # Chebyshev step) per row
     img_s = 0 if K.kernel("spmm32") == "k_boxc_mv8" else 15 * 8 * n
     img_c = 0 if M.kernel("cheb32") == "k_boxc_mv8_cheb" else 15 * 8 * n + 8 * n
-    emit(config=f"P1 K {N}^3 m={b}" + (" (variable diagonal)" if var else ""), op="SpMM bytes incl. image",
+    emit(config=f"P1 K {N}^3 m={b}" + (" (variable coefficients)" if var else ""), op="SpMM bytes incl. image",
          bytes=16 * b * n + img_s, frac=round((16 * b * n + img_s) / ts / 1e9 / PEAK, 4))
-    emit(config=f"P1 M {N}^3 m={b}" + (" (variable diagonal)" if var else ""), op="Chebyshev step (kBoxCheb)",
+    emit(config=f"P1 M {N}^3 m={b}" + (" (variable coefficients)" if var else ""), op="Chebyshev step (kBoxCheb)",
          kernel=M.kernel("cheb32"), us=round(tc * 1e6, 1), bytes=32 * b * n + img_c,
          frac=round((32 * b * n + img_c) / tc / 1e9 / PEAK, 4))
     X.free(), Y.free()
@@ -395,12 +403,7 @@ def c5si(ctx):
     steps, warm, b = 2, 1, 32
     n = N ** 3
     t0 = time.perf_counter()
-    rk, ck, vk = eigmi.gen_matrix(eigmi.GEN_P1STIFF3D, N)
-    K = eigmi.Matrix.from_bcsr(ctx, rk, ck, vk)
-    del rk, ck, vk
-    rm, cm, vm = eigmi.gen_matrix(eigmi.GEN_P1MASS3D, N)
-    M = eigmi.Matrix.from_bcsr(ctx, rm, cm, vm)
-    del rm, cm, vm
+    K, M, _ = c5_mats(ctx, N)
     t1 = time.perf_counter()
     mg = eigmi.Multigrid(K, (N, N, N), max_cols=b, smooth_degree=2, smooth_ratio=5.0)
     mg_setup = time.perf_counter() - t1
@@ -423,7 +426,8 @@ def c5si(ctx):
     t = bl.step(steps)
     ev, _, _ = bl.ritz(4, eigmi.WHICH_SA, want_resid=False)
     h = 1.0 / (N + 1)
-    emit(config=f"C5 P1 Kuhn K/M {N}^3, block Lanczos k={b}, smallest end (K^-1 M, multigrid K solve)",
+    emit(config=f"C5 P1 Kuhn K/M {N}^3, block Lanczos k={b}, smallest end (K^-1 M, multigrid K solve)" +
+         (" (variable coefficients, box image)" if c5_var() else ""),
          op="block step (multigrid solve, CGS2, CholQR2)", block_steps_per_s=round(steps / (t.total_ms * 1e-3), 3),
          ms_per_step=round(t.total_ms / steps, 2), solve_ms=round(t.cheb_ms / steps, 2),
          kspmm_ms=round(t.kspmm_ms / steps, 2), orth_ms=round(t.orth_ms / steps, 2), norm_ms=round(t.norm_ms / steps, 2),
