@@ -518,7 +518,7 @@ extern "C" int eig_mat_tune(eig_mat_t A, int key, int value)
                   key == EIG_TUNE_HALO,
               EIG_ERR_ARG, "eig_mat_tune: unknown key");
     EIG_CHECK(key != EIG_TUNE_HALO || value <= 1, EIG_ERR_ARG, "eig_mat_tune: halo mode 0 / 1");
-    EIG_CHECK(key != EIG_TUNE_MARCH_PREFETCH || value <= 10, EIG_ERR_ARG, "eig_mat_tune: march variant 0..10");
+    EIG_CHECK(key != EIG_TUNE_MARCH_PREFETCH || value <= 11, EIG_ERR_ARG, "eig_mat_tune: march variant 0..11");
     if (key == EIG_TUNE_MARCH_RUNS)
       A->tune_march_runs = value;
     else if (key == EIG_TUNE_MARCH_PREFETCH)
@@ -1098,6 +1098,7 @@ void destroy_mat(eig_mat_s *A)
   if (A->slice_list) (void)hipFree(A->slice_list);
   if (A->march_bnd) (void)hipFree(A->march_bnd);
   if (A->sym_val) (void)hipFree(A->sym_val);
+  if (A->sym_pack) (void)hipFree(A->sym_pack);
   if (A->sym_mask) (void)hipFree(A->sym_mask);
   if (A->box_val) (void)hipFree(A->box_val);
   if (A->box_ctab) (void)hipFree(A->box_ctab);

@@ -221,6 +221,9 @@ struct eig_mat_s {
   // offset; grid in sym_gx / gy / gz / gz0.  The box marches (k_spmv.hip, e.g. the P1 Kuhn 15-point
   // stencil of config C5) derive the masks from the coordinates
   unsigned sym_box27 = 0;
+  // packed copy of the 4 value arrays of a 7-point band ({+D, 0, +1, +nx} per row, 32 B) for march
+  // variant 13 (k_spmv.hip sym_pack_prepare; freed by a shift, rebuilt at the next use)
+  double *sym_pack = nullptr;
   // Plane-march split of a distributed slab (k_spmv.hip march_plan): planes [mz0, mz1) have no
   // ghost columns and are marched while the halo is in flight; march_bnd lists every slice outside
   // them (the boundary launch after the exchange).  mz1 <= mz0: no split.

@@ -216,6 +216,12 @@ __global__ void k_shift_sym(i64 nrows, i64 own, const MT *__restrict__ mask, int
 void launch_shift_diag(eig_mat_s &A, double shift, hipStream_t s)
 {
   box_invalidate(A);  // (the box image copies the band values; rebuilt at its next use)
+  if (A.sym_pack)      // (so does the packed value image of the value march)
+  {
+    EIG_HIP(hipStreamSynchronize(s));
+    (void)hipFree(A.sym_pack);
+    A.sym_pack = nullptr;
+  }
   A.diag_sum += shift * (double)A.diag_count;
   const i64 G = (A.nb_rows + 255) / 256;
   if (G == 0) return;

@@ -978,6 +978,8 @@ struct MarchPlan {
   // box marches (variant 12): band array of the upper offset at 27-box position (a+1) 9 + (b+1) 3 + (c+1),
   // -1 when the stencil does not store it
   signed char kj[27];
+  // variant 13: the packed value image (eig_mat_s::sym_pack)
+  const double *pack;
 };
 // store helper of the geo2 epilogues: temporal when the plan says the vectors fit the MALL
 template <class T>
@@ -1181,13 +1183,36 @@ __device__ __forceinline__ void march_rows_geo2(const SellB1 &A, const MarchPlan
     double aD, a0, ap, aq, an, ae;
   };
   const __amdgpu_buffer_rsrc_t vz = arr(0, false);
+  // VAL 3: the packed image (eig_mat_s::sym_pack: per row {+D, 0, +1, +nx} = 32 B, two 16-B loads; the
+  // mirrored -nx / -1 values from the (+1, +nx) half of rows w - nx / w - 1)
+  const __amdgpu_buffer_rsrc_t pk = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<double *>(mp.pack ? mp.pack : S.val), 0, VAL == 3 && mp.pack ? (int)(4u * vbytes) : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t pkn = VAL == 3 && mp.dn && yw > 0 ? pk : vz;
   auto vload = [&](unsigned o, Vals &v, bool on) {  // on: wave-uniform (false: zeros, no traffic)
-    v.aD = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(on ? vD : vz, (int)o, 0, 2));
-    v.a0 = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(on ? v0 : vz, (int)o, 0, 2));
-    v.ap = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(on ? v1 : vz, (int)o, 0, 2));
-    v.aq = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(on ? vq : vz, (int)o, 0, 0));
-    v.an = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(on ? vn : vz, (int)(o + dnv), 0, 0));
-    v.ae = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(on ? v1 : vz, (int)(o + eov), 0, 0));
+    if constexpr (VAL == 3)
+    {
+      const dpair p0 = __builtin_bit_cast(dpair, __builtin_amdgcn_raw_buffer_load_b128(pk, (int)(4 * o), 0, 2));
+      const dpair p1 = __builtin_bit_cast(dpair, __builtin_amdgcn_raw_buffer_load_b128(pk, (int)(4 * o + 16), 0, 0));
+      const dpair pn = __builtin_bit_cast(dpair, __builtin_amdgcn_raw_buffer_load_b128(pkn, (int)(4 * (o + dnv) + 16), 0, 0));
+      // (lane 0's edge row w - 1; the other lanes, and lane 0 at x = 0, an out-of-range offset)
+      const unsigned peo = eov == kOut ? kOut : 4 * o - 16;
+      const dpair pe = __builtin_bit_cast(dpair, __builtin_amdgcn_raw_buffer_load_b128(pk, (int)peo, 0, 0));
+      v.aD = p0.x;
+      v.a0 = p0.y;
+      v.ap = p1.x;
+      v.aq = mp.dq ? p1.y : 0.0;
+      v.an = pn.y;
+      v.ae = pe.x;
+    }
+    else
+    {
+      v.aD = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(on ? vD : vz, (int)o, 0, 2));
+      v.a0 = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(on ? v0 : vz, (int)o, 0, 2));
+      v.ap = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(on ? v1 : vz, (int)o, 0, 2));
+      v.aq = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(on ? vq : vz, (int)o, 0, 0));
+      v.an = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(on ? vn : vz, (int)(o + dnv), 0, 0));
+      v.ae = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(on ? v1 : vz, (int)(o + eov), 0, 0));
+    }
   };
   constexpr bool VPF = VAL == 2;  // value streams one plane ahead
   Vals vs[2];
@@ -1212,7 +1237,7 @@ __device__ __forceinline__ void march_rows_geo2(const SellB1 &A, const MarchPlan
       gather(vo + Db, gn);
     else
       gather(vo, gc);
-    if constexpr (VAL == 1) vload(vv, vc_, true);
+    if constexpr (VAL == 1 || VAL == 3) vload(vv, vc_, true);
     const int zg = z + mp.gz0;
     bload(zg + PF + 1 < mp.gz ? rs : r0, vo + (unsigned)(PF + 1) * Db, pf);
     if constexpr (VPF) vload(vv + Dv, vn_, z + 1 < z1);
@@ -1426,8 +1451,8 @@ __device__ __forceinline__ void march_rows(const SellB1 &A, const MarchPlan &mp,
   else if constexpr (UNI >= 3)
   {
     // 3, 4, 5: +D operand 1, 2, 3 planes ahead; 6: 3 planes ahead and the gathers one plane ahead
-    if constexpr (UNI >= 10)  // 10, 11: the value march (band arrays streamed), 11 one plane ahead
-      march_rows_geo2<0, false, UNI - 9>(A, mp, own, lane, wave, x, epi, pre);
+    if constexpr (UNI >= 10)  // 10, 11: the value march (band arrays streamed), 11 one plane ahead, 13 packed
+      march_rows_geo2<0, false, UNI == 13 ? 3 : UNI - 9>(A, mp, own, lane, wave, x, epi, pre);
     else if constexpr (UNI >= 7)  // 7, 8, 9: march_rows_geo2 with the prefetches of 3, 4, 6
       march_rows_geo2<UNI == 9 ? 2 : UNI - 7, UNI == 9, 0>(A, mp, own, lane, wave, x, epi, pre);
     else
@@ -1623,7 +1648,7 @@ __global__ __launch_bounds__(kStreamThreads, march_mv_waves(UNI)) void k_lanczos
 // resident waves per SIMD the fused march kernels are built for (registers: no spills)
 constexpr int march_fused_waves(int uni)
 {
-  return uni == 12 ? 5 : uni == 11 ? 5 : uni == 10 ? 6 : uni == 6 || uni == 9 ? 4 : uni == 5 ? 5 : uni == 4 || uni == 8 ? 6
+  return uni == 12 ? 5 : uni == 11 ? 5 : uni == 10 || uni == 13 ? 6 : uni == 6 || uni == 9 ? 4 : uni == 5 ? 5 : uni == 4 || uni == 8 ? 6
        : uni == 3 || uni == 7 ? 7 : uni ? 8 : 7;
 }
 
@@ -2090,6 +2115,32 @@ static int grid_for_slices(K kernel, i64 count, int num_cu)
   return (int)(need < cap ? need : cap);
 }
 
+// The packed value image of march variant 13: per window row {+D, 0, +1, +nx} values (32 B, the
+// 5-point 2-D band: {+D, 0, +1, 0}); built from the band arrays at first use, freed by a shift.
+__global__ void k_sym_pack(i64 ld, const double *__restrict__ UD, const double *__restrict__ U0,
+                           const double *__restrict__ U1, const double *__restrict__ Uq, double *__restrict__ out)
+{
+  for (i64 w = (i64)blockIdx.x * blockDim.x + threadIdx.x; w < ld; w += (i64)gridDim.x * blockDim.x)
+  {
+    reinterpret_cast<dpair *>(out)[2 * w] = dpair{UD[w], U0 ? U0[w] : 0.0};
+    reinterpret_cast<dpair *>(out)[2 * w + 1] = dpair{U1[w], Uq ? Uq[w] : 0.0};
+  }
+}
+const double *sym_pack_prepare(const eig_mat_s &Ac)
+{
+  eig_mat_s &A = const_cast<eig_mat_s &>(Ac);
+  if (A.sym_pack) return A.sym_pack;
+  const SellB1 b = sell_b1(A);
+  const SymImg &S = b.sym;
+  const double *UD = S.val + (i64)S.dj[S.nd - 1] * S.ld, *U1 = S.val + (i64)S.j1 * S.ld;
+  const double *U0 = S.j0 >= 0 ? S.val + (i64)S.j0 * S.ld : nullptr;
+  const double *Uq = S.khi < S.nd - 1 ? S.val + (i64)S.dj[S.khi] * S.ld : nullptr;
+  EIG_HIP(hipMalloc(&A.sym_pack, (size_t)S.ld * 32));
+  hipLaunchKernelGGL(k_sym_pack, dim3(2048), dim3(256), 0, A.ctx->stream, S.ld, UD, U0, U1, Uq, A.sym_pack);
+  EIG_HIP(hipGetLastError());
+  return A.sym_pack;
+}
+
 // EIG_MAT_NO_MARCH: the plane-marching kernels are off for this matrix (the slice kernels run).
 static bool march_enabled(const eig_mat_s &A) { return (A.kflags & EIG_MAT_NO_MARCH) == 0; }
 static bool march_span1(const eig_mat_s &A)
@@ -2135,8 +2186,8 @@ static int march_uniform(const eig_mat_s &A, bool fused = false, i64 nplanes = 0
   const bool geo2 = A.sym_geo && A.sym_gx % 64 == 0 && A.window * 16 < (i64(1) << 31);
   if (!A.sym_uniform || (A.kflags & EIG_MAT_NO_UNIFORM))
   {
-    if (!geo2 || !march_span1(A) || A.sym_ld * 8 >= (i64(1) << 31) || A.tune_march_prefetch == 1) return 0;
-    return A.tune_march_prefetch == 10 ? 11 : 10;
+    if (!geo2 || !march_span1(A) || A.sym_ld * 32 >= (i64(1) << 31) || A.tune_march_prefetch == 1) return 0;
+    return A.tune_march_prefetch == 10 ? 11 : A.tune_march_prefetch == 11 ? 13 : 10;
   }
   if (!A.sym_geo) return 1;
   int u = A.tune_march_prefetch > 0 ? 1 + A.tune_march_prefetch : geo2 ? 7 : 4;
@@ -2151,6 +2202,8 @@ static int march_uniform(const eig_mat_s &A, bool fused = false, i64 nplanes = 0
   do {                                                                                                    \
     if (mp.uni == 12)                                                                                     \
       hipLaunchKernelGGL((KERN<uint32_t, false, 12>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);     \
+    else if ((MODE) == kSymN8 && march_span1(A) && mp.uni == 13)                                          \
+      hipLaunchKernelGGL((KERN<uint8_t, true, 13>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);       \
     else if ((MODE) == kSymN8 && march_span1(A) && mp.uni == 11)                                          \
       hipLaunchKernelGGL((KERN<uint8_t, true, 11>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);       \
     else if ((MODE) == kSymN8 && march_span1(A) && mp.uni == 10)                                          \
@@ -2276,6 +2329,7 @@ static MarchPlan march_plan(const eig_mat_s &A, int mode, i64 zb = 0, i64 ze = -
     mp.cq = khi < A.sym_nd - 1 ? A.sym_uc[A.sym_dj[khi]] : 0.0;
   }
   mp.uni = uni;
+  mp.pack = uni == 13 ? sym_pack_prepare(A) : nullptr;
   // measured (tools/march_copy.hip *_pp, profiles/r03bo_march_copy.jsonl): the step's ping-pong at
   // 128^3 (2 x 32 MB of pairs) 12.9 us with plain stores vs 17.6 us nontemporal; at 256^3 (2 x 268
   // MB) no difference either way -- plain stores where every vector a launch touches fits in half
@@ -2593,7 +2647,7 @@ void lanczos_kernel_info(const eig_mat_s &A, bool fused, std::string &name, i64 
     // the band arrays and the vectors (geometric masks: no mask stream)
     const int mv = march && ((mode == kSymN8 && march_span1(A)) || march_kuhn(A)) ? march_uniform(A) : 0;
     if (mv >= 10)
-      bytes = 8 * (i64)A.sym_nup * n + vec;
+      bytes = 8 * (mv == 13 ? 4 : (i64)A.sym_nup) * n + vec;
     else if (mv)
       bytes = (mv >= 2 ? 0 : (i64)A.sym_mask_bytes * n) + vec;
     name = fused ? (march ? "k_lanczos_fused_march" : "k_lanczos_fused_b1")

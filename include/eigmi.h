@@ -216,7 +216,8 @@ enum { EIG_TUNE_MARCH_RUNS = 1, EIG_TUNE_BOX_SEGS = 2, EIG_TUNE_MARCH_PREFETCH =
  * selects (missing neighbours read as exact zeros; grids whose x extent is a multiple of 64);
  * on geometric bands whose values are not uniform (or EIG_MAT_NO_UNIFORM): 1 = the plain masked
  * march on the band arrays, 9 = the value march (eig_mat_info.march_variant 10: the band arrays
- * streamed, masks from the coordinates), 10 = the same with the value streams one plane ahead (11);
+ * streamed, masks from the coordinates), 10 = the same with the value streams one plane ahead (11),
+ * 11 = the value march on a packed copy of the 4 arrays (13: {+D, 0, +1, +nx} per row, two 16-B loads);
  * 0 = automatic.  Bitwise the same results for every value. */
 int eig_mat_tune(eig_mat_t mat, int key, int value);
 

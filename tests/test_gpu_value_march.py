@@ -106,9 +106,10 @@ def test_value_march_bitwise(ctx, mat):
     ref = oracle.csr_mv(A, x)
     for runs in (0, 1, 2, 3, 5, 7):
         base = {}
-        for pf in (1, 9, 10):  # 1: the plain masked march on the arrays; 9 / 10: variants 10 / 11
+        # 1: the plain masked march on the arrays; 9 / 10 / 11: variants 10 / 11 / 13 (13: packed image)
+        for pf in (1, 9, 10, 11):
             M.tune(runs, march_prefetch=pf)
-            assert M.info.march_variant == {1: 0, 9: 10, 10: 11}[pf]
+            assert M.info.march_variant == {1: 0, 9: 10, 10: 11, 11: 13}[pf]
             assert np.array_equal(M.mv_host(x), ref), (runs, pf)
             for fused in (False, True):
                 a, b, _ = eigmi.lanczos_run(M, 25, seed=7, fused=fused)
@@ -132,11 +133,16 @@ def test_value_march_after_shift(ctx):
     A = varcoef(64)
     M = eigmi.Matrix.from_bcsr(ctx, A.rowptr, A.col, A.val)
     assert M.info.march_variant == 10
+    x = np.random.default_rng(2).standard_normal(A.n)
+    M.tune(march_prefetch=11)  # the packed image (variant 13): built now, rebuilt after the shift
+    assert np.array_equal(M.mv_host(x), oracle.csr_mv(A, x))
     M.shift_diag(-2.375)
     val = A.val.copy()
     oracle.lib.orc_shift_diag(A.n, A.rowptr, A.col, val, -2.375)
-    x = np.random.default_rng(2).standard_normal(A.n)
-    assert np.array_equal(M.mv_host(x), oracle.csr_mv(oracle.CSR(A.nrows, A.rowptr, A.col, val), x))
+    B = oracle.CSR(A.nrows, A.rowptr, A.col, val)
+    for pf in (11, 0):
+        M.tune(march_prefetch=pf)
+        assert np.array_equal(M.mv_host(x), oracle.csr_mv(B, x)), pf
 
 
 @pytest.mark.gpu
