@@ -235,6 +235,10 @@ def main():
     ap.add_argument("--comm-self", action="store_true",
                     help="one GPU: attach a one-rank RCCL communicator with EIG_COMM_ALWAYS, so every step's "
                          "allreduce runs through ncclAllReduce (the transport's per-step cost without xGMI)")
+    ap.add_argument("--allreduce", choices=["auto", "rccl", "mailbox"], default="auto",
+                    help="N > 1: the step's allreduce transport -- ncclAllReduce, or the xGMI mailbox (one "
+                         "launch stores the 3 sums into every peer's mailbox; set up and validated by all "
+                         "ranks, else RCCL); auto = both in the trial, the faster wins")
     ap.add_argument("--launch", choices=["auto", "graph", "eager"], default="auto",
                     help="timed steps as one hipGraph replay or launched one by one; auto = graph when "
                          "N > 1 (host-bound halo/allreduce calls), eager at N = 1 (measured faster there)")
@@ -267,7 +271,9 @@ def main():
         uid = eigmi.Context.unique_id() if rank == 0 else bytes(128)
         t = torch.tensor(list(uid), dtype=torch.uint8)
         dist.broadcast(t, 0)
-        ctx.comm_init(world, rank, bytes(t.tolist()))
+        # RCCL, plus the xGMI mailbox allreduce where every rank validates it (eig_comm_init_ex
+        # EIG_COMM_MAILBOX; agreed by all ranks, else RCCL alone) -- the auto trial times both
+        ctx.comm_init(world, rank, bytes(t.tolist()), mailbox=args.allreduce != "rccl")
 
     N = args.N
     n = N ** 3
@@ -309,8 +315,12 @@ def main():
             # "whole" = the exchange first, then one launch (EIG_TUNE_HALO; no second launch's fixed
             # cost) -- N > 1 only, one GPU has no halo
             halos = ("split", "whole") if world > 1 else ("split",)
-            for var, halo in [(v, h) for v in ("fused", "pipelined") for h in halos]:
+            have_mb = world > 1 and ctx.comm_info()["allreduce"] == "mailbox"
+            ars = (("rccl", "mailbox") if args.allreduce == "auto" else (args.allreduce,)) if have_mb else ("rccl",)
+            for var, halo, ar in [(v, h, a) for v in ("fused", "pipelined") for h in halos for a in ars]:
                 M.tune(halo_whole=int(halo == "whole"))
+                if world > 1:
+                    ctx.select_allreduce(ar)
                 # every call below may already have queued a halo exchange or an allreduce on the
                 # other ranks when it fails here, so a failing rank cannot rejoin them at a barrier:
                 # it exits non-zero at once and the launcher tears the job down on every rank
@@ -346,13 +356,22 @@ def main():
                         tw.close()
                 barrier()
                 for la in launches:
-                    trial[f"{var}/{la}/{halo}"] = round(max_over_ranks(ms[la]), 4)
+                    trial[f"{var}/{la}/{halo}/{ar}"] = round(max_over_ranks(ms[la]), 4)
+            if "mailbox" in ars and max_over_ranks(ctx.comm_info()["mailbox_errors"]) > 0:
+                # a mailbox call timed out on some rank (its sums read NaN): not a candidate
+                trial = {k: (float("inf") if k.endswith("/mailbox") else v) for k, v in trial.items()}
             best = min(trial, key=trial.get)
-            variant, best_launch, best_halo = best.split("/")
+            variant, best_launch, best_halo, best_ar = best.split("/")
             if args.launch == "auto":
                 args.launch = best_launch
             M.tune(halo_whole=int(best_halo == "whole"))
+            if world > 1:
+                ctx.select_allreduce(best_ar)
             halo_mode = best_halo
+    if world > 1 and trial is None:
+        # no trial: RCCL unless the mailbox was asked for (and is set up on every rank)
+        ctx.select_allreduce("mailbox" if args.allreduce == "mailbox" and ctx.comm_info()["allreduce"] == "mailbox"
+                             else "rccl")
     fused = variant in ("fused", "pipelined")
     pipelined = variant == "pipelined"
     # the K timed steps are captured as one hipGraph before the clock starts (kernels, halo

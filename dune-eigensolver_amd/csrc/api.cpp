@@ -63,7 +63,7 @@ void *ctx_buffer(eig_ctx_t ctx, int slot, size_t bytes)
 void allreduce_sum(eig_ctx_t ctx, double *buf, i64 count, hipStream_t s)
 {
   if (!ctx->collectives() || count <= 0) return;
-  if (ctx->mbox && ctx->mbox->ready)
+  if (ctx->mbox && ctx->mbox->ready && ctx->mbox->on)
   {
     for (i64 off = 0; off < count; off += kMailboxVals)
       launch_mailbox_allreduce(buf + off, (int)std::min<i64>(kMailboxVals, count - off), ctx->mbox->dev,
@@ -96,7 +96,7 @@ void allreduce_sum(eig_ctx_t ctx, double *buf, i64 count, hipStream_t s)
 
 bool allreduce_overlaps(eig_ctx_t ctx)
 {
-  const bool ovl = ctx->collectives() && !ctx->loop && ((ctx->mbox && ctx->mbox->ready) || ctx->comm_red);
+  const bool ovl = ctx->collectives() && !ctx->loop && ((ctx->mbox && ctx->mbox->ready && ctx->mbox->on) || ctx->comm_red);
   // the reduction stream exists only where it is used (every stream takes a hardware queue)
   if (ovl && !ctx->red_stream) EIG_HIP(hipStreamCreateWithFlags(&ctx->red_stream, hipStreamNonBlocking));
   return ovl;
@@ -105,7 +105,7 @@ bool allreduce_overlaps(eig_ctx_t ctx)
 void allreduce_sum_red(eig_ctx_t ctx, double *buf, i64 count, hipStream_t s)
 {
   EIG_CHECK(allreduce_overlaps(ctx), EIG_ERR_ARG, "allreduce_sum_red: no concurrent allreduce transport");
-  if (ctx->mbox && ctx->mbox->ready)
+  if (ctx->mbox && ctx->mbox->ready && ctx->mbox->on)
   {
     allreduce_sum(ctx, buf, count, s);
     return;
@@ -477,6 +477,17 @@ extern "C" int eig_comm_ipc_open(eig_ctx_t ctx, const unsigned char *handles)
   });
 }
 
+extern "C" int eig_comm_select_allreduce(eig_ctx_t ctx, int kind)
+{
+  return guard(ctx, [&] {
+    EIG_CHECK(ctx && (kind == EIG_AR_RCCL || kind == EIG_AR_MAILBOX), EIG_ERR_ARG,
+              "eig_comm_select_allreduce: EIG_AR_RCCL or EIG_AR_MAILBOX");
+    EIG_CHECK(kind == EIG_AR_RCCL ? ctx->comm != nullptr : (ctx->mbox && ctx->mbox->ready), EIG_ERR_ARG,
+              "eig_comm_select_allreduce: that transport is not set up on this context");
+    if (ctx->mbox) ctx->mbox->on = kind == EIG_AR_MAILBOX;
+  });
+}
+
 extern "C" int eig_comm_info(eig_ctx_t ctx, int *nranks, int *rank, int *allreduce, int *mailbox_errors)
 {
   return guard(ctx, [&] {
@@ -485,7 +496,7 @@ extern "C" int eig_comm_info(eig_ctx_t ctx, int *nranks, int *rank, int *allredu
     if (rank) *rank = ctx->rank;
     if (allreduce)
       *allreduce = !ctx->collectives()                 ? EIG_AR_NONE
-                   : (ctx->mbox && ctx->mbox->ready)   ? EIG_AR_MAILBOX
+                   : (ctx->mbox && ctx->mbox->ready && ctx->mbox->on) ? EIG_AR_MAILBOX
                    : ctx->loop                         ? EIG_AR_LOOPBACK
                                                        : EIG_AR_RCCL;
     if (mailbox_errors)

@@ -112,6 +112,7 @@ struct MailboxHost {
   void *state = nullptr;         // ctr + err (hipMalloc)
   std::vector<void *> opened;    // IPC-opened peer mappings (closed on destroy)
   bool ready = false;            // peers opened and validated: allreduce_sum uses it
+  bool on = true;                // eig_comm_select_allreduce: false = ncclAllReduce although ready
 };
 constexpr unsigned long long kMailboxTimeout = 1000000000ull;  // 10 s of s_memrealtime (100 MHz)
 void launch_mailbox_allreduce(double *buf, int count, const Mailbox &mb, unsigned long long timeout, hipStream_t s);

@@ -104,6 +104,7 @@ SIGNATURES = {
     "eig_comm_info": (_int, [_vp, ctypes.POINTER(_int), ctypes.POINTER(_int), ctypes.POINTER(_int),
                              ctypes.POINTER(_int)]),
     "eig_comm_counters": (_int, [_vp, ctypes.POINTER(_i64)]),
+    "eig_comm_select_allreduce": (_int, [_vp, _int]),
     "eig_malloc": (_int, [_vp, ctypes.c_size_t, ctypes.POINTER(_vp)]),
     "eig_free": (_int, [_vp, _vp]),
     "eig_memcpy_h2d": (_int, [_vp, _vp, _vp, ctypes.c_size_t]),
@@ -312,6 +313,11 @@ class Context:
 
     def allreduce_sum(self, arr, count=None):
         self.check(lib.eig_comm_allreduce_sum(self.h, arr.ptr, arr.n if count is None else count))
+
+    def select_allreduce(self, kind):
+        """eig_comm_select_allreduce: "rccl" or "mailbox" (the latter set up and validated by
+        comm_init(mailbox=True)); every rank must select the same."""
+        self.check(lib.eig_comm_select_allreduce(self.h, {"rccl": 1, "mailbox": 2}[kind]))
 
     def comm_info(self):
         v = [_int(0) for _ in range(4)]

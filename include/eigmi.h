@@ -100,6 +100,9 @@ int eig_comm_ipc_handle(eig_ctx_t ctx, int nranks, int rank, unsigned char handl
 int eig_comm_ipc_open(eig_ctx_t ctx, const unsigned char *handles);
 /* nranks / rank / the allreduce in use (eig_allreduce_kind) / mailbox timeouts so far (syncs). */
 int eig_comm_info(eig_ctx_t ctx, int *nranks, int *rank, int *allreduce, int *mailbox_errors);
+/* Switch the allreduce transport of a communicator that has both (RCCL + a validated mailbox):
+ * EIG_AR_RCCL or EIG_AR_MAILBOX.  Every rank must select the same one (no collective inside). */
+int eig_comm_select_allreduce(eig_ctx_t ctx, int kind);
 
 /* ---------------------------------------------------------------- device memory ------------ */
 int eig_malloc(eig_ctx_t ctx, size_t bytes, void **ptr);
