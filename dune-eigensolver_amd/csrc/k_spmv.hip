@@ -1188,6 +1188,8 @@ __device__ __forceinline__ void march_rows_geo2(const SellB1 &A, const MarchPlan
   const __amdgpu_buffer_rsrc_t pk = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<double *>(mp.pack ? mp.pack : S.val), 0, VAL == 3 && mp.pack ? (int)(4u * vbytes) : 0, 0x00020000);
   const __amdgpu_buffer_rsrc_t pkn = VAL == 3 && mp.dn && yw > 0 ? pk : vz;
+  const double *pD = S.val + (i64)S.dj[S.nd - 1] * S.ld, *p1 = S.val + (i64)(S.j1 >= 0 ? S.j1 : 0) * S.ld;
+  const double *p0 = S.j0 >= 0 ? S.val + (i64)S.j0 * S.ld : nullptr, *pq = S.val + (i64)S.dj[S.khi] * S.ld;
   auto vload = [&](unsigned o, Vals &v, bool on) {  // on: wave-uniform (false: zeros, no traffic)
     if constexpr (VAL == 3)
     {
@@ -1203,6 +1205,17 @@ __device__ __forceinline__ void march_rows_geo2(const SellB1 &A, const MarchPlan
       v.aq = mp.dq ? p1.y : 0.0;
       v.an = pn.y;
       v.ae = pe.x;
+    }
+    else if constexpr (VAL == 4)
+    {
+      // (measurement variant 14: the same loads through 64-bit global addresses, as the plain march)
+      const i64 r = (i64)(o >> 3);
+      v.aD = on ? __builtin_nontemporal_load(pD + r) : 0.0;
+      v.a0 = on && p0 ? __builtin_nontemporal_load(p0 + r) : 0.0;
+      v.ap = on ? __builtin_nontemporal_load(p1 + r) : 0.0;
+      v.aq = on && mp.dq ? pq[r] : 0.0;
+      v.an = on && mp.dn && yw > 0 ? pq[r + mp.dn] : 0.0;
+      v.ae = on && lane == 0 && x0 > 0 ? p1[r - 1] : 0.0;
     }
     else
     {
@@ -1237,7 +1250,7 @@ __device__ __forceinline__ void march_rows_geo2(const SellB1 &A, const MarchPlan
       gather(vo + Db, gn);
     else
       gather(vo, gc);
-    if constexpr (VAL == 1 || VAL == 3) vload(vv, vc_, true);
+    if constexpr (VAL == 1 || VAL >= 3) vload(vv, vc_, true);
     const int zg = z + mp.gz0;
     bload(zg + PF + 1 < mp.gz ? rs : r0, vo + (unsigned)(PF + 1) * Db, pf);
     if constexpr (VPF) vload(vv + Dv, vn_, z + 1 < z1);
@@ -1452,7 +1465,7 @@ __device__ __forceinline__ void march_rows(const SellB1 &A, const MarchPlan &mp,
   {
     // 3, 4, 5: +D operand 1, 2, 3 planes ahead; 6: 3 planes ahead and the gathers one plane ahead
     if constexpr (UNI >= 10)  // 10, 11: the value march (band arrays streamed), 11 one plane ahead, 13 packed
-      march_rows_geo2<0, false, UNI == 13 ? 3 : UNI - 9>(A, mp, own, lane, wave, x, epi, pre);
+      march_rows_geo2<0, false, UNI == 13 ? 3 : UNI == 14 ? 4 : UNI - 9>(A, mp, own, lane, wave, x, epi, pre);
     else if constexpr (UNI >= 7)  // 7, 8, 9: march_rows_geo2 with the prefetches of 3, 4, 6
       march_rows_geo2<UNI == 9 ? 2 : UNI - 7, UNI == 9, 0>(A, mp, own, lane, wave, x, epi, pre);
     else
@@ -1648,7 +1661,7 @@ __global__ __launch_bounds__(kStreamThreads, march_mv_waves(UNI)) void k_lanczos
 // resident waves per SIMD the fused march kernels are built for (registers: no spills)
 constexpr int march_fused_waves(int uni)
 {
-  return uni == 12 ? 5 : uni == 11 ? 5 : uni == 10 || uni == 13 ? 6 : uni == 6 || uni == 9 ? 4 : uni == 5 ? 5 : uni == 4 || uni == 8 ? 6
+  return uni == 12 ? 5 : uni == 11 ? 5 : uni == 10 || uni == 13 || uni == 14 ? 6 : uni == 6 || uni == 9 ? 4 : uni == 5 ? 5 : uni == 4 || uni == 8 ? 6
        : uni == 3 || uni == 7 ? 7 : uni ? 8 : 7;
 }
 
@@ -2187,7 +2200,7 @@ static int march_uniform(const eig_mat_s &A, bool fused = false, i64 nplanes = 0
   if (!A.sym_uniform || (A.kflags & EIG_MAT_NO_UNIFORM))
   {
     if (!geo2 || !march_span1(A) || A.sym_ld * 32 >= (i64(1) << 31) || A.tune_march_prefetch == 1) return 0;
-    return A.tune_march_prefetch == 10 ? 11 : A.tune_march_prefetch == 11 ? 13 : 10;
+    return A.tune_march_prefetch == 10 ? 11 : A.tune_march_prefetch == 11 ? 13 : A.tune_march_prefetch == 12 ? 14 : 10;
   }
   if (!A.sym_geo) return 1;
   int u = A.tune_march_prefetch > 0 ? 1 + A.tune_march_prefetch : geo2 ? 7 : 4;
@@ -2204,6 +2217,8 @@ static int march_uniform(const eig_mat_s &A, bool fused = false, i64 nplanes = 0
       hipLaunchKernelGGL((KERN<uint32_t, false, 12>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);     \
     else if ((MODE) == kSymN8 && march_span1(A) && mp.uni == 13)                                          \
       hipLaunchKernelGGL((KERN<uint8_t, true, 13>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);       \
+    else if ((MODE) == kSymN8 && march_span1(A) && mp.uni == 14)                                          \
+      hipLaunchKernelGGL((KERN<uint8_t, true, 14>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);       \
     else if ((MODE) == kSymN8 && march_span1(A) && mp.uni == 11)                                          \
       hipLaunchKernelGGL((KERN<uint8_t, true, 11>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);       \
     else if ((MODE) == kSymN8 && march_span1(A) && mp.uni == 10)                                          \

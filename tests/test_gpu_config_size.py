@@ -29,11 +29,14 @@ def test_orthonormalize_blocked_128cubed(ctx, variant, name):
     Q.free()
     ref = oracle.orthonormalize_mv8(Qh, n, m, name)
     diff = np.abs(got - ref).max()
-    G = oracle.gram_mv8(got, got, n, m)
-    orth = np.abs(G - np.eye(m)).max()
-    print(f"orthonormalize_blocked {name} n={n} m={m}: |Q - Q_ref| = {diff:.3e}, |Q^T Q - I| = {orth:.3e}")
+    orth = np.abs(oracle.gram_mv8(got, got, n, m) - np.eye(m)).max()
+    orth_ref = np.abs(oracle.gram_mv8(ref, ref, n, m) - np.eye(m)).max()
+    print(f"orthonormalize_blocked {name} n={n} m={m}: |Q - Q_ref| = {diff:.3e}, |Q^T Q - I| = {orth:.3e} "
+          f"(reference algorithm {orth_ref:.3e})")
     assert diff < 1e-12
-    assert orth < 1e-13
+    # single-pass block CGS (kernels_cpp.hh:309-349) loses ~n eps of orthogonality at this n: the
+    # bar is the restated algorithm's own loss (measured 1.04e-13 at n = 2^21, m = 32)
+    assert orth <= 2 * orth_ref + 1e-14 and orth < 1e-12
 
 
 def test_b_orthonormalize_1m_rows(ctx):
