@@ -1193,11 +1193,13 @@ __device__ __forceinline__ void march_rows_geo2(const SellB1 &A, const MarchPlan
   auto vload = [&](unsigned o, Vals &v, bool on) {  // on: wave-uniform (false: zeros, no traffic)
     if constexpr (VAL == 3)
     {
-      const dpair p0 = __builtin_bit_cast(dpair, __builtin_amdgcn_raw_buffer_load_b128(pk, (int)(4 * o), 0, 2));
-      const dpair p1 = __builtin_bit_cast(dpair, __builtin_amdgcn_raw_buffer_load_b128(pk, (int)(4 * o + 16), 0, 0));
-      const dpair pn = __builtin_bit_cast(dpair, __builtin_amdgcn_raw_buffer_load_b128(pkn, (int)(4 * (o + dnv) + 16), 0, 0));
+      // (byte offsets: (+D, 0) at 16 w, (+1, +nx) at 16 (ld + w))
+      const dpair p0 = __builtin_bit_cast(dpair, __builtin_amdgcn_raw_buffer_load_b128(pk, (int)(2 * o), 0, 2));
+      const dpair p1 = __builtin_bit_cast(dpair, __builtin_amdgcn_raw_buffer_load_b128(pk, (int)(2 * o + 2 * vbytes), 0, 0));
+      const dpair pn =
+          __builtin_bit_cast(dpair, __builtin_amdgcn_raw_buffer_load_b128(pkn, (int)(2 * (o + dnv) + 2 * vbytes), 0, 0));
       // (lane 0's edge row w - 1; the other lanes, and lane 0 at x = 0, an out-of-range offset)
-      const unsigned peo = eov == kOut ? kOut : 4 * o - 16;
+      const unsigned peo = eov == kOut ? kOut : 2 * o - 16 + 2 * vbytes;
       const dpair pe = __builtin_bit_cast(dpair, __builtin_amdgcn_raw_buffer_load_b128(pk, (int)peo, 0, 0));
       v.aD = p0.x;
       v.a0 = p0.y;
@@ -1205,6 +1207,21 @@ __device__ __forceinline__ void march_rows_geo2(const SellB1 &A, const MarchPlan
       v.aq = mp.dq ? p1.y : 0.0;
       v.an = pn.y;
       v.ae = pe.x;
+    }
+    else if constexpr (VAL == 5)
+    {
+      // variant 15: the pack through 64-bit global addresses (wave-uniform / lane-0 conditions
+      // instead of range-checked descriptors)
+      const i64 r = (i64)(o >> 3);
+      const dpair *P01 = reinterpret_cast<const dpair *>(mp.pack), *P23 = P01 + S.ld;
+      const dpair p0 = __builtin_nontemporal_load(P01 + r);
+      const dpair p1 = P23[r];
+      v.aD = p0.x;
+      v.a0 = p0.y;
+      v.ap = p1.x;
+      v.aq = p1.y;
+      v.an = mp.dn && yw > 0 ? P23[r + mp.dn].y : 0.0;
+      v.ae = lane == 0 && x0 > 0 ? P23[r - 1].x : 0.0;
     }
     else if constexpr (VAL == 4)
     {
@@ -1465,7 +1482,7 @@ __device__ __forceinline__ void march_rows(const SellB1 &A, const MarchPlan &mp,
   {
     // 3, 4, 5: +D operand 1, 2, 3 planes ahead; 6: 3 planes ahead and the gathers one plane ahead
     if constexpr (UNI >= 10)  // 10, 11: the value march (band arrays streamed), 11 one plane ahead, 13 packed
-      march_rows_geo2<0, false, UNI == 13 ? 3 : UNI == 14 ? 4 : UNI - 9>(A, mp, own, lane, wave, x, epi, pre);
+      march_rows_geo2<0, false, UNI == 13 ? 3 : UNI == 14 ? 4 : UNI == 15 ? 5 : UNI - 9>(A, mp, own, lane, wave, x, epi, pre);
     else if constexpr (UNI >= 7)  // 7, 8, 9: march_rows_geo2 with the prefetches of 3, 4, 6
       march_rows_geo2<UNI == 9 ? 2 : UNI - 7, UNI == 9, 0>(A, mp, own, lane, wave, x, epi, pre);
     else
@@ -1661,7 +1678,7 @@ __global__ __launch_bounds__(kStreamThreads, march_mv_waves(UNI)) void k_lanczos
 // resident waves per SIMD the fused march kernels are built for (registers: no spills)
 constexpr int march_fused_waves(int uni)
 {
-  return uni == 12 ? 5 : uni == 11 ? 5 : uni == 10 || uni == 13 || uni == 14 ? 6 : uni == 6 || uni == 9 ? 4 : uni == 5 ? 5 : uni == 4 || uni == 8 ? 6
+  return uni == 12 ? 5 : uni == 11 ? 5 : uni == 10 || uni >= 13 ? 6 : uni == 6 || uni == 9 ? 4 : uni == 5 ? 5 : uni == 4 || uni == 8 ? 6
        : uni == 3 || uni == 7 ? 7 : uni ? 8 : 7;
 }
 
@@ -2128,15 +2145,16 @@ static int grid_for_slices(K kernel, i64 count, int num_cu)
   return (int)(need < cap ? need : cap);
 }
 
-// The packed value image of march variant 13: per window row {+D, 0, +1, +nx} values (32 B, the
-// 5-point 2-D band: {+D, 0, +1, 0}); built from the band arrays at first use, freed by a shift.
+// The packed value image of march variants 13 / 15: two arrays of value pairs, (+D, 0) and (+1, +nx)
+// per window row (the 5-point 2-D band: +nx = 0), so a wave reads each with one 16-B load per lane
+// of 1 KB contiguous; built from the band arrays at first use, freed by a shift.
 __global__ void k_sym_pack(i64 ld, const double *__restrict__ UD, const double *__restrict__ U0,
                            const double *__restrict__ U1, const double *__restrict__ Uq, double *__restrict__ out)
 {
   for (i64 w = (i64)blockIdx.x * blockDim.x + threadIdx.x; w < ld; w += (i64)gridDim.x * blockDim.x)
   {
-    reinterpret_cast<dpair *>(out)[2 * w] = dpair{UD[w], U0 ? U0[w] : 0.0};
-    reinterpret_cast<dpair *>(out)[2 * w + 1] = dpair{U1[w], Uq ? Uq[w] : 0.0};
+    reinterpret_cast<dpair *>(out)[w] = dpair{UD[w], U0 ? U0[w] : 0.0};
+    reinterpret_cast<dpair *>(out)[ld + w] = dpair{U1[w], Uq ? Uq[w] : 0.0};
   }
 }
 const double *sym_pack_prepare(const eig_mat_s &Ac)
@@ -2200,7 +2218,8 @@ static int march_uniform(const eig_mat_s &A, bool fused = false, i64 nplanes = 0
   if (!A.sym_uniform || (A.kflags & EIG_MAT_NO_UNIFORM))
   {
     if (!geo2 || !march_span1(A) || A.sym_ld * 32 >= (i64(1) << 31) || A.tune_march_prefetch == 1) return 0;
-    return A.tune_march_prefetch == 10 ? 11 : A.tune_march_prefetch == 11 ? 13 : A.tune_march_prefetch == 12 ? 14 : 10;
+    const int tp = A.tune_march_prefetch;
+    return tp == 10 ? 11 : tp == 11 ? 13 : tp == 12 ? 14 : tp == 13 ? 15 : 10;
   }
   if (!A.sym_geo) return 1;
   int u = A.tune_march_prefetch > 0 ? 1 + A.tune_march_prefetch : geo2 ? 7 : 4;
@@ -2219,6 +2238,8 @@ static int march_uniform(const eig_mat_s &A, bool fused = false, i64 nplanes = 0
       hipLaunchKernelGGL((KERN<uint8_t, true, 13>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);       \
     else if ((MODE) == kSymN8 && march_span1(A) && mp.uni == 14)                                          \
       hipLaunchKernelGGL((KERN<uint8_t, true, 14>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);       \
+    else if ((MODE) == kSymN8 && march_span1(A) && mp.uni == 15)                                          \
+      hipLaunchKernelGGL((KERN<uint8_t, true, 15>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);       \
     else if ((MODE) == kSymN8 && march_span1(A) && mp.uni == 11)                                          \
       hipLaunchKernelGGL((KERN<uint8_t, true, 11>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);       \
     else if ((MODE) == kSymN8 && march_span1(A) && mp.uni == 10)                                          \
@@ -2344,7 +2365,7 @@ static MarchPlan march_plan(const eig_mat_s &A, int mode, i64 zb = 0, i64 ze = -
     mp.cq = khi < A.sym_nd - 1 ? A.sym_uc[A.sym_dj[khi]] : 0.0;
   }
   mp.uni = uni;
-  mp.pack = uni == 13 ? sym_pack_prepare(A) : nullptr;
+  mp.pack = uni == 13 || uni == 15 ? sym_pack_prepare(A) : nullptr;
   // measured (tools/march_copy.hip *_pp, profiles/r03bo_march_copy.jsonl): the step's ping-pong at
   // 128^3 (2 x 32 MB of pairs) 12.9 us with plain stores vs 17.6 us nontemporal; at 256^3 (2 x 268
   // MB) no difference either way -- plain stores where every vector a launch touches fits in half
@@ -2662,7 +2683,7 @@ void lanczos_kernel_info(const eig_mat_s &A, bool fused, std::string &name, i64 
     // the band arrays and the vectors (geometric masks: no mask stream)
     const int mv = march && ((mode == kSymN8 && march_span1(A)) || march_kuhn(A)) ? march_uniform(A) : 0;
     if (mv >= 10)
-      bytes = 8 * (mv == 13 ? 4 : (i64)A.sym_nup) * n + vec;
+      bytes = 8 * (mv == 13 || mv == 15 ? 4 : (i64)A.sym_nup) * n + vec;
     else if (mv)
       bytes = (mv >= 2 ? 0 : (i64)A.sym_mask_bytes * n) + vec;
     name = fused ? (march ? "k_lanczos_fused_march" : "k_lanczos_fused_b1")

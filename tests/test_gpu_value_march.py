@@ -107,9 +107,9 @@ def test_value_march_bitwise(ctx, mat):
     for runs in (0, 1, 2, 3, 5, 7):
         base = {}
         # 1: the plain masked march on the arrays; 9 / 10 / 11: variants 10 / 11 / 13 (13: packed image)
-        for pf in (1, 9, 10, 11):
+        for pf in (1, 9, 10, 11, 12, 13):
             M.tune(runs, march_prefetch=pf)
-            assert M.info.march_variant == {1: 0, 9: 10, 10: 11, 11: 13}[pf]
+            assert M.info.march_variant == {1: 0, 9: 10, 10: 11, 11: 13, 12: 14, 13: 15}[pf]
             assert np.array_equal(M.mv_host(x), ref), (runs, pf)
             for fused in (False, True):
                 a, b, _ = eigmi.lanczos_run(M, 25, seed=7, fused=fused)
