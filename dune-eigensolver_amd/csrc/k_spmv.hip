@@ -1337,7 +1337,10 @@ __device__ __forceinline__ void march_rows_geo2(const SellB1 &A, const MarchPlan
 constexpr unsigned kKuhn15 = (1u << 0) | (1u << 1) | (1u << 3) | (1u << 4) | (1u << 9) | (1u << 10) | (1u << 12) |
                              (1u << 13) | (1u << 14) | (1u << 16) | (1u << 17) | (1u << 22) | (1u << 23) |
                              (1u << 25) | (1u << 26);
-template <class X, class EPI, class PRE>
+// KP (march variant 16): the values from the Kuhn pack (mp.pack: four arrays of value pairs (0, +1),
+// (+nx, +nx+1), (+D, +D+1), (+D+nx, +D+nx+1) per window row -- 4 instead of 8 16-B/8-B streams and
+// 2 instead of 4 gathers) through 64-bit global addresses, lane 0's edge values by exec-masked loads.
+template <bool KP, class X, class EPI, class PRE>
 __device__ __forceinline__ void march_rows_kuhn(const SellB1 &A, const MarchPlan &mp, i64 own, int lane, int wave,
                                                 X x, EPI &epi, PRE &pre)
 {
@@ -1395,8 +1398,39 @@ __device__ __forceinline__ void march_rows_kuhn(const SellB1 &A, const MarchPlan
   bload(rs, vo + eoff, rB0e);
   bload(rp, vo + nxb, rBp);
   bload(rp, vo + nxb + eoff, rBpe);
-  double aDp = below ? ld8(aDd, vv - Dv) : 0.0, aD1p = below ? ld8(aD1d, vv - Dv) : 0.0,
-         aD1pe = below ? ld8(aD1d, vv - Dv + eov) : 0.0;
+  // Kuhn pack: array q of pairs at byte 16 (q ld + w), one descriptor (32-bit offsets)
+  const __amdgpu_buffer_rsrc_t kp = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<double *>(KP && mp.pack ? mp.pack : S.val), 0, KP && mp.pack ? (int)(8u * vbytes) : 0, 0x00020000);
+  const unsigned kq = 2u * vbytes;  // bytes per pair array
+  auto kl = [&](int q, unsigned row_off) {  // pair of array q at byte offset row_off (= 16 row)
+    return __builtin_bit_cast(dpair, __builtin_amdgcn_raw_buffer_load_b128(kp, (int)(row_off + (unsigned)q * kq), 0, 0));
+  };
+  auto kle = [&](int q, unsigned row_off, bool on) {  // lane 0's edge value (.y); others: out of range
+    const unsigned o = on ? row_off + (unsigned)q * kq + 8u : kOut;
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(kp, (int)o, 0, 0));
+  };
+  auto klnt = [&](int q, unsigned row_off) {
+    return __builtin_bit_cast(dpair, __builtin_amdgcn_raw_buffer_load_b128(kp, (int)(row_off + (unsigned)q * kq), 0, 2));
+  };
+  const unsigned nxk = 2u * nxv, Dk = 2u * Dv;
+  const bool le = lane == 0 && x0 > 0;  // lane 0's value edge (row x0 - 1) exists
+  double aDp = 0.0, aD1p = 0.0, aD1pe = 0.0;
+  if constexpr (KP)
+  {
+    if (below)
+    {
+      const dpair k2 = kl(2, 2u * vv - Dk);
+      aDp = k2.x;
+      aD1p = k2.y;
+      aD1pe = kle(2, 2u * vv - Dk - 16u, le);
+    }
+  }
+  else
+  {
+    aDp = below ? ld8(aDd, vv - Dv) : 0.0;
+    aD1p = below ? ld8(aD1d, vv - Dv) : 0.0;
+    aD1pe = below ? ld8(aD1d, vv - Dv + eov) : 0.0;
+  }
   if (!pre(x)) return;
   double Am = x.val(rAm), Ame = x.val(rAme), A0 = x.val(rA0), A0e = x.val(rA0e), Bm = x.val(rBm), Bme = x.val(rBme),
          Bp = x.val(rBp), Bpe = x.val(rBpe);
@@ -1417,14 +1451,37 @@ __device__ __forceinline__ void march_rows_kuhn(const SellB1 &A, const MarchPlan
       bload(qm, vo + Db - nxb + eoff, rCme);
     }
     // the row's upper values (once-read streams nontemporal; +nx.. arrays are re-read by line y + 1)
-    const double a0 = ld8nt(a0d, vv), a1 = ld8nt(a1d, vv), aN = ld8(aNd, vv), aN1 = ld8(aN1d, vv),
-                 aD = ld8nt(aDd, vv), aD1 = ld8nt(aD1d, vv), aDN = ld8(aDNd, vv), aDN1 = ld8(aDN1d, vv);
-    const double a1e = ld8(a1d, vv + eov), aD1e = ld8(aD1d, vv + eov);
-    // mirrored lower entries at line y - 1 (plane z: -nx, -nx-1; plane z - 1: -D-nx, -D-nx-1)
-    const double aNl = ld8(aNm, vv - nxv), aN1l = ld8(aN1m, vv - nxv), aN1le = ld8(aN1m, vv - nxv + eov);
-    const __amdgpu_buffer_rsrc_t dnm = dn && yw > 0 ? aDNd : vz, dn1m = dn && yw > 0 ? aDN1d : vz;
-    const double aDNl = ld8(dnm, vv - Dv - nxv), aDN1l = ld8(dn1m, vv - Dv - nxv),
-                 aDN1le = ld8(dn1m, vv - Dv - nxv + eov);
+    double a0, a1, aN, aN1, aD, aD1, aDN, aDN1, a1e = 0.0, aD1e = 0.0;
+    double aNl = 0.0, aN1l = 0.0, aN1le = 0.0, aDNl = 0.0, aDN1l = 0.0, aDN1le = 0.0;
+    if constexpr (KP)
+    {
+      const unsigned ko = 2u * vv;
+      const dpair k0 = klnt(0, ko), k1 = kl(1, ko), k2 = klnt(2, ko), k3 = kl(3, ko);
+      a0 = k0.x, a1 = k0.y, aN = k1.x, aN1 = k1.y, aD = k2.x, aD1 = k2.y, aDN = k3.x, aDN1 = k3.y;
+      a1e = kle(0, ko - 16u, le);
+      aD1e = kle(2, ko - 16u, le);
+      // mirrored lower entries at line y - 1 (plane z: -nx, -nx-1; plane z - 1: -D-nx, -D-nx-1): the
+      // wave-uniform line / plane conditions pick an out-of-range offset (zeros, no traffic)
+      const bool ym = yw > 0, dm = dn && yw > 0;
+      const dpair kn = __builtin_bit_cast(
+          dpair, __builtin_amdgcn_raw_buffer_load_b128(kp, (int)(ym ? ko - nxk + kq : kOut), 0, 0));
+      aNl = kn.x, aN1l = kn.y;
+      aN1le = kle(1, ko - nxk - 16u, le && ym);
+      const dpair kd = __builtin_bit_cast(
+          dpair, __builtin_amdgcn_raw_buffer_load_b128(kp, (int)(dm ? ko - Dk - nxk + 3u * kq : kOut), 0, 0));
+      aDNl = kd.x, aDN1l = kd.y;
+      aDN1le = kle(3, ko - Dk - nxk - 16u, le && dm);
+    }
+    else
+    {
+      a0 = ld8nt(a0d, vv), a1 = ld8nt(a1d, vv), aN = ld8(aNd, vv), aN1 = ld8(aN1d, vv);
+      aD = ld8nt(aDd, vv), aD1 = ld8nt(aD1d, vv), aDN = ld8(aDNd, vv), aDN1 = ld8(aDN1d, vv);
+      a1e = ld8(a1d, vv + eov), aD1e = ld8(aD1d, vv + eov);
+      // mirrored lower entries at line y - 1 (plane z: -nx, -nx-1; plane z - 1: -D-nx, -D-nx-1)
+      aNl = ld8(aNm, vv - nxv), aN1l = ld8(aN1m, vv - nxv), aN1le = ld8(aN1m, vv - nxv + eov);
+      const __amdgpu_buffer_rsrc_t dnm = dn && yw > 0 ? aDNd : vz, dn1m = dn && yw > 0 ? aDN1d : vz;
+      aDNl = ld8(dnm, vv - Dv - nxv), aDN1l = ld8(dn1m, vv - Dv - nxv), aDN1le = ld8(dn1m, vv - Dv - nxv + eov);
+    }
     const double C0 = x.val(rC0), C0e = x.val(rC0e), Cp = x.val(rCp), Cpe = x.val(rCpe);
     double acc = 0.0;
     acc += lane_shift_or<false>(aDN1l, aDN1le) * lane_shift_or<false>(Am, Ame);  // (-1, -1, -1)
@@ -1472,10 +1529,10 @@ template <class MT, int KC, bool SPAN1, int UNI, class X, class EPI, class PRE =
 __device__ __forceinline__ void march_rows(const SellB1 &A, const MarchPlan &mp, i64 own, int lane, int wave,
                                            const X &x, EPI &epi, PRE &&pre = PRE{})
 {
-  static_assert(!UNI || SPAN1 || UNI == 12, "uniform-band march: far spans of at most one offset");
-  if constexpr (UNI == 12)
+  static_assert(!UNI || SPAN1 || UNI == 12 || UNI == 16, "uniform-band march: far spans of at most one offset");
+  if constexpr (UNI == 12 || UNI == 16)
   {
-    march_rows_kuhn(A, mp, own, lane, wave, x, epi, pre);
+    march_rows_kuhn<UNI == 16>(A, mp, own, lane, wave, x, epi, pre);
     return;
   }
   else if constexpr (UNI >= 3)
@@ -1620,7 +1677,7 @@ __device__ __forceinline__ void march_rows(const SellB1 &A, const MarchPlan &mp,
 
 // y[own + r] = (A x)[r] on the plane march (BCRSMatrix::mv; bitwise k_spmv_b1).
 // resident waves per SIMD of the eig_mv / K1 march kernels (the box march holds ~90 VGPRs)
-constexpr int march_mv_waves(int uni) { return uni == 12 ? 5 : 8; }
+constexpr int march_mv_waves(int uni) { return uni == 12 || uni == 16 ? 5 : 8; }
 
 template <class MT, bool SPAN1, int UNI>
 __global__ __launch_bounds__(kStreamThreads, march_mv_waves(UNI)) void k_spmv_march(i64 nrows, i64 own, SellB1 A, MarchPlan mp,
@@ -1678,7 +1735,7 @@ __global__ __launch_bounds__(kStreamThreads, march_mv_waves(UNI)) void k_lanczos
 // resident waves per SIMD the fused march kernels are built for (registers: no spills)
 constexpr int march_fused_waves(int uni)
 {
-  return uni == 12 ? 5 : uni == 11 ? 5 : uni == 10 || uni >= 13 ? 6 : uni == 6 || uni == 9 ? 4 : uni == 5 ? 5 : uni == 4 || uni == 8 ? 6
+  return uni == 16 ? 4 : uni == 12 ? 5 : uni == 11 ? 5 : uni == 10 || uni >= 13 ? 6 : uni == 6 || uni == 9 ? 4 : uni == 5 ? 5 : uni == 4 || uni == 8 ? 6
        : uni == 3 || uni == 7 ? 7 : uni ? 8 : 7;
 }
 
@@ -2157,10 +2214,35 @@ __global__ void k_sym_pack(i64 ld, const double *__restrict__ UD, const double *
     reinterpret_cast<dpair *>(out)[ld + w] = dpair{U1[w], Uq ? Uq[w] : 0.0};
   }
 }
+// Kuhn pack (march variant 16): four pair arrays, (0, +1), (+nx, +nx+1), (+D, +D+1), (+D+nx, +D+nx+1)
+__global__ void k_kuhn_pack(i64 ld, const double *__restrict__ val, int4 ja, int4 jb, double *__restrict__ out)
+{
+  const int j0[4] = {ja.x, ja.z, jb.x, jb.z}, j1[4] = {ja.y, ja.w, jb.y, jb.w};
+  for (i64 w = (i64)blockIdx.x * blockDim.x + threadIdx.x; w < ld; w += (i64)gridDim.x * blockDim.x)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      reinterpret_cast<dpair *>(out)[(i64)q * ld + w] = dpair{val[(i64)j0[q] * ld + w], val[(i64)j1[q] * ld + w]};
+}
+static bool march_kuhn(const eig_mat_s &A);
 const double *sym_pack_prepare(const eig_mat_s &Ac)
 {
   eig_mat_s &A = const_cast<eig_mat_s &>(Ac);
   if (A.sym_pack) return A.sym_pack;
+  if (A.sym_box27 == kKuhn15)
+  {
+    // band array of each upper Kuhn offset (the 27-box positions 13 14 | 16 17 | 22 23 | 25 26)
+    const i64 D = (i64)A.sym_gx * A.sym_gy;
+    int j[27];
+    for (int q = 0; q < 27; ++q) j[q] = 0;
+    for (int k = 0; k < A.sym_nd; ++k)
+      for (int q = 13; q < 27; ++q)
+        if ((i64)(q / 9 - 1) * D + (i64)((q / 3) % 3 - 1) * A.sym_gx + (q % 3 - 1) == A.sym_off[k]) j[q] = A.sym_dj[k];
+    EIG_HIP(hipMalloc(&A.sym_pack, (size_t)A.sym_ld * 64));
+    hipLaunchKernelGGL(k_kuhn_pack, dim3(2048), dim3(256), 0, A.ctx->stream, A.sym_ld, A.sym_val,
+                       make_int4(j[13], j[14], j[16], j[17]), make_int4(j[22], j[23], j[25], j[26]), A.sym_pack);
+    EIG_HIP(hipGetLastError());
+    return A.sym_pack;
+  }
   const SellB1 b = sell_b1(A);
   const SymImg &S = b.sym;
   const double *UD = S.val + (i64)S.dj[S.nd - 1] * S.ld, *U1 = S.val + (i64)S.j1 * S.ld;
@@ -2213,7 +2295,7 @@ static bool march_kuhn(const eig_mat_s &A)
 }
 static int march_uniform(const eig_mat_s &A, bool fused = false, i64 nplanes = 0)
 {
-  if (march_kuhn(A)) return 12;
+  if (march_kuhn(A)) return A.tune_march_prefetch == 14 ? 16 : 12;
   const bool geo2 = A.sym_geo && A.sym_gx % 64 == 0 && A.window * 16 < (i64(1) << 31);
   if (!A.sym_uniform || (A.kflags & EIG_MAT_NO_UNIFORM))
   {
@@ -2234,6 +2316,8 @@ static int march_uniform(const eig_mat_s &A, bool fused = false, i64 nplanes = 0
   do {                                                                                                    \
     if (mp.uni == 12)                                                                                     \
       hipLaunchKernelGGL((KERN<uint32_t, false, 12>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);     \
+    else if (mp.uni == 16)                                                                                \
+      hipLaunchKernelGGL((KERN<uint32_t, false, 16>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);     \
     else if ((MODE) == kSymN8 && march_span1(A) && mp.uni == 13)                                          \
       hipLaunchKernelGGL((KERN<uint8_t, true, 13>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);       \
     else if ((MODE) == kSymN8 && march_span1(A) && mp.uni == 14)                                          \
@@ -2365,7 +2449,7 @@ static MarchPlan march_plan(const eig_mat_s &A, int mode, i64 zb = 0, i64 ze = -
     mp.cq = khi < A.sym_nd - 1 ? A.sym_uc[A.sym_dj[khi]] : 0.0;
   }
   mp.uni = uni;
-  mp.pack = uni == 13 || uni == 15 ? sym_pack_prepare(A) : nullptr;
+  mp.pack = uni == 13 || uni == 15 || uni == 16 ? sym_pack_prepare(A) : nullptr;
   // measured (tools/march_copy.hip *_pp, profiles/r03bo_march_copy.jsonl): the step's ping-pong at
   // 128^3 (2 x 32 MB of pairs) 12.9 us with plain stores vs 17.6 us nontemporal; at 256^3 (2 x 268
   // MB) no difference either way -- plain stores where every vector a launch touches fits in half

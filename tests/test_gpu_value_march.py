@@ -224,15 +224,17 @@ def test_kuhn_box_march(ctx, kind, N):
     assert M.info.march_variant == -1
     assert np.array_equal(M.mv_host(x), ref)
     base = {f: eigmi.lanczos_run(M, 25, seed=7, fused=f)[:2] for f in (False, True)}
-    M.tune(march_prefetch=0)
-    for runs in (0, 1, 3, 7):
-        M.tune(runs)
-        assert np.array_equal(M.mv_host(x), ref), runs
-        for fused in (False, True):
-            a, b, _ = eigmi.lanczos_run(M, 25, seed=7, fused=fused)
-            assert np.allclose(a, base[fused][0], rtol=1e-12, atol=0) and \
-                np.allclose(b, base[fused][1], rtol=1e-12, atol=0), (runs, fused)
-    M.tune(0)
+    for pf in (0, 14):  # 14: the Kuhn pack (variant 16)
+        M.tune(march_prefetch=pf)
+        assert M.info.march_variant == (16 if pf else 12)
+        for runs in (0, 1, 3, 7):
+            M.tune(runs)
+            assert np.array_equal(M.mv_host(x), ref), (runs, pf)
+            for fused in (False, True):
+                a, b, _ = eigmi.lanczos_run(M, 25, seed=7, fused=fused)
+                assert np.allclose(a, base[fused][0], rtol=1e-12, atol=0) and \
+                    np.allclose(b, base[fused][1], rtol=1e-12, atol=0), (runs, pf, fused)
+    M.tune(0, march_prefetch=0)
     fa, fb, _ = eigmi.lanczos_run(M, 15, seed=123, fused=True)
     qa, qb = oracle.lanczos_fused(A, oracle.random_vec(n, 123), 15)
     assert np.allclose(fa, qa, rtol=1e-12, atol=0) and np.allclose(fb, qb, rtol=1e-12, atol=0)

@@ -21,7 +21,7 @@ step slab 200 python3 tools/lanczos_sweep.py --N 256 --slab 32 --matrix varcoef 
   --variants fused,fused#12,fused#11,fused#13,fused@4#13,mv,mv#13 > $O/slab.jsonl 2>> $O/sweep.err
 cat $O/slab.jsonl
 step p1k 300 python3 tools/lanczos_sweep.py --N 256 --matrix p1k --rounds 2 --steps 30 \
-  --variants fused@16,fused@24,fused@4,mv@16 > $O/p1k.jsonl 2>> $O/sweep.err
+  --variants fused@16,fused@24,fused@16#14,fused#14,mv@16,mv#14 > $O/p1k.jsonl 2>> $O/sweep.err
 cat $O/p1k.jsonl
 P="fused,fused#12,fused#13,mv#13"
 step ta 120 rocprofv3 --pmc TA_TA_BUSY_sum TA_BUSY_avr --output-format csv -d $O/pmc_ta -o pmc -- python3 tools/lanczos_sweep.py --N 256 --matrix varcoef --rounds 1 --steps 10 --variants $P > /dev/null 2> $O/pmc_ta.err
