@@ -529,7 +529,7 @@ extern "C" int eig_mat_tune(eig_mat_t A, int key, int value)
                   key == EIG_TUNE_HALO,
               EIG_ERR_ARG, "eig_mat_tune: unknown key");
     EIG_CHECK(key != EIG_TUNE_HALO || value <= 1, EIG_ERR_ARG, "eig_mat_tune: halo mode 0 / 1");
-    EIG_CHECK(key != EIG_TUNE_MARCH_PREFETCH || value <= 14, EIG_ERR_ARG, "eig_mat_tune: march variant 0..14");
+    EIG_CHECK(key != EIG_TUNE_MARCH_PREFETCH || value <= 15, EIG_ERR_ARG, "eig_mat_tune: march variant 0..15");
     if (key == EIG_TUNE_MARCH_RUNS)
       A->tune_march_runs = value;
     else if (key == EIG_TUNE_MARCH_PREFETCH)

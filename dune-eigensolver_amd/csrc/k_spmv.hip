@@ -1319,6 +1319,120 @@ __device__ __forceinline__ void march_rows_geo2(const SellB1 &A, const MarchPlan
            vs[VPF ? k & 1 : 0], vs[VPF ? (k + 1) & 1 : 1]);
 }
 
+// Patch value march (march variant 17; 3-D 7-point geometric bands, nx % 16 == 0, ny % 4 == 0):
+// what bounds the line march with streamed values is the per-CU vector-memory address path (TA busy
+// 81-88 % of the kernel, ~19 B per clock per CU: profiles/r04c_*), and a 64-row line wave moves 128 B
+// per row through it -- half of that the +-nx neighbour gathers, the edge loads and the mirrored -nx
+// value.  Here a wave owns a 16 x 4 patch (lane = x + 16 y) of every plane of its run: the y
+// neighbours of the inner lines and the row above's +nx value (= the row's mirrored -nx value) come
+// from the lanes 16 apart (ds_bpermute, not the TA), the x neighbours by DPP row shifts inside each
+// 16-lane row; only the patch's first / last line (one load: lanes y = 0 take row w - nx, lanes y = 3
+// row w + nx), its x edges (one load, 8 lanes) and lane row starts' -1 value touch memory besides the
+// row streams.  A missing neighbour (grid face) reads as an exact zero as in march_rows_geo2, so
+// each row's sum is the reference row loop's bit for bit; only the rows per wave (the fused step's
+// reduction order) differ from the line marches.
+__device__ __forceinline__ double lane_from_dbl(double v, int src_lane)
+{
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_ds_bpermute(src_lane << 2, (int)b);
+  const int hi = __builtin_amdgcn_ds_bpermute(src_lane << 2, (int)(b >> 32));
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+// DPP shift by one lane inside each 16-lane row (row_shr:1 / row_shl:1); a lane without a source in
+// its row keeps `old`
+template <bool NEXT>
+__device__ __forceinline__ double row_shift_or(double v, double old)
+{
+  return __builtin_amdgcn_update_dpp(old, v, NEXT ? 0x101 : 0x111, 0xf, 0xf, false);
+}
+template <class X, class EPI, class PRE>
+__device__ __forceinline__ void march_rows_patch(const SellB1 &A, const MarchPlan &mp, i64 own, int lane, int wave,
+                                                 X x, EPI &epi, PRE &pre)
+{
+  typedef typename X::raw raw;
+  constexpr unsigned SZ = sizeof(raw);
+  constexpr unsigned kOut = 0x80000000u;
+  const int D = (int)mp.D, own32 = (int)own, gx = mp.gx, gy = mp.gy;
+  const int item = (int)swizzled_block() * kWaves + wave;
+  if (item >= mp.ncol * mp.nseg) return;
+  const int col = item % mp.ncol, seg = item / mp.ncol;
+  const int z0 = (int)(mp.zb + seg * mp.nplanes / mp.nseg), z1 = (int)(mp.zb + (seg + 1) * mp.nplanes / mp.nseg);
+  const int npx = gx >> 4, px = col % npx, py = col / npx;
+  const int lx = lane & 15, ly = lane >> 4, x0 = px << 4, y0 = py << 2;
+  const unsigned nbytes = (unsigned)(A.xlast + 1) * SZ;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(x.ptr()), 0, (int)nbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t r0 = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(x.ptr()), 0, 0, 0x00020000);
+  int w = own32 + (y0 + ly) * gx + x0 + lx + z0 * D;
+  unsigned vo = (unsigned)w * SZ;
+  // y gather: lanes of the patch's first line take row w - nx, of its last line row w + nx (one load)
+  const unsigned oy = ly == 0 ? (y0 > 0 ? 0u - (unsigned)gx * SZ : kOut)
+                      : ly == 3 ? (y0 + 4 < gy ? (unsigned)gx * SZ : kOut) : kOut;
+  // x edges: lanes x = 0 take row w - 1, x = 15 row w + 1 (one load)
+  const unsigned ox = lx == 0 ? (x0 > 0 ? 0u - SZ : kOut) : lx == 15 ? (x0 + 16 < gx ? SZ : kOut) : kOut;
+  const unsigned Db = (unsigned)D * SZ;
+  const int zg0 = z0 + mp.gz0;
+  // values: the +D / 0 / +1 / +nx arrays (8-B slots, window-indexed)
+  const SymImg &S = A.sym;
+  const unsigned vbytes = (unsigned)S.ld * 8u;
+  auto arr = [&](int j) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(S.val + (i64)(j >= 0 ? j : 0) * S.ld), 0,
+                                             j >= 0 ? (int)vbytes : 0, 0x00020000);
+  };
+  const __amdgpu_buffer_rsrc_t vD = arr(S.dj[S.nd - 1]), v0 = arr(S.j0), v1 = arr(S.j1), vq = arr(S.dj[S.khi]);
+  const unsigned oyv = ly == 0 && y0 > 0 ? 0u - (unsigned)gx * 8u : kOut;  // the mirrored -nx value, first line
+  const unsigned oxv = lx == 0 && x0 > 0 ? 0u - 8u : kOut;                   // the mirrored -1 value, x = 0
+  unsigned vv = (unsigned)w * 8u;
+  const int up_lane = (lane - 16) & 63, dn_lane = (lane + 16) & 63;
+  auto ld8 = [&](__amdgpu_buffer_rsrc_t r, unsigned o) {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (int)o, 0, 0));
+  };
+  auto ld8nt = [&](__amdgpu_buffer_rsrc_t r, unsigned o) {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (int)o, 0, 2));
+  };
+  raw pm{}, pcur;
+  double amD = 0.0;
+  if (zg0 > 0)
+  {
+    bload(rs, vo - Db, pm);
+    amD = ld8(vD, vv - (unsigned)D * 8u);
+  }
+  bload(rs, vo, pcur);
+  if (!pre(x)) return;
+  double pmv = zg0 > 0 ? x.val(pm) : 0.0;
+  for (int z = z0; z < z1; ++z)
+  {
+    const int zg = z + mp.gz0;
+    raw ey, ex, pd;
+    bload(rs, vo + oy, ey);
+    bload(rs, vo + ox, ex);
+    bload(zg + 1 < mp.gz ? rs : r0, vo + Db, pd);
+    const double aD = ld8nt(vD, vv), a0 = ld8nt(v0, vv), ap = ld8nt(v1, vv), aq = ld8(vq, vv);
+    const double ayv = ld8(vq, vv + oyv), axv = ld8(v1, vv + oxv);
+    const double vc = x.val(pcur), vyg = x.val(ey), vxe = x.val(ex);
+    // y neighbours: the lanes 16 apart, the gathered row on the patch's first / last line
+    const double vun = lane_from_dbl(vc, up_lane), vdn = lane_from_dbl(vc, dn_lane);
+    const double vn = ly == 0 ? vyg : vun, vq2 = ly == 3 ? vyg : vdn;
+    const double an = ly == 0 ? ayv : lane_from_dbl(aq, up_lane);  // a(w, w - nx) = a_{+nx}(w - nx)
+    const double vl = row_shift_or<false>(vc, vxe), vr = row_shift_or<true>(vc, vxe);
+    const double am = row_shift_or<false>(ap, axv);                // a(w, w - 1) = a_{+1}(w - 1)
+    double acc = 0.0;
+    acc += amD * pmv;
+    acc += an * vn;
+    acc += am * vl;
+    acc += a0 * vc;
+    acc += ap * vr;
+    acc += aq * vq2;
+    acc += aD * x.val(pd);
+    epi(w - own32, w, acc, pcur);
+    pmv = vc;
+    amD = aD;
+    pcur = pd;
+    w += D;
+    vo += Db;
+    vv += (unsigned)D * 8u;
+  }
+}
+
 // Box march for the P1 Kuhn 15-point stencil (march variant 12; config C5's K and M, any values): the
 // band's offsets are a D + b nx + c with (a, b, c) in the Kuhn edge set {0, +-e_i, +-(e_i + e_j),
 // +-(1, 1, 1)} and every row stores exactly its in-grid neighbours among them (eig_mat_s::sym_box27,
@@ -1535,6 +1649,11 @@ __device__ __forceinline__ void march_rows(const SellB1 &A, const MarchPlan &mp,
     march_rows_kuhn<UNI == 16>(A, mp, own, lane, wave, x, epi, pre);
     return;
   }
+  else if constexpr (UNI == 17)
+  {
+    march_rows_patch(A, mp, own, lane, wave, x, epi, pre);
+    return;
+  }
   else if constexpr (UNI >= 3)
   {
     // 3, 4, 5: +D operand 1, 2, 3 planes ahead; 6: 3 planes ahead and the gathers one plane ahead
@@ -1735,7 +1854,7 @@ __global__ __launch_bounds__(kStreamThreads, march_mv_waves(UNI)) void k_lanczos
 // resident waves per SIMD the fused march kernels are built for (registers: no spills)
 constexpr int march_fused_waves(int uni)
 {
-  return uni == 16 ? 4 : uni == 12 ? 5 : uni == 11 ? 5 : uni == 10 || uni >= 13 ? 6 : uni == 6 || uni == 9 ? 4 : uni == 5 ? 5 : uni == 4 || uni == 8 ? 6
+  return uni == 16 ? 4 : uni == 17 ? 7 : uni == 12 ? 5 : uni == 11 ? 5 : uni == 10 || uni >= 13 ? 6 : uni == 6 || uni == 9 ? 4 : uni == 5 ? 5 : uni == 4 || uni == 8 ? 6
        : uni == 3 || uni == 7 ? 7 : uni ? 8 : 7;
 }
 
@@ -2301,7 +2420,9 @@ static int march_uniform(const eig_mat_s &A, bool fused = false, i64 nplanes = 0
   {
     if (!geo2 || !march_span1(A) || A.sym_ld * 32 >= (i64(1) << 31) || A.tune_march_prefetch == 1) return 0;
     const int tp = A.tune_march_prefetch;
-    return tp == 10 ? 11 : tp == 11 ? 13 : tp == 12 ? 14 : tp == 13 ? 15 : 10;
+    // the patch march: 3-D 7-point grids tiling into 16 x 4 patches
+    const bool patch = A.sym_nd == 7 && A.sym_gx % 16 == 0 && A.sym_gy % 4 == 0;
+    return tp == 10 ? 11 : tp == 11 ? 13 : tp == 12 ? 14 : tp == 13 ? 15 : tp == 15 && patch ? 17 : 10;
   }
   if (!A.sym_geo) return 1;
   int u = A.tune_march_prefetch > 0 ? 1 + A.tune_march_prefetch : geo2 ? 7 : 4;
@@ -2324,6 +2445,8 @@ static int march_uniform(const eig_mat_s &A, bool fused = false, i64 nplanes = 0
       hipLaunchKernelGGL((KERN<uint8_t, true, 14>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);       \
     else if ((MODE) == kSymN8 && march_span1(A) && mp.uni == 15)                                          \
       hipLaunchKernelGGL((KERN<uint8_t, true, 15>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);       \
+    else if ((MODE) == kSymN8 && march_span1(A) && mp.uni == 17)                                          \
+      hipLaunchKernelGGL((KERN<uint8_t, true, 17>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);       \
     else if ((MODE) == kSymN8 && march_span1(A) && mp.uni == 11)                                          \
       hipLaunchKernelGGL((KERN<uint8_t, true, 11>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);       \
     else if ((MODE) == kSymN8 && march_span1(A) && mp.uni == 10)                                          \

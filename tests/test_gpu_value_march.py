@@ -106,15 +106,21 @@ def test_value_march_bitwise(ctx, mat):
     ref = oracle.csr_mv(A, x)
     for runs in (0, 1, 2, 3, 5, 7):
         base = {}
-        # 1: the plain masked march on the arrays; 9 / 10 / 11: variants 10 / 11 / 13 (13: packed image)
-        for pf in (1, 9, 10, 11, 12, 13):
+        # 1: the plain masked march on the arrays; 9 / 10 / 11 / 12 / 13: variants 10 / 11 / 13 / 14 / 15
+        # (the same rows per wave: alpha / beta bitwise); 15: the 16 x 4 patch march (variant 17 where the
+        # grid tiles into patches; other rows per wave, so alpha / beta to rounding)
+        patch = A.n % 64 == 0 and mat != "box128x3x9"
+        for pf in (1, 9, 10, 11, 12, 13, 15):
             M.tune(runs, march_prefetch=pf)
-            assert M.info.march_variant == {1: 0, 9: 10, 10: 11, 11: 13, 12: 14, 13: 15}[pf]
+            assert M.info.march_variant == {1: 0, 9: 10, 10: 11, 11: 13, 12: 14, 13: 15, 15: 17 if patch else 10}[pf]
             assert np.array_equal(M.mv_host(x), ref), (runs, pf)
             for fused in (False, True):
                 a, b, _ = eigmi.lanczos_run(M, 25, seed=7, fused=fused)
                 if pf == 1:
                     base[fused] = (a, b)
+                elif pf == 15 and patch:
+                    assert np.allclose(a, base[fused][0], rtol=1e-12, atol=0) and \
+                        np.allclose(b, base[fused][1], rtol=1e-12, atol=0), (runs, pf, fused)
                 else:
                     assert np.array_equal(a, base[fused][0]) and np.array_equal(b, base[fused][1]), (runs, pf, fused)
     M.tune(0, march_prefetch=0)
