@@ -154,6 +154,10 @@ def image_name(M):
     v = info.march_variant
     if info.sym_offsets == 0:
         return "SELL-64 / CSR image (values + column structure: stencil slices keep offsets + a 1-B row mask)"
+    if v == 15:
+        return ("symmetric band values streamed every step as two pair arrays ((+D, 0) and (+1, +nx) per row: "
+                "the 4 upper diagonals, 32 B per row; lower entries through the mirrored slots; row masks from "
+                "the grid coordinates; the (t, u) pairs streamed)")
     if v >= 10:
         return (f"symmetric band arrays streamed every step ({info.sym_arrays} upper diagonals, "
                 f"{8 * info.sym_arrays} B per row; lower entries through the mirrored slots; row masks from "

@@ -1387,6 +1387,7 @@ extern "C" int eig_mat_get_info(eig_mat_t A, eig_mat_info *info)
                             : 0;
     info->sym_geo = A->sym_val && A->sym_geo ? 1 : 0;
     info->march_variant = march_variant(*A, true);
+    info->march_variant_mv = march_variant(*A, false);
   });
 }
 

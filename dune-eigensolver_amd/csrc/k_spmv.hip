@@ -1183,32 +1183,10 @@ __device__ __forceinline__ void march_rows_geo2(const SellB1 &A, const MarchPlan
     double aD, a0, ap, aq, an, ae;
   };
   const __amdgpu_buffer_rsrc_t vz = arr(0, false);
-  // VAL 3: the packed image (eig_mat_s::sym_pack: per row {+D, 0, +1, +nx} = 32 B, two 16-B loads; the
-  // mirrored -nx / -1 values from the (+1, +nx) half of rows w - nx / w - 1)
-  const __amdgpu_buffer_rsrc_t pk = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<double *>(mp.pack ? mp.pack : S.val), 0, VAL == 3 && mp.pack ? (int)(4u * vbytes) : 0, 0x00020000);
-  const __amdgpu_buffer_rsrc_t pkn = VAL == 3 && mp.dn && yw > 0 ? pk : vz;
   const double *pD = S.val + (i64)S.dj[S.nd - 1] * S.ld, *p1 = S.val + (i64)(S.j1 >= 0 ? S.j1 : 0) * S.ld;
   const double *p0 = S.j0 >= 0 ? S.val + (i64)S.j0 * S.ld : nullptr, *pq = S.val + (i64)S.dj[S.khi] * S.ld;
   auto vload = [&](unsigned o, Vals &v, bool on) {  // on: wave-uniform (false: zeros, no traffic)
-    if constexpr (VAL == 3)
-    {
-      // (byte offsets: (+D, 0) at 16 w, (+1, +nx) at 16 (ld + w))
-      const dpair p0 = __builtin_bit_cast(dpair, __builtin_amdgcn_raw_buffer_load_b128(pk, (int)(2 * o), 0, 2));
-      const dpair p1 = __builtin_bit_cast(dpair, __builtin_amdgcn_raw_buffer_load_b128(pk, (int)(2 * o + 2 * vbytes), 0, 0));
-      const dpair pn =
-          __builtin_bit_cast(dpair, __builtin_amdgcn_raw_buffer_load_b128(pkn, (int)(2 * (o + dnv) + 2 * vbytes), 0, 0));
-      // (lane 0's edge row w - 1; the other lanes, and lane 0 at x = 0, an out-of-range offset)
-      const unsigned peo = eov == kOut ? kOut : 2 * o - 16 + 2 * vbytes;
-      const dpair pe = __builtin_bit_cast(dpair, __builtin_amdgcn_raw_buffer_load_b128(pk, (int)peo, 0, 0));
-      v.aD = p0.x;
-      v.a0 = p0.y;
-      v.ap = p1.x;
-      v.aq = mp.dq ? p1.y : 0.0;
-      v.an = pn.y;
-      v.ae = pe.x;
-    }
-    else if constexpr (VAL == 5)
+    if constexpr (VAL == 5)
     {
       // variant 15: the pack through 64-bit global addresses (wave-uniform / lane-0 conditions
       // instead of range-checked descriptors)
@@ -1267,7 +1245,7 @@ __device__ __forceinline__ void march_rows_geo2(const SellB1 &A, const MarchPlan
       gather(vo + Db, gn);
     else
       gather(vo, gc);
-    if constexpr (VAL == 1 || VAL >= 3) vload(vv, vc_, true);
+    if constexpr (VAL == 1 || VAL >= 4) vload(vv, vc_, true);
     const int zg = z + mp.gz0;
     bload(zg + PF + 1 < mp.gz ? rs : r0, vo + (unsigned)(PF + 1) * Db, pf);
     if constexpr (VPF) vload(vv + Dv, vn_, z + 1 < z1);
@@ -1317,120 +1295,6 @@ __device__ __forceinline__ void march_rows_geo2(const SellB1 &A, const MarchPlan
     if (z + k < z1)
       body(z + k, sl[k], sl[(k + 1) % NS], sl[(k + PF + 1) % NS], gs[PG ? k & 1 : 0], gs[PG ? (k + 1) & 1 : 1],
            vs[VPF ? k & 1 : 0], vs[VPF ? (k + 1) & 1 : 1]);
-}
-
-// Patch value march (march variant 17; 3-D 7-point geometric bands, nx % 16 == 0, ny % 4 == 0):
-// what bounds the line march with streamed values is the per-CU vector-memory address path (TA busy
-// 81-88 % of the kernel, ~19 B per clock per CU: profiles/r04c_*), and a 64-row line wave moves 128 B
-// per row through it -- half of that the +-nx neighbour gathers, the edge loads and the mirrored -nx
-// value.  Here a wave owns a 16 x 4 patch (lane = x + 16 y) of every plane of its run: the y
-// neighbours of the inner lines and the row above's +nx value (= the row's mirrored -nx value) come
-// from the lanes 16 apart (ds_bpermute, not the TA), the x neighbours by DPP row shifts inside each
-// 16-lane row; only the patch's first / last line (one load: lanes y = 0 take row w - nx, lanes y = 3
-// row w + nx), its x edges (one load, 8 lanes) and lane row starts' -1 value touch memory besides the
-// row streams.  A missing neighbour (grid face) reads as an exact zero as in march_rows_geo2, so
-// each row's sum is the reference row loop's bit for bit; only the rows per wave (the fused step's
-// reduction order) differ from the line marches.
-__device__ __forceinline__ double lane_from_dbl(double v, int src_lane)
-{
-  const long long b = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_ds_bpermute(src_lane << 2, (int)b);
-  const int hi = __builtin_amdgcn_ds_bpermute(src_lane << 2, (int)(b >> 32));
-  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-}
-// DPP shift by one lane inside each 16-lane row (row_shr:1 / row_shl:1); a lane without a source in
-// its row keeps `old`
-template <bool NEXT>
-__device__ __forceinline__ double row_shift_or(double v, double old)
-{
-  return __builtin_amdgcn_update_dpp(old, v, NEXT ? 0x101 : 0x111, 0xf, 0xf, false);
-}
-template <class X, class EPI, class PRE>
-__device__ __forceinline__ void march_rows_patch(const SellB1 &A, const MarchPlan &mp, i64 own, int lane, int wave,
-                                                 X x, EPI &epi, PRE &pre)
-{
-  typedef typename X::raw raw;
-  constexpr unsigned SZ = sizeof(raw);
-  constexpr unsigned kOut = 0x80000000u;
-  const int D = (int)mp.D, own32 = (int)own, gx = mp.gx, gy = mp.gy;
-  const int item = (int)swizzled_block() * kWaves + wave;
-  if (item >= mp.ncol * mp.nseg) return;
-  const int col = item % mp.ncol, seg = item / mp.ncol;
-  const int z0 = (int)(mp.zb + seg * mp.nplanes / mp.nseg), z1 = (int)(mp.zb + (seg + 1) * mp.nplanes / mp.nseg);
-  const int npx = gx >> 4, px = col % npx, py = col / npx;
-  const int lx = lane & 15, ly = lane >> 4, x0 = px << 4, y0 = py << 2;
-  const unsigned nbytes = (unsigned)(A.xlast + 1) * SZ;
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(x.ptr()), 0, (int)nbytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t r0 = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(x.ptr()), 0, 0, 0x00020000);
-  int w = own32 + (y0 + ly) * gx + x0 + lx + z0 * D;
-  unsigned vo = (unsigned)w * SZ;
-  // y gather: lanes of the patch's first line take row w - nx, of its last line row w + nx (one load)
-  const unsigned oy = ly == 0 ? (y0 > 0 ? 0u - (unsigned)gx * SZ : kOut)
-                      : ly == 3 ? (y0 + 4 < gy ? (unsigned)gx * SZ : kOut) : kOut;
-  // x edges: lanes x = 0 take row w - 1, x = 15 row w + 1 (one load)
-  const unsigned ox = lx == 0 ? (x0 > 0 ? 0u - SZ : kOut) : lx == 15 ? (x0 + 16 < gx ? SZ : kOut) : kOut;
-  const unsigned Db = (unsigned)D * SZ;
-  const int zg0 = z0 + mp.gz0;
-  // values: the +D / 0 / +1 / +nx arrays (8-B slots, window-indexed)
-  const SymImg &S = A.sym;
-  const unsigned vbytes = (unsigned)S.ld * 8u;
-  auto arr = [&](int j) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(S.val + (i64)(j >= 0 ? j : 0) * S.ld), 0,
-                                             j >= 0 ? (int)vbytes : 0, 0x00020000);
-  };
-  const __amdgpu_buffer_rsrc_t vD = arr(S.dj[S.nd - 1]), v0 = arr(S.j0), v1 = arr(S.j1), vq = arr(S.dj[S.khi]);
-  const unsigned oyv = ly == 0 && y0 > 0 ? 0u - (unsigned)gx * 8u : kOut;  // the mirrored -nx value, first line
-  const unsigned oxv = lx == 0 && x0 > 0 ? 0u - 8u : kOut;                   // the mirrored -1 value, x = 0
-  unsigned vv = (unsigned)w * 8u;
-  const int up_lane = (lane - 16) & 63, dn_lane = (lane + 16) & 63;
-  auto ld8 = [&](__amdgpu_buffer_rsrc_t r, unsigned o) {
-    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (int)o, 0, 0));
-  };
-  auto ld8nt = [&](__amdgpu_buffer_rsrc_t r, unsigned o) {
-    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (int)o, 0, 2));
-  };
-  raw pm{}, pcur;
-  double amD = 0.0;
-  if (zg0 > 0)
-  {
-    bload(rs, vo - Db, pm);
-    amD = ld8(vD, vv - (unsigned)D * 8u);
-  }
-  bload(rs, vo, pcur);
-  if (!pre(x)) return;
-  double pmv = zg0 > 0 ? x.val(pm) : 0.0;
-  for (int z = z0; z < z1; ++z)
-  {
-    const int zg = z + mp.gz0;
-    raw ey, ex, pd;
-    bload(rs, vo + oy, ey);
-    bload(rs, vo + ox, ex);
-    bload(zg + 1 < mp.gz ? rs : r0, vo + Db, pd);
-    const double aD = ld8nt(vD, vv), a0 = ld8nt(v0, vv), ap = ld8nt(v1, vv), aq = ld8(vq, vv);
-    const double ayv = ld8(vq, vv + oyv), axv = ld8(v1, vv + oxv);
-    const double vc = x.val(pcur), vyg = x.val(ey), vxe = x.val(ex);
-    // y neighbours: the lanes 16 apart, the gathered row on the patch's first / last line
-    const double vun = lane_from_dbl(vc, up_lane), vdn = lane_from_dbl(vc, dn_lane);
-    const double vn = ly == 0 ? vyg : vun, vq2 = ly == 3 ? vyg : vdn;
-    const double an = ly == 0 ? ayv : lane_from_dbl(aq, up_lane);  // a(w, w - nx) = a_{+nx}(w - nx)
-    const double vl = row_shift_or<false>(vc, vxe), vr = row_shift_or<true>(vc, vxe);
-    const double am = row_shift_or<false>(ap, axv);                // a(w, w - 1) = a_{+1}(w - 1)
-    double acc = 0.0;
-    acc += amD * pmv;
-    acc += an * vn;
-    acc += am * vl;
-    acc += a0 * vc;
-    acc += ap * vr;
-    acc += aq * vq2;
-    acc += aD * x.val(pd);
-    epi(w - own32, w, acc, pcur);
-    pmv = vc;
-    amD = aD;
-    pcur = pd;
-    w += D;
-    vo += Db;
-    vv += (unsigned)D * 8u;
-  }
 }
 
 // Box march for the P1 Kuhn 15-point stencil (march variant 12; config C5's K and M, any values): the
@@ -1649,16 +1513,12 @@ __device__ __forceinline__ void march_rows(const SellB1 &A, const MarchPlan &mp,
     march_rows_kuhn<UNI == 16>(A, mp, own, lane, wave, x, epi, pre);
     return;
   }
-  else if constexpr (UNI == 17)
-  {
-    march_rows_patch(A, mp, own, lane, wave, x, epi, pre);
-    return;
-  }
+
   else if constexpr (UNI >= 3)
   {
     // 3, 4, 5: +D operand 1, 2, 3 planes ahead; 6: 3 planes ahead and the gathers one plane ahead
     if constexpr (UNI >= 10)  // 10, 11: the value march (band arrays streamed), 11 one plane ahead, 13 packed
-      march_rows_geo2<0, false, UNI == 13 ? 3 : UNI == 14 ? 4 : UNI == 15 ? 5 : UNI - 9>(A, mp, own, lane, wave, x, epi, pre);
+      march_rows_geo2<0, false, UNI == 14 ? 4 : UNI == 15 ? 5 : UNI - 9>(A, mp, own, lane, wave, x, epi, pre);
     else if constexpr (UNI >= 7)  // 7, 8, 9: march_rows_geo2 with the prefetches of 3, 4, 6
       march_rows_geo2<UNI == 9 ? 2 : UNI - 7, UNI == 9, 0>(A, mp, own, lane, wave, x, epi, pre);
     else
@@ -1854,7 +1714,7 @@ __global__ __launch_bounds__(kStreamThreads, march_mv_waves(UNI)) void k_lanczos
 // resident waves per SIMD the fused march kernels are built for (registers: no spills)
 constexpr int march_fused_waves(int uni)
 {
-  return uni == 16 ? 4 : uni == 17 ? 7 : uni == 12 ? 5 : uni == 11 ? 5 : uni == 10 || uni >= 13 ? 6 : uni == 6 || uni == 9 ? 4 : uni == 5 ? 5 : uni == 4 || uni == 8 ? 6
+  return uni == 16 ? 4 : uni == 12 ? 5 : uni == 11 ? 5 : uni == 10 || uni >= 13 ? 6 : uni == 6 || uni == 9 ? 4 : uni == 5 ? 5 : uni == 4 || uni == 8 ? 6
        : uni == 3 || uni == 7 ? 7 : uni ? 8 : 7;
 }
 
@@ -2414,15 +2274,18 @@ static bool march_kuhn(const eig_mat_s &A)
 }
 static int march_uniform(const eig_mat_s &A, bool fused = false, i64 nplanes = 0)
 {
-  if (march_kuhn(A)) return A.tune_march_prefetch == 14 ? 16 : 12;
+  // the Kuhn march on its value pack (16) by default: fused step 256^3 346 us, eig_mv 292 us (the arrays,
+  // 12: 407 / 330 us; profiles/r04d_p1k.jsonl); tune value 14 = the arrays
+  if (march_kuhn(A)) return A.tune_march_prefetch == 14 ? 12 : 16;
   const bool geo2 = A.sym_geo && A.sym_gx % 64 == 0 && A.window * 16 < (i64(1) << 31);
   if (!A.sym_uniform || (A.kflags & EIG_MAT_NO_UNIFORM))
   {
     if (!geo2 || !march_span1(A) || A.sym_ld * 32 >= (i64(1) << 31) || A.tune_march_prefetch == 1) return 0;
+    // automatic: the fused step on the value pack (15: 223.7 us at 256^3, one rank's 256^2 x 32 slab
+    // 30.4 us; the arrays 226.8 / 31.7), eig_mv / K1 on the plain masked march (0: 152.1 us against 161.4 on
+    // the pack): profiles/r04d_latency.jsonl, r04d_slab.jsonl
     const int tp = A.tune_march_prefetch;
-    // the patch march: 3-D 7-point grids tiling into 16 x 4 patches
-    const bool patch = A.sym_nd == 7 && A.sym_gx % 16 == 0 && A.sym_gy % 4 == 0;
-    return tp == 10 ? 11 : tp == 11 ? 13 : tp == 12 ? 14 : tp == 13 ? 15 : tp == 15 && patch ? 17 : 10;
+    return tp == 9 ? 10 : tp == 10 ? 11 : tp == 12 ? 14 : tp == 13 ? 15 : fused ? (A.sym_nd == 7 ? 15 : 10) : 0;
   }
   if (!A.sym_geo) return 1;
   int u = A.tune_march_prefetch > 0 ? 1 + A.tune_march_prefetch : geo2 ? 7 : 4;
@@ -2439,14 +2302,10 @@ static int march_uniform(const eig_mat_s &A, bool fused = false, i64 nplanes = 0
       hipLaunchKernelGGL((KERN<uint32_t, false, 12>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);     \
     else if (mp.uni == 16)                                                                                \
       hipLaunchKernelGGL((KERN<uint32_t, false, 16>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);     \
-    else if ((MODE) == kSymN8 && march_span1(A) && mp.uni == 13)                                          \
-      hipLaunchKernelGGL((KERN<uint8_t, true, 13>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);       \
     else if ((MODE) == kSymN8 && march_span1(A) && mp.uni == 14)                                          \
       hipLaunchKernelGGL((KERN<uint8_t, true, 14>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);       \
     else if ((MODE) == kSymN8 && march_span1(A) && mp.uni == 15)                                          \
       hipLaunchKernelGGL((KERN<uint8_t, true, 15>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);       \
-    else if ((MODE) == kSymN8 && march_span1(A) && mp.uni == 17)                                          \
-      hipLaunchKernelGGL((KERN<uint8_t, true, 17>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);       \
     else if ((MODE) == kSymN8 && march_span1(A) && mp.uni == 11)                                          \
       hipLaunchKernelGGL((KERN<uint8_t, true, 11>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);       \
     else if ((MODE) == kSymN8 && march_span1(A) && mp.uni == 10)                                          \
@@ -2572,7 +2431,7 @@ static MarchPlan march_plan(const eig_mat_s &A, int mode, i64 zb = 0, i64 ze = -
     mp.cq = khi < A.sym_nd - 1 ? A.sym_uc[A.sym_dj[khi]] : 0.0;
   }
   mp.uni = uni;
-  mp.pack = uni == 13 || uni == 15 || uni == 16 ? sym_pack_prepare(A) : nullptr;
+  mp.pack = uni == 15 || uni == 16 ? sym_pack_prepare(A) : nullptr;
   // measured (tools/march_copy.hip *_pp, profiles/r03bo_march_copy.jsonl): the step's ping-pong at
   // 128^3 (2 x 32 MB of pairs) 12.9 us with plain stores vs 17.6 us nontemporal; at 256^3 (2 x 268
   // MB) no difference either way -- plain stores where every vector a launch touches fits in half
@@ -2888,9 +2747,9 @@ void lanczos_kernel_info(const eig_mat_s &A, bool fused, std::string &name, i64 
                              : march_split_active(A);
     // the uniform-band march streams the row mask and the vectors only; the value march (10, 11)
     // the band arrays and the vectors (geometric masks: no mask stream)
-    const int mv = march && ((mode == kSymN8 && march_span1(A)) || march_kuhn(A)) ? march_uniform(A) : 0;
+    const int mv = march && ((mode == kSymN8 && march_span1(A)) || march_kuhn(A)) ? march_uniform(A, fused) : 0;
     if (mv >= 10)
-      bytes = 8 * (mv == 13 || mv == 15 ? 4 : (i64)A.sym_nup) * n + vec;
+      bytes = 8 * (mv == 15 ? 4 : (i64)A.sym_nup) * n + vec;
     else if (mv)
       bytes = (mv >= 2 ? 0 : (i64)A.sym_mask_bytes * n) + vec;
     name = fused ? (march ? "k_lanczos_fused_march" : "k_lanczos_fused_b1")

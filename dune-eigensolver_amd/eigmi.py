@@ -63,7 +63,7 @@ class _MatInfo(ctypes.Structure):
                [(k, ctypes.c_int64) for k in ("halo_recv", "halo_send", "device_bytes", "stencil_slices",
                                               "rows_per_lane", "sym_offsets", "sym_arrays",
                                               "sym_mask_bytes", "sym_uniform", "sym_geo",
-                                              "march_variant")]
+                                              "march_variant", "march_variant_mv")]
 
 
 class BlockTiming(ctypes.Structure):
@@ -1016,9 +1016,9 @@ def image_bytes(M, op, m=8):
     mat = (8 * info.sym_arrays + info.sym_mask_bytes) * n if band else 12 * nnz + 4 * (n + 1)
     if op == "spmv":
         if band and M.kernel("spmv") == "k_spmv_march":
-            v = info.march_variant
-            if v >= 10:  # the value march: band arrays streamed, geometric masks (no mask stream)
-                return 8 * info.sym_arrays * n + 16 * n
+            v = info.march_variant_mv
+            if v >= 10:  # the value marches: band values streamed, geometric masks (no mask stream)
+                return 8 * (4 if v == 15 else info.sym_arrays) * n + 16 * n
             if v >= 1:
                 # uniform band: the values ride in the arguments (2..9: the row masks are geometric too)
                 return (0 if v >= 2 else info.sym_mask_bytes * n) + 16 * n

@@ -186,7 +186,10 @@ typedef struct eig_mat_info {
   int64_t march_variant;  /* plane-march variant of a whole-matrix fused Lanczos launch (-1: no
                              march, the row kernels): 0 band arrays + loaded masks, 1 uniform values +
                              loaded masks, 2..9 uniform values + geometric masks, 10 / 11 band arrays
-                             streamed + geometric masks (the value march; 11 one plane ahead) */
+                             streamed + geometric masks (the value march; 11 one plane ahead, 14 / 15
+                             through global addresses, 15 on a pair-packed copy of the arrays), 12 / 16
+                             the P1 Kuhn 15-point box march (16 on its pair-packed values) */
+  int64_t march_variant_mv; /* the same for eig_mv (BCRSMatrix::mv) */
 } eig_mat_info;
 int eig_mat_get_info(eig_mat_t mat, eig_mat_info *info);
 

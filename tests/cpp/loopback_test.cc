@@ -89,7 +89,7 @@ static void fused_repair_run(eig_mat_t A, double *a, double *be, int *launches, 
   CK(eig_lanczos_destroy(ws));
 }
 
-// Value-streaming images (k_spmv.hip march variants 10 / 11 where the grid allows) and the uniform-
+// Value-streaming images (k_spmv.hip march variant 15 where the grid allows) and the uniform-
 // band check across rank interfaces: (a) the variable-coefficient 7-point matrix (eig_gen kind 8);
 // (b) the Poisson matrix whose z couplings across plane pz (rows of planes pz - 1 / pz, both mirror
 // entries) are -2: every rank's own upper entries are still one constant per diagonal, but the
@@ -200,9 +200,9 @@ static int value_images(int P, int N, const std::vector<double> &x)
         std::printf("FAIL %s rank %d: sym_uniform %lld, expected 0\n", nm, r, (long long)out[r].uniform);
         ++failures;
       }
-      if (cs == 0 && N % 64 == 0 && out[r].variant != 10 && out[r].variant != -1)
+      if (cs == 0 && N % 64 == 0 && out[r].variant != 15 && out[r].variant != -1)
       {
-        std::printf("FAIL %s rank %d: march variant %lld, expected the value march (10)\n", nm, r,
+        std::printf("FAIL %s rank %d: march variant %lld, expected the value march (15)\n", nm, r,
                     (long long)out[r].variant);
         ++failures;
       }

@@ -98,29 +98,25 @@ def test_value_march_bitwise(ctx, mat):
     A, flags = MATS[mat]()
     M = eigmi.Matrix.from_bcsr(ctx, A.rowptr, A.col, A.val, flags=flags)
     info = M.info
-    assert info.sym_geo == 1 and info.sym_uniform == 0 and info.march_variant == 10
+    # automatic: the fused step on the value pack (15), eig_mv on the plain masked march (0)
+    assert info.sym_geo == 1 and info.sym_uniform == 0 and info.march_variant == 15 and info.march_variant_mv == 0
     n = A.n
-    assert M.lanczos_kernel_info(True) == ("k_lanczos_fused_march", 8 * info.sym_arrays * n + 32 * n)
-    assert eigmi.image_bytes(M, "spmv") == 8 * info.sym_arrays * n + 16 * n
+    assert M.lanczos_kernel_info(True) == ("k_lanczos_fused_march", 8 * 4 * n + 32 * n)
+    assert eigmi.image_bytes(M, "spmv") == 8 * info.sym_arrays * n + n + 16 * n
     x = np.random.default_rng(11).standard_normal(n)
     ref = oracle.csr_mv(A, x)
     for runs in (0, 1, 2, 3, 5, 7):
         base = {}
-        # 1: the plain masked march on the arrays; 9 / 10 / 11 / 12 / 13: variants 10 / 11 / 13 / 14 / 15
-        # (the same rows per wave: alpha / beta bitwise); 15: the 16 x 4 patch march (variant 17 where the
-        # grid tiles into patches; other rows per wave, so alpha / beta to rounding)
-        patch = A.n % 64 == 0 and mat != "box128x3x9"
-        for pf in (1, 9, 10, 11, 12, 13, 15):
+        # 1: the plain masked march on the arrays; 9 / 10 / 12 / 13: variants 10 / 11 / 14 / 15 (the same
+        # rows per wave: alpha / beta bitwise)
+        for pf in (1, 9, 10, 12, 13):
             M.tune(runs, march_prefetch=pf)
-            assert M.info.march_variant == {1: 0, 9: 10, 10: 11, 11: 13, 12: 14, 13: 15, 15: 17 if patch else 10}[pf]
+            assert M.info.march_variant == {1: 0, 9: 10, 10: 11, 12: 14, 13: 15}[pf]
             assert np.array_equal(M.mv_host(x), ref), (runs, pf)
             for fused in (False, True):
                 a, b, _ = eigmi.lanczos_run(M, 25, seed=7, fused=fused)
                 if pf == 1:
                     base[fused] = (a, b)
-                elif pf == 15 and patch:
-                    assert np.allclose(a, base[fused][0], rtol=1e-12, atol=0) and \
-                        np.allclose(b, base[fused][1], rtol=1e-12, atol=0), (runs, pf, fused)
                 else:
                     assert np.array_equal(a, base[fused][0]) and np.array_equal(b, base[fused][1]), (runs, pf, fused)
     M.tune(0, march_prefetch=0)
@@ -134,21 +130,29 @@ def test_value_march_bitwise(ctx, mat):
 
 @pytest.mark.gpu
 def test_value_march_after_shift(ctx):
-    """A += sigma I updates the band arrays the value march streams (StandardLargest's shift,
-    eigensolver.hh:59-66): eig_mv bitwise the shifted reference matrix."""
+    """A += sigma I updates the band values the value marches stream (StandardLargest's shift,
+    eigensolver.hh:59-66), the value pack included (built at first use, dropped by the shift and
+    rebuilt): eig_mv bitwise the shifted reference matrix on every variant, and the fused step's alpha /
+    beta bitwise equal across the variants (same rows per wave)."""
     A = varcoef(64)
     M = eigmi.Matrix.from_bcsr(ctx, A.rowptr, A.col, A.val)
-    assert M.info.march_variant == 10
+    assert M.info.march_variant == 15
     x = np.random.default_rng(2).standard_normal(A.n)
-    M.tune(march_prefetch=11)  # the packed image (variant 13): built now, rebuilt after the shift
+    M.tune(march_prefetch=13)  # eig_mv on the pack too: built now
     assert np.array_equal(M.mv_host(x), oracle.csr_mv(A, x))
     M.shift_diag(-2.375)
     val = A.val.copy()
     oracle.lib.orc_shift_diag(A.n, A.rowptr, A.col, val, -2.375)
     B = oracle.CSR(A.nrows, A.rowptr, A.col, val)
-    for pf in (11, 0):
+    ref = None
+    for pf in (13, 9, 1, 0):
         M.tune(march_prefetch=pf)
         assert np.array_equal(M.mv_host(x), oracle.csr_mv(B, x)), pf
+        a, b, _ = eigmi.lanczos_run(M, 10, seed=3, fused=True)
+        if ref is None:
+            ref = (a, b)
+        else:
+            assert np.array_equal(a, ref[0]) and np.array_equal(b, ref[1]), pf
 
 
 @pytest.mark.gpu
@@ -183,7 +187,7 @@ def v256(ctx):
 def test_value_march_256_bitwise(ctx, v256):
     """Configuration size (C4's grid, variable coefficients): eig_mv bitwise the oracle row loop."""
     N, M, A = v256
-    assert M.info.march_variant == 10
+    assert M.info.march_variant == 15 and M.info.march_variant_mv == 0
     x = np.random.default_rng(9).standard_normal(N ** 3)
     assert np.array_equal(M.mv_host(x), oracle.csr_mv(A, x))
 
@@ -213,14 +217,14 @@ def test_value_march_256_lanczos(ctx, v256):
 @pytest.mark.gpu
 @pytest.mark.parametrize("kind,N", [(eigmi.GEN_P1STIFF3D, 64), (eigmi.GEN_P1MASS3D, 64), (eigmi.GEN_P1STIFF3D, 128)])
 def test_kuhn_box_march(ctx, kind, N):
-    """The P1 Kuhn 15-point box march (march variant 12, config C5's K and M): eig_mv bitwise the
+    """The P1 Kuhn 15-point box march (march variants 16 / 12, config C5's K and M): eig_mv bitwise the
     reference row loop; the fused and classic recurrences within 1e-12 of their restatements and of
     the row kernels (EIG_TUNE_MARCH_PREFETCH = 1: no march) at every plane-run count."""
     rp, c, v = eigmi.gen_matrix(kind, N)
     A = oracle.CSR(N ** 3, rp, c, v)
     M = eigmi.Matrix.from_bcsr(ctx, rp, c, v)
     info = M.info
-    assert info.sym_offsets == 15 and info.march_variant == 12, (info.sym_offsets, info.march_variant)
+    assert info.sym_offsets == 15 and info.march_variant == 16, (info.sym_offsets, info.march_variant)
     n = A.n
     assert M.lanczos_kernel_info(True) == ("k_lanczos_fused_march", 8 * info.sym_arrays * n + 32 * n)
     x = np.random.default_rng(13).standard_normal(n)
@@ -230,9 +234,9 @@ def test_kuhn_box_march(ctx, kind, N):
     assert M.info.march_variant == -1
     assert np.array_equal(M.mv_host(x), ref)
     base = {f: eigmi.lanczos_run(M, 25, seed=7, fused=f)[:2] for f in (False, True)}
-    for pf in (0, 14):  # 14: the Kuhn pack (variant 16)
+    for pf in (0, 14):  # 0: the Kuhn pack (variant 16, default), 14: the arrays (12)
         M.tune(march_prefetch=pf)
-        assert M.info.march_variant == (16 if pf else 12)
+        assert M.info.march_variant == (12 if pf else 16)
         for runs in (0, 1, 3, 7):
             M.tune(runs)
             assert np.array_equal(M.mv_host(x), ref), (runs, pf)
