@@ -1518,7 +1518,7 @@ __device__ __forceinline__ void march_rows(const SellB1 &A, const MarchPlan &mp,
   {
     // 3, 4, 5: +D operand 1, 2, 3 planes ahead; 6: 3 planes ahead and the gathers one plane ahead
     if constexpr (UNI >= 10)  // 10, 11: the value march (band arrays streamed), 11 one plane ahead, 13 packed
-      march_rows_geo2<0, false, UNI == 14 ? 4 : UNI == 15 ? 5 : UNI - 9>(A, mp, own, lane, wave, x, epi, pre);
+      march_rows_geo2<0, false, UNI == 14 ? 4 : UNI == 15 || UNI == 18 ? 5 : UNI - 9>(A, mp, own, lane, wave, x, epi, pre);
     else if constexpr (UNI >= 7)  // 7, 8, 9: march_rows_geo2 with the prefetches of 3, 4, 6
       march_rows_geo2<UNI == 9 ? 2 : UNI - 7, UNI == 9, 0>(A, mp, own, lane, wave, x, epi, pre);
     else
@@ -1714,7 +1714,7 @@ __global__ __launch_bounds__(kStreamThreads, march_mv_waves(UNI)) void k_lanczos
 // resident waves per SIMD the fused march kernels are built for (registers: no spills)
 constexpr int march_fused_waves(int uni)
 {
-  return uni == 16 ? 4 : uni == 12 ? 5 : uni == 11 ? 5 : uni == 10 || uni >= 13 ? 6 : uni == 6 || uni == 9 ? 4 : uni == 5 ? 5 : uni == 4 || uni == 8 ? 6
+  return uni == 18 ? 7 : uni == 16 ? 4 : uni == 12 ? 5 : uni == 11 ? 5 : uni == 10 || uni >= 13 ? 6 : uni == 6 || uni == 9 ? 4 : uni == 5 ? 5 : uni == 4 || uni == 8 ? 6
        : uni == 3 || uni == 7 ? 7 : uni ? 8 : 7;
 }
 
@@ -2285,7 +2285,7 @@ static int march_uniform(const eig_mat_s &A, bool fused = false, i64 nplanes = 0
     // 30.4 us; the arrays 226.8 / 31.7), eig_mv / K1 on the plain masked march (0: 152.1 us against 161.4 on
     // the pack): profiles/r04d_latency.jsonl, r04d_slab.jsonl
     const int tp = A.tune_march_prefetch;
-    return tp == 9 ? 10 : tp == 10 ? 11 : tp == 12 ? 14 : tp == 13 ? 15 : fused ? (A.sym_nd == 7 ? 15 : 10) : 0;
+    return tp == 9 ? 10 : tp == 10 ? 11 : tp == 12 ? 14 : tp == 13 ? 15 : tp == 15 ? 18 : fused ? (A.sym_nd == 7 ? 15 : 10) : 0;
   }
   if (!A.sym_geo) return 1;
   int u = A.tune_march_prefetch > 0 ? 1 + A.tune_march_prefetch : geo2 ? 7 : 4;
@@ -2306,6 +2306,8 @@ static int march_uniform(const eig_mat_s &A, bool fused = false, i64 nplanes = 0
       hipLaunchKernelGGL((KERN<uint8_t, true, 14>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);       \
     else if ((MODE) == kSymN8 && march_span1(A) && mp.uni == 15)                                          \
       hipLaunchKernelGGL((KERN<uint8_t, true, 15>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);       \
+    else if ((MODE) == kSymN8 && march_span1(A) && mp.uni == 18)                                          \
+      hipLaunchKernelGGL((KERN<uint8_t, true, 18>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);       \
     else if ((MODE) == kSymN8 && march_span1(A) && mp.uni == 11)                                          \
       hipLaunchKernelGGL((KERN<uint8_t, true, 11>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);       \
     else if ((MODE) == kSymN8 && march_span1(A) && mp.uni == 10)                                          \
@@ -2431,7 +2433,7 @@ static MarchPlan march_plan(const eig_mat_s &A, int mode, i64 zb = 0, i64 ze = -
     mp.cq = khi < A.sym_nd - 1 ? A.sym_uc[A.sym_dj[khi]] : 0.0;
   }
   mp.uni = uni;
-  mp.pack = uni == 15 || uni == 16 ? sym_pack_prepare(A) : nullptr;
+  mp.pack = uni == 15 || uni == 16 || uni == 18 ? sym_pack_prepare(A) : nullptr;
   // measured (tools/march_copy.hip *_pp, profiles/r03bo_march_copy.jsonl): the step's ping-pong at
   // 128^3 (2 x 32 MB of pairs) 12.9 us with plain stores vs 17.6 us nontemporal; at 256^3 (2 x 268
   // MB) no difference either way -- plain stores where every vector a launch touches fits in half
@@ -2749,7 +2751,7 @@ void lanczos_kernel_info(const eig_mat_s &A, bool fused, std::string &name, i64 
     // the band arrays and the vectors (geometric masks: no mask stream)
     const int mv = march && ((mode == kSymN8 && march_span1(A)) || march_kuhn(A)) ? march_uniform(A, fused) : 0;
     if (mv >= 10)
-      bytes = 8 * (mv == 15 ? 4 : (i64)A.sym_nup) * n + vec;
+      bytes = 8 * (mv == 15 || mv == 18 ? 4 : (i64)A.sym_nup) * n + vec;
     else if (mv)
       bytes = (mv >= 2 ? 0 : (i64)A.sym_mask_bytes * n) + vec;
     name = fused ? (march ? "k_lanczos_fused_march" : "k_lanczos_fused_b1")

@@ -109,9 +109,9 @@ def test_value_march_bitwise(ctx, mat):
         base = {}
         # 1: the plain masked march on the arrays; 9 / 10 / 12 / 13: variants 10 / 11 / 14 / 15 (the same
         # rows per wave: alpha / beta bitwise)
-        for pf in (1, 9, 10, 12, 13):
+        for pf in (1, 9, 10, 12, 13, 15):
             M.tune(runs, march_prefetch=pf)
-            assert M.info.march_variant == {1: 0, 9: 10, 10: 11, 12: 14, 13: 15}[pf]
+            assert M.info.march_variant == {1: 0, 9: 10, 10: 11, 12: 14, 13: 15, 15: 18}[pf]
             assert np.array_equal(M.mv_host(x), ref), (runs, pf)
             for fused in (False, True):
                 a, b, _ = eigmi.lanczos_run(M, 25, seed=7, fused=fused)

@@ -18,3 +18,9 @@ step boxkvar 300 env EIGMI_BOXK_VAR=1 python -u tools/bench_configs.py boxk > $O
 cat $O/boxk_var.jsonl
 step c5var 400 env EIGMI_C5_VAR=1 EIGMI_C5_N=256 python -u tools/bench_configs.py c5 > $O/c5_var.jsonl 2> $O/c5_var.err
 cat $O/c5_var.jsonl
+step sweep 300 python3 tools/lanczos_sweep.py --N 256 --matrix varcoef --rounds 3 --steps 40 \
+  --variants fused,fused#15,fused@12#15,fused@16#15,fused#12,mv > $O/latency.jsonl 2> $O/sweep.err
+cat $O/latency.jsonl
+step slab 200 python3 tools/lanczos_sweep.py --N 256 --slab 32 --matrix varcoef --rounds 3 --steps 40 \
+  --variants fused,fused#15,fused@4#15,fused@1#15,pipelined,mv > $O/slab.jsonl 2>> $O/sweep.err
+cat $O/slab.jsonl
