@@ -1507,10 +1507,10 @@ template <class MT, int KC, bool SPAN1, int UNI, class X, class EPI, class PRE =
 __device__ __forceinline__ void march_rows(const SellB1 &A, const MarchPlan &mp, i64 own, int lane, int wave,
                                            const X &x, EPI &epi, PRE &&pre = PRE{})
 {
-  static_assert(!UNI || SPAN1 || UNI == 12 || UNI == 16, "uniform-band march: far spans of at most one offset");
-  if constexpr (UNI == 12 || UNI == 16)
+  static_assert(!UNI || SPAN1 || UNI == 12 || UNI == 16 || UNI == 19, "uniform-band march: far spans of at most one offset");
+  if constexpr (UNI == 12 || UNI == 16 || UNI == 19)
   {
-    march_rows_kuhn<UNI == 16>(A, mp, own, lane, wave, x, epi, pre);
+    march_rows_kuhn<UNI != 12>(A, mp, own, lane, wave, x, epi, pre);
     return;
   }
 
@@ -1656,7 +1656,7 @@ __device__ __forceinline__ void march_rows(const SellB1 &A, const MarchPlan &mp,
 
 // y[own + r] = (A x)[r] on the plane march (BCRSMatrix::mv; bitwise k_spmv_b1).
 // resident waves per SIMD of the eig_mv / K1 march kernels (the box march holds ~90 VGPRs)
-constexpr int march_mv_waves(int uni) { return uni == 12 || uni == 16 ? 5 : 8; }
+constexpr int march_mv_waves(int uni) { return uni == 12 || uni == 16 || uni == 19 ? 5 : 8; }
 
 template <class MT, bool SPAN1, int UNI>
 __global__ __launch_bounds__(kStreamThreads, march_mv_waves(UNI)) void k_spmv_march(i64 nrows, i64 own, SellB1 A, MarchPlan mp,
@@ -1714,7 +1714,7 @@ __global__ __launch_bounds__(kStreamThreads, march_mv_waves(UNI)) void k_lanczos
 // resident waves per SIMD the fused march kernels are built for (registers: no spills)
 constexpr int march_fused_waves(int uni)
 {
-  return uni == 18 ? 7 : uni == 16 ? 4 : uni == 12 ? 5 : uni == 11 ? 5 : uni == 10 || uni >= 13 ? 6 : uni == 6 || uni == 9 ? 4 : uni == 5 ? 5 : uni == 4 || uni == 8 ? 6
+  return uni == 18 ? 7 : uni == 16 ? 4 : uni == 12 || uni == 19 ? 5 : uni == 11 ? 5 : uni == 10 || uni >= 13 ? 6 : uni == 6 || uni == 9 ? 4 : uni == 5 ? 5 : uni == 4 || uni == 8 ? 6
        : uni == 3 || uni == 7 ? 7 : uni ? 8 : 7;
 }
 
@@ -2276,7 +2276,7 @@ static int march_uniform(const eig_mat_s &A, bool fused = false, i64 nplanes = 0
 {
   // the Kuhn march on its value pack (16) by default: fused step 256^3 346 us, eig_mv 292 us (the arrays,
   // 12: 407 / 330 us; profiles/r04d_p1k.jsonl); tune value 14 = the arrays
-  if (march_kuhn(A)) return A.tune_march_prefetch == 14 ? 12 : 16;
+  if (march_kuhn(A)) return A.tune_march_prefetch == 14 ? 12 : A.tune_march_prefetch == 15 ? 19 : 16;
   const bool geo2 = A.sym_geo && A.sym_gx % 64 == 0 && A.window * 16 < (i64(1) << 31);
   if (!A.sym_uniform || (A.kflags & EIG_MAT_NO_UNIFORM))
   {
@@ -2302,6 +2302,8 @@ static int march_uniform(const eig_mat_s &A, bool fused = false, i64 nplanes = 0
       hipLaunchKernelGGL((KERN<uint32_t, false, 12>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);     \
     else if (mp.uni == 16)                                                                                \
       hipLaunchKernelGGL((KERN<uint32_t, false, 16>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);     \
+    else if (mp.uni == 19)                                                                                \
+      hipLaunchKernelGGL((KERN<uint32_t, false, 19>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);     \
     else if ((MODE) == kSymN8 && march_span1(A) && mp.uni == 14)                                          \
       hipLaunchKernelGGL((KERN<uint8_t, true, 14>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);       \
     else if ((MODE) == kSymN8 && march_span1(A) && mp.uni == 15)                                          \
@@ -2433,7 +2435,7 @@ static MarchPlan march_plan(const eig_mat_s &A, int mode, i64 zb = 0, i64 ze = -
     mp.cq = khi < A.sym_nd - 1 ? A.sym_uc[A.sym_dj[khi]] : 0.0;
   }
   mp.uni = uni;
-  mp.pack = uni == 15 || uni == 16 || uni == 18 ? sym_pack_prepare(A) : nullptr;
+  mp.pack = uni == 15 || uni == 16 || uni == 18 || uni == 19 ? sym_pack_prepare(A) : nullptr;
   // measured (tools/march_copy.hip *_pp, profiles/r03bo_march_copy.jsonl): the step's ping-pong at
   // 128^3 (2 x 32 MB of pairs) 12.9 us with plain stores vs 17.6 us nontemporal; at 256^3 (2 x 268
   // MB) no difference either way -- plain stores where every vector a launch touches fits in half
