@@ -978,8 +978,10 @@ struct MarchPlan {
   // box marches (variant 12): band array of the upper offset at 27-box position (a+1) 9 + (b+1) 3 + (c+1),
   // -1 when the stencil does not store it
   signed char kj[27];
-  // variant 13: the packed value image (eig_mat_s::sym_pack)
   const double *pack;
+  // eig_mat_tune(EIG_TUNE_CACHE) bits for the value march (measurement): 2 = the value streams with the
+  // default cache policy instead of nontemporal, 4 = the +D pair stream nontemporal
+  int cache;
 };
 // store helper of the geo2 epilogues: temporal when the plan says the vectors fit the MALL
 template <class T>
@@ -1098,6 +1100,14 @@ __device__ __forceinline__ void bload(__amdgpu_buffer_rsrc_t r, unsigned off, do
 {
   v = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0));
 }
+__device__ __forceinline__ void bload_nt(__amdgpu_buffer_rsrc_t r, unsigned off, dpair &v)
+{
+  v = __builtin_bit_cast(dpair, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 2));
+}
+__device__ __forceinline__ void bload_nt(__amdgpu_buffer_rsrc_t r, unsigned off, double &v)
+{
+  v = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 2));
+}
 // lane l takes v of lane l - 1 (NEXT = false) or l + 1; the lane without a source keeps `old`
 template <bool NEXT>
 __device__ __forceinline__ double lane_shift_or(double v, double old)
@@ -1192,7 +1202,7 @@ __device__ __forceinline__ void march_rows_geo2(const SellB1 &A, const MarchPlan
       // instead of range-checked descriptors)
       const i64 r = (i64)(o >> 3);
       const dpair *P01 = reinterpret_cast<const dpair *>(mp.pack), *P23 = P01 + S.ld;
-      const dpair p0 = __builtin_nontemporal_load(P01 + r);
+      const dpair p0 = (mp.cache & 2) ? P01[r] : __builtin_nontemporal_load(P01 + r);
       const dpair p1 = P23[r];
       v.aD = p0.x;
       v.a0 = p0.y;
@@ -1247,7 +1257,10 @@ __device__ __forceinline__ void march_rows_geo2(const SellB1 &A, const MarchPlan
       gather(vo, gc);
     if constexpr (VAL == 1 || VAL >= 4) vload(vv, vc_, true);
     const int zg = z + mp.gz0;
-    bload(zg + PF + 1 < mp.gz ? rs : r0, vo + (unsigned)(PF + 1) * Db, pf);
+    if (VAL == 5 && (mp.cache & 4))
+      bload_nt(zg + PF + 1 < mp.gz ? rs : r0, vo + (unsigned)(PF + 1) * Db, pf);
+    else
+      bload(zg + PF + 1 < mp.gz ? rs : r0, vo + (unsigned)(PF + 1) * Db, pf);
     if constexpr (VPF) vload(vv + Dv, vn_, z + 1 < z1);
     double acc = 0.0;
     const double vc = x.val(pcur), ve = x.val(gc.eg);
@@ -2442,7 +2455,8 @@ static MarchPlan march_plan(const eig_mat_s &A, int mode, i64 zb = 0, i64 ze = -
   // of the 256 MB MALL
   // fused step only (eig_mv's y, written repeatedly beside the same x, measured slower: 128^3 9.6 vs
   // 8.0 us)
-  mp.tstore = fused && uni >= 7 && A.window * 16 * 3 <= (i64(128) << 20);
+  mp.tstore = fused && uni >= 7 && (A.window * 16 * 3 <= (i64(128) << 20) || (A.tune_cache & 1));
+  mp.cache = A.tune_cache;
   mp.zb = zb;
   mp.nplanes = nplanes;
   mp.mrows = A.nslices * 64;

@@ -473,7 +473,7 @@ class Matrix:
         self.ctx.check(lib.eig_mv_host(self.h, _np_ptr(x), _np_ptr(y)))
         return y
 
-    def tune(self, march_runs=None, box_segs=None, march_prefetch=None, halo_whole=None):
+    def tune(self, march_runs=None, box_segs=None, march_prefetch=None, halo_whole=None, cache=None):
         """eig_mat_tune, only for the keys given (None leaves a key as it is): EIG_TUNE_MARCH_RUNS =
         plane runs per column of the plane-march kernels, EIG_TUNE_BOX_SEGS = z segments per tile
         column of the box kernels, EIG_TUNE_MARCH_PREFETCH = the geometric march variant (eigmi.h;
@@ -486,6 +486,8 @@ class Matrix:
             self.ctx.check(lib.eig_mat_tune(self.h, 3, int(march_prefetch)))
         if halo_whole is not None:  # EIG_TUNE_HALO: distributed steps, exchange first + one launch
             self.ctx.check(lib.eig_mat_tune(self.h, 4, int(halo_whole)))
+        if cache is not None:  # EIG_TUNE_CACHE: cache-policy bits of the value march (measurement)
+            self.ctx.check(lib.eig_mat_tune(self.h, 5, int(cache)))
 
     def shift_diag(self, shift):
         self.ctx.check(lib.eig_mat_shift_diag(self.h, shift))

@@ -211,7 +211,11 @@ int eig_mat_kernel_info(eig_mat_t mat, int op, char *name, int name_len);
  * EIG_TUNE_BOX_SEGS = z segments per tile column of the 3-D box kernels (0 = automatic; results
  * bitwise unchanged, every row's sum is formed in one place).  Results are otherwise unchanged except
  * for the summation order of the step's reductions. */
-enum { EIG_TUNE_MARCH_RUNS = 1, EIG_TUNE_BOX_SEGS = 2, EIG_TUNE_MARCH_PREFETCH = 3, EIG_TUNE_HALO = 4 };
+enum { EIG_TUNE_MARCH_RUNS = 1, EIG_TUNE_BOX_SEGS = 2, EIG_TUNE_MARCH_PREFETCH = 3, EIG_TUNE_HALO = 4,
+       EIG_TUNE_CACHE = 5 };
+/* EIG_TUNE_CACHE (measurement; fused value march): bit 0 = the (t, u) pairs stored with plain (MALL-
+ * allocating) stores instead of nontemporal ones, bit 1 = the value streams with the default cache
+ * policy, bit 2 = the +D pair stream nontemporal.  Results unchanged. */
 /* EIG_TUNE_HALO (distributed Lanczos steps): 0 = the interior planes run while the halo is in flight
  * and the boundary planes after it (two launches, the default); 1 = the exchange first, then ONE
  * launch over all owned rows (no second launch's fixed cost; the exchange is exposed).  The step's

@@ -30,12 +30,13 @@ IMAGES = {"band": 0, "arrays": eigmi.MAT_NO_UNIFORM, "gather": eigmi.MAT_BAND_GA
 
 
 def parse(spec):
-    """"op[:image][@runs][#pf]" -> (op, image flags, plane runs per column (0 = automatic),
-    geometric march variant (eig_mat_tune EIG_TUNE_MARCH_PREFETCH; 0 = automatic))."""
+    """"op[:image][@runs][#pf][%cache]" -> (op, image flags, plane runs per column (0 = automatic),
+    geometric march variant (eig_mat_tune EIG_TUNE_MARCH_PREFETCH; 0 = automatic), cache bits)."""
+    spec, _, cache = spec.partition("%")
     spec, _, pf = spec.partition("#")
     spec, _, runs = spec.partition("@")
     parts = spec.split(":")
-    return parts[0], IMAGES[parts[1] if len(parts) > 1 else "band"], int(runs or 0), int(pf or 0)
+    return parts[0], IMAGES[parts[1] if len(parts) > 1 else "band"], int(runs or 0), int(pf or 0), int(cache or 0)
 
 
 def main():
@@ -86,9 +87,9 @@ def main():
     xy = None
     for _ in range(args.rounds):
         for spec in specs:
-            op, fl, runs, pf = parse(spec)
+            op, fl, runs, pf, cache = parse(spec)
             M = mats[fl]
-            M.tune(runs, march_prefetch=pf)
+            M.tune(runs, march_prefetch=pf, cache=cache)
             if op == "mv":  # plain eig_mv (BCRSMatrix::mv) launches
                 if xy is None:
                     xy = (ctx.array(np.random.default_rng(0).standard_normal(n)), ctx.zeros(n))
@@ -104,9 +105,9 @@ def main():
             res[spec]["step_us"].append(t.total_ms / args.steps * 1e3)
             ws.close()
     for spec in specs:
-        op, fl, runs, pf = parse(spec)
+        op, fl, runs, pf, cache = parse(spec)
         M = mats[fl]
-        M.tune(runs, march_prefetch=pf)
+        M.tune(runs, march_prefetch=pf, cache=cache)
         kb = (eigmi.bytes_spmv(n, nnz) if op == "mv" else
               eigmi.bytes_spmv(n, nnz) + 56 * n if op == "pipelined" else
               eigmi.bytes_lanczos_fused(n, nnz) if op == "fused" else eigmi.bytes_lanczos_k1(n, nnz))
