@@ -446,6 +446,7 @@ extern "C" int eig_blanczos_step(eig_blanczos_t w, int steps, eig_blanczos_timin
       }
       timing->steps = steps;
       timing->cheb_launches = (int64_t)steps * std::max(0, w->degree - 1) * sell_mv8_launches(b);
+      timing->cholqr_recomputed = w->cholqr_recomputed;
     }
   });
 }

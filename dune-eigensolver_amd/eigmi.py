@@ -68,7 +68,7 @@ class _MatInfo(ctypes.Structure):
 
 class BlockTiming(ctypes.Structure):
     _fields_ = [(k, ctypes.c_double) for k in ("total_ms", "kspmm_ms", "cheb_ms", "orth_ms", "norm_ms")] + \
-               [("steps", ctypes.c_int64), ("cheb_launches", ctypes.c_int64)]
+               [("steps", ctypes.c_int64), ("cheb_launches", ctypes.c_int64), ("cholqr_recomputed", ctypes.c_int64)]
 
 
 class Timing(ctypes.Structure):

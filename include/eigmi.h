@@ -508,6 +508,8 @@ typedef struct eig_blanczos_timing {
   double norm_ms;    /* CholQR2: 2 x (M SpMM + Gram + host 32x32 Cholesky + triangular update) */
   int64_t steps;
   int64_t cheb_launches; /* fused Chebyshev kernel launches (one per 32 columns per Chebyshev step) */
+  int64_t cholqr_recomputed; /* CholQR2 second passes (since creation) that recomputed M Z because the
+                                first pass's R was ill-conditioned (diagonal spread > 1e4) */
 } eig_blanczos_timing;
 int eig_blanczos_create(eig_mat_t K, eig_mat_t M, int block, int max_steps, int degree, double lmin, double lmax,
                         unsigned seed, eig_blanczos_t *ws);
