@@ -56,11 +56,18 @@ def c1(ctx):
 
 
 def c2(ctx):
+    """Config C2 (3-D Poisson 128^3).  The band values are read from HBM (EIG_MAT_NO_UNIFORM, as the
+    benchmark's image) unless EIGMI_C2_UNIFORM=1 (the constant-coefficient shortcut)."""
     N = 128
     n = N ** 3
     rp, c, v = eigmi.gen_matrix(eigmi.GEN_POISSON3D, N)
     nnz = int(rp[-1])
-    M = eigmi.Matrix.from_bcsr(ctx, rp, c, v)
+    uni = os.environ.get("EIGMI_C2_UNIFORM", "0") == "1"
+    M = eigmi.Matrix.from_bcsr(ctx, rp, c, v, flags=0 if uni else eigmi.MAT_NO_UNIFORM)
+    image = "stencil-only (values in the kernel arguments)" if uni else "value-streaming (band values read)"
+
+    def emit(**kw):  # every C2 line names its image
+        globals()["emit"](image=image, **kw)
     x = ctx.array(np.random.default_rng(0).standard_normal(n))
     y = ctx.zeros(n)
     M.mv_timed(x, y, 10)

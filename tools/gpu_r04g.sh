@@ -16,3 +16,7 @@ cat $O/cache.jsonl
 step cacheslab 200 python3 tools/lanczos_sweep.py --N 256 --slab 32 --matrix varcoef --rounds 3 --steps 40 \
   --variants fused,fused%1,fused%2,fused%4,fused%6 > $O/cacheslab.jsonl 2>> $O/sweep.err
 cat $O/cacheslab.jsonl
+step c2 300 python3 tools/bench_configs.py c2 > $O/c2.jsonl 2> $O/c2.err
+cat $O/c2.jsonl
+step blanczos 300 python -u -m pytest tests/test_block_lanczos.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/blanczos.log 2>&1
+tail -3 $O/blanczos.log
