@@ -15,6 +15,7 @@
 #   inv                  the inverse-mode configs alone (64^2, 200^2)        -> cfg_inv*.jsonl
 #   gram                 a6 / a9 / panel-Gram timings under a kernel trace    -> gram.jsonl, gram_trace/
 #   grampmc              FETCH_SIZE / WRITE_SIZE passes over the gram timings -> grampmc/{fetch,write}
+#   boxkpmc              FETCH_SIZE / WRITE_SIZE / TA busy of the variable-coefficient box kernels -> boxkpmc/
 #   boxk                 row-class box kernels alone (SpMM, Chebyshev step) at 256^3 under a kernel trace -> boxk.jsonl, boxk_trace/
 #   c5 | c5si            block Lanczos 256^3: largest end / smallest end (multigrid solve)  -> c5*.jsonl
 #   c5trace              both under a kernel trace                            -> c5_trace/, c5si_trace/
@@ -80,6 +81,15 @@ run_task() {
         python3 tools/bench_configs.py boxk > "$O/boxk.jsonl" 2> "$O/boxk.err" && \
       EIGMI_BOXK_VAR=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/boxkvar_trace" -o trace -- \
         python3 tools/bench_configs.py boxk >> "$O/boxk.jsonl" 2>> "$O/boxk.err" ;;
+    boxkpmc)
+      # FETCH_SIZE / WRITE_SIZE / TA busy passes over the variable-coefficient box kernels (k_box_mv32)
+      prof_env
+      EIGMI_BOXK_VAR=1 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/boxkpmc/fetch" -o pmc -- \
+        python3 tools/bench_configs.py boxk > "$O/boxkpmc.jsonl" 2> "$O/boxkpmc_f.err" && \
+      EIGMI_BOXK_VAR=1 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/boxkpmc/write" -o pmc -- \
+        python3 tools/bench_configs.py boxk > /dev/null 2> "$O/boxkpmc_w.err" && \
+      EIGMI_BOXK_VAR=1 timeout -s KILL 300 rocprofv3 --pmc TA_TA_BUSY_sum TA_BUSY_avr --output-format csv -d "$O/boxkpmc/ta" -o pmc -- \
+        python3 tools/bench_configs.py boxk > /dev/null 2> "$O/boxkpmc_t.err" ;;
     c5)
       EIGMI_C5_N=256 timeout -k 10 300 python -u tools/bench_configs.py c5 > "$O/c5.jsonl" 2> "$O/c5.err" ;;
     c5si)
