@@ -233,6 +233,7 @@ struct eig_mat_s {
   int tune_halo_whole = 0;      // eig_mat_tune(EIG_TUNE_HALO): 1 = exchange first, then one whole launch
   int tune_march_prefetch = 0;  // eig_mat_tune(EIG_TUNE_MARCH_PREFETCH): geometric march variant, 0 = automatic
   int tune_cache = 0;           // eig_mat_tune(EIG_TUNE_CACHE): cache-policy bits of the march streams (measurement)
+  int tune_box_cols = 0;    // eig_mat_tune(EIG_TUNE_BOX_COLS): columns per box-image workgroup (16 / 32), 0 = automatic
   int tune_box_segs = 0;    // eig_mat_tune(EIG_TUNE_BOX_SEGS): z segments per box tile column, 0 = automatic
   // Box-stencil image for the 32-column SpMM / Chebyshev kernel (k_box.hip): box_state 0 = not
   // examined yet, 1 = built, -1 = the band is not a 3-D box stencil; box_val[k n + r] = the entry of
@@ -323,6 +324,7 @@ extern const i32 kMarchInteriorTag;
 // a2 SpMM (kernels_cpp.hh:626-657) on the band-image plane march for 1x1 matrices whose band
 // qualifies; false (nothing launched) otherwise.  X, Y: window-layout multivectors, m % 8 == 0.
 bool box_prepare(const eig_mat_s &A);
+int box_cols(const eig_mat_s &A);  // columns per box-image workgroup (k_box_mv32: 32, k_box_mv16p: 16)
 bool launch_box_spmm(const eig_mat_s &A, i64 m, const double *X, double *Y, hipStream_t s);
 // Xnew: x_{k+1} into a third buffer (nullptr: in place over Xold); Xold nullptr (with Xnew): x_{k-1} = 0
 bool launch_box_cheb(const eig_mat_s &M, i64 m, const double *Xk, double *Xold, const double *B, const double *dinv,

@@ -358,6 +358,268 @@ __global__ __launch_bounds__(kBoxThreads) void k_box_mv32(BoxGeom g, i64 ld, con
   }
 }
 
+// Push-order box kernel (round 4): 16 columns per workgroup and ONE X plane in LDS.  Iteration p
+// holds X of plane p (tile + halo) and adds its products into three rows' sums at once: the dz = +1
+// terms of the row on plane p - 1 (whose sum is then complete: epilogue), the dz = 0 terms of the row
+// on plane p and the dz = -1 terms of the row on plane p + 1.  A row still sums its entries in
+// ascending-column order (the dz = -1, 0, +1 groups in turn, ascending inside each), so kBoxStore
+// stays bitwise the reference SpMM and every EPI equals k_box_mv32's.  38 KB of LDS and 512
+// threads: two workgroups per CU, so one workgroup's load burst overlaps the other's barriers
+// (k_box_mv32 keeps three planes, 147 KB, and one workgroup per CU waits for each burst).  The two
+// 16-column halves of a tile are workgroups b and b + 8 -- the same XCD, in flight together -- so
+// the matrix values and D^-1 they both read come from HBM once.
+constexpr int kPCols = 16, kPThreads = 512;
+constexpr int kPChunks = kBoxHY * kBoxHX * (kPCols / 8) * 4;  // 16-B chunks of one plane (rows x 2 blocks x 4)
+constexpr int kPRounds = (kPChunks + kPThreads - 1) / kPThreads;
+
+template <int EPI, unsigned SHAPE>
+__global__ __launch_bounds__(kPThreads, 4) void k_box_mv16p(BoxGeom g, i64 ld, int items,
+                                                            const double *__restrict__ val,
+                                                            const uint32_t *__restrict__ mask32,
+                                                            const uint8_t *__restrict__ mask8,
+                                                            const double *__restrict__ X, double *__restrict__ Y,
+                                                            const double *__restrict__ Xold,
+                                                            const double *__restrict__ Bv,
+                                                            const double *__restrict__ dinv, double omega,
+                                                            double gamma)
+{
+  __shared__ __attribute__((aligned(16))) double slot[kBoxHY * kBoxHX][kPCols];
+  __shared__ double atile[kBoxMaxNd][kBoxTX * kBoxTY];
+  __shared__ unsigned mtile[kBoxTX * kBoxTY];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // 4 threads per row (4 columns each): a wave is one x line of the tile
+  const int yi = wave, xi = lane >> 2, cq = lane & 3, blk = cq >> 1, c4 = (cq & 1) * 4;
+  const int item = (int)(blockIdx.x >> 4) * 8 + (int)(blockIdx.x & 7), half = (int)(blockIdx.x >> 3) & 1;
+  if (item >= items) return;  // (whole workgroup: the grid is rounded up to 16 items)
+  const i64 cofs = (i64)half * 2 * ld * 8;  // this half's two column blocks
+  X += cofs;
+  Y += cofs;
+  if (Xold) Xold += cofs;
+  if (Bv) Bv += cofs;
+  const int tile = item % (g.ntx * g.nty), seg = item / (g.ntx * g.nty);
+  const int x0 = (tile % g.ntx) * kBoxTX, y0 = (tile / g.ntx) * kBoxTY;
+  const int z0 = seg * g.nz / g.nseg, z1 = (seg + 1) * g.nz / g.nseg;
+  const i64 n = (i64)g.P * g.nz;
+  auto swz = [](int row, int col) { return col ^ ((row & 1) << 1); };
+  dv2b pre[kPRounds];
+  auto fetch = [&](int zz) {
+#pragma unroll
+    for (int i = 0; i < kPRounds; ++i)
+    {
+      const int c = tid + i * kPThreads;
+      const int q = c & 3, hx = (c >> 2) % kBoxHX, rest = (c >> 2) / kBoxHX, b = rest & 1, hy = rest >> 1;
+      const int x = x0 + hx - 1, y = y0 + hy - 1;
+      const bool ok = c < kPChunks && zz >= 0 && zz < g.nz && x >= 0 && x < g.nx && y >= 0 && y < g.ny;
+      const i64 row = ok ? (i64)x + (i64)g.nx * y + (i64)g.P * zz : 0;
+      const dv2b *src = reinterpret_cast<const dv2b *>(X + (i64)b * ld * 8 + row * 8) + q;
+      pre[i] = ok ? *src : dv2b{0.0, 0.0};
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int i = 0; i < kPRounds; ++i)
+    {
+      const int c = tid + i * kPThreads;
+      if (c < kPChunks)
+      {
+        const int q = c & 3, hx = (c >> 2) % kBoxHX, rest = (c >> 2) / kBoxHX, b = rest & 1, hy = rest >> 1;
+        const int hr = hy * kBoxHX + hx;
+        *reinterpret_cast<dv2b *>(&slot[hr][swz(hr, b * 8 + q * 2)]) = pre[i];
+      }
+    }
+  };
+  // values of iteration p: offset k of the row on plane p - dz_k (staged by thread (row t % 128,
+  // offsets t / 128 + 4 j); plain loads, the other half's workgroup reads them from L2)
+  constexpr int kRows = kBoxTX * kBoxTY, kVal = (kBoxMaxNd * kRows + kPThreads - 1) / kPThreads;
+  const int srow = tid % kRows, sk0 = __builtin_amdgcn_readfirstlane(tid / kRows);
+  const int sx = x0 + (srow % kBoxTX), sy = y0 + (srow / kBoxTX);
+  const bool sown = sx < g.nx && sy < g.ny;
+  // the offsets' dz groups as bit sets (the generic path's row masks)
+  unsigned bneg = 0u, bzero = 0u, bpos = 0u;
+  if constexpr (SHAPE == 0)
+    for (int k = 0; k < g.nd; ++k)
+      (g.dz[k] < 0 ? bneg : g.dz[k] > 0 ? bpos : bzero) |= 1u << k;
+  double vpre[kVal];
+  unsigned mpre = 0u;
+  auto plane_row = [&](int zz) { return sown && zz >= z0 && zz < z1 ? (i64)sx + (i64)g.nx * sy + (i64)g.P * zz : (i64)-1; };
+  auto fetch_vals = [&](int pp) {
+#pragma unroll
+    for (int j = 0; j < kVal; ++j)
+    {
+      const int k = sk0 + j * (kPThreads / kRows);
+      double v = 0.0;
+      if (k < g.nd)
+      {
+        const i64 r = plane_row(pp - g.dz[k]);
+        if (r >= 0) v = val[(i64)k * n + r];
+      }
+      vpre[j] = v;
+    }
+    if (SHAPE == 0 && sk0 == 0)
+    {
+      auto mrow = [&](int zz) {
+        const i64 r = plane_row(zz);
+        return r >= 0 ? (mask32 ? mask32[r] : (unsigned)mask8[r]) : 0u;
+      };
+      mpre = (mrow(pp + 1) & bneg) | (mrow(pp) & bzero) | (mrow(pp - 1) & bpos);
+    }
+  };
+  auto store_vals = [&]() {
+#pragma unroll
+    for (int j = 0; j < kVal; ++j)
+    {
+      const int k = sk0 + j * (kPThreads / kRows);
+      if (k < kBoxMaxNd) atile[k][srow] = vpre[j];
+    }
+    if (sk0 == 0) mtile[srow] = mpre;
+  };
+  const int x = x0 + xi, y = y0 + yi;
+  const bool own = x < g.nx && y < g.ny;
+  const int trow = yi * kBoxTX + xi;
+  const int hrow = (yi + 1) * kBoxHX + xi + 1;
+  // Chebyshev operands of plane zz (loaded in iteration zz after the epilogue of plane zz - 1, used in
+  // iteration zz + 1)
+  dv2b bb[2] = {}, xo[2] = {};
+  double gd = 0.0;
+  auto fetch_cheb = [&](int zz, dv2b (&b2)[2], dv2b (&x2)[2], double &gg) {
+    if (EPI == kBoxStore || !own || zz < z0 || zz >= z1) return;
+    const i64 r = (i64)x + (i64)g.nx * y + (i64)g.P * zz;
+    const double *br = Bv + (i64)blk * ld * 8 + r * 8 + c4;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) b2[j] = __builtin_nontemporal_load(reinterpret_cast<const dv2b *>(br) + j);
+    if (EPI != kBoxCheb) return;
+    gg = gamma * dinv[r];
+    if (!Xold) return;
+    const double *yr = Xold + (i64)blk * ld * 8 + r * 8 + c4;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) x2[j] = __builtin_nontemporal_load(reinterpret_cast<const dv2b *>(yr) + j);
+  };
+  // sums of the rows on planes p - 1 (am: completed first, then reused for plane p + 1) and p (a0);
+  // X of the own row on plane p - 1
+  double am[4] = {}, a0[4] = {};
+  dv2b xc[2] = {};
+  fetch(z0 - 1);
+  fetch_vals(z0 - 1);
+  store();
+  store_vals();
+  for (int p = z0 - 1; p <= z1; ++p)
+  {
+    __syncthreads();  // slot holds X of plane p, atile / mtile the values of iteration p
+    if (p + 1 <= z1)
+    {
+      fetch_vals(p + 1);
+      fetch(p + 1);
+    }
+    auto add = [&](double (&acc)[4], double a, dv2b p0, dv2b p1) {
+      const double xr[4] = {p0.x, p0.y, p1.x, p1.y};
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+      {
+        if (EPI == kBoxStore) acc[j] = acc[j] + a * xr[j];
+        else acc[j] = __builtin_fma(a, xr[j], acc[j]);
+      }
+    };
+    // the products of the offsets with dz == D into acc (ascending offsets)
+    auto products = [&](auto dtag, double (&acc)[4]) {
+      constexpr int D = decltype(dtag)::value;
+      if constexpr (SHAPE != 0)
+      {
+        constexpr BoxShapeTab T = box_shape_tab(SHAPE);
+        constexpr int kGroup = 2;
+        const int hb0 = hrow - kBoxHX - 1;
+        const double *rg = &slot[0][0];
+        int pz = hb0 * kPCols;
+        const int par = hb0 & 1;
+        const int cA = blk * 8 + c4;
+        const int e0 = swz(par, cA), e1 = swz(par, cA + 2), o0 = swz(par ^ 1, cA), o1 = swz(par ^ 1, cA + 2);
+        asm volatile("" : "+v"(pz));
+        int cnt = 0;
+#pragma unroll
+        for (int k = 0; k < T.nd; ++k)
+        {
+          if (T.dz[k] != D) continue;
+          const int dr = (T.dy[k] + 1) * kBoxHX + T.dx[k] + 1;
+          const int base = pz + dr * kPCols;
+          const bool odd = dr & 1;
+          const dv2b p0 = *reinterpret_cast<const dv2b *>(rg + base + (odd ? o0 : e0));
+          const dv2b p1 = *reinterpret_cast<const dv2b *>(rg + base + (odd ? o1 : e1));
+          add(acc, atile[k][trow], p0, p1);
+          // (the next group's reads wait for these sums: a bounded number of LDS reads in flight)
+          if (++cnt % kGroup == 0)
+            asm volatile("" : "+v"(pz) : "v"(acc[0]), "v"(acc[1]), "v"(acc[2]), "v"(acc[3]));
+        }
+      }
+      else
+      {
+        const unsigned m = own ? mtile[trow] : 0u;
+#pragma unroll 2
+        for (int k = 0; k < g.nd; ++k)
+        {
+          if (g.dz[k] != D || !((m >> k) & 1u)) continue;
+          const double a = atile[k][trow];
+          const int hr = hrow + g.dxy[k];
+          add(acc, a, *reinterpret_cast<const dv2b *>(&slot[hr][swz(hr, blk * 8 + c4)]),
+              *reinterpret_cast<const dv2b *>(&slot[hr][swz(hr, blk * 8 + c4 + 2)]));
+        }
+      }
+    };
+    // dz = +1: the row on plane p - 1 is complete -> its epilogue (with the operands loaded in
+    // iteration p - 1), then this plane's operands into the same registers
+    products(std::integral_constant<int, 1>{}, am);
+    if (own && p - 1 >= z0)
+    {
+      const i64 r = (i64)x + (i64)g.nx * y + (i64)g.P * (p - 1);
+      double *yr = Y + (i64)blk * ld * 8 + r * 8 + c4;
+      if (EPI == kBoxStore)
+      {
+#pragma unroll
+        for (int j = 0; j < 4; j += 2) __builtin_nontemporal_store(dv2b{am[j], am[j + 1]}, reinterpret_cast<dv2b *>(yr + j));
+      }
+      else if (EPI == kBoxResid)
+      {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          __builtin_nontemporal_store(dv2b{bb[j].x - am[2 * j], bb[j].y - am[2 * j + 1]}, reinterpret_cast<dv2b *>(yr) + j);
+      }
+      else
+      {
+        const double xr[4] = {xc[0].x, xc[0].y, xc[1].x, xc[1].y};
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+        {
+          const double o0 = omega * (xr[2 * j] + gd * (bb[j].x - am[2 * j]) - xo[j].x) + xo[j].x;
+          const double o1 = omega * (xr[2 * j + 1] + gd * (bb[j].y - am[2 * j + 1]) - xo[j].y) + xo[j].y;
+          __builtin_nontemporal_store(dv2b{o0, o1}, reinterpret_cast<dv2b *>(yr) + j);
+        }
+      }
+    }
+    fetch_cheb(p, bb, xo, gd);
+    if (EPI == kBoxCheb)  // the own row's X on plane p, for its epilogue in iteration p + 1
+    {
+      xc[0] = *reinterpret_cast<const dv2b *>(&slot[hrow][swz(hrow, blk * 8 + c4)]);
+      xc[1] = *reinterpret_cast<const dv2b *>(&slot[hrow][swz(hrow, blk * 8 + c4 + 2)]);
+    }
+    products(std::integral_constant<int, 0>{}, a0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) am[j] = 0.0;
+    products(std::integral_constant<int, -1>{}, am);  // (am now holds the row on plane p + 1)
+    __syncthreads();  // everyone is done with the slot and atile
+    if (p + 1 <= z1)
+    {
+      store();
+      store_vals();
+    }
+    // rotate: plane p's sum becomes the one completed next iteration
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+    {
+      const double t = a0[j];
+      a0[j] = am[j];
+      am[j] = t;
+    }
+  }
+}
+
 
 // ---------------------------------------------------------------------------------------------
 // Row-class box kernels.  On a box grid whose matrix has constant entries per geometric class
@@ -793,6 +1055,9 @@ bool box_prepare(const eig_mat_s &Ac)
   return true;
 }
 
+// Columns per workgroup of the box-image kernels: eig_mat_tune(EIG_TUNE_BOX_COLS), else 32.
+int box_cols(const eig_mat_s &A) { return A.tune_box_cols == 16 ? 16 : 32; }
+
 // Y = A X (EPI store) or the Chebyshev step into Xold (EPI cheb) for m % 32 == 0 columns on the box
 // kernel; false when the matrix has no box geometry (the caller takes the band march).
 static bool launch_box(const eig_mat_s &A, i64 m, const double *X, double *Y, const double *Xold, const double *Bv,
@@ -894,11 +1159,31 @@ static bool launch_box(const eig_mat_s &A, i64 m, const double *X, double *Y, co
   unsigned shape = 0;
   for (int k = 0; k < A.sym_nd; ++k)
     shape |= 1u << ((A.box_dz[k] + 1) * 9 + (A.box_dy[k] + 1) * 3 + (A.box_dx[k] + 1));
+  // EIG_TUNE_BOX_COLS: 16 = the push-order kernel (two 16-column workgroups per tile), 32 = k_box_mv32
+  const bool push = box_cols(A) == 16;
   auto go = [&](auto shape_tag) {
     constexpr unsigned S = decltype(shape_tag)::value;
     for (i64 c0 = 0; c0 < m; c0 += 32)
     {
       const i64 off = c0 * ld;  // 4 column blocks of ld rows x 8
+      if (push)
+      {
+        const int items = tiles * g.nseg;
+        const dim3 pgrid((unsigned)(16 * ((items + 7) / 8)));
+        if (epi == kBoxCheb)
+          hipLaunchKernelGGL((k_box_mv16p<kBoxCheb, S>), pgrid, dim3(kPThreads), 0, s, g, ld, items,
+                             (const double *)A.box_val, m32, m8, X + off, Y + off, Xold ? Xold + off : nullptr,
+                             Bv + off, dinv, omega, gamma);
+        else if (epi == kBoxResid)
+          hipLaunchKernelGGL((k_box_mv16p<kBoxResid, S>), pgrid, dim3(kPThreads), 0, s, g, ld, items,
+                             (const double *)A.box_val, m32, m8, X + off, Y + off, (const double *)nullptr,
+                             Bv + off, (const double *)nullptr, 0.0, 0.0);
+        else
+          hipLaunchKernelGGL((k_box_mv16p<kBoxStore, S>), pgrid, dim3(kPThreads), 0, s, g, ld, items,
+                             (const double *)A.box_val, m32, m8, X + off, Y + off, (const double *)nullptr,
+                             (const double *)nullptr, (const double *)nullptr, 0.0, 0.0);
+        continue;
+      }
       const dim3 grid((unsigned)(tiles * g.nseg));
       if (epi == kBoxCheb)
         hipLaunchKernelGGL((k_box_mv32<kBoxCheb, S>), grid, dim3(kBoxThreads), 0, s, g, ld, (const double *)A.box_val,

@@ -2822,6 +2822,7 @@ std::string kernel_for(const eig_mat_s &A, int op)
       if (b1 && box_prepare(A))
       {
         if (A.box_ctab) return op == 5 ? "k_boxc_mv8" : "k_boxc_mv8_cheb";  // row-class image
+        if (box_cols(A) == 16) return op == 5 ? "k_box_mv16p" : "k_box_mv16p_cheb";
         return op == 5 ? "k_box_mv32" : "k_box_mv32_cheb";
       }
       return kernel_for(A, op - 2);

@@ -473,7 +473,8 @@ class Matrix:
         self.ctx.check(lib.eig_mv_host(self.h, _np_ptr(x), _np_ptr(y)))
         return y
 
-    def tune(self, march_runs=None, box_segs=None, march_prefetch=None, halo_whole=None, cache=None):
+    def tune(self, march_runs=None, box_segs=None, march_prefetch=None, halo_whole=None, cache=None,
+             box_cols=None):
         """eig_mat_tune, only for the keys given (None leaves a key as it is): EIG_TUNE_MARCH_RUNS =
         plane runs per column of the plane-march kernels, EIG_TUNE_BOX_SEGS = z segments per tile
         column of the box kernels, EIG_TUNE_MARCH_PREFETCH = the geometric march variant (eigmi.h;
@@ -488,6 +489,8 @@ class Matrix:
             self.ctx.check(lib.eig_mat_tune(self.h, 4, int(halo_whole)))
         if cache is not None:  # EIG_TUNE_CACHE: cache-policy bits of the value march (measurement)
             self.ctx.check(lib.eig_mat_tune(self.h, 5, int(cache)))
+        if box_cols is not None:  # EIG_TUNE_BOX_COLS: box-image kernel, 32 = k_box_mv32, 16 = k_box_mv16p
+            self.ctx.check(lib.eig_mat_tune(self.h, 6, int(box_cols)))
 
     def shift_diag(self, shift):
         self.ctx.check(lib.eig_mat_shift_diag(self.h, shift))

@@ -420,6 +420,52 @@ def test_box_no_class_flag(ctx, mat):
     assert np.array_equal(Y.get(), oracle.spmm_mv8(A, Qh, 32))
 
 
+def _dropped(A, rows=(1000, 2345)):
+    """A without the symmetric pair (i, i + 1) / (i + 1, i) for i in rows: rows that do not store an
+    offset staying inside the grid (the box image kernels' runtime-mask path)."""
+    keep = np.ones(len(A.col), dtype=bool)
+    for i in rows:
+        for r, c in ((i, i + 1), (i + 1, i)):
+            keep[A.rowptr[r] + int(np.nonzero(A.col[A.rowptr[r]:A.rowptr[r + 1]] == c)[0][0])] = False
+    rp = np.concatenate([[0], np.cumsum([keep[A.rowptr[r]:A.rowptr[r + 1]].sum() for r in range(A.n)])])
+    return oracle.CSR(A.n, rp.astype(A.rowptr.dtype), A.col[keep], A.val[keep])
+
+
+@pytest.mark.parametrize("mat", ["p1mass16var", "p1stiff20", "poisson18var", "poisson18drop", "p1mass16drop"])
+def test_box_push_kernel_bitwise(ctx, mat):
+    """EIG_TUNE_BOX_COLS = 16 (k_box_mv16p: one X plane in LDS, each row's dz = -1 / 0 / +1 groups
+    added in three consecutive iterations) against k_box_mv32: the SpMM bitwise the reference
+    (kernels_cpp.hh:626-657, oracle.spmm_mv8) and Chebyshev solves of degree 2 / 3 / 7 bitwise equal,
+    for 1 / 3 / nz z segments, on compile-time stencils (geometric masks) and runtime masks (rows
+    missing an in-grid entry: poisson18drop, p1mass16drop)."""
+    A = {"p1mass16var": lambda: _perturbed(_p1(16, "M")), "p1stiff20": lambda: _p1(20, "K"),
+         "poisson18var": lambda: _perturbed(oracle.poisson3d(18)),
+         "poisson18drop": lambda: _dropped(oracle.poisson3d(18)),
+         "p1mass16drop": lambda: _dropped(_p1(16, "M"))}[mat]()
+    M = upload(ctx, A, flags=eigmi.MAT_NO_CLASS)
+    n, m = A.n, 64
+    nz = round(n ** (1 / 3))
+    Qh = oracle.random_mv8(n, m, 29)
+    Q, Y = ctx.array(Qh), ctx.zeros(n * m)
+    ref = None
+    for cols, segs in ((32, 0), (16, 0), (16, 1), (16, 3), (16, nz)):
+        M.tune(box_cols=cols, box_segs=segs)
+        assert M.kernel("spmm32") == ("k_box_mv16p" if cols == 16 else "k_box_mv32")
+        eigmi.spmm_mv8(M, m, Q, Y)
+        out = {"spmm": Y.get()}
+        if not mat.startswith("poisson"):  # (Chebyshev-Jacobi: the SPD mass matrices)
+            for d in (2, 3, 7):
+                eigmi.mass_solve_mv8(M, m, d, Q, Y)
+                out[d] = Y.get()
+        if ref is None:
+            ref = out
+            assert np.array_equal(out["spmm"], oracle.spmm_mv8(A, Qh, m))
+        else:
+            for k in ref:
+                assert np.array_equal(out[k], ref[k]), (cols, segs, k)
+    M.tune(box_cols=0, box_segs=0)
+
+
 def test_box_shift_rebuilds_image(ctx):
     """eig_mat_shift_diag (A += sigma I) invalidates the box image; the next SpMM uses the new values."""
     A = _p1(16, "K")
