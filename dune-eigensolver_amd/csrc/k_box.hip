@@ -367,7 +367,10 @@ __global__ __launch_bounds__(kBoxThreads) void k_box_mv32(BoxGeom g, i64 ld, con
 // threads: two workgroups per CU, so one workgroup's load burst overlaps the other's barriers
 // (k_box_mv32 keeps three planes, 147 KB, and one workgroup per CU waits for each burst).  The two
 // 16-column halves of a tile are workgroups b and b + 8 -- the same XCD, in flight together -- so
-// the matrix values and D^-1 they both read come from HBM once.
+// the matrix values and D^-1 they both read can come from L2.  Measured (profiles/r04h_boxk_push.jsonl,
+// variable-coefficient P1 256^3, m = 32): SpMM 2561 vs 2252 us, Chebyshev step 4743 vs 3921 us for
+// k_box_mv32 -- slower, so it stays a measurement variant (EIG_TUNE_BOX_COLS = 16); k_box_mv32's
+// PMC (profiles/r04i_boxk_pmc_summary.json) puts its loss in the X halo re-read, not in the pipeline.
 constexpr int kPCols = 16, kPThreads = 512;
 constexpr int kPChunks = kBoxHY * kBoxHX * (kPCols / 8) * 4;  // 16-B chunks of one plane (rows x 2 blocks x 4)
 constexpr int kPRounds = (kPChunks + kPThreads - 1) / kPThreads;
