@@ -526,7 +526,8 @@ extern "C" int eig_mat_tune(eig_mat_t A, int key, int value)
   return guard(A ? A->ctx : nullptr, [&] {
     EIG_CHECK(A && value >= 0, EIG_ERR_ARG, "eig_mat_tune: bad argument");
     EIG_CHECK(key == EIG_TUNE_MARCH_RUNS || key == EIG_TUNE_BOX_SEGS || key == EIG_TUNE_MARCH_PREFETCH ||
-                  key == EIG_TUNE_HALO || key == EIG_TUNE_CACHE || key == EIG_TUNE_BOX_COLS,
+                  key == EIG_TUNE_HALO || key == EIG_TUNE_CACHE || key == EIG_TUNE_BOX_COLS ||
+                  key == EIG_TUNE_BOX_MAP,
               EIG_ERR_ARG, "eig_mat_tune: unknown key");
     EIG_CHECK(key != EIG_TUNE_HALO || value <= 1, EIG_ERR_ARG, "eig_mat_tune: halo mode 0 / 1");
     EIG_CHECK(key != EIG_TUNE_MARCH_PREFETCH || value <= 15, EIG_ERR_ARG, "eig_mat_tune: march variant 0..15");
@@ -538,6 +539,11 @@ extern "C" int eig_mat_tune(eig_mat_t A, int key, int value)
       A->tune_halo_whole = value;
     else if (key == EIG_TUNE_CACHE)
       A->tune_cache = value;
+    else if (key == EIG_TUNE_BOX_MAP)
+    {
+      EIG_CHECK(value <= 1, EIG_ERR_ARG, "eig_mat_tune: box map 0 / 1");
+      A->tune_box_map = value;
+    }
     else if (key == EIG_TUNE_BOX_COLS)
     {
       EIG_CHECK(value == 0 || value == 16 || value == 32, EIG_ERR_ARG, "eig_mat_tune: box columns 0 / 16 / 32");

@@ -58,6 +58,7 @@ struct BoxGeom {
   int ntx, nty;    // tiles per plane
   int nseg;        // z runs per tile column
   int nd;          // stored offsets
+  int xmap;        // k_box_mv32: 1 = XCD-contiguous item map (eig_mat_tune EIG_TUNE_BOX_MAP)
   // per offset k: plane step dz (-1 / 0 / +1), LDS row shift (dy * kBoxHX + dx)
   int dz[27], dxy[27];
 };
@@ -153,9 +154,10 @@ __global__ __launch_bounds__(kBoxThreads) void k_box_mv32(BoxGeom g, i64 ld, con
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   // 8 threads per row (4 columns each): 16 waves = 4 per SIMD with one workgroup per CU
   const int yi = wave >> 1, xi = (wave & 1) * 8 + (lane >> 3), cq = lane & 7, blk = cq >> 1, c4 = (cq & 1) * 4;
-  // item = (tile, z run) in dispatch order (an XCD-contiguous item map -- workgroup b on XCD b % 8
-  // taking one run of adjacent tiles -- measured no faster)
-  const int item = (int)blockIdx.x;
+  // item = (tile, z run) in dispatch order, or (xmap) XCD-contiguous: workgroup b (on XCD b % 8)
+  // takes item (b % 8) gridDim / 8 + b / 8, so the workgroups resident on one XCD hold two whole
+  // rows of adjacent tiles and read each other's halo rows from that XCD's L2
+  const int item = g.xmap ? (int)(blockIdx.x % 8) * (int)(gridDim.x / 8) + (int)(blockIdx.x / 8) : (int)blockIdx.x;
   const int tile = item % (g.ntx * g.nty), seg = item / (g.ntx * g.nty);
   const int x0 = (tile % g.ntx) * kBoxTX, y0 = (tile / g.ntx) * kBoxTY;
   const int z0 = seg * g.nz / g.nseg, z1 = (seg + 1) * g.nz / g.nseg;
@@ -1151,6 +1153,7 @@ static bool launch_box(const eig_mat_s &A, i64 m, const double *X, double *Y, co
   g.nseg = std::max(1, std::min(g.nz / 8, (2 * A.ctx->num_cu + tiles - 1) / tiles));
   if (A.tune_box_segs > 0) g.nseg = std::min(g.nz, A.tune_box_segs);
   g.nd = A.sym_nd;
+  g.xmap = A.tune_box_map == 1 && (tiles * g.nseg) % 8 == 0;
   for (int k = 0; k < 27; ++k)
   {
     g.dz[k] = k < A.sym_nd ? A.box_dz[k] : 0;

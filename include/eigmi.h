@@ -212,7 +212,9 @@ int eig_mat_kernel_info(eig_mat_t mat, int op, char *name, int name_len);
  * bitwise unchanged, every row's sum is formed in one place).  Results are otherwise unchanged except
  * for the summation order of the step's reductions. */
 enum { EIG_TUNE_MARCH_RUNS = 1, EIG_TUNE_BOX_SEGS = 2, EIG_TUNE_MARCH_PREFETCH = 3, EIG_TUNE_HALO = 4,
-       EIG_TUNE_CACHE = 5, EIG_TUNE_BOX_COLS = 6 };
+       EIG_TUNE_CACHE = 5, EIG_TUNE_BOX_COLS = 6, EIG_TUNE_BOX_MAP = 7 };
+/* EIG_TUNE_BOX_MAP (measurement; k_box_mv32): 1 = XCD-contiguous tile map (the workgroups resident on
+ * one XCD hold whole rows of adjacent tiles), 0 = dispatch order.  Results bitwise identical. */
 /* EIG_TUNE_BOX_COLS (box-image kernels, EIG_OP_SPMM32 / EIG_OP_CHEB32 on matrices without a row-class
  * image): 32 = k_box_mv32 (32 columns per workgroup, three X planes in LDS), 16 = k_box_mv16p (16
  * columns per workgroup, one X plane in LDS, sums pushed to the rows of planes p - 1, p, p + 1);

@@ -372,11 +372,12 @@ def boxk(ctx):
     X, Y = ctx.zeros(n * b), ctx.zeros(n * b)
     ctx.check(eigmi.lib.eig_fill_normal(ctx.h, n * b, 5, X.ptr))
     # box-image kernels (EIG_TUNE_BOX_COLS): 32 = k_box_mv32, 16 = k_box_mv16p (EIGMI_BOX_COLS list)
+    # (a value 33 = 32 columns with the XCD-contiguous tile map, EIG_TUNE_BOX_MAP)
     cols_list = [int(c) for c in os.environ.get("EIGMI_BOX_COLS", "0").split(",")]
     tag = f"{N}^3 m={b}" + (" (variable coefficients)" if var else "")
     for cols in cols_list:
-        K.tune(box_cols=cols)
-        M.tune(box_cols=cols)
+        K.tune(box_cols=min(cols, 32), box_map=int(cols == 33))
+        M.tune(box_cols=min(cols, 32), box_map=int(cols == 33))
         eigmi.spmm_mv8(K, b, X, Y)
         ctx.sync()
 
@@ -386,7 +387,7 @@ def boxk(ctx):
             ctx.sync()
         ts, _ = wall(spmm)
         ts /= reps
-        emit(config=f"P1 K {tag}", op="SpMM (kBoxStore)", kernel=K.kernel("spmm32"), us=round(ts * 1e6, 1),
+        emit(config=f"P1 K {tag}", op="SpMM (kBoxStore)", kernel=K.kernel("spmm32"), box_map=int(cols == 33), us=round(ts * 1e6, 1),
              bytes=16 * b * n, frac=round(16 * b * n / ts / 1e9 / PEAK, 4))
         d0, d1 = 2, 22
         eigmi.mass_solve_mv8(M, b, d0, X, Y)
@@ -400,7 +401,7 @@ def boxk(ctx):
         img_c = 0 if M.kernel("cheb32") == "k_boxc_mv8_cheb" else 15 * 8 * n + 8 * n
         emit(config=f"P1 K {tag}", op="SpMM bytes incl. image", kernel=K.kernel("spmm32"),
              bytes=16 * b * n + img_s, frac=round((16 * b * n + img_s) / ts / 1e9 / PEAK, 4))
-        emit(config=f"P1 M {tag}", op="Chebyshev step (kBoxCheb)", kernel=M.kernel("cheb32"), us=round(tc * 1e6, 1),
+        emit(config=f"P1 M {tag}", op="Chebyshev step (kBoxCheb)", kernel=M.kernel("cheb32"), box_map=int(cols == 33), us=round(tc * 1e6, 1),
              bytes=32 * b * n + img_c, frac=round((32 * b * n + img_c) / tc / 1e9 / PEAK, 4))
     X.free(), Y.free()
     K.close(), M.close()
