@@ -156,7 +156,8 @@ __global__ __launch_bounds__(kBoxThreads) void k_box_mv32(BoxGeom g, i64 ld, con
   const int yi = wave >> 1, xi = (wave & 1) * 8 + (lane >> 3), cq = lane & 7, blk = cq >> 1, c4 = (cq & 1) * 4;
   // item = (tile, z run) in dispatch order, or (xmap) XCD-contiguous: workgroup b (on XCD b % 8)
   // takes item (b % 8) gridDim / 8 + b / 8, so the workgroups resident on one XCD hold two whole
-  // rows of adjacent tiles and read each other's halo rows from that XCD's L2
+  // rows of adjacent tiles and read each other's halo rows from that XCD's L2 (measured: the same
+  // fetch per row, 8-11 % slower -- profiles/r04j_boxk_map.jsonl; a measurement variant)
   const int item = g.xmap ? (int)(blockIdx.x % 8) * (int)(gridDim.x / 8) + (int)(blockIdx.x / 8) : (int)blockIdx.x;
   const int tile = item % (g.ntx * g.nty), seg = item / (g.ntx * g.nty);
   const int x0 = (tile % g.ntx) * kBoxTX, y0 = (tile / g.ntx) * kBoxTY;
