@@ -59,6 +59,35 @@ def cpu_baseline(N, rp, c, v, steps, gpu_alpha, fused):
     return steps / dt, dt, rel
 
 
+def scipy_crosscheck(N, rp, c, v, steps, gpu_alpha):
+    """Same-host cross-check of the CPU baseline with a third-party implementation: the plain Lanczos
+    recurrence (w = A v - beta v_prev; alpha = w.v; w -= alpha v; beta = ||w||) on scipy.sparse's CSR
+    matvec (ARPACK's operator in scipy.sparse.linalg.eigsh) and numpy BLAS-1, single thread, same
+    matrix and start vector as the oracle baseline; a bounded sample of `steps` steps."""
+    import scipy.sparse as sp
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # noqa: E402  (the start vector generator only)
+    n = N ** 3
+    A = sp.csr_matrix((v, c, rp), shape=(n, n), copy=False)
+    q = np.zeros(n)
+    oracle.lib.orc_random_vec(n, 123, q)
+    q /= np.linalg.norm(q)
+    qprev, beta = np.zeros(n), 0.0
+    alpha = np.zeros(steps)
+    t0 = time.perf_counter()
+    for j in range(steps):
+        w = A @ q
+        w -= beta * qprev
+        alpha[j] = w @ q
+        w -= alpha[j] * q
+        beta = float(np.linalg.norm(w))
+        qprev, q = q, w / beta
+    dt = time.perf_counter() - t0
+    k = min(steps, len(gpu_alpha))
+    rel = float(np.max(np.abs(alpha[:k] - gpu_alpha[:k]) / np.abs(alpha[:k]))) if k else None
+    return steps / dt, dt, rel
+
+
 def cpu_replicas(N, rp0, c0, v0, steps, fused, threads):
     """SURVEY 8(d) CPU baseline (ii): the reference's own parallel mode (src/dune-eigensolver.cc:
     754-760, aggregate as at :292-294) -- `threads` independent replicas of the single-thread solve,
@@ -224,6 +253,7 @@ def main():
     ap.add_argument("--cpu-replicas", type=int, default=None,
                     help="replicas of the CPU baseline's parallel mode (default: usable cores, at most 16; 0 = skip)")
     ap.add_argument("--cpu-replica-steps", type=int, default=40)
+    ap.add_argument("--scipy-steps", type=int, default=20, help="steps of the scipy.sparse cross-check sample")
     ap.add_argument("--no-kernel-events", action="store_true", help="skip per-kernel HIP events")
     ap.add_argument("--kernel-events", choices=["auto", "per-launch"], default="auto",
                     help="auto: region events at N=1 for the fused step, per-launch events otherwise")
@@ -535,6 +565,12 @@ def main():
                                          f"vector, oracle/oracle.cc built -O3 -march=x86-64-v3 "
                                          f"(liboracle_fast.so), single thread ({cdt:.1f} s)",
                                "alpha_max_rel_diff_vs_gpu": rel, "cpu_model": cpu_model()}
+        sv, sdt, srel = scipy_crosscheck(N, rp, c, v, args.scipy_steps, alpha)
+        out["cpu_baseline"]["scipy_crosscheck"] = {
+            "value": round(sv, 4), "unit": "iters/s", "cores": 1,
+            "sample": f"{args.scipy_steps} plain Lanczos steps with scipy.sparse CSR matvec + numpy BLAS-1 "
+                      f"(ARPACK's operator in scipy eigsh), same matrix and start vector ({sdt:.1f} s)",
+            "alpha_max_rel_diff_vs_gpu": srel}
         P = args.cpu_replicas
         usable = len(os.sched_getaffinity(0))
         if P is None:
