@@ -70,3 +70,23 @@ def test_q1elast_64_spmv_bitwise(ctx):
         y = M.mv_host(x)
         assert np.array_equal(y, oracle.csr_mv(A, x))
     M.close()
+
+
+@pytest.mark.parametrize("cols", [32, 16])
+def test_box_spmm_p1var_128_bitwise(ctx, cols):
+    """Config C5's K at 128^3 with a coefficient per tetrahedron (eig_gen kind 9: the rows leave their
+    geometric class, so the box-image kernel streams its 15 value arrays): the 32-column SpMM of
+    k_box_mv32 (cols 32) and of the push-order k_box_mv16p (cols 16) BITWISE the reference
+    matmul_sparse_tallskinny_blocked (kernels_cpp.hh:626-657, oracle.spmm_mv8) on all 2,097,152 rows."""
+    N, m = 128, 32
+    rp, c, v = eigmi.gen_matrix(eigmi.GEN_P1STIFF3D_VAR, N)
+    A = oracle.CSR(N ** 3, rp.astype(np.int64), c.astype(np.int32), v)
+    M = eigmi.Matrix.from_bcsr(ctx, rp, c, v, flags=eigmi.MAT_NO_CLASS)
+    M.tune(box_cols=cols)
+    assert M.kernel("spmm32") == ("k_box_mv32" if cols == 32 else "k_box_mv16p")
+    Qh = oracle.random_mv8(A.n, m, 31)
+    Q, Y = ctx.array(Qh), ctx.zeros(A.n * m)
+    eigmi.spmm_mv8(M, m, Q, Y)
+    assert np.array_equal(Y.get(), oracle.spmm_mv8(A, Qh, m))
+    Q.free(), Y.free()
+    M.close()
