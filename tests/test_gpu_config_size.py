@@ -7,7 +7,9 @@ test_gpu_blas_mv8.py / test_gpu_spmv.py:
 * B_orthonormalize_blocked (kernels_cpp.hh:356-591) with n = 1024^2 rows (the 2-D Dirichlet
   Laplacian as B), m = 24, vs orc_b_orthonormalize_mv8 within 1e-12, and its returned norm;
 * config C3: the Q1 3x3-block BCRSMatrix::mv at 64^3 block rows (262,144 x 3x3, nnzb 6,859,000),
-  BITWISE the restated row loop (the block order of BCRSMatrix::mv; kernels_cpp.hh:611-617 per entry).
+  BITWISE the restated row loop (the block order of BCRSMatrix::mv; kernels_cpp.hh:611-617 per entry);
+* config C5's box-image SpMM (k_box_mv32 and the push-order k_box_mv16p) on the variable-coefficient
+  P1 K at 128^3, m = 32, BITWISE the reference SpMM (kernels_cpp.hh:626-657).
 Random well-conditioned start blocks (mt19937 / normal, the reference's generator) as everywhere."""
 import numpy as np
 import pytest
