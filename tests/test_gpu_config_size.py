@@ -9,7 +9,9 @@ test_gpu_blas_mv8.py / test_gpu_spmv.py:
 * config C3: the Q1 3x3-block BCRSMatrix::mv at 64^3 block rows (262,144 x 3x3, nnzb 6,859,000),
   BITWISE the restated row loop (the block order of BCRSMatrix::mv; kernels_cpp.hh:611-617 per entry);
 * config C5's box-image SpMM (k_box_mv32 and the push-order k_box_mv16p) on the variable-coefficient
-  P1 K at 128^3, m = 32, BITWISE the reference SpMM (kernels_cpp.hh:626-657).
+  P1 K at 128^3, m = 32, BITWISE the reference SpMM (kernels_cpp.hh:626-657);
+* config C2's StandardLargest driver (eigensolver.hh:28-112) for 10 iterations at 128^3 and
+  dot_products_diagonal_blocked (kernels_cpp.hh:24-55) at 128^3, m = 32, vs the restatements.
 Random well-conditioned start blocks (mt19937 / normal, the reference's generator) as everywhere."""
 import numpy as np
 import pytest
@@ -92,3 +94,31 @@ def test_box_spmm_p1var_128_bitwise(ctx, cols):
     assert np.array_equal(Y.get(), oracle.spmm_mv8(A, Qh, m))
     Q.free(), Y.free()
     M.close()
+
+
+def test_standard_largest_c2_iterations(ctx):
+    """Config C2 (3-D Poisson 128^3): StandardLargest (eigensolver.hh:28-112) with nev = 8 for a fixed
+    10 iterations (tol 0: the loop runs to maxiter) against the oracle restatement of the same driver
+    on the same matrix and seed: the same iteration count and the Ritz values within 1e-12 of the
+    largest (the Gram and dot sums round in another order)."""
+    A = oracle.poisson3d(128)
+    M = eigmi.Matrix.from_bcsr(ctx, A.rowptr, A.col, A.val)
+    ev, _, it = eigmi.standard_largest(M, 0.0, 0.0, 10, 8, 123, want_evec=False)
+    rev, _, rit = oracle.standard_largest(A, 0.0, 0.0, 10, 8, 123)
+    print(f"C2 StandardLargest 10 iterations: max |ev - ev_ref| = {np.abs(ev - rev).max():.2e}")
+    assert it == rit  # (the reference's counter: 9 after the 10th pass of the loop, eigensolver.hh:75-103)
+    assert np.abs(ev - rev).max() <= 1e-12 * np.abs(rev).max()
+    M.close()
+
+
+def test_dot_diag_128cubed(ctx):
+    """dot_products_diagonal_blocked (kernels_cpp.hh:24-55) on n = 128^3, m = 32 against the restatement
+    within 1e-13 relative (the reduction order differs)."""
+    n, m = 128 ** 3, 32
+    Q1h, Q2h = oracle.random_mv8(n, m, 5), oracle.random_mv8(n, m, 6)
+    Q1, Q2, dp = ctx.array(Q1h), ctx.array(Q2h), ctx.zeros(m)
+    eigmi.dot_diag_mv8(ctx, n, m, Q1, Q2, dp)
+    ref = oracle.dot_diag_mv8(Q1h, Q2h, n, m)
+    got = dp.get(m)
+    assert np.abs(got - ref).max() <= 1e-13 * np.abs(ref).max() + 1e-10
+    Q1.free(), Q2.free()
