@@ -230,3 +230,32 @@ def test_shift_invert_smallest_p1(ctx):
         r = K @ y - lam * (M @ y)
         assert np.linalg.norm(r) <= 1e-5 * lam * np.linalg.norm(M @ y)  # (a double eigenvalue: vectors ~ sqrt(eps_lambda))
     bl.close()
+
+
+@pytest.mark.gpu
+def test_block_lanczos_variable_coefficients_box_image(ctx):
+    """C5's block Lanczos (b = 32) on the variable-coefficient P1 K / M (eig_gen kinds 9 / 10: a
+    coefficient per tetrahedron) at 48^3 = 110,592 rows, uploaded with EIG_MAT_NO_CLASS so the K SpMM
+    and the Chebyshev mass solve run on the box-image kernels that stream the matrix values
+    (k_box_mv32): the block tridiagonal's eigenvalues against the numpy restatement of the same
+    recurrence (oracle.block_lanczos_gen, same start block) within 1e-9 relative."""
+    import scipy.sparse as sp
+    N, b, steps = 48, 32, 3
+    n = N ** 3
+    mats = []
+    for kind in (eigmi.GEN_P1STIFF3D_VAR, eigmi.GEN_P1MASS3D_VAR):
+        rp, c, v = eigmi.gen_matrix(kind, N)
+        mats.append((sp.csr_matrix((v, c, rp), shape=(n, n)),
+                     eigmi.Matrix.from_bcsr(ctx, rp, c, v, flags=eigmi.MAT_NO_CLASS)))
+    (Kh, K), (Mh, M) = mats
+    assert K.kernel("spmm32") == "k_box_mv32" and M.kernel("cheb32") == "k_box_mv32_cheb"
+    bl = eigmi.BlockLanczos(K, M, block=b, max_steps=steps, degree=36, seed=123)
+    bl.step(steps)
+    T = bl.tmatrix()
+    V0 = oracle.mv_to_cols(oracle.random_mv8(n, b, 123), n, b)
+    Tref, _ = oracle.block_lanczos_gen(Kh, Mh, V0, steps)
+    th, thr = np.linalg.eigvalsh(T), np.linalg.eigvalsh(Tref)
+    print(f"variable-coefficient block Lanczos 48^3: max rel diff {np.max(np.abs(th - thr) / np.abs(thr)):.2e}")
+    assert np.max(np.abs(th - thr) / np.abs(thr)) <= 1e-9
+    bl.close()
+    K.close(), M.close()
