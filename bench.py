@@ -296,7 +296,8 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    # EIGMI_FORCE_DEVICE pins every rank to one device (RCCL path rehearsal on a 1-GPU box)
+    # EIGMI_FORCE_DEVICE pins every rank to one device: it rehearses only the bootstrap (RCCL 2.27
+    # refuses two ranks on one device with ncclInvalidUsage at ncclCommInitRank, profiles/r04t_*)
     ctx = eigmi.Context(int(os.environ.get("EIGMI_FORCE_DEVICE", local)))
     if world == 1 and args.comm_self:
         ctx.comm_init(1, 0, eigmi.Context.unique_id(), always=True)
