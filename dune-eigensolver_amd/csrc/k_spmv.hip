@@ -1400,8 +1400,11 @@ __device__ __forceinline__ void march_rows_kuhn(const SellB1 &A, const MarchPlan
     const unsigned o = on ? row_off + (unsigned)q * kq + 8u : kOut;
     return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(kp, (int)o, 0, 0));
   };
+  // (eig_mat_tune EIG_TUNE_CACHE bit 1: the once-read pair streams with the default policy instead)
+  const bool kdef = (mp.cache & 2) != 0;
   auto klnt = [&](int q, unsigned row_off) {
-    return __builtin_bit_cast(dpair, __builtin_amdgcn_raw_buffer_load_b128(kp, (int)(row_off + (unsigned)q * kq), 0, 2));
+    return kdef ? __builtin_bit_cast(dpair, __builtin_amdgcn_raw_buffer_load_b128(kp, (int)(row_off + (unsigned)q * kq), 0, 0))
+                : __builtin_bit_cast(dpair, __builtin_amdgcn_raw_buffer_load_b128(kp, (int)(row_off + (unsigned)q * kq), 0, 2));
   };
   const unsigned nxk = 2u * nxv, Dk = 2u * Dv;
   const bool le = lane == 0 && x0 > 0;  // lane 0's value edge (row x0 - 1) exists
