@@ -1400,11 +1400,12 @@ __device__ __forceinline__ void march_rows_kuhn(const SellB1 &A, const MarchPlan
     const unsigned o = on ? row_off + (unsigned)q * kq + 8u : kOut;
     return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(kp, (int)o, 0, 0));
   };
-  // (eig_mat_tune EIG_TUNE_CACHE bit 1: the once-read pair streams with the default policy instead)
-  const bool kdef = (mp.cache & 2) != 0;
+  // the once-read pair streams (0, +1) and (+D, +D+1): default cache policy.  Measured against
+  // nontemporal loads at 256^3 (P1 K, profiles/r04v_p1k.jsonl, r04w_p1k.jsonl): fused step 336.0 vs
+  // 340.1 us and 337.0 vs 349.2 us on two boxes, eig_mv 282.9 vs 285.9 us -- although FETCH_SIZE
+  // rises (100.7 vs 97.6 B per row): the lines the edge lanes and the next plane re-touch stay cached
   auto klnt = [&](int q, unsigned row_off) {
-    return kdef ? __builtin_bit_cast(dpair, __builtin_amdgcn_raw_buffer_load_b128(kp, (int)(row_off + (unsigned)q * kq), 0, 0))
-                : __builtin_bit_cast(dpair, __builtin_amdgcn_raw_buffer_load_b128(kp, (int)(row_off + (unsigned)q * kq), 0, 2));
+    return __builtin_bit_cast(dpair, __builtin_amdgcn_raw_buffer_load_b128(kp, (int)(row_off + (unsigned)q * kq), 0, 0));
   };
   const unsigned nxk = 2u * nxv, Dk = 2u * Dv;
   const bool le = lane == 0 && x0 > 0;  // lane 0's value edge (row x0 - 1) exists
