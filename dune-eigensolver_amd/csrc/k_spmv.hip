@@ -1403,7 +1403,7 @@ __device__ __forceinline__ void march_rows_kuhn(const SellB1 &A, const MarchPlan
   // the once-read pair streams (0, +1) and (+D, +D+1): default cache policy.  Measured against
   // nontemporal loads at 256^3 (P1 K, profiles/r04v_p1k.jsonl, r04w_p1k.jsonl): fused step 336.0 vs
   // 340.1 us and 337.0 vs 349.2 us on two boxes, eig_mv 282.9 vs 285.9 us -- although FETCH_SIZE
-  // rises (100.7 vs 97.6 B per row): the lines the edge lanes and the next plane re-touch stay cached
+  // rises (100.7 vs 97.6 B per row; why the default policy is faster is not established)
   auto klnt = [&](int q, unsigned row_off) {
     return __builtin_bit_cast(dpair, __builtin_amdgcn_raw_buffer_load_b128(kp, (int)(row_off + (unsigned)q * kq), 0, 0));
   };
