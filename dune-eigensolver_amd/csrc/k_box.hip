@@ -59,8 +59,6 @@ struct BoxGeom {
   int nseg;        // z runs per tile column
   int nd;          // stored offsets
   int xmap;        // k_box_mv32: 1 = XCD-contiguous item map (eig_mat_tune EIG_TUNE_BOX_MAP)
-  int cache;       // k_box_mv32 (eig_mat_tune EIG_TUNE_CACHE, measurement): 2 = values / D^-1 with the
-                   // default policy, 4 = B / x_{k-1} too, 1 = plain stores (else nontemporal)
   // per offset k: plane step dz (-1 / 0 / +1), LDS row shift (dy * kBoxHX + dx)
   int dz[27], dxy[27];
 };
@@ -211,8 +209,7 @@ __global__ __launch_bounds__(kBoxThreads) void k_box_mv32(BoxGeom g, i64 ld, con
     for (int j = 0; j < kVal; ++j)
     {
       const int k = sk0 + j * (kBoxThreads / kRows);
-      vpre[j] = (r >= 0 && k < g.nd) ? ((g.cache & 2) ? val[(i64)k * n + r] : __builtin_nontemporal_load(val + (i64)k * n + r))
-                                     : 0.0;
+      vpre[j] = (r >= 0 && k < g.nd) ? __builtin_nontemporal_load(val + (i64)k * n + r) : 0.0;
     }
     if (SHAPE == 0 && sk0 == 0) mpre = r >= 0 ? (mask32 ? mask32[r] : (unsigned)mask8[r]) : 0u;
   };
@@ -237,15 +234,13 @@ __global__ __launch_bounds__(kBoxThreads) void k_box_mv32(BoxGeom g, i64 ld, con
     const i64 r = (i64)x + (i64)g.nx * y + (i64)g.P * zz;
     const double *br = Bv + (i64)blk * ld * 8 + r * 8 + c4;
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
-      b2[j] = (g.cache & 4) ? reinterpret_cast<const dv2b *>(br)[j] : __builtin_nontemporal_load(reinterpret_cast<const dv2b *>(br) + j);
+    for (int j = 0; j < 2; ++j) b2[j] = __builtin_nontemporal_load(reinterpret_cast<const dv2b *>(br) + j);
     if (EPI != kBoxCheb) return;
-    gg = gamma * ((g.cache & 2) ? dinv[r] : __builtin_nontemporal_load(dinv + r));
+    gg = gamma * __builtin_nontemporal_load(dinv + r);
     if (!Xold) return;  // x_{k-1} = 0 (the first step from a zero start): not read
     const double *yr = Xold + (i64)blk * ld * 8 + r * 8 + c4;
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
-      x2[j] = (g.cache & 4) ? reinterpret_cast<const dv2b *>(yr)[j] : __builtin_nontemporal_load(reinterpret_cast<const dv2b *>(yr) + j);
+    for (int j = 0; j < 2; ++j) x2[j] = __builtin_nontemporal_load(reinterpret_cast<const dv2b *>(yr) + j);
   };
   // prologue: X planes z0 - 1 .. z0 + 1, the values of plane z0, the Chebyshev operands of z0
   fetch(z0 - 1);
@@ -330,11 +325,7 @@ __global__ __launch_bounds__(kBoxThreads) void k_box_mv32(BoxGeom g, i64 ld, con
       if (EPI == kBoxStore)
       {
 #pragma unroll
-        for (int j = 0; j < 4; j += 2)
-        {
-          if (g.cache & 1) *reinterpret_cast<dv2b *>(yr + j) = dv2b{acc[j], acc[j + 1]};
-          else __builtin_nontemporal_store(dv2b{acc[j], acc[j + 1]}, reinterpret_cast<dv2b *>(yr + j));
-        }
+        for (int j = 0; j < 4; j += 2) __builtin_nontemporal_store(dv2b{acc[j], acc[j + 1]}, reinterpret_cast<dv2b *>(yr + j));
       }
       else if (EPI == kBoxResid)
       {
@@ -353,8 +344,7 @@ __global__ __launch_bounds__(kBoxThreads) void k_box_mv32(BoxGeom g, i64 ld, con
         {
           const double o0 = omega * (xc[2 * j] + gd * (bb[j].x - acc[2 * j]) - xo[j].x) + xo[j].x;
           const double o1 = omega * (xc[2 * j + 1] + gd * (bb[j].y - acc[2 * j + 1]) - xo[j].y) + xo[j].y;
-          if (g.cache & 1) reinterpret_cast<dv2b *>(yr)[j] = dv2b{o0, o1};
-          else __builtin_nontemporal_store(dv2b{o0, o1}, reinterpret_cast<dv2b *>(yr) + j);
+          __builtin_nontemporal_store(dv2b{o0, o1}, reinterpret_cast<dv2b *>(yr) + j);
         }
       }
     }
@@ -1087,7 +1077,7 @@ static bool launch_box(const eig_mat_s &A, i64 m, const double *X, double *Y, co
     // re-reads two halo planes, so shorter runs cost bytes; longer ones balance worse), but at least
     // one workgroup per CU on small grids and no run shorter than 8 planes (EIG_TUNE_BOX_SEGS sweeps,
     // profiles/r03aw_box_segs.jsonl: 128^3 m = 8 55.3 -> 46.8 us, 256^3 m = 32 1554 -> 1500 us)
-    BoxGeom g{};
+    BoxGeom g;
     g.nx = A.box_nx;
     g.ny = A.box_ny;
     g.nz = A.box_nz;
@@ -1152,7 +1142,7 @@ static bool launch_box(const eig_mat_s &A, i64 m, const double *X, double *Y, co
     return true;
   }
   if (m % 32 != 0) return false;  // the box-image kernel takes 32 columns per pass
-  BoxGeom g{};
+  BoxGeom g;
   g.nx = A.box_nx;
   g.ny = A.box_ny;
   g.nz = A.box_nz;
@@ -1165,7 +1155,6 @@ static bool launch_box(const eig_mat_s &A, i64 m, const double *X, double *Y, co
   if (A.tune_box_segs > 0) g.nseg = std::min(g.nz, A.tune_box_segs);
   g.nd = A.sym_nd;
   g.xmap = A.tune_box_map == 1 && (tiles * g.nseg) % 8 == 0;
-  g.cache = A.tune_cache;
   for (int k = 0; k < 27; ++k)
   {
     g.dz[k] = k < A.sym_nd ? A.box_dz[k] : 0;

@@ -221,9 +221,7 @@ enum { EIG_TUNE_MARCH_RUNS = 1, EIG_TUNE_BOX_SEGS = 2, EIG_TUNE_MARCH_PREFETCH =
  * 0 = automatic.  Results bitwise identical. */
 /* EIG_TUNE_CACHE (measurement; fused value march): bit 0 = the (t, u) pairs stored with plain (MALL-
  * allocating) stores instead of nontemporal ones, bit 1 = the value streams with the default cache
- * policy, bit 2 = the +D pair stream nontemporal.  Box-image kernel (k_box_mv32): bit 0 = plain
- * result stores, bit 1 = values and D^-1 with the default policy, bit 2 = B and x_{k-1} too.
- * Results unchanged. */
+ * policy, bit 2 = the +D pair stream nontemporal.  Results unchanged. */
 /* EIG_TUNE_HALO (distributed Lanczos steps): 0 = the interior planes run while the halo is in flight
  * and the boundary planes after it (two launches, the default); 1 = the exchange first, then ONE
  * launch over all owned rows (no second launch's fixed cost; the exchange is exposed).  The step's

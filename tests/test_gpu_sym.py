@@ -433,8 +433,7 @@ def _dropped(A, rows=(1000, 2345)):
 
 @pytest.mark.parametrize("mat", ["p1mass16var", "p1stiff20", "poisson18var", "poisson18drop", "p1mass16drop"])
 def test_box_push_kernel_bitwise(ctx, mat):
-    """EIG_TUNE_BOX_MAP = 1 (k_box_mv32's XCD-contiguous tile map), EIG_TUNE_CACHE = 7 (its cache
-    policies) and EIG_TUNE_BOX_COLS = 16 (k_box_mv16p: one X plane in LDS, each row's dz = -1 / 0 / +1 groups
+    """EIG_TUNE_BOX_MAP = 1 (k_box_mv32's XCD-contiguous tile map) and EIG_TUNE_BOX_COLS = 16 (k_box_mv16p: one X plane in LDS, each row's dz = -1 / 0 / +1 groups
     added in three consecutive iterations) against k_box_mv32: the SpMM bitwise the reference
     (kernels_cpp.hh:626-657, oracle.spmm_mv8) and Chebyshev solves of degree 2 / 3 / 7 bitwise equal,
     for 1 / 3 / nz z segments, on compile-time stencils (geometric masks) and runtime masks (rows
@@ -449,9 +448,8 @@ def test_box_push_kernel_bitwise(ctx, mat):
     Qh = oracle.random_mv8(n, m, 29)
     Q, Y = ctx.array(Qh), ctx.zeros(n * m)
     ref = None
-    for cols, segs, xmap, cache in ((32, 0, 0, 0), (32, 0, 1, 0), (32, 2, 1, 0), (32, 0, 0, 7), (16, 0, 0, 0),
-                                    (16, 1, 0, 0), (16, 3, 0, 0), (16, nz, 0, 0)):
-        M.tune(box_cols=cols, box_segs=segs, box_map=xmap, cache=cache)
+    for cols, segs, xmap in ((32, 0, 0), (32, 0, 1), (32, 2, 1), (16, 0, 0), (16, 1, 0), (16, 3, 0), (16, nz, 0)):
+        M.tune(box_cols=cols, box_segs=segs, box_map=xmap)
         assert M.kernel("spmm32") == ("k_box_mv16p" if cols == 16 else "k_box_mv32")
         eigmi.spmm_mv8(M, m, Q, Y)
         out = {"spmm": Y.get()}
@@ -464,8 +462,8 @@ def test_box_push_kernel_bitwise(ctx, mat):
             assert np.array_equal(out["spmm"], oracle.spmm_mv8(A, Qh, m))
         else:
             for k in ref:
-                assert np.array_equal(out[k], ref[k]), (cols, segs, xmap, cache, k)
-    M.tune(box_cols=0, box_segs=0, box_map=0, cache=0)
+                assert np.array_equal(out[k], ref[k]), (cols, segs, xmap, k)
+    M.tune(box_cols=0, box_segs=0, box_map=0)
 
 
 def test_box_shift_rebuilds_image(ctx):

@@ -373,17 +373,11 @@ def boxk(ctx):
     ctx.check(eigmi.lib.eig_fill_normal(ctx.h, n * b, 5, X.ptr))
     # box-image kernels (EIG_TUNE_BOX_COLS): 32 = k_box_mv32, 16 = k_box_mv16p (EIGMI_BOX_COLS list)
     # (a value 33 = 32 columns with the XCD-contiguous tile map, EIG_TUNE_BOX_MAP)
-    # EIGMI_BOX_CACHE: EIG_TUNE_CACHE bits per run (k_box_mv32's cache policies), paired with the list
     cols_list = [int(c) for c in os.environ.get("EIGMI_BOX_COLS", "0").split(",")]
-    cache_list = [int(c) for c in os.environ.get("EIGMI_BOX_CACHE", "0").split(",")]
-    if len(cache_list) < len(cols_list):
-        cache_list += [cache_list[-1]] * (len(cols_list) - len(cache_list))
-    if len(cols_list) < len(cache_list):
-        cols_list += [cols_list[-1]] * (len(cache_list) - len(cols_list))
     tag = f"{N}^3 m={b}" + (" (variable coefficients)" if var else "")
-    for cols, cache in zip(cols_list, cache_list):
-        K.tune(box_cols=min(cols, 32), box_map=int(cols == 33), cache=cache)
-        M.tune(box_cols=min(cols, 32), box_map=int(cols == 33), cache=cache)
+    for cols in cols_list:
+        K.tune(box_cols=min(cols, 32), box_map=int(cols == 33))
+        M.tune(box_cols=min(cols, 32), box_map=int(cols == 33))
         eigmi.spmm_mv8(K, b, X, Y)
         ctx.sync()
 
@@ -393,7 +387,7 @@ def boxk(ctx):
             ctx.sync()
         ts, _ = wall(spmm)
         ts /= reps
-        emit(config=f"P1 K {tag}", op="SpMM (kBoxStore)", kernel=K.kernel("spmm32"), box_map=int(cols == 33), cache=cache, us=round(ts * 1e6, 1),
+        emit(config=f"P1 K {tag}", op="SpMM (kBoxStore)", kernel=K.kernel("spmm32"), box_map=int(cols == 33), us=round(ts * 1e6, 1),
              bytes=16 * b * n, frac=round(16 * b * n / ts / 1e9 / PEAK, 4))
         d0, d1 = 2, 22
         eigmi.mass_solve_mv8(M, b, d0, X, Y)
@@ -407,7 +401,7 @@ def boxk(ctx):
         img_c = 0 if M.kernel("cheb32") == "k_boxc_mv8_cheb" else 15 * 8 * n + 8 * n
         emit(config=f"P1 K {tag}", op="SpMM bytes incl. image", kernel=K.kernel("spmm32"),
              bytes=16 * b * n + img_s, frac=round((16 * b * n + img_s) / ts / 1e9 / PEAK, 4))
-        emit(config=f"P1 M {tag}", op="Chebyshev step (kBoxCheb)", kernel=M.kernel("cheb32"), box_map=int(cols == 33), cache=cache, us=round(tc * 1e6, 1),
+        emit(config=f"P1 M {tag}", op="Chebyshev step (kBoxCheb)", kernel=M.kernel("cheb32"), box_map=int(cols == 33), us=round(tc * 1e6, 1),
              bytes=32 * b * n + img_c, frac=round((32 * b * n + img_c) / tc / 1e9 / PEAK, 4))
     X.free(), Y.free()
     K.close(), M.close()

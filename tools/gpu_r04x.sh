@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-4 GPU session x: k_box_mv32's cache policies (EIG_TUNE_CACHE bits) at 256^3, variable-coefficient P1.
+# Round-4 GPU session x (measurement build, since reverted): k_box_mv32 cache policies at 256^3.
 O=gpurun_out/${TAG:-r04x}; mkdir -p $O
 step() {
   local name=$1 t=$2; shift 2
