@@ -521,9 +521,135 @@ __global__ __launch_bounds__(kThreadsT) void k_binv_chain(i64 n, int gd, const d
   }
 }
 
+// k_binv_chain16 (round 4): the same chain on 16 waves per column block -- wave s multiplies the
+// 4 inner indices s*4 .. s*4+3 (half the products per thread, twice the waves per SIMD to hide the
+// LDS / FMA latency that bounds the 8-wave chain: PMC 44 % of wave cycles waiting) and finishes
+// rows s*4 .. s*4+3 of x.  Partials in LDS transposed ([slice][column][row], rows padded to 66:
+// lane r's stores are consecutive, the 8 column reads of a row hit distinct banks), double-buffered
+// by block parity; the same x = z - sum with the slices summed in fixed order (0 .. 15).
+constexpr int kChain16 = 1024;
+constexpr int kC16Pad = 66;
+template <bool LOWER, int GD, int PF, int RING>
+__global__ __launch_bounds__(kChain16) void k_binv_chain16(i64 n, int gd, const double *__restrict__ G,
+                                                           const double *Z, double *X)
+{
+  static_assert(RING >= GD && (RING & (RING - 1)) == 0, "ring slots");
+  __shared__ double part[2][16][8][kC16Pad];
+  __shared__ __attribute__((aligned(16))) double ring[16][RING][4][8];  // [wave s][slot][row u of slice s][column]
+  const int tid = threadIdx.x, r = tid & 63, s = tid >> 6;
+  const int u = (r >> 3) & 3, c = r & 7;  // reduction role of lanes r < 32: row s*4+u, column c
+  const bool red = r < 32;
+  const i64 cb = (i64)blockIdx.x * n * 8;
+  const i64 nblocks = (n + kTB - 1) / kTB;
+  if (red)
+#pragma unroll
+    for (int q = 0; q < RING; ++q) ring[s][q][u][c] = 0.0;
+  double pg[PF][GD][4], pz[PF];
+  auto fetch_g = [&](i64 bi, double (&g)[GD][4]) {
+    const i64 bc = bi < nblocks ? bi : nblocks - 1;
+    const i64 blk = LOWER ? bc : nblocks - 1 - bc;
+    const double *gb = G + blk * gd * (kTB * kTB);
+#pragma unroll
+    for (int d = 0; d < GD; ++d)
+    {
+      const int dd = d < gd ? d : 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) g[d][q] = gb[dd * (kTB * kTB) + (s * 4 + q) * kTB + r];
+    }
+  };
+  auto fetch_z = [&](i64 bi, double &z) {
+    const i64 bc = bi < nblocks ? bi : nblocks - 1;
+    const i64 i = (LOWER ? bc : nblocks - 1 - bc) * kTB + s * 4 + u;
+    z = gld(Z + cb + (i < n ? i : n - 1) * 8 + c);
+  };
+#pragma unroll
+  for (int p = 0; p < PF; ++p)
+  {
+    fetch_g(p, pg[p]);
+    fetch_z(p, pz[p]);
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();  // (ring zeroed)
+  typedef double d2v __attribute__((ext_vector_type(2)));
+  const i64 nround = (nblocks + PF - 1) / PF * PF;
+  for (i64 b0 = 0; b0 < nround; b0 += PF)
+  {
+#pragma unroll
+    for (int p = 0; p < PF; ++p)
+    {
+      const i64 bi = b0 + p;
+      const bool live = bi < nblocks;
+      const i64 blk = LOWER ? bi : nblocks - 1 - bi;
+      double acc[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] = 0.0;
+#pragma unroll
+      for (int d = 0; d < GD; ++d)
+        if (d < gd && d < bi)
+        {
+          const i64 src = LOWER ? blk - (d + 1) : blk + (d + 1);
+          const d2v *xr = reinterpret_cast<const d2v *>(&ring[s][src & (RING - 1)][0][0]);
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int k2 = 0; k2 < 4; ++k2)
+            {
+              const d2v xv = xr[q * 4 + k2];
+              acc[2 * k2] = fma(pg[p][d][q], xv.x, acc[2 * k2]);
+              acc[2 * k2 + 1] = fma(pg[p][d][q], xv.y, acc[2 * k2 + 1]);
+            }
+        }
+      fetch_g(bi + PF, pg[p]);
+      double(*pp)[8][kC16Pad] = part[bi & 1];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) pp[s][k][r] = acc[k];
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): LDS-only barrier, the tile loads stay in flight
+      __builtin_amdgcn_s_barrier();
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      const int t = s * 4 + u;
+      if (red)
+      {
+        double sum = pp[0][c][t];
+#pragma unroll
+        for (int q = 1; q < 16; ++q) sum += pp[q][c][t];
+        const i64 i = blk * kTB + t;
+        const bool own = live && i < n;
+        const double x = (own ? pz[p] : 0.0) - sum;
+        ring[s][blk & (RING - 1)][u][c] = x;  // read back by this wave only (LDS is in order per wave)
+        if (own) gst(X + cb + i * 8 + c, x);
+      }
+      fetch_z(bi + PF, pz[p]);
+      __builtin_amdgcn_wave_barrier();
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    }
+  }
+}
+
+// 16-wave chain (k_binv_chain16) unless EIGMI_BINV_CHAIN=8 (the 8-wave k_binv_chain, A/B)
+// (ADVICE-style note: an environment switch for measurement only, as EIGMI_TRSV)
+static bool binv_chain16()
+{
+  static const bool on = [] {
+    const char *e = std::getenv("EIGMI_BINV_CHAIN");
+    return !(e && std::strcmp(e, "8") == 0);
+  }();
+  return on;
+}
+
 template <bool LOWER>
 void launch_binv_chain(int gd, int nblk, i64 n, const double *G, const double *Z, double *X, hipStream_t s)
 {
+  // (16 waves for up to 4 coupled blocks: the 8-slot ring of gd > 4 does not fit beside the partials)
+  if (binv_chain16() && gd <= 4)
+  {
+    if (gd <= 1)
+      hipLaunchKernelGGL((k_binv_chain16<LOWER, 1, 4, 4>), dim3(nblk), dim3(kChain16), 0, s, n, gd, G, Z, X);
+    else if (gd == 2)
+      hipLaunchKernelGGL((k_binv_chain16<LOWER, 2, 4, 4>), dim3(nblk), dim3(kChain16), 0, s, n, gd, G, Z, X);
+    else
+      hipLaunchKernelGGL((k_binv_chain16<LOWER, 4, 2, 4>), dim3(nblk), dim3(kChain16), 0, s, n, gd, G, Z, X);
+    return;
+  }
   // prefetch depth by register budget: PF x GD x 8 doubles per thread (512-thread workgroups: up to
   // 256 VGPRs per lane)
   if (gd <= 1)
