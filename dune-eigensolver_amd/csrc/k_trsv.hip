@@ -639,15 +639,12 @@ static bool binv_chain16()
 template <bool LOWER>
 void launch_binv_chain(int gd, int nblk, i64 n, const double *G, const double *Z, double *X, hipStream_t s)
 {
-  // (16 waves for up to 4 coupled blocks: the 8-slot ring of gd > 4 does not fit beside the partials)
-  if (binv_chain16() && gd <= 4)
+  // 16 waves for 3 or 4 coupled blocks (the 8-slot ring of gd > 4 does not fit beside the partials).
+  // Measured (profiles/r04ab_*): 200^2 GenEO pencil (gd 4) matmul_inverse 4.05 vs 4.88 ms,
+  // GeneralizedInverse 1.39 vs 1.65 s; at 64^2 (gd 1) the 8-wave chain is faster (178 vs 200 us)
+  if (binv_chain16() && gd >= 3 && gd <= 4)
   {
-    if (gd <= 1)
-      hipLaunchKernelGGL((k_binv_chain16<LOWER, 1, 4, 4>), dim3(nblk), dim3(kChain16), 0, s, n, gd, G, Z, X);
-    else if (gd == 2)
-      hipLaunchKernelGGL((k_binv_chain16<LOWER, 2, 4, 4>), dim3(nblk), dim3(kChain16), 0, s, n, gd, G, Z, X);
-    else
-      hipLaunchKernelGGL((k_binv_chain16<LOWER, 4, 2, 4>), dim3(nblk), dim3(kChain16), 0, s, n, gd, G, Z, X);
+    hipLaunchKernelGGL((k_binv_chain16<LOWER, 4, 2, 4>), dim3(nblk), dim3(kChain16), 0, s, n, gd, G, Z, X);
     return;
   }
   // prefetch depth by register budget: PF x GD x 8 doubles per thread (512-thread workgroups: up to
