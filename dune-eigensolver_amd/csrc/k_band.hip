@@ -164,134 +164,6 @@ __global__ __launch_bounds__(kPanelThreads) void k_band_panel(i64 b, i64 nb, int
   }
 }
 
-// The same block step's panels with the tiles distributed in 4 x 4 sub-blocks (round 4): 512
-// threads, 256 on D (thread (tr, tc) holds rows 4 tr .. 4 tr + 3, columns 4 tc .. 4 tc + 3) and 256 on
-// the coupled tile X in the same layout.  Step k: the threads holding row k of D publish it (U(k, .)),
-// those holding column k publish its raw entries (A(i, k), the pivot A(k, k) among them), the tall
-// tile's column k / the wide tile's row k likewise; one barrier; every thread forms 1 / A(k, k) and
-// its rows' multipliers itself and updates its sub-block.  Parallel publication replaces k_band_panel's
-// one-thread pivot-row store (up to 63 LDS writes by one lane on every step's critical path).  The
-// operations per element are k_band_panel's, in the same order (the multiplier l = A(i, k) * (1 /
-// A(k, k)), then fma(-l, U(k, c), x) for pivots k ascending; the wide tile's substitution without
-// its one-step lag), so the factors are bitwise those of k_band_panel.
-constexpr int kPanel2Threads = 512;
-__global__ __launch_bounds__(kPanel2Threads) void k_band_panel2(i64 b, i64 nb, int gd, double *band, double *dfac,
-                                                                int *bad)
-{
-  __shared__ double prow[2][kB];  // row k of D (U(k, c))
-  __shared__ double lraw[2][kB];  // column k of D, raw (A(i, k); A(k, k) at i = k)
-  __shared__ double xpub[2][kB];  // tall: column k of X (raw); wide: row k of X
-  const int G = gd > 0 ? gd : 1;
-  const int w = blockIdx.x, t = threadIdx.x;
-  const bool tall = w < G;
-  const int off = tall ? w + 1 : w - G + 1;
-  const bool has = off <= gd && b + off < nb;
-  if (!has && w != 0) return;
-  const bool onD = t < 256;
-  const int e = t & 255, tr = e >> 4, tc = e & 15, r0 = tr * 4, c0 = tc * 4;
-  const double *D = band + tile_at(b, 0, gd);
-  double *X = has ? band + (tall ? tile_at(b + off, -off, gd) : tile_at(b, off, gd)) : nullptr;
-  const bool active = onD || has;
-  double a[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) a[i][j] = 0.0;
-  if (active)
-  {
-    const double *src = onD ? D : X;
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) a[i][j] = src[(c0 + j) * kB + r0 + i];  // column-major tiles
-  }
-#pragma unroll
-  for (int k = 0; k < kB; ++k)
-  {
-    const int kb = k >> 2, kl = k & 3, par = k & 1;
-    // publish (this step's pivot row / column are final: every update of pivots < k is applied)
-    if (onD)
-    {
-      if (tr == kb)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) prow[par][c0 + j] = a[kl][j];
-      if (tc == kb)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) lraw[par][r0 + i] = a[i][kl];
-    }
-    else if (has)
-    {
-      if (tall && tc == kb)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) xpub[par][r0 + i] = a[i][kl];
-      if (!tall && tr == kb)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) xpub[par][c0 + j] = a[kl][j];
-    }
-    __syncthreads();
-    const double piv = lraw[par][k];
-    const double rcp = 1.0 / piv;
-    if (w == 0 && t == 0)
-    {
-      const double p = fabs(piv);
-      if (!(p > 0.0 && p <= 1.7976931348623157e308)) bad[0] = 1;
-    }
-    if (onD || (has && tall))
-    {
-      // rows i (of D: below the pivot only; of the tall tile: all) take l = A(i, k) / A(k, k)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-      {
-        const int gi = r0 + i;
-        if (onD && gi <= k) continue;
-        const double l = (onD ? lraw[par][gi] : xpub[par][gi]) * rcp;
-        if (tc == kb) a[i][kl] = l;
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (c0 + j > k) a[i][j] = fma(-l, prow[par][c0 + j], a[i][j]);
-      }
-    }
-    else if (has)
-    {
-      // wide tile: forward substitution with L_bb, rows below the pivot
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-      {
-        const int gi = r0 + i;
-        if (gi <= k) continue;
-        const double l = lraw[par][gi] * rcp;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) a[i][j] = fma(-l, xpub[par][c0 + j], a[i][j]);
-      }
-    }
-  }
-  if (onD && w == 0)
-  {
-    double *Dw = dfac + b * kB2;
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) Dw[(c0 + j) * kB + r0 + i] = a[i][j];
-  }
-  if (!onD && has)
-  {
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) X[(c0 + j) * kB + r0 + i] = a[i][j];
-  }
-}
-
-// k_band_panel2 unless EIGMI_BAND_PANEL=1 (the one-thread-per-row k_band_panel, A/B)
-static bool band_panel2()
-{
-  static const bool on = [] {
-    const char *e = std::getenv("EIGMI_BAND_PANEL");
-    return !(e && std::strcmp(e, "1") == 0);
-  }();
-  return on;
-}
-
 // the factored diagonal tiles into the band
 __global__ __launch_bounds__(256) void k_band_diag_copy(int gd, const double *__restrict__ dfac, double *band)
 {
@@ -479,10 +351,7 @@ bool band_lu_device(eig_ctx_t ctx, i64 n, int gd, const std::vector<i64> &rp, co
       DevBuf dfac((size_t)nb * kB2 * 8);
       for (i64 b = 0; b < nb; ++b)
       {
-        if (band_panel2())
-          hipLaunchKernelGGL(k_band_panel2, dim3(2 * gdi), dim3(kPanel2Threads), 0, s, b, nb, gd, band, dfac.d(), bad);
-        else
-          hipLaunchKernelGGL(k_band_panel, dim3(2 * gdi), dim3(kPanelThreads), 0, s, b, nb, gd, band, dfac.d(), bad);
+        hipLaunchKernelGGL(k_band_panel, dim3(2 * gdi), dim3(kPanelThreads), 0, s, b, nb, gd, band, dfac.d(), bad);
         if (gd > 0 && b + 1 < nb) hipLaunchKernelGGL(k_band_update, dim3(gd * gd), dim3(256), 0, s, b, nb, gd, band);
       }
       hipLaunchKernelGGL(k_band_diag_copy, dim3((unsigned)nb), dim3(256), 0, s, gd, (const double *)dfac.d(), band);
