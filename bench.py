@@ -19,12 +19,19 @@ bytes) -- side numbers, never `value` or `roofline`.
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 --master-port P \
         bench.py --gpus N --steps K --warmup W
 
+`--gpus N` (N > 1) without a launcher (WORLD_SIZE unset) starts the N ranks itself: a
+torch.distributed.run child with --nproc-per-node N, launched before this process touches the GPU
+(libeigmi is imported only after that decision); its one JSON line is forwarded, and a line whose
+n_gpus or comm.nranks differs from N fails the run.  Under a launcher, WORLD_SIZE must equal --gpus.
+
 torch.distributed (gloo) is only the bootstrap / barrier / max-over-ranks channel; the data path
 is libeigmi's own RCCL communicator over xGMI.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -33,7 +40,89 @@ sys.path.insert(0, os.path.join(ROOT, "dune-eigensolver_amd"))
 
 import numpy as np  # noqa: E402
 
-import eigmi  # noqa: E402
+eigmi = None  # libeigmi (loads the HIP library): imported by load_eigmi() once the launch is decided
+
+
+def load_eigmi():
+    global eigmi
+    if eigmi is None:
+        import eigmi as _e
+        eigmi = _e
+    return eigmi
+
+
+# ----------------------------------------------------------------------------- N-rank launcher
+def launcher_command(gpus, argv, port):
+    """The torch.distributed.run command that runs this script on `gpus` ranks of this node."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+
+
+def free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def child_line(text, gpus):
+    """The N-rank child's stdout -> (its JSON line as a dict or None, error or None): exactly one
+    JSON line, n_gpus == gpus and comm.nranks == gpus (RCCL saw every rank)."""
+    lines = [ln for ln in text.splitlines() if ln.lstrip().startswith("{")]
+    if len(lines) != 1:
+        return None, f"expected one JSON line from the {gpus}-rank run, got {len(lines)}"
+    try:
+        d = json.loads(lines[0])
+    except ValueError as e:
+        return None, f"unparsable line from the {gpus}-rank run: {e}"
+    if d.get("n_gpus") != gpus:
+        return d, f"the {gpus}-rank run reported n_gpus = {d.get('n_gpus')}"
+    nr = (d.get("comm") or {}).get("nranks")
+    if nr != gpus:
+        return d, f"the {gpus}-rank run's communicator has {nr} ranks"
+    return d, None
+
+
+def run_ranks(gpus, argv):
+    """Run this script on `gpus` ranks (child launcher; nothing here has touched the GPU) and forward
+    its JSON line; the exit status is the child's, or 4 when its line does not show `gpus` ranks."""
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (RCCL across processes)
+    cmd = launcher_command(gpus, argv, free_port())
+    print("bench: " + " ".join(cmd), file=sys.stderr, flush=True)
+    p = subprocess.run(cmd, stdout=subprocess.PIPE, env=env)
+    d, err = child_line(p.stdout.decode(errors="replace"), gpus)
+    if p.returncode != 0:
+        print(f"bench: the {gpus}-rank run failed with status {p.returncode}", file=sys.stderr)
+        return p.returncode
+    if err:
+        print("bench: " + err, file=sys.stderr)
+        return 4
+    sys.stdout.write(json.dumps(d) + "\n")
+    sys.stdout.flush()
+    return 0
+
+
+def world_from_env(gpus):
+    """(world, rank, local rank) under a launcher; --gpus must match WORLD_SIZE (None: take it)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if gpus is not None and gpus != world:
+        raise SystemExit(f"bench: --gpus {gpus} but WORLD_SIZE={world}")
+    return world, int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0"))
+
+
+def ab_mismatch(a1, b1, a2, b2):
+    """Largest relative difference of two Lanczos coefficient sequences over their common steps."""
+    k = min(len(a1), len(a2))
+    if k == 0:
+        return 0.0
+    ra = np.abs(np.asarray(a1[:k]) - np.asarray(a2[:k])) / np.maximum(np.abs(np.asarray(a2[:k])), 1e-300)
+    kb = min(len(b1), len(b2))
+    rb = np.abs(np.asarray(b1[:kb]) - np.asarray(b2[:kb])) / np.maximum(np.abs(np.asarray(b2[:kb])), 1e-300)
+    m = max(float(ra.max()), float(rb.max()) if kb else 0.0)
+    return m if np.isfinite(m) else float("inf")
+
+
+AB_RTOL = 1e-12  # a non-RCCL transport must reproduce the RCCL run's alpha / beta to this
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 
@@ -171,10 +260,22 @@ def committed_traffic(kernel, N, world, build, image):
     return (best[0], best[1], best[2][0]) if best else None
 
 
+def comm_summary(ctx, world, ab_check):
+    ci = ctx.comm_info()
+    cc = ctx.comm_counters()
+    return {"nranks": ci["nranks"], "allreduce": ci["allreduce"],
+            "mailbox_errors": ci["mailbox_errors"], "allreduce_calls": cc["allreduce"] + cc["allreduce_split"],
+            "halo_groups": cc["halo_groups"], "transport_check": ab_check or None}
+
+
 VARIANT_NAME = {"fused": "fused one-reduction step", "pipelined": "pipelined one-reduction step",
                 "classic": "SpMV + update kernels"}
 # matrix images (eig_mat_create_bcsr_ex flags)
-IMAGES = {"arrays": eigmi.MAT_NO_UNIFORM, "csr": eigmi.MAT_NO_BAND, "uniform": 0}
+IMAGES = ("arrays", "csr", "uniform")
+
+
+def image_flags(image):
+    return {"arrays": eigmi.MAT_NO_UNIFORM, "csr": eigmi.MAT_NO_BAND, "uniform": 0}[image]
 
 
 def image_name(M):
@@ -200,18 +301,25 @@ def image_name(M):
 
 
 def kernel_instance(M, kname):
-    """The template instance of a march kernel (as rocprofv3 names it), else the bare name."""
+    """The template instance of a march or SELL-slice kernel (as rocprofv3 names it), else the bare
+    name.  SELL slice kernels: <R = 1, image mode> (k_spmv.hip: 0 explicit columns, 1 all slices
+    stencil, 2 mixed)."""
     info = M.info
     if kname.endswith("_march") and info.march_variant >= 0 and info.sym_mask_bytes == 1 and info.sym_offsets <= 7:
         return f"{kname}<unsigned char, true, {info.march_variant}>"
+    if kname.endswith("_b1") and info.sym_offsets == 0:
+        mode = 0 if info.stencil_slices == 0 else 1 if info.stencil_slices == info.nslices else 2
+        return f"{kname}<1, {mode}>"
     return kname
 
 
-def side_image(ctx, rp, c, v, image, steps, n, nnz):
+def side_image(ctx, rp, c, v, image, steps, n, nnz, traffic=None, flags=None, extra=None):
     """N = 1 side measurement: the same fused step on another image of the same matrix (K eager steps,
-    region events: one launch per step), priced at the bytes that image streams and at SURVEY 8(d)'s
-    CSR step bytes."""
-    M = eigmi.Matrix.from_bcsr(ctx, rp, c, v, flags=IMAGES[image])
+    region events: one launch per step), priced at the bytes that image streams (the kernel's byte
+    model: eig_lanczos_kernel_info -- for the SELL-64 image its padded values, column indices of the
+    explicit slices, stencil offsets and row masks, not the CSR count) with the committed PMC traffic
+    of the same kernel beside it, and at SURVEY 8(d)'s CSR step bytes."""
+    M = eigmi.Matrix.from_bcsr(ctx, rp, c, v, flags=image_flags(image) if flags is None else flags)
     try:
         ws = eigmi.LanczosWorkspace(M, steps + 5, seed=123, fused=True)
         ws.step(5)
@@ -224,18 +332,47 @@ def side_image(ctx, rp, c, v, image, steps, n, nnz):
         ws.close()
         us = tim.total_ms / steps * 1e3
         sb = eigmi.bytes_lanczos_step(n, nnz)
-        return {"image": image, "matrix_image": image_name(M), "kernel": kernel_instance(M, kname),
-                "value": round(steps / dt, 3), "unit": "iters/s", "ms_per_step": round(dt / steps * 1e3, 4),
-                "avg_launch_us": round(us, 2), "bytes_per_launch": kb,
-                "achieved_GBs": round(kb / us / 1e3, 1), "frac": round(kb / us / 1e3 / HBM_PEAK_GBS, 4),
-                "survey_step_bytes": sb, "survey_step_GBs": round(sb / (dt / steps) / 1e9, 1)}
+        ki = kernel_instance(M, kname)
+        out = {"image": image, "matrix_image": image_name(M), "kernel": ki,
+               "value": round(steps / dt, 3), "unit": "iters/s", "ms_per_step": round(dt / steps * 1e3, 4),
+               "avg_launch_us": round(us, 2), "bytes_per_launch": kb,
+               "achieved_GBs": round(kb / us / 1e3, 1), "frac": round(kb / us / 1e3 / HBM_PEAK_GBS, 4),
+               "survey_step_bytes": sb, "survey_step_GBs": round(sb / (dt / steps) / 1e9, 1),
+               "survey_step_frac": round(sb / (dt / steps) / 1e9 / HBM_PEAK_GBS, 4)}
+        tr = traffic(ki) if traffic else None
+        if tr:
+            out.update({"traffic": tr[0], "traffic_source": tr[1], "traffic_same_build": tr[2],
+                        "traffic_vs_bytes": round(tr[0] / kb, 4),
+                        "traffic_frac": round(tr[0] / us / 1e3 / HBM_PEAK_GBS, 4)})
+        if extra:
+            out.update(extra)
+        return out
     finally:
         M.close()
 
 
+def side_general(ctx, N, steps, traffic, seed=123):
+    """N = 1 side measurement on a GENERAL sparse matrix: the same 3-D Poisson N^3 under a seeded
+    random symmetric permutation and reverse Cuthill-McKee (eigmi.scrambled_rcm, tools/csr_general.py):
+    same nnz, no constant-offset band, explicit column indices in most SELL slices -- what an
+    unstructured BCRSMatrix looks like to the kernels.  Reordering on the host is outside the timing."""
+    t0 = time.perf_counter()
+    rp, c, v = eigmi.gen_matrix(eigmi.GEN_POISSON3D, N)
+    rp, c, v = eigmi.scrambled_rcm(rp, c, v, seed)
+    t_re = time.perf_counter() - t0
+    n, nnz = rp.size - 1, int(rp[-1])
+    rows = np.repeat(np.arange(n, dtype=np.int64), np.diff(rp))
+    bw = int(np.abs(c - rows).max())
+    del rows
+    return side_image(ctx, rp, c, v, "csr", steps, n, nnz, traffic=traffic, flags=0,
+                      extra={"matrix": f"3-D Poisson {N}^3 scrambled (seed {seed}) + RCM: bandwidth {bw}",
+                             "reorder_s": round(t_re, 1)})
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); N > 1 without a launcher starts torch.distributed.run itself")
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--N", type=int, default=256, help="grid points per axis (n = N^3)")
@@ -248,6 +385,8 @@ def main():
                          "constant-coefficient shortcut (band values in the kernel arguments, no matrix bytes)")
     ap.add_argument("--side-steps", type=int, default=50,
                     help="N = 1: steps of the csr / stencil_shortcut side measurements (0 = skip them)")
+    ap.add_argument("--general-steps", type=int, default=30,
+                    help="N = 1: steps of the general-matrix side measurement (scrambled + RCM; 0 = skip)")
     ap.add_argument("--cpu-steps", type=int, default=160, help="Lanczos steps of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-replicas", type=int, default=None,
@@ -277,15 +416,17 @@ def main():
                     help="timed steps as one hipGraph replay or launched one by one; auto = graph when "
                          "N > 1 (host-bound halo/allreduce calls), eager at N = 1 (measured faster there)")
     args = ap.parse_args()
+    if args.gpus is not None and args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # decided before anything loads the HIP library or touches the GPU
+        sys.exit(run_ranks(args.gpus, sys.argv[1:]))
+    world, rank, local = world_from_env(args.gpus)
+    load_eigmi()
     # stdout carries exactly one JSON line: native libraries that write to fd 1 (RCCL prints its
     # version banner there at communicator creation) are sent to stderr, the line goes to the saved fd
     sys.stdout.flush()
     out_fd = os.dup(1)
     os.dup2(2, 1)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     if world > 1:
         import torch
@@ -316,9 +457,9 @@ def main():
     gkind = eigmi.GEN_VARCOEF3D if args.matrix == "varcoef" else eigmi.GEN_POISSON3D
     rp, c, v = eigmi.gen_rows(gkind, N, b, cnt)
     if world > 1:
-        M = eigmi.Matrix.from_rows(ctx, n, b, rp, c, v, flags=IMAGES[args.image])
+        M = eigmi.Matrix.from_rows(ctx, n, b, rp, c, v, flags=image_flags(args.image))
     else:
-        M = eigmi.Matrix.from_bcsr(ctx, rp, c, v, flags=IMAGES[args.image])
+        M = eigmi.Matrix.from_bcsr(ctx, rp, c, v, flags=image_flags(args.image))
     nnz_total = int(eigmi.lib.eig_gen_nnzb(gkind, N))
     nnz_local = int(rp[-1])
 
@@ -338,6 +479,7 @@ def main():
     # allreduce latency over xGMI, so the auto variant measures both (graph replays, max over ranks)
     variant = args.variant
     trial = None
+    ab, ab_check = {}, {}
     halo_mode = "split"
     if variant == "auto":
         # one rank: EIG_LANCZOS_AUTO's choice for this image (the fused step on a 1x1 image)
@@ -382,6 +524,7 @@ def main():
                             tw.step(args.trial_steps)
                         ctx.sync()
                         ms[la] = (time.perf_counter() - t0) / args.trial_steps * 1e3
+                    ab[(var, halo, ar)] = tw.tridiag()
                 except eigmi.EigError as e:
                     print(f"bench: {var} trial failed on rank {rank}: {e}; stopping every rank", file=sys.stderr,
                           flush=True)
@@ -394,7 +537,22 @@ def main():
                     trial[f"{var}/{la}/{halo}/{ar}"] = round(max_over_ranks(ms[la]), 4)
             if "mailbox" in ars and max_over_ranks(ctx.comm_info()["mailbox_errors"]) > 0:
                 # a mailbox call timed out on some rank (its sums read NaN): not a candidate
-                trial = {k: (float("inf") if k.endswith("/mailbox") else v) for k, v in trial.items()}
+                trial = {k: (float("inf") if k.split("/")[3] != "rccl" else v) for k, v in trial.items()}
+            # a transport is a candidate only if its run reproduces the RCCL run of the same variant
+            # and halo mode (same start vector, same step count) to AB_RTOL -- never on timing alone
+            for (var, halo, ar), (a, b) in ab.items():
+                if ar == "rccl":
+                    continue
+                ref = ab.get((var, halo, "rccl"))
+                mm = ab_mismatch(a, b, *ref) if ref is not None else float("inf")
+                mm = max_over_ranks(mm)
+                ok = mm <= AB_RTOL
+                ab_check[f"{var}/{halo}/{ar}"] = {"max_rel_diff_vs_rccl": mm if np.isfinite(mm) else None,
+                                                  "steps": int(len(a)), "ok": bool(ok)}
+                if not ok:
+                    for k in trial:
+                        if k.startswith(f"{var}/") and k.endswith(f"/{halo}/{ar}"):
+                            trial[k] = float("inf")
             best = min(trial, key=trial.get)
             variant, best_launch, best_halo, best_ar = best.split("/")
             if args.launch == "auto":
@@ -505,9 +663,13 @@ def main():
     sides = {}
     if rank == 0 and world == 1 and args.side_steps > 0:
         # the same step on the other images of the same matrix (side numbers: never value / roofline)
+        def side_traffic(ki):
+            return committed_traffic(ki, N, world, build, args.image)
         for img, key in (("csr", "csr"), ("uniform", "stencil_shortcut")):
             if img != args.image:
-                sides[key] = side_image(ctx, rp, c, v, img, args.side_steps, n, nnz_total)
+                sides[key] = side_image(ctx, rp, c, v, img, args.side_steps, n, nnz_total, traffic=side_traffic)
+        if args.general_steps > 0 and args.matrix == "poisson":
+            sides["general"] = side_general(ctx, N, args.general_steps, side_traffic)
     if rank == 0:
         copy_GBs = eigmi.stream_copy_GBs(ctx)
         if spmv:
@@ -557,6 +719,8 @@ def main():
         # auto at N > 1: ms per step of each one-reduction variant in the trial (max over ranks)
         "variant_trial_ms": ({k: (v if v != float("inf") else None) for k, v in trial.items()} if trial else None),
         "launch": "hipGraph replay of the K steps" if graph else "eager",
+        # the communicator the timed steps ran on (RCCL saw nranks ranks) and its transport check
+        "comm": comm_summary(ctx, world, ab_check),
         "build": build,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

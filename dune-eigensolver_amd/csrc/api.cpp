@@ -787,7 +787,12 @@ void build_sell(eig_mat_s &A, i64 nb, const int64_t *rowptr, const int32_t *col,
   EIG_HIP(hipMemcpyAsync(A.col, cimg.data(), total * sizeof(i32), hipMemcpyHostToDevice, s));
   EIG_HIP(hipMemcpyAsync(A.val, vimg.data(), total * bb * sizeof(double), hipMemcpyHostToDevice, s));
   A.n_stencil_slices = 0;
-  for (i64 q = 0; q < ns; ++q) A.n_stencil_slices += swidth[q] > 0;
+  A.sell_explicit = 0;
+  for (i64 q = 0; q < ns; ++q)
+  {
+    A.n_stencil_slices += swidth[q] > 0;
+    if (swidth[q] <= 0) A.sell_explicit += sp[q + 1] - sp[q];
+  }
   if (A.n_stencil_slices > 0)
   {
     A.st_width = dev_alloc<i32>(ns);

@@ -145,8 +145,11 @@ constexpr double kCholQrReuseCond = 1e4;
 
 // Z (b columns) = Vdst R with Vdst M-orthonormal (CholQR twice); R (b x b upper, row-major) on
 // the host.  Vdst may equal Z.  The b x b factorisations run on the device (k_chol_small: the host
-// chol_upper / tri_upper_inv arithmetic), so the two passes queue without a host round trip; one
-// synchronisation at the end brings R and the breakdown flag back.
+// chol_upper / tri_upper_inv arithmetic).  One host round trip in the middle reads R0 back to pick
+// the second pass (reuse M Z or recompute it, below), one at the end brings R and the breakdown
+// flag back.  The pick is a heuristic: the spread of R0's diagonal is only a lower bound on
+// cond(R0), so an ill-conditioned block with an even diagonal can still take the reuse path (its
+// second pass then restores M-orthonormality to ~eps cond(Z) instead of ~eps).
 void mcholqr2(eig_blanczos_s &w, double *Z, double *Vdst, std::vector<double> &Rtot)
 {
   eig_mat_s &M = *w.M;

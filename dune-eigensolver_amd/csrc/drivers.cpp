@@ -1699,6 +1699,7 @@ extern "C" int eig_lanczos_capture(eig_lanczos_t ws, int steps, int flags, int *
     // the loopback transport synchronises with the host inside the step: eager replay only
     if (ctx->loop) return;
     hipStream_t s = ctx->stream;
+    march_prepare(*ws->A);  // (builds a value pack outside the graph, never as a captured node)
     EIG_HIP(hipStreamSynchronize(s));
     EIG_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
     hipGraph_t g = nullptr;

@@ -222,9 +222,13 @@ struct eig_mat_s {
   // offset; grid in sym_gx / gy / gz / gz0.  The box marches (k_spmv.hip, e.g. the P1 Kuhn 15-point
   // stencil of config C5) derive the masks from the coordinates
   unsigned sym_box27 = 0;
-  // packed copy of the 4 value arrays of a 7-point band ({+D, 0, +1, +nx} per row, 32 B) for march
-  // variant 13 (k_spmv.hip sym_pack_prepare; freed by a shift, rebuilt at the next use)
+  // packed copy of the 4 value arrays of a 7-point band ({+D, 0, +1, +nx} per row, 32 B; the P1 Kuhn
+  // band: 8 arrays, 64 B) for the value marches 15 / 16 / 18 / 19 (k_spmv.hip sym_pack_prepare: built
+  // at the first launch that marches on it, never by a query; refilled in place by a shift)
   double *sym_pack = nullptr;
+  eigmi::i64 sym_pack_bytes = 0;
+  // SELL image: padded entries of the explicit-column slices (their 4-B column indices are streamed)
+  eigmi::i64 sell_explicit = 0;
   // Plane-march split of a distributed slab (k_spmv.hip march_plan): planes [mz0, mz1) have no
   // ghost columns and are marched while the halo is in flight; march_bnd lists every slice outside
   // them (the boundary launch after the exchange).  mz1 <= mz0: no split.
@@ -348,6 +352,11 @@ bool launch_cheb_march(const eig_mat_s &M, i64 m, const double *Xk, double *Xold
                        double omega, double gamma, hipStream_t s);
 // Kernel a whole-matrix Lanczos step launch picks on this image, and its algorithmic bytes per launch.
 void lanczos_kernel_info(const eig_mat_s &A, bool fused, std::string &name, i64 &bytes);
+i64 sell_image_bytes(const eig_mat_s &A);
+// Build what a march launch on A streams beside the band arrays (the value pack), ahead of a capture
+void march_prepare(const eig_mat_s &A);
+// whether the P1 Kuhn value pack (64 B per row) fits the 32-bit buffer descriptor march 16 / 19 read it by
+bool kuhn_pack_fits(const eig_mat_s &A);
 // Whether EIG_LANCZOS_AUTO takes the fused step on this image: every 1x1 image (round 3: without
 // register spills the fused step beats the two-kernel step on scattered images too).
 bool fused_step_pays(const eig_mat_s &A);
@@ -371,6 +380,8 @@ void launch_stream_copy(i64 n, const double *x, double *y, int num_cu, hipStream
 void launch_scal_dev(i64 n, const double *a, bool reciprocal_sqrt, double *x, hipStream_t s);
 void launch_sqrt_inplace(double *v, int count, hipStream_t s);
 void launch_shift_diag(eig_mat_s &A, double shift, hipStream_t s);
+// (Re)fill the packed value image sym_pack from the band arrays on stream s (k_spmv.hip)
+void sym_pack_fill(eig_mat_s &A, hipStream_t s);
 
 // MultiVector<double,8> kernels.
 void launch_spmm_mv8(const eig_mat_s &A, i64 m, const double *Qin, double *Qout, hipStream_t s);

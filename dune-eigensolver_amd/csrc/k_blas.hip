@@ -213,18 +213,20 @@ __global__ void k_shift_sym(i64 nrows, i64 own, const MT *__restrict__ mask, int
   if (r >= nrows) return;
   if ((mask[r] >> k0) & 1u) diag[own + r] += shift;
 }
+static void launch_shift_values(eig_mat_s &A, double shift, i64 G, hipStream_t s);
 void launch_shift_diag(eig_mat_s &A, double shift, hipStream_t s)
 {
   box_invalidate(A);  // (the box image copies the band values; rebuilt at its next use)
-  if (A.sym_pack)      // (so does the packed value image of the value march)
-  {
-    EIG_HIP(hipStreamSynchronize(s));
-    (void)hipFree(A.sym_pack);
-    A.sym_pack = nullptr;
-  }
   A.diag_sum += shift * (double)A.diag_count;
   const i64 G = (A.nb_rows + 255) / 256;
   if (G == 0) return;
+  launch_shift_values(A, shift, G, s);
+  // the packed value image of the value march copies the band values too: refilled in place after the
+  // shift (same buffer, so a hipGraph captured over the march stays valid)
+  if (A.sym_pack) sym_pack_fill(A, s);
+}
+static void launch_shift_values(eig_mat_s &A, double shift, i64 G, hipStream_t s)
+{
   hipLaunchKernelGGL(k_shift_diag, dim3((unsigned)G), dim3(256), 0, s, A.nb_rows, A.own_offset / A.bc, A.slice_ptr,
                      A.col, A.val, A.br, A.bc, 64 * A.R, shift);
   if (A.sym_val)

@@ -2220,10 +2220,8 @@ __global__ void k_kuhn_pack(i64 ld, const double *__restrict__ val, int4 ja, int
       reinterpret_cast<dpair *>(out)[(i64)q * ld + w] = dpair{val[(i64)j0[q] * ld + w], val[(i64)j1[q] * ld + w]};
 }
 static bool march_kuhn(const eig_mat_s &A);
-const double *sym_pack_prepare(const eig_mat_s &Ac)
+void sym_pack_fill(eig_mat_s &A, hipStream_t s)
 {
-  eig_mat_s &A = const_cast<eig_mat_s &>(Ac);
-  if (A.sym_pack) return A.sym_pack;
   if (A.sym_box27 == kKuhn15)
   {
     // band array of each upper Kuhn offset (the 27-box positions 13 14 | 16 17 | 22 23 | 25 26)
@@ -2233,20 +2231,32 @@ const double *sym_pack_prepare(const eig_mat_s &Ac)
     for (int k = 0; k < A.sym_nd; ++k)
       for (int q = 13; q < 27; ++q)
         if ((i64)(q / 9 - 1) * D + (i64)((q / 3) % 3 - 1) * A.sym_gx + (q % 3 - 1) == A.sym_off[k]) j[q] = A.sym_dj[k];
-    EIG_HIP(hipMalloc(&A.sym_pack, (size_t)A.sym_ld * 64));
-    hipLaunchKernelGGL(k_kuhn_pack, dim3(2048), dim3(256), 0, A.ctx->stream, A.sym_ld, A.sym_val,
+    hipLaunchKernelGGL(k_kuhn_pack, dim3(2048), dim3(256), 0, s, A.sym_ld, A.sym_val,
                        make_int4(j[13], j[14], j[16], j[17]), make_int4(j[22], j[23], j[25], j[26]), A.sym_pack);
     EIG_HIP(hipGetLastError());
-    return A.sym_pack;
+    return;
   }
   const SellB1 b = sell_b1(A);
   const SymImg &S = b.sym;
   const double *UD = S.val + (i64)S.dj[S.nd - 1] * S.ld, *U1 = S.val + (i64)S.j1 * S.ld;
   const double *U0 = S.j0 >= 0 ? S.val + (i64)S.j0 * S.ld : nullptr;
   const double *Uq = S.khi < S.nd - 1 ? S.val + (i64)S.dj[S.khi] * S.ld : nullptr;
-  EIG_HIP(hipMalloc(&A.sym_pack, (size_t)S.ld * 32));
-  hipLaunchKernelGGL(k_sym_pack, dim3(2048), dim3(256), 0, A.ctx->stream, S.ld, UD, U0, U1, Uq, A.sym_pack);
+  hipLaunchKernelGGL(k_sym_pack, dim3(2048), dim3(256), 0, s, S.ld, UD, U0, U1, Uq, A.sym_pack);
   EIG_HIP(hipGetLastError());
+}
+
+// The value pack, built at the first launch that marches on it (never by a plan made for a query:
+// eig_mat_get_info, kernel names, byte models).  eig_lanczos_capture builds it before capturing,
+// so no graph records the pack kernel; a shift refills the same buffer in place.
+const double *sym_pack_prepare(const eig_mat_s &Ac)
+{
+  eig_mat_s &A = const_cast<eig_mat_s &>(Ac);
+  if (A.sym_pack) return A.sym_pack;
+  const i64 bytes = A.sym_ld * (A.sym_box27 == kKuhn15 ? 64 : 32);
+  EIG_HIP(hipMalloc(&A.sym_pack, (size_t)bytes));
+  A.sym_pack_bytes = bytes;
+  A.device_bytes += bytes;
+  sym_pack_fill(A, A.ctx->stream);
   return A.sym_pack;
 }
 
@@ -2289,11 +2299,14 @@ static bool march_kuhn(const eig_mat_s &A)
   return A.sym_box27 == kKuhn15 && A.sym_nd == 15 && !A.ctx->distributed() && A.sym_gx % 64 == 0 &&
          A.window * 16 < (i64(1) << 31) && A.sym_ld * 8 < (i64(1) << 31) && A.tune_march_prefetch != 1;
 }
+bool kuhn_pack_fits(const eig_mat_s &A) { return A.sym_ld * 64 < (i64(1) << 31); }
 static int march_uniform(const eig_mat_s &A, bool fused = false, i64 nplanes = 0)
 {
   // the Kuhn march on its value pack (16) by default: fused step 256^3 346 us, eig_mv 292 us (the arrays,
   // 12: 407 / 330 us; profiles/r04d_p1k.jsonl); tune value 14 = the arrays
-  if (march_kuhn(A)) return A.tune_march_prefetch == 14 ? 12 : A.tune_march_prefetch == 15 ? 19 : 16;
+  // (the pack is read through one 32-bit buffer descriptor of 64 B per row: larger grids take the arrays)
+  if (march_kuhn(A))
+    return A.tune_march_prefetch == 14 || !kuhn_pack_fits(A) ? 12 : A.tune_march_prefetch == 15 ? 19 : 16;
   const bool geo2 = A.sym_geo && A.sym_gx % 64 == 0 && A.window * 16 < (i64(1) << 31);
   if (!A.sym_uniform || (A.kflags & EIG_MAT_NO_UNIFORM))
   {
@@ -2375,8 +2388,9 @@ bool march_geometry(const eig_mat_s &A, i64 &D, int chunk)
 // [zb, ze): plane range of a split launch (the interior planes of a distributed slab); ze < 0 =
 // the whole matrix.
 // chunk: rows per wave column (64 for the scalar kernels, 16 for the 8-column SpMM).
+// pack: build the value pack the plan's variant streams (launch paths only; a query leaves it unbuilt)
 static MarchPlan march_plan(const eig_mat_s &A, int mode, i64 zb = 0, i64 ze = -1, bool fused = false,
-                            int chunk = 64)
+                            int chunk = 64, bool pack = false)
 {
   MarchPlan mp{};
   if (mode != kSymN8 && mode != kSymN32) return mp;
@@ -2452,7 +2466,7 @@ static MarchPlan march_plan(const eig_mat_s &A, int mode, i64 zb = 0, i64 ze = -
     mp.cq = khi < A.sym_nd - 1 ? A.sym_uc[A.sym_dj[khi]] : 0.0;
   }
   mp.uni = uni;
-  mp.pack = uni == 15 || uni == 16 || uni == 18 || uni == 19 ? sym_pack_prepare(A) : nullptr;
+  mp.pack = pack && (uni == 15 || uni == 16 || uni == 18 || uni == 19) ? sym_pack_prepare(A) : nullptr;
   // measured (tools/march_copy.hip *_pp, profiles/r03bo_march_copy.jsonl): the step's ping-pong at
   // 128^3 (2 x 32 MB of pairs) 12.9 us with plain stores vs 17.6 us nontemporal; at 256^3 (2 x 268
   // MB) no difference either way -- plain stores where every vector a launch touches fits in half
@@ -2479,6 +2493,17 @@ int march_variant(const eig_mat_s &A, bool fused)
 
 const i32 kMarchInteriorTag = 0;
 
+void march_prepare(const eig_mat_s &A)
+{
+  if (A.br != 1 || A.bc != 1) return;
+  const int mode = image_mode(A);
+  for (bool fused : {false, true})
+  {
+    (void)march_plan(A, mode, 0, -1, fused, 64, true);
+    if (A.mz1 > A.mz0) (void)march_plan(A, mode, A.mz0, A.mz1, fused, 64, true);
+  }
+}
+
 bool march_split_active(const eig_mat_s &A)
 {
   return A.mz1 > A.mz0 && march_plan(A, image_mode(A), A.mz0, A.mz1).nseg > 0;
@@ -2491,11 +2516,11 @@ static MarchPlan launch_plan(const eig_mat_s &A, int mode, const i32 *slices, i6
 {
   if (slices == &kMarchInteriorTag)
   {
-    const MarchPlan mp = march_plan(A, mode, A.mz0, A.mz1, fused);
+    const MarchPlan mp = march_plan(A, mode, A.mz0, A.mz1, fused, 64, true);
     EIG_CHECK(mp.nseg > 0, EIG_ERR_ARG, "interior-plane launch without a march plan");
     return mp;
   }
-  if (!slices && first == 0 && count == A.nslices) return march_plan(A, mode, 0, -1, fused);
+  if (!slices && first == 0 && count == A.nslices) return march_plan(A, mode, 0, -1, fused, 64, true);
   return MarchPlan{};
 }
 
@@ -2779,9 +2804,20 @@ void lanczos_kernel_info(const eig_mat_s &A, bool fused, std::string &name, i64 
   }
   else
   {
-    bytes = 12 * A.nnzb + 4 * (n + 1) + vec;
+    bytes = sell_image_bytes(A) + vec;
     name = fused ? "k_lanczos_fused_b1" : "k_lanczos_spmv_b1";
   }
+}
+
+// Bytes the SELL-64 slice kernels stream per pass over the image (one row per lane): every padded
+// value, the 4-B column index of each explicit-slice entry, per stencil slice its width and 8
+// offsets (36 B) and a 1-B mask per row, and the slice pointers -- not SURVEY 8(d)'s CSR count (the
+// stencil slices read no column indices).
+i64 sell_image_bytes(const eig_mat_s &A)
+{
+  const i64 bb = (i64)A.br * A.bc, C = 64 * (i64)A.R;
+  return 8 * bb * A.nnzb_padded + 4 * A.sell_explicit + 8 * (A.nslices + 1) +
+         (A.n_stencil_slices ? 4 * A.nslices + A.n_stencil_slices * (32 + C) : 0);
 }
 
 // EIG_LANCZOS_AUTO: the fused step on every 1x1 image.  (Round 3 took the two-kernel step on

@@ -1025,7 +1025,7 @@ def image_bytes(M, op, m=8):
         if band and M.kernel("spmv") == "k_spmv_march":
             v = info.march_variant_mv
             if v >= 10:  # the value marches: band values streamed, geometric masks (no mask stream)
-                return 8 * (4 if v == 15 else info.sym_arrays) * n + 16 * n
+                return 8 * (4 if v in (15, 18) else info.sym_arrays) * n + 16 * n
             if v >= 1:
                 # uniform band: the values ride in the arguments (2..9: the row masks are geometric too)
                 return (0 if v >= 2 else info.sym_mask_bytes * n) + 16 * n

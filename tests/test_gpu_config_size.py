@@ -122,3 +122,43 @@ def test_dot_diag_128cubed(ctx):
     got = dp.get(m)
     assert np.abs(got - ref).max() <= 1e-13 * np.abs(ref).max() + 1e-10
     Q1.free(), Q2.free()
+
+
+def test_c2_eigenpairs_128cubed(ctx):
+    """Config C2 at its size, eigenpairs of a converged run (the reference's ARPACK path,
+    arpack_geneo_wrapper.hh:621-632, returns eigenpairs): the 4 smallest eigenpairs
+    of the 3-D Poisson 128^3 matrix by block Lanczos (k = 32, 8 block steps) on A^-1 with the A solve by
+    multigrid to a residual <= 1e-13, against the analytic spectrum of the 7-point Laplacian,
+    4 sum_d sin^2(k_d pi / (2 (N + 1))): (1,1,1) and the triple (2,1,1), relative 1e-10; and each Ritz
+    vector's residual ||A y - lambda y|| (oracle row loop on the host) <= 1e-6 lambda ||y||."""
+    N = 128
+    n = N ** 3
+    rp, c, v = eigmi.gen_matrix(eigmi.GEN_POISSON3D, N)
+    K = eigmi.Matrix.from_bcsr(ctx, rp, c, v)
+    Id = eigmi.Matrix.from_bcsr(ctx, np.arange(n + 1, dtype=np.int64), np.arange(n, dtype=np.int32), np.ones(n))
+    mg = eigmi.Multigrid(K, (N, N, N), max_cols=32, smooth_degree=2, smooth_ratio=5.0)
+    B, X = ctx.zeros(n * 32), ctx.zeros(n * 32)
+    ctx.check(eigmi.lib.eig_fill_normal(ctx.h, n * 32, 5, B.ptr))
+    cycles = None
+    for cy in (8, 12, 16, 20, 24):
+        r = mg.solve(32, B, X, cy, resid=True)
+        if r <= 1e-13:
+            cycles = cy
+            break
+    B.free(), X.free()
+    assert cycles is not None, "multigrid did not reach 1e-13"
+    bl = eigmi.BlockLanczos(K, Id, block=32, max_steps=8, Ks=K, sigma=0.0, mg=mg, cycles=cycles, seed=123)
+    bl.step(8)
+    ev, Y, res = bl.ritz(4, eigmi.WHICH_SA, want_evec=True)
+    s = 4 * np.sin(np.arange(1, 6) * np.pi / (2 * (N + 1))) ** 2
+    lam = np.sort((s[:, None, None] + s[None, :, None] + s[None, None, :]).ravel())[:4]
+    rel = np.abs(np.asarray(ev) - lam) / lam
+    A = oracle.CSR(n, rp, c, v)
+    rres = [np.linalg.norm(oracle.csr_mv(A, y) - l * y) / (l * np.linalg.norm(y)) for l, y in zip(ev, Y)]
+    print(f"C2 128^3 smallest eigenpairs ({cycles} MG cycles): rel err {rel}, residuals {rres}, ritz res {res}")
+    assert rel.max() <= 1e-10
+    assert max(rres) <= 1e-6
+    bl.close()
+    mg.close()
+    Id.close()
+    K.close()

@@ -131,8 +131,8 @@ def test_value_march_bitwise(ctx, mat):
 @pytest.mark.gpu
 def test_value_march_after_shift(ctx):
     """A += sigma I updates the band values the value marches stream (StandardLargest's shift,
-    eigensolver.hh:59-66), the value pack included (built at first use, dropped by the shift and
-    rebuilt): eig_mv bitwise the shifted reference matrix on every variant, and the fused step's alpha /
+    eigensolver.hh:59-66), the value pack included (built at first use, refilled in place by the
+    shift): eig_mv bitwise the shifted reference matrix on every variant, and the fused step's alpha /
     beta bitwise equal across the variants (same rows per wave)."""
     A = varcoef(64)
     M = eigmi.Matrix.from_bcsr(ctx, A.rowptr, A.col, A.val)
@@ -192,34 +192,80 @@ def test_value_march_256_bitwise(ctx, v256):
     assert np.array_equal(M.mv_host(x), oracle.csr_mv(A, x))
 
 
-@pytest.mark.gpu
-def test_value_march_256_lanczos(ctx, v256):
-    """The benchmark step on the value-streaming image at 256^3: 3 fused steps vs orc_lanczos_fused
-    and 4 classic steps vs orc_lanczos_rotating (rtol 1e-12), then 30 fused GPU steps against the
-    two-kernel GPU recurrence (rtol 1e-11)."""
-    N, M, A = v256
-    n = N ** 3
+FULL_STEPS = 60  # fused steps compared with the restatement at 256^3 (the oracle: ~10 steps / s)
+
+
+def fused_vs_oracle(M, A, steps):
+    """`steps` fused GPU steps (the benchmark's kernel) against orc_lanczos_fused on the same matrix
+    and start vector -- GPU against the CPU restatement, no GPU-vs-GPU step -- rtol 1e-12."""
+    n = A.n
     U0 = np.zeros(n)
     oracle.lib.orc_random_vec(n, 123, U0)
-    fa, fb, _ = eigmi.lanczos_run(M, 3, seed=123, fused=True)
-    ra, rb = oracle.lanczos_fused(A, U0, 3)
+    fa, fb, _ = eigmi.lanczos_run(M, steps, seed=123, fused=True)
+    ra, rb = oracle.lanczos_fused(A, U0, steps)
+    assert fa.size == steps and rb.size == steps + 1
+    da = np.max(np.abs(fa - ra) / np.abs(ra))
+    db = np.max(np.abs(fb[1:] - rb[1:]) / np.abs(rb[1:]))
+    print(f"{steps} fused steps vs orc_lanczos_fused: max rel diff alpha {da:.2e}, beta {db:.2e}")
     assert np.allclose(fa, ra, rtol=1e-12, atol=0) and np.allclose(fb, rb, rtol=1e-12, atol=0)
+    return U0
+
+
+@pytest.mark.gpu
+def test_value_march_256_lanczos(ctx, v256):
+    """The benchmark step on the value-streaming image at 256^3 (kind 8, march variant 15): 60 fused
+    steps vs orc_lanczos_fused and 4 classic steps vs orc_lanczos_rotating, rtol 1e-12."""
+    N, M, A = v256
+    n = N ** 3
+    assert M.info.march_variant == 15
+    U0 = fused_vs_oracle(M, A, FULL_STEPS)
     ca, cb, _ = eigmi.lanczos_run(M, 4, seed=123)
     u1, u2 = np.zeros(n), np.zeros(n)
     qa, qb = np.zeros(4), np.zeros(5)
     oracle.lib.orc_lanczos_rotating(n, A.rowptr, A.col, A.val, 4, U0, u1, u2, qa, qb)
     assert np.allclose(ca, qa, rtol=1e-12, atol=0) and np.allclose(cb, qb, rtol=1e-12, atol=0)
-    fa, fb, _ = eigmi.lanczos_run(M, 30, seed=123, fused=True)
-    ca, cb, _ = eigmi.lanczos_run(M, 30, seed=123)
-    assert np.allclose(fa, ca, rtol=1e-11) and np.allclose(fb, cb, rtol=1e-11)
+
+
+@pytest.fixture(scope="module")
+def p256a(ctx):
+    """The benchmark's exact image: 3-D Poisson 256^3 uploaded with EIG_MAT_NO_UNIFORM (every band
+    value streamed from HBM on every step; bench.py --image arrays, the default)."""
+    N = 256
+    rp, c, v = eigmi.gen_matrix(eigmi.GEN_POISSON3D, N)
+    M = eigmi.Matrix.from_bcsr(ctx, rp, c, v, flags=eigmi.MAT_NO_UNIFORM)
+    yield N, M, oracle.CSR(N ** 3, rp, c, v)
+    M.close()
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kind,N", [(eigmi.GEN_P1STIFF3D, 64), (eigmi.GEN_P1MASS3D, 64), (eigmi.GEN_P1STIFF3D, 128)])
+def test_bench_image_256_spmv_bitwise(ctx, p256a):
+    """eig_mv (BCRSMatrix::mv, kernels_cpp.hh:596-621) on the benched image, bitwise the oracle row loop."""
+    N, M, A = p256a
+    info = M.info
+    assert info.sym_uniform == 0 and info.march_variant == 15 and info.march_variant_mv == 0
+    x = np.random.default_rng(21).standard_normal(N ** 3)
+    assert np.array_equal(M.mv_host(x), oracle.csr_mv(A, x))
+
+
+@pytest.mark.gpu
+def test_bench_image_256_fused_steps(ctx, p256a):
+    """The benched kernel (k_lanczos_fused_march<.., 15> on the Poisson 256^3 arrays image): 60 fused
+    steps vs orc_lanczos_fused, rtol 1e-12 (arpack_geneo_wrapper.hh:621-632 drives the same recurrence
+    through ARPACK's dsaupd)."""
+    N, M, A = p256a
+    assert M.lanczos_kernel_info(True) == ("k_lanczos_fused_march", 64 * N ** 3)
+    fused_vs_oracle(M, A, FULL_STEPS)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,N", [(eigmi.GEN_P1STIFF3D, 64), (eigmi.GEN_P1MASS3D, 64), (eigmi.GEN_P1STIFF3D, 128),
+                                    (eigmi.GEN_P1STIFF3D_VAR, 64), (eigmi.GEN_P1MASS3D_VAR, 64)])
 def test_kuhn_box_march(ctx, kind, N):
     """The P1 Kuhn 15-point box march (march variants 16 / 12, config C5's K and M): eig_mv bitwise the
     reference row loop; the fused and classic recurrences within 1e-12 of their restatements and of
-    the row kernels (EIG_TUNE_MARCH_PREFETCH = 1: no march) at every plane-run count."""
+    the row kernels (EIG_TUNE_MARCH_PREFETCH = 1: no march) at every plane-run count.  Kinds 9 / 10
+    (variable coefficients: every entry of an offset differs, so a mirrored lower value read from the
+    wrong row would show) as well as the constant-coefficient kinds 6 / 7."""
     rp, c, v = eigmi.gen_matrix(kind, N)
     A = oracle.CSR(N ** 3, rp, c, v)
     M = eigmi.Matrix.from_bcsr(ctx, rp, c, v)

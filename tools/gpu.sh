@@ -29,6 +29,14 @@
 #   csr                  general (scrambled + RCM) 256^3 matrix: SpMV / Lanczos kernels  -> csr.jsonl
 #   csrpmc               the same under a kernel trace and FETCH_SIZE / WRITE_SIZE passes -> csrpmc/
 #   commself             bench.py with and without a one-rank RCCL allreduce per step (eager / graph, 128^3 / 256^3)
+#   sweep                tools/lanczos_sweep.py $SWEEP (e.g. SWEEP="--N 256 --matrix p1k --variants fused,mv") -> sweep.jsonl
+#   sweeppmc             the same $SWEEP under a kernel trace, then FETCH_SIZE / WRITE_SIZE passes -> sweeppmc/
+#   sweepsq              SQ wave-cycle buckets + TA busy over $SWEEP                    -> sweepsq/
+#   p1kpmc               P1 Kuhn K 256^3 fused step + eig_mv: trace, FETCH_SIZE, WRITE_SIZE -> sweeppmc/
+#   round                tests smoke profile bench (the round-end evidence set)
+#
+# Session scripts of earlier rounds (tools/gpu_r04*.sh) are these tasks chained, e.g.
+#   TAG=r05a bash tools/gpu.sh tests:test_gpu_value_march.py sweep sweeppmc
 set -o pipefail
 TAG=${TAG:-scratch}
 O=gpurun_out/$TAG
@@ -153,6 +161,26 @@ run_task() {
         python3 tools/csr_general.py --reps 10 --steps 20 > /dev/null 2> "$O/csrpmc_f.err" && \
       timeout -s KILL 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/csrpmc/write" -o pmc -- \
         python3 tools/csr_general.py --reps 10 --steps 20 > /dev/null 2> "$O/csrpmc_w.err" ;;
+    sweep)
+      timeout -k 10 300 python3 tools/lanczos_sweep.py $SWEEP > "$O/sweep.jsonl" 2> "$O/sweep.err" ;;
+    sweeppmc)
+      prof_env
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/sweeppmc/trace" -o trace -- \
+        python3 tools/lanczos_sweep.py $SWEEP > "$O/sweeppmc.jsonl" 2> "$O/sweeppmc_t.err" && \
+      timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/sweeppmc/fetch" -o pmc -- \
+        python3 tools/lanczos_sweep.py $SWEEP > /dev/null 2> "$O/sweeppmc_f.err" && \
+      timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/sweeppmc/write" -o pmc -- \
+        python3 tools/lanczos_sweep.py $SWEEP > /dev/null 2> "$O/sweeppmc_w.err" ;;
+    sweepsq)
+      prof_env
+      timeout -s KILL 150 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_VMEM --output-format csv -d "$O/sweepsq/sq" -o pmc -- \
+        python3 tools/lanczos_sweep.py $SWEEP > /dev/null 2> "$O/sweepsq_sq.err" && \
+      timeout -s KILL 150 rocprofv3 --pmc TA_TA_BUSY_sum TA_BUSY_avr --output-format csv -d "$O/sweepsq/ta" -o pmc -- \
+        python3 tools/lanczos_sweep.py $SWEEP > /dev/null 2> "$O/sweepsq_ta.err" ;;
+    p1kpmc)
+      SWEEP="--N 256 --matrix p1k --rounds 1 --steps 10 --variants fused,mv" run_task sweeppmc ;;
+    round)
+      run_task tests && run_task smoke && run_task profile && run_task bench ;;
     *)
       echo "unknown task $1" >&2; return 2 ;;
   esac
