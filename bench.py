@@ -268,6 +268,8 @@ def comm_summary(ctx, world, ab_check):
             "halo_groups": cc["halo_groups"], "transport_check": ab_check or None}
 
 
+MAILBOX_KINDS = ("xgmi-mailbox", "xgmi-mailbox-step")  # eig_comm_info: a validated mailbox in use
+
 VARIANT_NAME = {"fused": "fused one-reduction step", "pipelined": "pipelined one-reduction step",
                 "classic": "SpMV + update kernels"}
 # matrix images (eig_mat_create_bcsr_ex flags)
@@ -408,10 +410,12 @@ def main():
     ap.add_argument("--comm-self", action="store_true",
                     help="one GPU: attach a one-rank RCCL communicator with EIG_COMM_ALWAYS, so every step's "
                          "allreduce runs through ncclAllReduce (the transport's per-step cost without xGMI)")
-    ap.add_argument("--allreduce", choices=["auto", "rccl", "mailbox"], default="auto",
-                    help="N > 1: the step's allreduce transport -- ncclAllReduce, or the xGMI mailbox (one "
+    ap.add_argument("--allreduce", choices=["auto", "rccl", "mailbox", "mailbox-step"], default="auto",
+                    help="N > 1: the step's allreduce transport -- ncclAllReduce, the xGMI mailbox (one "
                          "launch stores the 3 sums into every peer's mailbox; set up and validated by all "
-                         "ranks, else RCCL); auto = both in the trial, the faster wins")
+                         "ranks, else RCCL), or mailbox-step (the fused step's sums published by its last "
+                         "workgroup and gathered in the next launch's prologue: no allreduce launch); auto = "
+                         "all in the trial, the fastest whose alpha / beta match the RCCL run wins")
     ap.add_argument("--launch", choices=["auto", "graph", "eager"], default="auto",
                     help="timed steps as one hipGraph replay or launched one by one; auto = graph when "
                          "N > 1 (host-bound halo/allreduce calls), eager at N = 1 (measured faster there)")
@@ -441,7 +445,13 @@ def main():
     # refuses two ranks on one device with ncclInvalidUsage at ncclCommInitRank, profiles/r04t_*)
     ctx = eigmi.Context(int(os.environ.get("EIGMI_FORCE_DEVICE", local)))
     if world == 1 and args.comm_self:
-        ctx.comm_init(1, 0, eigmi.Context.unique_id(), always=True)
+        # one-rank RCCL communicator (+ the mailbox unless --allreduce rccl): the transports' per-step
+        # cost on one GPU
+        ctx.comm_init(1, 0, eigmi.Context.unique_id(), mailbox=args.allreduce != "rccl", always=True)
+        if args.allreduce not in ("auto",):
+            ctx.select_allreduce(args.allreduce)
+        elif not args.rehearse_trial:
+            ctx.select_allreduce("rccl")
     if world > 1:
         import torch
         uid = eigmi.Context.unique_id() if rank == 0 else bytes(128)
@@ -492,11 +502,18 @@ def main():
             # "whole" = the exchange first, then one launch (EIG_TUNE_HALO; no second launch's fixed
             # cost) -- N > 1 only, one GPU has no halo
             halos = ("split", "whole") if world > 1 else ("split",)
-            have_mb = world > 1 and ctx.comm_info()["allreduce"] == "mailbox"
-            ars = (("rccl", "mailbox") if args.allreduce == "auto" else (args.allreduce,)) if have_mb else ("rccl",)
-            for var, halo, ar in [(v, h, a) for v in ("fused", "pipelined") for h in halos for a in ars]:
+            multi = world > 1 or args.comm_self
+            have_mb = multi and ctx.comm_info()["allreduce"] in MAILBOX_KINDS
+            ars = ((("rccl", "mailbox", "mailbox-step") if args.allreduce == "auto" else (args.allreduce,))
+                   if have_mb else ("rccl",))
+            if "rccl" not in ars:
+                ars = ("rccl",) + ars  # the reference run of the alpha / beta check
+            # (the pipelined step keeps the allreduce launch under mailbox-step: same as mailbox)
+            combos = [(v, h, a) for v in ("fused", "pipelined") for h in halos for a in ars
+                      if not (v == "pipelined" and a == "mailbox-step")]
+            for var, halo, ar in combos:
                 M.tune(halo_whole=int(halo == "whole"))
-                if world > 1:
+                if multi:
                     ctx.select_allreduce(ar)
                 # every call below may already have queued a halo exchange or an allreduce on the
                 # other ranks when it fails here, so a failing rank cannot rejoin them at a barrier:
@@ -526,18 +543,23 @@ def main():
                         ms[la] = (time.perf_counter() - t0) / args.trial_steps * 1e3
                     ab[(var, halo, ar)] = tw.tridiag()
                 except eigmi.EigError as e:
-                    print(f"bench: {var} trial failed on rank {rank}: {e}; stopping every rank", file=sys.stderr,
-                          flush=True)
-                    os._exit(3)
+                    if not (ar == "mailbox-step" and e.code == eigmi.EIG_ERR_RCCL):
+                        print(f"bench: {var} trial failed on rank {rank}: {e}; stopping every rank", file=sys.stderr,
+                              flush=True)
+                        os._exit(3)
+                    # a timed-out in-kernel exchange: every rank reads NaN sums and stops at the same
+                    # launch (csrc/xch_dev.h), so the ranks stay in step -- the transport is out
+                    print(f"bench: {var} trial on {ar}: {e}", file=sys.stderr, flush=True)
+                    ms = {la: float("inf") for la in launches}
                 finally:
                     if tw is not None:
                         tw.close()
                 barrier()
+                # a mailbox call that timed out on some rank (its sums read NaN): not a candidate
+                # (checked per combination: selecting a transport clears the recorded timeouts)
+                failed = ar != "rccl" and max_over_ranks(ctx.comm_info()["mailbox_errors"]) > 0
                 for la in launches:
-                    trial[f"{var}/{la}/{halo}/{ar}"] = round(max_over_ranks(ms[la]), 4)
-            if "mailbox" in ars and max_over_ranks(ctx.comm_info()["mailbox_errors"]) > 0:
-                # a mailbox call timed out on some rank (its sums read NaN): not a candidate
-                trial = {k: (float("inf") if k.split("/")[3] != "rccl" else v) for k, v in trial.items()}
+                    trial[f"{var}/{la}/{halo}/{ar}"] = float("inf") if failed else round(max_over_ranks(ms[la]), 4)
             # a transport is a candidate only if its run reproduces the RCCL run of the same variant
             # and halo mode (same start vector, same step count) to AB_RTOL -- never on timing alone
             for (var, halo, ar), (a, b) in ab.items():
@@ -558,13 +580,13 @@ def main():
             if args.launch == "auto":
                 args.launch = best_launch
             M.tune(halo_whole=int(best_halo == "whole"))
-            if world > 1:
+            if multi:
                 ctx.select_allreduce(best_ar)
             halo_mode = best_halo
     if world > 1 and trial is None:
-        # no trial: RCCL unless the mailbox was asked for (and is set up on every rank)
-        ctx.select_allreduce("mailbox" if args.allreduce == "mailbox" and ctx.comm_info()["allreduce"] == "mailbox"
-                             else "rccl")
+        # no trial: RCCL unless a mailbox transport was asked for (and is set up on every rank)
+        ctx.select_allreduce(args.allreduce if args.allreduce in ("mailbox", "mailbox-step") and
+                             ctx.comm_info()["allreduce"] in MAILBOX_KINDS else "rccl")
     fused = variant in ("fused", "pipelined")
     pipelined = variant == "pipelined"
     # the K timed steps are captured as one hipGraph before the clock starts (kernels, halo

@@ -136,7 +136,9 @@ void mailbox_prepare(eig_ctx_t ctx, int nranks, int rank, unsigned char handle[H
   mailbox_free(ctx);
   auto *m = new MailboxHost();
   ctx->mbox = m;
-  const size_t bytes = (size_t)2 * nranks * (1 + kMailboxVals) * sizeof(u64);
+  // k_comm.hip region [2][P][1 + kMailboxVals], then the fused step's region [2][P][kXchWords]
+  const size_t foff = (size_t)2 * nranks * (1 + kMailboxVals);
+  const size_t bytes = (foff + (size_t)2 * nranks * kXchWords) * sizeof(u64);
   // uncached: a peer's stores over xGMI land in HBM and my polling loads must see them while
   // the kernel runs; fine-grained is the fallback where uncached memory cannot be exported
   void *p = nullptr;
@@ -151,7 +153,9 @@ void mailbox_prepare(eig_ctx_t ctx, int nranks, int rank, unsigned char handle[H
   EIG_HIP(hipMemset(m->state, 0, 256));
   m->dev.local = m->local;
   m->dev.ctr = static_cast<u64 *>(m->state);
+  m->dev.fctr = reinterpret_cast<u64 *>(static_cast<char *>(m->state) + 64);
   m->dev.err = reinterpret_cast<int *>(static_cast<char *>(m->state) + 128);
+  m->dev.foff = (long long)foff;
   m->dev.P = nranks;
   m->dev.me = rank;
   hipIpcMemHandle_t h;
@@ -381,7 +385,8 @@ bool all_ranks(eig_ctx_t ctx, bool mine)
 void mailbox_setup_rccl(eig_ctx_t ctx)
 {
   const int P = ctx->nranks, me = ctx->rank;
-  const bool want = P > 1 && P <= kMaxMailboxRanks;
+  // (one rank with EIG_COMM_ALWAYS: the one-GPU rehearsal of the mailbox transports)
+  const bool want = (P > 1 || ctx->comm_always) && P <= kMaxMailboxRanks;
   if (!all_ranks(ctx, want)) return;
   std::vector<unsigned char> h((size_t)P * HIP_IPC_HANDLE_SIZE, 0);
   bool ok = true;
@@ -448,8 +453,7 @@ extern "C" int eig_comm_init_ex(eig_ctx_t ctx, int nranks, int rank, const unsig
         ctx->comm_red = nullptr;
       }
     }
-    // the mailbox allreduce only on request: it is validated between processes on one GPU
-    // (tests/test_mailbox_gpu.py), not yet across xGMI
+    // the mailbox allreduce only on request: set up, validated and agreed by all ranks (else RCCL)
     if (flags & EIG_COMM_MAILBOX) mailbox_setup_rccl(ctx);
   });
 }
@@ -466,25 +470,41 @@ extern "C" int eig_comm_ipc_handle(eig_ctx_t ctx, int nranks, int rank, unsigned
 
 extern "C" int eig_comm_ipc_open(eig_ctx_t ctx, const unsigned char *handles)
 {
+  return eig_comm_ipc_open_ex(ctx, handles, 0);
+}
+
+extern "C" int eig_comm_ipc_open_ex(eig_ctx_t ctx, const unsigned char *handles, int flags)
+{
   return guard(ctx, [&] {
     EIG_CHECK(ctx && handles && ctx->mbox && !ctx->mbox->ready, EIG_ERR_ARG,
               "eig_comm_ipc_open: call eig_comm_ipc_handle first");
+    EIG_CHECK((flags & ~EIG_COMM_ALWAYS) == 0, EIG_ERR_ARG, "eig_comm_ipc_open_ex: unknown flag");
     DeviceGuard dg(ctx->device);
     mailbox_open(ctx, handles);
     ctx->nranks = ctx->mbox->dev.P;
     ctx->rank = ctx->mbox->dev.me;
     ctx->mbox->ready = true;
+    ctx->comm_always = (flags & EIG_COMM_ALWAYS) != 0;
   });
 }
 
 extern "C" int eig_comm_select_allreduce(eig_ctx_t ctx, int kind)
 {
   return guard(ctx, [&] {
-    EIG_CHECK(ctx && (kind == EIG_AR_RCCL || kind == EIG_AR_MAILBOX), EIG_ERR_ARG,
-              "eig_comm_select_allreduce: EIG_AR_RCCL or EIG_AR_MAILBOX");
+    EIG_CHECK(ctx && (kind == EIG_AR_RCCL || kind == EIG_AR_MAILBOX || kind == EIG_AR_MAILBOX_STEP), EIG_ERR_ARG,
+              "eig_comm_select_allreduce: EIG_AR_RCCL, EIG_AR_MAILBOX or EIG_AR_MAILBOX_STEP");
     EIG_CHECK(kind == EIG_AR_RCCL ? ctx->comm != nullptr : (ctx->mbox && ctx->mbox->ready), EIG_ERR_ARG,
               "eig_comm_select_allreduce: that transport is not set up on this context");
-    if (ctx->mbox) ctx->mbox->on = kind == EIG_AR_MAILBOX;
+    if (ctx->mbox)
+    {
+      DeviceGuard dg(ctx->device);
+      EIG_HIP(hipStreamSynchronize(ctx->stream));
+      ctx->mbox->on = kind != EIG_AR_RCCL;
+      ctx->mbox->step = kind == EIG_AR_MAILBOX_STEP;
+      // a new selection starts without a recorded timeout (a poisoned step exchange stays poisoned
+      // until then: xch_dev.h)
+      EIG_HIP(hipMemset(ctx->mbox->dev.err, 0, sizeof(int)));
+    }
   });
 }
 
@@ -496,6 +516,7 @@ extern "C" int eig_comm_info(eig_ctx_t ctx, int *nranks, int *rank, int *allredu
     if (rank) *rank = ctx->rank;
     if (allreduce)
       *allreduce = !ctx->collectives()                 ? EIG_AR_NONE
+                   : ctx->step_exchange()              ? EIG_AR_MAILBOX_STEP
                    : (ctx->mbox && ctx->mbox->ready && ctx->mbox->on) ? EIG_AR_MAILBOX
                    : ctx->loop                         ? EIG_AR_LOOPBACK
                                                        : EIG_AR_RCCL;
@@ -1241,6 +1262,25 @@ extern "C" int eig_mat_create_bcsr_dist_ex(eig_ctx_t ctx, int64_t nb_rows_global
         h.barrier();
         all = h.gather;
         h.barrier();
+      }
+      else if (!ctx->comm && P > 1 && ctx->mbox && ctx->mbox->ready)
+      {
+        // mailbox-only ranks (eig_comm_ipc_open): an allgather as an allreduce of zero-padded rows
+        // (integers below 2^53: the double sums are exact)
+        std::vector<double> g(4 * (size_t)P, 0.0);
+        for (int t = 0; t < 4; ++t) g[4 * me + t] = (double)mine[t];
+        double *d = dev_alloc<double>(g.size());
+        EIG_HIP(hipMemcpy(d, g.data(), g.size() * sizeof(double), hipMemcpyHostToDevice));
+        for (i64 off = 0; off < (i64)g.size(); off += kMailboxVals)
+          launch_mailbox_allreduce(d + off, (int)std::min<i64>(kMailboxVals, (i64)g.size() - off), ctx->mbox->dev,
+                                   kMailboxTimeout, ctx->stream);
+        EIG_HIP(hipStreamSynchronize(ctx->stream));
+        EIG_HIP(hipMemcpy(g.data(), d, g.size() * sizeof(double), hipMemcpyDeviceToHost));
+        (void)hipFree(d);
+        int err = 0;
+        EIG_HIP(hipMemcpy(&err, ctx->mbox->dev.err, sizeof(int), hipMemcpyDeviceToHost));
+        EIG_CHECK(err == 0, EIG_ERR_RCCL, "eig_mat_create_bcsr_dist: mailbox allgather timed out");
+        for (size_t t = 0; t < g.size(); ++t) all[t] = (i64)g[t];
       }
       else if (ctx->comm && P > 1)
       {

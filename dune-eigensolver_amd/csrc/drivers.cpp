@@ -1296,8 +1296,11 @@ void lanczos_step(eig_mat_s &A, double *u, double *up, double *t, int j, Lanczos
 // on the device): P = interleaved pairs of the previous launch (window layout, ghosts exchanged
 // here), the output pairs go to Pout; one allreduce of the launch's three sums.  Events as
 // lanczos_step: ev[0] before, ev[1] after the kernel, ev[2..4] after the allreduce.
+// xch = kXchPublish (EIG_AR_MAILBOX_STEP, xch_dev.h): the kernel's last workgroup allreduces the
+// sums through the peers' mailboxes, no allreduce call here.  (A split step: the boundary launch,
+// which completes the sums.)
 void lanczos_fused_step(eig_mat_s &A, double *P, double *Pout, int L, int force, LanczosBufs &lb, hipEvent_t *ev,
-                        int nev, hipEvent_t halo_ev0, hipEvent_t halo_ev1, bool ev_external)
+                        int nev, hipEvent_t halo_ev0, hipEvent_t halo_ev1, bool ev_external, int xch = 0)
 {
   eig_ctx_t ctx = A.ctx;
   hipStream_t s = ctx->stream;
@@ -1306,16 +1309,18 @@ void lanczos_fused_step(eig_mat_s &A, double *P, double *Pout, int L, int force,
       EIG_HIP(hipEventRecordWithFlags(ev[i], s, ev_external ? hipEventRecordExternal : hipEventRecordDefault));
   };
   double *out = lb.st.fred + 3 * (i64)L;
-  const FusedLaunch fl{lb.st, L, force};
+  FusedLaunch fl{lb.st, L, force, xch & kXchPublish};
+  FusedLaunch fl_first{lb.st, L, force, 0};
   mark(0);
   halo_split(
       A, halo_ev0, halo_ev1, [&](hipStream_t hs) { halo_exchange(A, P, hs, nullptr, 2); },
       [&](const i32 *sl, i64 first, i64 count, int part) {
-        launch_lanczos_fused(A, P, Pout, fl, sl, first, count, part == kPartSecond ? lb.carry : nullptr,
-                             part == kPartFirst ? lb.carry : out, 0, s, ctx->red);
+        launch_lanczos_fused(A, P, Pout, part == kPartFirst ? fl_first : fl, sl, first, count,
+                             part == kPartSecond ? lb.carry : nullptr, part == kPartFirst ? lb.carry : out, 0, s,
+                             ctx->red);
       });
   mark(1);
-  allreduce_sum(ctx, out, 3, s);
+  if (!(xch & kXchPublish)) allreduce_sum(ctx, out, 3, s);
   mark(2);
   mark(3);
   mark(4);
@@ -1465,7 +1470,8 @@ void enqueue_steps(eig_lanczos_s &ws, int steps, int nps, hipEvent_t *ev, bool e
     else if (ws.fused)
     {
       const int L = ws.L + i;
-      lanczos_fused_step(A, ws.B[L & 1]->d(), ws.B[(L + 1) & 1]->d(), L, 0, *ws.lb, e, nps, ws.h0, ws.h1, external);
+      lanczos_fused_step(A, ws.B[L & 1]->d(), ws.B[(L + 1) & 1]->d(), L, 0, *ws.lb, e, nps, ws.h0, ws.h1, external,
+                         A.ctx->step_exchange() ? kXchPublish : 0);
     }
     else
     {
@@ -1476,6 +1482,18 @@ void enqueue_steps(eig_lanczos_s &ws, int steps, int nps, hipEvent_t *ev, bool e
   }
   if (steps > 0) pipe_join(ws);
   EIG_HIP(hipEventRecordWithFlags(ev[1], s, fl));
+}
+
+// The in-kernel exchange of a fused batch: NaN sums mean a peer's exchange timed out (xch_dev.h:
+// then every rank reads NaN -- the same decision on all ranks).  Called after a synchronisation.
+void check_step_exchange(eig_lanczos_s &ws)
+{
+  if (!ws.fused || ws.pipe || ws.L == 0 || !ws.A->ctx->step_exchange()) return;
+  double f[3];
+  EIG_HIP(hipMemcpy(f, ws.lb->st.fred + 3 * (i64)(ws.L - 1), sizeof(f), hipMemcpyDeviceToHost));
+  if (!(std::isfinite(f[0]) && std::isfinite(f[1]) && std::isfinite(f[2])))
+    throw Error(EIG_ERR_RCCL, "fused Lanczos: the in-kernel xGMI exchange of the step sums failed (a peer timed "
+                              "out, or the recurrence produced NaN)");
 }
 
 // Fused workspace: control word of launch L (logical step, mode), read after a synchronisation.
@@ -1499,6 +1517,7 @@ void fused_settle(eig_lanczos_s &ws, int target, int nps, eig_timing *timing)
   for (;;)
   {
     int j, mode;
+    check_step_exchange(ws);
     fused_state(ws, j, mode);
     ws.k = j;
     if (mode == kFusedModeHalt)
@@ -1778,7 +1797,7 @@ extern "C" int eig_lanczos_tridiag(eig_lanczos_t ws, int *k, double *alpha_host,
         }
         else
           lanczos_fused_step(*ws->A, ws->B[ws->L & 1]->d(), ws->B[(ws->L + 1) & 1]->d(), ws->L, 1, *ws->lb, nullptr,
-                             0, ws->h0, ws->h1, false);
+                             0, ws->h0, ws->h1, false, ctx->step_exchange() ? kXchPublish : 0);
         ++ws->L;
       }
       launch_fused_tail(ws->lb->st, ws->L, ctx->stream);

@@ -98,11 +98,14 @@ struct LoopHub {
 // xGMI mailbox allreduce (k_comm.hip): each rank's uncached mailbox, IPC-mapped by every peer.
 constexpr int kMaxMailboxRanks = 16;
 constexpr int kMailboxVals = 63;  // values per call (slot = 1 sequence word + 63 values = 512 B)
+constexpr int kXchWords = 4;       // step region slot (xch_dev.h): sequence number + 3 sums
 struct Mailbox {
-  u64 *local = nullptr;                  // my mailbox: [2][P][1 + kMailboxVals]
+  u64 *local = nullptr;                  // my mailbox: [2][P][1 + kMailboxVals], then the step region
   u64 *peer[kMaxMailboxRanks] = {};      // peer[r] = rank r's mailbox mapped here (peer[me] = local)
   u64 *ctr = nullptr;                    // device: sequence number of the last completed call
+  u64 *fctr = nullptr;                   // device: sequence number of the last fused-step exchange
   int *err = nullptr;                    // device: set when a call timed out
+  long long foff = 0;                    // word offset of the step region [2][P][kXchWords] (xch_dev.h)
   int P = 1, me = 0;
 };
 // Host-side ownership of the mailbox resources of a context.
@@ -113,6 +116,7 @@ struct MailboxHost {
   std::vector<void *> opened;    // IPC-opened peer mappings (closed on destroy)
   bool ready = false;            // peers opened and validated: allreduce_sum uses it
   bool on = true;                // eig_comm_select_allreduce: false = ncclAllReduce although ready
+  bool step = false;             // EIG_AR_MAILBOX_STEP: the fused step exchanges its sums in-kernel
 };
 constexpr unsigned long long kMailboxTimeout = 1000000000ull;  // 10 s of s_memrealtime (100 MHz)
 void launch_mailbox_allreduce(double *buf, int count, const Mailbox &mb, unsigned long long timeout, hipStream_t s);
@@ -142,7 +146,9 @@ struct eig_ctx_s {
   bool comm_always = false;          // EIG_COMM_ALWAYS: collectives through `comm` even at one rank
   bool distributed() const { return nranks > 1 && (comm || loop || (mbox && mbox->ready)); }
   // whether allreduces go through a transport (distributed, or a forced one-rank RCCL communicator)
-  bool collectives() const { return distributed() || (comm_always && comm); }
+  bool collectives() const { return distributed() || (comm_always && (comm || (mbox && mbox->ready))); }
+  // the fused Lanczos step exchanges its three sums inside the step kernel (EIG_AR_MAILBOX_STEP)
+  bool step_exchange() const { return collectives() && !loop && mbox && mbox->ready && mbox->on && mbox->step; }
   // reusable device buffers for drivers (grown on demand)
   std::vector<std::pair<void *, size_t>> pool;
 };
@@ -304,9 +310,11 @@ struct LanczosState {
 enum { kFusedModeStep = 0, kFusedModePost = 1, kFusedModeHalt = 2 };  // ctl[2L + 1]
 struct FusedLaunch {
   LanczosState st;
-  int L;      // launch index
-  int force;  // repair regardless of the prediction (exact final beta, eig_lanczos_tridiag)
+  int L;        // launch index
+  int force;    // repair regardless of the prediction (exact final beta, eig_lanczos_tridiag)
+  int xch = 0;  // kXchPublish: the sums allreduced inside the kernel (EIG_AR_MAILBOX_STEP, xch_dev.h)
 };
+enum { kXchPublish = 2 };
 // P, Pout: interleaved (t, u) pair vectors in window layout (2 doubles per row).
 void launch_lanczos_fused(const eig_mat_s &A, const double *P, double *Pout, const FusedLaunch &fl,
                           const i32 *slices, i64 first, i64 count, const double *carry, double *out, int ticket,

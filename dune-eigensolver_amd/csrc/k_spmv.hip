@@ -14,6 +14,7 @@
 // rows that share x lines stay in one CU / one XCD's L2; 2048 workgroups (8 per CU) are resident.
 #include "internal.h"
 #include "reduce_dev.h"
+#include "xch_dev.h"
 
 namespace eigmi {
 
@@ -624,6 +625,9 @@ struct FusedArgs {
   double *pn;                   // per launch: nsum[j - 1] of its step (LanczosState::pn)
   int L;                        // launch index
   int force;                    // 1: repair even if the prediction is sound (exact final beta)
+  int xch;                      // kXchPublish: the last workgroup allreduces the sums through the
+                                // peers' mailboxes (xch_dev.h) instead of an allreduce launch after
+  Mailbox mb;                   // (xch != 0) this rank's mailbox
 };
 
 struct FusedStep {
@@ -747,6 +751,31 @@ __device__ __forceinline__ void fused_idle(double *out)
   if (blockIdx.x == 0 && threadIdx.x < 3) out[threadIdx.x] = 0.0;
 }
 
+// End of a fused launch: the grid reduction of the three sums (plus a split step's carry) into
+// out; with kXchPublish the last workgroup first allreduces them with the peers through their
+// mailboxes (xch_dev.h), so out holds the global sums when the kernel ends.  An idle launch takes
+// this path with zero sums when it exchanges (every rank idles at the same launch).
+template <int U>
+__device__ __forceinline__ void fused_finish(double (&v)[3], double *partials, unsigned *ticket, double *tot,
+                                             double *out, const double *carry, const FusedArgs &fa)
+{
+  if (grid_sum<3, kStreamThreads, U>(v, partials, ticket, tot))
+  {
+    if (fa.xch & kXchPublish)
+    {
+      if (carry)
+      {
+        if (threadIdx.x < 3) tot[threadIdx.x] += carry[threadIdx.x];
+        __syncthreads();
+      }
+      xch_exchange(fa.mb, tot);
+      if (threadIdx.x < 3) out[threadIdx.x] = tot[threadIdx.x];
+    }
+    else if (threadIdx.x < 3)
+      out[threadIdx.x] = carry ? (carry[threadIdx.x] + tot[threadIdx.x]) : tot[threadIdx.x];
+  }
+}
+
 // Repair launch body for rows [r0, r1) (owned-row indices, grid-stride): u = t - c u_prev into the
 // output pair (u, u_prev), and ||u||^2.  The same mul-then-sub as the gathers (XPair), so the step
 // that follows multiplies exactly the u_k the unrepaired step would have formed.
@@ -846,7 +875,9 @@ __global__ __launch_bounds__(kStreamThreads, fused_b1_waves<MODE>()) void k_lanc
   const FusedStep fs = fused_begin(fa);
   if (fs.act == kFusedHalt || fs.act == kFusedNoop)
   {
-    fused_idle(out);
+    double z[3] = {0.0, 0.0, 0.0};
+    if (fa.xch & kXchPublish) fused_finish<2>(z, partials, ticket, tot, out, nullptr, fa);
+    else fused_idle(out);
     return;
   }
   const double c = fs.c, gam = fs.gam, sig = fs.sig, mu = fs.mu;
@@ -874,10 +905,7 @@ __global__ __launch_bounds__(kStreamThreads, fused_b1_waves<MODE>()) void k_lanc
       }
     }
     double v[3] = {0.0, 0.0, m2};
-    if (grid_sum<3, kStreamThreads>(v, partials, ticket, tot))
-    {
-      if (threadIdx.x < 3) out[threadIdx.x] = carry ? (carry[threadIdx.x] + tot[threadIdx.x]) : tot[threadIdx.x];
-    }
+    fused_finish<2>(v, partials, ticket, tot, out, carry, fa);
     return;
   }
   const XPair xc{P, c};
@@ -933,10 +961,7 @@ __global__ __launch_bounds__(kStreamThreads, fused_b1_waves<MODE>()) void k_lanc
     }
   }
   double v[3] = {d, q2, m2};
-  if (grid_sum<3, kStreamThreads>(v, partials, ticket, tot))
-  {
-    if (threadIdx.x < 3) out[threadIdx.x] = carry ? (carry[threadIdx.x] + tot[threadIdx.x]) : tot[threadIdx.x];
-  }
+  fused_finish<2>(v, partials, ticket, tot, out, carry, fa);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1768,8 +1793,12 @@ __global__ __launch_bounds__(kStreamThreads, march_fused_waves(UNI)) void k_lanc
     if (!begun) fs = fused_begin(fa);
     if (fs.act == kFusedHalt || fs.act == kFusedNoop)
     {
-      fused_idle(out);
-      return;
+      if (!(fa.xch & kXchPublish))
+      {
+        fused_idle(out);
+        return;
+      }
+      d = q2 = m2 = 0.0;
     }
     if (fs.act == kFusedRepair)
     {
@@ -1777,16 +1806,15 @@ __global__ __launch_bounds__(kStreamThreads, march_fused_waves(UNI)) void k_lanc
       m2 = fused_repair_rows(r0, r1, own, fs.c, P, Pout);
     }
     double v[3] = {d, q2, m2};
-    if (grid_sum<3, kStreamThreads, 8>(v, partials, ticket, tot))
-    {
-      if (threadIdx.x < 3) out[threadIdx.x] = tot[threadIdx.x];
-    }
+    fused_finish<8>(v, partials, ticket, tot, out, nullptr, fa);
     return;
   }
   const FusedStep fs = fused_begin(fa);
   if (fs.act == kFusedHalt || fs.act == kFusedNoop)
   {
-    fused_idle(out);
+    double z[3] = {0.0, 0.0, 0.0};
+    if (fa.xch & kXchPublish) fused_finish<8>(z, partials, ticket, tot, out, nullptr, fa);
+    else fused_idle(out);
     return;
   }
   const double c = fs.c, gam = fs.gam, sig = fs.sig, mu = fs.mu;
@@ -1813,10 +1841,7 @@ __global__ __launch_bounds__(kStreamThreads, march_fused_waves(UNI)) void k_lanc
     march_rows<MT, 2, SPAN1, UNI>(A, mp, own, lane, wave, XPair{P, c}, epi);
   }
   double v[3] = {d, q2, m2};
-  if (grid_sum<3, kStreamThreads, 8>(v, partials, ticket, tot))
-  {
-    if (threadIdx.x < 3) out[threadIdx.x] = tot[threadIdx.x];
-  }
+  fused_finish<8>(v, partials, ticket, tot, out, nullptr, fa);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2627,8 +2652,14 @@ void launch_lanczos_fused(const eig_mat_s &A, const double *P, double *Pout, con
                           hipStream_t s, ReduceWS red)
 {
   EIG_CHECK(A.br == 1 && A.bc == 1, EIG_ERR_BLOCKSIZE, "Lanczos driver: 1x1 blocks only");
-  const FusedArgs fa{fl.st.nsum, fl.st.alpha, fl.st.beta, fl.st.fred, fl.st.ctl, fl.st.aux, fl.st.mu2, fl.st.pn, fl.L,
-                     fl.force};
+  FusedArgs fa{fl.st.nsum, fl.st.alpha, fl.st.beta, fl.st.fred, fl.st.ctl, fl.st.aux, fl.st.mu2, fl.st.pn, fl.L,
+               fl.force, 0, Mailbox{}};
+  if (fl.xch)
+  {
+    EIG_CHECK(A.ctx->step_exchange(), EIG_ERR_ARG, "fused step: in-kernel exchange without the mailbox");
+    fa.xch = fl.xch & kXchPublish;
+    fa.mb = A.ctx->mbox->dev;
+  }
   if (!carry)
   {
     const int mode = image_mode(A);
@@ -2672,7 +2703,7 @@ void launch_lanczos_pipe(const eig_mat_s &A, double *T, double *UZ, const double
   EIG_CHECK((own & 1) == 0 && (((uintptr_t)T | (uintptr_t)UZ | (uintptr_t)S) & 15) == 0, EIG_ERR_ARG,
             "pipelined Lanczos: vectors must be 16-B aligned");
   const FusedArgs fa{fl.st.nsum, fl.st.alpha, fl.st.beta, fl.st.fred, fl.st.ctl, fl.st.aux, fl.st.mu2, fl.st.pn, fl.L,
-                     fl.force};
+                     fl.force, 0, Mailbox{}};
   const i64 per = 2LL * kStreamThreads;
   const int G = (int)std::max<i64>(1, std::min<i64>(kStreamBlocks, (n + per - 1) / per));
   hipLaunchKernelGGL(k_lanczos_pipe, dim3(G), dim3(kStreamThreads), 0, s, n, T + own,

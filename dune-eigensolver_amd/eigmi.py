@@ -32,7 +32,7 @@ LANCZOS_FUSED = 4
 LANCZOS_PIPELINED = 8
 LANCZOS_AUTO = 16
 IPC_HANDLE_BYTES = 64
-ALLREDUCE_KINDS = {0: "none", 1: "rccl", 2: "xgmi-mailbox", 3: "loopback"}
+ALLREDUCE_KINDS = {0: "none", 1: "rccl", 2: "xgmi-mailbox", 3: "loopback", 4: "xgmi-mailbox-step"}
 
 
 def _tflags(timed):
@@ -101,6 +101,7 @@ SIGNATURES = {
     "eig_comm_init_loopback": (_int, [_vp, _vp, _int]),
     "eig_comm_ipc_handle": (_int, [_vp, _int, _int, ctypes.c_char_p]),
     "eig_comm_ipc_open": (_int, [_vp, ctypes.c_char_p]),
+    "eig_comm_ipc_open_ex": (_int, [_vp, ctypes.c_char_p, _int]),
     "eig_comm_info": (_int, [_vp, ctypes.POINTER(_int), ctypes.POINTER(_int), ctypes.POINTER(_int),
                              ctypes.POINTER(_int)]),
     "eig_comm_counters": (_int, [_vp, ctypes.POINTER(_i64)]),
@@ -305,9 +306,10 @@ class Context:
         self.check(lib.eig_comm_ipc_handle(self.h, nranks, rank, buf))
         return buf.raw
 
-    def ipc_open(self, handles):
-        """handles: the nranks exported handles concatenated in rank order."""
-        self.check(lib.eig_comm_ipc_open(self.h, bytes(handles)))
+    def ipc_open(self, handles, always=False):
+        """handles: the nranks exported handles concatenated in rank order; always: collectives through
+        the mailbox even at one rank (eig_comm_ipc_open_ex EIG_COMM_ALWAYS)."""
+        self.check(lib.eig_comm_ipc_open_ex(self.h, bytes(handles), COMM_ALWAYS if always else 0))
         info = self.comm_info()
         self.nranks, self.rank = info["nranks"], info["rank"]
 
@@ -315,9 +317,10 @@ class Context:
         self.check(lib.eig_comm_allreduce_sum(self.h, arr.ptr, arr.n if count is None else count))
 
     def select_allreduce(self, kind):
-        """eig_comm_select_allreduce: "rccl" or "mailbox" (the latter set up and validated by
-        comm_init(mailbox=True)); every rank must select the same."""
-        self.check(lib.eig_comm_select_allreduce(self.h, {"rccl": 1, "mailbox": 2}[kind]))
+        """eig_comm_select_allreduce: "rccl", "mailbox" or "mailbox-step" (the mailbox, and the fused
+        Lanczos step's sums exchanged inside the step kernel); the mailbox kinds need it set up and
+        validated (comm_init(mailbox=True) or ipc_open); every rank must select the same."""
+        self.check(lib.eig_comm_select_allreduce(self.h, {"rccl": 1, "mailbox": 2, "mailbox-step": 4}[kind]))
 
     def comm_info(self):
         v = [_int(0) for _ in range(4)]

@@ -37,7 +37,7 @@ enum eig_status {
   EIG_ERR_SHAPE = 1,      /* size mismatch (reference: std::invalid_argument "... does not match") */
   EIG_ERR_BLOCKSIZE = 2,  /* unsupported block size (reference: "only implemented for FieldMatrix<..,1,1>") */
   EIG_ERR_HIP = 3,        /* HIP runtime failure */
-  EIG_ERR_RCCL = 4,       /* RCCL failure */
+  EIG_ERR_RCCL = 4,       /* RCCL failure, or an xGMI mailbox exchange that timed out */
   EIG_ERR_BREAKDOWN = 5,  /* Krylov breakdown (beta == 0) or non-positive pivot in (B-)Gram-Schmidt */
   EIG_ERR_ARG = 6,        /* invalid argument (null handle, negative size, bad enum) */
   EIG_ERR_NODEVICE = 7    /* no HIP device visible */
@@ -90,7 +90,13 @@ int eig_comm_barrier(eig_ctx_t ctx);
  * only -- distributed matrices need RCCL or loopback): every rank exports its handle, the
  * nranks x 64 bytes travel by any side channel (rank order), then every rank opens them. */
 #define EIG_IPC_HANDLE_BYTES 64
-enum eig_allreduce_kind { EIG_AR_NONE = 0, EIG_AR_RCCL = 1, EIG_AR_MAILBOX = 2, EIG_AR_LOOPBACK = 3 };
+/* EIG_AR_MAILBOX_STEP: the mailbox for every allreduce, and the fused Lanczos step
+ * (EIG_LANCZOS_FUSED) exchanges its three sums INSIDE the step kernel: the last workgroup of launch L
+ * stores them into every peer's mailbox, launch L + 1's prologue polls its own mailbox (bounded: a
+ * peer that does not arrive within 2 s makes the sums NaN on every rank and the step call returns
+ * EIG_ERR_RCCL) -- no allreduce launch between two steps. */
+enum eig_allreduce_kind { EIG_AR_NONE = 0, EIG_AR_RCCL = 1, EIG_AR_MAILBOX = 2, EIG_AR_LOOPBACK = 3,
+                          EIG_AR_MAILBOX_STEP = 4 };
 /* Collectives the library has enqueued on its RCCL communicators since eig_comm_init (a captured
  * hipGraph counts once, at capture): out[0] = ncclAllReduce on the main communicator, out[1] =
  * ncclAllReduce on the split one (the pipelined step's overlapped allreduce), out[2] = halo groups
@@ -98,10 +104,15 @@ enum eig_allreduce_kind { EIG_AR_NONE = 0, EIG_AR_RCCL = 1, EIG_AR_MAILBOX = 2, 
 int eig_comm_counters(eig_ctx_t ctx, int64_t out[4]);
 int eig_comm_ipc_handle(eig_ctx_t ctx, int nranks, int rank, unsigned char handle[EIG_IPC_HANDLE_BYTES]);
 int eig_comm_ipc_open(eig_ctx_t ctx, const unsigned char *handles);
+/* flags: EIG_COMM_ALWAYS = route the collectives through the mailbox even at nranks == 1 (a one-rank
+ * mailbox: the one-GPU rehearsal of the transport, as eig_comm_init_ex's flag for RCCL). */
+int eig_comm_ipc_open_ex(eig_ctx_t ctx, const unsigned char *handles, int flags);
 /* nranks / rank / the allreduce in use (eig_allreduce_kind) / mailbox timeouts so far (syncs). */
 int eig_comm_info(eig_ctx_t ctx, int *nranks, int *rank, int *allreduce, int *mailbox_errors);
 /* Switch the allreduce transport of a communicator that has both (RCCL + a validated mailbox):
- * EIG_AR_RCCL or EIG_AR_MAILBOX.  Every rank must select the same one (no collective inside). */
+ * EIG_AR_RCCL, EIG_AR_MAILBOX or EIG_AR_MAILBOX_STEP (the mailbox alone: EIG_AR_MAILBOX or _STEP).
+ * Every rank must select the same one (no collective inside).  Synchronises the stream and clears
+ * the recorded mailbox timeouts. */
 int eig_comm_select_allreduce(eig_ctx_t ctx, int kind);
 
 /* ---------------------------------------------------------------- device memory ------------ */

@@ -1,8 +1,10 @@
 #!/usr/bin/env python3
 """A/B of Lanczos step / SpMV kernel images on one GPU, interleaved rounds in ONE process.
 
-Variant spec "<fused|pipelined|classic|mv>[:<image>][@<runs>][#<pf>]" (runs: plane runs per column of
-the march kernels, pf: the geometric march variant, eig_mat_tune; default automatic) with image one of
+Variant spec "<fused|pipelined|classic|mv>[:<image>][@<runs>][#<pf>][~<transport>]" (runs: plane runs per
+column of the march kernels, pf: the geometric march variant, eig_mat_tune; default automatic;
+transport, with --comm self: the one-rank allreduce of every step -- rccl, mailbox, or step = the
+fused step's sums exchanged inside the step kernel, EIG_AR_MAILBOX_STEP) with image one of
     band     (default) symmetric band image, plane march where the band allows it
     arrays   band image with the values streamed from the band arrays (EIG_MAT_NO_UNIFORM)
     gather   band image, every offset through its own gather (EIG_MAT_BAND_GATHER)
@@ -30,8 +32,10 @@ IMAGES = {"band": 0, "arrays": eigmi.MAT_NO_UNIFORM, "gather": eigmi.MAT_BAND_GA
 
 
 def parse(spec):
-    """"op[:image][@runs][#pf][%cache]" -> (op, image flags, plane runs per column (0 = automatic),
-    geometric march variant (eig_mat_tune EIG_TUNE_MARCH_PREFETCH; 0 = automatic), cache bits)."""
+    """"op[:image][@runs][#pf][%cache][~transport]" -> (op, image flags, plane runs per column (0 =
+    automatic), geometric march variant (eig_mat_tune EIG_TUNE_MARCH_PREFETCH; 0 = automatic), cache
+    bits)."""
+    spec = spec.partition("~")[0]
     spec, _, cache = spec.partition("%")
     spec, _, pf = spec.partition("#")
     spec, _, runs = spec.partition("@")
@@ -49,8 +53,14 @@ def main():
     ap.add_argument("--matrix", choices=["poisson", "varcoef", "p1k", "p1m"], default="poisson",
                     help="7-point Poisson (eig_gen kind 4), the variable-coefficient 7-point (kind 8), or the P1 "
                          "Kuhn stiffness / mass (kinds 6 / 7, config C5's 15-point K and M)")
+    ap.add_argument("--comm", choices=["none", "self"], default="none",
+                    help="self: a one-rank RCCL communicator + mailbox with EIG_COMM_ALWAYS, so every step's "
+                         "allreduce runs through the transport named by the variant's ~suffix (default rccl)")
     args = ap.parse_args()
     ctx = eigmi.Context(0)
+    if args.comm == "self":
+        ctx.comm_init(1, 0, eigmi.Context.unique_id(), mailbox=True, always=True)
+        assert ctx.comm_info()["allreduce"] == "xgmi-mailbox", ctx.comm_info()
     N = args.N
     if args.slab:
         # one rank's share of an 8-way row partition: a standalone N x N x slab 7-point box
@@ -90,6 +100,9 @@ def main():
             op, fl, runs, pf, cache = parse(spec)
             M = mats[fl]
             M.tune(runs, march_prefetch=pf, cache=cache)
+            if args.comm == "self":
+                tr = spec.partition("~")[2] or "rccl"
+                ctx.select_allreduce({"step": "mailbox-step"}.get(tr, tr))
             if op == "mv":  # plain eig_mv (BCRSMatrix::mv) launches
                 if xy is None:
                     xy = (ctx.array(np.random.default_rng(0).standard_normal(n)), ctx.zeros(n))
@@ -117,6 +130,7 @@ def main():
         info = M.info
         ib = eigmi.image_bytes(M, "spmv") + (16 * n if op == "fused" else 0)  # bytes the image streams
         print(json.dumps({"variant": spec, "matrix": args.matrix, "march_variant": info.march_variant,
+                          "comm": args.comm,
                           "image_bytes": ib if op in ("mv", "fused") else None,
                           "image_frac": round(ib / (float(np.median(res[spec]["k_us"])) * 1e3) / 8000, 4)
                           if op in ("mv", "fused") else None,
