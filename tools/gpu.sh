@@ -34,6 +34,8 @@
 #   sweepsq              SQ wave-cycle buckets + TA busy over $SWEEP                    -> sweepsq/
 #   p1kpmc               P1 Kuhn K 256^3 fused step + eig_mv: trace, FETCH_SIZE, WRITE_SIZE -> sweeppmc/
 #   round                tests smoke profile bench (the round-end evidence set)
+#   xch                  the step's allreduce transports on one GPU (one-rank RCCL / mailbox / in-kernel
+#                        mailbox-step): slab and cube sweeps + the bench's N > 1 trial rehearsed -> xch_*.jsonl
 #
 # Session scripts of earlier rounds (tools/gpu_r04*.sh) are these tasks chained, e.g.
 #   TAG=r05a bash tools/gpu.sh tests:test_gpu_value_march.py sweep sweeppmc
@@ -179,6 +181,13 @@ run_task() {
         python3 tools/lanczos_sweep.py $SWEEP > /dev/null 2> "$O/sweepsq_ta.err" ;;
     p1kpmc)
       SWEEP="--N 256 --matrix p1k --rounds 1 --steps 10 --variants fused,mv" run_task sweeppmc ;;
+    xch)
+      timeout -k 10 200 python3 tools/lanczos_sweep.py --N 256 --slab 32 --matrix varcoef --comm self --rounds 3 --steps 40 \
+        --variants fused~rccl,fused~mailbox,fused~step,mv > "$O/xch_slab.jsonl" 2> "$O/xch.err" && \
+      timeout -k 10 200 python3 tools/lanczos_sweep.py --N 256 --comm self --rounds 3 --steps 40 \
+        --variants fused:arrays~rccl,fused:arrays~mailbox,fused:arrays~step > "$O/xch_cube.jsonl" 2>> "$O/xch.err" && \
+      timeout -k 10 300 python bench.py --comm-self --rehearse-trial --no-cpu-baseline --side-steps 0 --general-steps 0 \
+        > "$O/xch_trial.json" 2>> "$O/xch.err" ;;
     round)
       run_task tests && run_task smoke && run_task profile && run_task bench ;;
     *)
