@@ -365,6 +365,9 @@ i64 sell_image_bytes(const eig_mat_s &A);
 void march_prepare(const eig_mat_s &A);
 // whether the P1 Kuhn value pack (64 B per row) fits the 32-bit buffer descriptor march 16 / 19 read it by
 bool kuhn_pack_fits(const eig_mat_s &A);
+// The P1 Kuhn march variant of a matrix the Kuhn march applies to (k_spmv.hip march_uniform): 16 / 19
+// on the value pack, 12 on the band arrays
+int kuhn_variant(const eig_mat_s &A);
 // Whether EIG_LANCZOS_AUTO takes the fused step on this image: every 1x1 image (round 3: without
 // register spills the fused step beats the two-kernel step on scattered images too).
 bool fused_step_pays(const eig_mat_s &A);

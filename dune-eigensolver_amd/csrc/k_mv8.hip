@@ -7,6 +7,8 @@
 // not a reduction, so SpMM / projections are bitwise the reference arithmetic on equal inputs.
 #include <algorithm>
 
+#include <cstdlib>
+
 #include "internal.h"
 #include "reduce_dev.h"
 
@@ -427,11 +429,135 @@ __global__ __launch_bounds__(kStreamThreads) void k_mgs_pass(i64 n, double *__re
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// The same MGS with read-only passes (the default): pass K reads the ORIGINAL block and replays
+// the row updates of steps 0 .. K-1 in registers (the S coefficients of every finished step come
+// from Ssum) before the sums of step K -- per row exactly the operations, in the same order, that
+// the in-place passes above apply one per launch.
+// Only pass 8 writes the block.  Traffic: 9 reads + 1 write of the n x 8 block instead of 9 reads
+// + 9 writes, and the unmodified block stays resident in the 256 MB memory-side cache (MALL) across
+// the passes wherever it fits (plain loads and stores, no streaming hints).  (The rows a lane sums
+// differ from the in-place passes', so the sums agree to rounding, not bitwise.)
+// ---------------------------------------------------------------------------------------------
+// Lane P of each quad (4 lanes = one row) broadcast to the quad: a DPP quad_perm move (VALU, no LDS
+// traffic), two 32-bit halves.
+template <int P>
+__device__ __forceinline__ double quad_bcast(double v)
+{
+  constexpr int ctrl = P | (P << 2) | (P << 4) | (P << 6);  // quad_perm [P, P, P, P]
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)(b & 0xffffffffll), ctrl, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), ctrl, 0xf, 0xf, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+// Steps KP .. K-1 of the row update on one lane's two columns (compile-time pivot: DPP control)
+template <int KP, int K, int N>
+__device__ __forceinline__ void mgs_replay_steps(double2 &v, const double (&sp0)[N], const double (&sp1)[N], int c0,
+                                                 int c1)
+{
+  if constexpr (KP < K)
+  {
+    const double qkp = quad_bcast<(KP >> 1)>((KP & 1) ? v.y : v.x);
+    if (c0 > KP) v.x -= sp0[KP] * qkp;
+    if (c1 > KP) v.y -= sp1[KP] * qkp;
+    if (c0 == KP) v.x *= sp0[KP];
+    if (c1 == KP) v.y *= sp1[KP];
+    mgs_replay_steps<KP + 1, K>(v, sp0, sp1, c0, c1);
+  }
+}
+
+template <int K>
+__global__ __launch_bounds__(kStreamThreads) void k_mgs_replay(i64 n, double *__restrict__ Qb,
+                                                               double *__restrict__ Ssum, double *partials,
+                                                               unsigned *ticket)
+{
+  // quad mapping as k_mgs_pass (4 lanes per row, lane ql holds columns 2 ql, 2 ql + 1: one 16-B
+  // load), the pivot column broadcast inside the quad by DPP instead of LDS shuffles
+  __shared__ double tot[8];
+  const int ql = threadIdx.x & 3;
+  const int c0 = 2 * ql, c1 = c0 + 1;
+  double sp0[K > 0 ? K : 1], sp1[K > 0 ? K : 1];  // this lane's S[kp][c] of every finished step kp
+#pragma unroll
+  for (int kp = 0; kp < K; ++kp)
+  {
+    const double skk = Ssum[kp * 8 + kp];
+    sp0[kp] = (c0 > kp) ? Ssum[kp * 8 + c0] / skk : ((c0 == kp) ? 1.0 / sqrt(skk) : 0.0);
+    sp1[kp] = (c1 > kp) ? Ssum[kp * 8 + c1] / skk : ((c1 == kp) ? 1.0 / sqrt(skk) : 0.0);
+  }
+  double a0 = 0.0, a1 = 0.0;
+  constexpr int U = 8;  // rows per lane per round, loads issued together
+  const i64 stride = (i64)gridDim.x * (kStreamThreads / 4);
+  for (i64 i0 = ((i64)blockIdx.x * kStreamThreads + threadIdx.x) >> 2; i0 < n; i0 += U * stride)
+  {
+    double2 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+    {
+      const i64 i = i0 + u * stride;
+      v[u] = i < n ? reinterpret_cast<const double2 *>(Qb + i * 8)[ql] : make_double2(0.0, 0.0);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+    {
+      // q_j -= S[kp][j] q_kp (j > kp) with the old q_kp, then q_kp *= S[kp][kp] (kernels_cpp.hh:218-228)
+      mgs_replay_steps<0, K>(v[u], sp0, sp1, c0, c1);
+      if constexpr (K == 8)
+      {
+        const i64 i = i0 + u * stride;
+        if (i < n) reinterpret_cast<double2 *>(Qb + i * 8)[ql] = v[u];
+      }
+      else
+      {
+        // (rows past n are zero: they add nothing)
+        const double qk = quad_bcast<(K >> 1)>((K & 1) ? v[u].y : v[u].x);
+        if (c0 >= K) a0 += qk * v[u].x;
+        if (c1 >= K) a1 += qk * v[u].y;
+      }
+    }
+  }
+  if constexpr (K < 8)
+  {
+    double vals[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) vals[j] = (j == c0) ? a0 : ((j == c1) ? a1 : 0.0);
+    if (grid_sum<8, kStreamThreads>(vals, partials, ticket, tot))
+    {
+      if (threadIdx.x < 8) Ssum[K * 8 + threadIdx.x] = (threadIdx.x >= (unsigned)K) ? tot[threadIdx.x] : 0.0;
+    }
+  }
+}
+
 void launch_mgs_pass(i64 n, double *Qb, int k, double *Ssum, int ticket, hipStream_t s, ReduceWS red)
 {
-  const int G = grid_for(n * 4, kStreamThreads * 4, 1024);
-  hipLaunchKernelGGL(k_mgs_pass, dim3(G), dim3(kStreamThreads), 0, s, n, Qb, k, Ssum, red.partials,
-                     red.ticket(ticket));
+  int G = grid_for(n * 4, kStreamThreads * 4, 1024);
+  static const bool inplace = std::getenv("EIGMI_MGS_INPLACE") != nullptr;  // (A/B measurements)
+  if (inplace)
+  {
+    hipLaunchKernelGGL(k_mgs_pass, dim3(G), dim3(kStreamThreads), 0, s, n, Qb, k, Ssum, red.partials,
+                       red.ticket(ticket));
+    return;
+  }
+  // read-only passes: fewer, longer-lived workgroups with 8 rows per lane in flight (the reduction
+  // tail and the prologue amortised over more rows)
+  static const int gmax = [] {
+    const char *e = std::getenv("EIGMI_MGS_GRID");
+    return e ? std::max(64, std::atoi(e)) : 512;
+  }();
+  G = grid_for(n * 4, kStreamThreads * 4, gmax);
+#define EIG_MGS_K(K_)                                                                                        \
+  case K_:                                                                                                   \
+    hipLaunchKernelGGL(k_mgs_replay<K_>, dim3(G), dim3(kStreamThreads), 0, s, n, Qb, Ssum, red.partials,     \
+                       red.ticket(ticket));                                                                  \
+    break;
+  switch (k)
+  {
+    EIG_MGS_K(0) EIG_MGS_K(1) EIG_MGS_K(2) EIG_MGS_K(3) EIG_MGS_K(4) EIG_MGS_K(5) EIG_MGS_K(6) EIG_MGS_K(7)
+    EIG_MGS_K(8)
+    default:
+      throw Error(EIG_ERR_ARG, "mgs pass: k outside 0..8");
+  }
+#undef EIG_MGS_K
 }
 
 // ---------------------------------------------------------------------------------------------

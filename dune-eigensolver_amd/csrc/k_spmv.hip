@@ -1356,7 +1356,14 @@ constexpr unsigned kKuhn15 = (1u << 0) | (1u << 1) | (1u << 3) | (1u << 4) | (1u
 // KP (march variant 16): the values from the Kuhn pack (mp.pack: four arrays of value pairs (0, +1),
 // (+nx, +nx+1), (+D, +D+1), (+D+nx, +D+nx+1) per window row -- 4 instead of 8 16-B/8-B streams and
 // 2 instead of 4 gathers) through 64-bit global addresses, lane 0's edge values by exec-masked loads.
-template <bool KP, class X, class EPI, class PRE>
+// LX (march variant 20, the pack): a workgroup's 4 waves march the SAME 64 x of 4 consecutive lines
+// y0 .. y0 + 3 (instead of 4 x-runs of one line), and every line a wave streams -- its operand line of
+// plane z + 1 and its pack pairs (+nx, +nx+1) of plane z and (+D+nx, +D+nx+1) of plane z - 1 -- goes
+// through LDS to the waves of lines y +- 1 (double-buffered, one barrier per plane): only lines
+// y0 - 1 and y0 + 4 are still gathered from L2, 2 of the 8 line gathers per plane of the workgroup
+// (the gathers that miss L2 were the Kuhn step's 1.32x read excess, profiles/r04af_kuhn_*).  Lines
+// per grid a multiple of 4; the same products in the same order as variant 16 (bitwise).
+template <bool KP, bool LX, class X, class EPI, class PRE>
 __device__ __forceinline__ void march_rows_kuhn(const SellB1 &A, const MarchPlan &mp, i64 own, int lane, int wave,
                                                 X x, EPI &epi, PRE &pre)
 {
@@ -1364,9 +1371,25 @@ __device__ __forceinline__ void march_rows_kuhn(const SellB1 &A, const MarchPlan
   constexpr unsigned SZ = sizeof(raw);
   constexpr unsigned kOut = 0x80000000u;
   const int D = (int)mp.D, own32 = (int)own, gx = mp.gx;
-  const int item = (int)swizzled_block() * kWaves + wave;
-  if (item >= mp.ncol * mp.nseg) return;
-  const int col = item % mp.ncol, seg = item / mp.ncol;
+  int col, seg;
+  if constexpr (LX)
+  {
+    // workgroup -> (x run, group of 4 lines, plane run); workgroup-uniform, so every wave of it reaches
+    // the same barriers
+    const int nxc = gx / 64, per = nxc * (mp.gy / 4);
+    const int wg = (int)swizzled_block();
+    if (wg >= per * mp.nseg) return;
+    seg = wg / per;
+    const int r = wg % per;
+    col = ((r / nxc) * 4 + wave) * nxc + r % nxc;
+  }
+  else
+  {
+    const int item = (int)swizzled_block() * kWaves + wave;
+    if (item >= mp.ncol * mp.nseg) return;
+    col = item % mp.ncol;
+    seg = item / mp.ncol;
+  }
   const int z0 = (int)(mp.zb + seg * mp.nplanes / mp.nseg), z1 = (int)(mp.zb + (seg + 1) * mp.nplanes / mp.nseg);
   const unsigned nbytes = (unsigned)(A.xlast + 1) * SZ;
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(x.ptr()), 0, (int)nbytes, 0x00020000);
@@ -1451,6 +1474,16 @@ __device__ __forceinline__ void march_rows_kuhn(const SellB1 &A, const MarchPlan
     aD1p = below ? ld8(aD1d, vv - Dv) : 0.0;
     aD1pe = below ? ld8(aD1d, vv - Dv + eov) : 0.0;
   }
+  // LX: the line exchange (raw operand line of plane z + 1, pack pairs (+nx, +nx+1) of plane z and
+  // (+D+nx, +D+nx+1) of plane z - 1 per wave), double-buffered by plane parity
+  __shared__ raw lx_c[LX ? 2 : 1][LX ? kWaves : 1][64];
+  __shared__ dpair lx_k1[LX ? 2 : 1][LX ? kWaves : 1][64], lx_k3[LX ? 2 : 1][LX ? kWaves : 1][64];
+  const bool lx_lo = LX && wave > 0, lx_hi = LX && wave < kWaves - 1;  // line y - 1 / y + 1 in this workgroup
+  dpair k3prev = {0.0, 0.0};  // LX: this line's (+D+nx, +D+nx+1) pair of the previous plane
+  if constexpr (LX && KP)
+  {
+    if (below) k3prev = kl(3, 2u * vv - Dk);
+  }
   if (!pre(x)) return;
   double Am = x.val(rAm), Ame = x.val(rAme), A0 = x.val(rA0), A0e = x.val(rA0e), Bm = x.val(rBm), Bme = x.val(rBme),
          Bp = x.val(rBp), Bpe = x.val(rBpe);
@@ -1465,9 +1498,9 @@ __device__ __forceinline__ void march_rows_kuhn(const SellB1 &A, const MarchPlan
       const __amdgpu_buffer_rsrc_t q0 = up ? rs : r0, qp = up ? rp : r0, qm = up ? rm : r0;
       bload(q0, vo + Db, rC0);
       bload(q0, vo + Db + eoff, rC0e);
-      bload(qp, vo + Db + nxb, rCp);
+      if (!lx_hi) bload(qp, vo + Db + nxb, rCp);
       bload(qp, vo + Db + nxb + eoff, rCpe);
-      bload(qm, vo + Db - nxb, rCm);
+      if (!lx_lo) bload(qm, vo + Db - nxb, rCm);
       bload(qm, vo + Db - nxb + eoff, rCme);
     }
     // the row's upper values (once-read streams nontemporal; +nx.. arrays are re-read by line y + 1)
@@ -1483,14 +1516,35 @@ __device__ __forceinline__ void march_rows_kuhn(const SellB1 &A, const MarchPlan
       // mirrored lower entries at line y - 1 (plane z: -nx, -nx-1; plane z - 1: -D-nx, -D-nx-1): the
       // wave-uniform line / plane conditions pick an out-of-range offset (zeros, no traffic)
       const bool ym = yw > 0, dm = dn && yw > 0;
-      const dpair kn = __builtin_bit_cast(
-          dpair, __builtin_amdgcn_raw_buffer_load_b128(kp, (int)(ym ? ko - nxk + kq : kOut), 0, 0));
-      aNl = kn.x, aN1l = kn.y;
+      dpair kn = {0.0, 0.0}, kd = {0.0, 0.0};
+      if (!lx_lo)
+      {
+        kn = __builtin_bit_cast(dpair,
+                                __builtin_amdgcn_raw_buffer_load_b128(kp, (int)(ym ? ko - nxk + kq : kOut), 0, 0));
+        kd = __builtin_bit_cast(
+            dpair, __builtin_amdgcn_raw_buffer_load_b128(kp, (int)(dm ? ko - Dk - nxk + 3u * kq : kOut), 0, 0));
+      }
       aN1le = kle(1, ko - nxk - 16u, le && ym);
-      const dpair kd = __builtin_bit_cast(
-          dpair, __builtin_amdgcn_raw_buffer_load_b128(kp, (int)(dm ? ko - Dk - nxk + 3u * kq : kOut), 0, 0));
-      aDNl = kd.x, aDN1l = kd.y;
       aDN1le = kle(3, ko - Dk - nxk - 16u, le && dm);
+      if constexpr (LX)
+      {
+        // this wave's lines to the workgroup, then the neighbours' from it
+        const int b = z & 1;
+        lx_c[b][wave][lane] = rC0;
+        lx_k1[b][wave][lane] = k1;
+        lx_k3[b][wave][lane] = k3prev;
+        k3prev = k3;
+        __syncthreads();
+        if (lx_hi) rCp = lx_c[b][wave + 1][lane];
+        if (lx_lo)
+        {
+          rCm = lx_c[b][wave - 1][lane];
+          kn = lx_k1[b][wave - 1][lane];
+          kd = dn ? lx_k3[b][wave - 1][lane] : dpair{0.0, 0.0};
+        }
+      }
+      aNl = kn.x, aN1l = kn.y;
+      aDNl = kd.x, aDN1l = kd.y;
     }
     else
     {
@@ -1549,10 +1603,11 @@ template <class MT, int KC, bool SPAN1, int UNI, class X, class EPI, class PRE =
 __device__ __forceinline__ void march_rows(const SellB1 &A, const MarchPlan &mp, i64 own, int lane, int wave,
                                            const X &x, EPI &epi, PRE &&pre = PRE{})
 {
-  static_assert(!UNI || SPAN1 || UNI == 12 || UNI == 16 || UNI == 19, "uniform-band march: far spans of at most one offset");
-  if constexpr (UNI == 12 || UNI == 16 || UNI == 19)
+  static_assert(!UNI || SPAN1 || UNI == 12 || UNI == 16 || UNI == 19 || UNI == 20,
+                "uniform-band march: far spans of at most one offset");
+  if constexpr (UNI == 12 || UNI == 16 || UNI == 19 || UNI == 20)
   {
-    march_rows_kuhn<UNI != 12>(A, mp, own, lane, wave, x, epi, pre);
+    march_rows_kuhn<UNI != 12, UNI == 20>(A, mp, own, lane, wave, x, epi, pre);
     return;
   }
 
@@ -1698,7 +1753,7 @@ __device__ __forceinline__ void march_rows(const SellB1 &A, const MarchPlan &mp,
 
 // y[own + r] = (A x)[r] on the plane march (BCRSMatrix::mv; bitwise k_spmv_b1).
 // resident waves per SIMD of the eig_mv / K1 march kernels (the box march holds ~90 VGPRs)
-constexpr int march_mv_waves(int uni) { return uni == 12 || uni == 16 || uni == 19 ? 5 : 8; }
+constexpr int march_mv_waves(int uni) { return uni == 12 || uni == 16 || uni == 19 || uni == 20 ? 5 : 8; }
 
 template <class MT, bool SPAN1, int UNI>
 __global__ __launch_bounds__(kStreamThreads, march_mv_waves(UNI)) void k_spmv_march(i64 nrows, i64 own, SellB1 A, MarchPlan mp,
@@ -1756,7 +1811,7 @@ __global__ __launch_bounds__(kStreamThreads, march_mv_waves(UNI)) void k_lanczos
 // resident waves per SIMD the fused march kernels are built for (registers: no spills)
 constexpr int march_fused_waves(int uni)
 {
-  return uni == 18 ? 7 : uni == 16 ? 4 : uni == 12 || uni == 19 ? 5 : uni == 11 ? 5 : uni == 10 || uni >= 13 ? 6 : uni == 6 || uni == 9 ? 4 : uni == 5 ? 5 : uni == 4 || uni == 8 ? 6
+  return uni == 18 ? 7 : uni == 16 || uni == 20 ? 4 : uni == 12 || uni == 19 ? 5 : uni == 11 ? 5 : uni == 10 || uni >= 13 ? 6 : uni == 6 || uni == 9 ? 4 : uni == 5 ? 5 : uni == 4 || uni == 8 ? 6
        : uni == 3 || uni == 7 ? 7 : uni ? 8 : 7;
 }
 
@@ -2325,13 +2380,22 @@ static bool march_kuhn(const eig_mat_s &A)
          A.window * 16 < (i64(1) << 31) && A.sym_ld * 8 < (i64(1) << 31) && A.tune_march_prefetch != 1;
 }
 bool kuhn_pack_fits(const eig_mat_s &A) { return A.sym_ld * 64 < (i64(1) << 31); }
+// the Kuhn march on its value pack (16): fused step 256^3 346 us, eig_mv 292 us (the arrays, 12: 407 /
+// 330 us; profiles/r04d_p1k.jsonl); tune value 14 = the arrays, 15 = the pack variant 19.
+// The pack is read through one 32-bit buffer descriptor of 64 B per row: grids of 2^25 rows and
+// more (e.g. 448^3, or 256 x 512 x 512, whose descriptor size would wrap to 0) take the arrays.
+// Default 20 (the pack with the line exchange in LDS) where the lines come in groups of 4: 256^3 fused
+// step 333.2 vs 340.8 us, eig_mv 278.7 vs 292.2 us (profiles/r05g_p1k.jsonl); tune value 13 = 16.
+int kuhn_variant(const eig_mat_s &A)
+{
+  const int tp = A.tune_march_prefetch;
+  if (tp == 14 || !kuhn_pack_fits(A)) return 12;
+  if (tp == 15) return 19;
+  return tp != 13 && A.sym_gy % 4 == 0 ? 20 : 16;
+}
 static int march_uniform(const eig_mat_s &A, bool fused = false, i64 nplanes = 0)
 {
-  // the Kuhn march on its value pack (16) by default: fused step 256^3 346 us, eig_mv 292 us (the arrays,
-  // 12: 407 / 330 us; profiles/r04d_p1k.jsonl); tune value 14 = the arrays
-  // (the pack is read through one 32-bit buffer descriptor of 64 B per row: larger grids take the arrays)
-  if (march_kuhn(A))
-    return A.tune_march_prefetch == 14 || !kuhn_pack_fits(A) ? 12 : A.tune_march_prefetch == 15 ? 19 : 16;
+  if (march_kuhn(A)) return kuhn_variant(A);
   const bool geo2 = A.sym_geo && A.sym_gx % 64 == 0 && A.window * 16 < (i64(1) << 31);
   if (!A.sym_uniform || (A.kflags & EIG_MAT_NO_UNIFORM))
   {
@@ -2357,6 +2421,8 @@ static int march_uniform(const eig_mat_s &A, bool fused = false, i64 nplanes = 0
       hipLaunchKernelGGL((KERN<uint32_t, false, 12>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);     \
     else if (mp.uni == 16)                                                                                \
       hipLaunchKernelGGL((KERN<uint32_t, false, 16>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);     \
+    else if (mp.uni == 20)                                                                                \
+      hipLaunchKernelGGL((KERN<uint32_t, false, 20>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);     \
     else if (mp.uni == 19)                                                                                \
       hipLaunchKernelGGL((KERN<uint32_t, false, 19>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);     \
     else if ((MODE) == kSymN8 && march_span1(A) && mp.uni == 14)                                          \
@@ -2491,7 +2557,7 @@ static MarchPlan march_plan(const eig_mat_s &A, int mode, i64 zb = 0, i64 ze = -
     mp.cq = khi < A.sym_nd - 1 ? A.sym_uc[A.sym_dj[khi]] : 0.0;
   }
   mp.uni = uni;
-  mp.pack = pack && (uni == 15 || uni == 16 || uni == 18 || uni == 19) ? sym_pack_prepare(A) : nullptr;
+  mp.pack = pack && (uni == 15 || uni == 16 || uni == 18 || uni == 19 || uni == 20) ? sym_pack_prepare(A) : nullptr;
   // measured (tools/march_copy.hip *_pp, profiles/r03bo_march_copy.jsonl): the step's ping-pong at
   // 128^3 (2 x 32 MB of pairs) 12.9 us with plain stores vs 17.6 us nontemporal; at 256^3 (2 x 268
   // MB) no difference either way -- plain stores where every vector a launch touches fits in half

@@ -261,7 +261,7 @@ def test_bench_image_256_fused_steps(ctx, p256a):
 @pytest.mark.parametrize("kind,N", [(eigmi.GEN_P1STIFF3D, 64), (eigmi.GEN_P1MASS3D, 64), (eigmi.GEN_P1STIFF3D, 128),
                                     (eigmi.GEN_P1STIFF3D_VAR, 64), (eigmi.GEN_P1MASS3D_VAR, 64)])
 def test_kuhn_box_march(ctx, kind, N):
-    """The P1 Kuhn 15-point box march (march variants 16 / 12, config C5's K and M): eig_mv bitwise the
+    """The P1 Kuhn 15-point box march (march variants 20 / 16 / 12, config C5's K and M): eig_mv bitwise the
     reference row loop; the fused and classic recurrences within 1e-12 of their restatements and of
     the row kernels (EIG_TUNE_MARCH_PREFETCH = 1: no march) at every plane-run count.  Kinds 9 / 10
     (variable coefficients: every entry of an offset differs, so a mirrored lower value read from the
@@ -270,7 +270,7 @@ def test_kuhn_box_march(ctx, kind, N):
     A = oracle.CSR(N ** 3, rp, c, v)
     M = eigmi.Matrix.from_bcsr(ctx, rp, c, v)
     info = M.info
-    assert info.sym_offsets == 15 and info.march_variant == 16, (info.sym_offsets, info.march_variant)
+    assert info.sym_offsets == 15 and info.march_variant == 20, (info.sym_offsets, info.march_variant)
     n = A.n
     assert M.lanczos_kernel_info(True) == ("k_lanczos_fused_march", 8 * info.sym_arrays * n + 32 * n)
     x = np.random.default_rng(13).standard_normal(n)
@@ -280,9 +280,11 @@ def test_kuhn_box_march(ctx, kind, N):
     assert M.info.march_variant == -1
     assert np.array_equal(M.mv_host(x), ref)
     base = {f: eigmi.lanczos_run(M, 25, seed=7, fused=f)[:2] for f in (False, True)}
-    for pf in (0, 14):  # 0: the Kuhn pack (variant 16, default), 14: the arrays (12)
+    # 0: the Kuhn pack with the line exchange in LDS (variant 20, default), 13: the pack alone (16),
+    # 14: the arrays (12)
+    for pf in (0, 13, 14):
         M.tune(march_prefetch=pf)
-        assert M.info.march_variant == (12 if pf else 16)
+        assert M.info.march_variant == {0: 20, 13: 16, 14: 12}[pf]
         for runs in (0, 1, 3, 7):
             M.tune(runs)
             assert np.array_equal(M.mv_host(x), ref), (runs, pf)

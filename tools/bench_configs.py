@@ -213,6 +213,31 @@ def gram(ctx):
         Q.free()
 
 
+def ortho(ctx):
+    """a9 orthonormalize_blocked at C2 size (n = 128^3), m = 8 / 32, best of 5 calls, against the
+    reference's byte model (kernels_cpp.hh:157-175); EIGMI_MGS_INPLACE=1 times the in-place passes."""
+    n = 128 ** 3
+    tag = ("in-place passes" if os.environ.get("EIGMI_MGS_INPLACE") else
+           f"read-only replay passes, grid <= {os.environ.get('EIGMI_MGS_GRID', '512')}")
+    for m in (8, 32):
+        Qh = oracle.random_mv8(n, m, 1)
+        Q = ctx.array(Qh)
+
+        def once():
+            Q.upload(Qh)
+            ctx.sync()
+            t0 = time.perf_counter()
+            eigmi.orthonormalize_mv8(ctx, n, m, Q)
+            ctx.sync()
+            return time.perf_counter() - t0
+        once()
+        tg = min(once() for _ in range(5))
+        ob = eigmi.lib.eig_bytes_orthonormalize_blocked(n, m, 8)
+        emit(config="C2 128^3", op=f"orthonormalize_blocked (MGS, {tag}) m={m}", gpu_ms=round(tg * 1e3, 4),
+             model_bytes=ob, model_GBs=round(ob / tg / 1e9, 1), model_frac=round(ob / tg / 1e9 / PEAK, 4))
+        Q.free()
+
+
 def c3(ctx):
     N = 64
     rp, c, v = eigmi.gen_matrix(eigmi.GEN_Q1ELAST3D, N)

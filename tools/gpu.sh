@@ -34,6 +34,8 @@
 #   sweepsq              SQ wave-cycle buckets + TA busy over $SWEEP                    -> sweepsq/
 #   p1kpmc               P1 Kuhn K 256^3 fused step + eig_mv: trace, FETCH_SIZE, WRITE_SIZE -> sweeppmc/
 #   round                tests smoke profile bench (the round-end evidence set)
+#   cfgtrace             tools/bench_configs.py $CFG under a kernel trace -> $CFG_trace/
+#   ortho                a9 orthonormalize_blocked m = 8 / 32 at 128^3, replay vs in-place passes -> ortho.jsonl
 #   xch                  the step's allreduce transports on one GPU (one-rank RCCL / mailbox / in-kernel
 #                        mailbox-step): slab and cube sweeps + the bench's N > 1 trial rehearsed -> xch_*.jsonl
 #
@@ -188,6 +190,19 @@ run_task() {
         --variants fused:arrays~rccl,fused:arrays~mailbox,fused:arrays~step > "$O/xch_cube.jsonl" 2>> "$O/xch.err" && \
       timeout -k 10 300 python bench.py --comm-self --rehearse-trial --no-cpu-baseline --side-steps 0 --general-steps 0 \
         > "$O/xch_trial.json" 2>> "$O/xch.err" ;;
+    ortho)
+      timeout -k 10 200 python -u tools/bench_configs.py ortho > "$O/ortho.jsonl" 2> "$O/ortho.err" && \
+      EIGMI_MGS_INPLACE=1 timeout -k 10 200 python -u tools/bench_configs.py ortho >> "$O/ortho.jsonl" 2>> "$O/ortho.err" ;;
+    orthogrid)
+      # the read-only passes' grid (EIGMI_MGS_GRID workgroups at most)
+      for g in 256 512 1024 2048; do
+        EIGMI_MGS_GRID=$g timeout -k 10 200 python -u tools/bench_configs.py ortho >> "$O/orthogrid.jsonl" 2>> "$O/ortho.err" || return 1
+      done ;;
+    cfgtrace)
+      # tools/bench_configs.py $CFG under a kernel trace (per-kernel durations of one configuration)
+      prof_env
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/${CFG}_trace" -o trace -- \
+        python3 tools/bench_configs.py $CFG > "$O/${CFG}_t.jsonl" 2> "$O/${CFG}_t.err" ;;
     round)
       run_task tests && run_task smoke && run_task profile && run_task bench ;;
     *)
