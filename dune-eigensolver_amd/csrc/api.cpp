@@ -596,6 +596,8 @@ extern "C" int eig_loopback_create(int nranks, void **hub)
     h->win_begin.assign(nranks, 0);
     h->red.assign(nranks, {});
     h->gather.assign(4 * (size_t)nranks, 0);
+    h->mbox.assign(nranks, nullptr);
+    h->flag.assign(nranks, 0);
     *hub = h;
   });
 }
@@ -615,6 +617,51 @@ extern "C" int eig_comm_init_loopback(eig_ctx_t ctx, void *hub, int rank)
     ctx->loop = h;
     ctx->nranks = h->P;
     ctx->rank = rank;
+  });
+}
+
+extern "C" int eig_comm_loopback_mailbox(eig_ctx_t ctx)
+{
+  return guard(ctx, [&] {
+    EIG_CHECK(ctx && ctx->loop && !ctx->mbox, EIG_ERR_ARG, "eig_comm_loopback_mailbox: loopback rank without a mailbox");
+    DeviceGuard dg(ctx->device);
+    LoopHub &h = *ctx->loop;
+    const int P = h.P, me = ctx->rank;
+    unsigned char handle[HIP_IPC_HANDLE_SIZE];
+    bool ok = true;
+    try
+    {
+      mailbox_prepare(ctx, P, me, handle);
+    }
+    catch (const Error &)
+    {
+      ok = false;
+    }
+    {
+      std::lock_guard<std::mutex> lk(h.m);
+      h.mbox[me] = ok ? ctx->mbox->local : nullptr;
+      h.flag[me] = ok ? 1 : 0;
+    }
+    h.barrier();
+    for (int r = 0; r < P; ++r) ok = ok && h.flag[r] && h.mbox[r];
+    // the virtual ranks share one process and device: the peers' mailboxes are plain device pointers
+    if (ok)
+      for (int r = 0; r < P; ++r) ctx->mbox->dev.peer[r] = h.mbox[r];
+    h.barrier();
+    if (ok) ok = mailbox_validate(ctx);  // (every rank's kernel runs concurrently: one queue each)
+    {
+      std::lock_guard<std::mutex> lk(h.m);
+      h.flag[me] = ok ? 1 : 0;
+    }
+    h.barrier();
+    for (int r = 0; r < P; ++r) ok = ok && h.flag[r];
+    h.barrier();
+    if (!ok)
+    {
+      mailbox_free(ctx);
+      throw Error(EIG_ERR_RCCL, "eig_comm_loopback_mailbox: mailbox setup or validation failed on some rank");
+    }
+    ctx->mbox->ready = true;
   });
 }
 

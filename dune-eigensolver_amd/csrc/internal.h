@@ -80,6 +80,8 @@ struct LoopHub {
   std::vector<i64> win_begin;      // per rank: window begin (scalar)
   std::vector<std::vector<double>> red;
   std::vector<i64> gather;
+  std::vector<u64 *> mbox;                 // per rank: its mailbox (eig_comm_loopback_mailbox)
+  std::vector<int> flag;                   // per rank: a flag agreed through the hub
   void barrier()
   {
     std::unique_lock<std::mutex> lk(m);
@@ -148,7 +150,7 @@ struct eig_ctx_s {
   // whether allreduces go through a transport (distributed, or a forced one-rank RCCL communicator)
   bool collectives() const { return distributed() || (comm_always && (comm || (mbox && mbox->ready))); }
   // the fused Lanczos step exchanges its three sums inside the step kernel (EIG_AR_MAILBOX_STEP)
-  bool step_exchange() const { return collectives() && !loop && mbox && mbox->ready && mbox->on && mbox->step; }
+  bool step_exchange() const { return collectives() && mbox && mbox->ready && mbox->on && mbox->step; }
   // reusable device buffers for drivers (grown on demand)
   std::vector<std::pair<void *, size_t>> pool;
 };

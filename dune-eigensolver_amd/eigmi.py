@@ -99,6 +99,7 @@ SIGNATURES = {
     "eig_loopback_create": (_int, [_int, ctypes.POINTER(_vp)]),
     "eig_loopback_destroy": (_int, [_vp]),
     "eig_comm_init_loopback": (_int, [_vp, _vp, _int]),
+    "eig_comm_loopback_mailbox": (_int, [_vp]),
     "eig_comm_ipc_handle": (_int, [_vp, _int, _int, ctypes.c_char_p]),
     "eig_comm_ipc_open": (_int, [_vp, ctypes.c_char_p]),
     "eig_comm_ipc_open_ex": (_int, [_vp, ctypes.c_char_p, _int]),

@@ -81,6 +81,12 @@ int eig_comm_allreduce_sum(eig_ctx_t ctx, double *buf, int64_t count);
 int eig_loopback_create(int nranks, void **hub);
 int eig_loopback_destroy(void *hub);
 int eig_comm_init_loopback(eig_ctx_t ctx, void *hub, int rank);
+/* Collective over a loopback hub (every virtual rank calls it after eig_comm_init_loopback): the
+ * xGMI mailbox allreduce between the virtual ranks (their mailboxes are device pointers of the same
+ * process), validated by all ranks; then eig_comm_select_allreduce may pick EIG_AR_MAILBOX /
+ * EIG_AR_MAILBOX_STEP while the halo keeps the loopback copies.  The ranks' kernels wait for each
+ * other, so each rank's stream needs a hardware queue of its own (GPU_MAX_HW_QUEUES >= 3 x ranks). */
+int eig_comm_loopback_mailbox(eig_ctx_t ctx);
 int eig_comm_barrier(eig_ctx_t ctx);
 /* Allreduce transport.  With RCCL and EIG_COMM_MAILBOX, eig_comm_init_ex also sets up the xGMI
  * mailbox allreduce (every rank exports a small uncached mailbox through IPC; one launch stores

@@ -222,6 +222,86 @@ static int value_images(int P, int N, const std::vector<double> &x)
   return failures;
 }
 
+// The fused step's allreduce inside the step kernel (EIG_AR_MAILBOX_STEP, csrc/xch_dev.h) between
+// the virtual ranks (eig_comm_loopback_mailbox: their mailboxes are device pointers of this process),
+// with the loopback halo: split launches (interior march + boundary slices, the boundary launch
+// completing and exchanging the sums) and whole launches, both within 1e-12 of the serial fused run
+// (fa / fb), and the repaired recurrence (outlier diagonal) against its serial run.  Skipped with
+// EIGMI_LOOPBACK_NO_MAILBOX=1 (the ranks' kernels wait for each other: one hardware queue per stream).
+static int mailbox_phase(int P, int N, int steps, const std::vector<double> &fa, const std::vector<double> &fb,
+                         const std::vector<double> &ra, const std::vector<double> &rb, int rl)
+{
+  if (std::getenv("EIGMI_LOOPBACK_NO_MAILBOX")) return 0;
+  const int64_t n = (int64_t)N * N * N;
+  void *hub;
+  CK(eig_loopback_create(P, &hub));
+  std::vector<std::vector<double>> sa(P, std::vector<double>(steps)), sb(P, std::vector<double>(steps + 1)),
+      wa(P, std::vector<double>(steps)), wb(P, std::vector<double>(steps + 1)),
+      qa(P, std::vector<double>(kRsteps)), qb(P, std::vector<double>(kRsteps + 1));
+  std::vector<int> kind(P, -1), errs(P, -1), ql(P, 0);
+  std::vector<std::thread> th;
+  for (int r = 0; r < P; ++r)
+    th.emplace_back([&, r] {
+      eig_ctx_t ctx;
+      CK(eig_ctx_create(0, &ctx));
+      CK(eig_comm_init_loopback(ctx, hub, r));
+      CK(eig_comm_loopback_mailbox(ctx));
+      CK(eig_comm_select_allreduce(ctx, EIG_AR_MAILBOX_STEP));
+      const int64_t p0 = (int64_t)N * r / P, p1 = (int64_t)N * (r + 1) / P;
+      const int64_t b = p0 * N * N, cnt = (p1 - p0) * N * N;
+      Rows rows = gen(N, b, cnt);
+      eig_mat_t A;
+      CK(eig_mat_create_bcsr_dist(ctx, n, b, cnt, 1, 1, rows.rp.data(), rows.c.data(), rows.v.data(), &A));
+      CK(eig_lanczos_run(A, steps, nullptr, 123, EIG_LANCZOS_FUSED, sa[r].data(), sb[r].data(), nullptr));
+      CK(eig_mat_tune(A, EIG_TUNE_HALO, 1));
+      CK(eig_lanczos_run(A, steps, nullptr, 123, EIG_LANCZOS_FUSED, wa[r].data(), wb[r].data(), nullptr));
+      eig_mat_destroy(A);
+      outliers(N, b, rows);
+      CK(eig_mat_create_bcsr_dist(ctx, n, b, cnt, 1, 1, rows.rp.data(), rows.c.data(), rows.v.data(), &A));
+      fused_repair_run(A, qa[r].data(), qb[r].data(), &ql[r]);
+      eig_mat_destroy(A);
+      int nr, rk;
+      CK(eig_comm_info(ctx, &nr, &rk, &kind[r], &errs[r]));
+      eig_ctx_destroy(ctx);
+    });
+  for (auto &t : th) t.join();
+  eig_loopback_destroy(hub);
+  int failures = 0;
+  for (int r = 0; r < P; ++r)
+  {
+    if (kind[r] != EIG_AR_MAILBOX_STEP || errs[r] != 0)
+    {
+      std::printf("FAIL mailbox-step rank %d: allreduce kind %d, timeouts %d\n", r, kind[r], errs[r]);
+      ++failures;
+    }
+    for (int j = 0; j < steps; ++j)
+      if (std::fabs(sa[r][j] - fa[j]) > 1e-12 * std::fabs(fa[j]) ||
+          std::fabs(sb[r][j + 1] - fb[j + 1]) > 1e-12 * std::fabs(fb[j + 1]) ||
+          std::fabs(wa[r][j] - fa[j]) > 1e-12 * std::fabs(fa[j]) ||
+          std::fabs(wb[r][j + 1] - fb[j + 1]) > 1e-12 * std::fabs(fb[j + 1]))
+      {
+        std::printf("FAIL mailbox-step rank %d fused step %d: alpha split %.17g whole %.17g serial %.17g\n", r, j,
+                    sa[r][j], wa[r][j], fa[j]);
+        ++failures;
+        break;
+      }
+    if (ql[r] != rl)
+    {
+      std::printf("FAIL mailbox-step rank %d: %d repaired launches vs %d serial\n", r, ql[r], rl);
+      ++failures;
+    }
+    for (int j = 0; j < kRsteps; ++j)
+      if (std::fabs(qa[r][j] - ra[j]) > 1e-12 * std::fabs(ra[j]) ||
+          std::fabs(qb[r][j + 1] - rb[j + 1]) > 1e-12 * std::fabs(rb[j + 1]))
+      {
+        std::printf("FAIL mailbox-step rank %d repaired step %d: alpha %.17g vs %.17g\n", r, j, qa[r][j], ra[j]);
+        ++failures;
+        break;
+      }
+  }
+  return failures;
+}
+
 int main(int argc, char **argv)
 {
   const int P = argc > 1 ? std::atoi(argv[1]) : 3;
@@ -455,6 +535,7 @@ int main(int argc, char **argv)
       }
   }
   failures += value_images(P, N, x);
+  failures += mailbox_phase(P, N, steps, fa_ser, fb_ser, ra_ser, rb_ser, rl_ser);
   // every rank's slab of whole planes takes the geometric-mask march (global plane coordinates)
   for (int r = 0; r < P; ++r)
     if (uni[r] != 2)
