@@ -1779,6 +1779,10 @@ void orthonormalize_device(eig_ctx_t ctx, i64 n, i64 m, double *Q, int variant)
     if (variant == EIG_ORTHO_MGS && !ctx->distributed() && !(flags & EIG_ORTHO_GRID) && launch_mgs_small(n, Qb, s))
     {
     }
+    else if (variant == EIG_ORTHO_MGS && !ctx->distributed() && !(flags & EIG_ORTHO_GRID) &&
+             launch_mgs_coop(ctx, n, Qb, S, s))
+    {
+    }
     else if (variant == EIG_ORTHO_MGS)
     {
       for (int k = 0; k <= 8; ++k)

@@ -410,6 +410,9 @@ void launch_gram_panel(eig_ctx_t ctx, i64 n, i64 ld, i64 m1, i64 m2, const doubl
 void launch_mgs_pass(i64 n, double *Qb, int k, double *S, int ticket, hipStream_t s, ReduceWS red);
 // Whole column MGS of one 8-column block in one workgroup (n <= 4096, one rank); false = not taken.
 bool launch_mgs_small(i64 n, double *Qb, hipStream_t s);
+// The 9 read-only MGS passes in one cooperative launch with grid barriers (k_mv8.hip k_mgs_coop; one
+// rank); false = refused or timed out (nothing written): run the per-pass launches instead
+bool launch_mgs_coop(eig_ctx_t ctx, i64 n, double *Qb, double *Ssum, hipStream_t s);
 void launch_apply_upper(i64 n, double *Qb, const double *U, hipStream_t s);
 void launch_cholqr_factor(const double *G, double *U, double *normmax, int flags, hipStream_t s);
 void launch_project(i64 n, i64 mrest, const double *Qk, double *Qrest, const double *S, hipStream_t s);

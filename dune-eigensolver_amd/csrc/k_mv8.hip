@@ -561,6 +561,189 @@ void launch_mgs_pass(i64 n, double *Qb, int k, double *Ssum, int ticket, hipStre
 }
 
 // ---------------------------------------------------------------------------------------------
+// The read-only MGS passes in ONE cooperative launch (one rank, the default for n > 4096): every
+// workgroup stays resident through the 9 passes, and a pass ends in a grid barrier instead of a
+// kernel boundary and a last-workgroup tail.  Each workgroup stores its 8 block sums (write-through),
+// arrives at the barrier, and after it EVERY workgroup sums the grid's partials itself, in the same
+// fixed order (so all hold the bitwise same row of S; workgroup 0 also stores it to Ssum for the
+// host).  Rows and per-row operations as k_mgs_replay.  Needs all workgroups co-resident
+// (hipLaunchCooperativeKernel refuses the launch otherwise and the per-pass launches run); the
+// barrier spin is bounded (1 s of s_memrealtime: err = 1, and the host falls back) so a broken
+// co-residency promise cannot hang the GPU.
+// ---------------------------------------------------------------------------------------------
+constexpr unsigned long long kMgsBarrierTimeout = 100000000ull;
+
+// grid barrier number b (1, 2, ...) of the launch on a counter zeroed before it
+__device__ __forceinline__ bool mgs_grid_barrier(unsigned *bar, unsigned b, int *err)
+{
+  __shared__ int s_late;
+  __syncthreads();  // (this workgroup's partial stores were drained by each storing thread)
+  if (threadIdx.x == 0)
+  {
+    s_late = 0;
+    // relaxed, as the grid reduction's ticket (reduce_dev.h): the partials went out write-through
+    // and are read with coherent loads, so no release / acquire fence (at agent scope those write
+    // back / invalidate the whole L2 of every XCD -- measured 2x slower per pass)
+    __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned target = b * gridDim.x;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target)
+    {
+      __builtin_amdgcn_s_sleep(1);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > kMgsBarrierTimeout)
+      {
+        s_late = 1;
+        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  return s_late == 0;
+}
+
+__global__ __launch_bounds__(kStreamThreads) void k_mgs_coop(i64 n, double *__restrict__ Qb, double *__restrict__ Ssum,
+                                                             double *__restrict__ partials, unsigned *bar, int *err)
+{
+  __shared__ double S[8][8];  // raw sums s[k][j] of the finished steps (bitwise the same in every workgroup)
+  const int ql = threadIdx.x & 3;
+  const int c0 = 2 * ql, c1 = c0 + 1;
+  const i64 stride = (i64)gridDim.x * (kStreamThreads / 4);
+  const i64 i00 = ((i64)blockIdx.x * kStreamThreads + threadIdx.x) >> 2;
+  constexpr int U = 8;
+  auto pass = [&](auto kc) {
+    constexpr int K = decltype(kc)::value;
+    double sp0[K > 0 ? K : 1], sp1[K > 0 ? K : 1];
+#pragma unroll
+    for (int kp = 0; kp < K; ++kp)
+    {
+      const double skk = S[kp][kp];
+      sp0[kp] = (c0 > kp) ? S[kp][c0] / skk : ((c0 == kp) ? 1.0 / sqrt(skk) : 0.0);
+      sp1[kp] = (c1 > kp) ? S[kp][c1] / skk : ((c1 == kp) ? 1.0 / sqrt(skk) : 0.0);
+    }
+    double a0 = 0.0, a1 = 0.0;
+    for (i64 i0 = i00; i0 < n; i0 += U * stride)
+    {
+      double2 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+      {
+        const i64 i = i0 + u * stride;
+        v[u] = i < n ? reinterpret_cast<const double2 *>(Qb + i * 8)[ql] : make_double2(0.0, 0.0);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+      {
+        mgs_replay_steps<0, K>(v[u], sp0, sp1, c0, c1);
+        if constexpr (K == 8)
+        {
+          const i64 i = i0 + u * stride;
+          if (i < n) reinterpret_cast<double2 *>(Qb + i * 8)[ql] = v[u];
+        }
+        else
+        {
+          const double qk = quad_bcast<(K >> 1)>((K & 1) ? v[u].y : v[u].x);
+          if (c0 >= K) a0 += qk * v[u].x;
+          if (c1 >= K) a1 += qk * v[u].y;
+        }
+      }
+    }
+    if constexpr (K < 8)
+    {
+      // block sums of the 8 values -> partials[block][8] (write-through), grid barrier, then every
+      // workgroup sums all blocks' partials in block order
+      double vals[8], bs[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) vals[j] = (j == c0) ? a0 : ((j == c1) ? a1 : 0.0);
+      block_sum<8, kStreamThreads>(vals, bs);
+      // two partial buffers by pass parity: pass K + 2's stores come after barrier K + 2, which every
+      // workgroup reaches only after reading pass K's partials -- so pass K + 2 may reuse the buffer
+      double *part = partials + (size_t)(K & 1) * gridDim.x * 8;
+      if (threadIdx.x == 0)
+      {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) st_sc1(&part[(size_t)blockIdx.x * 8 + j], bs[j]);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (!mgs_grid_barrier(bar, K + 1, err)) return false;
+      {
+        // thread t: value j = t & 7 over the 16 blocks b = (t >> 3) + 32 u (all loads in one round
+        // trip), then the 32 slices of value j summed in slice order through LDS (a fixed order:
+        // identical in every workgroup).  G <= 512 blocks.
+        __shared__ double sred[32][8];
+        const int j = threadIdx.x & 7, sl = threadIdx.x >> 3;
+        const unsigned G = gridDim.x;
+        double t[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+        {
+          const unsigned b = (unsigned)sl + 32u * u;
+          t[u] = b < G ? ld_sc1(&part[(size_t)b * 8 + j]) : 0.0;
+        }
+        double acc = 0.0;
+#pragma unroll
+        for (int u = 0; u < 16; ++u) acc += t[u];
+        sred[sl][j] = acc;
+        __syncthreads();
+        if (threadIdx.x < 8)
+        {
+          double r = 0.0;
+#pragma unroll
+          for (int q = 0; q < 32; ++q) r += sred[q][threadIdx.x];
+          r = (threadIdx.x >= (unsigned)K) ? r : 0.0;
+          S[K][threadIdx.x] = r;
+          if (blockIdx.x == 0) Ssum[K * 8 + threadIdx.x] = r;
+        }
+      }
+      __syncthreads();
+    }
+    return true;
+  };
+  if (!pass(std::integral_constant<int, 0>{})) return;
+  if (!pass(std::integral_constant<int, 1>{})) return;
+  if (!pass(std::integral_constant<int, 2>{})) return;
+  if (!pass(std::integral_constant<int, 3>{})) return;
+  if (!pass(std::integral_constant<int, 4>{})) return;
+  if (!pass(std::integral_constant<int, 5>{})) return;
+  if (!pass(std::integral_constant<int, 6>{})) return;
+  if (!pass(std::integral_constant<int, 7>{})) return;
+  pass(std::integral_constant<int, 8>{});
+}
+
+// One cooperative launch of the 9 passes; false when the runtime refuses it (co-residency) or a
+// barrier timed out -- the caller then runs the per-pass launches (Qb is written only by the last
+// pass, after the last barrier, so a failed attempt leaves it untouched).
+bool launch_mgs_coop(eig_ctx_t ctx, i64 n, double *Qb, double *Ssum, hipStream_t s)
+{
+  static const bool off = std::getenv("EIGMI_MGS_NOCOOP") != nullptr;
+  if (off || n <= 0) return false;
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_mgs_coop, kStreamThreads, 0) != hipSuccess || per_cu < 1)
+  {
+    (void)hipGetLastError();
+    return false;
+  }
+  const int G = std::min<int>({per_cu * ctx->num_cu, 512, grid_for(n * 4, kStreamThreads * 4, 512)});
+  // scratch: 2 x G x 8 partials, the barrier counter, the error word (context buffer slot 10)
+  char *buf = (char *)ctx_buffer(ctx, 10, (size_t)16 * G * 8 + 256);
+  double *part = reinterpret_cast<double *>(buf);
+  unsigned *bar = reinterpret_cast<unsigned *>(buf + (size_t)16 * G * 8);
+  int *err = reinterpret_cast<int *>(buf + (size_t)16 * G * 8 + 128);
+  EIG_HIP(hipMemsetAsync(bar, 0, 256, s));
+  void *args[] = {&n, &Qb, &Ssum, &part, &bar, &err};
+  if (hipLaunchCooperativeKernel(reinterpret_cast<const void *>(k_mgs_coop), dim3(G), dim3(kStreamThreads), args, 0,
+                                 s) != hipSuccess)
+  {
+    (void)hipGetLastError();
+    return false;
+  }
+  int e = 0;
+  EIG_HIP(hipMemcpyAsync(&e, err, sizeof(int), hipMemcpyDeviceToHost, s));
+  EIG_HIP(hipStreamSynchronize(s));
+  return e == 0;
+}
+
+// ---------------------------------------------------------------------------------------------
 // The same column MGS for a small block (n <= 512 R rows, one rank), in ONE workgroup: the 512
 // threads keep their R rows in registers for all 8 passes, and each pass's sums meet in a
 // workgroup reduction (a xor-shuffle tree per wave, the 8 wave partials summed in wave order by
