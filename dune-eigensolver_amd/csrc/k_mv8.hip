@@ -561,7 +561,7 @@ void launch_mgs_pass(i64 n, double *Qb, int k, double *Ssum, int ticket, hipStre
 }
 
 // ---------------------------------------------------------------------------------------------
-// The read-only MGS passes in ONE cooperative launch (one rank, the default for n > 4096): every
+// The read-only MGS passes in ONE cooperative launch (one rank, opt-in: EIGMI_MGS_COOP=1): every
 // workgroup stays resident through the 9 passes, and a pass ends in a grid barrier instead of a
 // kernel boundary and a last-workgroup tail.  Each workgroup stores its 8 block sums (write-through),
 // arrives at the barrier, and after it EVERY workgroup sums the grid's partials itself, in the same
@@ -715,8 +715,11 @@ __global__ __launch_bounds__(kStreamThreads) void k_mgs_coop(i64 n, double *__re
 // pass, after the last barrier, so a failed attempt leaves it untouched).
 bool launch_mgs_coop(eig_ctx_t ctx, i64 n, double *Qb, double *Ssum, hipStream_t s)
 {
-  static const bool off = std::getenv("EIGMI_MGS_NOCOOP") != nullptr;
-  if (off || n <= 0) return false;
+  // opt-in (EIGMI_MGS_COOP=1): measured slower than the 9 launches -- 411 vs ~330 us of kernel time at
+  // 128^3, m = 8 (profiles/r05m_ortho_*): the persistent passes stream at ~46 us each against ~33 us
+  // for a fresh launch, which the saved launch gaps (~2 us each) do not repay
+  static const bool on = std::getenv("EIGMI_MGS_COOP") != nullptr;
+  if (!on || n <= 0) return false;
   int per_cu = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_mgs_coop, kStreamThreads, 0) != hipSuccess || per_cu < 1)
   {

@@ -227,8 +227,8 @@ def ortho(ctx):
     reference's byte model (kernels_cpp.hh:157-175); EIGMI_MGS_INPLACE=1 times the in-place passes."""
     n = 128 ** 3
     tag = ("in-place passes" if os.environ.get("EIGMI_MGS_INPLACE") else
-           f"read-only replay passes, grid <= {os.environ.get('EIGMI_MGS_GRID', '512')}" if
-           os.environ.get("EIGMI_MGS_NOCOOP") else "one cooperative launch, grid barriers")
+           "one cooperative launch, grid barriers" if os.environ.get("EIGMI_MGS_COOP") else
+           f"read-only replay passes, grid <= {os.environ.get('EIGMI_MGS_GRID', '512')}")
     for m in (8, 32):
         Qh = oracle.random_mv8(n, m, 1)
         Q = ctx.array(Qh)

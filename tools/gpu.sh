@@ -192,8 +192,8 @@ run_task() {
         > "$O/xch_trial.json" 2>> "$O/xch.err" ;;
     ortho)
       timeout -k 10 200 python -u tools/bench_configs.py ortho > "$O/ortho.jsonl" 2> "$O/ortho.err" && \
-      EIGMI_MGS_NOCOOP=1 timeout -k 10 200 python -u tools/bench_configs.py ortho >> "$O/ortho.jsonl" 2>> "$O/ortho.err" && \
-      EIGMI_MGS_NOCOOP=1 EIGMI_MGS_INPLACE=1 timeout -k 10 200 python -u tools/bench_configs.py ortho >> "$O/ortho.jsonl" 2>> "$O/ortho.err" ;;
+      EIGMI_MGS_COOP=1 timeout -k 10 200 python -u tools/bench_configs.py ortho >> "$O/ortho.jsonl" 2>> "$O/ortho.err" && \
+      EIGMI_MGS_INPLACE=1 timeout -k 10 200 python -u tools/bench_configs.py ortho >> "$O/ortho.jsonl" 2>> "$O/ortho.err" ;;
     orthogrid)
       # the read-only passes' grid (EIGMI_MGS_GRID workgroups at most)
       for g in 256 512 1024 2048; do
