@@ -1765,8 +1765,10 @@ void gram_device(eig_ctx_t ctx, i64 n, i64 m1, i64 m2, const double *Q1, const d
 
 void orthonormalize_device(eig_ctx_t ctx, i64 n, i64 m, double *Q, int variant)
 {
-  const int flags = variant & EIG_ORTHO_GRID;
-  variant &= ~EIG_ORTHO_GRID;
+  const int flags = variant & (EIG_ORTHO_GRID | EIG_ORTHO_NO_COOP);
+  const int la = (variant >> EIG_ORTHO_LOOKAHEAD_SHIFT) & 15;  // EIG_ORTHO_LOOKAHEAD(L); 0: the default
+  const int L = la ? std::min(la, 8) : mgs_lookahead_default();
+  variant &= 0xff;
   hipStream_t s = ctx->stream;
   double *S = (double *)ctx_buffer(ctx, 3, 64 * sizeof(double));
   double *U = S + 0;  // reused: Ssum for MGS, Gram for CholQR
@@ -1781,6 +1783,9 @@ void orthonormalize_device(eig_ctx_t ctx, i64 n, i64 m, double *Q, int variant)
     }
     else if (variant == EIG_ORTHO_MGS && !ctx->distributed() && !(flags & EIG_ORTHO_GRID) &&
              launch_mgs_coop(ctx, n, Qb, S, s))
+    {
+    }
+    else if (variant == EIG_ORTHO_MGS && !ctx->distributed() && launch_mgs_lookahead(ctx, n, Qb, L, !(flags & EIG_ORTHO_NO_COOP), s))
     {
     }
     else if (variant == EIG_ORTHO_MGS)
@@ -1835,12 +1840,24 @@ extern "C" int eig_orthonormalize_mv8(eig_ctx_t ctx, int64_t n, int64_t m, doubl
 {
   return guard(ctx, [&] {
     EIG_CHECK(ctx && Q && n >= 0, EIG_ERR_ARG, "eig_orthonormalize_mv8: bad argument");
-    const int v = variant & ~EIG_ORTHO_GRID;
+    const int v = variant & 0xff;
     EIG_CHECK(v == EIG_ORTHO_MGS || v == EIG_ORTHO_CHOLQR || v == EIG_ORTHO_CHOLQR_SPLIT, EIG_ERR_ARG,
               "unknown variant");
+    EIG_CHECK((variant & ~(0xff | EIG_ORTHO_GRID | EIG_ORTHO_NO_COOP | (15 << EIG_ORTHO_LOOKAHEAD_SHIFT))) == 0 &&
+                  ((variant >> EIG_ORTHO_LOOKAHEAD_SHIFT) & 15) <= 8,
+              EIG_ERR_ARG, "unknown variant flags");
     EIG_MV8_CHECK(m);
     DeviceGuard dg(ctx->device);
     orthonormalize_device(ctx, n, m, Q, variant);
+  });
+}
+
+extern "C" int eig_orthonormalize_passes(eig_ctx_t ctx, int *passes)
+{
+  return guard(ctx, [&] {
+    EIG_CHECK(ctx && passes, EIG_ERR_ARG, "eig_orthonormalize_passes: null argument");
+    DeviceGuard dg(ctx->device);
+    *passes = mgs_lookahead_passes(ctx);
   });
 }
 

@@ -408,6 +408,11 @@ void launch_gram_panel(eig_ctx_t ctx, i64 n, i64 ld, i64 m1, i64 m2, const doubl
                        hipStream_t s);
 // Block Gram-Schmidt building blocks, see k_mv8.hip.
 void launch_mgs_pass(i64 n, double *Qb, int k, double *S, int ticket, hipStream_t s, ReduceWS red);
+// MGS with Gram look-ahead (k_mv8.hip): L steps per read pass, gated; false when L <= 1 or n <= 0
+constexpr int kMgsLookaheadDefault = 8;
+int mgs_lookahead_default();  // EIGMI_MGS_LOOKAHEAD or kMgsLookaheadDefault
+bool launch_mgs_lookahead(eig_ctx_t ctx, i64 n, double *Qb, int L, bool coop, hipStream_t s);
+int mgs_lookahead_passes(eig_ctx_t ctx);  // read passes of the last call (-1: none finished)
 // Whole column MGS of one 8-column block in one workgroup (n <= 4096, one rank); false = not taken.
 bool launch_mgs_small(i64 n, double *Qb, hipStream_t s);
 // The 9 read-only MGS passes in one cooperative launch with grid barriers (k_mv8.hip k_mgs_coop; one

@@ -747,6 +747,523 @@ bool launch_mgs_coop(eig_ctx_t ctx, i64 n, double *Qb, double *Ssum, hipStream_t
 }
 
 // ---------------------------------------------------------------------------------------------
+// The same column MGS with Gram LOOK-AHEAD (the default on one rank; EIG_ORTHO_LOOKAHEAD(L)).
+// A pass that starts with F finished steps replays them on each row (as k_mgs_replay) and sums,
+// besides step F's own row  s[F][j] = q_F . q_j  (j >= F), the rows a = F+1 .. F+W-1 of the same
+// Gram (W = min(L, 8 - F)).  The pass's tail then finishes step F exactly as the stepwise passes
+// do, and steps F+1 .. from the Schur complement of the window: after step b the sums of the
+// updated columns are  s'[a][j] = s[a][j] - (s[b][a] / s[b][b]) s[b][j]  -- in exact arithmetic the
+// very sums the next stepwise pass would form, so ONE pass finishes up to W steps and m = 8 takes
+// ceil(8 / L) read passes plus the write pass instead of 8 + 1.
+// Rounding: every term of s' is bounded by |q_a| |q_j| of the window's columns (Cauchy-Schwarz), so
+// the absolute error of s'[a][j] is O(W eps |q_a| |q_j|) where the stepwise pass has O(eps |q'_a|
+// |q'_j|): relative to the step's own scale that is an amplification of 1/r with r = s'[a][a] /
+// s[a][a], the fraction of q_a's squared norm left after projecting out the window's earlier
+// columns.  A look-ahead step is taken only while r >= kMgsLaTau (1/16: at most 16 W eps, well inside
+// the 1e-12 of the restatement); at the first column below it the pass stops and the next pass
+// starts there with a DIRECT row, so nearly dependent columns get exactly the stepwise arithmetic.
+// (The reference's own fast diagonal block, orthonormalize_avx2_b8_v2 (kernels_avx2.hh:385-622),
+// is CholQR: the whole 8 x 8 Gram in one pass, ungated.)
+// Layout: the read passes hold ONE ROW PER LANE (four 16-B loads; the window's <= 36 products per
+// row with no cross-lane traffic), the write pass the quad layout of k_mgs_replay (coalesced 16-B
+// stores).  Both replay a row with the same operations in the same order.
+// Launches: ceil(8 / L) read launches (a ticketed tail finishes the window), then ONE last launch
+// that writes the block -- and, only when a look-ahead was refused, first runs the missing read
+// passes in-kernel between grid barriers (its grid fits the device at one workgroup per CU; bounded
+// spins: on a timeout the workgroup poisons its rows with NaN and records the failure, so nothing
+// hangs and nothing passes silently).  EIG_ORTHO_NO_COOP instead enqueues the worst case, 9
+// launches, whose surplus ones only copy the state word forward.
+// State (context scratch, slot 11): Sfin[8][8] the finished S rows (S[k][k] = 1/sqrt, S[k][j] =
+// s'/s'[k][k], 0 below); words st[0..1] by launch parity (bits 0-3 F, bit 4 written, bits 8-15 read
+// passes so far: launch l reads word l & 1, exactly one thread writes word (l + 1) & 1), st[2] the
+// last call's final word, st[32] the last launch's barrier counter, st[33] its error flag.
+// ---------------------------------------------------------------------------------------------
+constexpr int kMgsLaThreads = 512;
+constexpr int kMgsLaGrid = 256;  // one workgroup per CU: the tails sum 256 x 8 W partials
+constexpr double kMgsLaTau = 1.0 / 16;
+constexpr unsigned kMgsLaWritten = 16u;
+constexpr int kMgsLaBar = 32, kMgsLaErr = 33, kMgsLaLast = 2;  // st[] word indices
+
+struct MgsLaArgs {
+  i64 n;
+  double *Qb;
+  int launch;
+  unsigned *st;
+  double *Sfin;
+  double *partials;
+  unsigned *ticket;
+};
+
+template <int L>
+struct MgsLaShared {
+  double red[kMgsLaThreads / 64][8 * L];  // wave totals
+  double fin[8][8 * L];                   // the tail's 8 slices
+  double Rw[L][8];                        // the window's grid sums
+  double S[64];                           // (last launch) the S rows
+  unsigned word, last;
+};
+
+// Steps 0 .. F-1 on one row held whole (S rows wave-uniform): per element the operations of
+// mgs_replay_steps, in its order -- q_j -= S[kp][j] q_kp (j > kp) with the old q_kp, then
+// q_kp *= S[kp][kp] (kernels_cpp.hh:218-228)
+template <int F>
+__device__ __forceinline__ void mgs_row_replay(double (&q)[8], const double (&S)[F > 0 ? F : 1][8])
+{
+#pragma unroll
+  for (int kp = 0; kp < F; ++kp)
+  {
+#pragma unroll
+    for (int j = kp + 1; j < 8; ++j) q[j] -= S[kp][j] * q[kp];
+    q[kp] *= S[kp][kp];
+  }
+}
+
+// a wave-uniform double into scalar registers (the S rows of the LDS copy: no VGPRs held)
+__device__ __forceinline__ double mgs_uniform(double x)
+{
+  const long long b = __double_as_longlong(x);
+  const int lo = __builtin_amdgcn_readfirstlane((int)(b & 0xffffffffll));
+  const int hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+// The read pass over this lane's rows: replay F steps, accumulate the window's Gram rows
+// acc[w][c] = sum q_{F+w} q_c (c >= F + w; the other slots stay 0)
+template <int F, int W, int U>  // U: rows per lane per batch; two batches in flight (ping-pong)
+__device__ __forceinline__ void mgs_la_rows(i64 n, const double *__restrict__ Qb, const double *S, double (&acc)[W][8])
+{
+#pragma unroll
+  for (int w = 0; w < W; ++w)
+#pragma unroll
+    for (int c = 0; c < 8; ++c) acc[w][c] = 0.0;
+  double Sr[F > 0 ? F : 1][8];
+#pragma unroll
+  for (int kp = 0; kp < F; ++kp)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) Sr[kp][j] = j < kp ? 0.0 : mgs_uniform(S[kp * 8 + j]);
+  const i64 stride = (i64)gridDim.x * kMgsLaThreads;
+  auto load = [&](double (&q)[U][8], i64 i0) {
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+    {
+      const i64 i = i0 + u * stride;
+      const double2 *r = reinterpret_cast<const double2 *>(Qb + (i < n ? i : 0) * 8);
+#pragma unroll
+      for (int h = 0; h < 4; ++h)
+      {
+        const double2 x = i < n ? r[h] : make_double2(0.0, 0.0);  // (rows past n add nothing)
+        q[u][2 * h] = x.x;
+        q[u][2 * h + 1] = x.y;
+      }
+    }
+  };
+  auto work = [&](double (&q)[U][8]) {
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+    {
+      mgs_row_replay<F>(q[u], Sr);
+#pragma unroll
+      for (int w = 0; w < W; ++w)
+#pragma unroll
+        for (int c = F + w; c < 8; ++c) acc[w][c] += q[u][F + w] * q[u][c];
+    }
+  };
+  const i64 step = (i64)U * stride;
+  i64 i0 = (i64)blockIdx.x * kMgsLaThreads + threadIdx.x;
+  double qa[U][8], qb[U][8];
+  load(qa, i0);
+  while (i0 < n)
+  {
+    load(qb, i0 + step);
+    work(qa);
+    i0 += step;
+    if (i0 >= n) break;
+    load(qa, i0 + step);
+    work(qb);
+    i0 += step;
+  }
+}
+
+// Workgroup sums of the 8 W slots (slot e = w 8 + c): a reduce-scatter by recursive halving inside
+// each wave (P - 1 shuffles for P slots, lane l ending with slot bitrev(l)), the lane groups summed
+// by xor shuffles, the waves' totals through LDS in wave order.  Threads < 8 W return their slot.
+template <int W, int L>
+__device__ __forceinline__ double mgs_la_block(double (&acc)[W][8], MgsLaShared<L> &sh)
+{
+  constexpr int E = 8 * W;
+  constexpr int P = E <= 8 ? 8 : (E <= 16 ? 16 : (E <= 32 ? 32 : 64));
+  constexpr int LOG = P == 8 ? 3 : (P == 16 ? 4 : (P == 32 ? 5 : 6));
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  double v[P];
+#pragma unroll
+  for (int e = 0; e < P; ++e) v[e] = e < E ? acc[e / 8][e % 8] : 0.0;
+  int slot = 0;
+#pragma unroll
+  for (int s = 0; s < LOG; ++s)
+  {
+    const int half = P >> (s + 1);
+    const bool hi = (lane >> s) & 1;
+#pragma unroll
+    for (int i = 0; i < half; ++i)
+    {
+      const double send = hi ? v[i] : v[half + i];
+      const double keep = hi ? v[half + i] : v[i];
+      v[i] = keep + __shfl_xor(send, 1 << s, 64);
+    }
+    slot += hi ? half : 0;
+  }
+  double x = v[0];
+#pragma unroll
+  for (int m = P; m < 64; m <<= 1) x += __shfl_xor(x, m, 64);
+  if (lane < P) sh.red[wave][slot] = x;
+  __syncthreads();
+  double t = 0.0;
+  if (threadIdx.x < E)
+  {
+#pragma unroll
+    for (int q = 0; q < kMgsLaThreads / 64; ++q) t += sh.red[q][threadIdx.x];
+  }
+  return t;
+}
+
+// Grid sums of the 8 W slots from nblk workgroups' partials (block b's slot e at part[b ld + e]):
+// value e over the blocks g, g + 8, ... (16 loads in flight per round), then the 8 slices in slice
+// order -- a fixed order, independent of arrival.  Into sh.Rw (every thread may call; all must).
+template <int W, int L>
+__device__ __forceinline__ void mgs_la_gather(const double *part, int ld, unsigned nblk, MgsLaShared<L> &sh)
+{
+  constexpr int E = 8 * W;
+  if (threadIdx.x < 8 * E)
+  {
+    const int e = threadIdx.x % E, g = threadIdx.x / E;
+    double x = 0.0;
+    for (unsigned b0 = (unsigned)g; b0 < nblk; b0 += 8u * 16u)
+    {
+      double t[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u)
+      {
+        const unsigned b = b0 + 8u * u;
+        t[u] = b < nblk ? ld_sc1(&part[(size_t)b * ld + e]) : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 16; ++u) x += t[u];
+    }
+    sh.fin[g][e] = x;
+  }
+  __syncthreads();
+  if (threadIdx.x < E)
+  {
+    double x = 0.0;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) x += sh.fin[g][threadIdx.x];
+    sh.Rw[threadIdx.x / 8][threadIdx.x % 8] = x;
+  }
+  __syncthreads();
+}
+
+// Lanes 0..7 of wave 0 (lane j holds column j of the window rows, col[w] = s[F + w][j]): finish
+// steps F .. into S; returns the new F (wave-uniform).  The pivot and the multipliers come by
+// shuffle, so every index is compile-time and the arithmetic is that of one thread doing
+// s'[b][j] -= (s[a][b] / s[a][a]) s[a][j] row by row.
+template <int F, int W>
+__device__ int mgs_la_finish(double (&col)[W], double *S)
+{
+  const int j = threadIdx.x & 63;
+  double r0[W];
+#pragma unroll
+  for (int w = 0; w < W; ++w) r0[w] = __shfl(col[w], F + w, 64);
+  int Fn = F;
+  bool go = true;  // (a predicate, not a break: every index stays compile-time)
+#pragma unroll
+  for (int w = 0; w < W; ++w)
+  {
+    const int a = F + w;
+    const double d = __shfl(col[w], a, 64);
+    if (w > 0) go = go && d >= kMgsLaTau * r0[w];  // (NaN refuses too)
+    if (!go) continue;
+    // S[a][j] = s[a][j] / s[a][a] (j > a), S[a][a] = 1 / sqrt(s[a][a]) (kernels_cpp.hh:214-228)
+    if (j < 8) S[a * 8 + j] = j < a ? 0.0 : (j == a ? 1.0 / sqrt(d) : col[w] / d);
+    Fn = a + 1;
+    // eliminate step a from the later window rows: s'[b][j] -= (s[a][b] / s[a][a]) s[a][j]
+#pragma unroll
+    for (int w2 = w + 1; w2 < W; ++w2)
+    {
+      const int b = F + w2;
+      const double f = __shfl(col[w], b, 64) / d;
+      if (j >= b) col[w2] -= f * col[w];
+    }
+  }
+  return Fn;
+}
+
+// wave 0: the window sums of sh.Rw -> S rows, new state word (returned in every lane of wave 0)
+template <int F, int W, int L>
+__device__ __forceinline__ unsigned mgs_la_close(MgsLaShared<L> &sh, double *S, unsigned word)
+{
+  const int j = threadIdx.x & 63;
+  double col[W];
+#pragma unroll
+  for (int w = 0; w < W; ++w) col[w] = j < 8 ? sh.Rw[w][j] : 0.0;
+  const int Fn = mgs_la_finish<F, W>(col, S);
+  return (unsigned)Fn | ((((word >> 8) & 255u) + 1u) << 8);
+}
+
+// An ordinary read launch: rows, workgroup partials, ticket; the last workgroup finishes the window.
+template <int F, int L>
+__device__ __forceinline__ void mgs_la_read(const MgsLaArgs a, unsigned word, MgsLaShared<L> &sh)
+{
+  constexpr int W = (8 - F) < L ? (8 - F) : L;
+  constexpr int E = 8 * W;
+  double acc[W][8];
+  mgs_la_rows<F, W, 2>(a.n, a.Qb, a.Sfin, acc);
+  const double part = mgs_la_block<W, L>(acc, sh);
+  const unsigned bid = blockIdx.x, nblk = gridDim.x;
+  if (threadIdx.x < E) st_sc1(&a.partials[(size_t)bid * E + threadIdx.x], part);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) sh.last = ticket_arrive(a.ticket, bid, nblk) ? 1u : 0u;
+  __syncthreads();
+  if (!sh.last) return;
+  mgs_la_gather<W, L>(a.partials, E, nblk, sh);
+  if (threadIdx.x < 64)
+  {
+    const unsigned nw = mgs_la_close<F, W, L>(sh, a.Sfin, word);
+    if (threadIdx.x == 0)
+    {
+      a.st[(a.launch + 1) & 1] = nw;
+      ticket_reset(a.ticket);
+    }
+  }
+}
+
+// The write pass, quad layout (as k_mgs_replay<8>): replay the 8 steps, store the rows.
+__device__ __forceinline__ void mgs_la_write(i64 n, double *__restrict__ Qb, const double *S)
+{
+  constexpr int U = 8;
+  const int ql = threadIdx.x & 3;
+  const int c0 = 2 * ql, c1 = c0 + 1;
+  double sp0[8], sp1[8];
+#pragma unroll
+  for (int kp = 0; kp < 8; ++kp)
+  {
+    sp0[kp] = S[kp * 8 + c0];
+    sp1[kp] = S[kp * 8 + c1];
+  }
+  const i64 stride = (i64)gridDim.x * (kMgsLaThreads / 4);
+  auto load = [&](double2 (&v)[U], i64 i0) {
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+    {
+      const i64 i = i0 + u * stride;
+      v[u] = i < n ? reinterpret_cast<const double2 *>(Qb + i * 8)[ql] : make_double2(0.0, 0.0);
+    }
+  };
+  auto work = [&](double2 (&v)[U], i64 i0) {
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+    {
+      mgs_replay_steps<0, 8>(v[u], sp0, sp1, c0, c1);
+      const i64 i = i0 + u * stride;
+      if (i < n) reinterpret_cast<double2 *>(Qb + i * 8)[ql] = v[u];
+    }
+  };
+  const i64 step = (i64)U * stride;
+  i64 i0 = ((i64)blockIdx.x * kMgsLaThreads + threadIdx.x) >> 2;
+  double2 va[U], vb[U];
+  load(va, i0);
+  while (i0 < n)
+  {
+    load(vb, i0 + step);
+    work(va, i0);
+    i0 += step;
+    if (i0 >= n) break;
+    load(va, i0 + step);
+    work(vb, i0);
+    i0 += step;
+  }
+}
+
+template <int L>
+__global__ __launch_bounds__(kMgsLaThreads) void k_mgs_la(MgsLaArgs a)
+{
+  __shared__ MgsLaShared<L> sh;  // (one copy for the nine pass bodies)
+  const unsigned word = a.launch == 0 ? 0u : a.st[a.launch & 1];
+  if (a.launch == 0 && blockIdx.x == 0 && threadIdx.x == 0)
+  {
+    a.st[kMgsLaBar] = 0u;  // for the last launch of this call
+    a.st[kMgsLaErr] = 0u;
+  }
+  if (word & kMgsLaWritten)
+  {
+    if (blockIdx.x == 0 && threadIdx.x == 0) a.st[(a.launch + 1) & 1] = word;
+    return;
+  }
+  switch (word & 15u)
+  {
+    case 0: mgs_la_read<0, L>(a, word, sh); break;
+    case 1: mgs_la_read<1, L>(a, word, sh); break;
+    case 2: mgs_la_read<2, L>(a, word, sh); break;
+    case 3: mgs_la_read<3, L>(a, word, sh); break;
+    case 4: mgs_la_read<4, L>(a, word, sh); break;
+    case 5: mgs_la_read<5, L>(a, word, sh); break;
+    case 6: mgs_la_read<6, L>(a, word, sh); break;
+    case 7: mgs_la_read<7, L>(a, word, sh); break;
+    default:
+      mgs_la_write(a.n, a.Qb, a.Sfin);
+      if (blockIdx.x == 0 && threadIdx.x == 0)
+      {
+        a.st[(a.launch + 1) & 1] = word | kMgsLaWritten;
+        a.st[kMgsLaLast] = word | kMgsLaWritten;
+      }
+      break;
+  }
+}
+
+// A read pass inside the last launch: workgroup partials into the pass's parity buffer, a
+// grid barrier, then EVERY workgroup sums all partials in the same fixed order and finishes the
+// window itself (bitwise the same S rows in each).  False when the barrier timed out.
+template <int F, int L>
+__device__ __forceinline__ bool mgs_la_read_coop(const MgsLaArgs a, MgsLaShared<L> &sh, unsigned &nb)
+{
+  constexpr int W = (8 - F) < L ? (8 - F) : L;
+  constexpr int E = 8 * W;
+  double acc[W][8];
+  mgs_la_rows<F, W, 1>(a.n, a.Qb, sh.S, acc);  // (the rare path: fewer rows in flight, no spills)
+  const double part = mgs_la_block<W, L>(acc, sh);
+  // two buffers by pass parity: pass nb + 2 stores only after barrier nb + 1, which every
+  // workgroup reaches after reading pass nb's partials
+  double *buf = a.partials + (size_t)(nb & 1u) * gridDim.x * 64;
+  if (threadIdx.x < E) st_sc1(&buf[(size_t)blockIdx.x * 64 + threadIdx.x], part);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  ++nb;
+  if (!mgs_grid_barrier(a.st + kMgsLaBar, nb, reinterpret_cast<int *>(a.st + kMgsLaErr))) return false;
+  mgs_la_gather<W, L>(buf, 64, gridDim.x, sh);
+  if (threadIdx.x < 64)
+  {
+    const unsigned nw = mgs_la_close<F, W, L>(sh, sh.S, sh.word);
+    if (threadIdx.x == 0) sh.word = nw;
+  }
+  __syncthreads();
+  return true;
+}
+
+// The last launch of a call (every workgroup resident: G <= CUs, one workgroup fits a CU).
+template <int L>
+__global__ __launch_bounds__(kMgsLaThreads) void k_mgs_la_final(MgsLaArgs a)
+{
+  __shared__ MgsLaShared<L> sh;
+  if (threadIdx.x < 64) sh.S[threadIdx.x] = a.Sfin[threadIdx.x];
+  if (threadIdx.x == 0) sh.word = a.st[a.launch & 1];
+  __syncthreads();
+  unsigned nb = 0;
+  while ((sh.word & 15u) < 8u)  // (uniform: sh.word changes only between barriers)
+  {
+    bool ok = true;
+    switch (sh.word & 15u)
+    {
+      case 0: ok = mgs_la_read_coop<0, L>(a, sh, nb); break;
+      case 1: ok = mgs_la_read_coop<1, L>(a, sh, nb); break;
+      case 2: ok = mgs_la_read_coop<2, L>(a, sh, nb); break;
+      case 3: ok = mgs_la_read_coop<3, L>(a, sh, nb); break;
+      case 4: ok = mgs_la_read_coop<4, L>(a, sh, nb); break;
+      case 5: ok = mgs_la_read_coop<5, L>(a, sh, nb); break;
+      case 6: ok = mgs_la_read_coop<6, L>(a, sh, nb); break;
+      default: ok = mgs_la_read_coop<7, L>(a, sh, nb); break;
+    }
+    if (!ok)
+    {
+      // a peer workgroup never arrived: poison this workgroup's rows (loud, never silent)
+      const double nan = __builtin_nan("");
+      for (i64 i = (i64)blockIdx.x * kMgsLaThreads + threadIdx.x; i < a.n; i += (i64)gridDim.x * kMgsLaThreads)
+      {
+        double2 *r = reinterpret_cast<double2 *>(a.Qb + i * 8);
+#pragma unroll
+        for (int h = 0; h < 4; ++h) r[h] = make_double2(nan, nan);
+      }
+      return;
+    }
+  }
+  mgs_la_write(a.n, a.Qb, sh.S);
+  if (blockIdx.x == 0)
+  {
+    if (threadIdx.x < 64) a.Sfin[threadIdx.x] = sh.S[threadIdx.x];
+    if (threadIdx.x == 0)
+    {
+      a.st[(a.launch + 1) & 1] = sh.word | kMgsLaWritten;
+      a.st[kMgsLaLast] = sh.word | kMgsLaWritten;
+    }
+  }
+}
+
+int mgs_lookahead_default()
+{
+  static const int L = [] {
+    const char *e = std::getenv("EIGMI_MGS_LOOKAHEAD");
+    const int v = e ? std::atoi(e) : kMgsLookaheadDefault;
+    return std::min(8, std::max(1, v));
+  }();
+  return L;
+}
+
+namespace {
+template <int L>
+void mgs_la_enqueue(MgsLaArgs a, int G, bool coop, hipStream_t s)
+{
+  const int reads = (8 + L - 1) / L;  // read launches when every look-ahead is taken
+  for (int l = 0; l < reads; ++l)
+  {
+    a.launch = l;
+    hipLaunchKernelGGL(k_mgs_la<L>, dim3(G), dim3(kMgsLaThreads), 0, s, a);
+  }
+  EIG_HIP(hipGetLastError());
+  a.launch = reads;
+  if (coop)
+  {
+    // an ordinary launch: G <= the CU count and one workgroup fits a CU (VGPRs, LDS), so on an idle
+    // device every workgroup is resident at once, and beside other streams' kernels the ones not
+    // yet resident only wait for CUs those kernels release -- the barriers need no cooperative
+    // launch (whose host call measured ~30 us per orthonormalisation, profiles/r05r_ortho.jsonl)
+    hipLaunchKernelGGL(k_mgs_la_final<L>, dim3(G), dim3(kMgsLaThreads), 0, s, a);
+    EIG_HIP(hipGetLastError());
+    return;
+  }
+  // the worst case in ordinary launches: every look-ahead refused -> 8 read launches + the write
+  for (int l = reads; l < 9; ++l)
+  {
+    a.launch = l;
+    hipLaunchKernelGGL(k_mgs_la<L>, dim3(G), dim3(kMgsLaThreads), 0, s, a);
+  }
+  EIG_HIP(hipGetLastError());
+}
+}  // namespace
+
+bool launch_mgs_lookahead(eig_ctx_t ctx, i64 n, double *Qb, int L, bool coop, hipStream_t s)
+{
+  if (L <= 1 || n <= 0) return false;
+  char *buf = (char *)ctx_buffer(ctx, 11, 64 * sizeof(double) + 64 * sizeof(unsigned));
+  MgsLaArgs a{n, Qb, 0, reinterpret_cast<unsigned *>(buf + 64 * sizeof(double)), reinterpret_cast<double *>(buf),
+              ctx->red.partials, ctx->red.ticket(0)};
+  const int G = grid_for(n, kMgsLaThreads * 2, std::min(kMgsLaGrid, ctx->num_cu > 0 ? ctx->num_cu : kMgsLaGrid));
+  if (L >= 8) mgs_la_enqueue<8>(a, G, coop, s);
+  else if (L >= 4) mgs_la_enqueue<4>(a, G, coop, s);
+  else mgs_la_enqueue<2>(a, G, coop, s);
+  return true;
+}
+
+// read passes of the last look-ahead call on this context (diagnostics; synchronises the stream):
+// -1 none finished, -2 the last launch's grid barrier timed out
+int mgs_lookahead_passes(eig_ctx_t ctx)
+{
+  char *buf = (char *)ctx_buffer(ctx, 11, 64 * sizeof(double) + 64 * sizeof(unsigned));
+  unsigned w[64] = {};
+  EIG_HIP(hipMemcpyAsync(w, buf + 64 * sizeof(double), sizeof(w), hipMemcpyDeviceToHost, ctx->stream));
+  EIG_HIP(hipStreamSynchronize(ctx->stream));
+  if (w[kMgsLaErr]) return -2;
+  return (w[kMgsLaLast] & kMgsLaWritten) ? (int)((w[kMgsLaLast] >> 8) & 255u) : -1;
+}
+
+// ---------------------------------------------------------------------------------------------
 // The same column MGS for a small block (n <= 512 R rows, one rank), in ONE workgroup: the 512
 // threads keep their R rows in registers for all 8 passes, and each pass's sums meet in a
 // workgroup reduction (a xor-shuffle tree per wave, the 8 wave partials summed in wave order by

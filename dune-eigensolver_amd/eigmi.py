@@ -17,6 +17,13 @@ LIB_PATH = os.path.join(_HERE, "lib", "libeigmi_san.so" if os.environ.get("EIGMI
 EIG_OK, EIG_ERR_SHAPE, EIG_ERR_BLOCKSIZE, EIG_ERR_HIP, EIG_ERR_RCCL, EIG_ERR_BREAKDOWN, EIG_ERR_ARG, EIG_ERR_NODEVICE = range(8)
 ORTHO_MGS, ORTHO_CHOLQR, ORTHO_CHOLQR_SPLIT = 0, 1, 2
 ORTHO_GRID = 0x100  # or-ed into the variant: grid-wide MGS passes even for blocks one workgroup holds
+ORTHO_NO_COOP = 0x200  # or-ed into the variant: look-ahead MGS as 9 launches (no in-kernel fallback passes)
+
+
+def ORTHO_LOOKAHEAD(L):
+    """or-ed into ORTHO_MGS: at most L steps per read pass of the diagonal block (include/eigmi.h)"""
+    return int(L) << 12
+
 # matrix kernel-image flags (eig_mat_create_bcsr_ex)
 MAT_NO_BAND, MAT_BAND_GATHER, MAT_NO_STENCIL, MAT_NO_MARCH, MAT_NO_CLASS, MAT_NO_UNIFORM = 1, 2, 4, 8, 16, 32
 # triangular-solve kernels of an LU (eig_lu_set_solver)
@@ -146,6 +153,7 @@ SIGNATURES = {
     "eig_dot_diag_mv8": (_int, [_vp, _i64, _i64, _vp, _vp, _vp]),
     "eig_gram_mv8": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _vp]),
     "eig_orthonormalize_mv8": (_int, [_vp, _i64, _i64, _vp, _int]),
+    "eig_orthonormalize_passes": (_int, [_vp, ctypes.POINTER(ctypes.c_int)]),
     "eig_orthonormalize_naive": (_int, [_vp, _i64, _i64, _vp]),
     "eig_b_orthonormalize_mv8": (_int, [_vp, _i64, _vp, _vp]),
     "eig_random_mv8": (_int, [_vp, _i64, _i64, _u, _vp]),
@@ -549,6 +557,13 @@ def gram_mv8(ctx, n, m1, m2, Q1, Q2, G):
 
 def orthonormalize_mv8(ctx, n, m, Q, variant=ORTHO_MGS):
     ctx.check(lib.eig_orthonormalize_mv8(ctx.h, n, m, Q.ptr, variant))
+
+
+def orthonormalize_passes(ctx):
+    """read passes the last look-ahead MGS on ctx took (its last diagonal block; -1: none)"""
+    p = ctypes.c_int(0)
+    ctx.check(lib.eig_orthonormalize_passes(ctx.h, ctypes.byref(p)))
+    return p.value
 
 
 def orthonormalize_naive(ctx, n, m, Q):

@@ -300,7 +300,20 @@ enum eig_ortho_variant { EIG_ORTHO_MGS = 0, EIG_ORTHO_CHOLQR = 1, EIG_ORTHO_CHOL
 /* or-ed into `variant`: keep the grid-wide MGS passes even where one workgroup holds the block
  * (n <= 4096 on one rank; the two do the same per-row operations -- A/B and tests) */
 enum { EIG_ORTHO_GRID = 0x100 };
+/* or-ed into `variant`: the look-ahead MGS without its barrier-capable last launch (the worst case
+ * of refused look-aheads enqueued as 9 launches; A/B and tests) */
+enum { EIG_ORTHO_NO_COOP = 0x200 };
+/* or-ed into `variant` for EIG_ORTHO_MGS on one rank: at most L (1..8) MGS steps per read pass of
+ * the diagonal block (Gram look-ahead: the window's later steps from the Schur complement of its
+ * Gram rows, taken only while a column keeps >= 1/16 of its squared norm, else that step runs
+ * direct in the next pass).  L = 1: one pass per step, as kernels_cpp.hh:202-229 orders them.
+ * 0: the library default (8, or EIGMI_MGS_LOOKAHEAD). */
+#define EIG_ORTHO_LOOKAHEAD_SHIFT 12
+#define EIG_ORTHO_LOOKAHEAD(L) ((L) << EIG_ORTHO_LOOKAHEAD_SHIFT)
 int eig_orthonormalize_mv8(eig_ctx_t ctx, int64_t n, int64_t m, double *Q, int variant);
+/* Diagnostics: read passes the last look-ahead MGS on ctx took for its last diagonal block (-1
+ * when none ran).  Synchronises the context stream. */
+int eig_orthonormalize_passes(eig_ctx_t ctx, int *passes);
 /* a8: orthonormalize_naive on a column-major (MultiVector<double,1>) block (kernels_cpp.hh:121-155). */
 int eig_orthonormalize_naive(eig_ctx_t ctx, int64_t n, int64_t m, double *Q);
 /* a11: B-orthonormalise Q (B_orthonormalize_blocked, kernels_cpp.hh:356-591); *norm (device)

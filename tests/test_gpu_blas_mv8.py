@@ -132,6 +132,58 @@ def test_orthonormalize_blocked(ctx, variant, name, n, m):
     assert np.abs(got - ref).max() < 1e-12
 
 
+@pytest.mark.parametrize("L", [1, 2, 4, 8])
+@pytest.mark.parametrize("n,m", [(20000, 8), (50001, 24)])
+def test_mgs_lookahead(ctx, L, n, m):
+    """The grid-wide MGS with Gram look-ahead (k_mgs_la, EIG_ORTHO_LOOKAHEAD(L)): at most L steps per
+    read pass, the later ones from the Schur complement of the window's Gram rows.  Well conditioned
+    input: every look-ahead is taken, so the last diagonal block takes ceil(8 / L) read passes, and Q
+    is within 1e-12 of the stepwise restatement orc_orthonormalize_mv8 (kernels_cpp.hh:180-351).
+    L = 1 is the stepwise replay (one pass per step)."""
+    Qh = oracle.random_mv8(n, m, 31)
+    Q = ctx.array(Qh)
+    eigmi.orthonormalize_mv8(ctx, n, m, Q, eigmi.ORTHO_MGS | eigmi.ORTHO_LOOKAHEAD(L))
+    passes = eigmi.orthonormalize_passes(ctx)
+    got = oracle.mv_to_cols(Q.get(), n, m)
+    ref = oracle.mv_to_cols(oracle.orthonormalize_mv8(Qh, n, m, "mgs"), n, m)
+    print(f"look-ahead L={L} n={n} m={m}: {passes} read passes, |Q - Q_ref| = {np.abs(got - ref).max():.2e}")
+    assert np.abs(got.T @ got - np.eye(m)).max() < 1e-13
+    assert np.abs(got - ref).max() < 1e-12
+    if L > 1:
+        assert passes == -(-8 // L)
+
+
+@pytest.mark.parametrize("coop", [True, False], ids=["coop", "launches"])
+@pytest.mark.parametrize("L", [2, 8])
+def test_mgs_lookahead_refused(ctx, L, coop):
+    """A column nearly in the span of the one before it (column 3 = column 2 + 1e-2 noise: after the
+    projection it keeps ~1e-4 of its squared norm, below the 1/16 gate): the look-ahead step for it is
+    refused and the next pass starts there with a direct row, so the block takes one pass more than
+    the well conditioned case for L = 8 (steps 0-2, then 3-7) and five for L = 2 (0-1, 2, 3-4, 5-6,
+    7).  Q stays orthonormal and within the conditioning-scaled tolerance of the restatement.  By
+    default the refused steps run inside the last launch between grid barriers; with
+    EIG_ORTHO_NO_COOP as separate launches of the 9-launch worst case -- the same Q bit for bit."""
+    n, m = 30000, 8
+    X = oracle.mv_to_cols(oracle.random_mv8(n, m, 41), n, m)
+    X[:, 3] = X[:, 2] + 1e-2 * X[:, 3]
+    Qh = oracle.cols_to_mv(X)
+    Q = ctx.array(Qh)
+    flags = 0 if coop else eigmi.ORTHO_NO_COOP
+    eigmi.orthonormalize_mv8(ctx, n, m, Q, eigmi.ORTHO_MGS | eigmi.ORTHO_LOOKAHEAD(L) | flags)
+    passes = eigmi.orthonormalize_passes(ctx)
+    Q2 = ctx.array(Qh)
+    eigmi.orthonormalize_mv8(ctx, n, m, Q2, eigmi.ORTHO_MGS | eigmi.ORTHO_LOOKAHEAD(L) | (flags ^ eigmi.ORTHO_NO_COOP))
+    assert np.array_equal(Q.get(), Q2.get())
+    got = oracle.mv_to_cols(Q.get(), n, m)
+    ref = oracle.mv_to_cols(oracle.orthonormalize_mv8(Qh, n, m, "mgs"), n, m)
+    cond = np.linalg.cond(X)
+    print(f"refused look-ahead L={L}: cond {cond:.1e}, {passes} read passes, |Q - Q_ref| = "
+          f"{np.abs(got - ref).max():.2e}, |Q^T Q - I| = {np.abs(got.T @ got - np.eye(m)).max():.2e}")
+    assert passes == {2: 5, 8: 2}[L]
+    assert np.abs(got.T @ got - np.eye(m)).max() < 1e-14 * cond
+    assert np.abs(got - ref).max() < 1e-14 * cond
+
+
 def test_cholqr_split_half_order(ctx):
     """orthonormalize_avx2_b8 (kernels_avx2.hh:255-381) projects a later block with columns 0-3 of
     the diagonal block, then 4-7 against the updated block; _v2 (:385-622) in one 8x8 step.  The two

@@ -224,27 +224,33 @@ def gram(ctx):
 
 def ortho(ctx):
     """a9 orthonormalize_blocked at C2 size (n = 128^3), m = 8 / 32, best of 5 calls, against the
-    reference's byte model (kernels_cpp.hh:157-175); EIGMI_MGS_INPLACE=1 times the in-place passes."""
+    reference's byte model (kernels_cpp.hh:157-175): the Gram look-ahead MGS with windows L = 8, 4, 2
+    (EIG_ORTHO_LOOKAHEAD; read passes reported) and the stepwise replay (L = 1; EIGMI_MGS_INPLACE=1
+    times the in-place passes there)."""
     n = 128 ** 3
-    tag = ("in-place passes" if os.environ.get("EIGMI_MGS_INPLACE") else
-           "one cooperative launch, grid barriers" if os.environ.get("EIGMI_MGS_COOP") else
-           f"read-only replay passes, grid <= {os.environ.get('EIGMI_MGS_GRID', '512')}")
+    step_tag = ("in-place passes" if os.environ.get("EIGMI_MGS_INPLACE") else
+                "one cooperative launch, grid barriers" if os.environ.get("EIGMI_MGS_COOP") else
+                f"read-only replay passes, grid <= {os.environ.get('EIGMI_MGS_GRID', '512')}")
     for m in (8, 32):
         Qh = oracle.random_mv8(n, m, 1)
         Q = ctx.array(Qh)
+        for L in (8, 4, 2, 1):
+            var = eigmi.ORTHO_MGS | eigmi.ORTHO_LOOKAHEAD(L)
 
-        def once():
-            Q.upload(Qh)
-            ctx.sync()
-            t0 = time.perf_counter()
-            eigmi.orthonormalize_mv8(ctx, n, m, Q)
-            ctx.sync()
-            return time.perf_counter() - t0
-        once()
-        tg = min(once() for _ in range(5))
-        ob = eigmi.lib.eig_bytes_orthonormalize_blocked(n, m, 8)
-        emit(config="C2 128^3", op=f"orthonormalize_blocked (MGS, {tag}) m={m}", gpu_ms=round(tg * 1e3, 4),
-             model_bytes=ob, model_GBs=round(ob / tg / 1e9, 1), model_frac=round(ob / tg / 1e9 / PEAK, 4))
+            def once():
+                Q.upload(Qh)
+                ctx.sync()
+                t0 = time.perf_counter()
+                eigmi.orthonormalize_mv8(ctx, n, m, Q, var)
+                ctx.sync()
+                return time.perf_counter() - t0
+            once()
+            tg = min(once() for _ in range(5))
+            passes = eigmi.orthonormalize_passes(ctx) if L > 1 else 8
+            tag = f"Gram look-ahead L={L}, {passes} read passes" if L > 1 else step_tag
+            ob = eigmi.lib.eig_bytes_orthonormalize_blocked(n, m, 8)
+            emit(config="C2 128^3", op=f"orthonormalize_blocked (MGS, {tag}) m={m}", gpu_ms=round(tg * 1e3, 4),
+                 model_bytes=ob, model_GBs=round(ob / tg / 1e9, 1), model_frac=round(ob / tg / 1e9 / PEAK, 4))
         Q.free()
 
 

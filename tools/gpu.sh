@@ -35,7 +35,7 @@
 #   p1kpmc               P1 Kuhn K 256^3 fused step + eig_mv: trace, FETCH_SIZE, WRITE_SIZE -> sweeppmc/
 #   round                tests smoke profile bench (the round-end evidence set)
 #   cfgtrace             tools/bench_configs.py $CFG under a kernel trace -> $CFG_trace/
-#   ortho                a9 orthonormalize_blocked m = 8 / 32 at 128^3, replay vs in-place passes -> ortho.jsonl
+#   ortho                a9 orthonormalize_blocked m = 8 / 32 at 128^3: look-ahead L = 8/4/2, stepwise replay, in-place -> ortho.jsonl
 #   xch                  the step's allreduce transports on one GPU (one-rank RCCL / mailbox / in-kernel
 #                        mailbox-step): slab and cube sweeps + the bench's N > 1 trial rehearsed -> xch_*.jsonl
 #
@@ -192,7 +192,6 @@ run_task() {
         > "$O/xch_trial.json" 2>> "$O/xch.err" ;;
     ortho)
       timeout -k 10 200 python -u tools/bench_configs.py ortho > "$O/ortho.jsonl" 2> "$O/ortho.err" && \
-      EIGMI_MGS_COOP=1 timeout -k 10 200 python -u tools/bench_configs.py ortho >> "$O/ortho.jsonl" 2>> "$O/ortho.err" && \
       EIGMI_MGS_INPLACE=1 timeout -k 10 200 python -u tools/bench_configs.py ortho >> "$O/ortho.jsonl" 2>> "$O/ortho.err" ;;
     orthogrid)
       # the read-only passes' grid (EIGMI_MGS_GRID workgroups at most)
