@@ -862,8 +862,22 @@ constexpr int fused_b1_waves()
 {
   return (MODE == kExplicit || MODE == kMixed) ? 6 : MODE == kStencil ? 7 : 8;
 }
-template <int R, int MODE>
-__global__ __launch_bounds__(kStreamThreads, fused_b1_waves<MODE>()) void k_lanczos_fused_b1(
+
+// Explicit-column slices, software-pipelined (CPF; eig_mat_tune EIG_TUNE_SELL_CPF): the NEXT slice's
+// first 8 column indices are loaded while this slice's gathers are in flight, so a slice issues its
+// value loads and its gathers together -- one memory round trip per slice instead of two (column
+// index, then the gather it addresses).  Products and their order are rows_dot's (bitwise).
+__device__ __forceinline__ void sell_cols8(const SellB1 &A, i64 s, int lane, i32 (&c)[8])
+{
+  const i64 base = A.slice_ptr[s];
+  const int width = (int)((A.slice_ptr[s + 1] - base) >> 6);
+  const i32 *cs = A.col + base;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) c[k] = k < width ? __builtin_nontemporal_load(cs + k * 64 + lane) : -1;
+}
+
+template <int R, int MODE, bool CPF = false>
+__global__ __launch_bounds__(kStreamThreads, CPF ? 5 : fused_b1_waves<MODE>()) void k_lanczos_fused_b1(
     i64 nrows, i64 own, SellB1 A, const i32 *__restrict__ slices, i64 first, i64 count,
     const dpair *__restrict__ P, dpair *__restrict__ Pout, FusedArgs fa, double *__restrict__ out,
     const double *__restrict__ carry, double *partials, unsigned *ticket)
@@ -910,12 +924,72 @@ __global__ __launch_bounds__(kStreamThreads, fused_b1_waves<MODE>()) void k_lanc
   }
   const XPair xc{P, c};
   double d = 0.0, q2 = 0.0, m2 = 0.0;
+  auto sid = [&](i64 it) { return slices ? (i64)slices[first + it] : first + it; };
+  auto expl = [&](i64 s) { return MODE == kExplicit || A.st_width[s] == 0; };
+  constexpr bool kCpf = CPF && R == 1 && (MODE == kExplicit || MODE == kMixed);
+  i32 cn[8];
+  if constexpr (kCpf)
+  {
+    if (it0 < end && expl(sid(it0))) sell_cols8(A, sid(it0), lane, cn);
+  }
   for (i64 it = it0; it < end; it += step)
   {
-    const i64 s = slices ? (i64)slices[first + it] : first + it;
+    const i64 s = sid(it);
     const i64 r0 = s * C + (i64)lane * R;
     double tv[R], uv[R], acc[R];
-    if constexpr (is_sym<MODE>())
+    if constexpr (kCpf)
+    {
+      const bool more = it + step < end;
+      if (expl(s))
+      {
+        i32 cc[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) cc[k] = cn[k];
+        const i64 base = A.slice_ptr[s];
+        const int width = (int)((A.slice_ptr[s + 1] - base) >> 6);
+        const double *vs = A.val + base;
+        const bool ok = r0 < nrows;
+        const dpair pv = ok ? P[own + r0] : dpair{0.0, 0.0};
+        double a[8], xv[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+        {
+          a[k] = k < width ? __builtin_nontemporal_load(vs + k * 64 + lane) : 0.0;
+          xv[k] = cc[k] >= 0 ? xc(cc[k]) : 0.0;
+        }
+        if (more && expl(sid(it + step))) sell_cols8(A, sid(it + step), lane, cn);  // next slice's columns
+        acc[0] = 0.0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if (cc[k] >= 0) acc[0] += a[k] * xv[k];
+        // (rows wider than 8 entries: the remaining rounds as rows_dot)
+        for (int k0 = 8; k0 < width; k0 += 8)
+        {
+          i32 c2[8];
+          double a2[8], x2[8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k)
+          {
+            const bool in = k0 + k < width;
+            c2[k] = in ? __builtin_nontemporal_load(A.col + base + (k0 + k) * 64 + lane) : -1;
+            a2[k] = in ? __builtin_nontemporal_load(vs + (k0 + k) * 64 + lane) : 0.0;
+          }
+#pragma unroll
+          for (int k = 0; k < 8; ++k) x2[k] = c2[k] >= 0 ? xc(c2[k]) : 0.0;
+#pragma unroll
+          for (int k = 0; k < 8; ++k)
+            if (c2[k] >= 0) acc[0] += a2[k] * x2[k];
+        }
+        tv[0] = pv.x;
+        uv[0] = pv.y;
+      }
+      else
+      {
+        if (more && expl(sid(it + step))) sell_cols8(A, sid(it + step), lane, cn);
+        fused_row_stencil<(W >= 8 ? 4 : 8)>(A, s, P, c, own, lane, acc[0], tv[0], uv[0]);
+      }
+    }
+    else if constexpr (is_sym<MODE>())
     {
       if constexpr (R == 1)
       {
@@ -2713,6 +2787,13 @@ void launch_lanczos_spmv(const eig_mat_s &A, const double *u, const double *up, 
 #undef EIG_LZ
 }
 
+// the explicit-column slices' cross-slice column prefetch (eig_mat_tune EIG_TUNE_SELL_CPF; automatic:
+// off until measured)
+static bool sell_cpf(const eig_mat_s &A)
+{
+  return A.tune_sell_cpf == 1;
+}
+
 void launch_lanczos_fused(const eig_mat_s &A, const double *P, double *Pout, const FusedLaunch &fl,
                           const i32 *slices, i64 first, i64 count, const double *carry, double *out, int ticket,
                           hipStream_t s, ReduceWS red)
@@ -2739,12 +2820,18 @@ void launch_lanczos_fused(const eig_mat_s &A, const double *P, double *Pout, con
       return;
     }
   }
-#define EIG_LF(R_, M_)                                                                                        \
-  hipLaunchKernelGGL((k_lanczos_fused_b1<R_, M_>),                                                           \
-                     dim3(grid_for_slices(k_lanczos_fused_b1<R_, M_>, count, A.ctx->num_cu)),                 \
+#define EIG_LF_(R_, M_, CPF_)                                                                                 \
+  hipLaunchKernelGGL((k_lanczos_fused_b1<R_, M_, CPF_>),                                                     \
+                     dim3(grid_for_slices(k_lanczos_fused_b1<R_, M_, CPF_>, count, A.ctx->num_cu)),           \
                      dim3(kStreamThreads), 0, s, A.nb_rows, A.own_offset, sell_b1(A), slices, first, count,      \
                      reinterpret_cast<const dpair *>(P), reinterpret_cast<dpair *>(Pout), fa, out, carry,        \
                      red.partials, red.ticket(ticket))
+#define EIG_LF(R_, M_)                                                                                        \
+  do                                                                                                          \
+  {                                                                                                           \
+    if (sell_cpf(A) && (M_ == kExplicit || M_ == kMixed)) EIG_LF_(R_, M_, true);                              \
+    else EIG_LF_(R_, M_, false);                                                                              \
+  } while (0)
 #define EIG_LFM(R_)                                                                                           \
   {                                                                                                           \
     const int m_ = image_mode(A);                                                                             \
@@ -2759,6 +2846,7 @@ void launch_lanczos_fused(const eig_mat_s &A, const double *P, double *Pout, con
   EIG_LFM(1)
 #undef EIG_LFM
 #undef EIG_LF
+#undef EIG_LF_
 }
 
 void launch_lanczos_pipe(const eig_mat_s &A, double *T, double *UZ, const double *S, const FusedLaunch &fl,
