@@ -447,6 +447,70 @@ static int image_mode(const eig_mat_s &A)
   return A.n_stencil_slices == A.nslices ? kStencil : kMixed;
 }
 
+// Explicit-column slices, software-pipelined (CPF; eig_mat_tune EIG_TUNE_SELL_CPF): the NEXT slice's
+// first 8 column indices are loaded while this slice's gathers are in flight, so a slice issues its
+// value loads and its gathers together -- one memory round trip per slice instead of two (column
+// index, then the gather it addresses).  Products and their order are rows_dot's (bitwise).
+__device__ __forceinline__ void sell_cols8(const SellB1 &A, i64 s, int lane, i32 (&c)[8])
+{
+  const i64 base = A.slice_ptr[s];
+  const int width = (int)((A.slice_ptr[s + 1] - base) >> 6);
+  const i32 *cs = A.col + base;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) c[k] = k < width ? __builtin_nontemporal_load(cs + k * 64 + lane) : -1;
+}
+
+// the explicit-column slices' cross-slice column prefetch (eig_mat_tune EIG_TUNE_SELL_CPF: 0 off, 1 on,
+// 2 automatic = the fused step only.  Scrambled + RCM Poisson 256^3, same-box A/B
+// (profiles/r05v_csr.jsonl): fused step 404-406 -> 364-366 us; eig_mv 308 -> 314 us, whose one
+// 8-B gather per entry already hides the column round trip at 8 waves / SIMD)
+static bool sell_cpf(const eig_mat_s &A, bool fused)
+{
+  return A.tune_sell_cpf == 1 || (A.tune_sell_cpf == 2 && fused);
+}
+
+// One explicit slice with its first 8 column indices already in registers (cc): the value loads
+// and the gathers issue together, then the next slice's columns (sn >= 0) into cn, then the
+// products in rows_dot's order (and its later rounds for rows wider than 8 entries).
+template <class X>
+__device__ __forceinline__ double sell_row_cpf(const SellB1 &A, i64 s, const X &x, int lane, const i32 (&cc)[8],
+                                               i64 sn, i32 (&cn)[8])
+{
+  const i64 base = A.slice_ptr[s];
+  const int width = (int)((A.slice_ptr[s + 1] - base) >> 6);
+  const double *vs = A.val + base;
+  double a[8], xv[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k)
+  {
+    a[k] = k < width ? __builtin_nontemporal_load(vs + k * 64 + lane) : 0.0;
+    xv[k] = cc[k] >= 0 ? x(cc[k]) : 0.0;
+  }
+  if (sn >= 0) sell_cols8(A, sn, lane, cn);
+  double acc = 0.0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k)
+    if (cc[k] >= 0) acc += a[k] * xv[k];
+  for (int k0 = 8; k0 < width; k0 += 8)
+  {
+    i32 c2[8];
+    double a2[8], x2[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+    {
+      const bool in = k0 + k < width;
+      c2[k] = in ? __builtin_nontemporal_load(A.col + base + (k0 + k) * 64 + lane) : -1;
+      a2[k] = in ? __builtin_nontemporal_load(vs + (k0 + k) * 64 + lane) : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) x2[k] = c2[k] >= 0 ? x(c2[k]) : 0.0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (c2[k] >= 0) acc += a2[k] * x2[k];
+  }
+  return acc;
+}
+
 // 8 waves per SIMD (8 workgroups per CU) except the mixed image, which carries both row paths.
 template <int MODE>
 constexpr int min_waves()
@@ -455,8 +519,8 @@ constexpr int min_waves()
 }
 
 // y[own + r] = (A x)[r], 1x1 blocks (x: window base).
-template <int R, int MODE>
-__global__ __launch_bounds__(kStreamThreads, min_waves<MODE>()) void k_spmv_b1(i64 nrows, i64 own, SellB1 A,
+template <int R, int MODE, bool CPF = false>
+__global__ __launch_bounds__(kStreamThreads, CPF ? 6 : min_waves<MODE>()) void k_spmv_b1(i64 nrows, i64 own, SellB1 A,
                                                                const i32 *__restrict__ slices, i64 first, i64 count,
                                                                const double *__restrict__ x, double *__restrict__ y)
 {
@@ -465,6 +529,38 @@ __global__ __launch_bounds__(kStreamThreads, min_waves<MODE>()) void k_spmv_b1(i
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   i64 it0, end, step;
   slice_sweep(count, wave, it0, end, step);
+  if constexpr (CPF && R == 1 && (MODE == kExplicit || MODE == kMixed))
+  {
+    // explicit slices software-pipelined (sell_row_cpf): the next slice's columns fly with this
+    // slice's gathers; stencil slices of a mixed image as slice_dot
+    auto sid = [&](i64 it) { return slices ? (i64)slices[first + it] : first + it; };
+    auto expl = [&](i64 s) { return MODE == kExplicit || A.st_width[s] == 0; };
+    i32 cn[8];
+    if (it0 < end && expl(sid(it0))) sell_cols8(A, sid(it0), lane, cn);
+    for (i64 it = it0; it < end; it += step)
+    {
+      const i64 s = sid(it);
+      const i64 sn = it + step < end && expl(sid(it + step)) ? sid(it + step) : -1;
+      double acc;
+      if (expl(s))
+      {
+        i32 cc[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) cc[k] = cn[k];
+        acc = sell_row_cpf(A, s, XPlain{x}, lane, cc, sn, cn);
+      }
+      else
+      {
+        if (sn >= 0) sell_cols8(A, sn, lane, cn);
+        double a1[1];
+        slice_dot<1, MODE>(A, s, XPlain{x}, own, lane, a1);
+        acc = a1[0];
+      }
+      const i64 r0 = s * C + lane;
+      if (r0 < nrows) y[own + r0] = acc;
+    }
+    return;
+  }
   for (i64 it = it0; it < end; it += step)
   {
     const i64 s = slices ? (i64)slices[first + it] : first + it;
@@ -863,19 +959,6 @@ constexpr int fused_b1_waves()
   return (MODE == kExplicit || MODE == kMixed) ? 6 : MODE == kStencil ? 7 : 8;
 }
 
-// Explicit-column slices, software-pipelined (CPF; eig_mat_tune EIG_TUNE_SELL_CPF): the NEXT slice's
-// first 8 column indices are loaded while this slice's gathers are in flight, so a slice issues its
-// value loads and its gathers together -- one memory round trip per slice instead of two (column
-// index, then the gather it addresses).  Products and their order are rows_dot's (bitwise).
-__device__ __forceinline__ void sell_cols8(const SellB1 &A, i64 s, int lane, i32 (&c)[8])
-{
-  const i64 base = A.slice_ptr[s];
-  const int width = (int)((A.slice_ptr[s + 1] - base) >> 6);
-  const i32 *cs = A.col + base;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) c[k] = k < width ? __builtin_nontemporal_load(cs + k * 64 + lane) : -1;
-}
-
 template <int R, int MODE, bool CPF = false>
 __global__ __launch_bounds__(kStreamThreads, CPF ? 5 : fused_b1_waves<MODE>()) void k_lanczos_fused_b1(
     i64 nrows, i64 own, SellB1 A, const i32 *__restrict__ slices, i64 first, i64 count,
@@ -945,41 +1028,9 @@ __global__ __launch_bounds__(kStreamThreads, CPF ? 5 : fused_b1_waves<MODE>()) v
         i32 cc[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) cc[k] = cn[k];
-        const i64 base = A.slice_ptr[s];
-        const int width = (int)((A.slice_ptr[s + 1] - base) >> 6);
-        const double *vs = A.val + base;
-        const bool ok = r0 < nrows;
-        const dpair pv = ok ? P[own + r0] : dpair{0.0, 0.0};
-        double a[8], xv[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k)
-        {
-          a[k] = k < width ? __builtin_nontemporal_load(vs + k * 64 + lane) : 0.0;
-          xv[k] = cc[k] >= 0 ? xc(cc[k]) : 0.0;
-        }
-        if (more && expl(sid(it + step))) sell_cols8(A, sid(it + step), lane, cn);  // next slice's columns
-        acc[0] = 0.0;
-#pragma unroll
-        for (int k = 0; k < 8; ++k)
-          if (cc[k] >= 0) acc[0] += a[k] * xv[k];
-        // (rows wider than 8 entries: the remaining rounds as rows_dot)
-        for (int k0 = 8; k0 < width; k0 += 8)
-        {
-          i32 c2[8];
-          double a2[8], x2[8];
-#pragma unroll
-          for (int k = 0; k < 8; ++k)
-          {
-            const bool in = k0 + k < width;
-            c2[k] = in ? __builtin_nontemporal_load(A.col + base + (k0 + k) * 64 + lane) : -1;
-            a2[k] = in ? __builtin_nontemporal_load(vs + (k0 + k) * 64 + lane) : 0.0;
-          }
-#pragma unroll
-          for (int k = 0; k < 8; ++k) x2[k] = c2[k] >= 0 ? xc(c2[k]) : 0.0;
-#pragma unroll
-          for (int k = 0; k < 8; ++k)
-            if (c2[k] >= 0) acc[0] += a2[k] * x2[k];
-        }
+        const dpair pv = r0 < nrows ? P[own + r0] : dpair{0.0, 0.0};
+        const i64 sn = more && expl(sid(it + step)) ? sid(it + step) : -1;
+        acc[0] = sell_row_cpf(A, s, xc, lane, cc, sn, cn);
         tv[0] = pv.x;
         uv[0] = pv.y;
       }
@@ -2717,11 +2768,16 @@ void launch_spmv(const eig_mat_s &A, const double *x, double *y, const i32 *slic
                        slices, first, count, A.val, A.col, x, yo);                                      \
     return;                                                                                             \
   }
+#define EIG_B1_(R_, M_, CPF_)                                                                            \
+  {                                                                                                      \
+    const int G = grid_for_slices(k_spmv_b1<R_, M_, CPF_>, count, ncu);                                  \
+    hipLaunchKernelGGL((k_spmv_b1<R_, M_, CPF_>), dim3(G), dim3(kStreamThreads), 0, s, A.nb_rows,         \
+                       A.own_offset, sell_b1(A), slices, first, count, x, y);                            \
+  }
 #define EIG_B1(R_, M_)                                                                                   \
   {                                                                                                      \
-    const int G = grid_for_slices(k_spmv_b1<R_, M_>, count, ncu);                                        \
-    hipLaunchKernelGGL((k_spmv_b1<R_, M_>), dim3(G), dim3(kStreamThreads), 0, s, A.nb_rows, A.own_offset, \
-                       sell_b1(A), slices, first, count, x, y);                                          \
+    if (sell_cpf(A, false) && (M_ == kExplicit || M_ == kMixed)) EIG_B1_(R_, M_, true)                   \
+    else EIG_B1_(R_, M_, false)                                                                          \
   }
 #define EIG_B1M(R_)                                                                                      \
   {                                                                                                      \
@@ -2741,6 +2797,7 @@ void launch_spmv(const eig_mat_s &A, const double *x, double *y, const i32 *slic
   }
 #undef EIG_B1M
 #undef EIG_B1
+#undef EIG_B1_
   EIG_BLK(1, 2) EIG_BLK(1, 3) EIG_BLK(1, 4)
   EIG_BLK(2, 1) EIG_BLK(2, 2) EIG_BLK(2, 3) EIG_BLK(2, 4)
   EIG_BLK(3, 1) EIG_BLK(3, 2) EIG_BLK(3, 3) EIG_BLK(3, 4)
@@ -2787,13 +2844,6 @@ void launch_lanczos_spmv(const eig_mat_s &A, const double *u, const double *up, 
 #undef EIG_LZ
 }
 
-// the explicit-column slices' cross-slice column prefetch (eig_mat_tune EIG_TUNE_SELL_CPF; automatic:
-// off until measured)
-static bool sell_cpf(const eig_mat_s &A)
-{
-  return A.tune_sell_cpf == 1;
-}
-
 void launch_lanczos_fused(const eig_mat_s &A, const double *P, double *Pout, const FusedLaunch &fl,
                           const i32 *slices, i64 first, i64 count, const double *carry, double *out, int ticket,
                           hipStream_t s, ReduceWS red)
@@ -2829,7 +2879,7 @@ void launch_lanczos_fused(const eig_mat_s &A, const double *P, double *Pout, con
 #define EIG_LF(R_, M_)                                                                                        \
   do                                                                                                          \
   {                                                                                                           \
-    if (sell_cpf(A) && (M_ == kExplicit || M_ == kMixed)) EIG_LF_(R_, M_, true);                              \
+    if (sell_cpf(A, true) && (M_ == kExplicit || M_ == kMixed)) EIG_LF_(R_, M_, true);                        \
     else EIG_LF_(R_, M_, false);                                                                              \
   } while (0)
 #define EIG_LFM(R_)                                                                                           \

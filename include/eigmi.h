@@ -230,10 +230,10 @@ int eig_mat_kernel_info(eig_mat_t mat, int op, char *name, int name_len);
  * for the summation order of the step's reductions. */
 enum { EIG_TUNE_MARCH_RUNS = 1, EIG_TUNE_BOX_SEGS = 2, EIG_TUNE_MARCH_PREFETCH = 3, EIG_TUNE_HALO = 4,
        EIG_TUNE_CACHE = 5, EIG_TUNE_BOX_COLS = 6, EIG_TUNE_BOX_MAP = 7, EIG_TUNE_SELL_CPF = 8 };
-/* EIG_TUNE_SELL_CPF (fused Lanczos step on explicit-column SELL slices): 1 = the next slice's column
- * indices loaded while this slice's gathers are in flight (one memory round trip per slice instead
- * of two; 5 waves per SIMD instead of 6), 0 = off, 2 = automatic (the library default).  Results
- * bitwise identical. */
+/* EIG_TUNE_SELL_CPF (explicit-column SELL slices): 1 = the next slice's column indices loaded while
+ * this slice's gathers are in flight (one memory round trip per slice instead of two), in the fused
+ * Lanczos step (5 waves per SIMD instead of 6) and in eig_mv; 0 = off; 2 = automatic (the library
+ * default: the fused step only).  Results bitwise identical. */
 /* EIG_TUNE_BOX_MAP (measurement; k_box_mv32): 1 = XCD-contiguous tile map (the workgroups resident on
  * one XCD hold whole rows of adjacent tiles), 0 = dispatch order.  Results bitwise identical. */
 /* EIG_TUNE_BOX_COLS (box-image kernels, EIG_OP_SPMM32 / EIG_OP_CHEB32 on matrices without a row-class

@@ -1,7 +1,8 @@
-"""The fused Lanczos step on explicit-column SELL slices with the cross-slice column prefetch
-(EIG_TUNE_SELL_CPF = 1, k_lanczos_fused_b1<1, MODE, true>): the next slice's column indices load while
-this slice's gathers fly, the products and their order stay rows_dot's -- so alpha / beta must be
-BITWISE those of the plain kernel, on a scrambled + RCM Poisson matrix (every slice explicit or mixed)
+"""Explicit-column SELL slices with the cross-slice column prefetch (EIG_TUNE_SELL_CPF, the default;
+k_lanczos_fused_b1<1, MODE, true> and k_spmv_b1<1, MODE, true>): the next slice's column indices load
+while this slice's gathers fly, the products and their order stay rows_dot's -- so eig_mv must be
+BITWISE the reference row loop (oracle.csr_mv) with and without it, and the fused step's alpha / beta
+bitwise those of the plain kernel, on a scrambled + RCM Poisson matrix (every slice explicit or mixed)
 and on ragged rows wider than one 8-entry round (the later rounds' path)."""
 import numpy as np
 import pytest
@@ -47,8 +48,26 @@ def test_sell_column_prefetch_bitwise(ctx, name, mat):
     a1, b1, k1 = _run(ctx, mat, 1)
     print(f"{name}: kernel {k1}, {a0.size} steps")
     assert np.array_equal(a0, a1) and np.array_equal(b0, b1)
-    # and the recurrence is the restatement's (tolerance: the sums' order differs)
+    # and the recurrence is the restatement's (tolerance: the sums' order differs; the first 12 steps,
+    # before the unreorthogonalised recurrence's rounding growth on the ragged matrix's cluster)
     rp, c, v = mat
     A = oracle.CSR(rp.size - 1, rp, c, v)
     ra, rb = oracle.lanczos_fused(A, oracle.random_vec(A.n, 9), a0.size)
-    assert np.allclose(a1, ra, rtol=1e-10, atol=1e-12) and np.allclose(b1, rb, rtol=1e-10, atol=1e-12)
+    assert np.allclose(a1[:12], ra[:12], rtol=1e-10, atol=0) and np.allclose(b1[:12], rb[:12], rtol=1e-10, atol=0)
+
+
+@pytest.mark.parametrize("name,mat", list(_mats()), ids=[m[0] for m in _mats()])
+def test_sell_column_prefetch_mv_bitwise(ctx, name, mat):
+    rp, c, v = mat
+    A = oracle.CSR(rp.size - 1, rp, c, v)
+    xh = np.random.default_rng(3).standard_normal(A.n)
+    ref = oracle.csr_mv(A, xh)
+    M = eigmi.Matrix.from_bcsr(ctx, rp, c, v, flags=eigmi.MAT_NO_BAND)
+    x, y = ctx.array(xh), ctx.zeros(A.n)
+    try:
+        for cpf in (0, 1, 2):
+            M.tune(sell_cpf=cpf)
+            M.mv(x, y)
+            assert np.array_equal(y.get(), ref), cpf
+    finally:
+        M.close()

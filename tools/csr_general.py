@@ -50,12 +50,15 @@ def main():
             "reorder_s": round(t_reorder, 1), "upload_s": round(t_up, 1)}
     x = ctx.array(np.random.default_rng(0).standard_normal(n))
     y = ctx.zeros(n)
-    M.mv_timed(x, y, 3)
-    ms = min(M.mv_timed(x, y, args.reps) for _ in range(3))
-    b = eigmi.bytes_spmv(n, nnz)
-    print(json.dumps(dict(base, op="eig_mv", kernel=M.kernel("spmv"), us=round(ms * 1e3, 2), csr_bytes=b,
-                          GBs=round(b / ms / 1e6, 1), frac=round(b / ms / 1e6 / PEAK, 4))), flush=True)
-    for fused, cpf in ((True, 0), (True, 1), (False, 0)):
+    for cpf in (0, 1, 0, 1):
+        M.tune(sell_cpf=cpf)  # EIG_TUNE_SELL_CPF: explicit slices' cross-slice column prefetch
+        M.mv_timed(x, y, 3)
+        ms = min(M.mv_timed(x, y, args.reps) for _ in range(3))
+        b = eigmi.bytes_spmv(n, nnz)
+        print(json.dumps(dict(base, op="eig_mv" + (" +col-prefetch" if cpf else ""), kernel=M.kernel("spmv"),
+                              us=round(ms * 1e3, 2), csr_bytes=b, GBs=round(b / ms / 1e6, 1),
+                              frac=round(b / ms / 1e6 / PEAK, 4))), flush=True)
+    for fused, cpf in ((True, 0), (True, 1), (True, 0), (True, 1), (False, 0)):
         M.tune(sell_cpf=cpf)  # EIG_TUNE_SELL_CPF: explicit slices' cross-slice column prefetch (fused step)
         ws = eigmi.LanczosWorkspace(M, args.steps + 4, seed=123, fused=fused)
         ws.step(2)
