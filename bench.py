@@ -311,6 +311,11 @@ def kernel_instance(M, kname):
         return f"{kname}<unsigned char, true, {info.march_variant}>"
     if kname.endswith("_b1") and info.sym_offsets == 0:
         mode = 0 if info.stencil_slices == 0 else 1 if info.stencil_slices == info.nslices else 2
+        if kname in ("k_lanczos_fused_b1", "k_spmv_b1"):
+            # <R, mode, CPF>: the explicit slices' column prefetch, by default in the fused step on
+            # explicit / mixed images (eigmi.h EIG_TUNE_SELL_CPF)
+            cpf = kname == "k_lanczos_fused_b1" and mode in (0, 2)
+            return f"{kname}<1, {mode}, {'true' if cpf else 'false'}>"
         return f"{kname}<1, {mode}>"
     return kname
 
