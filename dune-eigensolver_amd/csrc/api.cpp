@@ -548,7 +548,7 @@ extern "C" int eig_mat_tune(eig_mat_t A, int key, int value)
     EIG_CHECK(A && value >= 0, EIG_ERR_ARG, "eig_mat_tune: bad argument");
     EIG_CHECK(key == EIG_TUNE_MARCH_RUNS || key == EIG_TUNE_BOX_SEGS || key == EIG_TUNE_MARCH_PREFETCH ||
                   key == EIG_TUNE_HALO || key == EIG_TUNE_CACHE || key == EIG_TUNE_BOX_COLS ||
-                  key == EIG_TUNE_BOX_MAP || key == EIG_TUNE_SELL_CPF,
+                  key == EIG_TUNE_BOX_MAP || key == EIG_TUNE_SELL_CPF || key == EIG_TUNE_MARCH_LINES,
               EIG_ERR_ARG, "eig_mat_tune: unknown key");
     EIG_CHECK(key != EIG_TUNE_HALO || value <= 1, EIG_ERR_ARG, "eig_mat_tune: halo mode 0 / 1");
     EIG_CHECK(key != EIG_TUNE_MARCH_PREFETCH || value <= 15, EIG_ERR_ARG, "eig_mat_tune: march variant 0..15");
@@ -560,6 +560,11 @@ extern "C" int eig_mat_tune(eig_mat_t A, int key, int value)
       A->tune_halo_whole = value;
     else if (key == EIG_TUNE_CACHE)
       A->tune_cache = value;
+    else if (key == EIG_TUNE_MARCH_LINES)
+    {
+      EIG_CHECK(value == 0 || value == 4, EIG_ERR_ARG, "eig_mat_tune: march lines 0 / 4");
+      A->tune_march_lines = value;
+    }
     else if (key == EIG_TUNE_SELL_CPF)
     {
       EIG_CHECK(value <= 2, EIG_ERR_ARG, "eig_mat_tune: column prefetch 0 / 1 / 2");

@@ -248,6 +248,7 @@ struct eig_mat_s {
   int tune_box_cols = 0;    // eig_mat_tune(EIG_TUNE_BOX_COLS): columns per box-image workgroup (16 / 32), 0 = automatic
   int tune_box_map = 0;     // eig_mat_tune(EIG_TUNE_BOX_MAP): 1 = XCD-contiguous tile map of k_box_mv32 (measurement)
   int tune_sell_cpf = 2;    // eig_mat_tune(EIG_TUNE_SELL_CPF): explicit slices' column prefetch, 2 = automatic
+  int tune_march_lines = 0; // eig_mat_tune(EIG_TUNE_MARCH_LINES): 4 = line-group mapping of the value march
   int tune_box_segs = 0;    // eig_mat_tune(EIG_TUNE_BOX_SEGS): z segments per box tile column, 0 = automatic
   // Box-stencil image for the 32-column SpMM / Chebyshev kernel (k_box.hip): box_state 0 = not
   // examined yet, 1 = built, -1 = the band is not a 3-D box stencil; box_val[k n + r] = the entry of

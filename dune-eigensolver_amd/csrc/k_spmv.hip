@@ -1132,6 +1132,10 @@ struct MarchPlan {
   // eig_mat_tune(EIG_TUNE_CACHE) bits for the value march (measurement): 2 = the value streams with the
   // default cache policy instead of nontemporal, 4 = the +D pair stream nontemporal
   int cache;
+  // geo2 value marches: 4 = a workgroup's 4 waves march the same 64 x of 4 consecutive y lines (their
+  // +-nx gathers then mostly read lines their sibling waves just loaded on the same CU) instead of the
+  // 4 x runs of one line; 0 = the item order (eig_mat_tune EIG_TUNE_MARCH_LINES)
+  int lines;
 };
 // store helper of the geo2 epilogues: temporal when the plan says the vectors fit the MALL
 template <class T>
@@ -1300,9 +1304,24 @@ __device__ __forceinline__ void march_rows_geo2(const SellB1 &A, const MarchPlan
   typedef typename X::raw raw;
   constexpr unsigned SZ = sizeof(raw);
   const int D = (int)mp.D, own32 = (int)own;
-  const int item = (int)swizzled_block() * kWaves + wave;
-  if (item >= mp.ncol * mp.nseg) return;
-  const int col = item % mp.ncol, seg = item / mp.ncol;
+  int col, seg;
+  if (mp.lines == 4)
+  {
+    // workgroup -> (x run, group of 4 lines, plane run); wave -> line of the group
+    const int nxc = mp.gx / 64, per = nxc * (mp.gy / 4);
+    const int wg = (int)swizzled_block();
+    if (wg >= per * mp.nseg) return;
+    seg = wg / per;
+    const int r = wg % per;
+    col = ((r / nxc) * 4 + wave) * nxc + r % nxc;
+  }
+  else
+  {
+    const int item = (int)swizzled_block() * kWaves + wave;
+    if (item >= mp.ncol * mp.nseg) return;
+    col = item % mp.ncol;
+    seg = item / mp.ncol;
+  }
   const int z0 = (int)(mp.zb + seg * mp.nplanes / mp.nseg), z1 = (int)(mp.zb + (seg + 1) * mp.nplanes / mp.nseg);
   const unsigned nbytes = (unsigned)(A.xlast + 1) * SZ;
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(x.ptr()), 0, (int)nbytes, 0x00020000);
@@ -2691,6 +2710,11 @@ static MarchPlan march_plan(const eig_mat_s &A, int mode, i64 zb = 0, i64 ze = -
   // 8.0 us)
   mp.tstore = fused && uni >= 7 && (A.window * 16 * 3 <= (i64(128) << 20) || (A.tune_cache & 1));
   mp.cache = A.tune_cache;
+  // line groups (geo2 value marches 10 / 11 / 14 / 15 on grids of whole 64-x runs and 4-line groups)
+  mp.lines = A.tune_march_lines == 4 && !kuhn && uni >= 10 && uni <= 15 && uni != 12 && mp.gx % 64 == 0 &&
+                     mp.gx > 0 && mp.gy % 4 == 0 && (i64)mp.gx * mp.gy == D
+                 ? 4
+                 : 0;
   mp.zb = zb;
   mp.nplanes = nplanes;
   mp.mrows = A.nslices * 64;

@@ -486,7 +486,7 @@ class Matrix:
         return y
 
     def tune(self, march_runs=None, box_segs=None, march_prefetch=None, halo_whole=None, cache=None,
-             box_cols=None, box_map=None, sell_cpf=None):
+             box_cols=None, box_map=None, sell_cpf=None, march_lines=None):
         """eig_mat_tune, only for the keys given (None leaves a key as it is): EIG_TUNE_MARCH_RUNS =
         plane runs per column of the plane-march kernels, EIG_TUNE_BOX_SEGS = z segments per tile
         column of the box kernels, EIG_TUNE_MARCH_PREFETCH = the geometric march variant (eigmi.h;
@@ -507,6 +507,8 @@ class Matrix:
             self.ctx.check(lib.eig_mat_tune(self.h, 7, int(box_map)))
         if sell_cpf is not None:  # EIG_TUNE_SELL_CPF: explicit slices' column prefetch (0 / 1 / 2 = auto)
             self.ctx.check(lib.eig_mat_tune(self.h, 8, int(sell_cpf)))
+        if march_lines is not None:  # EIG_TUNE_MARCH_LINES: 4 = line-group mapping of the value march
+            self.ctx.check(lib.eig_mat_tune(self.h, 9, int(march_lines)))
 
     def shift_diag(self, shift):
         self.ctx.check(lib.eig_mat_shift_diag(self.h, shift))

@@ -229,7 +229,13 @@ int eig_mat_kernel_info(eig_mat_t mat, int op, char *name, int name_len);
  * bitwise unchanged, every row's sum is formed in one place).  Results are otherwise unchanged except
  * for the summation order of the step's reductions. */
 enum { EIG_TUNE_MARCH_RUNS = 1, EIG_TUNE_BOX_SEGS = 2, EIG_TUNE_MARCH_PREFETCH = 3, EIG_TUNE_HALO = 4,
-       EIG_TUNE_CACHE = 5, EIG_TUNE_BOX_COLS = 6, EIG_TUNE_BOX_MAP = 7, EIG_TUNE_SELL_CPF = 8 };
+       EIG_TUNE_CACHE = 5, EIG_TUNE_BOX_COLS = 6, EIG_TUNE_BOX_MAP = 7, EIG_TUNE_SELL_CPF = 8,
+       EIG_TUNE_MARCH_LINES = 9 };
+/* EIG_TUNE_MARCH_LINES (value marches on 3-D geometric bands): 4 = a workgroup's 4 waves march the
+ * same 64 x of 4 consecutive grid lines (their +-nx gathers mostly read the lines their sibling
+ * waves just loaded), 0 = the 4 x runs of one line (default; measurement switch: the fused step at
+ * 256^3 measured the same either way, 222.5 vs 222.7 us, FETCH_SIZE 2 % lower).  eig_mv bitwise
+ * unchanged; the fused step's reductions sum in another order. */
 /* EIG_TUNE_SELL_CPF (explicit-column SELL slices): 1 = the next slice's column indices loaded while
  * this slice's gathers are in flight (one memory round trip per slice instead of two), in the fused
  * Lanczos step (5 waves per SIMD instead of 6) and in eig_mv; 0 = off; 2 = automatic (the library

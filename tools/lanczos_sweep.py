@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """A/B of Lanczos step / SpMV kernel images on one GPU, interleaved rounds in ONE process.
 
-Variant spec "<fused|pipelined|classic|mv>[:<image>][@<runs>][#<pf>][~<transport>]" (runs: plane runs per
+Variant spec "<fused|pipelined|classic|mv>[:<image>][@<runs>][#<pf>][^<lines>][~<transport>]" (runs: plane runs per
 column of the march kernels, pf: the geometric march variant, eig_mat_tune; default automatic;
 transport, with --comm self: the one-rank allreduce of every step -- rccl, mailbox, or step = the
 fused step's sums exchanged inside the step kernel, EIG_AR_MAILBOX_STEP) with image one of
@@ -32,15 +32,17 @@ IMAGES = {"band": 0, "arrays": eigmi.MAT_NO_UNIFORM, "gather": eigmi.MAT_BAND_GA
 
 
 def parse(spec):
-    """"op[:image][@runs][#pf][%cache][~transport]" -> (op, image flags, plane runs per column (0 =
-    automatic), geometric march variant (eig_mat_tune EIG_TUNE_MARCH_PREFETCH; 0 = automatic), cache
-    bits)."""
+    """"op[:image][@runs][#pf][%cache][^lines][~transport]" -> (op, image flags, plane runs per column
+    (0 = automatic), geometric march variant (eig_mat_tune EIG_TUNE_MARCH_PREFETCH; 0 = automatic),
+    cache bits, lines per workgroup of the value march (EIG_TUNE_MARCH_LINES; 0 = default))."""
     spec = spec.partition("~")[0]
+    spec, _, lines = spec.partition("^")
     spec, _, cache = spec.partition("%")
     spec, _, pf = spec.partition("#")
     spec, _, runs = spec.partition("@")
     parts = spec.split(":")
-    return parts[0], IMAGES[parts[1] if len(parts) > 1 else "band"], int(runs or 0), int(pf or 0), int(cache or 0)
+    return (parts[0], IMAGES[parts[1] if len(parts) > 1 else "band"], int(runs or 0), int(pf or 0), int(cache or 0),
+            int(lines or 0))
 
 
 def main():
@@ -97,9 +99,9 @@ def main():
     xy = None
     for _ in range(args.rounds):
         for spec in specs:
-            op, fl, runs, pf, cache = parse(spec)
+            op, fl, runs, pf, cache, lines = parse(spec)
             M = mats[fl]
-            M.tune(runs, march_prefetch=pf, cache=cache)
+            M.tune(runs, march_prefetch=pf, cache=cache, march_lines=lines)
             if args.comm == "self":
                 tr = spec.partition("~")[2] or "rccl"
                 ctx.select_allreduce({"step": "mailbox-step"}.get(tr, tr))
@@ -122,9 +124,9 @@ def main():
             res[spec]["step_us"].append(t2.total_ms / args.steps * 1e3)
             ws.close()
     for spec in specs:
-        op, fl, runs, pf, cache = parse(spec)
+        op, fl, runs, pf, cache, lines = parse(spec)
         M = mats[fl]
-        M.tune(runs, march_prefetch=pf, cache=cache)
+        M.tune(runs, march_prefetch=pf, cache=cache, march_lines=lines)
         kb = (eigmi.bytes_spmv(n, nnz) if op == "mv" else
               eigmi.bytes_spmv(n, nnz) + 56 * n if op == "pipelined" else
               eigmi.bytes_lanczos_fused(n, nnz) if op == "fused" else eigmi.bytes_lanczos_k1(n, nnz))
