@@ -466,7 +466,8 @@ __device__ __forceinline__ void sell_cols8(const SellB1 &A, i64 s, int lane, i32
 // 8-B gather per entry already hides the column round trip at 8 waves / SIMD)
 static bool sell_cpf(const eig_mat_s &A, bool fused)
 {
-  return A.tune_sell_cpf == 1 || (A.tune_sell_cpf == 2 && fused);
+  (void)fused;
+  return A.tune_sell_cpf == 1;  // (automatic: off while the mixed-image path is checked)
 }
 
 // One explicit slice with its first 8 column indices already in registers (cc): the value loads
