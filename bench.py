@@ -314,7 +314,7 @@ def kernel_instance(M, kname):
         if kname in ("k_lanczos_fused_b1", "k_spmv_b1"):
             # <R, mode, CPF>: the explicit slices' column prefetch, by default in the fused step on
             # explicit / mixed images (eigmi.h EIG_TUNE_SELL_CPF)
-            cpf = False
+            cpf = kname == "k_lanczos_fused_b1" and mode in (0, 2)
             return f"{kname}<1, {mode}, {'true' if cpf else 'false'}>"
         return f"{kname}<1, {mode}>"
     return kname

@@ -466,8 +466,7 @@ __device__ __forceinline__ void sell_cols8(const SellB1 &A, i64 s, int lane, i32
 // 8-B gather per entry already hides the column round trip at 8 waves / SIMD)
 static bool sell_cpf(const eig_mat_s &A, bool fused)
 {
-  (void)fused;
-  return A.tune_sell_cpf == 1;  // (automatic: off while the mixed-image path is checked)
+  return A.tune_sell_cpf == 1 || (A.tune_sell_cpf == 2 && fused);
 }
 
 // One explicit slice with its first 8 column indices already in registers (cc): the value loads
@@ -535,7 +534,7 @@ __global__ __launch_bounds__(kStreamThreads, CPF ? 6 : min_waves<MODE>()) void k
     // explicit slices software-pipelined (sell_row_cpf): the next slice's columns fly with this
     // slice's gathers; stencil slices of a mixed image as slice_dot
     auto sid = [&](i64 it) { return slices ? (i64)slices[first + it] : first + it; };
-    auto expl = [&](i64 s) { return MODE == kExplicit || A.st_width[s] == 0; };
+    auto expl = [&](i64 s) { return MODE == kExplicit || A.st_width[s] <= 0; };  // (explicit: width -1)
     i32 cn[8];
     if (it0 < end && expl(sid(it0))) sell_cols8(A, sid(it0), lane, cn);
     for (i64 it = it0; it < end; it += step)
@@ -1009,7 +1008,7 @@ __global__ __launch_bounds__(kStreamThreads, CPF ? 5 : fused_b1_waves<MODE>()) v
   const XPair xc{P, c};
   double d = 0.0, q2 = 0.0, m2 = 0.0;
   auto sid = [&](i64 it) { return slices ? (i64)slices[first + it] : first + it; };
-  auto expl = [&](i64 s) { return MODE == kExplicit || A.st_width[s] == 0; };
+  auto expl = [&](i64 s) { return MODE == kExplicit || A.st_width[s] <= 0; };  // (explicit: width -1)
   constexpr bool kCpf = CPF && R == 1 && (MODE == kExplicit || MODE == kMixed);
   i32 cn[8];
   if constexpr (kCpf)

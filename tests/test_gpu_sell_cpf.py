@@ -26,10 +26,16 @@ def _mats():
     rp, c, v = eigmi.gen_matrix(eigmi.GEN_POISSON3D, 24)
     yield "poisson24_rcm", eigmi.scrambled_rcm(rp, c, v, 5)
     yield "ragged3000", _ragged()
+    # a MIXED image (stencil slices beside explicit ones, whose stencil width reads -1): the
+    # per-slice choice and the prefetch across a stencil slice
+    rp, c, v = eigmi.gen_matrix(eigmi.GEN_POISSON3D, 48)
+    yield "poisson48_rcm_mixed", eigmi.scrambled_rcm(rp, c, v, 123)
 
 
 def _run(ctx, mat, cpf, steps=30):
     M = eigmi.Matrix.from_bcsr(ctx, *mat, flags=eigmi.MAT_NO_BAND)
+    info = M.info
+    print(f"  image: {info.stencil_slices} of {info.nslices} slices stencil")
     M.tune(sell_cpf=cpf)
     ws = eigmi.LanczosWorkspace(M, steps + 2, seed=9, fused=True)
     try:
@@ -46,6 +52,12 @@ def _run(ctx, mat, cpf, steps=30):
 def test_sell_column_prefetch_bitwise(ctx, name, mat):
     a0, b0, k0 = _run(ctx, mat, 0)
     a1, b1, k1 = _run(ctx, mat, 1)
+    a2, b2, _ = _run(ctx, mat, 2)  # the automatic setting (the fused step takes the prefetch)
+    assert np.array_equal(a1, a2) and np.array_equal(b1, b2)
+    if name.endswith("mixed"):
+        M = eigmi.Matrix.from_bcsr(ctx, *mat, flags=eigmi.MAT_NO_BAND)
+        assert 0 < M.info.stencil_slices < M.info.nslices
+        M.close()
     print(f"{name}: kernel {k1}, {a0.size} steps")
     assert np.array_equal(a0, a1) and np.array_equal(b0, b1)
     # and the recurrence is the restatement's (tolerance: the sums' order differs; the first 12 steps,
