@@ -36,6 +36,7 @@
 #   round                tests smoke profile bench (the round-end evidence set)
 #   cfgtrace             tools/bench_configs.py $CFG under a kernel trace -> $CFG_trace/
 #   ortho                a9 orthonormalize_blocked m = 8 / 32 at 128^3: look-ahead L = 8/4/2, stepwise replay, in-place -> ortho.jsonl
+#   orthopmc             the same under a kernel trace + FETCH_SIZE / WRITE_SIZE passes -> orthopmc/
 #   xch                  the step's allreduce transports on one GPU (one-rank RCCL / mailbox / in-kernel
 #                        mailbox-step): slab and cube sweeps + the bench's N > 1 trial rehearsed -> xch_*.jsonl
 #
@@ -193,6 +194,15 @@ run_task() {
     ortho)
       timeout -k 10 200 python -u tools/bench_configs.py ortho > "$O/ortho.jsonl" 2> "$O/ortho.err" && \
       EIGMI_MGS_INPLACE=1 timeout -k 10 200 python -u tools/bench_configs.py ortho >> "$O/ortho.jsonl" 2>> "$O/ortho.err" ;;
+    orthopmc)
+      # a9 under a kernel trace and FETCH_SIZE / WRITE_SIZE passes (tools/summarize_pmc_dirs.py)
+      prof_env
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/orthopmc/trace" -o trace -- \
+        python3 tools/bench_configs.py ortho > "$O/orthopmc.jsonl" 2> "$O/orthopmc_t.err" && \
+      timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/orthopmc/fetch" -o pmc -- \
+        python3 tools/bench_configs.py ortho > /dev/null 2> "$O/orthopmc_f.err" && \
+      timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/orthopmc/write" -o pmc -- \
+        python3 tools/bench_configs.py ortho > /dev/null 2> "$O/orthopmc_w.err" ;;
     orthogrid)
       # the read-only passes' grid (EIGMI_MGS_GRID workgroups at most)
       for g in 256 512 1024 2048; do
