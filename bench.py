@@ -312,9 +312,9 @@ def kernel_instance(M, kname):
     if kname.endswith("_b1") and info.sym_offsets == 0:
         mode = 0 if info.stencil_slices == 0 else 1 if info.stencil_slices == info.nslices else 2
         if kname in ("k_lanczos_fused_b1", "k_spmv_b1"):
-            # <R, mode, CPF>: the explicit slices' column prefetch, by default in the fused step on
-            # explicit / mixed images (eigmi.h EIG_TUNE_SELL_CPF)
-            cpf = kname == "k_lanczos_fused_b1" and mode in (0, 2)
+            # <R, mode, CPF>: the explicit slices' column prefetch is a measurement switch (eigmi.h
+            # EIG_TUNE_SELL_CPF), off in the bench
+            cpf = False
             return f"{kname}<1, {mode}, {'true' if cpf else 'false'}>"
         return f"{kname}<1, {mode}>"
     return kname

@@ -460,13 +460,14 @@ __device__ __forceinline__ void sell_cols8(const SellB1 &A, i64 s, int lane, i32
   for (int k = 0; k < 8; ++k) c[k] = k < width ? __builtin_nontemporal_load(cs + k * 64 + lane) : -1;
 }
 
-// the explicit-column slices' cross-slice column prefetch (eig_mat_tune EIG_TUNE_SELL_CPF: 0 off, 1 on,
-// 2 automatic = the fused step only.  Scrambled + RCM Poisson 256^3, same-box A/B
-// (profiles/r05v_csr.jsonl): fused step 404-406 -> 364-366 us; eig_mv 308 -> 314 us, whose one
-// 8-B gather per entry already hides the column round trip at 8 waves / SIMD)
+// the explicit-column slices' cross-slice column prefetch (eig_mat_tune EIG_TUNE_SELL_CPF: 1 on; 0 and
+// 2 (automatic) off -- a measurement switch.  Scrambled + RCM Poisson 256^3, same-box A/B
+// (profiles/r05zf_csr.jsonl): fused step 402-403 -> 436-437 us, eig_mv 308 -> 315 us: the extra
+// registers cost a wave per SIMD, and those waves hid the column round trip already)
 static bool sell_cpf(const eig_mat_s &A, bool fused)
 {
-  return A.tune_sell_cpf == 1 || (A.tune_sell_cpf == 2 && fused);
+  (void)fused;
+  return A.tune_sell_cpf == 1;
 }
 
 // One explicit slice with its first 8 column indices already in registers (cc): the value loads

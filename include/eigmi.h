@@ -236,10 +236,11 @@ enum { EIG_TUNE_MARCH_RUNS = 1, EIG_TUNE_BOX_SEGS = 2, EIG_TUNE_MARCH_PREFETCH =
  * waves just loaded), 0 = the 4 x runs of one line (default; measurement switch: the fused step at
  * 256^3 measured the same either way, 222.5 vs 222.7 us, FETCH_SIZE 2 % lower).  eig_mv bitwise
  * unchanged; the fused step's reductions sum in another order. */
-/* EIG_TUNE_SELL_CPF (explicit-column SELL slices): 1 = the next slice's column indices loaded while
- * this slice's gathers are in flight (one memory round trip per slice instead of two), in the fused
- * Lanczos step (5 waves per SIMD instead of 6) and in eig_mv; 0 = off; 2 = automatic (the library
- * default: the fused step only).  Results bitwise identical. */
+/* EIG_TUNE_SELL_CPF (explicit-column SELL slices; measurement switch): 1 = the next slice's column
+ * indices loaded while this slice's gathers are in flight (one memory round trip per slice instead
+ * of two), in the fused Lanczos step (5 waves per SIMD instead of 6) and in eig_mv; 0 / 2 = off (the
+ * default: measured slower, 437 vs 402 us for the general 256^3 fused step).  Results bitwise
+ * identical. */
 /* EIG_TUNE_BOX_MAP (measurement; k_box_mv32): 1 = XCD-contiguous tile map (the workgroups resident on
  * one XCD hold whole rows of adjacent tiles), 0 = dispatch order.  Results bitwise identical. */
 /* EIG_TUNE_BOX_COLS (box-image kernels, EIG_OP_SPMM32 / EIG_OP_CHEB32 on matrices without a row-class
