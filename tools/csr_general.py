@@ -58,6 +58,7 @@ def main():
         print(json.dumps(dict(base, op="eig_mv" + (" +col-prefetch" if cpf else ""), kernel=M.kernel("spmv"),
                               us=round(ms * 1e3, 2), csr_bytes=b, GBs=round(b / ms / 1e6, 1),
                               frac=round(b / ms / 1e6 / PEAK, 4))), flush=True)
+    ref_ab = None
     for fused, cpf in ((True, 0), (True, 1), (True, 0), (True, 1), (False, 0)):
         M.tune(sell_cpf=cpf)  # EIG_TUNE_SELL_CPF: explicit slices' cross-slice column prefetch (fused step)
         ws = eigmi.LanczosWorkspace(M, args.steps + 4, seed=123, fused=fused)
@@ -66,7 +67,13 @@ def main():
         k_us = t.spmv_ms / max(1, t.spmv_launches) * 1e3
         kb = eigmi.bytes_lanczos_fused(n, nnz) if fused else eigmi.bytes_lanczos_k1(n, nnz)
         step_us = t.total_ms / args.steps * 1e3
+        # results first, timing second: a fused variant must reproduce the plain fused kernel bitwise
+        ab = ws.tridiag()
+        if fused and ref_ab is None:
+            ref_ab = ab
+        same = bool(np.array_equal(ab[0], ref_ab[0]) and np.array_equal(ab[1], ref_ab[1])) if fused else None
         print(json.dumps(dict(base, op="lanczos " + ("fused" if fused else "classic") + (" +col-prefetch" if cpf else ""),
+                              alpha_beta_bitwise_vs_plain=same,
                               kernel=M.kernel("fused" if fused else "k1"), kernel_us=round(k_us, 2), csr_bytes=kb,
                               GBs=round(kb / k_us / 1e3, 1), frac=round(kb / k_us / 1e3 / PEAK, 4),
                               step_us=round(step_us, 2), steps_per_s=round(1e6 / step_us, 1))), flush=True)
