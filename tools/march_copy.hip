@@ -6,6 +6,7 @@
 //
 // One JSON line per (pattern, plane runs): GB/s = 2 * n * 16 B / kernel time.
 // `march_copy N values`: the value march's streams instead (k_vmarch; GB/s over 64 B per row).
+// `march_copy N kuhn`: the P1 Kuhn march's streams (k_kmarch; GB/s over 96 B per row).
 //   linear     grid-stride 16-B copy (the reference rate)
 //   march      a wave owns a 64-row column of a plane run: load the +D pair, carry it, store the
 //              centre (the march's stream structure, one load in flight per wave)
@@ -161,6 +162,55 @@ __global__ __launch_bounds__(kThreads, 8) void k_vmarch(int n, int D, int nx, in
   }
 }
 
+// The P1 Kuhn march's streams (round 5, march variants 16 / 20): per row the (t, u) pair read once
+// (+D carried) and written once, plus the Kuhn pack's FOUR 16-B value pairs ((0, +1), (+nx, +nx+1),
+// (+D, +D+1), (+D+nx, +D+nx+1)) read once -- 80 B read + 16 B written per row, the Kuhn fused
+// step's algorithmic bytes.  LIN: grid-stride order; G: plus the y +- 1 line gathers of plane z + 1.
+template <bool LIN, bool G>
+__global__ __launch_bounds__(kThreads, 8) void k_kmarch(int n, int D, int nx, int ncol, int nseg, int nplanes,
+                                                        const dpair *__restrict__ P, const dpair *__restrict__ V,
+                                                        dpair *__restrict__ Q)
+{
+  if (LIN)
+  {
+    const int stride = gridDim.x * kThreads;
+    for (int i = blockIdx.x * kThreads + threadIdx.x; i < n; i += stride)
+    {
+      const dpair p = __builtin_nontemporal_load(P + i), a = __builtin_nontemporal_load(V + i),
+                  b = __builtin_nontemporal_load(V + n + i), c = __builtin_nontemporal_load(V + 2 * (size_t)n + i),
+                  d = __builtin_nontemporal_load(V + 3 * (size_t)n + i);
+      __builtin_nontemporal_store(dpair{p.x + a.x * b.y + c.x * d.y, p.y + a.y * b.x + c.y * d.x}, Q + i);
+    }
+    return;
+  }
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int item = swz() * kW + wave;
+  if (item >= ncol * nseg) return;
+  const int col = item % ncol, seg = item / ncol;
+  const int z0 = seg * nplanes / nseg, z1 = (seg + 1) * nplanes / nseg;
+  const int last = n - 1;
+  auto cl = [&](int g) { return g < 0 ? 0 : (g > last ? last : g); };
+  int w = col * 64 + lane + z0 * D;
+  dpair cur = P[cl(w)];
+  for (int z = z0; z < z1; ++z, w += D)
+  {
+    const dpair pd = P[cl(w + D)];
+    const dpair a = V[w], b = V[n + w], c = __builtin_nontemporal_load(V + 2 * (size_t)n + w),
+                d = V[3 * (size_t)n + w];
+    dpair o = cur;
+    if (G)
+    {
+      const dpair u = P[cl(w + D - nx)], v = P[cl(w + D + nx)];
+      o.x += u.x * b.y + v.x;
+      o.y += u.y + v.y * d.y;
+    }
+    o.x += pd.x * a.x * 1e-300 + c.x * d.x;
+    o.y += a.y * b.x + c.y;
+    __builtin_nontemporal_store(o, Q + w);
+    cur = pd;
+  }
+}
+
 // two columns per wave: c and c + ncol / 2 (ncol even)
 __global__ __launch_bounds__(kThreads, 8) void k_march2(int n, int D, int ncol, int nseg, int nplanes,
                                                         const dpair *__restrict__ P, dpair *__restrict__ Q)
@@ -228,6 +278,33 @@ int main(int argc, char **argv)
     std::fflush(stdout);
   };
   const char *only = argc > 2 ? argv[2] : "";
+  if (std::string(only) == "kuhn")
+  {
+    // the Kuhn march's streams: 80 B read + 16 B written per row (GB/s over those 96 B)
+    dpair *V;
+    CK(hipMalloc(&V, (size_t)4 * n * sizeof(dpair)));
+    CK(hipMemset(V, 0, (size_t)4 * n * sizeof(dpair)));
+    auto src = [&] { return rep & 1 ? Q : P; };
+    auto dst = [&] { return rep & 1 ? P : Q; };
+    auto outk = [&](const char *pat, int nseg, double us) {
+      std::printf("{\"pattern\": \"%s\", \"N\": %d, \"runs\": %d, \"us\": %.2f, \"GBs\": %.1f}\n", pat, N, nseg,
+                  us, 6.0 * n * sizeof(dpair) / us * 1e-3);
+      std::fflush(stdout);
+    };
+    for (int g : {2048, 4096, 8192})
+      outk("kuhn_linear_pp", g, time([&] { k_kmarch<true, false><<<g, kThreads>>>(n, D, nx, ncol, 1, N, src(), V, dst()); }));
+    for (int nseg : {4, 6, 8, 12})
+    {
+      const int items = ncol * nseg, G = (items + kW - 1) / kW;
+      outk("kuhn_march_pp", nseg, time([&] { k_kmarch<false, false><<<G, kThreads>>>(n, D, nx, ncol, nseg, N, src(), V, dst()); }));
+      outk("kuhn_march_g_pp", nseg, time([&] { k_kmarch<false, true><<<G, kThreads>>>(n, D, nx, ncol, nseg, N, src(), V, dst()); }));
+    }
+    CK(hipGetLastError());
+    CK(hipFree(V));
+    CK(hipFree(P));
+    CK(hipFree(Q));
+    return 0;
+  }
   if (std::string(only) == "values")
   {
     // the value march's streams: 48 B read + 16 B written per row (GB/s over those 64 B)
