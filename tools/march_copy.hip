@@ -7,6 +7,7 @@
 // One JSON line per (pattern, plane runs): GB/s = 2 * n * 16 B / kernel time.
 // `march_copy N values`: the value march's streams instead (k_vmarch; GB/s over 64 B per row).
 // `march_copy N kuhn`: the P1 Kuhn march's streams (k_kmarch; GB/s over 96 B per row).
+// `march_copy N box`: the C5 Chebyshev step's streams as a plain copy (k_boxcopy; 1152 B per row).
 //   linear     grid-stride 16-B copy (the reference rate)
 //   march      a wave owns a 64-row column of a plane run: load the +D pair, carry it, store the
 //              centre (the march's stream structure, one load in flight per wave)
@@ -211,6 +212,29 @@ __global__ __launch_bounds__(kThreads, 8) void k_kmarch(int n, int D, int nx, in
   }
 }
 
+// The C5 Chebyshev step's streams (k_box_mv32_cheb, 32 columns, P1 Kuhn box image): per row X,
+// x_{k-1} and B read (3 x 256 B), the 15 box-image values + D^-1 read (128 B), the result written
+// (256 B) -- 1152 B per row, no halo, no matrix arithmetic: a plain grid-stride stream of the
+// kernel's own bytes (16 lanes per row, one 16-B piece of each 256-B row per lane).
+__global__ __launch_bounds__(kThreads) void k_boxcopy(int nrows, const dpair *__restrict__ X, const dpair *__restrict__ Xo,
+                                                      const dpair *__restrict__ B, const double *__restrict__ V,
+                                                      dpair *__restrict__ Y)
+{
+  const long total = (long)nrows * 16;
+  const long stride = (long)gridDim.x * kThreads;
+  for (long t = (long)blockIdx.x * kThreads + threadIdx.x; t < total; t += stride)
+  {
+    const long r = t >> 4;
+    const int q = (int)(t & 15);
+    const dpair x = __builtin_nontemporal_load(X + t), xo = __builtin_nontemporal_load(Xo + t),
+                b = __builtin_nontemporal_load(B + t);
+    (void)r;
+    (void)q;
+    const double v = __builtin_nontemporal_load(V + t);  // the row's 15 values + D^-1, read coalesced
+    __builtin_nontemporal_store(dpair{x.x + v * (b.x - xo.x), x.y + v * (b.y - xo.y)}, Y + t);
+  }
+}
+
 // two columns per wave: c and c + ncol / 2 (ncol even)
 __global__ __launch_bounds__(kThreads, 8) void k_march2(int n, int D, int ncol, int nseg, int nplanes,
                                                         const dpair *__restrict__ P, dpair *__restrict__ Q)
@@ -278,6 +302,31 @@ int main(int argc, char **argv)
     std::fflush(stdout);
   };
   const char *only = argc > 2 ? argv[2] : "";
+  if (std::string(only) == "box")
+  {
+    // the C5 Chebyshev step's 1152 B per row (GB/s over those bytes)
+    dpair *X, *Xo, *B, *Y;
+    double *V;
+    const size_t nb = (size_t)n * 16 * sizeof(dpair);
+    CK(hipMalloc(&X, nb));
+    CK(hipMalloc(&Xo, nb));
+    CK(hipMalloc(&B, nb));
+    CK(hipMalloc(&Y, nb));
+    CK(hipMalloc(&V, (size_t)16 * n * sizeof(double)));
+    CK(hipMemset(X, 0, nb));
+    CK(hipMemset(Xo, 0, nb));
+    CK(hipMemset(B, 0, nb));
+    CK(hipMemset(V, 0, (size_t)16 * n * sizeof(double)));
+    for (int g : {2048, 4096, 8192})
+    {
+      const double us = time([&] { k_boxcopy<<<g, kThreads>>>(n, rep & 1 ? Y : X, Xo, B, V, rep & 1 ? X : Y); });
+      std::printf("{\"pattern\": \"box_cheb_linear_pp\", \"N\": %d, \"grid\": %d, \"us\": %.2f, \"GBs\": %.1f}\n", N, g,
+                  us, 1152.0 * n / us * 1e-3);
+      std::fflush(stdout);
+    }
+    CK(hipGetLastError());
+    return 0;
+  }
   if (std::string(only) == "kuhn")
   {
     // the Kuhn march's streams: 80 B read + 16 B written per row (GB/s over those 96 B)
