@@ -235,6 +235,142 @@ __global__ __launch_bounds__(kThreads) void k_boxcopy(int nrows, const dpair *__
   }
 }
 
+// Ablation of the value march toward the fused step (round 5): k_vmarch<false, true> (the streams +
+// the +-nx gathers) plus, by flag, EDGE = lane 0 / lane 63 load the pair past their end of the
+// 64-row line (exec-masked), ARITH = the fused step's per-row arithmetic (u = t - c u for the 7
+// operands, the 7 products in order, the t / u epilogue), RED = its three running sums reduced per
+// wave and added once per wave; built for W waves per SIMD.
+template <bool EDGE, bool ARITH, bool RED, int W, bool MIR = false, int POL = 0, bool TAIL = false>
+__global__ __launch_bounds__(kThreads, W) void k_vabl(int n, int D, int nx, int ncol, int nseg, int nplanes,
+                                                      const dpair *__restrict__ P, const dpair *__restrict__ V,
+                                                      dpair *__restrict__ Q, double *__restrict__ sums, double c)
+{
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int item = swz() * kW + wave;
+  if (item >= ncol * nseg) return;  // (the grid covers the items exactly: no workgroup leaves early)
+  const int col = item % ncol, seg = item / ncol;
+  const int z0 = seg * nplanes / nseg, z1 = (seg + 1) * nplanes / nseg;
+  const int lastrow = n - 1;
+  auto cl = [&](int g) { return g < 0 ? 0 : (g > lastrow ? lastrow : g); };
+  int w = col * 64 + lane + z0 * D;
+  dpair cur = P[cl(w)];
+  dpair prev = P[cl(w - D)];
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+  for (int z = z0; z < z1; ++z, w += D)
+  {
+    const dpair pd = P[cl(w + D)];
+    // POL 1: the (+1, +nx) stream with the default cache policy (its lines stay in L2 for the
+    // -nx mirror gather of line y + 1); 2: also no lane-0 -1 value load (DPP only)
+    const dpair a = __builtin_nontemporal_load(V + w), b = POL ? V[n + w] : __builtin_nontemporal_load(V + n + w);
+    const dpair u = P[cl(w - nx)], v = P[cl(w + nx)];
+    dpair e = dpair{0.0, 0.0};
+    if (EDGE && (lane == 0 || lane == 63)) e = P[cl(lane == 0 ? w - 1 : w + 1)];
+    // MIR: the mirrored lower values -- -nx from the (+1, +nx) pair of row w - nx (an L2 gather),
+    // -1 by lane shift of the +1 value with lane 0's own (w - 1) load
+    double mnx = 0.0, m1e = 0.0;
+    if (MIR)
+    {
+      mnx = V[n + cl(w - nx)].y;
+      if (POL < 2 && lane == 0) m1e = V[n + cl(w - 1)].x;
+    }
+    dpair o;
+    if (ARITH)
+    {
+      auto uk = [&](dpair p) { return p.x - c * p.y; };
+      const double vc = uk(cur);
+      const double vl = __shfl_up(vc, 1, 64), vr = __shfl_down(vc, 1, 64);
+      double acc = 0.0;
+      const double am1 = MIR ? (lane == 0 ? m1e : __shfl_up(b.x, 1, 64)) : b.x;
+      acc += b.y * uk(prev);
+      acc += (MIR ? mnx : a.y) * uk(u);
+      acc += am1 * (lane == 0 ? uk(e) : vl);
+      acc += a.x * vc;
+      acc += b.x * (lane == 63 ? uk(e) : vr);
+      acc += b.y * uk(v);
+      acc += a.x * uk(pd);
+      const double t = (acc - 0.5 * vc) * 0.25 - 0.125 * cur.y;
+      o = dpair{t, vc};
+      if (RED)
+      {
+        s0 += t * vc;
+        s1 += t * t;
+        s2 += vc * vc;
+      }
+    }
+    else
+    {
+      o = cur;
+      o.x += u.x * b.y + v.x + e.x;
+      o.y += u.y + v.y * b.y + e.y;
+      o.x += pd.x * a.x * 1e-300;
+      o.y += a.y * b.x;
+    }
+    __builtin_nontemporal_store(o, Q + w);
+    prev = cur;
+    cur = pd;
+  }
+  if (RED)
+  {
+    for (int off = 32; off > 0; off >>= 1)
+    {
+      s0 += __shfl_down(s0, off, 64);
+      s1 += __shfl_down(s1, off, 64);
+      s2 += __shfl_down(s2, off, 64);
+    }
+    if (!TAIL && lane == 0)  // one slot per wave (no contention; the fused step's partials + ticket tail aside)
+    {
+      sums[3 * item] = s0;
+      sums[3 * item + 1] = s1;
+      sums[3 * item + 2] = s2;
+    }
+    if (TAIL)
+    {
+      // the fused step's tail: workgroup sums -> partials, a ticket, the last workgroup sums them
+      __shared__ double ws[kW][3];
+      __shared__ int last;
+      if (lane == 0)
+      {
+        ws[wave][0] = s0;
+        ws[wave][1] = s1;
+        ws[wave][2] = s2;
+      }
+      __syncthreads();
+      double *part = sums + 64;
+      unsigned *ticket = reinterpret_cast<unsigned *>(sums);
+      if (threadIdx.x < 3)
+      {
+        double t = 0.0;
+        for (int q = 0; q < kW; ++q) t += ws[q][threadIdx.x];
+        __hip_atomic_store(reinterpret_cast<unsigned long long *>(part + 3 * blockIdx.x + threadIdx.x),
+                           (unsigned long long)__double_as_longlong(t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0)
+        last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+      __syncthreads();
+      if (last)
+      {
+        double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+        for (unsigned b = threadIdx.x; b < gridDim.x; b += kThreads)
+        {
+          a0 += __longlong_as_double((long long)__hip_atomic_load(reinterpret_cast<unsigned long long *>(part + 3 * b), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+          a1 += __longlong_as_double((long long)__hip_atomic_load(reinterpret_cast<unsigned long long *>(part + 3 * b + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+          a2 += __longlong_as_double((long long)__hip_atomic_load(reinterpret_cast<unsigned long long *>(part + 3 * b + 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        }
+        for (int off = 32; off > 0; off >>= 1)
+        {
+          a0 += __shfl_down(a0, off, 64);
+          a1 += __shfl_down(a1, off, 64);
+          a2 += __shfl_down(a2, off, 64);
+        }
+        if (lane == 0) atomicAdd(sums + 8, a0 + a1 + a2);
+        if (threadIdx.x == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+}
+
 // two columns per wave: c and c + ncol / 2 (ncol even)
 __global__ __launch_bounds__(kThreads, 8) void k_march2(int n, int D, int ncol, int nseg, int nplanes,
                                                         const dpair *__restrict__ P, dpair *__restrict__ Q)
@@ -374,6 +510,30 @@ int main(int argc, char **argv)
       const int items = ncol * nseg, G = (items + kW - 1) / kW;
       outv("values_march_pp", nseg, time([&] { k_vmarch<false, false><<<G, kThreads>>>(n, D, nx, ncol, nseg, N, src(), V, dst()); }));
       outv("values_march_g_pp", nseg, time([&] { k_vmarch<false, true><<<G, kThreads>>>(n, D, nx, ncol, nseg, N, src(), V, dst()); }));
+    }
+    if (argc > 3 && std::string(argv[3]) == "ablation")
+    {
+      double *sums;
+      const int nseg = 8, items = ncol * nseg, G = (items + kW - 1) / kW;
+      CK(hipMalloc(&sums, (size_t)(3 * items + 64) * sizeof(double)));
+      CK(hipMemset(sums, 0, (size_t)(3 * items + 64) * sizeof(double)));
+#define ABL(NAME, E, A, R, W_, ...)                                                                              \
+  outv(NAME, nseg, time([&] { k_vabl<E, A, R, W_, ##__VA_ARGS__><<<G, kThreads>>>(n, D, nx, ncol, nseg, N, src(), V, dst(), sums, 0.5); }))
+      ABL("abl_g_w8", false, false, false, 8);
+      ABL("abl_g_edge_w8", true, false, false, 8);
+      ABL("abl_g_edge_arith_w8", true, true, false, 8);
+      ABL("abl_g_edge_arith_red_w8", true, true, true, 8);
+      ABL("abl_g_edge_arith_red_w6", true, true, true, 6);
+      ABL("abl_g_w6", false, false, false, 6);
+      ABL("abl_g_edge_arith_red_mir_w8", true, true, true, 8, true);
+      ABL("abl_g_edge_arith_red_mir_w6", true, true, true, 6, true);
+      ABL("abl_g_edge_arith_red_mir_pol1_w8", true, true, true, 8, true, 1);
+      ABL("abl_g_edge_arith_red_mir_pol2_w8", true, true, true, 8, true, 2);
+      ABL("abl_g_edge_arith_red_pol1_w8", true, true, true, 8, false, 1);
+      ABL("abl_full_tail_w6", true, true, true, 6, true, 1, true);
+      ABL("abl_full_notail_w6", true, true, true, 6, true, 1, false);
+#undef ABL
+      CK(hipFree(sums));
     }
     CK(hipGetLastError());
     CK(hipFree(V));
