@@ -402,7 +402,9 @@ __global__ __launch_bounds__(kThreads, 8) void k_march2(int n, int D, int ncol, 
 int main(int argc, char **argv)
 {
   const int N = argc > 1 ? std::atoi(argv[1]) : 256;
-  const int n = N * N * N, D = N * N, nx = N, ncol = D / 64;
+  // MC_NZ: planes of the grid (default N; 32 = one rank's slab of the 8-GPU split of 256^3)
+  const int NZ = std::getenv("MC_NZ") ? std::atoi(std::getenv("MC_NZ")) : N;
+  const int n = N * N * NZ, D = N * N, nx = N, ncol = D / 64;
   if (D % 64 != 0 || (ncol & 1)) return 2;
   dpair *P, *Q;
   CK(hipMalloc(&P, (size_t)n * sizeof(dpair)));
@@ -505,20 +507,21 @@ int main(int argc, char **argv)
     };
     for (int g : {2048, 4096, 8192})
       outv("values_linear_pp", g, time([&] { k_vmarch<true, false><<<g, kThreads>>>(n, D, nx, ncol, 1, N, src(), V, dst()); }));
-    for (int nseg : {4, 6, 8, 12})
+    for (int nseg : {1, 2, 4, 6, 8, 12, 16})
     {
+      if (nseg > NZ) continue;
       const int items = ncol * nseg, G = (items + kW - 1) / kW;
-      outv("values_march_pp", nseg, time([&] { k_vmarch<false, false><<<G, kThreads>>>(n, D, nx, ncol, nseg, N, src(), V, dst()); }));
-      outv("values_march_g_pp", nseg, time([&] { k_vmarch<false, true><<<G, kThreads>>>(n, D, nx, ncol, nseg, N, src(), V, dst()); }));
+      outv("values_march_pp", nseg, time([&] { k_vmarch<false, false><<<G, kThreads>>>(n, D, nx, ncol, nseg, NZ, src(), V, dst()); }));
+      outv("values_march_g_pp", nseg, time([&] { k_vmarch<false, true><<<G, kThreads>>>(n, D, nx, ncol, nseg, NZ, src(), V, dst()); }));
     }
     if (argc > 3 && std::string(argv[3]) == "ablation")
     {
       double *sums;
-      const int nseg = 8, items = ncol * nseg, G = (items + kW - 1) / kW;
+      const int nseg = argc > 4 ? std::atoi(argv[4]) : 8, items = ncol * nseg, G = (items + kW - 1) / kW;
       CK(hipMalloc(&sums, (size_t)(3 * items + 64) * sizeof(double)));
       CK(hipMemset(sums, 0, (size_t)(3 * items + 64) * sizeof(double)));
 #define ABL(NAME, E, A, R, W_, ...)                                                                              \
-  outv(NAME, nseg, time([&] { k_vabl<E, A, R, W_, ##__VA_ARGS__><<<G, kThreads>>>(n, D, nx, ncol, nseg, N, src(), V, dst(), sums, 0.5); }))
+  outv(NAME, nseg, time([&] { k_vabl<E, A, R, W_, ##__VA_ARGS__><<<G, kThreads>>>(n, D, nx, ncol, nseg, NZ, src(), V, dst(), sums, 0.5); }))
       ABL("abl_g_w8", false, false, false, 8);
       ABL("abl_g_edge_w8", true, false, false, 8);
       ABL("abl_g_edge_arith_w8", true, true, false, 8);
