@@ -1775,7 +1775,7 @@ void gram_device(eig_ctx_t ctx, i64 n, i64 m1, i64 m2, const double *Q1, const d
 
 void orthonormalize_device(eig_ctx_t ctx, i64 n, i64 m, double *Q, int variant)
 {
-  const int flags = variant & (EIG_ORTHO_GRID | EIG_ORTHO_NO_COOP);
+  const int flags = variant & (EIG_ORTHO_GRID | EIG_ORTHO_NO_COOP | EIG_ORTHO_ONE_WG);
   const int la = (variant >> EIG_ORTHO_LOOKAHEAD_SHIFT) & 15;  // EIG_ORTHO_LOOKAHEAD(L); 0: the default
   const int L = la ? std::min(la, 8) : mgs_lookahead_default();
   variant &= 0xff;
@@ -1788,7 +1788,8 @@ void orthonormalize_device(eig_ctx_t ctx, i64 n, i64 m, double *Q, int variant)
   for (i64 bk = 0; bk < m; bk += 8)
   {
     double *Qb = Q + bk * n;
-    if (variant == EIG_ORTHO_MGS && !ctx->distributed() && !(flags & EIG_ORTHO_GRID) && launch_mgs_small(n, Qb, s))
+    if (variant == EIG_ORTHO_MGS && !ctx->distributed() && (flags & EIG_ORTHO_ONE_WG) && !(flags & EIG_ORTHO_GRID) &&
+        launch_mgs_small(n, Qb, s))
     {
     }
     else if (variant == EIG_ORTHO_MGS && !ctx->distributed() && !(flags & EIG_ORTHO_GRID) &&
@@ -1853,7 +1854,7 @@ extern "C" int eig_orthonormalize_mv8(eig_ctx_t ctx, int64_t n, int64_t m, doubl
     const int v = variant & 0xff;
     EIG_CHECK(v == EIG_ORTHO_MGS || v == EIG_ORTHO_CHOLQR || v == EIG_ORTHO_CHOLQR_SPLIT, EIG_ERR_ARG,
               "unknown variant");
-    EIG_CHECK((variant & ~(0xff | EIG_ORTHO_GRID | EIG_ORTHO_NO_COOP | (15 << EIG_ORTHO_LOOKAHEAD_SHIFT))) == 0 &&
+    EIG_CHECK((variant & ~(0xff | EIG_ORTHO_GRID | EIG_ORTHO_NO_COOP | EIG_ORTHO_ONE_WG | (15 << EIG_ORTHO_LOOKAHEAD_SHIFT))) == 0 &&
                   ((variant >> EIG_ORTHO_LOOKAHEAD_SHIFT) & 15) <= 8,
               EIG_ERR_ARG, "unknown variant flags");
     EIG_MV8_CHECK(m);

@@ -20,6 +20,29 @@ namespace {
 
 bool distributed(const eig_mat_s &A) { return A.ctx->distributed(); }
 
+// Page-locked host doubles (a hipMemcpyAsync into pageable memory would block the host until the
+// copy is done) and a timing-free event: the drivers' per-iteration stopping data.
+struct PinnedDoubles {
+  double *p = nullptr;
+  explicit PinnedDoubles(size_t n) { EIG_HIP(hipHostMalloc(reinterpret_cast<void **>(&p), (n ? n : 1) * sizeof(double))); }
+  ~PinnedDoubles()
+  {
+    if (p) (void)hipHostFree(p);
+  }
+  PinnedDoubles(const PinnedDoubles &) = delete;
+  PinnedDoubles &operator=(const PinnedDoubles &) = delete;
+};
+struct SyncEvent {
+  hipEvent_t e = nullptr;
+  SyncEvent() { EIG_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming)); }
+  ~SyncEvent()
+  {
+    if (e) (void)hipEventDestroy(e);
+  }
+  SyncEvent(const SyncEvent &) = delete;
+  SyncEvent &operator=(const SyncEvent &) = delete;
+};
+
 }  // namespace
 
 // ============================================================================================
@@ -39,45 +62,67 @@ extern "C" int eig_standard_largest(eig_mat_t A, double shift, double tol, int m
     hipStream_t s = ctx->stream;
     const i64 n = A->nb_rows;
     const i64 m = (nev / 8 + std::min(nev % 8, 1)) * 8;  // eigensolver.hh:43
-    DevBuf Q1b(n * m * 8), Q2b(n * m * 8), dpb(m * 8);
-    double *Q1 = Q1b.d(), *Q2 = Q2b.d();
+    // Three rotating n x m blocks: iteration k orthonormalises B[k % 3] in place (it holds A Q1 of
+    // the previous basis, eigensolver.hh:78-81), multiplies it into B[(k + 1) % 3] (:84) and takes the
+    // diagonal dots (:85).  So iteration k + 1 writes only B[(k + 1) % 3] and B[(k + 2) % 3], never
+    // iteration k's basis, and is queued BEFORE the host reads iteration k's dots for the stopping
+    // test (:87-102): the device never idles on the host's round trip.  If iteration k stops the loop,
+    // the extra iteration's results are ignored.  The same kernels on the same inputs as the
+    // reference's order (one SpMM per iteration from k = 2 on, see :78 below), so the iterates, the Ritz
+    // values and the iteration count are bitwise those of the plain loop
+    // (tests/test_gpu_drivers.py::test_standard_largest_reuses_product_bitwise).
+    DevBuf B0(n * m * 8), B1(n * m * 8), B2(n * m * 8), dpb(2 * m * 8);
+    double *B[3] = {B0.d(), B1.d(), B2.d()};
+    PinnedDoubles hd(2 * (size_t)m);
+    SyncEvent ev[2];
     {
       std::vector<double> h((size_t)(n * m));
       host_random_normal(n * m, seed, h.data());  // eigensolver.hh:50-55
-      EIG_HIP(hipMemcpyAsync(Q1, h.data(), h.size() * 8, hipMemcpyHostToDevice, s));
+      EIG_HIP(hipMemcpyAsync(B[0], h.data(), h.size() * 8, hipMemcpyHostToDevice, s));
       EIG_HIP(hipStreamSynchronize(s));
     }
     if (shift != 0.0) launch_shift_diag(*A, shift, s);  // eigensolver.hh:59-66
-    orthonormalize_device(ctx, n, m, Q1, EIG_ORTHO_MGS); // eigensolver.hh:69
+    orthonormalize_device(ctx, n, m, B[0], EIG_ORTHO_MGS); // eigensolver.hh:69
+    // :78 of iteration k recomputes A Q1, which iteration k - 1's :84 product already holds (same
+    // matrix, same input, deterministic kernel: bitwise the same block), so
+    // only iteration 1 runs it
+    if (maxiter > 1) launch_spmm_mv8(*A, m, B[0], B[1], s);  // :78 (k = 1)
+    auto enqueue = [&](int k) {
+      double *Q = B[k % 3], *P = B[(k + 1) % 3], *dp = dpb.d() + (k & 1) * m;
+      orthonormalize_device(ctx, n, m, Q, EIG_ORTHO_MGS);  // :81
+      launch_spmm_mv8(*A, m, Q, P, s);                     // :84
+      launch_dot_diag_mv8(n, m, Q, P, dp, 0, s, ctx->red); // :85
+      EIG_HIP(hipMemcpyAsync(hd.p + (k & 1) * m, dp, m * 8, hipMemcpyDeviceToHost, s));
+      EIG_HIP(hipEventRecord(ev[k & 1].e, s));
+    };
     std::vector<double> s1(m, 0.0), s2(m, 0.0);
-    int kk = 1;
+    int kk = 1, basis = 0;
+    if (maxiter > 1) enqueue(1);
     for (int k = 1; k < maxiter; ++k)
     {
       kk = k;
-      launch_spmm_mv8(*A, m, Q1, Q2, s);                 // :78
-      orthonormalize_device(ctx, n, m, Q2, EIG_ORTHO_MGS); // :81
-      launch_spmm_mv8(*A, m, Q2, Q1, s);                 // :84
-      launch_dot_diag_mv8(n, m, Q2, Q1, dpb.d(), 0, s, ctx->red);  // :85
-      EIG_HIP(hipMemcpyAsync(s1.data(), dpb.d(), m * 8, hipMemcpyDeviceToHost, s));
-      EIG_HIP(hipStreamSynchronize(s));
-      for (auto &x : s1) x -= shift;
+      if (k + 1 < maxiter) enqueue(k + 1);  // look-ahead: queued before iteration k's stopping test
+      EIG_HIP(hipEventSynchronize(ev[k & 1].e));
+      for (i64 i = 0; i < m; ++i) s1[i] = hd.p[(k & 1) * m + i] - shift;
       double dist = 0.0;
       for (i64 i = 0; i < m; ++i) dist = std::max(dist, std::fabs(s1[i] - s2[i]));
       if (verbose > 0 && k > 1) fprintf(stdout, "Iter=%d %.17g\n", k, dist);
       std::swap(s1, s2);
-      std::swap(Q1, Q2);
+      basis = k % 3;  // Q1 after the swap (:96)
       if (k > 1 && dist < tol) break;
     }
     for (int j = 0; j < nev; ++j) eval_host[j] = s2[j];
     if (evec_host)
     {
-      // evec[j][i] = Q1(i, j): column j sits at Q1 + (j/8)*8n + i*8 + j%8
+      // evec[j][i] = Q1(i, j): column j sits at Q1 + (j/8)*8n + i*8 + j%8 (after any look-ahead
+      // iteration on the stream, which leaves this block alone)
       std::vector<double> h((size_t)(n * m));
-      EIG_HIP(hipMemcpyAsync(h.data(), Q1, h.size() * 8, hipMemcpyDeviceToHost, s));
+      EIG_HIP(hipMemcpyAsync(h.data(), B[basis], h.size() * 8, hipMemcpyDeviceToHost, s));
       EIG_HIP(hipStreamSynchronize(s));
       for (int j = 0; j < nev; ++j)
         for (i64 i = 0; i < n; ++i) evec_host[(i64)j * n + i] = h[((j / 8) * n + i) * 8 + j % 8];
     }
+    EIG_HIP(hipStreamSynchronize(s));  // the look-ahead iteration uses this call's buffers
     if (iters) *iters = kk;
   });
 }

@@ -18,6 +18,7 @@ EIG_OK, EIG_ERR_SHAPE, EIG_ERR_BLOCKSIZE, EIG_ERR_HIP, EIG_ERR_RCCL, EIG_ERR_BRE
 ORTHO_MGS, ORTHO_CHOLQR, ORTHO_CHOLQR_SPLIT = 0, 1, 2
 ORTHO_GRID = 0x100  # or-ed into the variant: grid-wide MGS passes even for blocks one workgroup holds
 ORTHO_NO_COOP = 0x200  # or-ed into the variant: look-ahead MGS as 9 launches (no in-kernel fallback passes)
+ORTHO_ONE_WG = 0x400  # or-ed into ORTHO_MGS: the one-workgroup MGS for n <= 4096 (slower than the default; A/B)
 
 
 def ORTHO_LOOKAHEAD(L):

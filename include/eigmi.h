@@ -308,9 +308,14 @@ int eig_gram_mv8(eig_ctx_t ctx, int64_t n, int64_t m1, int64_t m2, const double 
  *                    diagonal block, later blocks projected in two halves (columns 0-3, then 4-7
  *                    against the updated block). */
 enum eig_ortho_variant { EIG_ORTHO_MGS = 0, EIG_ORTHO_CHOLQR = 1, EIG_ORTHO_CHOLQR_SPLIT = 2 };
-/* or-ed into `variant`: keep the grid-wide MGS passes even where one workgroup holds the block
- * (n <= 4096 on one rank; the two do the same per-row operations -- A/B and tests) */
+/* or-ed into `variant`: the grid-wide MGS passes (the default for every n since round 5; kept as a
+ * flag for A/B and tests) */
 enum { EIG_ORTHO_GRID = 0x100 };
+/* or-ed into `variant` for EIG_ORTHO_MGS on one rank: the diagonal block's 8 MGS steps in ONE
+ * workgroup that keeps the block in registers (n <= 4096).  Measured slower than the default
+ * look-ahead at every such n (17.8-28.9 us against 16.0-17.5 us per 8-column block, n = 512-4096,
+ * profiles/r05zs_small_ortho_kernel_stats.csv): an alternative for A/B and tests. */
+enum { EIG_ORTHO_ONE_WG = 0x400 };
 /* or-ed into `variant`: the look-ahead MGS without its barrier-capable last launch (the worst case
  * of refused look-aheads enqueued as 9 launches; A/B and tests) */
 enum { EIG_ORTHO_NO_COOP = 0x200 };

@@ -204,12 +204,12 @@ def test_cholqr_split_half_order(ctx):
 
 @pytest.mark.parametrize("n,m", [(3000, 16), (4096, 8), (513, 8)])
 def test_mgs_small_vs_grid(ctx, n, m):
-    """n <= 4096 on one rank: the diagonal block's MGS runs in one workgroup (k_mgs_small); the
-    grid-wide passes (variant | EIG_ORTHO_GRID) do the same per-row operations, so the two agree to the
-    rounding of the sums' order."""
+    """n <= 4096 on one rank: the diagonal block's MGS in one workgroup (k_mgs_small, EIG_ORTHO_ONE_WG)
+    and the grid-wide passes (the default look-ahead, and variant | EIG_ORTHO_GRID) do the same per-row
+    operations, so they agree to the rounding of the sums' order."""
     Qh = oracle.random_mv8(n, m, 5)
     Qa, Qb = ctx.array(Qh), ctx.array(Qh)
-    eigmi.orthonormalize_mv8(ctx, n, m, Qa, eigmi.ORTHO_MGS)
+    eigmi.orthonormalize_mv8(ctx, n, m, Qa, eigmi.ORTHO_MGS | eigmi.ORTHO_ONE_WG)
     eigmi.orthonormalize_mv8(ctx, n, m, Qb, eigmi.ORTHO_MGS | eigmi.ORTHO_GRID)
     a, b = Qa.get(), Qb.get()
     assert np.all(np.isfinite(a)) and np.abs(a - b).max() < 1e-13

@@ -262,3 +262,36 @@ def test_full_size_lanczos_fused_matches_oracle(ctx, p256):
     fa, fb, _ = eigmi.lanczos_run(M, 30, seed=123, fused=True)
     ca, cb, _ = eigmi.lanczos_run(M, 30, seed=123)
     assert np.allclose(fa, ca, rtol=1e-11) and np.allclose(fb, cb, rtol=1e-11)
+
+
+@pytest.mark.parametrize("make,nev,shift", [(lambda: oracle.laplace2d(48), 8, 0.0),
+                                            (lambda: oracle.poisson3d(20), 12, 0.25)])
+def test_standard_largest_reuses_product_bitwise(ctx, make, nev, shift):
+    """The driver computes ONE SpMM per iteration from k = 2 on: eigensolver.hh:78's A Q1 is the
+    previous iteration's :84 product, which the swap left in Q2.  Bar: the
+    Ritz values and vectors BITWISE those of the reference's order (two SpMMs per iteration) run
+    here from the same start block with the same primitives, for a fixed iteration count."""
+    A = make()
+    M = upload(ctx, A)
+    n, m, maxiter = M.n, (nev + 7) // 8 * 8, 12
+    ev, evec, it = eigmi.standard_largest(M, shift, 0.0, maxiter, nev, 5)
+    # the reference's loop (eigensolver.hh:69-103), primitive by primitive
+    Q1, Q2, dp = ctx.zeros(n * m), ctx.zeros(n * m), ctx.zeros(m)
+    eigmi.random_mv8(ctx, n, m, 5, Q1)
+    M = upload(ctx, A)  # a fresh copy: the driver shifted its matrix in place (eigensolver.hh:59-66)
+    if shift != 0.0:
+        M.shift_diag(shift)
+    eigmi.orthonormalize_mv8(ctx, n, m, Q1)
+    s2 = np.zeros(m)
+    for k in range(1, maxiter):
+        eigmi.spmm_mv8(M, m, Q1, Q2)
+        eigmi.orthonormalize_mv8(ctx, n, m, Q2)
+        eigmi.spmm_mv8(M, m, Q2, Q1)
+        eigmi.dot_diag_mv8(ctx, n, m, Q2, Q1, dp)
+        s2 = dp.get() - shift
+        Q1, Q2 = Q2, Q1
+    q = Q1.get().reshape(m // 8, n, 8)
+    ref_evec = np.stack([q[j // 8, :, j % 8] for j in range(nev)])
+    assert it == maxiter - 1
+    assert np.array_equal(ev, s2[:nev])
+    assert np.array_equal(evec, ref_evec)
