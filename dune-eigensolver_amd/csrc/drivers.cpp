@@ -90,8 +90,7 @@ extern "C" int eig_standard_largest(eig_mat_t A, double shift, double tol, int m
     auto enqueue = [&](int k) {
       double *Q = B[k % 3], *P = B[(k + 1) % 3], *dp = dpb.d() + (k & 1) * m;
       orthonormalize_device(ctx, n, m, Q, EIG_ORTHO_MGS);  // :81
-      launch_spmm_mv8(*A, m, Q, P, s);                     // :84
-      launch_dot_diag_mv8(n, m, Q, P, dp, 0, s, ctx->red); // :85
+      launch_spmm_dot_mv8(*A, m, Q, P, dp, s, ctx->red);   // :84-85 (one launch on the row-class image)
       EIG_HIP(hipMemcpyAsync(hd.p + (k & 1) * m, dp, m * 8, hipMemcpyDeviceToHost, s));
       EIG_HIP(hipEventRecord(ev[k & 1].e, s));
     };

@@ -343,6 +343,8 @@ extern const i32 kMarchInteriorTag;
 bool box_prepare(const eig_mat_s &A);
 int box_cols(const eig_mat_s &A);  // columns per box-image workgroup (k_box_mv32: 32, k_box_mv16p: 16)
 bool launch_box_spmm(const eig_mat_s &A, i64 m, const double *X, double *Y, hipStream_t s);
+bool launch_box_spmm_dot(const eig_mat_s &A, i64 m, const double *X, double *Y, double *dp, ReduceWS red,
+                         hipStream_t s);
 // Xnew: x_{k+1} into a third buffer (nullptr: in place over Xold); Xold nullptr (with Xnew): x_{k-1} = 0
 bool launch_box_cheb(const eig_mat_s &M, i64 m, const double *Xk, double *Xold, const double *B, const double *dinv,
                      double omega, double gamma, hipStream_t s, double *Xnew = nullptr);
@@ -400,6 +402,10 @@ void sym_pack_fill(eig_mat_s &A, hipStream_t s);
 
 // MultiVector<double,8> kernels.
 void launch_spmm_mv8(const eig_mat_s &A, i64 m, const double *Qin, double *Qout, hipStream_t s);
+// Y = A X and dp = the diagonal dots X_j . Y_j (StandardLargest's :84-85): one fused launch on the
+// row-class image, else the product and k_dot_diag_mv8 (tickets 0 .. m / 8 - 1 of red)
+void launch_spmm_dot_mv8(const eig_mat_s &A, i64 m, const double *X, double *Y, double *dp, hipStream_t s,
+                         ReduceWS red);
 void launch_dot_diag_mv8(i64 n, i64 m, const double *Q1, const double *Q2, double *dp, int ticket,
                          hipStream_t s, ReduceWS red);
 void launch_gram_mv8(i64 n, i64 m1, i64 m2, const double *Q1, const double *Q2, double *G, int ticket,

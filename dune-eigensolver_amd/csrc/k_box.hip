@@ -19,6 +19,7 @@
 // rounds products and sums separately (bitwise the reference SpMM, kernels_cpp.hh:644-655),
 // kBoxCheb uses fused multiply-adds and the Chebyshev-Jacobi update of k_spmm8_marchg.
 #include "internal.h"
+#include "reduce_dev.h"
 
 namespace eigmi {
 
@@ -45,7 +46,16 @@ enum {
   kBoxChebSecond = 4,
   kBoxChebFirstAdd = 5,
   kBoxResidCopy = 6,
-  kBoxResidAcc = 7
+  kBoxResidAcc = 7,
+  kBoxStoreDot = 8  // kBoxStore + the diagonal dots x_j . y_j of each column (row-class kernel only)
+};
+// kBoxStoreDot's reduction: dp[8 b + j] = sum_r X(r, 8b + j) Y(r, 8b + j), one deterministic grid sum
+// (workgroup partials in part, a ticket per column block) -- dot_products_diagonal_blocked fused into
+// the product that feeds it (StandardLargest, eigensolver.hh:84-85)
+struct BoxDot {
+  double *dp = nullptr;
+  double *part = nullptr;
+  unsigned *tick = nullptr;
 };
 constexpr int kBoxMaxNd = 15;  // offsets of the box-image kernel's LDS value tile (P1 Kuhn: 15, 7-point: 7)
 constexpr int kBoxClassMaxNd = 27;  // offsets of the row-class kernels (27: Galerkin coarse operators)
@@ -685,7 +695,8 @@ __global__ __launch_bounds__(kCThreads, 8) void k_boxc_mv8(BoxGeom g, i64 ld, co
                                                         const unsigned *__restrict__ cmask,
                                                         const double *__restrict__ X, double *__restrict__ Y,
                                                         const double *__restrict__ Xold,
-                                                        const double *__restrict__ Bv, double omega, double gamma)
+                                                        const double *__restrict__ Bv, double omega, double gamma,
+                                                        BoxDot bd)
 {
   __shared__ __attribute__((aligned(16))) dv2b ring[3][kCHY * kCHX][4];
   __shared__ double ct[kBoxClasses][kCStride];
@@ -706,6 +717,8 @@ __global__ __launch_bounds__(kCThreads, 8) void k_boxc_mv8(BoxGeom g, i64 ld, co
   const int z0 = seg * g.nz / g.nseg, z1 = (seg + 1) * g.nz / g.nseg;
   constexpr bool first = EPI == kBoxChebFirst || EPI == kBoxChebFirstAdd;
   constexpr bool cheb = EPI == kBoxCheb || first || EPI == kBoxChebSecond;
+  constexpr bool plain = EPI == kBoxStore || EPI == kBoxStoreDot;  // Y = A X, separately rounded
+  dv2b dsum = {0.0, 0.0};  // kBoxStoreDot: this thread's x . y over its rows, columns 2 cp, 2 cp + 1
   // X plane zz of the tile + halo (8 columns, 64-B rows) into ring slot zz mod 3 (kBoxChebFirst: X is
   // b, and the ring takes x_1 = (gamma / a_rr) b with the row's class diagonal, as k_cheb_init)
   dv2b pre[kCRounds];
@@ -748,7 +761,7 @@ __global__ __launch_bounds__(kCThreads, 8) void k_boxc_mv8(BoxGeom g, i64 ld, co
   const int cxy = (own ? box_cls1(y, g.ny) * 3 + box_cls1(x, g.nx) : 0);
   dv2b bb = {}, xo = {}, bn = {}, xn = {};
   auto fetch_cheb = [&](int zz, dv2b &b2, dv2b &x2) {
-    if (EPI == kBoxStore || !own || zz >= z1) return;
+    if (plain || !own || zz >= z1) return;
     const i64 r = (i64)x + (i64)g.nx * y + (i64)g.P * zz;
     if constexpr (first)
       b2 = Bb[r * 4 + cp];  // (the plane just went through the ring: an L2 hit)
@@ -776,7 +789,7 @@ __global__ __launch_bounds__(kCThreads, 8) void k_boxc_mv8(BoxGeom g, i64 ld, co
     // stored entry k: a * x, summed in ascending offset order; an offset the row does not store is
     // dropped by a select (the class entry is 0 there, but 0 * inf would not be)
     auto add = [&](bool on, double a, dv2b xv) {
-      if (EPI == kBoxStore)
+      if (plain)
       {
         const double s0v = acc.x + a * xv.x, s1v = acc.y + a * xv.y;
         acc.x = on ? s0v : acc.x;
@@ -831,8 +844,16 @@ __global__ __launch_bounds__(kCThreads, 8) void k_boxc_mv8(BoxGeom g, i64 ld, co
     if (own)
     {
       const i64 r = (i64)x + (i64)g.nx * y + (i64)g.P * z;
-      if (EPI == kBoxStore)
+      if (plain)
+      {
         __builtin_nontemporal_store(acc, Yb + r * 4 + cp);
+        if constexpr (EPI == kBoxStoreDot)
+        {
+          const dv2b xc = ring[s0][hrow][cp];  // the row's own X (plane z)
+          dsum.x += xc.x * acc.x;
+          dsum.y += xc.y * acc.y;
+        }
+      }
       else if (EPI == kBoxResid || EPI == kBoxResidCopy || EPI == kBoxResidAcc)
       {
         __builtin_nontemporal_store(dv2b{bb.x - acc.x, bb.y - acc.y}, Yb + r * 4 + cp);
@@ -868,6 +889,24 @@ __global__ __launch_bounds__(kCThreads, 8) void k_boxc_mv8(BoxGeom g, i64 ld, co
     store(z + 2);
     bb = bn;
     xo = xn;
+  }
+  if constexpr (EPI == kBoxStoreDot)
+  {
+    // every thread of every workgroup arrives here (no early exit above); the 8 column sums of this
+    // column block in workgroup order (grid_sum_n: fixed order, independent of dispatch)
+    __shared__ double tot[8];
+    double v[8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+    {
+      v[2 * q] = q == cp ? dsum.x : 0.0;
+      v[2 * q + 1] = q == cp ? dsum.y : 0.0;
+    }
+    if (grid_sum_n<8, kCThreads>(v, bd.part + (size_t)blockIdx.y * gridDim.x * 8, bd.tick + (size_t)blockIdx.y * kTicketStride,
+                                 tot, blockIdx.x, gridDim.x))
+    {
+      if (tid < 8) bd.dp[blockIdx.y * 8 + tid] = tot[tid];
+    }
   }
 }
 }  // namespace
@@ -1067,10 +1106,11 @@ int box_cols(const eig_mat_s &A) { return A.tune_box_cols == 16 ? 16 : 32; }
 // Y = A X (EPI store) or the Chebyshev step into Xold (EPI cheb) for m % 32 == 0 columns on the box
 // kernel; false when the matrix has no box geometry (the caller takes the band march).
 static bool launch_box(const eig_mat_s &A, i64 m, const double *X, double *Y, const double *Xold, const double *Bv,
-                       const double *dinv, double omega, double gamma, int epi, hipStream_t s)
+                       const double *dinv, double omega, double gamma, int epi, hipStream_t s, BoxDot bd = {})
 {
   if (m <= 0 || m % 8 != 0 || !box_prepare(A)) return false;
   if (epi >= kBoxChebFirst && !A.box_ctab) return false;  // (row-class only)
+  if (epi == kBoxStoreDot && !A.box_ctab) return false;
   if (A.box_ctab)
   {
     // row-class kernels: one launch, blockIdx.y = column block.  z runs of about 32 planes (a run
@@ -1095,6 +1135,9 @@ static bool launch_box(const eig_mat_s &A, i64 m, const double *X, double *Y, co
       g.dxy[k] = k < A.sym_nd ? A.box_dy[k] * kCHX + A.box_dx[k] : 0;
     }
     const dim3 grid((unsigned)(g.ntx * g.nty * g.nseg), (unsigned)(m / 8));
+    // kBoxStoreDot: one ticket and grid.x x 8 partials per column block
+    if (epi == kBoxStoreDot && ((i64)grid.x * 8 * grid.y > (i64)kMaxRedBlocks * kMaxRedVals || grid.y > kNumTickets))
+      return false;
     // the stencil's shape: compile-time kernels for the 7-point and the Kuhn 15-point stencils,
     // a runtime offset loop for any other
     unsigned shape = 0;
@@ -1106,28 +1149,31 @@ static bool launch_box(const eig_mat_s &A, i64 m, const double *X, double *Y, co
       const unsigned *cm = (const unsigned *)A.box_cmask;
       if (epi == kBoxCheb)
         hipLaunchKernelGGL((k_boxc_mv8<kBoxCheb, S>), grid, dim3(kCThreads), 0, s, g, A.window, ct, cm, X, Y, Xold,
-                           Bv, omega, gamma);
+                           Bv, omega, gamma, bd);
       else if (epi == kBoxChebFirst)
         hipLaunchKernelGGL((k_boxc_mv8<kBoxChebFirst, S>), grid, dim3(kCThreads), 0, s, g, A.window, ct, cm, X, Y,
-                           (const double *)nullptr, Bv, omega, gamma);
+                           (const double *)nullptr, Bv, omega, gamma, bd);
       else if (epi == kBoxChebFirstAdd)
         hipLaunchKernelGGL((k_boxc_mv8<kBoxChebFirstAdd, S>), grid, dim3(kCThreads), 0, s, g, A.window, ct, cm, X, Y,
-                           (const double *)nullptr, Bv, omega, gamma);
+                           (const double *)nullptr, Bv, omega, gamma, bd);
       else if (epi == kBoxResidCopy)
         hipLaunchKernelGGL((k_boxc_mv8<kBoxResidCopy, S>), grid, dim3(kCThreads), 0, s, g, A.window, ct, cm, X, Y,
-                           Xold, Bv, 0.0, 0.0);
+                           Xold, Bv, 0.0, 0.0, bd);
       else if (epi == kBoxResidAcc)
         hipLaunchKernelGGL((k_boxc_mv8<kBoxResidAcc, S>), grid, dim3(kCThreads), 0, s, g, A.window, ct, cm, X, Y,
-                           Xold, Bv, 0.0, 0.0);
+                           Xold, Bv, 0.0, 0.0, bd);
       else if (epi == kBoxChebSecond)
         hipLaunchKernelGGL((k_boxc_mv8<kBoxChebSecond, S>), grid, dim3(kCThreads), 0, s, g, A.window, ct, cm, X, Y,
-                           (const double *)nullptr, Bv, omega, gamma);
+                           (const double *)nullptr, Bv, omega, gamma, bd);
       else if (epi == kBoxResid)
         hipLaunchKernelGGL((k_boxc_mv8<kBoxResid, S>), grid, dim3(kCThreads), 0, s, g, A.window, ct, cm, X, Y,
-                           (const double *)nullptr, Bv, 0.0, 0.0);
+                           (const double *)nullptr, Bv, 0.0, 0.0, bd);
+      else if (epi == kBoxStoreDot)
+        hipLaunchKernelGGL((k_boxc_mv8<kBoxStoreDot, S>), grid, dim3(kCThreads), 0, s, g, A.window, ct, cm, X, Y,
+                           (const double *)nullptr, (const double *)nullptr, 0.0, 0.0, bd);
       else
         hipLaunchKernelGGL((k_boxc_mv8<kBoxStore, S>), grid, dim3(kCThreads), 0, s, g, A.window, ct, cm, X, Y,
-                           (const double *)nullptr, (const double *)nullptr, 0.0, 0.0);
+                           (const double *)nullptr, (const double *)nullptr, 0.0, 0.0, bd);
     };
     // (the image's offsets ascend, i.e. run in the shape's bit order: box_prepare builds them so)
     if (A.box_geomask && shape == kShape7 && A.sym_nd == 7)
@@ -1218,6 +1264,20 @@ static bool launch_box(const eig_mat_s &A, i64 m, const double *X, double *Y, co
 bool launch_box_spmm(const eig_mat_s &A, i64 m, const double *X, double *Y, hipStream_t s)
 {
   return launch_box(A, m, X, Y, nullptr, nullptr, nullptr, 0.0, 0.0, kBoxStore, s);
+}
+
+// Y = A X and dp[j] = X_j . Y_j (8 per column block) in one launch: the row-class kernel only
+// (false otherwise: the caller runs the product and dot_diag separately).  red: the context's
+// reduction workspace, its tickets 0 .. m / 8 - 1.
+bool launch_box_spmm_dot(const eig_mat_s &A, i64 m, const double *X, double *Y, double *dp, ReduceWS red,
+                         hipStream_t s)
+{
+  if (m <= 0 || m % 8 != 0 || !box_prepare(A) || !A.box_ctab) return false;
+  BoxDot bd;
+  bd.dp = dp;
+  bd.part = red.partials;
+  bd.tick = red.ticket(0);
+  return launch_box(A, m, X, Y, nullptr, nullptr, nullptr, 0.0, 0.0, kBoxStoreDot, s, bd);
 }
 
 bool launch_box_resid(const eig_mat_s &A, i64 m, const double *X, const double *B, double *R, hipStream_t s)

@@ -93,6 +93,15 @@ void launch_spmm_mv8(const eig_mat_s &A, i64 m, const double *Qin, double *Qout,
                      Qin, Qout, A.nb_rows, nblk, 64 * A.R);
 }
 
+void launch_spmm_dot_mv8(const eig_mat_s &A, i64 m, const double *X, double *Y, double *dp, hipStream_t s,
+                         ReduceWS red)
+{
+  static const bool off = std::getenv("EIGMI_NO_SPMM_DOT") != nullptr;  // A/B: the two launches
+  if (!off && A.R == 1 && A.br == 1 && A.bc == 1 && launch_box_spmm_dot(A, m, X, Y, dp, red, s)) return;
+  launch_spmm_mv8(A, m, X, Y, s);
+  launch_dot_diag_mv8(A.nb_rows, m, X, Y, dp, 0, s, red);
+}
+
 // ---------------------------------------------------------------------------------------------
 // a5: dp[j] = q1_j . q2_j (dot_products_diagonal_blocked, kernels_cpp.hh:24-55).  grid.y = column
 // block; thread t always sees the column pair 2 (t%4) because the grid stride is a multiple of 4.
