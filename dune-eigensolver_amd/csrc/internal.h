@@ -341,10 +341,17 @@ extern const i32 kMarchInteriorTag;
 // a2 SpMM (kernels_cpp.hh:626-657) on the band-image plane march for 1x1 matrices whose band
 // qualifies; false (nothing launched) otherwise.  X, Y: window-layout multivectors, m % 8 == 0.
 bool box_prepare(const eig_mat_s &A);
+// launch_box_spmm would take this product (row-class image, or the box image at m % 32 == 0)
+inline bool box_spmm_applies(const eig_mat_s &A, i64 m)
+{
+  return m > 0 && m % 8 == 0 && box_prepare(A) && (A.box_ctab != nullptr || m % 32 == 0);
+}
 int box_cols(const eig_mat_s &A);  // columns per box-image workgroup (k_box_mv32: 32, k_box_mv16p: 16)
 bool launch_box_spmm(const eig_mat_s &A, i64 m, const double *X, double *Y, hipStream_t s);
 bool launch_box_spmm_dot(const eig_mat_s &A, i64 m, const double *X, double *Y, double *dp, ReduceWS red,
                          hipStream_t s);
+bool launch_spmm_march_dot(const eig_mat_s &A, i64 m, const double *X, double *Y, double *dp, ReduceWS red,
+                           hipStream_t s);
 // Xnew: x_{k+1} into a third buffer (nullptr: in place over Xold); Xold nullptr (with Xnew): x_{k-1} = 0
 bool launch_box_cheb(const eig_mat_s &M, i64 m, const double *Xk, double *Xold, const double *B, const double *dinv,
                      double omega, double gamma, hipStream_t s, double *Xnew = nullptr);

@@ -97,7 +97,12 @@ void launch_spmm_dot_mv8(const eig_mat_s &A, i64 m, const double *X, double *Y, 
                          ReduceWS red)
 {
   static const bool off = std::getenv("EIGMI_NO_SPMM_DOT") != nullptr;  // A/B: the two launches
-  if (!off && A.R == 1 && A.br == 1 && A.bc == 1 && launch_box_spmm_dot(A, m, X, Y, dp, red, s)) return;
+  // the same kernel choice as launch_spmm_mv8 -> launch_sell_mv8 (box first, then the band march)
+  if (!off && A.R == 1 && A.br == 1 && A.bc == 1)
+  {
+    if (launch_box_spmm_dot(A, m, X, Y, dp, red, s)) return;
+    if (!box_spmm_applies(A, m) && launch_spmm_march_dot(A, m, X, Y, dp, red, s)) return;
+  }
   launch_spmm_mv8(A, m, X, Y, s);
   launch_dot_diag_mv8(A.nb_rows, m, X, Y, dp, 0, s, red);
 }

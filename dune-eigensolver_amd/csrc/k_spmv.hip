@@ -2148,10 +2148,14 @@ __device__ __forceinline__ double lane_from(double v, int src_lane)
 
 // One column block per workgroup (blockIdx.y): sharing the band stream between 2 / 4 blocks measured
 // equal / 6 % slower (m = 32 at 256^3) -- the vector streams bound the launch.
-template <class MT>
-__global__ __launch_bounds__(kStreamThreads, 8) void k_spmm8_march(i64 nrows, i64 own, i64 ld, SellB1 A,
+// DOT: also dp[8 qb + j] = X_j . Y_j over the rows (StandardLargest's :84-85 in one launch): each
+// lane adds its row's own operand x its result, one deterministic grid sum per column block
+// (partials part + grid.x * 8 qb, ticket tick + qb kTicketStride); Y is unchanged.
+template <class MT, bool DOT = false>
+__global__ __launch_bounds__(kStreamThreads, DOT ? 6 : 8) void k_spmm8_march(i64 nrows, i64 own, i64 ld, SellB1 A,
                                                                    MarchPlan mp, const double *__restrict__ X,
-                                                                   double *__restrict__ Y)
+                                                                   double *__restrict__ Y, double *dp = nullptr,
+                                                                   double *part = nullptr, unsigned *tick = nullptr)
 {
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int qb = (int)blockIdx.y;  // column block
@@ -2164,9 +2168,13 @@ __global__ __launch_bounds__(kStreamThreads, 8) void k_spmm8_march(i64 nrows, i6
   const double *U0 = S.val + (i64)(S.j0 >= 0 ? S.j0 : 0) * S.ld;
   const MT *mask = static_cast<const MT *>(S.mask);
   const int item = (int)swizzled_block() * kWaves + wave;
-  if (item >= mp.ncol * mp.nseg) return;
+  // (DOT: a wave past the last item joins the workgroup's reduction with an empty march)
+  const bool live = item < mp.ncol * mp.nseg;
+  if (!DOT && !live) return;
   const int col = item % mp.ncol, seg = item / mp.ncol;
-  const int z0 = (int)(mp.zb + seg * mp.nplanes / mp.nseg), z1 = (int)(mp.zb + (seg + 1) * mp.nplanes / mp.nseg);
+  const int z0 = (int)(mp.zb + seg * mp.nplanes / mp.nseg);
+  const int z1 = live ? (int)(mp.zb + (seg + 1) * mp.nplanes / mp.nseg) : z0;
+  dpair dsum{0.0, 0.0};
   // column block qb, column pair cp: row g's operand at Xb[g]
   const dpair *Xb = reinterpret_cast<const dpair *>(X + (i64)qb * ld * 8) + cp;
   dpair *Yb = reinterpret_cast<dpair *>(Y + (i64)qb * ld * 8) + cp;
@@ -2231,10 +2239,34 @@ __global__ __launch_bounds__(kStreamThreads, 8) void k_spmm8_march(i64 nrows, i6
     for (int k = kp0 + 1; k < kp1; ++k)
       if ((m >> k) & 1u) acc = fma2(acc, S.val[(i64)S.dj[k] * S.ld + wv], xat(w + S.off[k]));
     if ((m >> kp1) & 1u) acc = fma2(acc, aD, pD);
-    if (r < nrows) __builtin_nontemporal_store(acc, Yb + (unsigned)w * 4u);
+    if (r < nrows)
+    {
+      __builtin_nontemporal_store(acc, Yb + (unsigned)w * 4u);
+      if (DOT)
+      {
+        dsum.x += pcur.x * acc.x;
+        dsum.y += pcur.y * acc.y;
+      }
+    }
     pm = pcur;
     pcur = pD;
     amD = aD;
+  }
+  if constexpr (DOT)
+  {
+    __shared__ double tot[8];
+    double v[8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+    {
+      v[2 * q] = q == cp ? dsum.x : 0.0;
+      v[2 * q + 1] = q == cp ? dsum.y : 0.0;
+    }
+    if (grid_sum_n<8, kStreamThreads>(v, part + (size_t)qb * gridDim.x * 8, tick + (size_t)qb * kTicketStride, tot,
+                                      blockIdx.x, gridDim.x))
+    {
+      if (threadIdx.x < 8) dp[qb * 8 + threadIdx.x] = tot[threadIdx.x];
+    }
   }
 }
 
@@ -3038,6 +3070,28 @@ bool launch_spmm_march(const eig_mat_s &A, i64 m, const double *X, double *Y, hi
   else
     hipLaunchKernelGGL((k_spmm8_march<uint32_t>), grid, dim3(kStreamThreads), 0, s, A.nb_rows, A.own_offset, A.window,
                        sell_b1(A), mp, X, Y);
+  return true;
+}
+
+// Y = A X with the diagonal dots dp (k_spmm8_march<MT, true>) where the band march applies to the
+// whole matrix on one rank; false otherwise (the caller runs the product and k_dot_diag_mv8).
+bool launch_spmm_march_dot(const eig_mat_s &A, i64 m, const double *X, double *Y, double *dp, ReduceWS red,
+                           hipStream_t s)
+{
+  if (A.br != 1 || A.bc != 1 || m <= 0 || A.ctx->distributed()) return false;
+  const int mode = image_mode(A);
+  if (!is_sym_mode(mode)) return false;
+  const MarchPlan mp = march_plan(A, mode, 0, -1, false, 16);
+  if (mp.nseg == 0) return false;
+  const i64 items = mp.ncol * (i64)mp.nseg;
+  const dim3 grid((unsigned)((items + kWaves - 1) / kWaves), (unsigned)(m / 8));
+  if ((i64)grid.x * 8 * grid.y > (i64)kMaxRedBlocks * kMaxRedVals || grid.y > (unsigned)kNumTickets) return false;
+  if (mode == kSymN8)
+    hipLaunchKernelGGL((k_spmm8_march<uint8_t, true>), grid, dim3(kStreamThreads), 0, s, A.nb_rows, A.own_offset,
+                       A.window, sell_b1(A), mp, X, Y, dp, red.partials, red.ticket(0));
+  else
+    hipLaunchKernelGGL((k_spmm8_march<uint32_t, true>), grid, dim3(kStreamThreads), 0, s, A.nb_rows, A.own_offset,
+                       A.window, sell_b1(A), mp, X, Y, dp, red.partials, red.ticket(0));
   return true;
 }
 
