@@ -239,8 +239,9 @@ enum { EIG_TUNE_MARCH_RUNS = 1, EIG_TUNE_BOX_SEGS = 2, EIG_TUNE_MARCH_PREFETCH =
 /* EIG_TUNE_SELL_CPF (explicit-column SELL slices; measurement switch): 1 = the next slice's column
  * indices loaded while this slice's gathers are in flight (one memory round trip per slice instead
  * of two), in the fused Lanczos step (5 waves per SIMD instead of 6) and in eig_mv; 0 / 2 = off (the
- * default: measured slower, 437 vs 402 us for the general 256^3 fused step).  Results bitwise
- * identical. */
+ * default: measured slower, 437 vs 402 us for the general 256^3 fused step).  eig_mv and every
+ * row's products bitwise identical; the fused step's three sums are added in another order where
+ * the occupancy-derived grid differs (large matrices), so its alpha / beta agree to rounding there. */
 /* EIG_TUNE_BOX_MAP (measurement; k_box_mv32): 1 = XCD-contiguous tile map (the workgroups resident on
  * one XCD hold whole rows of adjacent tiles), 0 = dispatch order.  Results bitwise identical. */
 /* EIG_TUNE_BOX_COLS (box-image kernels, EIG_OP_SPMM32 / EIG_OP_CHEB32 on matrices without a row-class
