@@ -297,3 +297,40 @@ def test_standard_largest_reuses_product_bitwise(ctx, make, nev, shift):
     assert it == maxiter - 1
     assert np.array_equal(evec, ref_evec)
     assert np.abs(ev - s2[:nev]).max() <= 1e-14 * np.abs(s2).max()
+
+
+@pytest.mark.parametrize("maxiter,tol", [(1, 0.0), (2, 0.0), (4000, 1e-6)])
+def test_standard_largest_lookahead_stop(ctx, maxiter, tol):
+    """The look-ahead loop (iteration k + 1 queued before iteration k's stopping test) returns the
+    basis and Ritz values of the iteration that stopped, not of the queued one: the driver against
+    the reference's loop (eigensolver.hh:69-103) written with the primitives, incl. the stopping test
+    (:87-102) and the no-iteration / one-iteration edges.  Iterates bitwise, Ritz values within 1e-14
+    (the driver's dots are fused into the product)."""
+    A = oracle.laplace2d(24)
+    nev, m, shift = 4, 8, 0.0
+    M = upload(ctx, A)
+    n = M.n
+    ev, evec, it = eigmi.standard_largest(M, shift, tol, maxiter, nev, 11)
+    Q1, Q2, dp = ctx.zeros(n * m), ctx.zeros(n * m), ctx.zeros(m)
+    eigmi.random_mv8(ctx, n, m, 11, Q1)
+    eigmi.orthonormalize_mv8(ctx, n, m, Q1)
+    s2 = np.zeros(m)
+    kk = 1
+    for k in range(1, maxiter):
+        kk = k
+        eigmi.spmm_mv8(M, m, Q1, Q2)
+        eigmi.orthonormalize_mv8(ctx, n, m, Q2)
+        eigmi.spmm_mv8(M, m, Q2, Q1)
+        eigmi.dot_diag_mv8(ctx, n, m, Q2, Q1, dp)
+        s1 = dp.get() - shift
+        dist = np.abs(s1 - s2).max()
+        s2 = s1
+        Q1, Q2 = Q2, Q1
+        if k > 1 and dist < tol:
+            break
+    q = Q1.get().reshape(m // 8, n, 8)
+    ref_evec = np.stack([q[j // 8, :, j % 8] for j in range(nev)])
+    print(f"maxiter {maxiter} tol {tol}: {it} iterations (reference loop {kk})")
+    assert it == kk
+    assert np.array_equal(evec, ref_evec)
+    assert np.abs(ev - s2[:nev]).max() <= 1e-14 * max(1.0, np.abs(s2).max())
