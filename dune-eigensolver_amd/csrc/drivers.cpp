@@ -189,9 +189,14 @@ extern "C" int eig_standard_inverse(eig_mat_t A, eig_lu_t lu, double shift, doub
     hipStream_t s = ctx->stream;
     const i64 n = A->nb_rows;
     const i64 m = (nev / 8 + std::min(nev % 8, 1)) * 8;  // eigensolver.hh:133
-    DevBuf Q1b(n * m * 8), Q2b(n * m * 8), dpb(m * 8);
-    double *Q1 = Q1b.d(), *Q2 = Q2b.d();
-    random_block(ctx, n, m, seed, Q1);
+    // basis ping-pong B[0] / B[1] and a product block Z: iteration k solves from B[(k - 1) % 2] into
+    // B[k % 2], so the queued iteration k + 1 never touches iteration k's basis (look-ahead over the
+    // host's stopping test, as eig_standard_largest)
+    DevBuf Q1b(n * m * 8), Q2b(n * m * 8), Zb(n * m * 8), dpb(2 * m * 8);
+    double *Bk[2] = {Q1b.d(), Q2b.d()}, *Z = Zb.d();
+    PinnedDoubles hd(2 * (size_t)m);
+    SyncEvent ev[2];
+    random_block(ctx, n, m, seed, Bk[0]);
     if (shift != 0.0) launch_shift_diag(*A, shift, s);  // :145-153 (mutates A)
     LuRef F;                                           // :156 UMFPackFactorizedMatrix<ISTLM> F(A, 1)
     if (lu)
@@ -207,28 +212,34 @@ extern "C" int eig_standard_inverse(eig_mat_t A, eig_lu_t lu, double shift, doub
     }
     EIG_CHECK(lu_size(F.lu) == n, EIG_ERR_SHAPE,
               "matmul_inverse_tallskinny_blocked: Factorization does not match size of Qout/Qin");
-    orthonormalize_device(ctx, n, m, Q1, EIG_ORTHO_MGS);  // :159
+    orthonormalize_device(ctx, n, m, Bk[0], EIG_ORTHO_MGS);  // :159
+    auto enqueue = [&](int k) {
+      double *Q = Bk[k % 2], *dp = dpb.d() + (k & 1) * m;
+      lu_inverse_device(F.lu, m, Bk[(k + 1) % 2], Q, s);  // :168 Q2 = A^-1 Q1
+      orthonormalize_device(ctx, n, m, Q, EIG_ORTHO_MGS);  // :171
+      launch_spmm_dot_mv8(*A, m, Q, Z, dp, s, ctx->red);    // :174-175 (the product only feeds the dots)
+      EIG_HIP(hipMemcpyAsync(hd.p + (k & 1) * m, dp, m * 8, hipMemcpyDeviceToHost, s));
+      EIG_HIP(hipEventRecord(ev[k & 1].e, s));
+    };
     std::vector<double> s1(m, 0.0), s2(m, 0.0);
-    int kk = 1;
+    int kk = 1, basis = 0;
+    if (maxiter > 1) enqueue(1);
     for (int k = 1; k < maxiter; ++k)
     {
       kk = k;
-      lu_inverse_device(F.lu, m, Q1, Q2, s);               // :168 Q2 = A^-1 Q1
-      orthonormalize_device(ctx, n, m, Q2, EIG_ORTHO_MGS);  // :171
-      launch_spmm_mv8(*A, m, Q2, Q1, s);                   // :174
-      launch_dot_diag_mv8(n, m, Q2, Q1, dpb.d(), 0, s, ctx->red);  // :175
-      EIG_HIP(hipMemcpyAsync(s1.data(), dpb.d(), m * 8, hipMemcpyDeviceToHost, s));
-      EIG_HIP(hipStreamSynchronize(s));
-      for (auto &x : s1) x -= shift;
+      if (k + 1 < maxiter) enqueue(k + 1);  // look-ahead: queued before iteration k's stopping test
+      EIG_HIP(hipEventSynchronize(ev[k & 1].e));
+      for (i64 i = 0; i < m; ++i) s1[i] = hd.p[(k & 1) * m + i] - shift;
       double dist = 0.0;
       for (i64 i = 0; i < m; ++i) dist = std::max(dist, std::fabs(s1[i] - s2[i]));
       if (verbose > 0 && k > 1) fprintf(stdout, "iter=%d %.17g\n", k, dist);
       std::swap(s1, s2);
-      std::swap(Q1, Q2);
+      basis = k % 2;  // Q1 after the swap
       if (k > 1 && dist < tol) break;
     }
     for (int j = 0; j < nev; ++j) eval_host[j] = s2[j];
-    copy_evecs(ctx, Q1, n, nev, evec_host);
+    copy_evecs(ctx, Bk[basis], n, nev, evec_host);  // (stream order: after any queued iteration)
+    EIG_HIP(hipStreamSynchronize(s));
     if (iters) *iters = kk;
   });
 }
@@ -288,29 +299,39 @@ extern "C" int eig_generalized_inverse(eig_mat_t A, eig_mat_t B, eig_lu_t lu, do
     EIG_CHECK(lu_size(F.lu) == n, EIG_ERR_SHAPE,
               "matmul_inverse_tallskinny_blocked: Factorization does not match size of Qout/Qin");
     const i64 m = (nev / 8 + std::min(nev % 8, 1)) * 8;  // :224
-    DevBuf Q1b(n * m * 8), Q2b(n * m * 8), dpb(m * 8 + 8);
-    double *Q1 = Q1b.d(), *Q2 = Q2b.d(), *norm = dpb.d() + m;
-    random_block(ctx, n, m, seed, Q1);
-    std::vector<double> ra1(m, 0.0), ra2(m, 0.0), sA(m, 0.0);
-    b_orthonormalize_device(*B, m, Q1, norm);            // :273
-    launch_spmm_mv8(*As, m, Q1, Q2, s);                  // :274
-    launch_dot_diag_mv8(n, m, Q2, Q1, dpb.d(), 0, s, ctx->red);  // :275
-    EIG_HIP(hipMemcpyAsync(sA.data(), dpb.d(), m * 8, hipMemcpyDeviceToHost, s));
+    // basis ping-pong Bk[0] / Bk[1] and a scratch block Z (B Q1, then the As product): iteration i
+    // reads Bk[(i - 1) % 2] and leaves its basis in Bk[i % 2], so iteration i + 1 is queued before the
+    // host's relative-error test of iteration i without touching that basis (as eig_standard_largest)
+    DevBuf Q1b(n * m * 8), Q2b(n * m * 8), Zb(n * m * 8), dpb(2 * m * 8 + 8);
+    double *Bk[2] = {Q1b.d(), Q2b.d()}, *Z = Zb.d(), *norm = dpb.d() + 2 * m;
+    PinnedDoubles hd(2 * (size_t)m);
+    SyncEvent ev[2];
+    random_block(ctx, n, m, seed, Bk[0]);
+    std::vector<double> ra1(m, 0.0), ra2(m, 0.0);
+    b_orthonormalize_device(*B, m, Bk[0], norm);                 // :273
+    launch_spmm_dot_mv8(*As, m, Bk[0], Z, dpb.d(), s, ctx->red);  // :274-275
+    EIG_HIP(hipMemcpyAsync(hd.p, dpb.d(), m * 8, hipMemcpyDeviceToHost, s));
     EIG_HIP(hipStreamSynchronize(s));
-    for (i64 i = 0; i < m; ++i) ra2[i] = sA[i] - shift;
-    int iter = 0;
+    for (i64 i = 0; i < m; ++i) ra2[i] = hd.p[i] - shift;
+    auto enqueue = [&](int i) {
+      double *Q = Bk[i % 2], *dp = dpb.d() + (i & 1) * m;
+      launch_spmm_mv8(*B, m, Bk[(i + 1) % 2], Z, s);        // :302 Q2 = B Q1
+      lu_inverse_device(F.lu, m, Z, Q, s);                   // :303 Q1 = A^-1 Q2
+      b_orthonormalize_device(*B, m, Q, norm);               // :304
+      launch_spmm_dot_mv8(*As, m, Q, Z, dp, s, ctx->red);     // :317 and the dots
+      EIG_HIP(hipMemcpyAsync(hd.p + (i & 1) * m, dp, m * 8, hipMemcpyDeviceToHost, s));
+      EIG_HIP(hipEventRecord(ev[i & 1].e, s));
+    };
+    int iter = 0, basis = 0;
     double relerror = 0.0;
+    if (maxiter > 0) enqueue(1);
     while (iter < maxiter)
     {
-      launch_spmm_mv8(*B, m, Q1, Q2, s);       // :302 Q2 = B Q1
-      lu_inverse_device(F.lu, m, Q2, Q1, s);   // :303 Q1 = A^-1 Q2
-      b_orthonormalize_device(*B, m, Q1, norm);  // :304
       iter += 1;
-      launch_spmm_mv8(*As, m, Q1, Q2, s);      // :317
-      launch_dot_diag_mv8(n, m, Q2, Q1, dpb.d(), 0, s, ctx->red);
-      EIG_HIP(hipMemcpyAsync(sA.data(), dpb.d(), m * 8, hipMemcpyDeviceToHost, s));
-      EIG_HIP(hipStreamSynchronize(s));
-      for (i64 i = 0; i < m; ++i) ra1[i] = sA[i] - shift;
+      if (iter + 1 <= maxiter) enqueue(iter + 1);  // look-ahead: queued before this iteration's test
+      EIG_HIP(hipEventSynchronize(ev[iter & 1].e));
+      for (i64 i = 0; i < m; ++i) ra1[i] = hd.p[(iter & 1) * m + i] - shift;
+      basis = iter % 2;
       relerror = 0.0;
       for (i64 i = 0; i < m; ++i) relerror = std::max(relerror, std::fabs(ra1[i] - ra2[i]));
       relerror /= *std::max_element(ra1.begin(), ra1.end());
@@ -319,7 +340,8 @@ extern "C" int eig_generalized_inverse(eig_mat_t A, eig_mat_t B, eig_lu_t lu, do
       if ((iter > 10) & (relerror < tol)) break;  // :325
     }
     for (int j = 0; j < nev; ++j) eval_host[j] = ra2[j];
-    copy_evecs(ctx, Q1, n, nev, evec_host);
+    copy_evecs(ctx, Bk[basis], n, nev, evec_host);  // (stream order: after any queued iteration)
+    EIG_HIP(hipStreamSynchronize(s));
     if (iters) *iters = iter;
     if (verbose > 0) fprintf(stdout, "GeneralizedInverse: iterations=%d relerror=%.17g\n", iter, relerror);
   });
