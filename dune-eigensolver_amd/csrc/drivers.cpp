@@ -20,11 +20,17 @@ namespace {
 
 bool distributed(const eig_mat_s &A) { return A.ctx->distributed(); }
 
-// Page-locked host doubles (a hipMemcpyAsync into pageable memory would block the host until the
-// copy is done) and a timing-free event: the drivers' per-iteration stopping data.
+// Page-locked, device-mapped host doubles and a timing-free event: the drivers' per-iteration
+// stopping data.  The reducing kernel's last workgroup stores its sums straight into this memory
+// through `dev` (no device-to-host copy launch per iteration); the event recorded after the kernel
+// on the stream orders those stores before the host reads them.
 struct PinnedDoubles {
-  double *p = nullptr;
-  explicit PinnedDoubles(size_t n) { EIG_HIP(hipHostMalloc(reinterpret_cast<void **>(&p), (n ? n : 1) * sizeof(double))); }
+  double *p = nullptr, *dev = nullptr;
+  explicit PinnedDoubles(size_t n)
+  {
+    EIG_HIP(hipHostMalloc(reinterpret_cast<void **>(&p), (n ? n : 1) * sizeof(double), hipHostMallocMapped));
+    EIG_HIP(hipHostGetDevicePointer(reinterpret_cast<void **>(&dev), p, 0));
+  }
   ~PinnedDoubles()
   {
     if (p) (void)hipHostFree(p);
@@ -71,7 +77,7 @@ extern "C" int eig_standard_largest(eig_mat_t A, double shift, double tol, int m
     // reference's order (one SpMM per iteration from k = 2 on, see :78 below), so the iterates, the Ritz
     // values and the iteration count are bitwise those of the plain loop
     // (tests/test_gpu_drivers.py::test_standard_largest_reuses_product_bitwise).
-    DevBuf B0(n * m * 8), B1(n * m * 8), B2(n * m * 8), dpb(2 * m * 8);
+    DevBuf B0(n * m * 8), B1(n * m * 8), B2(n * m * 8);
     double *B[3] = {B0.d(), B1.d(), B2.d()};
     PinnedDoubles hd(2 * (size_t)m);
     SyncEvent ev[2];
@@ -88,10 +94,9 @@ extern "C" int eig_standard_largest(eig_mat_t A, double shift, double tol, int m
     // only iteration 1 runs it
     if (maxiter > 1) launch_spmm_mv8(*A, m, B[0], B[1], s);  // :78 (k = 1)
     auto enqueue = [&](int k) {
-      double *Q = B[k % 3], *P = B[(k + 1) % 3], *dp = dpb.d() + (k & 1) * m;
+      double *Q = B[k % 3], *P = B[(k + 1) % 3], *dp = hd.dev + (k & 1) * m;
       orthonormalize_device(ctx, n, m, Q, EIG_ORTHO_MGS);  // :81
-      launch_spmm_dot_mv8(*A, m, Q, P, dp, s, ctx->red);   // :84-85 (one launch on the row-class image)
-      EIG_HIP(hipMemcpyAsync(hd.p + (k & 1) * m, dp, m * 8, hipMemcpyDeviceToHost, s));
+      launch_spmm_dot_mv8(*A, m, Q, P, dp, s, ctx->red);   // :84-85, the dots straight to the host
       EIG_HIP(hipEventRecord(ev[k & 1].e, s));
     };
     std::vector<double> s1(m, 0.0), s2(m, 0.0);
@@ -192,7 +197,7 @@ extern "C" int eig_standard_inverse(eig_mat_t A, eig_lu_t lu, double shift, doub
     // basis ping-pong B[0] / B[1] and a product block Z: iteration k solves from B[(k - 1) % 2] into
     // B[k % 2], so the queued iteration k + 1 never touches iteration k's basis (look-ahead over the
     // host's stopping test, as eig_standard_largest)
-    DevBuf Q1b(n * m * 8), Q2b(n * m * 8), Zb(n * m * 8), dpb(2 * m * 8);
+    DevBuf Q1b(n * m * 8), Q2b(n * m * 8), Zb(n * m * 8);
     double *Bk[2] = {Q1b.d(), Q2b.d()}, *Z = Zb.d();
     PinnedDoubles hd(2 * (size_t)m);
     SyncEvent ev[2];
@@ -214,11 +219,10 @@ extern "C" int eig_standard_inverse(eig_mat_t A, eig_lu_t lu, double shift, doub
               "matmul_inverse_tallskinny_blocked: Factorization does not match size of Qout/Qin");
     orthonormalize_device(ctx, n, m, Bk[0], EIG_ORTHO_MGS);  // :159
     auto enqueue = [&](int k) {
-      double *Q = Bk[k % 2], *dp = dpb.d() + (k & 1) * m;
+      double *Q = Bk[k % 2], *dp = hd.dev + (k & 1) * m;
       lu_inverse_device(F.lu, m, Bk[(k + 1) % 2], Q, s);  // :168 Q2 = A^-1 Q1
       orthonormalize_device(ctx, n, m, Q, EIG_ORTHO_MGS);  // :171
       launch_spmm_dot_mv8(*A, m, Q, Z, dp, s, ctx->red);    // :174-175 (the product only feeds the dots)
-      EIG_HIP(hipMemcpyAsync(hd.p + (k & 1) * m, dp, m * 8, hipMemcpyDeviceToHost, s));
       EIG_HIP(hipEventRecord(ev[k & 1].e, s));
     };
     std::vector<double> s1(m, 0.0), s2(m, 0.0);
@@ -314,12 +318,11 @@ extern "C" int eig_generalized_inverse(eig_mat_t A, eig_mat_t B, eig_lu_t lu, do
     EIG_HIP(hipStreamSynchronize(s));
     for (i64 i = 0; i < m; ++i) ra2[i] = hd.p[i] - shift;
     auto enqueue = [&](int i) {
-      double *Q = Bk[i % 2], *dp = dpb.d() + (i & 1) * m;
+      double *Q = Bk[i % 2], *dp = hd.dev + (i & 1) * m;
       launch_spmm_mv8(*B, m, Bk[(i + 1) % 2], Z, s);        // :302 Q2 = B Q1
       lu_inverse_device(F.lu, m, Z, Q, s);                   // :303 Q1 = A^-1 Q2
       b_orthonormalize_device(*B, m, Q, norm);               // :304
-      launch_spmm_dot_mv8(*As, m, Q, Z, dp, s, ctx->red);     // :317 and the dots
-      EIG_HIP(hipMemcpyAsync(hd.p + (i & 1) * m, dp, m * 8, hipMemcpyDeviceToHost, s));
+      launch_spmm_dot_mv8(*As, m, Q, Z, dp, s, ctx->red);     // :317 and the dots, straight to the host
       EIG_HIP(hipEventRecord(ev[i & 1].e, s));
     };
     int iter = 0, basis = 0;
