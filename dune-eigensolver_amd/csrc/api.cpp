@@ -248,11 +248,39 @@ void halo_exchange(const eig_mat_s &A, double *x, hipStream_t s, double *x2, int
 
 // eigensolver.hh:49-55 generator (libstdc++ mt19937 + normal_distribution, bitwise the
 // reference's sequence).
+// The reference's start vectors: std::normal_distribution<double>{0, 1} over std::mt19937{seed}
+// (eigensolver.hh:50-55), bitwise.  libstdc++ draws them by Marsaglia's polar method on pairs of
+// generate_canonical<double, 53> uniforms (random.tcc: two 32-bit words per uniform, the second
+// variate of an accepted pair kept for the next call); its generic generate_canonical recomputes
+// long-double logarithms on every call, about two thirds of the 45 ns per variate it costs.  The
+// same arithmetic with the constants folded (the words are exact in double, the scales powers of
+// two) gives the same bits (tests/test_random_host.py against the oracle's std:: draws).
 void host_random_normal(i64 count, unsigned seed, double *out)
 {
   std::mt19937 urbg{seed};
-  std::normal_distribution<double> gen{0.0, 1.0};
-  for (i64 i = 0; i < count; ++i) out[i] = gen(urbg);
+  auto canonical = [&]() {
+    double sum = 0.0;
+    sum += double(urbg()) * 1.0;           // mt19937: min() = 0, range 2^32
+    sum += double(urbg()) * 4294967296.0;  // x 2^32
+    double r = sum / 18446744073709551616.0;  // / 2^64
+    if (r >= 1.0) r = std::nextafter(1.0, 0.0);
+    return r;
+  };
+  i64 i = 0;
+  while (i < count)
+  {
+    double x, y, r2;
+    do
+    {
+      x = 2.0 * canonical() - 1.0;
+      y = 2.0 * canonical() - 1.0;
+      r2 = x * x + y * y;
+    } while (r2 > 1.0 || r2 == 0.0);
+    const double mult = std::sqrt(-2 * std::log(r2) / r2);
+    const double a = y * mult, b = x * mult;  // returned now / cached for the next call
+    out[i++] = a * 1.0 + 0.0;                 // (ret * stddev + mean)
+    if (i < count) out[i++] = b * 1.0 + 0.0;
+  }
 }
 
 }  // namespace eigmi
@@ -260,6 +288,14 @@ void host_random_normal(i64 count, unsigned seed, double *out)
 // ============================================================================================
 // context
 // ============================================================================================
+extern "C" int eig_random_normal(int64_t count, unsigned seed, double *out)
+{
+  return guard(nullptr, [&] {
+    EIG_CHECK(count >= 0 && (out || count == 0), EIG_ERR_ARG, "eig_random_normal: bad argument");
+    host_random_normal(count, seed, out);
+  });
+}
+
 extern "C" int eig_device_count(int *count)
 {
   return guard(nullptr, [&] {

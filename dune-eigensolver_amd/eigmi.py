@@ -158,6 +158,7 @@ SIGNATURES = {
     "eig_orthonormalize_naive": (_int, [_vp, _i64, _i64, _vp]),
     "eig_b_orthonormalize_mv8": (_int, [_vp, _i64, _vp, _vp]),
     "eig_random_mv8": (_int, [_vp, _i64, _i64, _u, _vp]),
+    "eig_random_normal": (_int, [_i64, _u, _vp]),
     "eig_standard_largest": (_int, [_vp, _dbl, _dbl, _int, _int, _u, _vp, _vp, ctypes.POINTER(_int), _int]),
     "eig_lanczos_run": (_int, [_vp, _int, _vp, _u, _int, _vp, _vp, ctypes.POINTER(Timing)]),
     "eig_lanczos_solve": (_int, [_vp, _int, _int, _int, _u, _vp, _vp, _vp]),
@@ -581,6 +582,16 @@ def b_orthonormalize_mv8(B, m, Q, norm):
 
 def random_mv8(ctx, n, m, seed, Q):
     ctx.check(lib.eig_random_mv8(ctx.h, n, m, seed, Q.ptr))
+
+
+def random_normal(count, seed=123):
+    """The drivers' start-vector variates on the host (no device): bitwise
+    std::normal_distribution<double>{0, 1} over std::mt19937{seed} (eigensolver.hh:50-55)."""
+    out = np.zeros(count)
+    rc = lib.eig_random_normal(count, seed, _np_ptr(out))
+    if rc != 0:
+        raise EigError(rc, "eig_random_normal failed")
+    return out
 
 
 def standard_largest(A, shift, tol, maxiter, nev, seed=123, want_evec=True, verbose=0):

@@ -339,6 +339,10 @@ int eig_b_orthonormalize_mv8(eig_mat_t B, int64_t m, double *Q, double *norm);
 /* eigensolver.hh:49-55 start block: mt19937(seed) + normal_distribution(0,1), fill order
  * (block, row, col); generated on the host (bitwise the reference's numbers), uploaded. */
 int eig_random_mv8(eig_ctx_t ctx, int64_t n, int64_t m, unsigned seed, double *Q);
+/* Host only (no device): `count` N(0, 1) variates, bitwise std::normal_distribution<double>{0, 1}
+ * drawn from std::mt19937{seed} (libstdc++), the start blocks of eigensolver.hh:50-55 that the
+ * drivers and eig_random_mv8 use. */
+int eig_random_normal(int64_t count, unsigned seed, double *out);
 /* x[0..count) = N(0,1) numbers from a counter-based generator on the device (seeded; NOT the
  * reference's mt19937 sequence -- for synthetic workloads and measurements). */
 int eig_fill_normal(eig_ctx_t ctx, int64_t count, unsigned seed, double *x);
