@@ -28,6 +28,8 @@
 #   pipe                 fused vs pipelined on one rank's slab and the cube   -> pipe.jsonl
 #   csr                  general (scrambled + RCM) 256^3 matrix: SpMV / Lanczos kernels  -> csr.jsonl
 #   csrpmc               the same under a kernel trace and FETCH_SIZE / WRITE_SIZE passes -> csrpmc/
+#   sltrace              one C2 StandardLargest solve under a kernel trace (per-iteration kernels) -> sl/
+#   smallortho           orthonormalize_blocked m = 8 at n = 512 .. 4096: default look-ahead vs one workgroup
 #   commself             bench.py with and without a one-rank RCCL allreduce per step (eager / graph, 128^3 / 256^3)
 #   sweep                tools/lanczos_sweep.py $SWEEP (e.g. SWEEP="--N 256 --matrix p1k --variants fused,mv") -> sweep.jsonl
 #   sweeppmc             the same $SWEEP under a kernel trace, then FETCH_SIZE / WRITE_SIZE passes -> sweeppmc/
@@ -157,6 +159,12 @@ run_task() {
       done ;;
     csr)
       timeout -k 10 400 python -u tools/csr_general.py > "$O/csr.jsonl" 2> "$O/csr.err" ;;
+    sltrace)
+      prof_env
+      timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/sl" -o sl -- \
+        python3 -u tools/sl_trace.py > "$O/sl.log" 2>&1 ;;
+    smallortho)
+      timeout -k 10 200 python3 -u tools/small_ortho.py > "$O/small_ortho.jsonl" 2> "$O/small_ortho.err" ;;
     csrpmc)
       # the general-matrix kernels under a kernel trace and FETCH_SIZE / WRITE_SIZE passes
       prof_env
