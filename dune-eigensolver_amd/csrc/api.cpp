@@ -376,6 +376,7 @@ extern "C" int eig_ctx_sync(eig_ctx_t ctx)
   return guard(ctx, [&] {
     EIG_CHECK(ctx, EIG_ERR_ARG, "null context");
     EIG_HIP(hipStreamSynchronize(ctx->stream));
+    mgs_lookahead_check(ctx);  // (eig_orthonormalize_mv8 is asynchronous: its barrier error surfaces here)
   });
 }
 

@@ -127,6 +127,7 @@ extern "C" int eig_standard_largest(eig_mat_t A, double shift, double tol, int m
         for (i64 i = 0; i < n; ++i) evec_host[(i64)j * n + i] = h[((j / 8) * n + i) * 8 + j % 8];
     }
     EIG_HIP(hipStreamSynchronize(s));  // the look-ahead iteration uses this call's buffers
+    mgs_lookahead_check(ctx);          // a timed-out MGS barrier: EIG_ERR_HIP, never NaN with EIG_OK
     if (iters) *iters = kk;
   });
 }
@@ -244,6 +245,7 @@ extern "C" int eig_standard_inverse(eig_mat_t A, eig_lu_t lu, double shift, doub
     for (int j = 0; j < nev; ++j) eval_host[j] = s2[j];
     copy_evecs(ctx, Bk[basis], n, nev, evec_host);  // (stream order: after any queued iteration)
     EIG_HIP(hipStreamSynchronize(s));
+    mgs_lookahead_check(ctx);
     if (iters) *iters = kk;
   });
 }
@@ -1874,6 +1876,7 @@ extern "C" int eig_lanczos_tridiag(eig_lanczos_t ws, int *k, double *alpha_host,
     else
       launch_beta_tail(ws->lb->st, ws->k, ctx->stream);
     EIG_HIP(hipStreamSynchronize(ctx->stream));
+    check_step_exchange(*ws);  // the forced repair exchanged its sums in-kernel too: a timed-out peer -> EIG_ERR_RCCL
     if (k) *k = ws->k;
     if (alpha_host && ws->k > 0)
       EIG_HIP(hipMemcpy(alpha_host, ws->lb->st.alpha, ws->k * sizeof(double), hipMemcpyDeviceToHost));

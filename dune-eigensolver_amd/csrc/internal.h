@@ -153,6 +153,9 @@ struct eig_ctx_s {
   bool step_exchange() const { return collectives() && mbox && mbox->ready && mbox->on && mbox->step; }
   // reusable device buffers for drivers (grown on demand)
   std::vector<std::pair<void *, size_t>> pool;
+  // a look-ahead MGS last launch (grid barriers without a cooperative launch) has been enqueued
+  // since the last mgs_lookahead_check: its sticky error word must be read at the next sync point
+  bool mgs_la_armed = false;
 };
 
 namespace eigmi {
@@ -428,6 +431,9 @@ constexpr int kMgsLookaheadDefault = 8;
 int mgs_lookahead_default();  // EIGMI_MGS_LOOKAHEAD or kMgsLookaheadDefault
 bool launch_mgs_lookahead(eig_ctx_t ctx, i64 n, double *Qb, int L, bool coop, hipStream_t s);
 int mgs_lookahead_passes(eig_ctx_t ctx);  // read passes of the last call (-1: none finished)
+// After the stream is synchronised: throw EIG_ERR_HIP (and clear the sticky flag) when a look-ahead
+// MGS last launch since the previous check timed out in its grid barrier (its rows are NaN)
+void mgs_lookahead_check(eig_ctx_t ctx);
 // Whole column MGS of one 8-column block in one workgroup (n <= 4096, one rank); false = not taken.
 bool launch_mgs_small(i64 n, double *Qb, hipStream_t s);
 // The 9 read-only MGS passes in one cooperative launch with grid barriers (k_mv8.hip k_mgs_coop; one

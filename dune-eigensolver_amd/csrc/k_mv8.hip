@@ -1104,10 +1104,7 @@ __global__ __launch_bounds__(kMgsLaThreads) void k_mgs_la(MgsLaArgs a)
   __shared__ MgsLaShared<L> sh;  // (one copy for the nine pass bodies)
   const unsigned word = a.launch == 0 ? 0u : a.st[a.launch & 1];
   if (a.launch == 0 && blockIdx.x == 0 && threadIdx.x == 0)
-  {
-    a.st[kMgsLaBar] = 0u;  // for the last launch of this call
-    a.st[kMgsLaErr] = 0u;
-  }
+    a.st[kMgsLaBar] = 0u;  // for the last launch of this call (st[kMgsLaErr] is sticky: the host clears it)
   if (word & kMgsLaWritten)
   {
     if (blockIdx.x == 0 && threadIdx.x == 0) a.st[(a.launch + 1) & 1] = word;
@@ -1255,7 +1252,11 @@ void mgs_la_enqueue(MgsLaArgs a, int G, bool coop, hipStream_t s)
 bool launch_mgs_lookahead(eig_ctx_t ctx, i64 n, double *Qb, int L, bool coop, hipStream_t s)
 {
   if (L <= 1 || n <= 0) return false;
-  char *buf = (char *)ctx_buffer(ctx, 11, 64 * sizeof(double) + 64 * sizeof(unsigned));
+  const size_t bytes = 64 * sizeof(double) + 64 * sizeof(unsigned);
+  const bool fresh = (int)ctx->pool.size() <= 11 || ctx->pool[11].second < bytes;
+  char *buf = (char *)ctx_buffer(ctx, 11, bytes);
+  if (fresh) EIG_HIP(hipMemsetAsync(buf, 0, bytes, s));  // (the sticky error word starts clear)
+  if (coop) ctx->mgs_la_armed = true;
   MgsLaArgs a{n, Qb, 0, reinterpret_cast<unsigned *>(buf + 64 * sizeof(double)), reinterpret_cast<double *>(buf),
               ctx->red.partials, ctx->red.ticket(0)};
   const int G = grid_for(n, kMgsLaThreads * 2, std::min(kMgsLaGrid, ctx->num_cu > 0 ? ctx->num_cu : kMgsLaGrid));
@@ -1275,6 +1276,23 @@ int mgs_lookahead_passes(eig_ctx_t ctx)
   EIG_HIP(hipStreamSynchronize(ctx->stream));
   if (w[kMgsLaErr]) return -2;
   return (w[kMgsLaLast] & kMgsLaWritten) ? (int)((w[kMgsLaLast] >> 8) & 255u) : -1;
+}
+
+void mgs_lookahead_check(eig_ctx_t ctx)
+{
+  if (!ctx->mgs_la_armed) return;
+  ctx->mgs_la_armed = false;
+  unsigned *err = reinterpret_cast<unsigned *>((char *)ctx_buffer(ctx, 11, 64 * sizeof(double) + 64 * sizeof(unsigned)) +
+                                               64 * sizeof(double)) + kMgsLaErr;
+  unsigned e = 0;
+  EIG_HIP(hipMemcpyAsync(&e, err, sizeof(e), hipMemcpyDeviceToHost, ctx->stream));
+  EIG_HIP(hipStreamSynchronize(ctx->stream));
+  if (!e) return;
+  EIG_HIP(hipMemsetAsync(err, 0, sizeof(unsigned), ctx->stream));
+  EIG_HIP(hipStreamSynchronize(ctx->stream));
+  EIG_CHECK(false, EIG_ERR_HIP,
+            "orthonormalize_blocked: a look-ahead MGS grid barrier timed out (workgroups not co-resident); "
+            "the block was poisoned with NaN");
 }
 
 // ---------------------------------------------------------------------------------------------

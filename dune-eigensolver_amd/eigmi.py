@@ -4,8 +4,11 @@ add on the reference side, plus thin host-side helpers for tests and the benchma
 The compute path is libeigmi.so (hand-written HIP for gfx950).  Loading fails loudly when the
 library is missing; there is no CPU fallback in this module.
 """
+import atexit
 import ctypes
+import itertools
 import os
+import weakref
 
 import numpy as np
 
@@ -226,6 +229,36 @@ def load():
 
 lib = load()
 
+# Every live handle, so that an interpreter exit releases them while the HIP runtime (and a
+# profiler's API hooks) are still up: Python's atexit handlers run before the C runtime's exit
+# handlers, whereas a module-global Context would otherwise be finalised in any order relative to
+# libamdhip64's own teardown (an exit-time SIGSEGV under rocprofv3 --kernel-trace, round 5).
+_LIVE = weakref.WeakValueDictionary()
+_SEQ = itertools.count()
+
+
+def _track(obj):
+    _LIVE[next(_SEQ)] = obj
+
+
+@atexit.register
+def release_all():
+    """Destroy every handle still alive: newest first, contexts last (eig_ctx_destroy after every
+    matrix / workspace / buffer of that context), then wait for the device."""
+    objs = [o for _, o in sorted(_LIVE.items(), key=lambda kv: kv[0], reverse=True)]
+    for o in objs:
+        if not isinstance(o, Context):
+            try:
+                (o.free if isinstance(o, DeviceArray) else o.close)()
+            except Exception:
+                pass
+    for o in objs:
+        if isinstance(o, Context):
+            try:
+                o.close()
+            except Exception:
+                pass
+
 
 def build_id():
     """Identity of the kernel sources the loaded library was built from: sha1 over csrc/ (the .hip
@@ -263,6 +296,7 @@ class Context:
         self.h = h
         self.device = device
         self.nranks, self.rank = 1, 0
+        _track(self)
 
     def check(self, rc):
         if rc != EIG_OK:
@@ -301,6 +335,19 @@ class Context:
         flags = (COMM_MAILBOX if mailbox else 0) | (COMM_ALWAYS if always else 0)
         self.check(lib.eig_comm_init_ex(self.h, nranks, rank, uid, flags))
         self.nranks, self.rank = nranks, rank
+
+    def comm_init_loopback(self, hub, rank, mailbox=False):
+        """Attach this context as virtual rank `rank` of a loopback hub (eig_comm_init_loopback; halo
+        and allreduce by device copies + a host barrier).  mailbox=True: also the in-process xGMI
+        mailbox between the virtual ranks (eig_comm_loopback_mailbox, a collective of all ranks)."""
+        self.check(lib.eig_comm_init_loopback(self.h, hub, rank))
+        if mailbox:
+            self.check(lib.eig_comm_loopback_mailbox(self.h))
+        info = self.comm_info()
+        self.nranks, self.rank = info["nranks"], info["rank"]
+
+    def comm_loopback_mailbox(self):
+        self.check(lib.eig_comm_loopback_mailbox(self.h))
 
     def comm_counters(self):
         """Collectives the library has enqueued on its communicators (eig_comm_counters)."""
@@ -363,6 +410,7 @@ class DeviceArray:
         p = _vp()
         ctx.check(lib.eig_malloc(ctx.h, max(self.n, 1) * 8, ctypes.byref(p)))
         self.ptr = p
+        _track(self)
 
     def offset(self, k):
         """Raw pointer to element k (for window / owned-slice addressing)."""
@@ -396,6 +444,7 @@ class Matrix:
 
     def __init__(self, ctx, handle):
         self.ctx, self.h = ctx, handle
+        _track(self)
         self.info  # noqa: B018  (validates the handle)
 
     @property
@@ -632,6 +681,7 @@ class LanczosWorkspace:
         A.ctx.check(lib.eig_lanczos_create_ex(A.h, max_steps, u0.ptr if u0 is not None else None, seed,
                                               _lflags(fused, pipelined), ctypes.byref(h)))
         self.h = h
+        _track(self)
         self.variant, self.kernel, self.kernel_bytes = self.ws_info()
         self.fused = self.variant in ("fused", "pipelined")
         self.pipelined = self.variant == "pipelined"
@@ -714,6 +764,7 @@ class LU:
 
     def __init__(self, ctx, handle):
         self.ctx, self.h = ctx, handle
+        _track(self)
 
     @classmethod
     def from_factors(cls, ctx, Lp, Lj, Lx, Up, Ui, Ux, P, Q, Rs, do_recip=0):
@@ -862,6 +913,7 @@ class Multigrid:
         A.ctx.check(lib.eig_mg_create(A.h, dims[0], dims[1], dims[2], max_cols, smooth_degree, smooth_ratio,
                                       ctypes.byref(h)))
         self.h = h
+        _track(self)
 
     def info(self):
         lv, cr, cd, lm = _int(0), _i64(0), _int(0), _dbl(0)
@@ -907,6 +959,7 @@ class BlockLanczos:
             K.ctx.check(lib.eig_blanczos_create_si(K.h, M.h, Ks.h, sigma, block, max_steps, degree, lmin, lmax, seed,
                                                    ctypes.byref(h)))
         self.h = h
+        _track(self)
 
     def step(self, steps):
         t = BlockTiming()
@@ -939,6 +992,21 @@ class BlockLanczos:
             self.close()
         except Exception:
             pass
+
+
+# --------------------------------------------------------------------------------------- loopback
+def loopback_create(nranks):
+    """eig_loopback_create: a hub for `nranks` virtual ranks on one device (one host thread and one
+    Context per rank; ctypes releases the GIL, so the ranks' calls run concurrently)."""
+    h = _vp()
+    rc = lib.eig_loopback_create(int(nranks), ctypes.byref(h))
+    if rc != EIG_OK:
+        raise EigError(rc, lib.eig_last_error(None).decode())
+    return h
+
+
+def loopback_destroy(hub):
+    lib.eig_loopback_destroy(hub)
 
 
 # --------------------------------------------------------------------------------------- generators

@@ -98,8 +98,9 @@ int eig_comm_barrier(eig_ctx_t ctx);
 #define EIG_IPC_HANDLE_BYTES 64
 /* EIG_AR_MAILBOX_STEP: the mailbox for every allreduce, and the fused Lanczos step
  * (EIG_LANCZOS_FUSED) exchanges its three sums INSIDE the step kernel: the last workgroup of launch L
- * stores them into every peer's mailbox, launch L + 1's prologue polls its own mailbox (bounded: a
- * peer that does not arrive within 2 s makes the sums NaN on every rank and the step call returns
+ * stores them into every peer's mailbox and, before launch L ends, polls its own mailbox until every
+ * peer's sums of launch L have arrived (bounded: a peer that does not arrive within 2 s makes the
+ * sums NaN on every rank and the step call -- or eig_lanczos_tridiag's final repair launch -- returns
  * EIG_ERR_RCCL) -- no allreduce launch between two steps. */
 enum eig_allreduce_kind { EIG_AR_NONE = 0, EIG_AR_RCCL = 1, EIG_AR_MAILBOX = 2, EIG_AR_LOOPBACK = 3,
                           EIG_AR_MAILBOX_STEP = 4 };
@@ -327,6 +328,9 @@ enum { EIG_ORTHO_NO_COOP = 0x200 };
  * 0: the library default (8, or EIGMI_MGS_LOOKAHEAD). */
 #define EIG_ORTHO_LOOKAHEAD_SHIFT 12
 #define EIG_ORTHO_LOOKAHEAD(L) ((L) << EIG_ORTHO_LOOKAHEAD_SHIFT)
+/* Asynchronous like every kernel op.  The look-ahead MGS's last launch synchronises its workgroups
+ * with grid barriers (bounded wait): if they are not co-resident in time the block is set to NaN and
+ * the next eig_ctx_sync (or the driver that called it) returns EIG_ERR_HIP. */
 int eig_orthonormalize_mv8(eig_ctx_t ctx, int64_t n, int64_t m, double *Q, int variant);
 /* Diagnostics: read passes the last look-ahead MGS on ctx took for its last diagonal block (-1
  * when none ran).  Synchronises the context stream. */

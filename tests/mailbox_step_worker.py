@@ -11,6 +11,8 @@ MODE "run": the recurrence under "mailbox" (one allreduce launch per step) and "
 (eager batches and a hipGraph replay, then the exact final beta), saved to r<RANK>.npz.
 MODE "stall": rank 0 steps while rank 1 never does (it waits for rank 0's "done" file): rank 0's
 in-kernel exchange must time out and the step call return EIG_ERR_RCCL, without a hang.
+MODE "stall_tridiag": both ranks step, then only rank 0 calls tridiag(): the forced final repair's
+exchange times out and tridiag() returns EIG_ERR_RCCL (not a NaN beta with EIG_OK).
 """
 import os
 import sys
@@ -101,6 +103,27 @@ def main(rank, P, wd, mode):
             wait_for([os.path.join(wd, "done")], timeout=200.0)
         np.savez(os.path.join(wd, f"r{rank}.npz"), **out)
         # (no close of ws / M: rank 0's poisoned exchange has nothing left to run; the process ends)
+        return
+    if mode == "stall_tridiag":
+        # both ranks take 5 steps together; then only rank 0 asks for T: its forced final repair
+        # launch exchanges the sums in-kernel with a peer that never launches it
+        ctx.select_allreduce("mailbox-step")
+        ws = eigmi.LanczosWorkspace(M, 40, seed=123, fused=True)
+        ws.step(5)
+        if rank == 0:
+            t0 = time.perf_counter()
+            try:
+                ws.tridiag()
+                out["code"] = 0
+            except eigmi.EigError as e:
+                out["code"] = e.code
+                out["msg"] = str(e)
+            out["seconds"] = time.perf_counter() - t0
+            out["errors"] = ctx.comm_info()["mailbox_errors"]
+            publish(wd, "done")
+        else:
+            wait_for([os.path.join(wd, "done")], timeout=200.0)
+        np.savez(os.path.join(wd, f"r{rank}.npz"), **out)
         return
     for tr in ("mailbox", "mailbox-step"):
         ctx.select_allreduce(tr)

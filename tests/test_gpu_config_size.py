@@ -127,15 +127,17 @@ def test_dot_diag_128cubed(ctx):
 @pytest.mark.parametrize("N", [128, 256])
 def test_poisson_eigenpairs_config_size(ctx, N):
     """Configs C2 (128^3) and C4 (256^3, the benchmark's matrix) at their size, eigenpairs of a
-    converged run (the reference's ARPACK path, arpack_geneo_wrapper.hh:621-632, returns eigenpairs;
-    SURVEY 8(c) F7): the 4 smallest eigenpairs
-    of the 3-D Poisson N^3 matrix by block Lanczos (k = 32, 8 block steps) on A^-1 with the A solve by
-    multigrid to a residual <= 1e-13, against the analytic spectrum of the 7-point Laplacian,
-    4 sum_d sin^2(k_d pi / (2 (N + 1))): (1,1,1) and the triple (2,1,1), relative 1e-12 (asked: 1e-10);
-    the Ritz vectors against the analytic modes prod_d sin(k_d x_d pi / (N + 1)): the (1,1,1) vector
-    parallel to its mode (1 - |cos| <= 1e-12), the three (2,1,1) vectors inside the span of their three
-    modes (distance <= 1e-3 of ||y||: the angle is residual / gap to the (2,2,1) triple); and each
-    vector's residual ||A y - lambda y|| (oracle row loop on the host) <= 1e-4 lambda ||y||."""
+    CONVERGED run (the reference's ARPACK path runs to tol 1e-14: src/dune-eigensolver.cc:565,
+    arpack_geneo_wrapper.hh:621-632): the 4 smallest eigenpairs of the 3-D Poisson N^3
+    matrix by block Lanczos (k = 32, full CGS2 re-orthogonalisation) on A^-1 with the A solve by
+    multigrid to a residual <= 1e-13, block steps added until every device residual
+    ||A y - lambda y|| <= 1e-10 lambda ||y|| (the truncation error of the inverse iteration is
+    amplified by ||A|| / lambda_1 ~ 2.7e4 at 256^3: 8 block steps left 3e-5, ~16 are needed).
+    Against the analytic spectrum of the 7-point Laplacian 4 sum_d sin^2(k_d pi / (2 (N + 1))): the
+    (1,1,1) value and the (2,1,1) triple, relative 1e-12; the Ritz vectors against the analytic modes
+    prod_d sin(k_d x_d pi / (N + 1)): (1,1,1) parallel to its mode (1 - |cos| <= 1e-14), the three
+    (2,1,1) vectors inside the span of their three modes (distance <= 1e-8 of ||y||); each residual
+    recomputed on the host with the restated row loop (oracle.csr_mv) <= 1e-9 lambda ||y||."""
     n = N ** 3
     rp, c, v = eigmi.gen_matrix(eigmi.GEN_POISSON3D, N)
     K = eigmi.Matrix.from_bcsr(ctx, rp, c, v)
@@ -151,8 +153,18 @@ def test_poisson_eigenpairs_config_size(ctx, N):
             break
     B.free(), X.free()
     assert cycles is not None, "multigrid did not reach 1e-13"
-    bl = eigmi.BlockLanczos(K, Id, block=32, max_steps=8, Ks=K, sigma=0.0, mg=mg, cycles=cycles, seed=123)
-    bl.step(8)
+    max_steps = 20
+    bl = eigmi.BlockLanczos(K, Id, block=32, max_steps=max_steps, Ks=K, sigma=0.0, mg=mg, cycles=cycles, seed=123)
+    taken = 8
+    bl.step(taken)
+    history = []
+    while True:
+        ev, _, res = bl.ritz(4, eigmi.WHICH_SA, want_evec=False)
+        history.append((taken, float(np.max(res / ev))))
+        if history[-1][1] <= 1e-10 or taken >= max_steps:
+            break
+        bl.step(2)
+        taken += 2
     ev, Y, res = bl.ritz(4, eigmi.WHICH_SA, want_evec=True)
     s = 4 * np.sin(np.arange(1, 6) * np.pi / (2 * (N + 1))) ** 2
     lam = np.sort((s[:, None, None] + s[None, :, None] + s[None, None, :]).ravel())[:4]
@@ -168,11 +180,12 @@ def test_poisson_eigenpairs_config_size(ctx, N):
     T = np.stack([mode(2, 1, 1), mode(1, 2, 1), mode(1, 1, 2)])
     T /= np.linalg.norm(T, axis=1)[:, None]  # orthogonal modes
     dist = [np.linalg.norm(y - T.T @ (T @ y)) / np.linalg.norm(y) for y in Y[1:]]
-    print(f"Poisson {N}^3 smallest eigenpairs ({cycles} MG cycles): rel err {rel}, residuals {rres}, ritz res {res}, "
-          f"1-|cos| (1,1,1) {1 - cos:.2e}, distance to the (2,1,1) span {dist}")
+    print(f"Poisson {N}^3 smallest eigenpairs ({cycles} MG cycles, {taken} block steps, device residual "
+          f"history {history}): rel err {rel}, host residuals {rres}, 1-|cos| (1,1,1) {1 - cos:.2e}, "
+          f"distance to the (2,1,1) span {dist}")
     assert rel.max() <= 1e-12
-    assert 1 - cos <= 1e-12 and max(dist) <= 1e-3
-    assert max(rres) <= 1e-4
+    assert max(rres) <= 1e-9
+    assert 1 - cos <= 1e-14 and max(dist) <= 1e-8
     bl.close()
     mg.close()
     Id.close()

@@ -132,3 +132,14 @@ def test_step_exchange_peer_never_arrives(tmp_path):
     print(f"stalled peer: code {int(d['code'])} after {float(d['seconds']):.2f} s ({d['msg'] if 'msg' in d else ''})")
     assert int(d["code"]) == eigmi.EIG_ERR_RCCL
     assert float(d["seconds"]) < 60.0 and int(d["errors"]) == 1
+
+
+def test_step_exchange_peer_never_arrives_in_tridiag(tmp_path):
+    """eig_lanczos_tridiag's forced final repair launch exchanges its sums in-kernel; a peer
+    that never launches it must make the call return EIG_ERR_RCCL after the bounded poll."""
+    res = _spawn(2, str(tmp_path), "stall_tridiag")
+    d = res[0]
+    print(f"stalled peer in tridiag: code {int(d['code'])} after {float(d['seconds']):.2f} s "
+          f"({d['msg'] if 'msg' in d else ''})")
+    assert int(d["code"]) == eigmi.EIG_ERR_RCCL
+    assert float(d["seconds"]) < 60.0 and int(d["errors"]) == 1
