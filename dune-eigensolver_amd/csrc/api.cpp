@@ -1704,6 +1704,18 @@ extern "C" int eig_nrm2(eig_ctx_t ctx, int64_t n, const double *x, double *resul
     launch_sqrt_inplace(result, 1, ctx->stream);
   });
 }
+extern "C" int eig_lanczos_update(eig_ctx_t ctx, int64_t n, const double *alpha, const double *beta,
+                                  const double *v, const double *vprev, double *w, double *result)
+{
+  return guard(ctx, [&] {
+    EIG_CHECK(ctx && alpha && v && w && result && n >= 0 && (!vprev || beta), EIG_ERR_ARG,
+              "eig_lanczos_update: bad argument");
+    DeviceGuard dg(ctx->device);
+    launch_lanczos_update_ext(n, alpha, beta, v, vprev, w, result, 0, ctx->stream, ctx->red);
+    allreduce_sum(ctx, result, 2, ctx->stream);  // ||w||^2 and v.w in ONE allreduce
+    launch_sqrt_inplace(result, 1, ctx->stream);
+  });
+}
 extern "C" int eig_axpy(eig_ctx_t ctx, int64_t n, double a, const double *x, double *y)
 {
   return guard(ctx, [&] {

@@ -399,6 +399,8 @@ void launch_beta_tail(const LanczosState &st, int j, hipStream_t s);
 // BLAS-1 (results to device memory).
 void launch_dot(i64 n, const double *x, const double *y, double *out, int ticket, hipStream_t s, ReduceWS red);
 void launch_nrm2sq(i64 n, const double *x, double *out, int ticket, hipStream_t s, ReduceWS red);
+void launch_lanczos_update_ext(i64 n, const double *alpha, const double *beta, const double *v, const double *p,
+                               double *w, double *out, int ticket, hipStream_t s, ReduceWS red);
 void launch_axpy(i64 n, double a, const double *x, double *y, hipStream_t s);
 void launch_axpy_dev(i64 n, const double *a, double scale, const double *x, double *y, hipStream_t s);
 void launch_scal(i64 n, double a, double *x, hipStream_t s);

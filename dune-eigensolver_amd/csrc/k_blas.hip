@@ -112,6 +112,42 @@ void launch_nrm2sq(i64 n, const double *x, double *out, int ticket, hipStream_t 
                      red.ticket(ticket));
 }
 
+// The external driver's Lanczos update in one pass (eig_lanczos_update; what ARPACK's dsaitr does
+// with the vector multMv returned, arpack_geneo_wrapper.hh:257-279):
+//   w_i <- (w_i - alpha v_i) - beta p_i;   out[0] = sum w_i^2,  out[1] = sum v_i w_i  (new w)
+// alpha / beta from device memory (beta / p absent: no third term).  Per lane in index order, then
+// the fixed grid tree of reduce_dev.h: deterministic.
+__global__ __launch_bounds__(kStreamThreads) void k_lanczos_update_ext(i64 n, const double *__restrict__ alpha,
+                                                                       const double *__restrict__ beta,
+                                                                       const double *__restrict__ v,
+                                                                       const double *__restrict__ p,
+                                                                       double *__restrict__ w, double *out,
+                                                                       double *partials, unsigned *ticket)
+{
+  __shared__ double tot[2];
+  const double a = alpha[0], b = p ? beta[0] : 0.0;
+  double s0 = 0.0, s1 = 0.0;
+  for (i64 i = (i64)blockIdx.x * kStreamThreads + threadIdx.x; i < n; i += (i64)gridDim.x * kStreamThreads)
+  {
+    const double vi = v[i];
+    double r = w[i] - a * vi;
+    if (p) r -= b * p[i];
+    w[i] = r;
+    s0 += r * r;
+    s1 += vi * r;
+  }
+  double t[2] = {s0, s1};
+  if (grid_sum<2, kStreamThreads>(t, partials, ticket, tot))
+    if (threadIdx.x < 2) out[threadIdx.x] = tot[threadIdx.x];
+}
+
+void launch_lanczos_update_ext(i64 n, const double *alpha, const double *beta, const double *v, const double *p,
+                               double *w, double *out, int ticket, hipStream_t s, ReduceWS red)
+{
+  hipLaunchKernelGGL(k_lanczos_update_ext, dim3(stream_grid(n, 4)), dim3(kStreamThreads), 0, s, n, alpha, beta, v, p,
+                     w, out, red.partials, red.ticket(ticket));
+}
+
 // y += a x   (a from the host, or a = scale * (*a_dev) from device memory)
 __global__ __launch_bounds__(kStreamThreads) void k_axpy(i64 n, double a, const double *a_dev, double scale,
                                                          const double *__restrict__ x, double *__restrict__ y)

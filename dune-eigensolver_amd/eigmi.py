@@ -152,6 +152,7 @@ SIGNATURES = {
     "eig_axpy": (_int, [_vp, _i64, _dbl, _vp, _vp]),
     "eig_scal": (_int, [_vp, _i64, _dbl, _vp]),
     "eig_copy": (_int, [_vp, _i64, _vp, _vp]),
+    "eig_lanczos_update": (_int, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp]),
     "eig_stream_copy_timed": (_int, [_vp, _i64, _vp, _vp, _int, _int, ctypes.POINTER(_dbl)]),
     "eig_spmm_mv8": (_int, [_vp, _i64, _vp, _vp]),
     "eig_dot_diag_mv8": (_int, [_vp, _i64, _i64, _vp, _vp, _vp]),
@@ -580,6 +581,13 @@ def axpy(ctx, n, a, x, y):
 
 def scal(ctx, n, a, x):
     ctx.check(lib.eig_scal(ctx.h, n, a, x.ptr))
+
+
+def lanczos_update(ctx, n, alpha, beta, v, vprev, w, result):
+    """eig_lanczos_update: w <- (w - alpha v) - beta vprev; result[0] = ||w||, result[1] = v.w (device
+    scalars alpha / beta / result are DeviceArrays; vprev None: no beta term)."""
+    ctx.check(lib.eig_lanczos_update(ctx.h, n, alpha.ptr, beta.ptr if beta is not None else None, v.ptr,
+                                     vprev.ptr if vprev is not None else None, w.ptr, result.ptr))
 
 
 def copy(ctx, n, x, y):

@@ -286,6 +286,15 @@ int eig_nrm2(eig_ctx_t ctx, int64_t n, const double *x, double *result);
 int eig_axpy(eig_ctx_t ctx, int64_t n, double a, const double *x, double *y);   /* y += a x */
 int eig_scal(eig_ctx_t ctx, int64_t n, double a, double *x);                    /* x *= a */
 int eig_copy(eig_ctx_t ctx, int64_t n, const double *x, double *y);
+/* The Lanczos update an external Krylov driver applies to the vector its operator callback returned
+ * (ARPACK's dsaitr after multMv, arpack_geneo_wrapper.hh:257-279; SURVEY 8(b) "BlockVector ops"),
+ * as ONE pass instead of axpy + axpy + nrm2 (+ dot):
+ *   w <- (w - alpha v) - beta vprev;   result[0] = ||w||_2,  result[1] = v . w   (of the new w)
+ * alpha, beta: device scalars (vprev == NULL: no beta term, beta may be NULL); result: 2 device
+ * doubles.  result[1] is the loss of orthogonality a DGKS test compares with eta ||w||.  With a
+ * communicator both sums are global (one allreduce of 2 values). */
+int eig_lanczos_update(eig_ctx_t ctx, int64_t n, const double *alpha, const double *beta, const double *v,
+                       const double *vprev, double *w, double *result);
 /* Measurement helper: `reps` launches of a 16-B-per-lane nontemporal stream copy y = x (n doubles;
  * 16 n bytes moved per launch) bracketed by HIP events; *avg_ms per launch.  The measured HBM peak
  * the bench's roofline fractions are also quoted against.  mode: bit 0 nontemporal

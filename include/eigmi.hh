@@ -103,6 +103,22 @@ class DeviceVector {
   std::size_t n_;
 };
 
+// ------------------------------------------------------------------- BlockVector operations
+// The update an ARPACK-style driver applies after multMv (eig_lanczos_update): w <- (w - alpha v) -
+// beta vprev in one pass; result[0] = ||w||, result[1] = v . w of the new w.  alpha / beta / result
+// are device scalars (result: 2 entries), e.g. alpha from eig_dot into device memory; vprev may be
+// null for the first step.
+inline void lanczos_update(const Context &ctx, const DeviceVector &alpha, const DeviceVector *beta,
+                           const DeviceVector &v, const DeviceVector *vprev, DeviceVector &w, DeviceVector &result)
+{
+  if (result.size() < 2) throw std::invalid_argument("lanczos_update: result needs 2 entries");
+  if (v.size() != w.size() || (vprev && vprev->size() != w.size()))
+    throw std::invalid_argument("lanczos_update: vector sizes differ");
+  check(eig_lanczos_update(ctx.get(), (int64_t)w.size(), alpha.data(), beta ? beta->data() : nullptr, v.data(),
+                           vprev ? vprev->data() : nullptr, w.data(), result.data()),
+        ctx.get());
+}
+
 // ------------------------------------------------------------------------------------ matrix
 class Matrix {
  public:

@@ -155,6 +155,55 @@ int main(int argc, char **argv)
       }
   EXPECT(std::memcmp(yb.data(), rb.data(), 300 * 8) == 0);
 
+  // 2b) an external Lanczos loop on device BlockVectors: w = A v (eig_mv), alpha = v.w (eig_dot), then
+  //     the fused update (eig_lanczos_update) and v <- w / beta -- against the same loop in host doubles
+  {
+    const std::size_t n = A.N();
+    const int steps = 20;
+    eigmi::DeviceVector dv(ctx, n), dp(ctx, n), dw(ctx, n), da(ctx, 1), db(ctx, 1), dr(ctx, 2);
+    std::vector<double> v(n), p(n, 0.0), w(n), hv(n);
+    double nv = 0.0;
+    for (auto &e : v) e = nd(g), nv += e * e;
+    for (auto &e : v) e /= std::sqrt(nv);
+    dv.upload(v.data(), n);
+    double beta = 0.0, worst = 0.0;
+    for (int k = 0; k < steps; ++k)
+    {
+      // host reference: w = A v, alpha = v.w, w = (w - alpha v) - beta p, beta' = ||w||
+      for (auto r = A.begin(); r != A.end(); ++r)
+      {
+        double s = 0.0;
+        for (auto c = r->begin(); c != r->end(); ++c) s += (double)(*c) * v[c.index()];
+        w[r.index()] = s;
+      }
+      double alpha = 0.0;
+      for (std::size_t i = 0; i < n; ++i) alpha += v[i] * w[i];
+      for (std::size_t i = 0; i < n; ++i) w[i] = (w[i] - alpha * v[i]) - (k ? beta * p[i] : 0.0);
+      double bn = 0.0;
+      for (double e : w) bn += e * e;
+      bn = std::sqrt(bn);
+      // device loop
+      dA.mv(dv, dw);
+      eigmi::check(eig_dot(ctx.get(), (int64_t)n, dv.data(), dw.data(), da.data()), ctx.get());
+      eigmi::lanczos_update(ctx, da, k ? &db : nullptr, dv, k ? &dp : nullptr, dw, dr);
+      double res[2], ga;
+      dr.download(res, 2);
+      da.download(&ga, 1);
+      worst = std::max({worst, std::fabs(ga - alpha) / std::fabs(alpha), std::fabs(res[0] - bn) / bn,
+                        std::fabs(res[1]) / bn});
+      // next: p <- v, v <- w / beta'
+      eigmi::check(eig_copy(ctx.get(), (int64_t)n, dv.data(), dp.data()), ctx.get());
+      eigmi::check(eig_copy(ctx.get(), (int64_t)n, dw.data(), dv.data()), ctx.get());
+      eigmi::check(eig_scal(ctx.get(), (int64_t)n, 1.0 / res[0], dv.data()), ctx.get());
+      db.upload(&res[0], 1);
+      p = v;
+      for (std::size_t i = 0; i < n; ++i) v[i] = w[i] * (1.0 / bn);
+      beta = bn;
+    }
+    std::printf("external Lanczos loop through eig_lanczos_update: %d steps, worst rel diff %.2e\n", steps, worst);
+    EXPECT(worst < 1e-10);
+  }
+
   // 3) ARPACK++ operator signature
   eigmi::ArpackOperator op(dA);
   EXPECT(op.nrows() == 4096 && op.ncols() == 4096);

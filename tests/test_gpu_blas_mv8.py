@@ -32,6 +32,29 @@ def test_blas1(ctx, n):
     assert np.array_equal(dz.get(), x * 3.0)
 
 
+@pytest.mark.parametrize("n", [0, 1, 7, 1000, 65537, 1 << 20])
+@pytest.mark.parametrize("three_term", [True, False])
+def test_lanczos_update(ctx, n, three_term):
+    """eig_lanczos_update (SURVEY 8(b) BlockVector ops): the ARPACK-style update of the vector the
+    operator callback returned (arpack_geneo_wrapper.hh:257-279), w <- (w - alpha v) - beta vprev,
+    BITWISE the same two roundings per entry as numpy's elementwise order; ||w|| and v.w of the new
+    w within the summation-order bound."""
+    rng = np.random.default_rng(100 + n)
+    v, p, w = rng.standard_normal(n), rng.standard_normal(n), rng.standard_normal(n)
+    alpha, beta = 0.37, -1.25
+    dv, dp, dw = ctx.array(v), ctx.array(p), ctx.array(w)
+    da, db, out = ctx.array([alpha]), ctx.array([beta]), ctx.zeros(2)
+    eigmi.lanczos_update(ctx, n, da, db if three_term else None, dv, dp if three_term else None, dw, out)
+    ref = w - alpha * v
+    if three_term:
+        ref = ref - beta * p
+    got = dw.get()
+    assert np.array_equal(got, ref)
+    nrm, vw = out.get(2)
+    assert abs(nrm - np.sqrt(ref @ ref)) <= 1e-13 * max(1.0, np.sqrt(ref @ ref))
+    assert abs(vw - v @ ref) <= 4 * max(n, 1) * 2.3e-16 * np.abs(v * ref).sum() + 1e-300
+
+
 def test_random_mv8_bitwise(ctx):
     n, m = 1000, 16
     Q = ctx.zeros(n * m)
