@@ -1822,7 +1822,16 @@ void gram_device(eig_ctx_t ctx, i64 n, i64 m1, i64 m2, const double *Q1, const d
 }
 
 
-void orthonormalize_device(eig_ctx_t ctx, i64 n, i64 m, double *Q, int variant)
+void spmm_dot_gram_device(const eig_mat_s &A, const double *X, double *Y, double *dp, double *gram)
+{
+  eig_ctx_t ctx = A.ctx;
+  if (launch_spmm_dot_gram_mv8(A, 8, X, Y, dp, gram, ctx->stream, ctx->red)) return;
+  // no fused kernel on this image: the product with its dots, then the panel Gram of the block
+  launch_spmm_dot_mv8(A, 8, X, Y, dp, ctx->stream, ctx->red);
+  gram_device(ctx, A.nb_rows, 8, 8, Y, Y, gram);
+}
+
+void orthonormalize_device(eig_ctx_t ctx, i64 n, i64 m, double *Q, int variant, const double *gram0)
 {
   const int flags = variant & (EIG_ORTHO_GRID | EIG_ORTHO_NO_COOP | EIG_ORTHO_ONE_WG);
   const int la = (variant >> EIG_ORTHO_LOOKAHEAD_SHIFT) & 15;  // EIG_ORTHO_LOOKAHEAD(L); 0: the default
@@ -1837,7 +1846,12 @@ void orthonormalize_device(eig_ctx_t ctx, i64 n, i64 m, double *Q, int variant)
   for (i64 bk = 0; bk < m; bk += 8)
   {
     double *Qb = Q + bk * n;
-    if (variant == EIG_ORTHO_MGS && !ctx->distributed() && (flags & EIG_ORTHO_ONE_WG) && !(flags & EIG_ORTHO_GRID) &&
+    if (bk == 0 && gram0 && variant == EIG_ORTHO_MGS && !ctx->distributed() && L == 8 &&
+        launch_mgs_lookahead_gram(ctx, n, Qb, gram0, s))
+    {
+      // (the block's first read pass replaced by the Gram the caller's product summed)
+    }
+    else if (variant == EIG_ORTHO_MGS && !ctx->distributed() && (flags & EIG_ORTHO_ONE_WG) && !(flags & EIG_ORTHO_GRID) &&
         launch_mgs_small(n, Qb, s))
     {
     }
@@ -1909,6 +1923,29 @@ extern "C" int eig_orthonormalize_mv8(eig_ctx_t ctx, int64_t n, int64_t m, doubl
     EIG_MV8_CHECK(m);
     DeviceGuard dg(ctx->device);
     orthonormalize_device(ctx, n, m, Q, variant);
+  });
+}
+
+extern "C" int eig_orthonormalize_gram_mv8(eig_ctx_t ctx, int64_t n, int64_t m, double *Q, const double *gram)
+{
+  return guard(ctx, [&] {
+    EIG_CHECK(ctx && Q && gram && n >= 0, EIG_ERR_ARG, "eig_orthonormalize_gram_mv8: bad argument");
+    EIG_MV8_CHECK(m);
+    DeviceGuard dg(ctx->device);
+    orthonormalize_device(ctx, n, m, Q, EIG_ORTHO_MGS, gram);
+  });
+}
+
+extern "C" int eig_spmm_dot_gram_mv8(eig_mat_t mat, int64_t m, const double *Qin, double *Qout, double *dp,
+                                     double *gram)
+{
+  return guard(mat ? mat->ctx : nullptr, [&] {
+    EIG_CHECK(mat && Qin && Qout && dp && gram, EIG_ERR_ARG, "eig_spmm_dot_gram_mv8: bad argument");
+    EIG_CHECK(m == 8, EIG_ERR_SHAPE, "eig_spmm_dot_gram_mv8: one 8-column block (m = 8)");
+    EIG_CHECK(mat->br == 1 && mat->bc == 1, EIG_ERR_BLOCKSIZE,
+              "matmul_sparse_tallskinny_blocked: only implemented for FieldMatrix<..,1,1>");
+    DeviceGuard dg(mat->ctx->device);
+    spmm_dot_gram_device(*mat, Qin, Qout, dp, gram);
   });
 }
 

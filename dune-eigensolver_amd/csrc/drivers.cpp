@@ -91,12 +91,33 @@ extern "C" int eig_standard_largest(eig_mat_t A, double shift, double tol, int m
     orthonormalize_device(ctx, n, m, B[0], EIG_ORTHO_MGS); // eigensolver.hh:69
     // :78 of iteration k recomputes A Q1, which iteration k - 1's :84 product already holds (same
     // matrix, same input, deterministic kernel: bitwise the same block), so
-    // only iteration 1 runs it
-    if (maxiter > 1) launch_spmm_mv8(*A, m, B[0], B[1], s);  // :78 (k = 1)
+    // only iteration 1 runs it.
+    // m = 8 (nev <= 8: configs C1 / C2): the product also sums its window Gram (launch_spmm_dot_gram_mv8),
+    // so the next iteration's MGS (:81) starts from it (launch_mgs_lookahead_gram) instead of reading
+    // the block once more for its first look-ahead pass.  The same MGS steps on the same block; only
+    // the Gram's summation order is the product's (eig_spmm_dot_gram_mv8 / eig_orthonormalize_gram_mv8
+    // are the exported pair, tests/test_gpu_drivers.py runs the reference loop with them).
+    DevBuf Gb(64 * 8), dscr(8 * 8);
+    const bool gram = m == 8 && mgs_lookahead_default() == 8;
+    if (maxiter > 1)  // :78 (k = 1)
+    {
+      if (gram)
+        spmm_dot_gram_device(*A, B[0], B[1], dscr.d(), Gb.d());
+      else
+        launch_spmm_mv8(*A, m, B[0], B[1], s);
+    }
     auto enqueue = [&](int k) {
       double *Q = B[k % 3], *P = B[(k + 1) % 3], *dp = hd.dev + (k & 1) * m;
-      orthonormalize_device(ctx, n, m, Q, EIG_ORTHO_MGS);  // :81
-      launch_spmm_dot_mv8(*A, m, Q, P, dp, s, ctx->red);   // :84-85, the dots straight to the host
+      if (gram)
+      {
+        orthonormalize_device(ctx, n, m, Q, EIG_ORTHO_MGS, Gb.d());  // :81
+        spmm_dot_gram_device(*A, Q, P, dp, Gb.d());                  // :84-85, dots to the host, Gram for :81
+      }
+      else
+      {
+        orthonormalize_device(ctx, n, m, Q, EIG_ORTHO_MGS);  // :81
+        launch_spmm_dot_mv8(*A, m, Q, P, dp, s, ctx->red);   // :84-85, the dots straight to the host
+      }
       EIG_HIP(hipEventRecord(ev[k & 1].e, s));
     };
     std::vector<double> s1(m, 0.0), s2(m, 0.0);

@@ -353,6 +353,14 @@ int box_cols(const eig_mat_s &A);  // columns per box-image workgroup (k_box_mv3
 bool launch_box_spmm(const eig_mat_s &A, i64 m, const double *X, double *Y, hipStream_t s);
 bool launch_box_spmm_dot(const eig_mat_s &A, i64 m, const double *X, double *Y, double *dp, ReduceWS red,
                          hipStream_t s);
+bool launch_box_spmm_dot_gram(const eig_mat_s &A, i64 m, const double *X, double *Y, double *dp, double *gram,
+                              ReduceWS red, hipStream_t s);
+bool launch_spmm_march_dot_gram(const eig_mat_s &A, i64 m, const double *X, double *Y, double *dp, double *gram,
+                                ReduceWS red, hipStream_t s);
+// StandardLargest's product: Y = A X, dp = diag(X^T Y) and (gram != null, m = 8) the window Gram of Y
+// for the next iteration's MGS; false when no fused kernel applies (then gram is not written).
+bool launch_spmm_dot_gram_mv8(const eig_mat_s &A, i64 m, const double *X, double *Y, double *dp, double *gram,
+                              hipStream_t s, ReduceWS red);
 bool launch_spmm_march_dot(const eig_mat_s &A, i64 m, const double *X, double *Y, double *dp, ReduceWS red,
                            hipStream_t s);
 // Xnew: x_{k+1} into a third buffer (nullptr: in place over Xold); Xold nullptr (with Xnew): x_{k-1} = 0
@@ -432,6 +440,9 @@ void launch_mgs_pass(i64 n, double *Qb, int k, double *S, int ticket, hipStream_
 constexpr int kMgsLookaheadDefault = 8;
 int mgs_lookahead_default();  // EIGMI_MGS_LOOKAHEAD or kMgsLookaheadDefault
 bool launch_mgs_lookahead(eig_ctx_t ctx, i64 n, double *Qb, int L, bool coop, hipStream_t s);
+// The look-ahead MGS of one 8-column block whose window Gram G (8 x 8 row-major, device) is already
+// known: the first read pass is replaced by G (k_mgs_la_gram), then the last launch as usual.
+bool launch_mgs_lookahead_gram(eig_ctx_t ctx, i64 n, double *Qb, const double *G, hipStream_t s);
 int mgs_lookahead_passes(eig_ctx_t ctx);  // read passes of the last call (-1: none finished)
 // After the stream is synchronised: throw EIG_ERR_HIP (and clear the sticky flag) when a look-ahead
 // MGS last launch since the previous check timed out in its grid barrier (its rows are NaN)
@@ -572,7 +583,12 @@ bool gen_eig(int n, const std::vector<double> &g, std::vector<std::complex<doubl
 void halo_exchange(const eig_mat_s &A, double *x, hipStream_t s, double *x2 = nullptr, int width = 1);
 void mv_device(eig_mat_s &A, double *x, double *y);
 void gram_device(eig_ctx_t ctx, i64 n, i64 m1, i64 m2, const double *Q1, const double *Q2, double *G);
-void orthonormalize_device(eig_ctx_t ctx, i64 n, i64 m, double *Q, int variant);
+// gram0 (or null): the window Gram of the first 8-column block, already summed by the caller's
+// product (eig_orthonormalize_gram_mv8; MGS look-ahead on one rank only, else ignored)
+void orthonormalize_device(eig_ctx_t ctx, i64 n, i64 m, double *Q, int variant, const double *gram0 = nullptr);
+// Y = A X (one 8-column block), dp = diag(X^T Y), gram = Y^T Y (8 x 8): fused into the product where a
+// kernel has the epilogue (launch_spmm_dot_gram_mv8), else product + panel Gram
+void spmm_dot_gram_device(const eig_mat_s &A, const double *X, double *Y, double *dp, double *gram);
 void b_orthonormalize_device(eig_mat_s &B, i64 m, double *Q, double *norm);
 // Host CSR copy of a single-rank matrix's device image (rows in ISTL order, padding dropped).
 void mat_download_bcsr(const eig_mat_s &A, std::vector<i64> &rowptr, std::vector<i32> &col, std::vector<double> &vals);

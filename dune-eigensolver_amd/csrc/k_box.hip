@@ -47,7 +47,8 @@ enum {
   kBoxChebFirstAdd = 5,
   kBoxResidCopy = 6,
   kBoxResidAcc = 7,
-  kBoxStoreDot = 8  // kBoxStore + the diagonal dots x_j . y_j of each column (row-class kernel only)
+  kBoxStoreDot = 8,  // kBoxStore + the diagonal dots x_j . y_j of each column (row-class kernel only)
+  kBoxStoreDotGram = 9  // kBoxStoreDot + the window Gram y_w . y_c of the 8 columns (m = 8; reduce_dev.h)
 };
 // kBoxStoreDot's reduction: dp[8 b + j] = sum_r X(r, 8b + j) Y(r, 8b + j), one deterministic grid sum
 // (workgroup partials in part, a ticket per column block) -- dot_products_diagonal_blocked fused into
@@ -56,6 +57,7 @@ struct BoxDot {
   double *dp = nullptr;
   double *part = nullptr;
   unsigned *tick = nullptr;
+  double *gram = nullptr;  // kBoxStoreDotGram: the 8 x 8 window Gram of Y (row-major, upper triangle)
 };
 constexpr int kBoxMaxNd = 15;  // offsets of the box-image kernel's LDS value tile (P1 Kuhn: 15, 7-point: 7)
 constexpr int kBoxClassMaxNd = 27;  // offsets of the row-class kernels (27: Galerkin coarse operators)
@@ -691,7 +693,7 @@ __global__ void k_boxc_gather(i64 n, int nd, const double *__restrict__ val, con
 
 
 template <int EPI, unsigned SHAPE>
-__global__ __launch_bounds__(kCThreads, 8) void k_boxc_mv8(BoxGeom g, i64 ld, const double *__restrict__ ctab,
+__global__ __launch_bounds__(kCThreads, EPI == kBoxStoreDotGram ? 4 : 8) void k_boxc_mv8(BoxGeom g, i64 ld, const double *__restrict__ ctab,
                                                         const unsigned *__restrict__ cmask,
                                                         const double *__restrict__ X, double *__restrict__ Y,
                                                         const double *__restrict__ Xold,
@@ -717,8 +719,10 @@ __global__ __launch_bounds__(kCThreads, 8) void k_boxc_mv8(BoxGeom g, i64 ld, co
   const int z0 = seg * g.nz / g.nseg, z1 = (seg + 1) * g.nz / g.nseg;
   constexpr bool first = EPI == kBoxChebFirst || EPI == kBoxChebFirstAdd;
   constexpr bool cheb = EPI == kBoxCheb || first || EPI == kBoxChebSecond;
-  constexpr bool plain = EPI == kBoxStore || EPI == kBoxStoreDot;  // Y = A X, separately rounded
+  constexpr bool plain = EPI == kBoxStore || EPI == kBoxStoreDot || EPI == kBoxStoreDotGram;  // Y = A X
+  constexpr bool dot = EPI == kBoxStoreDot || EPI == kBoxStoreDotGram;
   dv2b dsum = {0.0, 0.0};  // kBoxStoreDot: this thread's x . y over its rows, columns 2 cp, 2 cp + 1
+  double gacc[2][8] = {};  // kBoxStoreDotGram: this lane's share of the window Gram (reduce_dev.h)
   // X plane zz of the tile + halo (8 columns, 64-B rows) into ring slot zz mod 3 (kBoxChebFirst: X is
   // b, and the ring takes x_1 = (gamma / a_rr) b with the row's class diagonal, as k_cheb_init)
   dv2b pre[kCRounds];
@@ -847,7 +851,7 @@ __global__ __launch_bounds__(kCThreads, 8) void k_boxc_mv8(BoxGeom g, i64 ld, co
       if (plain)
       {
         __builtin_nontemporal_store(acc, Yb + r * 4 + cp);
-        if constexpr (EPI == kBoxStoreDot)
+        if constexpr (dot)
         {
           const dv2b xc = ring[s0][hrow][cp];  // the row's own X (plane z)
           dsum.x += xc.x * acc.x;
@@ -885,10 +889,23 @@ __global__ __launch_bounds__(kCThreads, 8) void k_boxc_mv8(BoxGeom g, i64 ld, co
         __builtin_nontemporal_store(dv2b{o0, o1}, Yb + r * 4 + cp);
       }
     }
+    if constexpr (EPI == kBoxStoreDotGram) quad_gram_add(gacc, own ? acc.x : 0.0, own ? acc.y : 0.0);  // (a quad = a row)
     __syncthreads();  // everyone is done with slot (z - 1) mod 3
     store(z + 2);
     bb = bn;
     xo = xn;
+  }
+  if constexpr (EPI == kBoxStoreDotGram)
+  {
+    // the 8 dots and the 64 Gram slots: workgroup sums (fixed order) into LDS, then the two-level
+    // deterministic grid sum (grid.y = 1: one column block)
+    __shared__ double gv[72], gt[72];
+    quad_gram_block<kCThreads>(gacc, dsum.x, dsum.y, reinterpret_cast<double *>(&ring[0][0][0]), gv);
+    if (grid_sum2<kCThreads>(gv, 72, bd.part, bd.part + (size_t)gridDim.x * 72, bd.tick, blockIdx.x, gridDim.x, gt))
+    {
+      if (tid < 64) bd.gram[tid] = gt[tid];
+      if (tid < 8) bd.dp[tid] = gt[64 + tid];
+    }
   }
   if constexpr (EPI == kBoxStoreDot)
   {
@@ -1110,7 +1127,8 @@ static bool launch_box(const eig_mat_s &A, i64 m, const double *X, double *Y, co
 {
   if (m <= 0 || m % 8 != 0 || !box_prepare(A)) return false;
   if (epi >= kBoxChebFirst && !A.box_ctab) return false;  // (row-class only)
-  if (epi == kBoxStoreDot && !A.box_ctab) return false;
+  if ((epi == kBoxStoreDot || epi == kBoxStoreDotGram) && !A.box_ctab) return false;
+  if (epi == kBoxStoreDotGram && m != 8) return false;
   if (A.box_ctab)
   {
     // row-class kernels: one launch, blockIdx.y = column block.  z runs of about 32 planes (a run
@@ -1137,6 +1155,8 @@ static bool launch_box(const eig_mat_s &A, i64 m, const double *X, double *Y, co
     const dim3 grid((unsigned)(g.ntx * g.nty * g.nseg), (unsigned)(m / 8));
     // kBoxStoreDot: one ticket and grid.x x 8 partials per column block
     if (epi == kBoxStoreDot && ((i64)grid.x * 8 * grid.y > (i64)kMaxRedBlocks * kMaxRedVals || grid.y > kNumTickets))
+      return false;
+    if (epi == kBoxStoreDotGram && ((i64)grid.x * 72 + 8 * 72 > (i64)kMaxRedBlocks * kMaxRedVals || grid.y != 1))
       return false;
     // the stencil's shape: compile-time kernels for the 7-point and the Kuhn 15-point stencils,
     // a runtime offset loop for any other
@@ -1170,6 +1190,9 @@ static bool launch_box(const eig_mat_s &A, i64 m, const double *X, double *Y, co
                            (const double *)nullptr, Bv, 0.0, 0.0, bd);
       else if (epi == kBoxStoreDot)
         hipLaunchKernelGGL((k_boxc_mv8<kBoxStoreDot, S>), grid, dim3(kCThreads), 0, s, g, A.window, ct, cm, X, Y,
+                           (const double *)nullptr, (const double *)nullptr, 0.0, 0.0, bd);
+      else if (epi == kBoxStoreDotGram)
+        hipLaunchKernelGGL((k_boxc_mv8<kBoxStoreDotGram, S>), grid, dim3(kCThreads), 0, s, g, A.window, ct, cm, X, Y,
                            (const double *)nullptr, (const double *)nullptr, 0.0, 0.0, bd);
       else
         hipLaunchKernelGGL((k_boxc_mv8<kBoxStore, S>), grid, dim3(kCThreads), 0, s, g, A.window, ct, cm, X, Y,
@@ -1278,6 +1301,21 @@ bool launch_box_spmm_dot(const eig_mat_s &A, i64 m, const double *X, double *Y, 
   bd.part = red.partials;
   bd.tick = red.ticket(0);
   return launch_box(A, m, X, Y, nullptr, nullptr, nullptr, 0.0, 0.0, kBoxStoreDot, s, bd);
+}
+
+// Y = A X, dp (8 dots) and gram (the 8 x 8 window Gram of Y) in one launch, m = 8: the row-class
+// kernel only (false otherwise).  Uses the reduction workspace's partials (grid.x x 72 + 8 x 72) and
+// ticket 0.
+bool launch_box_spmm_dot_gram(const eig_mat_s &A, i64 m, const double *X, double *Y, double *dp, double *gram,
+                              ReduceWS red, hipStream_t s)
+{
+  if (m != 8 || !box_prepare(A) || !A.box_ctab) return false;
+  BoxDot bd;
+  bd.dp = dp;
+  bd.part = red.partials;
+  bd.tick = red.ticket(0);
+  bd.gram = gram;
+  return launch_box(A, m, X, Y, nullptr, nullptr, nullptr, 0.0, 0.0, kBoxStoreDotGram, s, bd);
 }
 
 bool launch_box_resid(const eig_mat_s &A, i64 m, const double *X, const double *B, double *R, hipStream_t s)

@@ -107,6 +107,16 @@ void launch_spmm_dot_mv8(const eig_mat_s &A, i64 m, const double *X, double *Y, 
   launch_dot_diag_mv8(A.nb_rows, m, X, Y, dp, 0, s, red);
 }
 
+bool launch_spmm_dot_gram_mv8(const eig_mat_s &A, i64 m, const double *X, double *Y, double *dp, double *gram,
+                              hipStream_t s, ReduceWS red)
+{
+  static const bool off = std::getenv("EIGMI_NO_SPMM_GRAM") != nullptr;  // A/B: the separate MGS read pass
+  if (off || m != 8 || A.R != 1 || A.br != 1 || A.bc != 1 || A.ctx->distributed()) return false;
+  // the same kernel choice as launch_spmm_dot_mv8 (the row-class box kernel, else the band march)
+  if (launch_box_spmm_dot_gram(A, m, X, Y, dp, gram, red, s)) return true;
+  return !box_spmm_applies(A, m) && launch_spmm_march_dot_gram(A, m, X, Y, dp, gram, red, s);
+}
+
 // ---------------------------------------------------------------------------------------------
 // a5: dp[j] = q1_j . q2_j (dot_products_diagonal_blocked, kernels_cpp.hh:24-55).  grid.y = column
 // block; thread t always sees the column pair 2 (t%4) because the grid stride is a multiple of 4.
@@ -1207,6 +1217,30 @@ __global__ __launch_bounds__(kMgsLaThreads) void k_mgs_la_final(MgsLaArgs a)
   }
 }
 
+// The first read pass from a Gram computed elsewhere (StandardLargest: the SpMM that wrote the
+// block summed its window Gram in its epilogue, k_boxc_mv8 / k_spmm8_march GRAM): ONE workgroup
+// finishes the window from G (row-major 8 x 8, upper triangle used) exactly as the read pass's tail
+// does from its grid sums, and hands the state word to launch 1 (k_mgs_la_final).
+__global__ __launch_bounds__(kMgsLaThreads) void k_mgs_la_gram(MgsLaArgs a, const double *__restrict__ G)
+{
+  __shared__ MgsLaShared<8> sh;
+  if (threadIdx.x < 64)
+  {
+    const int w = threadIdx.x / 8, c = threadIdx.x % 8;
+    sh.Rw[w][c] = c >= w ? G[threadIdx.x] : 0.0;
+  }
+  __syncthreads();
+  if (threadIdx.x < 64)
+  {
+    const unsigned nw = mgs_la_close<0, 8, 8>(sh, a.Sfin, 0u);
+    if (threadIdx.x == 0)
+    {
+      a.st[kMgsLaBar] = 0u;  // for the last launch of this call
+      a.st[1] = nw;          // launch 1's word
+    }
+  }
+}
+
 int mgs_lookahead_default()
 {
   static const int L = [] {
@@ -1263,6 +1297,24 @@ bool launch_mgs_lookahead(eig_ctx_t ctx, i64 n, double *Qb, int L, bool coop, hi
   if (L >= 8) mgs_la_enqueue<8>(a, G, coop, s);
   else if (L >= 4) mgs_la_enqueue<4>(a, G, coop, s);
   else mgs_la_enqueue<2>(a, G, coop, s);
+  return true;
+}
+
+bool launch_mgs_lookahead_gram(eig_ctx_t ctx, i64 n, double *Qb, const double *G, hipStream_t s)
+{
+  if (n <= 0 || !G) return false;
+  const size_t bytes = 64 * sizeof(double) + 64 * sizeof(unsigned);
+  const bool fresh = (int)ctx->pool.size() <= 11 || ctx->pool[11].second < bytes;
+  char *buf = (char *)ctx_buffer(ctx, 11, bytes);
+  if (fresh) EIG_HIP(hipMemsetAsync(buf, 0, bytes, s));
+  ctx->mgs_la_armed = true;
+  MgsLaArgs a{n, Qb, 0, reinterpret_cast<unsigned *>(buf + 64 * sizeof(double)), reinterpret_cast<double *>(buf),
+              ctx->red.partials, ctx->red.ticket(0)};
+  const int G8 = grid_for(n, kMgsLaThreads * 2, std::min(kMgsLaGrid, ctx->num_cu > 0 ? ctx->num_cu : kMgsLaGrid));
+  hipLaunchKernelGGL(k_mgs_la_gram, dim3(1), dim3(kMgsLaThreads), 0, s, a, G);
+  a.launch = 1;
+  hipLaunchKernelGGL(k_mgs_la_final<8>, dim3(G8), dim3(kMgsLaThreads), 0, s, a);
+  EIG_HIP(hipGetLastError());
   return true;
 }
 

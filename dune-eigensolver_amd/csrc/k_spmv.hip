@@ -2151,11 +2151,14 @@ __device__ __forceinline__ double lane_from(double v, int src_lane)
 // DOT: also dp[8 qb + j] = X_j . Y_j over the rows (StandardLargest's :84-85 in one launch): each
 // lane adds its row's own operand x its result, one deterministic grid sum per column block
 // (partials part + grid.x * 8 qb, ticket tick + qb kTicketStride); Y is unchanged.
-template <class MT, bool DOT = false>
-__global__ __launch_bounds__(kStreamThreads, DOT ? 6 : 8) void k_spmm8_march(i64 nrows, i64 own, i64 ld, SellB1 A,
+// DOT = 2: also the window Gram of Y (one column block, m = 8: StandardLargest's next MGS starts from
+// it, k_mgs_la_gram) -- dots and Gram in one two-level grid sum (reduce_dev.h quad_gram_block).
+template <class MT, int DOT = 0>
+__global__ __launch_bounds__(kStreamThreads, DOT == 2 ? 5 : DOT ? 6 : 8) void k_spmm8_march(i64 nrows, i64 own, i64 ld, SellB1 A,
                                                                    MarchPlan mp, const double *__restrict__ X,
                                                                    double *__restrict__ Y, double *dp = nullptr,
-                                                                   double *part = nullptr, unsigned *tick = nullptr)
+                                                                   double *part = nullptr, unsigned *tick = nullptr,
+                                                                   double *gram = nullptr)
 {
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int qb = (int)blockIdx.y;  // column block
@@ -2175,6 +2178,7 @@ __global__ __launch_bounds__(kStreamThreads, DOT ? 6 : 8) void k_spmm8_march(i64
   const int z0 = (int)(mp.zb + seg * mp.nplanes / mp.nseg);
   const int z1 = live ? (int)(mp.zb + (seg + 1) * mp.nplanes / mp.nseg) : z0;
   dpair dsum{0.0, 0.0};
+  double gacc[2][8] = {};  // DOT == 2: this lane's share of the window Gram
   // column block qb, column pair cp: row g's operand at Xb[g]
   const dpair *Xb = reinterpret_cast<const dpair *>(X + (i64)qb * ld * 8) + cp;
   dpair *Yb = reinterpret_cast<dpair *>(Y + (i64)qb * ld * 8) + cp;
@@ -2248,11 +2252,22 @@ __global__ __launch_bounds__(kStreamThreads, DOT ? 6 : 8) void k_spmm8_march(i64
         dsum.y += pcur.y * acc.y;
       }
     }
+    if constexpr (DOT == 2) quad_gram_add(gacc, r < nrows ? acc.x : 0.0, r < nrows ? acc.y : 0.0);  // (a quad = a row)
     pm = pcur;
     pcur = pD;
     amD = aD;
   }
-  if constexpr (DOT)
+  if constexpr (DOT == 2)
+  {
+    __shared__ double gs[kStreamThreads / 64 * 72], gv[72], gt[72];
+    quad_gram_block<kStreamThreads>(gacc, dsum.x, dsum.y, gs, gv);
+    if (grid_sum2<kStreamThreads>(gv, 72, part, part + (size_t)gridDim.x * 72, tick, blockIdx.x, gridDim.x, gt))
+    {
+      if (threadIdx.x < 64) gram[threadIdx.x] = gt[threadIdx.x];
+      if (threadIdx.x < 8) dp[threadIdx.x] = gt[64 + threadIdx.x];
+    }
+  }
+  else if constexpr (DOT)
   {
     __shared__ double tot[8];
     double v[8];
@@ -3092,6 +3107,27 @@ bool launch_spmm_march_dot(const eig_mat_s &A, i64 m, const double *X, double *Y
   else
     hipLaunchKernelGGL((k_spmm8_march<uint32_t, true>), grid, dim3(kStreamThreads), 0, s, A.nb_rows, A.own_offset,
                        A.window, sell_b1(A), mp, X, Y, dp, red.partials, red.ticket(0));
+  return true;
+}
+
+// The same with the window Gram of Y (k_spmm8_march<MT, 2>), m = 8 only.
+bool launch_spmm_march_dot_gram(const eig_mat_s &A, i64 m, const double *X, double *Y, double *dp, double *gram,
+                                ReduceWS red, hipStream_t s)
+{
+  if (A.br != 1 || A.bc != 1 || m != 8 || A.ctx->distributed()) return false;
+  const int mode = image_mode(A);
+  if (!is_sym_mode(mode)) return false;
+  const MarchPlan mp = march_plan(A, mode, 0, -1, false, 16);
+  if (mp.nseg == 0) return false;
+  const i64 items = mp.ncol * (i64)mp.nseg;
+  const dim3 grid((unsigned)((items + kWaves - 1) / kWaves), 1u);
+  if ((i64)grid.x * 72 + 8 * 72 > (i64)kMaxRedBlocks * kMaxRedVals) return false;
+  if (mode == kSymN8)
+    hipLaunchKernelGGL((k_spmm8_march<uint8_t, 2>), grid, dim3(kStreamThreads), 0, s, A.nb_rows, A.own_offset,
+                       A.window, sell_b1(A), mp, X, Y, dp, red.partials, red.ticket(0), gram);
+  else
+    hipLaunchKernelGGL((k_spmm8_march<uint32_t, 2>), grid, dim3(kStreamThreads), 0, s, A.nb_rows, A.own_offset,
+                       A.window, sell_b1(A), mp, X, Y, dp, red.partials, red.ticket(0), gram);
   return true;
 }
 

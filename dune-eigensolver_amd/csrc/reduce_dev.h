@@ -201,4 +201,87 @@ __device__ bool grid_sum2(const double *vals, int E, double *part, double *spart
   return true;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Window Gram of an 8-column MultiVector block held in the SpMM kernels' quad layout: lanes
+// 4 r .. 4 r + 3 hold one row, lane cp = lane & 3 its columns 2 cp, 2 cp + 1 (k_spmm8_march,
+// k_boxc_mv8).  StandardLargest orthonormalises the block the SpMM writes (eigensolver.hh:78-84), and
+// the first read pass of that MGS needs exactly s[w][c] = y_w . y_c (c >= w): summed here while the
+// rows are in registers, so the MGS starts from it (k_mgs_la_gram) instead of re-reading the block.
+// ---------------------------------------------------------------------------------------------
+// DPP quad exchange: the value of lane (lane ^ D) of the same quad (D = 1, 2, 3)
+template <int D>
+__device__ __forceinline__ double quad_xor(double v)
+{
+  constexpr int ctrl = D == 1 ? 0xB1 : (D == 2 ? 0x4E : 0x1B);  // quad_perm [1,0,3,2] / [2,3,0,1] / [3,2,1,0]
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, ctrl, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), ctrl, 0xF, 0xF, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+// g[w2][2 d + c2] += y_{2 cp + w2} y_{2 (cp ^ d) + c2} for this lane's row (every lane of the wave
+// calls it: the quad exchange reads the other lanes; a row that does not exist passes zeros)
+__device__ __forceinline__ void quad_gram_add(double (&g)[2][8], double y0, double y1)
+{
+  const double p[4][2] = {{y0, y1},
+                          {quad_xor<1>(y0), quad_xor<1>(y1)},
+                          {quad_xor<2>(y0), quad_xor<2>(y1)},
+                          {quad_xor<3>(y0), quad_xor<3>(y1)}};
+#pragma unroll
+  for (int d = 0; d < 4; ++d)
+#pragma unroll
+    for (int c2 = 0; c2 < 2; ++c2)
+    {
+      g[0][2 * d + c2] += y0 * p[d][c2];
+      g[1][2 * d + c2] += y1 * p[d][c2];
+    }
+}
+
+// Workgroup sums of the quad-layout Gram g and the column dots (d0, d1) of this lane's pair, into
+// out[72] (LDS, visible to all threads on return): out[8 w + c] = sum y_w y_c for c >= w (0 below the
+// diagonal), out[64 + j] = the dot of column j.  Lanes of one column pair are summed by xor shuffles
+// over lane bits 2..5, the waves' totals in wave order: a fixed order.  scratch: NT / 64 x 72
+// doubles of LDS.  Every thread calls it.
+template <int NT>
+__device__ __forceinline__ void quad_gram_block(double (&g)[2][8], double d0, double d1, double *scratch,
+                                                double *out)
+{
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, cp = lane & 3;
+  double v[18];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) v[i] = g[i / 8][i % 8];
+  v[16] = d0;
+  v[17] = d1;
+#pragma unroll
+  for (int m = 4; m < 64; m <<= 1)
+#pragma unroll
+    for (int i = 0; i < 18; ++i) v[i] += __shfl_xor(v[i], m, 64);
+  __syncthreads();  // (scratch may alias storage the caller used before)
+  if (lane < 4)
+  {
+    double *ws = scratch + wave * 72;
+#pragma unroll
+    for (int w2 = 0; w2 < 2; ++w2)
+#pragma unroll
+      for (int d = 0; d < 4; ++d)
+#pragma unroll
+        for (int c2 = 0; c2 < 2; ++c2)
+        {
+          const int w = 2 * cp + w2, c = 2 * (cp ^ d) + c2;
+          ws[w * 8 + c] = c >= w ? v[w2 * 8 + 2 * d + c2] : 0.0;
+        }
+    ws[64 + 2 * cp] = v[16];
+    ws[64 + 2 * cp + 1] = v[17];
+  }
+  __syncthreads();
+  if (threadIdx.x < 72)
+  {
+    double t = 0.0;
+#pragma unroll
+    for (int q = 0; q < NT / 64; ++q) t += scratch[q * 72 + threadIdx.x];
+    out[threadIdx.x] = t;
+  }
+  __syncthreads();
+}
+
 }  // namespace eigmi

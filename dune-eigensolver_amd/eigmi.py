@@ -153,6 +153,8 @@ SIGNATURES = {
     "eig_scal": (_int, [_vp, _i64, _dbl, _vp]),
     "eig_copy": (_int, [_vp, _i64, _vp, _vp]),
     "eig_lanczos_update": (_int, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "eig_spmm_dot_gram_mv8": (_int, [_vp, _i64, _vp, _vp, _vp, _vp]),
+    "eig_orthonormalize_gram_mv8": (_int, [_vp, _i64, _i64, _vp, _vp]),
     "eig_stream_copy_timed": (_int, [_vp, _i64, _vp, _vp, _int, _int, ctypes.POINTER(_dbl)]),
     "eig_spmm_mv8": (_int, [_vp, _i64, _vp, _vp]),
     "eig_dot_diag_mv8": (_int, [_vp, _i64, _i64, _vp, _vp, _vp]),
@@ -620,6 +622,16 @@ def gram_mv8(ctx, n, m1, m2, Q1, Q2, G):
 
 def orthonormalize_mv8(ctx, n, m, Q, variant=ORTHO_MGS):
     ctx.check(lib.eig_orthonormalize_mv8(ctx.h, n, m, Q.ptr, variant))
+
+
+def spmm_dot_gram_mv8(A, m, Qin, Qout, dp, gram):
+    """eig_spmm_dot_gram_mv8: Qout = A Qin, dp = diag(Qin^T Qout), gram = Qout's 8 x 8 window Gram (m = 8)."""
+    A.ctx.check(lib.eig_spmm_dot_gram_mv8(A.h, m, Qin.ptr, Qout.ptr, dp.ptr, gram.ptr))
+
+
+def orthonormalize_gram_mv8(ctx, n, m, Q, gram):
+    """eig_orthonormalize_gram_mv8: MGS orthonormalize_blocked whose first block starts from `gram`."""
+    ctx.check(lib.eig_orthonormalize_gram_mv8(ctx.h, n, m, Q.ptr, gram.ptr))
 
 
 def orthonormalize_passes(ctx):

@@ -337,6 +337,15 @@ enum { EIG_ORTHO_NO_COOP = 0x200 };
  * 0: the library default (8, or EIGMI_MGS_LOOKAHEAD). */
 #define EIG_ORTHO_LOOKAHEAD_SHIFT 12
 #define EIG_ORTHO_LOOKAHEAD(L) ((L) << EIG_ORTHO_LOOKAHEAD_SHIFT)
+/* StandardLargest's fused pair (eigensolver.hh:78-85 with the product reused),
+ * exported so a caller's loop can run exactly what eig_standard_largest runs:
+ *   eig_spmm_dot_gram_mv8: Qout = A Qin (m = 8), dp[j] = qin_j . qout_j (8 device doubles) and
+ *     gram[8 w + c] = qout_w . qout_c (8 x 8 device doubles, c >= w used) -- summed in the product's
+ *     epilogue while the rows are in registers (else a separate panel Gram);
+ *   eig_orthonormalize_gram_mv8: eig_orthonormalize_mv8 (MGS) whose first block starts from that Gram
+ *     instead of reading the block for its first look-ahead pass. */
+int eig_spmm_dot_gram_mv8(eig_mat_t mat, int64_t m, const double *Qin, double *Qout, double *dp, double *gram);
+int eig_orthonormalize_gram_mv8(eig_ctx_t ctx, int64_t n, int64_t m, double *Q, const double *gram);
 /* Asynchronous like every kernel op.  The look-ahead MGS's last launch synchronises its workgroups
  * with grid barriers (bounded wait): if they are not co-resident in time the block is set to NaN and
  * the next eig_ctx_sync (or the driver that called it) returns EIG_ERR_HIP. */

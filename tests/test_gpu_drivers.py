@@ -264,6 +264,22 @@ def test_full_size_lanczos_fused_matches_oracle(ctx, p256):
     assert np.allclose(fa, ca, rtol=1e-11) and np.allclose(fb, cb, rtol=1e-11)
 
 
+def reference_iteration(ctx, M, n, m, Q1, Q2, dp, G, scratch):
+    """One pass of the reference's loop body (eigensolver.hh:78-85: Q2 = A Q1, orthonormalize Q2,
+    Q1 = A Q2, dp = diag(Q2^T Q1)) with the primitives the driver uses: at m = 8 the product that
+    also sums the window Gram of its block and the MGS that starts from it (eig_spmm_dot_gram_mv8 /
+    eig_orthonormalize_gram_mv8), else the plain ones."""
+    if m == 8:
+        eigmi.spmm_dot_gram_mv8(M, m, Q1, Q2, scratch, G)
+        eigmi.orthonormalize_gram_mv8(ctx, n, m, Q2, G)
+        eigmi.spmm_dot_gram_mv8(M, m, Q2, Q1, dp, G)
+    else:
+        eigmi.spmm_mv8(M, m, Q1, Q2)
+        eigmi.orthonormalize_mv8(ctx, n, m, Q2)
+        eigmi.spmm_mv8(M, m, Q2, Q1)
+        eigmi.dot_diag_mv8(ctx, n, m, Q2, Q1, dp)
+
+
 @pytest.mark.parametrize("make,nev,shift", [(lambda: oracle.laplace2d(48), 8, 0.0),
                                             (lambda: oracle.poisson3d(20), 12, 0.25)])
 def test_standard_largest_reuses_product_bitwise(ctx, make, nev, shift):
@@ -279,6 +295,7 @@ def test_standard_largest_reuses_product_bitwise(ctx, make, nev, shift):
     ev, evec, it = eigmi.standard_largest(M, shift, 0.0, maxiter, nev, 5)
     # the reference's loop (eigensolver.hh:69-103), primitive by primitive
     Q1, Q2, dp = ctx.zeros(n * m), ctx.zeros(n * m), ctx.zeros(m)
+    G, scr = ctx.zeros(64), ctx.zeros(8)
     eigmi.random_mv8(ctx, n, m, 5, Q1)
     M = upload(ctx, A)  # a fresh copy: the driver shifted its matrix in place (eigensolver.hh:59-66)
     if shift != 0.0:
@@ -286,10 +303,7 @@ def test_standard_largest_reuses_product_bitwise(ctx, make, nev, shift):
     eigmi.orthonormalize_mv8(ctx, n, m, Q1)
     s2 = np.zeros(m)
     for k in range(1, maxiter):
-        eigmi.spmm_mv8(M, m, Q1, Q2)
-        eigmi.orthonormalize_mv8(ctx, n, m, Q2)
-        eigmi.spmm_mv8(M, m, Q2, Q1)
-        eigmi.dot_diag_mv8(ctx, n, m, Q2, Q1, dp)
+        reference_iteration(ctx, M, n, m, Q1, Q2, dp, G, scr)
         s2 = dp.get() - shift
         Q1, Q2 = Q2, Q1
     q = Q1.get().reshape(m // 8, n, 8)
@@ -312,16 +326,14 @@ def test_standard_largest_lookahead_stop(ctx, maxiter, tol):
     n = M.n
     ev, evec, it = eigmi.standard_largest(M, shift, tol, maxiter, nev, 11)
     Q1, Q2, dp = ctx.zeros(n * m), ctx.zeros(n * m), ctx.zeros(m)
+    G, scr = ctx.zeros(64), ctx.zeros(8)
     eigmi.random_mv8(ctx, n, m, 11, Q1)
     eigmi.orthonormalize_mv8(ctx, n, m, Q1)
     s2 = np.zeros(m)
     kk = 1
     for k in range(1, maxiter):
         kk = k
-        eigmi.spmm_mv8(M, m, Q1, Q2)
-        eigmi.orthonormalize_mv8(ctx, n, m, Q2)
-        eigmi.spmm_mv8(M, m, Q2, Q1)
-        eigmi.dot_diag_mv8(ctx, n, m, Q2, Q1, dp)
+        reference_iteration(ctx, M, n, m, Q1, Q2, dp, G, scr)
         s1 = dp.get() - shift
         dist = np.abs(s1 - s2).max()
         s2 = s1
