@@ -148,6 +148,7 @@ void mailbox_prepare(eig_ctx_t ctx, int nranks, int rank, unsigned char handle[H
     EIG_HIP(hipExtMallocWithFlags(&p, bytes, hipDeviceMallocFinegrained));
   }
   m->local = static_cast<u64 *>(p);
+  m->bytes = bytes;
   EIG_HIP(hipMemset(m->local, 0, bytes));
   EIG_HIP(hipMalloc(&m->state, 256));
   EIG_HIP(hipMemset(m->state, 0, 256));
@@ -535,12 +536,36 @@ extern "C" int eig_comm_select_allreduce(eig_ctx_t ctx, int kind)
     if (ctx->mbox)
     {
       DeviceGuard dg(ctx->device);
+      MailboxHost *m = ctx->mbox;
       EIG_HIP(hipStreamSynchronize(ctx->stream));
-      ctx->mbox->on = kind != EIG_AR_RCCL;
-      ctx->mbox->step = kind == EIG_AR_MAILBOX_STEP;
-      // a new selection starts without a recorded timeout (a poisoned step exchange stays poisoned
-      // until then: xch_dev.h)
-      EIG_HIP(hipMemset(ctx->mbox->dev.err, 0, sizeof(int)));
+      if (ctx->comm || ctx->loop)
+      {
+        // a new selection restarts the mailbox on every rank: after a timed-out call the
+        // ranks' sequence words disagree (a lagging rank could match a peer's OLD publication), so
+        // with the ranks quiet (barrier over RCCL / the loopback hub), each zeroes its mailbox, its
+        // call counters and its error word, and a second barrier keeps any rank from publishing
+        // into a mailbox that is not yet zeroed
+        m->on = false;
+        auto barrier = [&] {
+          double *d = ctx->scratch + 4000;
+          EIG_HIP(hipMemsetAsync(d, 0, sizeof(double), ctx->stream));
+          allreduce_sum(ctx, d, 1, ctx->stream);
+          EIG_HIP(hipStreamSynchronize(ctx->stream));
+        };
+        barrier();
+        EIG_HIP(hipMemsetAsync(m->local, 0, m->bytes, ctx->stream));
+        EIG_HIP(hipMemsetAsync(m->state, 0, 256, ctx->stream));
+        EIG_HIP(hipStreamSynchronize(ctx->stream));
+        barrier();
+      }
+      else
+      {
+        // mailbox alone (eig_comm_ipc_open, no other transport to agree on a restart): only the
+        // error word is cleared; after a timeout re-open the mailbox (eig_comm_ipc_handle / _open)
+        EIG_HIP(hipMemset(m->dev.err, 0, sizeof(int)));
+      }
+      m->on = kind != EIG_AR_RCCL;
+      m->step = kind == EIG_AR_MAILBOX_STEP;
     }
   });
 }
@@ -588,7 +613,7 @@ extern "C" int eig_mat_tune(eig_mat_t A, int key, int value)
                   key == EIG_TUNE_BOX_MAP || key == EIG_TUNE_SELL_CPF || key == EIG_TUNE_MARCH_LINES,
               EIG_ERR_ARG, "eig_mat_tune: unknown key");
     EIG_CHECK(key != EIG_TUNE_HALO || value <= 1, EIG_ERR_ARG, "eig_mat_tune: halo mode 0 / 1");
-    EIG_CHECK(key != EIG_TUNE_MARCH_PREFETCH || value <= 15, EIG_ERR_ARG, "eig_mat_tune: march variant 0..15");
+    EIG_CHECK(key != EIG_TUNE_MARCH_PREFETCH || value <= 18, EIG_ERR_ARG, "eig_mat_tune: march variant 0..18");
     if (key == EIG_TUNE_MARCH_RUNS)
       A->tune_march_runs = value;
     else if (key == EIG_TUNE_MARCH_PREFETCH)

@@ -98,7 +98,8 @@ extern "C" int eig_standard_largest(eig_mat_t A, double shift, double tol, int m
     // the Gram's summation order is the product's (eig_spmm_dot_gram_mv8 / eig_orthonormalize_gram_mv8
     // are the exported pair, tests/test_gpu_drivers.py runs the reference loop with them).
     DevBuf Gb(64 * 8), dscr(8 * 8);
-    const bool gram = m == 8 && mgs_lookahead_default() == 8;
+    static const bool no_gram = std::getenv("EIGMI_NO_SPMM_GRAM") != nullptr;  // A/B: the round-5 loop
+    const bool gram = m == 8 && mgs_lookahead_default() == 8 && !no_gram;
     if (maxiter > 1)  // :78 (k = 1)
     {
       if (gram)
@@ -242,7 +243,13 @@ extern "C" int eig_standard_inverse(eig_mat_t A, eig_lu_t lu, double shift, doub
     orthonormalize_device(ctx, n, m, Bk[0], EIG_ORTHO_MGS);  // :159
     auto enqueue = [&](int k) {
       double *Q = Bk[k % 2], *dp = hd.dev + (k & 1) * m;
-      lu_inverse_device(F.lu, m, Bk[(k + 1) % 2], Q, s);  // :168 Q2 = A^-1 Q1
+      // :168 Q2 = A^-1 Q1.  The factor apply may overwrite its input (kernels_cpp.hh:659, and
+      // launch_inverse_mv8 does), and with the look-ahead iteration k + 1 runs before the host knows
+      // whether iteration k stopped the loop -- so the apply takes a copy of the basis (in Z), and a
+      // stop at k still returns basis k intact (round 6: tests/test_inverse.py caught the clobbered
+      // eigenvectors of a tolerance-driven stop)
+      EIG_HIP(hipMemcpyAsync(Z, Bk[(k + 1) % 2], (size_t)n * m * sizeof(double), hipMemcpyDeviceToDevice, s));
+      lu_inverse_device(F.lu, m, Z, Q, s);
       orthonormalize_device(ctx, n, m, Q, EIG_ORTHO_MGS);  // :171
       launch_spmm_dot_mv8(*A, m, Q, Z, dp, s, ctx->red);    // :174-175 (the product only feeds the dots)
       EIG_HIP(hipEventRecord(ev[k & 1].e, s));

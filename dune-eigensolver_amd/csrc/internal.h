@@ -114,7 +114,8 @@ struct Mailbox {
 struct MailboxHost {
   Mailbox dev;
   u64 *local = nullptr;          // hipExtMallocWithFlags allocation (exported)
-  void *state = nullptr;         // ctr + err (hipMalloc)
+  size_t bytes = 0;              // its size
+  void *state = nullptr;         // ctr + fctr + err (hipMalloc, 256 B)
   std::vector<void *> opened;    // IPC-opened peer mappings (closed on destroy)
   bool ready = false;            // peers opened and validated: allreduce_sum uses it
   bool on = true;                // eig_comm_select_allreduce: false = ncclAllReduce although ready

@@ -110,8 +110,7 @@ void launch_spmm_dot_mv8(const eig_mat_s &A, i64 m, const double *X, double *Y, 
 bool launch_spmm_dot_gram_mv8(const eig_mat_s &A, i64 m, const double *X, double *Y, double *dp, double *gram,
                               hipStream_t s, ReduceWS red)
 {
-  static const bool off = std::getenv("EIGMI_NO_SPMM_GRAM") != nullptr;  // A/B: the separate MGS read pass
-  if (off || m != 8 || A.R != 1 || A.br != 1 || A.bc != 1 || A.ctx->distributed()) return false;
+  if (m != 8 || A.R != 1 || A.br != 1 || A.bc != 1 || A.ctx->distributed()) return false;
   // the same kernel choice as launch_spmm_dot_mv8 (the row-class box kernel, else the band march)
   if (launch_box_spmm_dot_gram(A, m, X, Y, dp, gram, red, s)) return true;
   return !box_spmm_applies(A, m) && launch_spmm_march_dot_gram(A, m, X, Y, dp, gram, red, s);

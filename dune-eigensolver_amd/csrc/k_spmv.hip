@@ -1480,6 +1480,116 @@ __device__ __forceinline__ void march_rows_geo2(const SellB1 &A, const MarchPlan
            vs[VPF ? k & 1 : 0], vs[VPF ? (k + 1) & 1 : 1]);
 }
 
+// Value march with TWO grid lines per wave (march variant 22; round 6): lane = x of a 64-x run, the
+// wave's rows (x, y0) and (x, y0 + 1) of every plane it marches (y0 even; mp.ncol counts line PAIRS).
+// Per plane and lane, two rows of variant 15 (the pair pack through 64-bit addresses, the +D operand
+// loaded, the centre and -D carried), except that each line's neighbour across the pair comes from
+// registers: line y0's +nx operand is line y0 + 1's centre, line y0 + 1's -nx operand is line y0's
+// centre and its mirrored -nx value a(w + nx, w) = a(w, w + nx) is line y0's own (+1, +nx) pack
+// entry.  Gathered: line y0 - 1's operand and mirrored value, line y0 + 2's operand -- half of the
+// gathers of variant 15, whose mirrored value gathers cost 13 us at 256^3 (section 4e ablation).  Every
+// row sums the same products in the same order as variant 15 (bitwise its rows); the launch's three
+// sums add the rows in another order (each lane adds its two rows per plane).
+// waves per SIMD of the 2-line fused march (variants 22 / 23 / 24) and whether it is the default
+constexpr bool kMarch2lDefault = false;
+constexpr bool is_march2l(int uni) { return uni == 22 || uni == 23 || uni == 24; }
+
+template <class X, class EPI, class PRE>
+__device__ __forceinline__ void march_rows_geo2_2l(const SellB1 &A, const MarchPlan &mp, i64 own, int lane, int wave,
+                                                   X x, EPI &epi, PRE &pre)
+{
+  typedef typename X::raw raw;
+  constexpr unsigned SZ = sizeof(raw);
+  const int D = (int)mp.D, own32 = (int)own, gx = mp.gx;
+  const int item = (int)swizzled_block() * kWaves + wave;
+  if (item >= mp.ncol * mp.nseg) return;
+  const int col2 = item % mp.ncol, seg = item / mp.ncol;
+  const int xcols = gx / 64;
+  const int x0 = (col2 % xcols) * 64, y0 = (col2 / xcols) * 2;
+  const int z0 = (int)(mp.zb + seg * mp.nplanes / mp.nseg), z1 = (int)(mp.zb + (seg + 1) * mp.nplanes / mp.nseg);
+  const unsigned nbytes = (unsigned)(A.xlast + 1) * SZ;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(x.ptr()), 0, (int)nbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t r0 = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(x.ptr()), 0, 0, 0x00020000);
+  // line y0 - 1 (operand + mirrored value gathered) and line y0 + 2 (operand gathered)
+  const bool has_n = mp.dn && y0 > 0, has_q = mp.dq && y0 + 2 < mp.gy;
+  const __amdgpu_buffer_rsrc_t rn = has_n ? rs : r0, rq = has_q ? rs : r0;
+  constexpr unsigned kOut = 0x80000000u;
+  const unsigned eoff = lane == 0 ? (x0 > 0 ? 0u - SZ : kOut) : lane == 63 ? (x0 + 64 < gx ? SZ : kOut) : kOut;
+  const unsigned dnb = (unsigned)mp.dn * SZ, dqb = (unsigned)mp.dq * SZ, Db = (unsigned)D * SZ, nxb = (unsigned)gx * SZ;
+  int w = own32 + y0 * gx + x0 + lane + z0 * D;  // line y0's row; line y0 + 1's at w + gx
+  unsigned vo = (unsigned)w * SZ;
+  const int zg0 = z0 + mp.gz0;
+  const SymImg &S = A.sym;
+  const dpair *P01 = reinterpret_cast<const dpair *>(mp.pack), *P23 = P01 + S.ld;
+  const bool le = lane == 0 && x0 > 0;  // lane 0's mirrored -1 value (row x0 - 1) exists
+  double amD0 = 0.0, amD1 = 0.0;
+  raw pm0{}, pm1{};
+  if (zg0 > 0)
+  {
+    bload(rs, vo - Db, pm0);
+    bload(rs, vo + nxb - Db, pm1);
+    amD0 = P01[w - D].x;
+    amD1 = P01[w + gx - D].x;
+  }
+  raw c0, c1;
+  bload(rs, vo, c0);
+  bload(rs, vo + nxb, c1);
+  if (!pre(x)) return;
+  double pmv0 = zg0 > 0 ? x.val(pm0) : 0.0, pmv1 = zg0 > 0 ? x.val(pm1) : 0.0;
+  for (int z = z0; z < z1; ++z)
+  {
+    const int zg = z + mp.gz0;
+    raw eg0, eg1, xn0, xq1, d0, d1;
+    bload(rs, vo + eoff, eg0);
+    bload(rs, vo + nxb + eoff, eg1);
+    bload(rn, vo + dnb, xn0);
+    bload(rq, vo + nxb + dqb, xq1);
+    const dpair p0a = (mp.cache & 2) ? P01[w] : __builtin_nontemporal_load(P01 + w), p0b = P23[w];
+    const dpair p1a = (mp.cache & 2) ? P01[w + gx] : __builtin_nontemporal_load(P01 + w + gx), p1b = P23[w + gx];
+    const double an0 = has_n ? P23[w + mp.dn].y : 0.0;
+    const double ae0 = le ? P23[w - 1].x : 0.0, ae1 = le ? P23[w + gx - 1].x : 0.0;
+    const __amdgpu_buffer_rsrc_t rd = zg + 1 < mp.gz ? rs : r0;
+    bload(rd, vo + Db, d0);
+    bload(rd, vo + nxb + Db, d1);
+    const double vc0 = x.val(c0), vc1 = x.val(c1);
+    double acc0 = 0.0, acc1 = 0.0;
+    {
+      const double ve = x.val(eg0);
+      const double vl = lane_shift_or<false>(vc0, ve), vr = lane_shift_or<true>(vc0, ve);
+      const double am = lane_shift_or<false>(p0b.x, ae0);
+      acc0 += amD0 * pmv0;
+      acc0 += an0 * x.val(xn0);
+      acc0 += am * vl;
+      acc0 += p0a.y * vc0;
+      acc0 += p0b.x * vr;
+      acc0 += p0b.y * vc1;  // +nx: line y0 + 1's centre
+      acc0 += p0a.x * x.val(d0);
+    }
+    {
+      const double ve = x.val(eg1);
+      const double vl = lane_shift_or<false>(vc1, ve), vr = lane_shift_or<true>(vc1, ve);
+      const double am = lane_shift_or<false>(p1b.x, ae1);
+      acc1 += amD1 * pmv1;
+      acc1 += p0b.y * vc0;  // -nx: line y0's centre, mirrored value = line y0's +nx entry
+      acc1 += am * vl;
+      acc1 += p1a.y * vc1;
+      acc1 += p1b.x * vr;
+      acc1 += p1b.y * x.val(xq1);
+      acc1 += p1a.x * x.val(d1);
+    }
+    epi(w - own32, w, acc0, c0);
+    epi(w + gx - own32, w + gx, acc1, c1);
+    pmv0 = vc0;
+    pmv1 = vc1;
+    amD0 = p0a.x;
+    amD1 = p1a.x;
+    c0 = d0;
+    c1 = d1;
+    w += D;
+    vo += Db;
+  }
+}
+
 // Box march for the P1 Kuhn 15-point stencil (march variant 12; config C5's K and M, any values): the
 // band's offsets are a D + b nx + c with (a, b, c) in the Kuhn edge set {0, +-e_i, +-(e_i + e_j),
 // +-(1, 1, 1)} and every row stores exactly its in-grid neighbours among them (eig_mat_s::sym_box27,
@@ -1748,11 +1858,16 @@ template <class MT, int KC, bool SPAN1, int UNI, class X, class EPI, class PRE =
 __device__ __forceinline__ void march_rows(const SellB1 &A, const MarchPlan &mp, i64 own, int lane, int wave,
                                            const X &x, EPI &epi, PRE &&pre = PRE{})
 {
-  static_assert(!UNI || SPAN1 || UNI == 12 || UNI == 16 || UNI == 19 || UNI == 20,
+  static_assert(!UNI || SPAN1 || UNI == 12 || UNI == 16 || UNI == 19 || UNI == 20 || is_march2l(UNI),
                 "uniform-band march: far spans of at most one offset");
   if constexpr (UNI == 12 || UNI == 16 || UNI == 19 || UNI == 20)
   {
     march_rows_kuhn<UNI != 12, UNI == 20>(A, mp, own, lane, wave, x, epi, pre);
+    return;
+  }
+  else if constexpr (is_march2l(UNI))
+  {
+    march_rows_geo2_2l(A, mp, own, lane, wave, x, epi, pre);
     return;
   }
 
@@ -1898,7 +2013,7 @@ __device__ __forceinline__ void march_rows(const SellB1 &A, const MarchPlan &mp,
 
 // y[own + r] = (A x)[r] on the plane march (BCRSMatrix::mv; bitwise k_spmv_b1).
 // resident waves per SIMD of the eig_mv / K1 march kernels (the box march holds ~90 VGPRs)
-constexpr int march_mv_waves(int uni) { return uni == 12 || uni == 16 || uni == 19 || uni == 20 ? 5 : 8; }
+constexpr int march_mv_waves(int uni) { return uni == 12 || uni == 16 || uni == 19 || uni == 20 || is_march2l(uni) ? 5 : 8; }
 
 template <class MT, bool SPAN1, int UNI>
 __global__ __launch_bounds__(kStreamThreads, march_mv_waves(UNI)) void k_spmv_march(i64 nrows, i64 own, SellB1 A, MarchPlan mp,
@@ -1956,7 +2071,7 @@ __global__ __launch_bounds__(kStreamThreads, march_mv_waves(UNI)) void k_lanczos
 // resident waves per SIMD the fused march kernels are built for (registers: no spills)
 constexpr int march_fused_waves(int uni)
 {
-  return uni == 18 ? 7 : uni == 16 || uni == 20 ? 4 : uni == 12 || uni == 19 ? 5 : uni == 11 ? 5 : uni == 10 || uni >= 13 ? 6 : uni == 6 || uni == 9 ? 4 : uni == 5 ? 5 : uni == 4 || uni == 8 ? 6
+  return uni == 22 ? 5 : uni == 23 ? 4 : uni == 24 ? 6 : uni == 18 ? 7 : uni == 16 || uni == 20 ? 4 : uni == 12 || uni == 19 ? 5 : uni == 11 ? 5 : uni == 10 || uni >= 13 ? 6 : uni == 6 || uni == 9 ? 4 : uni == 5 ? 5 : uni == 4 || uni == 8 ? 6
        : uni == 3 || uni == 7 ? 7 : uni ? 8 : 7;
 }
 
@@ -2596,7 +2711,11 @@ static int march_uniform(const eig_mat_s &A, bool fused = false, i64 nplanes = 0
     // 30.4 us; the arrays 226.8 / 31.7), eig_mv / K1 on the plain masked march (0: 152.1 us against 161.4 on
     // the pack): profiles/r04d_latency.jsonl, r04d_slab.jsonl
     const int tp = A.tune_march_prefetch;
-    return tp == 9 ? 10 : tp == 10 ? 11 : tp == 12 ? 14 : tp == 13 ? 15 : tp == 15 ? 18 : fused ? (A.sym_nd == 7 ? 15 : 10) : 0;
+    // 22: two grid lines per wave (7-point bands on grids of an even line count)
+    const bool two = A.sym_nd == 7 && A.sym_gy % 2 == 0 && A.sym_gy > 0;
+    if (tp >= 16 && tp <= 18) return two ? tp + 6 : 15;
+    return tp == 9 ? 10 : tp == 10 ? 11 : tp == 12 ? 14 : tp == 13 ? 15 : tp == 15 ? 18
+         : fused ? (A.sym_nd == 7 ? (two && kMarch2lDefault ? 22 : 15) : 10) : 0;
   }
   if (!A.sym_geo) return 1;
   int u = A.tune_march_prefetch > 0 ? 1 + A.tune_march_prefetch : geo2 ? 7 : 4;
@@ -2621,6 +2740,12 @@ static int march_uniform(const eig_mat_s &A, bool fused = false, i64 nplanes = 0
       hipLaunchKernelGGL((KERN<uint8_t, true, 14>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);       \
     else if ((MODE) == kSymN8 && march_span1(A) && mp.uni == 15)                                          \
       hipLaunchKernelGGL((KERN<uint8_t, true, 15>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);       \
+    else if ((MODE) == kSymN8 && march_span1(A) && mp.uni == 22)                                          \
+      hipLaunchKernelGGL((KERN<uint8_t, true, 22>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);       \
+    else if ((MODE) == kSymN8 && march_span1(A) && mp.uni == 23)                                          \
+      hipLaunchKernelGGL((KERN<uint8_t, true, 23>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);       \
+    else if ((MODE) == kSymN8 && march_span1(A) && mp.uni == 24)                                          \
+      hipLaunchKernelGGL((KERN<uint8_t, true, 24>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);       \
     else if ((MODE) == kSymN8 && march_span1(A) && mp.uni == 18)                                          \
       hipLaunchKernelGGL((KERN<uint8_t, true, 18>), dim3(G), dim3(kStreamThreads), 0, __VA_ARGS__);       \
     else if ((MODE) == kSymN8 && march_span1(A) && mp.uni == 11)                                          \
@@ -2703,9 +2828,12 @@ static MarchPlan march_plan(const eig_mat_s &A, int mode, i64 zb = 0, i64 ze = -
                          std::max<i64>(2, std::min<i64>(uni == 7 || uni >= 10 ? 8 : 6, nplanes / 32)));
   else if (fused)  // (geo2 marches: runs of >= 16 planes -- 128^3 8 runs 24.3 us, 12: 25.3, 16: 26.4)
     nseg = std::min(nseg, std::max<i64>({1, nplanes / (uni >= 7 ? 16 : 10), (resident / 4 + ncol - 1) / ncol}));
+  // variant 22 marches line PAIRS: half the items per plane run, so twice the runs for as many waves
+  const i64 items_per_run = is_march2l(uni) ? ncol / 2 : ncol;
+  if (is_march2l(uni)) nseg = std::min<i64>(nplanes, 2 * nseg);
   if (A.tune_march_runs > 0) nseg = std::min<i64>(A.tune_march_runs, nplanes);  // eig_mat_tune
-  while (nseg > 1 && (ncol * nseg + kWaves - 1) / kWaves > kMaxRedBlocks) --nseg;
-  if ((ncol * nseg + kWaves - 1) / kWaves > kMaxRedBlocks) return mp;
+  while (nseg > 1 && (items_per_run * nseg + kWaves - 1) / kWaves > kMaxRedBlocks) --nseg;
+  if ((items_per_run * nseg + kWaves - 1) / kWaves > kMaxRedBlocks) return mp;
   mp.D = D;
   int klo = A.sym_nd, khi = A.sym_nd;
   for (int k = A.sym_nd - 1; k >= 0; --k)
@@ -2749,7 +2877,7 @@ static MarchPlan march_plan(const eig_mat_s &A, int mode, i64 zb = 0, i64 ze = -
     mp.cq = khi < A.sym_nd - 1 ? A.sym_uc[A.sym_dj[khi]] : 0.0;
   }
   mp.uni = uni;
-  mp.pack = pack && (uni == 15 || uni == 16 || uni == 18 || uni == 19 || uni == 20) ? sym_pack_prepare(A) : nullptr;
+  mp.pack = pack && (uni == 15 || uni == 16 || uni == 18 || uni == 19 || uni == 20 || is_march2l(uni)) ? sym_pack_prepare(A) : nullptr;
   // measured (tools/march_copy.hip *_pp, profiles/r03bo_march_copy.jsonl): the step's ping-pong at
   // 128^3 (2 x 32 MB of pairs) 12.9 us with plain stores vs 17.6 us nontemporal; at 256^3 (2 x 268
   // MB) no difference either way -- plain stores where every vector a launch touches fits in half
@@ -2766,7 +2894,7 @@ static MarchPlan march_plan(const eig_mat_s &A, int mode, i64 zb = 0, i64 ze = -
   mp.zb = zb;
   mp.nplanes = nplanes;
   mp.mrows = A.nslices * 64;
-  mp.ncol = (int)ncol;
+  mp.ncol = (int)items_per_run;
   mp.nseg = (int)nseg;
   return mp;
 }
@@ -3146,7 +3274,7 @@ void lanczos_kernel_info(const eig_mat_s &A, bool fused, std::string &name, i64 
     // the band arrays and the vectors (geometric masks: no mask stream)
     const int mv = march && ((mode == kSymN8 && march_span1(A)) || march_kuhn(A)) ? march_uniform(A, fused) : 0;
     if (mv >= 10)
-      bytes = 8 * (mv == 15 || mv == 18 ? 4 : (i64)A.sym_nup) * n + vec;
+      bytes = 8 * (mv == 15 || mv == 18 || is_march2l(mv) ? 4 : (i64)A.sym_nup) * n + vec;
     else if (mv)
       bytes = (mv >= 2 ? 0 : (i64)A.sym_mask_bytes * n) + vec;
     name = fused ? (march ? "k_lanczos_fused_march" : "k_lanczos_fused_b1")

@@ -118,8 +118,11 @@ int eig_comm_ipc_open_ex(eig_ctx_t ctx, const unsigned char *handles, int flags)
 int eig_comm_info(eig_ctx_t ctx, int *nranks, int *rank, int *allreduce, int *mailbox_errors);
 /* Switch the allreduce transport of a communicator that has both (RCCL + a validated mailbox):
  * EIG_AR_RCCL, EIG_AR_MAILBOX or EIG_AR_MAILBOX_STEP (the mailbox alone: EIG_AR_MAILBOX or _STEP).
- * Every rank must select the same one (no collective inside).  Synchronises the stream and clears
- * the recorded mailbox timeouts. */
+ * A collective: every rank selects the same one.  Synchronises the stream; with RCCL (or loopback)
+ * beside the mailbox it restarts the mailbox on every rank between two barriers (mailbox, call
+ * counters and recorded timeouts zeroed), so a transport that timed out can be selected again with
+ * consistent sequence words.  A mailbox alone (eig_comm_ipc_open) only clears the recorded timeouts:
+ * after a timeout, re-open it. */
 int eig_comm_select_allreduce(eig_ctx_t ctx, int kind);
 
 /* ---------------------------------------------------------------- device memory ------------ */
@@ -264,7 +267,10 @@ enum { EIG_TUNE_MARCH_RUNS = 1, EIG_TUNE_BOX_SEGS = 2, EIG_TUNE_MARCH_PREFETCH =
  * march on the band arrays, 9 = the value march (eig_mat_info.march_variant 10: the band arrays
  * streamed, masks from the coordinates), 10 = the same with the value streams one plane ahead (11),
  * 11 = the value march on a packed copy of the 4 arrays (13: {+D, 0, +1, +nx} per row, two 16-B loads);
- * 0 = automatic.  Bitwise the same results for every value. */
+ * 16 / 17 / 18 = that pack marched TWO grid lines per wave (march variants 22 / 23 / 24: 5 / 4 / 6
+ * waves per SIMD; 7-point bands, an even line count) -- the +-nx neighbours across the pair from
+ * registers, half the gathers; the fused step's sums then add the rows in another order;
+ * 0 = automatic.  Bitwise the same rows for every value. */
 int eig_mat_tune(eig_mat_t mat, int key, int value);
 
 /* a13: A += shift*I on the diagonal of every diagonal block (eigensolver.hh:59-66). */

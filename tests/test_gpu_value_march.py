@@ -129,6 +129,35 @@ def test_value_march_bitwise(ctx, mat):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("mat", list(MATS))
+def test_value_march_two_lines(ctx, mat):
+    """March variants 22 / 23 (EIG_TUNE_MARCH_PREFETCH 16 / 17: the value pack marched TWO grid lines
+    per wave, the +-nx neighbours across the pair from registers): eig_mv BITWISE the reference row
+    loop (each row sums what variant 15 sums, in the same order), the fused and classic recurrences
+    within 1e-12 of their restatements, at several plane-run counts; a grid with an odd line count
+    keeps variant 15."""
+    A, flags = MATS[mat]()
+    M = eigmi.Matrix.from_bcsr(ctx, A.rowptr, A.col, A.val, flags=flags)
+    n = A.n
+    odd = mat == "box128x3x9"
+    x = np.random.default_rng(12).standard_normal(n)
+    ref = oracle.csr_mv(A, x)
+    U0 = oracle.random_vec(n, 123)
+    qa, qb = oracle.lanczos_fused(A, U0, 20)
+    _, ra, rb = oracle.lanczos(A, U0, 20)
+    for runs in (0, 1, 2, 5):
+        for pf in (16, 17):
+            M.tune(runs, march_prefetch=pf)
+            assert M.info.march_variant == (15 if odd else pf + 6), (runs, pf)
+            assert np.array_equal(M.mv_host(x), ref), (runs, pf)
+            fa, fb, _ = eigmi.lanczos_run(M, 20, seed=123, fused=True)
+            assert np.allclose(fa, qa, rtol=1e-12, atol=0) and np.allclose(fb, qb, rtol=1e-12, atol=0), (runs, pf)
+            ca, cb, _ = eigmi.lanczos_run(M, 20, seed=123)
+            assert np.allclose(ca, ra, rtol=1e-12, atol=0) and np.allclose(cb, rb, rtol=1e-12, atol=0), (runs, pf)
+    M.tune(0, march_prefetch=0)
+
+
+@pytest.mark.gpu
 def test_value_march_after_shift(ctx):
     """A += sigma I updates the band values the value marches stream (StandardLargest's shift,
     eigensolver.hh:59-66), the value pack included (built at first use, refilled in place by the
@@ -245,6 +274,22 @@ def test_bench_image_256_spmv_bitwise(ctx, p256a):
     assert info.sym_uniform == 0 and info.march_variant == 15 and info.march_variant_mv == 0
     x = np.random.default_rng(21).standard_normal(N ** 3)
     assert np.array_equal(M.mv_host(x), oracle.csr_mv(A, x))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pf", [16, 17])
+def test_bench_image_256_two_lines(ctx, p256a, pf):
+    """The benched image with the 2-line value march (variants 22 / 23): eig_mv bitwise the oracle row
+    loop and 60 fused steps vs orc_lanczos_fused, rtol 1e-12."""
+    N, M, A = p256a
+    M.tune(march_prefetch=pf)
+    try:
+        assert M.info.march_variant == pf + 6 and M.info.march_variant_mv == pf + 6
+        x = np.random.default_rng(22).standard_normal(N ** 3)
+        assert np.array_equal(M.mv_host(x), oracle.csr_mv(A, x))
+        fused_vs_oracle(M, A, FULL_STEPS)
+    finally:
+        M.tune(march_prefetch=0)
 
 
 @pytest.mark.gpu

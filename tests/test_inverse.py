@@ -366,3 +366,105 @@ def test_device_lu_rejects_factors_that_need_pivoting(ctx):
     good.sort_indices()
     lu = eigmi.LU.from_bcsr(ctx, good.indptr.astype(np.int64), good.indices.astype(np.int32), good.data.copy())
     lu.close()
+
+
+def _inverse_setup(ctx, A, shift):
+    """The device matrix, its shifted host copy and the LU of that copy (handed to the driver AND to the
+    loop below, so both apply the same factors)."""
+    M = eigmi.Matrix.from_bcsr(ctx, A.rowptr, A.col, A.val)
+    As = oracle.CSR(A.nrows, A.rowptr, A.col, A.val.copy())
+    oracle.lib.orc_shift_diag(As.n, As.rowptr, As.col, As.val, shift)
+    lu = eigmi.LU.from_bcsr(ctx, As.rowptr, As.col, As.val)
+    return M, As, lu
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("maxiter,tol", [(1, 0.0), (2, 0.0), (12, 0.0), (4000, 1e-9)])
+def test_standard_inverse_lookahead_loop(ctx, maxiter, tol):
+    """the look-ahead StandardInverse (iteration k + 1 queued before iteration k's stopping
+    test, basis ping-pong) against the reference's loop (eigensolver.hh:159-189) written with the
+    device primitives: Q2 = A^-1 Q1 (:168), orthonormalize_blocked (:171), the product and its
+    diagonal dots (:174-175), the absolute max|ds| test with k > 1 (:178-189).  Iterates BITWISE, the
+    same iteration count, Ritz values within 1e-14 (the driver's dots are fused into its product)."""
+    N, nev, shift = 20, 4, 0.2
+    A = oracle.laplace2d(N)
+    M, As, lu = _inverse_setup(ctx, A, shift)
+    ev, evec, it = eigmi.standard_inverse(M, shift, tol, maxiter, nev, 17, lu=lu)
+    n, m = A.n, 8
+    Ms = eigmi.Matrix.from_bcsr(ctx, As.rowptr, As.col, As.val)  # the driver shifted M in place (:145-153)
+    Q = [ctx.zeros(n * m), ctx.zeros(n * m)]
+    Z, dp = ctx.zeros(n * m), ctx.zeros(m)
+    eigmi.random_mv8(ctx, n, m, 17, Q[0])
+    eigmi.orthonormalize_mv8(ctx, n, m, Q[0])
+    s2 = np.zeros(m)
+    kk, basis = 1, 0
+    for k in range(1, maxiter):
+        kk = k
+        lu.inverse_mv8(m, Q[(k + 1) % 2], Q[k % 2])
+        eigmi.orthonormalize_mv8(ctx, n, m, Q[k % 2])
+        eigmi.spmm_mv8(Ms, m, Q[k % 2], Z)
+        eigmi.dot_diag_mv8(ctx, n, m, Q[k % 2], Z, dp)
+        s1 = dp.get() - shift
+        dist = np.abs(s1 - s2).max()
+        s2 = s1
+        basis = k % 2
+        if k > 1 and dist < tol:
+            break
+    q = Q[basis].get().reshape(m // 8, n, 8)
+    ref_evec = np.stack([q[j // 8, :, j % 8] for j in range(nev)])
+    print(f"StandardInverse maxiter {maxiter} tol {tol}: {it} iterations (reference loop {kk})")
+    assert it == kk
+    assert np.array_equal(evec, ref_evec)
+    assert np.abs(ev - s2[:nev]).max() <= 1e-14 * max(1.0, np.abs(s2).max())
+    lu.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("maxiter,tol", [(1, 0.0), (2, 0.0), (12, 0.0), (500, 1e-10)])
+def test_generalized_inverse_lookahead_loop(ctx, maxiter, tol):
+    """the look-ahead GeneralizedInverse against the reference's loop (eigensolver.hh:
+    270-325) written with the device primitives: B-orthonormalise (:273), product + dots (:274-275),
+    then per iteration Q2 = B Q1 (:302), Q1 = As^-1 Q2 (:303), B_orthonormalize_blocked (:304), the
+    product's dots (:317) and the relative test with iter > 10 (:315-325).  Iterates BITWISE, the
+    same iteration count, eigenvalues within 1e-14."""
+    N, nev, shift, reg = 14, 4, 0.75, 1e-3
+    A, B = oracle.laplace2d(N, "neumann"), oracle.laplace2d(N, "pu", overlap=3)
+    assert np.array_equal(A.rowptr, B.rowptr) and np.array_equal(A.col, B.col)
+    dA = eigmi.Matrix.from_bcsr(ctx, A.rowptr, A.col, A.val)
+    dB = eigmi.Matrix.from_bcsr(ctx, B.rowptr, B.col, B.val)
+    diag = A.col == np.repeat(np.arange(A.n), np.diff(A.rowptr))
+    sv = A.val + shift * B.val  # the driver's host copy: v += shift b, then v += reg on the diagonal (:240-252)
+    sv[diag] += reg
+    lu = eigmi.LU.from_bcsr(ctx, A.rowptr, A.col, sv)
+    ev, evec, it = eigmi.generalized_inverse(dA, dB, shift, reg, tol, maxiter, nev, 29, lu=lu)
+    n, m = A.n, 8
+    dAs = eigmi.Matrix.from_bcsr(ctx, A.rowptr, A.col, sv)
+    Q = [ctx.zeros(n * m), ctx.zeros(n * m)]
+    Z, dp, norm = ctx.zeros(n * m), ctx.zeros(m), ctx.zeros(1)
+    eigmi.random_mv8(ctx, n, m, 29, Q[0])
+    eigmi.b_orthonormalize_mv8(dB, m, Q[0], norm)
+    eigmi.spmm_mv8(dAs, m, Q[0], Z)
+    eigmi.dot_diag_mv8(ctx, n, m, Q[0], Z, dp)
+    ra2 = dp.get() - shift
+    it_ref, basis = 0, 0
+    while it_ref < maxiter:
+        it_ref += 1
+        i = it_ref
+        eigmi.spmm_mv8(dB, m, Q[(i + 1) % 2], Z)
+        lu.inverse_mv8(m, Z, Q[i % 2])
+        eigmi.b_orthonormalize_mv8(dB, m, Q[i % 2], norm)
+        eigmi.spmm_mv8(dAs, m, Q[i % 2], Z)
+        eigmi.dot_diag_mv8(ctx, n, m, Q[i % 2], Z, dp)
+        ra1 = dp.get() - shift
+        basis = i % 2
+        rel = np.abs(ra1 - ra2).max() / ra1.max()
+        ra2 = ra1
+        if it_ref > 10 and rel < tol:
+            break
+    q = Q[basis].get().reshape(m // 8, n, 8)
+    ref_evec = np.stack([q[j // 8, :, j % 8] for j in range(nev)])
+    print(f"GeneralizedInverse maxiter {maxiter} tol {tol}: {it} iterations (reference loop {it_ref})")
+    assert it == it_ref
+    assert np.array_equal(evec, ref_evec)
+    assert np.abs(ev - ra2[:nev]).max() <= 1e-14 * max(1.0, np.abs(ra2).max())
+    lu.close()

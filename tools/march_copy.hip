@@ -371,6 +371,117 @@ __global__ __launch_bounds__(kThreads, W) void k_vabl(int n, int D, int nx, int 
   }
 }
 
+// The full ablation step (k_vabl<true, true, true, W, true, 1, true>) with TWO grid lines per wave
+// (round 6 probe): lane = x, the wave's lines y0 = 2 ly and y0 + 1, so the +nx operand of line y0 and
+// the -nx operand and mirrored -nx value of line y0 + 1 are the other line's registers; only line
+// y0 - 1's operand and mirrored value and line y0 + 2's operand are gathered (half the gathers).
+template <int W>
+__global__ __launch_bounds__(kThreads, W) void k_vabl2(int n, int D, int nx, int ncol, int nseg, int nplanes,
+                                                       const dpair *__restrict__ P, const dpair *__restrict__ V,
+                                                       dpair *__restrict__ Q, double *__restrict__ sums, double c)
+{
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int ncol2 = ncol / 2, xc = nx / 64;
+  const int item = swz() * kW + wave;
+  if (item >= ncol2 * nseg) return;
+  const int col2 = item % ncol2, seg = item / ncol2;
+  const int z0 = seg * nplanes / nseg, z1 = (seg + 1) * nplanes / nseg;
+  const int lastrow = n - 1;
+  auto cl = [&](int g) { return g < 0 ? 0 : (g > lastrow ? lastrow : g); };
+  const int line0 = 2 * (col2 / xc);
+  int w = line0 * nx + (col2 % xc) * 64 + lane + z0 * D;  // row of line y0; line y0 + 1 at w + nx
+  dpair cur0 = P[cl(w)], cur1 = P[cl(w + nx)];
+  dpair prev0 = P[cl(w - D)], prev1 = P[cl(w + nx - D)];
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+  auto uk = [&](dpair p) { return p.x - c * p.y; };
+  for (int z = z0; z < z1; ++z, w += D)
+  {
+    const dpair pd0 = P[cl(w + D)], pd1 = P[cl(w + nx + D)];
+    const dpair a0 = __builtin_nontemporal_load(V + w), b0 = V[n + w];
+    const dpair a1 = __builtin_nontemporal_load(V + w + nx), b1 = V[n + w + nx];
+    const dpair u = P[cl(w - nx)], v = P[cl(w + 2 * nx)];
+    dpair e0 = dpair{0.0, 0.0}, e1 = dpair{0.0, 0.0};
+    if (lane == 0 || lane == 63)
+    {
+      e0 = P[cl(lane == 0 ? w - 1 : w + 1)];
+      e1 = P[cl(lane == 0 ? w + nx - 1 : w + nx + 1)];
+    }
+    const double mnx0 = V[n + cl(w - nx)].y;
+    double m1e0 = 0.0, m1e1 = 0.0;
+    if (lane == 0)
+    {
+      m1e0 = V[n + cl(w - 1)].x;
+      m1e1 = V[n + cl(w + nx - 1)].x;
+    }
+    const double vc0 = uk(cur0), vc1 = uk(cur1);
+    auto row = [&](dpair a, dpair b, dpair prev, double mnx, double vn, double m1e, dpair e, double vc, double vq,
+                   dpair pd, dpair cur) {
+      const double vl = __shfl_up(vc, 1, 64), vr = __shfl_down(vc, 1, 64);
+      const double am1 = lane == 0 ? m1e : __shfl_up(b.x, 1, 64);
+      double acc = 0.0;
+      acc += b.y * uk(prev);
+      acc += mnx * vn;
+      acc += am1 * (lane == 0 ? uk(e) : vl);
+      acc += a.x * vc;
+      acc += b.x * (lane == 63 ? uk(e) : vr);
+      acc += b.y * vq;
+      acc += a.x * uk(pd);
+      const double t = (acc - 0.5 * vc) * 0.25 - 0.125 * cur.y;
+      s0 += t * vc;
+      s1 += t * t;
+      s2 += vc * vc;
+      return dpair{t, vc};
+    };
+    const dpair o0 = row(a0, b0, prev0, mnx0, uk(u), m1e0, e0, vc0, vc1, pd0, cur0);
+    const dpair o1 = row(a1, b1, prev1, b0.y, vc0, m1e1, e1, vc1, uk(v), pd1, cur1);
+    __builtin_nontemporal_store(o0, Q + w);
+    __builtin_nontemporal_store(o1, Q + w + nx);
+    prev0 = cur0;
+    prev1 = cur1;
+    cur0 = pd0;
+    cur1 = pd1;
+  }
+  for (int off = 32; off > 0; off >>= 1)
+  {
+    s0 += __shfl_down(s0, off, 64);
+    s1 += __shfl_down(s1, off, 64);
+    s2 += __shfl_down(s2, off, 64);
+  }
+  __shared__ double ws[kW][3];
+  __shared__ int last;
+  if (lane == 0)
+  {
+    ws[wave][0] = s0;
+    ws[wave][1] = s1;
+    ws[wave][2] = s2;
+  }
+  __syncthreads();
+  double *part = sums + 64;
+  unsigned *ticket = reinterpret_cast<unsigned *>(sums);
+  if (threadIdx.x < 3)
+  {
+    double t = 0.0;
+    for (int q = 0; q < kW; ++q) t += ws[q][threadIdx.x];
+    __hip_atomic_store(reinterpret_cast<unsigned long long *>(part + 3 * blockIdx.x + threadIdx.x),
+                       (unsigned long long)__double_as_longlong(t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  __syncthreads();
+  if (last)
+  {
+    double a0 = 0.0;
+    for (unsigned b = threadIdx.x; b < 3 * gridDim.x; b += kThreads)
+      a0 += __longlong_as_double((long long)__hip_atomic_load(reinterpret_cast<unsigned long long *>(part + b),
+                                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    for (int off = 32; off > 0; off >>= 1) a0 += __shfl_down(a0, off, 64);
+    if (lane == 0) atomicAdd(sums + 8, a0);
+    if (threadIdx.x == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // two columns per wave: c and c + ncol / 2 (ncol even)
 __global__ __launch_bounds__(kThreads, 8) void k_march2(int n, int D, int ncol, int nseg, int nplanes,
                                                         const dpair *__restrict__ P, dpair *__restrict__ Q)
@@ -536,6 +647,12 @@ int main(int argc, char **argv)
       ABL("abl_full_tail_w6", true, true, true, 6, true, 1, true);
       ABL("abl_full_notail_w6", true, true, true, 6, true, 1, false);
 #undef ABL
+      // two lines per wave (half the items): W = 4 / 5 / 6 waves per SIMD
+      const int G2 = ((ncol / 2) * nseg + kW - 1) / kW;
+      outv("abl_full_tail_2lines_w4", nseg, time([&] { k_vabl2<4><<<G2, kThreads>>>(n, D, nx, ncol, nseg, NZ, src(), V, dst(), sums, 0.5); }));
+      outv("abl_full_tail_2lines_w5", nseg, time([&] { k_vabl2<5><<<G2, kThreads>>>(n, D, nx, ncol, nseg, NZ, src(), V, dst(), sums, 0.5); }));
+      outv("abl_full_tail_2lines_w6", nseg, time([&] { k_vabl2<6><<<G2, kThreads>>>(n, D, nx, ncol, nseg, NZ, src(), V, dst(), sums, 0.5); }));
+      outv("abl_full_tail_w6_again", nseg, time([&] { k_vabl<true, true, true, 6, true, 1, true><<<G, kThreads>>>(n, D, nx, ncol, nseg, NZ, src(), V, dst(), sums, 0.5); }));
       CK(hipFree(sums));
     }
     CK(hipGetLastError());
