@@ -157,6 +157,9 @@ struct eig_ctx_s {
   // a look-ahead MGS last launch (grid barriers without a cooperative launch) has been enqueued
   // since the last mgs_lookahead_check: its sticky error word must be read at the next sync point
   bool mgs_la_armed = false;
+  // the window Gram whose product also zeroed the look-ahead MGS's barrier word (launch_spmm_dot_gram_mv8);
+  // consumed by the next launch_mgs_lookahead_gram of that Gram
+  const double *mgs_bar_clean = nullptr;
 };
 
 namespace eigmi {
@@ -355,9 +358,11 @@ bool launch_box_spmm(const eig_mat_s &A, i64 m, const double *X, double *Y, hipS
 bool launch_box_spmm_dot(const eig_mat_s &A, i64 m, const double *X, double *Y, double *dp, ReduceWS red,
                          hipStream_t s);
 bool launch_box_spmm_dot_gram(const eig_mat_s &A, i64 m, const double *X, double *Y, double *dp, double *gram,
-                              ReduceWS red, hipStream_t s);
+                              ReduceWS red, hipStream_t s, unsigned *zero_word = nullptr);
 bool launch_spmm_march_dot_gram(const eig_mat_s &A, i64 m, const double *X, double *Y, double *dp, double *gram,
-                                ReduceWS red, hipStream_t s);
+                                ReduceWS red, hipStream_t s, unsigned *zero_word = nullptr);
+// the look-ahead MGS state's barrier word of this context (allocated and zeroed on first use)
+unsigned *mgs_lookahead_barrier(eig_ctx_t ctx);
 // StandardLargest's product: Y = A X, dp = diag(X^T Y) and (gram != null, m = 8) the window Gram of Y
 // for the next iteration's MGS; false when no fused kernel applies (then gram is not written).
 bool launch_spmm_dot_gram_mv8(const eig_mat_s &A, i64 m, const double *X, double *Y, double *dp, double *gram,

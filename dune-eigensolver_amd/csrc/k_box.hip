@@ -58,6 +58,7 @@ struct BoxDot {
   double *part = nullptr;
   unsigned *tick = nullptr;
   double *gram = nullptr;  // kBoxStoreDotGram: the 8 x 8 window Gram of Y (row-major, upper triangle)
+  unsigned *zero_word = nullptr;  // kBoxStoreDotGram: zeroed by the last workgroup (the next MGS's barrier)
 };
 constexpr int kBoxMaxNd = 15;  // offsets of the box-image kernel's LDS value tile (P1 Kuhn: 15, 7-point: 7)
 constexpr int kBoxClassMaxNd = 27;  // offsets of the row-class kernels (27: Galerkin coarse operators)
@@ -905,6 +906,7 @@ __global__ __launch_bounds__(kCThreads, EPI == kBoxStoreDotGram ? 4 : 8) void k_
     {
       if (tid < 64) bd.gram[tid] = gt[tid];
       if (tid < 8) bd.dp[tid] = gt[64 + tid];
+      if (tid == 0 && bd.zero_word) *bd.zero_word = 0u;
     }
   }
   if constexpr (EPI == kBoxStoreDot)
@@ -1307,7 +1309,7 @@ bool launch_box_spmm_dot(const eig_mat_s &A, i64 m, const double *X, double *Y, 
 // kernel only (false otherwise).  Uses the reduction workspace's partials (grid.x x 72 + 8 x 72) and
 // ticket 0.
 bool launch_box_spmm_dot_gram(const eig_mat_s &A, i64 m, const double *X, double *Y, double *dp, double *gram,
-                              ReduceWS red, hipStream_t s)
+                              ReduceWS red, hipStream_t s, unsigned *zero_word)
 {
   if (m != 8 || !box_prepare(A) || !A.box_ctab) return false;
   BoxDot bd;
@@ -1315,6 +1317,7 @@ bool launch_box_spmm_dot_gram(const eig_mat_s &A, i64 m, const double *X, double
   bd.part = red.partials;
   bd.tick = red.ticket(0);
   bd.gram = gram;
+  bd.zero_word = zero_word;
   return launch_box(A, m, X, Y, nullptr, nullptr, nullptr, 0.0, 0.0, kBoxStoreDotGram, s, bd);
 }
 

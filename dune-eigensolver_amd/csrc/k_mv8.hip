@@ -111,9 +111,14 @@ bool launch_spmm_dot_gram_mv8(const eig_mat_s &A, i64 m, const double *X, double
                               hipStream_t s, ReduceWS red)
 {
   if (m != 8 || A.R != 1 || A.br != 1 || A.bc != 1 || A.ctx->distributed()) return false;
-  // the same kernel choice as launch_spmm_dot_mv8 (the row-class box kernel, else the band march)
-  if (launch_box_spmm_dot_gram(A, m, X, Y, dp, gram, red, s)) return true;
-  return !box_spmm_applies(A, m) && launch_spmm_march_dot_gram(A, m, X, Y, dp, gram, red, s);
+  // the same kernel choice as launch_spmm_dot_mv8 (the row-class box kernel, else the band march);
+  // the kernel's last workgroup also zeroes the look-ahead MGS's barrier word, so the MGS of this
+  // block that follows (launch_mgs_lookahead_gram with this gram) needs no extra launch
+  unsigned *bar = mgs_lookahead_barrier(A.ctx);
+  const bool ok = launch_box_spmm_dot_gram(A, m, X, Y, dp, gram, red, s, bar) ||
+                  (!box_spmm_applies(A, m) && launch_spmm_march_dot_gram(A, m, X, Y, dp, gram, red, s, bar));
+  A.ctx->mgs_bar_clean = ok ? gram : nullptr;
+  return ok;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1169,12 +1174,32 @@ __device__ __forceinline__ bool mgs_la_read_coop(const MgsLaArgs a, MgsLaShared<
 }
 
 // The last launch of a call (every workgroup resident: G <= CUs, one workgroup fits a CU).
+// G (or null): the block's window Gram, summed by the product that wrote the block (StandardLargest,
+// launch_mgs_lookahead_gram): every workgroup finishes the window from it itself -- the same close
+// as the read pass's tail, so the same S rows in every workgroup -- instead of a first read pass.
 template <int L>
-__global__ __launch_bounds__(kMgsLaThreads) void k_mgs_la_final(MgsLaArgs a)
+__global__ __launch_bounds__(kMgsLaThreads) void k_mgs_la_final(MgsLaArgs a, const double *__restrict__ G = nullptr)
 {
   __shared__ MgsLaShared<L> sh;
-  if (threadIdx.x < 64) sh.S[threadIdx.x] = a.Sfin[threadIdx.x];
-  if (threadIdx.x == 0) sh.word = a.st[a.launch & 1];
+  if (G)
+  {
+    if (threadIdx.x < 64)
+    {
+      const int w = threadIdx.x / 8, c = threadIdx.x % 8;
+      sh.Rw[w][c] = c >= w ? G[threadIdx.x] : 0.0;
+    }
+    __syncthreads();
+    if (threadIdx.x < 64)
+    {
+      const unsigned nw = mgs_la_close<0, 8, L>(sh, sh.S, 0u);
+      if (threadIdx.x == 0) sh.word = nw;
+    }
+  }
+  else
+  {
+    if (threadIdx.x < 64) sh.S[threadIdx.x] = a.Sfin[threadIdx.x];
+    if (threadIdx.x == 0) sh.word = a.st[a.launch & 1];
+  }
   __syncthreads();
   unsigned nb = 0;
   while ((sh.word & 15u) < 8u)  // (uniform: sh.word changes only between barriers)
@@ -1268,7 +1293,7 @@ void mgs_la_enqueue(MgsLaArgs a, int G, bool coop, hipStream_t s)
     // device every workgroup is resident at once, and beside other streams' kernels the ones not
     // yet resident only wait for CUs those kernels release -- the barriers need no cooperative
     // launch (whose host call measured ~30 us per orthonormalisation, profiles/r05r_ortho.jsonl)
-    hipLaunchKernelGGL(k_mgs_la_final<L>, dim3(G), dim3(kMgsLaThreads), 0, s, a);
+    hipLaunchKernelGGL(k_mgs_la_final<L>, dim3(G), dim3(kMgsLaThreads), 0, s, a, (const double *)nullptr);
     EIG_HIP(hipGetLastError());
     return;
   }
@@ -1290,6 +1315,7 @@ bool launch_mgs_lookahead(eig_ctx_t ctx, i64 n, double *Qb, int L, bool coop, hi
   char *buf = (char *)ctx_buffer(ctx, 11, bytes);
   if (fresh) EIG_HIP(hipMemsetAsync(buf, 0, bytes, s));  // (the sticky error word starts clear)
   if (coop) ctx->mgs_la_armed = true;
+  ctx->mgs_bar_clean = nullptr;  // (this call's last launch leaves the barrier word set)
   MgsLaArgs a{n, Qb, 0, reinterpret_cast<unsigned *>(buf + 64 * sizeof(double)), reinterpret_cast<double *>(buf),
               ctx->red.partials, ctx->red.ticket(0)};
   const int G = grid_for(n, kMgsLaThreads * 2, std::min(kMgsLaGrid, ctx->num_cu > 0 ? ctx->num_cu : kMgsLaGrid));
@@ -1299,20 +1325,35 @@ bool launch_mgs_lookahead(eig_ctx_t ctx, i64 n, double *Qb, int L, bool coop, hi
   return true;
 }
 
-bool launch_mgs_lookahead_gram(eig_ctx_t ctx, i64 n, double *Qb, const double *G, hipStream_t s)
+unsigned *mgs_lookahead_barrier(eig_ctx_t ctx)
 {
-  if (n <= 0 || !G) return false;
   const size_t bytes = 64 * sizeof(double) + 64 * sizeof(unsigned);
   const bool fresh = (int)ctx->pool.size() <= 11 || ctx->pool[11].second < bytes;
   char *buf = (char *)ctx_buffer(ctx, 11, bytes);
-  if (fresh) EIG_HIP(hipMemsetAsync(buf, 0, bytes, s));
+  if (fresh) EIG_HIP(hipMemsetAsync(buf, 0, bytes, ctx->stream));  // (the sticky error word starts clear)
+  return reinterpret_cast<unsigned *>(buf + 64 * sizeof(double)) + kMgsLaBar;
+}
+
+bool launch_mgs_lookahead_gram(eig_ctx_t ctx, i64 n, double *Qb, const double *G, hipStream_t s)
+{
+  if (n <= 0 || !G) return false;
+  unsigned *bar = mgs_lookahead_barrier(ctx);
+  char *buf = reinterpret_cast<char *>(bar - kMgsLaBar) - 64 * sizeof(double);
   ctx->mgs_la_armed = true;
-  MgsLaArgs a{n, Qb, 0, reinterpret_cast<unsigned *>(buf + 64 * sizeof(double)), reinterpret_cast<double *>(buf),
-              ctx->red.partials, ctx->red.ticket(0)};
+  MgsLaArgs a{n, Qb, 1, bar - kMgsLaBar, reinterpret_cast<double *>(buf), ctx->red.partials, ctx->red.ticket(0)};
   const int G8 = grid_for(n, kMgsLaThreads * 2, std::min(kMgsLaGrid, ctx->num_cu > 0 ? ctx->num_cu : kMgsLaGrid));
-  hipLaunchKernelGGL(k_mgs_la_gram, dim3(1), dim3(kMgsLaThreads), 0, s, a, G);
-  a.launch = 1;
-  hipLaunchKernelGGL(k_mgs_la_final<8>, dim3(G8), dim3(kMgsLaThreads), 0, s, a);
+  if (ctx->mgs_bar_clean == G)
+  {
+    // the product that summed G zeroed the last launch's barrier word (its last workgroup): the
+    // window is finished in the last launch's prologue, ONE launch per block
+    ctx->mgs_bar_clean = nullptr;
+    hipLaunchKernelGGL(k_mgs_la_final<8>, dim3(G8), dim3(kMgsLaThreads), 0, s, a, G);
+  }
+  else
+  {
+    hipLaunchKernelGGL(k_mgs_la_gram, dim3(1), dim3(kMgsLaThreads), 0, s, a, G);
+    hipLaunchKernelGGL(k_mgs_la_final<8>, dim3(G8), dim3(kMgsLaThreads), 0, s, a, (const double *)nullptr);
+  }
   EIG_HIP(hipGetLastError());
   return true;
 }

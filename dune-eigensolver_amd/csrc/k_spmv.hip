@@ -2273,7 +2273,7 @@ __global__ __launch_bounds__(kStreamThreads, DOT == 2 ? 5 : DOT ? 6 : 8) void k_
                                                                    MarchPlan mp, const double *__restrict__ X,
                                                                    double *__restrict__ Y, double *dp = nullptr,
                                                                    double *part = nullptr, unsigned *tick = nullptr,
-                                                                   double *gram = nullptr)
+                                                                   double *gram = nullptr, unsigned *zero_word = nullptr)
 {
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int qb = (int)blockIdx.y;  // column block
@@ -2380,6 +2380,7 @@ __global__ __launch_bounds__(kStreamThreads, DOT == 2 ? 5 : DOT ? 6 : 8) void k_
     {
       if (threadIdx.x < 64) gram[threadIdx.x] = gt[threadIdx.x];
       if (threadIdx.x < 8) dp[threadIdx.x] = gt[64 + threadIdx.x];
+      if (threadIdx.x == 0 && zero_word) *zero_word = 0u;  // (the next MGS's barrier word)
     }
   }
   else if constexpr (DOT)
@@ -3240,7 +3241,7 @@ bool launch_spmm_march_dot(const eig_mat_s &A, i64 m, const double *X, double *Y
 
 // The same with the window Gram of Y (k_spmm8_march<MT, 2>), m = 8 only.
 bool launch_spmm_march_dot_gram(const eig_mat_s &A, i64 m, const double *X, double *Y, double *dp, double *gram,
-                                ReduceWS red, hipStream_t s)
+                                ReduceWS red, hipStream_t s, unsigned *zero_word)
 {
   if (A.br != 1 || A.bc != 1 || m != 8 || A.ctx->distributed()) return false;
   const int mode = image_mode(A);
@@ -3252,10 +3253,10 @@ bool launch_spmm_march_dot_gram(const eig_mat_s &A, i64 m, const double *X, doub
   if ((i64)grid.x * 72 + 8 * 72 > (i64)kMaxRedBlocks * kMaxRedVals) return false;
   if (mode == kSymN8)
     hipLaunchKernelGGL((k_spmm8_march<uint8_t, 2>), grid, dim3(kStreamThreads), 0, s, A.nb_rows, A.own_offset,
-                       A.window, sell_b1(A), mp, X, Y, dp, red.partials, red.ticket(0), gram);
+                       A.window, sell_b1(A), mp, X, Y, dp, red.partials, red.ticket(0), gram, zero_word);
   else
     hipLaunchKernelGGL((k_spmm8_march<uint32_t, 2>), grid, dim3(kStreamThreads), 0, s, A.nb_rows, A.own_offset,
-                       A.window, sell_b1(A), mp, X, Y, dp, red.partials, red.ticket(0), gram);
+                       A.window, sell_b1(A), mp, X, Y, dp, red.partials, red.ticket(0), gram, zero_word);
   return true;
 }
 
