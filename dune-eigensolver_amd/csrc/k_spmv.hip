@@ -1490,8 +1490,11 @@ __device__ __forceinline__ void march_rows_geo2(const SellB1 &A, const MarchPlan
 // gathers of variant 15, whose mirrored value gathers cost 13 us at 256^3 (section 4e ablation).  Every
 // row sums the same products in the same order as variant 15 (bitwise its rows); the launch's three
 // sums add the rows in another order (each lane adds its two rows per plane).
-// waves per SIMD of the 2-line fused march (variants 22 / 23 / 24) and whether it is the default
-constexpr bool kMarch2lDefault = false;
+// The 2-line fused march is the default on ranks of at least EIG_MARCH_2L_MIN_ROWS rows: 256^3 (16.8 M
+// rows) 206.5-206.8 us vs 223.5 us for variant 15 (profiles/r06e_sweep256_2lines.jsonl, 0.65 of HBM),
+// but 2 M-row grids (128^3, one rank's 256^2 x 32 slab) 28.2-28.4 vs 27.7-27.9 us: fewer, longer
+// wave chains cost more there than the halved gathers save.
+constexpr bool kMarch2lDefault = true;
 constexpr bool is_march2l(int uni) { return uni == 22 || uni == 23 || uni == 24; }
 
 template <class X, class EPI, class PRE>
@@ -2715,8 +2718,9 @@ static int march_uniform(const eig_mat_s &A, bool fused = false, i64 nplanes = 0
     // 22: two grid lines per wave (7-point bands on grids of an even line count)
     const bool two = A.sym_nd == 7 && A.sym_gy % 2 == 0 && A.sym_gy > 0;
     if (tp >= 16 && tp <= 18) return two ? tp + 6 : 15;
+    const bool big = A.nb_rows >= EIG_MARCH_2L_MIN_ROWS;
     return tp == 9 ? 10 : tp == 10 ? 11 : tp == 12 ? 14 : tp == 13 ? 15 : tp == 15 ? 18
-         : fused ? (A.sym_nd == 7 ? (two && kMarch2lDefault ? 22 : 15) : 10) : 0;
+         : fused ? (A.sym_nd == 7 ? (two && big && kMarch2lDefault ? 22 : 15) : 10) : 0;
   }
   if (!A.sym_geo) return 1;
   int u = A.tune_march_prefetch > 0 ? 1 + A.tune_march_prefetch : geo2 ? 7 : 4;

@@ -270,7 +270,9 @@ enum { EIG_TUNE_MARCH_RUNS = 1, EIG_TUNE_BOX_SEGS = 2, EIG_TUNE_MARCH_PREFETCH =
  * 16 / 17 / 18 = that pack marched TWO grid lines per wave (march variants 22 / 23 / 24: 5 / 4 / 6
  * waves per SIMD; 7-point bands, an even line count) -- the +-nx neighbours across the pair from
  * registers, half the gathers; the fused step's sums then add the rows in another order;
- * 0 = automatic.  Bitwise the same rows for every value. */
+ * 0 = automatic: the fused step on 3-D value images takes variant 22 on ranks of at least
+ * EIG_MARCH_2L_MIN_ROWS owned rows, else 15.  Bitwise the same rows for every value. */
+#define EIG_MARCH_2L_MIN_ROWS 8388608
 int eig_mat_tune(eig_mat_t mat, int key, int value);
 
 /* a13: A += shift*I on the diagonal of every diagonal block (eigensolver.hh:59-66). */

@@ -216,7 +216,7 @@ def v256(ctx):
 def test_value_march_256_bitwise(ctx, v256):
     """Configuration size (C4's grid, variable coefficients): eig_mv bitwise the oracle row loop."""
     N, M, A = v256
-    assert M.info.march_variant == 15 and M.info.march_variant_mv == 0
+    assert M.info.march_variant == 22 and M.info.march_variant_mv == 0
     x = np.random.default_rng(9).standard_normal(N ** 3)
     assert np.array_equal(M.mv_host(x), oracle.csr_mv(A, x))
 
@@ -242,11 +242,12 @@ def fused_vs_oracle(M, A, steps):
 
 @pytest.mark.gpu
 def test_value_march_256_lanczos(ctx, v256):
-    """The benchmark step on the value-streaming image at 256^3 (kind 8, march variant 15): 60 fused
-    steps vs orc_lanczos_fused and 4 classic steps vs orc_lanczos_rotating, rtol 1e-12."""
+    """The benchmark step on the value-streaming image at 256^3 (kind 8, march variant 22 -- the
+    2-line march, the default from EIG_MARCH_2L_MIN_ROWS rows): 60 fused steps vs orc_lanczos_fused
+    and 4 classic steps vs orc_lanczos_rotating, rtol 1e-12."""
     N, M, A = v256
     n = N ** 3
-    assert M.info.march_variant == 15
+    assert M.info.march_variant == 22
     U0 = fused_vs_oracle(M, A, FULL_STEPS)
     ca, cb, _ = eigmi.lanczos_run(M, 4, seed=123)
     u1, u2 = np.zeros(n), np.zeros(n)
@@ -271,20 +272,21 @@ def test_bench_image_256_spmv_bitwise(ctx, p256a):
     """eig_mv (BCRSMatrix::mv, kernels_cpp.hh:596-621) on the benched image, bitwise the oracle row loop."""
     N, M, A = p256a
     info = M.info
-    assert info.sym_uniform == 0 and info.march_variant == 15 and info.march_variant_mv == 0
+    assert info.sym_uniform == 0 and info.march_variant == 22 and info.march_variant_mv == 0
     x = np.random.default_rng(21).standard_normal(N ** 3)
     assert np.array_equal(M.mv_host(x), oracle.csr_mv(A, x))
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("pf", [16, 17])
-def test_bench_image_256_two_lines(ctx, p256a, pf):
-    """The benched image with the 2-line value march (variants 22 / 23): eig_mv bitwise the oracle row
-    loop and 60 fused steps vs orc_lanczos_fused, rtol 1e-12."""
+@pytest.mark.parametrize("pf", [13, 17])
+def test_bench_image_256_other_variants(ctx, p256a, pf):
+    """The benched image with variant 15 (one line per wave: the default below EIG_MARCH_2L_MIN_ROWS
+    rows, i.e. on the ranks of the 8-GPU split) and variant 23 (2 lines, 4 waves per SIMD): eig_mv
+    bitwise the oracle row loop and 60 fused steps vs orc_lanczos_fused, rtol 1e-12."""
     N, M, A = p256a
     M.tune(march_prefetch=pf)
     try:
-        assert M.info.march_variant == pf + 6 and M.info.march_variant_mv == pf + 6
+        assert M.info.march_variant == {13: 15, 17: 23}[pf] and M.info.march_variant_mv == {13: 15, 17: 23}[pf]
         x = np.random.default_rng(22).standard_normal(N ** 3)
         assert np.array_equal(M.mv_host(x), oracle.csr_mv(A, x))
         fused_vs_oracle(M, A, FULL_STEPS)

@@ -3,13 +3,16 @@ virtual ranks over the loopback hub, each running the benchmark's step kernel on
 (tests/loopback_c4_worker.py).  Against the CPU restatement on the global matrix: distributed eig_mv
 bitwise oracle.csr_mv (kernels_cpp.hh:596-621), 60 fused steps within rtol 1e-12 of
 orc_lanczos_fused, under split and whole halo launches, with the loopback allreduce and with the
-allreduce inside the step kernel (EIG_AR_MAILBOX_STEP); the value-march variant 15 on every rank."""
+allreduce inside the step kernel (EIG_AR_MAILBOX_STEP); on every rank the value march the bench runs at
+that rank size (variant 15 on the 2 M-row slabs of the 8-way split, the 2-line variant 22 on larger ranks)."""
 import json
 import os
 import subprocess
 import sys
 
 import pytest
+
+import eigmi
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 N, STEPS, PS = 256, 60, (2, 4, 8)
@@ -42,8 +45,11 @@ def test_c4_partition_256(c4_lines, P):
         assert rk["error"] is None, rk
         assert rk["rows"] == N * N * (N // P)
         assert rk["halo"] == (N * N if r > 0 else 0) + (N * N if r < P - 1 else 0)
-        # the benched kernel on every rank: the fused value march, variant 15, values streamed
-        assert rk["kernel"] == "k_lanczos_fused_march" and rk["variant"] == 15 and rk["uniform"] == 0, rk
+        # the benched kernel on every rank: the fused value march with the values streamed -- variant 15
+        # on the 2 M-row slabs of the 8-way split (the bench's N = 8 ranks), the 2-line march (22) on
+        # ranks of at least EIG_MARCH_2L_MIN_ROWS rows
+        want = 22 if rk["rows"] >= eigmi.MARCH_2L_MIN_ROWS else 15
+        assert rk["kernel"] == "k_lanczos_fused_march" and rk["variant"] == want and rk["uniform"] == 0, rk
         assert rk["mv_bitwise"], f"rank {r}: distributed eig_mv not bitwise the oracle row loop"
         assert set(rk["rel"]) == set(RUNS)
         for key in RUNS:
