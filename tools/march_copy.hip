@@ -482,6 +482,89 @@ __global__ __launch_bounds__(kThreads, W) void k_vabl2(int n, int D, int nx, int
   }
 }
 
+// The same with LN grid lines per wave (LN = 2 reproduces k_vabl2's loads): lines y0 .. y0 + LN - 1,
+// only line y0 - 1's operand / mirrored value and line y0 + LN's operand gathered
+template <int LN, int W>
+__global__ __launch_bounds__(kThreads, W) void k_vablN(int n, int D, int nx, int ncol, int nseg, int nplanes,
+                                                       const dpair *__restrict__ P, const dpair *__restrict__ V,
+                                                       dpair *__restrict__ Q, double *__restrict__ sums, double c)
+{
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int ncolN = ncol / LN, xc = nx / 64;
+  const int item = swz() * kW + wave;
+  if (item >= ncolN * nseg) return;
+  const int colN = item % ncolN, seg = item / ncolN;
+  const int z0 = seg * nplanes / nseg, z1 = (seg + 1) * nplanes / nseg;
+  const int lastrow = n - 1;
+  auto cl = [&](int g) { return g < 0 ? 0 : (g > lastrow ? lastrow : g); };
+  const int line0 = LN * (colN / xc);
+  int w = line0 * nx + (colN % xc) * 64 + lane + z0 * D;
+  dpair cur[LN], prev[LN];
+#pragma unroll
+  for (int l = 0; l < LN; ++l)
+  {
+    cur[l] = P[cl(w + l * nx)];
+    prev[l] = P[cl(w + l * nx - D)];
+  }
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+  auto uk = [&](dpair p) { return p.x - c * p.y; };
+  for (int z = z0; z < z1; ++z, w += D)
+  {
+    dpair pd[LN], a[LN], b[LN], e[LN];
+    double m1e[LN];
+#pragma unroll
+    for (int l = 0; l < LN; ++l)
+    {
+      pd[l] = P[cl(w + l * nx + D)];
+      a[l] = __builtin_nontemporal_load(V + w + l * nx);
+      b[l] = V[n + w + l * nx];
+      e[l] = dpair{0.0, 0.0};
+      if (lane == 0 || lane == 63) e[l] = P[cl(lane == 0 ? w + l * nx - 1 : w + l * nx + 1)];
+      m1e[l] = lane == 0 ? V[n + cl(w + l * nx - 1)].x : 0.0;
+    }
+    const dpair u = P[cl(w - nx)], v = P[cl(w + LN * nx)];
+    const double mnx0 = V[n + cl(w - nx)].y;
+    double vc[LN];
+#pragma unroll
+    for (int l = 0; l < LN; ++l) vc[l] = uk(cur[l]);
+#pragma unroll
+    for (int l = 0; l < LN; ++l)
+    {
+      const double vl = __shfl_up(vc[l], 1, 64), vr = __shfl_down(vc[l], 1, 64);
+      const double am1 = lane == 0 ? m1e[l] : __shfl_up(b[l].x, 1, 64);
+      const double mnx = l == 0 ? mnx0 : b[l > 0 ? l - 1 : 0].y;
+      const double vn = l == 0 ? uk(u) : vc[l > 0 ? l - 1 : 0];
+      const double vq = l == LN - 1 ? uk(v) : vc[l < LN - 1 ? l + 1 : 0];
+      double acc = 0.0;
+      acc += b[l].y * uk(prev[l]);
+      acc += mnx * vn;
+      acc += am1 * (lane == 0 ? uk(e[l]) : vl);
+      acc += a[l].x * vc[l];
+      acc += b[l].x * (lane == 63 ? uk(e[l]) : vr);
+      acc += b[l].y * vq;
+      acc += a[l].x * uk(pd[l]);
+      const double t = (acc - 0.5 * vc[l]) * 0.25 - 0.125 * cur[l].y;
+      s0 += t * vc[l];
+      s1 += t * t;
+      s2 += vc[l] * vc[l];
+      __builtin_nontemporal_store(dpair{t, vc[l]}, Q + w + l * nx);
+    }
+#pragma unroll
+    for (int l = 0; l < LN; ++l)
+    {
+      prev[l] = cur[l];
+      cur[l] = pd[l];
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1)
+  {
+    s0 += __shfl_down(s0, off, 64);
+    s1 += __shfl_down(s1, off, 64);
+    s2 += __shfl_down(s2, off, 64);
+  }
+  if (lane == 0) atomicAdd(sums + 8, s0 + s1 + s2);  // (no tail: compare with abl_full_notail_w6)
+}
+
 // two columns per wave: c and c + ncol / 2 (ncol even)
 __global__ __launch_bounds__(kThreads, 8) void k_march2(int n, int D, int ncol, int nseg, int nplanes,
                                                         const dpair *__restrict__ P, dpair *__restrict__ Q)
@@ -652,6 +735,13 @@ int main(int argc, char **argv)
       outv("abl_full_tail_2lines_w4", nseg, time([&] { k_vabl2<4><<<G2, kThreads>>>(n, D, nx, ncol, nseg, NZ, src(), V, dst(), sums, 0.5); }));
       outv("abl_full_tail_2lines_w5", nseg, time([&] { k_vabl2<5><<<G2, kThreads>>>(n, D, nx, ncol, nseg, NZ, src(), V, dst(), sums, 0.5); }));
       outv("abl_full_tail_2lines_w6", nseg, time([&] { k_vabl2<6><<<G2, kThreads>>>(n, D, nx, ncol, nseg, NZ, src(), V, dst(), sums, 0.5); }));
+      for (int ns : {4, 8, 16})
+      {
+        const int G4 = ((ncol / 4) * ns + kW - 1) / kW, GN2 = ((ncol / 2) * ns + kW - 1) / kW;
+        outv("abl_notail_lines2_w5", ns, time([&] { k_vablN<2, 5><<<GN2, kThreads>>>(n, D, nx, ncol, ns, NZ, src(), V, dst(), sums, 0.5); }));
+        outv("abl_notail_lines4_w3", ns, time([&] { k_vablN<4, 3><<<G4, kThreads>>>(n, D, nx, ncol, ns, NZ, src(), V, dst(), sums, 0.5); }));
+        outv("abl_notail_lines4_w4", ns, time([&] { k_vablN<4, 4><<<G4, kThreads>>>(n, D, nx, ncol, ns, NZ, src(), V, dst(), sums, 0.5); }));
+      }
       outv("abl_full_tail_w6_again", nseg, time([&] { k_vabl<true, true, true, 6, true, 1, true><<<G, kThreads>>>(n, D, nx, ncol, nseg, NZ, src(), V, dst(), sums, 0.5); }));
       CK(hipFree(sums));
     }
