@@ -347,6 +347,7 @@ extern "C" int eig_ctx_destroy(eig_ctx_t ctx)
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   mailbox_free(ctx);
+  if (ctx->mgs_err_host) (void)hipHostFree(ctx->mgs_err_host);
   if (ctx->comm_red) (void)ncclCommDestroy(ctx->comm_red);
   if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
   ctx->loop = nullptr;  // the hub is owned by eig_loopback_create / _destroy

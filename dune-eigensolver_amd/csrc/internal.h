@@ -157,6 +157,9 @@ struct eig_ctx_s {
   // a look-ahead MGS last launch (grid barriers without a cooperative launch) has been enqueued
   // since the last mgs_lookahead_check: its sticky error word must be read at the next sync point
   bool mgs_la_armed = false;
+  // its sticky error word in page-locked, device-mapped host memory: the kernel stores into it, the
+  // host reads it after any stream synchronisation without a copy (allocated at first use)
+  int *mgs_err_host = nullptr, *mgs_err_dev = nullptr;
   // the window Gram whose product also zeroed the look-ahead MGS's barrier word (launch_spmm_dot_gram_mv8);
   // consumed by the next launch_mgs_lookahead_gram of that Gram
   const double *mgs_bar_clean = nullptr;

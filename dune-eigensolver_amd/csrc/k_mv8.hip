@@ -804,13 +804,14 @@ bool launch_mgs_coop(eig_ctx_t ctx, i64 n, double *Qb, double *Ssum, hipStream_t
 // State (context scratch, slot 11): Sfin[8][8] the finished S rows (S[k][k] = 1/sqrt, S[k][j] =
 // s'/s'[k][k], 0 below); words st[0..1] by launch parity (bits 0-3 F, bit 4 written, bits 8-15 read
 // passes so far: launch l reads word l & 1, exactly one thread writes word (l + 1) & 1), st[2] the
-// last call's final word, st[32] the last launch's barrier counter, st[33] its error flag.
+// last call's final word, st[32] the last launch's barrier counter; the error flag is a host-mapped word
+// (eig_ctx_s::mgs_err_dev, sticky until the host reads it at a synchronisation).
 // ---------------------------------------------------------------------------------------------
 constexpr int kMgsLaThreads = 512;
 constexpr int kMgsLaGrid = 256;  // one workgroup per CU: the tails sum 256 x 8 W partials
 constexpr double kMgsLaTau = 1.0 / 16;
 constexpr unsigned kMgsLaWritten = 16u;
-constexpr int kMgsLaBar = 32, kMgsLaErr = 33, kMgsLaLast = 2;  // st[] word indices
+constexpr int kMgsLaBar = 32, kMgsLaLast = 2;  // st[] word indices
 
 struct MgsLaArgs {
   i64 n;
@@ -820,6 +821,7 @@ struct MgsLaArgs {
   double *Sfin;
   double *partials;
   unsigned *ticket;
+  int *err;  // sticky error word (host-mapped: eig_ctx_s::mgs_err_dev)
 };
 
 template <int L>
@@ -1118,7 +1120,7 @@ __global__ __launch_bounds__(kMgsLaThreads) void k_mgs_la(MgsLaArgs a)
   __shared__ MgsLaShared<L> sh;  // (one copy for the nine pass bodies)
   const unsigned word = a.launch == 0 ? 0u : a.st[a.launch & 1];
   if (a.launch == 0 && blockIdx.x == 0 && threadIdx.x == 0)
-    a.st[kMgsLaBar] = 0u;  // for the last launch of this call (st[kMgsLaErr] is sticky: the host clears it)
+    a.st[kMgsLaBar] = 0u;  // for the last launch of this call (the error word is sticky: the host clears it)
   if (word & kMgsLaWritten)
   {
     if (blockIdx.x == 0 && threadIdx.x == 0) a.st[(a.launch + 1) & 1] = word;
@@ -1162,7 +1164,7 @@ __device__ __forceinline__ bool mgs_la_read_coop(const MgsLaArgs a, MgsLaShared<
   if (threadIdx.x < E) st_sc1(&buf[(size_t)blockIdx.x * 64 + threadIdx.x], part);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   ++nb;
-  if (!mgs_grid_barrier(a.st + kMgsLaBar, nb, reinterpret_cast<int *>(a.st + kMgsLaErr))) return false;
+  if (!mgs_grid_barrier(a.st + kMgsLaBar, nb, a.err)) return false;
   mgs_la_gather<W, L>(buf, 64, gridDim.x, sh);
   if (threadIdx.x < 64)
   {
@@ -1265,6 +1267,8 @@ __global__ __launch_bounds__(kMgsLaThreads) void k_mgs_la_gram(MgsLaArgs a, cons
   }
 }
 
+static int *mgs_err_word(eig_ctx_t ctx);
+
 int mgs_lookahead_default()
 {
   static const int L = [] {
@@ -1317,12 +1321,23 @@ bool launch_mgs_lookahead(eig_ctx_t ctx, i64 n, double *Qb, int L, bool coop, hi
   if (coop) ctx->mgs_la_armed = true;
   ctx->mgs_bar_clean = nullptr;  // (this call's last launch leaves the barrier word set)
   MgsLaArgs a{n, Qb, 0, reinterpret_cast<unsigned *>(buf + 64 * sizeof(double)), reinterpret_cast<double *>(buf),
-              ctx->red.partials, ctx->red.ticket(0)};
+              ctx->red.partials, ctx->red.ticket(0), mgs_err_word(ctx)};
   const int G = grid_for(n, kMgsLaThreads * 2, std::min(kMgsLaGrid, ctx->num_cu > 0 ? ctx->num_cu : kMgsLaGrid));
   if (L >= 8) mgs_la_enqueue<8>(a, G, coop, s);
   else if (L >= 4) mgs_la_enqueue<4>(a, G, coop, s);
   else mgs_la_enqueue<2>(a, G, coop, s);
   return true;
+}
+
+static int *mgs_err_word(eig_ctx_t ctx)
+{
+  if (!ctx->mgs_err_host)
+  {
+    EIG_HIP(hipHostMalloc(reinterpret_cast<void **>(&ctx->mgs_err_host), sizeof(int), hipHostMallocMapped));
+    *ctx->mgs_err_host = 0;
+    EIG_HIP(hipHostGetDevicePointer(reinterpret_cast<void **>(&ctx->mgs_err_dev), ctx->mgs_err_host, 0));
+  }
+  return ctx->mgs_err_dev;
 }
 
 unsigned *mgs_lookahead_barrier(eig_ctx_t ctx)
@@ -1340,7 +1355,8 @@ bool launch_mgs_lookahead_gram(eig_ctx_t ctx, i64 n, double *Qb, const double *G
   unsigned *bar = mgs_lookahead_barrier(ctx);
   char *buf = reinterpret_cast<char *>(bar - kMgsLaBar) - 64 * sizeof(double);
   ctx->mgs_la_armed = true;
-  MgsLaArgs a{n, Qb, 1, bar - kMgsLaBar, reinterpret_cast<double *>(buf), ctx->red.partials, ctx->red.ticket(0)};
+  MgsLaArgs a{n, Qb, 1, bar - kMgsLaBar, reinterpret_cast<double *>(buf), ctx->red.partials, ctx->red.ticket(0),
+              mgs_err_word(ctx)};
   const int G8 = grid_for(n, kMgsLaThreads * 2, std::min(kMgsLaGrid, ctx->num_cu > 0 ? ctx->num_cu : kMgsLaGrid));
   if (ctx->mgs_bar_clean == G)
   {
@@ -1366,22 +1382,18 @@ int mgs_lookahead_passes(eig_ctx_t ctx)
   unsigned w[64] = {};
   EIG_HIP(hipMemcpyAsync(w, buf + 64 * sizeof(double), sizeof(w), hipMemcpyDeviceToHost, ctx->stream));
   EIG_HIP(hipStreamSynchronize(ctx->stream));
-  if (w[kMgsLaErr]) return -2;
+  if (ctx->mgs_err_host && *reinterpret_cast<volatile int *>(ctx->mgs_err_host)) return -2;
   return (w[kMgsLaLast] & kMgsLaWritten) ? (int)((w[kMgsLaLast] >> 8) & 255u) : -1;
 }
 
 void mgs_lookahead_check(eig_ctx_t ctx)
 {
+  // (called after a synchronisation of the stream: the word is host memory, no copy, no launch)
   if (!ctx->mgs_la_armed) return;
   ctx->mgs_la_armed = false;
-  unsigned *err = reinterpret_cast<unsigned *>((char *)ctx_buffer(ctx, 11, 64 * sizeof(double) + 64 * sizeof(unsigned)) +
-                                               64 * sizeof(double)) + kMgsLaErr;
-  unsigned e = 0;
-  EIG_HIP(hipMemcpyAsync(&e, err, sizeof(e), hipMemcpyDeviceToHost, ctx->stream));
-  EIG_HIP(hipStreamSynchronize(ctx->stream));
-  if (!e) return;
-  EIG_HIP(hipMemsetAsync(err, 0, sizeof(unsigned), ctx->stream));
-  EIG_HIP(hipStreamSynchronize(ctx->stream));
+  volatile int *e = ctx->mgs_err_host;
+  if (!e || !*e) return;
+  *e = 0;
   EIG_CHECK(false, EIG_ERR_HIP,
             "orthonormalize_blocked: a look-ahead MGS grid barrier timed out (workgroups not co-resident); "
             "the block was poisoned with NaN");
