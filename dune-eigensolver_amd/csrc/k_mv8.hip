@@ -1040,49 +1040,14 @@ __device__ __forceinline__ unsigned mgs_la_close(MgsLaShared<L> &sh, double *S, 
 }
 
 // An ordinary read launch: rows, workgroup partials, ticket; the last workgroup finishes the window.
-// The first read pass of an 8-wide window (F = 0, L = 8: no replay) in the quad layout of the SpMM
-// epilogues (round 6): 4 lanes per row, one 16-B column pair each, the row's other values by DPP
-// (reduce_dev.h quad_gram_add), 16 accumulators per lane instead of the row-per-lane form's 36
-// products over 8 held values.  Returns this thread's slot of the
-// workgroup's 64 window sums (threads < 64; the same slots as mgs_la_block).
-template <int L>
-__device__ __forceinline__ double mgs_la_rows0_quad(const MgsLaArgs a)
-{
-  constexpr int U = 8;  // 8 rows per lane in flight: 64 KB per workgroup, as the row-per-lane form's ping-pong
-  __shared__ double scratch[kMgsLaThreads / 64 * 72], out[72];
-  const int cp = threadIdx.x & 3;
-  double g[2][8] = {};
-  const i64 stride = (i64)gridDim.x * (kMgsLaThreads / 4);
-  for (i64 i0 = ((i64)blockIdx.x * kMgsLaThreads + threadIdx.x) >> 2; i0 < a.n; i0 += U * stride)
-  {
-    double2 v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-    {
-      const i64 i = i0 + u * stride;  // (a quad's 4 lanes share i: uniform per quad)
-      v[u] = i < a.n ? reinterpret_cast<const double2 *>(a.Qb + i * 8)[cp] : make_double2(0.0, 0.0);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) quad_gram_add(g, v[u].x, v[u].y);
-  }
-  quad_gram_block<kMgsLaThreads>(g, 0.0, 0.0, scratch, out);
-  return threadIdx.x < 64 ? out[threadIdx.x] : 0.0;
-}
-
 template <int F, int L>
 __device__ __forceinline__ void mgs_la_read(const MgsLaArgs a, unsigned word, MgsLaShared<L> &sh)
 {
   constexpr int W = (8 - F) < L ? (8 - F) : L;
   constexpr int E = 8 * W;
-  double part;
-  if constexpr (F == 0 && W == 8)
-    part = mgs_la_rows0_quad<L>(a);
-  else
-  {
-    double acc[W][8];
-    mgs_la_rows<F, W, 2>(a.n, a.Qb, a.Sfin, acc);
-    part = mgs_la_block<W, L>(acc, sh);
-  }
+  double acc[W][8];
+  mgs_la_rows<F, W, 2>(a.n, a.Qb, a.Sfin, acc);
+  const double part = mgs_la_block<W, L>(acc, sh);
   const unsigned bid = blockIdx.x, nblk = gridDim.x;
   if (threadIdx.x < E) st_sc1(&a.partials[(size_t)bid * E + threadIdx.x], part);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
