@@ -267,3 +267,47 @@ def test_b_orthonormalize(ctx, kind):
     assert orth < 1e-10
     assert diff < 1e-12
     assert abs(norm.get(1)[0] - refnorm) <= 1e-12 * abs(refnorm)
+
+
+@pytest.mark.parametrize("name", ["poisson3d_20_class", "varcoef3d_24_march", "laplace2d_64", "random_sell"])
+def test_spmm_dot_gram_pair(ctx, name):
+    """The StandardLargest pair (eigensolver.hh:78-85, m = 8): eig_spmm_dot_gram_mv8's product BITWISE the
+    reference SpMM (kernels_cpp.hh:626-657) on every image -- the row-class box kernel, the band march,
+    and the fallback (product + panel Gram) on a SELL-only matrix --, its diagonal dots and window Gram
+    within the summation-order bound of the restated dot_products_diagonal_blocked / _all_blocked; then
+    eig_orthonormalize_gram_mv8 from that Gram within 1e-12 of the restated orthonormalize_blocked."""
+    import scipy.sparse as sp
+    flags = 0
+    if name == "poisson3d_20_class":
+        A = oracle.poisson3d(20)
+    elif name == "varcoef3d_24_march":  # (no row classes: the band march with the Gram epilogue)
+        rp, c, v = eigmi.gen_matrix(eigmi.GEN_VARCOEF3D, 24)
+        A = oracle.CSR(24 ** 3, rp, c, v)
+    elif name == "laplace2d_64":
+        A = oracle.laplace2d(64)
+    else:
+        n0 = 3000
+        S = sp.random(n0, n0, density=6.0 / n0, random_state=8, format="csr")
+        S = (S + S.T + sp.identity(n0) * 8.0).tocsr()
+        S.sort_indices()
+        A = oracle.CSR(n0, S.indptr.astype(np.int64), S.indices.astype(np.int32), S.data.astype(np.float64))
+        flags = eigmi.MAT_NO_BAND
+    n, m = A.n, 8
+    M = eigmi.Matrix.from_bcsr(ctx, A.rowptr, A.col, A.val, flags=flags)
+    Xh = oracle.random_mv8(n, m, 31)
+    X, Y, dp, G = ctx.array(Xh), ctx.zeros(n * m), ctx.zeros(8), ctx.zeros(64)
+    eigmi.spmm_dot_gram_mv8(M, m, X, Y, dp, G)
+    Yh = Y.get()
+    assert np.array_equal(Yh, oracle.spmm_mv8(A, Xh, m))
+    Xc, Yc = oracle.mv_to_cols(Xh, n, m), oracle.mv_to_cols(Yh, n, m)
+    bound_d = 4 * n * 2.3e-16 * np.einsum("ij,ij->j", np.abs(Xc), np.abs(Yc))
+    assert np.all(np.abs(dp.get() - oracle.dot_diag_mv8(Xh, Yh, n, m)) <= bound_d)
+    Gref = oracle.gram_mv8(Yh, Yh, n, m)
+    bound_g = 4 * n * 2.3e-16 * (np.abs(Yc).T @ np.abs(Yc))
+    g = G.get().reshape(8, 8)
+    up = np.triu(np.ones((8, 8), bool))
+    assert np.all(np.abs(g - Gref)[up] <= bound_g[up])
+    eigmi.orthonormalize_gram_mv8(ctx, n, m, Y, G)
+    ctx.sync()
+    ref = oracle.orthonormalize_mv8(Yh, n, m)
+    assert np.abs(Y.get() - ref).max() < 1e-12 * max(1.0, np.abs(ref).max())
