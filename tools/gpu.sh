@@ -39,6 +39,11 @@
 #   cfgtrace             tools/bench_configs.py $CFG under a kernel trace -> $CFG_trace/
 #   ortho                a9 orthonormalize_blocked m = 8 / 32 at 128^3: look-ahead L = 8/4/2, stepwise replay, in-place -> ortho.jsonl
 #   orthopmc             the same under a kernel trace + FETCH_SIZE / WRITE_SIZE passes -> orthopmc/
+#   sweep2l              the fused step's 1-line (15) vs 2-line (22 / 23 / 24) value march: 256^3, 128^3, slab -> sweep2l_*.jsonl
+#   ablation             tools/march_copy.hip's value-march ablation incl. the 2- / N-line probes -> march_copy_abl.jsonl
+#   c4                   C4's row partition at 256^3 on 2 / 4 / 8 virtual ranks vs the oracle (tests/test_loopback_c4.py)
+#   slgram               StandardLargest with and without the fused window Gram (C1, C2) + one C2 solve's kernel trace
+#   detprobe             run-to-run determinism of the inverse-iteration pieces (tools/det_probe.py)
 #   xch                  the step's allreduce transports on one GPU (one-rank RCCL / mailbox / in-kernel
 #                        mailbox-step): slab and cube sweeps + the bench's N > 1 trial rehearsed -> xch_*.jsonl
 #
@@ -221,6 +226,25 @@ run_task() {
       prof_env
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/${CFG}_trace" -o trace -- \
         python3 tools/bench_configs.py $CFG > "$O/${CFG}_t.jsonl" 2> "$O/${CFG}_t.err" ;;
+    sweep2l)
+      timeout -k 10 400 python3 tools/lanczos_sweep.py --N 256 --rounds 3 --steps 40 \
+        --variants fused:arrays#13,fused:arrays#16,fused:arrays#17,fused:arrays#18,fused:arrays@8#16,fused:arrays@24#16,mv:arrays,mv:arrays#16 \
+        > "$O/sweep2l_256.jsonl" 2> "$O/sweep2l.err" && \
+      timeout -k 10 300 python3 tools/lanczos_sweep.py --N 128 --rounds 3 --steps 40 \
+        --variants fused:arrays#13,fused:arrays#16,fused:arrays#17 > "$O/sweep2l_128.jsonl" 2>> "$O/sweep2l.err" && \
+      timeout -k 10 300 python3 tools/lanczos_sweep.py --N 256 --slab 32 --rounds 3 --steps 40 \
+        --variants fused:arrays#13,fused:arrays#16,fused:arrays#17 > "$O/sweep2l_slab.jsonl" 2>> "$O/sweep2l.err" ;;
+    ablation)
+      timeout -k 10 300 tools/march_copy 256 values ablation 8 > "$O/march_copy_abl.jsonl" ;;
+    c4)
+      timeout -k 10 900 python -u -m pytest tests/test_loopback_c4.py -m gpu -v -s --timeout 900 --timeout-method thread \
+        > "$O/c4.log" 2>&1 ;;
+    slgram)
+      timeout -k 10 200 python -u tools/bench_configs.py c1 c2 > "$O/cfg_c12.jsonl" 2> "$O/cfg.err" && \
+      EIGMI_NO_SPMM_GRAM=1 timeout -k 10 200 python -u tools/bench_configs.py c1 c2 > "$O/cfg_c12_nogram.jsonl" 2>> "$O/cfg.err" && \
+      run_task sltrace ;;
+    detprobe)
+      timeout -k 10 300 python3 -u tools/det_probe.py > "$O/det_probe.log" 2>&1 ;;
     round)
       run_task tests && run_task smoke && run_task profile && run_task bench ;;
     *)
