@@ -41,12 +41,14 @@ static Rows gen(int N, int64_t b, int64_t cnt, int kind = 4)
   return r;
 }
 
-// Generalised block Lanczos (config C5) on the P1 pencil: Ritz values of `bsteps` steps, block 16.
+// Generalised block Lanczos (config C5) on the P1 pencil: Ritz values of `bsteps` steps, block 16 on
+// the constant-coefficient K / M (kinds 6 / 7); block 32 -- C5's k -- on the variable-coefficient
+// pencil (kinds 9 / 10, one coefficient per tetrahedron) when var is set.
 static const int kBlk = 16, kBsteps = 6, kBnev = 4;
-static void block_lanczos(eig_ctx_t ctx, int N, int64_t b, int64_t cnt, bool dist, double *ev)
+static void block_lanczos(eig_ctx_t ctx, int N, int64_t b, int64_t cnt, bool dist, double *ev, bool var = false)
 {
   const int64_t n = (int64_t)N * N * N;
-  Rows k = gen(N, b, cnt, 6), m = gen(N, b, cnt, 7);
+  Rows k = gen(N, b, cnt, var ? 9 : 6), m = gen(N, b, cnt, var ? 10 : 7);
   eig_mat_t K, M;
   if (dist)
   {
@@ -59,7 +61,7 @@ static void block_lanczos(eig_ctx_t ctx, int N, int64_t b, int64_t cnt, bool dis
     CK(eig_mat_create_bcsr(ctx, n, n, 1, 1, m.rp.data(), m.c.data(), m.v.data(), &M));
   }
   eig_blanczos_t bl;
-  CK(eig_blanczos_create(K, M, kBlk, kBsteps, 36, 0.5, 2.5, 123, &bl));
+  CK(eig_blanczos_create(K, M, var ? 32 : kBlk, kBsteps, 36, 0.5, 2.5, 123, &bl));
   CK(eig_blanczos_step(bl, kBsteps, nullptr));
   CK(eig_blanczos_ritz(bl, kBnev, EIG_WHICH_LA, ev, nullptr, nullptr));
   CK(eig_blanczos_destroy(bl));
@@ -321,7 +323,7 @@ int main(int argc, char **argv)
 
   // ---- serial reference on one context
   std::vector<double> x(n), y_ser(n), a_ser(steps), b_ser(steps + 1), ev_ser(nev), fa_ser(steps), fb_ser(steps + 1);
-  std::vector<double> bev_ser(kBnev);
+  std::vector<double> bev_ser(kBnev), vev_ser(kBnev);
   std::vector<double> ra_ser(kRsteps), rb_ser(kRsteps + 1), pra_ser(kRsteps), prb_ser(kRsteps + 1);
   // pipelined step (EIG_LANCZOS_PIPELINED: SpMV on t_{k-1} while the previous allreduce runs)
   std::vector<double> pa_ser(steps), pb_ser(steps + 1);
@@ -332,7 +334,7 @@ int main(int argc, char **argv)
   std::vector<std::vector<double>> ral(P, std::vector<double>(kRsteps)), rbe(P, std::vector<double>(kRsteps + 1));
   int rl_ser = 0;
   std::vector<int> rl(P, 0);
-  std::vector<std::vector<double>> bev(P, std::vector<double>(kBnev));
+  std::vector<std::vector<double>> bev(P, std::vector<double>(kBnev)), vev(P, std::vector<double>(kBnev));
   for (int64_t i = 0; i < n; ++i) x[i] = std::sin(0.37 * i) + 0.01 * (i % 7);
   {
     eig_ctx_t ctx;
@@ -352,6 +354,7 @@ int main(int argc, char **argv)
     fused_repair_run(A, pra_ser.data(), prb_ser.data(), &prl_ser, EIG_LANCZOS_PIPELINED);
     eig_mat_destroy(A);
     block_lanczos(ctx, N, 0, n, false, bev_ser.data());
+    block_lanczos(ctx, N, 0, n, false, vev_ser.data(), true);
     eig_ctx_destroy(ctx);
   }
 
@@ -429,6 +432,7 @@ int main(int argc, char **argv)
         eig_mat_destroy(B);
       }
       block_lanczos(ctx, N, b, cnt, true, bev[r].data());
+      block_lanczos(ctx, N, b, cnt, true, vev[r].data(), true);
       eig_free(ctx, dx);
       eig_free(ctx, dy);
       eig_free(ctx, dd);
@@ -540,6 +544,13 @@ int main(int argc, char **argv)
       if (std::fabs(bev[r][i] - bev_ser[i]) > 1e-10 * std::fabs(bev_ser[i]))
       {
         std::printf("FAIL rank %d: block Lanczos Ritz %d %.17g vs %.17g\n", r, i, bev[r][i], bev_ser[i]);
+        ++failures;
+      }
+    for (int i = 0; i < kBnev; ++i)
+      if (std::fabs(vev[r][i] - vev_ser[i]) > 1e-10 * std::fabs(vev_ser[i]))
+      {
+        std::printf("FAIL rank %d: block Lanczos k = 32, variable coefficients, Ritz %d %.17g vs %.17g\n", r, i,
+                    vev[r][i], vev_ser[i]);
         ++failures;
       }
   }
