@@ -234,6 +234,12 @@ run_task() {
         --variants fused:arrays#13,fused:arrays#16,fused:arrays#17 > "$O/sweep2l_128.jsonl" 2>> "$O/sweep2l.err" && \
       timeout -k 10 300 python3 tools/lanczos_sweep.py --N 256 --slab 32 --rounds 3 --steps 40 \
         --variants fused:arrays#13,fused:arrays#16,fused:arrays#17 > "$O/sweep2l_slab.jsonl" 2>> "$O/sweep2l.err" ;;
+    threshold)
+      # EIG_MARCH_2L_MIN_ROWS: variant 15 (#13) vs the 2-line march (#16) on 4 M / 6 M / 8 M-row slabs
+      for s in 64 96 128; do
+        timeout -k 10 200 python3 tools/lanczos_sweep.py --N 256 --slab $s --rounds 3 --steps 40 \
+          --variants fused:arrays#13,fused:arrays#16 >> "$O/threshold.jsonl" 2>> "$O/threshold.err" || return 1
+      done ;;
     ablation)
       timeout -k 10 300 tools/march_copy 256 values ablation 8 > "$O/march_copy_abl.jsonl" ;;
     c4)
