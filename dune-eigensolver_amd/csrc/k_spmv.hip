@@ -1493,7 +1493,8 @@ __device__ __forceinline__ void march_rows_geo2(const SellB1 &A, const MarchPlan
 // The 2-line fused march is the default on ranks of at least EIG_MARCH_2L_MIN_ROWS rows: 256^3 (16.8 M
 // rows) 206.5-206.8 us vs 223.5 us for variant 15 (profiles/r06e_sweep256_2lines.jsonl, 0.65 of HBM),
 // but 2 M-row grids (128^3, one rank's 256^2 x 32 slab) 28.2-28.4 vs 27.7-27.9 us: fewer, longer
-// wave chains cost more there than the halved gathers save.
+// wave chains cost more there than the halved gathers save.  256^2 slabs (profiles/r06m_threshold.jsonl):
+// 4 M rows 47.1 vs 46.1 us, 6 M rows 84.3 vs 89.8 us, 8 M rows 111.7 vs 116.7 us -- the threshold is 6 M.
 constexpr bool kMarch2lDefault = true;
 constexpr bool is_march2l(int uni) { return uni == 22 || uni == 23 || uni == 24; }
 
