@@ -118,8 +118,20 @@ void allreduce_sum_red(eig_ctx_t ctx, double *buf, i64 count, hipStream_t s)
 // xGMI mailbox (k_comm.hip).  prepare: allocate my uncached mailbox + state and export it;
 // open: map every peer's mailbox; validate: one allreduce of rank+1 must give P(P+1)/2 exactly.
 // ---------------------------------------------------------------------------------------------
+void halobox_free(eig_ctx_t ctx)
+{
+  HaloBoxHost *h = ctx->hbox;
+  if (!h) return;
+  for (void *p : h->opened) (void)hipIpcCloseMemHandle(p);
+  if (h->alloc) (void)hipFree(h->alloc);
+  if (h->state) (void)hipFree(h->state);
+  delete h;
+  ctx->hbox = nullptr;
+}
+
 void mailbox_free(eig_ctx_t ctx)
 {
+  halobox_free(ctx);  // its error word is the mailbox's
   MailboxHost *m = ctx->mbox;
   if (!m) return;
   for (void *p : m->opened) (void)hipIpcCloseMemHandle(p);
@@ -200,6 +212,118 @@ bool mailbox_validate(eig_ctx_t ctx)
   return err == 0 && v[0] == want && v[1] == (double)P && v[2] == 0.5 * want;
 }
 
+// Sum `vals` (count doubles) over the mailbox-only ranks, synchronously on ctx->stream; throws when
+// the mailbox timed out.  Also a barrier: no rank returns before every rank has published.
+static void mailbox_sum_sync(eig_ctx_t ctx, std::vector<double> &vals, const char *what)
+{
+  double *d = dev_alloc<double>(vals.size());
+  EIG_HIP(hipMemcpy(d, vals.data(), vals.size() * sizeof(double), hipMemcpyHostToDevice));
+  for (i64 off = 0; off < (i64)vals.size(); off += kMailboxVals)
+    launch_mailbox_allreduce(d + off, (int)std::min<i64>(kMailboxVals, (i64)vals.size() - off), ctx->mbox->dev,
+                             kMailboxTimeout, ctx->stream);
+  EIG_HIP(hipStreamSynchronize(ctx->stream));
+  EIG_HIP(hipMemcpy(vals.data(), d, vals.size() * sizeof(double), hipMemcpyDeviceToHost));
+  (void)hipFree(d);
+  int err = 0;
+  EIG_HIP(hipMemcpy(&err, ctx->mbox->dev.err, sizeof(int), hipMemcpyDeviceToHost));
+  EIG_CHECK(err == 0, EIG_ERR_RCCL, std::string(what) + ": mailbox timed out");
+}
+
+// (Re)build the halo mailbox with slots of `cap` doubles.  Collective over the mailbox-only ranks,
+// which all call it with the same cap (eig_mat_create_bcsr_dist computes it from every rank's plan):
+// the old staging is released once every rank is quiet, the new one exported and its IPC handle
+// gathered through the mailbox allreduce (each 16-bit chunk one exact double).
+void halobox_setup(eig_ctx_t ctx, i64 cap)
+{
+  MailboxHost *m = ctx->mbox;
+  const int P = m->dev.P, me = m->dev.me;
+  constexpr int kChunks = HIP_IPC_HANDLE_SIZE / 2;
+  EIG_HIP(hipStreamSynchronize(ctx->stream));
+  EIG_HIP(hipStreamSynchronize(ctx->comm_stream));
+  std::vector<double> bar(1, 0.0);
+  mailbox_sum_sync(ctx, bar, "halo mailbox");  // every rank's exchanges have completed
+  halobox_free(ctx);
+  auto *h = new HaloBoxHost();
+  ctx->hbox = h;
+  const size_t fbytes = (size_t)2 * P * kHaloFlagStride * sizeof(u64);
+  const size_t bytes = fbytes + (size_t)2 * P * (size_t)cap * sizeof(double);
+  std::vector<double> g((size_t)P * (kChunks + 1), 0.0);
+  bool ok = true;
+  try
+  {
+    void *p = nullptr;
+    if (hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached) != hipSuccess)
+    {
+      (void)hipGetLastError();
+      EIG_HIP(hipExtMallocWithFlags(&p, bytes, hipDeviceMallocFinegrained));
+    }
+    h->alloc = p;
+    EIG_HIP(hipMemset(p, 0, bytes));
+    EIG_HIP(hipMalloc(&h->state, 512));  // seq at 0, the push / pull tickets at 128 / 256
+    EIG_HIP(hipMemset(h->state, 0, 512));
+    hipIpcMemHandle_t ih;
+    EIG_HIP(hipIpcGetMemHandle(&ih, p));
+    unsigned char raw[HIP_IPC_HANDLE_SIZE];
+    std::memcpy(raw, &ih, HIP_IPC_HANDLE_SIZE);
+    for (int c = 0; c < kChunks; ++c) g[(size_t)me * (kChunks + 1) + c] = raw[2 * c] + 256.0 * raw[2 * c + 1];
+    g[(size_t)me * (kChunks + 1) + kChunks] = 1.0;
+  }
+  catch (const Error &)
+  {
+    ok = false;
+  }
+  mailbox_sum_sync(ctx, g, "halo mailbox");
+  for (int r = 0; r < P; ++r) ok = ok && g[(size_t)r * (kChunks + 1) + kChunks] == 1.0;
+  HaloBox &d = h->dev;
+  if (ok)
+  {
+    d.flags = static_cast<u64 *>(h->alloc);
+    d.stage = reinterpret_cast<double *>(static_cast<char *>(h->alloc) + fbytes);
+    d.seq = static_cast<u64 *>(h->state);
+    d.ticket = reinterpret_cast<unsigned *>(static_cast<char *>(h->state) + 128);
+    d.err = m->dev.err;
+    d.cap = cap;
+    d.P = P;
+    d.me = me;
+    try
+    {
+      for (int r = 0; r < P; ++r)
+      {
+        char *base = static_cast<char *>(h->alloc);
+        if (r != me)
+        {
+          unsigned char raw[HIP_IPC_HANDLE_SIZE];
+          for (int c = 0; c < kChunks; ++c)
+          {
+            const unsigned v = (unsigned)g[(size_t)r * (kChunks + 1) + c];
+            raw[2 * c] = (unsigned char)(v & 255u);
+            raw[2 * c + 1] = (unsigned char)(v >> 8);
+          }
+          hipIpcMemHandle_t ih;
+          std::memcpy(&ih, raw, HIP_IPC_HANDLE_SIZE);
+          void *p = nullptr;
+          EIG_HIP(hipIpcOpenMemHandle(&p, ih, hipIpcMemLazyEnablePeerAccess));
+          h->opened.push_back(p);
+          base = static_cast<char *>(p);
+        }
+        d.peer_flags[r] = reinterpret_cast<u64 *>(base);
+        d.peer_stage[r] = reinterpret_cast<double *>(base + fbytes);
+      }
+    }
+    catch (const Error &)
+    {
+      ok = false;
+    }
+  }
+  std::vector<double> agree(1, ok ? 1.0 : 0.0);
+  mailbox_sum_sync(ctx, agree, "halo mailbox");
+  if (agree[0] != (double)P)
+  {
+    halobox_free(ctx);
+    throw Error(EIG_ERR_RCCL, "halo mailbox: staging setup failed on some rank");
+  }
+}
+
 // Exchange the ghost entries of the window-layout vector x.  Runs on stream s.
 void halo_exchange(const eig_mat_s &A, double *x, hipStream_t s, double *x2, int width)
 {
@@ -228,8 +352,39 @@ void halo_exchange(const eig_mat_s &A, double *x, hipStream_t s, double *x2, int
     if (x2) halo_exchange(A, x2, s, nullptr, width);
     return;
   }
+  if (!ctx->comm && ctx->mbox && ctx->mbox->ready)
+  {
+    // mailbox-only ranks: the xGMI halo mailbox (k_comm.hip).  Every rank of the partition takes part
+    // in every exchange of the matrix (an empty side still publishes and waits for its lines).
+    HaloXfer snd, rcv, syn;
+    auto add_sync = [&](int peer) {
+      for (int k = 0; k < syn.n; ++k)
+        if (syn.peer[k] == peer) return;
+      syn.peer[syn.n++] = peer;
+    };
+    for (const auto &r : A.sends)
+    {
+      snd.peer[snd.n] = r.peer;
+      snd.off[snd.n] = r.offset;
+      snd.cnt[snd.n++] = r.count;
+      add_sync(r.peer);
+    }
+    for (const auto &r : A.recvs)
+    {
+      rcv.peer[rcv.n] = r.peer;
+      rcv.off[rcv.n] = r.offset;
+      rcv.cnt[rcv.n++] = r.count;
+      add_sync(r.peer);
+    }
+    if (syn.n == 0) return;
+    EIG_CHECK(ctx->hbox, EIG_ERR_ARG, "halo exchange: no halo mailbox (matrix created before the mailbox was reopened)");
+    launch_halo_mailbox(ctx->hbox->dev, snd, rcv, syn, x, x2, width, s);
+    ++ctx->n_halo;
+    ctx->n_p2p += (long long)(A.recvs.size() + A.sends.size()) * (x2 ? 2 : 1);
+    return;
+  }
   if (A.sends.empty() && A.recvs.empty()) return;
-  EIG_CHECK(ctx->comm, EIG_ERR_ARG, "halo exchange needs RCCL or the loopback transport");
+  EIG_CHECK(ctx->comm, EIG_ERR_ARG, "halo exchange needs RCCL, the mailbox or the loopback transport");
   EIG_NCCL(ncclGroupStart());
   // per peer, x then x2 on both sides: point-to-point operations match in issue order
   for (const auto &r : A.recvs)
@@ -1421,6 +1576,22 @@ extern "C" int eig_mat_create_bcsr_dist_ex(eig_ctx_t ctx, int64_t nb_rows_global
       {
         int rc = eig_plan_halo(nr, nr > 1 ? me : 0, all.data(), bc, wb_blk, rv.data(), &nrecv, sd.data(), &nsend);
         EIG_CHECK(rc == EIG_OK, rc, "eig_plan_halo failed");
+      }
+      if (!ctx->comm && !ctx->loop && P > 1 && ctx->mbox && ctx->mbox->ready)
+      {
+        // the halo mailbox's slots hold the largest range of any rank's plan, 8 columns wide
+        // (blanczos.cpp exchanges blocks of 8); grown collectively when a matrix needs more
+        i64 most = 0;
+        std::vector<int64_t> qr(3 * (size_t)P), qs(3 * (size_t)P);
+        for (int q = 0; q < P; ++q)
+        {
+          int nq = 0, ns = 0;
+          int rc = eig_plan_halo(P, q, all.data(), bc, 0, qr.data(), &nq, qs.data(), &ns);
+          EIG_CHECK(rc == EIG_OK, rc, "eig_plan_halo failed");
+          for (int k = 0; k < nq; ++k) most = std::max<i64>(most, qr[3 * k + 2]);
+        }
+        const i64 cap = 8 * most;
+        if (cap > 0 && (!ctx->hbox || ctx->hbox->dev.cap < cap)) halobox_setup(ctx, cap);
       }
       for (int k = 0; k < nrecv; ++k) A->recvs.push_back({(int)rv[3 * k], rv[3 * k + 1], rv[3 * k + 2]});
       for (int k = 0; k < nsend; ++k) A->sends.push_back({(int)sd[3 * k], sd[3 * k + 1], sd[3 * k + 2]});

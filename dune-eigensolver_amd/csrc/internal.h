@@ -124,6 +124,37 @@ struct MailboxHost {
 constexpr unsigned long long kMailboxTimeout = 1000000000ull;  // 10 s of s_memrealtime (100 MHz)
 void launch_mailbox_allreduce(double *buf, int count, const Mailbox &mb, unsigned long long timeout, hipStream_t s);
 
+// xGMI halo mailbox (k_comm.hip) of mailbox-only ranks (eig_comm_ipc_open, no RCCL): every rank's
+// uncached staging area, IPC-mapped by every peer.  Layout: [2][P] sequence lines (one 128-B line
+// per word), then [2][P][cap] doubles; parity = sequence & 1, slot = the sending rank.
+constexpr int kHaloFlagStride = 16;  // u64 words per sequence line
+struct HaloBox {
+  u64 *flags = nullptr;                         // mine: [2][P] lines
+  u64 *peer_flags[kMaxMailboxRanks] = {};       // rank r's lines mapped here (peer_flags[me] = flags)
+  double *stage = nullptr;                      // mine: [2][P][cap]
+  double *peer_stage[kMaxMailboxRanks] = {};
+  u64 *seq = nullptr;                           // device: sequence number of the last completed exchange
+  unsigned *ticket = nullptr;                   // device: push / pull last-workgroup tickets (128 B apart)
+  int *err = nullptr;                           // the mailbox's error word (Mailbox::err)
+  long long cap = 0;                            // doubles per slot
+  int P = 1, me = 0;
+};
+struct HaloBoxHost {
+  HaloBox dev;
+  void *alloc = nullptr;         // hipExtMallocWithFlags allocation (exported)
+  void *state = nullptr;         // seq + tickets (hipMalloc, 512 B)
+  std::vector<void *> opened;    // IPC-opened peer mappings
+};
+// One side of an exchange: n ranges (peer, window offset, count) in scalar units.
+struct HaloXfer {
+  int n = 0;
+  int peer[kMaxMailboxRanks] = {};
+  long long off[kMaxMailboxRanks] = {};
+  long long cnt[kMaxMailboxRanks] = {};
+};
+void launch_halo_mailbox(const HaloBox &hb, const HaloXfer &snd, const HaloXfer &rcv, const HaloXfer &sync, double *x,
+                         double *x2, int width, hipStream_t s);
+
 }  // namespace eigmi
 
 struct eig_mg_s;  // mg.cpp
@@ -144,6 +175,7 @@ struct eig_ctx_s {
   ncclComm_t comm_red = nullptr;
   eigmi::LoopHub *loop = nullptr;    // in-process loopback transport (tests), exclusive with comm
   eigmi::MailboxHost *mbox = nullptr; // xGMI mailbox allreduce (with RCCL, or alone for tests)
+  eigmi::HaloBoxHost *hbox = nullptr; // xGMI halo mailbox of mailbox-only ranks (grown by eig_mat_create_bcsr_dist)
   int nranks = 1, rank = 0;
   long long n_ar = 0, n_ar_red = 0, n_halo = 0, n_p2p = 0;  // eig_comm_counters
   bool comm_always = false;          // EIG_COMM_ALWAYS: collectives through `comm` even at one rank

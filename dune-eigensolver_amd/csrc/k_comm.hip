@@ -19,7 +19,11 @@
 // s_memrealtime ticks, 100 MHz): on timeout the result is NaN and *err is set, instead of a hang.
 #include "internal.h"
 
+#include <algorithm>
+
 namespace eigmi {
+
+constexpr unsigned long long kXchTimeoutHalo = 200000000ull;  // 2 s of s_memrealtime
 
 __global__ __launch_bounds__(64) void k_mailbox_allreduce(double *buf, int count, Mailbox mb, unsigned long long timeout)
 {
@@ -82,6 +86,141 @@ void launch_mailbox_allreduce(double *buf, int count, const Mailbox &mb, unsigne
   EIG_CHECK(count >= 1 && count <= kMailboxVals, EIG_ERR_ARG, "mailbox allreduce: bad count");
   EIG_CHECK(mb.P >= 1 && mb.P <= kMaxMailboxRanks, EIG_ERR_ARG, "mailbox allreduce: bad rank count");
   hipLaunchKernelGGL(k_mailbox_allreduce, dim3(1), dim3(64), 0, s, buf, count, mb, timeout);
+  EIG_HIP(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------------------------
+// The halo exchange of mailbox-only ranks over the same IPC mappings (HaloBox, internal.h): the
+// boundary rows a peer needs are stored straight into that peer's uncached staging slot over xGMI,
+// and the ghost rows are copied out of my own staging once every peer's sequence line carries the
+// exchange's number.  Two launches on the exchange stream:
+//   push: every workgroup streams its share of the send ranges into the peers' slots (parity
+//         s & 1) and fences at system scope; the last workgroup (ticket) then stores s into slot
+//         `me` of the sequence lines of EVERY peer this rank exchanges with (sends and receives);
+//   pull: every workgroup's first wave polls my lines of those peers until they read s (bounded,
+//         like k_mailbox_allreduce), then the workgroups copy the receive ranges out of my staging
+//         into the window; the last workgroup stores s as the completed sequence number.
+// Parity reuse: rank A pushes s + 2 (over the slot of s) only after its pull of s + 1, which needs
+// rank B's line of s + 1, which B stores only after its pull of s -- i.e. after B read slot s.  This
+// needs the line from every peer A writes to, hence the union of send and receive peers.  The
+// sequence number lives in device memory (captured exchanges replay correctly).  A timed-out pull,
+// or any pull or push once the mailbox's error word is set, writes NaN instead of values -- into the
+// ghosts and into the peers' slots -- so every rank's recurrence turns NaN the same way.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ bool halo_last_group(unsigned *ticket)
+{
+  __shared__ bool s_last;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    s_last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  __syncthreads();
+  return s_last;
+}
+
+__global__ __launch_bounds__(256) void k_halo_push(HaloBox hb, HaloXfer snd, HaloXfer sync, const double *x,
+                                                   const double *x2, int w)
+{
+  const u64 seq = __hip_atomic_load(hb.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+  const int par = (int)(seq & 1);
+  const bool poisoned = __hip_atomic_load(hb.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+  const double nan = __builtin_nan("");
+  const long long g0 = (long long)blockIdx.x * blockDim.x + threadIdx.x, gs = (long long)gridDim.x * blockDim.x;
+  for (int k = 0; k < snd.n; ++k)
+  {
+    double *dst = hb.peer_stage[snd.peer[k]] + ((long long)par * hb.P + hb.me) * hb.cap;
+    const long long n = snd.cnt[k] * w;
+    const double *a = x + snd.off[k] * w;
+    for (long long i = g0; i < n; i += gs) dst[i] = poisoned ? nan : a[i];
+    if (x2)
+    {
+      const double *b = x2 + snd.off[k] * w;
+      for (long long i = g0; i < n; i += gs) dst[n + i] = poisoned ? nan : b[i];
+    }
+  }
+  __threadfence_system();  // my slot stores are performed before the ticket
+  if (halo_last_group(hb.ticket))
+  {
+    const int t = threadIdx.x;
+    if (t < sync.n)
+      __hip_atomic_store(hb.peer_flags[sync.peer[t]] + ((long long)par * hb.P + hb.me) * kHaloFlagStride, seq,
+                         __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (t == 0) __hip_atomic_store(hb.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_halo_pull(HaloBox hb, HaloXfer rcv, HaloXfer sync, double *x, double *x2,
+                                                   int w, unsigned long long timeout)
+{
+  __shared__ int s_late;
+  const u64 seq = __hip_atomic_load(hb.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+  const int par = (int)(seq & 1);
+  const int t = threadIdx.x;
+  if (t < 64)
+  {
+    const bool mine = t < sync.n;
+    const u64 *line = hb.flags + ((long long)par * hb.P + (mine ? sync.peer[t] : 0)) * kHaloFlagStride;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    bool late = false;
+    for (;;)
+    {
+      const bool ok = !mine || __hip_atomic_load(line, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == seq;
+      if (__all(ok)) break;
+      if (__hip_atomic_load(hb.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 ||
+          __builtin_amdgcn_s_memrealtime() - t0 > timeout)
+      {
+        late = true;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    const bool any_late = __any(late) || __hip_atomic_load(hb.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+    if (t == 0)
+    {
+      s_late = any_late ? 1 : 0;
+      if (late) __hip_atomic_store(hb.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __syncthreads();
+  __atomic_thread_fence(__ATOMIC_ACQUIRE);  // the peers' slot stores are visible after their lines
+  const bool bad = s_late != 0;
+  const double nan = __builtin_nan("");
+  const long long g0 = (long long)blockIdx.x * blockDim.x + t, gs = (long long)gridDim.x * blockDim.x;
+  for (int k = 0; k < rcv.n; ++k)
+  {
+    const double *src = hb.stage + ((long long)par * hb.P + rcv.peer[k]) * hb.cap;
+    const long long n = rcv.cnt[k] * w;
+    double *a = x + rcv.off[k] * w;
+    for (long long i = g0; i < n; i += gs) a[i] = bad ? nan : src[i];
+    if (x2)
+    {
+      double *b = x2 + rcv.off[k] * w;
+      for (long long i = g0; i < n; i += gs) b[i] = bad ? nan : src[n + i];
+    }
+  }
+  if (halo_last_group(hb.ticket + 32))
+    if (t == 0)
+    {
+      __hip_atomic_store(hb.seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(hb.ticket + 32, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+void launch_halo_mailbox(const HaloBox &hb, const HaloXfer &snd, const HaloXfer &rcv, const HaloXfer &sync, double *x,
+                         double *x2, int w, hipStream_t s)
+{
+  EIG_CHECK(hb.P >= 2 && hb.P <= kMaxMailboxRanks && w >= 1, EIG_ERR_ARG, "halo mailbox: bad arguments");
+  const int m = x2 ? 2 : 1;
+  long long most = 0;
+  for (int k = 0; k < snd.n; ++k) most = std::max(most, snd.cnt[k]);
+  for (int k = 0; k < rcv.n; ++k) most = std::max(most, rcv.cnt[k]);
+  EIG_CHECK(most * w * m <= hb.cap, EIG_ERR_ARG, "halo mailbox: exchange larger than the staging slots");
+  // about 4 doubles per thread, at most 512 pushing / 256 polling workgroups
+  const long long per = std::max(1LL, most * w * m / (kStreamThreads * 4));
+  const int gp = (int)std::min<long long>(512, per), gq = (int)std::min<long long>(256, per);
+  hipLaunchKernelGGL(k_halo_push, dim3(gp), dim3(kStreamThreads), 0, s, hb, snd, sync, (const double *)x,
+                     (const double *)x2, w);
+  EIG_HIP(hipGetLastError());
+  hipLaunchKernelGGL(k_halo_pull, dim3(gq), dim3(kStreamThreads), 0, s, hb, rcv, sync, x, x2, w, kXchTimeoutHalo);
   EIG_HIP(hipGetLastError());
 }
 
