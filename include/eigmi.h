@@ -92,9 +92,15 @@ int eig_comm_barrier(eig_ctx_t ctx);
  * mailbox allreduce (every rank exports a small uncached mailbox through IPC; one launch stores
  * this rank's values into every peer's mailbox and sums all slots in rank order) for up to 16
  * ranks, validated and agreed by all ranks, else ncclAllReduce stays in use.
- * eig_comm_ipc_handle / eig_comm_ipc_open attach the mailbox alone (no RCCL; allreduce and dots
- * only -- distributed matrices need RCCL or loopback): every rank exports its handle, the
- * nranks x 64 bytes travel by any side channel (rank order), then every rank opens them. */
+ * eig_comm_ipc_handle / eig_comm_ipc_open attach the mailbox alone (no RCCL): every rank exports
+ * its handle, the nranks x 64 bytes travel by any side channel (rank order), then every rank opens
+ * them.  Allreduces and dots go through the mailbox; the halo of distributed matrices through the
+ * halo mailbox: each rank's uncached staging area (two parities x nranks slots of 8 x the largest
+ * halo range of any rank), set up -- and grown -- collectively by eig_mat_create_bcsr_dist, its
+ * handle gathered through the mailbox.  An exchange is two launches on the halo stream: the boundary
+ * rows stored straight into the peers' slots over xGMI, then, once every peer's sequence word has
+ * arrived (bounded: 2 s, then NaN ghosts and a recorded timeout), the ghosts copied out of the own
+ * slots.  Sequence numbers live on the device: exchanges captured into a hipGraph replay correctly. */
 #define EIG_IPC_HANDLE_BYTES 64
 /* EIG_AR_MAILBOX_STEP: the mailbox for every allreduce, and the fused Lanczos step
  * (EIG_LANCZOS_FUSED) exchanges its three sums INSIDE the step kernel: the last workgroup of launch L
