@@ -496,6 +496,7 @@ def main():
     trial = None
     ab, ab_check = {}, {}
     halo_mode = "split"
+    halo_x = "rccl"
     if variant == "auto":
         # one rank: EIG_LANCZOS_AUTO's choice for this image (the fused step on a 1x1 image)
         tw = eigmi.LanczosWorkspace(M, 1, seed=123, fused="auto")
@@ -514,12 +515,20 @@ def main():
             if "rccl" not in ars:
                 ars = ("rccl",) + ars  # the reference run of the alpha / beta check
             # (the pipelined step keeps the allreduce launch under mailbox-step: same as mailbox)
-            combos = [(v, h, a) for v in ("fused", "pipelined") for h in halos for a in ars
+            # N > 1 with the mailbox: the halo also through the halo mailbox (eig_comm_select_halo; the
+            # boundary planes stored into the peers' staging over xGMI) beside ncclSend / ncclRecv
+            # (--rehearse-trial: selected at one rank too, where no matrix has a halo)
+            hxs_mb = ("rccl", "mailbox") if (world > 1 or args.rehearse_trial) and have_mb else ("rccl",)
+            combos = [(v, h, a, x) for v in ("fused", "pipelined") for h in halos for a in ars
+                      for x in (hxs_mb if a != "rccl" else ("rccl",))
                       if not (v == "pipelined" and a == "mailbox-step")]
-            for var, halo, ar in combos:
+            for var, halo, ar, hx in combos:
                 M.tune(halo_whole=int(halo == "whole"))
                 if multi:
                     ctx.select_allreduce(ar)
+                if len(hxs_mb) > 1:
+                    ctx.select_halo(hx)
+                tkey = f"{halo}/{ar}" + ("/halo-mailbox" if hx == "mailbox" else "")
                 # every call below may already have queued a halo exchange or an allreduce on the
                 # other ranks when it fails here, so a failing rank cannot rejoin them at a barrier:
                 # it exits non-zero at once and the launcher tears the job down on every rank
@@ -546,7 +555,7 @@ def main():
                             tw.step(args.trial_steps)
                         ctx.sync()
                         ms[la] = (time.perf_counter() - t0) / args.trial_steps * 1e3
-                    ab[(var, halo, ar)] = tw.tridiag()
+                    ab[(var, halo, ar, hx)] = tw.tridiag()
                 except eigmi.EigError as e:
                     if not (ar == "mailbox-step" and e.code == eigmi.EIG_ERR_RCCL):
                         print(f"bench: {var} trial failed on rank {rank}: {e}; stopping every rank", file=sys.stderr,
@@ -564,29 +573,34 @@ def main():
                 # (checked per combination: selecting a transport clears the recorded timeouts)
                 failed = ar != "rccl" and max_over_ranks(ctx.comm_info()["mailbox_errors"]) > 0
                 for la in launches:
-                    trial[f"{var}/{la}/{halo}/{ar}"] = float("inf") if failed else round(max_over_ranks(ms[la]), 4)
+                    trial[f"{var}/{la}/{tkey}"] = float("inf") if failed else round(max_over_ranks(ms[la]), 4)
             # a transport is a candidate only if its run reproduces the RCCL run of the same variant
             # and halo mode (same start vector, same step count) to AB_RTOL -- never on timing alone
-            for (var, halo, ar), (a, b) in ab.items():
-                if ar == "rccl":
+            for (var, halo, ar, hx), (a, b) in ab.items():
+                if ar == "rccl" and hx == "rccl":
                     continue
-                ref = ab.get((var, halo, "rccl"))
+                ref = ab.get((var, halo, "rccl", "rccl"))
                 mm = ab_mismatch(a, b, *ref) if ref is not None else float("inf")
                 mm = max_over_ranks(mm)
                 ok = mm <= AB_RTOL
-                ab_check[f"{var}/{halo}/{ar}"] = {"max_rel_diff_vs_rccl": mm if np.isfinite(mm) else None,
-                                                  "steps": int(len(a)), "ok": bool(ok)}
+                tkey = f"{halo}/{ar}" + ("/halo-mailbox" if hx == "mailbox" else "")
+                ab_check[f"{var}/{tkey}"] = {"max_rel_diff_vs_rccl": mm if np.isfinite(mm) else None,
+                                             "steps": int(len(a)), "ok": bool(ok)}
                 if not ok:
                     for k in trial:
-                        if k.startswith(f"{var}/") and k.endswith(f"/{halo}/{ar}"):
+                        if k.startswith(f"{var}/") and k.split("/", 2)[2] == tkey:
                             trial[k] = float("inf")
             best = min(trial, key=trial.get)
-            variant, best_launch, best_halo, best_ar = best.split("/")
+            parts = best.split("/")
+            variant, best_launch, best_halo, best_ar = parts[:4]
             if args.launch == "auto":
                 args.launch = best_launch
             M.tune(halo_whole=int(best_halo == "whole"))
             if multi:
                 ctx.select_allreduce(best_ar)
+            halo_x = "mailbox" if len(parts) > 4 else "rccl"
+            if len(hxs_mb) > 1:
+                ctx.select_halo(halo_x)
             halo_mode = best_halo
     if world > 1 and trial is None:
         # no trial: RCCL unless a mailbox transport was asked for (and is set up on every rank)
@@ -723,7 +737,8 @@ def main():
                                f"{N}^3 Lanczos 3-term step, no re-orthogonalisation ({VARIANT_NAME[variant]})",
                    "N": N, "n": n, "nnz": nnz_total, "matrix": args.matrix, "image": args.image,
                    "matrix_image": image_name(M),
-                   "parallelism": (f"row-partition z-slabs x{world} (RCCL halo, {halo_mode} launch, "
+                   "parallelism": (f"row-partition z-slabs x{world} "
+                                   f"({'halo mailbox' if halo_x == 'mailbox' else 'RCCL halo'}, {halo_mode} launch, "
                                    f"{ctx.comm_info()['allreduce']} allreduce)") if world > 1 else
                                   ("single GPU, one-rank RCCL allreduce per step" if args.comm_self else "single GPU")},
         # SURVEY 8(d)'s CSR step bytes (12 nnz + 4(n+1) + 48 n) / step time: an equivalent rate, not

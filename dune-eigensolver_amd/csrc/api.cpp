@@ -352,9 +352,9 @@ void halo_exchange(const eig_mat_s &A, double *x, hipStream_t s, double *x2, int
     if (x2) halo_exchange(A, x2, s, nullptr, width);
     return;
   }
-  if (!ctx->comm && ctx->mbox && ctx->mbox->ready)
+  if ((!ctx->comm || ctx->halo_mailbox) && ctx->mbox && ctx->mbox->ready)
   {
-    // mailbox-only ranks: the xGMI halo mailbox (k_comm.hip).  Every rank of the partition takes part
+    // mailbox-only ranks, or EIG_HALO_MAILBOX: the xGMI halo mailbox (k_comm.hip).  Every rank of the partition takes part
     // in every exchange of the matrix (an empty side still publishes and waits for its lines).
     HaloXfer snd, rcv, syn;
     auto add_sync = [&](int peer) {
@@ -723,6 +723,20 @@ extern "C" int eig_comm_select_allreduce(eig_ctx_t ctx, int kind)
       m->on = kind != EIG_AR_RCCL;
       m->step = kind == EIG_AR_MAILBOX_STEP;
     }
+  });
+}
+
+extern "C" int eig_comm_select_halo(eig_ctx_t ctx, int kind)
+{
+  return guard(ctx, [&] {
+    EIG_CHECK(ctx && (kind == EIG_HALO_RCCL || kind == EIG_HALO_MAILBOX), EIG_ERR_ARG,
+              "eig_comm_select_halo: EIG_HALO_RCCL or EIG_HALO_MAILBOX");
+    EIG_CHECK(ctx->comm && ctx->mbox && ctx->mbox->ready, EIG_ERR_ARG,
+              "eig_comm_select_halo: needs RCCL and a validated mailbox (eig_comm_init_ex EIG_COMM_MAILBOX)");
+    DeviceGuard dg(ctx->device);
+    EIG_HIP(hipStreamSynchronize(ctx->stream));
+    EIG_HIP(hipStreamSynchronize(ctx->comm_stream));
+    ctx->halo_mailbox = kind == EIG_HALO_MAILBOX;
   });
 }
 
@@ -1577,7 +1591,7 @@ extern "C" int eig_mat_create_bcsr_dist_ex(eig_ctx_t ctx, int64_t nb_rows_global
         int rc = eig_plan_halo(nr, nr > 1 ? me : 0, all.data(), bc, wb_blk, rv.data(), &nrecv, sd.data(), &nsend);
         EIG_CHECK(rc == EIG_OK, rc, "eig_plan_halo failed");
       }
-      if (!ctx->comm && !ctx->loop && P > 1 && ctx->mbox && ctx->mbox->ready)
+      if (!ctx->loop && P > 1 && ctx->mbox && ctx->mbox->ready)
       {
         // the halo mailbox's slots hold the largest range of any rank's plan, 8 columns wide
         // (blanczos.cpp exchanges blocks of 8); grown collectively when a matrix needs more

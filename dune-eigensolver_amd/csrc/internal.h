@@ -179,6 +179,7 @@ struct eig_ctx_s {
   int nranks = 1, rank = 0;
   long long n_ar = 0, n_ar_red = 0, n_halo = 0, n_p2p = 0;  // eig_comm_counters
   bool comm_always = false;          // EIG_COMM_ALWAYS: collectives through `comm` even at one rank
+  bool halo_mailbox = false;         // eig_comm_select_halo(EIG_HALO_MAILBOX) beside RCCL
   bool distributed() const { return nranks > 1 && (comm || loop || (mbox && mbox->ready)); }
   // whether allreduces go through a transport (distributed, or a forced one-rank RCCL communicator)
   bool collectives() const { return distributed() || (comm_always && (comm || (mbox && mbox->ready))); }

@@ -119,6 +119,7 @@ SIGNATURES = {
                              ctypes.POINTER(_int)]),
     "eig_comm_counters": (_int, [_vp, ctypes.POINTER(_i64)]),
     "eig_comm_select_allreduce": (_int, [_vp, _int]),
+    "eig_comm_select_halo": (_int, [_vp, _int]),
     "eig_malloc": (_int, [_vp, ctypes.c_size_t, ctypes.POINTER(_vp)]),
     "eig_free": (_int, [_vp, _vp]),
     "eig_memcpy_h2d": (_int, [_vp, _vp, _vp, ctypes.c_size_t]),
@@ -383,6 +384,11 @@ class Context:
         Lanczos step's sums exchanged inside the step kernel); the mailbox kinds need it set up and
         validated (comm_init(mailbox=True) or ipc_open); every rank must select the same."""
         self.check(lib.eig_comm_select_allreduce(self.h, {"rccl": 1, "mailbox": 2, "mailbox-step": 4}[kind]))
+
+    def select_halo(self, kind):
+        """eig_comm_select_halo: "rccl" (ncclSend / ncclRecv) or "mailbox" (the halo mailbox); every rank
+        must select the same."""
+        self.check(lib.eig_comm_select_halo(self.h, {"rccl": 1, "mailbox": 2}[kind]))
 
     def comm_info(self):
         v = [_int(0) for _ in range(4)]

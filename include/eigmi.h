@@ -130,6 +130,13 @@ int eig_comm_info(eig_ctx_t ctx, int *nranks, int *rank, int *allreduce, int *ma
  * consistent sequence words.  A mailbox alone (eig_comm_ipc_open) only clears the recorded timeouts:
  * after a timeout, re-open it. */
 int eig_comm_select_allreduce(eig_ctx_t ctx, int kind);
+/* Halo transport of the distributed matrices of a context that has RCCL and a validated mailbox
+ * (eig_comm_init_ex with EIG_COMM_MAILBOX): EIG_HALO_RCCL (grouped ncclSend / ncclRecv, the
+ * default) or EIG_HALO_MAILBOX (the halo mailbox, as on mailbox-only ranks; its staging is set up
+ * by eig_mat_create_bcsr_dist whenever the mailbox is).  A collective: every rank selects the same
+ * one; synchronises the context's streams. */
+enum eig_halo_kind { EIG_HALO_RCCL = 1, EIG_HALO_MAILBOX = 2 };
+int eig_comm_select_halo(eig_ctx_t ctx, int kind);
 
 /* ---------------------------------------------------------------- device memory ------------ */
 int eig_malloc(eig_ctx_t ctx, size_t bytes, void **ptr);

@@ -234,6 +234,15 @@ run_task() {
         --variants fused:arrays#13,fused:arrays#16,fused:arrays#17 > "$O/sweep2l_128.jsonl" 2>> "$O/sweep2l.err" && \
       timeout -k 10 300 python3 tools/lanczos_sweep.py --N 256 --slab 32 --rounds 3 --steps 40 \
         --variants fused:arrays#13,fused:arrays#16,fused:arrays#17 > "$O/sweep2l_slab.jsonl" 2>> "$O/sweep2l.err" ;;
+    halotime)
+      # the halo mailbox between 2 / 4 mailbox-only processes on one GPU (256^3 z-slabs) under a kernel
+      # trace; then the bench's N > 1 trial rehearsed at one rank (the halo selection included)
+      prof_env
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/halo_trace" -o trace -- \
+        python3 tools/halo_time.py 256 2 20 40 > "$O/halo_time.jsonl" 2> "$O/halo_time.err" && \
+      timeout -k 10 200 python3 tools/halo_time.py 256 4 20 40 >> "$O/halo_time.jsonl" 2>> "$O/halo_time.err" && \
+      timeout -k 10 300 python bench.py --comm-self --rehearse-trial --no-cpu-baseline --side-steps 0 --general-steps 0 \
+        > "$O/trial.json" 2> "$O/trial.err" ;;
     threshold)
       # EIG_MARCH_2L_MIN_ROWS: variant 15 (#13) vs the 2-line march (#16) on 4 M / 6 M / 8 M-row slabs
       for s in 64 96 128; do
