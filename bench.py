@@ -421,6 +421,11 @@ def main():
                          "ranks, else RCCL), or mailbox-step (the fused step's sums published by its last "
                          "workgroup and gathered in the next launch's prologue: no allreduce launch); auto = "
                          "all in the trial, the fastest whose alpha / beta match the RCCL run wins")
+    ap.add_argument("--transport", choices=["rccl", "mailbox-only"], default="rccl",
+                    help="N > 1: rccl = libeigmi's RCCL communicator (+ the mailbox unless --allreduce rccl); "
+                         "mailbox-only = no RCCL, every exchange over the xGMI mailbox (eig_comm_ipc_open: the "
+                         "handles travel over gloo) -- with EIGMI_FORCE_DEVICE=0 the whole N-rank run rehearsed "
+                         "on ONE GPU, which RCCL refuses")
     ap.add_argument("--launch", choices=["auto", "graph", "eager"], default="auto",
                     help="timed steps as one hipGraph replay or launched one by one; auto = graph when "
                          "N > 1 (host-bound halo/allreduce calls), eager at N = 1 (measured faster there)")
@@ -462,9 +467,17 @@ def main():
         uid = eigmi.Context.unique_id() if rank == 0 else bytes(128)
         t = torch.tensor(list(uid), dtype=torch.uint8)
         dist.broadcast(t, 0)
-        # RCCL, plus the xGMI mailbox allreduce where every rank validates it (eig_comm_init_ex
-        # EIG_COMM_MAILBOX; agreed by all ranks, else RCCL alone) -- the auto trial times both
-        ctx.comm_init(world, rank, bytes(t.tolist()), mailbox=args.allreduce != "rccl")
+        if args.transport == "mailbox-only":
+            # every rank's mailbox handle to every rank over gloo, then all open them
+            h = torch.tensor(list(ctx.ipc_handle(world, rank)), dtype=torch.uint8)
+            hs = [torch.zeros_like(h) for _ in range(world)]
+            dist.all_gather(hs, h)
+            ctx.ipc_open(b"".join(bytes(x.tolist()) for x in hs))
+        else:
+            # RCCL, plus the xGMI mailbox allreduce where every rank validates it (eig_comm_init_ex
+            # EIG_COMM_MAILBOX; agreed by all ranks, else RCCL alone) -- the auto trial times both
+            ctx.comm_init(world, rank, bytes(t.tolist()), mailbox=args.allreduce != "rccl")
+    mb_only = world > 1 and args.transport == "mailbox-only"
 
     N = args.N
     n = N ** 3
@@ -512,13 +525,16 @@ def main():
             have_mb = multi and ctx.comm_info()["allreduce"] in MAILBOX_KINDS
             ars = ((("rccl", "mailbox", "mailbox-step") if args.allreduce == "auto" else (args.allreduce,))
                    if have_mb else ("rccl",))
-            if "rccl" not in ars:
-                ars = ("rccl",) + ars  # the reference run of the alpha / beta check
+            if mb_only:
+                ars = ("mailbox", "mailbox-step")  # mailbox-only ranks: the allreduce launch is the reference
+            ref_ar = "mailbox" if mb_only else "rccl"
+            if ref_ar not in ars:
+                ars = (ref_ar,) + ars  # the reference run of the alpha / beta check
             # (the pipelined step keeps the allreduce launch under mailbox-step: same as mailbox)
             # N > 1 with the mailbox: the halo also through the halo mailbox (eig_comm_select_halo; the
             # boundary planes stored into the peers' staging over xGMI) beside ncclSend / ncclRecv
             # (--rehearse-trial: selected at one rank too, where no matrix has a halo)
-            hxs_mb = ("rccl", "mailbox") if (world > 1 or args.rehearse_trial) and have_mb else ("rccl",)
+            hxs_mb = ("rccl", "mailbox") if (world > 1 or args.rehearse_trial) and have_mb and not mb_only else ("rccl",)
             combos = [(v, h, a, x) for v in ("fused", "pipelined") for h in halos for a in ars
                       for x in (hxs_mb if a != "rccl" else ("rccl",))
                       if not (v == "pipelined" and a == "mailbox-step")]
@@ -577,15 +593,15 @@ def main():
             # a transport is a candidate only if its run reproduces the RCCL run of the same variant
             # and halo mode (same start vector, same step count) to AB_RTOL -- never on timing alone
             for (var, halo, ar, hx), (a, b) in ab.items():
-                if ar == "rccl" and hx == "rccl":
+                if ar == ref_ar and hx == "rccl":
                     continue
-                ref = ab.get((var, halo, "rccl", "rccl"))
+                ref = ab.get((var, halo, ref_ar, "rccl"))
                 mm = ab_mismatch(a, b, *ref) if ref is not None else float("inf")
                 mm = max_over_ranks(mm)
                 ok = mm <= AB_RTOL
                 tkey = f"{halo}/{ar}" + ("/halo-mailbox" if hx == "mailbox" else "")
                 ab_check[f"{var}/{tkey}"] = {"max_rel_diff_vs_rccl": mm if np.isfinite(mm) else None,
-                                             "steps": int(len(a)), "ok": bool(ok)}
+                                             "reference": ref_ar, "steps": int(len(a)), "ok": bool(ok)}
                 if not ok:
                     for k in trial:
                         if k.startswith(f"{var}/") and k.split("/", 2)[2] == tkey:
@@ -598,14 +614,18 @@ def main():
             M.tune(halo_whole=int(best_halo == "whole"))
             if multi:
                 ctx.select_allreduce(best_ar)
-            halo_x = "mailbox" if len(parts) > 4 else "rccl"
+            halo_x = "mailbox" if len(parts) > 4 or mb_only else "rccl"
             if len(hxs_mb) > 1:
                 ctx.select_halo(halo_x)
             halo_mode = best_halo
     if world > 1 and trial is None:
         # no trial: RCCL unless a mailbox transport was asked for (and is set up on every rank)
-        ctx.select_allreduce(args.allreduce if args.allreduce in ("mailbox", "mailbox-step") and
-                             ctx.comm_info()["allreduce"] in MAILBOX_KINDS else "rccl")
+        if mb_only:
+            ctx.select_allreduce(args.allreduce if args.allreduce == "mailbox-step" else "mailbox")
+            halo_x = "mailbox"
+        else:
+            ctx.select_allreduce(args.allreduce if args.allreduce in ("mailbox", "mailbox-step") and
+                                 ctx.comm_info()["allreduce"] in MAILBOX_KINDS else "rccl")
     fused = variant in ("fused", "pipelined")
     pipelined = variant == "pipelined"
     # the K timed steps are captured as one hipGraph before the clock starts (kernels, halo

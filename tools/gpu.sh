@@ -243,6 +243,13 @@ run_task() {
       timeout -k 10 200 python3 tools/halo_time.py 256 4 20 40 >> "$O/halo_time.jsonl" 2>> "$O/halo_time.err" && \
       timeout -k 10 300 python bench.py --comm-self --rehearse-trial --no-cpu-baseline --side-steps 0 --general-steps 0 \
         > "$O/trial.json" 2> "$O/trial.err" ;;
+    mbonly)
+      # the whole N > 1 bench path (launcher, z-slab partition, trial, timed graph, max over ranks) on ONE
+      # GPU: mailbox-only ranks (no RCCL, which refuses two ranks on a device), every rank on device 0
+      EIGMI_FORCE_DEVICE=0 timeout -k 10 600 python bench.py --gpus 2 --transport mailbox-only --steps 50 --warmup 5 \
+        > "$O/bench_mbonly2.json" 2> "$O/bench_mbonly2.err" && \
+      EIGMI_FORCE_DEVICE=0 timeout -k 10 600 python bench.py --gpus 4 --transport mailbox-only --steps 50 --warmup 5 \
+        > "$O/bench_mbonly4.json" 2> "$O/bench_mbonly4.err" ;;
     threshold)
       # EIG_MARCH_2L_MIN_ROWS: variant 15 (#13) vs the 2-line march (#16) on 4 M / 6 M / 8 M-row slabs
       for s in 64 96 128; do
