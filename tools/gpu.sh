@@ -46,6 +46,9 @@
 #   detprobe             run-to-run determinism of the inverse-iteration pieces (tools/det_probe.py)
 #   xch                  the step's allreduce transports on one GPU (one-rank RCCL / mailbox / in-kernel
 #                        mailbox-step): slab and cube sweeps + the bench's N > 1 trial rehearsed -> xch_*.jsonl
+#   threshold            variant 15 vs the 2-line march on 4 / 6 / 8 M-row slabs (EIG_MARCH_2L_MIN_ROWS) -> threshold.jsonl
+#   halotime             the halo mailbox between 2 / 4 processes on one GPU (kernel trace) + the trial rehearsal
+#   mbonly               bench.py --gpus 2 / 4 --transport mailbox-only on ONE GPU (the whole N > 1 bench path)
 #
 # Session scripts of earlier rounds (tools/gpu_r04*.sh) are these tasks chained, e.g.
 #   TAG=r05a bash tools/gpu.sh tests:test_gpu_value_march.py sweep sweeppmc
