@@ -253,6 +253,20 @@ run_task() {
         > "$O/bench_mbonly2.json" 2> "$O/bench_mbonly2.err" && \
       EIGMI_FORCE_DEVICE=0 timeout -k 10 600 python bench.py --gpus 4 --transport mailbox-only --steps 50 --warmup 5 \
         > "$O/bench_mbonly4.json" 2> "$O/bench_mbonly4.err" ;;
+    runs2l)
+      # plane runs of the 2-line march (#16) and the 1-line march (#13): few long wave chains, one
+      # workgroup per CU, vs the default plan
+      timeout -k 10 300 python3 tools/lanczos_sweep.py --N 256 --rounds 3 --steps 40 \
+        --variants fused:arrays#16,fused:arrays@1#16,fused:arrays@2#16,fused:arrays#13,fused:arrays@1#13,fused:arrays@2#13,fused:arrays@4#13,mv:arrays,mv:arrays@1,mv:arrays@2,mv:arrays@4 \
+        > "$O/runs_256.jsonl" 2> "$O/runs.err" && \
+      timeout -k 10 300 python3 tools/lanczos_sweep.py --N 128 --rounds 3 --steps 40 \
+        --variants fused:arrays#13,fused:arrays#16,fused:arrays@1#16,fused:arrays@2#16,fused:arrays@4#16,fused:arrays@1#13,fused:arrays@2#13 \
+        > "$O/runs_128.jsonl" 2>> "$O/runs.err" && \
+      for s in 32 64 96 128; do
+        timeout -k 10 200 python3 tools/lanczos_sweep.py --N 256 --slab $s --rounds 3 --steps 40 \
+          --variants fused:arrays#13,fused:arrays#16,fused:arrays@1#16,fused:arrays@2#16,fused:arrays@1#13,fused:arrays@2#13 \
+          >> "$O/runs_slab.jsonl" 2>> "$O/runs.err" || return 1
+      done ;;
     threshold)
       # EIG_MARCH_2L_MIN_ROWS: variant 15 (#13) vs the 2-line march (#16) on 4 M / 6 M / 8 M-row slabs
       for s in 64 96 128; do
