@@ -1494,7 +1494,9 @@ __device__ __forceinline__ void march_rows_geo2(const SellB1 &A, const MarchPlan
 // rows) 206.5-206.8 us vs 223.5 us for variant 15 (profiles/r06e_sweep256_2lines.jsonl, 0.65 of HBM),
 // but 2 M-row grids (128^3, one rank's 256^2 x 32 slab) 28.2-28.4 vs 27.7-27.9 us: fewer, longer
 // wave chains cost more there than the halved gathers save.  256^2 slabs (profiles/r06m_threshold.jsonl):
-// 4 M rows 47.1 vs 46.1 us, 6 M rows 84.3 vs 89.8 us, 8 M rows 111.7 vs 116.7 us -- the threshold is 6 M.
+// 4 M rows 47.1 vs 46.1 us, 6 M rows 84.3 vs 89.8 us, 8 M rows 111.7 vs 116.7 us; with two plane runs
+// per column on wide planes (march_plan, round 6) 4 M rows 45.6 vs 46.0 us, 2 M rows 27.6 either way --
+// the threshold is 4 M.
 constexpr bool kMarch2lDefault = true;
 constexpr bool is_march2l(int uni) { return uni == 22 || uni == 23 || uni == 24; }
 
@@ -2828,15 +2830,24 @@ static MarchPlan march_plan(const eig_mat_s &A, int mode, i64 zb = 0, i64 ze = -
   //    runs of >= 10 planes, as long as that leaves a quarter of the resident slots busy (64^3, 64
   //    columns: 6 runs of 10 planes took 20.1 us, 64 runs of one plane 13.3)
   //  * (round 3, uniform-band march: 256^3 6 runs 129.8-134.0 us, 8 runs 133.6-137.1: at most 6)
+  //  * round 6, the value pack marches (15, 22-24) on wide planes: TWO runs per column, i.e. long
+  //    chains of half the planes each (profiles/r06q_*, r06r_runs_*: 256^3 2-line 193.2 us at 2 runs
+  //    vs 208.3 at its former 16 (1: 268.2); 1-line 204.4 at 2 vs 225.2 at 8 (1: 255.8, 4: 261.6);
+  //    256^2 slabs of 32 / 64 / 96 / 128 planes 27.6 / 45.6 / 77.9 / 102.2 us for the 2-line march
+  //    at 2 runs, the best or equal of every count tried).  On 128^3 (256 columns) 2 runs are slow
+  //    (52.3 us vs 28.3): the rule is for wide planes only.
   const int uni = march_uniform(A, fused, nplanes);
-  if (fused && ncol >= 1024)
+  const bool wide_pack = fused && ncol >= 1024 && (uni == 15 || is_march2l(uni));
+  if (wide_pack)
+    nseg = std::min<i64>(2, nplanes);
+  else if (fused && ncol >= 1024)
     nseg = std::min<i64>(nplanes / 2 > 0 ? nplanes / 2 : 1,
                          std::max<i64>(2, std::min<i64>(uni == 7 || uni >= 10 ? 8 : 6, nplanes / 32)));
   else if (fused)  // (geo2 marches: runs of >= 16 planes -- 128^3 8 runs 24.3 us, 12: 25.3, 16: 26.4)
     nseg = std::min(nseg, std::max<i64>({1, nplanes / (uni >= 7 ? 16 : 10), (resident / 4 + ncol - 1) / ncol}));
   // variant 22 marches line PAIRS: half the items per plane run, so twice the runs for as many waves
   const i64 items_per_run = is_march2l(uni) ? ncol / 2 : ncol;
-  if (is_march2l(uni)) nseg = std::min<i64>(nplanes, 2 * nseg);
+  if (is_march2l(uni) && !wide_pack) nseg = std::min<i64>(nplanes, 2 * nseg);
   if (A.tune_march_runs > 0) nseg = std::min<i64>(A.tune_march_runs, nplanes);  // eig_mat_tune
   while (nseg > 1 && (items_per_run * nseg + kWaves - 1) / kWaves > kMaxRedBlocks) --nseg;
   if ((items_per_run * nseg + kWaves - 1) / kWaves > kMaxRedBlocks) return mp;

@@ -43,7 +43,7 @@ LANCZOS_FUSED = 4
 LANCZOS_PIPELINED = 8
 LANCZOS_AUTO = 16
 IPC_HANDLE_BYTES = 64
-MARCH_2L_MIN_ROWS = 6291456  # EIG_MARCH_2L_MIN_ROWS: owned rows from which the fused step marches line pairs
+MARCH_2L_MIN_ROWS = 4194304  # EIG_MARCH_2L_MIN_ROWS: owned rows from which the fused step marches line pairs
 ALLREDUCE_KINDS = {0: "none", 1: "rccl", 2: "xgmi-mailbox", 3: "loopback", 4: "xgmi-mailbox-step"}
 
 

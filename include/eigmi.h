@@ -285,7 +285,7 @@ enum { EIG_TUNE_MARCH_RUNS = 1, EIG_TUNE_BOX_SEGS = 2, EIG_TUNE_MARCH_PREFETCH =
  * registers, half the gathers; the fused step's sums then add the rows in another order;
  * 0 = automatic: the fused step on 3-D value images takes variant 22 on ranks of at least
  * EIG_MARCH_2L_MIN_ROWS owned rows, else 15.  Bitwise the same rows for every value. */
-#define EIG_MARCH_2L_MIN_ROWS 6291456
+#define EIG_MARCH_2L_MIN_ROWS 4194304
 int eig_mat_tune(eig_mat_t mat, int key, int value);
 
 /* a13: A += shift*I on the diagonal of every diagonal block (eigensolver.hh:59-66). */
