@@ -2835,9 +2835,12 @@ static MarchPlan march_plan(const eig_mat_s &A, int mode, i64 zb = 0, i64 ze = -
   //    vs 208.3 at its former 16 (1: 268.2); 1-line 204.4 at 2 vs 225.2 at 8 (1: 255.8, 4: 261.6);
   //    256^2 slabs of 32 / 64 / 96 / 128 planes 27.6 / 45.6 / 77.9 / 102.2 us for the 2-line march
   //    at 2 runs, the best or equal of every count tried).  On 128^3 (256 columns) 2 runs are slow
-  //    (52.3 us vs 28.3): the rule is for wide planes only.
+  //    (52.3 us vs 28.3): the rule is for wide planes only.  The same holds for the P1 Kuhn march
+  //    (profiles/r06t_runs_p1k.jsonl: fused step 312.5 us at 2 runs vs 333.9 at 8, 4: 380.9; eig_mv
+  //    263.2 vs 280.0) and the 7-point value eig_mv (151.9 vs 154.7, r06r_runs_256.jsonl).
   const int uni = march_uniform(A, fused, nplanes);
-  const bool wide_pack = fused && ncol >= 1024 && (uni == 15 || is_march2l(uni));
+  const bool wide_pack = ncol >= 1024 && chunk == 64 &&
+                         (kuhn || (fused ? (uni == 15 || is_march2l(uni)) : (uni == 0 && A.sym_geo)));
   if (wide_pack)
     nseg = std::min<i64>(2, nplanes);
   else if (fused && ncol >= 1024)
