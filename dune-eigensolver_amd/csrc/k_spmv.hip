@@ -2837,10 +2837,11 @@ static MarchPlan march_plan(const eig_mat_s &A, int mode, i64 zb = 0, i64 ze = -
   //    at 2 runs, the best or equal of every count tried).  On 128^3 (256 columns) 2 runs are slow
   //    (52.3 us vs 28.3): the rule is for wide planes only.  The same holds for the P1 Kuhn march
   //    (profiles/r06t_runs_p1k.jsonl: fused step 312.5 us at 2 runs vs 333.9 at 8, 4: 380.9; eig_mv
-  //    263.2 vs 280.0) and the 7-point value eig_mv (151.9 vs 154.7, r06r_runs_256.jsonl).
+  //    263.2 vs 280.0); not for the 7-point value eig_mv (151.9 vs 154.7 on one box, 152.8 vs 152.2 on
+  //    another: r06r_runs_256.jsonl, r06u_runs_uniform_mv.jsonl) nor the uniform-band march (fused
+  //    132.7 vs 132.1, eig_mv 61.3 vs 48.9).
   const int uni = march_uniform(A, fused, nplanes);
-  const bool wide_pack = ncol >= 1024 && chunk == 64 &&
-                         (kuhn || (fused ? (uni == 15 || is_march2l(uni)) : (uni == 0 && A.sym_geo)));
+  const bool wide_pack = ncol >= 1024 && chunk == 64 && (kuhn || (fused && (uni == 15 || is_march2l(uni))));
   if (wide_pack)
     nseg = std::min<i64>(2, nplanes);
   else if (fused && ncol >= 1024)
