@@ -267,6 +267,8 @@ run_task() {
           --variants fused:arrays#13,fused:arrays#16,fused:arrays@1#16,fused:arrays@2#16,fused:arrays@1#13,fused:arrays@2#13 \
           >> "$O/runs_slab.jsonl" 2>> "$O/runs.err" || return 1
       done ;;
+    spmmruns)
+      timeout -k 10 300 python3 tools/spmm_runs.py 128 256 > "$O/spmm_runs.jsonl" 2> "$O/spmm_runs.err" ;;
     threshold)
       # EIG_MARCH_2L_MIN_ROWS: variant 15 (#13) vs the 2-line march (#16) on 4 M / 6 M / 8 M-row slabs
       for s in 64 96 128; do
