@@ -4,7 +4,7 @@ process, so GPU_MAX_HW_QUEUES can be set before the HIP runtime starts).
 The 3-D Poisson matrix at N^3 (the benchmark's image: EIG_MAT_NO_UNIFORM, every band value streamed)
 is split into P z-slabs of N/P planes, one virtual rank (host thread + context) per slab over the
 in-process loopback hub (eig_loopback_create).  Every rank runs the step kernel the benchmark times
-on its slab (k_lanczos_fused_march, value-march variant 15) with
+on its slab (k_lanczos_fused_march: the value march, variant 15 or the 2-line 22 by rank size) with
   * the loopback halo (device copies) and the loopback allreduce, split launches (interior march +
     boundary slices) and whole launches (EIG_TUNE_HALO = 1),
   * the in-kernel allreduce (EIG_AR_MAILBOX_STEP, csrc/xch_dev.h: the last workgroup of a launch
