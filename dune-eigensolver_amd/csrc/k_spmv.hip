@@ -2586,12 +2586,7 @@ static int grid_for_slices(K kernel, i64 count, int num_cu)
       per_cu = 4;
     cache = {(const void *)kernel, per_cu};
   }
-  // EIGMI_SLICE_GRID (measurement): at most that many workgroups, i.e. fewer rows in flight per XCD
-  static const i64 env_cap = [] {
-    const char *e = std::getenv("EIGMI_SLICE_GRID");
-    return e ? (i64)std::atoll(e) : (i64)0;
-  }();
-  const i64 cap = env_cap > 0 ? std::min<i64>(env_cap, (i64)per_cu * num_cu) : (i64)per_cu * num_cu;
+  const i64 cap = (i64)per_cu * num_cu;
   const i64 need = (count + kWaves - 1) / kWaves;
   if (need < 1) return 1;
   return (int)(need < cap ? need : cap);

@@ -267,11 +267,6 @@ run_task() {
           --variants fused:arrays#13,fused:arrays#16,fused:arrays@1#16,fused:arrays@2#16,fused:arrays@1#13,fused:arrays@2#13 \
           >> "$O/runs_slab.jsonl" 2>> "$O/runs.err" || return 1
       done ;;
-    slicegrid)
-      # the row kernels' grid capped (EIGMI_SLICE_GRID): general scrambled + RCM 256^3 SpMV / steps
-      for g in 0 256 512 1024; do
-        EIGMI_SLICE_GRID=$g timeout -k 10 300 python -u tools/csr_general.py > "$O/slicegrid_$g.jsonl" 2>> "$O/slicegrid.err" || return 1
-      done ;;
     spmmruns)
       timeout -k 10 300 python3 tools/spmm_runs.py 128 256 > "$O/spmm_runs.jsonl" 2> "$O/spmm_runs.err" ;;
     threshold)
