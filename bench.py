@@ -535,6 +535,15 @@ def main():
             # boundary planes stored into the peers' staging over xGMI) beside ncclSend / ncclRecv
             # (--rehearse-trial: selected at one rank too, where no matrix has a halo)
             hxs_mb = ("rccl", "mailbox") if (world > 1 or args.rehearse_trial) and have_mb and not mb_only else ("rccl",)
+            if len(hxs_mb) > 1:
+                # the halo mailbox's staging is built at matrix creation; a rank set that could not build
+                # it (agreed there) keeps ncclSend / ncclRecv, and every rank gets the same answer here
+                try:
+                    ctx.select_halo("mailbox")
+                    ctx.select_halo("rccl")
+                except eigmi.EigError as e:
+                    print(f"bench: halo mailbox unavailable ({e}); RCCL halo only", file=sys.stderr, flush=True)
+                    hxs_mb = ("rccl",)
             combos = [(v, h, a, x) for v in ("fused", "pipelined") for h in halos for a in ars
                       for x in (hxs_mb if a != "rccl" else ("rccl",))
                       if not (v == "pipelined" and a == "mailbox-step")]

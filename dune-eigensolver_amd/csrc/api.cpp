@@ -733,6 +733,9 @@ extern "C" int eig_comm_select_halo(eig_ctx_t ctx, int kind)
               "eig_comm_select_halo: EIG_HALO_RCCL or EIG_HALO_MAILBOX");
     EIG_CHECK(ctx->comm && ctx->mbox && ctx->mbox->ready, EIG_ERR_ARG,
               "eig_comm_select_halo: needs RCCL and a validated mailbox (eig_comm_init_ex EIG_COMM_MAILBOX)");
+    EIG_CHECK(kind == EIG_HALO_RCCL || ctx->hbox || ctx->nranks == 1, EIG_ERR_RCCL,
+              "eig_comm_select_halo: no halo mailbox staging (set up by eig_mat_create_bcsr_dist; it failed or no "
+              "distributed matrix with a halo exists yet)");
     DeviceGuard dg(ctx->device);
     EIG_HIP(hipStreamSynchronize(ctx->stream));
     EIG_HIP(hipStreamSynchronize(ctx->comm_stream));
@@ -1605,7 +1608,25 @@ extern "C" int eig_mat_create_bcsr_dist_ex(eig_ctx_t ctx, int64_t nb_rows_global
           for (int k = 0; k < nq; ++k) most = std::max<i64>(most, qr[3 * k + 2]);
         }
         const i64 cap = 8 * most;
-        if (cap > 0 && (!ctx->hbox || ctx->hbox->dev.cap < cap)) halobox_setup(ctx, cap);
+        if (cap > 0 && (!ctx->hbox || ctx->hbox->dev.cap < cap))
+        {
+          if (!ctx->comm)
+            halobox_setup(ctx, cap);  // mailbox-only ranks: their only halo transport
+          else
+          {
+            // beside RCCL the halo mailbox is an option (eig_comm_select_halo): a rank set that could
+            // not build it keeps ncclSend / ncclRecv (the failure is agreed inside halobox_setup)
+            try
+            {
+              halobox_setup(ctx, cap);
+            }
+            catch (const Error &)
+            {
+              halobox_free(ctx);
+              ctx->halo_mailbox = false;
+            }
+          }
+        }
       }
       for (int k = 0; k < nrecv; ++k) A->recvs.push_back({(int)rv[3 * k], rv[3 * k + 1], rv[3 * k + 2]});
       for (int k = 0; k < nsend; ++k) A->sends.push_back({(int)sd[3 * k], sd[3 * k + 1], sd[3 * k + 2]});
