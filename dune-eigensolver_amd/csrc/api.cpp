@@ -259,7 +259,7 @@ void halobox_setup(eig_ctx_t ctx, i64 cap)
     }
     h->alloc = p;
     EIG_HIP(hipMemset(p, 0, bytes));
-    EIG_HIP(hipMalloc(&h->state, 512));  // seq at 0, the push / pull tickets at 128 / 256
+    EIG_HIP(hipMalloc(&h->state, 512));  // seq[16] at 0, the push / pull tickets at 128 / 256
     EIG_HIP(hipMemset(h->state, 0, 512));
     hipIpcMemHandle_t ih;
     EIG_HIP(hipIpcGetMemHandle(&ih, p));

@@ -133,7 +133,7 @@ struct HaloBox {
   u64 *peer_flags[kMaxMailboxRanks] = {};       // rank r's lines mapped here (peer_flags[me] = flags)
   double *stage = nullptr;                      // mine: [2][P][cap]
   double *peer_stage[kMaxMailboxRanks] = {};
-  u64 *seq = nullptr;                           // device: sequence number of the last completed exchange
+  u64 *seq = nullptr;                           // device: [P] exchanges completed with each peer
   unsigned *ticket = nullptr;                   // device: push / pull last-workgroup tickets (128 B apart)
   int *err = nullptr;                           // the mailbox's error word (Mailbox::err)
   long long cap = 0;                            // doubles per slot

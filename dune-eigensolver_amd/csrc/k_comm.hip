@@ -100,10 +100,12 @@ void launch_mailbox_allreduce(double *buf, int count, const Mailbox &mb, unsigne
 //   pull: every workgroup's first wave polls my lines of those peers until they read s (bounded,
 //         like k_mailbox_allreduce), then the workgroups copy the receive ranges out of my staging
 //         into the window; the last workgroup stores s as the completed sequence number.
-// Parity reuse: rank A pushes s + 2 (over the slot of s) only after its pull of s + 1, which needs
-// rank B's line of s + 1, which B stores only after its pull of s -- i.e. after B read slot s.  This
-// needs the line from every peer A writes to, hence the union of send and receive peers.  The
-// sequence number lives in device memory (captured exchanges replay correctly).  A timed-out pull,
+// Sequence numbers count the exchanges of each PAIR of ranks (seq[peer]): a matrix may connect rank A
+// with B but not with C, and C must not see A's count move.  Every exchange of a matrix involves both
+// ranks of each pair it connects (the peer relation, sends union receives, is symmetric), so a pair's
+// two counters stay equal.  Parity reuse: rank A pushes s + 2 to B (over the slot of s) only after its
+// pull of s + 1, which needs B's line of s + 1, which B stores only after its pull of s -- i.e. after
+// B read slot s.  The counters live in device memory (captured exchanges replay correctly).  A timed-out pull,
 // or any pull or push once the mailbox's error word is set, writes NaN instead of values -- into the
 // ghosts and into the peers' slots -- so every rank's recurrence turns NaN the same way.
 // ---------------------------------------------------------------------------------------------
@@ -120,13 +122,12 @@ __device__ __forceinline__ bool halo_last_group(unsigned *ticket)
 __global__ __launch_bounds__(256) void k_halo_push(HaloBox hb, HaloXfer snd, HaloXfer sync, const double *x,
                                                    const double *x2, int w)
 {
-  const u64 seq = __hip_atomic_load(hb.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
-  const int par = (int)(seq & 1);
   const bool poisoned = __hip_atomic_load(hb.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
   const double nan = __builtin_nan("");
   const long long g0 = (long long)blockIdx.x * blockDim.x + threadIdx.x, gs = (long long)gridDim.x * blockDim.x;
   for (int k = 0; k < snd.n; ++k)
   {
+    const int par = (int)((__hip_atomic_load(hb.seq + snd.peer[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1) & 1);
     double *dst = hb.peer_stage[snd.peer[k]] + ((long long)par * hb.P + hb.me) * hb.cap;
     const long long n = snd.cnt[k] * w;
     const double *a = x + snd.off[k] * w;
@@ -142,8 +143,11 @@ __global__ __launch_bounds__(256) void k_halo_push(HaloBox hb, HaloXfer snd, Hal
   {
     const int t = threadIdx.x;
     if (t < sync.n)
-      __hip_atomic_store(hb.peer_flags[sync.peer[t]] + ((long long)par * hb.P + hb.me) * kHaloFlagStride, seq,
+    {
+      const u64 seq = __hip_atomic_load(hb.seq + sync.peer[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+      __hip_atomic_store(hb.peer_flags[sync.peer[t]] + ((long long)(seq & 1) * hb.P + hb.me) * kHaloFlagStride, seq,
                          __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     if (t == 0) __hip_atomic_store(hb.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
@@ -152,13 +156,13 @@ __global__ __launch_bounds__(256) void k_halo_pull(HaloBox hb, HaloXfer rcv, Hal
                                                    int w, unsigned long long timeout)
 {
   __shared__ int s_late;
-  const u64 seq = __hip_atomic_load(hb.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
-  const int par = (int)(seq & 1);
   const int t = threadIdx.x;
   if (t < 64)
   {
     const bool mine = t < sync.n;
-    const u64 *line = hb.flags + ((long long)par * hb.P + (mine ? sync.peer[t] : 0)) * kHaloFlagStride;
+    const int peer = mine ? sync.peer[t] : 0;
+    const u64 seq = __hip_atomic_load(hb.seq + peer, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+    const u64 *line = hb.flags + ((long long)(seq & 1) * hb.P + peer) * kHaloFlagStride;
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     bool late = false;
     for (;;)
@@ -187,6 +191,7 @@ __global__ __launch_bounds__(256) void k_halo_pull(HaloBox hb, HaloXfer rcv, Hal
   const long long g0 = (long long)blockIdx.x * blockDim.x + t, gs = (long long)gridDim.x * blockDim.x;
   for (int k = 0; k < rcv.n; ++k)
   {
+    const int par = (int)((__hip_atomic_load(hb.seq + rcv.peer[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1) & 1);
     const double *src = hb.stage + ((long long)par * hb.P + rcv.peer[k]) * hb.cap;
     const long long n = rcv.cnt[k] * w;
     double *a = x + rcv.off[k] * w;
@@ -198,11 +203,16 @@ __global__ __launch_bounds__(256) void k_halo_pull(HaloBox hb, HaloXfer rcv, Hal
     }
   }
   if (halo_last_group(hb.ticket + 32))
-    if (t == 0)
+  {
+    // (every workgroup has read the counters: the last one advances them)
+    if (t < sync.n)
     {
-      __hip_atomic_store(hb.seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(hb.ticket + 32, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      u64 *c = hb.seq + sync.peer[t];
+      __hip_atomic_store(c, __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
     }
+    if (t == 0) __hip_atomic_store(hb.ticket + 32, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 void launch_halo_mailbox(const HaloBox &hb, const HaloXfer &snd, const HaloXfer &rcv, const HaloXfer &sync, double *x,

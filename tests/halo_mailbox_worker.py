@@ -13,6 +13,10 @@ N (r + 1) / P), so every interface carries a full plane of ghosts:
     exchanges of 8-column blocks (width 8).
 
     python tests/halo_mailbox_worker.py RANK NRANKS WORKDIR MODE
+With P = 3 the run starts on a matrix that couples ranks 0 and 1 only (rank 2 owns a separate block:
+it takes no part in that matrix's exchanges), so the exchange counters are per pair of ranks -- the
+z-slab matrices after it would otherwise wait for numbers rank 2 never published.
+
 MODE "run": everything above, saved to r<RANK>.npz (with the rank's serial block Lanczos Ritz values,
 computed on a second context without a transport).
 MODE "stall": rank 0 calls eig_mv while rank 1 never exchanges (it waits for rank 0's "done" file):
@@ -34,6 +38,33 @@ N = 64       # the 7-point boxes: 64^3 (grid lines of 64 rows: the value march a
 NB = 16      # the P1 pencil: 16^3
 STEPS = 40
 BLOCK, BSTEPS, BNEV = 16, 5, 4
+
+
+def box7(nz, seed, nx=64, ny=4):
+    """A random symmetric diagonally dominant 7-point box nx x ny x nz (scipy CSR)."""
+    import scipy.sparse as sp
+    rng = np.random.default_rng(seed)
+    n = nx * ny * nz
+    idx = np.arange(n)
+    x, y, z = idx % nx, (idx // nx) % ny, idx // (nx * ny)
+    rows, cols, vals = [idx], [idx], [6.0 + rng.random(n)]
+    for step, ok in ((1, x < nx - 1), (nx, y < ny - 1), (nx * ny, z < nz - 1)):
+        i = idx[ok]
+        w = -0.5 - rng.random(i.size)
+        rows += [i, i + step]
+        cols += [i + step, i]
+        vals += [w, w]
+    S = sp.csr_matrix((np.concatenate(vals), (np.concatenate(rows), np.concatenate(cols))), shape=(n, n))
+    S.sort_indices()
+    return S
+
+
+def partial_matrix():
+    """Ranks 0 and 1 split a 64 x 4 x 12 box (6 planes each, coupled), rank 2 owns a 64 x 4 x 6 box."""
+    import scipy.sparse as sp
+    G = sp.block_diag([box7(12, 7), box7(6, 8)], format="csr")
+    G.sort_indices()
+    return G, [0, 6 * 256, 12 * 256, 18 * 256]
 
 
 def slab(n_planes, D, P, r):
@@ -84,6 +115,23 @@ def main(rank, P, wd, mode):
             wait_for([os.path.join(wd, "done")], timeout=200.0)
         np.savez(os.path.join(wd, f"r{rank}.npz"), **out)
         return
+    if P == 3:
+        # first a matrix whose exchanges involve ranks 0 and 1 only
+        G, cuts = partial_matrix()
+        gb, ge = cuts[rank], cuts[rank + 1]
+        Gr = G[gb:ge]
+        Q = eigmi.Matrix.from_rows(ctx, G.shape[0], gb, Gr.indptr.astype(np.int64), Gr.indices.astype(np.int32),
+                                   Gr.data)
+        out["partial_halo"] = int(Q.info.halo_recv)
+        xq = np.random.default_rng(5).standard_normal(G.shape[0])
+        qx, qy = Q.window_vector(xq[gb:ge]), Q.window_vector()
+        Q.mv(qx, qy)
+        out["partial_y"] = Q.owned(qy)
+        qx.free()
+        qy.free()
+        ctx.select_allreduce("mailbox")
+        out["partial_a"], out["partial_b"], _ = eigmi.lanczos_run(Q, 20, seed=123, fused=True)
+        Q.close()
     # eig_mv: the window vector's ghosts through the halo mailbox, interior planes overlapped
     xv, yv = M.window_vector(x[b:b + cnt]), M.window_vector()
     M.mv(xv, yv)

@@ -94,6 +94,17 @@ def test_halo_mailbox_processes(tmp_path, P):
         assert np.allclose(d["ritz_dist"], d["ritz_serial"], rtol=1e-10, atol=0), (d["ritz_dist"], d["ritz_serial"])
         cnt_ = d["counters"]
         assert int(cnt_[0]) == 0 and int(cnt_[2]) > 0, cnt_  # no RCCL allreduce; halo groups exchanged
+    if P == 3:
+        # the matrix coupling ranks 0 and 1 only, run first: exchange counters per pair of ranks
+        G, cuts = W.partial_matrix()
+        Ap = oracle.CSR(G.shape[0], G.indptr.astype(np.int64), G.indices.astype(np.int32), G.data)
+        xq = np.random.default_rng(5).standard_normal(G.shape[0])
+        yq = oracle.csr_mv(Ap, xq)
+        qa, qb = oracle.lanczos_fused(Ap, oracle.random_vec(Ap.n, 123), 20)
+        for r, d in enumerate(res):
+            assert int(d["partial_halo"]) == (256 if r < 2 else 0)
+            assert np.array_equal(d["partial_y"], yq[cuts[r]:cuts[r + 1]]), r
+            assert _rel(d["partial_a"], qa) <= 1e-12 and _rel(d["partial_b"][1:], qb[1:]) <= 1e-12, r
     print(f"P={P}: worst rel diff vs orc_lanczos_fused {worst:.2e}; Ritz {res[0]['ritz_dist']}")
 
 
