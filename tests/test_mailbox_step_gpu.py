@@ -86,6 +86,21 @@ def test_step_exchange_one_rank_bitwise(ctx, mb_ctx, name, mat, flags, mv):
     mb_ctx.select_allreduce("rccl")
 
 
+def test_select_halo_one_rank(ctx, mb_ctx):
+    """eig_comm_select_halo: accepted on a context with RCCL and the mailbox (one rank: no halo to move,
+    the recurrence bitwise unchanged), refused without RCCL."""
+    mat = list(_mats())[1]
+    ref = _run(ctx, mat[1], mat[2], "fused", False)
+    mb_ctx.select_allreduce("mailbox")
+    for hx in ("mailbox", "rccl"):
+        mb_ctx.select_halo(hx)
+        a, b, _ = _run(mb_ctx, mat[1], mat[2], "fused", True)
+        assert np.array_equal(a, ref[0]) and np.array_equal(b, ref[1]), hx
+    mb_ctx.select_allreduce("rccl")
+    with pytest.raises(eigmi.EigError):
+        ctx.select_halo("mailbox")  # no transport at all
+
+
 def _spawn(P, wd, mode):
     procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "mailbox_step_worker.py"), str(r), str(P),
                                wd, mode], stdout=subprocess.PIPE, stderr=subprocess.STDOUT) for r in range(P)]
