@@ -534,7 +534,8 @@ def main():
             # N > 1 with the mailbox: the halo also through the halo mailbox (eig_comm_select_halo; the
             # boundary planes stored into the peers' staging over xGMI) beside ncclSend / ncclRecv
             # (--rehearse-trial: selected at one rank too, where no matrix has a halo)
-            hxs_mb = ("rccl", "mailbox") if (world > 1 or args.rehearse_trial) and have_mb and not mb_only else ("rccl",)
+            hx_ok = (world > 1 or args.rehearse_trial) and have_mb and not mb_only
+            hxs_mb = ("rccl", "mailbox") if hx_ok else ("rccl",)
             if len(hxs_mb) > 1:
                 # the halo mailbox's staging is built at matrix creation; a rank set that could not build
                 # it (agreed there) keeps ncclSend / ncclRecv, and every rank gets the same answer here
