@@ -8,7 +8,8 @@ Against the CPU restatement on the GLOBAL matrix (oracle/oracle.cc, the checker 
   * fused steps within rtol 1e-12 of orc_lanczos_fused on the value march and on the SELL image,
     split and whole halo launches, the mailbox allreduce launch and the in-kernel exchange, eager and
     replayed from a hipGraph -- the in-kernel exchange BITWISE the allreduce launch (both sum the
-    slots in rank order), and every rank holding the same coefficients;
+    slots in rank order), BITWISE the same runs over the in-process loopback transport (device-copy
+    halo, host allreduce), and every rank holding the same coefficients;
   * the classic and pipelined steps within 1e-12 of their restatements;
   * C5's block Lanczos (P1 K / M, block 16, exchanges of 8-column blocks) within 1e-10 of the
     single-rank run.
@@ -18,6 +19,7 @@ SURVEY 8(e)."""
 import os
 import subprocess
 import sys
+import threading
 
 import numpy as np
 import pytest
@@ -47,6 +49,41 @@ def _spawn(P, wd, mode):
     for r, p in enumerate(procs):
         assert p.returncode == 0, f"rank {r} failed:\n{logs[r][-3000:]}"
     return [np.load(os.path.join(wd, f"r{r}.npz")) for r in range(P)]
+
+
+def _loopback_runs(P):
+    """The same slabs and fused runs over the in-process loopback transport (device copies for the halo,
+    a host sum in rank order for the allreduce): {(name, halo): (alpha, beta)} of every rank."""
+    n, D = W.N ** 3, W.N * W.N
+    hub = eigmi.loopback_create(P)
+    out = [None] * P
+
+    def rank(r):
+        c = eigmi.Context(0)
+        res = {}
+        try:
+            c.comm_init_loopback(hub, r)
+            b, cnt = W.slab(W.N, D, P, r)
+            rp, col, v = eigmi.gen_rows(eigmi.GEN_VARCOEF3D, W.N, b, cnt)
+            for name, flags in (("march", 0), ("sell", eigmi.MAT_NO_BAND)):
+                A = eigmi.Matrix.from_rows(c, n, b, rp, col, v, flags=flags)
+                for halo in ("split", "whole"):
+                    A.tune(halo_whole=int(halo == "whole"))
+                    a, be, _ = eigmi.lanczos_run(A, W.STEPS, seed=123, fused=True)
+                    res[(name, halo)] = (a, be)
+                A.close()
+        except Exception as e:  # noqa: BLE001 -- reported below
+            res["error"] = repr(e)
+        finally:
+            c.close()
+        out[r] = res
+    th = [threading.Thread(target=rank, args=(r,)) for r in range(P)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    eigmi.loopback_destroy(hub)
+    return out
 
 
 def _rel(a, ref):
@@ -94,6 +131,14 @@ def test_halo_mailbox_processes(tmp_path, P):
         assert np.allclose(d["ritz_dist"], d["ritz_serial"], rtol=1e-10, atol=0), (d["ritz_dist"], d["ritz_serial"])
         cnt_ = d["counters"]
         assert int(cnt_[0]) == 0 and int(cnt_[2]) > 0, cnt_  # no RCCL allreduce; halo groups exchanged
+    # bitwise the loopback transport: the halo moves exact copies and both allreduces sum the ranks'
+    # values in rank order, so the transport must not change a bit
+    lb = _loopback_runs(P)
+    for r, d in enumerate(res):
+        assert "error" not in lb[r], lb[r]
+        for (name, halo), (a, be) in lb[r].items():
+            assert np.array_equal(d[f"a_{name}_mailbox_{halo}"], a), (r, name, halo)
+            assert np.array_equal(d[f"b_{name}_mailbox_{halo}"], be), (r, name, halo)
     if P == 3:
         # the matrix coupling ranks 0 and 1 only, run first: exchange counters per pair of ranks
         G, cuts = W.partial_matrix()
