@@ -267,6 +267,8 @@ run_task() {
           --variants fused:arrays#13,fused:arrays#16,fused:arrays@1#16,fused:arrays@2#16,fused:arrays@1#13,fused:arrays@2#13 \
           >> "$O/runs_slab.jsonl" 2>> "$O/runs.err" || return 1
       done ;;
+    chebsegs)
+      timeout -k 10 400 python3 tools/cheb_segs.py 256 > "$O/cheb_segs.jsonl" 2> "$O/cheb_segs.err" ;;
     spmmruns)
       timeout -k 10 300 python3 tools/spmm_runs.py 128 256 > "$O/spmm_runs.jsonl" 2> "$O/spmm_runs.err" ;;
     threshold)
