@@ -49,6 +49,9 @@
 #   threshold            variant 15 vs the 2-line march on 4 / 6 / 8 M-row slabs (EIG_MARCH_2L_MIN_ROWS) -> threshold.jsonl
 #   halotime             the halo mailbox between 2 / 4 processes on one GPU (kernel trace) + the trial rehearsal
 #   mbonly               bench.py --gpus 2 / 4 --transport mailbox-only on ONE GPU (the whole N > 1 bench path)
+#   runs2l               plane runs of the 1- and 2-line value marches (256^3, 128^3, 256^2 slabs)  -> runs_*.jsonl
+#   spmmruns             plane runs of the 8-column SpMM / SpMM + dots + Gram (tools/spmm_runs.py)
+#   chebsegs             C5's Chebyshev step per box z-segment count (tools/cheb_segs.py; whole-solve differences)
 #
 # Session scripts of earlier rounds (tools/gpu_r04*.sh) are these tasks chained, e.g.
 #   TAG=r05a bash tools/gpu.sh tests:test_gpu_value_march.py sweep sweeppmc
