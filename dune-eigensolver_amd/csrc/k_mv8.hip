@@ -957,9 +957,9 @@ __device__ __forceinline__ double mgs_la_block(double (&acc)[W][8], MgsLaShared<
 }
 
 // Grid sums of the 8 W slots from nblk workgroups' partials (block b's slot e at part[b ld + e]):
-// value e over the blocks g, g + 8, ... (NIN loads in flight per round), then the 8 slices in slice
+// value e over the blocks g, g + 8, ... (16 loads in flight per round), then the 8 slices in slice
 // order -- a fixed order, independent of arrival.  Into sh.Rw (every thread may call; all must).
-template <int W, int L, int NIN = 16>
+template <int W, int L>
 __device__ __forceinline__ void mgs_la_gather(const double *part, int ld, unsigned nblk, MgsLaShared<L> &sh)
 {
   constexpr int E = 8 * W;
@@ -967,17 +967,17 @@ __device__ __forceinline__ void mgs_la_gather(const double *part, int ld, unsign
   {
     const int e = threadIdx.x % E, g = threadIdx.x / E;
     double x = 0.0;
-    for (unsigned b0 = (unsigned)g; b0 < nblk; b0 += 8u * NIN)
+    for (unsigned b0 = (unsigned)g; b0 < nblk; b0 += 8u * 16u)
     {
-      double t[NIN];
+      double t[16];
 #pragma unroll
-      for (int u = 0; u < NIN; ++u)
+      for (int u = 0; u < 16; ++u)
       {
         const unsigned b = b0 + 8u * u;
         t[u] = b < nblk ? ld_sc1(&part[(size_t)b * ld + e]) : 0.0;
       }
 #pragma unroll
-      for (int u = 0; u < NIN; ++u) x += t[u];
+      for (int u = 0; u < 16; ++u) x += t[u];
     }
     sh.fin[g][e] = x;
   }
@@ -1040,13 +1040,13 @@ __device__ __forceinline__ unsigned mgs_la_close(MgsLaShared<L> &sh, double *S, 
 }
 
 // An ordinary read launch: rows, workgroup partials, ticket; the last workgroup finishes the window.
-template <int F, int L, int U, int NIN>
+template <int F, int L>
 __device__ __forceinline__ void mgs_la_read(const MgsLaArgs a, unsigned word, MgsLaShared<L> &sh)
 {
   constexpr int W = (8 - F) < L ? (8 - F) : L;
   constexpr int E = 8 * W;
   double acc[W][8];
-  mgs_la_rows<F, W, U>(a.n, a.Qb, a.Sfin, acc);
+  mgs_la_rows<F, W, 2>(a.n, a.Qb, a.Sfin, acc);
   const double part = mgs_la_block<W, L>(acc, sh);
   const unsigned bid = blockIdx.x, nblk = gridDim.x;
   if (threadIdx.x < E) st_sc1(&a.partials[(size_t)bid * E + threadIdx.x], part);
@@ -1055,7 +1055,7 @@ __device__ __forceinline__ void mgs_la_read(const MgsLaArgs a, unsigned word, Mg
   if (threadIdx.x == 0) sh.last = ticket_arrive(a.ticket, bid, nblk) ? 1u : 0u;
   __syncthreads();
   if (!sh.last) return;
-  mgs_la_gather<W, L, NIN>(a.partials, E, nblk, sh);
+  mgs_la_gather<W, L>(a.partials, E, nblk, sh);
   if (threadIdx.x < 64)
   {
     const unsigned nw = mgs_la_close<F, W, L>(sh, a.Sfin, word);
@@ -1114,7 +1114,7 @@ __device__ __forceinline__ void mgs_la_write(i64 n, double *__restrict__ Qb, con
   }
 }
 
-template <int L, int U = 2, int NIN = 16>  // U rows per lane per batch, NIN tail loads per round
+template <int L>
 __global__ __launch_bounds__(kMgsLaThreads) void k_mgs_la(MgsLaArgs a)
 {
   __shared__ MgsLaShared<L> sh;  // (one copy for the nine pass bodies)
@@ -1128,14 +1128,14 @@ __global__ __launch_bounds__(kMgsLaThreads) void k_mgs_la(MgsLaArgs a)
   }
   switch (word & 15u)
   {
-    case 0: mgs_la_read<0, L, U, NIN>(a, word, sh); break;
-    case 1: mgs_la_read<1, L, U, NIN>(a, word, sh); break;
-    case 2: mgs_la_read<2, L, U, NIN>(a, word, sh); break;
-    case 3: mgs_la_read<3, L, U, NIN>(a, word, sh); break;
-    case 4: mgs_la_read<4, L, U, NIN>(a, word, sh); break;
-    case 5: mgs_la_read<5, L, U, NIN>(a, word, sh); break;
-    case 6: mgs_la_read<6, L, U, NIN>(a, word, sh); break;
-    case 7: mgs_la_read<7, L, U, NIN>(a, word, sh); break;
+    case 0: mgs_la_read<0, L>(a, word, sh); break;
+    case 1: mgs_la_read<1, L>(a, word, sh); break;
+    case 2: mgs_la_read<2, L>(a, word, sh); break;
+    case 3: mgs_la_read<3, L>(a, word, sh); break;
+    case 4: mgs_la_read<4, L>(a, word, sh); break;
+    case 5: mgs_la_read<5, L>(a, word, sh); break;
+    case 6: mgs_la_read<6, L>(a, word, sh); break;
+    case 7: mgs_la_read<7, L>(a, word, sh); break;
     default:
       mgs_la_write(a.n, a.Qb, a.Sfin);
       if (blockIdx.x == 0 && threadIdx.x == 0)
@@ -1279,45 +1279,15 @@ int mgs_lookahead_default()
   return L;
 }
 
-// The read launches' batch shape (EIGMI_MGS_LA_ROWS, a measurement switch for L = 8): 2 = two rows
-// per lane per batch and 16 tail loads per round (default); 3 = the same rows, 32 tail loads; 4 = four
-// rows per lane per batch and 32 tail loads
-static int mgs_la_rows_sel()
-{
-  static const int v = [] {
-    const char *e = std::getenv("EIGMI_MGS_LA_ROWS");
-    const int r = e ? std::atoi(e) : 2;
-    return r == 3 || r == 4 ? r : 2;
-  }();
-  return v;
-}
-
 namespace {
 template <int L>
 void mgs_la_enqueue(MgsLaArgs a, int G, bool coop, hipStream_t s)
 {
   const int reads = (8 + L - 1) / L;  // read launches when every look-ahead is taken
-  auto read = [&](void) {
-    if constexpr (L == 8)
-    {
-      const int r = mgs_la_rows_sel();
-      if (r == 4)
-      {
-        hipLaunchKernelGGL((k_mgs_la<8, 4, 32>), dim3(G), dim3(kMgsLaThreads), 0, s, a);
-        return;
-      }
-      if (r == 3)
-      {
-        hipLaunchKernelGGL((k_mgs_la<8, 2, 32>), dim3(G), dim3(kMgsLaThreads), 0, s, a);
-        return;
-      }
-    }
-    hipLaunchKernelGGL(k_mgs_la<L>, dim3(G), dim3(kMgsLaThreads), 0, s, a);
-  };
   for (int l = 0; l < reads; ++l)
   {
     a.launch = l;
-    read();
+    hipLaunchKernelGGL(k_mgs_la<L>, dim3(G), dim3(kMgsLaThreads), 0, s, a);
   }
   EIG_HIP(hipGetLastError());
   a.launch = reads;
@@ -1335,7 +1305,7 @@ void mgs_la_enqueue(MgsLaArgs a, int G, bool coop, hipStream_t s)
   for (int l = reads; l < 9; ++l)
   {
     a.launch = l;
-    read();
+    hipLaunchKernelGGL(k_mgs_la<L>, dim3(G), dim3(kMgsLaThreads), 0, s, a);
   }
   EIG_HIP(hipGetLastError());
 }

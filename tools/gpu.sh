@@ -51,7 +51,7 @@
 #   mbonly               bench.py --gpus 2 / 4 --transport mailbox-only on ONE GPU (the whole N > 1 bench path)
 #   runs2l               plane runs of the 1- and 2-line value marches (256^3, 128^3, 256^2 slabs)  -> runs_*.jsonl
 #   spmmruns             plane runs of the 8-column SpMM / SpMM + dots + Gram (tools/spmm_runs.py)
-#   larows               look-ahead MGS read launch: rows per lane per batch / tail loads (EIGMI_MGS_LA_ROWS 2/3/4) traced
+#   c5part               C5 256^3 block Lanczos on 8 loopback ranks vs one rank, under a kernel trace
 #   chebsegs             C5's Chebyshev step per box z-segment count (tools/cheb_segs.py; whole-solve differences)
 #
 # Session scripts of earlier rounds (tools/gpu_r04*.sh) are these tasks chained, e.g.
@@ -223,13 +223,11 @@ run_task() {
         python3 tools/bench_configs.py ortho > /dev/null 2> "$O/orthopmc_f.err" && \
       timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/orthopmc/write" -o pmc -- \
         python3 tools/bench_configs.py ortho > /dev/null 2> "$O/orthopmc_w.err" ;;
-    larows)
-      # the look-ahead read launch's batch shape (EIGMI_MGS_LA_ROWS 2 / 3 / 4) under a kernel trace each
+    c5part)
+      # C5's block Lanczos at 256^3 on 8 loopback ranks (tests/loopback_c5_worker.py) under a kernel trace
       prof_env
-      for r in 2 3 4; do
-        EIGMI_MGS_LA_ROWS=$r timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/larows$r" -o trace -- \
-          python3 tools/bench_configs.py ortho > "$O/larows$r.jsonl" 2> "$O/larows$r.err" || return 1
-      done ;;
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/c5part_trace" -o trace -- \
+        python3 tests/loopback_c5_worker.py 256 2 8 > "$O/c5part.jsonl" 2> "$O/c5part.err" ;;
     orthogrid)
       # the read-only passes' grid (EIGMI_MGS_GRID workgroups at most)
       for g in 256 512 1024 2048; do
