@@ -299,6 +299,9 @@ struct eig_mat_s {
   int box_state = 0;
   double *box_val = nullptr;
   int box_nx = 0, box_ny = 0, box_nz = 0;
+  // a rank's slab of whole planes (distributed contexts): ghost planes below / above the owned ones
+  // in the window (0 or 1 each; the owned rows start at own_offset = box_glo planes)
+  int box_glo = 0, box_ghi = 0;
   int box_dz[27] = {}, box_dxy[27] = {}, box_dx[27] = {}, box_dy[27] = {};
   // Row classes (k_box.hip k_boxc_mv8): when every row's stored entries equal those of its
   // geometric class representative (27 classes: first / interior / last position in x, y and z),

@@ -72,6 +72,7 @@ struct BoxGeom {
   int nseg;        // z runs per tile column
   int nd;          // stored offsets
   int xmap;        // k_box_mv32: 1 = XCD-contiguous item map (eig_mat_tune EIG_TUNE_BOX_MAP)
+  int zlo = 0, zhi = 0;  // k_box_mv32 on a rank's slab: ghost planes -1 / nz present in the window
   // per offset k: plane step dz (-1 / 0 / +1), LDS row shift (dy * kBoxHX + dx)
   int dz[27], dxy[27];
 };
@@ -103,7 +104,9 @@ constexpr BoxShapeTab box_shape_tab(unsigned shape)
 }
 
 // Box image of the band: val[k * n + r] = a(r, r + off[k]) (0 where row r does not store it).
-__global__ void k_box_image(i64 n, i64 ld, int nd, const i32 *__restrict__ off, const i32 *__restrict__ dj,
+// (band arrays window-indexed: owned row r is window row own + r; a slab's mirrored lower entries
+// of its first plane sit at ghost window rows)
+__global__ void k_box_image(i64 n, i64 ld, i64 own, int nd, const i32 *__restrict__ off, const i32 *__restrict__ dj,
                             const double *__restrict__ sym, const void *__restrict__ mask, int mask_bytes,
                             double *__restrict__ val)
 {
@@ -115,7 +118,7 @@ __global__ void k_box_image(i64 n, i64 ld, int nd, const i32 *__restrict__ off, 
       double v = 0.0;
       if ((m >> k) & 1u)
       {
-        const i64 w = off[k] < 0 ? r + off[k] : r;
+        const i64 w = own + (off[k] < 0 ? r + off[k] : r);
         v = sym[(i64)dj[k] * ld + w];
       }
       val[(i64)k * n + r] = v;
@@ -125,8 +128,9 @@ __global__ void k_box_image(i64 n, i64 ld, int nd, const i32 *__restrict__ off, 
 
 // Geometry check: every stored entry of row r stays inside the grid (no x / y / z wrap-around),
 // else bad |= 1; a row that does not store an offset staying inside the grid sets bad |= 2 (the
-// masks are then not the geometric ones: box_geomask stays false).
-__global__ void k_box_check(i64 n, int nx, int ny, int nz, int nd, const i32 *__restrict__ dx,
+// masks are then not the geometric ones: box_geomask stays false).  z is the global plane: a rank's
+// slab starts at plane z0 of a grid of nz planes.
+__global__ void k_box_check(i64 n, int nx, int ny, int nz, int z0, int nd, const i32 *__restrict__ dx,
                             const i32 *__restrict__ dy, const i32 *__restrict__ dzz, const void *__restrict__ mask,
                             int mask_bytes, unsigned *__restrict__ bad)
 {
@@ -134,7 +138,7 @@ __global__ void k_box_check(i64 n, int nx, int ny, int nz, int nd, const i32 *__
   for (i64 r = (i64)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (i64)gridDim.x * blockDim.x)
   {
     const unsigned m = mask_bytes == 1 ? static_cast<const uint8_t *>(mask)[r] : static_cast<const uint32_t *>(mask)[r];
-    const int x = (int)(r % nx), y = (int)((r / nx) % ny), z = (int)(r / ((i64)nx * ny));
+    const int x = (int)(r % nx), y = (int)((r / nx) % ny), z = z0 + (int)(r / ((i64)nx * ny));
     for (int k = 0; k < nd; ++k)
     {
       const int X = x + dx[k], Y = y + dy[k], Z = z + dzz[k];
@@ -187,7 +191,8 @@ __global__ __launch_bounds__(kBoxThreads) void k_box_mv32(BoxGeom g, i64 ld, con
       const int c = tid + i * kBoxThreads;
       const int q = c & 3, hx = (c >> 2) % kBoxHX, rest = (c >> 2) / kBoxHX, b = rest & 3, hy = rest >> 2;
       const int x = x0 + hx - 1, y = y0 + hy - 1;
-      const bool ok = c < kBoxChunks && zz >= 0 && zz < g.nz && x >= 0 && x < g.nx && y >= 0 && y < g.ny;
+      // (planes -1 and nz: a slab's ghost planes where the window holds them, else zero rows)
+      const bool ok = c < kBoxChunks && zz >= -g.zlo && zz < g.nz + g.zhi && x >= 0 && x < g.nx && y >= 0 && y < g.ny;
       const i64 row = ok ? (i64)x + (i64)g.nx * y + (i64)g.P * zz : 0;
       // plain loads: a plane's rows are also the halo of the neighbouring tiles (nontemporal X
       // loads measured the same, 4.21 vs 4.23 ms, in one interleaved run)
@@ -1016,8 +1021,11 @@ bool box_prepare(const eig_mat_s &Ac)
   eig_mat_s &A = const_cast<eig_mat_s &>(Ac);
   if (A.box_state != 0) return A.box_state > 0;
   A.box_state = -1;
-  if (!A.sym_val || A.br != 1 || A.bc != 1 || A.ctx->distributed() || (A.kflags & EIG_MAT_NO_MARCH)) return false;
-  if (A.sym_nd > kBoxClassMaxNd || A.nb_rows != A.nb_rows_global || A.window != A.nb_rows) return false;
+  if (!A.sym_val || A.br != 1 || A.bc != 1 || (A.kflags & EIG_MAT_NO_MARCH)) return false;
+  // a rank of a distributed context: its slab of whole planes (checked below, once the plane size is
+  // known); one rank: the whole grid in its own window
+  const bool slab = A.ctx->distributed();
+  if (A.sym_nd > kBoxClassMaxNd || (!slab && (A.nb_rows != A.nb_rows_global || A.window != A.nb_rows))) return false;
   // Grid from the offsets: Nx is the smallest offset > 1 (+1 when the stencil has the (0, +1, -1)
   // neighbour, d = Nx - 1), P = Nx Ny the smallest offset past Nx + 1 (+ 0, 1, Nx - 1, Nx or Nx + 1
   // for the neighbours with dz = 1 and dy, dx < 0 .. dy = 1); every offset must be a P + b Nx + c
@@ -1061,6 +1069,19 @@ bool box_prepare(const eig_mat_s &Ac)
   if (!P) return false;
   const i64 ny = P / nx, nz = A.nb_rows / P;
   if (nz < 3 || nz > (1 << 24)) return false;
+  // slab: whole planes, the window = at most one ghost plane below and above the owned ones in global
+  // order (the box kernel reads planes -1 and nz from there; the band arrays are window-indexed)
+  int glo = 0, ghi = 0;
+  if (slab)
+  {
+    const i64 tail = A.window - A.own_offset - A.nb_rows;
+    if (A.row_begin % P != 0 || A.nb_rows_global % P != 0 || A.own_offset % P != 0 || tail < 0 || tail % P != 0)
+      return false;
+    glo = (int)(A.own_offset / P);
+    ghi = (int)(tail / P);
+    if (glo > 1 || ghi > 1 || A.nb_rows_global / P > (1 << 24)) return false;
+  }
+  const int z0 = slab ? (int)(A.row_begin / P) : 0, nzg = slab ? (int)(A.nb_rows_global / P) : (int)nz;
   decompose(nx, P);
   hipStream_t s = A.ctx->stream;
   const i64 n = A.nb_rows;
@@ -1073,7 +1094,7 @@ bool box_prepare(const eig_mat_s &Ac)
     EIG_HIP(hipMemcpyAsync(dm, h.data(), h.size() * sizeof(i32), hipMemcpyHostToDevice, s));
     unsigned *bad = reinterpret_cast<unsigned *>(dm + 3 * A.sym_nd);
     EIG_HIP(hipMemsetAsync(bad, 0, sizeof(unsigned), s));
-    hipLaunchKernelGGL(k_box_check, dim3(2048), dim3(256), 0, s, n, (int)nx, (int)ny, (int)nz, A.sym_nd, dm,
+    hipLaunchKernelGGL(k_box_check, dim3(2048), dim3(256), 0, s, n, (int)nx, (int)ny, nzg, z0, A.sym_nd, dm,
                        dm + A.sym_nd, dm + 2 * A.sym_nd, (const void *)A.sym_mask, A.sym_mask_bytes, bad);
     unsigned hb = 0;
     EIG_HIP(hipMemcpyAsync(&hb, bad, sizeof(unsigned), hipMemcpyDeviceToHost, s));
@@ -1090,15 +1111,18 @@ bool box_prepare(const eig_mat_s &Ac)
     double *val = nullptr;
     EIG_HIP(hipMalloc(&val, (size_t)A.sym_nd * n * sizeof(double)));
     const i32 *o = static_cast<const i32 *>(od.p);
-    hipLaunchKernelGGL(k_box_image, dim3(2048), dim3(256), 0, s, n, A.sym_ld, A.sym_nd, o, o + A.sym_nd,
+    hipLaunchKernelGGL(k_box_image, dim3(2048), dim3(256), 0, s, n, A.sym_ld, (i64)A.own_offset, A.sym_nd, o, o + A.sym_nd,
                        (const double *)A.sym_val, (const void *)A.sym_mask, A.sym_mask_bytes, val);
     EIG_HIP(hipStreamSynchronize(s));
     A.box_val = val;
   }
-  box_classes(A, nx, ny, nz);
+  // (row classes by global position: one rank only -- a slab takes the box-image kernel)
+  if (!slab) box_classes(A, nx, ny, nz);
   A.box_nx = (int)nx;
   A.box_ny = (int)ny;
   A.box_nz = (int)nz;
+  A.box_glo = glo;
+  A.box_ghi = ghi;
   for (int k = 0; k < A.sym_nd; ++k)
   {
     A.box_dz[k] = dz[k];
@@ -1213,6 +1237,10 @@ static bool launch_box(const eig_mat_s &A, i64 m, const double *X, double *Y, co
     return true;
   }
   if (m % 32 != 0) return false;  // the box-image kernel takes 32 columns per pass
+  // a rank's slab (A.ctx->distributed()): k_box_mv32's product and Chebyshev step only, the window's
+  // ghost planes as planes -1 / nz, every window-layout vector from its owned rows (own_offset)
+  const bool slab = A.ctx->distributed();
+  if (slab && epi != kBoxStore && epi != kBoxCheb) return false;
   BoxGeom g;
   g.nx = A.box_nx;
   g.ny = A.box_ny;
@@ -1226,6 +1254,8 @@ static bool launch_box(const eig_mat_s &A, i64 m, const double *X, double *Y, co
   if (A.tune_box_segs > 0) g.nseg = std::min(g.nz, A.tune_box_segs);
   g.nd = A.sym_nd;
   g.xmap = A.tune_box_map == 1 && (tiles * g.nseg) % 8 == 0;
+  g.zlo = A.box_glo;
+  g.zhi = A.box_ghi;
   for (int k = 0; k < 27; ++k)
   {
     g.dz[k] = k < A.sym_nd ? A.box_dz[k] : 0;
@@ -1238,12 +1268,13 @@ static bool launch_box(const eig_mat_s &A, i64 m, const double *X, double *Y, co
   for (int k = 0; k < A.sym_nd; ++k)
     shape |= 1u << ((A.box_dz[k] + 1) * 9 + (A.box_dy[k] + 1) * 3 + (A.box_dx[k] + 1));
   // EIG_TUNE_BOX_COLS: 16 = the push-order kernel (two 16-column workgroups per tile), 32 = k_box_mv32
-  const bool push = box_cols(A) == 16;
+  const bool push = box_cols(A) == 16 && !slab;
   auto go = [&](auto shape_tag) {
     constexpr unsigned S = decltype(shape_tag)::value;
     for (i64 c0 = 0; c0 < m; c0 += 32)
     {
-      const i64 off = c0 * ld;  // 4 column blocks of ld rows x 8
+      // 4 column blocks of ld rows x 8, from the owned rows (one rank: own_offset 0)
+      const i64 off = c0 * ld + (slab ? A.own_offset * 8 : 0);
       if (push)
       {
         const int items = tiles * g.nseg;

@@ -1,9 +1,9 @@
 """Config C5 (generalised block Lanczos, k = 32, variable-coefficient P1 K/M) row-partitioned at its
 own size, 256^3, on ONE GPU: P = 8 z-slabs (32 planes per virtual rank, the 8-GPU split) over the
-loopback hub (tests/loopback_c5_worker.py).  The one-rank run streams the box image (k_box_mv32 SpMM,
-k_box_mv32_cheb mass-solve step); a slab rank streams its symmetric band image through the carried-offset
-march (k_spmm8_marchg / k_spmm8_marchg_cheb: the box image is built for one-rank matrices only,
-k_box.hip box_prepare), the kernels an 8-GPU run takes.  Against the one-rank run of the same pencil: the
+loopback hub (tests/loopback_c5_worker.py).  Every rank streams the box image the one-rank run streams
+(k_box_mv32 SpMM, k_box_mv32_cheb mass-solve step): a slab's box kernel reads its ghost planes from
+the window as planes -1 / nz (k_box.hip box_prepare, launch_box) -- the kernels an 8-GPU run takes.
+Against the one-rank run of the same pencil: the
 block-tridiagonal T within 1e-10 of max |T|, the 8 largest Ritz values within 1e-10 relative, their
 residuals within 1e-7 relative (eigensolver.hh:283-325, kernels_cpp.hh:356-591)."""
 import json
@@ -42,7 +42,7 @@ def test_c5_partition_256(c5_lines, P):
         r = rk["rank"]
         assert rk["error"] is None, rk
         assert rk["rows"] == N * N * (N // P)
-        assert rk["spmm"] == "k_spmm8_marchg" and rk["cheb"] == "k_spmm8_marchg_cheb", rk
+        assert rk["spmm"] == "k_box_mv32" and rk["cheb"] == "k_box_mv32_cheb", rk
         assert rk["T_shape_ok"], rk
         assert rk["T_rel"] <= 1e-10, f"rank {r}: T differs from the one-rank run by {rk['T_rel']:.2e} of max |T|"
         assert rk["ev_rel"] <= 1e-10, f"rank {r}: Ritz values differ by {rk['ev_rel']:.2e}"
