@@ -72,7 +72,8 @@ struct BoxGeom {
   int nseg;        // z runs per tile column
   int nd;          // stored offsets
   int xmap;        // k_box_mv32: 1 = XCD-contiguous item map (eig_mat_tune EIG_TUNE_BOX_MAP)
-  int zlo = 0, zhi = 0;  // k_box_mv32 on a rank's slab: ghost planes -1 / nz present in the window
+  int zlo = 0, zhi = 0;  // a rank's slab (k_box_mv32, k_boxc_mv8): ghost planes -1 / nz present in the window
+  int gz0 = 0, gnz = 0;  // k_boxc_mv8: the slab's first global plane and the grid's planes (row classes)
   // per offset k: plane step dz (-1 / 0 / +1), LDS row shift (dy * kBoxHX + dx)
   int dz[27], dxy[27];
 };
@@ -667,14 +668,15 @@ constexpr int kCStride = 28;  // doubles per class: nd <= 27 values, then 1 / a_
 __device__ __forceinline__ int box_cls1(int v, int nv) { return v == 0 ? 0 : (v == nv - 1 ? 2 : 1); }
 
 // bad |= 1 when a row's mask or a stored entry differs from its class's (bitwise).
-__global__ void k_boxc_check(i64 n, int nx, int ny, int nd, const double *__restrict__ val,
+// (z: the global plane -- a rank's slab starts at plane z0 of a grid of nz planes)
+__global__ void k_boxc_check(i64 n, int nx, int ny, int z0, int nz, int nd, const double *__restrict__ val,
                              const void *__restrict__ mask, int mask_bytes, const double *__restrict__ ctab,
                              const unsigned *__restrict__ cmask, unsigned *__restrict__ bad)
 {
   for (i64 r = (i64)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (i64)gridDim.x * blockDim.x)
   {
     const int x = (int)(r % nx), y = (int)((r / nx) % ny);
-    const i64 z = r / ((i64)nx * ny), nz = n / ((i64)nx * ny);
+    const i64 z = z0 + r / ((i64)nx * ny);
     const int c = (z == 0 ? 0 : (z == nz - 1 ? 2 : 1)) * 9 + box_cls1(y, ny) * 3 + box_cls1(x, nx);
     const unsigned m = mask_bytes == 1 ? static_cast<const uint8_t *>(mask)[r] : static_cast<const uint32_t *>(mask)[r];
     bool ok = m == cmask[c];
@@ -738,7 +740,7 @@ __global__ __launch_bounds__(kCThreads, EPI == kBoxStoreDotGram ? 4 : 8) void k_
     {
       const int c = tid + i * kCThreads, q = c & 3, hr = c >> 2, hx = hr % kCHX, hy = hr / kCHX;
       const int x = x0 + hx - 1, y = y0 + hy - 1;
-      const bool ok = c < kCChunks && zz >= 0 && zz < g.nz && x >= 0 && x < g.nx && y >= 0 && y < g.ny;
+      const bool ok = c < kCChunks && zz >= -g.zlo && zz < g.nz + g.zhi && x >= 0 && x < g.nx && y >= 0 && y < g.ny;
       const i64 row = ok ? (i64)x + (i64)g.nx * y + (i64)g.P * zz : 0;
       pre[i] = ok ? Xb[row * 4 + q] : dv2b{0.0, 0.0};
     }
@@ -791,7 +793,8 @@ __global__ __launch_bounds__(kCThreads, EPI == kBoxStoreDotGram ? 4 : 8) void k_
     __syncthreads();  // ring holds planes z - 1, z, z + 1 (and the class table)
     fetch_cheb(z + 1, bn, xn);
     fetch(z + 2);
-    const int cls = (z == 0 ? 0 : (z == g.nz - 1 ? 2 : 1)) * 9 + cxy;
+    const int gz = g.gz0 + z;  // (the global plane: a slab's rows take their grid classes)
+    const int cls = (gz == 0 ? 0 : (gz == g.gnz - 1 ? 2 : 1)) * 9 + cxy;
     const unsigned m = own ? cm[cls] : 0u;
     // ring slots of planes z - 1, z, z + 1 (scalar)
     const int s0 = z % 3, sm = s0 == 0 ? 2 : s0 - 1, sp = s0 == 2 ? 0 : s0 + 1;
@@ -959,7 +962,9 @@ void box_invalidate(eig_mat_s &A)
 // Row classes of a box image (k_boxc_mv8): the 27 representatives' entries and masks to the host,
 // 1 / a_rr per class, then every row checked bitwise against its class on the device; on success
 // A.box_ctab / box_cmask are set.  Needs a stored diagonal in every class.
-static void box_classes(eig_mat_s &A, i64 nx, i64 ny, i64 nz)
+// A rank's slab (planes z0 .. z0 + nz - 1 of nzg): classes by global plane; a z class the slab does not
+// hold (first / last plane of the grid) takes the interior representative (never read).
+static void box_classes(eig_mat_s &A, i64 nx, i64 ny, i64 nz, i64 z0, i64 nzg)
 {
   if (nx < 3 || ny < 3 || nz < 3 || A.sym_nd >= kCStride || (A.kflags & EIG_MAT_NO_CLASS)) return;
   int k0 = -1;
@@ -970,8 +975,11 @@ static void box_classes(eig_mat_s &A, i64 nx, i64 ny, i64 nz)
   const i64 n = A.nb_rows;
   std::vector<i64> rep(kBoxClasses);
   auto pos = [](int c, i64 nv) { return c == 0 ? (i64)0 : (c == 1 ? (i64)1 : nv - 1); };
+  // local plane of z class c (1: local plane 1, global interior since nz >= 3 and the slab's planes
+  // are whole): 0 / nz - 1 only where the slab holds the grid's first / last plane
+  auto zpos = [&](int c) { return c == 0 ? (z0 == 0 ? (i64)0 : (i64)1) : (c == 2 ? (z0 + nz == nzg ? nz - 1 : (i64)1) : (i64)1); };
   for (int c = 0; c < kBoxClasses; ++c)
-    rep[c] = pos(c % 3, nx) + nx * pos((c / 3) % 3, ny) + nx * ny * pos(c / 9, nz);
+    rep[c] = pos(c % 3, nx) + nx * pos((c / 3) % 3, ny) + nx * ny * zpos(c / 9);
   DevBuf drep(kBoxClasses * sizeof(i64)), dout((size_t)kBoxClasses * (kCStride + 1) * sizeof(double));
   EIG_HIP(hipMemcpyAsync(drep.p, rep.data(), kBoxClasses * sizeof(i64), hipMemcpyHostToDevice, s));
   hipLaunchKernelGGL(k_boxc_gather, dim3(kBoxClasses), dim3(64), 0, s, n, A.sym_nd, (const double *)A.box_val,
@@ -999,7 +1007,7 @@ static void box_classes(eig_mat_s &A, i64 nx, i64 ny, i64 nz)
   EIG_HIP(hipMemcpyAsync(dcm, cmask.data(), kBoxClasses * sizeof(unsigned), hipMemcpyHostToDevice, s));
   unsigned *bad = dcm + kBoxClasses;
   EIG_HIP(hipMemsetAsync(bad, 0, sizeof(unsigned), s));
-  hipLaunchKernelGGL(k_boxc_check, dim3(2048), dim3(256), 0, s, n, (int)nx, (int)ny, A.sym_nd,
+  hipLaunchKernelGGL(k_boxc_check, dim3(2048), dim3(256), 0, s, n, (int)nx, (int)ny, (int)z0, (int)nzg, A.sym_nd,
                      (const double *)A.box_val, (const void *)A.sym_mask, A.sym_mask_bytes, dct, dcm, bad);
   unsigned hb = 1;
   EIG_HIP(hipMemcpyAsync(&hb, bad, sizeof(unsigned), hipMemcpyDeviceToHost, s));
@@ -1116,8 +1124,7 @@ bool box_prepare(const eig_mat_s &Ac)
     EIG_HIP(hipStreamSynchronize(s));
     A.box_val = val;
   }
-  // (row classes by global position: one rank only -- a slab takes the box-image kernel)
-  if (!slab) box_classes(A, nx, ny, nz);
+  box_classes(A, nx, ny, nz, z0, nzg);
   A.box_nx = (int)nx;
   A.box_ny = (int)ny;
   A.box_nz = (int)nz;
@@ -1155,6 +1162,11 @@ static bool launch_box(const eig_mat_s &A, i64 m, const double *X, double *Y, co
   if (epi >= kBoxChebFirst && !A.box_ctab) return false;  // (row-class only)
   if ((epi == kBoxStoreDot || epi == kBoxStoreDotGram) && !A.box_ctab) return false;
   if (epi == kBoxStoreDotGram && m != 8) return false;
+  // a rank's slab (A.ctx->distributed()): the product and the Chebyshev step only, the window's ghost
+  // planes as planes -1 / nz, every window-layout vector from its owned rows (own_offset)
+  const bool slab = A.ctx->distributed();
+  if (slab && epi != kBoxStore && epi != kBoxCheb) return false;
+  const i64 own8 = slab ? A.own_offset * 8 : 0;
   if (A.box_ctab)
   {
     // row-class kernels: one launch, blockIdx.y = column block.  z runs of about 32 planes (a run
@@ -1165,6 +1177,10 @@ static bool launch_box(const eig_mat_s &A, i64 m, const double *X, double *Y, co
     g.nx = A.box_nx;
     g.ny = A.box_ny;
     g.nz = A.box_nz;
+    g.zlo = A.box_glo;
+    g.zhi = A.box_ghi;
+    g.gz0 = slab ? (int)(A.row_begin / ((i64)A.box_nx * A.box_ny)) : 0;
+    g.gnz = slab ? (int)(A.nb_rows_global / ((i64)A.box_nx * A.box_ny)) : A.box_nz;
     g.P = g.nx * g.ny;
     g.ntx = (g.nx + kCTX - 1) / kCTX;
     g.nty = (g.ny + kCTY - 1) / kCTY;
@@ -1193,6 +1209,16 @@ static bool launch_box(const eig_mat_s &A, i64 m, const double *X, double *Y, co
       constexpr unsigned S = decltype(shape_tag)::value;
       const double *ct = (const double *)A.box_ctab;
       const unsigned *cm = (const unsigned *)A.box_cmask;
+      if (slab)  // (kBoxStore / kBoxCheb only, from the owned rows)
+      {
+        if (epi == kBoxCheb)
+          hipLaunchKernelGGL((k_boxc_mv8<kBoxCheb, S>), grid, dim3(kCThreads), 0, s, g, A.window, ct, cm, X + own8,
+                             Y + own8, Xold ? Xold + own8 : nullptr, Bv + own8, omega, gamma, bd);
+        else
+          hipLaunchKernelGGL((k_boxc_mv8<kBoxStore, S>), grid, dim3(kCThreads), 0, s, g, A.window, ct, cm, X + own8,
+                             Y + own8, (const double *)nullptr, (const double *)nullptr, 0.0, 0.0, bd);
+        return;
+      }
       if (epi == kBoxCheb)
         hipLaunchKernelGGL((k_boxc_mv8<kBoxCheb, S>), grid, dim3(kCThreads), 0, s, g, A.window, ct, cm, X, Y, Xold,
                            Bv, omega, gamma, bd);
@@ -1237,10 +1263,6 @@ static bool launch_box(const eig_mat_s &A, i64 m, const double *X, double *Y, co
     return true;
   }
   if (m % 32 != 0) return false;  // the box-image kernel takes 32 columns per pass
-  // a rank's slab (A.ctx->distributed()): k_box_mv32's product and Chebyshev step only, the window's
-  // ghost planes as planes -1 / nz, every window-layout vector from its owned rows (own_offset)
-  const bool slab = A.ctx->distributed();
-  if (slab && epi != kBoxStore && epi != kBoxCheb) return false;
   BoxGeom g;
   g.nx = A.box_nx;
   g.ny = A.box_ny;
@@ -1274,7 +1296,7 @@ static bool launch_box(const eig_mat_s &A, i64 m, const double *X, double *Y, co
     for (i64 c0 = 0; c0 < m; c0 += 32)
     {
       // 4 column blocks of ld rows x 8, from the owned rows (one rank: own_offset 0)
-      const i64 off = c0 * ld + (slab ? A.own_offset * 8 : 0);
+      const i64 off = c0 * ld + own8;
       if (push)
       {
         const int items = tiles * g.nseg;

@@ -12,7 +12,10 @@ allreduced over the hub.  Checked against the one-rank run of the same pencil in
   * the NEV largest Ritz values within 1e-10 relative, their device residuals within 1e-7 relative.
 One JSON line per P on stdout (the first line is the one-rank run).
 
-    python tests/loopback_c5_worker.py N STEPS P [P ...]
+    python tests/loopback_c5_worker.py N STEPS P [P ...] [--const]
+
+--const: the constant-coefficient P1 pencil (eig_gen kinds 6 / 7) with its row classes, so every rank
+runs the row-class kernels (k_boxc_mv8: the class table in LDS, no matrix stream) on its slab.
 """
 import json
 import os
@@ -27,6 +30,10 @@ sys.path.insert(0, os.path.join(ROOT, "dune-eigensolver_amd"))
 import eigmi  # noqa: E402
 
 BLOCK, NEV = 32, 8
+CONST = "--const" in sys.argv
+KIND_K, KIND_M = ((eigmi.GEN_P1STIFF3D, eigmi.GEN_P1MASS3D) if CONST else
+                  (eigmi.GEN_P1STIFF3D_VAR, eigmi.GEN_P1MASS3D_VAR))
+FLAGS = 0 if CONST else eigmi.MAT_NO_CLASS
 
 
 def solve(K, M, steps):
@@ -50,11 +57,11 @@ def rank_run(hub, r, P, N, steps, out):
     K = M = None
     try:
         ctx.comm_init_loopback(hub, r)
-        rk, ck, vk = eigmi.gen_rows(eigmi.GEN_P1STIFF3D_VAR, N, b, cnt)
-        K = eigmi.Matrix.from_rows(ctx, n, b, rk, ck, vk, flags=eigmi.MAT_NO_CLASS)
+        rk, ck, vk = eigmi.gen_rows(KIND_K, N, b, cnt)
+        K = eigmi.Matrix.from_rows(ctx, n, b, rk, ck, vk, flags=FLAGS)
         del rk, ck, vk
-        rm, cm, vm = eigmi.gen_rows(eigmi.GEN_P1MASS3D_VAR, N, b, cnt)
-        M = eigmi.Matrix.from_rows(ctx, n, b, rm, cm, vm, flags=eigmi.MAT_NO_CLASS)
+        rm, cm, vm = eigmi.gen_rows(KIND_M, N, b, cnt)
+        M = eigmi.Matrix.from_rows(ctx, n, b, rm, cm, vm, flags=FLAGS)
         del rm, cm, vm
         res.update(spmm=K.kernel("spmm32"), cheb=M.kernel("cheb32"), halo=int(K.info.halo_recv))
         t0 = time.time()
@@ -72,22 +79,22 @@ def rank_run(hub, r, P, N, steps, out):
 
 def main():
     N, steps = int(sys.argv[1]), int(sys.argv[2])
-    Ps = [int(p) for p in sys.argv[3:]]
+    Ps = [int(p) for p in sys.argv[3:] if not p.startswith("--")]
     n = N ** 3
     t0 = time.time()
     ctx = eigmi.Context(0)
-    rk, ck, vk = eigmi.gen_matrix(eigmi.GEN_P1STIFF3D_VAR, N)
-    K = eigmi.Matrix.from_bcsr(ctx, rk, ck, vk, flags=eigmi.MAT_NO_CLASS)
+    rk, ck, vk = eigmi.gen_matrix(KIND_K, N)
+    K = eigmi.Matrix.from_bcsr(ctx, rk, ck, vk, flags=FLAGS)
     del rk, ck, vk
-    rm, cm, vm = eigmi.gen_matrix(eigmi.GEN_P1MASS3D_VAR, N)
-    M = eigmi.Matrix.from_bcsr(ctx, rm, cm, vm, flags=eigmi.MAT_NO_CLASS)
+    rm, cm, vm = eigmi.gen_matrix(KIND_M, N)
+    M = eigmi.Matrix.from_bcsr(ctx, rm, cm, vm, flags=FLAGS)
     del rm, cm, vm
     kinfo = (K.kernel("spmm32"), M.kernel("cheb32"))
     T1, ev1, res1 = solve(K, M, steps)
     K.close()
     M.close()
     ctx.close()
-    print(json.dumps({"P": 1, "N": N, "n": n, "steps": steps, "spmm": kinfo[0], "cheb": kinfo[1],
+    print(json.dumps({"P": 1, "N": N, "const": CONST, "n": n, "steps": steps, "spmm": kinfo[0], "cheb": kinfo[1],
                       "ev": ev1.tolist(), "res": res1.tolist(), "seconds": round(time.time() - t0, 1)}), flush=True)
     tmax = float(np.abs(T1).max())
     for P in Ps:

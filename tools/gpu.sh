@@ -51,7 +51,7 @@
 #   mbonly               bench.py --gpus 2 / 4 --transport mailbox-only on ONE GPU (the whole N > 1 bench path)
 #   runs2l               plane runs of the 1- and 2-line value marches (256^3, 128^3, 256^2 slabs)  -> runs_*.jsonl
 #   spmmruns             plane runs of the 8-column SpMM / SpMM + dots + Gram (tools/spmm_runs.py)
-#   c5part               C5 256^3 block Lanczos on 8 loopback ranks vs one rank, under a kernel trace
+#   c5part               C5 256^3 block Lanczos on 8 loopback ranks vs one rank (variable / constant coefficients), traced
 #   chebsegs             C5's Chebyshev step per box z-segment count (tools/cheb_segs.py; whole-solve differences)
 #
 # Session scripts of earlier rounds (tools/gpu_r04*.sh) are these tasks chained, e.g.
@@ -227,7 +227,9 @@ run_task() {
       # C5's block Lanczos at 256^3 on 8 loopback ranks (tests/loopback_c5_worker.py) under a kernel trace
       prof_env
       timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/c5part_trace" -o trace -- \
-        python3 tests/loopback_c5_worker.py 256 2 8 > "$O/c5part.jsonl" 2> "$O/c5part.err" ;;
+        python3 tests/loopback_c5_worker.py 256 2 8 > "$O/c5part.jsonl" 2> "$O/c5part.err" && \
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/c5partc_trace" -o trace -- \
+        python3 tests/loopback_c5_worker.py 256 2 8 --const > "$O/c5partc.jsonl" 2> "$O/c5partc.err" ;;
     orthogrid)
       # the read-only passes' grid (EIGMI_MGS_GRID workgroups at most)
       for g in 256 512 1024 2048; do
