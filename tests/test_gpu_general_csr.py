@@ -96,3 +96,17 @@ def test_lanczos_auto_picks_per_image(ctx, s64):
     assert ws.kernel_bytes == Mp.lanczos_kernel_info(True)[1]
     ws.close()
     Mp.close()
+
+
+def test_stencil_image_fused_64(ctx):
+    """The fused step on the SELL stencil image (3-D Poisson 64^3 without the band image: every slice a
+    stencil slice, k_lanczos_fused_b1 kStencil): 60 steps within 1e-12 of the restatement
+    orc_lanczos_fused (only the three sums' order differs)."""
+    A = oracle.poisson3d(64)
+    M = eigmi.Matrix.from_bcsr(ctx, A.rowptr, A.col, A.val, flags=eigmi.MAT_NO_BAND)
+    assert M.info.stencil_slices == M.info.nslices and M.kernel("fused") == "k_lanczos_fused_b1"
+    a, b, _ = eigmi.lanczos_run(M, 60, seed=123, fused=True)
+    M.close()
+    ra, rb = oracle.lanczos_fused(A, oracle.random_vec(A.n, 123), 60)
+    assert np.max(np.abs(a - ra) / np.abs(ra)) <= 1e-12
+    assert np.max(np.abs(b[1:] - rb[1:]) / np.abs(rb[1:])) <= 1e-12
